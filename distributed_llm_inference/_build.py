@@ -1,0 +1,160 @@
+"""In-tree build of the native extensions (no JIT cache, no hipify, no setuptools magic).
+
+* ``_C``        — CDNA4 kernels (``csrc/kernels/*.hip``, compiled by hipcc for gfx950 only),
+                  their torch bindings and the RCCL communicator (``csrc/bindings.hip``,
+                  ``csrc/comm/rccl_p2p.hip``).
+* ``_runtime``  — torch-free C++ host runtime (block manager, shared-memory channels), built with
+                  g++ so CPU-only tests can use it.
+
+Both land next to this file so the built ``.so`` travels with the repository snapshot to the GPU
+box.  Rebuilds are incremental (object files are cached under ``build/``).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from typing import List, Optional
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+BUILD_DIR = os.path.join(REPO_DIR, "build", "native")
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ARCH = os.environ.get("DLI_OFFLOAD_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+KERNEL_SOURCES = ["kernels/norm.hip", "kernels/activation.hip", "kernels/rope_cache.hip",
+                  "kernels/attention.hip", "kernels/sampling.hip", "kernels/quant.hip",
+                  "kernels/gemm.hip"]
+TORCH_SOURCES = ["bindings.hip", "comm/rccl_p2p.hip"]
+RUNTIME_SOURCES = ["runtime/block_manager.cpp", "runtime/shm_channel.cpp"]
+
+
+def kernels_so_path() -> str:
+    return os.path.join(PKG_DIR, "_C" + EXT_SUFFIX)
+
+
+def runtime_so_path() -> str:
+    return os.path.join(PKG_DIR, "_runtime" + EXT_SUFFIX)
+
+
+def _headers() -> List[str]:
+    out = []
+    for root, _, files in os.walk(CSRC):
+        out += [os.path.join(root, f) for f in files if f.endswith((".h", ".hpp", ".cuh"))]
+    return out
+
+
+def _mtime(paths) -> float:
+    return max((os.path.getmtime(p) for p in paths if os.path.exists(p)), default=0.0)
+
+
+def _run(cmd: List[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build command failed ({r.returncode}):\n{' '.join(cmd)}\n{r.stdout}")
+    if verbose and r.stdout.strip():
+        print(r.stdout)
+
+
+def _py_includes() -> List[str]:
+    import pybind11
+    return [sysconfig.get_paths()["include"], pybind11.get_include()]
+
+
+def _torch_flags():
+    import torch
+    from torch.utils import cpp_extension as ce
+    inc = ce.include_paths()
+    libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cflags = [f"-I{p}" for p in inc + _py_includes()] + [
+        "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=_C",
+        f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1", "-DHIPBLAS_V2",
+        "-D__HIP_PLATFORM_AMD__=1",
+    ]
+    ldflags = [f"-L{libdir}", f"-Wl,-rpath,{libdir}", "-lc10", "-ltorch", "-ltorch_cpu",
+               "-ltorch_python", "-lc10_hip", "-ltorch_hip", "-lamdhip64", "-lrccl"]
+    return cflags, ldflags
+
+
+def _compile_many(jobs, verbose: bool, workers: int) -> None:
+    if not jobs:
+        return
+    with cf.ThreadPoolExecutor(max_workers=workers) as ex:
+        futs = [ex.submit(_run, cmd, verbose) for cmd in jobs]
+        for f in futs:
+            f.result()
+
+
+def build_kernels(force: bool = False, verbose: bool = False, workers: Optional[int] = None) -> str:
+    """Compile the gfx950 kernels + torch bindings into ``_C``; returns the .so path."""
+    hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+    out = kernels_so_path()
+    srcs = [os.path.join(CSRC, s) for s in KERNEL_SOURCES + TORCH_SOURCES]
+    srcs = [s for s in srcs if os.path.exists(s)]
+    deps = srcs + _headers() + [__file__]
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= _mtime(deps):
+        return out
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    tcflags, ldflags = _torch_flags()
+    base = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
+            f"-I{CSRC}", "-Wno-unused-result", "-Wno-deprecated-declarations"]
+    hdr_m = _mtime(_headers() + [__file__])
+    jobs, objs = [], []
+    for s in srcs:
+        rel = os.path.relpath(s, CSRC)
+        is_torch = rel in TORCH_SOURCES
+        flags = base + (tcflags if is_torch else [])
+        key = hashlib.sha1(" ".join(flags).encode()).hexdigest()[:8]
+        obj = os.path.join(BUILD_DIR, rel.replace("/", "_") + f".{key}.o")
+        objs.append(obj)
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(s), hdr_m):
+            jobs.append(flags + ["-c", s, "-o", obj])
+    _compile_many(jobs, verbose, workers or min(8, os.cpu_count() or 4))
+    tmp = out + ".tmp"
+    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ldflags, verbose)
+    os.replace(tmp, out)
+    return out
+
+
+def build_runtime(force: bool = False, verbose: bool = False) -> str:
+    """Compile the torch-free host runtime into ``_runtime`` with the system C++ compiler."""
+    out = runtime_so_path()
+    srcs = [os.path.join(CSRC, s) for s in RUNTIME_SOURCES]
+    deps = srcs + _headers() + [__file__]
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= _mtime(deps):
+        return out
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "c++"
+    tmp = out + ".tmp"
+    cmd = [cxx, "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden"] + \
+          [f"-I{p}" for p in _py_includes()] + srcs + ["-o", tmp, "-lrt", "-pthread"]
+    _run(cmd, verbose)
+    os.replace(tmp, out)
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_runtime(force=force, verbose=verbose)
+    build_kernels(force=force, verbose=verbose)
+
+
+if __name__ == "__main__":
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--runtime-only", action="store_true")
+    a = ap.parse_args()
+    build_runtime(a.force, a.verbose)
+    if not a.runtime_only:
+        build_kernels(a.force, a.verbose)
+    print("built:", runtime_so_path(), "" if a.runtime_only else kernels_so_path())
+    sys.exit(0)

@@ -1,0 +1,316 @@
+"""Model / stage / serving configuration.
+
+The reference takes its model description straight from ``transformers.AutoConfig``
+(``/root/reference/distributed_llm_inference/utils/model.py:83``) and reads a handful of
+``LlamaConfig`` fields (``models/llama/model.py:19-23``, ``modules.py:44-45``).  This framework
+owns its model code, so it parses the HF ``config.json`` itself into a small, frozen
+:class:`ModelSpec` that every layer (kernels, KV pool sizing, pipeline planner) shares.  No
+network access and no HF import are needed at runtime.
+
+Unlike the reference (bug B9 in SURVEY.md) ``rms_norm_eps`` is honoured.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import math
+import os
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+
+@dataclass(frozen=True)
+class ModelSpec:
+    """Architecture description shared by every stage of a pipeline."""
+
+    arch: str = "llama"  # "llama" | "gpt2"
+    vocab_size: int = 128256
+    hidden_size: int = 4096
+    intermediate_size: int = 14336
+    num_layers: int = 32
+    num_heads: int = 32
+    num_kv_heads: int = 8
+    head_dim: int = 128
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    rope_scaling: Optional[Tuple[Tuple[str, Any], ...]] = None  # frozen dict items
+    max_position_embeddings: int = 8192
+    tie_word_embeddings: bool = False
+    pad_token_id: Optional[int] = None
+    bos_token_id: Optional[int] = 128000
+    eos_token_id: Optional[int] = 128001
+    hidden_act: str = "silu"
+    pretraining_tp: int = 1
+    attention_bias: bool = False
+    mlp_bias: bool = False
+    name: str = "custom"
+
+    # ------------------------------------------------------------------ derived
+    @property
+    def group_size(self) -> int:
+        return self.num_heads // self.num_kv_heads
+
+    @property
+    def q_size(self) -> int:
+        return self.num_heads * self.head_dim
+
+    @property
+    def kv_size(self) -> int:
+        return self.num_kv_heads * self.head_dim
+
+    @property
+    def qkv_size(self) -> int:
+        return self.q_size + 2 * self.kv_size
+
+    @property
+    def rope_scaling_dict(self) -> Optional[Dict[str, Any]]:
+        return dict(self.rope_scaling) if self.rope_scaling is not None else None
+
+    def layer_param_count(self) -> int:
+        h, i = self.hidden_size, self.intermediate_size
+        if self.arch == "gpt2":
+            return 4 * h * h + 4 * h + 2 * h * i + i + h + 4 * h
+        return h * self.qkv_size + self.q_size * h + 3 * h * i + 2 * h
+
+    def param_count(self) -> int:
+        emb = self.vocab_size * self.hidden_size
+        head = 0 if self.tie_word_embeddings else emb
+        return self.num_layers * self.layer_param_count() + emb + head + self.hidden_size
+
+    def kv_bytes_per_token_per_layer(self, dtype_bytes: int = 2) -> int:
+        return 2 * self.num_kv_heads * self.head_dim * dtype_bytes
+
+    def replace(self, **kw) -> "ModelSpec":
+        return dataclasses.replace(self, **kw)
+
+    def to_dict(self) -> Dict[str, Any]:
+        d = dataclasses.asdict(self)
+        d["rope_scaling"] = self.rope_scaling_dict
+        return d
+
+    # ------------------------------------------------------------------ parsing
+    @classmethod
+    def from_hf_config(cls, cfg: Any) -> "ModelSpec":
+        """Build from a HF ``config.json`` path / directory / dict / ``PretrainedConfig``."""
+        if isinstance(cfg, (str, os.PathLike)):
+            p = str(cfg)
+            if os.path.isdir(p):
+                p = os.path.join(p, "config.json")
+            with open(p) as f:
+                cfg = json.load(f)
+        elif not isinstance(cfg, dict):
+            cfg = cfg.to_dict()
+        mt = cfg.get("model_type", "llama")
+        if mt == "gpt2":
+            h = cfg.get("n_embd", 768)
+            nh = cfg.get("n_head", 12)
+            return cls(
+                arch="gpt2",
+                vocab_size=cfg.get("vocab_size", 50257),
+                hidden_size=h,
+                intermediate_size=cfg.get("n_inner") or 4 * h,
+                num_layers=cfg.get("n_layer", 12),
+                num_heads=nh,
+                num_kv_heads=nh,
+                head_dim=h // nh,
+                rms_norm_eps=cfg.get("layer_norm_epsilon", 1e-5),
+                rope_theta=0.0,
+                max_position_embeddings=cfg.get("n_positions", 1024),
+                tie_word_embeddings=True,
+                pad_token_id=cfg.get("pad_token_id"),
+                bos_token_id=cfg.get("bos_token_id", 50256),
+                eos_token_id=cfg.get("eos_token_id", 50256),
+                hidden_act=cfg.get("activation_function", "gelu_new"),
+                attention_bias=True,
+                mlp_bias=True,
+                name=cfg.get("_name_or_path", "gpt2") or "gpt2",
+            )
+        if mt not in ("llama", "mistral"):
+            raise ValueError(f"unsupported model_type {mt!r} (supported: llama, gpt2)")
+        nh = cfg["num_attention_heads"]
+        h = cfg["hidden_size"]
+        rs = cfg.get("rope_scaling")
+        if rs is not None and rs.get("rope_type", rs.get("type")) in (None, "default"):
+            rs = None
+        eos = cfg.get("eos_token_id")
+        if isinstance(eos, list):
+            eos = eos[0]
+        return cls(
+            arch="llama",
+            vocab_size=cfg["vocab_size"],
+            hidden_size=h,
+            intermediate_size=cfg["intermediate_size"],
+            num_layers=cfg["num_hidden_layers"],
+            num_heads=nh,
+            num_kv_heads=cfg.get("num_key_value_heads") or nh,
+            head_dim=cfg.get("head_dim") or h // nh,
+            rms_norm_eps=cfg.get("rms_norm_eps", 1e-6),
+            rope_theta=float(cfg.get("rope_theta", 10000.0)),
+            rope_scaling=tuple(sorted(rs.items())) if rs else None,
+            max_position_embeddings=cfg.get("max_position_embeddings", 4096),
+            tie_word_embeddings=bool(cfg.get("tie_word_embeddings", False)),
+            pad_token_id=cfg.get("pad_token_id"),
+            bos_token_id=cfg.get("bos_token_id"),
+            eos_token_id=eos,
+            hidden_act=cfg.get("hidden_act", "silu"),
+            pretraining_tp=cfg.get("pretraining_tp", 1) or 1,
+            attention_bias=bool(cfg.get("attention_bias", False)),
+            mlp_bias=bool(cfg.get("mlp_bias", False)),
+            name=cfg.get("_name_or_path", "llama") or "llama",
+        )
+
+    def to_hf_dict(self) -> Dict[str, Any]:
+        """Inverse of :meth:`from_hf_config` (used to write ``config.json`` for random-init dirs)."""
+        if self.arch == "gpt2":
+            return dict(
+                model_type="gpt2", vocab_size=self.vocab_size, n_embd=self.hidden_size,
+                n_inner=self.intermediate_size, n_layer=self.num_layers, n_head=self.num_heads,
+                layer_norm_epsilon=self.rms_norm_eps, n_positions=self.max_position_embeddings,
+                activation_function=self.hidden_act, bos_token_id=self.bos_token_id,
+                eos_token_id=self.eos_token_id,
+            )
+        return dict(
+            model_type="llama", architectures=["LlamaForCausalLM"], vocab_size=self.vocab_size,
+            hidden_size=self.hidden_size, intermediate_size=self.intermediate_size,
+            num_hidden_layers=self.num_layers, num_attention_heads=self.num_heads,
+            num_key_value_heads=self.num_kv_heads, head_dim=self.head_dim,
+            rms_norm_eps=self.rms_norm_eps, rope_theta=self.rope_theta,
+            rope_scaling=self.rope_scaling_dict,
+            max_position_embeddings=self.max_position_embeddings,
+            tie_word_embeddings=self.tie_word_embeddings, pad_token_id=self.pad_token_id,
+            bos_token_id=self.bos_token_id, eos_token_id=self.eos_token_id,
+            hidden_act=self.hidden_act, pretraining_tp=self.pretraining_tp,
+            attention_bias=self.attention_bias, mlp_bias=self.mlp_bias,
+        )
+
+
+_LLAMA3_ROPE = (("factor", 8.0), ("high_freq_factor", 4.0), ("low_freq_factor", 1.0),
+                ("original_max_position_embeddings", 8192), ("rope_type", "llama3"))
+
+PRESETS: Dict[str, ModelSpec] = {
+    "llama-3-8b": ModelSpec(name="llama-3-8b"),
+    "llama-3-70b": ModelSpec(
+        name="llama-3-70b", hidden_size=8192, intermediate_size=28672, num_layers=80,
+        num_heads=64, num_kv_heads=8),
+    "llama-3.1-8b": ModelSpec(name="llama-3.1-8b", rope_scaling=_LLAMA3_ROPE,
+                              max_position_embeddings=131072),
+    "llama-3.1-70b": ModelSpec(
+        name="llama-3.1-70b", hidden_size=8192, intermediate_size=28672, num_layers=80,
+        num_heads=64, num_kv_heads=8, rope_scaling=_LLAMA3_ROPE, max_position_embeddings=131072),
+    "llama-2-7b": ModelSpec(
+        name="llama-2-7b", vocab_size=32000, hidden_size=4096, intermediate_size=11008,
+        num_layers=32, num_heads=32, num_kv_heads=32, rope_theta=10000.0, rms_norm_eps=1e-5,
+        max_position_embeddings=4096, bos_token_id=1, eos_token_id=2),
+    "gpt2": ModelSpec(
+        name="gpt2", arch="gpt2", vocab_size=50257, hidden_size=768, intermediate_size=3072,
+        num_layers=12, num_heads=12, num_kv_heads=12, head_dim=64, rms_norm_eps=1e-5,
+        rope_theta=0.0, max_position_embeddings=1024, tie_word_embeddings=True,
+        bos_token_id=50256, eos_token_id=50256, hidden_act="gelu_new", attention_bias=True,
+        mlp_bias=True),
+    # tiny configs for CPU tests / smoke
+    "tiny-llama": ModelSpec(
+        name="tiny-llama", vocab_size=512, hidden_size=128, intermediate_size=256, num_layers=4,
+        num_heads=4, num_kv_heads=2, head_dim=32, max_position_embeddings=2048,
+        rope_theta=10000.0, bos_token_id=1, eos_token_id=2),
+    "tiny-gpt2": ModelSpec(
+        name="tiny-gpt2", arch="gpt2", vocab_size=512, hidden_size=128, intermediate_size=512,
+        num_layers=4, num_heads=4, num_kv_heads=4, head_dim=32, max_position_embeddings=512,
+        rope_theta=0.0, tie_word_embeddings=True, bos_token_id=1, eos_token_id=2,
+        hidden_act="gelu_new", attention_bias=True, mlp_bias=True),
+}
+
+
+def resolve_model(model: Any) -> ModelSpec:
+    """Accept a preset name, a ``config.json`` path/dir, a dict, a HF config or a ModelSpec."""
+    if isinstance(model, ModelSpec):
+        return model
+    if isinstance(model, str):
+        key = model.lower().replace("meta-llama/", "").replace("_", "-")
+        key = key.replace("meta-llama-3", "llama-3")
+        if key in PRESETS:
+            return PRESETS[key]
+        if os.path.exists(model):
+            return ModelSpec.from_hf_config(model)
+        raise ValueError(f"unknown model {model!r}: not a preset ({sorted(PRESETS)}) nor a path")
+    return ModelSpec.from_hf_config(model)
+
+
+# ---------------------------------------------------------------------------------------------
+# Stage placement (pipeline planner).  The reference's server stub wants to "choose optimal block
+# ids" (server/server.py:7-8) and the worker owns [block_index_start, block_index_end)
+# (server/worker.py:13-14).  On one MI355X node every GPU is identical and fully connected, so the
+# optimal placement is the contiguous, cost-balanced split below.  The first stage also pays the
+# embedding gather and the last stage the LM head, so their layer counts are trimmed by the
+# equivalent layer cost.
+# ---------------------------------------------------------------------------------------------
+def plan_stages(spec: ModelSpec, num_stages: int,
+                weights: Optional[Sequence[float]] = None) -> List[Tuple[int, int]]:
+    """Split ``spec.num_layers`` into ``num_stages`` contiguous ``[start, end)`` ranges.
+
+    ``weights`` (optional, one per stage) expresses relative stage speed (e.g. for a degraded GPU
+    during rebalancing); the default is uniform hardware.
+    """
+    L = spec.num_layers
+    if num_stages < 1:
+        raise ValueError("num_stages must be >= 1")
+    if num_stages > L:
+        raise ValueError(f"cannot split {L} layers into {num_stages} stages")
+    w = list(weights) if weights is not None else [1.0] * num_stages
+    if len(w) != num_stages or min(w) <= 0:
+        raise ValueError("weights must be positive, one per stage")
+    # LM head ≈ vocab*hidden params read per step; express it in layer-equivalents.
+    head_cost = spec.vocab_size * spec.hidden_size / max(1, spec.layer_param_count())
+    extra = [0.0] * num_stages
+    if num_stages > 1:
+        extra[-1] += head_cost
+    total = (L + sum(extra))
+    tw = sum(w)
+    # target layer cost per stage proportional to its speed
+    targets = [total * wi / tw - ei for wi, ei in zip(w, extra)]
+    # round to integers keeping the sum == L and every stage >= 1 layer
+    counts = [max(1, int(math.floor(t))) for t in targets]
+    while sum(counts) < L:
+        # give a layer to the stage furthest below its target
+        i = max(range(num_stages), key=lambda k: targets[k] - counts[k])
+        counts[i] += 1
+    while sum(counts) > L:
+        i = max((k for k in range(num_stages) if counts[k] > 1), key=lambda k: counts[k] - targets[k])
+        counts[i] -= 1
+    out, s = [], 0
+    for c in counts:
+        out.append((s, s + c))
+        s += c
+    return out
+
+
+@dataclass
+class CacheConfig:
+    """KV-cache policy for one stage.
+
+    ``window_length``/``num_sink_tokens`` mirror ``PartialLlamaSinkCache(window_length,
+    num_sink_tokens)`` (reference ``models/llama/cache.py:11``).  ``window_length=0`` means a full
+    (non-evicting) cache sized from HBM.
+    """
+
+    block_size: int = 64
+    num_blocks: Optional[int] = None  # None -> sized from free HBM
+    gpu_memory_utilization: float = 0.90
+    window_length: int = 0
+    num_sink_tokens: int = 0
+    max_chunk: int = 512  # extra ring headroom so a prefill chunk never evicts keys it needs
+    dtype: str = "bf16"
+
+    @property
+    def windowed(self) -> bool:
+        return self.window_length > 0
+
+
+@dataclass
+class ServeConfig:
+    max_batch_size: int = 256
+    max_num_batched_tokens: int = 8192
+    num_micro_batches: int = 0  # 0 -> num_stages (+0) for a full pipeline
+    max_seq_len: int = 8192
+    use_graphs: bool = True
+    graph_batch_sizes: List[int] = field(default_factory=lambda: [1, 2, 4, 8, 16, 32, 64, 96, 128,
+                                                                  160, 192, 224, 256])

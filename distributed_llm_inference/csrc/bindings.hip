@@ -1,0 +1,342 @@
+// Torch bindings for the CDNA4 kernels and the RCCL point-to-point communicator.
+//
+// Every entry point validates device / dtype / contiguity / shapes on the host before launching:
+// a mis-shaped operand must raise a Python error, never become an out-of-bounds GPU access.
+// Kernels run on the caller's current HIP stream (so they are hipGraph-capturable).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include "kernels/kernels.h"
+
+using at::Tensor;
+using c10::optional;
+
+namespace {
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
+#define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
+#define CHECK_I64(t) TORCH_CHECK((t).scalar_type() == at::kLong, #t " must be int64")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+#define CHECK_IN(t) \
+  CHECK_DEV(t);     \
+  CHECK_CONTIG(t)
+
+inline dli::bf16* bp(const Tensor& t) { return reinterpret_cast<dli::bf16*>(t.data_ptr()); }
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+inline void check_rc(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, ": unsupported shape/configuration (rc=", rc, ")");
+}
+
+// ------------------------------------------------------------------------------ normalisation
+void rms_norm(Tensor out, Tensor x, optional<Tensor> residual, Tensor w, double eps) {
+  CHECK_IN(out); CHECK_IN(x); CHECK_IN(w);
+  CHECK_BF16(out); CHECK_BF16(x); CHECK_BF16(w);
+  const int64_t hidden = x.size(-1);
+  const int64_t rows = x.numel() / hidden;
+  TORCH_CHECK(w.numel() == hidden && out.numel() == x.numel(), "rms_norm: shape mismatch");
+  dli::bf16* r = nullptr;
+  if (residual.has_value()) {
+    CHECK_IN(*residual); CHECK_BF16(*residual);
+    TORCH_CHECK(residual->numel() == x.numel(), "rms_norm: residual shape mismatch");
+    r = bp(*residual);
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_rc(dli::launch_rms_norm(bp(out), bp(x), r, bp(w), (float)eps, (int)rows, (int)hidden,
+                                r != nullptr, cur_stream()), "rms_norm");
+}
+
+void layer_norm(Tensor out, Tensor x, optional<Tensor> residual, Tensor w, Tensor b, double eps) {
+  CHECK_IN(out); CHECK_IN(x); CHECK_IN(w); CHECK_IN(b);
+  CHECK_BF16(out); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(b);
+  const int64_t hidden = x.size(-1);
+  const int64_t rows = x.numel() / hidden;
+  TORCH_CHECK(w.numel() == hidden && b.numel() == hidden && out.numel() == x.numel(),
+              "layer_norm: shape mismatch");
+  dli::bf16* r = nullptr;
+  if (residual.has_value()) {
+    CHECK_IN(*residual); CHECK_BF16(*residual);
+    TORCH_CHECK(residual->numel() == x.numel(), "layer_norm: residual shape mismatch");
+    r = bp(*residual);
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_rc(dli::launch_layer_norm(bp(out), bp(x), r, bp(w), bp(b), (float)eps, (int)rows,
+                                  (int)hidden, r != nullptr, cur_stream()), "layer_norm");
+}
+
+// ------------------------------------------------------------------------------ activations
+void silu_mul(Tensor out, Tensor x) {
+  CHECK_IN(out); CHECK_IN(x); CHECK_BF16(out); CHECK_BF16(x);
+  const int64_t two_i = x.size(-1);
+  TORCH_CHECK(two_i % 2 == 0, "silu_mul: last dim must be even");
+  const int64_t rows = x.numel() / two_i;
+  TORCH_CHECK(out.numel() == rows * (two_i / 2), "silu_mul: out shape mismatch");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_rc(dli::launch_silu_mul(bp(out), bp(x), (int)rows, (int)(two_i / 2), cur_stream()),
+           "silu_mul");
+}
+
+void gelu_bias(Tensor out, Tensor x, optional<Tensor> bias) {
+  CHECK_IN(out); CHECK_IN(x); CHECK_BF16(out); CHECK_BF16(x);
+  const int64_t cols = x.size(-1);
+  const int64_t rows = x.numel() / cols;
+  TORCH_CHECK(out.numel() == x.numel(), "gelu: out shape mismatch");
+  dli::bf16* bb = nullptr;
+  if (bias.has_value()) {
+    CHECK_IN(*bias); CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() == cols, "gelu: bias shape mismatch");
+    bb = bp(*bias);
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_rc(dli::launch_gelu_bias(bp(out), bp(x), bb, (int)rows, (int)cols, cur_stream()), "gelu");
+}
+
+void add(Tensor out, Tensor a, Tensor b) {
+  CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
+  CHECK_BF16(out); CHECK_BF16(a); CHECK_BF16(b);
+  TORCH_CHECK(a.numel() == b.numel() && out.numel() == a.numel(), "add: shape mismatch");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
+  check_rc(dli::launch_add(bp(out), bp(a), bp(b), (size_t)a.numel(), cur_stream()), "add");
+}
+
+// ------------------------------------------------------------------------------ rope + cache
+void check_cache(const Tensor& k_cache, const Tensor& v_cache, int64_t nkv, int64_t D) {
+  CHECK_IN(k_cache); CHECK_IN(v_cache); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4, "caches must be 4-D");
+  // k: [blocks, nkv, bs, D]; v: [blocks, nkv, D, bs]
+  TORCH_CHECK(k_cache.size(1) == nkv && k_cache.size(3) == D, "k_cache must be [blocks, nkv, bs, D]");
+  TORCH_CHECK(v_cache.size(0) == k_cache.size(0) && v_cache.size(1) == nkv &&
+                  v_cache.size(2) == D && v_cache.size(3) == k_cache.size(2),
+              "v_cache must be [blocks, nkv, D, bs]");
+}
+
+void rope_cache(Tensor qkv, optional<Tensor> positions, optional<Tensor> slot_mapping,
+                optional<Tensor> cos_sin, Tensor q_out, optional<Tensor> q_sink_out,
+                int64_t window, Tensor k_cache, Tensor v_cache, int64_t nh, int64_t nkv) {
+  CHECK_DEV(qkv); CHECK_BF16(qkv);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "qkv must be [T, *] with unit inner stride");
+  const int64_t T = qkv.size(0);
+  CHECK_IN(q_out); CHECK_BF16(q_out);
+  TORCH_CHECK(q_out.dim() == 3 && q_out.size(0) == T && q_out.size(1) == nh, "q_out must be [T, nh, D]");
+  const int64_t D = q_out.size(2);
+  TORCH_CHECK(qkv.size(1) >= (nh + 2 * nkv) * D, "qkv too narrow for nh/nkv/D");
+  check_cache(k_cache, v_cache, nkv, D);
+  dli::RopeCacheParams p{};
+  p.qkv = bp(qkv);
+  p.qkv_stride = qkv.stride(0);
+  if (positions.has_value()) {
+    CHECK_IN(*positions); CHECK_I32(*positions);
+    TORCH_CHECK(positions->numel() == T, "positions must have T entries");
+    p.positions = positions->data_ptr<int>();
+  }
+  if (slot_mapping.has_value()) {
+    CHECK_IN(*slot_mapping); CHECK_I64(*slot_mapping);
+    TORCH_CHECK(slot_mapping->numel() == T, "slot_mapping must have T entries");
+    p.slot_mapping = reinterpret_cast<const long*>(slot_mapping->data_ptr<int64_t>());
+  }
+  if (cos_sin.has_value()) {
+    CHECK_IN(*cos_sin); CHECK_F32(*cos_sin);
+    TORCH_CHECK(cos_sin->dim() == 2 && cos_sin->size(1) == D, "cos_sin must be [max_pos, D]");
+    TORCH_CHECK(positions.has_value(), "rope needs positions");
+    p.cos_sin = cos_sin->data_ptr<float>();
+    p.max_pos = (int)cos_sin->size(0);
+  }
+  p.q_out = bp(q_out);
+  if (q_sink_out.has_value()) {
+    CHECK_IN(*q_sink_out); CHECK_BF16(*q_sink_out);
+    TORCH_CHECK(q_sink_out->sizes() == q_out.sizes(), "q_sink_out shape mismatch");
+    TORCH_CHECK(window > 0, "q_sink_out requires window > 0");
+    p.q_sink_out = bp(*q_sink_out);
+  }
+  p.window = (int)window;
+  p.k_cache = bp(k_cache);
+  p.v_cache = bp(v_cache);
+  p.nh = (int)nh;
+  p.nkv = (int)nkv;
+  p.D = (int)D;
+  p.bs = (int)k_cache.size(2);
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  check_rc(dli::launch_rope_cache(p, (int)T, cur_stream()), "rope_cache");
+}
+
+// ------------------------------------------------------------------------------ attention
+dli::AttnParams attn_common(Tensor& out, Tensor& q, optional<Tensor>& q_sink, Tensor& k_cache,
+                            Tensor& v_cache, Tensor& block_tables, Tensor& seq_lens, double scale,
+                            int64_t n_sink, int64_t sink_pad, int64_t ring, int64_t window,
+                            int64_t& D) {
+  CHECK_IN(out); CHECK_IN(q); CHECK_BF16(out); CHECK_BF16(q);
+  TORCH_CHECK(q.dim() == 3, "q must be [T, nh, D]");
+  TORCH_CHECK(out.sizes() == q.sizes(), "out must match q");
+  const int64_t nh = q.size(1);
+  D = q.size(2);
+  const int64_t nkv = k_cache.size(1);
+  TORCH_CHECK(nkv > 0 && nh % nkv == 0, "nh must be a multiple of nkv");
+  check_cache(k_cache, v_cache, nkv, D);
+  CHECK_IN(block_tables); CHECK_I32(block_tables); CHECK_IN(seq_lens); CHECK_I32(seq_lens);
+  TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) == seq_lens.size(0),
+              "block_tables must be [B, max_blocks]");
+  dli::AttnParams p{};
+  p.q = bp(q);
+  if (ring > 0) {
+    TORCH_CHECK(q_sink.has_value() || n_sink == 0, "window mode with sinks needs q_sink");
+    TORCH_CHECK(window > n_sink && sink_pad >= n_sink && sink_pad % 32 == 0 && ring % 32 == 0,
+                "invalid window configuration");
+  }
+  if (q_sink.has_value()) {
+    CHECK_IN(*q_sink); CHECK_BF16(*q_sink);
+    TORCH_CHECK(q_sink->sizes() == q.sizes(), "q_sink must match q");
+    p.q_sink = bp(*q_sink);
+  }
+  p.k_cache = bp(k_cache);
+  p.v_cache = bp(v_cache);
+  p.out = bp(out);
+  p.block_tables = block_tables.data_ptr<int>();
+  p.bt_stride = (int)block_tables.size(1);
+  p.seq_lens = seq_lens.data_ptr<int>();
+  p.scale_log2 = (float)(scale * 1.4426950408889634);
+  p.nh = (int)nh;
+  p.nkv = (int)nkv;
+  p.bs = (int)k_cache.size(2);
+  p.n_sink = (int)n_sink;
+  p.sink_pad = (int)sink_pad;
+  p.ring = (int)ring;
+  p.window = (int)window;
+  p.num_splits = 1;
+  TORCH_CHECK(p.bs % 32 == 0, "cache block size must be a multiple of 32");
+  return p;
+}
+
+void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, Tensor v_cache,
+                 Tensor block_tables, Tensor seq_lens, double scale, int64_t n_sink,
+                 int64_t sink_pad, int64_t ring, int64_t window, int64_t num_splits,
+                 optional<Tensor> part_o, optional<Tensor> part_ml) {
+  int64_t D = 0;
+  auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
+                       sink_pad, ring, window, D);
+  const int64_t B = q.size(0);
+  TORCH_CHECK(seq_lens.numel() == B, "decode: one token per sequence (seq_lens must have T entries)");
+  TORCH_CHECK(num_splits >= 1, "num_splits >= 1");
+  p.num_splits = (int)num_splits;
+  if (num_splits > 1) {
+    TORCH_CHECK(part_o.has_value() && part_ml.has_value(), "split-K needs workspaces");
+    CHECK_IN(*part_o); CHECK_IN(*part_ml); CHECK_F32(*part_o); CHECK_F32(*part_ml);
+    TORCH_CHECK(part_o->numel() >= num_splits * B * p.nh * D, "part_o workspace too small");
+    TORCH_CHECK(part_ml->numel() >= num_splits * B * p.nh * 2, "part_ml workspace too small");
+    p.part_o = part_o->data_ptr<float>();
+    p.part_ml = part_ml->data_ptr<float>();
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  check_rc(dli::launch_attn_decode(p, (int)B, (int)D, cur_stream()), "attn_decode");
+}
+
+void attn_prefill(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, Tensor v_cache,
+                  Tensor block_tables, Tensor seq_lens, Tensor q_start, int64_t max_q,
+                  double scale, int64_t n_sink, int64_t sink_pad, int64_t ring, int64_t window) {
+  int64_t D = 0;
+  auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
+                       sink_pad, ring, window, D);
+  CHECK_IN(q_start); CHECK_I32(q_start);
+  const int64_t B = seq_lens.numel();
+  TORCH_CHECK(q_start.numel() == B + 1, "q_start must have B+1 entries");
+  p.q_start = q_start.data_ptr<int>();
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  check_rc(dli::launch_attn_prefill(p, (int)B, (int)max_q, (int)D, cur_stream()), "attn_prefill");
+}
+
+// ------------------------------------------------------------------------------ sampling
+void sample(Tensor out_tokens, optional<Tensor> out_logprobs, Tensor logits,
+            optional<Tensor> temperature, optional<Tensor> top_k, optional<Tensor> top_p,
+            optional<Tensor> seeds, optional<Tensor> step) {
+  CHECK_DEV(logits);
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [B, V] row-major");
+  TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat,
+              "logits must be bf16 or f32");
+  const int64_t B = logits.size(0);
+  CHECK_IN(out_tokens); CHECK_I32(out_tokens);
+  TORCH_CHECK(out_tokens.numel() == B, "out_tokens must have B entries");
+  dli::SampleParams p{};
+  p.logits = logits.data_ptr();
+  p.logits_is_f32 = logits.scalar_type() == at::kFloat;
+  p.row_stride = logits.stride(0);
+  p.V = (int)logits.size(1);
+  auto opt_f = [&](optional<Tensor>& t, const char* n) -> const float* {
+    if (!t.has_value()) return nullptr;
+    CHECK_IN(*t); CHECK_F32(*t);
+    TORCH_CHECK(t->numel() == B, n, " must have B entries");
+    return t->data_ptr<float>();
+  };
+  p.temperature = opt_f(temperature, "temperature");
+  p.top_p = opt_f(top_p, "top_p");
+  if (top_k.has_value()) {
+    CHECK_IN(*top_k); CHECK_I32(*top_k);
+    TORCH_CHECK(top_k->numel() == B, "top_k must have B entries");
+    p.top_k = top_k->data_ptr<int>();
+  }
+  if (seeds.has_value()) {
+    CHECK_IN(*seeds); CHECK_I64(*seeds);
+    TORCH_CHECK(seeds->numel() == B, "seeds must have B entries");
+    p.seeds = reinterpret_cast<const unsigned long long*>(seeds->data_ptr<int64_t>());
+  }
+  if (step.has_value()) {
+    CHECK_IN(*step); CHECK_I64(*step);
+    p.step = reinterpret_cast<const long*>(step->data_ptr<int64_t>());
+  }
+  p.out_tokens = out_tokens.data_ptr<int>();
+  if (out_logprobs.has_value()) {
+    CHECK_IN(*out_logprobs); CHECK_F32(*out_logprobs);
+    TORCH_CHECK(out_logprobs->numel() == B, "out_logprobs must have B entries");
+    p.out_logprobs = out_logprobs->data_ptr<float>();
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  check_rc(dli::launch_sample(p, (int)B, cur_stream()), "sample");
+}
+
+// ------------------------------------------------------------------------------ fp8 quant
+void quant_rowwise(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> residual,
+                   optional<Tensor> norm_w, double eps) {
+  CHECK_IN(q_out); CHECK_IN(scale); CHECK_IN(x); CHECK_BF16(x); CHECK_F32(scale);
+  TORCH_CHECK(q_out.element_size() == 1, "q_out must be an 8-bit tensor");
+  const int64_t K = x.size(-1);
+  const int64_t rows = x.numel() / K;
+  TORCH_CHECK(q_out.numel() == x.numel() && scale.numel() == rows, "quant: shape mismatch");
+  dli::bf16* r = nullptr;
+  if (residual.has_value()) {
+    CHECK_IN(*residual); CHECK_BF16(*residual);
+    TORCH_CHECK(residual->numel() == x.numel(), "quant: residual shape mismatch");
+    r = bp(*residual);
+  }
+  const dli::bf16* w = nullptr;
+  if (norm_w.has_value()) {
+    CHECK_IN(*norm_w); CHECK_BF16(*norm_w);
+    TORCH_CHECK(norm_w->numel() == K, "quant: norm weight shape mismatch");
+    w = bp(*norm_w);
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_rc(dli::launch_quant_rowwise(reinterpret_cast<uint8_t*>(q_out.data_ptr()),
+                                     scale.data_ptr<float>(), bp(x), r, w, (float)eps, (int)rows,
+                                     (int)K, r != nullptr, cur_stream()),
+           "quant_rowwise");
+}
+
+}  // namespace
+
+void register_rccl(pybind11::module_& m);  // comm/rccl_p2p.hip
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "CDNA4 (gfx950) kernels of distributed_llm_inference";
+  m.def("rms_norm", &rms_norm, "RMSNorm (+fused residual add)", py::arg("out"), py::arg("x"),
+        py::arg("residual"), py::arg("w"), py::arg("eps"));
+  m.def("layer_norm", &layer_norm, "LayerNorm (+fused residual add)");
+  m.def("silu_mul", &silu_mul, "SwiGLU: out = silu(x[:, :I]) * x[:, I:]");
+  m.def("gelu_bias", &gelu_bias, "gelu_tanh(x + bias)");
+  m.def("add", &add, "out = a + b");
+  m.def("rope_cache", &rope_cache, "fused RoPE + paged KV cache write");
+  m.def("attn_decode", &attn_decode, "paged GQA decode attention (split-K)");
+  m.def("attn_prefill", &attn_prefill, "paged causal prefill attention (varlen)");
+  m.def("sample", &sample, "greedy / temperature / top-k / top-p sampling");
+  m.def("quant_rowwise", &quant_rowwise, "row-wise fp8 e4m3 quantisation (+fused RMSNorm)");
+  register_rccl(m);
+}

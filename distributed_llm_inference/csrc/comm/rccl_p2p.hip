@@ -1,0 +1,143 @@
+// RCCL communicator owned by the framework (not by torch.distributed).
+//
+// The reference moves hidden states between stages over hivemind/libp2p + protobuf (SURVEY N5,
+// §5.8).  On one MI355X node every GPU pair has a direct xGMI link, so stage i -> i+1 activations
+// and the last-stage -> stage-0 token feedback are plain RCCL point-to-point transfers.  Owning the
+// ncclComm_t here (instead of going through ProcessGroupNCCL) lets the runtime:
+//   * put send/recv on its own comm HIP stream, ordered against compute with HIP events;
+//   * capture send/recv into the same hipGraph as the stage's compute;
+//   * create exactly one communicator for the whole pipeline (no lazy per-pair communicators).
+// The unique id is distributed by the launcher through the torch.distributed TCP store.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <rccl/rccl.h>
+
+#include <string>
+
+namespace {
+
+#define RCCL_CHECK(expr)                                                              \
+  do {                                                                                \
+    ncclResult_t _r = (expr);                                                         \
+    TORCH_CHECK(_r == ncclSuccess, "RCCL error ", ncclGetErrorString(_r), " in ", #expr); \
+  } while (0)
+
+inline hipStream_t resolve_stream(int64_t s) {
+  return s ? reinterpret_cast<hipStream_t>(s) : c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+}
+
+ncclDataType_t to_nccl(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ncclFloat32;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kHalf: return ncclFloat16;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    default: return ncclUint8;
+  }
+}
+
+class RcclComm {
+ public:
+  RcclComm(const std::string& uid, int rank, int world, int device)
+      : rank_(rank), world_(world), device_(device) {
+    TORCH_CHECK(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id size");
+    ncclUniqueId id;
+    memcpy(&id, uid.data(), sizeof(id));
+    TORCH_CHECK(hipSetDevice(device) == hipSuccess, "hipSetDevice failed");
+    RCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+  }
+  ~RcclComm() { destroy(); }
+
+  void destroy() {
+    if (comm_) {
+      ncclCommDestroy(comm_);
+      comm_ = nullptr;
+    }
+  }
+  void abort() {
+    if (comm_) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+  }
+
+  void send(const at::Tensor& t, int peer, int64_t stream) {
+    check(t);
+    RCCL_CHECK(ncclSend(t.data_ptr(), t.nbytes(), ncclUint8, peer, comm_, resolve_stream(stream)));
+  }
+  void recv(at::Tensor& t, int peer, int64_t stream) {
+    check(t);
+    RCCL_CHECK(ncclRecv(t.data_ptr(), t.nbytes(), ncclUint8, peer, comm_, resolve_stream(stream)));
+  }
+  void group_start() { RCCL_CHECK(ncclGroupStart()); }
+  void group_end() { RCCL_CHECK(ncclGroupEnd()); }
+
+  void all_reduce(at::Tensor& t, int64_t stream) {
+    check(t);
+    RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t), ncclSum, comm_,
+                             resolve_stream(stream)));
+  }
+  void broadcast(at::Tensor& t, int root, int64_t stream) {
+    check(t);
+    RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.nbytes(), ncclUint8, root, comm_,
+                             resolve_stream(stream)));
+  }
+  void all_gather(const at::Tensor& in, at::Tensor& out, int64_t stream) {
+    check(in);
+    check(out);
+    TORCH_CHECK(out.nbytes() == in.nbytes() * (size_t)world_, "all_gather: out size mismatch");
+    RCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.nbytes(), ncclUint8, comm_,
+                             resolve_stream(stream)));
+  }
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+
+ private:
+  void check(const at::Tensor& t) const {
+    TORCH_CHECK(comm_ != nullptr, "communicator destroyed");
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RCCL tensors must be contiguous GPU tensors");
+    TORCH_CHECK(t.get_device() == device_, "tensor on wrong device");
+  }
+  ncclComm_t comm_ = nullptr;
+  int rank_, world_, device_;
+};
+
+pybind11::bytes get_unique_id() {
+  ncclUniqueId id;
+  RCCL_CHECK(ncclGetUniqueId(&id));
+  return pybind11::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+int rccl_version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return v;
+}
+
+}  // namespace
+
+void register_rccl(pybind11::module_& m) {
+  m.def("rccl_unique_id", &get_unique_id);
+  m.def("rccl_version", &rccl_version);
+  pybind11::class_<RcclComm>(m, "RcclComm")
+      .def(pybind11::init<const std::string&, int, int, int>(), pybind11::arg("uid"),
+           pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("device"))
+      .def("send", &RcclComm::send, pybind11::arg("t"), pybind11::arg("peer"),
+           pybind11::arg("stream") = 0)
+      .def("recv", &RcclComm::recv, pybind11::arg("t"), pybind11::arg("peer"),
+           pybind11::arg("stream") = 0)
+      .def("group_start", &RcclComm::group_start)
+      .def("group_end", &RcclComm::group_end)
+      .def("all_reduce", &RcclComm::all_reduce, pybind11::arg("t"), pybind11::arg("stream") = 0)
+      .def("broadcast", &RcclComm::broadcast, pybind11::arg("t"), pybind11::arg("root"),
+           pybind11::arg("stream") = 0)
+      .def("all_gather", &RcclComm::all_gather, pybind11::arg("inp"), pybind11::arg("out"),
+           pybind11::arg("stream") = 0)
+      .def("destroy", &RcclComm::destroy)
+      .def("abort", &RcclComm::abort)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world", &RcclComm::world);
+}

@@ -1,0 +1,417 @@
+// Paged attention for CDNA4 (gfx950): decode (split-K flash-decoding) and prefill (causal flash).
+//
+// Replaces the reference's eager attention core (modules.py:87-97: repeat_kv materialisation,
+// QK^T/sqrt(D) + additive mask, fp32 softmax, PV) and its mask builder (model.py:78-143).
+//   * GQA is native: one workgroup serves all q heads of a kv head (decode) — K/V are read once.
+//   * causality / window / padding come from seq_lens and slot arithmetic, never from a mask tensor.
+//   * both products run on MFMA v_mfma_f32_16x16x32_bf16 in the "swapped" orientation
+//        S^T[key, q] = K[key, d] . Q^T[d, q]        (A = K rows, B = Q^T)
+//        O^T[d, q]  += V^T[d, key] . P^T[key, q]     (A = V^T rows, B = P^T)
+//     With K cached as [blocks, nkv, bs, D] and V cached *transposed* as [blocks, nkv, D, bs], every
+//     MFMA A operand is one 16-byte global load per lane, and the S^T accumulator is re-used as the
+//     P^T operand with no lane movement: the K rows of the two 16-key S tiles of a 32-key step are
+//     permuted (row i of tile t holds key 8(i>>2) + 4t + (i&3)) so that lane (h=l>>4, col=l&15)
+//     ends up holding the scores of keys 8h..8h+7 for query column col — exactly the k-slice the
+//     P^T operand of the next MFMA needs (cdna_hip_programming.md §3, "accumulator as operand").
+//   * softmax is online (running max per column, exp2 with log2(e) folded into the scale); the
+//     row max needs two xor-shuffles (lanes 16 and 32 apart share a column); row sums are kept
+//     per lane and reduced once at the end.
+//   * Attention-sink (StreamingLLM) windows, the reference's PartialLlamaSinkCache semantics
+//     (cache.py:64-135), are handled in slot space: sink slots [0, n_sink) are scored with
+//     q_sink (q rotated at min(pos, W-1)); rolling slots live in a ring of `ring` slots starting
+//     at `sink_pad`, stored rotated at their absolute positions and scored with q rotated at its
+//     absolute position — relative distances are then exactly the re-rotated ones, with no
+//     re-rotation pass over the cache.
+#include "kernels.h"
+
+namespace dli {
+
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 zero8() {
+  i32x4 z = {0, 0, 0, 0};
+  return __builtin_bit_cast(bf16x8, z);
+}
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Absolute token index of ring slot `u` (window mode) given the sequence length L.
+__device__ __forceinline__ int ring_abs(int u, int L, const AttnParams& p) {
+  const int o = u - p.sink_pad;
+  const int newest = (L - 1 - p.n_sink) % p.ring;
+  int back = newest - o;
+  if (back < 0) back += p.ring;
+  return (L - 1) - back;
+}
+
+// One 32-key step of online-softmax attention for the 16 query columns held by this wave.
+//   kbase/vbase: start of this kv head's page in the K / V^T cache, offk: slot offset of the step
+//   inside the page.  valid(j) decides visibility of key 8h+j (h = lane>>4) for this lane's column.
+template <int D>
+struct WaveState {
+  f32x4 o[D / 16];
+  float m, l;
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int e = 0; e < D / 16; ++e) o[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    m = -1e30f;
+    l = 0.f;
+  }
+};
+
+template <int D>
+__device__ __forceinline__ void attn_step(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
+                                          const bf16* __restrict__ kbase,
+                                          const bf16* __restrict__ vbase, int offk, int bs,
+                                          float scale_log2, unsigned valid_mask) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 15, h4 = lane >> 4;
+  // ---- issue all loads of the step (K rows permuted, V^T rows) ----
+  bf16x8 kf[2][D / 32];
+  const int krow0 = offk + 8 * (col >> 2) + (col & 3);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int c = 0; c < D / 32; ++c)
+      kf[t][c] = *reinterpret_cast<const bf16x8*>(kbase + (size_t)(krow0 + 4 * t) * D + 32 * c +
+                                                  8 * h4);
+  bf16x8 vf[D / 16];
+#pragma unroll
+  for (int e = 0; e < D / 16; ++e)
+    vf[e] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)(16 * e + col) * bs + offk + 8 * h4);
+  // ---- S^T = K . Q^T ----
+  f32x4 s[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < D / 32; ++c) s[t] = mfma16(kf[t][c], qf[c], s[t]);
+  }
+  // ---- online softmax over the 8 keys 8h..8h+7 of this lane ----
+  float x[8];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = s[j >> 2][j & 3] * scale_log2;
+    x[j] = ((valid_mask >> j) & 1u) ? v : -INFINITY;
+    mx = fmaxf(mx, x[j]);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float m_new = fmaxf(st.m, mx);
+  const float alpha = __builtin_amdgcn_exp2f(st.m - m_new);
+  bf16x8 pb;
+  float ps = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float pj = __builtin_amdgcn_exp2f(x[j] - m_new);
+    ps += pj;
+    pb[j] = (bf16)pj;
+  }
+  st.l = st.l * alpha + ps;
+  st.m = m_new;
+  // ---- O^T += V^T . P^T ----
+#pragma unroll
+  for (int e = 0; e < D / 16; ++e) {
+    st.o[e] *= alpha;
+    st.o[e] = mfma16(vf[e], pb, st.o[e]);
+  }
+}
+
+// ===========================================================================================
+// Decode: grid (num_splits, nkv * head_groups, B), 256 threads.  The 4 waves split the keys of the
+// (sequence, kv-head, split) in interleaved 32-key steps and are merged through LDS at the end.
+// ===========================================================================================
+template <int D, bool WIN>
+__global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p) {
+  const int split = blockIdx.x;
+  const int b = blockIdx.z;
+  const int G = p.nh / p.nkv;
+  const int hgroups = (G + 15) >> 4;
+  const int kvh = blockIdx.y / hgroups;
+  const int g0 = (blockIdx.y % hgroups) * 16;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, h4 = lane >> 4;
+  const bool col_valid = (g0 + col) < G;
+  const int qh = kvh * G + g0 + (col_valid ? col : 0);
+  const int L = p.seq_lens[b];
+  const int* bt = p.block_tables + (size_t)b * p.bt_stride;
+
+  __shared__ float sm_o[4][D][16];
+  __shared__ float sm_m[4][16];
+  __shared__ float sm_l[4][16];
+
+  WaveState<D> st;
+  st.init();
+
+  if (L > 0) {
+    bf16x8 qf[D / 32];
+    const bf16* qrow = p.q + ((size_t)b * p.nh + qh) * D;
+#pragma unroll
+    for (int c = 0; c < D / 32; ++c)
+      qf[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qrow + 32 * c + 8 * h4) : zero8();
+
+    const size_t head_stride_k = (size_t)p.bs * D;  // per (block, kv head)
+    // ---- rolling / full segment ----
+    int seg_base, seg_len;
+    if (WIN) {
+      seg_base = p.sink_pad;
+      seg_len = L > p.n_sink ? min(p.ring, L - p.n_sink) : 0;
+    } else {
+      seg_base = 0;
+      seg_len = L;
+    }
+    const int nsteps = (seg_len + 31) >> 5;
+    const int per_split = (nsteps + p.num_splits - 1) / p.num_splits;
+    const int s_lo = split * per_split;
+    const int s_hi = min(nsteps, s_lo + per_split);
+    const int pq = L - 1;
+    for (int sidx = s_lo + w; sidx < s_hi; sidx += 4) {
+      const int u0 = seg_base + sidx * 32;
+      const int page = bt[u0 / p.bs];
+      const int offk = u0 % p.bs;
+      const bf16* kbase = p.k_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
+      const bf16* vbase = p.v_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
+      unsigned vm = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int u = u0 + 8 * h4 + j;
+        bool ok = (u - seg_base) < seg_len;
+        if (WIN && ok) {
+          const int a = ring_abs(u, L, p);
+          ok = a >= p.n_sink && (pq - a) < (p.window - p.n_sink);
+        }
+        vm |= (ok ? 1u : 0u) << j;
+      }
+      attn_step<D>(st, qf, kbase, vbase, offk, p.bs, p.scale_log2, vm);
+    }
+    // ---- sink segment (window mode): split 0, wave 0 ----
+    if (WIN && split == 0 && w == 0 && p.n_sink > 0) {
+      bf16x8 qs[D / 32];
+      const bf16* qsrow = p.q_sink + ((size_t)b * p.nh + qh) * D;
+#pragma unroll
+      for (int c = 0; c < D / 32; ++c)
+        qs[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qsrow + 32 * c + 8 * h4) : zero8();
+      const int nS = min(p.n_sink, L);
+      for (int u0 = 0; u0 < nS; u0 += 32) {
+        const int page = bt[u0 / p.bs];
+        const int offk = u0 % p.bs;
+        const bf16* kbase = p.k_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
+        const bf16* vbase = p.v_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
+        unsigned vm = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vm |= ((u0 + 8 * h4 + j) < nS ? 1u : 0u) << j;
+        attn_step<D>(st, qs, kbase, vbase, offk, p.bs, p.scale_log2, vm);
+      }
+    }
+  }
+  // ---- merge the 4 waves through LDS ----
+  float lsum = st.l;
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (h4 == 0) {
+    sm_m[w][col] = st.m;
+    sm_l[w][col] = lsum;
+  }
+#pragma unroll
+  for (int e = 0; e < D / 16; ++e)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sm_o[w][16 * e + 4 * h4 + r][col] = st.o[e][r];
+  __syncthreads();
+  for (int it = threadIdx.x; it < 16 * D; it += 256) {
+    const int c = it / D, d = it % D;  // consecutive threads -> consecutive d (coalesced out)
+    if (g0 + c >= G) continue;
+    const float M = fmaxf(fmaxf(sm_m[0][c], sm_m[1][c]), fmaxf(sm_m[2][c], sm_m[3][c]));
+    float O = 0.f, Lt = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = __builtin_amdgcn_exp2f(sm_m[ww][c] - M);
+      O += f * sm_o[ww][d][c];
+      Lt += f * sm_l[ww][c];
+    }
+    const int head = kvh * G + g0 + c;
+    if (p.num_splits == 1) {
+      p.out[((size_t)b * p.nh + head) * D + d] = (bf16)(Lt > 0.f ? O / Lt : 0.f);
+    } else {
+      const size_t T = gridDim.z;
+      p.part_o[(((size_t)split * T + b) * p.nh + head) * D + d] = O;
+      if (d == 0) {
+        float* ml = p.part_ml + (((size_t)split * T + b) * p.nh + head) * 2;
+        ml[0] = M;
+        ml[1] = Lt;
+      }
+    }
+  }
+}
+
+// Merge split-K partials: grid (T * nh), D threads.
+template <int D>
+__global__ void __launch_bounds__(128) attn_combine_kernel(AttnParams p, int T) {
+  const int th = blockIdx.x;  // t * nh + head
+  const int d = threadIdx.x;
+  float M = -1e30f;
+  for (int s = 0; s < p.num_splits; ++s)
+    M = fmaxf(M, p.part_ml[((size_t)s * T * p.nh + th) * 2]);
+  float O = 0.f, Lt = 0.f;
+  for (int s = 0; s < p.num_splits; ++s) {
+    const float* ml = p.part_ml + ((size_t)s * T * p.nh + th) * 2;
+    const float f = __builtin_amdgcn_exp2f(ml[0] - M);
+    Lt += f * ml[1];
+    O += f * p.part_o[((size_t)s * T * p.nh + th) * D + d];
+  }
+  p.out[(size_t)th * D + d] = (bf16)(Lt > 0.f ? O / Lt : 0.f);
+}
+
+// ===========================================================================================
+// Prefill (varlen, chunked): grid (ceil(max_q/64), nh, B), 256 threads.  Wave w owns 16
+// consecutive query tokens of one q head; keys are visited causally up to the wave's last token.
+// ===========================================================================================
+template <int D, bool WIN>
+__global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p) {
+  const int b = blockIdx.z;
+  const int qh = blockIdx.y;
+  const int G = p.nh / p.nkv;
+  const int kvh = qh / G;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, h4 = lane >> 4;
+  const int qs0 = p.q_start[b];
+  const int qlen = p.q_start[b + 1] - qs0;
+  const int tok0 = blockIdx.x * 64 + w * 16;
+  if (tok0 >= qlen) return;  // whole wave idle (no LDS / barriers in this kernel)
+  const int L = p.seq_lens[b];
+  const int tok = tok0 + col;
+  const bool col_valid = tok < qlen;
+  const int pq = L - qlen + (col_valid ? tok : qlen - 1);  // this column's absolute position
+  const int pq_max = L - qlen + min(qlen - 1, tok0 + 15);
+  const int* bt = p.block_tables + (size_t)b * p.bt_stride;
+  const size_t head_stride_k = (size_t)p.bs * D;
+
+  bf16x8 qf[D / 32];
+  const bf16* qrow = p.q + ((size_t)(qs0 + (col_valid ? tok : 0)) * p.nh + qh) * D;
+#pragma unroll
+  for (int c = 0; c < D / 32; ++c)
+    qf[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qrow + 32 * c + 8 * h4) : zero8();
+
+  WaveState<D> st;
+  st.init();
+  if (!WIN) {
+    const int nkeys = pq_max + 1;  // slots 0..pq_max
+    for (int u0 = 0; u0 < nkeys; u0 += 32) {
+      const int page = bt[u0 / p.bs];
+      const int offk = u0 % p.bs;
+      const bf16* kbase = p.k_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
+      const bf16* vbase = p.v_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
+      unsigned vm = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vm |= ((u0 + 8 * h4 + j) <= pq ? 1u : 0u) << j;
+      attn_step<D>(st, qf, kbase, vbase, offk, p.bs, p.scale_log2, vm);
+    }
+  } else {
+    const int seg_len = L > p.n_sink ? min(p.ring, L - p.n_sink) : 0;
+    for (int s0 = 0; s0 < seg_len; s0 += 32) {
+      const int u0 = p.sink_pad + s0;
+      const int page = bt[u0 / p.bs];
+      const int offk = u0 % p.bs;
+      const bf16* kbase = p.k_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
+      const bf16* vbase = p.v_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
+      unsigned vm = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int u = u0 + 8 * h4 + j;
+        bool ok = (u - p.sink_pad) < seg_len;
+        if (ok) {
+          const int a = ring_abs(u, L, p);
+          ok = a >= p.n_sink && a <= pq && (pq - a) < (p.window - p.n_sink);
+        }
+        vm |= (ok ? 1u : 0u) << j;
+      }
+      attn_step<D>(st, qf, kbase, vbase, offk, p.bs, p.scale_log2, vm);
+    }
+    if (p.n_sink > 0) {
+      bf16x8 qsf[D / 32];
+      const bf16* qsrow = p.q_sink + ((size_t)(qs0 + (col_valid ? tok : 0)) * p.nh + qh) * D;
+#pragma unroll
+      for (int c = 0; c < D / 32; ++c)
+        qsf[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qsrow + 32 * c + 8 * h4) : zero8();
+      const int nS = min(p.n_sink, L);
+      for (int u0 = 0; u0 < nS; u0 += 32) {
+        const int page = bt[u0 / p.bs];
+        const int offk = u0 % p.bs;
+        const bf16* kbase = p.k_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
+        const bf16* vbase = p.v_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
+        unsigned vm = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int u = u0 + 8 * h4 + j;
+          vm |= (u < nS && u <= pq ? 1u : 0u) << j;
+        }
+        attn_step<D>(st, qsf, kbase, vbase, offk, p.bs, p.scale_log2, vm);
+      }
+    }
+  }
+  float lsum = st.l;
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (col_valid) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16* orow = p.out + ((size_t)(qs0 + tok) * p.nh + qh) * D;
+#pragma unroll
+    for (int e = 0; e < D / 16; ++e) {
+      bf16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (bf16)(st.o[e][r] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 16 * e + 4 * h4) = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+template <int D>
+static int launch_decode_d(const AttnParams& p, int B, hipStream_t stream) {
+  const int G = p.nh / p.nkv;
+  const int hgroups = (G + 15) / 16;
+  dim3 grid(p.num_splits, p.nkv * hgroups, B);
+  if (p.ring > 0)
+    attn_decode_kernel<D, true><<<grid, 256, 0, stream>>>(p);
+  else
+    attn_decode_kernel<D, false><<<grid, 256, 0, stream>>>(p);
+  if (p.num_splits > 1) attn_combine_kernel<D><<<B * p.nh, D, 0, stream>>>(p, B);
+  return 0;
+}
+
+int launch_attn_decode(const AttnParams& p, int B, int D, hipStream_t stream) {
+  if (B == 0) return 0;
+  if (p.bs % 32 != 0 || (p.ring > 0 && (p.sink_pad % 32 != 0 || p.ring % 32 != 0))) return -2;
+  switch (D) {
+    case 32: return launch_decode_d<32>(p, B, stream);
+    case 64: return launch_decode_d<64>(p, B, stream);
+    case 128: return launch_decode_d<128>(p, B, stream);
+    default: return -1;
+  }
+}
+
+template <int D>
+static int launch_prefill_d(const AttnParams& p, int B, int max_q, hipStream_t stream) {
+  dim3 grid((max_q + 63) / 64, p.nh, B);
+  if (p.ring > 0)
+    attn_prefill_kernel<D, true><<<grid, 256, 0, stream>>>(p);
+  else
+    attn_prefill_kernel<D, false><<<grid, 256, 0, stream>>>(p);
+  return 0;
+}
+
+int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_t stream) {
+  if (B == 0 || max_q == 0) return 0;
+  if (p.bs % 32 != 0 || (p.ring > 0 && (p.sink_pad % 32 != 0 || p.ring % 32 != 0))) return -2;
+  switch (D) {
+    case 32: return launch_prefill_d<32>(p, B, max_q, stream);
+    case 64: return launch_prefill_d<64>(p, B, max_q, stream);
+    case 128: return launch_prefill_d<128>(p, B, max_q, stream);
+    default: return -1;
+  }
+}
+
+}  // namespace dli

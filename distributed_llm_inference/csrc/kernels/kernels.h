@@ -1,0 +1,70 @@
+// Launch interface of the CDNA4 kernels (shared by the .hip kernel TUs and the torch bindings).
+#pragma once
+#include "common.h"
+
+namespace dli {
+
+struct AttnParams {
+  const bf16* q;        // [T, nh, D]
+  const bf16* q_sink;   // [T, nh, D] or nullptr (window mode only)
+  const bf16* k_cache;  // [blocks, nkv, bs, D]
+  const bf16* v_cache;  // [blocks, nkv, D, bs]
+  bf16* out;            // [T, nh, D]
+  const int* block_tables;  // [B, bt_stride]
+  int bt_stride;
+  const int* seq_lens;  // [B] absolute length incl. this step's tokens
+  const int* q_start;   // [B+1] prefill token offsets; nullptr for decode (token b == seq b)
+  float scale_log2;     // softmax scale * log2(e)
+  int nh, nkv, bs;
+  int n_sink, sink_pad, ring, window;  // window mode iff ring > 0
+  float* part_o;        // [splits, T, nh, D]     (decode, num_splits > 1)
+  float* part_ml;       // [splits, T, nh, 2]
+  int num_splits;
+};
+
+struct RopeCacheParams {
+  const bf16* qkv;        // [T, qkv_stride]
+  long qkv_stride;        // elements
+  const int* positions;   // [T] rope positions
+  const long* slot_mapping;  // [T]
+  const float* cos_sin;   // [max_pos, D] (cos | sin) or nullptr (no rope, e.g. GPT-2)
+  int max_pos;
+  bf16* q_out;            // [T, nh, D]
+  bf16* q_sink_out;       // [T, nh, D] or nullptr
+  int window;             // > 0: q_sink rotated at min(pos, window-1)
+  bf16* k_cache;          // [blocks, nkv, bs, D]
+  bf16* v_cache;          // [blocks, nkv, D, bs]
+  int nh, nkv, D, bs;
+};
+
+struct SampleParams {
+  const void* logits;       // [B, row_stride] bf16 or f32
+  int logits_is_f32;
+  long row_stride;
+  int V;
+  const float* temperature; // [B]
+  const int* top_k;         // [B] (<=0 or >=V: disabled)
+  const float* top_p;       // [B] (>=1: disabled)
+  const unsigned long long* seeds;  // [B]
+  const long* step;         // [1] device counter (read only) or nullptr
+  int* out_tokens;          // [B]
+  float* out_logprobs;      // [B] or nullptr
+};
+
+int launch_rms_norm(bf16* out, const bf16* x, bf16* residual, const bf16* w, float eps, int rows,
+                    int hidden, bool add_residual, hipStream_t stream);
+int launch_layer_norm(bf16* out, const bf16* x, bf16* residual, const bf16* w, const bf16* b,
+                      float eps, int rows, int hidden, bool add_residual, hipStream_t stream);
+int launch_silu_mul(bf16* out, const bf16* x, int rows, int inter, hipStream_t stream);
+int launch_gelu_bias(bf16* out, const bf16* x, const bf16* bias, int rows, int cols,
+                     hipStream_t stream);
+int launch_add(bf16* out, const bf16* a, const bf16* b, size_t n, hipStream_t stream);
+int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stream);
+int launch_attn_decode(const AttnParams& p, int B, int D, hipStream_t stream);
+int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_t stream);
+int launch_sample(const SampleParams& p, int B, hipStream_t stream);
+int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, bf16* residual,
+                         const bf16* norm_w, float eps, int rows, int K, bool add_residual,
+                         hipStream_t stream);
+
+}  // namespace dli

@@ -1,0 +1,168 @@
+// Normalisation kernels: RMSNorm, fused residual-add + RMSNorm, LayerNorm (+ residual).
+//
+// Reference behaviour: LlamaRMSNorm applied at models/llama/modules.py:124-125, 159-162, 173-179
+// (input norm, post-attention norm).  The reference computes RMSNorm(h + h) because `residual is
+// hidden_states` and uses the default eps (B9); here the intended
+//     residual' = x + residual ; out = w * residual' * rsqrt(mean(residual'^2) + eps)
+// is computed in one pass over HBM: one workgroup per row, the row held in registers (16-byte
+// bf16x8 accesses per lane), fp32 statistics, one rounding to bf16 at the end.
+#include "kernels.h"
+
+namespace dli {
+
+template <int VPT>  // bf16x8 vectors per thread
+__global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
+                                                       const bf16* __restrict__ x,
+                                                       bf16* __restrict__ residual,
+                                                       const bf16* __restrict__ w, float eps,
+                                                       int hidden, int add_residual) {
+  __shared__ float scratch[8];
+  const int row = blockIdx.x;
+  const int nvec = hidden >> 3;
+  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * hidden);
+  bf16x8* rr = reinterpret_cast<bf16x8*>(residual + (size_t)row * hidden);
+  const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
+  bf16x8* outr = reinterpret_cast<bf16x8*>(out + (size_t)row * hidden);
+
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * blockDim.x;
+    if (idx < nvec) {
+      bf16x8 a = xr[idx];
+      if (add_residual) {
+        bf16x8 r = rr[idx];
+        bf16x8 s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] = (bf16)((float)a[j] + (float)r[j]);
+        rr[idx] = s;
+        a = s;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = (float)a[j];
+        ss += v[i][j] * v[i][j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  ss = block_reduce_sum(ss, scratch);
+  const float rstd = rsqrtf(ss / (float)hidden + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * blockDim.x;
+    if (idx < nvec) {
+      bf16x8 ww = wr[idx];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[i][j] * rstd * (float)ww[j]);
+      outr[idx] = o;
+    }
+  }
+}
+
+template <int VPT>
+__global__ void __launch_bounds__(256) layer_norm_kernel(bf16* __restrict__ out,
+                                                         const bf16* __restrict__ x,
+                                                         bf16* __restrict__ residual,
+                                                         const bf16* __restrict__ w,
+                                                         const bf16* __restrict__ b, float eps,
+                                                         int hidden, int add_residual) {
+  __shared__ float scratch[8];
+  const int row = blockIdx.x;
+  const int nvec = hidden >> 3;
+  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * hidden);
+  bf16x8* rr = reinterpret_cast<bf16x8*>(residual + (size_t)row * hidden);
+  const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
+  const bf16x8* br = reinterpret_cast<const bf16x8*>(b);
+  bf16x8* outr = reinterpret_cast<bf16x8*>(out + (size_t)row * hidden);
+  float v[VPT][8];
+  float s1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * blockDim.x;
+    if (idx < nvec) {
+      bf16x8 a = xr[idx];
+      if (add_residual) {
+        bf16x8 r = rr[idx];
+        bf16x8 s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] = (bf16)((float)a[j] + (float)r[j]);
+        rr[idx] = s;
+        a = s;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = (float)a[j];
+        s1 += v[i][j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  const float mean = block_reduce_sum(s1, scratch) / (float)hidden;
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * blockDim.x;
+    if (idx < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[i][j] - mean;
+        s2 += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(block_reduce_sum(s2, scratch) / (float)hidden + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * blockDim.x;
+    if (idx < nvec) {
+      bf16x8 ww = wr[idx], bb = br[idx];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        o[j] = (bf16)((v[i][j] - mean) * rstd * (float)ww[j] + (float)bb[j]);
+      outr[idx] = o;
+    }
+  }
+}
+
+static inline int norm_threads(int hidden) {
+  int nvec = hidden / 8;
+  int t = ((nvec + 63) / 64) * 64;
+  return t > 256 ? 256 : t;
+}
+
+#define DLI_NORM_DISPATCH(KERNEL, ...)                                                    \
+  do {                                                                                    \
+    const int nvec = hidden / 8;                                                          \
+    const int threads = norm_threads(hidden);                                             \
+    const int vpt = (nvec + threads - 1) / threads;                                       \
+    if (vpt <= 1) KERNEL<1><<<rows, threads, 0, stream>>>(__VA_ARGS__);                   \
+    else if (vpt <= 2) KERNEL<2><<<rows, threads, 0, stream>>>(__VA_ARGS__);              \
+    else if (vpt <= 4) KERNEL<4><<<rows, threads, 0, stream>>>(__VA_ARGS__);              \
+    else if (vpt <= 8) KERNEL<8><<<rows, threads, 0, stream>>>(__VA_ARGS__);              \
+    else return -1;                                                                       \
+  } while (0)
+
+// Returns 0 on success, -1 if `hidden` is unsupported (must be a multiple of 8, <= 16384).
+int launch_rms_norm(bf16* out, const bf16* x, bf16* residual, const bf16* w, float eps, int rows,
+                    int hidden, bool add_residual, hipStream_t stream) {
+  if (hidden % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -1;
+  DLI_NORM_DISPATCH(rms_norm_kernel, out, x, residual, w, eps, hidden, add_residual ? 1 : 0);
+  return 0;
+}
+
+int launch_layer_norm(bf16* out, const bf16* x, bf16* residual, const bf16* w, const bf16* b,
+                      float eps, int rows, int hidden, bool add_residual, hipStream_t stream) {
+  if (hidden % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -1;
+  DLI_NORM_DISPATCH(layer_norm_kernel, out, x, residual, w, b, eps, hidden, add_residual ? 1 : 0);
+  return 0;
+}
+
+}  // namespace dli

@@ -1,0 +1,106 @@
+// Fused RoPE + paged-KV-cache write.
+//
+// Replaces, per layer, the reference's rotary application (modules.py:17-20, 71-76; cos/sin from
+// model.py:55 — computed there in int64) and the per-token `torch.cat` KV append
+// (cache.py:103-109, an O(S) copy per token per layer).  Here one pass over the fused QKV GEMM
+// output:
+//   * rotates q (rotate-half convention, fp32 math, cos/sin from a host-built fp32 table that
+//     already contains llama3 rope scaling) and writes it packed [T, nh, D];
+//   * in attention-sink (StreamingLLM) mode also writes q rotated at the *in-window* position
+//     min(pos, W-1) — the attention kernel scores sink keys with it, which is exactly the
+//     reference's key re-rotation (cache.py:21-48, 111-124) expressed on the query side, so no
+//     cached key is ever re-rotated;
+//   * rotates k and scatters it into the paged K cache [blocks, nkv, bs, D];
+//   * scatters v into the paged, *transposed* V cache [blocks, nkv, D, bs] — the layout the MFMA
+//     P·V product wants as a 16-byte-per-lane operand (see attention.hip).
+// slot_mapping[t] = physical slot (block*bs + offset) or -1 to skip the cache write.
+#include "kernels.h"
+
+namespace dli {
+
+
+__device__ __forceinline__ void rotate4(const bf16x4& a, const bf16x4& b, const float* cs,
+                                        int i, int half, bf16x4& oa, bf16x4& ob) {
+  // out[i] = a*cos - b*sin ; out[i+half] = b*cos + a*sin   (i .. i+3)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float c = cs[i + j], s = cs[half + i + j];
+    const float x = (float)a[j], y = (float)b[j];
+    oa[j] = (bf16)(x * c - y * s);
+    ob[j] = (bf16)(y * c + x * s);
+  }
+}
+
+__global__ void __launch_bounds__(256) rope_cache_kernel(RopeCacheParams p) {
+  const int t = blockIdx.x;
+  const int D = p.D, half = D >> 1;
+  const int gpr = half >> 2;  // 4-element groups per rotation half
+  const bf16* row = p.qkv + (size_t)t * p.qkv_stride;
+  const int pos = p.positions ? p.positions[t] : 0;
+  const float* cs = nullptr;
+  const float* cs_sink = nullptr;
+  if (p.cos_sin) {
+    int pc = pos < 0 ? 0 : (pos >= p.max_pos ? p.max_pos - 1 : pos);
+    cs = p.cos_sin + (size_t)pc * D;
+    if (p.q_sink_out) {
+      int ps = pos < p.window - 1 ? pos : p.window - 1;
+      ps = ps < 0 ? 0 : (ps >= p.max_pos ? p.max_pos - 1 : ps);
+      cs_sink = p.cos_sin + (size_t)ps * D;
+    }
+  }
+  const long slot = p.slot_mapping ? p.slot_mapping[t] : -1;
+  const long blk = slot >= 0 ? slot / p.bs : 0;
+  const int off = slot >= 0 ? (int)(slot % p.bs) : 0;
+
+  // ---- q and k heads (rotation) -------------------------------------------------------------
+  const int n_rot_items = (p.nh + p.nkv) * gpr;
+  for (int it = threadIdx.x; it < n_rot_items; it += blockDim.x) {
+    const int head = it / gpr;
+    const int i = (it % gpr) * 4;
+    const bf16* src = row + (size_t)head * D;
+    const bf16x4 a = *reinterpret_cast<const bf16x4*>(src + i);
+    const bf16x4 b = *reinterpret_cast<const bf16x4*>(src + half + i);
+    bf16x4 oa = a, ob = b;
+    if (cs) rotate4(a, b, cs, i, half, oa, ob);
+    if (head < p.nh) {
+      bf16* dst = p.q_out + ((size_t)t * p.nh + head) * D;
+      *reinterpret_cast<bf16x4*>(dst + i) = oa;
+      *reinterpret_cast<bf16x4*>(dst + half + i) = ob;
+      if (p.q_sink_out) {
+        bf16x4 sa = a, sb = b;
+        if (cs_sink) rotate4(a, b, cs_sink, i, half, sa, sb);
+        bf16* ds = p.q_sink_out + ((size_t)t * p.nh + head) * D;
+        *reinterpret_cast<bf16x4*>(ds + i) = sa;
+        *reinterpret_cast<bf16x4*>(ds + half + i) = sb;
+      }
+    } else if (slot >= 0) {
+      const int kh = head - p.nh;
+      bf16* dst = p.k_cache + (((size_t)blk * p.nkv + kh) * p.bs + off) * D;
+      *reinterpret_cast<bf16x4*>(dst + i) = oa;
+      *reinterpret_cast<bf16x4*>(dst + half + i) = ob;
+    }
+  }
+  // ---- v heads (transposed scatter) ---------------------------------------------------------
+  if (slot >= 0) {
+    const int vpr = D >> 3;
+    const int n_v_items = p.nkv * vpr;
+    const bf16* vsrc = row + (size_t)(p.nh + p.nkv) * D;
+    for (int it = threadIdx.x; it < n_v_items; it += blockDim.x) {
+      const int kh = it / vpr;
+      const int d0 = (it % vpr) * 8;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(vsrc + (size_t)kh * D + d0);
+      bf16* dst = p.v_cache + (((size_t)blk * p.nkv + kh) * D + d0) * p.bs + off;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dst[(size_t)j * p.bs] = v[j];
+    }
+  }
+}
+
+int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stream) {
+  if (num_tokens == 0) return 0;
+  if (p.D % 8 != 0 || p.qkv_stride % 4 != 0) return -1;
+  rope_cache_kernel<<<num_tokens, 256, 0, stream>>>(p);
+  return 0;
+}
+
+}  // namespace dli

@@ -1,0 +1,204 @@
+// Token sampling on the last pipeline stage (absent in the reference, which has no LM head —
+// SURVEY K13; required to close the generation loop of SURVEY §3.6).
+//
+// One 1024-thread workgroup per row of logits [B, V] (V = 128256 for Llama-3):
+//   * temperature <= 0  -> greedy argmax (ties -> lowest index), one pass.
+//   * otherwise x = logits / T, then optional top-k and top-p filtering by *radix select* on the
+//     order-preserving uint32 image of x (4 passes of 8 bits, LDS histograms: counts for top-k,
+//     probability mass for top-p), and finally Gumbel-max over the kept set:
+//     argmax(x_i + g_i), g_i = -log(-log(u_i)) — an exact sample of the renormalised softmax with
+//     no sort and no normalisation pass.  u_i comes from a counter-based hash of
+//     (seed, step, row, i) so a replayed graph produces fresh randomness via the device-side step
+//     counter.
+//   * optional log-probability of the chosen token under softmax(x).
+#include "kernels.h"
+
+namespace dli {
+
+
+__device__ __forceinline__ float load_logit(const SampleParams& p, int row, int i) {
+  if (p.logits_is_f32) return reinterpret_cast<const float*>(p.logits)[row * p.row_stride + i];
+  return (float)reinterpret_cast<const bf16*>(p.logits)[row * p.row_stride + i];
+}
+
+__device__ __forceinline__ unsigned f2key(float f) {
+  unsigned u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ float uniform01(unsigned long long seed, unsigned long long ctr) {
+  const unsigned long long r = splitmix64(seed ^ splitmix64(ctr));
+  // 24 random bits -> (0, 1)
+  return ((float)(r >> 40) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+// block argmax of (value, index) pairs; lower index wins ties.
+__device__ __forceinline__ void argmax_pair(float& v, int& idx, float ov, int oi) {
+  if (ov > v || (ov == v && oi < idx)) {
+    v = ov;
+    idx = oi;
+  }
+}
+
+__device__ void block_argmax(float& v, int& idx, float* sv, int* si) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(idx, o, 64);
+    argmax_pair(v, idx, ov, oi);
+  }
+  const int nw = blockDim.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sv[threadIdx.x >> 6] = v;
+    si[threadIdx.x >> 6] = idx;
+  }
+  __syncthreads();
+  v = sv[0];
+  idx = si[0];
+  for (int i = 1; i < nw; ++i) argmax_pair(v, idx, sv[i], si[i]);
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(1024) sample_kernel(SampleParams p) {
+  const int row = blockIdx.x;
+  const int V = p.V;
+  __shared__ float s_f[16];
+  __shared__ int s_i[16];
+  __shared__ unsigned h_cnt[256];
+  __shared__ float h_mass[256];
+  __shared__ unsigned s_prefix;
+  __shared__ float s_target;
+  __shared__ unsigned s_remaining;
+
+  const float temp = p.temperature ? p.temperature[row] : 0.f;
+  // ---------------- greedy ----------------
+  if (!(temp > 0.f)) {
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = threadIdx.x; i < V; i += blockDim.x) argmax_pair(best, bi, load_logit(p, row, i), i);
+    block_argmax(best, bi, s_f, s_i);
+    if (p.out_logprobs) {
+      float s = 0.f;
+      for (int i = threadIdx.x; i < V; i += blockDim.x) s += __expf(load_logit(p, row, i) - best);
+      s = block_reduce_sum(s, s_f);
+      if (threadIdx.x == 0) p.out_logprobs[row] = -logf(s);
+    }
+    if (threadIdx.x == 0) p.out_tokens[row] = bi;
+    return;
+  }
+  const float inv_t = 1.f / temp;
+  // row max of x
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < V; i += blockDim.x) mx = fmaxf(mx, load_logit(p, row, i) * inv_t);
+  mx = block_reduce_max(mx, s_f);
+
+  unsigned thr_key = 0;  // keep elements with key >= thr_key
+  // ---------------- top-k (radix select on counts) ----------------
+  const int k = p.top_k ? p.top_k[row] : 0;
+  if (k > 0 && k < V) {
+    unsigned prefix = 0, remaining = (unsigned)k;
+    for (int pass = 0; pass < 4; ++pass) {
+      const int shift = 24 - 8 * pass;
+      const unsigned hi_mask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+      for (int i = threadIdx.x; i < 256; i += blockDim.x) h_cnt[i] = 0;
+      __syncthreads();
+      for (int i = threadIdx.x; i < V; i += blockDim.x) {
+        const unsigned key = f2key(load_logit(p, row, i) * inv_t);
+        if ((key & hi_mask) == (prefix & hi_mask)) atomicAdd(&h_cnt[(key >> shift) & 255], 1u);
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned acc = 0;
+        int bin = 255;
+        for (; bin > 0; --bin) {
+          if (acc + h_cnt[bin] >= remaining) break;
+          acc += h_cnt[bin];
+        }
+        s_prefix = prefix | ((unsigned)bin << shift);
+        s_remaining = remaining - acc;
+      }
+      __syncthreads();
+      prefix = s_prefix;
+      remaining = s_remaining;
+      __syncthreads();
+    }
+    thr_key = prefix;
+  }
+  // ---------------- top-p (radix select on probability mass) ----------------
+  const float tp = p.top_p ? p.top_p[row] : 1.f;
+  if (tp < 1.f) {
+    float z = 0.f;
+    for (int i = threadIdx.x; i < V; i += blockDim.x) {
+      const float x = load_logit(p, row, i) * inv_t;
+      if (f2key(x) >= thr_key) z += __expf(x - mx);
+    }
+    z = block_reduce_sum(z, s_f);
+    unsigned prefix = 0;
+    float target = tp * z;  // mass that must be covered, from the top
+    for (int pass = 0; pass < 4; ++pass) {
+      const int shift = 24 - 8 * pass;
+      const unsigned hi_mask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+      for (int i = threadIdx.x; i < 256; i += blockDim.x) h_mass[i] = 0.f;
+      __syncthreads();
+      for (int i = threadIdx.x; i < V; i += blockDim.x) {
+        const float x = load_logit(p, row, i) * inv_t;
+        const unsigned key = f2key(x);
+        if (key >= thr_key && (key & hi_mask) == (prefix & hi_mask))
+          atomicAdd(&h_mass[(key >> shift) & 255], __expf(x - mx));
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        float acc = 0.f;
+        int bin = 255;
+        for (; bin > 0; --bin) {
+          if (acc + h_mass[bin] >= target) break;
+          acc += h_mass[bin];
+        }
+        s_prefix = prefix | ((unsigned)bin << shift);
+        s_target = target - acc;
+      }
+      __syncthreads();
+      prefix = s_prefix;
+      target = s_target;
+      __syncthreads();
+    }
+    thr_key = thr_key > prefix ? thr_key : prefix;
+  }
+  // ---------------- Gumbel-max over the kept set ----------------
+  const unsigned long long seed = p.seeds ? p.seeds[row] : 0x1234ull;
+  const unsigned long long st = p.step ? (unsigned long long)p.step[0] : 0ull;
+  const unsigned long long base = (st * 0x100000001B3ull) ^ ((unsigned long long)row << 40);
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int i = threadIdx.x; i < V; i += blockDim.x) {
+    const float x = load_logit(p, row, i) * inv_t;
+    if (f2key(x) < thr_key) continue;
+    const float u = uniform01(seed, base + (unsigned long long)i);
+    const float g = -__logf(-__logf(u));
+    argmax_pair(best, bi, x + g, i);
+  }
+  block_argmax(best, bi, s_f, s_i);
+  if (bi >= V) bi = 0;
+  if (p.out_logprobs) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < V; i += blockDim.x) s += __expf(load_logit(p, row, i) * inv_t - mx);
+    s = block_reduce_sum(s, s_f);
+    if (threadIdx.x == 0) p.out_logprobs[row] = load_logit(p, row, bi) * inv_t - mx - logf(s);
+  }
+  if (threadIdx.x == 0) p.out_tokens[row] = bi;
+}
+
+int launch_sample(const SampleParams& p, int B, hipStream_t stream) {
+  if (B == 0) return 0;
+  sample_kernel<<<B, 1024, 0, stream>>>(p);
+  return 0;
+}
+
+}  // namespace dli

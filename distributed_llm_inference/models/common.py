@@ -1,0 +1,128 @@
+"""Building blocks shared by the model families (Llama, GPT-2).
+
+* :class:`Linear` — bf16 weight GEMM through hipBLASLt (``F.linear``), or fp8-e4m3 weights with
+  per-output-channel scales and per-token dynamic activation scales through hipBLASLt's row-wise
+  scaled GEMM (``torch._scaled_mm``).  This is the MI355X replacement of the reference's
+  bitsandbytes ``Linear8bitLt`` (utils/model.py:93-113).
+* :class:`AttnMetadata` — per-batch device metadata consumed by the attention / cache kernels
+  (positions, slot mapping, block tables, sequence lengths, varlen offsets, window policy).  It
+  replaces the reference's dense additive causal/padding mask (model.py:78-143): causality,
+  padding and windows are all derived in-kernel from these small int tensors.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+
+
+class Linear(nn.Module):
+    """``y = x W^T (+ b)`` with W stored [out, in]; optional fp8 weights."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = False,
+                 dtype: torch.dtype = torch.bfloat16, device=None):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.weight = nn.Parameter(torch.empty(out_features, in_features, dtype=dtype,
+                                               device=device), requires_grad=False)
+        self.bias = (nn.Parameter(torch.zeros(out_features, dtype=dtype, device=device),
+                                  requires_grad=False) if bias else None)
+        self.register_buffer("weight_fp8", None, persistent=False)
+        self.register_buffer("weight_scale", None, persistent=False)
+
+    @property
+    def is_fp8(self) -> bool:
+        return self.weight_fp8 is not None
+
+    def quantize_fp8(self, keep_bf16: bool = False) -> None:
+        """Quantise W to fp8 e4m3 (per output channel).  Frees the bf16 copy unless asked not to."""
+        q, s = ops.quantize_weight_fp8(self.weight.data)
+        self.weight_fp8, self.weight_scale = q, s
+        if not keep_bf16:
+            self.weight = nn.Parameter(torch.empty(0, dtype=self.weight.dtype,
+                                                   device=self.weight.device), requires_grad=False)
+
+    def forward(self, x: torch.Tensor,
+                x_q: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+        if self.weight_fp8 is None:
+            return F.linear(x, self.weight, self.bias)
+        if x_q is None:
+            x_q = ops.quant_rowwise(x)
+        xq, xs = x_q
+        if xq.is_cuda:
+            y = torch._scaled_mm(xq, self.weight_fp8.t(), scale_a=xs, scale_b=self.weight_scale,
+                                 out_dtype=torch.bfloat16)
+        else:  # CPU: dequantised reference
+            y = ((xq.float() * xs) @ (self.weight_fp8.float() * self.weight_scale.t()).t()
+                 ).to(torch.bfloat16)
+        if self.bias is not None:
+            y = y + self.bias
+        return y
+
+    def extra_repr(self) -> str:
+        return (f"in={self.in_features}, out={self.out_features}, bias={self.bias is not None}, "
+                f"fp8={self.is_fp8}")
+
+
+@dataclass
+class AttnMetadata:
+    """Device metadata of one forward batch (varlen: T tokens from B sequences)."""
+
+    num_tokens: int
+    num_seqs: int
+    is_decode: bool                  # every sequence contributes exactly one new token
+    positions: torch.Tensor          # [T] int32 rope positions
+    slot_mapping: torch.Tensor       # [T] int64 physical cache slot (-1: don't write)
+    block_tables: torch.Tensor       # [B, max_blocks] int32
+    seq_lens: torch.Tensor           # [B] int32 (absolute length incl. new tokens)
+    q_start: torch.Tensor            # [B+1] int32 token offsets
+    max_q: int
+    num_splits: int = 1
+    workspace: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+    # attention-sink window policy (all zero for a full cache)
+    n_sink: int = 0
+    sink_pad: int = 0
+    ring: int = 0
+    window: int = 0
+    # rows (token index) whose hidden state feeds the LM head, or None = all rows
+    logits_rows: Optional[torch.Tensor] = None
+
+    @property
+    def windowed(self) -> bool:
+        return self.ring > 0
+
+    @property
+    def want_sink(self) -> bool:
+        return self.ring > 0 and self.n_sink > 0
+
+
+def seeded_normal_(t: torch.Tensor, seed: int, std: float) -> torch.Tensor:
+    """Deterministic N(0, std) init independent of device placement order (so a PP=8 split and a
+    PP=1 model built from the same seed hold identical weights)."""
+    g = torch.Generator(device=t.device)
+    g.manual_seed(seed & 0x7FFFFFFFFFFFFFFF)
+    with torch.no_grad():
+        if t.dtype in (torch.float32, torch.float64):
+            t.normal_(0.0, std, generator=g)
+        else:
+            # generate in chunks to bound the fp32 temporary
+            flat = t.view(-1)
+            step = 1 << 26
+            for i in range(0, flat.numel(), step):
+                chunk = flat[i:i + step]
+                tmp = torch.empty(chunk.shape, dtype=torch.float32, device=t.device)
+                tmp.normal_(0.0, std, generator=g)
+                chunk.copy_(tmp)
+    return t
+
+
+def param_seed(base: int, layer_idx: int, name: str) -> int:
+    h = 1469598103934665603
+    for ch in f"{layer_idx}:{name}".encode():
+        h = ((h ^ ch) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return (h ^ (base * 0x9E3779B97F4A7C15)) & 0x7FFFFFFFFFFFFFFF

@@ -1,0 +1,152 @@
+"""Llama decoder layer on the CDNA4 kernels.
+
+Reference: ``OptimizedLlamaDecoderLayer`` / ``OptimizedLlamaInferenceAttention``
+(/root/reference/distributed_llm_inference/models/llama/modules.py:23-184).  Same computation,
+intended semantics (SURVEY B1/B2/B6/B7/B8/B9 fixed), MI355X-first data flow per layer:
+
+    normed, residual = add_rmsnorm(h, residual)            # csrc/kernels/norm.hip
+    qkv  = normed @ W_qkv^T                                 # ONE fused GEMM (hipBLASLt / fp8)
+    q    = rope_cache(qkv) ; k,v -> paged KV cache          # csrc/kernels/rope_cache.hip
+    o    = paged attention (decode split-K | prefill)       # csrc/kernels/attention.hip (MFMA)
+    a    = o @ W_o^T
+    normed, residual = add_rmsnorm(a, residual)
+    h    = silu_mul(normed @ W_gate_up^T) @ W_down^T        # fused gate|up GEMM + activation.hip
+
+The residual stream is carried *separately* from the layer output, so each residual add is fused
+into the following RMSNorm kernel (one HBM pass) instead of being a standalone elementwise op.
+``pretraining_tp`` (reference modules.py:44-59, 107-110) is single-device weight slicing that is
+mathematically identical to the unsliced projection; it is accepted and ignored.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from ... import ops
+from ...config import ModelSpec
+from ..common import AttnMetadata, Linear
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, hidden: int, eps: float, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(hidden, dtype=dtype, device=device), requires_grad=False)
+        self.eps = eps
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None):
+        return ops.rms_norm(x, self.weight, self.eps, residual=residual)
+
+
+class LlamaAttention(nn.Module):
+    def __init__(self, spec: ModelSpec, layer_idx: int, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        self.layer_idx = layer_idx
+        self.num_heads = spec.num_heads
+        self.num_kv_heads = spec.num_kv_heads
+        self.head_dim = spec.head_dim
+        self.scale = spec.head_dim ** -0.5
+        self.qkv_proj = Linear(spec.hidden_size, spec.qkv_size, bias=spec.attention_bias,
+                               dtype=dtype, device=device)
+        self.o_proj = Linear(spec.q_size, spec.hidden_size, bias=spec.attention_bias, dtype=dtype,
+                             device=device)
+
+    def forward(self, normed: torch.Tensor, meta: AttnMetadata, k_cache: torch.Tensor,
+                v_cache: torch.Tensor, cos_sin: torch.Tensor) -> torch.Tensor:
+        T = normed.shape[0]
+        qkv = self.qkv_proj(normed)
+        q, q_sink = ops.rope_cache(qkv, meta.positions, meta.slot_mapping, cos_sin, self.num_heads,
+                                   self.num_kv_heads, self.head_dim, k_cache, v_cache,
+                                   window=meta.window, want_sink=meta.want_sink)
+        if meta.is_decode:
+            o = ops.attn_decode(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
+                                self.scale, meta.n_sink, meta.sink_pad, meta.ring, meta.window,
+                                num_splits=meta.num_splits, workspace=meta.workspace)
+        else:
+            o = ops.attn_prefill(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
+                                 meta.q_start, meta.max_q, self.scale, meta.n_sink, meta.sink_pad,
+                                 meta.ring, meta.window)
+        return self.o_proj(o.view(T, self.num_heads * self.head_dim))
+
+
+class LlamaMLP(nn.Module):
+    def __init__(self, spec: ModelSpec, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        if spec.hidden_act != "silu":
+            raise ValueError(f"unsupported Llama activation {spec.hidden_act!r}")
+        self.intermediate_size = spec.intermediate_size
+        self.gate_up_proj = Linear(spec.hidden_size, 2 * spec.intermediate_size, bias=spec.mlp_bias,
+                                   dtype=dtype, device=device)
+        self.down_proj = Linear(spec.intermediate_size, spec.hidden_size, bias=spec.mlp_bias,
+                                dtype=dtype, device=device)
+
+    def forward(self, normed: torch.Tensor) -> torch.Tensor:
+        return self.down_proj(ops.silu_mul(self.gate_up_proj(normed)))
+
+
+class LlamaDecoderLayer(nn.Module):
+    """One decoder layer; ``layer_idx`` is the GLOBAL layer index (as in the reference)."""
+
+    def __init__(self, spec: ModelSpec, layer_idx: int, device=None, dtype=torch.bfloat16):
+        super().__init__()
+        self.layer_idx = layer_idx
+        self.hidden_size = spec.hidden_size
+        self.self_attn = LlamaAttention(spec, layer_idx, device, dtype)
+        self.mlp = LlamaMLP(spec, device, dtype)
+        self.input_layernorm = RMSNorm(spec.hidden_size, spec.rms_norm_eps, device, dtype)
+        self.post_attention_layernorm = RMSNorm(spec.hidden_size, spec.rms_norm_eps, device, dtype)
+
+    def forward(self, hidden: torch.Tensor, residual: Optional[torch.Tensor], meta: AttnMetadata,
+                k_cache: torch.Tensor, v_cache: torch.Tensor,
+                cos_sin: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        if residual is None:
+            residual = hidden
+            normed, _ = self.input_layernorm(hidden)
+        else:
+            normed, residual = self.input_layernorm(hidden, residual)
+        attn = self.self_attn(normed, meta, k_cache, v_cache, cos_sin)
+        normed, residual = self.post_attention_layernorm(attn, residual)
+        return self.mlp(normed), residual
+
+    # ------------------------------------------------------------------ weights
+    def load_hf_state_dict(self, sd: dict) -> None:
+        """Load a HF ``LlamaDecoderLayer`` state dict (keys relative to ``model.layers.{i}.``),
+        fusing q|k|v and gate|up into the single GEMM weights."""
+        def g(k):
+            if k not in sd:
+                raise KeyError(f"parameter {k} not found in state dict for layer {self.layer_idx}")
+            return sd[k]
+        dt = self.input_layernorm.weight.dtype
+        with torch.no_grad():
+            qkv = torch.cat([g("self_attn.q_proj.weight"), g("self_attn.k_proj.weight"),
+                             g("self_attn.v_proj.weight")], 0)
+            self.self_attn.qkv_proj.weight.copy_(qkv.to(dt))
+            self.self_attn.o_proj.weight.copy_(g("self_attn.o_proj.weight").to(dt))
+            if self.self_attn.qkv_proj.bias is not None:
+                self.self_attn.qkv_proj.bias.copy_(torch.cat(
+                    [g("self_attn.q_proj.bias"), g("self_attn.k_proj.bias"),
+                     g("self_attn.v_proj.bias")], 0).to(dt))
+                if "self_attn.o_proj.bias" in sd:
+                    self.self_attn.o_proj.bias.copy_(sd["self_attn.o_proj.bias"].to(dt))
+            gu = torch.cat([g("mlp.gate_proj.weight"), g("mlp.up_proj.weight")], 0)
+            self.mlp.gate_up_proj.weight.copy_(gu.to(dt))
+            self.mlp.down_proj.weight.copy_(g("mlp.down_proj.weight").to(dt))
+            self.input_layernorm.weight.copy_(g("input_layernorm.weight").to(dt))
+            self.post_attention_layernorm.weight.copy_(g("post_attention_layernorm.weight").to(dt))
+
+    def hf_state_dict(self) -> dict:
+        """Inverse of :meth:`load_hf_state_dict` (used to write checkpoints / test parity)."""
+        a, m = self.self_attn, self.mlp
+        q, k, v = a.qkv_proj.weight.split([a.num_heads * a.head_dim,
+                                           a.num_kv_heads * a.head_dim,
+                                           a.num_kv_heads * a.head_dim], 0)
+        gate, up = m.gate_up_proj.weight.split([m.intermediate_size, m.intermediate_size], 0)
+        return {
+            "self_attn.q_proj.weight": q, "self_attn.k_proj.weight": k,
+            "self_attn.v_proj.weight": v, "self_attn.o_proj.weight": a.o_proj.weight,
+            "mlp.gate_proj.weight": gate, "mlp.up_proj.weight": up,
+            "mlp.down_proj.weight": m.down_proj.weight,
+            "input_layernorm.weight": self.input_layernorm.weight,
+            "post_attention_layernorm.weight": self.post_attention_layernorm.weight,
+        }

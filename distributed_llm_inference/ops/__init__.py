@@ -1,0 +1,225 @@
+"""Operator front-end: GPU tensors -> hand-written CDNA4 HIP kernels, CPU tensors -> torch reference.
+
+There is deliberately no silent fallback: a GPU tensor with the native extension missing raises
+(``NativeKernelsMissing``), so a GPU run can never "pass" on an eager PyTorch path.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+
+from . import reference as ref
+
+_C = None
+
+
+class NativeKernelsMissing(RuntimeError):
+    pass
+
+
+def native():
+    """The compiled ``_C`` extension (kernels + RCCL).  Raises if it was not built."""
+    global _C
+    if _C is None:
+        try:
+            from .. import _C as mod  # type: ignore[attr-defined]
+        except ImportError as e:  # pragma: no cover - depends on build state
+            raise NativeKernelsMissing(
+                "distributed_llm_inference native kernels are not built; run "
+                "`python -m distributed_llm_inference._build` (hipcc, gfx950)") from e
+        _C = mod
+    return _C
+
+
+def native_available() -> bool:
+    try:
+        native()
+        return True
+    except NativeKernelsMissing:
+        return False
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ----------------------------------------------------------------------------- normalisation
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+             out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """``residual' = x + residual`` (in place, if given); ``out = RMSNorm(residual' or x) * w``."""
+    if not _gpu(x):
+        y, r = ref.rms_norm(x, w, eps, residual)
+        if out is not None:
+            out.copy_(y)
+            y = out
+        return y, r
+    out = torch.empty_like(x) if out is None else out
+    native().rms_norm(out, x, residual, w, float(eps))
+    return out, residual
+
+
+def layer_norm(x, w, b, eps, residual=None, out=None):
+    if not _gpu(x):
+        y, r = ref.layer_norm(x, w, b, eps, residual)
+        if out is not None:
+            out.copy_(y)
+            y = out
+        return y, r
+    out = torch.empty_like(x) if out is None else out
+    native().layer_norm(out, x, residual, w, b, float(eps))
+    return out, residual
+
+
+# ----------------------------------------------------------------------------- activations
+def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(x):
+        y = ref.silu_mul(x)
+        return out.copy_(y) if out is not None else y
+    if out is None:
+        out = torch.empty(*x.shape[:-1], x.shape[-1] // 2, dtype=x.dtype, device=x.device)
+    native().silu_mul(out, x)
+    return out
+
+
+def gelu_bias(x: torch.Tensor, bias: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(x):
+        y = ref.gelu_bias(x, bias)
+        return out.copy_(y) if out is not None else y
+    out = torch.empty_like(x) if out is None else out
+    native().gelu_bias(out, x, bias)
+    return out
+
+
+def add(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(a):
+        y = (a.float() + b.float()).to(a.dtype)
+        return out.copy_(y) if out is not None else y
+    out = torch.empty_like(a) if out is None else out
+    native().add(out, a, b)
+    return out
+
+
+# ----------------------------------------------------------------------------- rope + cache
+def rope_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
+               slot_mapping: Optional[torch.Tensor], cos_sin: Optional[torch.Tensor], nh: int,
+               nkv: int, head_dim: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
+               window: int = 0, want_sink: bool = False, q_out: Optional[torch.Tensor] = None,
+               q_sink_out: Optional[torch.Tensor] = None):
+    """Rotate q/k, write k/v to the paged cache; returns ``(q [T, nh, D], q_sink or None)``."""
+    if not _gpu(qkv):
+        q, qs = ref.rope_cache(qkv, positions, slot_mapping, cos_sin, nh, nkv, head_dim, k_cache,
+                               v_cache, window, want_sink)
+        if q_out is not None:
+            q_out.copy_(q)
+            q = q_out
+        if qs is not None and q_sink_out is not None:
+            q_sink_out.copy_(qs)
+            qs = q_sink_out
+        return q, qs
+    T = qkv.shape[0]
+    if q_out is None:
+        q_out = torch.empty(T, nh, head_dim, dtype=qkv.dtype, device=qkv.device)
+    if want_sink and q_sink_out is None:
+        q_sink_out = torch.empty_like(q_out)
+    native().rope_cache(qkv, positions, slot_mapping, cos_sin, q_out,
+                        q_sink_out if want_sink else None, int(window), k_cache, v_cache,
+                        int(nh), int(nkv))
+    return q_out, (q_sink_out if want_sink else None)
+
+
+# ----------------------------------------------------------------------------- attention
+def decode_splits(batch: int, nkv: int, group: int, max_len: int, cu: int = 256) -> int:
+    """Split-K factor for decode so that the grid has >= ~2 workgroups per CU."""
+    wgs = batch * nkv * ((group + 15) // 16)
+    if wgs >= 2 * cu:
+        return 1
+    want = (2 * cu + wgs - 1) // wgs
+    max_useful = max(1, (max_len + 255) // 256)  # >= 256 keys per split
+    return int(max(1, min(want, max_useful, 32)))
+
+
+def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink=0, sink_pad=0,
+                ring=0, window=0, num_splits=1, workspace=None, out=None):
+    if not _gpu(q):
+        y = ref.attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
+                            sink_pad, ring, window)
+        return out.copy_(y) if out is not None else y
+    out = torch.empty_like(q) if out is None else out
+    part_o = part_ml = None
+    if num_splits > 1:
+        B, nh, D = q.shape
+        if workspace is None:
+            part_o = torch.empty(num_splits * B * nh * D, dtype=torch.float32, device=q.device)
+            part_ml = torch.empty(num_splits * B * nh * 2, dtype=torch.float32, device=q.device)
+        else:
+            part_o, part_ml = workspace
+    native().attn_decode(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, float(scale),
+                         int(n_sink), int(sink_pad), int(ring), int(window), int(num_splits),
+                         part_o, part_ml)
+    return out
+
+
+def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, max_q, scale,
+                 n_sink=0, sink_pad=0, ring=0, window=0, out=None):
+    if not _gpu(q):
+        y = ref.attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, scale,
+                             n_sink, sink_pad, ring, window)
+        return out.copy_(y) if out is not None else y
+    out = torch.empty_like(q) if out is None else out
+    native().attn_prefill(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start,
+                          int(max_q), float(scale), int(n_sink), int(sink_pad), int(ring),
+                          int(window))
+    return out
+
+
+# ----------------------------------------------------------------------------- sampling
+def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
+           top_k: Optional[torch.Tensor] = None, top_p: Optional[torch.Tensor] = None,
+           seeds: Optional[torch.Tensor] = None, step: Optional[torch.Tensor] = None,
+           out: Optional[torch.Tensor] = None, logprobs: Optional[torch.Tensor] = None,
+           generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    if not _gpu(logits):
+        y = ref.sample(logits, temperature, top_k, top_p, generator)
+        return out.copy_(y) if out is not None else y
+    if out is None:
+        out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
+    native().sample(out, logprobs, logits, temperature, top_k, top_p, seeds, step)
+    return out
+
+
+# ----------------------------------------------------------------------------- fp8
+FP8 = torch.float8_e4m3fn
+FP8_MAX = 448.0
+
+
+def quant_rowwise(x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                  norm_w: Optional[torch.Tensor] = None, eps: float = 0.0):
+    """Per-row dynamic fp8-e4m3 quantisation (optionally fused residual-add + RMSNorm first)."""
+    K = x.shape[-1]
+    rows = x.numel() // K
+    if not _gpu(x):
+        if norm_w is not None:
+            x, _ = ref.rms_norm(x, norm_w, eps, residual)
+        xf = x.float().reshape(rows, K)
+        s = (xf.abs().amax(-1).clamp_min(1e-12) / FP8_MAX)
+        q = (xf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+        return q.reshape(x.shape), s.reshape(rows, 1)
+    q = torch.empty(x.shape, dtype=FP8, device=x.device)
+    s = torch.empty(rows, 1, dtype=torch.float32, device=x.device)
+    native().quant_rowwise(q, s, x, residual, norm_w, float(eps))
+    return q, s
+
+
+def quantize_weight_fp8(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Offline per-output-channel fp8 quantisation of a [N, K] weight: returns (w_fp8, scale[1, N])."""
+    wf = w.float()
+    s = wf.abs().amax(-1).clamp_min(1e-12) / FP8_MAX
+    q = (wf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    return q, s.reshape(1, -1).contiguous()
+
+
+def softmax_scale(head_dim: int) -> float:
+    return 1.0 / math.sqrt(head_dim)

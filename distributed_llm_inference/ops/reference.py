@@ -1,0 +1,244 @@
+"""Plain-PyTorch reference implementations of every kernel in ``csrc/kernels``.
+
+They serve two purposes only:
+  1. the fp32 numerics oracle for the GPU kernel tests (``tests/test_kernels_gpu.py``);
+  2. the CPU execution path (GPT-2 / tiny-Llama CPU plumbing config, CPU unit tests).
+On a GPU tensor the HIP kernels are ALWAYS used (``ops/__init__.py`` never falls back silently).
+
+Cache layouts are identical to the kernels':
+  k_cache [num_blocks, nkv, block_size, D], v_cache [num_blocks, nkv, D, block_size] (transposed).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+
+# ----------------------------------------------------------------------------- normalisation
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float,
+             residual: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    if residual is not None:
+        residual.copy_((x.float() + residual.float()).to(residual.dtype))
+        x = residual
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    return y.to(x.dtype), residual
+
+
+def layer_norm(x, w, b, eps, residual=None):
+    if residual is not None:
+        residual.copy_((x.float() + residual.float()).to(residual.dtype))
+        x = residual
+    y = F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps)
+    return y.to(x.dtype), residual
+
+
+# ----------------------------------------------------------------------------- activations
+def silu_mul(x: torch.Tensor) -> torch.Tensor:
+    i = x.shape[-1] // 2
+    return (F.silu(x[..., :i].float()) * x[..., i:].float()).to(x.dtype)
+
+
+def gelu_bias(x: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    xf = x.float() + (bias.float() if bias is not None else 0.0)
+    return F.gelu(xf, approximate="tanh").to(x.dtype)
+
+
+# ----------------------------------------------------------------------------- rope + cache
+def _rotate(x: torch.Tensor, cs: torch.Tensor) -> torch.Tensor:
+    """x [T, H, D] (any float), cs [T, D] fp32 (cos | sin halves) -> rotated fp32."""
+    D = x.shape[-1]
+    half = D // 2
+    c = cs[:, None, :half]
+    s = cs[:, None, half:]
+    x1, x2 = x[..., :half].float(), x[..., half:].float()
+    return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+
+def rope_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
+               slot_mapping: Optional[torch.Tensor], cos_sin: Optional[torch.Tensor],
+               nh: int, nkv: int, D: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
+               window: int = 0, want_sink: bool = False
+               ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    T = qkv.shape[0]
+    q = qkv[:, : nh * D].reshape(T, nh, D)
+    k = qkv[:, nh * D: (nh + nkv) * D].reshape(T, nkv, D)
+    v = qkv[:, (nh + nkv) * D: (nh + 2 * nkv) * D].reshape(T, nkv, D)
+    q_sink = None
+    if cos_sin is not None:
+        maxp = cos_sin.shape[0]
+        pos = positions.long().clamp(0, maxp - 1)
+        cs = cos_sin[pos]
+        qr = _rotate(q, cs).to(qkv.dtype)
+        kr = _rotate(k, cs).to(qkv.dtype)
+        if want_sink:
+            ps = torch.minimum(positions.long(), torch.full_like(positions.long(), window - 1))
+            q_sink = _rotate(q, cos_sin[ps.clamp(0, maxp - 1)]).to(qkv.dtype)
+    else:
+        qr, kr = q.clone(), k.clone()
+        if want_sink:
+            q_sink = q.clone()
+    if slot_mapping is not None:
+        bs = k_cache.shape[2]
+        sm = slot_mapping.long()
+        ok = sm >= 0
+        if ok.any():
+            blk, off = sm[ok] // bs, sm[ok] % bs
+            k_cache[blk, :, off, :] = kr[ok]
+            v_cache[blk, :, :, off] = v[ok]
+    return qr.contiguous(), (q_sink.contiguous() if q_sink is not None else None)
+
+
+# ----------------------------------------------------------------------------- attention
+def _gather_seq(k_cache, v_cache, block_table, nslots):
+    """Return K [nslots, nkv, D], V [nslots, nkv, D] in slot order."""
+    bs = k_cache.shape[2]
+    nb = (nslots + bs - 1) // bs
+    blocks = block_table[:nb].long()
+    K = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * bs, k_cache.shape[1], -1)[:nslots]
+    V = v_cache[blocks].permute(0, 3, 1, 2).reshape(nb * bs, v_cache.shape[1], -1)[:nslots]
+    return K, V
+
+
+def _ring_abs(u: torch.Tensor, L: int, n_sink: int, sink_pad: int, ring: int) -> torch.Tensor:
+    o = u - sink_pad
+    newest = (L - 1 - n_sink) % ring
+    back = (newest - o) % ring
+    return (L - 1) - back
+
+
+def _attend_one(q_cols: torch.Tensor, q_sink_cols: Optional[torch.Tensor], qpos: torch.Tensor,
+                K: torch.Tensor, V: torch.Tensor, L: int, scale: float, n_sink: int,
+                sink_pad: int, ring: int, window: int) -> torch.Tensor:
+    """q_cols [n, nh, D] with absolute positions qpos [n]; K/V [slots, nkv, D] -> [n, nh, D] fp32."""
+    n, nh, D = q_cols.shape
+    nkv = K.shape[1]
+    G = nh // nkv
+    Kf = K.float().repeat_interleave(G, dim=1)  # [S, nh, D]
+    Vf = V.float().repeat_interleave(G, dim=1)
+    S = K.shape[0]
+    u = torch.arange(S, device=K.device)
+    if ring <= 0:
+        # full cache: slot == absolute position
+        vis = u[None, :] <= qpos[:, None]  # [n, S]
+        vis &= (u < L)[None, :]
+        scores = torch.einsum("nhd,shd->nhs", q_cols.float(), Kf) * scale
+        scores = scores.masked_fill(~vis[:, None, :], float("-inf"))
+    else:
+        is_sink = u < n_sink
+        a = torch.where(is_sink, u, _ring_abs(u, L, n_sink, sink_pad, ring))
+        roll_valid = (u >= sink_pad) & ((u - sink_pad) < max(0, min(ring, L - n_sink)))
+        vis_roll = roll_valid[None, :] & (a[None, :] >= n_sink) & (a[None, :] <= qpos[:, None]) \
+            & ((qpos[:, None] - a[None, :]) < (window - n_sink))
+        vis_sink = (is_sink & (u < min(n_sink, L)))[None, :] & (u[None, :] <= qpos[:, None])
+        s_roll = torch.einsum("nhd,shd->nhs", q_cols.float(), Kf) * scale
+        qs = q_sink_cols if q_sink_cols is not None else q_cols
+        s_sink = torch.einsum("nhd,shd->nhs", qs.float(), Kf) * scale
+        scores = torch.where(is_sink[None, None, :], s_sink, s_roll)
+        vis = torch.where(is_sink[None, :], vis_sink, vis_roll)
+        scores = scores.masked_fill(~vis[:, None, :], float("-inf"))
+    p = torch.softmax(scores, dim=-1)
+    p = torch.nan_to_num(p, nan=0.0)
+    return torch.einsum("nhs,shd->nhd", p, Vf)
+
+
+def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale,
+                n_sink=0, sink_pad=0, ring=0, window=0) -> torch.Tensor:
+    B, nh, D = q.shape
+    out = torch.zeros_like(q)
+    for b in range(B):
+        L = int(seq_lens[b])
+        if L <= 0:
+            continue
+        nslots = L if ring <= 0 else (L if L <= n_sink else sink_pad + min(ring, L - n_sink))
+        K, V = _gather_seq(k_cache, v_cache, block_tables[b], nslots)
+        qpos = torch.tensor([L - 1], device=q.device)
+        o = _attend_one(q[b:b + 1], q_sink[b:b + 1] if q_sink is not None else None, qpos, K, V,
+                        L, scale, n_sink, sink_pad, ring, window)
+        out[b] = o[0].to(q.dtype)
+    return out
+
+
+def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, scale,
+                 n_sink=0, sink_pad=0, ring=0, window=0) -> torch.Tensor:
+    out = torch.zeros_like(q)
+    B = seq_lens.numel()
+    for b in range(B):
+        s0, s1 = int(q_start[b]), int(q_start[b + 1])
+        ql = s1 - s0
+        if ql == 0:
+            continue
+        L = int(seq_lens[b])
+        nslots = L if ring <= 0 else (L if L <= n_sink else sink_pad + min(ring, L - n_sink))
+        K, V = _gather_seq(k_cache, v_cache, block_tables[b], nslots)
+        qpos = torch.arange(L - ql, L, device=q.device)
+        o = _attend_one(q[s0:s1], q_sink[s0:s1] if q_sink is not None else None, qpos, K, V, L,
+                        scale, n_sink, sink_pad, ring, window)
+        out[s0:s1] = o.to(q.dtype)
+    return out
+
+
+# ----------------------------------------------------------------------------- sampling
+def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
+           top_k: Optional[torch.Tensor] = None, top_p: Optional[torch.Tensor] = None,
+           generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    B, V = logits.shape
+    out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    for b in range(B):
+        x = logits[b].float()
+        t = float(temperature[b]) if temperature is not None else 0.0
+        if not t > 0:
+            out[b] = int(torch.argmax(x))
+            continue
+        x = x / t
+        k = int(top_k[b]) if top_k is not None else 0
+        if 0 < k < V:
+            thr = torch.topk(x, k).values[-1]
+            x = x.masked_fill(x < thr, float("-inf"))
+        p = float(top_p[b]) if top_p is not None else 1.0
+        if p < 1.0:
+            probs = torch.softmax(x, -1)
+            sp, si = torch.sort(probs, descending=True)
+            cum = torch.cumsum(sp, 0)
+            keep_n = int(torch.searchsorted(cum, torch.tensor(p * float(cum[-1])))) + 1
+            thr = sp[min(keep_n, V) - 1]
+            x = x.masked_fill(probs < thr, float("-inf"))
+        probs = torch.softmax(x, -1)
+        out[b] = int(torch.multinomial(probs, 1, generator=generator))
+    return out
+
+
+# ----------------------------------------------------------------------------- rope table
+def build_cos_sin(head_dim: int, max_pos: int, theta: float, rope_scaling=None,
+                  device=None) -> torch.Tensor:
+    """fp32 table [max_pos, head_dim] = (cos | sin) of the rotate-half convention, with llama3
+    frequency scaling when configured (HF ``_compute_llama3_parameters`` semantics)."""
+    inv_freq = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    attn_factor = 1.0
+    if rope_scaling:
+        rt = rope_scaling.get("rope_type", rope_scaling.get("type"))
+        if rt == "llama3":
+            factor = rope_scaling["factor"]
+            lo = rope_scaling.get("low_freq_factor", 1.0)
+            hi = rope_scaling.get("high_freq_factor", 4.0)
+            old = rope_scaling.get("original_max_position_embeddings", 8192)
+            lo_wl, hi_wl = old / lo, old / hi
+            wl = 2 * math.pi / inv_freq
+            scaled = torch.where(wl > lo_wl, inv_freq / factor, inv_freq)
+            smooth = (old / wl - lo) / (hi - lo)
+            smoothed = (1 - smooth) * scaled / factor + smooth * scaled
+            is_med = (wl >= hi_wl) & (wl <= lo_wl)
+            inv_freq = torch.where(is_med, smoothed, scaled)
+        elif rt == "linear":
+            inv_freq = inv_freq / rope_scaling["factor"]
+        elif rt == "dynamic":
+            pass  # only changes beyond max_position_embeddings; tables are built per length
+        else:
+            raise ValueError(f"unsupported rope_scaling type {rt!r}")
+    t = torch.arange(max_pos, dtype=torch.float64)
+    freqs = torch.outer(t, inv_freq)
+    cs = torch.cat([freqs.cos() * attn_factor, freqs.sin() * attn_factor], dim=-1)
+    return cs.to(torch.float32).to(device) if device is not None else cs.to(torch.float32)

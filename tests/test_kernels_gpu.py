@@ -1,0 +1,225 @@
+"""Numerics of every CDNA4 HIP kernel against the plain-PyTorch fp32 reference (ops/reference.py).
+
+Run on an MI355X: ``python -m pytest tests -m gpu``.
+"""
+import math
+
+import pytest
+import torch
+
+from distributed_llm_inference import ops
+from distributed_llm_inference.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def _close(a, b, atol, rtol=0.0, msg=""):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol)
+    assert not bad.any(), f"{msg} max err {err.max().item():.4g} at {bad.nonzero()[:5].tolist()}"
+
+
+@pytest.mark.parametrize("rows,hidden", [(1, 128), (5, 4096), (7, 8192), (3, 1000 * 8)])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rms_norm(gpu, rows, hidden, with_res):
+    torch.manual_seed(0)
+    x = torch.randn(rows, hidden, device=gpu, dtype=BF)
+    w = (1 + 0.1 * torch.randn(hidden, device=gpu)).to(BF)
+    r = torch.randn(rows, hidden, device=gpu, dtype=BF) if with_res else None
+    r_ref = r.clone().cpu() if with_res else None
+    y, r2 = ops.rms_norm(x, w, 1e-5, residual=r)
+    y_ref, r_ref2 = ref.rms_norm(x.cpu(), w.cpu(), 1e-5, residual=r_ref)
+    _close(y, y_ref, 2e-2, 1e-2, "rms_norm")
+    if with_res:
+        _close(r2, r_ref2, 1e-2, 1e-2, "residual")
+
+
+def test_layer_norm(gpu):
+    x = torch.randn(9, 768, device=gpu, dtype=BF)
+    w = torch.randn(768, device=gpu, dtype=BF)
+    b = torch.randn(768, device=gpu, dtype=BF)
+    y, _ = ops.layer_norm(x, w, b, 1e-5)
+    y_ref, _ = ref.layer_norm(x.cpu(), w.cpu(), b.cpu(), 1e-5)
+    _close(y, y_ref, 5e-2, 2e-2, "layer_norm")
+
+
+def test_silu_mul_gelu_add(gpu):
+    x = torch.randn(13, 2 * 1024, device=gpu, dtype=BF)
+    _close(ops.silu_mul(x), ref.silu_mul(x.cpu()), 1e-2, 1e-2, "silu_mul")
+    b = torch.randn(2048, device=gpu, dtype=BF)
+    _close(ops.gelu_bias(x, b), ref.gelu_bias(x.cpu(), b.cpu()), 2e-2, 1e-2, "gelu")
+    y = torch.randn_like(x)
+    _close(ops.add(x, y), (x.float() + y.float()), 1e-2, 1e-2, "add")
+
+
+def _make_cache(nblocks, nkv, bs, D, dev):
+    k = torch.randn(nblocks, nkv, bs, D, device=dev, dtype=BF)
+    v = torch.randn(nblocks, nkv, D, bs, device=dev, dtype=BF)
+    return k, v
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (8, 8, 64), (4, 2, 32)])
+@pytest.mark.parametrize("window", [0, 64])
+def test_rope_cache(gpu, nh, nkv, D, window):
+    torch.manual_seed(1)
+    T, bs, nblocks = 37, 64, 16
+    qkv = torch.randn(T, (nh + 2 * nkv) * D, device=gpu, dtype=BF)
+    pos = torch.randint(0, 300, (T,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(nblocks * bs, device=gpu)[:T].to(torch.int64)
+    slots[3] = -1  # a token that is not written
+    cs = ref.build_cos_sin(D, 512, 500000.0, device=gpu)
+    k1, v1 = _make_cache(nblocks, nkv, bs, D, gpu)
+    k2, v2 = k1.clone().cpu(), v1.clone().cpu()
+    q, qs = ops.rope_cache(qkv, pos, slots, cs, nh, nkv, D, k1, v1, window=window,
+                           want_sink=window > 0)
+    q_r, qs_r = ref.rope_cache(qkv.cpu(), pos.cpu(), slots.cpu(), cs.cpu(), nh, nkv, D, k2, v2,
+                               window, window > 0)
+    _close(q, q_r, 2e-2, 1e-2, "q")
+    if window:
+        _close(qs, qs_r, 2e-2, 1e-2, "q_sink")
+    _close(k1, k2, 2e-2, 1e-2, "k_cache")
+    _close(v1, v2, 0.0, 0.0, "v_cache")
+
+
+def _tables(B, max_blocks, nblocks, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    perm = torch.randperm(nblocks, generator=g)[: B * max_blocks]
+    return perm.reshape(B, max_blocks).to(torch.int32).to(dev)
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(64, 8, 128), (32, 8, 128), (12, 12, 64), (4, 2, 32)])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_attn_decode(gpu, nh, nkv, D, splits):
+    torch.manual_seed(2)
+    bs, B = 64, 6
+    lens = torch.tensor([1, 0, 33, 64, 257, 1000], dtype=torch.int32)
+    max_blocks = (int(lens.max()) + bs - 1) // bs
+    nblocks = B * max_blocks + 3
+    kc, vc = _make_cache(nblocks, nkv, bs, D, gpu)
+    bt = _tables(B, max_blocks, nblocks, gpu)
+    q = torch.randn(B, nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    out = ops.attn_decode(q, None, kc, vc, bt, lens.to(gpu), scale, num_splits=splits)
+    out_r = ref.attn_decode(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, scale)
+    _close(out, out_r, 2e-2, 2e-2, "decode")
+
+
+@pytest.mark.parametrize("splits", [1, 2])
+def test_attn_decode_window(gpu, splits):
+    torch.manual_seed(3)
+    nh, nkv, D, bs = 32, 8, 128, 64
+    n_sink, sink_pad, window, ring = 4, 32, 100, 160
+    lens = torch.tensor([3, 50, 104, 200, 517], dtype=torch.int32)
+    B = lens.numel()
+    max_blocks = (sink_pad + ring + bs - 1) // bs
+    nblocks = B * max_blocks
+    kc, vc = _make_cache(nblocks, nkv, bs, D, gpu)
+    bt = _tables(B, max_blocks, nblocks, gpu, seed=1)
+    q = torch.randn(B, nh, D, device=gpu, dtype=BF)
+    qs = torch.randn(B, nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    out = ops.attn_decode(q, qs, kc, vc, bt, lens.to(gpu), scale, n_sink, sink_pad, ring, window,
+                          num_splits=splits)
+    out_r = ref.attn_decode(q.cpu(), qs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), lens, scale, n_sink,
+                            sink_pad, ring, window)
+    _close(out, out_r, 2e-2, 2e-2, "decode-window")
+
+
+@pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (8, 8, 64), (4, 2, 32)])
+def test_attn_prefill(gpu, nh, nkv, D):
+    torch.manual_seed(4)
+    bs = 64
+    q_lens = [5, 64, 130, 1]
+    ctx = [0, 10, 70, 300]  # tokens already in the cache before this chunk
+    lens = torch.tensor([a + b for a, b in zip(q_lens, ctx)], dtype=torch.int32)
+    B = len(q_lens)
+    q_start = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
+    T = int(q_start[-1])
+    max_blocks = (int(lens.max()) + bs - 1) // bs
+    nblocks = B * max_blocks
+    kc, vc = _make_cache(nblocks, nkv, bs, D, gpu)
+    bt = _tables(B, max_blocks, nblocks, gpu, seed=2)
+    q = torch.randn(T, nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    out = ops.attn_prefill(q, None, kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens), scale)
+    out_r = ref.attn_prefill(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale)
+    _close(out, out_r, 2e-2, 2e-2, "prefill")
+
+
+def test_attn_prefill_window(gpu):
+    torch.manual_seed(5)
+    nh, nkv, D, bs = 8, 2, 64, 64
+    n_sink, sink_pad, window, ring = 4, 32, 96, 192
+    q_lens = [40, 7]
+    lens = torch.tensor([40, 300], dtype=torch.int32)
+    B = 2
+    q_start = torch.tensor([0, 40, 47], dtype=torch.int32)
+    max_blocks = (sink_pad + ring + bs - 1) // bs
+    kc, vc = _make_cache(B * max_blocks, nkv, bs, D, gpu)
+    bt = _tables(B, max_blocks, B * max_blocks, gpu, seed=3)
+    q = torch.randn(47, nh, D, device=gpu, dtype=BF)
+    qs = torch.randn(47, nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    out = ops.attn_prefill(q, qs, kc, vc, bt, lens.to(gpu), q_start.to(gpu), 40, scale, n_sink,
+                           sink_pad, ring, window)
+    out_r = ref.attn_prefill(q.cpu(), qs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale,
+                             n_sink, sink_pad, ring, window)
+    _close(out, out_r, 2e-2, 2e-2, "prefill-window")
+
+
+def test_sample_greedy_and_topk1(gpu):
+    torch.manual_seed(6)
+    B, V = 9, 128256
+    logits = torch.randn(B, V, device=gpu, dtype=BF) * 3
+    greedy = ops.sample(logits)
+    assert torch.equal(greedy.cpu().long(), logits.float().argmax(-1).cpu())
+    t = torch.full((B,), 0.7, device=gpu)
+    k1 = torch.ones(B, dtype=torch.int32, device=gpu)
+    # fp32 logits: bf16 rows of 128k values contain tied maxima, which top-k=1 keeps together
+    lf = torch.randn(B, V, device=gpu) * 3
+    s = ops.sample(lf, temperature=t, top_k=k1, seeds=torch.arange(B, device=gpu))
+    assert torch.equal(s.cpu().long(), lf.argmax(-1).cpu())
+    lp = torch.empty(B, device=gpu)
+    ops.sample(logits.float(), out=torch.empty(B, dtype=torch.int32, device=gpu), logprobs=lp)
+    lp_ref = torch.log_softmax(logits.float(), -1).max(-1).values
+    _close(lp, lp_ref, 1e-3, 1e-3, "logprob")
+
+
+def test_sample_distribution(gpu):
+    # V small, many rows with the same logits -> empirical frequencies ~ softmax
+    V, B = 16, 4096
+    base = torch.linspace(-2, 2, V, device=gpu)
+    logits = base.repeat(B, 1).contiguous()
+    t = torch.ones(B, device=gpu)
+    s = ops.sample(logits, temperature=t, seeds=torch.arange(B, device=gpu) * 7919)
+    freq = torch.bincount(s.long().cpu(), minlength=V).float() / B
+    p = torch.softmax(base.cpu(), -1)
+    assert (freq - p).abs().max() < 0.03
+    # top-k=4 keeps only the 4 largest
+    s = ops.sample(logits, temperature=t, top_k=torch.full((B,), 4, dtype=torch.int32, device=gpu),
+                   seeds=torch.arange(B, device=gpu))
+    assert int(s.min()) >= V - 4
+    # top-p=0.5 keeps the smallest top set with mass >= 0.5
+    sp, _ = torch.sort(p, descending=True)
+    need = int((torch.cumsum(sp, 0) < 0.5).sum()) + 1
+    s = ops.sample(logits, temperature=t, top_p=torch.full((B,), 0.5, device=gpu),
+                   seeds=torch.arange(B, device=gpu))
+    assert int(s.min()) >= V - need
+
+
+def test_quant_rowwise(gpu):
+    x = torch.randn(17, 4096, device=gpu, dtype=BF) * 3
+    q, s = ops.quant_rowwise(x)
+    deq = q.float() * s
+    rel = (deq - x.float()).abs().max() / x.float().abs().max()
+    assert rel < 0.07
+    w = (1 + 0.1 * torch.randn(4096, device=gpu)).to(BF)
+    r = torch.randn_like(x)
+    r2 = r.clone()
+    q2, s2 = ops.quant_rowwise(x, residual=r, norm_w=w, eps=1e-5)
+    y, _ = ref.rms_norm(x.cpu(), w.cpu(), 1e-5, residual=r2.cpu())
+    deq2 = (q2.float() * s2).cpu()
+    assert (deq2 - y.float()).abs().max() / y.float().abs().max() < 0.07
