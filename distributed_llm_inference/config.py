@@ -129,7 +129,11 @@ class ModelSpec:
             raise ValueError(f"unsupported model_type {mt!r} (supported: llama, gpt2)")
         nh = cfg["num_attention_heads"]
         h = cfg["hidden_size"]
-        rs = cfg.get("rope_scaling")
+        # transformers 4.x: rope_theta + rope_scaling; transformers 5.x: rope_parameters
+        rp = cfg.get("rope_parameters") or {}
+        rope_theta = cfg.get("rope_theta", rp.get("rope_theta", 10000.0))
+        rs = cfg.get("rope_scaling") or ({k: v for k, v in rp.items() if k != "rope_theta"}
+                                         if rp else None)
         if rs is not None and rs.get("rope_type", rs.get("type")) in (None, "default"):
             rs = None
         eos = cfg.get("eos_token_id")
@@ -145,7 +149,7 @@ class ModelSpec:
             num_kv_heads=cfg.get("num_key_value_heads") or nh,
             head_dim=cfg.get("head_dim") or h // nh,
             rms_norm_eps=cfg.get("rms_norm_eps", 1e-6),
-            rope_theta=float(cfg.get("rope_theta", 10000.0)),
+            rope_theta=float(rope_theta),
             rope_scaling=tuple(sorted(rs.items())) if rs else None,
             max_position_embeddings=cfg.get("max_position_embeddings", 4096),
             tie_word_embeddings=bool(cfg.get("tie_word_embeddings", False)),

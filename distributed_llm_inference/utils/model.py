@@ -1,0 +1,260 @@
+"""Checkpoint loading / random init / quantisation of stages.
+
+Reference: /root/reference/distributed_llm_inference/utils/model.py —
+``get_sharded_block_state_from_file`` (:16-24), ``get_block_state_dict`` (:27-52), ``_load_layer``
+(:55-72), ``load_block`` (:75-90), ``convert_to_optimized_block`` (:116-123).  Same API; fixes:
+  * B14 — index (``model.safetensors.index.json``), single-file (``model.safetensors``) and local
+    directories all work; nothing is fetched from the network (the benchmark boxes have none):
+    hub repos are resolved from the local HF cache only;
+  * B16 — weights load in bf16 (MI355X native), not fp16;
+  * B10/B11 — quantisation happens only when asked (``use_quantized`` is wired through) and is
+    fp8 e4m3 with per-channel scales (CDNA4 fp8 MFMA via hipBLASLt), not bitsandbytes int8;
+  * a random-init path builds any config without a checkpoint (``random_init=True``).
+Weights are read with ``safetensors`` (memory-mapped, no pickle execution).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+from typing import Dict, Iterable, List, Optional, Sequence
+
+import torch
+
+from ..config import ModelSpec, resolve_model
+from ..models.llama.model import LlamaBlock
+from ..models.stage import CausalLMStage, make_block
+
+log = logging.getLogger(__name__)
+
+INDEX_FILE_PATTERNS = ["model.safetensors.index.json", "model.safetensors"]
+
+
+def _resolve_file(repo: str, filename: str, cache_dir: Optional[str] = None,
+                  token=False) -> Optional[str]:
+    """Local path of ``filename`` in a local directory or in the local HF hub cache."""
+    if os.path.isdir(repo):
+        p = os.path.join(repo, filename)
+        return p if os.path.exists(p) else None
+    try:
+        from huggingface_hub import try_to_load_from_cache
+        p = try_to_load_from_cache(repo, filename, cache_dir=cache_dir)
+        return p if isinstance(p, str) and os.path.exists(p) else None
+    except Exception:  # pragma: no cover - hub layout differences
+        return None
+
+
+def get_sharded_block_state_from_file(file: str, block_prefix: str) -> Dict[str, torch.Tensor]:
+    """All tensors of ``file`` whose key starts with ``block_prefix`` (prefix stripped)."""
+    from safetensors import safe_open
+    out = {}
+    with safe_open(file, framework="pt", device="cpu") as f:
+        for key in f.keys():
+            if key.startswith(block_prefix):
+                out[key[len(block_prefix):]] = f.get_tensor(key)
+    return out
+
+
+def _weight_files(repo: str, cache_dir=None, token=False) -> Dict[str, str]:
+    """Map tensor name -> local shard path."""
+    idx = _resolve_file(repo, "model.safetensors.index.json", cache_dir, token)
+    if idx is not None:
+        with open(idx) as f:
+            index = json.load(f)
+        if "weight_map" not in index:
+            raise ValueError("Index file does not contain a weight map")
+        out = {}
+        for k, shard in index["weight_map"].items():
+            p = _resolve_file(repo, shard, cache_dir, token)
+            if p is None:
+                raise FileNotFoundError(f"shard {shard} of {repo} is not available locally")
+            out[k] = p
+        return out
+    single = _resolve_file(repo, "model.safetensors", cache_dir, token)
+    if single is not None:
+        from safetensors import safe_open
+        with safe_open(single, framework="pt", device="cpu") as f:
+            return {k: single for k in f.keys()}
+    raise FileNotFoundError(
+        f"no safetensors checkpoint found for {repo!r} (local dir or local HF cache); "
+        "use random_init=True to build the architecture without weights")
+
+
+def get_block_state_dict(repo: str, block_idx: int, cache_dir: Optional[str] = None,
+                         token=False, prefix_fmt: str = "model.layers.{}.") -> Dict[str, torch.Tensor]:
+    """State dict of decoder layer ``block_idx``, reading only the shards that contain it."""
+    prefix = prefix_fmt.format(block_idx)
+    files = sorted({p for k, p in _weight_files(repo, cache_dir, token).items() if k.startswith(prefix)})
+    sd: Dict[str, torch.Tensor] = {}
+    for f in files:
+        sd.update(get_sharded_block_state_from_file(f, prefix))
+    if not sd:
+        raise KeyError(f"layer {block_idx} not found in {repo}")
+    return sd
+
+
+def _load_config(model_name: str, cache_dir=None, token=False) -> ModelSpec:
+    try:
+        return resolve_model(model_name)
+    except ValueError:
+        p = _resolve_file(model_name, "config.json", cache_dir, token)
+        if p is None:
+            raise
+        return ModelSpec.from_hf_config(p)
+
+
+def load_block(model_name: str, layer_ids: Sequence[int], use_quantized: bool = False,
+               cache_dir: Optional[str] = None, token=False, device=None,
+               dtype: torch.dtype = torch.bfloat16, random_init: bool = False,
+               seed: int = 0) -> LlamaBlock:
+    """Build the block of ``layer_ids`` and load its weights (per layer, only the needed shards)."""
+    spec = _load_config(model_name, cache_dir, token)
+    log.info("building %s block for layers %s", spec.name, list(layer_ids))
+    block = make_block(spec, layer_ids, device=device, dtype=dtype)
+    if random_init:
+        block.init_random(seed)
+    else:
+        prefix_fmt = "transformer.h.{}." if spec.arch == "gpt2" else "model.layers.{}."
+        for layer in block.layers:
+            log.info("loading weights for layer %d", layer.layer_idx)
+            sd = get_block_state_dict(model_name, layer.layer_idx, cache_dir, token, prefix_fmt)
+            layer.load_hf_state_dict(sd)
+    if use_quantized:
+        block.quantize_fp8()
+    return block
+
+
+def convert_to_optimized_block(block, quantize: bool = False, threshold: float = 5.0,
+                               device=None):
+    """Move a block to the GPU and (only if ``quantize``) convert its linears to fp8.
+
+    ``threshold`` is accepted for API compatibility with the reference's LLM.int8 outlier
+    threshold; fp8 e4m3 has enough dynamic range that no outlier decomposition is needed.
+    """
+    if device is None:
+        if not torch.cuda.is_available():
+            if quantize:
+                raise NotImplementedError("fp8 quantisation needs an MI355X GPU")
+            return block
+        device = torch.device("cuda", torch.cuda.current_device())
+    block = block.to(device)
+    if quantize:
+        block.quantize_fp8()
+    return block
+
+
+# --------------------------------------------------------------------------- whole stages
+def load_stage_weights(stage: CausalLMStage, model_name: str, cache_dir=None, token=False) -> None:
+    """Load layers + (embedding / final norm / LM head, if owned) of a stage from a checkpoint."""
+    spec = stage.spec
+    files = _weight_files(model_name, cache_dir, token)
+    needed_prefixes = []
+    if spec.arch == "gpt2":
+        lp = "transformer.h.{}."
+        extra = {"embed": ["transformer.wte.weight", "transformer.wpe.weight"],
+                 "head": ["transformer.ln_f.weight", "transformer.ln_f.bias"]}
+    else:
+        lp = "model.layers.{}."
+        extra = {"embed": ["model.embed_tokens.weight"],
+                 "head": ["model.norm.weight", "lm_head.weight"]}
+    for layer in stage.block.layers:
+        layer.load_hf_state_dict(get_block_state_dict(model_name, layer.layer_idx, cache_dir, token, lp))
+    want = []
+    if stage.embed is not None:
+        want += extra["embed"]
+    if stage.head is not None:
+        want += extra["head"]
+    sd = {}
+    for f in sorted({files[k] for k in want if k in files}):
+        from safetensors import safe_open
+        with safe_open(f, framework="pt", device="cpu") as fh:
+            for k in want:
+                if k in fh.keys():
+                    sd[k] = fh.get_tensor(k)
+    load_stage_extras(stage, sd)
+
+
+def load_stage_extras(stage: CausalLMStage, sd: Dict[str, torch.Tensor]) -> None:
+    """Embedding / final norm / head from a (partial) HF state dict with full key names."""
+    spec = stage.spec
+    with torch.no_grad():
+        if spec.arch == "gpt2":
+            if stage.embed is not None:
+                stage.embed.weight.copy_(sd["transformer.wte.weight"])
+                if stage.embed.position is not None and "transformer.wpe.weight" in sd:
+                    stage.embed.position.copy_(sd["transformer.wpe.weight"])
+            if stage.head is not None:
+                stage.head.norm_weight.copy_(sd["transformer.ln_f.weight"])
+                stage.head.norm_bias.copy_(sd["transformer.ln_f.bias"])
+        else:
+            if stage.embed is not None:
+                stage.embed.weight.copy_(sd["model.embed_tokens.weight"])
+            if stage.head is not None:
+                stage.head.norm_weight.copy_(sd["model.norm.weight"])
+                if stage.head.proj is not None:
+                    w = sd.get("lm_head.weight", sd.get("model.embed_tokens.weight"))
+                    stage.head.proj.weight.copy_(w)
+
+
+def stage_from_hf_model(hf_model, start: int, end: int, device=None,
+                        dtype=torch.bfloat16) -> CausalLMStage:
+    """Build a stage from an in-memory HF ``*ForCausalLM`` (tests / conversions)."""
+    spec = ModelSpec.from_hf_config(hf_model.config)
+    stage = CausalLMStage(spec, start, end, device=device, dtype=dtype)
+    full = {k: v.detach() for k, v in hf_model.state_dict().items()}
+    lp = "transformer.h.{}." if spec.arch == "gpt2" else "model.layers.{}."
+    for layer in stage.block.layers:
+        pre = lp.format(layer.layer_idx)
+        layer.load_hf_state_dict({k[len(pre):]: v for k, v in full.items() if k.startswith(pre)})
+    load_stage_extras(stage, full)
+    return stage
+
+
+def build_stage(model: str, start: int, end: int, device=None, dtype=torch.bfloat16,
+                random_init: bool = True, seed: int = 0, quantize: bool = False,
+                checkpoint: Optional[str] = None) -> CausalLMStage:
+    """Construct a stage for ``[start, end)``; random-init or load from ``checkpoint``."""
+    spec = _load_config(checkpoint or model)
+    stage = CausalLMStage(spec, start, end, device=device, dtype=dtype)
+    if random_init and checkpoint is None:
+        stage.init_random(seed)
+    else:
+        load_stage_weights(stage, checkpoint or model)
+    if quantize:
+        stage.quantize_fp8()
+    return stage
+
+
+def save_random_checkpoint(spec: ModelSpec, path: str, seed: int = 0, shard_layers: int = 2) -> None:
+    """Write a random-init HF-format sharded checkpoint (config.json + safetensors + index)."""
+    from safetensors.torch import save_file
+    os.makedirs(path, exist_ok=True)
+    with open(os.path.join(path, "config.json"), "w") as f:
+        json.dump(spec.to_hf_dict(), f)
+    stage = CausalLMStage(spec, 0, spec.num_layers).init_random(seed)
+    lp = "transformer.h.{}." if spec.arch == "gpt2" else "model.layers.{}."
+    weight_map = {}
+    shards: List[Dict[str, torch.Tensor]] = []
+    for li, layer in enumerate(stage.block.layers):
+        if li % shard_layers == 0:
+            shards.append({})
+        for k, v in layer.hf_state_dict().items():
+            shards[-1][lp.format(layer.layer_idx) + k] = v.contiguous().clone()
+    extra = {}
+    if spec.arch == "gpt2":
+        extra["transformer.wte.weight"] = stage.embed.weight.data.clone()
+        extra["transformer.wpe.weight"] = stage.embed.position.data.clone()
+        extra["transformer.ln_f.weight"] = stage.head.norm_weight.data.clone()
+        extra["transformer.ln_f.bias"] = stage.head.norm_bias.data.clone()
+    else:
+        extra["model.embed_tokens.weight"] = stage.embed.weight.data.clone()
+        extra["model.norm.weight"] = stage.head.norm_weight.data.clone()
+        if stage.head.proj is not None:
+            extra["lm_head.weight"] = stage.head.proj.weight.data.clone()
+    shards.append(extra)
+    for i, sh in enumerate(shards):
+        name = f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors"
+        save_file(sh, os.path.join(path, name))
+        weight_map.update({k: name for k in sh})
+    with open(os.path.join(path, "model.safetensors.index.json"), "w") as f:
+        json.dump({"metadata": {}, "weight_map": weight_map}, f)

@@ -1,0 +1,142 @@
+"""Numerics of the model stages on CPU against the installed HF transformers implementations.
+
+These run the same code path as the GPU runtime (packed varlen tokens, paged KV pool, native
+block manager) with the torch reference ops, so they pin the *model* semantics (RoPE incl. llama3
+scaling, GQA, causal masking, residual stream, RMSNorm eps, GPT-2 Conv1D layout) independently of
+the kernels, whose numerics are pinned by tests/test_kernels_gpu.py.
+"""
+import math
+
+import pytest
+import torch
+
+from distributed_llm_inference.config import ModelSpec
+from distributed_llm_inference.models import CausalLMStage
+from distributed_llm_inference.ops.reference import build_cos_sin
+from distributed_llm_inference.utils.model import stage_from_hf_model
+
+transformers = pytest.importorskip("transformers")
+
+
+def _hf_llama(layers=3, rope_scaling=None, seed=0):
+    from transformers import LlamaConfig, LlamaForCausalLM
+    torch.manual_seed(seed)
+    kw = dict(vocab_size=256, hidden_size=128, intermediate_size=256, num_hidden_layers=layers,
+              num_attention_heads=4, num_key_value_heads=2, rms_norm_eps=1e-5,
+              max_position_embeddings=16384, tie_word_embeddings=False)
+    if rope_scaling:
+        kw["rope_parameters"] = dict(rope_scaling, rope_theta=500000.0)
+    else:
+        kw["rope_parameters"] = {"rope_type": "default", "rope_theta": 10000.0}
+    cfg = LlamaConfig(**kw)
+    m = LlamaForCausalLM(cfg).eval()
+    with torch.no_grad():  # round weights to bf16 so both sides see identical parameters
+        for p in m.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    return m
+
+
+def _run_stage(stage, prompts, decode_steps=0, hf=None):
+    """Prefill all prompts as one varlen batch, then greedy-decode; returns list of logits rows."""
+    pool = stage.make_pool(64, block_size=32)
+    m = pool.manager
+    sids = list(range(len(prompts)))
+    for s, p in zip(sids, prompts):
+        m.append(s, len(p))
+    meta = pool.build_metadata(sids, [len(p) for p in prompts])
+    ends = torch.cumsum(torch.tensor([len(p) for p in prompts]), 0) - 1
+    meta.logits_rows = ends
+    ids = torch.tensor([t for p in prompts for t in p])
+    logits = [stage(ids, meta, pool).float()]
+    toks = logits[-1].argmax(-1)
+    for _ in range(decode_steps):
+        for s in sids:
+            m.append(s, 1)
+        meta = pool.build_metadata(sids, [1] * len(sids))
+        logits.append(stage(toks.to(torch.int32), meta, pool).float())
+        toks = logits[-1].argmax(-1)
+    return logits
+
+
+@pytest.mark.parametrize("rope_scaling", [None, {"rope_type": "llama3", "factor": 8.0,
+                                                  "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                                  "original_max_position_embeddings": 64}])
+def test_llama_prefill_and_decode_match_hf(rope_scaling):
+    hf = _hf_llama(rope_scaling=rope_scaling)
+    stage = stage_from_hf_model(hf, 0, hf.config.num_hidden_layers)
+    prompts = [[5, 17, 99, 3, 250, 7, 7, 1, 42, 11, 19], [8, 2, 64]]
+    steps = 4
+    ours = _run_stage(stage, prompts, decode_steps=steps)
+    # HF reference: run each full sequence (prompt + our generated tokens) without cache
+    gen = torch.stack([o.argmax(-1) for o in ours], 1)  # [B, steps+1]
+    for b, p in enumerate(prompts):
+        seq = torch.tensor(p + gen[b, :steps].tolist())[None]
+        with torch.no_grad():
+            ref_logits = hf(seq).logits[0].float()
+        for s in range(steps + 1):
+            pos = len(p) - 1 + s
+            a, r = ours[s][b], ref_logits[pos]
+            err = (a - r).abs().max().item()
+            assert err < 0.05 * max(1.0, r.abs().max().item()), f"b={b} step={s} err={err}"
+
+
+def test_rope_table_matches_hf_llama3():
+    from transformers.models.llama.modeling_llama import LlamaRotaryEmbedding
+    from transformers import LlamaConfig
+    rs = {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+          "original_max_position_embeddings": 8192, "rope_theta": 500000.0}
+    cfg = LlamaConfig(hidden_size=4096, num_attention_heads=32, rope_parameters=rs,
+                      max_position_embeddings=131072)
+    rot = LlamaRotaryEmbedding(cfg)
+    pos = torch.tensor([[0, 1, 100, 5000, 20000, 100000]])
+    cos, sin = rot(torch.zeros(1, dtype=torch.float32), pos)
+    table = build_cos_sin(128, 100001, 500000.0, {k: v for k, v in rs.items() if k != "rope_theta"})
+    ours = table[pos[0]]
+    # HF forms position*inv_freq in fp32 (error grows ~linearly with position); ours is fp64-exact
+    tol = (2e-4 + 1e-7 * pos[0].float())[:, None]
+    assert ((ours[:, :64] - cos[0, :, :64]).abs() <= tol).all()
+    assert ((ours[:, 64:] - sin[0, :, :64]).abs() <= tol).all()
+
+
+def test_pipeline_split_equals_single_stage():
+    spec = ModelSpec(name="t", vocab_size=300, hidden_size=128, intermediate_size=256, num_layers=4,
+                     num_heads=4, num_kv_heads=2, head_dim=32, rope_theta=10000.0,
+                     max_position_embeddings=2048)
+    full = CausalLMStage(spec, 0, 4).init_random(7)
+    s0 = CausalLMStage(spec, 0, 2).init_random(7)
+    s1 = CausalLMStage(spec, 2, 4).init_random(7)
+    prompts = [[1, 2, 3, 4, 5], [9, 8]]
+    ref = _run_stage(full, prompts, decode_steps=2)
+    # run the two stages by hand with their own pools
+    p0, p1 = s0.make_pool(64, 32), s1.make_pool(64, 32)
+    sids = [0, 1]
+    for pool in (p0, p1):
+        for s, p in zip(sids, prompts):
+            pool.manager.append(s, len(p))
+    ids = torch.tensor([t for p in prompts for t in p])
+    m0 = p0.build_metadata(sids, [5, 2])
+    m1 = p1.build_metadata(sids, [5, 2], logits_rows=torch.tensor([4, 6]))
+    h = s0(ids, m0, p0)
+    out = s1(h, m1, p1).float()
+    assert torch.allclose(out, ref[0], atol=1e-2, rtol=1e-2)
+
+
+def test_gpt2_matches_hf():
+    from transformers import GPT2Config, GPT2LMHeadModel
+    torch.manual_seed(0)
+    cfg = GPT2Config(vocab_size=256, n_embd=128, n_layer=2, n_head=4, n_positions=128)
+    hf = GPT2LMHeadModel(cfg).eval()
+    with torch.no_grad():
+        for p in hf.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    stage = stage_from_hf_model(hf, 0, 2)
+    prompts = [[3, 1, 4, 1, 5, 9, 2, 6], [2, 7, 1]]
+    ours = _run_stage(stage, prompts, decode_steps=2)
+    gen = torch.stack([o.argmax(-1) for o in ours], 1)
+    for b, p in enumerate(prompts):
+        seq = torch.tensor(p + gen[b, :2].tolist())[None]
+        with torch.no_grad():
+            ref_logits = hf(seq).logits[0].float()
+        for s in range(3):
+            a, r = ours[s][b], ref_logits[len(p) - 1 + s]
+            assert (a - r).abs().max() < 0.05 * max(1.0, r.abs().max().item())
