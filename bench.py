@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""Headline benchmark: output tokens/s (whole node) + p50 per-token latency, Llama-3-70B, PP=N.
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One process per GPU; stage i of an N-stage pipeline (``plan_stages``) on GPU i; hidden states
+move over RCCL P2P (xGMI), the control plane over shared memory.  Random-init weights of the real
+Llama-3-70B architecture (bf16), synthetic random prompts.  Work per GPU is fixed as N grows
+(M = N+1 micro-batches of ``--batch-per-mb`` sequences, N=1 uses M=2 for host/GPU overlap), so the
+scaling mode is "weak".  A "step" = every in-flight sequence decodes one token.  Timed region:
+barrier + device sync -> exactly K decode steps -> barrier + device sync; the max over ranks is
+reported.  Prefill and W warmup steps (incl. hipGraph capture) run before the timed region.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "output tokens/sec (whole node) + p50 token latency, Llama-3-70B PP=8"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="llama-3-70b")
+    ap.add_argument("--batch-per-mb", type=int, default=128)
+    ap.add_argument("--micro-batches", type=int, default=0, help="0 = N+1 (N=1: 2)")
+    ap.add_argument("--prompt-len", type=int, default=512)
+    ap.add_argument("--max-batched-tokens", type=int, default=16384)
+    ap.add_argument("--fp8", action="store_true", help="fp8-e4m3 weights (BASELINE config 5)")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    from distributed_llm_inference import _build
+    from distributed_llm_inference.config import CacheConfig, ServeConfig, resolve_model
+    from distributed_llm_inference.runtime.engine import EngineConfig, init_pipeline_rank
+    from distributed_llm_inference.runtime.sequence import SamplingParams, Sequence
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one rank per GPU)")
+        raise SystemExit(f"WORLD_SIZE={world} != --gpus={a.gpus}")
+    if rank == 0:
+        _build.build_all()
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    spec = resolve_model(a.model)
+    M = a.micro_batches or (a.gpus + 1 if a.gpus > 1 else 2)
+    total_len = a.prompt_len + a.warmup + a.steps + 72
+    cfg = EngineConfig(
+        model=a.model, random_init=True, seed=0, quantize=a.fp8, pp=a.gpus,
+        cache=CacheConfig(block_size=64, gpu_memory_utilization=0.92),
+        serve=ServeConfig(max_batch_size=a.batch_per_mb, max_num_batched_tokens=a.max_batched_tokens,
+                          num_micro_batches=M, max_seq_len=total_len, use_graphs=not a.no_graphs,
+                          graph_batch_sizes=[a.batch_per_mb]))
+    t_init = time.perf_counter()
+    role, obj = init_pipeline_rank(cfg)
+    if role == "follower":
+        obj.run()
+        interval = obj.barrier_times[-1] - obj.barrier_times[-2] if len(obj.barrier_times) >= 2 else 0.0
+        t = torch.tensor([interval], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    drv = obj
+    init_s = time.perf_counter() - t_init
+    rng = random.Random(1234)
+    G = M * a.batch_per_mb
+    # generous max_tokens: sequences prefilled early keep decoding during the remaining prefill
+    # rounds, and none may finish inside the timed window (constant batch)
+    params = SamplingParams(max_tokens=a.warmup + a.steps + 64, ignore_eos=True)
+    seqs = [Sequence([rng.randrange(spec.vocab_size) for _ in range(a.prompt_len)], params)
+            for _ in range(G)]
+    for s in seqs:
+        drv.sched.add(s)
+    # prefill: run until every sequence produced its first token
+    t_pf = time.perf_counter()
+    while any(len(s.output) == 0 for s in seqs):
+        drv.round()
+    prefill_s = time.perf_counter() - t_pf
+    for _ in range(a.warmup):
+        drv.round()
+    drv.barrier()
+    if world > 1:
+        pass  # followers recorded the barrier time
+    n0 = sum(len(s.output) for s in seqs)
+    for s in seqs:
+        s.token_times.clear()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        drv.round()
+    drv.barrier()
+    t1 = time.perf_counter()
+    n1 = sum(len(s.output) for s in seqs)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        drv.stop()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    toks = n1 - n0
+    lat = []
+    for s in seqs:
+        tt = s.token_times
+        lat += [(tt[i + 1] - tt[i]) * 1e3 for i in range(len(tt) - 1)]
+    p50 = statistics.median(lat) if lat else float("nan")
+    p90 = statistics.quantiles(lat, n=10)[-1] if len(lat) >= 10 else float("nan")
+    value = toks / elapsed
+    res = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "tokens/s",
+        "n_gpus": a.gpus,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp8-weights/bf16-act" if a.fp8 else "bf16",
+        "data": "synthetic (random-init Llama-3-70B weights, random prompt tokens)",
+        "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
+                   "global_batch": G, "seq_len": total_len,
+                   "parallelism": f"pp{a.gpus}"},
+        "p50_token_latency_ms": round(p50, 3),
+        "p90_token_latency_ms": round(p90, 3),
+        "micro_batches": M,
+        "batch_per_micro_batch": a.batch_per_mb,
+        "prompt_len": a.prompt_len,
+        "tokens_timed": toks,
+        "prefill_s": round(prefill_s, 3),
+        "init_s": round(init_s, 1),
+    }
+    line = json.dumps(res)
+    print(line, flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

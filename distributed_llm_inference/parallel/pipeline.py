@@ -1,0 +1,296 @@
+"""Pipeline-parallel execution of stages.
+
+Topology (one node, one process per GPU, launched by ``distribute`` / torchrun):
+
+  rank 0 (driver)  : scheduler + stage 0 (embedding + first layers)
+  rank i (0<i<N-1) : middle layers
+  rank N-1         : last layers + final norm + LM head + sampling kernel
+
+Per micro-batch step:
+  * the driver publishes the step plan (sequence ids, new-token counts, frees, sampling params) on
+    a shared-memory broadcast channel (csrc/runtime/shm_channel.cpp) — the *control plane*;
+  * hidden states move rank i -> i+1 with RCCL send/recv over xGMI on dedicated streams — the
+    *data plane* (parallel/transport.py);
+  * the last rank's sampled token ids (B int32) come back to the driver on a second shm channel,
+    published by a helper thread once the sampling kernel's event completes, so the last stage
+    never stalls its own GPU queue waiting on a device->host copy.
+With M >= N micro-batches in flight every stage is busy; the driver plans micro-batch m's next step
+as soon as its tokens return (FIFO order == issue order).
+
+The same driver loop also runs an in-process pipeline (:class:`LocalPipeline`) — PP=1 on one GPU,
+or several stages in one process for tests / single-GPU rehearsal of PP=2/4/8.
+"""
+from __future__ import annotations
+
+import collections
+import logging
+import os
+import queue
+import threading
+import time
+from typing import Deque, Dict, List, Optional, Sequence
+
+import msgpack
+import torch
+import torch.distributed as dist
+
+from ..runtime.executor import StageExecutor, StepPlan
+from ..runtime.scheduler import Scheduler
+from ..runtime.sequence import SamplingParams, Sequence as Seq
+from .transport import LoopbackTransport, RcclTransport, TorchDistTransport, Transport
+
+log = logging.getLogger(__name__)
+
+
+def _runtime():
+    from .. import _runtime
+    return _runtime
+
+
+# =============================================================================================
+# driver loop (shared by the in-process and the multi-process pipeline)
+# =============================================================================================
+class DriverBase:
+    """Owns the scheduler; subclasses implement ``_issue(plan)`` and ``_collect(plan)``."""
+
+    def __init__(self, scheduler: Scheduler):
+        self.sched = scheduler
+        self.inflight: Deque[StepPlan] = collections.deque()
+        self.collect_times: Dict[int, List[float]] = collections.defaultdict(list)
+        self.tokens_generated = 0
+
+    # -- to implement
+    def _issue(self, plan: StepPlan) -> None:
+        raise NotImplementedError
+
+    def _collect(self, plan: StepPlan) -> List[int]:
+        raise NotImplementedError
+
+    def _broadcast_control(self, kind: str) -> None:
+        pass
+
+    # -- loop
+    def _collect_front(self) -> None:
+        p = self.inflight.popleft()
+        toks = self._collect(p)
+        now = time.perf_counter()
+        self.collect_times[p.mb].append(now)
+        self.tokens_generated += len(toks)
+        self.sched.on_tokens(p.mb, toks, now)
+
+    def round(self) -> bool:
+        """Give every micro-batch one step (collecting results as needed).  Returns False when
+        there is nothing left to do."""
+        progressed = False
+        for mb in range(self.sched.M):
+            while self.sched.inflight[mb] is not None:
+                self._collect_front()
+            plan = self.sched.plan(mb)
+            if plan is None:
+                continue
+            self._issue(plan)
+            if plan.seq_ids:
+                self.inflight.append(plan)
+            progressed = True
+        if not progressed:
+            if self.inflight:
+                self._collect_front()
+                return True
+            return False
+        return True
+
+    def drain(self) -> None:
+        while self.inflight:
+            self._collect_front()
+
+    def run_until_done(self) -> List[Seq]:
+        while self.round():
+            pass
+        self.drain()
+        return self.sched.pop_finished()
+
+    def generate(self, prompts: Sequence[Sequence[int]], params: Optional[SamplingParams] = None,
+                 eos_token_id: Optional[int] = None) -> List[Seq]:
+        params = params or SamplingParams()
+        seqs = [Seq(list(p), params) for p in prompts]
+        for s in seqs:
+            self.sched.add(s)
+        done = {s.seq_id: s for s in self.run_until_done()}
+        return [done.get(s.seq_id, s) for s in seqs]
+
+    def barrier(self) -> None:
+        """Drain everything in flight on every stage and synchronise all ranks."""
+        self.drain()
+        self._broadcast_control("barrier")
+
+    def stop(self) -> None:
+        self.drain()
+        self._broadcast_control("stop")
+
+
+def _sample_tokens_to_host(out: torch.Tensor):
+    """Async D2H of sampled tokens; returns (pinned tensor, event)."""
+    if out.is_cuda:
+        pinned = torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
+        pinned.copy_(out, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return pinned, ev
+    return out.clone(), None
+
+
+# =============================================================================================
+# in-process pipeline
+# =============================================================================================
+class LocalPipeline(DriverBase):
+    """All stages in this process (PP=1, or PP>1 loopback on one device / CPU)."""
+
+    def __init__(self, executors: List[StageExecutor], scheduler: Scheduler):
+        super().__init__(scheduler)
+        self.executors = executors
+        self._results: Dict[int, tuple] = {}
+
+    def _issue(self, plan: StepPlan) -> None:
+        x = None
+        for i, ex in enumerate(self.executors):
+            x = ex.execute(plan, x)
+        if plan.seq_ids:
+            self._results[plan.step] = _sample_tokens_to_host(x)
+
+    def _collect(self, plan: StepPlan) -> List[int]:
+        pinned, ev = self._results.pop(plan.step)
+        if ev is not None:
+            ev.synchronize()
+        return pinned.tolist()
+
+    def _broadcast_control(self, kind: str) -> None:
+        if any(ex.device.type == "cuda" for ex in self.executors):
+            torch.cuda.synchronize()
+
+
+# =============================================================================================
+# multi-process pipeline
+# =============================================================================================
+class _Channels:
+    """Shared-memory control (driver -> all) and token (last -> driver) channels."""
+
+    def __init__(self, job: str, rank: int, world: int, slot_size: int = 1 << 20):
+        R = _runtime()
+        self.ctrl = None
+        self.tok = None
+        if world == 1:
+            return
+        ctrl_name = f"/dli_{job}_ctrl"
+        tok_name = f"/dli_{job}_tok"
+        if rank == 0:
+            self.ctrl = R.ShmChannel(ctrl_name, -1, 64, slot_size, world - 1, True)
+            self.tok = R.ShmChannel(tok_name, 0, 64, slot_size, 1, False, 120.0)
+        else:
+            self.ctrl = R.ShmChannel(ctrl_name, rank - 1, 64, slot_size, world - 1, False, 120.0)
+            if rank == world - 1:
+                self.tok = R.ShmChannel(tok_name, -1, 64, slot_size, 1, True)
+
+
+class DistributedDriver(DriverBase):
+    """Rank 0 of a multi-process pipeline."""
+
+    def __init__(self, executor: StageExecutor, scheduler: Scheduler, transport: Transport,
+                 channels: _Channels, world: int, ctrl_group=None, timeout: float = 300.0):
+        super().__init__(scheduler)
+        self.ex = executor
+        self.tr = transport
+        self.ch = channels
+        self.world = world
+        self.group = ctrl_group
+        self.timeout = timeout
+
+    def _issue(self, plan: StepPlan) -> None:
+        self.ch.ctrl.send(msgpack.packb(plan.to_wire()), self.timeout)
+        out = self.ex.execute(plan, None)
+        if plan.seq_ids:
+            self.tr.send(out, 1)
+
+    def _collect(self, plan: StepPlan) -> List[int]:
+        msg = msgpack.unpackb(self.ch.tok.recv(self.timeout))
+        if msg["step"] != plan.step:
+            raise RuntimeError(f"token stream out of order: got step {msg['step']}, want {plan.step}")
+        return list(msg["tokens"])
+
+    def _broadcast_control(self, kind: str) -> None:
+        self.ch.ctrl.send(msgpack.packb({"kind": kind}), self.timeout)
+        if self.ex.device.type == "cuda":
+            torch.cuda.synchronize()
+        if kind == "barrier":
+            dist.barrier(group=self.group)
+
+
+class StageFollower:
+    """Ranks 1..N-1: execute plans as they are published."""
+
+    def __init__(self, executor: StageExecutor, transport: Transport, channels: _Channels,
+                 rank: int, world: int, ctrl_group=None, timeout: float = 300.0):
+        self.ex, self.tr, self.ch = executor, transport, channels
+        self.rank, self.world = rank, world
+        self.group = ctrl_group
+        self.timeout = timeout
+        self.is_last = rank == world - 1
+        self.barrier_times: List[float] = []
+        self._pub_q: "queue.Queue" = queue.Queue()
+        self._pub_thread = None
+        if self.is_last:
+            self._pub_thread = threading.Thread(target=self._publisher, daemon=True)
+            self._pub_thread.start()
+
+    def _publisher(self) -> None:
+        while True:
+            item = self._pub_q.get()
+            if item is None:
+                self._pub_q.task_done()
+                return
+            step, mb, pinned, ev = item
+            if ev is not None:
+                ev.synchronize()
+            self.ch.tok.send(msgpack.packb({"step": step, "mb": mb, "tokens": pinned.tolist()}),
+                             self.timeout)
+            self._pub_q.task_done()
+
+    def run(self) -> None:
+        while True:
+            msg = msgpack.unpackb(self.ch.ctrl.recv(self.timeout))
+            kind = msg.get("kind", "run")
+            if kind == "stop":
+                break
+            if kind == "barrier":
+                if self.ex.device.type == "cuda":
+                    torch.cuda.synchronize()
+                self._pub_q.join()
+                dist.barrier(group=self.group)
+                self.barrier_times.append(time.perf_counter())
+                continue
+            plan = StepPlan.from_wire(msg)
+            if not plan.seq_ids:
+                self.ex.execute(plan, None)  # frees only
+                continue
+            buf = self.ex.input_buffer(plan)
+            x = self.tr.recv(buf, self.rank - 1)
+            out = self.ex.execute(plan, x)
+            if self.is_last:
+                pinned, ev = _sample_tokens_to_host(out)
+                self._pub_q.put((plan.step, plan.mb, pinned, ev))
+            else:
+                self.tr.send(out, self.rank + 1)
+        if self.is_last:
+            self._pub_q.join()
+            self._pub_q.put(None)
+            self._pub_thread.join()
+        if self.ex.device.type == "cuda":
+            torch.cuda.synchronize()
+
+
+def make_transport(rank: int, world: int, device: torch.device) -> Transport:
+    if world == 1:
+        return LoopbackTransport(1)
+    if device.type == "cuda":
+        store = dist.distributed_c10d._get_default_store()
+        return RcclTransport(store, rank, world, device)
+    return TorchDistTransport()

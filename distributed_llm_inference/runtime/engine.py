@@ -1,0 +1,161 @@
+"""Engine construction: stages -> executors -> pipeline driver.
+
+* :func:`build_executor` — one stage on one device: weights (random-init or checkpoint, optional
+  fp8), KV pool sized from free HBM (288 GB per MI355X), executor with graph buckets.  In a
+  multi-process pipeline every rank agrees on the MIN block count (all-reduce over the gloo
+  control group) so the driver's admission control is valid on every stage.
+* :class:`LLMEngine` — in-process engine (PP=1, or PP>1 stages in one process).
+* :func:`init_pipeline_rank` — per-rank bootstrap of the multi-process pipeline launched by
+  ``distribute`` / torchrun: rank 0 gets a :class:`DistributedDriver`, other ranks a
+  :class:`StageFollower` whose ``run()`` serves until the driver stops it.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import uuid
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..config import CacheConfig, ModelSpec, ServeConfig, plan_stages, resolve_model
+from ..models.llama.cache import KVPool
+from ..parallel.pipeline import (DistributedDriver, LocalPipeline, StageFollower, _Channels,
+                                 make_transport)
+from ..utils.model import build_stage
+from .executor import StageExecutor
+from .scheduler import Scheduler
+from .sequence import SamplingParams, Sequence as Seq
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama-3-8b"
+    checkpoint: Optional[str] = None
+    random_init: bool = True
+    seed: int = 0
+    dtype: str = "bf16"
+    quantize: bool = False          # fp8 weights
+    pp: int = 1
+    cache: CacheConfig = field(default_factory=CacheConfig)
+    serve: ServeConfig = field(default_factory=ServeConfig)
+
+
+def _activation_reserve(spec: ModelSpec, serve: ServeConfig) -> int:
+    T = serve.max_num_batched_tokens
+    per_tok = 2 * (spec.qkv_size + 3 * spec.intermediate_size + 4 * spec.hidden_size)
+    logits = serve.max_batch_size * spec.vocab_size * 4
+    return int(T * per_tok * 2 + logits + (2 << 30))
+
+
+def build_executor(spec: ModelSpec, start: int, end: int, device: torch.device, cfg: EngineConfig,
+                   group=None, num_blocks: Optional[int] = None,
+                   kv_share: float = 1.0) -> StageExecutor:
+    stage = build_stage(cfg.checkpoint or spec, start, end, device=device,
+                        random_init=cfg.random_init and cfg.checkpoint is None, seed=cfg.seed,
+                        quantize=cfg.quantize, checkpoint=cfg.checkpoint)
+    cc, sc = cfg.cache, cfg.serve
+    nlayers = end - start
+    if num_blocks is None:
+        num_blocks = cc.num_blocks
+    if num_blocks is None:
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+            free, _ = torch.cuda.mem_get_info(device)
+            num_blocks = KVPool.size_from_memory(spec, nlayers, cc.block_size, int(free * kv_share),
+                                                 cc.gpu_memory_utilization,
+                                                 _activation_reserve(spec, sc))
+        else:
+            num_blocks = 1024
+    if group is not None:
+        t = torch.tensor([num_blocks], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        num_blocks = int(t.item())
+    pool = stage.make_pool(num_blocks, cc.block_size, cc.window_length, cc.num_sink_tokens,
+                           cc.max_chunk)
+    log.info("stage [%d,%d) on %s: %d KV blocks x %d tokens", start, end, device, num_blocks,
+             cc.block_size)
+    return StageExecutor(stage, pool, max_num_seqs=sc.max_batch_size,
+                         max_num_batched_tokens=sc.max_num_batched_tokens,
+                         max_seq_len=sc.max_seq_len, use_graphs=sc.use_graphs,
+                         graph_batch_sizes=sc.graph_batch_sizes)
+
+
+def make_scheduler(spec: ModelSpec, ex: StageExecutor, cfg: EngineConfig, num_stages: int) -> Scheduler:
+    sc = cfg.serve
+    M = sc.num_micro_batches or (num_stages + 1 if num_stages > 1 else 1)
+    m = ex.pool.manager
+    return Scheduler(M, sc.max_batch_size, sc.max_num_batched_tokens, m.blocks_for, m.num_blocks,
+                     eos_token_id=spec.eos_token_id, max_seq_len=sc.max_seq_len)
+
+
+class LLMEngine:
+    """In-process engine: ``LLMEngine("llama-3-8b").generate([[1, 2, 3]], SamplingParams(...))``."""
+
+    def __init__(self, model="llama-3-8b", pp: int = 1, device=None, cfg: Optional[EngineConfig] = None,
+                 **kw):
+        cfg = cfg or EngineConfig(model=model if isinstance(model, str) else "custom", pp=pp, **kw)
+        self.cfg = cfg
+        spec = resolve_model(cfg.checkpoint or model)
+        self.spec = spec
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
+                else torch.device("cpu")
+        device = torch.device(device)
+        ranges = plan_stages(spec, cfg.pp)
+        self.executors: List[StageExecutor] = []
+        total_layers = spec.num_layers
+        for (s, e) in ranges:
+            share = (e - s) / total_layers
+            # later stages see less free memory: give each its layer share of what remains
+            remaining_layers = sum(b - a for a, b in ranges[len(self.executors):])
+            self.executors.append(build_executor(spec, s, e, device, cfg,
+                                                 kv_share=(e - s) / remaining_layers))
+        nb = min(ex.pool.num_blocks for ex in self.executors)
+        self.scheduler = make_scheduler(spec, self.executors[0], cfg, len(ranges))
+        self.scheduler.total_blocks = nb
+        self.pipeline = LocalPipeline(self.executors, self.scheduler)
+
+    def generate(self, prompts: Sequence[Sequence[int]],
+                 params: Optional[SamplingParams] = None) -> List[Seq]:
+        return self.pipeline.generate(prompts, params)
+
+
+# =============================================================================================
+def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
+    """Bootstrap this rank of a multi-process pipeline (env: RANK, WORLD_SIZE, LOCAL_RANK,
+    MASTER_ADDR, MASTER_PORT).  Returns ``("driver", DistributedDriver | LocalPipeline)`` on rank 0
+    and ``("follower", StageFollower)`` elsewhere."""
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    spec = resolve_model(cfg.checkpoint or cfg.model)
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world == 1:
+        eng = LLMEngine(cfg.model, pp=1, device=device, cfg=cfg)
+        return "driver", eng.pipeline
+    if not dist.is_initialized():
+        dist.init_process_group(backend)
+    group = dist.group.WORLD
+    store = dist.distributed_c10d._get_default_store()
+    if rank == 0:
+        store.set("dli_job", uuid.uuid4().hex[:12])
+    job = store.get("dli_job").decode()
+    ranges = plan_stages(spec, world)
+    start, end = ranges[rank]
+    ex = build_executor(spec, start, end, device, cfg, group=group)
+    channels = _Channels(job, rank, world)
+    transport = make_transport(rank, world, device)
+    dist.barrier(group=group)
+    if rank == 0:
+        sched = make_scheduler(spec, ex, cfg, world)
+        return "driver", DistributedDriver(ex, sched, transport, channels, world, group)
+    return "follower", StageFollower(ex, transport, channels, rank, world, group)

@@ -1,0 +1,385 @@
+"""Per-GPU stage executor.
+
+Owns one :class:`CausalLMStage` (layer range [+ embedding] [+ LM head]), its paged KV pool and the
+per-step host->device metadata path.  One ``execute(plan, inputs)`` call runs one micro-batch step:
+
+  1. free finished sequences / reserve KV blocks for the new tokens (native BlockManager);
+  2. write slot_mapping, positions, block tables, seq_lens, q_start (and sampling parameters on
+     the last stage) straight into a pinned staging buffer (C++, no Python loops) and issue one
+     small async H2D copy per section into persistent device buffers;
+  3. decode steps (every sequence feeds one token) replay a hipGraph captured per batch-size
+     bucket — the whole stage (all local layers [+ head + sampling]) is ONE graph launch, padded
+     rows carry seq_len 0 / slot -1 so one graph serves every batch up to its bucket; prefill /
+     mixed steps run eagerly on the same kernels (varlen, chunked).
+
+This replaces the reference's per-op graph capture of RoPE / RMSNorm pieces
+(modules.py:28-34, 130-144 via utils/cuda.py) with whole-step capture.
+"""
+from __future__ import annotations
+
+import bisect
+import logging
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .. import ops
+from ..models.common import AttnMetadata
+from ..models.llama.cache import KVPool
+from ..models.stage import CausalLMStage
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class StepPlan:
+    """One micro-batch step, identical on every stage (broadcast by the driver)."""
+
+    step: int
+    mb: int
+    seq_ids: List[int]
+    q_lens: List[int]
+    free_ids: List[int] = field(default_factory=list)
+    sample_rows: List[int] = field(default_factory=list)   # indices into seq_ids
+    temperature: List[float] = field(default_factory=list)  # one per sample row
+    top_k: List[int] = field(default_factory=list)
+    top_p: List[float] = field(default_factory=list)
+    seeds: List[int] = field(default_factory=list)
+    kind: str = "run"                                       # run | barrier | stop
+    tokens: Optional[List[int]] = None                      # stage-0 input (not broadcast)
+
+    @property
+    def is_decode(self) -> bool:
+        return bool(self.seq_ids) and all(q == 1 for q in self.q_lens)
+
+    @property
+    def num_tokens(self) -> int:
+        return int(sum(self.q_lens))
+
+    def to_wire(self) -> dict:
+        d = dict(step=self.step, mb=self.mb, seq_ids=self.seq_ids, q_lens=self.q_lens,
+                 free_ids=self.free_ids, sample_rows=self.sample_rows,
+                 temperature=self.temperature, top_k=self.top_k, top_p=self.top_p,
+                 seeds=self.seeds, kind=self.kind)
+        return d
+
+    @classmethod
+    def from_wire(cls, d: dict) -> "StepPlan":
+        return cls(**d)
+
+
+class _Staging:
+    """Pinned host staging + persistent device buffers with typed section views."""
+
+    def __init__(self, max_tokens: int, max_seqs: int, max_blocks: int, device: torch.device):
+        self.max_tokens, self.max_seqs, self.max_blocks = max_tokens, max_seqs, max_blocks
+        specs = [("slot_mapping", torch.int64, (max_tokens,)),
+                 ("seeds", torch.int64, (max_seqs,)),
+                 ("logits_rows", torch.int64, (max_seqs,)),
+                 ("step", torch.int64, (1,)),
+                 ("positions", torch.int32, (max_tokens,)),
+                 ("tokens", torch.int32, (max_tokens,)),
+                 ("block_tables", torch.int32, (max_seqs, max_blocks)),
+                 ("seq_lens", torch.int32, (max_seqs,)),
+                 ("q_start", torch.int32, (max_seqs + 1,)),
+                 ("top_k", torch.int32, (max_seqs,)),
+                 ("temperature", torch.float32, (max_seqs,)),
+                 ("top_p", torch.float32, (max_seqs,))]
+        self.offsets: Dict[str, Tuple[int, torch.dtype, tuple]] = {}
+        off = 0
+        for name, dt, shape in specs:
+            n = 1
+            for s in shape:
+                n *= s
+            nbytes = n * torch.empty((), dtype=dt).element_size()
+            self.offsets[name] = (off, dt, shape)
+            off += (nbytes + 255) // 256 * 256
+        pin = device.type == "cuda"
+        self.host = torch.zeros(off, dtype=torch.uint8, pin_memory=pin)
+        self.dev = torch.zeros(off, dtype=torch.uint8, device=device)
+        self.h = {k: self._view(self.host, k) for k in self.offsets}
+        self.d = {k: self._view(self.dev, k) for k in self.offsets}
+        self.device = device
+
+    def _view(self, buf, name):
+        off, dt, shape = self.offsets[name]
+        n = 1
+        for s in shape:
+            n *= s
+        es = torch.empty((), dtype=dt).element_size()
+        return buf[off: off + n * es].view(dt).view(shape)
+
+    def upload(self, name: str, count: int) -> None:
+        """Copy the first ``count`` elements (rows for 2-D) of section ``name`` to the device."""
+        if count <= 0:
+            return
+        off, dt, shape = self.offsets[name]
+        row = 1
+        for s in shape[1:]:
+            row *= s
+        es = torch.empty((), dtype=dt).element_size()
+        nb = count * row * es
+        if self.device.type == "cuda":
+            self.dev[off: off + nb].copy_(self.host[off: off + nb], non_blocking=True)
+        else:
+            self.dev[off: off + nb].copy_(self.host[off: off + nb])
+
+
+class StageExecutor:
+    def __init__(self, stage: CausalLMStage, pool: KVPool, max_num_seqs: int = 256,
+                 max_num_batched_tokens: int = 8192, max_seq_len: int = 8192,
+                 use_graphs: bool = True, graph_batch_sizes: Optional[Sequence[int]] = None):
+        self.stage = stage
+        self.pool = pool
+        self.spec = stage.spec
+        self.device = stage.device
+        self.max_num_seqs = max_num_seqs
+        self.max_tokens = max(max_num_batched_tokens, max_num_seqs)
+        self.max_seq_len = max_seq_len
+        self.max_blocks = pool.manager.max_blocks_per_seq(max_seq_len)
+        self.staging = _Staging(self.max_tokens, max_num_seqs, self.max_blocks, self.device)
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        gbs = sorted(set(graph_batch_sizes or [1, 2, 4, 8, 16, 32, 48, 64, 96, 128, 160, 192, 224, 256]))
+        self.graph_sizes = [b for b in gbs if b <= max_num_seqs]
+        if self.use_graphs and (not self.graph_sizes or self.graph_sizes[-1] < max_num_seqs):
+            self.graph_sizes.append(max_num_seqs)
+        self._graphs: Dict[int, "_GraphEntry"] = {}
+        self._graph_pool = None
+        H = self.spec.hidden_size
+        self._hidden_in = torch.empty(max_num_seqs, H, dtype=torch.bfloat16, device=self.device) \
+            if not stage.has_embed else None
+        self._sample_out = torch.empty(max_num_seqs, dtype=torch.int32, device=self.device)
+        wp = pool.window_params()
+        self._wp = wp
+        self._step_counter = 0
+
+    # ------------------------------------------------------------------ capacity / bookkeeping
+    def apply_frees(self, ids: Sequence[int]) -> None:
+        for s in ids:
+            self.pool.manager.free_sequence(int(s))
+
+    def reserve(self, seq_ids: Sequence[int], q_lens: Sequence[int]) -> None:
+        m = self.pool.manager
+        if not m.can_append(list(seq_ids), list(q_lens)):
+            raise MemoryError(f"KV pool exhausted on stage [{self.stage.start},{self.stage.end}) "
+                              f"({m.num_free_blocks} free blocks)")
+        for s, q in zip(seq_ids, q_lens):
+            m.append(int(s), int(q))
+
+    # ------------------------------------------------------------------ metadata
+    def _stage_metadata(self, plan: StepPlan, rows: int) -> Tuple[int, int]:
+        """Fill the staging buffers for ``plan`` padded to ``rows`` sequences; returns (T, nb)."""
+        st = self.staging
+        h = st.h
+        B = len(plan.seq_ids)
+        if rows > self.max_num_seqs or plan.num_tokens > self.max_tokens:
+            raise ValueError("step exceeds executor limits (max_num_seqs / max_num_batched_tokens)")
+        nb = self.max_blocks
+        T = self.pool.manager.prepare(
+            plan.seq_ids, plan.q_lens, h["slot_mapping"].data_ptr(), h["positions"].data_ptr(),
+            h["block_tables"].data_ptr(), nb, h["seq_lens"].data_ptr(), h["q_start"].data_ptr(),
+            rows, [])
+        Tp = max(T, rows) if plan.is_decode else T
+        if Tp > T:  # padded decode rows: no cache write, position 0
+            h["slot_mapping"][T:Tp] = -1
+            h["positions"][T:Tp] = 0
+        st.upload("slot_mapping", Tp)
+        st.upload("positions", Tp)
+        st.upload("block_tables", rows)
+        st.upload("seq_lens", rows)
+        st.upload("q_start", rows + 1)
+        if plan.tokens is not None:
+            tok = h["tokens"]
+            tok[:T] = torch.as_tensor(plan.tokens, dtype=torch.int32)
+            if Tp > T:
+                tok[T:Tp] = 0
+            st.upload("tokens", Tp)
+        if self.stage.has_head:
+            ns = len(plan.sample_rows)
+            if plan.is_decode and ns == B:
+                # every row samples (graph path): parameters per row, padded greedy
+                h["temperature"][:B] = torch.as_tensor(plan.temperature, dtype=torch.float32)
+                h["top_k"][:B] = torch.as_tensor(plan.top_k, dtype=torch.int32)
+                h["top_p"][:B] = torch.as_tensor(plan.top_p, dtype=torch.float32)
+                h["seeds"][:B] = torch.as_tensor(plan.seeds, dtype=torch.int64)
+                if rows > B:
+                    h["temperature"][B:rows] = 0.0
+                    h["top_k"][B:rows] = 0
+                    h["top_p"][B:rows] = 1.0
+                    h["seeds"][B:rows] = 0
+                n = rows
+            else:
+                qs = h["q_start"]
+                h["logits_rows"][:ns] = torch.as_tensor([int(qs[r + 1]) - 1 for r in plan.sample_rows],
+                                                        dtype=torch.int64)
+                h["temperature"][:ns] = torch.as_tensor(plan.temperature, dtype=torch.float32)
+                h["top_k"][:ns] = torch.as_tensor(plan.top_k, dtype=torch.int32)
+                h["top_p"][:ns] = torch.as_tensor(plan.top_p, dtype=torch.float32)
+                h["seeds"][:ns] = torch.as_tensor(plan.seeds, dtype=torch.int64)
+                st.upload("logits_rows", ns)
+                n = ns
+            st.upload("temperature", n)
+            st.upload("top_k", n)
+            st.upload("top_p", n)
+            st.upload("seeds", n)
+            h["step"][0] = plan.step
+            st.upload("step", 1)
+        return T, nb
+
+    def _metadata(self, plan: StepPlan, rows: int, num_splits: int,
+                  decode: bool) -> AttnMetadata:
+        d = self.staging.d
+        T = rows if decode else plan.num_tokens
+        logits_rows = None
+        if self.stage.has_head and not (decode and len(plan.sample_rows) == len(plan.seq_ids)):
+            logits_rows = d["logits_rows"][: len(plan.sample_rows)]
+        return AttnMetadata(
+            num_tokens=T, num_seqs=rows, is_decode=decode, positions=d["positions"][:T],
+            slot_mapping=d["slot_mapping"][:T], block_tables=d["block_tables"][:rows],
+            seq_lens=d["seq_lens"][:rows], q_start=d["q_start"][: rows + 1],
+            max_q=max(plan.q_lens) if plan.q_lens else 0, num_splits=num_splits,
+            workspace=self._workspace(rows, num_splits) if decode else None,
+            logits_rows=logits_rows, **self._wp)
+
+    def _workspace(self, rows: int, splits: int):
+        if splits <= 1:
+            return None
+        key = (rows, splits)
+        ws = getattr(self, "_ws", {})
+        self._ws = ws
+        if key not in ws:
+            nh, D = self.spec.num_heads, self.spec.head_dim
+            ws[key] = (torch.empty(splits * rows * nh * D, dtype=torch.float32, device=self.device),
+                       torch.empty(splits * rows * nh * 2, dtype=torch.float32, device=self.device))
+        return ws[key]
+
+    def _splits(self, rows: int) -> int:
+        if self.device.type != "cuda":
+            return 1
+        return ops.decode_splits(rows, self.spec.num_kv_heads, self.spec.group_size,
+                                 self.max_seq_len)
+
+    # ------------------------------------------------------------------ forward
+    def _forward(self, meta: AttnMetadata, inputs: torch.Tensor, n_sample: int) -> torch.Tensor:
+        out = self.stage(inputs, meta, self.pool)
+        if not self.stage.has_head:
+            return out
+        d = self.staging.d
+        tokens = self._sample_out[:n_sample]
+        ops.sample(out, temperature=d["temperature"][:n_sample], top_k=d["top_k"][:n_sample],
+                   top_p=d["top_p"][:n_sample], seeds=d["seeds"][:n_sample], step=d["step"],
+                   out=tokens)
+        return tokens
+
+    def input_buffer(self, plan: StepPlan) -> Optional[torch.Tensor]:
+        """Where the previous stage's hidden states for ``plan`` should be received (non-first
+        stages): the graph's static input for decode steps, a fresh tensor otherwise."""
+        if self.stage.has_embed:
+            return None
+        if plan.is_decode and self._graph_rows(len(plan.seq_ids)) is not None:
+            return self._hidden_in[: len(plan.seq_ids)]
+        return torch.empty(plan.num_tokens, self.spec.hidden_size, dtype=torch.bfloat16,
+                           device=self.device)
+
+    def _graph_rows(self, B: int) -> Optional[int]:
+        if not self.use_graphs or B > self.graph_sizes[-1]:
+            return None
+        return self.graph_sizes[bisect.bisect_left(self.graph_sizes, B)]
+
+    @torch.inference_mode()
+    def execute(self, plan: StepPlan, inputs: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Run one step.  ``inputs``: hidden states [T, H] for non-first stages (ignored on stage 0,
+        which embeds ``plan.tokens``).  Returns hidden [T, H] or sampled tokens [n_sample] int32
+        (device tensors; the caller decides when to synchronise)."""
+        self.apply_frees(plan.free_ids)
+        if not plan.seq_ids:
+            return torch.empty(0, device=self.device)
+        self.reserve(plan.seq_ids, plan.q_lens)
+        B = len(plan.seq_ids)
+        decode = plan.is_decode
+        grows = self._graph_rows(B) if decode else None
+        rows = grows if grows is not None else B
+        self._stage_metadata(plan, rows)
+        n_sample = len(plan.sample_rows)
+        all_sample = decode and n_sample == B
+        if grows is not None and (not self.stage.has_head or all_sample):
+            g = self._graphs.get(grows)
+            if g is None:
+                g = self._capture(grows)
+            if not self.stage.has_embed:
+                src = inputs[:B]
+                if src.data_ptr() != self._hidden_in.data_ptr():
+                    self._hidden_in[:B].copy_(src)
+            g.graph.replay()
+            return g.out[:n_sample] if self.stage.has_head else g.out[:B].clone()
+        splits = self._splits(rows) if decode else 1
+        meta = self._metadata(plan, rows, splits, decode)
+        if self.stage.has_embed:
+            x = self.staging.d["tokens"][: meta.num_tokens]
+        else:
+            x = inputs
+        out = self._forward(meta, x, n_sample if self.stage.has_head else 0)
+        return out
+
+    # ------------------------------------------------------------------ graphs
+    def _capture(self, rows: int) -> "_GraphEntry":
+        """Capture the decode step for ``rows`` sequences (buffers already staged by the caller)."""
+        splits = self._splits(rows)
+        plan_like = StepPlan(0, 0, list(range(rows)), [1] * rows,
+                             sample_rows=list(range(rows)))
+        meta = self._metadata(plan_like, rows, splits, True)
+        x = self.staging.d["tokens"][:rows] if self.stage.has_embed else self._hidden_in[:rows]
+        n_sample = rows if self.stage.has_head else 0
+        # warm up on a side stream (hipBLASLt heuristics, allocator) then capture
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._forward(meta, x, n_sample)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(graph, pool=self._graph_pool):
+            out = self._forward(meta, x, n_sample)
+        entry = _GraphEntry(graph, out)
+        self._graphs[rows] = entry
+        log.info("captured decode graph rows=%d splits=%d stage=[%d,%d)", rows, splits,
+                 self.stage.start, self.stage.end)
+        # the captured run did not execute; run the real step now
+        graph.replay()
+        return entry
+
+    def warmup_graphs(self, sizes: Optional[Sequence[int]] = None) -> None:
+        """Pre-capture decode graphs with dummy (empty, seq_len 0) batches."""
+        if not self.use_graphs:
+            return
+        for r in sizes or self.graph_sizes:
+            if r in self._graphs:
+                continue
+            h = self.staging.h
+            h["seq_lens"][:r] = 0
+            h["slot_mapping"][:r] = -1
+            h["positions"][:r] = 0
+            h["block_tables"][:r] = 0
+            h["q_start"][: r + 1] = 0
+            h["tokens"][:r] = 0
+            h["temperature"][:r] = 0
+            h["top_k"][:r] = 0
+            h["top_p"][:r] = 1
+            h["seeds"][:r] = 0
+            for k, n in (("seq_lens", r), ("slot_mapping", r), ("positions", r), ("block_tables", r),
+                         ("q_start", r + 1), ("tokens", r), ("temperature", r), ("top_k", r),
+                         ("top_p", r), ("seeds", r)):
+                self.staging.upload(k, n)
+            if self._hidden_in is not None:
+                self._hidden_in[:r].zero_()
+            self._capture(r)
+        torch.cuda.synchronize()
+
+
+@dataclass
+class _GraphEntry:
+    graph: "torch.cuda.CUDAGraph"
+    out: torch.Tensor

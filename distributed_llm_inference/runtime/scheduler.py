@@ -1,0 +1,168 @@
+"""Continuous-batching scheduler for a pipeline of stages (runs on the driver, stage 0).
+
+The reference batches independent requests with hivemind's TaskPool (server/backend.py:42;
+SURVEY §3.4) and keys sessions by generation_id.  Here the driver keeps M micro-batches in flight
+through the N-stage pipeline (M >= N keeps every stage busy; a micro-batch's next step can only be
+planned once its sampled tokens came back from the last stage — the loop-carried dependency of
+SURVEY §7.4 item 2).  Per micro-batch step it packs:
+  * one decode token for every running sequence of the micro-batch,
+  * prefill chunks of newly admitted sequences (chunked to ``max_num_batched_tokens``),
+and frees the KV blocks of sequences that finished in the previous step.
+
+Admission reserves the worst case (prompt + max_tokens) in KV blocks, so a running sequence can
+never run out of cache mid-generation (no preemption needed).  Every stage runs the identical
+block-manager call sequence, so stage-local block tables agree without being communicated.
+"""
+from __future__ import annotations
+
+import collections
+from typing import Callable, Deque, Dict, List, Optional
+
+from .executor import StepPlan
+from .sequence import Sequence, SeqStatus
+
+
+class Scheduler:
+    def __init__(self, num_micro_batches: int, max_seqs_per_mb: int, max_tokens_per_step: int,
+                 blocks_for: Callable[[int], int], total_blocks: int,
+                 eos_token_id: Optional[int] = None, max_seq_len: int = 8192):
+        self.M = max(1, num_micro_batches)
+        self.max_seqs = max_seqs_per_mb
+        self.max_tokens = max_tokens_per_step
+        self.blocks_for = blocks_for
+        self.total_blocks = total_blocks
+        self.eos = eos_token_id
+        self.max_seq_len = max_seq_len
+        self.waiting: Deque[Sequence] = collections.deque()
+        self.mbs: List[List[Sequence]] = [[] for _ in range(self.M)]
+        self.pending_free: List[List[int]] = [[] for _ in range(self.M)]
+        self.inflight: List[Optional[StepPlan]] = [None] * self.M
+        self.reserved_blocks = 0
+        self._reserve: Dict[int, int] = {}
+        self.step = 0
+        self.finished: List[Sequence] = []
+
+    # ------------------------------------------------------------------ requests
+    def add(self, seq: Sequence) -> None:
+        total = len(seq.prompt) + seq.params.max_tokens
+        if total > self.max_seq_len:
+            raise ValueError(f"prompt + max_tokens = {total} exceeds max_seq_len {self.max_seq_len}")
+        if self.blocks_for(total) > self.total_blocks:
+            raise ValueError("request can never fit in the KV cache")
+        self.waiting.append(seq)
+
+    def abort(self, seq_id: int) -> None:
+        for q in [self.waiting] + self.mbs:
+            for s in list(q):
+                if s.seq_id == seq_id:
+                    s.status = SeqStatus.ABORTED
+                    s.finish_reason = "abort"
+
+    def has_work(self) -> bool:
+        return bool(self.waiting) or any(self.mbs) or any(p is not None for p in self.inflight)
+
+    def num_running(self) -> int:
+        return sum(len(m) for m in self.mbs)
+
+    # ------------------------------------------------------------------ planning
+    def _admit(self, mb: int, budget: int) -> List[Sequence]:
+        admitted = []
+        m = self.mbs[mb]
+        # balance: fill this micro-batch up to its fair share of (running + waiting)
+        share = -(-(self.num_running() + len(self.waiting)) // self.M)
+        target = min(self.max_seqs, max(1, share))
+        while self.waiting and len(m) < target and budget > 0:
+            s = self.waiting[0]
+            if s.status == SeqStatus.ABORTED:
+                self.waiting.popleft()
+                self.finished.append(s)
+                continue
+            need = self.blocks_for(len(s.prompt) + s.params.max_tokens)
+            if self.reserved_blocks + need > self.total_blocks:
+                break
+            self.waiting.popleft()
+            self.reserved_blocks += need
+            self._reserve[s.seq_id] = need
+            s.status = SeqStatus.RUNNING
+            s.micro_batch = mb
+            m.append(s)
+            admitted.append(s)
+            budget -= min(len(s.prompt), budget)
+        return admitted
+
+    def plan(self, mb: int) -> Optional[StepPlan]:
+        """Next step for micro-batch ``mb`` (None if it has nothing to do)."""
+        assert self.inflight[mb] is None, "micro-batch still in flight"
+        m = self.mbs[mb]
+        # drop aborted sequences
+        for s in [s for s in m if s.status == SeqStatus.ABORTED]:
+            self._retire(mb, s)
+        decode = [s for s in m if s.num_computed >= len(s.prompt)]
+        budget = self.max_tokens - len(decode)
+        self._admit(mb, budget)
+        seq_ids, q_lens, tokens, sample_rows = [], [], [], []
+        temps, topk, topp, seeds = [], [], [], []
+        for s in m:
+            pend = s.pending_tokens()
+            if s.num_computed >= len(s.prompt):
+                take = 1  # decode: the last sampled token
+                pend = pend[-1:]
+            else:
+                take = min(len(pend), budget)
+                if take <= 0:
+                    continue
+                budget -= take
+                pend = pend[:take]
+            row = len(seq_ids)
+            seq_ids.append(s.seq_id)
+            q_lens.append(take)
+            tokens.extend(pend)
+            if s.num_computed + take >= s.total_len:  # reaches the end of known tokens: sample
+                sample_rows.append(row)
+                temps.append(float(s.params.temperature))
+                topk.append(int(s.params.top_k))
+                topp.append(float(s.params.top_p))
+                seeds.append(int(s.seed))
+        free_ids = self.pending_free[mb]
+        self.pending_free[mb] = []
+        if not seq_ids and not free_ids:
+            return None
+        plan = StepPlan(step=self.step, mb=mb, seq_ids=seq_ids, q_lens=q_lens, free_ids=free_ids,
+                        sample_rows=sample_rows, temperature=temps, top_k=topk, top_p=topp,
+                        seeds=seeds, tokens=tokens)
+        self.step += 1
+        # the tokens are (about to be) in the cache on every stage
+        byid = {s.seq_id: s for s in m}
+        for sid, q in zip(seq_ids, q_lens):
+            byid[sid].num_computed += q
+        self.inflight[mb] = plan if seq_ids else None
+        return plan
+
+    # ------------------------------------------------------------------ results
+    def _retire(self, mb: int, s: Sequence) -> None:
+        self.mbs[mb].remove(s)
+        self.pending_free[mb].append(s.seq_id)
+        self.reserved_blocks -= self._reserve.pop(s.seq_id, 0)
+        self.finished.append(s)
+
+    def on_tokens(self, mb: int, tokens: List[int], now: Optional[float] = None) -> List[Sequence]:
+        """Sampled tokens for the in-flight step of ``mb`` (one per sample row, in order)."""
+        plan = self.inflight[mb]
+        self.inflight[mb] = None
+        if plan is None:
+            return []
+        byid = {s.seq_id: s for s in self.mbs[mb]}
+        done = []
+        for row, tok in zip(plan.sample_rows, tokens):
+            s = byid.get(plan.seq_ids[row])
+            if s is None or s.is_finished():
+                continue
+            if s.append_token(int(tok), self.eos, now):
+                done.append(s)
+        for s in done:
+            self._retire(mb, s)
+        return done
+
+    def pop_finished(self) -> List[Sequence]:
+        out, self.finished = self.finished, []
+        return out
