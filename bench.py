@@ -35,7 +35,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="llama-3-70b")
-    ap.add_argument("--batch-per-mb", type=int, default=128)
+    ap.add_argument("--batch-per-mb", type=int, default=256)
     ap.add_argument("--micro-batches", type=int, default=0, help="0 = N+1 (N=1: 2)")
     ap.add_argument("--prompt-len", type=int, default=512)
     ap.add_argument("--max-batched-tokens", type=int, default=16384)

@@ -60,6 +60,12 @@ def build_executor(spec: ModelSpec, start: int, end: int, device: torch.device, 
                         quantize=cfg.quantize, checkpoint=cfg.checkpoint)
     cc, sc = cfg.cache, cfg.serve
     nlayers = end - start
+    if device.type == "cuda" and sc.use_graphs:
+        from .gemm_tuning import tune_decode_gemms
+        buckets = [b for b in sc.graph_batch_sizes if 16 <= b <= sc.max_batch_size]
+        tdir = os.environ.get("DLI_TUNING_DIR", os.path.join(os.path.dirname(os.path.dirname(
+            os.path.dirname(os.path.abspath(__file__)))), "build", "tuning"))
+        tune_decode_gemms(stage, buckets, os.path.join(tdir, "tunableop_results.csv"))
     if num_blocks is None:
         num_blocks = cc.num_blocks
     if num_blocks is None:

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 kernel trace for the decode phase of bench.py.
+
+Decode steps are delimited by the sampling kernel (one per micro-batch step); the last
+``--steps`` decode steps are aggregated per kernel (short names), with per-step time, share,
+achieved bandwidth for GEMMs (given the shape table) and the gaps between kernels.
+"""
+import argparse
+import collections
+import csv
+import re
+
+
+def short(name: str) -> str:
+    if name.startswith("Cijk") or name.startswith("Custom_Cijk"):
+        m = re.search(r"MT(\d+x\d+x\d+)", name)
+        return f"hipBLASLt_GEMM[{m.group(1) if m else '?'}]" + ("_SK" if "_SK" in name else "")
+    name = re.sub(r"\(.*", "", name)
+    name = name.replace("void ", "")
+    return name[:90]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--steps", type=int, default=4, help="decode micro-batch steps to aggregate")
+    ap.add_argument("--marker", default="sample_kernel")
+    a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
+    if len(marks) < a.steps + 1:
+        raise SystemExit(f"only {len(marks)} marker kernels")
+    lo, hi = marks[-a.steps - 1] + 1, marks[-1] + 1
+    seg = rows[lo:hi]
+    t0 = int(seg[0]["Start_Timestamp"])
+    t1 = int(seg[-1]["End_Timestamp"])
+    busy = collections.Counter()
+    calls = collections.Counter()
+    for r in seg:
+        k = short(r["Kernel_Name"])
+        busy[k] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        calls[k] += 1
+    total_busy = sum(busy.values())
+    wall = t1 - t0
+    print(f"decode window: {a.steps} micro-batch steps, wall {wall/1e6:.3f} ms "
+          f"({wall/1e6/a.steps:.3f} ms/step), kernel busy {total_busy/1e6:.3f} ms "
+          f"({100*total_busy/wall:.1f}% of wall), kernels {len(seg)}")
+    print(f"{'kernel':<60} {'calls/step':>10} {'us/step':>10} {'share':>7}")
+    for k, v in busy.most_common():
+        print(f"{k:<60} {calls[k]/a.steps:>10.1f} {v/1e3/a.steps:>10.1f} {100*v/total_busy:>6.1f}%")
+
+
+if __name__ == "__main__":
+    main()

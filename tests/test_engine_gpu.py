@@ -76,12 +76,33 @@ def test_pipeline_loopback_equals_single_stage(gpu, pp, mbs):
     assert a == b
 
 
+def _forced_logits(stage, prompts, forced, window=0, sinks=0):
+    pool = stage.make_pool(128, 64, window_length=window, num_sink_tokens=sinks, max_chunk=256)
+    sids = list(range(len(prompts)))
+    for s, p in zip(sids, prompts):
+        pool.manager.append(s, len(p))
+    meta = pool.build_metadata(sids, [len(p) for p in prompts])
+    meta.logits_rows = (torch.cumsum(torch.tensor([len(p) for p in prompts]), 0) - 1).to(stage.device)
+    ids = torch.tensor([t for p in prompts for t in p], dtype=torch.int32, device=stage.device)
+    outs = [stage(ids, meta, pool).float().cpu()]
+    for step in forced:
+        for s in sids:
+            pool.manager.append(s, 1)
+        meta = pool.build_metadata(sids, [1] * len(sids))
+        outs.append(stage(torch.tensor(step, dtype=torch.int32, device=stage.device), meta,
+                          pool).float().cpu())
+    return outs
+
+
 def test_window_mode_runs_and_matches_full_cache_before_eviction(gpu):
-    # while the sequence is shorter than the window the sink cache equals a full cache
-    p = SamplingParams(max_tokens=6, ignore_eos=True)
-    a = [s.output for s in _engine().generate(PROMPTS[:2], p)]
-    b = [s.output for s in _engine(window=512, sinks=4).generate(PROMPTS[:2], p)]
-    assert a == b
+    # while the sequences are shorter than the window the sink cache equals a full cache
+    stage = CausalLMStage(SPEC, 0, 4, device=gpu).init_random(3)
+    prompts = PROMPTS[:2]
+    forced = [[17, 23], [5, 900], [44, 1], [2, 3]]
+    a = _forced_logits(stage, prompts, forced)
+    b = _forced_logits(stage, prompts, forced, window=512, sinks=4)
+    for x, y in zip(a, b):
+        assert (x - y).abs().max() < 0.03 * max(1.0, x.abs().max().item())
     # and it keeps generating past the window (ring eviction) without error
     long = [list(range(1, 600))]
     out = _engine(window=256, sinks=4).generate(long, SamplingParams(max_tokens=20, ignore_eos=True))
@@ -104,3 +125,17 @@ def test_sampling_params_in_engine(gpu):
     b = [s.output for s in _engine().generate(PROMPTS, p)]
     assert a == b  # seeded sampling is reproducible
     assert all(len(x) == 10 for x in a)
+
+
+def test_sink_window_matches_streamingllm_definition_gpu(gpu):
+    """GPU version of the CPU test: 1-layer model, long decode through the ring with sinks equals
+    a fresh full-cache forward of [sinks] + [last W - n_sink tokens] at positions 0..W-1."""
+    spec = SPEC.replace(num_layers=1)
+    stage = CausalLMStage(spec, 0, 1, device=gpu).init_random(11)
+    W, S = 96, 4
+    g = torch.Generator().manual_seed(0)
+    toks = torch.randint(0, spec.vocab_size, (300,), generator=g).tolist()
+    outs = _forced_logits(stage, [toks[:16]], [[t] for t in toks[16:]], window=W, sinks=S)
+    view = toks[:S] + toks[len(toks) - (W - S):]
+    ref = _forced_logits(stage, [view], [])[0]
+    assert (outs[-1] - ref).abs().max() < 0.03 * max(1.0, ref.abs().max().item())
