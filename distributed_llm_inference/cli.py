@@ -1,0 +1,194 @@
+"""``distribute`` — command-line entry point (the reference's ``distribute`` file is empty).
+
+    distribute plan     --model llama-3-70b --gpus 8
+    distribute generate --model llama-3-8b --gpus 2 --prompt-ids 1,2,3 --max-tokens 32
+    distribute serve    --model llama-3-70b --gpus 8 --port 8000 [--tokenizer DIR]
+    distribute bench    --gpus 8 --steps 20 --warmup 5          (runs bench.py under the launcher)
+
+One process per GPU (``launcher.launch``); each process owns one pipeline stage (``plan_stages``).
+Rank 0 is the driver (scheduler + stage 0) and hosts the action (generate / serve); the other
+ranks run the stage follower loop until the driver stops them.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+from typing import List, Optional
+
+log = logging.getLogger("distribute")
+
+
+def _common(ap: argparse.ArgumentParser) -> None:
+    ap.add_argument("--model", default="llama-3-8b", help="preset name or HF config/checkpoint dir")
+    ap.add_argument("--checkpoint", default=None, help="HF safetensors dir (default: random init)")
+    ap.add_argument("--gpus", type=int, default=1, help="pipeline stages = processes = GPUs")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--fp8", action="store_true", help="fp8-e4m3 weights")
+    ap.add_argument("--window", type=int, default=0, help="attention-sink window length (0=full)")
+    ap.add_argument("--sinks", type=int, default=0, help="attention-sink tokens")
+    ap.add_argument("--block-size", type=int, default=64)
+    ap.add_argument("--gpu-mem", type=float, default=0.90)
+    ap.add_argument("--max-batch", type=int, default=256)
+    ap.add_argument("--max-batched-tokens", type=int, default=8192)
+    ap.add_argument("--max-seq-len", type=int, default=8192)
+    ap.add_argument("--micro-batches", type=int, default=0)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--tokenizer", default=None, help="HF tokenizer dir (local files only)")
+    ap.add_argument("-v", "--verbose", action="store_true")
+
+
+def engine_config(a):
+    from .config import CacheConfig, ServeConfig
+    from .runtime.engine import EngineConfig
+    return EngineConfig(
+        model=a.model, checkpoint=a.checkpoint, random_init=a.checkpoint is None, seed=a.seed,
+        quantize=a.fp8, pp=a.gpus,
+        cache=CacheConfig(block_size=a.block_size, gpu_memory_utilization=a.gpu_mem,
+                          window_length=a.window, num_sink_tokens=a.sinks),
+        serve=ServeConfig(max_batch_size=a.max_batch, max_num_batched_tokens=a.max_batched_tokens,
+                          num_micro_batches=a.micro_batches, max_seq_len=a.max_seq_len,
+                          use_graphs=not a.no_graphs))
+
+
+def load_tokenizer(path: Optional[str]):
+    if not path:
+        return None
+    from transformers import AutoTokenizer
+    return AutoTokenizer.from_pretrained(path, local_files_only=True)
+
+
+# ------------------------------------------------------------------------------ actions
+def cmd_plan(a) -> int:
+    from .config import plan_stages, resolve_model
+    from .models.llama.cache import KVPool
+    spec = resolve_model(a.checkpoint or a.model)
+    ranges = plan_stages(spec, a.gpus)
+    per_layer = spec.layer_param_count() * (1 if a.fp8 else 2)
+    emb = spec.vocab_size * spec.hidden_size * 2
+    out = []
+    for i, (s, e) in enumerate(ranges):
+        w = (e - s) * per_layer + (emb if i == 0 else 0) + (emb if i == len(ranges) - 1 else 0)
+        free = 288e9 * a.gpu_mem - w
+        kv_tok = KVPool.bytes_per_block(spec, e - s, 1)
+        out.append(dict(stage=i, gpu=i, layers=[s, e], weights_gb=round(w / 1e9, 2),
+                        kv_capacity_tokens=int(max(0, free) // kv_tok)))
+    print(json.dumps({"model": spec.name, "num_layers": spec.num_layers, "stages": out}, indent=1))
+    return 0
+
+
+def _spawn_self(a, action: str, argv: List[str]) -> int:
+    from .launcher import launch
+    return launch(a.gpus, ["-m", "distributed_llm_inference.cli", "worker", "--action", action] + argv)
+
+
+def cmd_worker(a) -> int:
+    """Per-rank entry (started by the launcher)."""
+    import torch.distributed as dist
+    from .runtime.engine import init_pipeline_rank
+    from .runtime.sequence import SamplingParams
+    logging.basicConfig(level=logging.INFO if a.verbose else logging.WARNING,
+                        format=f"[rank {os.environ.get('RANK', '0')}] %(levelname)s %(name)s: %(message)s")
+    cfg = engine_config(a)
+    role, obj = init_pipeline_rank(cfg)
+    if role == "follower":
+        obj.run()
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return 0
+    drv = obj
+    tok = load_tokenizer(a.tokenizer)
+    try:
+        if a.action == "generate":
+            prompts = []
+            if a.prompt_ids:
+                prompts = [[int(x) for x in p.split(",") if x] for p in a.prompt_ids]
+            for p in a.prompt or []:
+                if tok is None:
+                    raise SystemExit("--prompt needs --tokenizer (or use --prompt-ids)")
+                prompts.append(tok.encode(p))
+            if not prompts:
+                raise SystemExit("no prompts (use --prompt-ids 1,2,3 or --prompt TEXT)")
+            params = SamplingParams(max_tokens=a.max_tokens, temperature=a.temperature,
+                                    top_k=a.top_k, top_p=a.top_p, seed=a.sample_seed,
+                                    ignore_eos=a.ignore_eos)
+            outs = drv.generate(prompts, params)
+            for s in outs:
+                rec = {"prompt_ids": s.prompt, "output_ids": s.output,
+                       "finish_reason": s.finish_reason}
+                if tok is not None:
+                    rec["text"] = tok.decode(s.output, skip_special_tokens=True)
+                print(json.dumps(rec), flush=True)
+        elif a.action == "serve":
+            from .server.http import serve
+            from .server.service import EngineService
+            svc = EngineService(drv, eos_token_id=getattr(drv.sched, "eos", None))
+            try:
+                serve(svc, a.host, a.port, tok, a.model)
+            finally:
+                svc.shutdown(stop_driver=False)
+        else:
+            raise SystemExit(f"unknown action {a.action}")
+    finally:
+        drv.stop()
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    return 0
+
+
+def _gen_args(ap):
+    ap.add_argument("--prompt", action="append", help="text prompt (repeatable; needs --tokenizer)")
+    ap.add_argument("--prompt-ids", action="append", help="comma-separated token ids (repeatable)")
+    ap.add_argument("--max-tokens", type=int, default=32)
+    ap.add_argument("--temperature", type=float, default=0.0)
+    ap.add_argument("--top-k", type=int, default=0)
+    ap.add_argument("--top-p", type=float, default=1.0)
+    ap.add_argument("--sample-seed", type=int, default=None)
+    ap.add_argument("--ignore-eos", action="store_true")
+
+
+def _serve_args(ap):
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=8000)
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    ap = argparse.ArgumentParser(prog="distribute", description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    p = sub.add_parser("plan", help="print the stage placement and memory plan")
+    _common(p)
+    g = sub.add_parser("generate", help="offline generation")
+    _common(g)
+    _gen_args(g)
+    s = sub.add_parser("serve", help="HTTP server (rank 0) over the pipeline")
+    _common(s)
+    _serve_args(s)
+    b = sub.add_parser("bench", help="headline benchmark (bench.py) on N GPUs")
+    b.add_argument("--gpus", type=int, default=1)
+    b.add_argument("rest", nargs=argparse.REMAINDER)
+    w = sub.add_parser("worker", help=argparse.SUPPRESS)
+    _common(w)
+    _gen_args(w)
+    _serve_args(w)
+    w.add_argument("--action", required=True)
+    a = ap.parse_args(argv)
+    if a.cmd == "plan":
+        return cmd_plan(a)
+    if a.cmd == "worker":
+        return cmd_worker(a)
+    if a.cmd == "bench":
+        from .launcher import launch
+        bench = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+        rest = [x for x in a.rest if x != "--"]
+        return launch(a.gpus, [bench, "--gpus", str(a.gpus)] + rest)
+    # generate / serve: re-run this CLI as `worker` in N processes
+    idx = argv.index(a.cmd)
+    return _spawn_self(a, a.cmd, argv[:idx] + argv[idx + 1:])
+
+
+if __name__ == "__main__":
+    sys.exit(main())

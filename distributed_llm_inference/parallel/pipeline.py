@@ -35,6 +35,7 @@ import torch
 import torch.distributed as dist
 
 from ..runtime.executor import StageExecutor, StepPlan
+from ..runtime.faults import FaultInjector, StageStats
 from ..runtime.scheduler import Scheduler
 from ..runtime.sequence import SamplingParams, Sequence as Seq
 from .transport import LoopbackTransport, RcclTransport, TorchDistTransport, Transport
@@ -203,10 +204,16 @@ class DistributedDriver(DriverBase):
         self.world = world
         self.group = ctrl_group
         self.timeout = timeout
+        self.faults = FaultInjector(0)
+        self.stats = StageStats(0, executor.device)
 
     def _issue(self, plan: StepPlan) -> None:
         self.ch.ctrl.send(msgpack.packb(plan.to_wire()), self.timeout)
+        if plan.seq_ids and self.faults.active:
+            self.faults.on_step()
+        tok = self.stats.begin(self.faults.delay_ms) if plan.seq_ids else None
         out = self.ex.execute(plan, None)
+        self.stats.end(tok)
         if plan.seq_ids:
             self.tr.send(out, 1)
 
@@ -235,6 +242,8 @@ class StageFollower:
         self.timeout = timeout
         self.is_last = rank == world - 1
         self.barrier_times: List[float] = []
+        self.faults = FaultInjector(rank)
+        self.stats = StageStats(rank, executor.device)
         self._pub_q: "queue.Queue" = queue.Queue()
         self._pub_thread = None
         if self.is_last:
@@ -273,7 +282,11 @@ class StageFollower:
                 continue
             buf = self.ex.input_buffer(plan)
             x = self.tr.recv(buf, self.rank - 1)
+            if self.faults.active:
+                self.faults.on_step()
+            tok = self.stats.begin(self.faults.delay_ms)
             out = self.ex.execute(plan, x)
+            self.stats.end(tok)
             if self.is_last:
                 pinned, ev = _sample_tokens_to_host(out)
                 self._pub_q.put((plan.step, plan.mb, pinned, ev))

@@ -156,6 +156,11 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         store.set("dli_job", uuid.uuid4().hex[:12])
     job = store.get("dli_job").decode()
     ranges = plan_stages(spec, world)
+    if os.environ.get("DLI_STAGE_RANGES"):  # placement chosen by the server (rebalance)
+        import json
+        ranges = [tuple(r) for r in json.loads(os.environ["DLI_STAGE_RANGES"])]
+        if len(ranges) != world:
+            raise ValueError("DLI_STAGE_RANGES must have one range per rank")
     start, end = ranges[rank]
     ex = build_executor(spec, start, end, device, cfg, group=group)
     channels = _Channels(job, rank, world)

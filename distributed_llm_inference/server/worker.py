@@ -1,0 +1,88 @@
+"""Worker holding a contiguous block range.
+
+Reference: ``Block`` TypedDict and ``InferenceWorker(model, block_index_start, block_index_end,
+block_)`` (/root/reference/distributed_llm_inference/server/worker.py:4-23), a stub meant to build
+``Dict[block_id, TransformerBackend]`` via ``load_block()``.  Implemented: the worker loads (or
+random-initialises) the layers ``[start, end)`` on its device, groups them into blocks of
+``layers_per_block`` layers (default: the whole range — one MI355X-sized block), wraps each in an
+:class:`InferenceBackend` with its own session cache and batching pool, and routes
+``forward(block_id, generation_id, hidden)`` / ``forward_range(generation_id, hidden)`` calls.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Dict, List, Optional, TypedDict
+
+import torch
+
+from ..config import resolve_model
+from ..models.llama.cache import PartialLlamaSinkCache
+from ..utils.model import convert_to_optimized_block, load_block
+from .backend import BatchTensorDescriptor, InferenceBackend
+
+log = logging.getLogger(__name__)
+
+
+class Block(TypedDict):
+    block_index: int
+    block_id: str
+
+
+class InferenceWorker:
+    def __init__(self, model: str, block_index_start: int, block_index_end: int,
+                 layers_per_block: Optional[int] = None, device=None, random_init: bool = True,
+                 checkpoint: Optional[str] = None, quantize: bool = False,
+                 max_batch_size: int = 64, window_length: int = 0, num_sink_tokens: int = 0,
+                 num_blocks: int = 512):
+        self.model = model
+        self.spec = resolve_model(checkpoint or model)
+        if not (0 <= block_index_start < block_index_end <= self.spec.num_layers):
+            raise ValueError("bad block range")
+        self.start, self.end = block_index_start, block_index_end
+        n = layers_per_block or (block_index_end - block_index_start)
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
+            else torch.device("cpu"))
+        self.block_ids: List[Block] = []
+        self.blocks: Dict[str, InferenceBackend] = {}
+        for s in range(block_index_start, block_index_end, n):
+            e = min(block_index_end, s + n)
+            bid = f"{self.spec.name}.{s}-{e}"
+            blk = load_block(checkpoint or model, list(range(s, e)), use_quantized=False,
+                             device=self.device, random_init=checkpoint is None and random_init)
+            if quantize:
+                blk = convert_to_optimized_block(blk, quantize=True, device=self.device)
+            cache = PartialLlamaSinkCache(window_length, num_sink_tokens, num_blocks=num_blocks)
+            be = InferenceBackend(bid, blk,
+                                  args_schema=(BatchTensorDescriptor((1, self.spec.hidden_size)),),
+                                  max_batch_size=max_batch_size, cache=cache)
+            self.blocks[bid] = be
+            self.block_ids.append(Block(block_index=s, block_id=bid))
+        self._running = False
+
+    def run(self) -> None:
+        for be in self.blocks.values():
+            be.inference_pool.start()
+        self._running = True
+
+    def shutdown(self) -> None:
+        for be in self.blocks.values():
+            be.shutdown()
+        self._running = False
+
+    def is_healthy(self) -> bool:
+        return self._running and all(be.inference_pool.is_alive for be in self.blocks.values())
+
+    def forward(self, block_id: str, generation_id: str, hidden: torch.Tensor) -> torch.Tensor:
+        (out,) = self.blocks[block_id].submit(hidden, generation_id=generation_id).result()
+        return out
+
+    def forward_range(self, generation_id: str, hidden: torch.Tensor) -> torch.Tensor:
+        """Run every block of this worker in order (the whole stage)."""
+        for b in self.block_ids:
+            hidden = self.forward(b["block_id"], generation_id, hidden)
+        return hidden
+
+    def close_session(self, generation_id: str) -> None:
+        for be in self.blocks.values():
+            be.close_session(generation_id)
