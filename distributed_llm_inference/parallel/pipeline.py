@@ -301,9 +301,15 @@ class StageFollower:
 
 
 def make_transport(rank: int, world: int, device: torch.device) -> Transport:
+    """RCCL P2P on GPUs (default); ``DLI_TRANSPORT=host`` stages GPU tensors through gloo
+    (several ranks sharing one GPU); gloo on CPU."""
     if world == 1:
         return LoopbackTransport(1)
+    kind = os.environ.get("DLI_TRANSPORT", "rccl" if device.type == "cuda" else "gloo")
+    if device.type == "cuda" and kind == "rccl":
+        from ..runtime.faults import raw_store
+        return RcclTransport(raw_store(), rank, world, device)
     if device.type == "cuda":
-        store = dist.distributed_c10d._get_default_store()
-        return RcclTransport(store, rank, world, device)
+        from .transport import HostStagedTransport
+        return HostStagedTransport()
     return TorchDistTransport()

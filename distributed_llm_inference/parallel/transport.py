@@ -55,6 +55,29 @@ class TorchDistTransport(Transport):
         return t
 
 
+class HostStagedTransport(Transport):
+    """GPU tensors over torch.distributed (gloo) through host memory.
+
+    A fallback / test transport: it lets several stage processes share ONE GPU (RCCL refuses two
+    ranks on the same device), which is how the multi-process GPU code path is exercised on a
+    single-GPU box.  Never the production path on a multi-GPU node.
+    """
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+
+    def send(self, t, peer):
+        dist.send(t.detach().to("cpu").contiguous(), peer, group=self.group)
+
+    def recv(self, t, peer):
+        host = torch.empty(t.shape, dtype=t.dtype)
+        dist.recv(host, peer, group=self.group)
+        t.copy_(host, non_blocking=False)
+        return t
+
+
 class LoopbackTransport(Transport):
     """In-process hand-off: ``send`` enqueues, ``recv`` dequeues (FIFO per (src, dst) pair)."""
 

@@ -141,6 +141,10 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     local = int(os.environ.get("LOCAL_RANK", rank))
     spec = resolve_model(cfg.checkpoint or cfg.model)
     if torch.cuda.is_available():
+        # DLI_SHARE_GPU=1: several stage processes on the visible GPUs round-robin (tests on a
+        # single-GPU box); otherwise one GPU per local rank
+        if os.environ.get("DLI_SHARE_GPU") == "1":
+            local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:

@@ -1,0 +1,141 @@
+"""Multi-process pipeline on the GPU (one process per stage).
+
+The box used for GPU tests has ONE MI355X, so stage processes share it (``DLI_SHARE_GPU=1``).
+RCCL refuses two ranks on the same device, so the full driver/follower GPU path (graphs, shm
+control plane, token feedback, micro-batching) is exercised with the host-staged transport, and the
+RCCL communicator itself is exercised by a same-device 2-rank smoke test that is skipped if RCCL
+rejects the duplicate device.  The 8-GPU xGMI run is the driver's round-end scaling bench.
+"""
+import multiprocessing as mp
+import os
+import socket
+import traceback
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+PROMPTS = [list(range(3, 40)), [7, 8, 9], list(range(200, 330)), [11], [5, 5, 5, 5]]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg(world, mbs):
+    from distributed_llm_inference.config import CacheConfig, ModelSpec, ServeConfig
+    from distributed_llm_inference.runtime.engine import EngineConfig
+    spec = ModelSpec(name="t", vocab_size=1000, hidden_size=256, intermediate_size=512,
+                     num_layers=4, num_heads=8, num_kv_heads=2, head_dim=32, rope_theta=10000.0,
+                     max_position_embeddings=4096)
+    cfg = EngineConfig(model=spec, pp=world, seed=5,  # type: ignore[arg-type]
+                       cache=CacheConfig(num_blocks=256, block_size=64),
+                       serve=ServeConfig(max_batch_size=8, max_num_batched_tokens=512,
+                                         max_seq_len=1024, num_micro_batches=mbs,
+                                         graph_batch_sizes=[1, 2, 4, 8]))
+    return spec, cfg
+
+
+def _pipeline_worker(rank, world, port, mbs, q):
+    try:
+        os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                          MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_SHARE_GPU="1",
+                          DLI_TRANSPORT="host", DLI_TUNABLEOP="0")
+        import torch.distributed as dist
+        from distributed_llm_inference.runtime.engine import init_pipeline_rank
+        from distributed_llm_inference.runtime.sequence import SamplingParams
+        _, cfg = _cfg(world, mbs)
+        role, obj = init_pipeline_rank(cfg)
+        if role == "driver":
+            out = obj.generate(PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))
+            obj.stop()
+            q.put(("ok", [s.output for s in out]))
+        else:
+            obj.run()
+        dist.destroy_process_group()
+    except Exception:
+        q.put(("err", traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize("world,mbs", [(2, 3), (4, 5)])
+def test_multiprocess_pipeline_on_gpu(gpu, world, mbs):
+    from distributed_llm_inference.runtime.engine import LLMEngine
+    from distributed_llm_inference.runtime.sequence import SamplingParams
+    os.environ["DLI_TUNABLEOP"] = "0"
+    spec, cfg = _cfg(1, mbs)
+    ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
+        PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_pipeline_worker, args=(r, world, port, mbs, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    status, got = q.get(timeout=600)
+    for p in ps:
+        p.join(120)
+    assert status == "ok", got
+    assert all(p.exitcode == 0 for p in ps)
+    assert got == ref
+
+
+def _rccl_worker(rank, port, q):
+    try:
+        os.environ.update(RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        from distributed_llm_inference.parallel.transport import RcclTransport
+        from distributed_llm_inference.runtime.faults import raw_store
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        tr = RcclTransport(raw_store(), rank, 2, dev)
+        x = torch.arange(1 << 20, device=dev, dtype=torch.float32) * (rank + 1)
+        if rank == 0:
+            tr.send(x, 1)
+            torch.cuda.synchronize()
+            q.put(("ok", None))
+        else:
+            y = torch.empty_like(x)
+            tr.recv(y, 0)
+            torch.cuda.synchronize()
+            ok = torch.equal(y, torch.arange(1 << 20, device=dev, dtype=torch.float32))
+            q.put(("ok" if ok else "bad", None))
+        tr.close()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put(("err", repr(e)))
+
+
+def test_rccl_p2p_same_device(gpu):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_rccl_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    import queue as _queue
+    res = []
+    try:
+        for _ in ps:
+            res.append(q.get(timeout=120))
+    except _queue.Empty:
+        res.append(("err", "timeout"))
+    finally:
+        for p in ps:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+                p.join(10)
+    errs = [m for s, m in res if s == "err"]
+    if errs == ["timeout"]:
+        pytest.skip("RCCL with two ranks on one device did not complete (expected on 1-GPU boxes)")
+    if errs and any("uplicate" in m or "invalid usage" in m.lower() for m in errs):
+        pytest.skip(f"RCCL rejects two ranks on one device: {errs[0][:200]}")
+    assert all(s == "ok" for s, _ in res), res
