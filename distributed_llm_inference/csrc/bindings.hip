@@ -32,39 +32,55 @@ inline void check_rc(int rc, const char* what) {
 }
 
 // ------------------------------------------------------------------------------ normalisation
-void rms_norm(Tensor out, Tensor x, optional<Tensor> residual, Tensor w, double eps) {
+void rms_norm(Tensor out, Tensor x, optional<Tensor> residual, Tensor w, double eps,
+              optional<Tensor> residual_out) {
   CHECK_IN(out); CHECK_IN(x); CHECK_IN(w);
   CHECK_BF16(out); CHECK_BF16(x); CHECK_BF16(w);
   const int64_t hidden = x.size(-1);
   const int64_t rows = x.numel() / hidden;
   TORCH_CHECK(w.numel() == hidden && out.numel() == x.numel(), "rms_norm: shape mismatch");
-  dli::bf16* r = nullptr;
+  const dli::bf16* r = nullptr;
+  dli::bf16* ro = nullptr;
   if (residual.has_value()) {
     CHECK_IN(*residual); CHECK_BF16(*residual);
     TORCH_CHECK(residual->numel() == x.numel(), "rms_norm: residual shape mismatch");
     r = bp(*residual);
+    ro = bp(*residual);
+    if (residual_out.has_value()) {
+      CHECK_IN(*residual_out); CHECK_BF16(*residual_out);
+      TORCH_CHECK(residual_out->numel() == x.numel(), "rms_norm: residual_out shape mismatch");
+      ro = bp(*residual_out);
+    }
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  check_rc(dli::launch_rms_norm(bp(out), bp(x), r, bp(w), (float)eps, (int)rows, (int)hidden,
-                                r != nullptr, cur_stream()), "rms_norm");
+  check_rc(dli::launch_rms_norm(bp(out), bp(x), r, ro, bp(w), (float)eps, (int)rows, (int)hidden,
+                                cur_stream()), "rms_norm");
 }
 
-void layer_norm(Tensor out, Tensor x, optional<Tensor> residual, Tensor w, Tensor b, double eps) {
+void layer_norm(Tensor out, Tensor x, optional<Tensor> residual, Tensor w, Tensor b, double eps,
+                optional<Tensor> residual_out) {
   CHECK_IN(out); CHECK_IN(x); CHECK_IN(w); CHECK_IN(b);
   CHECK_BF16(out); CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(b);
   const int64_t hidden = x.size(-1);
   const int64_t rows = x.numel() / hidden;
   TORCH_CHECK(w.numel() == hidden && b.numel() == hidden && out.numel() == x.numel(),
               "layer_norm: shape mismatch");
-  dli::bf16* r = nullptr;
+  const dli::bf16* r = nullptr;
+  dli::bf16* ro = nullptr;
   if (residual.has_value()) {
     CHECK_IN(*residual); CHECK_BF16(*residual);
     TORCH_CHECK(residual->numel() == x.numel(), "layer_norm: residual shape mismatch");
     r = bp(*residual);
+    ro = bp(*residual);
+    if (residual_out.has_value()) {
+      CHECK_IN(*residual_out); CHECK_BF16(*residual_out);
+      TORCH_CHECK(residual_out->numel() == x.numel(), "layer_norm: residual_out shape mismatch");
+      ro = bp(*residual_out);
+    }
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  check_rc(dli::launch_layer_norm(bp(out), bp(x), r, bp(w), bp(b), (float)eps, (int)rows,
-                                  (int)hidden, r != nullptr, cur_stream()), "layer_norm");
+  check_rc(dli::launch_layer_norm(bp(out), bp(x), r, ro, bp(w), bp(b), (float)eps, (int)rows,
+                                  (int)hidden, cur_stream()), "layer_norm");
 }
 
 // ------------------------------------------------------------------------------ activations
@@ -328,8 +344,10 @@ void register_rccl(pybind11::module_& m);  // comm/rccl_p2p.hip
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "CDNA4 (gfx950) kernels of distributed_llm_inference";
   m.def("rms_norm", &rms_norm, "RMSNorm (+fused residual add)", py::arg("out"), py::arg("x"),
-        py::arg("residual"), py::arg("w"), py::arg("eps"));
-  m.def("layer_norm", &layer_norm, "LayerNorm (+fused residual add)");
+        py::arg("residual"), py::arg("w"), py::arg("eps"), py::arg("residual_out") = py::none());
+  m.def("layer_norm", &layer_norm, "LayerNorm (+fused residual add)", py::arg("out"),
+        py::arg("x"), py::arg("residual"), py::arg("w"), py::arg("b"), py::arg("eps"),
+        py::arg("residual_out") = py::none());
   m.def("silu_mul", &silu_mul, "SwiGLU: out = silu(x[:, :I]) * x[:, I:]");
   m.def("gelu_bias", &gelu_bias, "gelu_tanh(x + bias)");
   m.def("add", &add, "out = a + b");

@@ -51,10 +51,11 @@ struct SampleParams {
   float* out_logprobs;      // [B] or nullptr
 };
 
-int launch_rms_norm(bf16* out, const bf16* x, bf16* residual, const bf16* w, float eps, int rows,
-                    int hidden, bool add_residual, hipStream_t stream);
-int launch_layer_norm(bf16* out, const bf16* x, bf16* residual, const bf16* w, const bf16* b,
-                      float eps, int rows, int hidden, bool add_residual, hipStream_t stream);
+int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* residual_out,
+                    const bf16* w, float eps, int rows, int hidden, hipStream_t stream);
+int launch_layer_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* residual_out,
+                      const bf16* w, const bf16* b, float eps, int rows, int hidden,
+                      hipStream_t stream);
 int launch_silu_mul(bf16* out, const bf16* x, int rows, int inter, hipStream_t stream);
 int launch_gelu_bias(bf16* out, const bf16* x, const bf16* bias, int rows, int cols,
                      hipStream_t stream);

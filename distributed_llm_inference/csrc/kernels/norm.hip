@@ -3,9 +3,11 @@
 // Reference behaviour: LlamaRMSNorm applied at models/llama/modules.py:124-125, 159-162, 173-179
 // (input norm, post-attention norm).  The reference computes RMSNorm(h + h) because `residual is
 // hidden_states` and uses the default eps (B9); here the intended
-//     residual' = x + residual ; out = w * residual' * rsqrt(mean(residual'^2) + eps)
+//     residual_out = x + residual_in ; out = w * residual_out * rsqrt(mean(residual_out^2) + eps)
 // is computed in one pass over HBM: one workgroup per row, the row held in registers (16-byte
 // bf16x8 accesses per lane), fp32 statistics, one rounding to bf16 at the end.
+// residual_out may alias residual_in (in-place residual stream) or not (the first add of a
+// pipeline stage must not modify the stage's input buffer, which a hipGraph replays from).
 #include "kernels.h"
 
 namespace dli {
@@ -13,14 +15,15 @@ namespace dli {
 template <int VPT>  // bf16x8 vectors per thread
 __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
                                                        const bf16* __restrict__ x,
-                                                       bf16* __restrict__ residual,
+                                                       const bf16* residual_in, bf16* residual_out,
                                                        const bf16* __restrict__ w, float eps,
                                                        int hidden, int add_residual) {
   __shared__ float scratch[8];
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
   const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * hidden);
-  bf16x8* rr = reinterpret_cast<bf16x8*>(residual + (size_t)row * hidden);
+  const bf16x8* ri = reinterpret_cast<const bf16x8*>(residual_in + (size_t)row * hidden);
+  bf16x8* ro = reinterpret_cast<bf16x8*>(residual_out + (size_t)row * hidden);
   const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
   bf16x8* outr = reinterpret_cast<bf16x8*>(out + (size_t)row * hidden);
 
@@ -32,11 +35,11 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
     if (idx < nvec) {
       bf16x8 a = xr[idx];
       if (add_residual) {
-        bf16x8 r = rr[idx];
+        bf16x8 r = ri[idx];
         bf16x8 s;
 #pragma unroll
         for (int j = 0; j < 8; ++j) s[j] = (bf16)((float)a[j] + (float)r[j]);
-        rr[idx] = s;
+        ro[idx] = s;
         a = s;
       }
 #pragma unroll
@@ -67,7 +70,8 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
 template <int VPT>
 __global__ void __launch_bounds__(256) layer_norm_kernel(bf16* __restrict__ out,
                                                          const bf16* __restrict__ x,
-                                                         bf16* __restrict__ residual,
+                                                         const bf16* residual_in,
+                                                         bf16* residual_out,
                                                          const bf16* __restrict__ w,
                                                          const bf16* __restrict__ b, float eps,
                                                          int hidden, int add_residual) {
@@ -75,7 +79,8 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(bf16* __restrict__ out,
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
   const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * hidden);
-  bf16x8* rr = reinterpret_cast<bf16x8*>(residual + (size_t)row * hidden);
+  const bf16x8* ri = reinterpret_cast<const bf16x8*>(residual_in + (size_t)row * hidden);
+  bf16x8* ro = reinterpret_cast<bf16x8*>(residual_out + (size_t)row * hidden);
   const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
   const bf16x8* br = reinterpret_cast<const bf16x8*>(b);
   bf16x8* outr = reinterpret_cast<bf16x8*>(out + (size_t)row * hidden);
@@ -87,11 +92,11 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(bf16* __restrict__ out,
     if (idx < nvec) {
       bf16x8 a = xr[idx];
       if (add_residual) {
-        bf16x8 r = rr[idx];
+        bf16x8 r = ri[idx];
         bf16x8 s;
 #pragma unroll
         for (int j = 0; j < 8; ++j) s[j] = (bf16)((float)a[j] + (float)r[j]);
-        rr[idx] = s;
+        ro[idx] = s;
         a = s;
       }
 #pragma unroll
@@ -151,17 +156,20 @@ static inline int norm_threads(int hidden) {
   } while (0)
 
 // Returns 0 on success, -1 if `hidden` is unsupported (must be a multiple of 8, <= 16384).
-int launch_rms_norm(bf16* out, const bf16* x, bf16* residual, const bf16* w, float eps, int rows,
-                    int hidden, bool add_residual, hipStream_t stream) {
+int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* residual_out,
+                    const bf16* w, float eps, int rows, int hidden, hipStream_t stream) {
   if (hidden % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -1;
-  DLI_NORM_DISPATCH(rms_norm_kernel, out, x, residual, w, eps, hidden, add_residual ? 1 : 0);
+  const int add = residual_in != nullptr ? 1 : 0;
+  DLI_NORM_DISPATCH(rms_norm_kernel, out, x, residual_in, residual_out, w, eps, hidden, add);
   return 0;
 }
 
-int launch_layer_norm(bf16* out, const bf16* x, bf16* residual, const bf16* w, const bf16* b,
-                      float eps, int rows, int hidden, bool add_residual, hipStream_t stream) {
+int launch_layer_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* residual_out,
+                      const bf16* w, const bf16* b, float eps, int rows, int hidden,
+                      hipStream_t stream) {
   if (hidden % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -1;
-  DLI_NORM_DISPATCH(layer_norm_kernel, out, x, residual, w, b, eps, hidden, add_residual ? 1 : 0);
+  const int add = residual_in != nullptr ? 1 : 0;
+  DLI_NORM_DISPATCH(layer_norm_kernel, out, x, residual_in, residual_out, w, b, eps, hidden, add);
   return 0;
 }
 

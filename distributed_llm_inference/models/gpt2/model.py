@@ -26,8 +26,9 @@ class LayerNorm(nn.Module):
         self.bias = nn.Parameter(torch.zeros(h, dtype=dtype, device=device), requires_grad=False)
         self.eps = eps
 
-    def forward(self, x, residual=None):
-        return ops.layer_norm(x, self.weight, self.bias, self.eps, residual)
+    def forward(self, x, residual=None, residual_out=None):
+        return ops.layer_norm(x, self.weight, self.bias, self.eps, residual,
+                              residual_out=residual_out)
 
 
 class GPT2Layer(nn.Module):
@@ -48,8 +49,9 @@ class GPT2Layer(nn.Module):
 
     def forward(self, hidden, residual, meta: AttnMetadata, k_cache, v_cache, cos_sin=None):
         T = hidden.shape[0]
-        if residual is None:
-            residual = hidden
+        first = residual is None
+        if first:
+            residual = hidden  # never modified in place (see LlamaDecoderLayer.forward)
             normed, _ = self.ln_1(hidden)
         else:
             normed, residual = self.ln_1(hidden, residual)
@@ -66,7 +68,8 @@ class GPT2Layer(nn.Module):
                                  meta.q_start, meta.max_q, self.scale, meta.n_sink, meta.sink_pad,
                                  meta.ring, meta.window)
         attn = self.attn_proj(o.view(T, -1))
-        normed, residual = self.ln_2(attn, residual)
+        normed, residual = self.ln_2(attn, residual,
+                                     residual_out=torch.empty_like(residual) if first else None)
         act = ops.gelu_bias(self.c_fc(normed), self.c_fc_bias)
         return self.mlp_proj(act), residual
 

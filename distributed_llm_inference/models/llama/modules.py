@@ -35,8 +35,9 @@ class RMSNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(hidden, dtype=dtype, device=device), requires_grad=False)
         self.eps = eps
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None):
-        return ops.rms_norm(x, self.weight, self.eps, residual=residual)
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                residual_out: Optional[torch.Tensor] = None):
+        return ops.rms_norm(x, self.weight, self.eps, residual=residual, residual_out=residual_out)
 
 
 class LlamaAttention(nn.Module):
@@ -100,13 +101,17 @@ class LlamaDecoderLayer(nn.Module):
     def forward(self, hidden: torch.Tensor, residual: Optional[torch.Tensor], meta: AttnMetadata,
                 k_cache: torch.Tensor, v_cache: torch.Tensor,
                 cos_sin: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-        if residual is None:
+        first = residual is None
+        if first:
+            # first layer of the stage: the input IS the residual; never modify it in place (it
+            # may be a hipGraph's static input buffer that warmup / capture replays re-read)
             residual = hidden
             normed, _ = self.input_layernorm(hidden)
         else:
             normed, residual = self.input_layernorm(hidden, residual)
         attn = self.self_attn(normed, meta, k_cache, v_cache, cos_sin)
-        normed, residual = self.post_attention_layernorm(attn, residual)
+        normed, residual = self.post_attention_layernorm(
+            attn, residual, residual_out=torch.empty_like(residual) if first else None)
         return self.mlp(normed), residual
 
     # ------------------------------------------------------------------ weights

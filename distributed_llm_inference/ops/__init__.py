@@ -47,29 +47,31 @@ def _gpu(t: torch.Tensor) -> bool:
 
 # ----------------------------------------------------------------------------- normalisation
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
-             out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
-    """``residual' = x + residual`` (in place, if given); ``out = RMSNorm(residual' or x) * w``."""
+             out: Optional[torch.Tensor] = None, residual_out: Optional[torch.Tensor] = None
+             ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """``r = x + residual`` written to ``residual_out`` (default: in place into ``residual``);
+    ``out = RMSNorm(r or x) * w``.  Returns ``(out, r)``."""
     if not _gpu(x):
-        y, r = ref.rms_norm(x, w, eps, residual)
+        y, r = ref.rms_norm(x, w, eps, residual, residual_out)
         if out is not None:
             out.copy_(y)
             y = out
         return y, r
     out = torch.empty_like(x) if out is None else out
-    native().rms_norm(out, x, residual, w, float(eps))
-    return out, residual
+    native().rms_norm(out, x, residual, w, float(eps), residual_out)
+    return out, (residual_out if residual_out is not None else residual)
 
 
-def layer_norm(x, w, b, eps, residual=None, out=None):
+def layer_norm(x, w, b, eps, residual=None, out=None, residual_out=None):
     if not _gpu(x):
-        y, r = ref.layer_norm(x, w, b, eps, residual)
+        y, r = ref.layer_norm(x, w, b, eps, residual, residual_out)
         if out is not None:
             out.copy_(y)
             y = out
         return y, r
     out = torch.empty_like(x) if out is None else out
-    native().layer_norm(out, x, residual, w, b, float(eps))
-    return out, residual
+    native().layer_norm(out, x, residual, w, b, float(eps), residual_out)
+    return out, (residual_out if residual_out is not None else residual)
 
 
 # ----------------------------------------------------------------------------- activations

@@ -19,19 +19,22 @@ import torch.nn.functional as F
 
 # ----------------------------------------------------------------------------- normalisation
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float,
-             residual: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+             residual: Optional[torch.Tensor] = None, residual_out: Optional[torch.Tensor] = None
+             ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     if residual is not None:
-        residual.copy_((x.float() + residual.float()).to(residual.dtype))
-        x = residual
+        dst = residual if residual_out is None else residual_out
+        dst.copy_((x.float() + residual.float()).to(residual.dtype))
+        x = residual = dst
     xf = x.float()
     y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
     return y.to(x.dtype), residual
 
 
-def layer_norm(x, w, b, eps, residual=None):
+def layer_norm(x, w, b, eps, residual=None, residual_out=None):
     if residual is not None:
-        residual.copy_((x.float() + residual.float()).to(residual.dtype))
-        x = residual
+        dst = residual if residual_out is None else residual_out
+        dst.copy_((x.float() + residual.float()).to(residual.dtype))
+        x = residual = dst
     y = F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps)
     return y.to(x.dtype), residual
 

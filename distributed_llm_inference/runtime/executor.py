@@ -96,11 +96,35 @@ class _Staging:
             self.offsets[name] = (off, dt, shape)
             off += (nbytes + 255) // 256 * 256
         pin = device.type == "cuda"
-        self.host = torch.zeros(off, dtype=torch.uint8, pin_memory=pin)
+        # a RING of pinned host slots: async H2D copies of step k may still be pending on the
+        # stream when the host already stages step k+1 (the host runs ahead of the GPU), so a
+        # slot is reused only after the event recorded behind its uploads has completed
+        self.nslots = 4 if pin else 1
+        self.hosts = [torch.zeros(off, dtype=torch.uint8, pin_memory=pin) for _ in range(self.nslots)]
+        self.hviews = [{k: self._view(h, k) for k in self.offsets} for h in self.hosts]
+        self.events: List[Optional[torch.cuda.Event]] = [None] * self.nslots
+        self.slot = 0
+        self.host = self.hosts[0]
+        self.h = self.hviews[0]
         self.dev = torch.zeros(off, dtype=torch.uint8, device=device)
-        self.h = {k: self._view(self.host, k) for k in self.offsets}
         self.d = {k: self._view(self.dev, k) for k in self.offsets}
         self.device = device
+
+    def acquire(self) -> None:
+        """Switch to the next host slot, waiting until its previous uploads have executed."""
+        self.slot = (self.slot + 1) % self.nslots
+        ev = self.events[self.slot]
+        if ev is not None:
+            ev.synchronize()
+        self.host = self.hosts[self.slot]
+        self.h = self.hviews[self.slot]
+
+    def release(self) -> None:
+        """Mark the current slot's uploads as enqueued (reusable once this event completes)."""
+        if self.device.type == "cuda":
+            ev = self.events[self.slot] or torch.cuda.Event()
+            ev.record()
+            self.events[self.slot] = ev
 
     def _view(self, buf, name):
         off, dt, shape = self.offsets[name]
@@ -171,10 +195,11 @@ class StageExecutor:
     def _stage_metadata(self, plan: StepPlan, rows: int) -> Tuple[int, int]:
         """Fill the staging buffers for ``plan`` padded to ``rows`` sequences; returns (T, nb)."""
         st = self.staging
-        h = st.h
         B = len(plan.seq_ids)
         if rows > self.max_num_seqs or plan.num_tokens > self.max_tokens:
             raise ValueError("step exceeds executor limits (max_num_seqs / max_num_batched_tokens)")
+        st.acquire()
+        h = st.h
         nb = self.max_blocks
         T = self.pool.manager.prepare(
             plan.seq_ids, plan.q_lens, h["slot_mapping"].data_ptr(), h["positions"].data_ptr(),
@@ -225,6 +250,7 @@ class StageExecutor:
             st.upload("seeds", n)
             h["step"][0] = plan.step
             st.upload("step", 1)
+        st.release()
         return T, nb
 
     def _metadata(self, plan: StepPlan, rows: int, num_splits: int,
@@ -358,6 +384,7 @@ class StageExecutor:
         for r in sizes or self.graph_sizes:
             if r in self._graphs:
                 continue
+            self.staging.acquire()
             h = self.staging.h
             h["seq_lens"][:r] = 0
             h["slot_mapping"][:r] = -1
@@ -373,6 +400,7 @@ class StageExecutor:
                          ("q_start", r + 1), ("tokens", r), ("temperature", r), ("top_k", r),
                          ("top_p", r), ("seeds", r)):
                 self.staging.upload(k, n)
+            self.staging.release()
             if self._hidden_in is not None:
                 self._hidden_in[:r].zero_()
             self._capture(r)

@@ -223,3 +223,16 @@ def test_quant_rowwise(gpu):
     y, _ = ref.rms_norm(x.cpu(), w.cpu(), 1e-5, residual=r2.cpu())
     deq2 = (q2.float() * s2).cpu()
     assert (deq2 - y.float()).abs().max() / y.float().abs().max() < 0.07
+
+
+def test_rms_norm_residual_out_of_place(gpu):
+    x = torch.randn(5, 4096, device=gpu, dtype=BF)
+    r = torch.randn(5, 4096, device=gpu, dtype=BF)
+    w = torch.ones(4096, device=gpu, dtype=BF)
+    r0 = r.clone()
+    ro = torch.empty_like(r)
+    y, r2 = ops.rms_norm(x, w, 1e-5, residual=r, residual_out=ro)
+    assert r2 is ro and torch.equal(r, r0)  # input residual untouched
+    _close(ro, x.float() + r0.float(), 1e-2, 1e-2, "residual_out")
+    y_ref, _ = ref.rms_norm(x.cpu(), w.cpu(), 1e-5, residual=r0.cpu().clone())
+    _close(y, y_ref, 2e-2, 1e-2, "rms_norm")
