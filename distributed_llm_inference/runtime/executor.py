@@ -31,6 +31,13 @@ from ..models.stage import CausalLMStage
 
 log = logging.getLogger(__name__)
 
+import os as _os  # noqa: E402
+
+# DLI_TRACE=1: roctx range per stage step (visible with rocprofv3 --marker-trace / torch profiler)
+# DLI_DEBUG_SYNC=1: synchronise after every stage step and check outputs (NaN/Inf, token range)
+_TRACE = _os.environ.get("DLI_TRACE", "0") == "1"
+_DEBUG = _os.environ.get("DLI_DEBUG_SYNC", "0") == "1"
+
 
 @dataclass
 class StepPlan:
@@ -318,6 +325,27 @@ class StageExecutor:
         """Run one step.  ``inputs``: hidden states [T, H] for non-first stages (ignored on stage 0,
         which embeds ``plan.tokens``).  Returns hidden [T, H] or sampled tokens [n_sample] int32
         (device tensors; the caller decides when to synchronise)."""
+        if not (_TRACE or _DEBUG):
+            return self._execute(plan, inputs)
+        tag = f"stage[{self.stage.start},{self.stage.end}) step={plan.step} mb={plan.mb} " \
+              f"{'decode' if plan.is_decode else 'prefill'} B={len(plan.seq_ids)} T={plan.num_tokens}"
+        if _TRACE and self.device.type == "cuda":
+            torch.cuda.nvtx.range_push(tag)  # roctx range on ROCm (rocprofv3 --marker-trace)
+        try:
+            out = self._execute(plan, inputs)
+        finally:
+            if _TRACE and self.device.type == "cuda":
+                torch.cuda.nvtx.range_pop()
+        if _DEBUG and out.numel():
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            if out.is_floating_point() and not torch.isfinite(out.float()).all():
+                raise FloatingPointError(f"non-finite output in {tag}")
+            if not out.is_floating_point() and (out.min() < 0 or out.max() >= self.spec.vocab_size):
+                raise ValueError(f"sampled token out of range in {tag}")
+        return out
+
+    def _execute(self, plan: StepPlan, inputs: Optional[torch.Tensor]) -> torch.Tensor:
         self.apply_frees(plan.free_ids)
         if not plan.seq_ids:
             return torch.empty(0, device=self.device)
@@ -330,13 +358,13 @@ class StageExecutor:
         n_sample = len(plan.sample_rows)
         all_sample = decode and n_sample == B
         if grows is not None and (not self.stage.has_head or all_sample):
-            g = self._graphs.get(grows)
-            if g is None:
-                g = self._capture(grows)
             if not self.stage.has_embed:
                 src = inputs[:B]
                 if src.data_ptr() != self._hidden_in.data_ptr():
                     self._hidden_in[:B].copy_(src)
+            g = self._graphs.get(grows)
+            if g is None:
+                g = self._capture(grows)
             g.graph.replay()
             return g.out[:n_sample] if self.stage.has_head else g.out[:B].clone()
         splits = self._splits(rows) if decode else 1
@@ -373,8 +401,7 @@ class StageExecutor:
         self._graphs[rows] = entry
         log.info("captured decode graph rows=%d splits=%d stage=[%d,%d)", rows, splits,
                  self.stage.start, self.stage.end)
-        # the captured run did not execute; run the real step now
-        graph.replay()
+        # (the captured run did not execute; the caller replays the graph for the real step)
         return entry
 
     def warmup_graphs(self, sizes: Optional[Sequence[int]] = None) -> None:
