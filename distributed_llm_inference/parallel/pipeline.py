@@ -250,6 +250,25 @@ class StageFollower:
             self._pub_thread = threading.Thread(target=self._publisher, daemon=True)
             self._pub_thread.start()
 
+    # ring of receive buffers: the receive of micro-batch m+1 only waits until the compute that
+    # READ the slot (two steps earlier) is done, not for everything queued on the compute stream
+    def _recv_slot(self, T: int):
+        if not hasattr(self, "_rbufs"):
+            n = 3
+            H = self.ex.spec.hidden_size
+            self._rbufs = [torch.empty(self.ex.max_tokens, H, dtype=torch.bfloat16,
+                                       device=self.ex.device) for _ in range(n)]
+            self._rfree = [None] * n
+            self._rslot = 0
+        self._rslot = (self._rslot + 1) % len(self._rbufs)
+        return self._rbufs[self._rslot][:T], self._rfree[self._rslot]
+
+    def _release_slot(self) -> None:
+        if self.ex.device.type == "cuda":
+            ev = self._rfree[self._rslot] or torch.cuda.Event()
+            ev.record()
+            self._rfree[self._rslot] = ev
+
     def _publisher(self) -> None:
         while True:
             item = self._pub_q.get()
@@ -280,13 +299,14 @@ class StageFollower:
             if not plan.seq_ids:
                 self.ex.execute(plan, None)  # frees only
                 continue
-            buf = self.ex.input_buffer(plan)
-            x = self.tr.recv(buf, self.rank - 1)
+            buf, free_ev = self._recv_slot(plan.num_tokens)
+            x = self.tr.recv(buf, self.rank - 1, free_event=free_ev)
             if self.faults.active:
                 self.faults.on_step()
             tok = self.stats.begin(self.faults.delay_ms)
             out = self.ex.execute(plan, x)
             self.stats.end(tok)
+            self._release_slot()
             if self.is_last:
                 pinned, ev = _sample_tokens_to_host(out)
                 self._pub_q.put((plan.step, plan.mb, pinned, ev))

@@ -32,7 +32,7 @@ class Transport:
     def send(self, t: torch.Tensor, peer: int) -> None:
         raise NotImplementedError
 
-    def recv(self, t: torch.Tensor, peer: int) -> torch.Tensor:
+    def recv(self, t: torch.Tensor, peer: int, free_event=None) -> torch.Tensor:
         raise NotImplementedError
 
     def close(self) -> None:
@@ -50,7 +50,7 @@ class TorchDistTransport(Transport):
     def send(self, t, peer):
         dist.send(t.contiguous(), peer, group=self.group)
 
-    def recv(self, t, peer):
+    def recv(self, t, peer, free_event=None):
         dist.recv(t, peer, group=self.group)
         return t
 
@@ -71,7 +71,9 @@ class HostStagedTransport(Transport):
     def send(self, t, peer):
         dist.send(t.detach().to("cpu").contiguous(), peer, group=self.group)
 
-    def recv(self, t, peer):
+    def recv(self, t, peer, free_event=None):
+        if free_event is not None:
+            free_event.synchronize()
         host = torch.empty(t.shape, dtype=t.dtype)
         dist.recv(host, peer, group=self.group)
         t.copy_(host, non_blocking=False)
@@ -110,13 +112,11 @@ class RcclTransport(Transport):
         self._comms: Dict[int, object] = {}
         dev_idx = device.index if device.index is not None else torch.cuda.current_device()
         # pair (i, i+1): the lower rank creates the id; both ends create a 2-rank communicator.
-        # Ring closure (last -> 0) pair as well, for generic use (e.g. token feedback on device).
-        pairs = set()
-        for r in range(world - 1):
-            pairs.add((r, r + 1))
-        if world > 2:
-            pairs.add((0, world - 1))
-        for (a, b) in sorted(pairs):
+        # (sampled tokens return to the driver over the shm control plane, so no ring closure).
+        # Init order: every rank initialises its lower pair first, so the chain of blocking
+        # ncclCommInitRank calls resolves from rank 0 upwards without a cycle.
+        pairs = [(r, r + 1) for r in range(world - 1)]
+        for (a, b) in pairs:
             if rank not in (a, b):
                 continue
             key = f"{prefix}/{a}-{b}"
@@ -141,10 +141,17 @@ class RcclTransport(Transport):
         t.record_stream(self.send_stream)
         self._comm(peer).send(t, self._peer_index(peer), self.send_stream.cuda_stream)
 
-    def recv(self, t: torch.Tensor, peer: int) -> torch.Tensor:
-        """Asynchronous: later work on the current stream waits for the data."""
+    def recv(self, t: torch.Tensor, peer: int, free_event: Optional["torch.cuda.Event"] = None
+             ) -> torch.Tensor:
+        """Asynchronous: later work on the current stream waits for the data.
+
+        ``free_event`` (optional) marks when ``t`` is no longer read by earlier compute; without it
+        the receive waits for everything queued on the compute stream (no overlap)."""
         cur = torch.cuda.current_stream(self.device)
-        self.recv_stream.wait_stream(cur)  # the buffer may still be read by earlier compute
+        if free_event is not None:
+            self.recv_stream.wait_event(free_event)
+        else:
+            self.recv_stream.wait_stream(cur)
         t.record_stream(self.recv_stream)
         self._comm(peer).recv(t, self._peer_index(peer), self.recv_stream.cuda_stream)
         cur.wait_stream(self.recv_stream)
