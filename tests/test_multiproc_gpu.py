@@ -139,3 +139,29 @@ def test_rccl_p2p_same_device(gpu):
     if errs and any("uplicate" in m or "invalid usage" in m.lower() for m in errs):
         pytest.skip(f"RCCL rejects two ranks on one device: {errs[0][:200]}")
     assert all(s == "ok" for s, _ in res), res
+
+
+def test_rccl_single_rank_self_p2p_and_collectives(gpu):
+    """The RCCL binding on real hardware with a 1-rank communicator: send/recv to self inside a
+    group on explicit streams, all_reduce / broadcast / all_gather."""
+    from distributed_llm_inference import ops
+    C = ops.native()
+    assert C.rccl_version() > 0
+    comm = C.RcclComm(bytes(C.rccl_unique_id()), 0, 1, 0)
+    s = torch.cuda.Stream()
+    x = torch.arange(4096, device=gpu, dtype=torch.bfloat16)
+    y = torch.zeros_like(x)
+    comm.group_start()
+    comm.send(x, 0, s.cuda_stream)
+    comm.recv(y, 0, s.cuda_stream)
+    comm.group_end()
+    s.synchronize()
+    assert torch.equal(x, y)
+    z = torch.ones(1000, device=gpu)
+    comm.all_reduce(z)
+    comm.broadcast(z, 0)
+    out = torch.empty(1000, device=gpu)
+    comm.all_gather(z, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, z)
+    comm.destroy()
