@@ -337,6 +337,29 @@ void quant_rowwise(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> residu
            "quant_rowwise");
 }
 
+// ------------------------------------------------------------------------------ decode GEMM
+void gemm_nt(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t bn,
+             optional<Tensor> workspace) {
+  CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
+  CHECK_BF16(out); CHECK_BF16(a); CHECK_BF16(b);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_nt: 2-D tensors");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "gemm_nt: shape mismatch");
+  TORCH_CHECK(M >= 1 && M <= 256, "gemm_nt: M must be in [1, 256]");
+  TORCH_CHECK(K % 64 == 0 && N % bn == 0 && (bn == 64 || bn == 128), "gemm_nt: K%64, N%bn");
+  TORCH_CHECK(splits >= 1 && (K / 64) % splits == 0, "gemm_nt: splits must divide K/64");
+  float* ws = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(workspace.has_value(), "gemm_nt: split-K needs a workspace");
+    CHECK_IN(*workspace); CHECK_F32(*workspace);
+    TORCH_CHECK(workspace->numel() >= splits * M * N, "gemm_nt: workspace too small");
+    ws = workspace->data_ptr<float>();
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
+  check_rc(dli::launch_gemm_nt(bp(out), bp(a), bp(b), ws, (int)M, (int)N, (int)K, (int)splits,
+                               (int)bn, cur_stream()), "gemm_nt");
+}
+
 }  // namespace
 
 void register_rccl(pybind11::module_& m);  // comm/rccl_p2p.hip
@@ -356,5 +379,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_prefill", &attn_prefill, "paged causal prefill attention (varlen)");
   m.def("sample", &sample, "greedy / temperature / top-k / top-p sampling");
   m.def("quant_rowwise", &quant_rowwise, "row-wise fp8 e4m3 quantisation (+fused RMSNorm)");
+  m.def("gemm_nt", &gemm_nt, "decode GEMM C = A . B^T (M <= 256, split-K MFMA)", py::arg("out"),
+        py::arg("a"), py::arg("b"), py::arg("splits"), py::arg("bn"),
+        py::arg("workspace") = py::none());
   register_rccl(m);
 }

@@ -64,6 +64,8 @@ int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stre
 int launch_attn_decode(const AttnParams& p, int B, int D, hipStream_t stream);
 int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_t stream);
 int launch_sample(const SampleParams& p, int B, hipStream_t stream);
+int launch_gemm_nt(bf16* C, const bf16* A, const bf16* B, float* workspace, int M, int N, int K,
+                   int splits, int bn, hipStream_t stream);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, bf16* residual,
                          const bf16* norm_w, float eps, int rows, int K, bool add_residual,
                          hipStream_t stream);

@@ -225,3 +225,20 @@ def quantize_weight_fp8(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
 
 def softmax_scale(head_dim: int) -> float:
     return 1.0 / math.sqrt(head_dim)
+
+
+# ----------------------------------------------------------------------------- decode GEMM
+def gemm_nt(x: torch.Tensor, w: torch.Tensor, splits: int = 1, bn: int = 128,
+            out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None
+            ) -> torch.Tensor:
+    """``x [M, K] @ w[N, K]^T`` with the hand-written split-K MFMA kernel (M <= 256)."""
+    if not _gpu(x):
+        y = (x.float() @ w.float().t()).to(x.dtype)
+        return out.copy_(y) if out is not None else y
+    M, N = x.shape[0], w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    if splits > 1 and workspace is None:
+        workspace = torch.empty(splits * M * N, dtype=torch.float32, device=x.device)
+    native().gemm_nt(out, x, w, int(splits), int(bn), workspace)
+    return out
