@@ -121,12 +121,13 @@ void add(Tensor out, Tensor a, Tensor b) {
 // ------------------------------------------------------------------------------ rope + cache
 void check_cache(const Tensor& k_cache, const Tensor& v_cache, int64_t nkv, int64_t D) {
   CHECK_IN(k_cache); CHECK_IN(v_cache); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
-  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4, "caches must be 4-D");
-  // k: [blocks, nkv, bs, D]; v: [blocks, nkv, D, bs]
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 5, "k_cache must be 4-D, v_cache 5-D");
+  // k: [blocks, nkv, bs, D]; v: [blocks, nkv, bs/8, D, 8]
   TORCH_CHECK(k_cache.size(1) == nkv && k_cache.size(3) == D, "k_cache must be [blocks, nkv, bs, D]");
   TORCH_CHECK(v_cache.size(0) == k_cache.size(0) && v_cache.size(1) == nkv &&
-                  v_cache.size(2) == D && v_cache.size(3) == k_cache.size(2),
-              "v_cache must be [blocks, nkv, D, bs]");
+                  v_cache.size(2) * 8 == k_cache.size(2) && v_cache.size(3) == D &&
+                  v_cache.size(4) == 8,
+              "v_cache must be [blocks, nkv, bs/8, D, 8]");
 }
 
 void rope_cache(Tensor qkv, optional<Tensor> positions, optional<Tensor> slot_mapping,
@@ -312,17 +313,24 @@ void sample(Tensor out_tokens, optional<Tensor> out_logprobs, Tensor logits,
 
 // ------------------------------------------------------------------------------ fp8 quant
 void quant_rowwise(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> residual,
-                   optional<Tensor> norm_w, double eps) {
+                   optional<Tensor> norm_w, double eps, optional<Tensor> residual_out) {
   CHECK_IN(q_out); CHECK_IN(scale); CHECK_IN(x); CHECK_BF16(x); CHECK_F32(scale);
   TORCH_CHECK(q_out.element_size() == 1, "q_out must be an 8-bit tensor");
   const int64_t K = x.size(-1);
   const int64_t rows = x.numel() / K;
   TORCH_CHECK(q_out.numel() == x.numel() && scale.numel() == rows, "quant: shape mismatch");
-  dli::bf16* r = nullptr;
+  const dli::bf16* ri = nullptr;
+  dli::bf16* ro = nullptr;
   if (residual.has_value()) {
     CHECK_IN(*residual); CHECK_BF16(*residual);
     TORCH_CHECK(residual->numel() == x.numel(), "quant: residual shape mismatch");
-    r = bp(*residual);
+    ri = bp(*residual);
+    ro = bp(*residual);
+    if (residual_out.has_value()) {
+      CHECK_IN(*residual_out); CHECK_BF16(*residual_out);
+      TORCH_CHECK(residual_out->numel() == x.numel(), "quant: residual_out shape mismatch");
+      ro = bp(*residual_out);
+    }
   }
   const dli::bf16* w = nullptr;
   if (norm_w.has_value()) {
@@ -332,9 +340,22 @@ void quant_rowwise(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> residu
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_rc(dli::launch_quant_rowwise(reinterpret_cast<uint8_t*>(q_out.data_ptr()),
-                                     scale.data_ptr<float>(), bp(x), r, w, (float)eps, (int)rows,
-                                     (int)K, r != nullptr, cur_stream()),
+                                     scale.data_ptr<float>(), bp(x), ri, ro, w, (float)eps,
+                                     (int)rows, (int)K, cur_stream()),
            "quant_rowwise");
+}
+
+void silu_mul_quant(Tensor q_out, Tensor scale, Tensor x) {
+  CHECK_IN(q_out); CHECK_IN(scale); CHECK_IN(x); CHECK_BF16(x); CHECK_F32(scale);
+  TORCH_CHECK(q_out.element_size() == 1, "q_out must be an 8-bit tensor");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 2 == 0, "silu_mul_quant: x must be [rows, 2I]");
+  const int64_t rows = x.size(0), I = x.size(1) / 2;
+  TORCH_CHECK(q_out.numel() == rows * I && scale.numel() == rows, "silu_mul_quant: shape mismatch");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_rc(dli::launch_silu_mul_quant(reinterpret_cast<uint8_t*>(q_out.data_ptr()),
+                                      scale.data_ptr<float>(), bp(x), (int)rows, (int)I,
+                                      cur_stream()),
+           "silu_mul_quant");
 }
 
 // ------------------------------------------------------------------------------ decode GEMM
@@ -378,7 +399,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_decode", &attn_decode, "paged GQA decode attention (split-K)");
   m.def("attn_prefill", &attn_prefill, "paged causal prefill attention (varlen)");
   m.def("sample", &sample, "greedy / temperature / top-k / top-p sampling");
-  m.def("quant_rowwise", &quant_rowwise, "row-wise fp8 e4m3 quantisation (+fused RMSNorm)");
+  m.def("quant_rowwise", &quant_rowwise, "row-wise fp8 e4m3 quantisation (+fused RMSNorm)",
+        py::arg("q_out"), py::arg("scale"), py::arg("x"), py::arg("residual"), py::arg("norm_w"),
+        py::arg("eps"), py::arg("residual_out") = py::none());
+  m.def("silu_mul_quant", &silu_mul_quant, "SwiGLU fused with row-wise fp8 quantisation");
   m.def("gemm_nt", &gemm_nt, "decode GEMM C = A . B^T (M <= 256, split-K MFMA)", py::arg("out"),
         py::arg("a"), py::arg("b"), py::arg("splits"), py::arg("bn"),
         py::arg("workspace") = py::none());

@@ -7,7 +7,8 @@
 //   * both products run on MFMA v_mfma_f32_16x16x32_bf16 in the "swapped" orientation
 //        S^T[key, q] = K[key, d] . Q^T[d, q]        (A = K rows, B = Q^T)
 //        O^T[d, q]  += V^T[d, key] . P^T[key, q]     (A = V^T rows, B = P^T)
-//     With K cached as [blocks, nkv, bs, D] and V cached *transposed* as [blocks, nkv, D, bs], every
+//     With K cached as [blocks, nkv, bs, D] and V cached as V^T in 8-key groups
+//     [blocks, nkv, bs/8, D, 8] (16 lanes with consecutive d read 256 contiguous bytes), every
 //     MFMA A operand is one 16-byte global load per lane, and the S^T accumulator is re-used as the
 //     P^T operand with no lane movement: the K rows of the two 16-key S tiles of a 32-key step are
 //     permuted (row i of tile t holds key 8(i>>2) + 4t + (i&3)) so that lane (h=l>>4, col=l&15)
@@ -81,7 +82,7 @@ __device__ __forceinline__ void attn_step(WaveState<D>& st, const bf16x8 (&qf)[D
   bf16x8 vf[D / 16];
 #pragma unroll
   for (int e = 0; e < D / 16; ++e)
-    vf[e] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)(16 * e + col) * bs + offk + 8 * h4);
+    vf[e] = *reinterpret_cast<const bf16x8*>(vbase + ((size_t)((offk >> 3) + h4) * D + 16 * e + col) * 8);
   // ---- S^T = K . Q^T ----
   f32x4 s[2];
 #pragma unroll

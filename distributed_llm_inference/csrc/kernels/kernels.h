@@ -8,7 +8,7 @@ struct AttnParams {
   const bf16* q;        // [T, nh, D]
   const bf16* q_sink;   // [T, nh, D] or nullptr (window mode only)
   const bf16* k_cache;  // [blocks, nkv, bs, D]
-  const bf16* v_cache;  // [blocks, nkv, D, bs]
+  const bf16* v_cache;  // [blocks, nkv, bs/8, D, 8]  (V^T in 8-key groups)
   bf16* out;            // [T, nh, D]
   const int* block_tables;  // [B, bt_stride]
   int bt_stride;
@@ -33,7 +33,7 @@ struct RopeCacheParams {
   bf16* q_sink_out;       // [T, nh, D] or nullptr
   int window;             // > 0: q_sink rotated at min(pos, window-1)
   bf16* k_cache;          // [blocks, nkv, bs, D]
-  bf16* v_cache;          // [blocks, nkv, D, bs]
+  bf16* v_cache;          // [blocks, nkv, bs/8, D, 8]
   int nh, nkv, D, bs;
 };
 
@@ -66,8 +66,10 @@ int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_
 int launch_sample(const SampleParams& p, int B, hipStream_t stream);
 int launch_gemm_nt(bf16* C, const bf16* A, const bf16* B, float* workspace, int M, int N, int K,
                    int splits, int bn, hipStream_t stream);
-int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, bf16* residual,
-                         const bf16* norm_w, float eps, int rows, int K, bool add_residual,
+int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
+                         bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,
                          hipStream_t stream);
+int launch_silu_mul_quant(uint8_t* q, float* scale, const bf16* x, int rows, int inter,
+                          hipStream_t stream);
 
 }  // namespace dli

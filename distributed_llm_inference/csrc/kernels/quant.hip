@@ -18,19 +18,52 @@ __device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d
   return (unsigned)r;
 }
 
+// Row amax -> scale, then quantise the VPT x 8 register-resident values of each thread (vector
+// index threadIdx.x + i * blockDim.x) and store them as 8-byte fp8 groups.
+template <int VPT>
+__device__ __forceinline__ void store_fp8_row(float (&v)[VPT][8], uint8_t* __restrict__ qrow,
+                                              float* __restrict__ srow, int nvec, float* scratch) {
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[i][j]));
+  amax = block_reduce_max(amax, scratch);
+  const float s = amax > 0.f ? amax / kFp8Max : 1.f;
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) *srow = s;
+  uint2* qr = reinterpret_cast<uint2*>(qrow);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * blockDim.x;
+    if (idx < nvec) {
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = fminf(fmaxf(v[i][j] * inv, -kFp8Max), kFp8Max);
+      uint2 o;
+      o.x = pack4_fp8(t[0], t[1], t[2], t[3]);
+      o.y = pack4_fp8(t[4], t[5], t[6], t[7]);
+      qr[idx] = o;
+    }
+  }
+}
+
 // x [rows, K] bf16 -> q [rows, K] fp8, scale [rows] f32 (x ~= q * scale).
-// If `norm_w` is given the row is first RMS-normalised (with optional residual add, like
-// rms_norm_kernel) and `norm_out` (optional) receives the bf16 normalised row.
+// If `residual_in` is given, x + residual_in is quantised and also written to `residual_out`
+// (which may alias residual_in; like rms_norm_kernel).  If `norm_w` is given the row is
+// RMS-normalised first, so "add residual -> RMSNorm -> fp8" is one HBM pass.
 template <int VPT>
 __global__ void __launch_bounds__(256) quant_rowwise_kernel(
     uint8_t* __restrict__ q, float* __restrict__ scale, const bf16* __restrict__ x,
-    bf16* __restrict__ residual, const bf16* __restrict__ norm_w, float eps, int K,
-    int add_residual) {
+    const bf16* residual_in, bf16* residual_out, const bf16* __restrict__ norm_w, float eps,
+    int K) {
   __shared__ float scratch[8];
   const int row = blockIdx.x;
   const int nvec = K >> 3;
+  const bool add_residual = residual_in != nullptr;
   const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * K);
-  bf16x8* rr = reinterpret_cast<bf16x8*>(residual + (size_t)row * K);
+  const bf16x8* ri = reinterpret_cast<const bf16x8*>(residual_in + (size_t)row * K);
+  bf16x8* ro = reinterpret_cast<bf16x8*>(residual_out + (size_t)row * K);
   float v[VPT][8];
   float ss = 0.f;
 #pragma unroll
@@ -39,10 +72,10 @@ __global__ void __launch_bounds__(256) quant_rowwise_kernel(
     if (idx < nvec) {
       bf16x8 a = xr[idx];
       if (add_residual) {
-        bf16x8 r = rr[idx];
+        bf16x8 r = ri[idx];
 #pragma unroll
         for (int j = 0; j < 8; ++j) a[j] = (bf16)((float)a[j] + (float)r[j]);
-        rr[idx] = a;
+        ro[idx] = a;
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -68,47 +101,76 @@ __global__ void __launch_bounds__(256) quant_rowwise_kernel(
       }
     }
   }
-  float amax = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[i][j]));
-  amax = block_reduce_max(amax, scratch);
-  const float s = amax > 0.f ? amax / kFp8Max : 1.f;
-  const float inv = 1.f / s;
-  if (threadIdx.x == 0) scale[row] = s;
-  uint2* qr = reinterpret_cast<uint2*>(q + (size_t)row * K);
+  store_fp8_row<VPT>(v, q + (size_t)row * K, scale + row, nvec, scratch);
+}
+
+// out = silu(x[:, :I]) * x[:, I:] quantised per row: [rows, 2I] bf16 -> [rows, I] fp8 + scale.
+// The activation is rounded to bf16 before quantisation, exactly as silu_mul_kernel would store
+// it, so the fp8 path differs from the bf16 path only by the quantisation step.
+template <int VPT>
+__global__ void __launch_bounds__(512) silu_mul_quant_kernel(uint8_t* __restrict__ q,
+                                                             float* __restrict__ scale,
+                                                             const bf16* __restrict__ x, int I) {
+  __shared__ float scratch[8];
+  const int row = blockIdx.x;
+  const int nvec = I >> 3;
+  const bf16x8* g = reinterpret_cast<const bf16x8*>(x + (size_t)row * 2 * I);
+  const bf16x8* u = reinterpret_cast<const bf16x8*>(x + (size_t)row * 2 * I + I);
+  float v[VPT][8];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * blockDim.x;
     if (idx < nvec) {
-      float t[8];
+      const bf16x8 a = g[idx], b = u[idx];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) t[j] = fminf(fmaxf(v[i][j] * inv, -kFp8Max), kFp8Max);
-      uint2 o;
-      o.x = pack4_fp8(t[0], t[1], t[2], t[3]);
-      o.y = pack4_fp8(t[4], t[5], t[6], t[7]);
-      qr[idx] = o;
+      for (int j = 0; j < 8; ++j) v[i][j] = (float)(bf16)(silu((float)a[j]) * (float)b[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
     }
   }
+  store_fp8_row<VPT>(v, q + (size_t)row * I, scale + row, nvec, scratch);
 }
 
-int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, bf16* residual,
-                         const bf16* norm_w, float eps, int rows, int K, bool add_residual,
+int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
+                         bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,
                          hipStream_t stream) {
   if (K % 8 != 0) return -1;
+  if (residual_in != nullptr && residual_out == nullptr) return -2;
   if (rows == 0) return 0;
   const int nvec = K / 8;
   int threads = ((nvec + 63) / 64) * 64;
   if (threads > 256) threads = 256;
   const int vpt = (nvec + threads - 1) / threads;
-  const int ar = add_residual ? 1 : 0;
-  if (vpt <= 1) quant_rowwise_kernel<1><<<rows, threads, 0, stream>>>(q, scale, x, residual, norm_w, eps, K, ar);
-  else if (vpt <= 2) quant_rowwise_kernel<2><<<rows, threads, 0, stream>>>(q, scale, x, residual, norm_w, eps, K, ar);
-  else if (vpt <= 4) quant_rowwise_kernel<4><<<rows, threads, 0, stream>>>(q, scale, x, residual, norm_w, eps, K, ar);
-  else if (vpt <= 8) quant_rowwise_kernel<8><<<rows, threads, 0, stream>>>(q, scale, x, residual, norm_w, eps, K, ar);
-  else if (vpt <= 16) quant_rowwise_kernel<16><<<rows, threads, 0, stream>>>(q, scale, x, residual, norm_w, eps, K, ar);
+#define DLI_QUANT(V) \
+  quant_rowwise_kernel<V><<<rows, threads, 0, stream>>>(q, scale, x, residual_in, residual_out, \
+                                                        norm_w, eps, K)
+  if (vpt <= 1) DLI_QUANT(1);
+  else if (vpt <= 2) DLI_QUANT(2);
+  else if (vpt <= 4) DLI_QUANT(4);
+  else if (vpt <= 8) DLI_QUANT(8);
+  else if (vpt <= 16) DLI_QUANT(16);
   else return -1;
+#undef DLI_QUANT
+  return 0;
+}
+
+int launch_silu_mul_quant(uint8_t* q, float* scale, const bf16* x, int rows, int inter,
+                          hipStream_t stream) {
+  if (inter % 8 != 0) return -1;
+  if (rows == 0) return 0;
+  const int nvec = inter / 8;
+  int threads = ((nvec + 63) / 64) * 64;
+  if (threads > 512) threads = 512;
+  const int vpt = (nvec + threads - 1) / threads;
+#define DLI_SMQ(V) silu_mul_quant_kernel<V><<<rows, threads, 0, stream>>>(q, scale, x, inter)
+  if (vpt <= 1) DLI_SMQ(1);
+  else if (vpt <= 2) DLI_SMQ(2);
+  else if (vpt <= 4) DLI_SMQ(4);
+  else if (vpt <= 8) DLI_SMQ(8);
+  else if (vpt <= 16) DLI_SMQ(16);
+  else return -1;
+#undef DLI_SMQ
   return 0;
 }
 

@@ -11,8 +11,9 @@
 //     reference's key re-rotation (cache.py:21-48, 111-124) expressed on the query side, so no
 //     cached key is ever re-rotated;
 //   * rotates k and scatters it into the paged K cache [blocks, nkv, bs, D];
-//   * scatters v into the paged, *transposed* V cache [blocks, nkv, D, bs] — the layout the MFMA
-//     P·V product wants as a 16-byte-per-lane operand (see attention.hip).
+//   * scatters v into the paged V^T cache [blocks, nkv, bs/8, D, 8] (8-key groups) — the MFMA
+//     P·V product reads 8 consecutive keys of one d as a 16-byte-per-lane operand (attention.hip),
+//     and one token's write stays inside 16 cache lines per head instead of D (one per d row).
 // slot_mapping[t] = physical slot (block*bs + offset) or -1 to skip the cache write.
 #include "kernels.h"
 
@@ -31,8 +32,14 @@ __device__ __forceinline__ void rotate4(const bf16x4& a, const bf16x4& b, const 
   }
 }
 
-__global__ void __launch_bounds__(256) rope_cache_kernel(RopeCacheParams p) {
+// grid (T, ceil(total_heads / kHeadsPerWG)): one workgroup per (token, group of 8 heads) so a
+// decode step of B tokens launches B * 10 workgroups (70B) instead of B — the kernel is
+// latency-bound, not bandwidth-bound, at one workgroup per token.
+constexpr int kHeadsPerWG = 8;
+
+__global__ void __launch_bounds__(128) rope_cache_kernel(RopeCacheParams p) {
   const int t = blockIdx.x;
+  const int h_lo = blockIdx.y * kHeadsPerWG;
   const int D = p.D, half = D >> 1;
   const int gpr = half >> 2;  // 4-element groups per rotation half
   const bf16* row = p.qkv + (size_t)t * p.qkv_stride;
@@ -52,9 +59,13 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(RopeCacheParams p) {
   const long blk = slot >= 0 ? slot / p.bs : 0;
   const int off = slot >= 0 ? (int)(slot % p.bs) : 0;
 
+  // heads of this workgroup: [h_lo, h_hi) over the concatenated q | k | v head list
+  const int n_qk = p.nh + p.nkv;
+  const int h_hi = min(h_lo + kHeadsPerWG, n_qk + p.nkv);
+
   // ---- q and k heads (rotation) -------------------------------------------------------------
-  const int n_rot_items = (p.nh + p.nkv) * gpr;
-  for (int it = threadIdx.x; it < n_rot_items; it += blockDim.x) {
+  const int rot_lo = h_lo * gpr, rot_hi = min(h_hi, n_qk) * gpr;
+  for (int it = rot_lo + threadIdx.x; it < rot_hi; it += blockDim.x) {
     const int head = it / gpr;
     const int i = (it % gpr) * 4;
     const bf16* src = row + (size_t)head * D;
@@ -80,18 +91,20 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(RopeCacheParams p) {
       *reinterpret_cast<bf16x4*>(dst + half + i) = ob;
     }
   }
-  // ---- v heads (transposed scatter) ---------------------------------------------------------
-  if (slot >= 0) {
+  // ---- v heads (V^T scatter) ---------------------------------------------------------
+  if (slot >= 0 && h_hi > n_qk) {
     const int vpr = D >> 3;
-    const int n_v_items = p.nkv * vpr;
-    const bf16* vsrc = row + (size_t)(p.nh + p.nkv) * D;
-    for (int it = threadIdx.x; it < n_v_items; it += blockDim.x) {
+    const int v_lo = max(h_lo - n_qk, 0) * vpr, v_hi = (h_hi - n_qk) * vpr;
+    const bf16* vsrc = row + (size_t)n_qk * D;
+    for (int it = v_lo + threadIdx.x; it < v_hi; it += blockDim.x) {
       const int kh = it / vpr;
       const int d0 = (it % vpr) * 8;
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(vsrc + (size_t)kh * D + d0);
-      bf16* dst = p.v_cache + (((size_t)blk * p.nkv + kh) * D + d0) * p.bs + off;
+      // [bs/8, D, 8] layout: the 8 values land 16 B apart inside one 128-B line
+      bf16* dst = p.v_cache + ((((size_t)blk * p.nkv + kh) * (p.bs >> 3) + (off >> 3)) * D + d0) * 8 +
+                  (off & 7);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dst[(size_t)j * p.bs] = v[j];
+      for (int j = 0; j < 8; ++j) dst[j * 8] = v[j];
     }
   }
 }
@@ -99,7 +112,9 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(RopeCacheParams p) {
 int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stream) {
   if (num_tokens == 0) return 0;
   if (p.D % 8 != 0 || p.qkv_stride % 4 != 0) return -1;
-  rope_cache_kernel<<<num_tokens, 256, 0, stream>>>(p);
+  const int heads = p.nh + 2 * p.nkv;
+  dim3 grid(num_tokens, (heads + kHeadsPerWG - 1) / kHeadsPerWG);
+  rope_cache_kernel<<<grid, 128, 0, stream>>>(p);
   return 0;
 }
 

@@ -47,8 +47,10 @@ class Linear(nn.Module):
             self.weight = nn.Parameter(torch.empty(0, dtype=self.weight.dtype,
                                                    device=self.weight.device), requires_grad=False)
 
-    def forward(self, x: torch.Tensor,
+    def forward(self, x: Optional[torch.Tensor],
                 x_q: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+        """``x_q`` = (fp8 rows, scales) already quantised by a fused producer kernel; then ``x`` may
+        be None (fp8 weights only)."""
         if self.weight_fp8 is None:
             return F.linear(x, self.weight, self.bias)
         if x_q is None:

@@ -7,7 +7,7 @@ layer) and re-rotated on eviction.
 
 MI355X design:
 * :class:`KVPool` allocates ONE K tensor ``[L, blocks, nkv, bs, D]`` and ONE transposed V tensor
-  ``[L, blocks, nkv, D, bs]`` per stage, sized from free HBM (288 GB per MI355X: for Llama-3-70B
+  ``[L, blocks, nkv, bs/8, D, 8]`` per stage, sized from free HBM (288 GB per MI355X: for Llama-3-70B
   PP=8 that is millions of cached tokens per stage).  Blocks are handed out by the native
   :class:`BlockManager` (csrc/runtime/block_manager.cpp).
 * :class:`PartialLlamaSinkCache` keeps the reference's public surface — construction from
@@ -49,7 +49,8 @@ class KVPool:
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         nkv, D = spec.num_kv_heads, spec.head_dim
         self.k = torch.zeros(num_layers, num_blocks, nkv, block_size, D, dtype=dtype, device=self.device)
-        self.v = torch.zeros(num_layers, num_blocks, nkv, D, block_size, dtype=dtype, device=self.device)
+        self.v = torch.zeros(num_layers, num_blocks, nkv, block_size // 8, D, 8, dtype=dtype,
+                             device=self.device)
         self.manager = _runtime().BlockManager(num_blocks, block_size, window_length,
                                                num_sink_tokens, max_chunk)
 
@@ -221,12 +222,12 @@ class PartialLlamaSinkCache:
             slots = torch.tensor([m.slot_of(sid, a) for a in range(L - T, L)], dtype=torch.long)
             blk, off = (slots // bs).to(kc.device), (slots % bs).to(kc.device)
             kc[blk, :, off, :] = key_states[b].transpose(0, 1).to(kc.dtype)
-            vc[blk, :, :, off] = value_states[b].transpose(0, 1).to(vc.dtype)
+            vc[blk, :, off // 8, :, off % 8] = value_states[b].transpose(0, 1).to(vc.dtype)
             nslots = m.slots_for(L)
             bt = torch.tensor(m.block_table(sid), dtype=torch.long, device=kc.device)
             nb = (nslots + bs - 1) // bs
             K = kc[bt[:nb]].permute(1, 0, 2, 3).reshape(nkv, nb * bs, D)[:, :nslots]
-            V = vc[bt[:nb]].permute(1, 0, 3, 2).reshape(nkv, nb * bs, D)[:, :nslots]
+            V = vc[bt[:nb]].permute(1, 0, 2, 4, 3).reshape(nkv, nb * bs, D)[:, :nslots]
             if self.window_length > 0 and L > self.num_sink_tokens:
                 keep = list(range(min(L, self.num_sink_tokens)))
                 sink_pad = m.sink_pad

@@ -53,10 +53,10 @@ class LlamaAttention(nn.Module):
         self.o_proj = Linear(spec.q_size, spec.hidden_size, bias=spec.attention_bias, dtype=dtype,
                              device=device)
 
-    def forward(self, normed: torch.Tensor, meta: AttnMetadata, k_cache: torch.Tensor,
-                v_cache: torch.Tensor, cos_sin: torch.Tensor) -> torch.Tensor:
-        T = normed.shape[0]
-        qkv = self.qkv_proj(normed)
+    def forward(self, normed: Optional[torch.Tensor], meta: AttnMetadata, k_cache: torch.Tensor,
+                v_cache: torch.Tensor, cos_sin: torch.Tensor, x_q=None) -> torch.Tensor:
+        qkv = self.qkv_proj(normed, x_q)
+        T = qkv.shape[0]
         q, q_sink = ops.rope_cache(qkv, meta.positions, meta.slot_mapping, cos_sin, self.num_heads,
                                    self.num_kv_heads, self.head_dim, k_cache, v_cache,
                                    window=meta.window, want_sink=meta.want_sink)
@@ -68,7 +68,8 @@ class LlamaAttention(nn.Module):
             o = ops.attn_prefill(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
                                  meta.q_start, meta.max_q, self.scale, meta.n_sink, meta.sink_pad,
                                  meta.ring, meta.window)
-        return self.o_proj(o.view(T, self.num_heads * self.head_dim))
+        o = o.view(T, self.num_heads * self.head_dim)
+        return self.o_proj(o)
 
 
 class LlamaMLP(nn.Module):
@@ -82,8 +83,11 @@ class LlamaMLP(nn.Module):
         self.down_proj = Linear(spec.intermediate_size, spec.hidden_size, bias=spec.mlp_bias,
                                 dtype=dtype, device=device)
 
-    def forward(self, normed: torch.Tensor) -> torch.Tensor:
-        return self.down_proj(ops.silu_mul(self.gate_up_proj(normed)))
+    def forward(self, normed: Optional[torch.Tensor], x_q=None) -> torch.Tensor:
+        gu = self.gate_up_proj(normed, x_q)
+        if self.down_proj.is_fp8:  # SwiGLU fused with the fp8 quantisation of down_proj's input
+            return self.down_proj(None, ops.silu_mul_quant(gu))
+        return self.down_proj(ops.silu_mul(gu))
 
 
 class LlamaDecoderLayer(nn.Module):
@@ -101,6 +105,8 @@ class LlamaDecoderLayer(nn.Module):
     def forward(self, hidden: torch.Tensor, residual: Optional[torch.Tensor], meta: AttnMetadata,
                 k_cache: torch.Tensor, v_cache: torch.Tensor,
                 cos_sin: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self.self_attn.qkv_proj.is_fp8:
+            return self._forward_fp8(hidden, residual, meta, k_cache, v_cache, cos_sin)
         first = residual is None
         if first:
             # first layer of the stage: the input IS the residual; never modify it in place (it
@@ -113,6 +119,21 @@ class LlamaDecoderLayer(nn.Module):
         normed, residual = self.post_attention_layernorm(
             attn, residual, residual_out=torch.empty_like(residual) if first else None)
         return self.mlp(normed), residual
+
+    def _forward_fp8(self, hidden, residual, meta, k_cache, v_cache, cos_sin):
+        """fp8 weights: every RMSNorm is fused with the fp8 quantisation of the GEMM input that
+        follows it (quant.hip), so the bf16 normalised activation never touches HBM."""
+        ln1, ln2 = self.input_layernorm, self.post_attention_layernorm
+        first = residual is None
+        if first:  # input is the residual; never modify it in place (graph static input)
+            residual = hidden
+            xq = ops.quant_rowwise(hidden, norm_w=ln1.weight, eps=ln1.eps)
+        else:
+            xq = ops.quant_rowwise(hidden, residual, ln1.weight, ln1.eps)
+        attn = self.self_attn(None, meta, k_cache, v_cache, cos_sin, x_q=xq)
+        res_out = torch.empty_like(residual) if first else residual
+        xq = ops.quant_rowwise(attn, residual, ln2.weight, ln2.eps, residual_out=res_out)
+        return self.mlp(None, x_q=xq), res_out
 
     # ------------------------------------------------------------------ weights
     def load_hf_state_dict(self, sd: dict) -> None:

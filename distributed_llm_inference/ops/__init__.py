@@ -198,21 +198,45 @@ FP8_MAX = 448.0
 
 
 def quant_rowwise(x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                  norm_w: Optional[torch.Tensor] = None, eps: float = 0.0):
-    """Per-row dynamic fp8-e4m3 quantisation (optionally fused residual-add + RMSNorm first)."""
+                  norm_w: Optional[torch.Tensor] = None, eps: float = 0.0,
+                  residual_out: Optional[torch.Tensor] = None):
+    """Per-row dynamic fp8-e4m3 quantisation, optionally of ``RMSNorm(x + residual)``.
+
+    With ``residual`` the sum ``x + residual`` is written back to ``residual_out`` (default: in
+    place into ``residual``) exactly like :func:`rms_norm`.  Returns ``(q, scale[rows, 1])``."""
     K = x.shape[-1]
     rows = x.numel() // K
     if not _gpu(x):
+        if residual is not None:
+            s = (x.float() + residual.float()).to(x.dtype)
+            (residual if residual_out is None else residual_out).copy_(s)
+            x = s
         if norm_w is not None:
-            x, _ = ref.rms_norm(x, norm_w, eps, residual)
-        xf = x.float().reshape(rows, K)
-        s = (xf.abs().amax(-1).clamp_min(1e-12) / FP8_MAX)
-        q = (xf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
-        return q.reshape(x.shape), s.reshape(rows, 1)
+            x, _ = ref.rms_norm(x, norm_w, eps)
+        return _quant_ref(x.reshape(rows, K), x.shape)
     q = torch.empty(x.shape, dtype=FP8, device=x.device)
     s = torch.empty(rows, 1, dtype=torch.float32, device=x.device)
-    native().quant_rowwise(q, s, x, residual, norm_w, float(eps))
+    native().quant_rowwise(q, s, x, residual, norm_w, float(eps), residual_out)
     return q, s
+
+
+def silu_mul_quant(x: torch.Tensor):
+    """``silu(x[:, :I]) * x[:, I:]`` quantised per row to fp8: returns ``(q [T, I], scale [T, 1])``."""
+    T, I = x.shape[0], x.shape[1] // 2
+    if not _gpu(x):
+        return _quant_ref(silu_mul(x), (T, I))
+    q = torch.empty(T, I, dtype=FP8, device=x.device)
+    s = torch.empty(T, 1, dtype=torch.float32, device=x.device)
+    native().silu_mul_quant(q, s, x)
+    return q, s
+
+
+def _quant_ref(x2: torch.Tensor, shape):
+    xf = x2.float()
+    s = xf.abs().amax(-1).clamp_min(1e-12) / FP8_MAX
+    s = torch.where(xf.abs().amax(-1) > 0, s, torch.ones_like(s))
+    q = (xf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8)
+    return q.reshape(shape), s.reshape(-1, 1)
 
 
 def quantize_weight_fp8(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -6,7 +6,9 @@ They serve two purposes only:
 On a GPU tensor the HIP kernels are ALWAYS used (``ops/__init__.py`` never falls back silently).
 
 Cache layouts are identical to the kernels':
-  k_cache [num_blocks, nkv, block_size, D], v_cache [num_blocks, nkv, D, block_size] (transposed).
+  k_cache [num_blocks, nkv, block_size, D],
+  v_cache [num_blocks, nkv, block_size/8, D, 8] (V^T in 8-key groups: element (key, d) at
+  [key // 8, d, key % 8]).
 """
 from __future__ import annotations
 
@@ -91,7 +93,7 @@ def rope_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
         if ok.any():
             blk, off = sm[ok] // bs, sm[ok] % bs
             k_cache[blk, :, off, :] = kr[ok]
-            v_cache[blk, :, :, off] = v[ok]
+            v_cache[blk, :, off // 8, :, off % 8] = v[ok]
     return qr.contiguous(), (q_sink.contiguous() if q_sink is not None else None)
 
 
@@ -102,7 +104,7 @@ def _gather_seq(k_cache, v_cache, block_table, nslots):
     nb = (nslots + bs - 1) // bs
     blocks = block_table[:nb].long()
     K = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * bs, k_cache.shape[1], -1)[:nslots]
-    V = v_cache[blocks].permute(0, 3, 1, 2).reshape(nb * bs, v_cache.shape[1], -1)[:nslots]
+    V = v_cache[blocks].permute(0, 2, 4, 1, 3).reshape(nb * bs, v_cache.shape[1], -1)[:nslots]
     return K, V
 
 

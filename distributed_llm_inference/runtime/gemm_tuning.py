@@ -25,6 +25,7 @@ SHIPPED = os.path.join(PKG_DIR, "tuning", "tunableop_gfx950.csv")
 
 
 def _weights(stage) -> List[torch.Tensor]:
+    """One representative bf16 weight per distinct GEMM shape."""
     from ..models.common import Linear
     ws, seen = [], set()
     for m in stage.modules():
@@ -36,6 +37,19 @@ def _weights(stage) -> List[torch.Tensor]:
     if getattr(stage, "head", None) is not None and stage.head.proj is None and stage.embed is not None:
         ws.append(stage.embed.weight)  # tied LM head
     return ws
+
+
+def _fp8_linears(stage) -> list:
+    """One representative fp8 Linear per distinct weight shape (row-wise scaled GEMMs)."""
+    from ..models.common import Linear
+    out, seen = [], set()
+    for m in stage.modules():
+        if isinstance(m, Linear) and m.is_fp8:
+            key = tuple(m.weight_fp8.shape)
+            if key not in seen:
+                seen.add(key)
+                out.append(m)
+    return out
 
 
 def tune_decode_gemms(stage, batch_sizes: Iterable[int], results_file: Optional[str] = None,
@@ -64,6 +78,11 @@ def tune_decode_gemms(stage, batch_sizes: Iterable[int], results_file: Optional[
             for M in sorted(set(int(b) for b in batch_sizes)):
                 x = torch.randn(M, w.shape[1], dtype=w.dtype, device=w.device)
                 F.linear(x, w)
+        from .. import ops
+        for lin in _fp8_linears(stage):
+            for M in sorted(set(int(b) for b in batch_sizes)):
+                x = torch.randn(M, lin.in_features, dtype=torch.bfloat16, device=stage.device)
+                lin(None, x_q=ops.quant_rowwise(x))
     torch.cuda.synchronize()
     t.tuning_enable(False)  # keep using the results; never tune inside serving / capture
     log.info("TunableOp: decode GEMMs tuned for batch sizes %s", sorted(set(batch_sizes)))

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 kernel trace for the decode phase of bench.py.
+"""Summarise a rocprofv3 kernel trace (CSV or rocpd .db) for the decode phase of bench.py.
 
 Decode steps are delimited by the sampling kernel (one per micro-batch step); the last
 ``--steps`` decode steps are aggregated per kernel (short names), with per-step time, share,
@@ -26,7 +26,13 @@ def main():
     ap.add_argument("--steps", type=int, default=4, help="decode micro-batch steps to aggregate")
     ap.add_argument("--marker", default="sample_kernel")
     a = ap.parse_args()
-    rows = list(csv.DictReader(open(a.trace)))
+    if a.trace.endswith(".db"):  # rocprofv3 rocpd (SQLite) output
+        import sqlite3
+        con = sqlite3.connect(a.trace)
+        rows = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+                for n, s, e in con.execute("select name, start, end from kernels")]
+    else:
+        rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
     if len(marks) < a.steps + 1:

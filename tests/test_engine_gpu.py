@@ -119,6 +119,21 @@ def test_fp8_weights_close_to_bf16(gpu):
     assert rel < 0.1, rel
 
 
+def test_fp8_stage_gpu_matches_cpu(gpu):
+    """The fused fp8 path (norm->quant, silu->quant, hipBLASLt row-wise scaled GEMM) against the
+    CPU dequantised reference with identical fp8 weights."""
+    prompts = [list(range(1, 70)), [5, 6, 7]]
+    cpu = CausalLMStage(SPEC, 0, 4).init_random(3)
+    g = CausalLMStage(SPEC, 0, 4, device=gpu).init_random(3)
+    g.load_state_dict({k: v.to(gpu) for k, v in cpu.state_dict().items()})
+    cpu.quantize_fp8()
+    g.quantize_fp8()
+    a = _stage_logits(cpu, prompts, 0)[0]
+    b = _stage_logits(g, prompts, 0)[0]
+    rel = ((a - b).norm() / a.norm()).item()
+    assert rel < 0.05, rel
+
+
 def test_sampling_params_in_engine(gpu):
     p = SamplingParams(max_tokens=10, temperature=0.8, top_k=50, top_p=0.9, seed=1, ignore_eos=True)
     a = [s.output for s in _engine().generate(PROMPTS, p)]

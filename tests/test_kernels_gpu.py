@@ -57,7 +57,7 @@ def test_silu_mul_gelu_add(gpu):
 
 def _make_cache(nblocks, nkv, bs, D, dev):
     k = torch.randn(nblocks, nkv, bs, D, device=dev, dtype=BF)
-    v = torch.randn(nblocks, nkv, D, bs, device=dev, dtype=BF)
+    v = torch.randn(nblocks, nkv, bs // 8, D, 8, device=dev, dtype=BF)
     return k, v
 
 
@@ -223,6 +223,34 @@ def test_quant_rowwise(gpu):
     y, _ = ref.rms_norm(x.cpu(), w.cpu(), 1e-5, residual=r2.cpu())
     deq2 = (q2.float() * s2).cpu()
     assert (deq2 - y.float()).abs().max() / y.float().abs().max() < 0.07
+
+
+def test_quant_rowwise_residual_out_of_place(gpu):
+    x = torch.randn(9, 8192, device=gpu, dtype=BF)
+    r = torch.randn_like(x)
+    w = (1 + 0.1 * torch.randn(8192, device=gpu)).to(BF)
+    r0, ro = r.clone(), torch.empty_like(r)
+    q, s = ops.quant_rowwise(x, r, w, 1e-5, residual_out=ro)
+    assert torch.equal(r, r0)  # input residual untouched
+    _close(ro, x.float() + r0.float(), 1e-2, 1e-2, "residual_out")
+    # identical to the CPU reference path (same bf16 rounding before quantisation)
+    rc = r0.cpu().clone()
+    qc, sc = ops.quant_rowwise(x.cpu(), rc, w.cpu(), 1e-5)
+    torch.testing.assert_close(s.cpu(), sc, rtol=1e-2, atol=0)
+    deq, deqc = q.float().cpu() * s.cpu(), qc.float() * sc
+    assert (deq - deqc).abs().max() / deqc.abs().max() < 0.07
+
+
+@pytest.mark.parametrize("T,I", [(1, 512), (33, 3584), (256, 28672)])
+def test_silu_mul_quant(gpu, T, I):
+    x = torch.randn(T, 2 * I, device=gpu, dtype=BF) * 2
+    q, s = ops.silu_mul_quant(x)
+    assert q.shape == (T, I) and s.shape == (T, 1)
+    y = ref.silu_mul(x.cpu()).float()
+    sr = y.abs().amax(-1, keepdim=True) / 448.0
+    torch.testing.assert_close(s.cpu(), sr, rtol=1e-2, atol=1e-6)
+    deq = q.float().cpu() * s.cpu()
+    assert (deq - y).abs().max() / y.abs().max() < 0.07
 
 
 def test_rms_norm_residual_out_of_place(gpu):

@@ -121,6 +121,20 @@ def test_pipeline_split_equals_single_stage():
     assert torch.allclose(out, ref[0], atol=1e-2, rtol=1e-2)
 
 
+def test_fp8_stage_close_to_bf16_cpu():
+    """fp8-weight path (fused norm->quant and silu->quant producers) on the CPU reference ops."""
+    spec = ModelSpec(name="t", vocab_size=300, hidden_size=128, intermediate_size=256, num_layers=2,
+                     num_heads=4, num_kv_heads=2, head_dim=32, rope_theta=10000.0,
+                     max_position_embeddings=2048)
+    st = CausalLMStage(spec, 0, 2).init_random(11)
+    prompts = [[1, 2, 3, 4, 5], [9, 8]]
+    a = _run_stage(st, prompts, decode_steps=1)
+    st.quantize_fp8()
+    b = _run_stage(st, prompts, decode_steps=1)
+    for x, y in zip(a, b):
+        assert ((x - y).norm() / x.norm()).item() < 0.1
+
+
 def test_gpt2_matches_hf():
     from transformers import GPT2Config, GPT2LMHeadModel
     torch.manual_seed(0)
