@@ -109,10 +109,12 @@ def main():
     for s in seqs:
         s.token_times.clear()
     t0 = time.perf_counter()
+    w0 = drv.wait_s
     for _ in range(a.steps):
         drv.round()
     drv.barrier()
     t1 = time.perf_counter()
+    driver_busy = (t1 - t0) - (drv.wait_s - w0)
     n1 = sum(len(s.output) for s in seqs)
     elapsed = t1 - t0
     if world > 1:
@@ -122,6 +124,9 @@ def main():
         elapsed = float(t.item())
         dist.barrier()
     toks = n1 - n0
+    if toks != a.steps * G:
+        print(f"WARNING: {toks} tokens in the timed window, expected {a.steps * G} "
+              "(KV cache too small to run every sequence at once?)", file=sys.stderr, flush=True)
     lat = []
     for s in seqs:
         tt = s.token_times
@@ -152,7 +157,11 @@ def main():
         "prompt_len": a.prompt_len,
         "tokens_timed": toks,
         "prefill_s": round(prefill_s, 3),
+        # host time of the driver rank per micro-batch step NOT spent waiting for results
+        "driver_host_ms_per_mb_step": round(driver_busy / (a.steps * M) * 1e3, 3),
         "init_s": round(init_s, 1),
+        "kv_blocks": int(drv.sched.total_blocks),
+        "kv_blocks_needed": int(G * drv.sched.blocks_for(a.prompt_len + params.max_tokens)),
     }
     line = json.dumps(res)
     print(line, flush=True)

@@ -59,6 +59,7 @@ class DriverBase:
         self.inflight: Deque[StepPlan] = collections.deque()
         self.collect_times: Dict[int, List[float]] = collections.defaultdict(list)
         self.tokens_generated = 0
+        self.wait_s = 0.0  # host time blocked on results (the rest of a round is driver work)
 
     # -- to implement
     def _issue(self, plan: StepPlan) -> None:
@@ -73,8 +74,10 @@ class DriverBase:
     # -- loop
     def _collect_front(self) -> None:
         p = self.inflight.popleft()
+        t0 = time.perf_counter()
         toks = self._collect(p)
         now = time.perf_counter()
+        self.wait_s += now - t0
         self.collect_times[p.mb].append(now)
         self.tokens_generated += len(toks)
         self.sched.on_tokens(p.mb, toks, now)

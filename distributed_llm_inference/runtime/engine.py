@@ -70,13 +70,23 @@ def build_executor(spec: ModelSpec, start: int, end: int, device: torch.device, 
         num_blocks = cc.num_blocks
     if num_blocks is None:
         if device.type == "cuda":
+            # memory freed by load-time conversions (fp8 quantisation drops the bf16 weights) is
+            # still held by this process's caching allocator and would not count as free
             torch.cuda.synchronize(device)
+            torch.cuda.empty_cache()
+            if group is not None:
+                # ranks sharing a device (DLI_SHARE_GPU) must all hold their weights, and have
+                # released their caches, before any of them measures what is left for KV
+                dist.barrier(group=group)
             free, _ = torch.cuda.mem_get_info(device)
             num_blocks = KVPool.size_from_memory(spec, nlayers, cc.block_size, int(free * kv_share),
                                                  cc.gpu_memory_utilization,
                                                  _activation_reserve(spec, sc))
         else:
             num_blocks = 1024
+        if num_blocks < 2:
+            raise RuntimeError(f"stage [{start},{end}) on {device}: no HBM left for the KV cache "
+                               "(lower max_num_batched_tokens or use fp8 weights)")
     if group is not None:
         t = torch.tensor([num_blocks], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
@@ -140,11 +150,14 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", rank))
     spec = resolve_model(cfg.checkpoint or cfg.model)
+    kv_share = 1.0
     if torch.cuda.is_available():
         # DLI_SHARE_GPU=1: several stage processes on the visible GPUs round-robin (tests on a
         # single-GPU box); otherwise one GPU per local rank
         if os.environ.get("DLI_SHARE_GPU") == "1":
-            local = local % torch.cuda.device_count()
+            ndev = torch.cuda.device_count()
+            kv_share = 1.0 / ((world + ndev - 1) // ndev)
+            local = local % ndev
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
@@ -166,7 +179,7 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         if len(ranges) != world:
             raise ValueError("DLI_STAGE_RANGES must have one range per rank")
     start, end = ranges[rank]
-    ex = build_executor(spec, start, end, device, cfg, group=group)
+    ex = build_executor(spec, start, end, device, cfg, group=group, kv_share=kv_share)
     channels = _Channels(job, rank, world)
     transport = make_transport(rank, world, device)
     dist.barrier(group=group)
