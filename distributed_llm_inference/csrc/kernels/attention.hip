@@ -48,9 +48,7 @@ __device__ __forceinline__ int ring_abs(int u, int L, const AttnParams& p) {
   return (L - 1) - back;
 }
 
-// One 32-key step of online-softmax attention for the 16 query columns held by this wave.
-//   kbase/vbase: start of this kv head's page in the K / V^T cache, offk: slot offset of the step
-//   inside the page.  valid(j) decides visibility of key 8h+j (h = lane>>4) for this lane's column.
+// Online-softmax state of one wave: O^T accumulators, running max (log2 domain) and row sum.
 template <int D>
 struct WaveState {
   f32x4 o[D / 16];
@@ -63,33 +61,45 @@ struct WaveState {
   }
 };
 
+// K/V fragments of one 32-key step (registers): K rows permuted (see header), V^T rows.
 template <int D>
-__device__ __forceinline__ void attn_step(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
-                                          const bf16* __restrict__ kbase,
-                                          const bf16* __restrict__ vbase, int offk, int bs,
-                                          float scale_log2, unsigned valid_mask) {
+struct KVFrag {
+  bf16x8 k[2][D / 32];
+  bf16x8 v[D / 16];
+};
+
+//   kbase/vbase: start of this kv head's page in the K / V^T cache, offk: slot offset of the step
+//   inside the page.
+template <int D>
+__device__ __forceinline__ void attn_load(KVFrag<D>& f, const bf16* __restrict__ kbase,
+                                          const bf16* __restrict__ vbase, int offk) {
   const int lane = threadIdx.x & 63;
   const int col = lane & 15, h4 = lane >> 4;
-  // ---- issue all loads of the step (K rows permuted, V^T rows) ----
-  bf16x8 kf[2][D / 32];
   const int krow0 = offk + 8 * (col >> 2) + (col & 3);
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int c = 0; c < D / 32; ++c)
-      kf[t][c] = *reinterpret_cast<const bf16x8*>(kbase + (size_t)(krow0 + 4 * t) * D + 32 * c +
-                                                  8 * h4);
-  bf16x8 vf[D / 16];
+      f.k[t][c] = *reinterpret_cast<const bf16x8*>(kbase + (size_t)(krow0 + 4 * t) * D + 32 * c +
+                                                   8 * h4);
 #pragma unroll
   for (int e = 0; e < D / 16; ++e)
-    vf[e] = *reinterpret_cast<const bf16x8*>(vbase + ((size_t)((offk >> 3) + h4) * D + 16 * e + col) * 8);
+    f.v[e] = *reinterpret_cast<const bf16x8*>(vbase + ((size_t)((offk >> 3) + h4) * D + 16 * e + col) * 8);
+}
+
+// One 32-key step of online-softmax attention for the 16 query columns held by this wave.
+// valid_mask bit j decides visibility of key 8h+j (h = lane>>4) for this lane's column.
+template <int D>
+__device__ __forceinline__ void attn_compute(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
+                                             const KVFrag<D>& f, float scale_log2,
+                                             unsigned valid_mask) {
   // ---- S^T = K . Q^T ----
   f32x4 s[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < D / 32; ++c) s[t] = mfma16(kf[t][c], qf[c], s[t]);
+    for (int c = 0; c < D / 32; ++c) s[t] = mfma16(f.k[t][c], qf[c], s[t]);
   }
   // ---- online softmax over the 8 keys 8h..8h+7 of this lane ----
   float x[8];
@@ -118,44 +128,77 @@ __device__ __forceinline__ void attn_step(WaveState<D>& st, const bf16x8 (&qf)[D
 #pragma unroll
   for (int e = 0; e < D / 16; ++e) {
     st.o[e] *= alpha;
-    st.o[e] = mfma16(vf[e], pb, st.o[e]);
+    st.o[e] = mfma16(f.v[e], pb, st.o[e]);
   }
 }
 
+template <int D>
+__device__ __forceinline__ void attn_step(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
+                                          const bf16* __restrict__ kbase,
+                                          const bf16* __restrict__ vbase, int offk,
+                                          float scale_log2, unsigned valid_mask) {
+  KVFrag<D> f;
+  attn_load<D>(f, kbase, vbase, offk);
+  attn_compute<D>(st, qf, f, scale_log2, valid_mask);
+}
+
 // ===========================================================================================
-// Decode: grid (num_splits, nkv * head_groups, B), 256 threads.  The 4 waves split the keys of the
-// (sequence, kv-head, split) in interleaved 32-key steps and are merged through LDS at the end.
+// Decode: one wave per work item (sequence b, kv head, group of 16 q heads, split), 4 independent
+// waves per 256-thread workgroup (no LDS, no barriers).  A wave walks its split's 32-key steps with
+// the loads of step s+1 in flight while step s computes (two register fragment sets; the prefetch
+// index is clamped instead of branched so the loads stay straight-line and hipcc can wait with a
+// counted vmcnt).  With one split the wave writes the normalised output; otherwise unnormalised
+// partials (O, m, l) for attn_combine_kernel.
 // ===========================================================================================
 template <int D, bool WIN>
-__global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p) {
-  const int split = blockIdx.x;
-  const int b = blockIdx.z;
+__device__ __forceinline__ unsigned step_mask(int u0, int h4, int seg_base, int seg_len, int L,
+                                              const AttnParams& p) {
+  unsigned vm = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int u = u0 + 8 * h4 + j;
+    bool ok = (u - seg_base) < seg_len;
+    if (WIN && ok) {
+      const int a = ring_abs(u, L, p);
+      ok = a >= p.n_sink && (L - 1 - a) < (p.window - p.n_sink);
+    }
+    vm |= (ok ? 1u : 0u) << j;
+  }
+  return vm;
+}
+
+template <int D, bool WIN>
+__global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int items) {
+  // wave-uniform by construction; readfirstlane tells hipcc so, which turns every index derived
+  // from it (seq_lens, block-table entries) into scalar loads that never join the vmcnt queue
+  // of the K/V prefetch
+  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (item >= items) return;  // whole wave idle
+  const int splits = p.num_splits;
+  const int split = item % splits;
+  int rest = item / splits;
   const int G = p.nh / p.nkv;
   const int hgroups = (G + 15) >> 4;
-  const int kvh = blockIdx.y / hgroups;
-  const int g0 = (blockIdx.y % hgroups) * 16;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int g0 = (rest % hgroups) * 16;
+  rest /= hgroups;
+  const int kvh = rest % p.nkv;
+  const int b = rest / p.nkv;
+  const int lane = threadIdx.x & 63;
   const int col = lane & 15, h4 = lane >> 4;
   const bool col_valid = (g0 + col) < G;
   const int qh = kvh * G + g0 + (col_valid ? col : 0);
   const int L = p.seq_lens[b];
   const int* bt = p.block_tables + (size_t)b * p.bt_stride;
-
-  __shared__ float sm_o[4][D][16];
-  __shared__ float sm_m[4][16];
-  __shared__ float sm_l[4][16];
+  const size_t head_stride = (size_t)p.bs * D;  // per (block, kv head)
 
   WaveState<D> st;
   st.init();
-
   if (L > 0) {
     bf16x8 qf[D / 32];
     const bf16* qrow = p.q + ((size_t)b * p.nh + qh) * D;
 #pragma unroll
     for (int c = 0; c < D / 32; ++c)
       qf[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qrow + 32 * c + 8 * h4) : zero8();
-
-    const size_t head_stride_k = (size_t)p.bs * D;  // per (block, kv head)
     // ---- rolling / full segment ----
     int seg_base, seg_len;
     if (WIN) {
@@ -166,31 +209,34 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p) {
       seg_len = L;
     }
     const int nsteps = (seg_len + 31) >> 5;
-    const int per_split = (nsteps + p.num_splits - 1) / p.num_splits;
+    const int per_split = (nsteps + splits - 1) / splits;
     const int s_lo = split * per_split;
     const int s_hi = min(nsteps, s_lo + per_split);
-    const int pq = L - 1;
-    for (int sidx = s_lo + w; sidx < s_hi; sidx += 4) {
-      const int u0 = seg_base + sidx * 32;
-      const int page = bt[u0 / p.bs];
-      const int offk = u0 % p.bs;
-      const bf16* kbase = p.k_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
-      const bf16* vbase = p.v_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
-      unsigned vm = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int u = u0 + 8 * h4 + j;
-        bool ok = (u - seg_base) < seg_len;
-        if (WIN && ok) {
-          const int a = ring_abs(u, L, p);
-          ok = a >= p.n_sink && (pq - a) < (p.window - p.n_sink);
-        }
-        vm |= (ok ? 1u : 0u) << j;
+    if (s_lo < s_hi) {
+      auto load = [&](KVFrag<D>& f, int sidx) {
+        const int u0 = seg_base + sidx * 32;
+        const int page = bt[u0 / p.bs];
+        const size_t hb = ((size_t)page * p.nkv + kvh) * head_stride;
+        attn_load<D>(f, p.k_cache + hb, p.v_cache + hb, u0 % p.bs);
+      };
+      KVFrag<D> fa, fb;
+      load(fa, s_lo);
+      // sched_barrier(0): keep each prefetch group issued ahead of the previous step's MFMAs
+      // (the machine scheduler otherwise sinks the loads next to their first use)
+      for (int sidx = s_lo; sidx < s_hi; sidx += 2) {
+        load(fb, min(sidx + 1, s_hi - 1));
+        __builtin_amdgcn_sched_barrier(0);
+        attn_compute<D>(st, qf, fa, p.scale_log2,
+                        step_mask<D, WIN>(seg_base + sidx * 32, h4, seg_base, seg_len, L, p));
+        load(fa, min(sidx + 2, s_hi - 1));
+        __builtin_amdgcn_sched_barrier(0);
+        if (sidx + 1 < s_hi)
+          attn_compute<D>(st, qf, fb, p.scale_log2,
+                          step_mask<D, WIN>(seg_base + (sidx + 1) * 32, h4, seg_base, seg_len, L, p));
       }
-      attn_step<D>(st, qf, kbase, vbase, offk, p.bs, p.scale_log2, vm);
     }
-    // ---- sink segment (window mode): split 0, wave 0 ----
-    if (WIN && split == 0 && w == 0 && p.n_sink > 0) {
+    // ---- sink segment (window mode): scored with q_sink by the split-0 wave ----
+    if (WIN && split == 0 && p.n_sink > 0) {
       bf16x8 qs[D / 32];
       const bf16* qsrow = p.q_sink + ((size_t)b * p.nh + qh) * D;
 #pragma unroll
@@ -199,51 +245,39 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p) {
       const int nS = min(p.n_sink, L);
       for (int u0 = 0; u0 < nS; u0 += 32) {
         const int page = bt[u0 / p.bs];
-        const int offk = u0 % p.bs;
-        const bf16* kbase = p.k_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
-        const bf16* vbase = p.v_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
+        const size_t hb = ((size_t)page * p.nkv + kvh) * head_stride;
         unsigned vm = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) vm |= ((u0 + 8 * h4 + j) < nS ? 1u : 0u) << j;
-        attn_step<D>(st, qs, kbase, vbase, offk, p.bs, p.scale_log2, vm);
+        attn_step<D>(st, qs, p.k_cache + hb, p.v_cache + hb, u0 % p.bs, p.scale_log2, vm);
       }
     }
   }
-  // ---- merge the 4 waves through LDS ----
+  // ---- write: lane (col, h4) holds O^T rows d = 16e + 4h4 + r of query column col ----
   float lsum = st.l;
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
-  if (h4 == 0) {
-    sm_m[w][col] = st.m;
-    sm_l[w][col] = lsum;
-  }
+  if (!col_valid) return;
+  const int head = kvh * G + g0 + col;
+  if (splits == 1) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16* orow = p.out + ((size_t)b * p.nh + head) * D;
 #pragma unroll
-  for (int e = 0; e < D / 16; ++e)
+    for (int e = 0; e < D / 16; ++e) {
+      bf16x4 v;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sm_o[w][16 * e + 4 * h4 + r][col] = st.o[e][r];
-  __syncthreads();
-  for (int it = threadIdx.x; it < 16 * D; it += 256) {
-    const int c = it / D, d = it % D;  // consecutive threads -> consecutive d (coalesced out)
-    if (g0 + c >= G) continue;
-    const float M = fmaxf(fmaxf(sm_m[0][c], sm_m[1][c]), fmaxf(sm_m[2][c], sm_m[3][c]));
-    float O = 0.f, Lt = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
-      const float f = __builtin_amdgcn_exp2f(sm_m[ww][c] - M);
-      O += f * sm_o[ww][d][c];
-      Lt += f * sm_l[ww][c];
+      for (int r = 0; r < 4; ++r) v[r] = (bf16)(st.o[e][r] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 16 * e + 4 * h4) = v;
     }
-    const int head = kvh * G + g0 + c;
-    if (p.num_splits == 1) {
-      p.out[((size_t)b * p.nh + head) * D + d] = (bf16)(Lt > 0.f ? O / Lt : 0.f);
-    } else {
-      const size_t T = gridDim.z;
-      p.part_o[(((size_t)split * T + b) * p.nh + head) * D + d] = O;
-      if (d == 0) {
-        float* ml = p.part_ml + (((size_t)split * T + b) * p.nh + head) * 2;
-        ml[0] = M;
-        ml[1] = Lt;
-      }
+  } else {
+    const size_t T = (size_t)items / ((size_t)splits * hgroups * p.nkv);  // = B
+    const size_t r0 = ((size_t)split * T + b) * p.nh + head;
+    float* prow = p.part_o + r0 * D;
+#pragma unroll
+    for (int e = 0; e < D / 16; ++e) *reinterpret_cast<f32x4*>(prow + 16 * e + 4 * h4) = st.o[e];
+    if (h4 == 0) {
+      p.part_ml[r0 * 2] = st.m;
+      p.part_ml[r0 * 2 + 1] = lsum;
     }
   }
 }
@@ -276,7 +310,8 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p) {
   const int qh = blockIdx.y;
   const int G = p.nh / p.nkv;
   const int kvh = qh / G;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, h4 = lane >> 4;
   const int qs0 = p.q_start[b];
   const int qlen = p.q_start[b + 1] - qs0;
@@ -308,7 +343,7 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p) {
       unsigned vm = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) vm |= ((u0 + 8 * h4 + j) <= pq ? 1u : 0u) << j;
-      attn_step<D>(st, qf, kbase, vbase, offk, p.bs, p.scale_log2, vm);
+      attn_step<D>(st, qf, kbase, vbase, offk, p.scale_log2, vm);
     }
   } else {
     const int seg_len = L > p.n_sink ? min(p.ring, L - p.n_sink) : 0;
@@ -329,7 +364,7 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p) {
         }
         vm |= (ok ? 1u : 0u) << j;
       }
-      attn_step<D>(st, qf, kbase, vbase, offk, p.bs, p.scale_log2, vm);
+      attn_step<D>(st, qf, kbase, vbase, offk, p.scale_log2, vm);
     }
     if (p.n_sink > 0) {
       bf16x8 qsf[D / 32];
@@ -349,7 +384,7 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p) {
           const int u = u0 + 8 * h4 + j;
           vm |= (u < nS && u <= pq ? 1u : 0u) << j;
         }
-        attn_step<D>(st, qsf, kbase, vbase, offk, p.bs, p.scale_log2, vm);
+        attn_step<D>(st, qsf, kbase, vbase, offk, p.scale_log2, vm);
       }
     }
   }
@@ -374,11 +409,13 @@ template <int D>
 static int launch_decode_d(const AttnParams& p, int B, hipStream_t stream) {
   const int G = p.nh / p.nkv;
   const int hgroups = (G + 15) / 16;
-  dim3 grid(p.num_splits, p.nkv * hgroups, B);
+  const long items = (long)B * p.nkv * hgroups * p.num_splits;
+  if (items > (1L << 30)) return -3;
+  const int grid = (int)((items + 3) / 4);
   if (p.ring > 0)
-    attn_decode_kernel<D, true><<<grid, 256, 0, stream>>>(p);
+    attn_decode_kernel<D, true><<<grid, 256, 0, stream>>>(p, (int)items);
   else
-    attn_decode_kernel<D, false><<<grid, 256, 0, stream>>>(p);
+    attn_decode_kernel<D, false><<<grid, 256, 0, stream>>>(p, (int)items);
   if (p.num_splits > 1) attn_combine_kernel<D><<<B * p.nh, D, 0, stream>>>(p, B);
   return 0;
 }

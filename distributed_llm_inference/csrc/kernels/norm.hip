@@ -28,11 +28,13 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
   bf16x8* outr = reinterpret_cast<bf16x8*>(out + (size_t)row * hidden);
 
   float v[VPT][8];
+  bf16x8 wv[VPT];  // weights loaded with the row: no dependent L2 round trip after the reduction
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * blockDim.x;
     if (idx < nvec) {
+      wv[i] = wr[idx];
       bf16x8 a = xr[idx];
       if (add_residual) {
         bf16x8 r = ri[idx];
@@ -58,7 +60,7 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * blockDim.x;
     if (idx < nvec) {
-      bf16x8 ww = wr[idx];
+      const bf16x8 ww = wv[i];
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[i][j] * rstd * (float)ww[j]);
@@ -85,11 +87,14 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(bf16* __restrict__ out,
   const bf16x8* br = reinterpret_cast<const bf16x8*>(b);
   bf16x8* outr = reinterpret_cast<bf16x8*>(out + (size_t)row * hidden);
   float v[VPT][8];
+  bf16x8 wv[VPT], bv[VPT];
   float s1 = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * blockDim.x;
     if (idx < nvec) {
+      wv[i] = wr[idx];
+      bv[i] = br[idx];
       bf16x8 a = xr[idx];
       if (add_residual) {
         bf16x8 r = ri[idx];
@@ -127,7 +132,7 @@ __global__ void __launch_bounds__(256) layer_norm_kernel(bf16* __restrict__ out,
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * blockDim.x;
     if (idx < nvec) {
-      bf16x8 ww = wr[idx], bb = br[idx];
+      const bf16x8 ww = wv[i], bb = bv[i];
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j)

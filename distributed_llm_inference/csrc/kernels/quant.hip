@@ -65,11 +65,14 @@ __global__ void __launch_bounds__(256) quant_rowwise_kernel(
   const bf16x8* ri = reinterpret_cast<const bf16x8*>(residual_in + (size_t)row * K);
   bf16x8* ro = reinterpret_cast<bf16x8*>(residual_out + (size_t)row * K);
   float v[VPT][8];
+  bf16x8 wv[VPT];  // norm weights loaded with the row (no dependent load after the reduction)
+  const bf16x8* wr = reinterpret_cast<const bf16x8*>(norm_w);
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = threadIdx.x + i * blockDim.x;
     if (idx < nvec) {
+      if (norm_w) wv[i] = wr[idx];
       bf16x8 a = xr[idx];
       if (add_residual) {
         bf16x8 r = ri[idx];
@@ -90,12 +93,11 @@ __global__ void __launch_bounds__(256) quant_rowwise_kernel(
   if (norm_w) {
     ss = block_reduce_sum(ss, scratch);
     const float rstd = rsqrtf(ss / (float)K + eps);
-    const bf16x8* wr = reinterpret_cast<const bf16x8*>(norm_w);
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
       const int idx = threadIdx.x + i * blockDim.x;
       if (idx < nvec) {
-        bf16x8 ww = wr[idx];
+        const bf16x8 ww = wv[i];
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[i][j] = (float)(bf16)(v[i][j] * rstd * (float)ww[j]);
       }

@@ -134,13 +134,15 @@ def rope_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
 
 # ----------------------------------------------------------------------------- attention
 def decode_splits(batch: int, nkv: int, group: int, max_len: int, cu: int = 256) -> int:
-    """Split-K factor for decode so that the grid has >= ~2 workgroups per CU."""
-    wgs = batch * nkv * ((group + 15) // 16)
-    if wgs >= 2 * cu:
+    """Split-K factor for decode.  The kernel runs one wave per (sequence, kv head, 16-head group,
+    split); aim for ~2 waves per SIMD (8 per CU) while keeping >= 4 key steps per split."""
+    waves = batch * nkv * ((group + 15) // 16)
+    target = 8 * cu
+    if waves >= target:
         return 1
-    want = (2 * cu + wgs - 1) // wgs
-    max_useful = max(1, (max_len + 255) // 256)  # >= 256 keys per split
-    return int(max(1, min(want, max_useful, 32)))
+    want = (target + waves - 1) // waves
+    max_useful = max(1, max_len // 128)
+    return int(max(1, min(want, max_useful, 64)))
 
 
 def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink=0, sink_pad=0,
