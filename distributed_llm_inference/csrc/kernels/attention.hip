@@ -301,92 +301,165 @@ __global__ void __launch_bounds__(128) attn_combine_kernel(AttnParams p, int T) 
 }
 
 // ===========================================================================================
-// Prefill (varlen, chunked): grid (ceil(max_q/64), nh, B), 256 threads.  Wave w owns 16
-// consecutive query tokens of one q head; keys are visited causally up to the wave's last token.
+// Prefill (varlen, chunked) with LDS-staged K/V tiles.
+//
+// Workgroup = 4 waves = HPW q heads (of ONE kv head) x TPW tiles of 16 query tokens, HPW*TPW = 4
+// (HPW = 4 when the GQA group allows it: the 4 waves then share every K/V tile).  Grid
+// (ceil(max_q / (16 TPW)), nkv * G / HPW, B).  Per 32-key step the workgroup copies the K tile
+// (32 rows x D, contiguous in the page) and the V^T tile (4 groups x D x 8, contiguous) into one of
+// two LDS buffers (register-staged: the global loads of step s+1 are issued before the MFMAs of
+// step s and written after them; one barrier per step).  Waves read their MFMA fragments from LDS:
+//   * K rows are stored with the 16-B chunk c of row r at c ^ kswz(r), kswz(r) = (r & 3) |
+//     ((r >> 3) & 3) << 2 (masked to the row's chunk count): the permuted-row A-fragment reads
+//     (rows 8(i>>2) + 4t + (i&3), chunk 4c + h) then hit 16 distinct 16-B bank slots in every
+//     ds_read_b128 lane group (derivation in docs/kernels.md);
+//   * V^T units (group h, d) are read by 16 lanes with consecutive d: conflict-free unswizzled.
+// Causality / windows / sinks use the same masks as decode; waves whose tokens are past the end of
+// the chunk still join every barrier and only skip their store.
 // ===========================================================================================
+template <int D>
+__device__ __forceinline__ int kswz(int row) {
+  constexpr int CH = D / 8;  // 16-B chunks per K row
+  return ((row & 3) | (((row >> 3) & 3) << 2)) & (CH - 1);
+}
+
 template <int D, bool WIN>
-__global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p) {
+__global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw) {
+  constexpr int CH = D / 8;            // 16-B units per K row
+  constexpr int UNITS = 32 * CH;       // 16-B units per K tile (= per V^T tile)
+  constexpr int UPT = (UNITS + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2][2][32 * D];  // [buf][K | V][...]
+
   const int b = blockIdx.z;
-  const int qh = blockIdx.y;
   const int G = p.nh / p.nkv;
-  const int kvh = qh / G;
+  const int tpw = 4 / hpw;
+  const int wgs_per_kv = G / hpw;
+  const int kvh = blockIdx.y / wgs_per_kv;
+  const int h0 = kvh * G + (blockIdx.y % wgs_per_kv) * hpw;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, h4 = lane >> 4;
+  const int qh = h0 + (w % hpw);
   const int qs0 = p.q_start[b];
   const int qlen = p.q_start[b + 1] - qs0;
-  const int tok0 = blockIdx.x * 64 + w * 16;
-  if (tok0 >= qlen) return;  // whole wave idle (no LDS / barriers in this kernel)
+  const int wg_tok0 = blockIdx.x * 16 * tpw;
+  if (wg_tok0 >= qlen) return;  // whole workgroup idle (uniform: before any barrier)
+  const int tok0 = wg_tok0 + (w / hpw) * 16;
   const int L = p.seq_lens[b];
   const int tok = tok0 + col;
   const bool col_valid = tok < qlen;
   const int pq = L - qlen + (col_valid ? tok : qlen - 1);  // this column's absolute position
-  const int pq_max = L - qlen + min(qlen - 1, tok0 + 15);
+  const int pq_max = L - qlen + min(qlen - 1, wg_tok0 + 16 * tpw - 1);  // workgroup's last token
   const int* bt = p.block_tables + (size_t)b * p.bt_stride;
-  const size_t head_stride_k = (size_t)p.bs * D;
+  const size_t head_stride = (size_t)p.bs * D;
 
-  bf16x8 qf[D / 32];
-  const bf16* qrow = p.q + ((size_t)(qs0 + (col_valid ? tok : 0)) * p.nh + qh) * D;
+  bf16x8 qf[D / 32], qsf[D / 32];
+  const size_t qoff = ((size_t)(qs0 + (col_valid ? tok : 0)) * p.nh + qh) * D;
 #pragma unroll
-  for (int c = 0; c < D / 32; ++c)
-    qf[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qrow + 32 * c + 8 * h4) : zero8();
+  for (int c = 0; c < D / 32; ++c) {
+    qf[c] = col_valid ? *reinterpret_cast<const bf16x8*>(p.q + qoff + 32 * c + 8 * h4) : zero8();
+    qsf[c] = (WIN && p.n_sink > 0 && col_valid)
+                 ? *reinterpret_cast<const bf16x8*>(p.q_sink + qoff + 32 * c + 8 * h4) : zero8();
+  }
+
+  // virtual steps: [0, n_main) = full cache / ring segment, [n_main, n_main + n_sinkst) = sinks
+  int seg_len, n_main, n_sinkst = 0, nS = 0;
+  if (WIN) {
+    seg_len = L > p.n_sink ? min(p.ring, L - p.n_sink) : 0;
+    n_main = (seg_len + 31) >> 5;
+    nS = min(p.n_sink, L);
+    n_sinkst = (nS + 31) >> 5;
+  } else {
+    seg_len = pq_max + 1;
+    n_main = (seg_len + 31) >> 5;
+  }
+  const int nsteps = n_main + n_sinkst;
+  auto slot0 = [&](int sidx) -> int {  // first cache slot of virtual step sidx
+    if (!WIN) return sidx * 32;
+    return sidx < n_main ? p.sink_pad + sidx * 32 : (sidx - n_main) * 32;
+  };
+
+  typedef int i32x4v __attribute__((ext_vector_type(4)));
+  i32x4v rk[UPT], rv[UPT];
+  auto gload = [&](int sidx) {
+    const int u0 = slot0(sidx);
+    const int page = bt[u0 / p.bs];
+    const int offk = u0 % p.bs;
+    const size_t hb = ((size_t)page * p.nkv + kvh) * head_stride;
+    const bf16* ks = p.k_cache + hb + (size_t)offk * D;   // 32 rows x D, contiguous
+    const bf16* vs = p.v_cache + hb + (size_t)offk * D;   // 4 groups x D x 8, contiguous
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int u = threadIdx.x + i * 256;
+      if (UNITS % 256 == 0 || u < UNITS) {
+        rk[i] = *reinterpret_cast<const i32x4v*>(ks + (size_t)u * 8);
+        rv[i] = *reinterpret_cast<const i32x4v*>(vs + (size_t)u * 8);
+      }
+    }
+  };
+  auto swrite = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int u = threadIdx.x + i * 256;
+      if (UNITS % 256 == 0 || u < UNITS) {
+        const int row = u / CH, ch = u % CH;
+        *reinterpret_cast<i32x4v*>(&smem[buf][0][(row * CH + (ch ^ kswz<D>(row))) * 8]) = rk[i];
+        *reinterpret_cast<i32x4v*>(&smem[buf][1][u * 8]) = rv[i];
+      }
+    }
+  };
 
   WaveState<D> st;
   st.init();
-  if (!WIN) {
-    const int nkeys = pq_max + 1;  // slots 0..pq_max
-    for (int u0 = 0; u0 < nkeys; u0 += 32) {
-      const int page = bt[u0 / p.bs];
-      const int offk = u0 % p.bs;
-      const bf16* kbase = p.k_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
-      const bf16* vbase = p.v_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
-      unsigned vm = 0;
+  if (nsteps > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+  for (int sidx = 0; sidx < nsteps; ++sidx) {
+    const int buf = sidx & 1;
+    if (sidx + 1 < nsteps) gload(sidx + 1);
+    // ---- fragments from LDS ----
+    KVFrag<D> f;
+    const int krow0 = 8 * (col >> 2) + (col & 3);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vm |= ((u0 + 8 * h4 + j) <= pq ? 1u : 0u) << j;
-      attn_step<D>(st, qf, kbase, vbase, offk, p.scale_log2, vm);
+    for (int t = 0; t < 2; ++t) {
+      const int row = krow0 + 4 * t;
+#pragma unroll
+      for (int c = 0; c < D / 32; ++c)
+        f.k[t][c] = *reinterpret_cast<const bf16x8*>(
+            &smem[buf][0][(row * CH + ((4 * c + h4) ^ kswz<D>(row))) * 8]);
     }
-  } else {
-    const int seg_len = L > p.n_sink ? min(p.ring, L - p.n_sink) : 0;
-    for (int s0 = 0; s0 < seg_len; s0 += 32) {
-      const int u0 = p.sink_pad + s0;
-      const int page = bt[u0 / p.bs];
-      const int offk = u0 % p.bs;
-      const bf16* kbase = p.k_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
-      const bf16* vbase = p.v_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
-      unsigned vm = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int u = u0 + 8 * h4 + j;
-        bool ok = (u - p.sink_pad) < seg_len;
+    for (int e = 0; e < D / 16; ++e)
+      f.v[e] = *reinterpret_cast<const bf16x8*>(&smem[buf][1][(h4 * D + 16 * e + col) * 8]);
+    // ---- visibility of keys 8h4 .. 8h4+7 for this lane's query column ----
+    const int u0 = slot0(sidx);
+    unsigned vm = 0;
+    const bool sink_step = WIN && sidx >= n_main;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int u = u0 + 8 * h4 + j;
+      bool ok;
+      if (!WIN) {
+        ok = u <= pq;
+      } else if (sink_step) {
+        ok = u < nS && u <= pq;
+      } else {
+        ok = (u - p.sink_pad) < seg_len;
         if (ok) {
           const int a = ring_abs(u, L, p);
           ok = a >= p.n_sink && a <= pq && (pq - a) < (p.window - p.n_sink);
         }
-        vm |= (ok ? 1u : 0u) << j;
       }
-      attn_step<D>(st, qf, kbase, vbase, offk, p.scale_log2, vm);
+      vm |= (ok ? 1u : 0u) << j;
     }
-    if (p.n_sink > 0) {
-      bf16x8 qsf[D / 32];
-      const bf16* qsrow = p.q_sink + ((size_t)(qs0 + (col_valid ? tok : 0)) * p.nh + qh) * D;
-#pragma unroll
-      for (int c = 0; c < D / 32; ++c)
-        qsf[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qsrow + 32 * c + 8 * h4) : zero8();
-      const int nS = min(p.n_sink, L);
-      for (int u0 = 0; u0 < nS; u0 += 32) {
-        const int page = bt[u0 / p.bs];
-        const int offk = u0 % p.bs;
-        const bf16* kbase = p.k_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
-        const bf16* vbase = p.v_cache + ((size_t)page * p.nkv + kvh) * head_stride_k;
-        unsigned vm = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int u = u0 + 8 * h4 + j;
-          vm |= (u < nS && u <= pq ? 1u : 0u) << j;
-        }
-        attn_step<D>(st, qsf, kbase, vbase, offk, p.scale_log2, vm);
-      }
-    }
+    if (sink_step)
+      attn_compute<D>(st, qsf, f, p.scale_log2, vm);
+    else
+      attn_compute<D>(st, qf, f, p.scale_log2, vm);
+    if (sidx + 1 < nsteps) swrite(buf ^ 1);
+    __syncthreads();
   }
   float lsum = st.l;
   lsum += __shfl_xor(lsum, 16, 64);
@@ -433,11 +506,14 @@ int launch_attn_decode(const AttnParams& p, int B, int D, hipStream_t stream) {
 
 template <int D>
 static int launch_prefill_d(const AttnParams& p, int B, int max_q, hipStream_t stream) {
-  dim3 grid((max_q + 63) / 64, p.nh, B);
+  const int G = p.nh / p.nkv;
+  const int hpw = (G % 4 == 0) ? 4 : (G % 2 == 0 ? 2 : 1);  // q heads sharing each K/V tile
+  const int tpw = 4 / hpw;
+  dim3 grid((max_q + 16 * tpw - 1) / (16 * tpw), p.nkv * (G / hpw), B);
   if (p.ring > 0)
-    attn_prefill_kernel<D, true><<<grid, 256, 0, stream>>>(p);
+    attn_prefill_kernel<D, true><<<grid, 256, 0, stream>>>(p, hpw);
   else
-    attn_prefill_kernel<D, false><<<grid, 256, 0, stream>>>(p);
+    attn_prefill_kernel<D, false><<<grid, 256, 0, stream>>>(p, hpw);
   return 0;
 }
 

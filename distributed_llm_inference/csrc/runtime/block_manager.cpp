@@ -109,6 +109,15 @@ class BlockManager {
     return true;
   }
 
+  // All-or-nothing batch reservation: grows every sids[i] by ns[i] tokens if the pool can hold
+  // all of them, otherwise changes nothing and returns false (one call per step instead of B).
+  bool append_batch(const std::vector<int64_t>& sids, const std::vector<int64_t>& ns) {
+    if (sids.size() != ns.size()) throw std::invalid_argument("append_batch: size mismatch");
+    if (!can_append(sids, ns)) return false;
+    for (size_t i = 0; i < sids.size(); ++i) append(sids[i], ns[i]);
+    return true;
+  }
+
   int64_t slot_of(int64_t sid, int64_t a) const {
     const SeqState& s = get(sid);
     return physical(s, logical_slot(a));
@@ -217,6 +226,7 @@ void register_block_manager(py::module_& m) {
       .def("blocks_needed", &BlockManager::blocks_needed)
       .def("can_append", &BlockManager::can_append)
       .def("append", &BlockManager::append)
+      .def("append_batch", &BlockManager::append_batch)
       .def("slot_of", &BlockManager::slot_of)
       .def("block_table", &BlockManager::block_table)
       .def("prepare", &BlockManager::prepare, py::arg("sids"), py::arg("q_lens"),

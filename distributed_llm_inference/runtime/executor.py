@@ -56,13 +56,18 @@ class StepPlan:
     kind: str = "run"                                       # run | barrier | stop
     tokens: Optional[List[int]] = None                      # stage-0 input (not broadcast)
 
+    def __post_init__(self):
+        # computed once: both are read several times per step on every stage
+        self._num_tokens = int(sum(self.q_lens))
+        self._decode = bool(self.seq_ids) and self._num_tokens == len(self.q_lens)
+
     @property
     def is_decode(self) -> bool:
-        return bool(self.seq_ids) and all(q == 1 for q in self.q_lens)
+        return self._decode
 
     @property
     def num_tokens(self) -> int:
-        return int(sum(self.q_lens))
+        return self._num_tokens
 
     def to_wire(self) -> dict:
         d = dict(step=self.step, mb=self.mb, seq_ids=self.seq_ids, q_lens=self.q_lens,
@@ -192,11 +197,9 @@ class StageExecutor:
 
     def reserve(self, seq_ids: Sequence[int], q_lens: Sequence[int]) -> None:
         m = self.pool.manager
-        if not m.can_append(list(seq_ids), list(q_lens)):
+        if not m.append_batch(seq_ids, q_lens):
             raise MemoryError(f"KV pool exhausted on stage [{self.stage.start},{self.stage.end}) "
                               f"({m.num_free_blocks} free blocks)")
-        for s, q in zip(seq_ids, q_lens):
-            m.append(int(s), int(q))
 
     # ------------------------------------------------------------------ metadata
     def _stage_metadata(self, plan: StepPlan, rows: int) -> Tuple[int, int]:

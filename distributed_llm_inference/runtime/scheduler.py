@@ -41,6 +41,11 @@ class Scheduler:
         self._reserve: Dict[int, int] = {}
         self.step = 0
         self.finished: List[Sequence] = []
+        # steady-state decode fast path: while a micro-batch's membership is unchanged and every
+        # member is decoding, the next plan differs from the last one only in its tokens
+        self._dirty: List[bool] = [True] * self.M
+        self._decode_cache: List[Optional[dict]] = [None] * self.M
+        self._rows: List[List[Sequence]] = [[] for _ in range(self.M)]  # plan row -> sequence
 
     # ------------------------------------------------------------------ requests
     def add(self, seq: Sequence) -> None:
@@ -57,6 +62,8 @@ class Scheduler:
                 if s.seq_id == seq_id:
                     s.status = SeqStatus.ABORTED
                     s.finish_reason = "abort"
+                    if s.micro_batch >= 0:
+                        self._dirty[s.micro_batch] = True
 
     def has_work(self) -> bool:
         return bool(self.waiting) or any(self.mbs) or any(p is not None for p in self.inflight)
@@ -87,6 +94,7 @@ class Scheduler:
             s.micro_batch = mb
             m.append(s)
             admitted.append(s)
+            self._dirty[mb] = True
             budget -= min(len(s.prompt), budget)
         return admitted
 
@@ -97,9 +105,14 @@ class Scheduler:
         # drop aborted sequences
         for s in [s for s in m if s.status == SeqStatus.ABORTED]:
             self._retire(mb, s)
-        decode = [s for s in m if s.num_computed >= len(s.prompt)]
-        budget = self.max_tokens - len(decode)
-        self._admit(mb, budget)
+        if self._dirty[mb]:
+            decode_n = sum(1 for s in m if s.num_computed >= len(s.prompt))
+        else:
+            decode_n = len(m)  # a clean micro-batch is all-decode (see _decode_plan)
+        self._admit(mb, self.max_tokens - decode_n)
+        if not self._dirty[mb] and m:
+            return self._decode_plan(mb)
+        budget = self.max_tokens - decode_n
         seq_ids, q_lens, tokens, sample_rows = [], [], [], []
         temps, topk, topp, seeds = [], [], [], []
         for s in m:
@@ -133,14 +146,43 @@ class Scheduler:
         self.step += 1
         # the tokens are (about to be) in the cache on every stage
         byid = {s.seq_id: s for s in m}
-        for sid, q in zip(seq_ids, q_lens):
-            byid[sid].num_computed += q
+        rows = [byid[sid] for sid in seq_ids]
+        for s, q in zip(rows, q_lens):
+            s.num_computed += q
+        self._rows[mb] = rows
         self.inflight[mb] = plan if seq_ids else None
+        # cache the all-decode layout; it stays valid until the membership changes
+        if seq_ids and len(rows) == len(m) and all(q == 1 for q in q_lens) \
+                and len(sample_rows) == len(rows):
+            self._decode_cache[mb] = dict(seq_ids=seq_ids, q_lens=q_lens, sample_rows=sample_rows,
+                                          temperature=temps, top_k=topk, top_p=topp, seeds=seeds)
+            self._dirty[mb] = False
+        else:
+            self._decode_cache[mb] = None
+            self._dirty[mb] = True
+        return plan
+
+    def _decode_plan(self, mb: int) -> StepPlan:
+        """Plan of a clean micro-batch: same rows as last step, one new token each."""
+        c = self._decode_cache[mb]
+        rows = self._rows[mb]
+        tokens = [s.output[-1] for s in rows]
+        for s in rows:
+            s.num_computed += 1
+        free_ids = self.pending_free[mb]
+        self.pending_free[mb] = []
+        plan = StepPlan(step=self.step, mb=mb, seq_ids=c["seq_ids"], q_lens=c["q_lens"],
+                        free_ids=free_ids, sample_rows=c["sample_rows"],
+                        temperature=c["temperature"], top_k=c["top_k"], top_p=c["top_p"],
+                        seeds=c["seeds"], tokens=tokens)
+        self.step += 1
+        self.inflight[mb] = plan
         return plan
 
     # ------------------------------------------------------------------ results
     def _retire(self, mb: int, s: Sequence) -> None:
         self.mbs[mb].remove(s)
+        self._dirty[mb] = True
         self.pending_free[mb].append(s.seq_id)
         self.reserved_blocks -= self._reserve.pop(s.seq_id, 0)
         self.finished.append(s)
@@ -151,13 +193,13 @@ class Scheduler:
         self.inflight[mb] = None
         if plan is None:
             return []
-        byid = {s.seq_id: s for s in self.mbs[mb]}
+        rows = self._rows[mb]
         done = []
         for row, tok in zip(plan.sample_rows, tokens):
-            s = byid.get(plan.seq_ids[row])
-            if s is None or s.is_finished():
+            s = rows[row]
+            if s.status is not SeqStatus.RUNNING:  # finished / aborted meanwhile
                 continue
-            if s.append_token(int(tok), self.eos, now):
+            if s.append_token(tok, self.eos, now):
                 done.append(s)
         for s in done:
             self._retire(mb, s)

@@ -1,0 +1,56 @@
+"""Prefill-attention microbenchmark (Llama-3-70B heads: 64 q / 8 kv, D=128) on one MI355X.
+
+Cases are (sequences, new tokens per sequence, tokens already cached).  Prints µs per call and the
+achieved causal-attention TFLOP/s (4 * D FLOPs per visible (query, key) pair per head).
+"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_llm_inference import ops  # noqa: E402
+
+dev = torch.device("cuda:0")
+nh, nkv, D, bs = 64, 8, 128, 64
+CASES = [(32, 512, 0), (4, 4096, 0), (1, 2048, 6144), (256, 16, 512)]
+
+
+def run(B, q, ctx):
+    L = q + ctx
+    nbps = (L + bs - 1) // bs
+    nblk = B * nbps
+    kc = torch.randn(nblk, nkv, bs, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(nblk, nkv, bs // 8, D, 8, device=dev, dtype=torch.bfloat16)
+    bt = torch.arange(nblk, device=dev, dtype=torch.int32).view(B, nbps)
+    lens = torch.full((B,), L, dtype=torch.int32, device=dev)
+    q_start = torch.arange(0, (B + 1) * q, q, dtype=torch.int32, device=dev)
+    Q = torch.randn(B * q, nh, D, device=dev, dtype=torch.bfloat16)
+    out = torch.empty_like(Q)
+
+    def call():
+        ops.attn_prefill(Q, None, kc, vc, bt, lens, q_start, q, D ** -0.5)
+
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    n = 20
+    t0 = time.perf_counter()
+    for _ in range(n):
+        call()
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / n * 1e6
+    pairs = B * sum(ctx + i + 1 for i in range(q))
+    tf = 4 * D * nh * pairs / us / 1e6
+    return dict(B=B, q=q, ctx=ctx, us=round(us, 1), TFLOPs=round(tf, 1))
+
+
+res = []
+for c in CASES:
+    r = run(*c)
+    print(r, flush=True)
+    res.append(r)
+os.makedirs("gpurun_out", exist_ok=True)
+json.dump(res, open("gpurun_out/attn_prefill_bench.json", "w"), indent=1)
