@@ -84,6 +84,7 @@ def main():
         t = torch.tensor([interval], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.barrier()
+        obj.close()
         dist.destroy_process_group()
         return
     drv = obj
@@ -171,6 +172,7 @@ def main():
         with open(a.json_out, "w") as f:
             f.write(line + "\n")
     if world > 1:
+        drv.close()
         dist.destroy_process_group()
 
 

@@ -95,6 +95,7 @@ def cmd_worker(a) -> int:
     role, obj = init_pipeline_rank(cfg)
     if role == "follower":
         obj.run()
+        obj.close()
         if dist.is_initialized():
             dist.destroy_process_group()
         return 0
@@ -133,6 +134,7 @@ def cmd_worker(a) -> int:
             raise SystemExit(f"unknown action {a.action}")
     finally:
         drv.stop()
+        drv.close()
         if dist.is_initialized():
             dist.destroy_process_group()
     return 0

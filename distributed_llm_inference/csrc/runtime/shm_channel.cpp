@@ -106,7 +106,14 @@ class ShmChannel {
 
   ~ShmChannel() {
     if (base_ && base_ != MAP_FAILED) munmap(base_, size_);
+    unlink();
+  }
+
+  // Remove the name from /dev/shm (creator only).  Existing mappings stay valid, so calling this
+  // once every peer has attached leaves nothing behind even if a process is killed later.
+  void unlink() {
     if (creator_) shm_unlink(name_.c_str());
+    creator_ = false;
   }
 
   void send(const py::bytes& msg, double timeout_s) {
@@ -219,6 +226,7 @@ void register_shm_channel(py::module_& m) {
       .def("recv", &ShmChannel::recv, py::arg("timeout") = 0.0)
       .def("poll", &ShmChannel::poll)
       .def("close", &ShmChannel::close_channel)
+      .def("unlink", &ShmChannel::unlink)
       .def_property_readonly("closed", &ShmChannel::closed)
       .def("heartbeat", &ShmChannel::heartbeat)
       .def("idle_seconds", &ShmChannel::idle_seconds)

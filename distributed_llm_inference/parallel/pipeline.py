@@ -171,6 +171,9 @@ class LocalPipeline(DriverBase):
         if any(ex.device.type == "cuda" for ex in self.executors):
             torch.cuda.synchronize()
 
+    def close(self) -> None:
+        pass
+
 
 # =============================================================================================
 # multi-process pipeline
@@ -193,6 +196,13 @@ class _Channels:
             self.ctrl = R.ShmChannel(ctrl_name, rank - 1, 64, slot_size, world - 1, False, 120.0)
             if rank == world - 1:
                 self.tok = R.ShmChannel(tok_name, -1, 64, slot_size, 1, True)
+
+
+    def unlink(self) -> None:
+        """Drop the /dev/shm names once every rank has attached (mappings stay valid)."""
+        for ch in (self.ctrl, self.tok):
+            if ch is not None:
+                ch.unlink()
 
 
 class DistributedDriver(DriverBase):
@@ -232,6 +242,12 @@ class DistributedDriver(DriverBase):
             torch.cuda.synchronize()
         if kind == "barrier":
             dist.barrier(group=self.group)
+
+    def close(self) -> None:
+        """After :meth:`stop`: wait for every rank to finish, then tear down the RCCL
+        communicators explicitly (never from an interpreter-exit destructor)."""
+        dist.barrier(group=self.group)
+        self.tr.close()
 
 
 class StageFollower:
@@ -321,6 +337,11 @@ class StageFollower:
             self._pub_thread.join()
         if self.ex.device.type == "cuda":
             torch.cuda.synchronize()
+
+    def close(self) -> None:
+        """Counterpart of :meth:`DistributedDriver.close` (call after :meth:`run` returns)."""
+        dist.barrier(group=self.group)
+        self.tr.close()
 
 
 def make_transport(rank: int, world: int, device: torch.device) -> Transport:

@@ -183,6 +183,7 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     channels = _Channels(job, rank, world)
     transport = make_transport(rank, world, device)
     dist.barrier(group=group)
+    channels.unlink()  # every rank has attached: nothing may be left in /dev/shm after this
     if rank == 0:
         sched = make_scheduler(spec, ex, cfg, world)
         return "driver", DistributedDriver(ex, sched, transport, channels, world, group)

@@ -54,9 +54,11 @@ def _pipeline_worker(rank, world, port, mbs, q):
         if role == "driver":
             out = obj.generate(PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))
             obj.stop()
+            obj.close()
             q.put(("ok", [s.output for s in out]))
         else:
             obj.run()
+            obj.close()
         dist.destroy_process_group()
     except Exception:
         q.put(("err", traceback.format_exc()))

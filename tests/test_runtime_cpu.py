@@ -209,9 +209,11 @@ def _mp_worker(rank, world, port, q):
     if role == "driver":
         out = obj.generate(PROMPTS, SamplingParams(max_tokens=6, ignore_eos=True))
         obj.stop()
+        obj.close()
         q.put([s.output for s in out])
     else:
         obj.run()
+        obj.close()
     dist.destroy_process_group()
 
 
