@@ -155,6 +155,7 @@ def main():
                    "parallelism": f"pp{a.gpus}"},
         "p50_token_latency_ms": round(p50, 3),
         "p90_token_latency_ms": round(p90, 3),
+        "transport": type(getattr(drv, "tr", None)).__name__ if world > 1 else "none",
         "micro_batches": M,
         "batch_per_micro_batch": a.batch_per_mb,
         "prompt_len": a.prompt_len,

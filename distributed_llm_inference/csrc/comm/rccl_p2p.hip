@@ -2,19 +2,23 @@
 //
 // The reference moves hidden states between stages over hivemind/libp2p + protobuf (SURVEY N5,
 // §5.8).  On one MI355X node every GPU pair has a direct xGMI link, so stage i -> i+1 activations
-// and the last-stage -> stage-0 token feedback are plain RCCL point-to-point transfers.  Owning the
-// ncclComm_t here (instead of going through ProcessGroupNCCL) lets the runtime:
-//   * put send/recv on its own comm HIP stream, ordered against compute with HIP events;
-//   * capture send/recv into the same hipGraph as the stage's compute;
-//   * create exactly one communicator for the whole pipeline (no lazy per-pair communicators).
-// The unique id is distributed by the launcher through the torch.distributed TCP store.
+// are plain RCCL point-to-point transfers.  Owning the ncclComm_t here (instead of going through
+// ProcessGroupNCCL) lets the runtime put sends and receives on its own HIP streams, ordered against
+// compute with HIP events, on one 2-rank communicator per neighbouring stage pair.
+//
+// Communicators are created NON-BLOCKING and initialisation is polled with a deadline: a peer that
+// never shows up (or fails) turns into a Python exception after `timeout_s` instead of a process
+// stuck forever inside ncclCommInitRank, so the pipeline can agree on a fallback transport.
+// The unique id is distributed through the torch.distributed TCP store.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <string>
+#include <thread>
 
 namespace {
 
@@ -41,13 +45,22 @@ ncclDataType_t to_nccl(const at::Tensor& t) {
 
 class RcclComm {
  public:
-  RcclComm(const std::string& uid, int rank, int world, int device)
+  RcclComm(const std::string& uid, int rank, int world, int device, double timeout_s)
       : rank_(rank), world_(world), device_(device) {
     TORCH_CHECK(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id size");
     ncclUniqueId id;
     memcpy(&id, uid.data(), sizeof(id));
     TORCH_CHECK(hipSetDevice(device) == hipSuccess, "hipSetDevice failed");
-    RCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+    ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+    config.blocking = 0;
+    pybind11::gil_scoped_release nogil;
+    const ncclResult_t r = ncclCommInitRankConfig(&comm_, world, id, rank, &config);
+    if (r != ncclSuccess && r != ncclInProgress) {
+      if (comm_) ncclCommAbort(comm_);
+      comm_ = nullptr;
+      TORCH_CHECK(false, "RCCL error ", ncclGetErrorString(r), " in ncclCommInitRankConfig");
+    }
+    wait_ready(timeout_s, "ncclCommInitRankConfig");
   }
   ~RcclComm() { destroy(); }
 
@@ -66,36 +79,67 @@ class RcclComm {
 
   void send(const at::Tensor& t, int peer, int64_t stream) {
     check(t);
-    RCCL_CHECK(ncclSend(t.data_ptr(), t.nbytes(), ncclUint8, peer, comm_, resolve_stream(stream)));
+    enq(ncclSend(t.data_ptr(), t.nbytes(), ncclUint8, peer, comm_, resolve_stream(stream)), "ncclSend");
   }
   void recv(at::Tensor& t, int peer, int64_t stream) {
     check(t);
-    RCCL_CHECK(ncclRecv(t.data_ptr(), t.nbytes(), ncclUint8, peer, comm_, resolve_stream(stream)));
+    enq(ncclRecv(t.data_ptr(), t.nbytes(), ncclUint8, peer, comm_, resolve_stream(stream)), "ncclRecv");
   }
   void group_start() { RCCL_CHECK(ncclGroupStart()); }
-  void group_end() { RCCL_CHECK(ncclGroupEnd()); }
+  void group_end() { enq(ncclGroupEnd(), "ncclGroupEnd"); }
 
   void all_reduce(at::Tensor& t, int64_t stream) {
     check(t);
-    RCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t), ncclSum, comm_,
-                             resolve_stream(stream)));
+    enq(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl(t), ncclSum, comm_,
+                      resolve_stream(stream)), "ncclAllReduce");
   }
   void broadcast(at::Tensor& t, int root, int64_t stream) {
     check(t);
-    RCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.nbytes(), ncclUint8, root, comm_,
-                             resolve_stream(stream)));
+    enq(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.nbytes(), ncclUint8, root, comm_,
+                      resolve_stream(stream)), "ncclBroadcast");
   }
   void all_gather(const at::Tensor& in, at::Tensor& out, int64_t stream) {
     check(in);
     check(out);
     TORCH_CHECK(out.nbytes() == in.nbytes() * (size_t)world_, "all_gather: out size mismatch");
-    RCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.nbytes(), ncclUint8, comm_,
-                             resolve_stream(stream)));
+    enq(ncclAllGather(in.data_ptr(), out.data_ptr(), in.nbytes(), ncclUint8, comm_,
+                      resolve_stream(stream)), "ncclAllGather");
   }
   int rank() const { return rank_; }
   int world() const { return world_; }
 
  private:
+  // Poll the (non-blocking) communicator until it leaves ncclInProgress; abort it on an error or
+  // when the deadline passes.
+  void wait_ready(double timeout_s, const char* what) {
+    const auto deadline = std::chrono::steady_clock::now() +
+                          std::chrono::microseconds((int64_t)(timeout_s * 1e6));
+    ncclResult_t st = ncclInProgress;
+    while (true) {
+      const ncclResult_t q = ncclCommGetAsyncError(comm_, &st);
+      if (q != ncclSuccess) st = q;
+      if (st != ncclInProgress) break;
+      if (std::chrono::steady_clock::now() > deadline) {
+        ncclCommAbort(comm_);
+        comm_ = nullptr;
+        TORCH_CHECK(false, "RCCL ", what, " timed out after ", timeout_s, " s");
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    if (st != ncclSuccess) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+      TORCH_CHECK(false, "RCCL error ", ncclGetErrorString(st), " in ", what);
+    }
+  }
+  // A non-blocking communicator may return ncclInProgress from an enqueue call.
+  void enq(ncclResult_t r, const char* what) {
+    if (r == ncclInProgress) {
+      wait_ready(120.0, what);
+      return;
+    }
+    TORCH_CHECK(r == ncclSuccess, "RCCL error ", ncclGetErrorString(r), " in ", what);
+  }
   void check(const at::Tensor& t) const {
     TORCH_CHECK(comm_ != nullptr, "communicator destroyed");
     TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RCCL tensors must be contiguous GPU tensors");
@@ -123,8 +167,9 @@ void register_rccl(pybind11::module_& m) {
   m.def("rccl_unique_id", &get_unique_id);
   m.def("rccl_version", &rccl_version);
   pybind11::class_<RcclComm>(m, "RcclComm")
-      .def(pybind11::init<const std::string&, int, int, int>(), pybind11::arg("uid"),
-           pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("device"))
+      .def(pybind11::init<const std::string&, int, int, int, double>(), pybind11::arg("uid"),
+           pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("device"),
+           pybind11::arg("timeout_s") = 300.0)
       .def("send", &RcclComm::send, pybind11::arg("t"), pybind11::arg("peer"),
            pybind11::arg("stream") = 0)
       .def("recv", &RcclComm::recv, pybind11::arg("t"), pybind11::arg("peer"),

@@ -26,6 +26,7 @@ import collections
 import logging
 import os
 import queue
+import sys
 import threading
 import time
 from typing import Deque, Dict, List, Optional, Sequence
@@ -344,15 +345,39 @@ class StageFollower:
         self.tr.close()
 
 
-def make_transport(rank: int, world: int, device: torch.device) -> Transport:
+def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
+                   rccl_timeout_s: float = 300.0) -> Transport:
     """RCCL P2P on GPUs (default); ``DLI_TRANSPORT=host`` stages GPU tensors through gloo
-    (several ranks sharing one GPU); gloo on CPU."""
+    (several ranks sharing one GPU); gloo on CPU.
+
+    RCCL initialisation is agreed on by all ranks: every rank publishes whether its communicators
+    came up (a failure or a peer that never arrives ends in a timeout, not a hang), and if ANY rank
+    failed, every rank falls back to the host-staged transport together and says so on stderr."""
     if world == 1:
         return LoopbackTransport(1)
     kind = os.environ.get("DLI_TRANSPORT", "rccl" if device.type == "cuda" else "gloo")
     if device.type == "cuda" and kind == "rccl":
         from ..runtime.faults import raw_store
-        return RcclTransport(raw_store(), rank, world, device)
+        store = raw_store()
+        prefix = f"dli_rccl_{job}"
+        tr, err = None, ""
+        try:
+            tr = RcclTransport(store, rank, world, device, prefix=prefix, timeout_s=rccl_timeout_s)
+        except Exception as e:  # noqa: BLE001 - reported and agreed on below
+            err = repr(e)
+        store.set(f"{prefix}/ok/{rank}", "1" if tr is not None else "0")
+        ok = [store.get(f"{prefix}/ok/{r}") == b"1" for r in range(world)]
+        if all(ok):
+            return tr
+        if tr is not None:
+            tr.abort()
+        bad = [r for r, o in enumerate(ok) if not o]
+        msg = (f"[rank {rank}] RCCL transport unavailable (failed on ranks {bad}"
+               + (f": {err}" if err else "") + "); falling back to host-staged transport")
+        log.warning(msg)
+        print(msg, file=sys.stderr, flush=True)
+        from .transport import HostStagedTransport
+        return HostStagedTransport()
     if device.type == "cuda":
         from .transport import HostStagedTransport
         return HostStagedTransport()

@@ -103,7 +103,7 @@ class RcclTransport(Transport):
     """RCCL P2P over xGMI with dedicated send/recv streams (see module docstring)."""
 
     def __init__(self, store: "dist.Store", rank: int, world: int, device: torch.device,
-                 prefix: str = "dli_rccl"):
+                 prefix: str = "dli_rccl", timeout_s: float = 300.0):
         from .. import ops
         C = ops.native()
         self.rank, self.world, self.device = rank, world, device
@@ -126,7 +126,8 @@ class RcclTransport(Transport):
             else:
                 uid = store.get(key)
             peer = b if rank == a else a
-            self._comms[peer] = C.RcclComm(bytes(uid), 0 if rank == a else 1, 2, dev_idx)
+            self._comms[peer] = C.RcclComm(bytes(uid), 0 if rank == a else 1, 2, dev_idx,
+                                           timeout_s)
 
     def _comm(self, peer: int):
         c = self._comms.get(peer)
@@ -165,4 +166,9 @@ class RcclTransport(Transport):
     def close(self) -> None:
         for c in self._comms.values():
             c.destroy()
+        self._comms.clear()
+
+    def abort(self) -> None:
+        for c in self._comms.values():
+            c.abort()
         self._comms.clear()

@@ -181,7 +181,7 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     start, end = ranges[rank]
     ex = build_executor(spec, start, end, device, cfg, group=group, kv_share=kv_share)
     channels = _Channels(job, rank, world)
-    transport = make_transport(rank, world, device)
+    transport = make_transport(rank, world, device, job=job)
     dist.barrier(group=group)
     channels.unlink()  # every rank has attached: nothing may be left in /dev/shm after this
     if rank == 0:

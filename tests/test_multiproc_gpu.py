@@ -41,11 +41,11 @@ def _cfg(world, mbs):
     return spec, cfg
 
 
-def _pipeline_worker(rank, world, port, mbs, q):
+def _pipeline_worker(rank, world, port, mbs, q, transport="host"):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_SHARE_GPU="1",
-                          DLI_TRANSPORT="host", DLI_TUNABLEOP="0")
+                          DLI_TRANSPORT=transport, DLI_TUNABLEOP="0")
         import torch.distributed as dist
         from distributed_llm_inference.runtime.engine import init_pipeline_rank
         from distributed_llm_inference.runtime.sequence import SamplingParams
@@ -54,14 +54,15 @@ def _pipeline_worker(rank, world, port, mbs, q):
         if role == "driver":
             out = obj.generate(PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))
             obj.stop()
+            kind = type(obj.tr).__name__
             obj.close()
-            q.put(("ok", [s.output for s in out]))
+            q.put(("ok", [s.output for s in out], kind))
         else:
             obj.run()
             obj.close()
         dist.destroy_process_group()
     except Exception:
-        q.put(("err", traceback.format_exc()))
+        q.put(("err", traceback.format_exc(), None))
         raise
 
 
@@ -79,12 +80,37 @@ def test_multiprocess_pipeline_on_gpu(gpu, world, mbs):
     ps = [ctx.Process(target=_pipeline_worker, args=(r, world, port, mbs, q)) for r in range(world)]
     for p in ps:
         p.start()
-    status, got = q.get(timeout=600)
+    status, got, *_ = q.get(timeout=600)
     for p in ps:
         p.join(120)
     assert status == "ok", got
     assert all(p.exitcode == 0 for p in ps)
     assert got == ref
+
+
+def test_rccl_failure_falls_back_to_host_transport(gpu):
+    """Two ranks on ONE GPU with the default RCCL transport: RCCL rejects the duplicate device,
+    every rank must agree on the failure (non-blocking init, no hang) and fall back together to
+    the host-staged transport, producing the same tokens as PP=1."""
+    from distributed_llm_inference.runtime.engine import LLMEngine
+    from distributed_llm_inference.runtime.sequence import SamplingParams
+    os.environ["DLI_TUNABLEOP"] = "0"
+    spec, cfg = _cfg(1, 3)
+    ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
+        PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_pipeline_worker, args=(r, 2, port, 3, q, "rccl")) for r in range(2)]
+    for p in ps:
+        p.start()
+    status, got, *rest = q.get(timeout=600)
+    for p in ps:
+        p.join(120)
+    assert status == "ok", got
+    assert all(p.exitcode == 0 for p in ps)
+    assert got == ref
+    assert rest and rest[0] == "HostStagedTransport", rest
 
 
 def _rccl_worker(rank, port, q):
@@ -97,7 +123,7 @@ def _rccl_worker(rank, port, q):
         from distributed_llm_inference.runtime.faults import raw_store
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        tr = RcclTransport(raw_store(), rank, 2, dev)
+        tr = RcclTransport(raw_store(), rank, 2, dev, timeout_s=60.0)
         x = torch.arange(1 << 20, device=dev, dtype=torch.float32) * (rank + 1)
         if rank == 0:
             tr.send(x, 1)
