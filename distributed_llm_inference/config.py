@@ -262,24 +262,29 @@ def plan_stages(spec: ModelSpec, num_stages: int,
     w = list(weights) if weights is not None else [1.0] * num_stages
     if len(w) != num_stages or min(w) <= 0:
         raise ValueError("weights must be positive, one per stage")
-    # LM head ≈ vocab*hidden params read per step; express it in layer-equivalents.
-    head_cost = spec.vocab_size * spec.hidden_size / max(1, spec.layer_param_count())
+    # LM head (+ final norm + sampling) in layer-equivalents of decode time.  By bytes/FLOPs the
+    # head is vocab*hidden / layer_params (1.22 layers for Llama-3-70B), but its single wide GEMM
+    # runs far more efficiently than a layer (which also carries attention, norms, activation):
+    # measured on MI355X at 512 rows, head + sampling 0.78 ms vs 1.06 ms per layer
+    # (profiles/pp1_bf16_b512_decode_breakdown.txt) -> factor 0.6.
+    head_cost = 0.6 * spec.vocab_size * spec.hidden_size / max(1, spec.layer_param_count())
     extra = [0.0] * num_stages
     if num_stages > 1:
         extra[-1] += head_cost
     total = (L + sum(extra))
     tw = sum(w)
-    # target layer cost per stage proportional to its speed
+    # start below the proportional target, then hand out the remaining layers one at a time to
+    # the stage whose time after taking it is smallest: this minimises the slowest stage, which
+    # sets the pipeline's throughput
     targets = [total * wi / tw - ei for wi, ei in zip(w, extra)]
-    # round to integers keeping the sum == L and every stage >= 1 layer
     counts = [max(1, int(math.floor(t))) for t in targets]
-    while sum(counts) < L:
-        # give a layer to the stage furthest below its target
-        i = max(range(num_stages), key=lambda k: targets[k] - counts[k])
-        counts[i] += 1
     while sum(counts) > L:
-        i = max((k for k in range(num_stages) if counts[k] > 1), key=lambda k: counts[k] - targets[k])
+        i = max((k for k in range(num_stages) if counts[k] > 1),
+                key=lambda k: (counts[k] + extra[k]) / w[k])
         counts[i] -= 1
+    while sum(counts) < L:
+        i = min(range(num_stages), key=lambda k: ((counts[k] + 1 + extra[k]) / w[k], k))
+        counts[i] += 1
     out, s = [], 0
     for c in counts:
         out.append((s, s + c))

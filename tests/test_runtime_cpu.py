@@ -311,3 +311,29 @@ def test_plan_stages_balanced():
     assert r[0][0] == 0 and r[-1][1] == 80 and all(b > a for a, b in r)
     assert all(r[i][1] == r[i + 1][0] for i in range(7))
     assert r[-1][1] - r[-1][0] <= r[0][1] - r[0][0]  # last stage also runs the LM head
+
+
+def test_plan_stages_minimises_slowest_stage():
+    """The planner's slowest stage (layers + LM-head equivalent on the last stage, divided by the
+    stage's speed) equals the brute-force optimum over all contiguous splits."""
+    import itertools
+    import math
+    from distributed_llm_inference.config import PRESETS
+    assert [b - a for a, b in plan_stages(PRESETS["llama-3-70b"], 8)] == [10] * 8
+    for name in ("llama-3-8b", "llama-3-70b", "tiny-llama"):
+        spec = PRESETS[name]
+        head = 0.6 * spec.vocab_size * spec.hidden_size / spec.layer_param_count()
+        L = spec.num_layers
+        for n in (2, 3, 4):
+            if n > L:
+                continue
+            for w in ([1.0] * n, [1.0] * (n - 1) + [0.5], [0.5] + [1.0] * (n - 1)):
+                def cost(counts):
+                    return max((c + (head if i == n - 1 else 0.0)) / w[i]
+                               for i, c in enumerate(counts))
+                got = cost([b - a for a, b in plan_stages(spec, n, weights=w)])
+                best = math.inf
+                for cuts in itertools.combinations(range(1, L), n - 1):
+                    edges = (0,) + cuts + (L,)
+                    best = min(best, cost([edges[i + 1] - edges[i] for i in range(n)]))
+                assert got <= best + 1e-9, (name, n, w, got, best)
