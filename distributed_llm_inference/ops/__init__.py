@@ -186,7 +186,7 @@ def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, logprobs: Optional[torch.Tensor] = None,
            generator: Optional[torch.Generator] = None) -> torch.Tensor:
     if not _gpu(logits):
-        y = ref.sample(logits, temperature, top_k, top_p, generator)
+        y = ref.sample(logits, temperature, top_k, top_p, generator, seeds=seeds, step=step)
         return out.copy_(y) if out is not None else y
     if out is None:
         out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)

@@ -150,17 +150,35 @@ def _sample_tokens_to_host(out: torch.Tensor):
 class LocalPipeline(DriverBase):
     """All stages in this process (PP=1, or PP>1 loopback on one device / CPU)."""
 
-    def __init__(self, executors: List[StageExecutor], scheduler: Scheduler):
+    def __init__(self, executors: List[StageExecutor], scheduler: Scheduler,
+                 lookahead: bool = True):
         super().__init__(scheduler)
         self.executors = executors
         self._results: Dict[int, tuple] = {}
+        # one-step lookahead keeps a single micro-batch's GPU queue non-empty while the host
+        # consumes the previous step's tokens (see Scheduler.plan_lookahead)
+        self.lookahead = lookahead and scheduler.M == 1
+        self._last_tokens: Optional[torch.Tensor] = None
 
     def _issue(self, plan: StepPlan) -> None:
         x = None
         for i, ex in enumerate(self.executors):
-            x = ex.execute(plan, x)
+            x = ex.execute(plan, x, token_src=self._last_tokens if i == 0 else None)
         if plan.seq_ids:
+            # sampled tokens stay referenced on the device for a lookahead step
+            self._last_tokens = x
             self._results[plan.step] = _sample_tokens_to_host(x)
+
+    def round(self) -> bool:
+        s = self.sched
+        if not self.lookahead or s.inflight[0] is None:
+            return super().round()
+        la = s.plan_lookahead(0)
+        if la is not None:
+            self._issue(la)
+            self.inflight.append(la)
+        self._collect_front()  # the older step; its successor (if any) is already queued
+        return True
 
     def _collect(self, plan: StepPlan) -> List[int]:
         pinned, ev = self._results.pop(plan.step)

@@ -324,18 +324,19 @@ class StageExecutor:
         return self.graph_sizes[bisect.bisect_left(self.graph_sizes, B)]
 
     @torch.inference_mode()
-    def execute(self, plan: StepPlan, inputs: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def execute(self, plan: StepPlan, inputs: Optional[torch.Tensor] = None,
+                token_src: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Run one step.  ``inputs``: hidden states [T, H] for non-first stages (ignored on stage 0,
         which embeds ``plan.tokens``).  Returns hidden [T, H] or sampled tokens [n_sample] int32
         (device tensors; the caller decides when to synchronise)."""
         if not (_TRACE or _DEBUG):
-            return self._execute(plan, inputs)
+            return self._execute(plan, inputs, token_src)
         tag = f"stage[{self.stage.start},{self.stage.end}) step={plan.step} mb={plan.mb} " \
               f"{'decode' if plan.is_decode else 'prefill'} B={len(plan.seq_ids)} T={plan.num_tokens}"
         if _TRACE and self.device.type == "cuda":
             torch.cuda.nvtx.range_push(tag)  # roctx range on ROCm (rocprofv3 --marker-trace)
         try:
-            out = self._execute(plan, inputs)
+            out = self._execute(plan, inputs, token_src)
         finally:
             if _TRACE and self.device.type == "cuda":
                 torch.cuda.nvtx.range_pop()
@@ -348,7 +349,8 @@ class StageExecutor:
                 raise ValueError(f"sampled token out of range in {tag}")
         return out
 
-    def _execute(self, plan: StepPlan, inputs: Optional[torch.Tensor]) -> torch.Tensor:
+    def _execute(self, plan: StepPlan, inputs: Optional[torch.Tensor],
+                 token_src: Optional[torch.Tensor] = None) -> torch.Tensor:
         self.apply_frees(plan.free_ids)
         if not plan.seq_ids:
             return torch.empty(0, device=self.device)
@@ -358,6 +360,12 @@ class StageExecutor:
         grows = self._graph_rows(B) if decode else None
         rows = grows if grows is not None else B
         self._stage_metadata(plan, rows)
+        if self.stage.has_embed and plan.tokens is None:
+            # lookahead step: this step's input tokens are the previous step's sampler output,
+            # still on the device (stream order makes the copy wait for that sampler)
+            if token_src is None or not decode:
+                raise ValueError("a plan without tokens needs token_src (decode steps only)")
+            self.staging.d["tokens"][:B].copy_(token_src[:B], non_blocking=True)
         n_sample = len(plan.sample_rows)
         all_sample = decode and n_sample == B
         if grows is not None and (not self.stage.has_head or all_sample):

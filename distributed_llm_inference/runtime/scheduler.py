@@ -46,6 +46,9 @@ class Scheduler:
         self._dirty: List[bool] = [True] * self.M
         self._decode_cache: List[Optional[dict]] = [None] * self.M
         self._rows: List[List[Sequence]] = [[] for _ in range(self.M)]  # plan row -> sequence
+        # one-step lookahead (single micro-batch pipelines): the next decode step of a clean
+        # micro-batch, issued before the in-flight step's tokens reached the host
+        self.lookahead: List[Optional[StepPlan]] = [None] * self.M
 
     # ------------------------------------------------------------------ requests
     def add(self, seq: Sequence) -> None:
@@ -66,7 +69,8 @@ class Scheduler:
                         self._dirty[s.micro_batch] = True
 
     def has_work(self) -> bool:
-        return bool(self.waiting) or any(self.mbs) or any(p is not None for p in self.inflight)
+        return (bool(self.waiting) or any(self.mbs) or any(p is not None for p in self.inflight)
+                or any(p is not None for p in self.lookahead))
 
     def num_running(self) -> int:
         return sum(len(m) for m in self.mbs)
@@ -162,6 +166,31 @@ class Scheduler:
             self._dirty[mb] = True
         return plan
 
+    def plan_lookahead(self, mb: int) -> Optional[StepPlan]:
+        """The step after the in-flight one, planned BEFORE its tokens are known (their values
+        stay on the device: stage 0 reads them from the sampler output).  Only for a clean,
+        all-decode micro-batch with nobody waiting for admission and no sequence that could
+        reach max_tokens within the two steps; an EOS inside the window costs one wasted token.
+        Returns None when any condition fails (the caller then plans normally)."""
+        if (self.inflight[mb] is None or self.lookahead[mb] is not None or self._dirty[mb]
+                or self.waiting or self.pending_free[mb] or not self.mbs[mb]):
+            return None
+        rows = self._rows[mb]
+        if len(rows) != len(self.mbs[mb]):
+            return None
+        for s in rows:
+            if s.status is not SeqStatus.RUNNING or len(s.output) + 2 > s.params.max_tokens:
+                return None
+        c = self._decode_cache[mb]
+        for s in rows:
+            s.num_computed += 1
+        plan = StepPlan(step=self.step, mb=mb, seq_ids=c["seq_ids"], q_lens=c["q_lens"],
+                        free_ids=[], sample_rows=c["sample_rows"], temperature=c["temperature"],
+                        top_k=c["top_k"], top_p=c["top_p"], seeds=c["seeds"], tokens=None)
+        self.step += 1
+        self.lookahead[mb] = plan
+        return plan
+
     def _decode_plan(self, mb: int) -> StepPlan:
         """Plan of a clean micro-batch: same rows as last step, one new token each."""
         c = self._decode_cache[mb]
@@ -190,7 +219,8 @@ class Scheduler:
     def on_tokens(self, mb: int, tokens: List[int], now: Optional[float] = None) -> List[Sequence]:
         """Sampled tokens for the in-flight step of ``mb`` (one per sample row, in order)."""
         plan = self.inflight[mb]
-        self.inflight[mb] = None
+        self.inflight[mb] = self.lookahead[mb]  # the lookahead step (if any) is now the oldest
+        self.lookahead[mb] = None
         if plan is None:
             return []
         rows = self._rows[mb]

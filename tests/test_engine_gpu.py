@@ -154,3 +154,16 @@ def test_sink_window_matches_streamingllm_definition_gpu(gpu):
     view = toks[:S] + toks[len(toks) - (W - S):]
     ref = _forced_logits(stage, [view], [])[0]
     assert (outs[-1] - ref).abs().max() < 0.03 * max(1.0, ref.abs().max().item())
+
+
+def test_lookahead_equals_plain_decode_gpu(gpu):
+    """Single micro-batch lookahead on the GPU (hipGraph decode, sampled tokens fed back on the
+    device) gives exactly the tokens of the plain loop, greedy and seeded-temperature."""
+    for p in (SamplingParams(max_tokens=10, ignore_eos=True),
+              SamplingParams(max_tokens=10, temperature=0.9, top_k=40, seed=3, ignore_eos=True)):
+        outs = []
+        for la in (False, True):
+            eng = _engine(mbs=1)
+            eng.pipeline.lookahead = la
+            outs.append([s.output for s in eng.generate(PROMPTS, p)])
+        assert outs[0] == outs[1]

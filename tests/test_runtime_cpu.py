@@ -182,6 +182,37 @@ def test_local_pipeline_equals_single_stage(pp, mbs):
     assert a == b
 
 
+def test_lookahead_matches_plain_decode():
+    """One-step lookahead (single micro-batch: step t+1 issued before step t's tokens reach the
+    host, its input tokens taken from the device sampler output) changes nothing observable:
+    same tokens, same finish reasons, including sequences that stop on EOS inside the lookahead
+    window and sequences with different max_tokens."""
+    from distributed_llm_inference.runtime.sequence import Sequence
+    ref_eng = LLMEngine(SPEC, cfg=_cfg(mbs=1))
+    ref_eng.pipeline.lookahead = False
+    p0 = SamplingParams(max_tokens=12, ignore_eos=True)
+    base = [s.output for s in ref_eng.generate(PROMPTS, p0)]
+    # an EOS id that some sequences emit mid-generation
+    eos = base[0][4]
+
+    def run(lookahead):
+        eng = LLMEngine(SPEC, cfg=_cfg(mbs=1))
+        eng.pipeline.lookahead = lookahead
+        eng.pipeline.sched.eos = eos
+        seqs = [Sequence(list(pr), SamplingParams(max_tokens=mt, temperature=t, seed=7))
+                for pr, mt, t in zip(PROMPTS, (12, 3, 9, 12), (0.0, 0.0, 0.9, 0.0))]
+        for s_ in seqs:
+            eng.pipeline.sched.add(s_)
+        eng.pipeline.run_until_done()
+        return [(s_.output, s_.finish_reason) for s_ in seqs], eng
+
+    off, _ = run(False)
+    on, eng = run(True)
+    assert on == off
+    assert any(r == "stop" for _, r in on) and any(r == "length" for _, r in on)
+    assert eng.pipeline.lookahead
+
+
 def test_sampling_reproducible_and_max_tokens():
     p = SamplingParams(max_tokens=7, temperature=1.0, top_k=20, ignore_eos=True, seed=4)
     g = torch.Generator().manual_seed(0)
