@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--prompt-len", type=int, default=512)
     ap.add_argument("--max-batched-tokens", type=int, default=16384)
     ap.add_argument("--fp8", action="store_true", help="fp8-e4m3 weights (BASELINE config 5)")
+    ap.add_argument("--kv-fp8", action="store_true", help="fp8-e4m3 KV cache")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
@@ -72,7 +73,8 @@ def main():
     total_len = a.prompt_len + a.warmup + a.steps + 72
     cfg = EngineConfig(
         model=a.model, random_init=True, seed=0, quantize=a.fp8, pp=a.gpus,
-        cache=CacheConfig(block_size=64, gpu_memory_utilization=0.92),
+        cache=CacheConfig(block_size=64, gpu_memory_utilization=0.92,
+                          dtype="fp8" if a.kv_fp8 else "bf16"),
         serve=ServeConfig(max_batch_size=a.batch_per_mb, max_num_batched_tokens=a.max_batched_tokens,
                           num_micro_batches=M, max_seq_len=total_len, use_graphs=not a.no_graphs,
                           graph_batch_sizes=[a.batch_per_mb]))
@@ -148,7 +150,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp8-weights/bf16-act" if a.fp8 else "bf16",
+        "dtype": ("fp8-weights/bf16-act" if a.fp8 else "bf16") + ("/fp8-kv" if a.kv_fp8 else ""),
         "data": "synthetic (random-init Llama-3-70B weights, random prompt tokens)",
         "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
                    "global_batch": G, "seq_len": total_len,

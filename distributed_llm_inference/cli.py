@@ -27,6 +27,8 @@ def _common(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--gpus", type=int, default=1, help="pipeline stages = processes = GPUs")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--fp8", action="store_true", help="fp8-e4m3 weights")
+    ap.add_argument("--kv-dtype", choices=["bf16", "fp8"], default="bf16",
+                    help="KV cache element type (fp8 = e4m3, half the bytes)")
     ap.add_argument("--window", type=int, default=0, help="attention-sink window length (0=full)")
     ap.add_argument("--sinks", type=int, default=0, help="attention-sink tokens")
     ap.add_argument("--block-size", type=int, default=64)
@@ -47,7 +49,7 @@ def engine_config(a):
         model=a.model, checkpoint=a.checkpoint, random_init=a.checkpoint is None, seed=a.seed,
         quantize=a.fp8, pp=a.gpus,
         cache=CacheConfig(block_size=a.block_size, gpu_memory_utilization=a.gpu_mem,
-                          window_length=a.window, num_sink_tokens=a.sinks),
+                          window_length=a.window, num_sink_tokens=a.sinks, dtype=a.kv_dtype),
         serve=ServeConfig(max_batch_size=a.max_batch, max_num_batched_tokens=a.max_batched_tokens,
                           num_micro_batches=a.micro_batches, max_seq_len=a.max_seq_len,
                           use_graphs=not a.no_graphs))
@@ -72,7 +74,7 @@ def cmd_plan(a) -> int:
     for i, (s, e) in enumerate(ranges):
         w = (e - s) * per_layer + (emb if i == 0 else 0) + (emb if i == len(ranges) - 1 else 0)
         free = 288e9 * a.gpu_mem - w
-        kv_tok = KVPool.bytes_per_block(spec, e - s, 1)
+        kv_tok = KVPool.bytes_per_block(spec, e - s, 1, 1 if a.kv_dtype == "fp8" else 2)
         out.append(dict(stage=i, gpu=i, layers=[s, e], weights_gb=round(w / 1e9, 2),
                         kv_capacity_tokens=int(max(0, free) // kv_tok)))
     print(json.dumps({"model": spec.name, "num_layers": spec.num_layers, "stages": out}, indent=1))

@@ -307,11 +307,26 @@ class CacheConfig:
     window_length: int = 0
     num_sink_tokens: int = 0
     max_chunk: int = 512  # extra ring headroom so a prefill chunk never evicts keys it needs
-    dtype: str = "bf16"
+    dtype: str = "bf16"   # "bf16" | "fp8" (e4m3fn: half the decode-attention bytes, 2x tokens)
+    k_scale: float = 1.0  # fp8 cache stores k / k_scale and v / v_scale
+    v_scale: float = 1.0
+
+    def __post_init__(self):
+        if self.dtype not in ("bf16", "fp8"):
+            raise ValueError(f"KV cache dtype must be 'bf16' or 'fp8', got {self.dtype!r}")
 
     @property
     def windowed(self) -> bool:
         return self.window_length > 0
+
+    @property
+    def torch_dtype(self):
+        import torch
+        return torch.float8_e4m3fn if self.dtype == "fp8" else torch.bfloat16
+
+    @property
+    def dtype_bytes(self) -> int:
+        return 1 if self.dtype == "fp8" else 2
 
 
 @dataclass

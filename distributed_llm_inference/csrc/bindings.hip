@@ -119,8 +119,12 @@ void add(Tensor out, Tensor a, Tensor b) {
 }
 
 // ------------------------------------------------------------------------------ rope + cache
-void check_cache(const Tensor& k_cache, const Tensor& v_cache, int64_t nkv, int64_t D) {
-  CHECK_IN(k_cache); CHECK_IN(v_cache); CHECK_BF16(k_cache); CHECK_BF16(v_cache);
+// Returns true for an fp8 (e4m3fn) cache, false for bf16.
+bool check_cache(const Tensor& k_cache, const Tensor& v_cache, int64_t nkv, int64_t D) {
+  CHECK_IN(k_cache); CHECK_IN(v_cache);
+  const bool fp8 = k_cache.scalar_type() == at::kFloat8_e4m3fn;
+  TORCH_CHECK(fp8 || k_cache.scalar_type() == at::kBFloat16, "KV cache must be bf16 or fp8 e4m3fn");
+  TORCH_CHECK(v_cache.scalar_type() == k_cache.scalar_type(), "k/v caches must share a dtype");
   TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 5, "k_cache must be 4-D, v_cache 5-D");
   // k: [blocks, nkv, bs, D]; v: [blocks, nkv, bs/8, D, 8]
   TORCH_CHECK(k_cache.size(1) == nkv && k_cache.size(3) == D, "k_cache must be [blocks, nkv, bs, D]");
@@ -128,11 +132,13 @@ void check_cache(const Tensor& k_cache, const Tensor& v_cache, int64_t nkv, int6
                   v_cache.size(2) * 8 == k_cache.size(2) && v_cache.size(3) == D &&
                   v_cache.size(4) == 8,
               "v_cache must be [blocks, nkv, bs/8, D, 8]");
+  return fp8;
 }
 
 void rope_cache(Tensor qkv, optional<Tensor> positions, optional<Tensor> slot_mapping,
                 optional<Tensor> cos_sin, Tensor q_out, optional<Tensor> q_sink_out,
-                int64_t window, Tensor k_cache, Tensor v_cache, int64_t nh, int64_t nkv) {
+                int64_t window, Tensor k_cache, Tensor v_cache, int64_t nh, int64_t nkv,
+                double k_scale, double v_scale) {
   CHECK_DEV(qkv); CHECK_BF16(qkv);
   TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "qkv must be [T, *] with unit inner stride");
   const int64_t T = qkv.size(0);
@@ -140,8 +146,12 @@ void rope_cache(Tensor qkv, optional<Tensor> positions, optional<Tensor> slot_ma
   TORCH_CHECK(q_out.dim() == 3 && q_out.size(0) == T && q_out.size(1) == nh, "q_out must be [T, nh, D]");
   const int64_t D = q_out.size(2);
   TORCH_CHECK(qkv.size(1) >= (nh + 2 * nkv) * D, "qkv too narrow for nh/nkv/D");
-  check_cache(k_cache, v_cache, nkv, D);
+  const bool fp8 = check_cache(k_cache, v_cache, nkv, D);
+  TORCH_CHECK(k_scale > 0 && v_scale > 0, "KV scales must be positive");
   dli::RopeCacheParams p{};
+  p.kv_fp8 = fp8 ? 1 : 0;
+  p.k_inv_scale = (float)(1.0 / k_scale);
+  p.v_inv_scale = (float)(1.0 / v_scale);
   p.qkv = bp(qkv);
   p.qkv_stride = qkv.stride(0);
   if (positions.has_value()) {
@@ -169,8 +179,8 @@ void rope_cache(Tensor qkv, optional<Tensor> positions, optional<Tensor> slot_ma
     p.q_sink_out = bp(*q_sink_out);
   }
   p.window = (int)window;
-  p.k_cache = bp(k_cache);
-  p.v_cache = bp(v_cache);
+  p.k_cache = k_cache.data_ptr();
+  p.v_cache = v_cache.data_ptr();
   p.nh = (int)nh;
   p.nkv = (int)nkv;
   p.D = (int)D;
@@ -183,7 +193,7 @@ void rope_cache(Tensor qkv, optional<Tensor> positions, optional<Tensor> slot_ma
 dli::AttnParams attn_common(Tensor& out, Tensor& q, optional<Tensor>& q_sink, Tensor& k_cache,
                             Tensor& v_cache, Tensor& block_tables, Tensor& seq_lens, double scale,
                             int64_t n_sink, int64_t sink_pad, int64_t ring, int64_t window,
-                            int64_t& D) {
+                            double k_scale, double v_scale, int64_t& D) {
   CHECK_IN(out); CHECK_IN(q); CHECK_BF16(out); CHECK_BF16(q);
   TORCH_CHECK(q.dim() == 3, "q must be [T, nh, D]");
   TORCH_CHECK(out.sizes() == q.sizes(), "out must match q");
@@ -191,7 +201,8 @@ dli::AttnParams attn_common(Tensor& out, Tensor& q, optional<Tensor>& q_sink, Te
   D = q.size(2);
   const int64_t nkv = k_cache.size(1);
   TORCH_CHECK(nkv > 0 && nh % nkv == 0, "nh must be a multiple of nkv");
-  check_cache(k_cache, v_cache, nkv, D);
+  const bool fp8 = check_cache(k_cache, v_cache, nkv, D);
+  TORCH_CHECK(k_scale > 0 && v_scale > 0, "KV scales must be positive");
   CHECK_IN(block_tables); CHECK_I32(block_tables); CHECK_IN(seq_lens); CHECK_I32(seq_lens);
   TORCH_CHECK(block_tables.dim() == 2 && block_tables.size(0) == seq_lens.size(0),
               "block_tables must be [B, max_blocks]");
@@ -207,8 +218,11 @@ dli::AttnParams attn_common(Tensor& out, Tensor& q, optional<Tensor>& q_sink, Te
     TORCH_CHECK(q_sink->sizes() == q.sizes(), "q_sink must match q");
     p.q_sink = bp(*q_sink);
   }
-  p.k_cache = bp(k_cache);
-  p.v_cache = bp(v_cache);
+  p.k_cache = k_cache.data_ptr();
+  p.v_cache = v_cache.data_ptr();
+  p.kv_fp8 = fp8 ? 1 : 0;
+  p.k_scale = (float)k_scale;
+  p.v_scale = (float)v_scale;
   p.out = bp(out);
   p.block_tables = block_tables.data_ptr<int>();
   p.bt_stride = (int)block_tables.size(1);
@@ -229,10 +243,11 @@ dli::AttnParams attn_common(Tensor& out, Tensor& q, optional<Tensor>& q_sink, Te
 void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, Tensor v_cache,
                  Tensor block_tables, Tensor seq_lens, double scale, int64_t n_sink,
                  int64_t sink_pad, int64_t ring, int64_t window, int64_t num_splits,
-                 optional<Tensor> part_o, optional<Tensor> part_ml) {
+                 optional<Tensor> part_o, optional<Tensor> part_ml, double k_scale,
+                 double v_scale) {
   int64_t D = 0;
   auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
-                       sink_pad, ring, window, D);
+                       sink_pad, ring, window, k_scale, v_scale, D);
   const int64_t B = q.size(0);
   TORCH_CHECK(seq_lens.numel() == B, "decode: one token per sequence (seq_lens must have T entries)");
   TORCH_CHECK(num_splits >= 1, "num_splits >= 1");
@@ -251,10 +266,11 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
 
 void attn_prefill(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, Tensor v_cache,
                   Tensor block_tables, Tensor seq_lens, Tensor q_start, int64_t max_q,
-                  double scale, int64_t n_sink, int64_t sink_pad, int64_t ring, int64_t window) {
+                  double scale, int64_t n_sink, int64_t sink_pad, int64_t ring, int64_t window,
+                  double k_scale, double v_scale) {
   int64_t D = 0;
   auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
-                       sink_pad, ring, window, D);
+                       sink_pad, ring, window, k_scale, v_scale, D);
   CHECK_IN(q_start); CHECK_I32(q_start);
   const int64_t B = seq_lens.numel();
   TORCH_CHECK(q_start.numel() == B + 1, "q_start must have B+1 entries");

@@ -25,6 +25,8 @@
 //     re-rotation pass over the cache.
 #include "kernels.h"
 
+#include <type_traits>
+
 namespace dli {
 
 
@@ -68,23 +70,33 @@ struct KVFrag {
   bf16x8 v[D / 16];
 };
 
-//   kbase/vbase: start of this kv head's page in the K / V^T cache, offk: slot offset of the step
-//   inside the page.
-template <int D>
-__device__ __forceinline__ void attn_load(KVFrag<D>& f, const bf16* __restrict__ kbase,
-                                          const bf16* __restrict__ vbase, int offk) {
+//   kc/vc: the K / V^T caches, hb: element offset of this kv head's page, offk: slot offset of the
+//   step inside the page.  fp8 caches load 8 bytes per fragment and widen to bf16 in registers
+//   (exact), so both MFMA products stay bf16 x bf16.
+template <int D, bool FP8>
+__device__ __forceinline__ void attn_load(KVFrag<D>& f, const void* __restrict__ kc,
+                                          const void* __restrict__ vc, size_t hb, int offk) {
   const int lane = threadIdx.x & 63;
   const int col = lane & 15, h4 = lane >> 4;
   const int krow0 = offk + 8 * (col >> 2) + (col & 3);
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int c = 0; c < D / 32; ++c)
-      f.k[t][c] = *reinterpret_cast<const bf16x8*>(kbase + (size_t)(krow0 + 4 * t) * D + 32 * c +
-                                                   8 * h4);
+    for (int c = 0; c < D / 32; ++c) {
+      const size_t e = hb + (size_t)(krow0 + 4 * t) * D + 32 * c + 8 * h4;
+      if (FP8)
+        f.k[t][c] = fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(kc) + e));
+      else
+        f.k[t][c] = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(kc) + e);
+    }
 #pragma unroll
-  for (int e = 0; e < D / 16; ++e)
-    f.v[e] = *reinterpret_cast<const bf16x8*>(vbase + ((size_t)((offk >> 3) + h4) * D + 16 * e + col) * 8);
+  for (int e = 0; e < D / 16; ++e) {
+    const size_t o = hb + ((size_t)((offk >> 3) + h4) * D + 16 * e + col) * 8;
+    if (FP8)
+      f.v[e] = fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(vc) + o));
+    else
+      f.v[e] = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(vc) + o);
+  }
 }
 
 // One 32-key step of online-softmax attention for the 16 query columns held by this wave.
@@ -132,13 +144,12 @@ __device__ __forceinline__ void attn_compute(WaveState<D>& st, const bf16x8 (&qf
   }
 }
 
-template <int D>
+template <int D, bool FP8>
 __device__ __forceinline__ void attn_step(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
-                                          const bf16* __restrict__ kbase,
-                                          const bf16* __restrict__ vbase, int offk,
+                                          const void* kc, const void* vc, size_t hb, int offk,
                                           float scale_log2, unsigned valid_mask) {
   KVFrag<D> f;
-  attn_load<D>(f, kbase, vbase, offk);
+  attn_load<D, FP8>(f, kc, vc, hb, offk);
   attn_compute<D>(st, qf, f, scale_log2, valid_mask);
 }
 
@@ -167,7 +178,7 @@ __device__ __forceinline__ unsigned step_mask(int u0, int h4, int seg_base, int 
   return vm;
 }
 
-template <int D, bool WIN>
+template <int D, bool WIN, bool FP8>
 __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int items) {
   // wave-uniform by construction; readfirstlane tells hipcc so, which turns every index derived
   // from it (seq_lens, block-table entries) into scalar loads that never join the vmcnt queue
@@ -191,6 +202,9 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
   const int* bt = p.block_tables + (size_t)b * p.bt_stride;
   const size_t head_stride = (size_t)p.bs * D;  // per (block, kv head)
 
+  // fp8 caches: K's scale folds into the softmax scale, V's into the output
+  const float sl2 = FP8 ? p.scale_log2 * p.k_scale : p.scale_log2;
+  const float vsc = FP8 ? p.v_scale : 1.f;
   WaveState<D> st;
   st.init();
   if (L > 0) {
@@ -217,7 +231,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
         const int u0 = seg_base + sidx * 32;
         const int page = bt[u0 / p.bs];
         const size_t hb = ((size_t)page * p.nkv + kvh) * head_stride;
-        attn_load<D>(f, p.k_cache + hb, p.v_cache + hb, u0 % p.bs);
+        attn_load<D, FP8>(f, p.k_cache, p.v_cache, hb, u0 % p.bs);
       };
       KVFrag<D> fa, fb;
       load(fa, s_lo);
@@ -226,12 +240,12 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
       for (int sidx = s_lo; sidx < s_hi; sidx += 2) {
         load(fb, min(sidx + 1, s_hi - 1));
         __builtin_amdgcn_sched_barrier(0);
-        attn_compute<D>(st, qf, fa, p.scale_log2,
+        attn_compute<D>(st, qf, fa, sl2,
                         step_mask<D, WIN>(seg_base + sidx * 32, h4, seg_base, seg_len, L, p));
         load(fa, min(sidx + 2, s_hi - 1));
         __builtin_amdgcn_sched_barrier(0);
         if (sidx + 1 < s_hi)
-          attn_compute<D>(st, qf, fb, p.scale_log2,
+          attn_compute<D>(st, qf, fb, sl2,
                           step_mask<D, WIN>(seg_base + (sidx + 1) * 32, h4, seg_base, seg_len, L, p));
       }
     }
@@ -249,7 +263,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
         unsigned vm = 0;
 #pragma unroll
         for (int j = 0; j < 8; ++j) vm |= ((u0 + 8 * h4 + j) < nS ? 1u : 0u) << j;
-        attn_step<D>(st, qs, p.k_cache + hb, p.v_cache + hb, u0 % p.bs, p.scale_log2, vm);
+        attn_step<D, FP8>(st, qs, p.k_cache, p.v_cache, hb, u0 % p.bs, sl2, vm);
       }
     }
   }
@@ -260,7 +274,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
   if (!col_valid) return;
   const int head = kvh * G + g0 + col;
   if (splits == 1) {
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    const float inv = lsum > 0.f ? vsc / lsum : 0.f;
     bf16* orow = p.out + ((size_t)b * p.nh + head) * D;
 #pragma unroll
     for (int e = 0; e < D / 16; ++e) {
@@ -274,7 +288,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
     const size_t r0 = ((size_t)split * T + b) * p.nh + head;
     float* prow = p.part_o + r0 * D;
 #pragma unroll
-    for (int e = 0; e < D / 16; ++e) *reinterpret_cast<f32x4*>(prow + 16 * e + 4 * h4) = st.o[e];
+    for (int e = 0; e < D / 16; ++e) *reinterpret_cast<f32x4*>(prow + 16 * e + 4 * h4) = st.o[e] * vsc;
     if (h4 == 0) {
       p.part_ml[r0 * 2] = st.m;
       p.part_ml[r0 * 2 + 1] = lsum;
@@ -323,7 +337,7 @@ __device__ __forceinline__ int kswz(int row) {
   return ((row & 3) | (((row >> 3) & 3) << 2)) & (CH - 1);
 }
 
-template <int D, bool WIN>
+template <int D, bool WIN, bool FP8>
 __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw) {
   constexpr int CH = D / 8;            // 16-B units per K row
   constexpr int UNITS = 32 * CH;       // 16-B units per K tile (= per V^T tile)
@@ -380,20 +394,27 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw
   };
 
   typedef int i32x4v __attribute__((ext_vector_type(4)));
-  i32x4v rk[UPT], rv[UPT];
+  // staging registers: one 8-element unit per tile unit (16 B bf16, or 8 B fp8 widened to bf16
+  // when written to LDS, so the LDS tiles and everything after them are bf16 either way)
+  typedef typename std::conditional<FP8, uint2, i32x4v>::type Unit;
+  Unit rk[UPT], rv[UPT];
   auto gload = [&](int sidx) {
     const int u0 = slot0(sidx);
     const int page = bt[u0 / p.bs];
     const int offk = u0 % p.bs;
-    const size_t hb = ((size_t)page * p.nkv + kvh) * head_stride;
-    const bf16* ks = p.k_cache + hb + (size_t)offk * D;   // 32 rows x D, contiguous
-    const bf16* vs = p.v_cache + hb + (size_t)offk * D;   // 4 groups x D x 8, contiguous
+    // 32 K rows x D and 4 V^T groups x D x 8, both contiguous from element offset `e0`
+    const size_t e0 = ((size_t)page * p.nkv + kvh) * head_stride + (size_t)offk * D;
 #pragma unroll
     for (int i = 0; i < UPT; ++i) {
       const int u = threadIdx.x + i * 256;
       if (UNITS % 256 == 0 || u < UNITS) {
-        rk[i] = *reinterpret_cast<const i32x4v*>(ks + (size_t)u * 8);
-        rv[i] = *reinterpret_cast<const i32x4v*>(vs + (size_t)u * 8);
+        if constexpr (FP8) {
+          rk[i] = *reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(p.k_cache) + e0 + (size_t)u * 8);
+          rv[i] = *reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(p.v_cache) + e0 + (size_t)u * 8);
+        } else {
+          rk[i] = *reinterpret_cast<const i32x4v*>(static_cast<const bf16*>(p.k_cache) + e0 + (size_t)u * 8);
+          rv[i] = *reinterpret_cast<const i32x4v*>(static_cast<const bf16*>(p.v_cache) + e0 + (size_t)u * 8);
+        }
       }
     }
   };
@@ -403,11 +424,20 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw
       const int u = threadIdx.x + i * 256;
       if (UNITS % 256 == 0 || u < UNITS) {
         const int row = u / CH, ch = u % CH;
-        *reinterpret_cast<i32x4v*>(&smem[buf][0][(row * CH + (ch ^ kswz<D>(row))) * 8]) = rk[i];
-        *reinterpret_cast<i32x4v*>(&smem[buf][1][u * 8]) = rv[i];
+        bf16x8* kd = reinterpret_cast<bf16x8*>(&smem[buf][0][(row * CH + (ch ^ kswz<D>(row))) * 8]);
+        bf16x8* vd = reinterpret_cast<bf16x8*>(&smem[buf][1][u * 8]);
+        if constexpr (FP8) {
+          *kd = fp8x8_to_bf16x8(rk[i]);
+          *vd = fp8x8_to_bf16x8(rv[i]);
+        } else {
+          *kd = __builtin_bit_cast(bf16x8, rk[i]);
+          *vd = __builtin_bit_cast(bf16x8, rv[i]);
+        }
       }
     }
   };
+  const float sl2 = FP8 ? p.scale_log2 * p.k_scale : p.scale_log2;
+  const float vsc = FP8 ? p.v_scale : 1.f;
 
   WaveState<D> st;
   st.init();
@@ -455,9 +485,9 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw
       vm |= (ok ? 1u : 0u) << j;
     }
     if (sink_step)
-      attn_compute<D>(st, qsf, f, p.scale_log2, vm);
+      attn_compute<D>(st, qsf, f, sl2, vm);
     else
-      attn_compute<D>(st, qf, f, p.scale_log2, vm);
+      attn_compute<D>(st, qf, f, sl2, vm);
     if (sidx + 1 < nsteps) swrite(buf ^ 1);
     __syncthreads();
   }
@@ -465,7 +495,7 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
   if (col_valid) {
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    const float inv = lsum > 0.f ? vsc / lsum : 0.f;
     bf16* orow = p.out + ((size_t)(qs0 + tok) * p.nh + qh) * D;
 #pragma unroll
     for (int e = 0; e < D / 16; ++e) {
@@ -485,10 +515,13 @@ static int launch_decode_d(const AttnParams& p, int B, hipStream_t stream) {
   const long items = (long)B * p.nkv * hgroups * p.num_splits;
   if (items > (1L << 30)) return -3;
   const int grid = (int)((items + 3) / 4);
-  if (p.ring > 0)
-    attn_decode_kernel<D, true><<<grid, 256, 0, stream>>>(p, (int)items);
-  else
-    attn_decode_kernel<D, false><<<grid, 256, 0, stream>>>(p, (int)items);
+  if (p.ring > 0) {
+    if (p.kv_fp8) attn_decode_kernel<D, true, true><<<grid, 256, 0, stream>>>(p, (int)items);
+    else attn_decode_kernel<D, true, false><<<grid, 256, 0, stream>>>(p, (int)items);
+  } else {
+    if (p.kv_fp8) attn_decode_kernel<D, false, true><<<grid, 256, 0, stream>>>(p, (int)items);
+    else attn_decode_kernel<D, false, false><<<grid, 256, 0, stream>>>(p, (int)items);
+  }
   if (p.num_splits > 1) attn_combine_kernel<D><<<B * p.nh, D, 0, stream>>>(p, B);
   return 0;
 }
@@ -510,10 +543,13 @@ static int launch_prefill_d(const AttnParams& p, int B, int max_q, hipStream_t s
   const int hpw = (G % 4 == 0) ? 4 : (G % 2 == 0 ? 2 : 1);  // q heads sharing each K/V tile
   const int tpw = 4 / hpw;
   dim3 grid((max_q + 16 * tpw - 1) / (16 * tpw), p.nkv * (G / hpw), B);
-  if (p.ring > 0)
-    attn_prefill_kernel<D, true><<<grid, 256, 0, stream>>>(p, hpw);
-  else
-    attn_prefill_kernel<D, false><<<grid, 256, 0, stream>>>(p, hpw);
+  if (p.ring > 0) {
+    if (p.kv_fp8) attn_prefill_kernel<D, true, true><<<grid, 256, 0, stream>>>(p, hpw);
+    else attn_prefill_kernel<D, true, false><<<grid, 256, 0, stream>>>(p, hpw);
+  } else {
+    if (p.kv_fp8) attn_prefill_kernel<D, false, true><<<grid, 256, 0, stream>>>(p, hpw);
+    else attn_prefill_kernel<D, false, false><<<grid, 256, 0, stream>>>(p, hpw);
+  }
   return 0;
 }
 

@@ -63,6 +63,31 @@ __device__ __forceinline__ float block_reduce_max(float v, float* scratch) {
   return r;
 }
 
+// ---- fp8 e4m3 (OCP "fn" encoding: gfx950's native fp8, identical to torch.float8_e4m3fn) ------
+// 4 floats -> 4 packed fp8 bytes (saturating conversion in hardware).
+__device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d) {
+  int r = 0;
+  r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, r, false);
+  r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+  return (unsigned)r;
+}
+
+// 8 packed fp8 bytes -> 8 bf16 (exact: every e4m3 value is representable in bf16).
+__device__ __forceinline__ bf16x8 fp8x8_to_bf16x8(uint2 v) {
+  const f32x2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)v.x, false);
+  const f32x2 b = __builtin_amdgcn_cvt_pk_f32_fp8((int)v.x, true);
+  const f32x2 c = __builtin_amdgcn_cvt_pk_f32_fp8((int)v.y, false);
+  const f32x2 d = __builtin_amdgcn_cvt_pk_f32_fp8((int)v.y, true);
+  bf16x8 o;
+  o[0] = (bf16)a[0]; o[1] = (bf16)a[1]; o[2] = (bf16)b[0]; o[3] = (bf16)b[1];
+  o[4] = (bf16)c[0]; o[5] = (bf16)c[1]; o[6] = (bf16)d[0]; o[7] = (bf16)d[1];
+  return o;
+}
+
+__device__ __forceinline__ uint8_t f32_to_fp8(float x) {
+  return (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(x, 0.f, 0, false) & 0xff);
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
 __device__ __forceinline__ float gelu_tanh(float x) {

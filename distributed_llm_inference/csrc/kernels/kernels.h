@@ -7,8 +7,10 @@ namespace dli {
 struct AttnParams {
   const bf16* q;        // [T, nh, D]
   const bf16* q_sink;   // [T, nh, D] or nullptr (window mode only)
-  const bf16* k_cache;  // [blocks, nkv, bs, D]
-  const bf16* v_cache;  // [blocks, nkv, bs/8, D, 8]  (V^T in 8-key groups)
+  const void* k_cache;  // [blocks, nkv, bs, D]           bf16, or fp8 e4m3 if kv_fp8
+  const void* v_cache;  // [blocks, nkv, bs/8, D, 8]      (V^T in 8-key groups), same dtype
+  int kv_fp8;           // caches hold fp8 e4m3: stored = x / scale
+  float k_scale, v_scale;
   bf16* out;            // [T, nh, D]
   const int* block_tables;  // [B, bt_stride]
   int bt_stride;
@@ -32,8 +34,10 @@ struct RopeCacheParams {
   bf16* q_out;            // [T, nh, D]
   bf16* q_sink_out;       // [T, nh, D] or nullptr
   int window;             // > 0: q_sink rotated at min(pos, window-1)
-  bf16* k_cache;          // [blocks, nkv, bs, D]
-  bf16* v_cache;          // [blocks, nkv, bs/8, D, 8]
+  void* k_cache;          // [blocks, nkv, bs, D]        bf16, or fp8 e4m3 if kv_fp8
+  void* v_cache;          // [blocks, nkv, bs/8, D, 8]
+  int kv_fp8;
+  float k_inv_scale, v_inv_scale;  // fp8: stored = x * inv_scale
   int nh, nkv, D, bs;
 };
 

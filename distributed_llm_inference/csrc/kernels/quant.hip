@@ -11,13 +11,6 @@ namespace dli {
 
 constexpr float kFp8Max = 448.f;
 
-__device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d) {
-  int r = 0;
-  r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, r, false);
-  r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
-  return (unsigned)r;
-}
-
 // Row amax -> scale, then quantise the VPT x 8 register-resident values of each thread (vector
 // index threadIdx.x + i * blockDim.x) and store them as 8-byte fp8 groups.
 template <int VPT>

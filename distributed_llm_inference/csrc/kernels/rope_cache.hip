@@ -11,6 +11,7 @@
 //     reference's key re-rotation (cache.py:21-48, 111-124) expressed on the query side, so no
 //     cached key is ever re-rotated;
 //   * rotates k and scatters it into the paged K cache [blocks, nkv, bs, D];
+//   * with an fp8 KV cache, k and v are stored as e4m3 (x * inv_scale), converted in registers;
 //   * scatters v into the paged V^T cache [blocks, nkv, bs/8, D, 8] (8-key groups) — the MFMA
 //     P·V product reads 8 consecutive keys of one d as a 16-byte-per-lane operand (attention.hip),
 //     and one token's write stays inside 16 cache lines per head instead of D (one per d row).
@@ -37,6 +38,7 @@ __device__ __forceinline__ void rotate4(const bf16x4& a, const bf16x4& b, const 
 // latency-bound, not bandwidth-bound, at one workgroup per token.
 constexpr int kHeadsPerWG = 8;
 
+template <bool FP8>
 __global__ void __launch_bounds__(128) rope_cache_kernel(RopeCacheParams p) {
   const int t = blockIdx.x;
   const int h_lo = blockIdx.y * kHeadsPerWG;
@@ -86,25 +88,36 @@ __global__ void __launch_bounds__(128) rope_cache_kernel(RopeCacheParams p) {
       }
     } else if (slot >= 0) {
       const int kh = head - p.nh;
-      bf16* dst = p.k_cache + (((size_t)blk * p.nkv + kh) * p.bs + off) * D;
-      *reinterpret_cast<bf16x4*>(dst + i) = oa;
-      *reinterpret_cast<bf16x4*>(dst + half + i) = ob;
+      const size_t base = (((size_t)blk * p.nkv + kh) * p.bs + off) * D;
+      if (FP8) {
+        uint8_t* dst = static_cast<uint8_t*>(p.k_cache) + base;
+        const float s = p.k_inv_scale;
+        *reinterpret_cast<unsigned*>(dst + i) =
+            pack4_fp8((float)oa[0] * s, (float)oa[1] * s, (float)oa[2] * s, (float)oa[3] * s);
+        *reinterpret_cast<unsigned*>(dst + half + i) =
+            pack4_fp8((float)ob[0] * s, (float)ob[1] * s, (float)ob[2] * s, (float)ob[3] * s);
+      } else {
+        bf16* dst = static_cast<bf16*>(p.k_cache) + base;
+        *reinterpret_cast<bf16x4*>(dst + i) = oa;
+        *reinterpret_cast<bf16x4*>(dst + half + i) = ob;
+      }
     }
   }
-  // ---- v heads (V^T scatter) ---------------------------------------------------------
+  // ---- v heads (V^T scatter) ----------------------------------------------------------------
+  // one element per lane, consecutive lanes -> consecutive d: in the [bs/8, D, 8] layout the 8
+  // lanes d0..d0+7 store into ONE 128-B line (16-B stride, same key slot), so a wave's store
+  // instruction touches 8 lines instead of 64
   if (slot >= 0 && h_hi > n_qk) {
-    const int vpr = D >> 3;
-    const int v_lo = max(h_lo - n_qk, 0) * vpr, v_hi = (h_hi - n_qk) * vpr;
+    const int v_lo = max(h_lo - n_qk, 0) * D, v_hi = (h_hi - n_qk) * D;
     const bf16* vsrc = row + (size_t)n_qk * D;
+    const size_t grp = ((size_t)blk * p.nkv) * (p.bs >> 3) + (off >> 3);
     for (int it = v_lo + threadIdx.x; it < v_hi; it += blockDim.x) {
-      const int kh = it / vpr;
-      const int d0 = (it % vpr) * 8;
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(vsrc + (size_t)kh * D + d0);
-      // [bs/8, D, 8] layout: the 8 values land 16 B apart inside one 128-B line
-      bf16* dst = p.v_cache + ((((size_t)blk * p.nkv + kh) * (p.bs >> 3) + (off >> 3)) * D + d0) * 8 +
-                  (off & 7);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dst[j * 8] = v[j];
+      const int kh = it / D, d = it % D;
+      const size_t e = ((grp + (size_t)kh * (p.bs >> 3)) * D + d) * 8 + (off & 7);
+      if (FP8)
+        static_cast<uint8_t*>(p.v_cache)[e] = f32_to_fp8((float)vsrc[it] * p.v_inv_scale);
+      else
+        static_cast<bf16*>(p.v_cache)[e] = vsrc[it];
     }
   }
 }
@@ -114,7 +127,10 @@ int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stre
   if (p.D % 8 != 0 || p.qkv_stride % 4 != 0) return -1;
   const int heads = p.nh + 2 * p.nkv;
   dim3 grid(num_tokens, (heads + kHeadsPerWG - 1) / kHeadsPerWG);
-  rope_cache_kernel<<<grid, 128, 0, stream>>>(p);
+  if (p.kv_fp8)
+    rope_cache_kernel<true><<<grid, 128, 0, stream>>>(p);
+  else
+    rope_cache_kernel<false><<<grid, 128, 0, stream>>>(p);
   return 0;
 }
 

@@ -91,6 +91,9 @@ class AttnMetadata:
     sink_pad: int = 0
     ring: int = 0
     window: int = 0
+    # fp8 KV cache scales (stored = x / scale); 1.0 for bf16 caches
+    k_scale: float = 1.0
+    v_scale: float = 1.0
     # rows (token index) whose hidden state feeds the LM head, or None = all rows
     logits_rows: Optional[torch.Tensor] = None
 

@@ -58,15 +58,18 @@ class GPT2Layer(nn.Module):
         qkv = self.c_attn(normed)
         q, q_sink = ops.rope_cache(qkv, meta.positions, meta.slot_mapping, None, self.num_heads,
                                    self.num_heads, self.head_dim, k_cache, v_cache,
-                                   window=meta.window, want_sink=meta.want_sink)
+                                   window=meta.window, want_sink=meta.want_sink,
+                                   k_scale=meta.k_scale, v_scale=meta.v_scale)
         if meta.is_decode:
             o = ops.attn_decode(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
                                 self.scale, meta.n_sink, meta.sink_pad, meta.ring, meta.window,
-                                num_splits=meta.num_splits, workspace=meta.workspace)
+                                num_splits=meta.num_splits, workspace=meta.workspace,
+                                k_scale=meta.k_scale, v_scale=meta.v_scale)
         else:
             o = ops.attn_prefill(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
                                  meta.q_start, meta.max_q, self.scale, meta.n_sink, meta.sink_pad,
-                                 meta.ring, meta.window)
+                                 meta.ring, meta.window, k_scale=meta.k_scale,
+                                 v_scale=meta.v_scale)
         attn = self.attn_proj(o.view(T, -1))
         normed, residual = self.ln_2(attn, residual,
                                      residual_out=torch.empty_like(residual) if first else None)

@@ -39,9 +39,16 @@ class KVPool:
 
     def __init__(self, spec: ModelSpec, num_layers: int, num_blocks: int, block_size: int = 64,
                  device=None, dtype=torch.bfloat16, window_length: int = 0,
-                 num_sink_tokens: int = 0, max_chunk: int = 512):
+                 num_sink_tokens: int = 0, max_chunk: int = 512, k_scale: float = 1.0,
+                 v_scale: float = 1.0):
+        """``dtype`` bf16, or ``torch.float8_e4m3fn`` for an fp8 cache that stores k / k_scale
+        and v / v_scale (half the bytes the decode attention streams, twice the tokens)."""
         if block_size % 32:
             raise ValueError("block_size must be a multiple of 32")
+        if dtype not in (torch.bfloat16, torch.float8_e4m3fn):
+            raise ValueError(f"unsupported KV cache dtype {dtype}")
+        self.dtype = dtype
+        self.k_scale, self.v_scale = float(k_scale), float(v_scale)
         self.spec = spec
         self.num_layers = num_layers
         self.block_size = block_size
@@ -60,12 +67,19 @@ class KVPool:
 
     @classmethod
     def size_from_memory(cls, spec: ModelSpec, num_layers: int, block_size: int,
-                         free_bytes: int, utilization: float, reserve_bytes: int = 0) -> int:
-        per = cls.bytes_per_block(spec, num_layers, block_size)
+                         free_bytes: int, utilization: float, reserve_bytes: int = 0,
+                         dtype_bytes: int = 2) -> int:
+        per = cls.bytes_per_block(spec, num_layers, block_size, dtype_bytes)
         return max(1, int((free_bytes * utilization - reserve_bytes) // per))
 
     def layer(self, i: int) -> Tuple[torch.Tensor, torch.Tensor]:
         return self.k[i], self.v[i]
+
+    def attn_params(self) -> Dict[str, float]:
+        """Everything the attention kernels need besides the batch: window policy + KV scales."""
+        d = dict(self.window_params())
+        d.update(k_scale=self.k_scale, v_scale=self.v_scale)
+        return d
 
     # window policy exposed to AttnMetadata
     def window_params(self) -> Dict[str, int]:
@@ -96,7 +110,7 @@ class KVPool:
                   list(pos_offsets) if pos_offsets is not None else [])
         dev = self.device
         is_decode = all(q == 1 for q in q_lens)
-        wp = self.window_params()
+        wp = self.attn_params()
         if num_splits is None:
             max_len = int(sl.max()) if B else 1
             num_splits = ops.decode_splits(B, self.spec.num_kv_heads, self.spec.group_size,

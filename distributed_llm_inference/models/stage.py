@@ -66,9 +66,11 @@ class CausalLMStage(nn.Module):
         return self
 
     def make_pool(self, num_blocks: int, block_size: int = 64, window_length: int = 0,
-                  num_sink_tokens: int = 0, max_chunk: int = 512) -> KVPool:
+                  num_sink_tokens: int = 0, max_chunk: int = 512,
+                  kv_dtype: torch.dtype = torch.bfloat16, k_scale: float = 1.0,
+                  v_scale: float = 1.0) -> KVPool:
         return KVPool(self.spec, self.num_layers, num_blocks, block_size, self.device,
-                      torch.bfloat16, window_length, num_sink_tokens, max_chunk)
+                      kv_dtype, window_length, num_sink_tokens, max_chunk, k_scale, v_scale)
 
     def forward(self, inputs: torch.Tensor, meta: AttnMetadata, pool: KVPool) -> torch.Tensor:
         """``inputs``: token ids [T] (stage 0) or hidden states [T, H].  Returns hidden [T, H]

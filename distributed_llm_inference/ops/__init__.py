@@ -109,11 +109,13 @@ def rope_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
                slot_mapping: Optional[torch.Tensor], cos_sin: Optional[torch.Tensor], nh: int,
                nkv: int, head_dim: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
                window: int = 0, want_sink: bool = False, q_out: Optional[torch.Tensor] = None,
-               q_sink_out: Optional[torch.Tensor] = None):
-    """Rotate q/k, write k/v to the paged cache; returns ``(q [T, nh, D], q_sink or None)``."""
+               q_sink_out: Optional[torch.Tensor] = None, k_scale: float = 1.0,
+               v_scale: float = 1.0):
+    """Rotate q/k, write k/v to the paged cache; returns ``(q [T, nh, D], q_sink or None)``.
+    fp8 (e4m3fn) caches store ``k / k_scale`` and ``v / v_scale``."""
     if not _gpu(qkv):
         q, qs = ref.rope_cache(qkv, positions, slot_mapping, cos_sin, nh, nkv, head_dim, k_cache,
-                               v_cache, window, want_sink)
+                               v_cache, window, want_sink, k_scale, v_scale)
         if q_out is not None:
             q_out.copy_(q)
             q = q_out
@@ -128,7 +130,7 @@ def rope_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
         q_sink_out = torch.empty_like(q_out)
     native().rope_cache(qkv, positions, slot_mapping, cos_sin, q_out,
                         q_sink_out if want_sink else None, int(window), k_cache, v_cache,
-                        int(nh), int(nkv))
+                        int(nh), int(nkv), float(k_scale), float(v_scale))
     return q_out, (q_sink_out if want_sink else None)
 
 
@@ -146,10 +148,10 @@ def decode_splits(batch: int, nkv: int, group: int, max_len: int, cu: int = 256)
 
 
 def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink=0, sink_pad=0,
-                ring=0, window=0, num_splits=1, workspace=None, out=None):
+                ring=0, window=0, num_splits=1, workspace=None, out=None, k_scale=1.0, v_scale=1.0):
     if not _gpu(q):
         y = ref.attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
-                            sink_pad, ring, window)
+                            sink_pad, ring, window, k_scale, v_scale)
         return out.copy_(y) if out is not None else y
     out = torch.empty_like(q) if out is None else out
     part_o = part_ml = None
@@ -162,20 +164,20 @@ def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_si
             part_o, part_ml = workspace
     native().attn_decode(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, float(scale),
                          int(n_sink), int(sink_pad), int(ring), int(window), int(num_splits),
-                         part_o, part_ml)
+                         part_o, part_ml, float(k_scale), float(v_scale))
     return out
 
 
 def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, max_q, scale,
-                 n_sink=0, sink_pad=0, ring=0, window=0, out=None):
+                 n_sink=0, sink_pad=0, ring=0, window=0, out=None, k_scale=1.0, v_scale=1.0):
     if not _gpu(q):
         y = ref.attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, scale,
-                             n_sink, sink_pad, ring, window)
+                             n_sink, sink_pad, ring, window, k_scale, v_scale)
         return out.copy_(y) if out is not None else y
     out = torch.empty_like(q) if out is None else out
     native().attn_prefill(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start,
                           int(max_q), float(scale), int(n_sink), int(sink_pad), int(ring),
-                          int(window))
+                          int(window), float(k_scale), float(v_scale))
     return out
 
 

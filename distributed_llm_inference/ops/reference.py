@@ -6,7 +6,7 @@ They serve two purposes only:
 On a GPU tensor the HIP kernels are ALWAYS used (``ops/__init__.py`` never falls back silently).
 
 Cache layouts are identical to the kernels':
-  k_cache [num_blocks, nkv, block_size, D],
+  k_cache [num_blocks, nkv, block_size, D] (bf16, or fp8 e4m3fn storing k / k_scale),
   v_cache [num_blocks, nkv, block_size/8, D, 8] (V^T in 8-key groups: element (key, d) at
   [key // 8, d, key % 8]).
 """
@@ -66,8 +66,8 @@ def _rotate(x: torch.Tensor, cs: torch.Tensor) -> torch.Tensor:
 def rope_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
                slot_mapping: Optional[torch.Tensor], cos_sin: Optional[torch.Tensor],
                nh: int, nkv: int, D: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
-               window: int = 0, want_sink: bool = False
-               ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+               window: int = 0, want_sink: bool = False, k_scale: float = 1.0,
+               v_scale: float = 1.0) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     T = qkv.shape[0]
     q = qkv[:, : nh * D].reshape(T, nh, D)
     k = qkv[:, nh * D: (nh + nkv) * D].reshape(T, nkv, D)
@@ -92,19 +92,25 @@ def rope_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
         ok = sm >= 0
         if ok.any():
             blk, off = sm[ok] // bs, sm[ok] % bs
-            k_cache[blk, :, off, :] = kr[ok]
-            v_cache[blk, :, off // 8, :, off % 8] = v[ok]
+            if k_cache.dtype == torch.bfloat16:
+                k_cache[blk, :, off, :] = kr[ok]
+                v_cache[blk, :, off // 8, :, off % 8] = v[ok]
+            else:  # fp8 cache: stored = x / scale (from the bf16-rounded value, as the kernel)
+                k_cache[blk, :, off, :] = (kr[ok].float() / k_scale).to(k_cache.dtype)
+                v_cache[blk, :, off // 8, :, off % 8] = (v[ok].float() / v_scale).to(v_cache.dtype)
     return qr.contiguous(), (q_sink.contiguous() if q_sink is not None else None)
 
 
 # ----------------------------------------------------------------------------- attention
-def _gather_seq(k_cache, v_cache, block_table, nslots):
-    """Return K [nslots, nkv, D], V [nslots, nkv, D] in slot order."""
+def _gather_seq(k_cache, v_cache, block_table, nslots, k_scale=1.0, v_scale=1.0):
+    """Return K [nslots, nkv, D], V [nslots, nkv, D] in slot order (fp8 caches dequantised)."""
     bs = k_cache.shape[2]
     nb = (nslots + bs - 1) // bs
     blocks = block_table[:nb].long()
     K = k_cache[blocks].permute(0, 2, 1, 3).reshape(nb * bs, k_cache.shape[1], -1)[:nslots]
     V = v_cache[blocks].permute(0, 2, 4, 1, 3).reshape(nb * bs, v_cache.shape[1], -1)[:nslots]
+    if K.dtype != torch.bfloat16 and K.dtype != torch.float32:
+        K, V = K.float() * k_scale, V.float() * v_scale
     return K, V
 
 
@@ -151,7 +157,7 @@ def _attend_one(q_cols: torch.Tensor, q_sink_cols: Optional[torch.Tensor], qpos:
 
 
 def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale,
-                n_sink=0, sink_pad=0, ring=0, window=0) -> torch.Tensor:
+                n_sink=0, sink_pad=0, ring=0, window=0, k_scale=1.0, v_scale=1.0) -> torch.Tensor:
     B, nh, D = q.shape
     out = torch.zeros_like(q)
     for b in range(B):
@@ -159,7 +165,7 @@ def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale,
         if L <= 0:
             continue
         nslots = L if ring <= 0 else (L if L <= n_sink else sink_pad + min(ring, L - n_sink))
-        K, V = _gather_seq(k_cache, v_cache, block_tables[b], nslots)
+        K, V = _gather_seq(k_cache, v_cache, block_tables[b], nslots, k_scale, v_scale)
         qpos = torch.tensor([L - 1], device=q.device)
         o = _attend_one(q[b:b + 1], q_sink[b:b + 1] if q_sink is not None else None, qpos, K, V,
                         L, scale, n_sink, sink_pad, ring, window)
@@ -168,7 +174,7 @@ def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale,
 
 
 def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, scale,
-                 n_sink=0, sink_pad=0, ring=0, window=0) -> torch.Tensor:
+                 n_sink=0, sink_pad=0, ring=0, window=0, k_scale=1.0, v_scale=1.0) -> torch.Tensor:
     out = torch.zeros_like(q)
     B = seq_lens.numel()
     for b in range(B):
@@ -178,7 +184,7 @@ def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, s
             continue
         L = int(seq_lens[b])
         nslots = L if ring <= 0 else (L if L <= n_sink else sink_pad + min(ring, L - n_sink))
-        K, V = _gather_seq(k_cache, v_cache, block_tables[b], nslots)
+        K, V = _gather_seq(k_cache, v_cache, block_tables[b], nslots, k_scale, v_scale)
         qpos = torch.arange(L - ql, L, device=q.device)
         o = _attend_one(q[s0:s1], q_sink[s0:s1] if q_sink is not None else None, qpos, K, V, L,
                         scale, n_sink, sink_pad, ring, window)

@@ -81,7 +81,7 @@ def build_executor(spec: ModelSpec, start: int, end: int, device: torch.device, 
             free, _ = torch.cuda.mem_get_info(device)
             num_blocks = KVPool.size_from_memory(spec, nlayers, cc.block_size, int(free * kv_share),
                                                  cc.gpu_memory_utilization,
-                                                 _activation_reserve(spec, sc))
+                                                 _activation_reserve(spec, sc), cc.dtype_bytes)
         else:
             num_blocks = 1024
         if num_blocks < 2:
@@ -92,7 +92,7 @@ def build_executor(spec: ModelSpec, start: int, end: int, device: torch.device, 
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
         num_blocks = int(t.item())
     pool = stage.make_pool(num_blocks, cc.block_size, cc.window_length, cc.num_sink_tokens,
-                           cc.max_chunk)
+                           cc.max_chunk, cc.torch_dtype, cc.k_scale, cc.v_scale)
     log.info("stage [%d,%d) on %s: %d KV blocks x %d tokens", start, end, device, num_blocks,
              cc.block_size)
     return StageExecutor(stage, pool, max_num_seqs=sc.max_batch_size,

@@ -186,8 +186,7 @@ class StageExecutor:
         self._hidden_in = torch.empty(max_num_seqs, H, dtype=torch.bfloat16, device=self.device) \
             if not stage.has_embed else None
         self._sample_out = torch.empty(max_num_seqs, dtype=torch.int32, device=self.device)
-        wp = pool.window_params()
-        self._wp = wp
+        self._wp = pool.attn_params()
         self._step_counter = 0
 
     # ------------------------------------------------------------------ capacity / bookkeeping

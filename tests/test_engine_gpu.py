@@ -167,3 +167,29 @@ def test_lookahead_equals_plain_decode_gpu(gpu):
             eng.pipeline.lookahead = la
             outs.append([s.output for s in eng.generate(PROMPTS, p)])
         assert outs[0] == outs[1]
+
+
+def test_fp8_kv_cache_engine_close_to_bf16(gpu):
+    stage = CausalLMStage(SPEC, 0, 4, device=gpu).init_random(21)
+    prompts = [list(range(1, 90)), [5, 6, 7]]
+
+    def run(kv_dtype):
+        pool = stage.make_pool(128, 64, kv_dtype=kv_dtype)
+        sids = [0, 1]
+        for s, p in zip(sids, prompts):
+            pool.manager.append(s, len(p))
+        meta = pool.build_metadata(sids, [len(p) for p in prompts])
+        meta.logits_rows = torch.tensor([88, 91], device=gpu)
+        ids = torch.tensor([t for p in prompts for t in p], dtype=torch.int32, device=gpu)
+        outs = [stage(ids, meta, pool).float().cpu()]
+        for toks in ([3, 4], [9, 10], [11, 12]):
+            for s in sids:
+                pool.manager.append(s, 1)
+            meta = pool.build_metadata(sids, [1, 1])
+            outs.append(stage(torch.tensor(toks, dtype=torch.int32, device=gpu), meta,
+                              pool).float().cpu())
+        return outs
+
+    a, b = run(torch.bfloat16), run(torch.float8_e4m3fn)
+    for x, y in zip(a, b):
+        assert ((x - y).norm() / x.norm()).item() < 0.08

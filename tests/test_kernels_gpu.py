@@ -264,3 +264,74 @@ def test_rms_norm_residual_out_of_place(gpu):
     _close(ro, x.float() + r0.float(), 1e-2, 1e-2, "residual_out")
     y_ref, _ = ref.rms_norm(x.cpu(), w.cpu(), 1e-5, residual=r0.cpu().clone())
     _close(y, y_ref, 2e-2, 1e-2, "rms_norm")
+
+
+# ------------------------------------------------------------------------------ fp8 KV cache
+F8 = torch.float8_e4m3fn
+
+
+def _make_cache_fp8(nblocks, nkv, bs, D, dev, ks, vs):
+    k, v = _make_cache(nblocks, nkv, bs, D, dev)
+    return (k.float() / ks).to(F8), (v.float() / vs).to(F8)
+
+
+@pytest.mark.parametrize("window", [0, 64])
+def test_rope_cache_fp8(gpu, window):
+    torch.manual_seed(11)
+    nh, nkv, D, T, bs, nblocks = 32, 8, 128, 29, 64, 8
+    qkv = torch.randn(T, (nh + 2 * nkv) * D, device=gpu, dtype=BF) * 3
+    pos = torch.randint(0, 300, (T,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(nblocks * bs, device=gpu)[:T].to(torch.int64)
+    cs = ref.build_cos_sin(D, 512, 500000.0, device=gpu)
+    ks, vs = 0.5, 2.0
+    k1, v1 = _make_cache_fp8(nblocks, nkv, bs, D, gpu, ks, vs)
+    k2, v2 = k1.clone().cpu(), v1.clone().cpu()
+    q, _ = ops.rope_cache(qkv, pos, slots, cs, nh, nkv, D, k1, v1, window=window,
+                          want_sink=window > 0, k_scale=ks, v_scale=vs)
+    q_r, _ = ref.rope_cache(qkv.cpu(), pos.cpu(), slots.cpu(), cs.cpu(), nh, nkv, D, k2, v2,
+                            window, window > 0, ks, vs)
+    _close(q, q_r, 2e-2, 1e-2, "q")
+    # the same fp8 encoding up to one rounding step of the bf16 intermediate
+    kd = (k1.float().cpu() - k2.float()).abs()
+    assert (kd <= 0.13 * k2.float().abs() + 1e-3).all(), kd.max()  # <= one e4m3 step
+    assert (kd > 0).float().mean() < 0.01  # and almost always bit-identical
+    assert torch.equal(v1.cpu().view(torch.uint8), v2.view(torch.uint8))
+
+
+@pytest.mark.parametrize("splits", [1, 3])
+def test_attn_decode_fp8_kv(gpu, splits):
+    torch.manual_seed(12)
+    nh, nkv, D, bs, B = 64, 8, 128, 64, 5
+    lens = torch.tensor([1, 33, 64, 257, 700], dtype=torch.int32)
+    max_blocks = (int(lens.max()) + bs - 1) // bs
+    nblocks = B * max_blocks
+    ks, vs = 0.25, 1.5
+    kc, vc = _make_cache_fp8(nblocks, nkv, bs, D, gpu, ks, vs)
+    bt = _tables(B, max_blocks, nblocks, gpu, seed=4)
+    q = torch.randn(B, nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    out = ops.attn_decode(q, None, kc, vc, bt, lens.to(gpu), scale, num_splits=splits,
+                          k_scale=ks, v_scale=vs)
+    out_r = ref.attn_decode(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, scale,
+                            k_scale=ks, v_scale=vs)
+    _close(out, out_r, 2e-2, 2e-2, "decode-fp8")
+
+
+def test_attn_prefill_fp8_kv(gpu):
+    torch.manual_seed(13)
+    nh, nkv, D, bs = 32, 8, 128, 64
+    q_lens, ctx = [5, 64, 130], [0, 10, 300]
+    lens = torch.tensor([a + b for a, b in zip(q_lens, ctx)], dtype=torch.int32)
+    B = len(q_lens)
+    q_start = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
+    max_blocks = (int(lens.max()) + bs - 1) // bs
+    ks, vs = 2.0, 0.5
+    kc, vc = _make_cache_fp8(B * max_blocks, nkv, bs, D, gpu, ks, vs)
+    bt = _tables(B, max_blocks, B * max_blocks, gpu, seed=5)
+    q = torch.randn(int(q_start[-1]), nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    out = ops.attn_prefill(q, None, kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens), scale,
+                           k_scale=ks, v_scale=vs)
+    out_r = ref.attn_prefill(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale,
+                             k_scale=ks, v_scale=vs)
+    _close(out, out_r, 2e-2, 2e-2, "prefill-fp8")

@@ -368,3 +368,30 @@ def test_plan_stages_minimises_slowest_stage():
                     edges = (0,) + cuts + (L,)
                     best = min(best, cost([edges[i + 1] - edges[i] for i in range(n)]))
                 assert got <= best + 1e-9, (name, n, w, got, best)
+
+
+def test_fp8_kv_cache_close_to_bf16_cpu():
+    """fp8 (e4m3) KV cache through the CPU reference path: same greedy tokens in the first steps
+    and logits close to the bf16 cache."""
+    from distributed_llm_inference.models import CausalLMStage
+    st = CausalLMStage(SPEC, 0, 4).init_random(5)
+    prompts = [[1, 2, 3, 4, 5, 6, 7, 8], [9, 8, 7]]
+
+    def logits(kv_dtype):
+        pool = st.make_pool(64, 32, kv_dtype=kv_dtype)
+        sids = [0, 1]
+        for s_, p_ in zip(sids, prompts):
+            pool.manager.append(s_, len(p_))
+        meta = pool.build_metadata(sids, [len(p_) for p_ in prompts],
+                                   logits_rows=torch.tensor([7, 10]))
+        ids = torch.tensor([t for p_ in prompts for t in p_])
+        out = [st(ids, meta, pool).float()]
+        for tok in ([3, 4], [5, 6]):
+            for s_ in sids:
+                pool.manager.append(s_, 1)
+            out.append(st(torch.tensor(tok), pool.build_metadata(sids, [1, 1]), pool).float())
+        return out
+
+    a, b = logits(torch.bfloat16), logits(torch.float8_e4m3fn)
+    for x, y in zip(a, b):
+        assert ((x - y).norm() / x.norm()).item() < 0.08
