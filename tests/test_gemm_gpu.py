@@ -7,12 +7,15 @@ from distributed_llm_inference import ops
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("M", [1, 37, 128, 256])
-@pytest.mark.parametrize("N,K", [(128, 128), (256, 1024), (384, 2048)])
-@pytest.mark.parametrize("bn,splits", [(128, 1), (64, 1), (128, 2), (64, 4)])
+_CASES = [(M, N, K, bn, splits)
+          for M in (1, 37, 128, 256)
+          for N, K in ((128, 128), (256, 1024), (384, 2048))
+          for bn, splits in ((128, 1), (64, 1), (128, 2), (64, 4))
+          if N % bn == 0 and (K // 64) % splits == 0]  # only tileable shapes
+
+
+@pytest.mark.parametrize("M,N,K,bn,splits", _CASES)
 def test_gemm_nt_matches_fp32(gpu, M, N, K, bn, splits):
-    if N % bn or (K // 64) % splits:
-        pytest.skip("shape not tileable")
     torch.manual_seed(M + N + K)
     x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
     w = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)

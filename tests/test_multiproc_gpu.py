@@ -1,10 +1,11 @@
 """Multi-process pipeline on the GPU (one process per stage).
 
-The box used for GPU tests has ONE MI355X, so stage processes share it (``DLI_SHARE_GPU=1``).
-RCCL refuses two ranks on the same device, so the full driver/follower GPU path (graphs, shm
-control plane, token feedback, micro-batching) is exercised with the host-staged transport, and the
-RCCL communicator itself is exercised by a same-device 2-rank smoke test that is skipped if RCCL
-rejects the duplicate device.  The 8-GPU xGMI run is the driver's round-end scaling bench.
+On a ONE-GPU box stage processes share the card (``DLI_SHARE_GPU=1``).  RCCL refuses two ranks on
+the same device, so there the full driver/follower GPU path (graphs, shm control plane, token
+feedback, micro-batching) runs over the host-staged transport, the RCCL binding is exercised with
+a 1-rank communicator, and the RCCL-failure path (all ranks agree, fall back together) is tested
+by asking for RCCL on a shared GPU.  With two or more GPUs the RCCL P2P transport and a PP=2
+RCCL pipeline are tested for real.
 """
 import multiprocessing as mp
 import os
@@ -121,52 +122,98 @@ def _rccl_worker(rank, port, q):
         dist.init_process_group("gloo")
         from distributed_llm_inference.parallel.transport import RcclTransport
         from distributed_llm_inference.runtime.faults import raw_store
-        dev = torch.device("cuda", 0)
+        dev = torch.device("cuda", rank)
         torch.cuda.set_device(dev)
-        tr = RcclTransport(raw_store(), rank, 2, dev, timeout_s=60.0)
-        x = torch.arange(1 << 20, device=dev, dtype=torch.float32) * (rank + 1)
-        if rank == 0:
-            tr.send(x, 1)
-            torch.cuda.synchronize()
-            q.put(("ok", None))
+        tr = RcclTransport(raw_store(), rank, 2, dev, timeout_s=120.0)
+        for n in (1 << 10, 8 << 20):  # a decode-sized and a prefill-sized hidden-state message
+            x = torch.arange(n, device=dev, dtype=torch.float32) * (rank + 1)
+            if rank == 0:
+                tr.send(x, 1)
+                torch.cuda.synchronize()
+            else:
+                y = torch.empty_like(x)
+                tr.recv(y, 0)
+                torch.cuda.synchronize()
+                if not torch.equal(y, torch.arange(n, device=dev, dtype=torch.float32)):
+                    q.put(("bad", n))
+                    break
         else:
-            y = torch.empty_like(x)
-            tr.recv(y, 0)
-            torch.cuda.synchronize()
-            ok = torch.equal(y, torch.arange(1 << 20, device=dev, dtype=torch.float32))
-            q.put(("ok" if ok else "bad", None))
+            q.put(("ok", None))
+        dist.barrier()
         tr.close()
         dist.destroy_process_group()
     except Exception as e:
         q.put(("err", repr(e)))
 
 
-def test_rccl_p2p_same_device(gpu):
+two_gpus = pytest.mark.skipif(torch.cuda.device_count() < 2,
+                              reason="needs 2 GPUs (RCCL refuses two ranks on one device; the "
+                                     "1-GPU box covers the fallback path instead)")
+
+
+@two_gpus
+def test_rccl_p2p_two_gpus(gpu):
+    """RcclTransport between two real GPUs (xGMI): send/recv of decode- and prefill-sized
+    messages on the transport's dedicated streams."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     ps = [ctx.Process(target=_rccl_worker, args=(r, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    import queue as _queue
-    res = []
-    try:
-        for _ in ps:
-            res.append(q.get(timeout=120))
-    except _queue.Empty:
-        res.append(("err", "timeout"))
-    finally:
-        for p in ps:
-            p.join(30)
-            if p.is_alive():
-                p.kill()
-                p.join(10)
-    errs = [m for s, m in res if s == "err"]
-    if errs == ["timeout"]:
-        pytest.skip("RCCL with two ranks on one device did not complete (expected on 1-GPU boxes)")
-    if errs and any("uplicate" in m or "invalid usage" in m.lower() for m in errs):
-        pytest.skip(f"RCCL rejects two ranks on one device: {errs[0][:200]}")
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(60)
     assert all(s == "ok" for s, _ in res), res
+
+
+def _pipeline_worker_gpus(rank, world, port, q):
+    try:
+        os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                          MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_TUNABLEOP="0",
+                          DLI_TRANSPORT="rccl")
+        os.environ.pop("DLI_SHARE_GPU", None)
+        import torch.distributed as dist
+        from distributed_llm_inference.runtime.engine import init_pipeline_rank
+        from distributed_llm_inference.runtime.sequence import SamplingParams
+        _, cfg = _cfg(world, world + 1)
+        role, obj = init_pipeline_rank(cfg)
+        if role == "driver":
+            out = obj.generate(PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))
+            obj.stop()
+            kind = type(obj.tr).__name__
+            obj.close()
+            q.put(("ok", [s.output for s in out], kind))
+        else:
+            obj.run()
+            obj.close()
+        dist.destroy_process_group()
+    except Exception:
+        q.put(("err", traceback.format_exc(), None))
+        raise
+
+
+@two_gpus
+def test_multiprocess_pipeline_rccl_two_gpus(gpu):
+    """PP=2 over RCCL P2P between two GPUs equals PP=1 (same micro-batch count)."""
+    from distributed_llm_inference.runtime.engine import LLMEngine
+    from distributed_llm_inference.runtime.sequence import SamplingParams
+    os.environ["DLI_TUNABLEOP"] = "0"
+    spec, cfg = _cfg(1, 3)
+    ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
+        PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_pipeline_worker_gpus, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    status, got, *rest = q.get(timeout=600)
+    for p in ps:
+        p.join(120)
+    assert status == "ok", got
+    assert rest and rest[0] == "RcclTransport", rest
+    assert got == ref
 
 
 def test_rccl_single_rank_self_p2p_and_collectives(gpu):
