@@ -267,7 +267,7 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
 void attn_prefill(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, Tensor v_cache,
                   Tensor block_tables, Tensor seq_lens, Tensor q_start, int64_t max_q,
                   double scale, int64_t n_sink, int64_t sink_pad, int64_t ring, int64_t window,
-                  double k_scale, double v_scale) {
+                  double k_scale, double v_scale, optional<Tensor> tile_map) {
   int64_t D = 0;
   auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
                        sink_pad, ring, window, k_scale, v_scale, D);
@@ -275,6 +275,12 @@ void attn_prefill(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache,
   const int64_t B = seq_lens.numel();
   TORCH_CHECK(q_start.numel() == B + 1, "q_start must have B+1 entries");
   p.q_start = q_start.data_ptr<int>();
+  if (tile_map.has_value()) {
+    CHECK_IN(*tile_map); CHECK_I32(*tile_map);
+    TORCH_CHECK(tile_map->dim() == 2 && tile_map->size(1) == 2, "tile_map must be [n_tiles, 2]");
+    p.tile_map = tile_map->data_ptr<int>();
+    p.n_tiles = (int)tile_map->size(0);
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   check_rc(dli::launch_attn_prefill(p, (int)B, (int)max_q, (int)D, cur_stream()), "attn_prefill");
 }

@@ -319,7 +319,8 @@ __global__ void __launch_bounds__(128) attn_combine_kernel(AttnParams p, int T) 
 //
 // Workgroup = 4 waves = HPW q heads (of ONE kv head) x TPW tiles of 16 query tokens, HPW*TPW = 4
 // (HPW = 4 when the GQA group allows it: the 4 waves then share every K/V tile).  Grid
-// (ceil(max_q / (16 TPW)), nkv * G / HPW, B).  Per 32-key step the workgroup copies the K tile
+// (n_tiles, nkv * G / HPW) over a host-built (sequence, tile) list — so decode rows mixed into a
+// prefill batch cost one tile each — or the dense (ceil(max_q / (16 TPW)), nkv * G / HPW, B).  Per 32-key step the workgroup copies the K tile
 // (32 rows x D, contiguous in the page) and the V^T tile (4 groups x D x 8, contiguous) into one of
 // two LDS buffers (register-staged: the global loads of step s+1 are issued before the MFMAs of
 // step s and written after them; one barrier per step).  Waves read their MFMA fragments from LDS:
@@ -344,7 +345,16 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw
   constexpr int UPT = (UNITS + 255) / 256;
   __shared__ __attribute__((aligned(16))) bf16 smem[2][2][32 * D];  // [buf][K | V][...]
 
-  const int b = blockIdx.z;
+  // work item: from the compact tile list (mixed prefill/decode batches: a 1-token decode row
+  // gets one tile instead of max_q / 16 empty ones) or the dense (tile, ., sequence) grid
+  int b, tile;
+  if (p.tile_map) {
+    b = p.tile_map[2 * blockIdx.x];
+    tile = p.tile_map[2 * blockIdx.x + 1];
+  } else {
+    b = blockIdx.z;
+    tile = blockIdx.x;
+  }
   const int G = p.nh / p.nkv;
   const int tpw = 4 / hpw;
   const int wgs_per_kv = G / hpw;
@@ -356,7 +366,7 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw
   const int qh = h0 + (w % hpw);
   const int qs0 = p.q_start[b];
   const int qlen = p.q_start[b + 1] - qs0;
-  const int wg_tok0 = blockIdx.x * 16 * tpw;
+  const int wg_tok0 = tile * 16 * tpw;
   if (wg_tok0 >= qlen) return;  // whole workgroup idle (uniform: before any barrier)
   const int tok0 = wg_tok0 + (w / hpw) * 16;
   const int L = p.seq_lens[b];
@@ -543,6 +553,8 @@ static int launch_prefill_d(const AttnParams& p, int B, int max_q, hipStream_t s
   const int hpw = (G % 4 == 0) ? 4 : (G % 2 == 0 ? 2 : 1);  // q heads sharing each K/V tile
   const int tpw = 4 / hpw;
   dim3 grid((max_q + 16 * tpw - 1) / (16 * tpw), p.nkv * (G / hpw), B);
+  if (p.tile_map) grid = dim3(p.n_tiles, p.nkv * (G / hpw), 1);
+  if (grid.x == 0) return 0;
   if (p.ring > 0) {
     if (p.kv_fp8) attn_prefill_kernel<D, true, true><<<grid, 256, 0, stream>>>(p, hpw);
     else attn_prefill_kernel<D, true, false><<<grid, 256, 0, stream>>>(p, hpw);

@@ -16,6 +16,8 @@ struct AttnParams {
   int bt_stride;
   const int* seq_lens;  // [B] absolute length incl. this step's tokens
   const int* q_start;   // [B+1] prefill token offsets; nullptr for decode (token b == seq b)
+  const int* tile_map;  // prefill: [n_tiles, 2] (sequence, token tile) work list, or nullptr
+  int n_tiles;          //   (nullptr: dense grid over max_q x B)
   float scale_log2;     // softmax scale * log2(e)
   int nh, nkv, bs;
   int n_sink, sink_pad, ring, window;  // window mode iff ring > 0

@@ -94,6 +94,8 @@ class AttnMetadata:
     # fp8 KV cache scales (stored = x / scale); 1.0 for bf16 caches
     k_scale: float = 1.0
     v_scale: float = 1.0
+    # prefill work list [n_tiles, 2] (sequence, token tile) for the attention kernel, or None
+    tile_map: Optional[torch.Tensor] = None
     # rows (token index) whose hidden state feeds the LM head, or None = all rows
     logits_rows: Optional[torch.Tensor] = None
 

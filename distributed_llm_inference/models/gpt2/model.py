@@ -69,7 +69,7 @@ class GPT2Layer(nn.Module):
             o = ops.attn_prefill(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
                                  meta.q_start, meta.max_q, self.scale, meta.n_sink, meta.sink_pad,
                                  meta.ring, meta.window, k_scale=meta.k_scale,
-                                 v_scale=meta.v_scale)
+                                 v_scale=meta.v_scale, tile_map=meta.tile_map)
         attn = self.attn_proj(o.view(T, -1))
         normed, residual = self.ln_2(attn, residual,
                                      residual_out=torch.empty_like(residual) if first else None)

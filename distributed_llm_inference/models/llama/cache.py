@@ -115,8 +115,12 @@ class KVPool:
             max_len = int(sl.max()) if B else 1
             num_splits = ops.decode_splits(B, self.spec.num_kv_heads, self.spec.group_size,
                                            max_len) if (is_decode and dev.type == "cuda") else 1
+        tile_map = None
+        if not is_decode and dev.type == "cuda" and B:
+            tile_map = ops.prefill_tiles(q_lens, self.spec.num_heads,
+                                         self.spec.num_kv_heads).to(dev, non_blocking=True)
         return AttnMetadata(
-            num_tokens=T, num_seqs=B, is_decode=is_decode,
+            num_tokens=T, num_seqs=B, is_decode=is_decode, tile_map=tile_map,
             positions=pos.to(dev, non_blocking=True), slot_mapping=slot.to(dev, non_blocking=True),
             block_tables=bt.to(dev, non_blocking=True), seq_lens=sl.to(dev, non_blocking=True),
             q_start=qs.to(dev, non_blocking=True), max_q=int(max(q_lens)) if B else 0,

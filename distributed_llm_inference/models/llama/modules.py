@@ -70,7 +70,7 @@ class LlamaAttention(nn.Module):
             o = ops.attn_prefill(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
                                  meta.q_start, meta.max_q, self.scale, meta.n_sink, meta.sink_pad,
                                  meta.ring, meta.window, k_scale=meta.k_scale,
-                                 v_scale=meta.v_scale)
+                                 v_scale=meta.v_scale, tile_map=meta.tile_map)
         o = o.view(T, self.num_heads * self.head_dim)
         return self.o_proj(o)
 

@@ -168,8 +168,34 @@ def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_si
     return out
 
 
+def prefill_tile_tokens(nh: int, nkv: int) -> int:
+    """Query tokens per prefill workgroup tile (attention.hip: 16 * TPW, TPW = 4 / HPW)."""
+    G = nh // nkv
+    hpw = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
+    return 16 * (4 // hpw)
+
+
+def prefill_tiles(q_lens, nh: int, nkv: int, out=None) -> torch.Tensor:
+    """Compact (sequence, token-tile) work list of the prefill kernel: one row per tile that
+    holds query tokens.  A 1-token decode row mixed into a prefill batch gets a single tile
+    instead of ``max_q / tile`` empty workgroups.  Returns int32 [n_tiles, 2] (or fills ``out``)."""
+    import numpy as np
+    tt = prefill_tile_tokens(nh, nkv)
+    ql = np.asarray(q_lens, dtype=np.int64)
+    nt = (ql + tt - 1) // tt
+    b = np.repeat(np.arange(len(ql), dtype=np.int32), nt)
+    starts = np.repeat(np.cumsum(nt) - nt, nt)
+    tile = (np.arange(int(nt.sum())) - starts).astype(np.int32)
+    m = np.stack([b, tile], axis=1)
+    if out is not None:
+        out.numpy()[: len(m)] = m
+        return out[: len(m)]
+    return torch.from_numpy(np.ascontiguousarray(m))
+
+
 def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, max_q, scale,
-                 n_sink=0, sink_pad=0, ring=0, window=0, out=None, k_scale=1.0, v_scale=1.0):
+                 n_sink=0, sink_pad=0, ring=0, window=0, out=None, k_scale=1.0, v_scale=1.0,
+                 tile_map=None):
     if not _gpu(q):
         y = ref.attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, scale,
                              n_sink, sink_pad, ring, window, k_scale, v_scale)
@@ -177,7 +203,7 @@ def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, m
     out = torch.empty_like(q) if out is None else out
     native().attn_prefill(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start,
                           int(max_q), float(scale), int(n_sink), int(sink_pad), int(ring),
-                          int(window), float(k_scale), float(v_scale))
+                          int(window), float(k_scale), float(v_scale), tile_map)
     return out
 
 

@@ -92,6 +92,7 @@ class _Staging:
                  ("step", torch.int64, (1,)),
                  ("positions", torch.int32, (max_tokens,)),
                  ("tokens", torch.int32, (max_tokens,)),
+                 ("tile_map", torch.int32, (max_tokens + max_seqs, 2)),
                  ("block_tables", torch.int32, (max_seqs, max_blocks)),
                  ("seq_lens", torch.int32, (max_seqs,)),
                  ("q_start", torch.int32, (max_seqs + 1,)),
@@ -223,6 +224,12 @@ class StageExecutor:
         st.upload("block_tables", rows)
         st.upload("seq_lens", rows)
         st.upload("q_start", rows + 1)
+        self._n_tiles = 0
+        if not plan.is_decode and self.device.type == "cuda":
+            tm = ops.prefill_tiles(plan.q_lens, self.spec.num_heads, self.spec.num_kv_heads,
+                                   out=h["tile_map"])
+            self._n_tiles = tm.shape[0]
+            st.upload("tile_map", self._n_tiles)
         if plan.tokens is not None:
             tok = h["tokens"]
             tok[:T] = torch.as_tensor(plan.tokens, dtype=torch.int32)
@@ -275,6 +282,7 @@ class StageExecutor:
             seq_lens=d["seq_lens"][:rows], q_start=d["q_start"][: rows + 1],
             max_q=max(plan.q_lens) if plan.q_lens else 0, num_splits=num_splits,
             workspace=self._workspace(rows, num_splits) if decode else None,
+            tile_map=(d["tile_map"][: self._n_tiles] if (not decode and self._n_tiles) else None),
             logits_rows=logits_rows, **self._wp)
 
     def _workspace(self, rows: int, splits: int):

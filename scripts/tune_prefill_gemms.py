@@ -72,7 +72,6 @@ def main():
                           flush=True)
             del w
             torch.cuda.empty_cache()
-    t.write_file()
 
 
 if __name__ == "__main__":

@@ -129,11 +129,12 @@ def test_attn_decode_window(gpu, splits):
 
 
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (8, 8, 64), (4, 2, 32)])
-def test_attn_prefill(gpu, nh, nkv, D):
+@pytest.mark.parametrize("tiles", [False, True])
+def test_attn_prefill(gpu, nh, nkv, D, tiles):
     torch.manual_seed(4)
     bs = 64
-    q_lens = [5, 64, 130, 1]
-    ctx = [0, 10, 70, 300]  # tokens already in the cache before this chunk
+    q_lens = [5, 64, 130, 1, 1, 1]  # mixed batch: prefill chunks and decode rows
+    ctx = [0, 10, 70, 300, 3, 129]  # tokens already in the cache before this chunk
     lens = torch.tensor([a + b for a, b in zip(q_lens, ctx)], dtype=torch.int32)
     B = len(q_lens)
     q_start = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
@@ -144,7 +145,9 @@ def test_attn_prefill(gpu, nh, nkv, D):
     bt = _tables(B, max_blocks, nblocks, gpu, seed=2)
     q = torch.randn(T, nh, D, device=gpu, dtype=BF)
     scale = 1 / math.sqrt(D)
-    out = ops.attn_prefill(q, None, kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens), scale)
+    tm = ops.prefill_tiles(q_lens, nh, nkv).to(gpu) if tiles else None
+    out = ops.attn_prefill(q, None, kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens), scale,
+                           tile_map=tm)
     out_r = ref.attn_prefill(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale)
     _close(out, out_r, 2e-2, 2e-2, "prefill")
 
