@@ -403,6 +403,25 @@ void gemm_nt(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t bn,
                                (int)bn, cur_stream()), "gemm_nt");
 }
 
+// ------------------------------------------------------------------------------ skinny GEMM
+void skinny_gemm(Tensor out, Tensor x, Tensor w, optional<Tensor> bias) {
+  CHECK_IN(out); CHECK_IN(x); CHECK_IN(w);
+  CHECK_BF16(out); CHECK_BF16(x); CHECK_BF16(w);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm: 2-D tensors");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N, "skinny_gemm: shape mismatch");
+  TORCH_CHECK(M >= 1 && M <= 4 && K % 8 == 0, "skinny_gemm: M in [1, 4], K % 8 == 0");
+  const dli::bf16* b = nullptr;
+  if (bias.has_value()) {
+    CHECK_IN(*bias); CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() == N, "skinny_gemm: bias must have N entries");
+    b = bp(*bias);
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_rc(dli::launch_skinny_gemm(bp(out), bp(x), bp(w), b, (int)M, (int)N, (int)K,
+                                   cur_stream()), "skinny_gemm");
+}
+
 }  // namespace
 
 void register_rccl(pybind11::module_& m);  // comm/rccl_p2p.hip
@@ -428,5 +447,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt, "decode GEMM C = A . B^T (M <= 256, split-K MFMA)", py::arg("out"),
         py::arg("a"), py::arg("b"), py::arg("splits"), py::arg("bn"),
         py::arg("workspace") = py::none());
+  m.def("skinny_gemm", &skinny_gemm, "y = x . W^T (+ bias) for M <= 4 (weight-streaming GEMV)",
+        py::arg("out"), py::arg("x"), py::arg("w"), py::arg("bias") = py::none());
   register_rccl(m);
 }

@@ -72,6 +72,8 @@ int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_
 int launch_sample(const SampleParams& p, int B, hipStream_t stream);
 int launch_gemm_nt(bf16* C, const bf16* A, const bf16* B, float* workspace, int M, int N, int K,
                    int splits, int bn, hipStream_t stream);
+int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
+                       int K, hipStream_t stream);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
                          bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,
                          hipStream_t stream);

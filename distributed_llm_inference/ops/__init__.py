@@ -296,3 +296,22 @@ def gemm_nt(x: torch.Tensor, w: torch.Tensor, splits: int = 1, bn: int = 128,
         workspace = torch.empty(splits * M * N, dtype=torch.float32, device=x.device)
     native().gemm_nt(out, x, w, int(splits), int(bn), workspace)
     return out
+
+
+# ----------------------------------------------------------------------------- skinny GEMM
+SKINNY_MAX_M = 4        # kernel limit
+SKINNY_DISPATCH_M = 2   # Linear uses it up to here: measured faster than hipBLASLt at M <= 2 on
+                        # every Llama-3-70B decode shape (5.3-6.9 vs 4.3-6.0 TB/s), slower at M = 4
+
+
+def skinny_gemm(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x [M, K] @ w[N, K]^T (+ bias)`` for M <= 4 with the weight-streaming HIP kernel."""
+    if not _gpu(x):
+        y = (x.float() @ w.float().t() + (bias.float() if bias is not None else 0.0)).to(x.dtype)
+        return out.copy_(y) if out is not None else y
+    if out is None:
+        out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+    native().skinny_gemm(out, x, w, bias)
+    return out
+
