@@ -347,19 +347,30 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw
 
   // work item: from the compact tile list (mixed prefill/decode batches: a 1-token decode row
   // gets one tile instead of max_q / 16 empty ones) or the dense (tile, ., sequence) grid
-  int b, tile;
+  int b, tile, grp;
   if (p.tile_map) {
-    b = p.tile_map[2 * blockIdx.x];
-    tile = p.tile_map[2 * blockIdx.x + 1];
+    // 1-D grid padded to a multiple of 8; workgroup L runs on XCD L % 8 (round-robin dispatch).
+    // Give every XCD one contiguous run of work items w = grp * n_tiles + t, so consecutive
+    // token tiles of one (sequence, kv-head group) — which read the same K/V — share an L2.
+    const int total = p.n_tiles * p.nkv * ((p.nh / p.nkv) / hpw);
+    const int per = (int)gridDim.x >> 3;
+    const int L = (int)blockIdx.x;
+    const int w = (L & 7) * per + (L >> 3);
+    if (w >= total) return;  // padding (uniform per workgroup: before any barrier)
+    grp = w / p.n_tiles;
+    const int t = w - grp * p.n_tiles;
+    b = p.tile_map[2 * t];
+    tile = p.tile_map[2 * t + 1];
   } else {
     b = blockIdx.z;
     tile = blockIdx.x;
+    grp = blockIdx.y;
   }
   const int G = p.nh / p.nkv;
   const int tpw = 4 / hpw;
   const int wgs_per_kv = G / hpw;
-  const int kvh = blockIdx.y / wgs_per_kv;
-  const int h0 = kvh * G + (blockIdx.y % wgs_per_kv) * hpw;
+  const int kvh = grp / wgs_per_kv;
+  const int h0 = kvh * G + (grp % wgs_per_kv) * hpw;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, h4 = lane >> 4;
@@ -553,7 +564,11 @@ static int launch_prefill_d(const AttnParams& p, int B, int max_q, hipStream_t s
   const int hpw = (G % 4 == 0) ? 4 : (G % 2 == 0 ? 2 : 1);  // q heads sharing each K/V tile
   const int tpw = 4 / hpw;
   dim3 grid((max_q + 16 * tpw - 1) / (16 * tpw), p.nkv * (G / hpw), B);
-  if (p.tile_map) grid = dim3(p.n_tiles, p.nkv * (G / hpw), 1);
+  if (p.tile_map) {
+    // XCD-aware 1-D grid over (group, tile) work items (see attn_prefill_kernel)
+    const long total = (long)p.n_tiles * p.nkv * (G / hpw);
+    grid = dim3((unsigned)((total + 7) / 8 * 8), 1, 1);
+  }
   if (grid.x == 0) return 0;
   if (p.ring > 0) {
     if (p.kv_fp8) attn_prefill_kernel<D, true, true><<<grid, 256, 0, stream>>>(p, hpw);

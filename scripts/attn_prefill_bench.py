@@ -30,8 +30,10 @@ def run(B, q, ctx):
     Q = torch.randn(B * q, nh, D, device=dev, dtype=torch.bfloat16)
     out = torch.empty_like(Q)
 
+    tm = ops.prefill_tiles([q] * B, nh, nkv).to(dev) if os.environ.get("DENSE") != "1" else None
+
     def call():
-        ops.attn_prefill(Q, None, kc, vc, bt, lens, q_start, q, D ** -0.5)
+        ops.attn_prefill(Q, None, kc, vc, bt, lens, q_start, q, D ** -0.5, tile_map=tm)
 
     for _ in range(3):
         call()
