@@ -52,7 +52,7 @@ class Linear(nn.Module):
         """``x_q`` = (fp8 rows, scales) already quantised by a fused producer kernel; then ``x`` may
         be None (fp8 weights only)."""
         if self.weight_fp8 is None:
-            if (x.is_cuda and x.dim() == 2 and x.shape[0] <= ops.SKINNY_DISPATCH_M
+            if (x.is_cuda and x.dim() == 2 and 1 <= x.shape[0] <= ops.SKINNY_DISPATCH_M
                     and x.dtype == torch.bfloat16 and x.is_contiguous()
                     and self.in_features % 8 == 0):
                 # 1-2 row decode batches: weight-streaming HIP kernel (csrc/kernels/gemv.hip)
