@@ -84,14 +84,15 @@ void layer_norm(Tensor out, Tensor x, optional<Tensor> residual, Tensor w, Tenso
 }
 
 // ------------------------------------------------------------------------------ activations
-void silu_mul(Tensor out, Tensor x) {
+void silu_mul(Tensor out, Tensor x, bool interleaved) {
   CHECK_IN(out); CHECK_IN(x); CHECK_BF16(out); CHECK_BF16(x);
   const int64_t two_i = x.size(-1);
   TORCH_CHECK(two_i % 2 == 0, "silu_mul: last dim must be even");
   const int64_t rows = x.numel() / two_i;
   TORCH_CHECK(out.numel() == rows * (two_i / 2), "silu_mul: out shape mismatch");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-  check_rc(dli::launch_silu_mul(bp(out), bp(x), (int)rows, (int)(two_i / 2), cur_stream()),
+  check_rc(dli::launch_silu_mul(bp(out), bp(x), (int)rows, (int)(two_i / 2), interleaved,
+                                cur_stream()),
            "silu_mul");
 }
 
@@ -403,6 +404,35 @@ void gemm_nt(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t bn,
                                (int)bn, cur_stream()), "gemm_nt");
 }
 
+// ------------------------------------------------------------------------------ tile GEMM
+// epilogue 0: out = A . B^T (bf16); 2: out[:, n] = silu(g) * u with B rows interleaved by
+// ops.swiglu_interleave (out has N / 2 columns).  splits > 1 (epilogue 0 only) needs an fp32
+// workspace of splits * M * N.
+void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
+               optional<Tensor> workspace) {
+  CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
+  CHECK_BF16(out); CHECK_BF16(a); CHECK_BF16(b);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_tile: 2-D tensors");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K && out.size(0) == M, "gemm_tile: shape mismatch");
+  TORCH_CHECK(epilogue == 0 || epilogue == 2, "gemm_tile: epilogue must be 0 (store) or 2 (swiglu)");
+  TORCH_CHECK(out.size(1) == (epilogue == 2 ? N / 2 : N), "gemm_tile: output columns");
+  TORCH_CHECK(M >= 1 && M <= (1 << 20) && N % 256 == 0 && K % 64 == 0 && K > 0,
+              "gemm_tile: needs N % 256 == 0 and K % 64 == 0");
+  TORCH_CHECK(splits >= 1 && splits <= K / 64, "gemm_tile: 1 <= splits <= K / 64");
+  float* ws = nullptr;
+  if (splits > 1) {
+    TORCH_CHECK(epilogue == 0, "gemm_tile: split-K only with the plain store epilogue");
+    TORCH_CHECK(workspace.has_value(), "gemm_tile: split-K needs a workspace");
+    CHECK_IN(*workspace); CHECK_F32(*workspace);
+    TORCH_CHECK(workspace->numel() >= splits * M * N, "gemm_tile: workspace too small");
+    ws = workspace->data_ptr<float>();
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
+  check_rc(dli::launch_gemm_tile(out.data_ptr(), bp(a), bp(b), ws, (int)M, (int)N, (int)K,
+                                 (int)splits, (int)epilogue, cur_stream()), "gemm_tile");
+}
+
 // ------------------------------------------------------------------------------ skinny GEMM
 void skinny_gemm(Tensor out, Tensor x, Tensor w, optional<Tensor> bias) {
   CHECK_IN(out); CHECK_IN(x); CHECK_IN(w);
@@ -433,7 +463,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layer_norm", &layer_norm, "LayerNorm (+fused residual add)", py::arg("out"),
         py::arg("x"), py::arg("residual"), py::arg("w"), py::arg("b"), py::arg("eps"),
         py::arg("residual_out") = py::none());
-  m.def("silu_mul", &silu_mul, "SwiGLU: out = silu(x[:, :I]) * x[:, I:]");
+  m.def("silu_mul", &silu_mul, "SwiGLU: out = silu(x[:, :I]) * x[:, I:] (or tile-interleaved)",
+        py::arg("out"), py::arg("x"), py::arg("interleaved") = false);
   m.def("gelu_bias", &gelu_bias, "gelu_tanh(x + bias)");
   m.def("add", &add, "out = a + b");
   m.def("rope_cache", &rope_cache, "fused RoPE + paged KV cache write");
@@ -447,6 +478,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &gemm_nt, "decode GEMM C = A . B^T (M <= 256, split-K MFMA)", py::arg("out"),
         py::arg("a"), py::arg("b"), py::arg("splits"), py::arg("bn"),
         py::arg("workspace") = py::none());
+  m.def("gemm_tile", &gemm_tile, "C = A . B^T, 256x256 LDS-DMA 8-phase MFMA tile GEMM",
+        py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
+        py::arg("epilogue") = 0, py::arg("workspace") = py::none());
   m.def("skinny_gemm", &skinny_gemm, "y = x . W^T (+ bias) for M <= 4 (weight-streaming GEMV)",
         py::arg("out"), py::arg("x"), py::arg("w"), py::arg("bias") = py::none());
   register_rccl(m);

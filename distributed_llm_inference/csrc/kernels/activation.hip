@@ -10,6 +10,9 @@
 
 namespace dli {
 
+// INTERLEAVED: the row is in the tile-GEMM SwiGLU order (ops.swiglu_interleave): output column o
+// = 128 t + 32 w + 16 p + l has its gate at 256 t + 64 w + 32 p + l and its up 16 columns later.
+template <bool INTERLEAVED>
 __global__ void __launch_bounds__(256) silu_mul_kernel(bf16* __restrict__ out,
                                                        const bf16* __restrict__ x, int rows,
                                                        int inter) {
@@ -18,8 +21,17 @@ __global__ void __launch_bounds__(256) silu_mul_kernel(bf16* __restrict__ out,
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
        i += (size_t)gridDim.x * blockDim.x) {
     const size_t r = i / nvec, c = i % nvec;
-    const bf16x8 g = reinterpret_cast<const bf16x8*>(x + r * 2 * inter)[c];
-    const bf16x8 u = reinterpret_cast<const bf16x8*>(x + r * 2 * inter + inter)[c];
+    const bf16* row = x + r * 2 * inter;
+    bf16x8 g, u;
+    if (INTERLEAVED) {
+      const int o = (int)c * 8;
+      const int gc = (o >> 7) * 256 + ((o & 127) >> 5) * 64 + ((o & 31) >> 4) * 32 + (o & 15);
+      g = *reinterpret_cast<const bf16x8*>(row + gc);
+      u = *reinterpret_cast<const bf16x8*>(row + gc + 16);
+    } else {
+      g = reinterpret_cast<const bf16x8*>(row)[c];
+      u = reinterpret_cast<const bf16x8*>(row + inter)[c];
+    }
     bf16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = (bf16)(silu((float)g[j]) * (float)u[j]);
@@ -70,10 +82,14 @@ static inline int ew_grid(size_t work) {
   return (int)g;
 }
 
-int launch_silu_mul(bf16* out, const bf16* x, int rows, int inter, hipStream_t stream) {
-  if (inter % 8 != 0) return -1;
+int launch_silu_mul(bf16* out, const bf16* x, int rows, int inter, bool interleaved,
+                    hipStream_t stream) {
+  if (inter % 8 != 0 || (interleaved && inter % 128 != 0)) return -1;
   if (rows == 0) return 0;
-  silu_mul_kernel<<<ew_grid((size_t)rows * inter / 8), 256, 0, stream>>>(out, x, rows, inter);
+  if (interleaved)
+    silu_mul_kernel<true><<<ew_grid((size_t)rows * inter / 8), 256, 0, stream>>>(out, x, rows, inter);
+  else
+    silu_mul_kernel<false><<<ew_grid((size_t)rows * inter / 8), 256, 0, stream>>>(out, x, rows, inter);
   return 0;
 }
 

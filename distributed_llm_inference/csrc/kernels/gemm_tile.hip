@@ -1,0 +1,309 @@
+// Projection GEMM for CDNA4:  C[M, N] = A[M, K] . B[N, K]^T   (bf16 in, fp32 accumulate)
+//
+// The decode step of a pipeline stage multiplies a micro-batch of activations (M = 256..512 rows)
+// by each weight matrix (fused QKV, O, gate|up, down).  This kernel is the 256 x 256 x 64,
+// 8-wave, LDS-DMA-staged, 8-phase MFMA structure of cdna_hip_programming.md §5 ("The 256² 8-phase
+// template"), written for the NT layout both operands have here (A = activations [M, K] and
+// B = nn.Linear weight [N, K], both K-contiguous):
+//
+//   * workgroup = 8 waves as 2 (M) x 4 (N); wave tile 128 x 64 = 8 x 4 fragments of
+//     v_mfma_f32_16x16x32_bf16 (128 fp32 accumulators per lane);
+//   * each 256 x 64 operand tile is staged as two 128-row HALF-TILES; half h of A holds the rows
+//     the waves' m-quadrant h uses (tile rows {r : (r % 128) / 64 == h}), half h of B the columns
+//     of their n-quadrant h ({c : (c % 64) / 32 == h}).  One half-tile = 16 KB = two
+//     `global_load_lds_dwordx4` per thread, lane-linear in LDS; the XOR swizzle
+//     chunk ^ ((row >> 1) & 7) is applied to the per-lane GLOBAL address (LDS-DMA cannot scatter)
+//     and makes every fragment `ds_read_b128` conflict-free (docs/kernels.md derivation);
+//   * per k-tile 4 phases, one output quadrant (64 x 32, 16 MFMAs) each:
+//        phase 0: read A-half 0 + B-half 0 fragments | DMA A-half 1 of tile t+1
+//        phase 1: read B-half 1                      |
+//        phase 2: read A-half 1                      | DMA A-half 0 of tile t+2 (same buffer)
+//        phase 3: (reuse B-half 0 registers)         | DMA B-halves 0, 1 of tile t+2; vmcnt(6)
+//     so three half-tiles stay in flight across every barrier (counted `s_waitcnt vmcnt(6)`,
+//     never 0 in the steady state);
+//   * the two wave groups (waves 0-3 / 4-7, one of each per SIMD) run one barrier apart
+//     (§5 "if (wr == 1) s_barrier"): each SIMD alternates one wave's MFMA segment with the other
+//     wave's ds_reads and DMA issue.  With that stagger a half-tile is restaged >= 2 phases after
+//     its last ds_read (WAR across the lagging group) and read >= 1 phase after the vmcnt that
+//     retired its DMA (RAW across the leading group);
+//   * raw `s_barrier` (no __syncthreads: its fence would drain the DMA queue) and one __shared__
+//     array (a second one makes hipcc wait vmcnt(0) before the first ds_read of every phase);
+//   * blockIdx is remapped so the blocks of one XCD run neighbouring tiles (§5.5 T1, bijective);
+//   * epilogues: bf16 store, fp32 split-K slab (summed by `splitk_reduce`), or fused SwiGLU:
+//     with B's rows interleaved by `swiglu_interleave` (gate and up rows of the same output
+//     column land in n-fragments 2p and 2p+1 of one wave) the wave holds gate and up of an output
+//     element in the same lane and register, and stores silu(gate) * up directly.
+#include "kernels.h"
+
+namespace dli {
+
+namespace {
+
+constexpr int kTM = 256, kTN = 256, kTK = 64, kThreads = 512;
+constexpr int kHalf = 128 * 128;       // bytes of one half-tile (128 rows x 64 bf16)
+constexpr int kBuf = 4 * kHalf;        // A0 A1 B0 B1
+constexpr int kLds = 2 * kBuf;         // double buffer: 128 KB
+
+enum Epilogue { kStoreBf16 = 0, kStoreF32 = 1, kSwiGLU = 2 };
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+__device__ __forceinline__ void dma16(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+
+template <int EPI>
+__global__ void __launch_bounds__(kThreads, 1)
+gemm_tile_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __restrict__ C,
+                 int M, int N, int K, int tiles_m, int tiles_n, int k_tiles_per_split) {
+  __shared__ __attribute__((aligned(1024))) char smem[kLds];
+
+  // ---- XCD-aware, bijective block remap (consecutive logical ids share an XCD / its L2) ----
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tm = lid % tiles_m;               // the M tiles of one N panel are neighbours:
+  const int tn = (lid / tiles_m) % tiles_n;   // they share the streamed weight panel via L2
+  const int split = lid / (tiles_m * tiles_n);
+  const int m0 = tm * kTM, n0 = tn * kTN;
+  const int kt0 = split * k_tiles_per_split;
+  const int T = min(k_tiles_per_split, K / kTK - kt0);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  // ---- DMA source rows: thread stages LDS units u = j*512 + tid (j = 0, 1) of each half-tile ----
+  // unit u -> local row lr = u >> 3, LDS slot s = u & 7, global chunk s ^ ((lr >> 1) & 7)
+  const bf16* srcA[2][2];
+  const bf16* srcB[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int u = j * kThreads + tid;
+    const int lr = u >> 3, ch = (u & 7) ^ ((lr >> 1) & 7);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ga = (lr >> 6) * 128 + h * 64 + (lr & 63);
+      const int gb = (lr >> 5) * 64 + h * 32 + (lr & 31);
+      const int ra = min(m0 + ga, M - 1);       // rows past M are computed, never stored
+      srcA[h][j] = A + (size_t)ra * K + (size_t)kt0 * kTK + ch * 8;
+      srcB[h][j] = B + (size_t)(n0 + gb) * K + (size_t)kt0 * kTK + ch * 8;
+    }
+  }
+  // stage half `which` (0 = A0, 1 = A1, 2 = B0, 3 = B1) of k-tile t into buffer t & 1
+  auto stage = [&](int which, int t) {
+    char* dst = smem + (t & 1) * kBuf + which * kHalf + wave * 1024;
+    const size_t koff = (size_t)t * kTK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16* src = which < 2 ? srcA[which][j] : srcB[which - 2][j];
+      dma16(src + koff, dst + j * 8192);
+    }
+  };
+
+  // ---- fragment read offsets (lane constant part; ds_read immediates do the rest) ----
+  const int fr = lane & 15;
+  int sch[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) sch[kk] = ((kk * 4 + (lane >> 4)) ^ (fr >> 1)) << 4;
+  const int a_lane = (wr * 64 + fr) * 128;
+  const int b_lane = (wc * 32 + fr) * 128;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  auto read_a = [&](const char* buf, int h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        af[i][kk] = *reinterpret_cast<const bf16x8*>(buf + h * kHalf + a_lane + i * 16 * 128 + sch[kk]);
+  };
+  auto read_b = [&](const char* buf, int h, bf16x8 (&bf)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        bf[j][kk] = *reinterpret_cast<const bf16x8*>(buf + (2 + h) * kHalf + b_lane + j * 16 * 128 + sch[kk]);
+  };
+  auto quadrant = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mq * 4 + i][nq * 2 + j] = mfma(af[i][kk], bf[j][kk], acc[mq * 4 + i][nq * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // ---- prologue: tile 0 complete, three halves of tile 1 in flight ----
+  if (T > 0) {
+    stage(0, 0); stage(2, 0); stage(3, 0); stage(1, 0);
+    if (T > 1) {
+      stage(0, 1); stage(2, 1); stage(3, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  barrier();
+
+  // the two wave groups (wr = 0: waves 0-3, wr = 1: waves 4-7, one of each per SIMD) run one
+  // barrier apart, so every SIMD alternates one wave's MFMA segment with the other's LDS reads
+  if (wr == 1) barrier();
+  for (int t = 0; t < T; ++t) {
+    const char* buf = smem + (t & 1) * kBuf;
+    const bool more1 = t + 1 < T, more2 = t + 2 < T;
+    // phase 0: quadrant (0, 0)
+    read_a(buf, 0);
+    read_b(buf, 0, b0);
+    if (more1) stage(1, t + 1);
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    quadrant(0, 0, b0);
+    barrier();
+    // phase 1: quadrant (0, 1)
+    read_b(buf, 1, b1);
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    quadrant(0, 1, b1);
+    barrier();
+    // phase 2: quadrant (1, 1); A-half 0 was last read two phases ago
+    read_a(buf, 1);
+    if (more2) stage(0, t + 2);
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    quadrant(1, 1, b1);
+    barrier();
+    // phase 3: quadrant (1, 0); restage both B halves; retire tile t+1 (all but 3 newest halves)
+    if (more2) {
+      stage(2, t + 2);
+      stage(3, t + 2);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    barrier();
+    quadrant(1, 0, b0);
+    barrier();
+  }
+  if (wr == 0) barrier();
+
+  // ---- epilogue: C/D fragment map col = lane & 15, row = 4 * (lane >> 4) + r ----
+  const int crow = m0 + wr * 128 + (lane >> 4) * 4;
+  const int ccol = n0 + wc * 64 + fr;
+  if (EPI == kSwiGLU) {
+    // n-fragments (2p, 2p+1) = (gate, up) of output columns n0/2 + wc*32 + p*16 + fr
+    bf16* out = reinterpret_cast<bf16*>(C);
+    const int I = N >> 1;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int col = (n0 >> 1) + wc * 32 + p * 16 + fr;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = crow + i * 16 + e;
+          // round gate and up to bf16 first: bit-matches the unfused GEMM -> silu_mul path
+          const float g = (float)(bf16)acc[i][2 * p][e];
+          const float u = (float)(bf16)acc[i][2 * p + 1][e];
+          if (row < M) out[(size_t)row * I + col] = (bf16)(silu(g) * u);
+        }
+      }
+  } else if (EPI == kStoreF32) {
+    float* out = reinterpret_cast<float*>(C) + (size_t)split * M * N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = crow + i * 16 + e;
+          if (row < M) out[(size_t)row * N + ccol + j * 16] = acc[i][j][e];
+        }
+  } else {
+    bf16* out = reinterpret_cast<bf16*>(C);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = crow + i * 16 + e;
+          if (row < M) out[(size_t)row * N + ccol + j * 16] = (bf16)acc[i][j][e];
+        }
+  }
+}
+
+__global__ void __launch_bounds__(256) tile_splitk_reduce_kernel(bf16* __restrict__ C,
+                                                                 const float* __restrict__ part,
+                                                                 int splits, size_t MN) {
+  for (size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) * 8; i < MN;
+       i += (size_t)gridDim.x * blockDim.x * 8) {
+    f32x4 s0 = *reinterpret_cast<const f32x4*>(part + i);
+    f32x4 s1 = *reinterpret_cast<const f32x4*>(part + i + 4);
+    for (int k = 1; k < splits; ++k) {
+      s0 += *reinterpret_cast<const f32x4*>(part + k * MN + i);
+      s1 += *reinterpret_cast<const f32x4*>(part + k * MN + i + 4);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = (bf16)s0[j];
+      o[j + 4] = (bf16)s1[j];
+    }
+    *reinterpret_cast<bf16x8*>(C + i) = o;
+  }
+}
+
+}  // namespace
+
+int launch_gemm_tile(void* C, const bf16* A, const bf16* B, float* workspace, int M, int N, int K,
+                     int splits, int epilogue, hipStream_t stream) {
+  if (M <= 0 || N % kTN != 0 || K % kTK != 0 || splits < 1) return -1;
+  const int kt = K / kTK;
+  if (splits > kt) return -2;
+  const int kps = (kt + splits - 1) / splits;
+  if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
+  if (splits > 1 && (workspace == nullptr || epilogue != kStoreBf16)) return -3;
+  const int tiles_m = (M + kTM - 1) / kTM, tiles_n = N / kTN;
+  const int grid = tiles_m * tiles_n * splits;
+  if (splits > 1) {
+    gemm_tile_kernel<kStoreF32><<<grid, kThreads, 0, stream>>>(A, B, workspace, M, N, K, tiles_m,
+                                                               tiles_n, kps);
+    const size_t MN = (size_t)M * N;
+    size_t blocks = (MN / 8 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    tile_splitk_reduce_kernel<<<(int)blocks, 256, 0, stream>>>(reinterpret_cast<bf16*>(C),
+                                                               workspace, splits, MN);
+  } else if (epilogue == kSwiGLU) {
+    gemm_tile_kernel<kSwiGLU><<<grid, kThreads, 0, stream>>>(A, B, C, M, N, K, tiles_m, tiles_n, kps);
+  } else if (epilogue == kStoreBf16) {
+    gemm_tile_kernel<kStoreBf16><<<grid, kThreads, 0, stream>>>(A, B, C, M, N, K, tiles_m, tiles_n,
+                                                                kps);
+  } else {
+    return -4;
+  }
+  return 0;
+}
+
+}  // namespace dli

@@ -62,7 +62,8 @@ int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* res
 int launch_layer_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* residual_out,
                       const bf16* w, const bf16* b, float eps, int rows, int hidden,
                       hipStream_t stream);
-int launch_silu_mul(bf16* out, const bf16* x, int rows, int inter, hipStream_t stream);
+int launch_silu_mul(bf16* out, const bf16* x, int rows, int inter, bool interleaved,
+                    hipStream_t stream);
 int launch_gelu_bias(bf16* out, const bf16* x, const bf16* bias, int rows, int cols,
                      hipStream_t stream);
 int launch_add(bf16* out, const bf16* a, const bf16* b, size_t n, hipStream_t stream);
@@ -72,6 +73,8 @@ int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_
 int launch_sample(const SampleParams& p, int B, hipStream_t stream);
 int launch_gemm_nt(bf16* C, const bf16* A, const bf16* B, float* workspace, int M, int N, int K,
                    int splits, int bn, hipStream_t stream);
+int launch_gemm_tile(void* C, const bf16* A, const bf16* B, float* workspace, int M, int N, int K,
+                     int splits, int epilogue, hipStream_t stream);
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
                        int K, hipStream_t stream);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,

@@ -47,6 +47,13 @@ class Linear(nn.Module):
             self.weight = nn.Parameter(torch.empty(0, dtype=self.weight.dtype,
                                                    device=self.weight.device), requires_grad=False)
 
+    def tile_splits(self, x: torch.Tensor) -> int:
+        """Split-K factor if ``gemm_tile`` takes this product on the GPU, else 0."""
+        if (self.bias is not None or not x.is_cuda or x.dim() != 2 or x.dtype != torch.bfloat16
+                or not x.is_contiguous() or self.weight_fp8 is not None):
+            return 0
+        return ops.tile_gemm_splits(x.shape[0], self.out_features, self.in_features)
+
     def forward(self, x: Optional[torch.Tensor],
                 x_q: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
         """``x_q`` = (fp8 rows, scales) already quantised by a fused producer kernel; then ``x`` may
@@ -57,6 +64,9 @@ class Linear(nn.Module):
                     and self.in_features % 8 == 0):
                 # 1-2 row decode batches: weight-streaming HIP kernel (csrc/kernels/gemv.hip)
                 return ops.skinny_gemm(x, self.weight, self.bias)
+            sp = self.tile_splits(x)
+            if sp:  # decode micro-batches: 256x256 MFMA tile kernel (csrc/kernels/gemm_tile.hip)
+                return ops.gemm_tile(x, self.weight, splits=sp)
             return F.linear(x, self.weight, self.bias)
         if x_q is None:
             x_q = ops.quant_rowwise(x)

@@ -66,7 +66,14 @@ class LlamaBlock(nn.Module):
                     seeded_normal_(p.data, param_seed(seed, layer.layer_idx, name), std)
         return self
 
+    def set_fused_swiglu(self, on: bool = True) -> "LlamaBlock":
+        """Reorder every gate|up weight for the tile GEMM's fused SwiGLU epilogue (GPU decode)."""
+        for layer in self.layers:
+            layer.mlp.set_fused_swiglu(on)
+        return self
+
     def quantize_fp8(self) -> "LlamaBlock":
+        self.set_fused_swiglu(False)
         for layer in self.layers:
             for lin in (layer.self_attn.qkv_proj, layer.self_attn.o_proj, layer.mlp.gate_up_proj,
                         layer.mlp.down_proj):

@@ -11,6 +11,7 @@ intended semantics (SURVEY B1/B2/B6/B7/B8/B9 fixed), MI355X-first data flow per 
     a    = o @ W_o^T
     normed, residual = add_rmsnorm(a, residual)
     h    = silu_mul(normed @ W_gate_up^T) @ W_down^T        # fused gate|up GEMM + activation.hip
+                                                            # (decode: SwiGLU in the tile GEMM epilogue)
 
 The residual stream is carried *separately* from the layer output, so each residual add is fused
 into the following RMSNorm kernel (one HBM pass) instead of being a standalone elementwise op.
@@ -85,8 +86,27 @@ class LlamaMLP(nn.Module):
                                    dtype=dtype, device=device)
         self.down_proj = Linear(spec.intermediate_size, spec.hidden_size, bias=spec.mlp_bias,
                                 dtype=dtype, device=device)
+        # True once gate_up_proj.weight's rows are in ops.swiglu_interleave order, so the tile
+        # GEMM's epilogue can apply SwiGLU itself (no [M, 2I] intermediate, no silu_mul launch)
+        self.fused_swiglu = False
+
+    def set_fused_swiglu(self, on: bool) -> None:
+        """Permute gate_up_proj's rows in place to / from the fused-SwiGLU tile order."""
+        w = self.gate_up_proj
+        if on == self.fused_swiglu:
+            return
+        if w.is_fp8 or w.bias is not None or w.out_features % 256:
+            return
+        with torch.no_grad():
+            perm = ops.swiglu_interleave if on else ops.swiglu_deinterleave
+            w.weight.data.copy_(perm(w.weight.data))
+        self.fused_swiglu = on
 
     def forward(self, normed: Optional[torch.Tensor], x_q=None) -> torch.Tensor:
+        if self.fused_swiglu:
+            if self.gate_up_proj.tile_splits(normed):
+                return self.down_proj(ops.gemm_tile(normed, self.gate_up_proj.weight, swiglu=True))
+            return self.down_proj(ops.swiglu_interleaved(self.gate_up_proj(normed)))
         gu = self.gate_up_proj(normed, x_q)
         if self.down_proj.is_fp8:  # SwiGLU fused with the fp8 quantisation of down_proj's input
             return self.down_proj(None, ops.silu_mul_quant(gu))
@@ -159,6 +179,8 @@ class LlamaDecoderLayer(nn.Module):
                 if "self_attn.o_proj.bias" in sd:
                     self.self_attn.o_proj.bias.copy_(sd["self_attn.o_proj.bias"].to(dt))
             gu = torch.cat([g("mlp.gate_proj.weight"), g("mlp.up_proj.weight")], 0)
+            if self.mlp.fused_swiglu:
+                gu = ops.swiglu_interleave(gu)
             self.mlp.gate_up_proj.weight.copy_(gu.to(dt))
             self.mlp.down_proj.weight.copy_(g("mlp.down_proj.weight").to(dt))
             self.input_layernorm.weight.copy_(g("input_layernorm.weight").to(dt))
@@ -170,7 +192,10 @@ class LlamaDecoderLayer(nn.Module):
         q, k, v = a.qkv_proj.weight.split([a.num_heads * a.head_dim,
                                            a.num_kv_heads * a.head_dim,
                                            a.num_kv_heads * a.head_dim], 0)
-        gate, up = m.gate_up_proj.weight.split([m.intermediate_size, m.intermediate_size], 0)
+        gu = m.gate_up_proj.weight
+        if m.fused_swiglu:
+            gu = ops.swiglu_deinterleave(gu)
+        gate, up = gu.split([m.intermediate_size, m.intermediate_size], 0)
         return {
             "self_attn.q_proj.weight": q, "self_attn.k_proj.weight": k,
             "self_attn.v_proj.weight": v, "self_attn.o_proj.weight": a.o_proj.weight,

@@ -6,6 +6,7 @@ There is deliberately no silent fallback: a GPU tensor with the native extension
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -295,6 +296,97 @@ def gemm_nt(x: torch.Tensor, w: torch.Tensor, splits: int = 1, bn: int = 128,
     if splits > 1 and workspace is None:
         workspace = torch.empty(splits * M * N, dtype=torch.float32, device=x.device)
     native().gemm_nt(out, x, w, int(splits), int(bn), workspace)
+    return out
+
+
+# ----------------------------------------------------------------------------- tile GEMM
+def _swiglu_src(n2: int, device) -> torch.Tensor:
+    """Row ``c`` of the interleaved weight is row ``src[c]`` of the fused [gate; up] weight."""
+    if n2 % 256:
+        raise ValueError("swiglu_interleave needs 2I % 256 == 0")
+    c = torch.arange(n2, device=device)
+    tile, cl = c // 256, c % 256
+    wave, f, lc = cl // 64, (cl % 64) // 16, cl % 16
+    out_col = tile * 128 + wave * 32 + (f // 2) * 16 + lc
+    return torch.where(f % 2 == 0, out_col, n2 // 2 + out_col)
+
+
+def swiglu_interleave(w_gate_up: torch.Tensor) -> torch.Tensor:
+    """Reorder the rows of a fused ``[gate; up]`` weight ([2I, K]) for ``gemm_tile(swiglu=True)``.
+
+    Tile-local column c (256 per tile) = wave ``c // 64``, n-fragment ``f = (c % 64) // 16``,
+    lane column ``c % 16``; fragments 2p / 2p+1 carry gate / up of output column
+    ``tile * 128 + wave * 32 + p * 16 + c % 16`` (csrc/kernels/gemm_tile.hip epilogue)."""
+    return w_gate_up.index_select(0, _swiglu_src(w_gate_up.shape[0], w_gate_up.device)).contiguous()
+
+
+def swiglu_deinterleave(w: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``swiglu_interleave``."""
+    out = torch.empty_like(w)
+    out[_swiglu_src(w.shape[0], w.device)] = w
+    return out
+
+
+def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = False,
+              out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None
+              ) -> torch.Tensor:
+    """``x [M, K] @ w[N, K]^T`` with the 256x256 LDS-DMA MFMA kernel (N % 256 == 0, K % 64 == 0).
+    ``swiglu=True``: ``w`` is a ``swiglu_interleave``d [gate; up] weight and the result is
+    ``silu(x @ gate^T) * (x @ up^T)`` ([M, N/2])."""
+    M, N = x.shape[0], w.shape[0]
+    if not _gpu(x):
+        if swiglu:
+            h = (x.float() @ swiglu_deinterleave(w).float().t()).to(x.dtype).float()
+            r = (torch.nn.functional.silu(h[:, :N // 2]) * h[:, N // 2:]).to(x.dtype)
+        else:
+            r = (x.float() @ w.float().t()).to(x.dtype)
+        return out.copy_(r) if out is not None else r
+    if out is None:
+        out = torch.empty(M, N // 2 if swiglu else N, dtype=x.dtype, device=x.device)
+    if splits > 1 and workspace is None:
+        workspace = torch.empty(splits * M * N, dtype=torch.float32, device=x.device)
+    native().gemm_tile(out, x, w, int(splits), 2 if swiglu else 0, workspace)
+    return out
+
+
+TILE_GEMM_MIN_M = 128    # below: too few rows to fill a 256-row tile (hipBLASLt / skinny path)
+TILE_GEMM_MAX_M = 2048   # above (prefill chunks): hipBLASLt's large-M solutions
+_CUS = 256
+
+
+def tile_gemm_splits(M: int, N: int, K: int) -> int:
+    """Split-K factor for ``gemm_tile`` on an [M, K] x [N, K]^T product, or 0 = not eligible.
+
+    Picks the split that best fills the 256 CUs with whole waves of 256x256 tiles (ties -> fewer
+    splits), e.g. 70B at M = 512: QKV 80 tiles x 3, O / down 64 x 4, gate|up 448 x 1 (measured
+    best per shape, profiles/gemm_tile_bench.json).  ``DLI_TILE_GEMM=0`` disables the kernel."""
+    if os.environ.get("DLI_TILE_GEMM", "1") == "0":
+        return 0
+    if not (TILE_GEMM_MIN_M <= M <= TILE_GEMM_MAX_M) or N % 256 or K % 64:
+        return 0
+    tiles = ((M + 255) // 256) * (N // 256)
+    best, best_util = 1, 0.0
+    for s in range(1, 9):
+        if s > K // 64 or (s > 1 and tiles * s > 2 * _CUS):
+            break
+        work = tiles * s
+        util = work / (_CUS * ((work + _CUS - 1) // _CUS))
+        if util > best_util + 1e-9:
+            best, best_util = s, util
+    return best
+
+
+def swiglu_interleaved(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(gate) * up from a GEMM output whose columns follow ``swiglu_interleave``'s order
+    (shapes the fused tile epilogue does not take: prefill chunks, 1-2 row batches)."""
+    M, n2 = gu.shape
+    if not _gpu(gu):
+        v = gu.float().reshape(M, n2 // 256, 4, 2, 2, 16)
+        y = (torch.nn.functional.silu(v[..., 0, :]) * v[..., 1, :]).reshape(M, n2 // 2).to(gu.dtype)
+        return out.copy_(y) if out is not None else y
+    if out is None:
+        out = torch.empty(M, n2 // 2, dtype=gu.dtype, device=gu.device)
+    native().silu_mul(out, gu, True)
     return out
 
 

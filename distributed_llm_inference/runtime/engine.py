@@ -60,6 +60,9 @@ def build_executor(spec: ModelSpec, start: int, end: int, device: torch.device, 
                         quantize=cfg.quantize, checkpoint=cfg.checkpoint)
     cc, sc = cfg.cache, cfg.serve
     nlayers = end - start
+    if device.type == "cuda" and hasattr(stage.block, "set_fused_swiglu"):
+        # bf16 gate|up weights in the tile GEMM's SwiGLU order (fp8 stages keep theirs)
+        stage.block.set_fused_swiglu(True)
     if device.type == "cuda" and sc.use_graphs:
         from .gemm_tuning import tune_decode_gemms
         buckets = [b for b in sc.graph_batch_sizes if 16 <= b <= sc.max_batch_size]

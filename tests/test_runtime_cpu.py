@@ -395,3 +395,23 @@ def test_fp8_kv_cache_close_to_bf16_cpu():
     a, b = logits(torch.bfloat16), logits(torch.float8_e4m3fn)
     for x, y in zip(a, b):
         assert ((x - y).norm() / x.norm()).item() < 0.08
+
+
+def test_swiglu_interleave_roundtrip_and_tile_splits():
+    import torch
+    from distributed_llm_inference import ops
+    w = torch.randn(1024, 8)
+    wi = ops.swiglu_interleave(w)
+    assert torch.equal(ops.swiglu_deinterleave(wi), w)
+    # interleaved GEMM output -> silu(gate) * up in natural column order
+    x = torch.randn(5, 8)
+    ref = ops.silu_mul((x @ w.t()).bfloat16()).float()
+    got = ops.swiglu_interleaved((x @ wi.t()).bfloat16()).float()
+    assert (ref - got).abs().max() < 2e-2 * ref.abs().max()
+    # split-K choice fills whole waves of 256 CUs (70B decode shapes at M = 512)
+    assert ops.tile_gemm_splits(512, 10240, 8192) == 3
+    assert ops.tile_gemm_splits(512, 8192, 8192) == 4
+    assert ops.tile_gemm_splits(512, 8192, 28672) == 4
+    assert ops.tile_gemm_splits(512, 57344, 8192) == 1
+    assert ops.tile_gemm_splits(64, 8192, 8192) == 0      # too few rows
+    assert ops.tile_gemm_splits(512, 100, 8192) == 0      # N not a multiple of 256
