@@ -29,6 +29,12 @@
 //   * raw `s_barrier` (no __syncthreads: its fence would drain the DMA queue) and one __shared__
 //     array (a second one makes hipcc wait vmcnt(0) before the first ds_read of every phase);
 //   * blockIdx is remapped so the blocks of one XCD run neighbouring tiles (§5.5 T1, bijective);
+//   * the MFMAs take the weight fragment as the A operand, so the accumulator holds the tile
+//     transposed and every lane owns 4 consecutive output columns (vector stores);
+//   * split-K partials are reduced by a separate full-chip pass: an in-launch stream-K fix-up
+//     (last-arriving workgroup sums the other partials) was measured 20-70 % slower on these
+//     shapes — a 256 KB fp32 partial tile is far past what one CU's ~100 GB/s read path
+//     reduces cheaply (§5 "In-launch split-K reduction": worth it at tens of KB per tile);
 //   * epilogues: bf16 store, fp32 split-K slab (summed by `splitk_reduce`), or fused SwiGLU:
 //     with B's rows interleaved by `swiglu_interleave` (gate and up rows of the same output
 //     column land in n-fragments 2p and 2p+1 of one wave) the wave holds gate and up of an output
@@ -151,7 +157,7 @@ gemm_tile_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* _
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[mq * 4 + i][nq * 2 + j] = mfma(af[i][kk], bf[j][kk], acc[mq * 4 + i][nq * 2 + j]);
+          acc[mq * 4 + i][nq * 2 + j] = mfma(bf[j][kk], af[i][kk], acc[mq * 4 + i][nq * 2 + j]);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -208,49 +214,57 @@ gemm_tile_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* _
   }
   if (wr == 0) barrier();
 
-  // ---- epilogue: C/D fragment map col = lane & 15, row = 4 * (lane >> 4) + r ----
-  const int crow = m0 + wr * 128 + (lane >> 4) * 4;
-  const int ccol = n0 + wc * 64 + fr;
+  // ---- epilogue ----
+  // The MFMAs compute the transposed tile (A operand = weight rows): fragment (i, j) element e of
+  // lane l is C[row = 16 i + (l & 15)][col = 16 j + 4 (l >> 4) + e], so each lane owns 4
+  // consecutive output columns of one row -> 8-B (bf16) / 16-B (fp32) vector stores.
+  const int crow = m0 + wr * 128 + fr;
+  const int cq = 4 * (lane >> 4);
   if (EPI == kSwiGLU) {
-    // n-fragments (2p, 2p+1) = (gate, up) of output columns n0/2 + wc*32 + p*16 + fr
+    // n-fragments (2p, 2p+1) = (gate, up) of output columns n0/2 + wc*32 + p*16 + cq + e
     bf16* out = reinterpret_cast<bf16*>(C);
     const int I = N >> 1;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i) {
+      const int row = crow + i * 16;
+      if (row >= M) continue;
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
-        const int col = (n0 >> 1) + wc * 32 + p * 16 + fr;
+        bf16x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int row = crow + i * 16 + e;
-          // round gate and up to bf16 first: bit-matches the unfused GEMM -> silu_mul path
+          // round gate and up to bf16 first: matches the unfused GEMM -> silu_mul path
           const float g = (float)(bf16)acc[i][2 * p][e];
           const float u = (float)(bf16)acc[i][2 * p + 1][e];
-          if (row < M) out[(size_t)row * I + col] = (bf16)(silu(g) * u);
+          o[e] = (bf16)(silu(g) * u);
         }
+        *reinterpret_cast<bf16x4*>(out + (size_t)row * I + (n0 >> 1) + wc * 32 + p * 16 + cq) = o;
       }
+    }
   } else if (EPI == kStoreF32) {
     float* out = reinterpret_cast<float*>(C) + (size_t)split * M * N;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i) {
+      const int row = crow + i * 16;
+      if (row >= M) continue;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = crow + i * 16 + e;
-          if (row < M) out[(size_t)row * N + ccol + j * 16] = acc[i][j][e];
-        }
+        *reinterpret_cast<f32x4*>(out + (size_t)row * N + n0 + wc * 64 + j * 16 + cq) = acc[i][j];
+    }
   } else {
     bf16* out = reinterpret_cast<bf16*>(C);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i) {
+      const int row = crow + i * 16;
+      if (row >= M) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 4; ++j) {
+        bf16x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = crow + i * 16 + e;
-          if (row < M) out[(size_t)row * N + ccol + j * 16] = (bf16)acc[i][j][e];
-        }
+        for (int e = 0; e < 4; ++e) o[e] = (bf16)acc[i][j][e];
+        *reinterpret_cast<bf16x4*>(out + (size_t)row * N + n0 + wc * 64 + j * 16 + cq) = o;
+      }
+    }
   }
 }
 

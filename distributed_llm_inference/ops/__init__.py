@@ -365,6 +365,8 @@ def tile_gemm_splits(M: int, N: int, K: int) -> int:
     if not (TILE_GEMM_MIN_M <= M <= TILE_GEMM_MAX_M) or N % 256 or K % 64:
         return 0
     tiles = ((M + 255) // 256) * (N // 256)
+    if tiles > 2 * _CUS:
+        return 0  # e.g. the 128256-wide LM head: hipBLASLt's wide-N solutions are faster (690 vs 824 us)
     best, best_util = 1, 0.0
     for s in range(1, 9):
         if s > K // 64 or (s > 1 and tiles * s > 2 * _CUS):

@@ -15,6 +15,7 @@ def short(name: str) -> str:
     if name.startswith("Cijk") or name.startswith("Custom_Cijk"):
         m = re.search(r"MT(\d+x\d+x\d+)", name)
         return f"hipBLASLt_GEMM[{m.group(1) if m else '?'}]" + ("_SK" if "_SK" in name else "")
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*", "", name)
     name = name.replace("void ", "")
     return name[:90]

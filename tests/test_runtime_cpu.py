@@ -415,3 +415,4 @@ def test_swiglu_interleave_roundtrip_and_tile_splits():
     assert ops.tile_gemm_splits(512, 57344, 8192) == 1
     assert ops.tile_gemm_splits(64, 8192, 8192) == 0      # too few rows
     assert ops.tile_gemm_splits(512, 100, 8192) == 0      # N not a multiple of 256
+    assert ops.tile_gemm_splits(512, 128256, 8192) == 0   # LM head stays on hipBLASLt
