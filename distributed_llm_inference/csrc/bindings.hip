@@ -381,45 +381,35 @@ void silu_mul_quant(Tensor q_out, Tensor scale, Tensor x) {
            "silu_mul_quant");
 }
 
-// ------------------------------------------------------------------------------ decode GEMM
-void gemm_nt(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t bn,
-             optional<Tensor> workspace) {
-  CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
-  CHECK_BF16(out); CHECK_BF16(a); CHECK_BF16(b);
-  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_nt: 2-D tensors");
-  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
-  TORCH_CHECK(b.size(1) == K && out.size(0) == M && out.size(1) == N, "gemm_nt: shape mismatch");
-  TORCH_CHECK(M >= 1 && M <= 256, "gemm_nt: M must be in [1, 256]");
-  TORCH_CHECK(K % 64 == 0 && N % bn == 0 && (bn == 64 || bn == 128), "gemm_nt: K%64, N%bn");
-  TORCH_CHECK(splits >= 1 && (K / 64) % splits == 0, "gemm_nt: splits must divide K/64");
-  float* ws = nullptr;
-  if (splits > 1) {
-    TORCH_CHECK(workspace.has_value(), "gemm_nt: split-K needs a workspace");
-    CHECK_IN(*workspace); CHECK_F32(*workspace);
-    TORCH_CHECK(workspace->numel() >= splits * M * N, "gemm_nt: workspace too small");
-    ws = workspace->data_ptr<float>();
-  }
-  const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
-  check_rc(dli::launch_gemm_nt(bp(out), bp(a), bp(b), ws, (int)M, (int)N, (int)K, (int)splits,
-                               (int)bn, cur_stream()), "gemm_nt");
-}
-
 // ------------------------------------------------------------------------------ tile GEMM
 // epilogue 0: out = A . B^T (bf16); 2: out[:, n] = silu(g) * u with B rows interleaved by
 // ops.swiglu_interleave (out has N / 2 columns).  splits > 1 (epilogue 0 only) needs an fp32
-// workspace of splits * M * N.
+// workspace of splits * M * N.  fp8: A, B are e4m3 bytes with a_scale [M] and b_scale [N] (fp32,
+// both required); out = (A . B^T) * a_scale[:, None] * b_scale[None, :].
 void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
-               optional<Tensor> workspace) {
-  CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
-  CHECK_BF16(out); CHECK_BF16(a); CHECK_BF16(b);
+               optional<Tensor> workspace, optional<Tensor> a_scale, optional<Tensor> b_scale) {
+  CHECK_IN(out); CHECK_IN(a); CHECK_IN(b); CHECK_BF16(out);
+  const bool fp8 = a.element_size() == 1;
+  TORCH_CHECK(a.scalar_type() == b.scalar_type(), "gemm_tile: a and b must share a dtype");
+  TORCH_CHECK(fp8 || a.scalar_type() == at::kBFloat16, "gemm_tile: bf16 or fp8 (e4m3) operands");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_tile: 2-D tensors");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K && out.size(0) == M, "gemm_tile: shape mismatch");
   TORCH_CHECK(epilogue == 0 || epilogue == 2, "gemm_tile: epilogue must be 0 (store) or 2 (swiglu)");
   TORCH_CHECK(out.size(1) == (epilogue == 2 ? N / 2 : N), "gemm_tile: output columns");
-  TORCH_CHECK(M >= 1 && M <= (1 << 20) && N % 256 == 0 && K % 64 == 0 && K > 0,
-              "gemm_tile: needs N % 256 == 0 and K % 64 == 0");
-  TORCH_CHECK(splits >= 1 && splits <= K / 64, "gemm_tile: 1 <= splits <= K / 64");
+  const int64_t kt = K * a.element_size() / 128;
+  TORCH_CHECK(M >= 1 && M <= (1 << 20) && N % 256 == 0 && (K * a.element_size()) % 128 == 0 && K > 0,
+              "gemm_tile: needs N % 256 == 0 and 128-byte multiples of K");
+  TORCH_CHECK(splits >= 1 && splits <= kt, "gemm_tile: 1 <= splits <= k-tiles");
+  const float* sa = nullptr;
+  const float* sb = nullptr;
+  if (fp8) {
+    TORCH_CHECK(a_scale.has_value() && b_scale.has_value(), "gemm_tile: fp8 needs a_scale, b_scale");
+    CHECK_IN(*a_scale); CHECK_IN(*b_scale); CHECK_F32(*a_scale); CHECK_F32(*b_scale);
+    TORCH_CHECK(a_scale->numel() == M && b_scale->numel() == N, "gemm_tile: scale sizes");
+    sa = a_scale->data_ptr<float>();
+    sb = b_scale->data_ptr<float>();
+  }
   float* ws = nullptr;
   if (splits > 1) {
     TORCH_CHECK(epilogue == 0, "gemm_tile: split-K only with the plain store epilogue");
@@ -429,8 +419,9 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
     ws = workspace->data_ptr<float>();
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
-  check_rc(dli::launch_gemm_tile(out.data_ptr(), bp(a), bp(b), ws, (int)M, (int)N, (int)K,
-                                 (int)splits, (int)epilogue, cur_stream()), "gemm_tile");
+  check_rc(dli::launch_gemm_tile(out.data_ptr(), a.data_ptr(), b.data_ptr(), sa, sb, ws, (int)M,
+                                 (int)N, (int)K, (int)splits, (int)epilogue, fp8, cur_stream()),
+           "gemm_tile");
 }
 
 // ------------------------------------------------------------------------------ skinny GEMM
@@ -475,12 +466,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("q_out"), py::arg("scale"), py::arg("x"), py::arg("residual"), py::arg("norm_w"),
         py::arg("eps"), py::arg("residual_out") = py::none());
   m.def("silu_mul_quant", &silu_mul_quant, "SwiGLU fused with row-wise fp8 quantisation");
-  m.def("gemm_nt", &gemm_nt, "decode GEMM C = A . B^T (M <= 256, split-K MFMA)", py::arg("out"),
-        py::arg("a"), py::arg("b"), py::arg("splits"), py::arg("bn"),
-        py::arg("workspace") = py::none());
   m.def("gemm_tile", &gemm_tile, "C = A . B^T, 256x256 LDS-DMA 8-phase MFMA tile GEMM",
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
-        py::arg("epilogue") = 0, py::arg("workspace") = py::none());
+        py::arg("epilogue") = 0, py::arg("workspace") = py::none(),
+        py::arg("a_scale") = py::none(), py::arg("b_scale") = py::none());
   m.def("skinny_gemm", &skinny_gemm, "y = x . W^T (+ bias) for M <= 4 (weight-streaming GEMV)",
         py::arg("out"), py::arg("x"), py::arg("w"), py::arg("bias") = py::none());
   register_rccl(m);

@@ -71,10 +71,32 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
-template <int EPI>
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// fp8 e4m3 x fp8 e4m3 -> fp32, K = 128, through the block-scaled MFMA (2x the bf16 rate on
+// gfx950; the plain fp8 16x16x32 form only runs at the bf16 rate).  Block scales are all 1.0
+// (e8m0 127): the per-row activation and per-channel weight scales are applied in the epilogue.
+// Both operands are read with the same lane/byte pattern, so the products pair the same k.
+__device__ __forceinline__ f32x4 mfma_fp8(const bf16x8& a0, const bf16x8& a1, const bf16x8& b0,
+                                          const bf16x8& b1, const f32x4& c) {
+  typedef int i32x4_t __attribute__((ext_vector_type(4)));
+  const i32x4_t al = __builtin_bit_cast(i32x4_t, a0), ah = __builtin_bit_cast(i32x4_t, a1);
+  const i32x4_t bl = __builtin_bit_cast(i32x4_t, b0), bh = __builtin_bit_cast(i32x4_t, b1);
+  const i32x8 a = {al[0], al[1], al[2], al[3], ah[0], ah[1], ah[2], ah[3]};
+  const i32x8 b = {bl[0], bl[1], bl[2], bl[3], bh[0], bh[1], bh[2], bh[3]};
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
+// FP8: A and B are e4m3 bytes (K counted in elements = bytes), a_scale[M] / b_scale[N] fp32.
+// Staging is byte-identical to bf16 (a k-tile is 128 bytes of every row: 64 bf16 or 128 fp8).
+template <int EPI, bool FP8>
 __global__ void __launch_bounds__(kThreads, 1)
-gemm_tile_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __restrict__ C,
+gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __restrict__ C,
+                 const float* __restrict__ a_scale, const float* __restrict__ b_scale,
                  int M, int N, int K, int tiles_m, int tiles_n, int k_tiles_per_split) {
+  const char* A = reinterpret_cast<const char*>(Av);
+  const char* B = reinterpret_cast<const char*>(Bv);
+  const size_t Kb = (size_t)K * (FP8 ? 1 : 2);   // row stride in bytes
   __shared__ __attribute__((aligned(1024))) char smem[kLds];
 
   // ---- XCD-aware, bijective block remap (consecutive logical ids share an XCD / its L2) ----
@@ -87,15 +109,15 @@ gemm_tile_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* _
   const int split = lid / (tiles_m * tiles_n);
   const int m0 = tm * kTM, n0 = tn * kTN;
   const int kt0 = split * k_tiles_per_split;
-  const int T = min(k_tiles_per_split, K / kTK - kt0);
+  const int T = min(k_tiles_per_split, (int)(Kb / 128) - kt0);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
 
   // ---- DMA source rows: thread stages LDS units u = j*512 + tid (j = 0, 1) of each half-tile ----
   // unit u -> local row lr = u >> 3, LDS slot s = u & 7, global chunk s ^ ((lr >> 1) & 7)
-  const bf16* srcA[2][2];
-  const bf16* srcB[2][2];
+  const char* srcA[2][2];
+  const char* srcB[2][2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int u = j * kThreads + tid;
@@ -105,17 +127,17 @@ gemm_tile_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* _
       const int ga = (lr >> 6) * 128 + h * 64 + (lr & 63);
       const int gb = (lr >> 5) * 64 + h * 32 + (lr & 31);
       const int ra = min(m0 + ga, M - 1);       // rows past M are computed, never stored
-      srcA[h][j] = A + (size_t)ra * K + (size_t)kt0 * kTK + ch * 8;
-      srcB[h][j] = B + (size_t)(n0 + gb) * K + (size_t)kt0 * kTK + ch * 8;
+      srcA[h][j] = A + (size_t)ra * Kb + (size_t)kt0 * 128 + ch * 16;
+      srcB[h][j] = B + (size_t)(n0 + gb) * Kb + (size_t)kt0 * 128 + ch * 16;
     }
   }
   // stage half `which` (0 = A0, 1 = A1, 2 = B0, 3 = B1) of k-tile t into buffer t & 1
   auto stage = [&](int which, int t) {
     char* dst = smem + (t & 1) * kBuf + which * kHalf + wave * 1024;
-    const size_t koff = (size_t)t * kTK;
+    const size_t koff = (size_t)t * 128;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const bf16* src = which < 2 ? srcA[which][j] : srcB[which - 2][j];
+      const char* src = which < 2 ? srcA[which][j] : srcB[which - 2][j];
       dma16(src + koff, dst + j * 8192);
     }
   };
@@ -151,13 +173,23 @@ gemm_tile_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* _
   };
   auto quadrant = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
     __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    if (FP8) {
+      // one K=128 MFMA per fragment pair: the two 16-B chunks (g, g+4) of the 128-B k-tile row
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[mq * 4 + i][nq * 2 + j] = mfma(bf[j][kk], af[i][kk], acc[mq * 4 + i][nq * 2 + j]);
+          acc[mq * 4 + i][nq * 2 + j] = mfma_fp8(bf[j][0], bf[j][1], af[i][0], af[i][1],
+                                                 acc[mq * 4 + i][nq * 2 + j]);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[mq * 4 + i][nq * 2 + j] = mfma(bf[j][kk], af[i][kk], acc[mq * 4 + i][nq * 2 + j]);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -220,6 +252,17 @@ gemm_tile_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* _
   // consecutive output columns of one row -> 8-B (bf16) / 16-B (fp32) vector stores.
   const int crow = m0 + wr * 128 + fr;
   const int cq = 4 * (lane >> 4);
+  if (FP8) {  // dequantise: per-row activation scale x per-output-channel weight scale
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float sa = a_scale[min(crow + i * 16, M - 1)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 sb = *reinterpret_cast<const f32x4*>(b_scale + n0 + wc * 64 + j * 16 + cq);
+        acc[i][j] = acc[i][j] * sb * sa;
+      }
+    }
+  }
   if (EPI == kSwiGLU) {
     // n-fragments (2p, 2p+1) = (gate, up) of output columns n0/2 + wc*32 + p*16 + cq + e
     bf16* out = reinterpret_cast<bf16*>(C);
@@ -289,35 +332,48 @@ __global__ void __launch_bounds__(256) tile_splitk_reduce_kernel(bf16* __restric
   }
 }
 
-}  // namespace
-
-int launch_gemm_tile(void* C, const bf16* A, const bf16* B, float* workspace, int M, int N, int K,
-                     int splits, int epilogue, hipStream_t stream) {
-  if (M <= 0 || N % kTN != 0 || K % kTK != 0 || splits < 1) return -1;
-  const int kt = K / kTK;
+template <bool FP8>
+int launch_tile(void* C, const void* A, const void* B, const float* sa, const float* sb,
+                float* workspace, int M, int N, int K, int splits, int epilogue,
+                hipStream_t stream) {
+  const int kt = (int)((size_t)K * (FP8 ? 1 : 2) / 128);
+  if (M <= 0 || N % kTN != 0 || (size_t)K * (FP8 ? 1 : 2) % 128 != 0 || splits < 1) return -1;
   if (splits > kt) return -2;
   const int kps = (kt + splits - 1) / splits;
   if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
   if (splits > 1 && (workspace == nullptr || epilogue != kStoreBf16)) return -3;
+  if (FP8 && (sa == nullptr || sb == nullptr)) return -5;
   const int tiles_m = (M + kTM - 1) / kTM, tiles_n = N / kTN;
   const int grid = tiles_m * tiles_n * splits;
   if (splits > 1) {
-    gemm_tile_kernel<kStoreF32><<<grid, kThreads, 0, stream>>>(A, B, workspace, M, N, K, tiles_m,
-                                                               tiles_n, kps);
+    gemm_tile_kernel<kStoreF32, FP8><<<grid, kThreads, 0, stream>>>(A, B, workspace, sa, sb, M, N,
+                                                                    K, tiles_m, tiles_n, kps);
     const size_t MN = (size_t)M * N;
     size_t blocks = (MN / 8 + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     tile_splitk_reduce_kernel<<<(int)blocks, 256, 0, stream>>>(reinterpret_cast<bf16*>(C),
                                                                workspace, splits, MN);
   } else if (epilogue == kSwiGLU) {
-    gemm_tile_kernel<kSwiGLU><<<grid, kThreads, 0, stream>>>(A, B, C, M, N, K, tiles_m, tiles_n, kps);
+    gemm_tile_kernel<kSwiGLU, FP8><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K, tiles_m,
+                                                                  tiles_n, kps);
   } else if (epilogue == kStoreBf16) {
-    gemm_tile_kernel<kStoreBf16><<<grid, kThreads, 0, stream>>>(A, B, C, M, N, K, tiles_m, tiles_n,
-                                                                kps);
+    gemm_tile_kernel<kStoreBf16, FP8><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
+                                                                     tiles_m, tiles_n, kps);
   } else {
     return -4;
   }
   return 0;
+}
+
+}  // namespace
+
+int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale,
+                     const float* b_scale, float* workspace, int M, int N, int K, int splits,
+                     int epilogue, bool fp8, hipStream_t stream) {
+  return fp8 ? launch_tile<true>(C, A, B, a_scale, b_scale, workspace, M, N, K, splits, epilogue,
+                                 stream)
+             : launch_tile<false>(C, A, B, nullptr, nullptr, workspace, M, N, K, splits, epilogue,
+                                  stream);
 }
 
 }  // namespace dli

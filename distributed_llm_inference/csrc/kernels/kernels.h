@@ -71,10 +71,9 @@ int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stre
 int launch_attn_decode(const AttnParams& p, int B, int D, hipStream_t stream);
 int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_t stream);
 int launch_sample(const SampleParams& p, int B, hipStream_t stream);
-int launch_gemm_nt(bf16* C, const bf16* A, const bf16* B, float* workspace, int M, int N, int K,
-                   int splits, int bn, hipStream_t stream);
-int launch_gemm_tile(void* C, const bf16* A, const bf16* B, float* workspace, int M, int N, int K,
-                     int splits, int epilogue, hipStream_t stream);
+int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale,
+                     const float* b_scale, float* workspace, int M, int N, int K, int splits,
+                     int epilogue, bool fp8, hipStream_t stream);
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
                        int K, hipStream_t stream);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,

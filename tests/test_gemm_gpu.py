@@ -1,37 +1,10 @@
-"""Hand-written decode GEMM (csrc/kernels/gemm.hip) vs an fp32 PyTorch reference."""
+"""Hand-written GEMMs (csrc/kernels/gemm_tile.hip, gemv.hip) vs fp32 PyTorch references."""
 import pytest
 import torch
 
 from distributed_llm_inference import ops
 
 pytestmark = pytest.mark.gpu
-
-
-_CASES = [(M, N, K, bn, splits)
-          for M in (1, 37, 128, 256)
-          for N, K in ((128, 128), (256, 1024), (384, 2048))
-          for bn, splits in ((128, 1), (64, 1), (128, 2), (64, 4))
-          if N % bn == 0 and (K // 64) % splits == 0]  # only tileable shapes
-
-
-@pytest.mark.parametrize("M,N,K,bn,splits", _CASES)
-def test_gemm_nt_matches_fp32(gpu, M, N, K, bn, splits):
-    torch.manual_seed(M + N + K)
-    x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
-    w = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
-    y = ops.gemm_nt(x, w, splits=splits, bn=bn)
-    ref = x.float() @ w.float().t()
-    err = (y.float() - ref).abs().max().item()
-    assert err < 2e-2 * max(1.0, ref.abs().max().item()), err
-
-
-def test_gemm_nt_asymmetric_identity(gpu):
-    # A = I (rows 0..M-1 of identity) with an asymmetric B catches transposed C writes
-    M, K, N = 64, 128, 128
-    x = torch.eye(M, K, device=gpu, dtype=torch.bfloat16)
-    w = torch.arange(N * K, device=gpu, dtype=torch.float32).reshape(N, K).remainder(251).to(torch.bfloat16)
-    y = ops.gemm_nt(x, w, splits=1, bn=128)
-    assert torch.equal(y.float(), w.float().t()[:M])
 
 
 @pytest.mark.parametrize("M", [1, 2, 3, 4])
@@ -131,3 +104,35 @@ def test_linear_dispatches_decode_batches_to_tile_gemm(gpu, monkeypatch):
     assert calls, "M=512 decode batch did not use the tile GEMM"
     ref = x.float() @ lin.weight.float().t()
     assert (y.float() - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(256, 256, 128, 1), (512, 512, 2048, 1), (100, 768, 1024, 3),
+                                          (512, 1024, 8192, 4), (33, 256, 384, 1)])
+def test_gemm_tile_fp8_matches_dequantised_fp32(gpu, M, N, K, splits):
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=gpu)
+    w = torch.randn(N, K, device=gpu) / K ** 0.5
+    xq, xs = ops.quant_rowwise(x.to(torch.bfloat16))
+    wq, ws = ops.quantize_weight_fp8(w.to(torch.bfloat16))
+    ref = (xq.float() * xs.reshape(-1, 1)) @ (wq.float() * ws.reshape(-1, 1)).t()
+    y = ops.gemm_tile_fp8(xq, xs, wq, ws, splits).float()
+    assert (y - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+
+
+def test_gemm_tile_fp8_exact_integers_and_swiglu(gpu):
+    # exact small integers: any k-pairing mistake between the operands shows up bit-exactly
+    xi = torch.zeros(256, 128, device=gpu)
+    xi[torch.arange(128), torch.arange(128)] = 1.0
+    wi = (torch.arange(256 * 128, device=gpu, dtype=torch.float32).reshape(256, 128) % 13) - 6
+    one = torch.ones(256, device=gpu)
+    y = ops.gemm_tile_fp8(xi.to(torch.float8_e4m3fn), one, wi.to(torch.float8_e4m3fn), one).float()
+    assert torch.equal(y, xi @ wi.t())
+    x = torch.randn(512, 1024, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(1024, 1024, device=gpu) / 32).to(torch.bfloat16)
+    xq, xs = ops.quant_rowwise(x)
+    wq, ws = ops.quantize_weight_fp8(w)
+    ref = ops.silu_mul(((xq.float() * xs) @ (wq.float() * ws.reshape(-1, 1)).t()).to(torch.bfloat16)).float()
+    wqi = ops.swiglu_interleave(wq.view(torch.uint8)).view(wq.dtype)
+    wsi = ops.swiglu_interleave(ws.reshape(-1, 1)).reshape(-1)
+    y = ops.gemm_tile_fp8(xq, xs, wqi, wsi, swiglu=True).float()
+    assert (y - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
