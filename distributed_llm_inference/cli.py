@@ -27,6 +27,10 @@ def _common(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--gpus", type=int, default=1, help="pipeline stages = processes = GPUs")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--fp8", action="store_true", help="fp8-e4m3 weights")
+    ap.add_argument("--int8", action="store_true",
+                    help="LLM.int8 weights (int8 MFMA + bf16 outlier columns), the reference's mode")
+    ap.add_argument("--int8-threshold", type=float, default=6.0,
+                    help="LLM.int8 outlier threshold (bitsandbytes / reference default 6.0 / 5.0)")
     ap.add_argument("--kv-dtype", choices=["bf16", "fp8"], default="bf16",
                     help="KV cache element type (fp8 = e4m3, half the bytes)")
     ap.add_argument("--window", type=int, default=0, help="attention-sink window length (0=full)")
@@ -47,7 +51,8 @@ def engine_config(a):
     from .runtime.engine import EngineConfig
     return EngineConfig(
         model=a.model, checkpoint=a.checkpoint, random_init=a.checkpoint is None, seed=a.seed,
-        quantize=a.fp8, pp=a.gpus,
+        quantize="fp8" if a.fp8 else ("int8" if a.int8 else False),
+        int8_threshold=a.int8_threshold, pp=a.gpus,
         cache=CacheConfig(block_size=a.block_size, gpu_memory_utilization=a.gpu_mem,
                           window_length=a.window, num_sink_tokens=a.sinks, dtype=a.kv_dtype),
         serve=ServeConfig(max_batch_size=a.max_batch, max_num_batched_tokens=a.max_batched_tokens,
@@ -68,7 +73,7 @@ def cmd_plan(a) -> int:
     from .models.llama.cache import KVPool
     spec = resolve_model(a.checkpoint or a.model)
     ranges = plan_stages(spec, a.gpus)
-    per_layer = spec.layer_param_count() * (1 if a.fp8 else 2)
+    per_layer = spec.layer_param_count() * (1 if (a.fp8 or a.int8) else 2)
     emb = spec.vocab_size * spec.hidden_size * 2
     out = []
     for i, (s, e) in enumerate(ranges):

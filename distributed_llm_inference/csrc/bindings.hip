@@ -368,6 +368,26 @@ void quant_rowwise(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> residu
            "quant_rowwise");
 }
 
+void quant_rowwise_int8(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> outlier) {
+  CHECK_IN(q_out); CHECK_IN(scale); CHECK_IN(x); CHECK_BF16(x); CHECK_F32(scale);
+  TORCH_CHECK(q_out.scalar_type() == at::kChar, "q_out must be int8");
+  TORCH_CHECK(x.dim() == 2, "quant_rowwise_int8: x must be [rows, K]");
+  const int64_t rows = x.size(0), K = x.size(1);
+  TORCH_CHECK(q_out.numel() == x.numel() && scale.numel() == rows, "quant_rowwise_int8: shape mismatch");
+  const uint8_t* f = nullptr;
+  if (outlier.has_value()) {
+    CHECK_IN(*outlier);
+    TORCH_CHECK(outlier->element_size() == 1 && outlier->numel() == K,
+                "quant_rowwise_int8: outlier must be K bytes");
+    f = reinterpret_cast<const uint8_t*>(outlier->data_ptr());
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_rc(dli::launch_quant_rowwise_int8(reinterpret_cast<int8_t*>(q_out.data_ptr()),
+                                          scale.data_ptr<float>(), bp(x), f, (int)rows, (int)K,
+                                          cur_stream()),
+           "quant_rowwise_int8");
+}
+
 void silu_mul_quant(Tensor q_out, Tensor scale, Tensor x) {
   CHECK_IN(q_out); CHECK_IN(scale); CHECK_IN(x); CHECK_BF16(x); CHECK_F32(scale);
   TORCH_CHECK(q_out.element_size() == 1, "q_out must be an 8-bit tensor");
@@ -389,9 +409,10 @@ void silu_mul_quant(Tensor q_out, Tensor scale, Tensor x) {
 void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
                optional<Tensor> workspace, optional<Tensor> a_scale, optional<Tensor> b_scale) {
   CHECK_IN(out); CHECK_IN(a); CHECK_IN(b); CHECK_BF16(out);
-  const bool fp8 = a.element_size() == 1;
+  const bool fp8 = a.element_size() == 1;   // 1-byte operands: fp8 e4m3 or int8
   TORCH_CHECK(a.scalar_type() == b.scalar_type(), "gemm_tile: a and b must share a dtype");
-  TORCH_CHECK(fp8 || a.scalar_type() == at::kBFloat16, "gemm_tile: bf16 or fp8 (e4m3) operands");
+  TORCH_CHECK(fp8 || a.scalar_type() == at::kBFloat16, "gemm_tile: bf16, fp8 (e4m3) or int8 operands");
+  const int precision = !fp8 ? 0 : (a.scalar_type() == at::kChar ? 2 : 1);
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_tile: 2-D tensors");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K && out.size(0) == M, "gemm_tile: shape mismatch");
@@ -404,7 +425,7 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
   const float* sa = nullptr;
   const float* sb = nullptr;
   if (fp8) {
-    TORCH_CHECK(a_scale.has_value() && b_scale.has_value(), "gemm_tile: fp8 needs a_scale, b_scale");
+    TORCH_CHECK(a_scale.has_value() && b_scale.has_value(), "gemm_tile: 8-bit needs a_scale, b_scale");
     CHECK_IN(*a_scale); CHECK_IN(*b_scale); CHECK_F32(*a_scale); CHECK_F32(*b_scale);
     TORCH_CHECK(a_scale->numel() == M && b_scale->numel() == N, "gemm_tile: scale sizes");
     sa = a_scale->data_ptr<float>();
@@ -420,7 +441,7 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
   check_rc(dli::launch_gemm_tile(out.data_ptr(), a.data_ptr(), b.data_ptr(), sa, sb, ws, (int)M,
-                                 (int)N, (int)K, (int)splits, (int)epilogue, fp8, cur_stream()),
+                                 (int)N, (int)K, (int)splits, (int)epilogue, precision, cur_stream()),
            "gemm_tile");
 }
 
@@ -465,6 +486,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("quant_rowwise", &quant_rowwise, "row-wise fp8 e4m3 quantisation (+fused RMSNorm)",
         py::arg("q_out"), py::arg("scale"), py::arg("x"), py::arg("residual"), py::arg("norm_w"),
         py::arg("eps"), py::arg("residual_out") = py::none());
+  m.def("quant_rowwise_int8", &quant_rowwise_int8, "LLM.int8 row-wise int8 quantisation (outlier columns zeroed)",
+        py::arg("q_out"), py::arg("scale"), py::arg("x"), py::arg("outlier") = py::none());
   m.def("silu_mul_quant", &silu_mul_quant, "SwiGLU fused with row-wise fp8 quantisation");
   m.def("gemm_tile", &gemm_tile, "C = A . B^T, 256x256 LDS-DMA 8-phase MFMA tile GEMM",
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,

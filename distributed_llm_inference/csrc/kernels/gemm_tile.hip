@@ -35,6 +35,9 @@
 //     (last-arriving workgroup sums the other partials) was measured 20-70 % slower on these
 //     shapes — a 256 KB fp32 partial tile is far past what one CU's ~100 GB/s read path
 //     reduces cheaply (§5 "In-launch split-K reduction": worth it at tens of KB per tile);
+//   * 1-byte operands (same staging: a k-tile is 128 bytes per row): fp8 e4m3 on the block-scaled
+//     K=128 MFMA (2x the bf16 rate, unit block scales) and int8 on v_mfma_i32_16x16x64_i8 (LLM.int8
+//     weights); per-row / per-channel scales are applied in the epilogue;
 //   * epilogues: bf16 store, fp32 split-K slab (summed by `splitk_reduce`), or fused SwiGLU:
 //     with B's rows interleaved by `swiglu_interleave` (gate and up rows of the same output
 //     column land in n-fragments 2p and 2p+1 of one wave) the wave holds gate and up of an output
@@ -87,16 +90,29 @@ __device__ __forceinline__ f32x4 mfma_fp8(const bf16x8& a0, const bf16x8& a1, co
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
 }
 
-// FP8: A and B are e4m3 bytes (K counted in elements = bytes), a_scale[M] / b_scale[N] fp32.
-// Staging is byte-identical to bf16 (a k-tile is 128 bytes of every row: 64 bf16 or 128 fp8).
-template <int EPI, bool FP8>
+// int8 x int8 -> int32, K = 64 (2x the bf16 rate); the accumulator registers hold int32 bits.
+__device__ __forceinline__ f32x4 mfma_i8(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  typedef int i32x4_t __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
+      __builtin_bit_cast(i32x4_t, a), __builtin_bit_cast(i32x4_t, b),
+      __builtin_bit_cast(i32x4_t, c), 0, 0, 0));
+}
+
+enum Prec { kBf16 = 0, kFp8 = 1, kInt8 = 2 };
+
+// FP8 / INT8: A and B are 1-byte elements (K counted in elements = bytes) with fp32 a_scale[M]
+// (per row) and b_scale[N] (per output channel).  Staging is byte-identical to bf16: a k-tile is
+// 128 bytes of every row (64 bf16, 128 fp8 / int8).
+template <int EPI, int PREC>
 __global__ void __launch_bounds__(kThreads, 1)
 gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __restrict__ C,
                  const float* __restrict__ a_scale, const float* __restrict__ b_scale,
                  int M, int N, int K, int tiles_m, int tiles_n, int k_tiles_per_split) {
+  constexpr bool FP8 = PREC == kFp8;
+  constexpr bool BYTES = PREC != kBf16;   // 1-byte operands
   const char* A = reinterpret_cast<const char*>(Av);
   const char* B = reinterpret_cast<const char*>(Bv);
-  const size_t Kb = (size_t)K * (FP8 ? 1 : 2);   // row stride in bytes
+  const size_t Kb = (size_t)K * (BYTES ? 1 : 2);   // row stride in bytes
   __shared__ __attribute__((aligned(1024))) char smem[kLds];
 
   // ---- XCD-aware, bijective block remap (consecutive logical ids share an XCD / its L2) ----
@@ -181,6 +197,15 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
         for (int j = 0; j < 2; ++j)
           acc[mq * 4 + i][nq * 2 + j] = mfma_fp8(bf[j][0], bf[j][1], af[i][0], af[i][1],
                                                  acc[mq * 4 + i][nq * 2 + j]);
+    } else if (PREC == kInt8) {
+      // two K=64 int8 MFMAs per k-tile (16-B chunks g and g+4), like the two bf16 k-steps
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[mq * 4 + i][nq * 2 + j] = mfma_i8(bf[j][kk], af[i][kk], acc[mq * 4 + i][nq * 2 + j]);
     } else {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
@@ -252,14 +277,20 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
   // consecutive output columns of one row -> 8-B (bf16) / 16-B (fp32) vector stores.
   const int crow = m0 + wr * 128 + fr;
   const int cq = 4 * (lane >> 4);
-  if (FP8) {  // dequantise: per-row activation scale x per-output-channel weight scale
+  if (BYTES) {  // dequantise: per-row activation scale x per-output-channel weight scale
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float sa = a_scale[min(crow + i * 16, M - 1)];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const f32x4 sb = *reinterpret_cast<const f32x4*>(b_scale + n0 + wc * 64 + j * 16 + cq);
-        acc[i][j] = acc[i][j] * sb * sa;
+        f32x4 v = acc[i][j];
+        if (PREC == kInt8) {
+          typedef int i32x4_t __attribute__((ext_vector_type(4)));
+          const i32x4_t iv = __builtin_bit_cast(i32x4_t, v);
+          v = f32x4{(float)iv[0], (float)iv[1], (float)iv[2], (float)iv[3]};
+        }
+        acc[i][j] = v * sb * sa;
       }
     }
   }
@@ -332,21 +363,22 @@ __global__ void __launch_bounds__(256) tile_splitk_reduce_kernel(bf16* __restric
   }
 }
 
-template <bool FP8>
+template <int PREC>
 int launch_tile(void* C, const void* A, const void* B, const float* sa, const float* sb,
                 float* workspace, int M, int N, int K, int splits, int epilogue,
                 hipStream_t stream) {
-  const int kt = (int)((size_t)K * (FP8 ? 1 : 2) / 128);
-  if (M <= 0 || N % kTN != 0 || (size_t)K * (FP8 ? 1 : 2) % 128 != 0 || splits < 1) return -1;
+  constexpr int esz = PREC == kBf16 ? 2 : 1;
+  const int kt = (int)((size_t)K * esz / 128);
+  if (M <= 0 || N % kTN != 0 || (size_t)K * esz % 128 != 0 || splits < 1) return -1;
   if (splits > kt) return -2;
   const int kps = (kt + splits - 1) / splits;
   if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
   if (splits > 1 && (workspace == nullptr || epilogue != kStoreBf16)) return -3;
-  if (FP8 && (sa == nullptr || sb == nullptr)) return -5;
+  if (PREC != kBf16 && (sa == nullptr || sb == nullptr)) return -5;
   const int tiles_m = (M + kTM - 1) / kTM, tiles_n = N / kTN;
   const int grid = tiles_m * tiles_n * splits;
   if (splits > 1) {
-    gemm_tile_kernel<kStoreF32, FP8><<<grid, kThreads, 0, stream>>>(A, B, workspace, sa, sb, M, N,
+    gemm_tile_kernel<kStoreF32, PREC><<<grid, kThreads, 0, stream>>>(A, B, workspace, sa, sb, M, N,
                                                                     K, tiles_m, tiles_n, kps);
     const size_t MN = (size_t)M * N;
     size_t blocks = (MN / 8 + 255) / 256;
@@ -354,10 +386,10 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
     tile_splitk_reduce_kernel<<<(int)blocks, 256, 0, stream>>>(reinterpret_cast<bf16*>(C),
                                                                workspace, splits, MN);
   } else if (epilogue == kSwiGLU) {
-    gemm_tile_kernel<kSwiGLU, FP8><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K, tiles_m,
+    gemm_tile_kernel<kSwiGLU, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K, tiles_m,
                                                                   tiles_n, kps);
   } else if (epilogue == kStoreBf16) {
-    gemm_tile_kernel<kStoreBf16, FP8><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
+    gemm_tile_kernel<kStoreBf16, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
                                                                      tiles_m, tiles_n, kps);
   } else {
     return -4;
@@ -369,11 +401,19 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
 
 int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale,
                      const float* b_scale, float* workspace, int M, int N, int K, int splits,
-                     int epilogue, bool fp8, hipStream_t stream) {
-  return fp8 ? launch_tile<true>(C, A, B, a_scale, b_scale, workspace, M, N, K, splits, epilogue,
-                                 stream)
-             : launch_tile<false>(C, A, B, nullptr, nullptr, workspace, M, N, K, splits, epilogue,
-                                  stream);
+                     int epilogue, int precision, hipStream_t stream) {
+  switch (precision) {
+    case kBf16:
+      return launch_tile<kBf16>(C, A, B, nullptr, nullptr, workspace, M, N, K, splits, epilogue,
+                                stream);
+    case kFp8:
+      return launch_tile<kFp8>(C, A, B, a_scale, b_scale, workspace, M, N, K, splits, epilogue,
+                               stream);
+    case kInt8:
+      return launch_tile<kInt8>(C, A, B, a_scale, b_scale, workspace, M, N, K, splits, epilogue,
+                                stream);
+  }
+  return -6;
 }
 
 }  // namespace dli

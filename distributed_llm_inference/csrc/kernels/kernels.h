@@ -73,12 +73,14 @@ int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_
 int launch_sample(const SampleParams& p, int B, hipStream_t stream);
 int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale,
                      const float* b_scale, float* workspace, int M, int N, int K, int splits,
-                     int epilogue, bool fp8, hipStream_t stream);
+                     int epilogue, int precision, hipStream_t stream);
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
                        int K, hipStream_t stream);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
                          bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,
                          hipStream_t stream);
+int launch_quant_rowwise_int8(int8_t* q, float* scale, const bf16* x, const uint8_t* outlier,
+                              int rows, int K, hipStream_t stream);
 int launch_silu_mul_quant(uint8_t* q, float* scale, const bf16* x, int rows, int inter,
                           hipStream_t stream);
 

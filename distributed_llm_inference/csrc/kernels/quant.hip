@@ -127,6 +127,79 @@ __global__ void __launch_bounds__(512) silu_mul_quant_kernel(uint8_t* __restrict
   store_fp8_row<VPT>(v, q + (size_t)row * I, scale + row, nvec, scratch);
 }
 
+// LLM.int8 activation quantisation (reference utils/model.py:93-113 -> bitsandbytes Linear8bitLt):
+// x [rows, K] bf16 -> q [rows, K] int8, scale [rows] f32 with x ~= q * scale on the regular
+// columns.  Columns flagged in `outlier` (nullable) are zeroed here: they are multiplied in bf16
+// by the caller (the mixed-precision decomposition of LLM.int8).
+template <int VPT>
+__global__ void __launch_bounds__(256) quant_rowwise_int8_kernel(
+    int8_t* __restrict__ q, float* __restrict__ scale, const bf16* __restrict__ x,
+    const uint8_t* __restrict__ outlier, int K) {
+  __shared__ float scratch[8];
+  const int row = blockIdx.x;
+  const int nvec = K >> 3;
+  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * K);
+  const uint2* fr = reinterpret_cast<const uint2*>(outlier);
+  float v[VPT][8];
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * blockDim.x;
+    if (idx < nvec) {
+      const bf16x8 a = xr[idx];
+      uint2 f = {0u, 0u};
+      if (outlier) f = fr[idx];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned byte = ((j < 4 ? f.x : f.y) >> (8 * (j & 3))) & 0xffu;
+        v[i][j] = byte ? 0.f : (float)a[j];
+        amax = fmaxf(amax, fabsf(v[i][j]));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  amax = block_reduce_max(amax, scratch);
+  const float s = amax > 0.f ? amax / 127.f : 1.f;
+  const float inv = 1.f / s;
+  if (threadIdx.x == 0) scale[row] = s;
+  uint2* qr = reinterpret_cast<uint2*>(q + (size_t)row * K);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = threadIdx.x + i * blockDim.x;
+    if (idx < nvec) {
+      unsigned w[2] = {0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int qi = (int)rintf(fminf(fmaxf(v[i][j] * inv, -127.f), 127.f));
+        w[j >> 2] |= ((unsigned)qi & 0xffu) << (8 * (j & 3));
+      }
+      qr[idx] = uint2{w[0], w[1]};
+    }
+  }
+}
+
+int launch_quant_rowwise_int8(int8_t* q, float* scale, const bf16* x, const uint8_t* outlier,
+                              int rows, int K, hipStream_t stream) {
+  if (K % 8 != 0) return -1;
+  if (rows == 0) return 0;
+  const int nvec = K / 8;
+  int threads = ((nvec + 63) / 64) * 64;
+  if (threads > 256) threads = 256;
+  const int vpt = (nvec + threads - 1) / threads;
+#define DLI_QI8(V) \
+  quant_rowwise_int8_kernel<V><<<rows, threads, 0, stream>>>(q, scale, x, outlier, K)
+  if (vpt <= 1) DLI_QI8(1);
+  else if (vpt <= 2) DLI_QI8(2);
+  else if (vpt <= 4) DLI_QI8(4);
+  else if (vpt <= 8) DLI_QI8(8);
+  else if (vpt <= 16) DLI_QI8(16);
+  else return -1;
+#undef DLI_QI8
+  return 0;
+}
+
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
                          bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,
                          hipStream_t stream) {

@@ -1,9 +1,10 @@
 """Building blocks shared by the model families (Llama, GPT-2).
 
-* :class:`Linear` — bf16 weight GEMM through hipBLASLt (``F.linear``), or fp8-e4m3 weights with
-  per-output-channel scales and per-token dynamic activation scales through hipBLASLt's row-wise
-  scaled GEMM (``torch._scaled_mm``).  This is the MI355X replacement of the reference's
-  bitsandbytes ``Linear8bitLt`` (utils/model.py:93-113).
+* :class:`Linear` — bf16 weights (hand-written tile GEMM / GEMV for decode, hipBLASLt otherwise),
+  fp8-e4m3 weights with per-output-channel scales and per-token dynamic activation scales (the
+  MI355X-native 8-bit default), or LLM.int8 weights with the reference's outlier ``threshold``
+  (int8 MFMA + bf16 outlier columns) — the replacements of the reference's bitsandbytes
+  ``Linear8bitLt`` (utils/model.py:93-113).
 * :class:`AttnMetadata` — per-batch device metadata consumed by the attention / cache kernels
   (positions, slot mapping, block tables, sequence lengths, varlen offsets, window policy).  It
   replaces the reference's dense additive causal/padding mask (model.py:78-143): causality,
@@ -34,10 +35,26 @@ class Linear(nn.Module):
                                   requires_grad=False) if bias else None)
         self.register_buffer("weight_fp8", None, persistent=False)
         self.register_buffer("weight_scale", None, persistent=False)
+        self.register_buffer("weight_int8", None, persistent=False)
+        self.int8_threshold = 0.0
 
     @property
     def is_fp8(self) -> bool:
         return self.weight_fp8 is not None
+
+    @property
+    def is_int8(self) -> bool:
+        return self.weight_int8 is not None
+
+    def quantize_int8(self, threshold: float = 6.0, keep_bf16: bool = False) -> None:
+        """LLM.int8 weights (reference utils/model.py:93-113, bitsandbytes ``Linear8bitLt(threshold)``):
+        per-channel absmax int8 + bf16 outlier-column decomposition at run time."""
+        q, s = ops.quantize_weight_int8(self.weight.data)
+        self.weight_int8, self.weight_scale = q, s
+        self.int8_threshold = float(threshold)
+        if not keep_bf16:
+            self.weight = nn.Parameter(torch.empty(0, dtype=self.weight.dtype,
+                                                   device=self.weight.device), requires_grad=False)
 
     def quantize_fp8(self, keep_bf16: bool = False) -> None:
         """Quantise W to fp8 e4m3 (per output channel).  Frees the bf16 copy unless asked not to."""
@@ -50,7 +67,8 @@ class Linear(nn.Module):
     def tile_splits(self, x: torch.Tensor) -> int:
         """Split-K factor if ``gemm_tile`` takes this product on the GPU, else 0."""
         if (self.bias is not None or not x.is_cuda or x.dim() != 2 or x.dtype != torch.bfloat16
-                or not x.is_contiguous() or self.weight_fp8 is not None):
+                or not x.is_contiguous() or self.weight_fp8 is not None
+                or self.weight_int8 is not None):
             return 0
         return ops.tile_gemm_splits(x.shape[0], self.out_features, self.in_features)
 
@@ -58,6 +76,11 @@ class Linear(nn.Module):
                 x_q: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
         """``x_q`` = (fp8 rows, scales) already quantised by a fused producer kernel; then ``x`` may
         be None (fp8 weights only)."""
+        if self.weight_int8 is not None:
+            y = ops.llm_int8_linear(x.reshape(-1, self.in_features), self.weight_int8,
+                                    self.weight_scale, self.int8_threshold)
+            y = y.reshape(*x.shape[:-1], self.out_features)
+            return y + self.bias if self.bias is not None else y
         if self.weight_fp8 is None:
             if (x.is_cuda and x.dim() == 2 and 1 <= x.shape[0] <= ops.SKINNY_DISPATCH_M
                     and x.dtype == torch.bfloat16 and x.is_contiguous()
@@ -87,7 +110,7 @@ class Linear(nn.Module):
 
     def extra_repr(self) -> str:
         return (f"in={self.in_features}, out={self.out_features}, bias={self.bias is not None}, "
-                f"fp8={self.is_fp8}")
+                f"fp8={self.is_fp8}, int8={self.is_int8}")
 
 
 @dataclass

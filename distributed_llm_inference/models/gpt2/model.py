@@ -133,6 +133,12 @@ class GPT2Block(nn.Module):
                     seeded_normal_(p.data, param_seed(seed, layer.layer_idx, name), std)
         return self
 
+    def quantize_int8(self, threshold: float = 6.0) -> "GPT2Block":
+        for layer in self.layers:
+            for lin in (layer.c_attn, layer.attn_proj, layer.c_fc, layer.mlp_proj):
+                lin.quantize_int8(threshold)
+        return self
+
     def quantize_fp8(self) -> "GPT2Block":
         for layer in self.layers:
             for lin in (layer.c_attn, layer.attn_proj, layer.c_fc, layer.mlp_proj):

@@ -72,6 +72,15 @@ class LlamaBlock(nn.Module):
             layer.mlp.set_fused_swiglu(on)
         return self
 
+    def quantize_int8(self, threshold: float = 6.0) -> "LlamaBlock":
+        """LLM.int8 weights for every projection (reference convert_to_optimized_block)."""
+        self.set_fused_swiglu(False)
+        for layer in self.layers:
+            for lin in (layer.self_attn.qkv_proj, layer.self_attn.o_proj, layer.mlp.gate_up_proj,
+                        layer.mlp.down_proj):
+                lin.quantize_int8(threshold)
+        return self
+
     def quantize_fp8(self) -> "LlamaBlock":
         self.set_fused_swiglu(False)
         for layer in self.layers:

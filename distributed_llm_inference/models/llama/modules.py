@@ -95,7 +95,7 @@ class LlamaMLP(nn.Module):
         w = self.gate_up_proj
         if on == self.fused_swiglu:
             return
-        if w.is_fp8 or w.bias is not None or w.out_features % 256:
+        if w.is_fp8 or w.is_int8 or w.bias is not None or w.out_features % 256:
             return
         with torch.no_grad():
             perm = ops.swiglu_interleave if on else ops.swiglu_deinterleave

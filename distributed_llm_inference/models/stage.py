@@ -20,6 +20,18 @@ from .llama.cache import KVPool
 from .llama.model import LlamaBlock
 
 
+def apply_quantization(block, mode, threshold: float = 6.0):
+    """Quantise a Llama / GPT-2 block in place: ``mode`` False / None / "none" (bf16), True /
+    "fp8" (e4m3 weights, per-channel scales) or "int8" (LLM.int8, outlier ``threshold``)."""
+    if mode in (False, None, "none", "bf16"):
+        return block
+    if mode is True or mode == "fp8":
+        return block.quantize_fp8()
+    if mode == "int8":
+        return block.quantize_int8(threshold)
+    raise ValueError(f"unknown quantisation mode {mode!r} (expected fp8 / int8)")
+
+
 def make_block(spec: ModelSpec, layer_ids, device=None, dtype=torch.bfloat16):
     if spec.arch == "llama":
         return LlamaBlock(spec, layer_ids, device=device, dtype=dtype)
@@ -63,6 +75,16 @@ class CausalLMStage(nn.Module):
 
     def quantize_fp8(self) -> "CausalLMStage":
         self.block.quantize_fp8()
+        return self
+
+    def quantize_int8(self, threshold: float = 6.0) -> "CausalLMStage":
+        self.block.quantize_int8(threshold)
+        return self
+
+    def quantize(self, mode, threshold: float = 6.0) -> "CausalLMStage":
+        """``mode``: False / None / "none"; True / "fp8" (e4m3, the MI355X default); "int8"
+        (LLM.int8 with outlier ``threshold``)."""
+        apply_quantization(self.block, mode, threshold)
         return self
 
     def make_pool(self, num_blocks: int, block_size: int = 64, window_length: int = 0,

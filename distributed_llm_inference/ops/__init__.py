@@ -337,7 +337,7 @@ TILE_GEMM_MAX_M = 2048   # above (prefill chunks): hipBLASLt's large-M solutions
 _CUS = 256
 
 
-def tile_gemm_splits(M: int, N: int, K: int) -> int:
+def tile_gemm_splits(M: int, N: int, K: int, elem_bytes: int = 2) -> int:
     """Split-K factor for ``gemm_tile`` on an [M, K] x [N, K]^T product, or 0 = not eligible.
 
     Picks the split that best fills the 256 CUs with whole waves of 256x256 tiles (ties -> fewer
@@ -345,20 +345,87 @@ def tile_gemm_splits(M: int, N: int, K: int) -> int:
     best per shape, profiles/gemm_tile_bench.json).  ``DLI_TILE_GEMM=0`` disables the kernel."""
     if os.environ.get("DLI_TILE_GEMM", "1") == "0":
         return 0
-    if not (TILE_GEMM_MIN_M <= M <= TILE_GEMM_MAX_M) or N % 256 or K % 64:
+    if not (TILE_GEMM_MIN_M <= M <= TILE_GEMM_MAX_M) or N % 256 or (K * elem_bytes) % 128:
         return 0
+    k_tiles = K * elem_bytes // 128
     tiles = ((M + 255) // 256) * (N // 256)
     if tiles > 2 * _CUS:
         return 0  # e.g. the 128256-wide LM head: hipBLASLt's wide-N solutions are faster (690 vs 824 us)
     best, best_util = 1, 0.0
     for s in range(1, 9):
-        if s > K // 64 or (s > 1 and tiles * s > 2 * _CUS):
+        if s > k_tiles or (s > 1 and tiles * s > 2 * _CUS):
             break
         work = tiles * s
         util = work / (_CUS * ((work + _CUS - 1) // _CUS))
         if util > best_util + 1e-9:
             best, best_util = s, util
     return best
+
+
+# ----------------------------------------------------------------------------- LLM.int8
+def quantize_weight_int8(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Row-wise (per output channel) absmax int8 weights, as bitsandbytes' ``Linear8bitLt``
+    stores them (reference utils/model.py:93-113): returns (w_int8 [N, K], scale [N])."""
+    wf = w.float()
+    s = wf.abs().amax(-1).clamp_min(1e-12) / 127.0
+    q = torch.round(wf / s[:, None]).clamp(-127, 127).to(torch.int8)
+    return q, s.contiguous()
+
+
+def quant_rowwise_int8(x: torch.Tensor, outlier: Optional[torch.Tensor] = None
+                       ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-row absmax int8 quantisation of ``x [rows, K]``; columns with ``outlier[c] != 0`` are
+    zeroed (LLM.int8 computes them in bf16).  Returns (q int8, scale [rows])."""
+    rows, K = x.shape
+    if not _gpu(x):
+        xf = x.float()
+        if outlier is not None:
+            xf = xf * (outlier == 0).to(xf.dtype)
+        s = xf.abs().amax(-1).clamp_min(0)
+        s = torch.where(s > 0, s / 127.0, torch.ones_like(s))
+        return torch.round(xf / s[:, None]).clamp(-127, 127).to(torch.int8), s
+    q = torch.empty(rows, K, dtype=torch.int8, device=x.device)
+    s = torch.empty(rows, dtype=torch.float32, device=x.device)
+    native().quant_rowwise_int8(q, s, x.contiguous(), outlier)
+    return q, s
+
+
+LLM_INT8_MAX_OUTLIERS = 64   # static outlier-column capacity (graph-capturable shapes)
+
+
+def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, threshold: float = 6.0,
+                    max_outliers: int = LLM_INT8_MAX_OUTLIERS) -> torch.Tensor:
+    """LLM.int8 matmul ``x [M, K] @ W^T`` with ``W ~= wq * ws[:, None]`` (int8, per-channel).
+
+    Mixed-precision decomposition as in bitsandbytes ``Linear8bitLt(threshold=...)``: feature
+    columns whose magnitude exceeds ``threshold`` anywhere in the batch are multiplied in bf16
+    (with the dequantised weight columns); every other column goes through per-row int8
+    quantisation and the int8 MFMA tile GEMM (``gemm_tile.hip``, v_mfma_i32_16x16x64_i8).  To keep
+    shapes static (hipGraph decode) the outlier set is the ``max_outliers`` largest columns that
+    pass the threshold; ``threshold <= 0`` disables the decomposition."""
+    M, K = x.shape
+    N = wq.shape[0]
+    y_out = None
+    flags = None
+    if threshold > 0 and M > 0:
+        colmax = x.abs().amax(0).float()
+        vals, idx = colmax.topk(min(max_outliers, K))
+        sel = vals > threshold
+        flags = torch.zeros(K, dtype=torch.uint8, device=x.device).scatter_(0, idx, sel.to(torch.uint8))
+        xo = x.index_select(1, idx) * sel.to(x.dtype)
+        wo = (wq.index_select(1, idx).float() * ws[:, None]).to(x.dtype)
+        y_out = xo @ wo.t()
+    xq, xs = quant_rowwise_int8(x, flags)
+    if _gpu(x) and N % 256 == 0 and K % 128 == 0 and M > 0:
+        sp = tile_gemm_splits(max(M, TILE_GEMM_MIN_M), N, K, elem_bytes=1) or 1
+        y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+        ws_ = torch.empty(sp * M * N, dtype=torch.float32, device=x.device) if sp > 1 else None
+        native().gemm_tile(y, xq, wq, int(sp), 0, ws_, xs, ws)
+    else:  # CPU / untileable shapes: dequantised reference
+        y = ((xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()).to(torch.bfloat16)
+    if y_out is not None:
+        y = (y.float() + y_out.float()).to(torch.bfloat16)
+    return y
 
 
 def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
@@ -389,7 +456,7 @@ def tile_gemm_splits_fp8(M: int, N: int, K: int) -> int:
     K = 28672); at K = 8192 the split-K pass costs more than it saves (O 52 vs 41 us)."""
     if K < 16384:
         return 0
-    return tile_gemm_splits(M, N, K)
+    return tile_gemm_splits(M, N, K, elem_bytes=1)
 
 
 def swiglu_interleaved(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

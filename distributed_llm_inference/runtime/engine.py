@@ -39,7 +39,8 @@ class EngineConfig:
     random_init: bool = True
     seed: int = 0
     dtype: str = "bf16"
-    quantize: bool = False          # fp8 weights
+    quantize: object = False        # False | True / "fp8" (e4m3 weights) | "int8" (LLM.int8)
+    int8_threshold: float = 6.0     # LLM.int8 outlier threshold (quantize="int8")
     pp: int = 1
     cache: CacheConfig = field(default_factory=CacheConfig)
     serve: ServeConfig = field(default_factory=ServeConfig)
@@ -57,7 +58,8 @@ def build_executor(spec: ModelSpec, start: int, end: int, device: torch.device, 
                    kv_share: float = 1.0) -> StageExecutor:
     stage = build_stage(cfg.checkpoint or spec, start, end, device=device,
                         random_init=cfg.random_init and cfg.checkpoint is None, seed=cfg.seed,
-                        quantize=cfg.quantize, checkpoint=cfg.checkpoint)
+                        quantize=cfg.quantize, checkpoint=cfg.checkpoint,
+                        int8_threshold=cfg.int8_threshold)
     cc, sc = cfg.cache, cfg.serve
     nlayers = end - start
     if device.type == "cuda" and hasattr(stage.block, "set_fused_swiglu"):

@@ -7,8 +7,9 @@ Reference: /root/reference/distributed_llm_inference/utils/model.py —
     directories all work; nothing is fetched from the network (the benchmark boxes have none):
     hub repos are resolved from the local HF cache only;
   * B16 — weights load in bf16 (MI355X native), not fp16;
-  * B10/B11 — quantisation happens only when asked (``use_quantized`` is wired through) and is
-    fp8 e4m3 with per-channel scales (CDNA4 fp8 MFMA via hipBLASLt), not bitsandbytes int8;
+  * B10/B11 — quantisation happens only when asked (``use_quantized`` is wired through): fp8 e4m3
+    with per-channel scales (CDNA4 fp8 MFMA) by default, or ``"int8"`` = LLM.int8 (int8 MFMA tile
+    GEMM + bf16 outlier columns above ``threshold``);
   * a random-init path builds any config without a checkpoint (``random_init=True``).
 Weights are read with ``safetensors`` (memory-mapped, no pickle execution).
 """
@@ -23,7 +24,7 @@ import torch
 
 from ..config import ModelSpec, resolve_model
 from ..models.llama.model import LlamaBlock
-from ..models.stage import CausalLMStage, make_block
+from ..models.stage import CausalLMStage, apply_quantization, make_block
 
 log = logging.getLogger(__name__)
 
@@ -119,17 +120,17 @@ def load_block(model_name: str, layer_ids: Sequence[int], use_quantized: bool = 
             log.info("loading weights for layer %d", layer.layer_idx)
             sd = get_block_state_dict(model_name, layer.layer_idx, cache_dir, token, prefix_fmt)
             layer.load_hf_state_dict(sd)
-    if use_quantized:
-        block.quantize_fp8()
+    apply_quantization(block, use_quantized)
     return block
 
 
-def convert_to_optimized_block(block, quantize: bool = False, threshold: float = 5.0,
-                               device=None):
-    """Move a block to the GPU and (only if ``quantize``) convert its linears to fp8.
+def convert_to_optimized_block(block, quantize=False, threshold: float = 5.0, device=None):
+    """Move a block to the GPU and (only if ``quantize``) convert its linears to 8-bit.
 
-    ``threshold`` is accepted for API compatibility with the reference's LLM.int8 outlier
-    threshold; fp8 e4m3 has enough dynamic range that no outlier decomposition is needed.
+    ``quantize=True`` / ``"fp8"``: fp8 e4m3 weights (the MI355X-native default; enough dynamic
+    range that no outlier decomposition is needed).  ``quantize="int8"``: the reference's
+    LLM.int8 semantics — int8 weights, activation columns above ``threshold`` (reference default
+    5.0) computed in bf16 (reference utils/model.py:93-123).
     """
     if device is None:
         if not torch.cuda.is_available():
@@ -138,8 +139,7 @@ def convert_to_optimized_block(block, quantize: bool = False, threshold: float =
             return block
         device = torch.device("cuda", torch.cuda.current_device())
     block = block.to(device)
-    if quantize:
-        block.quantize_fp8()
+    apply_quantization(block, quantize, threshold)
     return block
 
 
@@ -211,8 +211,8 @@ def stage_from_hf_model(hf_model, start: int, end: int, device=None,
 
 
 def build_stage(model: str, start: int, end: int, device=None, dtype=torch.bfloat16,
-                random_init: bool = True, seed: int = 0, quantize: bool = False,
-                checkpoint: Optional[str] = None) -> CausalLMStage:
+                random_init: bool = True, seed: int = 0, quantize=False,
+                checkpoint: Optional[str] = None, int8_threshold: float = 6.0) -> CausalLMStage:
     """Construct a stage for ``[start, end)``; random-init or load from ``checkpoint``."""
     spec = _load_config(checkpoint or model)
     stage = CausalLMStage(spec, start, end, device=device, dtype=dtype)
@@ -220,8 +220,7 @@ def build_stage(model: str, start: int, end: int, device=None, dtype=torch.bfloa
         stage.init_random(seed)
     else:
         load_stage_weights(stage, checkpoint or model)
-    if quantize:
-        stage.quantize_fp8()
+    stage.quantize(quantize, int8_threshold)
     return stage
 
 

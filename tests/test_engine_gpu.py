@@ -193,3 +193,16 @@ def test_fp8_kv_cache_engine_close_to_bf16(gpu):
     a, b = run(torch.bfloat16), run(torch.float8_e4m3fn)
     for x, y in zip(a, b):
         assert ((x - y).norm() / x.norm()).item() < 0.08
+
+
+def test_int8_weights_close_to_bf16(gpu):
+    """LLM.int8 mode (reference convert_to_optimized_block(quantize=True, threshold)): int8 MFMA
+    tile GEMM + bf16 outlier columns, end to end through the stage."""
+    stage = CausalLMStage(SPEC, 0, 4, device=gpu).init_random(9)
+    prompts = [list(range(1, 50))]
+    a = _stage_logits(stage, prompts, 0)[0]
+    stage.quantize("int8", threshold=5.0)
+    assert stage.block.layers[0].self_attn.qkv_proj.is_int8
+    b = _stage_logits(stage, prompts, 0)[0]
+    rel = (a - b).norm() / a.norm()
+    assert rel < 0.1, rel

@@ -136,3 +136,49 @@ def test_gemm_tile_fp8_exact_integers_and_swiglu(gpu):
     wsi = ops.swiglu_interleave(ws.reshape(-1, 1)).reshape(-1)
     y = ops.gemm_tile_fp8(xq, xs, wqi, wsi, swiglu=True).float()
     assert (y - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+
+
+# ------------------------------------------------------------------ LLM.int8 (int8 MFMA tile GEMM)
+def test_gemm_tile_int8_exact_and_random(gpu):
+    xi = torch.zeros(256, 128, device=gpu)
+    xi[torch.arange(128), torch.arange(128)] = 1.0
+    wi = (torch.arange(256 * 128, device=gpu, dtype=torch.float32).reshape(256, 128) % 29) - 14
+    one = torch.ones(256, device=gpu)
+    y = torch.empty(256, 256, device=gpu, dtype=torch.bfloat16)
+    ops.native().gemm_tile(y, xi.to(torch.int8), wi.to(torch.int8), 1, 0, None, one, one)
+    assert torch.equal(y.float(), xi @ wi.t())
+    for M, N, K, sp in ((512, 1024, 4096, 4), (77, 512, 384, 1), (300, 768, 2048, 3)):
+        x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+        xq, xs = ops.quant_rowwise_int8(x)
+        wq, ws = ops.quantize_weight_int8(w)
+        ref = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()
+        out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        wsp = torch.empty(sp * M * N, device=gpu) if sp > 1 else None
+        ops.native().gemm_tile(out, xq, wq, sp, 0, wsp, xs, ws)
+        assert (out.float() - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
+
+
+def test_quant_rowwise_int8_kernel_matches_reference(gpu):
+    x = torch.randn(37, 1024, device=gpu).to(torch.bfloat16)
+    flags = torch.zeros(1024, dtype=torch.uint8, device=gpu)
+    flags[[3, 500, 1023]] = 1
+    q, s = ops.quant_rowwise_int8(x, flags)
+    qr, sr = ops.quant_rowwise_int8(x.cpu(), flags.cpu())
+    assert torch.allclose(s.cpu(), sr, rtol=1e-6)
+    assert (q.cpu().int() - qr.int()).abs().max().item() <= 1   # rounding of exact halves
+
+
+def test_llm_int8_linear_gpu_matches_cpu_and_bf16(gpu):
+    torch.manual_seed(0)
+    M, K, N = 64, 1024, 512
+    x = torch.randn(M, K)
+    x[:, [11, 600]] *= 50.0
+    xb = x.to(torch.bfloat16)
+    w = (torch.randn(N, K) / K ** 0.5).to(torch.bfloat16)
+    wq, ws = ops.quantize_weight_int8(w)
+    y_cpu = ops.llm_int8_linear(xb, wq, ws, 6.0).float()
+    y_gpu = ops.llm_int8_linear(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0).float().cpu()
+    ref = xb.float() @ w.float().t()
+    assert ((y_gpu - y_cpu).norm() / y_cpu.norm()).item() < 5e-3
+    assert ((y_gpu - ref).norm() / ref.norm()).item() < 0.02

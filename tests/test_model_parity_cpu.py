@@ -154,3 +154,49 @@ def test_gpt2_matches_hf():
         for s in range(3):
             a, r = ours[s][b], ref_logits[len(p) - 1 + s]
             assert (a - r).abs().max() < 0.05 * max(1.0, r.abs().max().item())
+
+
+# ------------------------------------------------------------------ LLM.int8 (reference Linear8bitLt)
+def test_llm_int8_outlier_decomposition_cpu():
+    """Activation columns above the threshold are multiplied in bf16: with a few large-magnitude
+    feature columns (the LLM.int8 outlier pattern) the decomposed product stays accurate, while
+    plain row-wise int8 of the same input loses the small features."""
+    import torch
+    from distributed_llm_inference import ops
+    torch.manual_seed(0)
+    M, K, N = 16, 512, 256
+    x = torch.randn(M, K)
+    x[:, [7, 100, 301]] *= 60.0                      # systematic outlier features
+    w = torch.randn(N, K) / K ** 0.5
+    xb = x.to(torch.bfloat16)
+    ref = xb.float() @ w.to(torch.bfloat16).float().t()
+    wq, ws = ops.quantize_weight_int8(w.to(torch.bfloat16))
+    y_dec = ops.llm_int8_linear(xb, wq, ws, threshold=6.0).float()
+    y_all = ops.llm_int8_linear(xb, wq, ws, threshold=0.0).float()
+    e_dec = ((y_dec - ref).norm() / ref.norm()).item()
+    e_all = ((y_all - ref).norm() / ref.norm()).item()
+    assert e_dec < 0.02, e_dec
+    assert e_all > 2 * e_dec, (e_all, e_dec)
+    # the quantiser zeroes flagged columns and scales the rest by their own row absmax
+    flags = torch.zeros(K, dtype=torch.uint8)
+    flags[[7, 100, 301]] = 1
+    q, s = ops.quant_rowwise_int8(xb, flags)
+    assert int(q[:, [7, 100, 301]].abs().sum()) == 0
+    assert torch.allclose(s, xb.float().masked_fill(flags.bool(), 0).abs().amax(-1) / 127)
+
+
+def test_int8_stage_close_to_bf16_cpu():
+    import torch
+    from distributed_llm_inference.config import PRESETS
+    from distributed_llm_inference.models.stage import CausalLMStage
+    from distributed_llm_inference.utils import convert_to_optimized_block
+    spec = PRESETS["llama-3-8b"].replace(hidden_size=256, intermediate_size=512, num_layers=2,
+                                         num_heads=4, num_kv_heads=2, head_dim=64, vocab_size=1000)
+    st = CausalLMStage(spec, 0, 2).init_random(5)
+    torch.manual_seed(1)
+    h = torch.randn(1, 29, 256).to(torch.bfloat16)
+    a = st.block("g", h.clone())[0].float()
+    convert_to_optimized_block(st.block, quantize="int8", threshold=5.0, device=torch.device("cpu"))
+    assert st.block.layers[0].mlp.gate_up_proj.is_int8
+    b = st.block("g2", h.clone())[0].float()
+    assert ((a - b).norm() / a.norm()).item() < 0.05
