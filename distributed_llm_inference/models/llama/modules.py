@@ -30,6 +30,24 @@ from ...config import ModelSpec
 from ..common import AttnMetadata, Linear
 
 
+def rotate_half(x: torch.Tensor) -> torch.Tensor:
+    """``cat(-x2, x1)`` over the last dim (HF / reference ``rotate_half``)."""
+    x1, x2 = x.chunk(2, dim=-1)
+    return torch.cat((-x2, x1), dim=-1)
+
+
+def apply_rotary_pos_emb(q: torch.Tensor, k: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
+                         unsqueeze_dim: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Reference ``apply_rotary_pos_emb`` (modules.py:17-20) with the intended broadcasting (B2):
+    ``cos``/``sin`` [B, T, D] are unsqueezed over the head axis of q [B, H, T, D] / k [B, KVH, T, D],
+    and the rotation is computed in fp32.  The runtime path fuses RoPE into the KV-cache write
+    kernel (csrc/kernels/rope_cache.hip); this helper serves library users and tests."""
+    c = cos.unsqueeze(unsqueeze_dim).float()
+    s = sin.unsqueeze(unsqueeze_dim).float()
+    qf, kf = q.float(), k.float()
+    return ((qf * c + rotate_half(qf) * s).to(q.dtype), (kf * c + rotate_half(kf) * s).to(k.dtype))
+
+
 class RMSNorm(nn.Module):
     def __init__(self, hidden: int, eps: float, device=None, dtype=torch.bfloat16):
         super().__init__()

@@ -200,3 +200,18 @@ def test_int8_stage_close_to_bf16_cpu():
     assert st.block.layers[0].mlp.gate_up_proj.is_int8
     b = st.block("g2", h.clone())[0].float()
     assert ((a - b).norm() / a.norm()).item() < 0.05
+
+
+def test_apply_rotary_pos_emb_matches_hf_with_batch():
+    """Reference helper name, B2 fixed: batch > 1 broadcasts over heads and equals HF's."""
+    import torch
+    from transformers.models.llama.modeling_llama import apply_rotary_pos_emb as hf_apply
+    from distributed_llm_inference.models.llama import apply_rotary_pos_emb
+    torch.manual_seed(0)
+    B, H, KVH, T, D = 3, 4, 2, 5, 16
+    q, k = torch.randn(B, H, T, D), torch.randn(B, KVH, T, D)
+    ang = torch.randn(B, T, D // 2)
+    cos, sin = torch.cat([ang.cos()] * 2, -1), torch.cat([ang.sin()] * 2, -1)
+    a = apply_rotary_pos_emb(q, k, cos, sin)
+    b = hf_apply(q, k, cos, sin)
+    assert torch.allclose(a[0], b[0], atol=1e-6) and torch.allclose(a[1], b[1], atol=1e-6)
