@@ -421,7 +421,7 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
   const int64_t kt = K * a.element_size() / 128;
   TORCH_CHECK(M >= 1 && M <= (1 << 20) && N % 256 == 0 && (K * a.element_size()) % 128 == 0 && K > 0,
               "gemm_tile: needs N % 256 == 0 and 128-byte multiples of K");
-  TORCH_CHECK(splits >= 1 && splits <= kt, "gemm_tile: 1 <= splits <= k-tiles");
+  TORCH_CHECK(splits >= 0 && splits <= kt, "gemm_tile: 0 (stream-K tail) <= splits <= k-tiles");
   const float* sa = nullptr;
   const float* sb = nullptr;
   if (fp8) {
@@ -432,7 +432,14 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
     sb = b_scale->data_ptr<float>();
   }
   float* ws = nullptr;
-  if (splits > 1) {
+  if (splits == 0) {
+    TORCH_CHECK(workspace.has_value(), "gemm_tile: the stream-K tail needs a workspace");
+    CHECK_IN(*workspace); CHECK_F32(*workspace);
+    const c10::hip::HIPGuardMasqueradingAsCUDA g0(a.device());
+    TORCH_CHECK(workspace->numel() >= dli::gemm_tile_sk_workspace_floats(),
+                "gemm_tile: stream-K workspace too small");
+    ws = workspace->data_ptr<float>();
+  } else if (splits > 1) {
     TORCH_CHECK(epilogue == 0, "gemm_tile: split-K only with the plain store epilogue");
     TORCH_CHECK(workspace.has_value(), "gemm_tile: split-K needs a workspace");
     CHECK_IN(*workspace); CHECK_F32(*workspace);
@@ -493,6 +500,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
         py::arg("epilogue") = 0, py::arg("workspace") = py::none(),
         py::arg("a_scale") = py::none(), py::arg("b_scale") = py::none());
+  m.def("gemm_tile_sk_workspace_floats", []() { return dli::gemm_tile_sk_workspace_floats(); },
+        "fp32 workspace elements gemm_tile(splits=0) needs on the current device");
   m.def("skinny_gemm", &skinny_gemm, "y = x . W^T (+ bias) for M <= 4 (weight-streaming GEMV)",
         py::arg("out"), py::arg("x"), py::arg("w"), py::arg("bias") = py::none());
   register_rccl(m);

@@ -55,6 +55,9 @@ constexpr int kLds = 2 * kBuf;         // double buffer: 128 KB
 
 enum Epilogue { kStoreBf16 = 0, kStoreF32 = 1, kSwiGLU = 2 };
 
+// stream-K workspace header: flags [0, kSkMaxWgs), error counter at kSkErrWord, slabs after
+constexpr int kSkMaxWgs = 1020, kSkErrWord = 1023, kSkHeaderFloats = 1024;
+
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void gbl_void_t;
 
@@ -100,6 +103,29 @@ __device__ __forceinline__ f32x4 mfma_i8(const bf16x8& a, const bf16x8& b, const
 
 enum Prec { kBf16 = 0, kFp8 = 1, kInt8 = 2 };
 
+// Stream-K tail (splits == 1, bf16 / SwiGLU epilogues).  With more tiles than CUs the last wave
+// of whole tiles leaves CUs idle (Llama-3-70B gate|up at M = 512: 448 tiles = 1.75 waves on 256
+// CUs).  Workgroups [0, n_dp) compute tiles [0, n_dp) whole (data-parallel part, a multiple of the
+// CU count); workgroups [n_dp, n_dp + sk_wgs) split the k-tiles of the remaining tiles evenly
+// (sk_wgs = CU count, so they are co-resident).  A tile whose k-range spans several workgroups is
+// finished by the one holding its last k-tile: every other holder publishes its fp32 partial
+// (write-through `sc1` slab stores, drained, then one relaxed agent-scope flag store) and the
+// finisher polls each flag, acquires, and adds the slab to its accumulators before the epilogue
+// (cdna_hip_programming.md §6 Guideline 16, R1 form).  Each workgroup runs its publishing piece
+// FIRST and its finishing piece LAST, and never waits before it has published, so every wait is
+// on a co-resident workgroup that is already past its own publish point (no deadlock, whatever
+// the dispatch order).
+struct SkArgs {
+  int n_dp;          // workgroups computing whole tiles; == grid when the tail is off
+  int sk_wgs;        // stream-K workgroups (0 = off)
+  unsigned* flags;   // [sk_wgs] publish flags, zeroed by a memset node before every launch
+  unsigned* err;     // spin-timeout counter (diagnostic; tests zero it once)
+  float* slabs;      // [sk_wgs][256 * 256] fp32 partials in accumulator (register) order
+};
+
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
 // FP8 / INT8: A and B are 1-byte elements (K counted in elements = bytes) with fp32 a_scale[M]
 // (per row) and b_scale[N] (per output channel).  Staging is byte-identical to bf16: a k-tile is
 // 128 bytes of every row (64 bf16, 128 fp8 / int8).
@@ -107,236 +133,336 @@ template <int EPI, int PREC>
 __global__ void __launch_bounds__(kThreads, 1)
 gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __restrict__ C,
                  const float* __restrict__ a_scale, const float* __restrict__ b_scale,
-                 int M, int N, int K, int tiles_m, int tiles_n, int k_tiles_per_split) {
+                 int M, int N, int K, int tiles_m, int tiles_n, int k_tiles_per_split, SkArgs sk) {
   constexpr bool FP8 = PREC == kFp8;
   constexpr bool BYTES = PREC != kBf16;   // 1-byte operands
   const char* A = reinterpret_cast<const char*>(Av);
   const char* B = reinterpret_cast<const char*>(Bv);
   const size_t Kb = (size_t)K * (BYTES ? 1 : 2);   // row stride in bytes
+  const int kt_all = (int)(Kb / 128);              // k-tiles of a whole tile
   __shared__ __attribute__((aligned(1024))) char smem[kLds];
 
+  const int tid0 = threadIdx.x;
+
   // ---- XCD-aware, bijective block remap (consecutive logical ids share an XCD / its L2) ----
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tm = lid % tiles_m;               // the M tiles of one N panel are neighbours:
-  const int tn = (lid / tiles_m) % tiles_n;   // they share the streamed weight panel via L2
-  const int split = lid / (tiles_m * tiles_n);
-  const int m0 = tm * kTM, n0 = tn * kTN;
-  const int kt0 = split * k_tiles_per_split;
-  const int T = min(k_tiles_per_split, (int)(Kb / 128) - kt0);
+  auto remap = [](int b, int n) {
+    const int x = b & 7, q = n >> 3, r = n & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+  };
+  // (bf16 only: in the 1-byte variants the hand-off code pushes the allocator into spilling)
+  constexpr bool kSk = PREC == kBf16 && EPI != kStoreF32;
+  const bool is_sk = kSk && (int)blockIdx.x >= sk.n_dp;
+  const int lid = is_sk ? remap(blockIdx.x - sk.n_dp, sk.sk_wgs) : remap(blockIdx.x, sk.n_dp);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
-
-  // ---- DMA source rows: thread stages LDS units u = j*512 + tid (j = 0, 1) of each half-tile ----
-  // unit u -> local row lr = u >> 3, LDS slot s = u & 7, global chunk s ^ ((lr >> 1) & 7)
-  const char* srcA[2][2];
-  const char* srcB[2][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int u = j * kThreads + tid;
-    const int lr = u >> 3, ch = (u & 7) ^ ((lr >> 1) & 7);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int ga = (lr >> 6) * 128 + h * 64 + (lr & 63);
-      const int gb = (lr >> 5) * 64 + h * 32 + (lr & 31);
-      const int ra = min(m0 + ga, M - 1);       // rows past M are computed, never stored
-      srcA[h][j] = A + (size_t)ra * Kb + (size_t)kt0 * 128 + ch * 16;
-      srcB[h][j] = B + (size_t)(n0 + gb) * Kb + (size_t)kt0 * 128 + ch * 16;
-    }
+  // ---- segments: one (tile, k-range) for data-parallel / split-K blocks; for a stream-K block
+  // the tiles its k-iteration range [lo, hi) touches: the last one first (it may be a partial
+  // that others wait for), the first one last (it may wait for its predecessors' partials) ----
+  long long sk_total = 0, lo = 0, hi = 0;
+  int first_t = 0, nseg = 1;
+  if (is_sk) {
+    sk_total = (long long)(tiles_m * tiles_n - sk.n_dp) * kt_all;
+    lo = sk_total * lid / sk.sk_wgs;
+    hi = sk_total * (lid + 1) / sk.sk_wgs;
+    first_t = (int)(lo / kt_all);
+    nseg = (int)((hi - 1) / kt_all) - first_t + 1;
   }
-  // stage half `which` (0 = A0, 1 = A1, 2 = B0, 3 = B1) of k-tile t into buffer t & 1
-  auto stage = [&](int which, int t) {
-    char* dst = smem + (t & 1) * kBuf + which * kHalf + wave * 1024;
-    const size_t koff = (size_t)t * 128;
+
+  for (int seg = 0; seg < nseg; ++seg) {
+    // re-derive the lane-dependent addressing in every segment instead of keeping it live
+    // across the loop (hoisted, it costs ~20 VGPRs the accumulators need)
+    int tid = tid0;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wave = tid >> 6, wr = wave >> 2, wc = wave & 3, fr = lane & 15;
+    int sch[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) sch[kk] = ((kk * 4 + (lane >> 4)) ^ (fr >> 1)) << 4;
+    const int a_lane = (wr * 64 + fr) * 128;
+    const int b_lane = (wc * 32 + fr) * 128;
+    int tile, kt0, T, split = 0;
+    bool publish = false, finish = false;
+    long long tile_k0 = 0;
+    if (!is_sk) {
+      tile = lid % (tiles_m * tiles_n);
+      split = lid / (tiles_m * tiles_n);
+      kt0 = split * k_tiles_per_split;
+      T = min(k_tiles_per_split, kt_all - kt0);
+    } else {
+      const int t = first_t + (nseg == 1 ? 0 : seg == 0 ? nseg - 1 : seg == nseg - 1 ? 0 : seg);
+      tile_k0 = (long long)t * kt_all;
+      const long long s0 = max(lo, tile_k0), s1 = min(hi, tile_k0 + kt_all);
+      kt0 = (int)(s0 - tile_k0);
+      T = (int)(s1 - s0);
+      publish = s1 < tile_k0 + kt_all;   // stops short of the tile's end: hand the partial on
+      finish = !publish && s0 > tile_k0; // ends the tile but did not start it: add predecessors'
+      tile = sk.n_dp + t;
+    }
+    const int tm = tile % tiles_m;              // the M tiles of one N panel are neighbours:
+    const int tn = tile / tiles_m;              // they share the streamed weight panel via L2
+    const int m0 = tm * kTM, n0 = tn * kTN;
+
+    // ---- DMA source rows: thread stages LDS units u = j*512 + tid (j = 0, 1) of each half-tile ----
+    // unit u -> local row lr = u >> 3, LDS slot s = u & 7, global chunk s ^ ((lr >> 1) & 7)
+    const char* srcA[2][2];
+    const char* srcB[2][2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const char* src = which < 2 ? srcA[which][j] : srcB[which - 2][j];
-      dma16(src + koff, dst + j * 8192);
+      const int u = j * kThreads + tid;
+      const int lr = u >> 3, ch = (u & 7) ^ ((lr >> 1) & 7);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ga = (lr >> 6) * 128 + h * 64 + (lr & 63);
+        const int gb = (lr >> 5) * 64 + h * 32 + (lr & 31);
+        const int ra = min(m0 + ga, M - 1);       // rows past M are computed, never stored
+        srcA[h][j] = A + (size_t)ra * Kb + (size_t)kt0 * 128 + ch * 16;
+        srcB[h][j] = B + (size_t)(n0 + gb) * Kb + (size_t)kt0 * 128 + ch * 16;
+      }
     }
-  };
+    // stage half `which` (0 = A0, 1 = A1, 2 = B0, 3 = B1) of k-tile t into buffer t & 1
+    auto stage = [&](int which, int t) {
+      char* dst = smem + (t & 1) * kBuf + which * kHalf + wave * 1024;
+      const size_t koff = (size_t)t * 128;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const char* src = which < 2 ? srcA[which][j] : srcB[which - 2][j];
+        dma16(src + koff, dst + j * 8192);
+      }
+    };
 
-  // ---- fragment read offsets (lane constant part; ds_read immediates do the rest) ----
-  const int fr = lane & 15;
-  int sch[2];
+    f32x4 acc[8][4];
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk) sch[kk] = ((kk * 4 + (lane >> 4)) ^ (fr >> 1)) << 4;
-  const int a_lane = (wr * 64 + fr) * 128;
-  const int b_lane = (wc * 32 + fr) * 128;
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8 af[4][2], b0[2][2], b1[2][2];
-  auto read_a = [&](const char* buf, int h) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        af[i][kk] = *reinterpret_cast<const bf16x8*>(buf + h * kHalf + a_lane + i * 16 * 128 + sch[kk]);
-  };
-  auto read_b = [&](const char* buf, int h, bf16x8 (&bf)[2][2]) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        bf[j][kk] = *reinterpret_cast<const bf16x8*>(buf + (2 + h) * kHalf + b_lane + j * 16 * 128 + sch[kk]);
-  };
-  auto quadrant = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
-    __builtin_amdgcn_s_setprio(1);
-    if (FP8) {
-      // one K=128 MFMA per fragment pair: the two 16-B chunks (g, g+4) of the 128-B k-tile row
+    bf16x8 af[4][2], b0[2][2], b1[2][2];
+    auto read_a = [&](const char* buf, int h) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[mq * 4 + i][nq * 2 + j] = mfma_fp8(bf[j][0], bf[j][1], af[i][0], af[i][1],
-                                                 acc[mq * 4 + i][nq * 2 + j]);
-    } else if (PREC == kInt8) {
-      // two K=64 int8 MFMAs per k-tile (16-B chunks g and g+4), like the two bf16 k-steps
+        for (int kk = 0; kk < 2; ++kk)
+          af[i][kk] = *reinterpret_cast<const bf16x8*>(buf + h * kHalf + a_lane + i * 16 * 128 + sch[kk]);
+    };
+    auto read_b = [&](const char* buf, int h, bf16x8 (&bf)[2][2]) {
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          bf[j][kk] = *reinterpret_cast<const bf16x8*>(buf + (2 + h) * kHalf + b_lane + j * 16 * 128 + sch[kk]);
+    };
+    auto quadrant = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
+      __builtin_amdgcn_s_setprio(1);
+      if (FP8) {
+        // one K=128 MFMA per fragment pair: the two 16-B chunks (g, g+4) of the 128-B k-tile row
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            acc[mq * 4 + i][nq * 2 + j] = mfma_i8(bf[j][kk], af[i][kk], acc[mq * 4 + i][nq * 2 + j]);
-    } else {
+            acc[mq * 4 + i][nq * 2 + j] = mfma_fp8(bf[j][0], bf[j][1], af[i][0], af[i][1],
+                                                   acc[mq * 4 + i][nq * 2 + j]);
+      } else if (PREC == kInt8) {
+        // two K=64 int8 MFMAs per k-tile (16-B chunks g and g+4), like the two bf16 k-steps
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[mq * 4 + i][nq * 2 + j] = mfma(bf[j][kk], af[i][kk], acc[mq * 4 + i][nq * 2 + j]);
-    }
-    __builtin_amdgcn_s_setprio(0);
-  };
+            for (int j = 0; j < 2; ++j)
+              acc[mq * 4 + i][nq * 2 + j] = mfma_i8(bf[j][kk], af[i][kk], acc[mq * 4 + i][nq * 2 + j]);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[mq * 4 + i][nq * 2 + j] = mfma(bf[j][kk], af[i][kk], acc[mq * 4 + i][nq * 2 + j]);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    };
 
-  // ---- prologue: tile 0 complete, three halves of tile 1 in flight ----
-  if (T > 0) {
-    stage(0, 0); stage(2, 0); stage(3, 0); stage(1, 0);
-    if (T > 1) {
-      stage(0, 1); stage(2, 1); stage(3, 1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  barrier();
-
-  // the two wave groups (wr = 0: waves 0-3, wr = 1: waves 4-7, one of each per SIMD) run one
-  // barrier apart, so every SIMD alternates one wave's MFMA segment with the other's LDS reads
-  if (wr == 1) barrier();
-  for (int t = 0; t < T; ++t) {
-    const char* buf = smem + (t & 1) * kBuf;
-    const bool more1 = t + 1 < T, more2 = t + 2 < T;
-    // phase 0: quadrant (0, 0)
-    read_a(buf, 0);
-    read_b(buf, 0, b0);
-    if (more1) stage(1, t + 1);
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    quadrant(0, 0, b0);
-    barrier();
-    // phase 1: quadrant (0, 1)
-    read_b(buf, 1, b1);
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    quadrant(0, 1, b1);
-    barrier();
-    // phase 2: quadrant (1, 1); A-half 0 was last read two phases ago
-    read_a(buf, 1);
-    if (more2) stage(0, t + 2);
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    quadrant(1, 1, b1);
-    barrier();
-    // phase 3: quadrant (1, 0); restage both B halves; retire tile t+1 (all but 3 newest halves)
-    if (more2) {
-      stage(2, t + 2);
-      stage(3, t + 2);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    barrier();
-    quadrant(1, 0, b0);
-    barrier();
-  }
-  if (wr == 0) barrier();
-
-  // ---- epilogue ----
-  // The MFMAs compute the transposed tile (A operand = weight rows): fragment (i, j) element e of
-  // lane l is C[row = 16 i + (l & 15)][col = 16 j + 4 (l >> 4) + e], so each lane owns 4
-  // consecutive output columns of one row -> 8-B (bf16) / 16-B (fp32) vector stores.
-  const int crow = m0 + wr * 128 + fr;
-  const int cq = 4 * (lane >> 4);
-  if (BYTES) {  // dequantise: per-row activation scale x per-output-channel weight scale
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float sa = a_scale[min(crow + i * 16, M - 1)];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const f32x4 sb = *reinterpret_cast<const f32x4*>(b_scale + n0 + wc * 64 + j * 16 + cq);
-        f32x4 v = acc[i][j];
-        if (PREC == kInt8) {
-          typedef int i32x4_t __attribute__((ext_vector_type(4)));
-          const i32x4_t iv = __builtin_bit_cast(i32x4_t, v);
-          v = f32x4{(float)iv[0], (float)iv[1], (float)iv[2], (float)iv[3]};
-        }
-        acc[i][j] = v * sb * sa;
+    // ---- prologue: tile 0 complete, three halves of tile 1 in flight ----
+    // (LDS is free here: every wave passed the realigning barrier after its last ds_read)
+    if (T > 0) {
+      stage(0, 0); stage(2, 0); stage(3, 0); stage(1, 0);
+      if (T > 1) {
+        stage(0, 1); stage(2, 1); stage(3, 1);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-  }
-  if (EPI == kSwiGLU) {
-    // n-fragments (2p, 2p+1) = (gate, up) of output columns n0/2 + wc*32 + p*16 + cq + e
-    bf16* out = reinterpret_cast<bf16*>(C);
-    const int I = N >> 1;
+    barrier();
+
+    // the two wave groups (wr = 0: waves 0-3, wr = 1: waves 4-7, one of each per SIMD) run one
+    // barrier apart, so every SIMD alternates one wave's MFMA segment with the other's LDS reads
+    if (wr == 1) barrier();
+    for (int t = 0; t < T; ++t) {
+      const char* buf = smem + (t & 1) * kBuf;
+      const bool more1 = t + 1 < T, more2 = t + 2 < T;
+      // phase 0: quadrant (0, 0)
+      read_a(buf, 0);
+      read_b(buf, 0, b0);
+      if (more1) stage(1, t + 1);
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      quadrant(0, 0, b0);
+      barrier();
+      // phase 1: quadrant (0, 1)
+      read_b(buf, 1, b1);
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      quadrant(0, 1, b1);
+      barrier();
+      // phase 2: quadrant (1, 1); A-half 0 was last read two phases ago
+      read_a(buf, 1);
+      if (more2) stage(0, t + 2);
+      barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      quadrant(1, 1, b1);
+      barrier();
+      // phase 3: quadrant (1, 0); restage both B halves; retire tile t+1 (all but 3 newest halves)
+      if (more2) {
+        stage(2, t + 2);
+        stage(3, t + 2);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      barrier();
+      quadrant(1, 0, b0);
+      barrier();
+    }
+    if (wr == 0) barrier();
+
+    // ---- stream-K hand-off ----
+    if (kSk && publish) {
+      // slab layout = register order: element (i, j) of thread tid at f32x4 index (i*4+j)*512+tid
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(sk.slabs + (size_t)lid * (kTM * kTN), 0,
+                                                        kTM * kTN * 4, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = crow + i * 16;
-      if (row >= M) continue;
+      for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        bf16x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          // round gate and up to bf16 first: matches the unfused GEMM -> silu_mul path
-          const float g = (float)(bf16)acc[i][2 * p][e];
-          const float u = (float)(bf16)acc[i][2 * p + 1][e];
-          o[e] = (bf16)(silu(g) * u);
+        for (int j = 0; j < 4; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs,
+                                                 tid * 16, (i * 4 + j) * kThreads * 16,
+                                                 16 /* sc1: write-through */);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_store((gu32*)(sk.flags + lid), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;   // nothing to store: the finisher owns the epilogue
+    }
+    // predecessors lid-1, lid-2, ... hold the earlier k-tiles of this tile; the last of them is
+    // the one whose range starts at or before the tile's first k-tile (counted first, on scalars:
+    // a `break` out of the accumulating loop makes the compiler copy and spill the accumulators)
+    int npred = 0;
+    if (kSk && finish)
+      for (int p = lid - 1; p >= 0; --p) {
+        ++npred;
+        if (sk_total * p / sk.sk_wgs <= tile_k0) break;
+      }
+    {
+      for (int q = 1; q <= npred; ++q) {
+        const int p = lid - q;
+        if (__builtin_amdgcn_readfirstlane(tid >> 6) == 0) {   // wave 0 polls (uniform loop)
+          unsigned spins = 0;
+          while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                     (gu32*)(sk.flags + p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins == (1u << 20)) {   // bounded: count the timeout, never hang the GPU
+              if (tid == 0) atomicAdd(sk.err, 1u);
+              break;
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        *reinterpret_cast<bf16x4*>(out + (size_t)row * I + (n0 >> 1) + wc * 32 + p * 16 + cq) = o;
+        __syncthreads();
+        // buffer loads: one VGPR offset (tid * 16) + a constant SGPR offset per fragment, and 4
+        // loads in flight at a time (all 32 at once would need 128 more VGPRs)
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(sk.slabs + (size_t)p * (kTM * kTN), 0,
+                                                          kTM * kTN * 4, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          f32x4 v[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            v[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rs, tid * 16, (i * 4 + j) * kThreads * 16, 0));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] += v[j];
+          __builtin_amdgcn_sched_barrier(0);   // keep the chunks apart (no batching of 32 loads)
+        }
       }
     }
-  } else if (EPI == kStoreF32) {
-    float* out = reinterpret_cast<float*>(C) + (size_t)split * M * N;
+
+    // ---- epilogue ----
+    // The MFMAs compute the transposed tile (A operand = weight rows): fragment (i, j) element e of
+    // lane l is C[row = 16 i + (l & 15)][col = 16 j + 4 (l >> 4) + e], so each lane owns 4
+    // consecutive output columns of one row -> 8-B (bf16) / 16-B (fp32) vector stores.
+    const int crow = m0 + wr * 128 + fr;
+    const int cq = 4 * (lane >> 4);
+    if (BYTES) {  // dequantise: per-row activation scale x per-output-channel weight scale
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = crow + i * 16;
-      if (row >= M) continue;
+      for (int i = 0; i < 8; ++i) {
+        const float sa = a_scale[min(crow + i * 16, M - 1)];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        *reinterpret_cast<f32x4*>(out + (size_t)row * N + n0 + wc * 64 + j * 16 + cq) = acc[i][j];
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 sb = *reinterpret_cast<const f32x4*>(b_scale + n0 + wc * 64 + j * 16 + cq);
+          f32x4 v = acc[i][j];
+          if (PREC == kInt8) {
+            typedef int i32x4_t __attribute__((ext_vector_type(4)));
+            const i32x4_t iv = __builtin_bit_cast(i32x4_t, v);
+            v = f32x4{(float)iv[0], (float)iv[1], (float)iv[2], (float)iv[3]};
+          }
+          acc[i][j] = v * sb * sa;
+        }
+      }
     }
-  } else {
-    bf16* out = reinterpret_cast<bf16*>(C);
+    if (EPI == kSwiGLU) {
+      // n-fragments (2p, 2p+1) = (gate, up) of output columns n0/2 + wc*32 + p*16 + cq + e
+      bf16* out = reinterpret_cast<bf16*>(C);
+      const int I = N >> 1;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = crow + i * 16;
-      if (row >= M) continue;
+      for (int i = 0; i < 8; ++i) {
+        const int row = crow + i * 16;
+        if (row >= M) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        bf16x4 o;
+        for (int p = 0; p < 2; ++p) {
+          bf16x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (bf16)acc[i][j][e];
-        *reinterpret_cast<bf16x4*>(out + (size_t)row * N + n0 + wc * 64 + j * 16 + cq) = o;
+          for (int e = 0; e < 4; ++e) {
+            // round gate and up to bf16 first: matches the unfused GEMM -> silu_mul path
+            const float g = (float)(bf16)acc[i][2 * p][e];
+            const float u = (float)(bf16)acc[i][2 * p + 1][e];
+            o[e] = (bf16)(silu(g) * u);
+          }
+          *reinterpret_cast<bf16x4*>(out + (size_t)row * I + (n0 >> 1) + wc * 32 + p * 16 + cq) = o;
+        }
+      }
+    } else if (EPI == kStoreF32) {
+      float* out = reinterpret_cast<float*>(C) + (size_t)split * M * N;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = crow + i * 16;
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<f32x4*>(out + (size_t)row * N + n0 + wc * 64 + j * 16 + cq) = acc[i][j];
+      }
+    } else {
+      bf16* out = reinterpret_cast<bf16*>(C);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = crow + i * 16;
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (bf16)acc[i][j][e];
+          *reinterpret_cast<bf16x4*>(out + (size_t)row * N + n0 + wc * 64 + j * 16 + cq) = o;
+        }
       }
     }
   }
@@ -363,23 +489,65 @@ __global__ void __launch_bounds__(256) tile_splitk_reduce_kernel(bf16* __restric
   }
 }
 
+int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
+// splits == 0: data-parallel whole tiles + stream-K tail (SkArgs); workspace = the
+// gemm_tile_sk_workspace_floats() layout: [flags | err | pad] 4 KB, then sk_wgs fp32 slabs.
 template <int PREC>
 int launch_tile(void* C, const void* A, const void* B, const float* sa, const float* sb,
                 float* workspace, int M, int N, int K, int splits, int epilogue,
                 hipStream_t stream) {
   constexpr int esz = PREC == kBf16 ? 2 : 1;
   const int kt = (int)((size_t)K * esz / 128);
-  if (M <= 0 || N % kTN != 0 || (size_t)K * esz % 128 != 0 || splits < 1) return -1;
+  if (M <= 0 || N % kTN != 0 || (size_t)K * esz % 128 != 0 || splits < 0) return -1;
   if (splits > kt) return -2;
+  if (PREC != kBf16 && (sa == nullptr || sb == nullptr)) return -5;
+  const int tiles_m = (M + kTM - 1) / kTM, tiles_n = N / kTN;
+  const int tiles = tiles_m * tiles_n;
+  SkArgs sk{0, 0, nullptr, nullptr, nullptr};
+    if (splits == 0) {
+    if (PREC != kBf16) return -10;   // the stream-K tail is compiled for bf16 operands only
+    const int cus = device_cus();
+    if (cus <= 0 || cus > kSkMaxWgs) return -7;
+    if (workspace == nullptr || epilogue == kStoreF32) return -3;
+    sk.sk_wgs = cus;
+    sk.n_dp = tiles / cus * cus;
+    // needs a tail and >= 1 k-tile per stream-K workgroup
+    if (tiles == sk.n_dp || (long long)(tiles - sk.n_dp) * kt < cus) return -8;
+    sk.flags = reinterpret_cast<unsigned*>(workspace);
+    sk.err = reinterpret_cast<unsigned*>(workspace) + kSkErrWord;
+    sk.slabs = workspace + kSkHeaderFloats;
+    // zero the flags (a memset node under graph capture); 16-byte multiple from the allocation start
+    if (hipMemsetAsync(workspace, 0, ((size_t)cus * 4 + 15) / 16 * 16, stream) != hipSuccess) return -9;
+    const int grid = sk.n_dp + sk.sk_wgs;
+    if (epilogue == kSwiGLU)
+      gemm_tile_kernel<kSwiGLU, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
+                                                                    tiles_m, tiles_n, kt, sk);
+    else if (epilogue == kStoreBf16)
+      gemm_tile_kernel<kStoreBf16, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
+                                                                       tiles_m, tiles_n, kt, sk);
+    else
+      return -4;
+    return 0;
+  }
   const int kps = (kt + splits - 1) / splits;
   if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
   if (splits > 1 && (workspace == nullptr || epilogue != kStoreBf16)) return -3;
-  if (PREC != kBf16 && (sa == nullptr || sb == nullptr)) return -5;
-  const int tiles_m = (M + kTM - 1) / kTM, tiles_n = N / kTN;
-  const int grid = tiles_m * tiles_n * splits;
+  const int grid = tiles * splits;
+  sk.n_dp = grid;
   if (splits > 1) {
     gemm_tile_kernel<kStoreF32, PREC><<<grid, kThreads, 0, stream>>>(A, B, workspace, sa, sb, M, N,
-                                                                    K, tiles_m, tiles_n, kps);
+                                                                    K, tiles_m, tiles_n, kps, sk);
     const size_t MN = (size_t)M * N;
     size_t blocks = (MN / 8 + 255) / 256;
     if (blocks > 4096) blocks = 4096;
@@ -387,10 +555,10 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
                                                                workspace, splits, MN);
   } else if (epilogue == kSwiGLU) {
     gemm_tile_kernel<kSwiGLU, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K, tiles_m,
-                                                                  tiles_n, kps);
+                                                                  tiles_n, kps, sk);
   } else if (epilogue == kStoreBf16) {
     gemm_tile_kernel<kStoreBf16, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
-                                                                     tiles_m, tiles_n, kps);
+                                                                     tiles_m, tiles_n, kps, sk);
   } else {
     return -4;
   }
@@ -398,6 +566,11 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
 }
 
 }  // namespace
+
+long long gemm_tile_sk_workspace_floats() {
+  const int cus = device_cus();
+  return cus <= 0 ? -1 : kSkHeaderFloats + (long long)cus * kTM * kTN;
+}
 
 int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale,
                      const float* b_scale, float* workspace, int M, int N, int K, int splits,

@@ -326,10 +326,43 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = 
         return out.copy_(r) if out is not None else r
     if out is None:
         out = torch.empty(M, N // 2 if swiglu else N, dtype=x.dtype, device=x.device)
+    if splits == 1 and tile_gemm_stream_k(M, N, x.device):
+        splits = 0   # data-parallel waves + stream-K tail (csrc/kernels/gemm_tile.hip SkArgs)
+        if workspace is None or workspace.numel() < native().gemm_tile_sk_workspace_floats():
+            workspace = torch.empty(native().gemm_tile_sk_workspace_floats(), dtype=torch.float32,
+                                    device=x.device)
     if splits > 1 and workspace is None:
         workspace = torch.empty(splits * M * N, dtype=torch.float32, device=x.device)
     native().gemm_tile(out, x, w, int(splits), 2 if swiglu else 0, workspace)
     return out
+
+
+_CU_COUNT = {}
+
+
+def device_cus(device) -> int:
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    if idx not in _CU_COUNT:
+        _CU_COUNT[idx] = torch.cuda.get_device_properties(idx).multi_processor_count
+    return _CU_COUNT[idx]
+
+
+def tile_gemm_stream_k(M: int, N: int, device) -> bool:
+    """Whether a whole-K (splits = 1) bf16 ``gemm_tile`` should run its last, partial wave of tiles
+    as a stream-K tail: more tiles than CUs and a remainder of at least half the CUs (Llama-3-70B
+    gate|up at M = 512: 448 tiles = 256 whole + 192 shared k-wise by 256 workgroups, instead of a
+    second wave with 64 idle CUs).  Opt-in (``DLI_TILE_SK=1``): in isolation (back-to-back
+    launches) it is 6-12 % faster (profiles/gemm_sk_bench.json), but inside the decode step the
+    gate|up GEMM runs at the same ~386 us either way (rocprofv3, profiles/stream_k_decode_ab.txt),
+    and bench.py is unchanged within noise.  In the decode step the whole-tile kernel already runs
+    25 % faster than in the isolated loop (386 vs 480 us), so the idle-CU tail is not what bounds
+    it there; a GRBM_GUI_ACTIVE pass shows the stream-K variant at a ~1 % lower clock."""
+    if os.environ.get("DLI_TILE_SK", "0") != "1":
+        return False
+    cus = device_cus(device)
+    tiles = ((M + 255) // 256) * (N // 256)
+    return tiles > cus and tiles % cus >= cus // 2
 
 
 TILE_GEMM_MIN_M = 128    # below: too few rows to fill a 256-row tile (hipBLASLt / skinny path)
@@ -352,7 +385,7 @@ def tile_gemm_splits(M: int, N: int, K: int, elem_bytes: int = 2) -> int:
     if tiles > 2 * _CUS:
         return 0  # e.g. the 128256-wide LM head: hipBLASLt's wide-N solutions are faster (690 vs 824 us)
     best, best_util = 1, 0.0
-    for s in range(1, 9):
+    for s in range(1, int(os.environ.get("DLI_TILE_MAX_SPLITS", "8")) + 1):
         if s > k_tiles or (s > 1 and tiles * s > 2 * _CUS):
             break
         work = tiles * s

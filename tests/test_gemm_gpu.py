@@ -182,3 +182,65 @@ def test_llm_int8_linear_gpu_matches_cpu_and_bf16(gpu):
     ref = xb.float() @ w.float().t()
     assert ((y_gpu - y_cpu).norm() / y_cpu.norm()).item() < 5e-3
     assert ((y_gpu - ref).norm() / ref.norm()).item() < 0.02
+
+
+# ------------------------------------------------- stream-K tail (gemm_tile splits = 0, SkArgs)
+def _sk_workspace(gpu):
+    n = ops.native().gemm_tile_sk_workspace_floats()
+    ws = torch.empty(n, dtype=torch.float32, device=gpu)
+    ws.view(torch.int32)[1023] = 0   # the kernel's spin-timeout counter
+    return ws
+
+
+# tiles = ceil(M/256) * N/256 on 256 CUs: 448 (tail 192, 2 owners per tile, the 70B gate|up
+# case), 384 with K = 256 (4 k-tiles, 2 per workgroup), 288 (tail 32: 8 workgroups per tile,
+# a 7-deep predecessor chain), 260 with K = 4096 (tail 4: 64 workgroups per tile)
+@pytest.mark.parametrize("M,N,K", [(512, 57344, 1024), (256, 98304, 256), (512, 36864, 2048),
+                                   (300, 33280, 4096)])
+@pytest.mark.parametrize("swiglu", [False, True])
+def test_gemm_tile_stream_k_matches_fp32(gpu, M, N, K, swiglu):
+    if ops.device_cus(gpu) != 256:
+        pytest.skip("shapes sized for 256 CUs")
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    ws = _sk_workspace(gpu)
+    out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=gpu)
+    wi = ops.swiglu_interleave(w) if swiglu else w
+    h = x.float() @ w.float().t()
+    ref = ops.silu_mul(h.to(torch.bfloat16)).float() if swiglu else h
+    tol = 2e-2 * max(1.0, ref.abs().max().item())
+    for it in range(3):   # repeated launches: flags re-zeroed, L1/L2 hold the previous slabs
+        out.zero_()
+        ops.native().gemm_tile(out, x, wi, 0, 2 if swiglu else 0, ws)
+        err = (out.float() - ref).abs().max().item()
+        assert err < tol, (it, err)
+    torch.cuda.synchronize()
+    assert int(ws.view(torch.int32)[1023].item()) == 0, "stream-K hand-off spin timed out"
+
+
+def test_gemm_tile_stream_k_dispatch_and_graph(gpu, monkeypatch):
+    """With DLI_TILE_SK=1 ops.gemm_tile picks the stream-K tail for the 70B gate|up shape, also
+    under graph replay."""
+    monkeypatch.setenv("DLI_TILE_SK", "1")
+    if ops.device_cus(gpu) != 256:
+        pytest.skip("shape sized for 256 CUs")
+    M, I, K = 512, 28672, 512
+    assert ops.tile_gemm_stream_k(M, 2 * I, gpu)
+    assert not ops.tile_gemm_stream_k(M, 8192, gpu)       # 64 tiles: split-K instead
+    torch.manual_seed(5)
+    x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
+    w = (torch.randn(2 * I, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    wi = ops.swiglu_interleave(w)
+    ref = ops.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16)).float()
+    out = torch.empty(M, I, dtype=torch.bfloat16, device=gpu)
+    ops.gemm_tile(x, wi, swiglu=True, out=out)       # warm-up outside capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.gemm_tile(x, wi, swiglu=True, out=out)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert (out.float() - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
