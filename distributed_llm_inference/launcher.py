@@ -28,6 +28,14 @@ def free_port() -> int:
     return port
 
 
+def package_pythonpath(current: Optional[str] = None) -> str:
+    """PYTHONPATH for child processes that import this package (``-m distributed_llm_inference``)
+    however the parent was started (e.g. ``/path/to/distribute`` from another directory)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    parts = [p for p in (current or "").split(os.pathsep) if p]
+    return os.pathsep.join([root] + [p for p in parts if p != root])
+
+
 def launch(nproc: int, argv: Sequence[str], env: Optional[Dict[str, str]] = None,
            port: Optional[int] = None, grace_s: float = 10.0, poll_s: float = 0.2,
            gpus: Optional[Sequence[int]] = None) -> int:
@@ -36,6 +44,7 @@ def launch(nproc: int, argv: Sequence[str], env: Optional[Dict[str, str]] = None
     base = dict(os.environ)
     base.update(env or {})
     base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    base["PYTHONPATH"] = package_pythonpath(base.get("PYTHONPATH"))
     base["MASTER_ADDR"] = "127.0.0.1"
     base["MASTER_PORT"] = str(port)
     base["WORLD_SIZE"] = str(nproc)

@@ -32,7 +32,7 @@ import urllib.request
 from typing import Dict, List, Optional, Sequence, Tuple
 
 from ..config import plan_stages, resolve_model
-from ..launcher import _shutdown, free_port
+from ..launcher import _shutdown, free_port, package_pythonpath
 
 log = logging.getLogger(__name__)
 
@@ -77,6 +77,7 @@ class Server:
                     WORLD_SIZE=str(self.num_gpus), LOCAL_WORLD_SIZE=str(self.num_gpus),
                     DLI_STAGE_RANGES=json.dumps(ranges), DLI_PUBLISH_STATS="1")
         base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        base["PYTHONPATH"] = package_pythonpath(base.get("PYTHONPATH"))
         args = [sys.executable, "-m", "distributed_llm_inference.cli", "worker", "--action", "serve",
                 "--model", self.model, "--gpus", str(self.num_gpus), "--port", str(self.port)]
         if self.checkpoint:
