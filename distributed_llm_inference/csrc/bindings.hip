@@ -57,6 +57,44 @@ void rms_norm(Tensor out, Tensor x, optional<Tensor> residual, Tensor w, double 
                                 cur_stream()), "rms_norm");
 }
 
+void splitk_reduce(Tensor out, Tensor parts) {
+  CHECK_IN(out); CHECK_IN(parts); CHECK_BF16(out); CHECK_F32(parts);
+  TORCH_CHECK(parts.dim() == 3 && out.numel() == parts.size(1) * parts.size(2),
+              "splitk_reduce: parts [S, M, N] and out [M, N]");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(parts.device());
+  check_rc(dli::launch_splitk_reduce(bp(out), parts.data_ptr<float>(), (int)parts.size(0),
+                                     (size_t)out.numel(), cur_stream()), "splitk_reduce");
+}
+
+// RMSNorm whose input is the un-reduced fp32 split-K output of gemm_tile(defer_reduce=True):
+// parts [splits, rows, hidden]; the sum (rounded to bf16) replaces x.
+void rms_norm_splitk(Tensor out, Tensor parts, optional<Tensor> residual, Tensor w, double eps,
+                     optional<Tensor> residual_out) {
+  CHECK_IN(out); CHECK_IN(parts); CHECK_IN(w);
+  CHECK_BF16(out); CHECK_F32(parts); CHECK_BF16(w);
+  TORCH_CHECK(parts.dim() == 3, "rms_norm_splitk: parts must be [splits, rows, hidden]");
+  const int64_t splits = parts.size(0), rows = parts.size(1), hidden = parts.size(2);
+  TORCH_CHECK(splits >= 1 && w.numel() == hidden && out.numel() == rows * hidden,
+              "rms_norm_splitk: shape mismatch");
+  const dli::bf16* r = nullptr;
+  dli::bf16* ro = nullptr;
+  if (residual.has_value()) {
+    CHECK_IN(*residual); CHECK_BF16(*residual);
+    TORCH_CHECK(residual->numel() == rows * hidden, "rms_norm_splitk: residual shape mismatch");
+    r = bp(*residual);
+    ro = bp(*residual);
+    if (residual_out.has_value()) {
+      CHECK_IN(*residual_out); CHECK_BF16(*residual_out);
+      TORCH_CHECK(residual_out->numel() == rows * hidden, "rms_norm_splitk: residual_out shape");
+      ro = bp(*residual_out);
+    }
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(parts.device());
+  check_rc(dli::launch_rms_norm(bp(out), nullptr, r, ro, bp(w), (float)eps, (int)rows,
+                                (int)hidden, cur_stream(), parts.data_ptr<float>(), (int)splits),
+           "rms_norm_splitk");
+}
+
 void layer_norm(Tensor out, Tensor x, optional<Tensor> residual, Tensor w, Tensor b, double eps,
                 optional<Tensor> residual_out) {
   CHECK_IN(out); CHECK_IN(x); CHECK_IN(w); CHECK_IN(b);
@@ -416,8 +454,10 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_tile: 2-D tensors");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K && out.size(0) == M, "gemm_tile: shape mismatch");
-  TORCH_CHECK(epilogue == 0 || epilogue == 2, "gemm_tile: epilogue must be 0 (store) or 2 (swiglu)");
-  TORCH_CHECK(out.size(1) == (epilogue == 2 ? N / 2 : N), "gemm_tile: output columns");
+  TORCH_CHECK(epilogue >= 0 && epilogue <= 2,
+              "gemm_tile: epilogue must be 0 (store), 1 (split-K partials only) or 2 (swiglu)");
+  TORCH_CHECK(epilogue == 1 || out.size(1) == (epilogue == 2 ? N / 2 : N), "gemm_tile: output columns");
+  TORCH_CHECK(epilogue != 1 || splits > 1, "gemm_tile: epilogue 1 (partials only) needs splits > 1");
   const int64_t kt = K * a.element_size() / 128;
   TORCH_CHECK(M >= 1 && M <= (1 << 20) && N % 256 == 0 && (K * a.element_size()) % 128 == 0 && K > 0,
               "gemm_tile: needs N % 256 == 0 and 128-byte multiples of K");
@@ -440,7 +480,7 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
                 "gemm_tile: stream-K workspace too small");
     ws = workspace->data_ptr<float>();
   } else if (splits > 1) {
-    TORCH_CHECK(epilogue == 0, "gemm_tile: split-K only with the plain store epilogue");
+    TORCH_CHECK(epilogue != 2, "gemm_tile: split-K only with the store / partials epilogues");
     TORCH_CHECK(workspace.has_value(), "gemm_tile: split-K needs a workspace");
     CHECK_IN(*workspace); CHECK_F32(*workspace);
     TORCH_CHECK(workspace->numel() >= splits * M * N, "gemm_tile: workspace too small");
@@ -500,6 +540,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
         py::arg("epilogue") = 0, py::arg("workspace") = py::none(),
         py::arg("a_scale") = py::none(), py::arg("b_scale") = py::none());
+  m.def("rms_norm_splitk", &rms_norm_splitk, "residual add + RMSNorm over un-reduced split-K partials",
+        py::arg("out"), py::arg("parts"), py::arg("residual"), py::arg("w"), py::arg("eps"),
+        py::arg("residual_out") = py::none());
+  m.def("splitk_reduce", &splitk_reduce, "bf16 out = sum of fp32 split-K partials [S, M, N]");
   m.def("gemm_tile_sk_workspace_floats", []() { return dli::gemm_tile_sk_workspace_floats(); },
         "fp32 workspace elements gemm_tile(splits=0) needs on the current device");
   m.def("skinny_gemm", &skinny_gemm, "y = x . W^T (+ bias) for M <= 4 (weight-streaming GEMV)",

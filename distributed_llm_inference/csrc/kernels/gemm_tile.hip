@@ -542,12 +542,15 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
   }
   const int kps = (kt + splits - 1) / splits;
   if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
-  if (splits > 1 && (workspace == nullptr || epilogue != kStoreBf16)) return -3;
+  // kStoreF32 with splits > 1: partials only, the consumer reduces them (rms_norm_splitk)
+  if (splits > 1 && (workspace == nullptr || epilogue == kSwiGLU)) return -3;
+  if (splits == 1 && epilogue == kStoreF32) return -3;
   const int grid = tiles * splits;
   sk.n_dp = grid;
   if (splits > 1) {
     gemm_tile_kernel<kStoreF32, PREC><<<grid, kThreads, 0, stream>>>(A, B, workspace, sa, sb, M, N,
                                                                     K, tiles_m, tiles_n, kps, sk);
+    if (epilogue == kStoreF32) return 0;
     const size_t MN = (size_t)M * N;
     size_t blocks = (MN / 8 + 255) / 256;
     if (blocks > 4096) blocks = 4096;
@@ -566,6 +569,15 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
 }
 
 }  // namespace
+
+int launch_splitk_reduce(bf16* C, const float* parts, int splits, size_t MN, hipStream_t stream) {
+  if (splits < 1 || MN % 8 != 0) return -1;
+  if (MN == 0) return 0;
+  size_t blocks = (MN / 8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  tile_splitk_reduce_kernel<<<(int)blocks, 256, 0, stream>>>(C, parts, splits, MN);
+  return 0;
+}
 
 long long gemm_tile_sk_workspace_floats() {
   const int cus = device_cus();

@@ -58,7 +58,8 @@ struct SampleParams {
 };
 
 int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* residual_out,
-                    const bf16* w, float eps, int rows, int hidden, hipStream_t stream);
+                    const bf16* w, float eps, int rows, int hidden, hipStream_t stream,
+                    const float* x_parts = nullptr, int splits = 0);
 int launch_layer_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* residual_out,
                       const bf16* w, const bf16* b, float eps, int rows, int hidden,
                       hipStream_t stream);
@@ -74,6 +75,8 @@ int launch_sample(const SampleParams& p, int B, hipStream_t stream);
 int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale,
                      const float* b_scale, float* workspace, int M, int N, int K, int splits,
                      int epilogue, int precision, hipStream_t stream);
+// C[MN] (bf16) = sum over `splits` fp32 partial products parts[splits][MN]
+int launch_splitk_reduce(bf16* C, const float* parts, int splits, size_t MN, hipStream_t stream);
 // fp32 elements of the workspace gemm_tile needs for splits == 0 (stream-K tail) on this device
 long long gemm_tile_sk_workspace_floats();
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,

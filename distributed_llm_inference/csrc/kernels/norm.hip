@@ -12,12 +12,18 @@
 
 namespace dli {
 
+// x_parts (optional): x is given as `splits` fp32 split-K partial products [splits, rows, hidden]
+// of the tile GEMM that produced it (gemm_tile.hip kStoreF32); they are summed and rounded to bf16
+// here, exactly as tile_splitk_reduce_kernel would, so the reduction pass and its bf16 round trip
+// through HBM disappear while the numerics stay bit-identical.
 template <int VPT>  // bf16x8 vectors per thread
 __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
                                                        const bf16* __restrict__ x,
                                                        const bf16* residual_in, bf16* residual_out,
                                                        const bf16* __restrict__ w, float eps,
-                                                       int hidden, int add_residual) {
+                                                       int hidden, int add_residual,
+                                                       const float* __restrict__ x_parts,
+                                                       int splits, size_t split_stride) {
   __shared__ float scratch[8];
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
@@ -35,7 +41,23 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
     const int idx = threadIdx.x + i * blockDim.x;
     if (idx < nvec) {
       wv[i] = wr[idx];
-      bf16x8 a = xr[idx];
+      bf16x8 a;
+      if (x_parts != nullptr) {
+        const float* pp = x_parts + (size_t)row * hidden + (size_t)idx * 8;
+        f32x4 s0 = *reinterpret_cast<const f32x4*>(pp);
+        f32x4 s1 = *reinterpret_cast<const f32x4*>(pp + 4);
+        for (int k = 1; k < splits; ++k) {
+          s0 += *reinterpret_cast<const f32x4*>(pp + k * split_stride);
+          s1 += *reinterpret_cast<const f32x4*>(pp + k * split_stride + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = (bf16)s0[j];
+          a[j + 4] = (bf16)s1[j];
+        }
+      } else {
+        a = xr[idx];
+      }
       if (add_residual) {
         bf16x8 r = ri[idx];
         bf16x8 s;
@@ -162,10 +184,14 @@ static inline int norm_threads(int hidden) {
 
 // Returns 0 on success, -1 if `hidden` is unsupported (must be a multiple of 8, <= 16384).
 int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* residual_out,
-                    const bf16* w, float eps, int rows, int hidden, hipStream_t stream) {
+                    const bf16* w, float eps, int rows, int hidden, hipStream_t stream,
+                    const float* x_parts, int splits) {
   if (hidden % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -1;
+  if (x_parts != nullptr && splits < 1) return -2;
   const int add = residual_in != nullptr ? 1 : 0;
-  DLI_NORM_DISPATCH(rms_norm_kernel, out, x, residual_in, residual_out, w, eps, hidden, add);
+  const size_t stride = (size_t)rows * hidden;
+  DLI_NORM_DISPATCH(rms_norm_kernel, out, x, residual_in, residual_out, w, eps, hidden, add,
+                    x_parts, splits, stride);
   return 0;
 }
 

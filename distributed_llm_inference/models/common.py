@@ -73,9 +73,11 @@ class Linear(nn.Module):
         return ops.tile_gemm_splits(x.shape[0], self.out_features, self.in_features)
 
     def forward(self, x: Optional[torch.Tensor],
-                x_q: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> torch.Tensor:
+                x_q: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                defer_reduce: bool = False):
         """``x_q`` = (fp8 rows, scales) already quantised by a fused producer kernel; then ``x`` may
-        be None (fp8 weights only)."""
+        be None (fp8 weights only).  ``defer_reduce``: a split-K tile GEMM returns its fp32
+        partials (``ops.SplitKPartials``) for an RMSNorm consumer to reduce."""
         if self.weight_int8 is not None:
             y = ops.llm_int8_linear(x.reshape(-1, self.in_features), self.weight_int8,
                                     self.weight_scale, self.int8_threshold)
@@ -89,7 +91,7 @@ class Linear(nn.Module):
                 return ops.skinny_gemm(x, self.weight, self.bias)
             sp = self.tile_splits(x)
             if sp:  # decode micro-batches: 256x256 MFMA tile kernel (csrc/kernels/gemm_tile.hip)
-                return ops.gemm_tile(x, self.weight, splits=sp)
+                return ops.gemm_tile(x, self.weight, splits=sp, defer_reduce=defer_reduce)
             return F.linear(x, self.weight, self.bias)
         if x_q is None:
             x_q = ops.quant_rowwise(x)

@@ -100,11 +100,15 @@ class LlamaBlock(nn.Module):
                        collect: Optional[list] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """Run the local layers on packed tokens ``hidden [T, H]``.  Returns ``(out, residual)``;
         the stage output hidden state is ``out + residual``."""
+        last = len(self.layers) - 1
         for i, layer in enumerate(self.layers):
             if collect is not None:
                 collect.append(hidden if residual is None else ops.add(hidden, residual))
             k, v = pool.layer(layer_offset + i)
-            hidden, residual = layer(hidden, residual, meta, k, v, self.cos_sin)
+            # between layers the down projection's split-K partials go straight into the next
+            # input RMSNorm; the block's output is always materialised
+            hidden, residual = layer(hidden, residual, meta, k, v, self.cos_sin,
+                                     defer_out=collect is None and i < last)
         return hidden, residual
 
     # ------------------------------------------------------------------ reference API

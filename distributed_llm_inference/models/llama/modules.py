@@ -73,7 +73,7 @@ class LlamaAttention(nn.Module):
                              device=device)
 
     def forward(self, normed: Optional[torch.Tensor], meta: AttnMetadata, k_cache: torch.Tensor,
-                v_cache: torch.Tensor, cos_sin: torch.Tensor, x_q=None) -> torch.Tensor:
+                v_cache: torch.Tensor, cos_sin: torch.Tensor, x_q=None, defer_reduce: bool = False):
         qkv = self.qkv_proj(normed, x_q)
         T = qkv.shape[0]
         q, q_sink = ops.rope_cache(qkv, meta.positions, meta.slot_mapping, cos_sin, self.num_heads,
@@ -91,7 +91,7 @@ class LlamaAttention(nn.Module):
                                  meta.ring, meta.window, k_scale=meta.k_scale,
                                  v_scale=meta.v_scale, tile_map=meta.tile_map)
         o = o.view(T, self.num_heads * self.head_dim)
-        return self.o_proj(o)
+        return self.o_proj(o, defer_reduce=defer_reduce)
 
 
 class LlamaMLP(nn.Module):
@@ -120,15 +120,17 @@ class LlamaMLP(nn.Module):
             w.weight.data.copy_(perm(w.weight.data))
         self.fused_swiglu = on
 
-    def forward(self, normed: Optional[torch.Tensor], x_q=None) -> torch.Tensor:
+    def forward(self, normed: Optional[torch.Tensor], x_q=None, defer_reduce: bool = False):
         if self.fused_swiglu:
             if self.gate_up_proj.tile_splits(normed):
-                return self.down_proj(ops.gemm_tile(normed, self.gate_up_proj.weight, swiglu=True))
-            return self.down_proj(ops.swiglu_interleaved(self.gate_up_proj(normed)))
+                h = ops.gemm_tile(normed, self.gate_up_proj.weight, swiglu=True)
+            else:
+                h = ops.swiglu_interleaved(self.gate_up_proj(normed))
+            return self.down_proj(h, defer_reduce=defer_reduce)
         gu = self.gate_up_proj(normed, x_q)
         if self.down_proj.is_fp8:  # SwiGLU fused with the fp8 quantisation of down_proj's input
             return self.down_proj(None, ops.silu_mul_quant(gu))
-        return self.down_proj(ops.silu_mul(gu))
+        return self.down_proj(ops.silu_mul(gu), defer_reduce=defer_reduce)
 
 
 class LlamaDecoderLayer(nn.Module):
@@ -143,9 +145,12 @@ class LlamaDecoderLayer(nn.Module):
         self.input_layernorm = RMSNorm(spec.hidden_size, spec.rms_norm_eps, device, dtype)
         self.post_attention_layernorm = RMSNorm(spec.hidden_size, spec.rms_norm_eps, device, dtype)
 
-    def forward(self, hidden: torch.Tensor, residual: Optional[torch.Tensor], meta: AttnMetadata,
-                k_cache: torch.Tensor, v_cache: torch.Tensor,
-                cos_sin: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    def forward(self, hidden, residual: Optional[torch.Tensor], meta: AttnMetadata,
+                k_cache: torch.Tensor, v_cache: torch.Tensor, cos_sin: torch.Tensor,
+                defer_out: bool = False):
+        """``defer_out``: the returned hidden state may be ``ops.SplitKPartials`` (the next
+        layer's input RMSNorm reduces them); the O projection's partials always go straight
+        into the post-attention RMSNorm."""
         if self.self_attn.qkv_proj.is_fp8:
             return self._forward_fp8(hidden, residual, meta, k_cache, v_cache, cos_sin)
         first = residual is None
@@ -156,10 +161,10 @@ class LlamaDecoderLayer(nn.Module):
             normed, _ = self.input_layernorm(hidden)
         else:
             normed, residual = self.input_layernorm(hidden, residual)
-        attn = self.self_attn(normed, meta, k_cache, v_cache, cos_sin)
+        attn = self.self_attn(normed, meta, k_cache, v_cache, cos_sin, defer_reduce=True)
         normed, residual = self.post_attention_layernorm(
             attn, residual, residual_out=torch.empty_like(residual) if first else None)
-        return self.mlp(normed), residual
+        return self.mlp(normed, defer_reduce=defer_out), residual
 
     def _forward_fp8(self, hidden, residual, meta, k_cache, v_cache, cos_sin):
         """fp8 weights: every RMSNorm is fused with the fp8 quantisation of the GEMM input that

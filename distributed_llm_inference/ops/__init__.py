@@ -47,11 +47,45 @@ def _gpu(t: torch.Tensor) -> bool:
 
 
 # ----------------------------------------------------------------------------- normalisation
+class SplitKPartials:
+    """The un-reduced output of a split-K tile GEMM: fp32 partial products ``parts [S, M, N]``.
+
+    ``gemm_tile(..., defer_reduce=True)`` returns this instead of running the reduction pass;
+    ``rms_norm`` sums the partials while it reads them (norm.hip ``x_parts``), so the reduce
+    kernel and the bf16 [M, N] round trip through HBM disappear.  Any other consumer calls
+    :meth:`materialize`."""
+
+    __slots__ = ("parts",)
+
+    def __init__(self, parts: torch.Tensor):
+        self.parts = parts
+
+    @property
+    def shape(self):
+        return torch.Size(self.parts.shape[1:])
+
+    @property
+    def device(self):
+        return self.parts.device
+
+    dtype = torch.bfloat16
+    is_cuda = True
+
+    def materialize(self) -> torch.Tensor:
+        out = torch.empty(self.parts.shape[1:], dtype=torch.bfloat16, device=self.parts.device)
+        native().splitk_reduce(out, self.parts)
+        return out
+
+
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
              out: Optional[torch.Tensor] = None, residual_out: Optional[torch.Tensor] = None
              ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """``r = x + residual`` written to ``residual_out`` (default: in place into ``residual``);
-    ``out = RMSNorm(r or x) * w``.  Returns ``(out, r)``."""
+    ``out = RMSNorm(r or x) * w``.  Returns ``(out, r)``.  ``x`` may be :class:`SplitKPartials`."""
+    if isinstance(x, SplitKPartials):
+        out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if out is None else out
+        native().rms_norm_splitk(out, x.parts, residual, w, float(eps), residual_out)
+        return out, (residual_out if residual_out is not None else residual)
     if not _gpu(x):
         y, r = ref.rms_norm(x, w, eps, residual, residual_out)
         if out is not None:
@@ -311,12 +345,19 @@ def swiglu_deinterleave(w: torch.Tensor) -> torch.Tensor:
 
 
 def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = False,
-              out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None
-              ) -> torch.Tensor:
+              out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+              defer_reduce: bool = False):
     """``x [M, K] @ w[N, K]^T`` with the 256x256 LDS-DMA MFMA kernel (N % 256 == 0, K % 64 == 0).
     ``swiglu=True``: ``w`` is a ``swiglu_interleave``d [gate; up] weight and the result is
-    ``silu(x @ gate^T) * (x @ up^T)`` ([M, N/2])."""
+    ``silu(x @ gate^T) * (x @ up^T)`` ([M, N/2]).  ``defer_reduce`` (split-K only): return the
+    fp32 partials as :class:`SplitKPartials` for a consumer that reduces them (``rms_norm``)."""
     M, N = x.shape[0], w.shape[0]
+    if (defer_reduce and splits > 1 and _gpu(x) and not swiglu
+            and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
+        parts = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+        dummy = torch.empty(M, 0, dtype=torch.bfloat16, device=x.device)   # C is unused
+        native().gemm_tile(dummy, x, w, int(splits), 1, parts.view(-1))
+        return SplitKPartials(parts)
     if not _gpu(x):
         if swiglu:
             h = (x.float() @ swiglu_deinterleave(w).float().t()).to(x.dtype).float()

@@ -206,3 +206,16 @@ def test_int8_weights_close_to_bf16(gpu):
     b = _stage_logits(stage, prompts, 0)[0]
     rel = (a - b).norm() / a.norm()
     assert rel < 0.1, rel
+
+
+def test_deferred_splitk_reduce_is_bit_identical(gpu, monkeypatch):
+    """Split-K partials reduced inside the next RMSNorm (default) vs the separate reduce pass
+    (DLI_SPLITK_DEFER=0): same bf16 rounding points, so the stage output is bit-identical."""
+    spec = SPEC.replace(hidden_size=512, intermediate_size=1024, num_heads=4, num_kv_heads=2,
+                        head_dim=128)
+    g = CausalLMStage(spec, 0, 4, device=gpu).init_random(5)
+    prompts = [list(range(1, 200)), list(range(3, 150))]   # 347 rows: tile GEMMs with split-K
+    a = _stage_logits(g, prompts, 0)[0]
+    monkeypatch.setenv("DLI_SPLITK_DEFER", "0")
+    b = _stage_logits(g, prompts, 0)[0]
+    assert torch.equal(a, b)

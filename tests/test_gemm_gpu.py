@@ -244,3 +244,45 @@ def test_gemm_tile_stream_k_dispatch_and_graph(gpu, monkeypatch):
         g.replay()
         torch.cuda.synchronize()
         assert (out.float() - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
+
+
+# ------------------------------------- split-K partials reduced inside the consumer RMSNorm
+@pytest.mark.parametrize("S,M,H", [(3, 512, 8192), (4, 300, 4096), (2, 7, 1024)])
+@pytest.mark.parametrize("mode", ["none", "inplace", "out_of_place"])
+def test_rms_norm_splitk_bit_identical_to_reduce_then_norm(gpu, S, M, H, mode):
+    torch.manual_seed(S * M + H)
+    parts = torch.randn(S, M, H, device=gpu)
+    w = torch.randn(H, device=gpu, dtype=torch.bfloat16)
+    res = torch.randn(M, H, device=gpu, dtype=torch.bfloat16) if mode != "none" else None
+    x = ops.SplitKPartials(parts).materialize()
+    assert torch.equal(x, parts.sum(0).to(torch.bfloat16)) or \
+        (x.float() - parts.sum(0)).abs().max().item() < 1e-2
+    r1 = res.clone() if res is not None else None
+    r2 = res.clone() if res is not None else None
+    ro1 = torch.empty_like(res) if mode == "out_of_place" else None
+    ro2 = torch.empty_like(res) if mode == "out_of_place" else None
+    y1, rr1 = ops.rms_norm(x, w, 1e-5, residual=r1, residual_out=ro1)
+    y2, rr2 = ops.rms_norm(ops.SplitKPartials(parts), w, 1e-5, residual=r2, residual_out=ro2)
+    assert torch.equal(y1, y2)
+    if res is not None:
+        assert torch.equal(rr1, rr2)
+        if mode == "out_of_place":
+            assert torch.equal(r2, res)   # residual_in untouched
+
+
+def test_gemm_tile_defer_reduce_feeds_rms_norm(gpu):
+    torch.manual_seed(11)
+    M, N, K = 512, 8192, 8192
+    x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    nw = torch.randn(N, device=gpu, dtype=torch.bfloat16)
+    res = torch.randn(M, N, device=gpu, dtype=torch.bfloat16)
+    sp = ops.tile_gemm_splits(M, N, K)
+    assert sp > 1
+    p = ops.gemm_tile(x, w, splits=sp, defer_reduce=True)
+    assert isinstance(p, ops.SplitKPartials) and p.parts.shape == (sp, M, N)
+    y_ref = ops.gemm_tile(x, w, splits=sp)
+    assert torch.equal(p.materialize(), y_ref)
+    a, ra = ops.rms_norm(y_ref, nw, 1e-5, residual=res.clone())
+    b, rb = ops.rms_norm(p, nw, 1e-5, residual=res.clone())
+    assert torch.equal(a, b) and torch.equal(ra, rb)
