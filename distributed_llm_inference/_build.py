@@ -54,6 +54,34 @@ def _mtime(paths) -> float:
     return max((os.path.getmtime(p) for p in paths if os.path.exists(p)), default=0.0)
 
 
+def _content_hash(paths: List[str], extra: str = "") -> str:
+    h = hashlib.sha1(extra.encode())
+    for p in sorted(paths):
+        if os.path.exists(p):
+            h.update(os.path.relpath(p, PKG_DIR).encode())
+            with open(p, "rb") as f:
+                h.update(f.read())
+    return h.hexdigest()
+
+
+def _up_to_date(out: str, deps: List[str], extra: str) -> bool:
+    """The built ``out`` matches the sources: by the content hash recorded next to it at build
+    time (robust to a copy that does not preserve mtimes, e.g. a repository snapshot shipped to
+    another machine), else — no record yet — by modification times."""
+    if not os.path.exists(out):
+        return False
+    rec = out + ".srchash"
+    if os.path.exists(rec):
+        with open(rec) as f:
+            return f.read().strip() == _content_hash(deps, extra)
+    return os.path.getmtime(out) >= _mtime(deps)
+
+
+def _record(out: str, deps: List[str], extra: str) -> None:
+    with open(out + ".srchash", "w") as f:
+        f.write(_content_hash(deps, extra) + "\n")
+
+
 def _run(cmd: List[str], verbose: bool) -> None:
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -101,7 +129,7 @@ def build_kernels(force: bool = False, verbose: bool = False, workers: Optional[
     srcs = [os.path.join(CSRC, s) for s in KERNEL_SOURCES + TORCH_SOURCES]
     srcs = [s for s in srcs if os.path.exists(s)]
     deps = srcs + _headers() + [__file__]
-    if not force and os.path.exists(out) and os.path.getmtime(out) >= _mtime(deps):
+    if not force and _up_to_date(out, deps, ARCH):
         return out
     os.makedirs(BUILD_DIR, exist_ok=True)
     tcflags, ldflags = _torch_flags()
@@ -122,6 +150,7 @@ def build_kernels(force: bool = False, verbose: bool = False, workers: Optional[
     tmp = out + ".tmp"
     _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ldflags, verbose)
     os.replace(tmp, out)
+    _record(out, deps, ARCH)
     return out
 
 
@@ -130,7 +159,7 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
     out = runtime_so_path()
     srcs = [os.path.join(CSRC, s) for s in RUNTIME_SOURCES]
     deps = srcs + _headers() + [__file__]
-    if not force and os.path.exists(out) and os.path.getmtime(out) >= _mtime(deps):
+    if not force and _up_to_date(out, deps, "runtime"):
         return out
     cxx = os.environ.get("CXX") or shutil.which("g++") or "c++"
     tmp = out + ".tmp"
@@ -138,6 +167,7 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
           [f"-I{p}" for p in _py_includes()] + srcs + ["-o", tmp, "-lrt", "-pthread"]
     _run(cmd, verbose)
     os.replace(tmp, out)
+    _record(out, deps, "runtime")
     return out
 
 
