@@ -178,21 +178,36 @@ void rope_cache(Tensor qkv, optional<Tensor> positions, optional<Tensor> slot_ma
                 optional<Tensor> cos_sin, Tensor q_out, optional<Tensor> q_sink_out,
                 int64_t window, Tensor k_cache, Tensor v_cache, int64_t nh, int64_t nkv,
                 double k_scale, double v_scale) {
-  CHECK_DEV(qkv); CHECK_BF16(qkv);
-  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "qkv must be [T, *] with unit inner stride");
-  const int64_t T = qkv.size(0);
+  CHECK_DEV(qkv);
+  // qkv: the bf16 GEMM output [T, *], or its un-reduced fp32 split-K partials [S, T, N]
+  const bool parts = qkv.scalar_type() == at::kFloat;
+  if (parts) {
+    TORCH_CHECK(qkv.dim() == 3 && qkv.is_contiguous(), "qkv partials must be contiguous [S, T, N]");
+  } else {
+    CHECK_BF16(qkv);
+    TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "qkv must be [T, *] with unit inner stride");
+  }
+  const int64_t T = parts ? qkv.size(1) : qkv.size(0);
   CHECK_IN(q_out); CHECK_BF16(q_out);
   TORCH_CHECK(q_out.dim() == 3 && q_out.size(0) == T && q_out.size(1) == nh, "q_out must be [T, nh, D]");
   const int64_t D = q_out.size(2);
-  TORCH_CHECK(qkv.size(1) >= (nh + 2 * nkv) * D, "qkv too narrow for nh/nkv/D");
+  TORCH_CHECK(qkv.size(qkv.dim() - 1) >= (nh + 2 * nkv) * D, "qkv too narrow for nh/nkv/D");
   const bool fp8 = check_cache(k_cache, v_cache, nkv, D);
   TORCH_CHECK(k_scale > 0 && v_scale > 0, "KV scales must be positive");
   dli::RopeCacheParams p{};
   p.kv_fp8 = fp8 ? 1 : 0;
   p.k_inv_scale = (float)(1.0 / k_scale);
   p.v_inv_scale = (float)(1.0 / v_scale);
-  p.qkv = bp(qkv);
-  p.qkv_stride = qkv.stride(0);
+  if (parts) {
+    p.qkv = nullptr;
+    p.qkv_parts = qkv.data_ptr<float>();
+    p.splits = (int)qkv.size(0);
+    p.qkv_stride = qkv.size(2);
+    p.split_stride = (long)(T * qkv.size(2));
+  } else {
+    p.qkv = bp(qkv);
+    p.qkv_stride = qkv.stride(0);
+  }
   if (positions.has_value()) {
     CHECK_IN(*positions); CHECK_I32(*positions);
     TORCH_CHECK(positions->numel() == T, "positions must have T entries");

@@ -41,6 +41,11 @@ struct RopeCacheParams {
   int kv_fp8;
   float k_inv_scale, v_inv_scale;  // fp8: stored = x * inv_scale
   int nh, nkv, D, bs;
+  // optional: qkv given as un-reduced fp32 split-K partials [splits, T, qkv_stride] of the QKV
+  // tile GEMM (summed and rounded to bf16 on load, as the reduce pass would); qkv is unused then
+  const float* qkv_parts;
+  int splits;
+  long split_stride;      // elements between consecutive partials (T * qkv_stride)
 };
 
 struct SampleParams {

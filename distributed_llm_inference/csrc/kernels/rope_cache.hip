@@ -33,6 +33,29 @@ __device__ __forceinline__ void rotate4(const bf16x4& a, const bf16x4& b, const 
   }
 }
 
+// 4 consecutive qkv elements of token row t starting at column c: from the bf16 GEMM output, or
+// summed over the fp32 split-K partials and rounded once (bit-identical to the reduce pass)
+__device__ __forceinline__ bf16x4 load_qkv4(const RopeCacheParams& p, const bf16* row, int t,
+                                            int c) {
+  if (p.qkv_parts == nullptr) return *reinterpret_cast<const bf16x4*>(row + c);
+  const float* q = p.qkv_parts + (size_t)t * p.qkv_stride + c;
+  f32x4 s = *reinterpret_cast<const f32x4*>(q);
+  for (int k = 1; k < p.splits; ++k) s += *reinterpret_cast<const f32x4*>(q + k * p.split_stride);
+  bf16x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = (bf16)s[j];
+  return o;
+}
+
+__device__ __forceinline__ bf16 load_qkv1(const RopeCacheParams& p, const bf16* row, int t,
+                                          int c) {
+  if (p.qkv_parts == nullptr) return row[c];
+  const float* q = p.qkv_parts + (size_t)t * p.qkv_stride + c;
+  float s = q[0];
+  for (int k = 1; k < p.splits; ++k) s += q[k * p.split_stride];
+  return (bf16)s;
+}
+
 // grid (T, ceil(total_heads / kHeadsPerWG)): one workgroup per (token, group of 8 heads) so a
 // decode step of B tokens launches B * 10 workgroups (70B) instead of B — the kernel is
 // latency-bound, not bandwidth-bound, at one workgroup per token.
@@ -70,9 +93,8 @@ __global__ void __launch_bounds__(128) rope_cache_kernel(RopeCacheParams p) {
   for (int it = rot_lo + threadIdx.x; it < rot_hi; it += blockDim.x) {
     const int head = it / gpr;
     const int i = (it % gpr) * 4;
-    const bf16* src = row + (size_t)head * D;
-    const bf16x4 a = *reinterpret_cast<const bf16x4*>(src + i);
-    const bf16x4 b = *reinterpret_cast<const bf16x4*>(src + half + i);
+    const bf16x4 a = load_qkv4(p, row, t, head * D + i);
+    const bf16x4 b = load_qkv4(p, row, t, head * D + half + i);
     bf16x4 oa = a, ob = b;
     if (cs) rotate4(a, b, cs, i, half, oa, ob);
     if (head < p.nh) {
@@ -109,15 +131,16 @@ __global__ void __launch_bounds__(128) rope_cache_kernel(RopeCacheParams p) {
   // instruction touches 8 lines instead of 64
   if (slot >= 0 && h_hi > n_qk) {
     const int v_lo = max(h_lo - n_qk, 0) * D, v_hi = (h_hi - n_qk) * D;
-    const bf16* vsrc = row + (size_t)n_qk * D;
+    const int vcol = n_qk * D;
     const size_t grp = ((size_t)blk * p.nkv) * (p.bs >> 3) + (off >> 3);
     for (int it = v_lo + threadIdx.x; it < v_hi; it += blockDim.x) {
       const int kh = it / D, d = it % D;
       const size_t e = ((grp + (size_t)kh * (p.bs >> 3)) * D + d) * 8 + (off & 7);
+      const bf16 v = load_qkv1(p, row, t, vcol + it);
       if (FP8)
-        static_cast<uint8_t*>(p.v_cache)[e] = f32_to_fp8((float)vsrc[it] * p.v_inv_scale);
+        static_cast<uint8_t*>(p.v_cache)[e] = f32_to_fp8((float)v * p.v_inv_scale);
       else
-        static_cast<bf16*>(p.v_cache)[e] = vsrc[it];
+        static_cast<bf16*>(p.v_cache)[e] = v;
     }
   }
 }
@@ -125,6 +148,7 @@ __global__ void __launch_bounds__(128) rope_cache_kernel(RopeCacheParams p) {
 int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stream) {
   if (num_tokens == 0) return 0;
   if (p.D % 8 != 0 || p.qkv_stride % 4 != 0) return -1;
+  if (p.qkv_parts != nullptr && (p.splits < 1 || p.split_stride % 4 != 0)) return -2;
   const int heads = p.nh + 2 * p.nkv;
   dim3 grid(num_tokens, (heads + kHeadsPerWG - 1) / kHeadsPerWG);
   if (p.kv_fp8)

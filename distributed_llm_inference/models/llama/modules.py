@@ -74,7 +74,8 @@ class LlamaAttention(nn.Module):
 
     def forward(self, normed: Optional[torch.Tensor], meta: AttnMetadata, k_cache: torch.Tensor,
                 v_cache: torch.Tensor, cos_sin: torch.Tensor, x_q=None, defer_reduce: bool = False):
-        qkv = self.qkv_proj(normed, x_q)
+        # split-K partials of the QKV GEMM are summed inside the RoPE / KV-write kernel
+        qkv = self.qkv_proj(normed, x_q, defer_reduce=True)
         T = qkv.shape[0]
         q, q_sink = ops.rope_cache(qkv, meta.positions, meta.slot_mapping, cos_sin, self.num_heads,
                                    self.num_kv_heads, self.head_dim, k_cache, v_cache,

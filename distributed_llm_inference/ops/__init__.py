@@ -147,7 +147,18 @@ def rope_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
                q_sink_out: Optional[torch.Tensor] = None, k_scale: float = 1.0,
                v_scale: float = 1.0):
     """Rotate q/k, write k/v to the paged cache; returns ``(q [T, nh, D], q_sink or None)``.
-    fp8 (e4m3fn) caches store ``k / k_scale`` and ``v / v_scale``."""
+    fp8 (e4m3fn) caches store ``k / k_scale`` and ``v / v_scale``.  ``qkv`` may be
+    :class:`SplitKPartials` (summed while loaded, bit-identical to the reduce pass)."""
+    if isinstance(qkv, SplitKPartials):
+        T = qkv.shape[0]
+        if q_out is None:
+            q_out = torch.empty(T, nh, head_dim, dtype=torch.bfloat16, device=qkv.device)
+        if want_sink and q_sink_out is None:
+            q_sink_out = torch.empty_like(q_out)
+        native().rope_cache(qkv.parts, positions, slot_mapping, cos_sin, q_out,
+                            q_sink_out if want_sink else None, int(window), k_cache, v_cache,
+                            int(nh), int(nkv), float(k_scale), float(v_scale))
+        return q_out, (q_sink_out if want_sink else None)
     if not _gpu(qkv):
         q, qs = ref.rope_cache(qkv, positions, slot_mapping, cos_sin, nh, nkv, head_dim, k_cache,
                                v_cache, window, want_sink, k_scale, v_scale)

@@ -84,6 +84,31 @@ def test_rope_cache(gpu, nh, nkv, D, window):
     _close(v1, v2, 0.0, 0.0, "v_cache")
 
 
+@pytest.mark.parametrize("nh,nkv,D,S", [(64, 8, 128, 3), (4, 2, 32, 2)])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_rope_cache_from_splitk_partials_bit_identical(gpu, nh, nkv, D, S, fp8):
+    """qkv given as un-reduced fp32 split-K partials == reduce pass, then rope_cache."""
+    torch.manual_seed(4)
+    T, bs, nblocks = 29, 64, 8
+    parts = torch.randn(S, T, (nh + 2 * nkv) * D, device=gpu)
+    pos = torch.randint(0, 300, (T,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(nblocks * bs, device=gpu)[:T].to(torch.int64)
+    slots[5] = -1
+    cs = ref.build_cos_sin(D, 512, 500000.0, device=gpu)
+    k1, v1 = _make_cache(nblocks, nkv, bs, D, gpu)
+    if fp8:
+        k1, v1 = k1.to(torch.float8_e4m3fn), v1.to(torch.float8_e4m3fn)
+    k2, v2 = k1.clone(), v1.clone()
+    qkv = ops.SplitKPartials(parts).materialize()
+    q1, qs1 = ops.rope_cache(qkv, pos, slots, cs, nh, nkv, D, k1, v1, window=100, want_sink=True,
+                             k_scale=0.5, v_scale=0.25)
+    q2, qs2 = ops.rope_cache(ops.SplitKPartials(parts), pos, slots, cs, nh, nkv, D, k2, v2,
+                             window=100, want_sink=True, k_scale=0.5, v_scale=0.25)
+    assert torch.equal(q1, q2) and torch.equal(qs1, qs2)
+    assert torch.equal(k1.view(torch.uint8), k2.view(torch.uint8))
+    assert torch.equal(v1.view(torch.uint8), v2.view(torch.uint8))
+
+
 def _tables(B, max_blocks, nblocks, dev, seed=0):
     g = torch.Generator().manual_seed(seed)
     perm = torch.randperm(nblocks, generator=g)[: B * max_blocks]
