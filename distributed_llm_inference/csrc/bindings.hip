@@ -390,21 +390,29 @@ void sample(Tensor out_tokens, optional<Tensor> out_logprobs, Tensor logits,
 // ------------------------------------------------------------------------------ fp8 quant
 void quant_rowwise(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> residual,
                    optional<Tensor> norm_w, double eps, optional<Tensor> residual_out) {
-  CHECK_IN(q_out); CHECK_IN(scale); CHECK_IN(x); CHECK_BF16(x); CHECK_F32(scale);
+  CHECK_IN(q_out); CHECK_IN(scale); CHECK_IN(x); CHECK_F32(scale);
+  // x: bf16 [rows, K], or fp32 split-K partials [S, rows, K] (summed on load)
+  const bool parts = x.scalar_type() == at::kFloat;
+  if (parts) {
+    TORCH_CHECK(x.dim() == 3, "quant: partials must be [S, rows, K]");
+  } else {
+    CHECK_BF16(x);
+  }
   TORCH_CHECK(q_out.element_size() == 1, "q_out must be an 8-bit tensor");
   const int64_t K = x.size(-1);
-  const int64_t rows = x.numel() / K;
-  TORCH_CHECK(q_out.numel() == x.numel() && scale.numel() == rows, "quant: shape mismatch");
+  const int64_t n = parts ? x.numel() / x.size(0) : x.numel();
+  const int64_t rows = n / K;
+  TORCH_CHECK(q_out.numel() == n && scale.numel() == rows, "quant: shape mismatch");
   const dli::bf16* ri = nullptr;
   dli::bf16* ro = nullptr;
   if (residual.has_value()) {
     CHECK_IN(*residual); CHECK_BF16(*residual);
-    TORCH_CHECK(residual->numel() == x.numel(), "quant: residual shape mismatch");
+    TORCH_CHECK(residual->numel() == n, "quant: residual shape mismatch");
     ri = bp(*residual);
     ro = bp(*residual);
     if (residual_out.has_value()) {
       CHECK_IN(*residual_out); CHECK_BF16(*residual_out);
-      TORCH_CHECK(residual_out->numel() == x.numel(), "quant: residual_out shape mismatch");
+      TORCH_CHECK(residual_out->numel() == n, "quant: residual_out shape mismatch");
       ro = bp(*residual_out);
     }
   }
@@ -416,8 +424,10 @@ void quant_rowwise(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> residu
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_rc(dli::launch_quant_rowwise(reinterpret_cast<uint8_t*>(q_out.data_ptr()),
-                                     scale.data_ptr<float>(), bp(x), ri, ro, w, (float)eps,
-                                     (int)rows, (int)K, cur_stream()),
+                                     scale.data_ptr<float>(), parts ? nullptr : bp(x), ri, ro, w,
+                                     (float)eps, (int)rows, (int)K, cur_stream(),
+                                     parts ? x.data_ptr<float>() : nullptr,
+                                     parts ? (int)x.size(0) : 0),
            "quant_rowwise");
 }
 

@@ -41,6 +41,69 @@ __device__ __forceinline__ T wave_reduce_max(T v) {
 }
 
 // Block-wide sum of one float per thread.  `scratch` must hold >= blockDim.x/64 floats.
+// Split-K partials consumed in place of a reduce pass (gemm_tile.hip kStoreF32 slabs).  NS
+// partials of N consecutive fp32 elements, all loads issued before the adds (NS is a compile-time
+// count so they are independent and in flight together), summed in split order 0..NS-1 and
+// rounded to bf16 once: bit-identical to tile_splitk_reduce_kernel.
+template <int NS>
+__device__ __forceinline__ void sum_parts8(const float* p, size_t stride, bf16x8& out) {
+  f32x4 a[NS], b[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    a[k] = *reinterpret_cast<const f32x4*>(p + k * stride);
+    b[k] = *reinterpret_cast<const f32x4*>(p + k * stride + 4);
+  }
+  f32x4 s0 = a[0], s1 = b[0];
+#pragma unroll
+  for (int k = 1; k < NS; ++k) {
+    s0 += a[k];
+    s1 += b[k];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    out[j] = (bf16)s0[j];
+    out[j + 4] = (bf16)s1[j];
+  }
+}
+
+template <int NS>
+__device__ __forceinline__ void sum_parts4(const float* p, size_t stride, bf16x4& out) {
+  f32x4 a[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) a[k] = *reinterpret_cast<const f32x4*>(p + k * stride);
+  f32x4 s = a[0];
+#pragma unroll
+  for (int k = 1; k < NS; ++k) s += a[k];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) out[j] = (bf16)s[j];
+}
+
+template <int NS>
+__device__ __forceinline__ bf16 sum_parts1(const float* p, size_t stride) {
+  float a[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) a[k] = p[k * stride];
+  float s = a[0];
+#pragma unroll
+  for (int k = 1; k < NS; ++k) s += a[k];
+  return (bf16)s;
+}
+
+// dispatch a runtime split count 1..8 to a compile-time NS (0 = no partials)
+#define DLI_SPLITS_SWITCH(splits, MACRO) \
+  switch (splits) {                      \
+    case 0: MACRO(0); break;             \
+    case 1: MACRO(1); break;             \
+    case 2: MACRO(2); break;             \
+    case 3: MACRO(3); break;             \
+    case 4: MACRO(4); break;             \
+    case 5: MACRO(5); break;             \
+    case 6: MACRO(6); break;             \
+    case 7: MACRO(7); break;             \
+    case 8: MACRO(8); break;             \
+    default: return -2;                  \
+  }
+
 __device__ __forceinline__ float block_reduce_sum(float v, float* scratch) {
   v = wave_reduce_sum(v);
   const int nw = blockDim.x >> 6;

@@ -88,7 +88,7 @@ int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, 
                        int K, hipStream_t stream);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
                          bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,
-                         hipStream_t stream);
+                         hipStream_t stream, const float* x_parts = nullptr, int splits = 0);
 int launch_quant_rowwise_int8(int8_t* q, float* scale, const bf16* x, const uint8_t* outlier,
                               int rows, int K, hipStream_t stream);
 int launch_silu_mul_quant(uint8_t* q, float* scale, const bf16* x, int rows, int inter,

@@ -16,14 +16,14 @@ namespace dli {
 // of the tile GEMM that produced it (gemm_tile.hip kStoreF32); they are summed and rounded to bf16
 // here, exactly as tile_splitk_reduce_kernel would, so the reduction pass and its bf16 round trip
 // through HBM disappear while the numerics stay bit-identical.
-template <int VPT>  // bf16x8 vectors per thread
+template <int VPT, int NS>  // bf16x8 vectors per thread; NS > 0: x is NS fp32 partials
 __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
                                                        const bf16* __restrict__ x,
                                                        const bf16* residual_in, bf16* residual_out,
                                                        const bf16* __restrict__ w, float eps,
                                                        int hidden, int add_residual,
                                                        const float* __restrict__ x_parts,
-                                                       int splits, size_t split_stride) {
+                                                       size_t split_stride) {
   __shared__ float scratch[8];
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
@@ -42,22 +42,10 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
     if (idx < nvec) {
       wv[i] = wr[idx];
       bf16x8 a;
-      if (x_parts != nullptr) {
-        const float* pp = x_parts + (size_t)row * hidden + (size_t)idx * 8;
-        f32x4 s0 = *reinterpret_cast<const f32x4*>(pp);
-        f32x4 s1 = *reinterpret_cast<const f32x4*>(pp + 4);
-        for (int k = 1; k < splits; ++k) {
-          s0 += *reinterpret_cast<const f32x4*>(pp + k * split_stride);
-          s1 += *reinterpret_cast<const f32x4*>(pp + k * split_stride + 4);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a[j] = (bf16)s0[j];
-          a[j + 4] = (bf16)s1[j];
-        }
-      } else {
+      if constexpr (NS > 0)
+        sum_parts8<NS>(x_parts + (size_t)row * hidden + (size_t)idx * 8, split_stride, a);
+      else
         a = xr[idx];
-      }
       if (add_residual) {
         bf16x8 r = ri[idx];
         bf16x8 s;
@@ -69,7 +57,7 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         v[i][j] = (float)a[j];
-        ss += v[i][j] * v[i][j];
+        ss = __builtin_fmaf(v[i][j], v[i][j], ss);   // explicit: same rounding in every instantiation
       }
     } else {
 #pragma unroll
@@ -190,8 +178,24 @@ int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* res
   if (x_parts != nullptr && splits < 1) return -2;
   const int add = residual_in != nullptr ? 1 : 0;
   const size_t stride = (size_t)rows * hidden;
-  DLI_NORM_DISPATCH(rms_norm_kernel, out, x, residual_in, residual_out, w, eps, hidden, add,
-                    x_parts, splits, stride);
+  const int ns = x_parts != nullptr ? splits : 0;
+#define DLI_RMS(NS)                                                                          \
+  do {                                                                                       \
+    const int nvec = hidden / 8;                                                             \
+    const int threads = norm_threads(hidden);                                                \
+    const int vpt = (nvec + threads - 1) / threads;                                          \
+    if (vpt <= 1) rms_norm_kernel<1, NS><<<rows, threads, 0, stream>>>(                      \
+        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride);           \
+    else if (vpt <= 2) rms_norm_kernel<2, NS><<<rows, threads, 0, stream>>>(                 \
+        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride);           \
+    else if (vpt <= 4) rms_norm_kernel<4, NS><<<rows, threads, 0, stream>>>(                 \
+        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride);           \
+    else if (vpt <= 8) rms_norm_kernel<8, NS><<<rows, threads, 0, stream>>>(                 \
+        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride);           \
+    else return -1;                                                                          \
+  } while (0)
+  DLI_SPLITS_SWITCH(ns, DLI_RMS)
+#undef DLI_RMS
   return 0;
 }
 

@@ -45,11 +45,13 @@ __device__ __forceinline__ void store_fp8_row(float (&v)[VPT][8], uint8_t* __res
 // If `residual_in` is given, x + residual_in is quantised and also written to `residual_out`
 // (which may alias residual_in; like rms_norm_kernel).  If `norm_w` is given the row is
 // RMS-normalised first, so "add residual -> RMSNorm -> fp8" is one HBM pass.
-template <int VPT>
+// x_parts (optional): x given as fp32 split-K partials [splits, rows, K] of the tile GEMM that
+// produced it, summed and rounded to bf16 on load (bit-identical to the reduce pass).
+template <int VPT, int NS>
 __global__ void __launch_bounds__(256) quant_rowwise_kernel(
     uint8_t* __restrict__ q, float* __restrict__ scale, const bf16* __restrict__ x,
     const bf16* residual_in, bf16* residual_out, const bf16* __restrict__ norm_w, float eps,
-    int K) {
+    int K, const float* __restrict__ x_parts, size_t split_stride) {
   __shared__ float scratch[8];
   const int row = blockIdx.x;
   const int nvec = K >> 3;
@@ -66,7 +68,11 @@ __global__ void __launch_bounds__(256) quant_rowwise_kernel(
     const int idx = threadIdx.x + i * blockDim.x;
     if (idx < nvec) {
       if (norm_w) wv[i] = wr[idx];
-      bf16x8 a = xr[idx];
+      bf16x8 a;
+      if constexpr (NS > 0)
+        sum_parts8<NS>(x_parts + (size_t)row * K + (size_t)idx * 8, split_stride, a);
+      else
+        a = xr[idx];
       if (add_residual) {
         bf16x8 r = ri[idx];
 #pragma unroll
@@ -76,7 +82,7 @@ __global__ void __launch_bounds__(256) quant_rowwise_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         v[i][j] = (float)a[j];
-        ss += v[i][j] * v[i][j];
+        ss = __builtin_fmaf(v[i][j], v[i][j], ss);   // explicit: same rounding in every instantiation
       }
     } else {
 #pragma unroll
@@ -202,23 +208,32 @@ int launch_quant_rowwise_int8(int8_t* q, float* scale, const bf16* x, const uint
 
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
                          bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,
-                         hipStream_t stream) {
+                         hipStream_t stream, const float* x_parts, int splits) {
   if (K % 8 != 0) return -1;
+  if (x_parts != nullptr && splits < 1) return -3;
+  const size_t split_stride = (size_t)rows * K;
   if (residual_in != nullptr && residual_out == nullptr) return -2;
   if (rows == 0) return 0;
   const int nvec = K / 8;
   int threads = ((nvec + 63) / 64) * 64;
   if (threads > 256) threads = 256;
   const int vpt = (nvec + threads - 1) / threads;
-#define DLI_QUANT(V) \
-  quant_rowwise_kernel<V><<<rows, threads, 0, stream>>>(q, scale, x, residual_in, residual_out, \
-                                                        norm_w, eps, K)
-  if (vpt <= 1) DLI_QUANT(1);
-  else if (vpt <= 2) DLI_QUANT(2);
-  else if (vpt <= 4) DLI_QUANT(4);
-  else if (vpt <= 8) DLI_QUANT(8);
-  else if (vpt <= 16) DLI_QUANT(16);
-  else return -1;
+  const int ns = x_parts != nullptr ? splits : 0;
+#define DLI_QUANT(V, NS)                                                                    \
+  quant_rowwise_kernel<V, NS><<<rows, threads, 0, stream>>>(q, scale, x, residual_in,       \
+                                                            residual_out, norm_w, eps, K,   \
+                                                            x_parts, split_stride)
+#define DLI_QUANT_NS(NS)                       \
+  do {                                         \
+    if (vpt <= 1) DLI_QUANT(1, NS);            \
+    else if (vpt <= 2) DLI_QUANT(2, NS);       \
+    else if (vpt <= 4) DLI_QUANT(4, NS);       \
+    else if (vpt <= 8) DLI_QUANT(8, NS);       \
+    else if (vpt <= 16) DLI_QUANT(16, NS);     \
+    else return -1;                            \
+  } while (0)
+  DLI_SPLITS_SWITCH(ns, DLI_QUANT_NS)
+#undef DLI_QUANT_NS
 #undef DLI_QUANT
   return 0;
 }

@@ -28,32 +28,35 @@ __device__ __forceinline__ void rotate4(const bf16x4& a, const bf16x4& b, const 
   for (int j = 0; j < 4; ++j) {
     const float c = cs[i + j], s = cs[half + i + j];
     const float x = (float)a[j], y = (float)b[j];
-    oa[j] = (bf16)(x * c - y * s);
-    ob[j] = (bf16)(y * c + x * s);
+    // explicit fma: every instantiation (bf16 input, split-K partials) rounds identically,
+    // whatever contraction -ffp-contract=fast would pick per instantiation
+    oa[j] = (bf16)__builtin_fmaf(x, c, -(y * s));
+    ob[j] = (bf16)__builtin_fmaf(y, c, x * s);
   }
 }
 
 // 4 consecutive qkv elements of token row t starting at column c: from the bf16 GEMM output, or
-// summed over the fp32 split-K partials and rounded once (bit-identical to the reduce pass)
+// (NS > 0) summed over the NS fp32 split-K partials and rounded once (bit-identical to the
+// reduce pass)
+template <int NS>
 __device__ __forceinline__ bf16x4 load_qkv4(const RopeCacheParams& p, const bf16* row, int t,
                                             int c) {
-  if (p.qkv_parts == nullptr) return *reinterpret_cast<const bf16x4*>(row + c);
-  const float* q = p.qkv_parts + (size_t)t * p.qkv_stride + c;
-  f32x4 s = *reinterpret_cast<const f32x4*>(q);
-  for (int k = 1; k < p.splits; ++k) s += *reinterpret_cast<const f32x4*>(q + k * p.split_stride);
-  bf16x4 o;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = (bf16)s[j];
-  return o;
+  if constexpr (NS == 0) {
+    return *reinterpret_cast<const bf16x4*>(row + c);
+  } else {
+    bf16x4 o;
+    sum_parts4<NS>(p.qkv_parts + (size_t)t * p.qkv_stride + c, p.split_stride, o);
+    return o;
+  }
 }
 
+template <int NS>
 __device__ __forceinline__ bf16 load_qkv1(const RopeCacheParams& p, const bf16* row, int t,
                                           int c) {
-  if (p.qkv_parts == nullptr) return row[c];
-  const float* q = p.qkv_parts + (size_t)t * p.qkv_stride + c;
-  float s = q[0];
-  for (int k = 1; k < p.splits; ++k) s += q[k * p.split_stride];
-  return (bf16)s;
+  if constexpr (NS == 0)
+    return row[c];
+  else
+    return sum_parts1<NS>(p.qkv_parts + (size_t)t * p.qkv_stride + c, p.split_stride);
 }
 
 // grid (T, ceil(total_heads / kHeadsPerWG)): one workgroup per (token, group of 8 heads) so a
@@ -61,7 +64,7 @@ __device__ __forceinline__ bf16 load_qkv1(const RopeCacheParams& p, const bf16* 
 // latency-bound, not bandwidth-bound, at one workgroup per token.
 constexpr int kHeadsPerWG = 8;
 
-template <bool FP8>
+template <bool FP8, int NS>
 __global__ void __launch_bounds__(128) rope_cache_kernel(RopeCacheParams p) {
   const int t = blockIdx.x;
   const int h_lo = blockIdx.y * kHeadsPerWG;
@@ -93,8 +96,8 @@ __global__ void __launch_bounds__(128) rope_cache_kernel(RopeCacheParams p) {
   for (int it = rot_lo + threadIdx.x; it < rot_hi; it += blockDim.x) {
     const int head = it / gpr;
     const int i = (it % gpr) * 4;
-    const bf16x4 a = load_qkv4(p, row, t, head * D + i);
-    const bf16x4 b = load_qkv4(p, row, t, head * D + half + i);
+    const bf16x4 a = load_qkv4<NS>(p, row, t, head * D + i);
+    const bf16x4 b = load_qkv4<NS>(p, row, t, head * D + half + i);
     bf16x4 oa = a, ob = b;
     if (cs) rotate4(a, b, cs, i, half, oa, ob);
     if (head < p.nh) {
@@ -136,7 +139,7 @@ __global__ void __launch_bounds__(128) rope_cache_kernel(RopeCacheParams p) {
     for (int it = v_lo + threadIdx.x; it < v_hi; it += blockDim.x) {
       const int kh = it / D, d = it % D;
       const size_t e = ((grp + (size_t)kh * (p.bs >> 3)) * D + d) * 8 + (off & 7);
-      const bf16 v = load_qkv1(p, row, t, vcol + it);
+      const bf16 v = load_qkv1<NS>(p, row, t, vcol + it);
       if (FP8)
         static_cast<uint8_t*>(p.v_cache)[e] = f32_to_fp8((float)v * p.v_inv_scale);
       else
@@ -151,10 +154,16 @@ int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stre
   if (p.qkv_parts != nullptr && (p.splits < 1 || p.split_stride % 4 != 0)) return -2;
   const int heads = p.nh + 2 * p.nkv;
   dim3 grid(num_tokens, (heads + kHeadsPerWG - 1) / kHeadsPerWG);
-  if (p.kv_fp8)
-    rope_cache_kernel<true><<<grid, 128, 0, stream>>>(p);
-  else
-    rope_cache_kernel<false><<<grid, 128, 0, stream>>>(p);
+  const int ns = p.qkv_parts != nullptr ? p.splits : 0;
+#define DLI_ROPE(NS)                                               \
+  do {                                                             \
+    if (p.kv_fp8)                                                  \
+      rope_cache_kernel<true, NS><<<grid, 128, 0, stream>>>(p);    \
+    else                                                           \
+      rope_cache_kernel<false, NS><<<grid, 128, 0, stream>>>(p);   \
+  } while (0)
+  DLI_SPLITS_SWITCH(ns, DLI_ROPE)
+#undef DLI_ROPE
   return 0;
 }
 

@@ -99,7 +99,8 @@ class Linear(nn.Module):
         if xq.is_cuda and self.bias is None and xq.dim() == 2:
             sp = ops.tile_gemm_splits_fp8(xq.shape[0], self.out_features, self.in_features)
             if sp:  # long-K fp8 products: block-scaled MFMA tile kernel (csrc/kernels/gemm_tile.hip)
-                return ops.gemm_tile_fp8(xq, xs, self.weight_fp8, self.weight_scale, sp)
+                return ops.gemm_tile_fp8(xq, xs, self.weight_fp8, self.weight_scale, sp,
+                                         defer_reduce=defer_reduce)
         if xq.is_cuda:
             y = torch._scaled_mm(xq, self.weight_fp8.t(), scale_a=xs, scale_b=self.weight_scale,
                                  out_dtype=torch.bfloat16)

@@ -130,7 +130,7 @@ class LlamaMLP(nn.Module):
             return self.down_proj(h, defer_reduce=defer_reduce)
         gu = self.gate_up_proj(normed, x_q)
         if self.down_proj.is_fp8:  # SwiGLU fused with the fp8 quantisation of down_proj's input
-            return self.down_proj(None, ops.silu_mul_quant(gu))
+            return self.down_proj(None, ops.silu_mul_quant(gu), defer_reduce=defer_reduce)
         return self.down_proj(ops.silu_mul(gu), defer_reduce=defer_reduce)
 
 
@@ -153,7 +153,7 @@ class LlamaDecoderLayer(nn.Module):
         layer's input RMSNorm reduces them); the O projection's partials always go straight
         into the post-attention RMSNorm."""
         if self.self_attn.qkv_proj.is_fp8:
-            return self._forward_fp8(hidden, residual, meta, k_cache, v_cache, cos_sin)
+            return self._forward_fp8(hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out)
         first = residual is None
         if first:
             # first layer of the stage: the input IS the residual; never modify it in place (it
@@ -167,7 +167,7 @@ class LlamaDecoderLayer(nn.Module):
             attn, residual, residual_out=torch.empty_like(residual) if first else None)
         return self.mlp(normed, defer_reduce=defer_out), residual
 
-    def _forward_fp8(self, hidden, residual, meta, k_cache, v_cache, cos_sin):
+    def _forward_fp8(self, hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out=False):
         """fp8 weights: every RMSNorm is fused with the fp8 quantisation of the GEMM input that
         follows it (quant.hip), so the bf16 normalised activation never touches HBM."""
         ln1, ln2 = self.input_layernorm, self.post_attention_layernorm
@@ -180,7 +180,8 @@ class LlamaDecoderLayer(nn.Module):
         attn = self.self_attn(None, meta, k_cache, v_cache, cos_sin, x_q=xq)
         res_out = torch.empty_like(residual) if first else residual
         xq = ops.quant_rowwise(attn, residual, ln2.weight, ln2.eps, residual_out=res_out)
-        return self.mlp(None, x_q=xq), res_out
+        # defer_out: the down projection's split-K partials go into the next layer's quantiser
+        return self.mlp(None, x_q=xq, defer_reduce=defer_out), res_out
 
     # ------------------------------------------------------------------ weights
     def load_hf_state_dict(self, sd: dict) -> None:

@@ -279,7 +279,13 @@ def quant_rowwise(x: torch.Tensor, residual: Optional[torch.Tensor] = None,
     """Per-row dynamic fp8-e4m3 quantisation, optionally of ``RMSNorm(x + residual)``.
 
     With ``residual`` the sum ``x + residual`` is written back to ``residual_out`` (default: in
-    place into ``residual``) exactly like :func:`rms_norm`.  Returns ``(q, scale[rows, 1])``."""
+    place into ``residual``) exactly like :func:`rms_norm`.  Returns ``(q, scale[rows, 1])``.
+    ``x`` may be :class:`SplitKPartials` (summed on load)."""
+    if isinstance(x, SplitKPartials):
+        q = torch.empty(x.shape, dtype=FP8, device=x.device)
+        s = torch.empty(x.shape[0], 1, dtype=torch.float32, device=x.device)
+        native().quant_rowwise(q, s, x.parts, residual, norm_w, float(eps), residual_out)
+        return q, s
     K = x.shape[-1]
     rows = x.numel() // K
     if not _gpu(x):
@@ -515,11 +521,19 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
 
 def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
                   splits: int = 1, swiglu: bool = False, out: Optional[torch.Tensor] = None,
-                  workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  workspace: Optional[torch.Tensor] = None, defer_reduce: bool = False):
     """fp8 e4m3 tile GEMM: ``(xq [M, K] @ wq[N, K]^T) * xs[M] * ws[N]`` -> bf16, on the
     block-scaled K=128 MFMA (2x the bf16 MFMA rate; unit block scales, per-row / per-channel
-    scales applied in the epilogue).  ``swiglu``: ``wq`` / ``ws`` rows in swiglu_interleave order."""
+    scales applied in the epilogue).  ``swiglu``: ``wq`` / ``ws`` rows in swiglu_interleave order.
+    ``defer_reduce`` (split-K): return :class:`SplitKPartials` (scaled fp32 partials)."""
     M, N = xq.shape[0], wq.shape[0]
+    if (defer_reduce and splits > 1 and _gpu(xq) and not swiglu
+            and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
+        parts = torch.empty(splits, M, N, dtype=torch.float32, device=xq.device)
+        dummy = torch.empty(M, 0, dtype=torch.bfloat16, device=xq.device)   # C is unused
+        native().gemm_tile(dummy, xq, wq, int(splits), 1, parts.view(-1),
+                           xs.reshape(-1).contiguous(), ws.reshape(-1).contiguous())
+        return SplitKPartials(parts)
     if not _gpu(xq):
         h = (xq.float() * xs.reshape(-1, 1).float()) @ (wq.float() * ws.reshape(-1, 1).float()).t()
         if swiglu:

@@ -219,3 +219,17 @@ def test_deferred_splitk_reduce_is_bit_identical(gpu, monkeypatch):
     monkeypatch.setenv("DLI_SPLITK_DEFER", "0")
     b = _stage_logits(g, prompts, 0)[0]
     assert torch.equal(a, b)
+
+
+def test_deferred_splitk_reduce_is_bit_identical_fp8(gpu, monkeypatch):
+    """fp8 weights: the long-K down projection (fp8 tile GEMM, split-K) hands its partials to the
+    next layer's fused RMSNorm + fp8 quantiser; bit-identical to the separate reduce pass."""
+    spec = SPEC.replace(hidden_size=512, intermediate_size=16384, num_heads=4, num_kv_heads=2,
+                        head_dim=128)
+    g = CausalLMStage(spec, 0, 3, device=gpu).init_random(6)
+    g.quantize_fp8()
+    prompts = [list(range(1, 200)), list(range(3, 150))]
+    a = _stage_logits(g, prompts, 0)[0]
+    monkeypatch.setenv("DLI_SPLITK_DEFER", "0")
+    b = _stage_logits(g, prompts, 0)[0]
+    assert torch.equal(a, b)

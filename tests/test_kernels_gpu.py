@@ -363,3 +363,18 @@ def test_attn_prefill_fp8_kv(gpu):
     out_r = ref.attn_prefill(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale,
                              k_scale=ks, v_scale=vs)
     _close(out, out_r, 2e-2, 2e-2, "prefill-fp8")
+
+
+@pytest.mark.parametrize("S,rows,K", [(4, 512, 8192), (3, 33, 1024)])
+@pytest.mark.parametrize("with_norm", [False, True])
+def test_quant_rowwise_from_splitk_partials_bit_identical(gpu, S, rows, K, with_norm):
+    torch.manual_seed(S + rows)
+    parts = torch.randn(S, rows, K, device=gpu)
+    res = torch.randn(rows, K, device=gpu, dtype=BF)
+    w = torch.randn(K, device=gpu, dtype=BF) if with_norm else None
+    x = ops.SplitKPartials(parts).materialize()
+    r1, r2 = res.clone(), res.clone()
+    q1, s1 = ops.quant_rowwise(x, r1, w, 1e-5)
+    q2, s2 = ops.quant_rowwise(ops.SplitKPartials(parts), r2, w, 1e-5)
+    assert torch.equal(q1.view(torch.uint8), q2.view(torch.uint8))
+    assert torch.equal(s1, s2) and torch.equal(r1, r2)
