@@ -248,7 +248,7 @@ def _mp_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_multiprocess_pipeline_gloo(world):
     ref = [s.output for s in LLMEngine(SPEC, cfg=_cfg()).generate(
         PROMPTS, SamplingParams(max_tokens=6, ignore_eos=True))]
