@@ -151,7 +151,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": ("fp8-weights/bf16-act" if a.fp8 else "bf16") + ("/fp8-kv" if a.kv_fp8 else ""),
-        "data": "synthetic (random-init Llama-3-70B weights, random prompt tokens)",
+        "data": f"synthetic (random-init {spec.name} weights, random prompt tokens)",
         "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
                    "global_batch": G, "seq_len": total_len,
                    "parallelism": f"pp{a.gpus}"},

@@ -1,0 +1,46 @@
+"""bench.py's driver contract on the multi-rank path (torchrun, one process per stage), exercised
+on the CPU with a tiny Llama so it runs here: ONE JSON line from rank 0 with the required fields,
+every in-flight sequence decoding one token per timed step, the max-over-ranks timing."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+            "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_multirank_json_contract(n):
+    steps, warmup, bpm = 3, 1, 4
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", str(steps),
+           "--warmup", str(warmup), "--model", "tiny-llama", "--batch-per-mb", str(bpm),
+           "--prompt-len", "16", "--max-batched-tokens", "64"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in REQUIRED:
+        assert k in d, k
+    assert d["n_gpus"] == n and d["steps"] == steps and d["warmup"] == warmup
+    assert d["config"]["parallelism"] == f"pp{n}" and d["scaling"] == "weak"
+    assert d["micro_batches"] == n + 1
+    G = d["config"]["global_batch"]
+    assert G == (n + 1) * bpm and d["tokens_timed"] == steps * G
+    assert abs(d["value"] - d["tokens_timed"] / (d["ms_per_step"] * steps / 1e3)) < 0.02 * d["value"]
