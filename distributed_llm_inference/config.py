@@ -44,6 +44,16 @@ class ModelSpec:
     attention_bias: bool = False
     mlp_bias: bool = False
     name: str = "custom"
+    # Llama-family variants: "llama" | "mistral" | "qwen2" (the HF model_type)
+    model_type: str = "llama"
+    # bias on o_proj; None = same as attention_bias (Llama).  Qwen2 has q/k/v bias only.
+    o_proj_bias: Optional[bool] = None
+    # Mistral-style sliding-window attention length (None = full causal attention)
+    sliding_window: Optional[int] = None
+
+    @property
+    def has_o_proj_bias(self) -> bool:
+        return self.attention_bias if self.o_proj_bias is None else self.o_proj_bias
 
     # ------------------------------------------------------------------ derived
     @property
@@ -125,8 +135,13 @@ class ModelSpec:
                 mlp_bias=True,
                 name=cfg.get("_name_or_path", "gpt2") or "gpt2",
             )
-        if mt not in ("llama", "mistral"):
-            raise ValueError(f"unsupported model_type {mt!r} (supported: llama, gpt2)")
+        if mt not in ("llama", "mistral", "qwen2"):
+            raise ValueError(f"unsupported model_type {mt!r} (supported: llama, mistral, qwen2, gpt2)")
+        # Qwen2: q/k/v projections always carry a bias, o_proj never does (no config key)
+        qwen2 = mt == "qwen2"
+        sw = cfg.get("sliding_window")
+        if qwen2 and not cfg.get("use_sliding_window", False):
+            sw = None
         nh = cfg["num_attention_heads"]
         h = cfg["hidden_size"]
         # transformers 4.x: rope_theta + rope_scaling; transformers 5.x: rope_parameters
@@ -158,9 +173,12 @@ class ModelSpec:
             eos_token_id=eos,
             hidden_act=cfg.get("hidden_act", "silu"),
             pretraining_tp=cfg.get("pretraining_tp", 1) or 1,
-            attention_bias=bool(cfg.get("attention_bias", False)),
+            attention_bias=True if qwen2 else bool(cfg.get("attention_bias", False)),
             mlp_bias=bool(cfg.get("mlp_bias", False)),
-            name=cfg.get("_name_or_path", "llama") or "llama",
+            name=cfg.get("_name_or_path", mt) or mt,
+            model_type=mt,
+            o_proj_bias=False if qwen2 else None,
+            sliding_window=int(sw) if sw else None,
         )
 
     def to_hf_dict(self) -> Dict[str, Any]:
@@ -173,8 +191,17 @@ class ModelSpec:
                 activation_function=self.hidden_act, bos_token_id=self.bos_token_id,
                 eos_token_id=self.eos_token_id,
             )
+        arch_name = {"llama": "LlamaForCausalLM", "mistral": "MistralForCausalLM",
+                     "qwen2": "Qwen2ForCausalLM"}[self.model_type]
+        extra: Dict[str, Any] = {}
+        if self.model_type == "mistral":
+            extra["sliding_window"] = self.sliding_window
+        if self.model_type == "qwen2":
+            extra.update(use_sliding_window=self.sliding_window is not None,
+                         sliding_window=self.sliding_window)
         return dict(
-            model_type="llama", architectures=["LlamaForCausalLM"], vocab_size=self.vocab_size,
+            extra, model_type=self.model_type, architectures=[arch_name],
+            vocab_size=self.vocab_size,
             hidden_size=self.hidden_size, intermediate_size=self.intermediate_size,
             num_hidden_layers=self.num_layers, num_attention_heads=self.num_heads,
             num_key_value_heads=self.num_kv_heads, head_dim=self.head_dim,
@@ -211,6 +238,16 @@ PRESETS: Dict[str, ModelSpec] = {
         rope_theta=0.0, max_position_embeddings=1024, tie_word_embeddings=True,
         bos_token_id=50256, eos_token_id=50256, hidden_act="gelu_new", attention_bias=True,
         mlp_bias=True),
+    "mistral-7b": ModelSpec(
+        name="mistral-7b", model_type="mistral", vocab_size=32000, hidden_size=4096,
+        intermediate_size=14336, num_layers=32, num_heads=32, num_kv_heads=8, head_dim=128,
+        rms_norm_eps=1e-5, rope_theta=10000.0, max_position_embeddings=32768, bos_token_id=1,
+        eos_token_id=2, sliding_window=4096),
+    "qwen2-7b": ModelSpec(
+        name="qwen2-7b", model_type="qwen2", vocab_size=152064, hidden_size=3584,
+        intermediate_size=18944, num_layers=28, num_heads=28, num_kv_heads=4, head_dim=128,
+        rms_norm_eps=1e-6, rope_theta=1000000.0, max_position_embeddings=32768,
+        bos_token_id=151643, eos_token_id=151645, attention_bias=True, o_proj_bias=False),
     # tiny configs for CPU tests / smoke
     "tiny-llama": ModelSpec(
         name="tiny-llama", vocab_size=512, hidden_size=128, intermediate_size=256, num_layers=4,

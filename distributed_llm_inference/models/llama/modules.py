@@ -69,7 +69,7 @@ class LlamaAttention(nn.Module):
         self.scale = spec.head_dim ** -0.5
         self.qkv_proj = Linear(spec.hidden_size, spec.qkv_size, bias=spec.attention_bias,
                                dtype=dtype, device=device)
-        self.o_proj = Linear(spec.q_size, spec.hidden_size, bias=spec.attention_bias, dtype=dtype,
+        self.o_proj = Linear(spec.q_size, spec.hidden_size, bias=spec.has_o_proj_bias, dtype=dtype,
                              device=device)
 
     def forward(self, normed: Optional[torch.Tensor], meta: AttnMetadata, k_cache: torch.Tensor,
@@ -197,17 +197,21 @@ class LlamaDecoderLayer(nn.Module):
                              g("self_attn.v_proj.weight")], 0)
             self.self_attn.qkv_proj.weight.copy_(qkv.to(dt))
             self.self_attn.o_proj.weight.copy_(g("self_attn.o_proj.weight").to(dt))
-            if self.self_attn.qkv_proj.bias is not None:
+            if self.self_attn.qkv_proj.bias is not None:   # Llama attention_bias, Qwen2
                 self.self_attn.qkv_proj.bias.copy_(torch.cat(
                     [g("self_attn.q_proj.bias"), g("self_attn.k_proj.bias"),
                      g("self_attn.v_proj.bias")], 0).to(dt))
-                if "self_attn.o_proj.bias" in sd:
-                    self.self_attn.o_proj.bias.copy_(sd["self_attn.o_proj.bias"].to(dt))
+            if self.self_attn.o_proj.bias is not None:     # Llama attention_bias (not Qwen2)
+                self.self_attn.o_proj.bias.copy_(g("self_attn.o_proj.bias").to(dt))
             gu = torch.cat([g("mlp.gate_proj.weight"), g("mlp.up_proj.weight")], 0)
             if self.mlp.fused_swiglu:
                 gu = ops.swiglu_interleave(gu)
             self.mlp.gate_up_proj.weight.copy_(gu.to(dt))
             self.mlp.down_proj.weight.copy_(g("mlp.down_proj.weight").to(dt))
+            if self.mlp.gate_up_proj.bias is not None:     # Llama mlp_bias
+                self.mlp.gate_up_proj.bias.copy_(torch.cat(
+                    [g("mlp.gate_proj.bias"), g("mlp.up_proj.bias")], 0).to(dt))
+                self.mlp.down_proj.bias.copy_(g("mlp.down_proj.bias").to(dt))
             self.input_layernorm.weight.copy_(g("input_layernorm.weight").to(dt))
             self.post_attention_layernorm.weight.copy_(g("post_attention_layernorm.weight").to(dt))
 
@@ -221,7 +225,7 @@ class LlamaDecoderLayer(nn.Module):
         if m.fused_swiglu:
             gu = ops.swiglu_deinterleave(gu)
         gate, up = gu.split([m.intermediate_size, m.intermediate_size], 0)
-        return {
+        sd = {
             "self_attn.q_proj.weight": q, "self_attn.k_proj.weight": k,
             "self_attn.v_proj.weight": v, "self_attn.o_proj.weight": a.o_proj.weight,
             "mlp.gate_proj.weight": gate, "mlp.up_proj.weight": up,
@@ -229,3 +233,16 @@ class LlamaDecoderLayer(nn.Module):
             "input_layernorm.weight": self.input_layernorm.weight,
             "post_attention_layernorm.weight": self.post_attention_layernorm.weight,
         }
+        if a.qkv_proj.bias is not None:
+            qb, kb, vb = a.qkv_proj.bias.split([a.num_heads * a.head_dim,
+                                                a.num_kv_heads * a.head_dim,
+                                                a.num_kv_heads * a.head_dim], 0)
+            sd.update({"self_attn.q_proj.bias": qb, "self_attn.k_proj.bias": kb,
+                       "self_attn.v_proj.bias": vb})
+        if a.o_proj.bias is not None:
+            sd["self_attn.o_proj.bias"] = a.o_proj.bias
+        if m.gate_up_proj.bias is not None:
+            gb, ub = m.gate_up_proj.bias.split([m.intermediate_size, m.intermediate_size], 0)
+            sd.update({"mlp.gate_proj.bias": gb, "mlp.up_proj.bias": ub,
+                       "mlp.down_proj.bias": m.down_proj.bias})
+        return sd

@@ -96,7 +96,13 @@ def build_executor(spec: ModelSpec, start: int, end: int, device: torch.device, 
         t = torch.tensor([num_blocks], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
         num_blocks = int(t.item())
-    pool = stage.make_pool(num_blocks, cc.block_size, cc.window_length, cc.num_sink_tokens,
+    win, sinks = cc.window_length, cc.num_sink_tokens
+    if not win and spec.sliding_window and sc.max_seq_len > spec.sliding_window:
+        # Mistral-style sliding-window attention IS the ring window with no sink tokens (each
+        # query sees itself and the W-1 keys before it, at their true relative positions;
+        # tests/test_model_parity_cpu.py::test_mistral_sliding_window_matches_hf_beyond_window)
+        win, sinks = spec.sliding_window, 0
+    pool = stage.make_pool(num_blocks, cc.block_size, win, sinks,
                            cc.max_chunk, cc.torch_dtype, cc.k_scale, cc.v_scale)
     log.info("stage [%d,%d) on %s: %d KV blocks x %d tokens", start, end, device, num_blocks,
              cc.block_size)

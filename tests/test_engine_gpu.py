@@ -233,3 +233,35 @@ def test_deferred_splitk_reduce_is_bit_identical_fp8(gpu, monkeypatch):
     monkeypatch.setenv("DLI_SPLITK_DEFER", "0")
     b = _stage_logits(g, prompts, 0)[0]
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("preset", ["qwen2-7b", "mistral-7b"])
+def test_llama_family_variants_gpu_match_cpu(gpu, preset):
+    """Qwen2 (q/k/v bias, GQA group 7, hidden 3584) and Mistral (sliding window) shapes on the
+    HIP kernels vs the CPU reference path, 2 real-size layers, prefill + sliding-window decode."""
+    from distributed_llm_inference.config import PRESETS
+    spec = PRESETS[preset].replace(num_layers=2, vocab_size=4096)
+    if spec.sliding_window:
+        spec = spec.replace(sliding_window=64)
+    cpu = CausalLMStage(spec, 0, 2).init_random(7)
+    with torch.no_grad():
+        for n, p in cpu.named_parameters():
+            if n.endswith(".bias"):
+                p.normal_(0, 0.5)
+    g = CausalLMStage(spec, 0, 2, device=gpu)
+    g.load_state_dict({k: v.to(gpu) for k, v in cpu.state_dict().items()})
+    prompts = [list(range(1, 90)), [5, 6, 7]]
+
+    def run(stage):
+        pool = stage.make_pool(64, block_size=64, window_length=spec.sliding_window or 0)
+        sids = [0, 1]
+        for s, p in zip(sids, prompts):
+            pool.manager.append(s, len(p))
+        meta = pool.build_metadata(sids, [len(p) for p in prompts])
+        meta.logits_rows = (torch.cumsum(torch.tensor([len(p) for p in prompts]), 0) - 1).to(stage.device)
+        ids = torch.tensor([t for p in prompts for t in p], dtype=torch.int32, device=stage.device)
+        return stage(ids, meta, pool).float().cpu()
+
+    a, b = run(cpu), run(g)
+    rel = ((a - b).norm() / a.norm()).item()
+    assert rel < 0.03, rel

@@ -215,3 +215,100 @@ def test_apply_rotary_pos_emb_matches_hf_with_batch():
     a = apply_rotary_pos_emb(q, k, cos, sin)
     b = hf_apply(q, k, cos, sin)
     assert torch.allclose(a[0], b[0], atol=1e-6) and torch.allclose(a[1], b[1], atol=1e-6)
+
+
+# ------------------------------------------------------------ Llama-family variants (Qwen2, Mistral)
+def _hf_variant(kind, layers=2, seed=1, sliding_window=None):
+    torch.manual_seed(seed)
+    kw = dict(vocab_size=256, hidden_size=128, intermediate_size=256, num_hidden_layers=layers,
+              num_attention_heads=4, num_key_value_heads=2, rms_norm_eps=1e-6,
+              max_position_embeddings=4096, tie_word_embeddings=False)
+    if kind == "qwen2":
+        from transformers import Qwen2Config as C, Qwen2ForCausalLM as M
+        kw["rope_parameters"] = {"rope_type": "default", "rope_theta": 1000000.0}
+    else:
+        from transformers import MistralConfig as C, MistralForCausalLM as M
+        kw["rope_parameters"] = {"rope_type": "default", "rope_theta": 10000.0}
+        kw["sliding_window"] = sliding_window
+    m = M(C(**kw)).eval()
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith(".bias"):   # HF zero-inits biases: make them matter
+                p.normal_(0, 0.5)
+            p.copy_(p.to(torch.bfloat16).float())
+    return m
+
+
+def _check_against_hf(hf, stage_logits, prompts, steps):
+    gen = torch.stack([o.argmax(-1) for o in stage_logits], 1)
+    for b, p in enumerate(prompts):
+        seq = torch.tensor(p + gen[b, :steps].tolist())[None]
+        with torch.no_grad():
+            ref_logits = hf(seq).logits[0].float()
+        for s in range(steps + 1):
+            a, r = stage_logits[s][b], ref_logits[len(p) - 1 + s]
+            err = (a - r).abs().max().item()
+            assert err < 0.05 * max(1.0, r.abs().max().item()), f"b={b} step={s} err={err}"
+
+
+def test_qwen2_matches_hf():
+    """Qwen2 = Llama with q/k/v bias only (no o_proj bias), parsed from model_type."""
+    hf = _hf_variant("qwen2")
+    stage = stage_from_hf_model(hf, 0, hf.config.num_hidden_layers)
+    spec = stage.spec
+    assert spec.model_type == "qwen2" and spec.attention_bias and not spec.has_o_proj_bias
+    assert stage.block.layers[0].self_attn.o_proj.bias is None
+    prompts = [[5, 17, 99, 3, 250, 7, 7, 1], [8, 2, 64]]
+    _check_against_hf(hf, _run_stage(stage, prompts, decode_steps=3), prompts, 3)
+    # round trip through the HF config / state-dict writers
+    assert ModelSpec.from_hf_config(spec.to_hf_dict()).replace(name=spec.name) == spec
+    sd = stage.block.layers[0].hf_state_dict()
+    assert "self_attn.q_proj.bias" in sd and "self_attn.o_proj.bias" not in sd
+
+
+def test_mistral_matches_hf_within_window():
+    hf = _hf_variant("mistral", sliding_window=4096)
+    stage = stage_from_hf_model(hf, 0, hf.config.num_hidden_layers)
+    assert stage.spec.model_type == "mistral" and stage.spec.sliding_window == 4096
+    prompts = [[5, 17, 99, 3, 250, 7, 7, 1, 42], [8, 2, 64]]
+    _check_against_hf(hf, _run_stage(stage, prompts, decode_steps=3), prompts, 3)
+
+
+def test_mistral_sliding_window_matches_hf_beyond_window():
+    """Sliding-window attention (W = 8) past the window, in prefill (13-token prompt) and decode:
+    the ring window with no sink tokens reproduces HF Mistral exactly."""
+    W = 8
+    hf = _hf_variant("mistral", sliding_window=W)
+    stage = stage_from_hf_model(hf, 0, hf.config.num_hidden_layers)
+    prompts = [list(range(3, 16)), [8, 2, 64, 9, 10, 11]]
+    steps = 10
+    pool = stage.make_pool(64, block_size=32, window_length=W, num_sink_tokens=0)
+    m = pool.manager
+    sids = [0, 1]
+    for s, p in zip(sids, prompts):
+        m.append(s, len(p))
+    meta = pool.build_metadata(sids, [len(p) for p in prompts])
+    meta.logits_rows = torch.cumsum(torch.tensor([len(p) for p in prompts]), 0) - 1
+    outs = [stage(torch.tensor([t for p in prompts for t in p]), meta, pool).float()]
+    for _ in range(steps):
+        toks = outs[-1].argmax(-1)
+        for s in sids:
+            m.append(s, 1)
+        meta = pool.build_metadata(sids, [1, 1])
+        outs.append(stage(toks.to(torch.int32), meta, pool).float())
+    _check_against_hf(hf, outs, prompts, steps)
+
+
+def test_engine_uses_sliding_window_from_config():
+    from distributed_llm_inference.config import CacheConfig, ServeConfig
+    from distributed_llm_inference.runtime.engine import EngineConfig, LLMEngine
+    from distributed_llm_inference.runtime.sequence import SamplingParams
+    hf = _hf_variant("mistral", sliding_window=8)
+    spec = ModelSpec.from_hf_config(hf.config)
+    cfg = EngineConfig(model="m", cache=CacheConfig(num_blocks=64, block_size=32),
+                       serve=ServeConfig(max_batch_size=4, max_num_batched_tokens=64,
+                                         max_seq_len=64, use_graphs=False))
+    eng = LLMEngine(spec, device="cpu", cfg=cfg)
+    assert eng.executors[0].pool.manager.window_length == 8
+    out = eng.generate([list(range(3, 16))], SamplingParams(max_tokens=4, ignore_eos=True))
+    assert len(out[0].output) == 4
