@@ -134,7 +134,7 @@ def cmd_worker(a) -> int:
             from .server.service import EngineService
             svc = EngineService(drv, eos_token_id=getattr(drv.sched, "eos", None))
             try:
-                serve(svc, a.host, a.port, tok, a.model)
+                serve(svc, a.host, a.port, tok, a.model, a.request_timeout)
             finally:
                 svc.shutdown(stop_driver=False)
         else:
@@ -161,6 +161,8 @@ def _gen_args(ap):
 def _serve_args(ap):
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--request-timeout", type=float, default=None,
+                    help="abort (504) requests still running after this many seconds")
 
 
 def main(argv: Optional[List[str]] = None) -> int:

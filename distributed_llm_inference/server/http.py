@@ -18,7 +18,11 @@ from ..runtime.sequence import SamplingParams
 from .service import EngineService
 
 
-def build_app(service: EngineService, tokenizer=None, model_name: str = "model"):
+def build_app(service: EngineService, tokenizer=None, model_name: str = "model",
+              request_timeout_s: Optional[float] = None):
+    """``request_timeout_s`` (or a request's ``timeout_s``): a request still running after that
+    long is aborted (KV freed) and answered 504; a streaming client that disconnects aborts its
+    sequence as well."""
     from fastapi import FastAPI, HTTPException
     from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 
@@ -52,18 +56,44 @@ def build_app(service: EngineService, tokenizer=None, model_name: str = "model")
         except ValueError as e:
             raise HTTPException(400, str(e))
 
-    async def _stream(q, prefix: str = ""):
+    def _timeout(body: dict) -> Optional[float]:
+        t = body.get("timeout_s", request_timeout_s)
+        return float(t) if t is not None else None
+
+    async def _result(fut, timeout: Optional[float]):
+        try:
+            return await asyncio.wait_for(asyncio.shield(asyncio.wrap_future(fut)), timeout)
+        except asyncio.TimeoutError:
+            service.abort(fut.seq_id)
+            raise HTTPException(504, f"request timed out after {timeout} s (generation aborted)")
+
+    async def _stream(q, fut=None, timeout: Optional[float] = None):
+        """SSE token stream.  A client that disconnects (the generator is closed early) or a
+        stream that outlives its timeout aborts the sequence, so its KV blocks are freed."""
         loop = asyncio.get_running_loop()
-        while True:
-            tok = await loop.run_in_executor(None, q.get)
-            if tok is None:
-                break
-            payload = {"token_id": tok}
-            txt = _decode([tok])
-            if txt is not None:
-                payload["text"] = txt
-            yield f"data: {json.dumps(payload)}\n\n"
-        yield "data: [DONE]\n\n"
+        deadline = time.monotonic() + timeout if timeout is not None else None
+        finished = False
+        try:
+            while True:
+                wait = None if deadline is None else max(0.0, deadline - time.monotonic())
+                try:
+                    tok = await asyncio.wait_for(loop.run_in_executor(None, q.get), wait)
+                except asyncio.TimeoutError:
+                    yield f"data: {json.dumps({'error': 'timeout'})}\n\n"
+                    break
+                if tok is None:
+                    finished = True
+                    break
+                payload = {"token_id": tok}
+                txt = _decode([tok])
+                if txt is not None:
+                    payload["text"] = txt
+                yield f"data: {json.dumps(payload)}\n\n"
+            if finished:
+                yield "data: [DONE]\n\n"
+        finally:
+            if not finished and fut is not None:
+                service.abort(fut.seq_id)
 
     @app.post("/generate")
     async def generate(body: dict):
@@ -74,8 +104,9 @@ def build_app(service: EngineService, tokenizer=None, model_name: str = "model")
         except Exception as e:
             raise HTTPException(400, str(e))
         if q is not None:
-            return StreamingResponse(_stream(q), media_type="text/event-stream")
-        res = await asyncio.wrap_future(fut)
+            return StreamingResponse(_stream(q, fut=fut, timeout=_timeout(body)),
+                                     media_type="text/event-stream")
+        res = await _result(fut, _timeout(body))
         return {"output_ids": res.output_ids, "text": _decode(res.output_ids),
                 "finish_reason": res.finish_reason,
                 "usage": {"prompt_tokens": res.prompt_len,
@@ -89,8 +120,9 @@ def build_app(service: EngineService, tokenizer=None, model_name: str = "model")
         params = _params(body)
         fut, q = service.submit(ids, params, stream=bool(body.get("stream")))
         if q is not None:
-            return StreamingResponse(_stream(q), media_type="text/event-stream")
-        res = await asyncio.wrap_future(fut)
+            return StreamingResponse(_stream(q, fut=fut, timeout=_timeout(body)),
+                                     media_type="text/event-stream")
+        res = await _result(fut, _timeout(body))
         return {"id": f"cmpl-{res.seq_id}", "object": "text_completion", "created": int(time.time()),
                 "model": model_name,
                 "choices": [{"index": 0, "text": _decode(res.output_ids),
@@ -119,6 +151,7 @@ def build_app(service: EngineService, tokenizer=None, model_name: str = "model")
 
 
 def serve(service: EngineService, host: str = "127.0.0.1", port: int = 8000, tokenizer=None,
-          model_name: str = "model") -> None:
+          model_name: str = "model", request_timeout_s: Optional[float] = None) -> None:
     import uvicorn
-    uvicorn.run(build_app(service, tokenizer, model_name), host=host, port=port, log_level="info")
+    uvicorn.run(build_app(service, tokenizer, model_name, request_timeout_s), host=host, port=port,
+                log_level="info")

@@ -7,6 +7,7 @@ their KV blocks immediately).
 """
 from __future__ import annotations
 
+import collections
 import logging
 import queue
 import threading
@@ -47,6 +48,11 @@ class EngineService:
         self.total_requests = 0
         self.last_step_time = time.time()
         self.error: Optional[BaseException] = None
+        # rolling windows for /metrics: per-token latency, time to first token
+        self._tok_lat_ms: "collections.deque" = collections.deque(maxlen=8192)
+        self._ttft_ms: "collections.deque" = collections.deque(maxlen=1024)
+        self.completed = 0
+        self.aborted = 0
         self._thread = threading.Thread(target=self._loop, name="dli-engine", daemon=True)
         self._thread.start()
 
@@ -57,6 +63,7 @@ class EngineService:
             raise RuntimeError(f"engine failed: {self.error!r}")
         seq = Sequence(list(prompt_ids), params)
         fut: Future = Future()
+        fut.seq_id = seq.seq_id  # type: ignore[attr-defined]  (for abort on timeout / disconnect)
         q = queue.Queue() if stream else None
         self._new.put((seq, fut, q))
         return fut, q
@@ -67,14 +74,31 @@ class EngineService:
         return fut.result(timeout)
 
     def abort(self, seq_id: int) -> None:
+        """Stop generating for ``seq_id`` (request timeout, client gone); its KV blocks are freed
+        at the next step and its future resolves with ``finish_reason="abort"``."""
         self._new.put(("abort", seq_id, None))
+
+    @staticmethod
+    def _pct(xs, q: float) -> float:
+        if not xs:
+            return 0.0
+        v = sorted(xs)
+        return round(v[min(len(v) - 1, int(q * len(v)))], 3)
 
     def stats(self) -> dict:
         s = self.driver.sched
         up = time.time() - self.started
+        lat, ttft = list(self._tok_lat_ms), list(self._ttft_ms)
         return dict(running=s.num_running(), waiting=len(s.waiting), uptime_s=round(up, 1),
                     total_tokens=self.total_tokens, total_requests=self.total_requests,
+                    completed_requests=self.completed, aborted_requests=self.aborted,
+                    tokens_per_s=round(self.total_tokens / up, 2) if up > 0 else 0.0,
+                    token_latency_p50_ms=self._pct(lat, 0.5),
+                    token_latency_p90_ms=self._pct(lat, 0.9),
+                    token_latency_p99_ms=self._pct(lat, 0.99),
+                    ttft_p50_ms=self._pct(ttft, 0.5), ttft_p90_ms=self._pct(ttft, 0.9),
                     kv_reserved_blocks=s.reserved_blocks, kv_total_blocks=s.total_blocks,
+                    kv_occupancy=round(s.reserved_blocks / s.total_blocks, 4) if s.total_blocks else 0.0,
                     seconds_since_last_step=round(time.time() - self.last_step_time, 3),
                     healthy=self.error is None and self._thread.is_alive())
 
@@ -131,6 +155,14 @@ class EngineService:
                 q.put(None)
             self._sent.pop(s.seq_id, None)
             self.total_tokens += len(s.output)
+            tt = s.token_times
+            self._tok_lat_ms.extend((tt[i + 1] - tt[i]) * 1e3 for i in range(len(tt) - 1))
+            if s.first_token_time:
+                self._ttft_ms.append((s.first_token_time - s.arrival) * 1e3)
+            if s.finish_reason == "abort":
+                self.aborted += 1
+            else:
+                self.completed += 1
             if fut is not None and not fut.done():
                 tt = s.token_times
                 fut.set_result(Completion(

@@ -129,8 +129,28 @@ def test_engine_service_and_http():
         events = [l for l in s.iter_lines() if l.startswith("data:")]
     assert events[-1] == "data: [DONE]" and len(events) == 4
     assert app.get("/health").json()["healthy"]
-    assert "dli_total_tokens" in app.get("/metrics").text
+    m = app.get("/metrics").text
+    assert "dli_total_tokens" in m and "dli_token_latency_p50_ms" in m and "dli_ttft_p90_ms" in m
     assert app.post("/generate", json={"max_tokens": 3}).status_code == 400
+    # request timeout: 504, and the sequence is aborted (its KV blocks come back)
+    r = app.post("/generate", json={"prompt_ids": [4, 4], "max_tokens": 200, "ignore_eos": True,
+                                    "timeout_s": 0.05})
+    assert r.status_code == 504
+    deadline = time.time() + 30
+    while (svc.stats()["running"] or svc.stats()["waiting"]) and time.time() < deadline:
+        time.sleep(0.05)
+    st = svc.stats()
+    assert st["running"] == 0 and st["aborted_requests"] >= 1 and st["kv_reserved_blocks"] == 0
+    # a stream that times out also aborts its sequence
+    with app.stream("POST", "/generate", json={"prompt_ids": [2], "max_tokens": 200,
+                                                "ignore_eos": True, "stream": True,
+                                                "timeout_s": 0.05}) as s:
+        events = [l for l in s.iter_lines() if l.startswith("data:")]
+    assert "timeout" in events[-1]
+    deadline = time.time() + 30
+    while svc.stats()["aborted_requests"] < 2 and time.time() < deadline:
+        time.sleep(0.05)
+    assert svc.stats()["aborted_requests"] >= 2
     svc.shutdown()
 
 
