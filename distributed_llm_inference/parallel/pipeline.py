@@ -238,6 +238,7 @@ class DistributedDriver(DriverBase):
         self.timeout = timeout
         self.faults = FaultInjector(0)
         self.stats = StageStats(0, executor.device)
+        self.stats.transport = transport
 
     def _issue(self, plan: StepPlan) -> None:
         self.ch.ctrl.send(msgpack.packb(plan.to_wire()), self.timeout)
@@ -282,6 +283,7 @@ class StageFollower:
         self.barrier_times: List[float] = []
         self.faults = FaultInjector(rank)
         self.stats = StageStats(rank, executor.device)
+        self.stats.transport = transport
         self._pub_q: "queue.Queue" = queue.Queue()
         self._pub_thread = None
         if self.is_last:

@@ -28,6 +28,24 @@ import torch.distributed as dist
 class Transport:
     rank: int
     world: int
+    # traffic counters (SURVEY §5.5 "comm bytes per stage"); published with the stage stats
+    bytes_sent: int = 0
+    bytes_recv: int = 0
+    msgs_sent: int = 0
+    msgs_recv: int = 0
+
+    def _count(self, t: torch.Tensor, sent: bool) -> None:
+        n = t.numel() * t.element_size()
+        if sent:
+            self.bytes_sent += n
+            self.msgs_sent += 1
+        else:
+            self.bytes_recv += n
+            self.msgs_recv += 1
+
+    def traffic(self) -> dict:
+        return {"bytes_sent": self.bytes_sent, "bytes_recv": self.bytes_recv,
+                "msgs_sent": self.msgs_sent, "msgs_recv": self.msgs_recv}
 
     def send(self, t: torch.Tensor, peer: int) -> None:
         raise NotImplementedError
@@ -48,10 +66,12 @@ class TorchDistTransport(Transport):
         self.world = dist.get_world_size()
 
     def send(self, t, peer):
+        self._count(t, True)
         dist.send(t.contiguous(), peer, group=self.group)
 
     def recv(self, t, peer, free_event=None):
         dist.recv(t, peer, group=self.group)
+        self._count(t, False)
         return t
 
 
@@ -69,6 +89,7 @@ class HostStagedTransport(Transport):
         self.world = dist.get_world_size()
 
     def send(self, t, peer):
+        self._count(t, True)
         dist.send(t.detach().to("cpu").contiguous(), peer, group=self.group)
 
     def recv(self, t, peer, free_event=None):
@@ -77,6 +98,7 @@ class HostStagedTransport(Transport):
         host = torch.empty(t.shape, dtype=t.dtype)
         dist.recv(host, peer, group=self.group)
         t.copy_(host, non_blocking=False)
+        self._count(t, False)
         return t
 
 
@@ -141,6 +163,7 @@ class RcclTransport(Transport):
         self.send_stream.wait_stream(cur)
         t.record_stream(self.send_stream)
         self._comm(peer).send(t, self._peer_index(peer), self.send_stream.cuda_stream)
+        self._count(t, True)
 
     def recv(self, t: torch.Tensor, peer: int, free_event: Optional["torch.cuda.Event"] = None
              ) -> torch.Tensor:
@@ -156,6 +179,7 @@ class RcclTransport(Transport):
         t.record_stream(self.recv_stream)
         self._comm(peer).recv(t, self._peer_index(peer), self.recv_stream.cuda_stream)
         cur.wait_stream(self.recv_stream)
+        self._count(t, False)
         return t
 
     def _peer_index(self, peer: int) -> int:

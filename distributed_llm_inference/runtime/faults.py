@@ -79,6 +79,7 @@ class StageStats:
         self._pending: Deque[Tuple] = collections.deque()
         self._t0 = 0.0
         self._store = None
+        self.transport = None   # set by the pipeline: its traffic counters are published too
 
     def begin(self, extra_ms: float = 0.0):
         if not self.enabled:
@@ -112,7 +113,9 @@ class StageStats:
         try:
             if self._store is None:
                 self._store = raw_store()
-            self._store.set(f"dli_stats/{self.rank}",
-                            json.dumps({"step_ms": self.ewma, "steps": self.steps}))
+            rec = {"step_ms": self.ewma, "steps": self.steps}
+            if self.transport is not None:
+                rec.update(self.transport.traffic())
+            self._store.set(f"dli_stats/{self.rank}", json.dumps(rec))
         except Exception:
             pass

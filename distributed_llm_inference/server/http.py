@@ -145,6 +145,10 @@ def build_app(service: EngineService, tokenizer=None, model_name: str = "model",
                 v = int(v)
             if isinstance(v, (int, float)):
                 lines.append(f"dli_{k} {v}")
+        for r, rec in enumerate(service.stage_stats()):   # per pipeline stage (rank)
+            for k, v in (rec or {}).items():
+                if isinstance(v, (int, float)):
+                    lines.append(f'dli_stage_{k}{{stage="{r}"}} {v}')
         return PlainTextResponse("\n".join(lines) + "\n")
 
     return app

@@ -8,6 +8,8 @@ their KV blocks immediately).
 from __future__ import annotations
 
 import collections
+import json
+import os
 import logging
 import queue
 import threading
@@ -101,6 +103,22 @@ class EngineService:
                     kv_occupancy=round(s.reserved_blocks / s.total_blocks, 4) if s.total_blocks else 0.0,
                     seconds_since_last_step=round(time.time() - self.last_step_time, 3),
                     healthy=self.error is None and self._thread.is_alive())
+
+    def stage_stats(self) -> list:
+        """Per-rank ``{"step_ms", "steps", "bytes_sent", "bytes_recv", ...}`` that every stage
+        publishes to the job store when ``DLI_PUBLISH_STATS=1`` (empty otherwise)."""
+        if os.environ.get("DLI_PUBLISH_STATS", "0") != "1":
+            return []
+        try:
+            from ..runtime.faults import raw_store
+            store = raw_store()
+            out = []
+            for r in range(int(os.environ.get("WORLD_SIZE", "1"))):
+                key = f"dli_stats/{r}"
+                out.append(json.loads(store.get(key)) if store.check([key]) else None)
+            return out
+        except Exception:  # pragma: no cover - store unavailable (single process)
+            return []
 
     def shutdown(self, stop_driver: bool = True) -> None:
         self._stop.set()

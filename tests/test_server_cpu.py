@@ -217,6 +217,11 @@ def test_server_rebalances_slow_stage():
             reb = srv.should_rebalance()
             time.sleep(0.3)
         assert reb
+        st = srv.stage_stats()
+        # traffic counters ride along with the step times: stage 0 sends, stage 1 receives
+        assert st[0]["bytes_sent"] > 0 and st[1]["bytes_recv"] > 0
+        m = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=10).read().decode()
+        assert 'dli_stage_step_ms{stage="1"}' in m and 'dli_stage_bytes_sent{stage="0"}' in m
         new = srv.choose_blocks()
         assert new[1][1] - new[1][0] < 2  # the slow stage gets fewer layers
     finally:
