@@ -265,3 +265,32 @@ def test_llama_family_variants_gpu_match_cpu(gpu, preset):
     a, b = run(cpu), run(g)
     rel = ((a - b).norm() / a.norm()).item()
     assert rel < 0.03, rel
+
+
+def test_reference_llama_block_api_on_gpu(gpu):
+    """The reference's stage API (LlamaBlock(config, layer_ids)(generation_id, hidden_states,
+    past_key_value=PartialLlamaSinkCache)) on the HIP kernels: incremental session decoding
+    equals the full causal pass, sessions are isolated, close_session frees them, and the GPU
+    agrees with the CPU reference path."""
+    from distributed_llm_inference.models import LlamaBlock, PartialLlamaSinkCache
+    spec = SPEC.replace(hidden_size=512, intermediate_size=1024, num_heads=4, num_kv_heads=2,
+                        head_dim=128)
+    cpu = LlamaBlock(spec, [0, 1, 2]).init_random(4)
+    blk = LlamaBlock(spec, [0, 1, 2], device=gpu)
+    blk.load_state_dict({k: v.to(gpu) for k, v in cpu.state_dict().items()})
+    torch.manual_seed(3)
+    x = torch.randn(2, 40, 512, dtype=torch.bfloat16)
+    (full_cpu,) = cpu("g", x)
+    xg = x.to(gpu)
+    (full,) = blk("g-full", xg)
+    rel = ((full.float().cpu() - full_cpu.float()).norm() / full_cpu.float().norm()).item()
+    assert rel < 0.02, rel
+    cache = PartialLlamaSinkCache(0, 0, num_blocks=64, block_size=64)
+    parts = [blk("g1", xg[:, a:b], past_key_value=cache)[0] for a, b in ((0, 30), (30, 31), (31, 40))]
+    (other,) = blk("g2", xg[:, :5].flip(0), past_key_value=cache)   # another session in between
+    inc = torch.cat(parts, 1)
+    rel = ((inc.float() - full.float()).norm() / full.float().norm()).item()
+    assert rel < 0.02, rel
+    assert cache.get_seq_length(0, "g1") == 40 and cache.get_seq_length(0, "g2") == 5
+    cache.close_session("g1")
+    assert cache.get_seq_length(0, "g1") == 0
