@@ -129,12 +129,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // FP8 / INT8: A and B are 1-byte elements (K counted in elements = bytes) with fp32 a_scale[M]
 // (per row) and b_scale[N] (per output channel).  Staging is byte-identical to bf16: a k-tile is
 // 128 bytes of every row (64 bf16, 128 fp8 / int8).
-// EVEN: DMA schedule with exactly one half-tile staged per phase (B1, A1 of tile t+1 in phases
-// 0, 1; B0, A0 of tile t+2 in phases 2, 3: each restage >= 2 phases after the half's last read)
-// and a counted vmcnt(8) in phases 0, 1 and 3 (4 half-tiles in flight), so every phase
-// interleaves LDS reads, one DMA issue and its MFMAs.  !EVEN: the (1, 0, 1, 2) schedule with one
-// vmcnt(6) per k-tile.
-template <int EPI, int PREC, bool EVEN>
+template <int EPI, int PREC>
 __global__ void __launch_bounds__(kThreads, 1)
 gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __restrict__ C,
                  const float* __restrict__ a_scale, const float* __restrict__ b_scale,
@@ -287,18 +282,7 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
 
     // ---- prologue: tile 0 complete, three halves of tile 1 in flight ----
     // (LDS is free here: every wave passed the realigning barrier after its last ds_read)
-    if (EVEN) {
-      // tile 0 (B0 A0 B1 A1) + B0, A0 of tile 1; retire tile 0's B0 / A0 (read in phase 0)
-      if (T > 0) {
-        stage(2, 0); stage(0, 0); stage(3, 0); stage(1, 0);
-        if (T > 1) {
-          stage(2, 1); stage(0, 1);
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        }
-      }
-    } else if (T > 0) {
+    if (T > 0) {
       stage(0, 0); stage(2, 0); stage(3, 0); stage(1, 0);
       if (T > 1) {
         stage(0, 1); stage(2, 1); stage(3, 1);
@@ -312,56 +296,7 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
     // the two wave groups (wr = 0: waves 0-3, wr = 1: waves 4-7, one of each per SIMD) run one
     // barrier apart, so every SIMD alternates one wave's MFMA segment with the other's LDS reads
     if (wr == 1) barrier();
-    if (EVEN) {
-      for (int t = 0; t < T; ++t) {
-        const char* buf = smem + (t & 1) * kBuf;
-        const bool more1 = t + 1 < T, more2 = t + 2 < T;
-        // phase 0: quadrant (0, 0); stage B1(t+1); retire B1(t) (newer: A1(t), B0 A0 B1 of t+1)
-        read_a(buf, 0);
-        read_b(buf, 0, b0);
-        if (more1) {
-          stage(3, t + 1);
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        }
-        barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        quadrant(0, 0, b0);
-        barrier();
-        // phase 1: quadrant (0, 1); stage A1(t+1); retire A1(t) (newer: B0 A0 B1 A1 of t+1)
-        read_b(buf, 1, b1);
-        if (more1) {
-          stage(1, t + 1);
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        quadrant(0, 1, b1);
-        barrier();
-        // phase 2: quadrant (1, 1); stage B0(t+2) (B0(t) last read in phase 0)
-        read_a(buf, 1);
-        if (more2) stage(2, t + 2);
-        barrier();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        quadrant(1, 1, b1);
-        barrier();
-        // phase 3: quadrant (1, 0); stage A0(t+2); retire B0, A0 of t+1 for the next phase 0
-        if (more2) {
-          stage(0, t + 2);
-          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        } else if (more1) {
-          asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        barrier();
-        quadrant(1, 0, b0);
-        barrier();
-      }
-    } else for (int t = 0; t < T; ++t) {
+    for (int t = 0; t < T; ++t) {
       const char* buf = smem + (t & 1) * kBuf;
       const bool more1 = t + 1 < T, more2 = t + 2 < T;
       // phase 0: quadrant (0, 0)
@@ -566,17 +501,6 @@ int device_cus() {
   return cus[dev];
 }
 
-// DLI_TILE_EVEN_DMA=1 selects the one-half-tile-per-phase DMA schedule (kernel comment above)
-bool even_dma() {
-  static const bool on = [] {
-    const char* e = getenv("DLI_TILE_EVEN_DMA");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on;
-}
-
-#define KLAUNCH(E) (even_dma() ? gemm_tile_kernel<E, PREC, true> : gemm_tile_kernel<E, PREC, false>)
-
 // splits == 0: data-parallel whole tiles + stream-K tail (SkArgs); workspace = the
 // gemm_tile_sk_workspace_floats() layout: [flags | err | pad] 4 KB, then sk_wgs fp32 slabs.
 template <int PREC>
@@ -607,10 +531,10 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
     if (hipMemsetAsync(workspace, 0, ((size_t)cus * 4 + 15) / 16 * 16, stream) != hipSuccess) return -9;
     const int grid = sk.n_dp + sk.sk_wgs;
     if (epilogue == kSwiGLU)
-      KLAUNCH(kSwiGLU)<<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
+      gemm_tile_kernel<kSwiGLU, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
                                                                     tiles_m, tiles_n, kt, sk);
     else if (epilogue == kStoreBf16)
-      KLAUNCH(kStoreBf16)<<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
+      gemm_tile_kernel<kStoreBf16, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
                                                                        tiles_m, tiles_n, kt, sk);
     else
       return -4;
@@ -624,7 +548,7 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
   const int grid = tiles * splits;
   sk.n_dp = grid;
   if (splits > 1) {
-    KLAUNCH(kStoreF32)<<<grid, kThreads, 0, stream>>>(A, B, workspace, sa, sb, M, N,
+    gemm_tile_kernel<kStoreF32, PREC><<<grid, kThreads, 0, stream>>>(A, B, workspace, sa, sb, M, N,
                                                                     K, tiles_m, tiles_n, kps, sk);
     if (epilogue == kStoreF32) return 0;
     const size_t MN = (size_t)M * N;
@@ -633,10 +557,10 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
     tile_splitk_reduce_kernel<<<(int)blocks, 256, 0, stream>>>(reinterpret_cast<bf16*>(C),
                                                                workspace, splits, MN);
   } else if (epilogue == kSwiGLU) {
-    KLAUNCH(kSwiGLU)<<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K, tiles_m,
+    gemm_tile_kernel<kSwiGLU, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K, tiles_m,
                                                                   tiles_n, kps, sk);
   } else if (epilogue == kStoreBf16) {
-    KLAUNCH(kStoreBf16)<<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
+    gemm_tile_kernel<kStoreBf16, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
                                                                      tiles_m, tiles_n, kps, sk);
   } else {
     return -4;
