@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--prompt-len", type=int, default=512)
     ap.add_argument("--max-batched-tokens", type=int, default=16384)
     ap.add_argument("--fp8", action="store_true", help="fp8-e4m3 weights (BASELINE config 5)")
+    ap.add_argument("--int8", action="store_true",
+                    help="LLM.int8 weights (the reference's 8-bit mode: int8 MFMA + bf16 outliers)")
     ap.add_argument("--kv-fp8", action="store_true", help="fp8-e4m3 KV cache")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--json-out", default=None)
@@ -72,7 +74,7 @@ def main():
     M = a.micro_batches or (a.gpus + 1 if a.gpus > 1 else 1)
     total_len = a.prompt_len + a.warmup + a.steps + 72
     cfg = EngineConfig(
-        model=a.model, random_init=True, seed=0, quantize=a.fp8, pp=a.gpus,
+        model=a.model, random_init=True, seed=0, quantize="int8" if a.int8 else a.fp8, pp=a.gpus,
         cache=CacheConfig(block_size=64, gpu_memory_utilization=0.92,
                           dtype="fp8" if a.kv_fp8 else "bf16"),
         serve=ServeConfig(max_batch_size=a.batch_per_mb, max_num_batched_tokens=a.max_batched_tokens,
@@ -150,7 +152,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("fp8-weights/bf16-act" if a.fp8 else "bf16") + ("/fp8-kv" if a.kv_fp8 else ""),
+        "dtype": ("int8-weights/bf16-act" if a.int8 else "fp8-weights/bf16-act" if a.fp8 else "bf16")
+                 + ("/fp8-kv" if a.kv_fp8 else ""),
         "data": f"synthetic (random-init {spec.name} weights, random prompt tokens)",
         "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
                    "global_batch": G, "seq_len": total_len,
