@@ -451,6 +451,42 @@ void quant_rowwise_int8(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> o
            "quant_rowwise_int8");
 }
 
+// LLM.int8 outlier columns of x [M, K] against int8 weights wq [N, K] (scale ws [N]): returns
+// (flags uint8 [K], x_out bf16 [M, max_out], w_out bf16 [N, max_out]) with x_out . w_out^T the
+// bf16 outlier product (padding columns are zero).  Four kernels, static shapes, no host sync.
+std::vector<Tensor> llm_int8_outliers(Tensor x, Tensor wq, Tensor ws, double threshold,
+                                      int64_t max_out) {
+  CHECK_IN(x); CHECK_BF16(x); CHECK_IN(wq); CHECK_IN(ws); CHECK_F32(ws);
+  TORCH_CHECK(wq.scalar_type() == at::kChar, "llm_int8_outliers: wq must be int8");
+  TORCH_CHECK(x.dim() == 2 && wq.dim() == 2 && wq.size(1) == x.size(1) && ws.numel() == wq.size(0),
+              "llm_int8_outliers: shape mismatch");
+  const int64_t M = x.size(0), K = x.size(1), N = wq.size(0);
+  TORCH_CHECK(K % 8 == 0 && max_out > 0 && max_out <= K, "llm_int8_outliers: K % 8 and 0 < max_out <= K");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  auto o = x.options();
+  Tensor colmax = at::empty({K}, o.dtype(at::kFloat));
+  Tensor idx = at::empty({max_out}, o.dtype(at::kLong));
+  Tensor sel = at::empty({max_out}, o.dtype(at::kFloat));
+  Tensor flags = at::empty({K}, o.dtype(at::kByte));
+  Tensor xo = at::empty({M, max_out}, o);
+  Tensor wo = at::empty({N, max_out}, o);
+  hipStream_t st = cur_stream();
+  check_rc(dli::launch_llm_int8_colmax(colmax.data_ptr<float>(), bp(x), (int)M, (int)K, st),
+           "llm_int8_colmax");
+  check_rc(dli::launch_llm_int8_select(colmax.data_ptr<float>(), (int)K, (float)threshold,
+                                       (int)max_out, idx.data_ptr<int64_t>(), sel.data_ptr<float>(),
+                                       flags.data_ptr<uint8_t>(), st),
+           "llm_int8_select");
+  check_rc(dli::launch_llm_int8_gather_x(bp(xo), bp(x), idx.data_ptr<int64_t>(),
+                                         sel.data_ptr<float>(), (int)M, (int)K, (int)max_out, st),
+           "llm_int8_gather_x");
+  check_rc(dli::launch_llm_int8_gather_w(bp(wo), reinterpret_cast<const int8_t*>(wq.data_ptr()),
+                                         ws.data_ptr<float>(), idx.data_ptr<int64_t>(),
+                                         sel.data_ptr<float>(), (int)N, (int)K, (int)max_out, st),
+           "llm_int8_gather_w");
+  return {flags, xo, wo};
+}
+
 void silu_mul_quant(Tensor q_out, Tensor scale, Tensor x) {
   CHECK_IN(q_out); CHECK_IN(scale); CHECK_IN(x); CHECK_BF16(x); CHECK_F32(scale);
   TORCH_CHECK(q_out.element_size() == 1, "q_out must be an 8-bit tensor");
@@ -560,6 +596,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps"), py::arg("residual_out") = py::none());
   m.def("quant_rowwise_int8", &quant_rowwise_int8, "LLM.int8 row-wise int8 quantisation (outlier columns zeroed)",
         py::arg("q_out"), py::arg("scale"), py::arg("x"), py::arg("outlier") = py::none());
+  m.def("llm_int8_outliers", &llm_int8_outliers,
+        "LLM.int8 outlier columns: (flags, x_out, w_out) for the bf16 outlier product");
   m.def("silu_mul_quant", &silu_mul_quant, "SwiGLU fused with row-wise fp8 quantisation");
   m.def("gemm_tile", &gemm_tile, "C = A . B^T, 256x256 LDS-DMA 8-phase MFMA tile GEMM",
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,

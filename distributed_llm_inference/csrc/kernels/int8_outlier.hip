@@ -1,0 +1,197 @@
+// LLM.int8 outlier bookkeeping on the GPU (reference utils/model.py:93-113 -> bitsandbytes
+// Linear8bitLt(threshold)): per product, the activation columns whose magnitude exceeds
+// `threshold` anywhere in the batch are multiplied in bf16 with the dequantised weight columns.
+// Static shapes for graph capture: at most `max_out` columns (the largest ones passing the
+// threshold) are taken.  Four kernels replace a torch chain of abs / amax / topk / scatter /
+// gathers / casts:
+//   * llm_int8_colmax_kernel     colmax[k] = max_m |x[m, k]|   (atomicMax on the float bits)
+//   * llm_int8_select_kernel     one workgroup: the <= max_out largest columns above threshold,
+//                                in column order -> idx[max_out] (padded), sel[max_out], flags[K]
+//   * llm_int8_gather_w_kernel   w_out[n, j] = bf16(wq[n, idx[j]] * ws[n]) * sel[j]
+//   * llm_int8_gather_x_kernel   x_out[m, j] = x[m, idx[j]] * sel[j]
+#include "kernels.h"
+
+namespace dli {
+
+// grid (ceil(K/8 / 256), ceil(rows / kRowsPerWG)); colmax (as uint bits) zeroed by the caller.
+constexpr int kRowsPerWG = 32;
+
+__global__ void __launch_bounds__(256) llm_int8_colmax_kernel(unsigned* __restrict__ colmax,
+                                                              const bf16* __restrict__ x,
+                                                              int rows, int K) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;   // 8-column vector index
+  if (v * 8 >= K) return;
+  const int r0 = blockIdx.y * kRowsPerWG, r1 = min(rows, r0 + kRowsPerWG);
+  float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int r = r0; r < r1; ++r) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(x + (size_t)r * K + (size_t)v * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf((float)a[j]));
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j)   // non-negative floats order like their bit patterns
+    atomicMax(colmax + v * 8 + j, __float_as_uint(m[j]));
+}
+
+// One 1024-thread workgroup; thread t owns the contiguous columns [t * per, t * per + per) in
+// registers (K <= 1024 * kSelMaxPer).  Column maxima are non-negative, so their float bits order
+// like the values and the cut is found on the bits.
+constexpr int kSelThreads = 1024, kSelMaxPer = 32;
+
+__device__ int block_sum(int c, int* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  int total = 0;
+#pragma unroll
+  for (int w = 0; w < kSelThreads / 64; ++w) total += red[w];
+  return total;
+}
+
+__global__ void __launch_bounds__(kSelThreads) llm_int8_select_kernel(
+    const float* __restrict__ colmax, int K, float threshold, int max_out, long* __restrict__ idx,
+    float* __restrict__ sel, uint8_t* __restrict__ flags) {
+  __shared__ int red[kSelThreads / 64];
+  __shared__ int scan[kSelThreads];
+  __shared__ int hist[256];
+  __shared__ unsigned s_prefix;
+  __shared__ int s_rank;
+  const int per = (K + kSelThreads - 1) / kSelThreads;
+  const int k0 = threadIdx.x * per, n_mine = max(0, min(per, K - k0));
+  unsigned v[kSelMaxPer];   // padding = +0.0, never above a positive cut
+#pragma unroll
+  for (int i = 0; i < kSelMaxPer; ++i) v[i] = i < n_mine ? __float_as_uint(colmax[k0 + i]) : 0u;
+
+  // the cut t: `threshold`, or -- when more than max_out columns pass it -- the bits of the
+  // (max_out + 1)-th largest column maximum, found by an MSB-first 8-bit radix select
+  unsigned t = __float_as_uint(fmaxf(threshold, 0.f));
+  int c = 0;
+#pragma unroll
+  for (int i = 0; i < kSelMaxPer; ++i) c += v[i] > t;
+  if (block_sum(c, red) > max_out) {
+    unsigned prefix = 0;
+    int r = max_out + 1;   // rank (from the top) of the value being located
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      const unsigned hmask = shift == 24 ? 0u : 0xffffffffu << (shift + 8);
+      if (threadIdx.x < 256) hist[threadIdx.x] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < kSelMaxPer; ++i)
+        if (i < n_mine && (v[i] & hmask) == prefix) atomicAdd(&hist[(v[i] >> shift) & 255], 1);
+      __syncthreads();
+      if (threadIdx.x < 64) {   // wave 0: lane l holds bins 255-4l .. 252-4l (descending)
+        const int l = threadIdx.x;
+        int h[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) h[q] = hist[255 - 4 * l - q];
+        const int mine = h[0] + h[1] + h[2] + h[3];
+        int inc = mine;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(inc, o);
+          if (l >= o) inc += y;
+        }
+        const int exc = inc - mine;
+        if (exc < r && r <= inc) {   // exactly one lane
+          int cum = exc, q = 0;
+          for (; q < 3 && cum + h[q] < r; ++q) cum += h[q];
+          s_prefix = prefix | ((unsigned)(255 - 4 * l - q) << shift);
+          s_rank = r - cum;
+        }
+      }
+      __syncthreads();
+      prefix = s_prefix;
+      r = s_rank;
+      __syncthreads();
+    }
+    t = prefix;
+  }
+
+  // compaction in column order (block-wide exclusive scan of per-thread counts)
+  int mine = 0;
+#pragma unroll
+  for (int i = 0; i < kSelMaxPer; ++i) mine += i < n_mine && v[i] > t;
+  scan[threadIdx.x] = mine;
+  __syncthreads();
+  for (int o = 1; o < kSelThreads; o <<= 1) {   // inclusive Hillis-Steele scan
+    const int add = (int)threadIdx.x >= o ? scan[threadIdx.x - o] : 0;
+    __syncthreads();
+    scan[threadIdx.x] += add;
+    __syncthreads();
+  }
+  int pos = scan[threadIdx.x] - mine;
+  const int total = scan[kSelThreads - 1];
+#pragma unroll
+  for (int i = 0; i < kSelMaxPer; ++i) {
+    if (i < n_mine) {
+      const bool on = v[i] > t;
+      flags[k0 + i] = on ? 1 : 0;
+      if (on && pos < max_out) {
+        idx[pos] = k0 + i;
+        sel[pos] = 1.f;
+        ++pos;
+      }
+    }
+  }
+  for (int j = min(total, max_out) + threadIdx.x; j < max_out; j += kSelThreads) {
+    idx[j] = 0;     // padding: column 0 with weight 0 (contributes nothing)
+    sel[j] = 0.f;
+  }
+}
+
+__global__ void __launch_bounds__(256) llm_int8_gather_w_kernel(
+    bf16* __restrict__ w_out, const int8_t* __restrict__ wq, const float* __restrict__ ws,
+    const long* __restrict__ idx, const float* __restrict__ sel, int N, int K, int max_out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)N * max_out) return;
+  const int n = (int)(e / max_out), j = (int)(e % max_out);
+  const float v = (float)wq[(size_t)n * K + idx[j]] * ws[n];
+  w_out[e] = (bf16)(v * sel[j]);
+}
+
+__global__ void __launch_bounds__(256) llm_int8_gather_x_kernel(
+    bf16* __restrict__ x_out, const bf16* __restrict__ x, const long* __restrict__ idx,
+    const float* __restrict__ sel, int M, int K, int max_out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (long)M * max_out) return;
+  const int m = (int)(e / max_out), j = (int)(e % max_out);
+  x_out[e] = (bf16)((float)x[(size_t)m * K + idx[j]] * sel[j]);
+}
+
+int launch_llm_int8_colmax(float* colmax, const bf16* x, int rows, int K, hipStream_t stream) {
+  if (K % 8 != 0 || rows < 0) return -1;
+  if (hipMemsetAsync(colmax, 0, (size_t)K * sizeof(float), stream) != hipSuccess) return -2;
+  if (rows == 0) return 0;
+  dim3 grid((K / 8 + 255) / 256, (rows + kRowsPerWG - 1) / kRowsPerWG);
+  llm_int8_colmax_kernel<<<grid, 256, 0, stream>>>(reinterpret_cast<unsigned*>(colmax), x, rows, K);
+  return 0;
+}
+
+int launch_llm_int8_select(const float* colmax, int K, float threshold, int max_out, long* idx,
+                           float* sel, uint8_t* flags, hipStream_t stream) {
+  if (K <= 0 || K > kSelThreads * kSelMaxPer || max_out <= 0 || max_out > K) return -1;
+  llm_int8_select_kernel<<<1, kSelThreads, 0, stream>>>(colmax, K, threshold, max_out, idx, sel, flags);
+  return 0;
+}
+
+int launch_llm_int8_gather_w(bf16* w_out, const int8_t* wq, const float* ws, const long* idx,
+                             const float* sel, int N, int K, int max_out, hipStream_t stream) {
+  const long total = (long)N * max_out;
+  if (total == 0) return 0;
+  llm_int8_gather_w_kernel<<<(int)((total + 255) / 256), 256, 0, stream>>>(w_out, wq, ws, idx, sel,
+                                                                          N, K, max_out);
+  return 0;
+}
+
+int launch_llm_int8_gather_x(bf16* x_out, const bf16* x, const long* idx, const float* sel, int M,
+                             int K, int max_out, hipStream_t stream) {
+  const long total = (long)M * max_out;
+  if (total == 0) return 0;
+  llm_int8_gather_x_kernel<<<(int)((total + 255) / 256), 256, 0, stream>>>(x_out, x, idx, sel, M,
+                                                                          K, max_out);
+  return 0;
+}
+
+}  // namespace dli

@@ -91,6 +91,14 @@ int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* re
                          hipStream_t stream, const float* x_parts = nullptr, int splits = 0);
 int launch_quant_rowwise_int8(int8_t* q, float* scale, const bf16* x, const uint8_t* outlier,
                               int rows, int K, hipStream_t stream);
+// LLM.int8 outlier bookkeeping (int8_outlier.hip)
+int launch_llm_int8_colmax(float* colmax, const bf16* x, int rows, int K, hipStream_t stream);
+int launch_llm_int8_select(const float* colmax, int K, float threshold, int max_out, long* idx,
+                           float* sel, uint8_t* flags, hipStream_t stream);
+int launch_llm_int8_gather_w(bf16* w_out, const int8_t* wq, const float* ws, const long* idx,
+                             const float* sel, int N, int K, int max_out, hipStream_t stream);
+int launch_llm_int8_gather_x(bf16* x_out, const bf16* x, const long* idx, const float* sel, int M,
+                             int K, int max_out, hipStream_t stream);
 int launch_silu_mul_quant(uint8_t* q, float* scale, const bf16* x, int rows, int inter,
                           hipStream_t stream);
 

@@ -496,27 +496,35 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
     pass the threshold; ``threshold <= 0`` disables the decomposition."""
     M, K = x.shape
     N = wq.shape[0]
-    y_out = None
+    outl = None   # (x_out [M, J], w_out [N, J]) bf16: the outlier product
     flags = None
     if threshold > 0 and M > 0:
-        colmax = x.abs().amax(0).float()
-        vals, idx = colmax.topk(min(max_outliers, K))
-        sel = vals > threshold
-        flags = torch.zeros(K, dtype=torch.uint8, device=x.device).scatter_(0, idx, sel.to(torch.uint8))
-        xo = x.index_select(1, idx) * sel.to(x.dtype)
-        wo = (wq.index_select(1, idx).float() * ws[:, None]).to(x.dtype)
-        y_out = xo @ wo.t()
+        J = min(max_outliers, K)
+        if _gpu(x) and K % 8 == 0:   # int8_outlier.hip: colmax / radix select / two gathers
+            flags, xo, wo = native().llm_int8_outliers(x.contiguous(), wq, ws.float().contiguous(),
+                                                       float(threshold), int(J))
+        else:
+            colmax = x.abs().amax(0).float()
+            vals, idx = colmax.topk(J)
+            sel = vals > threshold
+            flags = torch.zeros(K, dtype=torch.uint8, device=x.device).scatter_(0, idx, sel.to(torch.uint8))
+            xo = x.index_select(1, idx) * sel.to(x.dtype)
+            wo = (wq.index_select(1, idx).float() * ws[:, None]).to(x.dtype)
+        outl = (xo, wo)
     xq, xs = quant_rowwise_int8(x, flags)
     if _gpu(x) and N % 256 == 0 and K % 128 == 0 and M > 0:
         sp = tile_gemm_splits(max(M, TILE_GEMM_MIN_M), N, K, elem_bytes=1) or 1
         y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
         ws_ = torch.empty(sp * M * N, dtype=torch.float32, device=x.device) if sp > 1 else None
         native().gemm_tile(y, xq, wq, int(sp), 0, ws_, xs, ws)
-    else:  # CPU / untileable shapes: dequantised reference
-        y = ((xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()).to(torch.bfloat16)
-    if y_out is not None:
-        y = (y.float() + y_out.float()).to(torch.bfloat16)
-    return y
+        if outl is not None:   # y += x_out . w_out^T in one hipBLASLt call (bf16 C input)
+            y.addmm_(outl[0], outl[1].t())
+        return y
+    # CPU / untileable shapes: dequantised reference
+    y = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()
+    if outl is not None:
+        y = y + outl[0].float() @ outl[1].float().t()
+    return y.to(torch.bfloat16)
 
 
 def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,

@@ -184,6 +184,45 @@ def test_llm_int8_linear_gpu_matches_cpu_and_bf16(gpu):
     assert ((y_gpu - ref).norm() / ref.norm()).item() < 0.02
 
 
+def _llm_int8_outliers_ref(x, wq, ws, threshold, J):
+    """fp32 PyTorch reference of int8_outlier.hip: the <= J largest column maxima above
+    `threshold` (distinct values), in column order, padded with (column 0, weight 0)."""
+    colmax = x.float().abs().amax(0)
+    vals, _ = colmax.sort(descending=True)
+    t = threshold if (colmax > threshold).sum() <= J else max(threshold, vals[J].item())
+    on = colmax > t
+    cols = on.nonzero().flatten()
+    idx = torch.zeros(J, dtype=torch.long)
+    idx[:cols.numel()] = cols
+    sel = torch.zeros(J)
+    sel[:cols.numel()] = 1.0
+    xo = (x.float()[:, idx] * sel).to(torch.bfloat16)
+    wo = ((wq.float()[:, idx] * ws[:, None]).to(torch.bfloat16).float() * sel).to(torch.bfloat16)
+    return on.to(torch.uint8), xo, wo
+
+
+# (K, outlier columns planted): below the 64-column cap (threshold cut) and above it (radix
+# select of the 65th largest column maximum), K = 28672 is the 70B down projection (28 / thread)
+@pytest.mark.parametrize("K,n_out", [(1024, 5), (8192, 40), (8192, 300), (28672, 1000), (4096, 0)])
+def test_llm_int8_outlier_kernels_match_reference(gpu, K, n_out):
+    torch.manual_seed(K + n_out)
+    M, N, J = 96, 512, 64
+    x = torch.randn(M, K) * 0.5
+    cols = torch.randperm(K)[:n_out]
+    xb = x.to(torch.bfloat16)
+    # distinct bf16 magnitudes >= 8 (consecutive bit patterns: no ties at the cut), random rows
+    planted = (torch.randperm(n_out).to(torch.int16) + 0x4100).view(torch.bfloat16)
+    xb[torch.randint(0, M, (n_out,)), cols] = planted
+    wq = torch.randint(-127, 128, (N, K), dtype=torch.int8)
+    ws = torch.rand(N) * 0.01 + 1e-3
+    flags, xo, wo = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J)
+    rf, rx, rw = _llm_int8_outliers_ref(xb, wq, ws, 6.0, J)
+    assert int(flags.sum()) == min(n_out, J)
+    assert torch.equal(flags.cpu(), rf)
+    assert torch.equal(xo.cpu(), rx)
+    assert torch.equal(wo.cpu(), rw)
+
+
 # ------------------------------------------------- stream-K tail (gemm_tile splits = 0, SkArgs)
 def _sk_workspace(gpu):
     n = ops.native().gemm_tile_sk_workspace_floats()
