@@ -4,7 +4,7 @@
 // Static shapes for graph capture: at most `max_out` columns (the largest ones passing the
 // threshold) are taken.  Four kernels replace a torch chain of abs / amax / topk / scatter /
 // gathers / casts:
-//   * llm_int8_colmax_kernel     colmax[k] = max_m |x[m, k]|   (atomicMax on the float bits)
+//   * llm_int8_colmax_kernel     colmax[k] = max_m |x[m, k]|   (LDS row-lane fold, one store)
 //   * llm_int8_select_kernel     one workgroup: the <= max_out largest columns above threshold,
 //                                in column order -> idx[max_out] (padded), sel[max_out], flags[K]
 //   * llm_int8_gather_w_kernel   w_out[n, j] = bf16(wq[n, idx[j]] * ws[n]) * sel[j]
@@ -13,24 +13,50 @@
 
 namespace dli {
 
-// grid (ceil(K/8 / 256), ceil(rows / kRowsPerWG)); colmax (as uint bits) zeroed by the caller.
-constexpr int kRowsPerWG = 32;
+// One workgroup per 64 columns: 256 threads = 8 column vectors (8 bf16 each) x 32 row lanes.  A
+// wave reads 8 rows x 128 contiguous bytes per load; the 32 row-lane maxima are folded in LDS and
+// written once, so no pre-zeroing memset and no atomics.  grid = ceil(K / 64) (>= 128 workgroups
+// for the Llama K = 8192 / 28672 projections).
+constexpr int kColVecs = 8, kRowLanes = 32;
 
-__global__ void __launch_bounds__(256) llm_int8_colmax_kernel(unsigned* __restrict__ colmax,
+__global__ void __launch_bounds__(256) llm_int8_colmax_kernel(float* __restrict__ colmax,
                                                               const bf16* __restrict__ x,
                                                               int rows, int K) {
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;   // 8-column vector index
-  if (v * 8 >= K) return;
-  const int r0 = blockIdx.y * kRowsPerWG, r1 = min(rows, r0 + kRowsPerWG);
+  __shared__ float red[kRowLanes][kColVecs * 8 + 1];
+  const int cv = threadIdx.x % kColVecs, lane = threadIdx.x / kColVecs;
+  const int v = blockIdx.x * kColVecs + cv;   // 8-column vector index
+  const bool live = v * 8 < K;
   float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int r = r0; r < r1; ++r) {
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(x + (size_t)r * K + (size_t)v * 8);
+  if (live) {
+    const bf16* p = x + (size_t)v * 8;
+    int r = lane;
+    for (; r + 3 * kRowLanes < rows; r += 4 * kRowLanes) {   // four independent loads in flight
+      bf16x8 a[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf((float)a[j]));
+      for (int u = 0; u < 4; ++u)
+        a[u] = *reinterpret_cast<const bf16x8*>(p + (size_t)(r + u * kRowLanes) * K);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf((float)a[u][j]));
+    }
+    for (; r < rows; r += kRowLanes) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(p + (size_t)r * K);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf((float)a[j]));
+    }
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j)   // non-negative floats order like their bit patterns
-    atomicMax(colmax + v * 8 + j, __float_as_uint(m[j]));
+  for (int j = 0; j < 8; ++j) red[lane][cv * 8 + j] = m[j];
+  __syncthreads();
+  if (threadIdx.x < kColVecs * 8) {
+    const int c = threadIdx.x;
+    float r = red[0][c];
+#pragma unroll
+    for (int l = 1; l < kRowLanes; ++l) r = fmaxf(r, red[l][c]);
+    const int col = blockIdx.x * kColVecs * 8 + c;
+    if (col < K) colmax[col] = r;
+  }
 }
 
 // One 1024-thread workgroup; thread t owns the contiguous columns [t * per, t * per + per) in
@@ -162,10 +188,9 @@ __global__ void __launch_bounds__(256) llm_int8_gather_x_kernel(
 
 int launch_llm_int8_colmax(float* colmax, const bf16* x, int rows, int K, hipStream_t stream) {
   if (K % 8 != 0 || rows < 0) return -1;
-  if (hipMemsetAsync(colmax, 0, (size_t)K * sizeof(float), stream) != hipSuccess) return -2;
-  if (rows == 0) return 0;
-  dim3 grid((K / 8 + 255) / 256, (rows + kRowsPerWG - 1) / kRowsPerWG);
-  llm_int8_colmax_kernel<<<grid, 256, 0, stream>>>(reinterpret_cast<unsigned*>(colmax), x, rows, K);
+  if (K == 0) return 0;
+  const int grid = (K + kColVecs * 8 - 1) / (kColVecs * 8);
+  llm_int8_colmax_kernel<<<grid, kColVecs * kRowLanes, 0, stream>>>(colmax, x, rows, K);
   return 0;
 }
 

@@ -203,10 +203,12 @@ def _llm_int8_outliers_ref(x, wq, ws, threshold, J):
 
 # (K, outlier columns planted): below the 64-column cap (threshold cut) and above it (radix
 # select of the 65th largest column maximum), K = 28672 is the 70B down projection (28 / thread)
-@pytest.mark.parametrize("K,n_out", [(1024, 5), (8192, 40), (8192, 300), (28672, 1000), (4096, 0)])
-def test_llm_int8_outlier_kernels_match_reference(gpu, K, n_out):
+# M = 1 / 96 / 300 / 512: column-max row loop tail only, and the 4-deep unrolled body + tail
+@pytest.mark.parametrize("K,n_out,M", [(1024, 5, 96), (8192, 40, 512), (8192, 300, 1),
+                                       (28672, 1000, 300), (4096, 0, 96), (8200, 30, 130)])
+def test_llm_int8_outlier_kernels_match_reference(gpu, K, n_out, M):
     torch.manual_seed(K + n_out)
-    M, N, J = 96, 512, 64
+    N, J = 512, 64
     x = torch.randn(M, K) * 0.5
     cols = torch.randperm(K)[:n_out]
     xb = x.to(torch.bfloat16)
