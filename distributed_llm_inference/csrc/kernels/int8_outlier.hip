@@ -76,19 +76,50 @@ __device__ int block_sum(int c, int* red) {
   return total;
 }
 
+// Exclusive block scan: a shuffle scan per wave, then the 16 wave totals through LDS (2 barriers).
+__device__ __forceinline__ int block_exclusive_scan(int x, int* wsum, int& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  __syncthreads();   // wsum may still be read by an earlier block_sum
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int before = 0;
+  total = 0;
+#pragma unroll
+  for (int i = 0; i < kSelThreads / 64; ++i) {
+    const int t = wsum[i];
+    before += i < w ? t : 0;
+    total += t;
+  }
+  return before + inc - x;
+}
+
 __global__ void __launch_bounds__(kSelThreads) llm_int8_select_kernel(
     const float* __restrict__ colmax, int K, float threshold, int max_out, long* __restrict__ idx,
     float* __restrict__ sel, uint8_t* __restrict__ flags) {
   __shared__ int red[kSelThreads / 64];
-  __shared__ int scan[kSelThreads];
   __shared__ int hist[256];
   __shared__ unsigned s_prefix;
   __shared__ int s_rank;
   const int per = (K + kSelThreads - 1) / kSelThreads;
   const int k0 = threadIdx.x * per, n_mine = max(0, min(per, K - k0));
   unsigned v[kSelMaxPer];   // padding = +0.0, never above a positive cut
+  if ((per & 3) == 0 && n_mine == per) {   // 16-byte loads (k0 = t * per is 4-aligned)
+    const uint4* src = reinterpret_cast<const uint4*>(colmax + k0);
 #pragma unroll
-  for (int i = 0; i < kSelMaxPer; ++i) v[i] = i < n_mine ? __float_as_uint(colmax[k0 + i]) : 0u;
+    for (int i = 0; i < kSelMaxPer / 4; ++i) {
+      const uint4 q = 4 * i < per ? src[i] : make_uint4(0u, 0u, 0u, 0u);
+      v[4 * i] = q.x; v[4 * i + 1] = q.y; v[4 * i + 2] = q.z; v[4 * i + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kSelMaxPer; ++i) v[i] = i < n_mine ? __float_as_uint(colmax[k0 + i]) : 0u;
+  }
 
   // the cut t: `threshold`, or -- when more than max_out columns pass it -- the bits of the
   // (max_out + 1)-th largest column maximum, found by an MSB-first 8-bit radix select
@@ -139,16 +170,8 @@ __global__ void __launch_bounds__(kSelThreads) llm_int8_select_kernel(
   int mine = 0;
 #pragma unroll
   for (int i = 0; i < kSelMaxPer; ++i) mine += i < n_mine && v[i] > t;
-  scan[threadIdx.x] = mine;
-  __syncthreads();
-  for (int o = 1; o < kSelThreads; o <<= 1) {   // inclusive Hillis-Steele scan
-    const int add = (int)threadIdx.x >= o ? scan[threadIdx.x - o] : 0;
-    __syncthreads();
-    scan[threadIdx.x] += add;
-    __syncthreads();
-  }
-  int pos = scan[threadIdx.x] - mine;
-  const int total = scan[kSelThreads - 1];
+  int total;
+  int pos = block_exclusive_scan(mine, red, total);
 #pragma unroll
   for (int i = 0; i < kSelMaxPer; ++i) {
     if (i < n_mine) {
