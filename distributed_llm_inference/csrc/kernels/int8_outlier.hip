@@ -134,9 +134,19 @@ __global__ void __launch_bounds__(kSelThreads) llm_int8_select_kernel(
       const unsigned hmask = shift == 24 ? 0u : 0xffffffffu << (shift + 8);
       if (threadIdx.x < 256) hist[threadIdx.x] = 0;
       __syncthreads();
+      // run-length aggregated: a thread's contiguous columns mostly share the high digits, so
+      // one LDS atomic per run instead of one per column (same-bin atomics serialise)
+      int cur = 0, cnt = 0;
 #pragma unroll
-      for (int i = 0; i < kSelMaxPer; ++i)
-        if (i < n_mine && (v[i] & hmask) == prefix) atomicAdd(&hist[(v[i] >> shift) & 255], 1);
+      for (int i = 0; i < kSelMaxPer; ++i) {
+        if (i < n_mine && (v[i] & hmask) == prefix) {
+          const int b = (v[i] >> shift) & 255;
+          if (b != cur && cnt) { atomicAdd(&hist[cur], cnt); cnt = 0; }
+          cur = b;
+          ++cnt;
+        }
+      }
+      if (cnt) atomicAdd(&hist[cur], cnt);
       __syncthreads();
       if (threadIdx.x < 64) {   // wave 0: lane l holds bins 255-4l .. 252-4l (descending)
         const int l = threadIdx.x;
