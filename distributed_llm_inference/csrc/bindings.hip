@@ -455,7 +455,7 @@ void quant_rowwise_int8(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> o
 // (flags uint8 [K], x_out bf16 [M, max_out], w_out bf16 [N, max_out]) with x_out . w_out^T the
 // bf16 outlier product (padding columns are zero).  Four kernels, static shapes, no host sync.
 std::vector<Tensor> llm_int8_outliers(Tensor x, Tensor wq, Tensor ws, double threshold,
-                                      int64_t max_out) {
+                                      int64_t max_out, optional<Tensor> wq_t) {
   CHECK_IN(x); CHECK_BF16(x); CHECK_IN(wq); CHECK_IN(ws); CHECK_F32(ws);
   TORCH_CHECK(wq.scalar_type() == at::kChar, "llm_int8_outliers: wq must be int8");
   TORCH_CHECK(x.dim() == 2 && wq.dim() == 2 && wq.size(1) == x.size(1) && ws.numel() == wq.size(0),
@@ -480,10 +480,20 @@ std::vector<Tensor> llm_int8_outliers(Tensor x, Tensor wq, Tensor ws, double thr
   check_rc(dli::launch_llm_int8_gather_x(bp(xo), bp(x), idx.data_ptr<int64_t>(),
                                          sel.data_ptr<float>(), (int)M, (int)K, (int)max_out, st),
            "llm_int8_gather_x");
-  check_rc(dli::launch_llm_int8_gather_w(bp(wo), reinterpret_cast<const int8_t*>(wq.data_ptr()),
-                                         ws.data_ptr<float>(), idx.data_ptr<int64_t>(),
-                                         sel.data_ptr<float>(), (int)N, (int)K, (int)max_out, st),
-           "llm_int8_gather_w");
+  if (wq_t.has_value()) {   // transposed copy [K, N]: coalesced column gather
+    CHECK_IN((*wq_t));
+    TORCH_CHECK(wq_t->scalar_type() == at::kChar && wq_t->dim() == 2 && wq_t->size(0) == K &&
+                    wq_t->size(1) == N, "llm_int8_outliers: wq_t must be int8 [K, N]");
+    check_rc(dli::launch_llm_int8_gather_wt(bp(wo), reinterpret_cast<const int8_t*>(wq_t->data_ptr()),
+                                            ws.data_ptr<float>(), idx.data_ptr<int64_t>(),
+                                            sel.data_ptr<float>(), (int)N, (int)max_out, st),
+             "llm_int8_gather_wt");
+  } else {
+    check_rc(dli::launch_llm_int8_gather_w(bp(wo), reinterpret_cast<const int8_t*>(wq.data_ptr()),
+                                           ws.data_ptr<float>(), idx.data_ptr<int64_t>(),
+                                           sel.data_ptr<float>(), (int)N, (int)K, (int)max_out, st),
+             "llm_int8_gather_w");
+  }
   return {flags, xo, wo};
 }
 
@@ -597,7 +607,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("quant_rowwise_int8", &quant_rowwise_int8, "LLM.int8 row-wise int8 quantisation (outlier columns zeroed)",
         py::arg("q_out"), py::arg("scale"), py::arg("x"), py::arg("outlier") = py::none());
   m.def("llm_int8_outliers", &llm_int8_outliers,
-        "LLM.int8 outlier columns: (flags, x_out, w_out) for the bf16 outlier product");
+        "LLM.int8 outlier columns: (flags, x_out, w_out) for the bf16 outlier product",
+        py::arg("x"), py::arg("wq"), py::arg("ws"), py::arg("threshold"), py::arg("max_out"),
+        py::arg("wq_t") = py::none());
   m.def("silu_mul_quant", &silu_mul_quant, "SwiGLU fused with row-wise fp8 quantisation");
   m.def("gemm_tile", &gemm_tile, "C = A . B^T, 256x256 LDS-DMA 8-phase MFMA tile GEMM",
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,

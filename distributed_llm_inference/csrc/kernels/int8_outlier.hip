@@ -8,6 +8,7 @@
 //   * llm_int8_select_kernel     one workgroup: the <= max_out largest columns above threshold,
 //                                in column order -> idx[max_out] (padded), sel[max_out], flags[K]
 //   * llm_int8_gather_w_kernel   w_out[n, j] = bf16(wq[n, idx[j]] * ws[n]) * sel[j]
+//   * llm_int8_gather_wt_kernel  same from the transposed copy wqT [K, N] (coalesced)
 //   * llm_int8_gather_x_kernel   x_out[m, j] = x[m, idx[j]] * sel[j]
 #include "kernels.h"
 
@@ -234,12 +235,41 @@ int launch_llm_int8_select(const float* colmax, int K, float threshold, int max_
   return 0;
 }
 
+// Same product from the transposed weight copy wqT [K, N] (kept resident on 288 GB parts): a
+// 64 (n) x 64 (j) tile reads 64 contiguous bytes of row idx[j] per wave, transposes through LDS
+// and writes 64 contiguous bf16 of w_out row n -- instead of 64 scattered bytes per weight row.
+__global__ void __launch_bounds__(256) llm_int8_gather_wt_kernel(
+    bf16* __restrict__ w_out, const int8_t* __restrict__ wqT, const float* __restrict__ ws,
+    const long* __restrict__ idx, const float* __restrict__ sel, int N, int max_out) {
+  __shared__ float tile[64][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
+  for (int jj = ty; jj < 64; jj += 4) {
+    const int j = j0 + jj, n = n0 + tx;
+    tile[jj][tx] = (j < max_out && n < N) ? (float)wqT[(size_t)idx[j] * N + n] : 0.f;
+  }
+  __syncthreads();
+  for (int nn = ty; nn < 64; nn += 4) {
+    const int n = n0 + nn, j = j0 + tx;
+    if (n < N && j < max_out)
+      w_out[(size_t)n * max_out + j] = (bf16)((tile[tx][nn] * ws[n]) * sel[j]);
+  }
+}
+
 int launch_llm_int8_gather_w(bf16* w_out, const int8_t* wq, const float* ws, const long* idx,
                              const float* sel, int N, int K, int max_out, hipStream_t stream) {
   const long total = (long)N * max_out;
   if (total == 0) return 0;
   llm_int8_gather_w_kernel<<<(int)((total + 255) / 256), 256, 0, stream>>>(w_out, wq, ws, idx, sel,
                                                                           N, K, max_out);
+  return 0;
+}
+
+int launch_llm_int8_gather_wt(bf16* w_out, const int8_t* wqT, const float* ws, const long* idx,
+                              const float* sel, int N, int max_out, hipStream_t stream) {
+  if ((long)N * max_out == 0) return 0;
+  dim3 grid((N + 63) / 64, (max_out + 63) / 64);
+  llm_int8_gather_wt_kernel<<<grid, 256, 0, stream>>>(w_out, wqT, ws, idx, sel, N, max_out);
   return 0;
 }
 

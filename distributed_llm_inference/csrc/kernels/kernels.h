@@ -97,6 +97,8 @@ int launch_llm_int8_select(const float* colmax, int K, float threshold, int max_
                            float* sel, uint8_t* flags, hipStream_t stream);
 int launch_llm_int8_gather_w(bf16* w_out, const int8_t* wq, const float* ws, const long* idx,
                              const float* sel, int N, int K, int max_out, hipStream_t stream);
+int launch_llm_int8_gather_wt(bf16* w_out, const int8_t* wqT, const float* ws, const long* idx,
+                              const float* sel, int N, int max_out, hipStream_t stream);
 int launch_llm_int8_gather_x(bf16* x_out, const bf16* x, const long* idx, const float* sel, int M,
                              int K, int max_out, hipStream_t stream);
 int launch_silu_mul_quant(uint8_t* q, float* scale, const bf16* x, int rows, int inter,

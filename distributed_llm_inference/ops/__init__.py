@@ -485,7 +485,8 @@ LLM_INT8_MAX_OUTLIERS = 64   # static outlier-column capacity (graph-capturable 
 
 
 def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, threshold: float = 6.0,
-                    max_outliers: int = LLM_INT8_MAX_OUTLIERS) -> torch.Tensor:
+                    max_outliers: int = LLM_INT8_MAX_OUTLIERS,
+                    wq_t: Optional[torch.Tensor] = None) -> torch.Tensor:
     """LLM.int8 matmul ``x [M, K] @ W^T`` with ``W ~= wq * ws[:, None]`` (int8, per-channel).
 
     Mixed-precision decomposition as in bitsandbytes ``Linear8bitLt(threshold=...)``: feature
@@ -493,7 +494,9 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
     (with the dequantised weight columns); every other column goes through per-row int8
     quantisation and the int8 MFMA tile GEMM (``gemm_tile.hip``, v_mfma_i32_16x16x64_i8).  To keep
     shapes static (hipGraph decode) the outlier set is the ``max_outliers`` largest columns that
-    pass the threshold; ``threshold <= 0`` disables the decomposition."""
+    pass the threshold; ``threshold <= 0`` disables the decomposition.  ``wq_t``: optional
+    transposed copy ``[K, N]`` of ``wq`` (GPU) that makes the outlier weight-column gather
+    coalesced."""
     M, K = x.shape
     N = wq.shape[0]
     outl = None   # (x_out [M, J], w_out [N, J]) bf16: the outlier product
@@ -502,7 +505,7 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
         J = min(max_outliers, K)
         if _gpu(x) and K % 8 == 0:   # int8_outlier.hip: colmax / radix select / two gathers
             flags, xo, wo = native().llm_int8_outliers(x.contiguous(), wq, ws.float().contiguous(),
-                                                       float(threshold), int(J))
+                                                       float(threshold), int(J), wq_t)
         else:
             colmax = x.abs().amax(0).float()
             vals, idx = colmax.topk(J)

@@ -223,6 +223,10 @@ def test_llm_int8_outlier_kernels_match_reference(gpu, K, n_out, M):
     assert torch.equal(flags.cpu(), rf)
     assert torch.equal(xo.cpu(), rx)
     assert torch.equal(wo.cpu(), rw)
+    # the coalesced gather from the transposed weight copy gives the same bits
+    wq_t = wq.t().contiguous().to(gpu)
+    _, _, wo_t = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J, wq_t)
+    assert torch.equal(wo_t.cpu(), rw)
 
 
 # ------------------------------------------------- stream-K tail (gemm_tile splits = 0, SkArgs)
