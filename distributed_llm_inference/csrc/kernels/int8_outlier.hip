@@ -235,24 +235,45 @@ int launch_llm_int8_select(const float* colmax, int K, float threshold, int max_
   return 0;
 }
 
-// Same product from the transposed weight copy wqT [K, N] (kept resident on 288 GB parts): a
-// 64 (n) x 64 (j) tile reads 64 contiguous bytes of row idx[j] per wave, transposes through LDS
-// and writes 64 contiguous bf16 of w_out row n -- instead of 64 scattered bytes per weight row.
+// Same product from the transposed weight copy wqT [K, N]: a workgroup covers 256 n x 16 j.  Each
+// wave reads 4 rows idx[j] as 256 contiguous bytes each (4 independent dword loads per lane), the
+// tile is transposed through LDS, and lane n writes its 16 outputs as two 16-byte stores.
+// Requires N % 4 == 0 (launcher).
 __global__ void __launch_bounds__(256) llm_int8_gather_wt_kernel(
     bf16* __restrict__ w_out, const int8_t* __restrict__ wqT, const float* __restrict__ ws,
     const long* __restrict__ idx, const float* __restrict__ sel, int N, int max_out) {
-  __shared__ float tile[64][65];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * 64, j0 = blockIdx.y * 64;
-  for (int jj = ty; jj < 64; jj += 4) {
-    const int j = j0 + jj, n = n0 + tx;
-    tile[jj][tx] = (j < max_out && n < N) ? (float)wqT[(size_t)idx[j] * N + n] : 0.f;
+  __shared__ float tile[16][257];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n0 = blockIdx.x * 256, j0 = blockIdx.y * 16;
+  const int nl = n0 + 4 * lane;
+  unsigned q[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = j0 + wv * 4 + u;
+    q[u] = (j < max_out && nl < N)
+               ? *reinterpret_cast<const unsigned*>(wqT + (size_t)idx[j] * N + nl) : 0u;
   }
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+      tile[wv * 4 + u][4 * lane + b] = (float)(int8_t)((q[u] >> (8 * b)) & 255u);
   __syncthreads();
-  for (int nn = ty; nn < 64; nn += 4) {
-    const int n = n0 + nn, j = j0 + tx;
-    if (n < N && j < max_out)
-      w_out[(size_t)n * max_out + j] = (bf16)((tile[tx][nn] * ws[n]) * sel[j]);
+  const int n = n0 + threadIdx.x;
+  if (n >= N) return;
+  const float sn = ws[n];
+  bf16* dst = w_out + (size_t)n * max_out + j0;
+  if ((max_out & 7) == 0 && j0 + 16 <= max_out) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (bf16)((tile[8 * h + i][threadIdx.x] * sn) * sel[j0 + 8 * h + i]);
+      *reinterpret_cast<bf16x8*>(dst + 8 * h) = o;
+    }
+  } else {
+    for (int i = 0; i < 16 && j0 + i < max_out; ++i)
+      dst[i] = (bf16)((tile[i][threadIdx.x] * sn) * sel[j0 + i]);
   }
 }
 
@@ -267,8 +288,9 @@ int launch_llm_int8_gather_w(bf16* w_out, const int8_t* wq, const float* ws, con
 
 int launch_llm_int8_gather_wt(bf16* w_out, const int8_t* wqT, const float* ws, const long* idx,
                               const float* sel, int N, int max_out, hipStream_t stream) {
+  if (N % 4 != 0) return -1;
   if ((long)N * max_out == 0) return 0;
-  dim3 grid((N + 63) / 64, (max_out + 63) / 64);
+  dim3 grid((N + 255) / 256, (max_out + 15) / 16);
   llm_int8_gather_wt_kernel<<<grid, 256, 0, stream>>>(w_out, wqT, ws, idx, sel, N, max_out);
   return 0;
 }

@@ -53,11 +53,11 @@ class Linear(nn.Module):
         per-channel absmax int8 + bf16 outlier-column decomposition at run time."""
         q, s = ops.quantize_weight_int8(self.weight.data)
         self.weight_int8, self.weight_scale = q, s
-        # DLI_INT8_WT=1 (GPU): keep a transposed [K, N] copy (1 byte/param) so the per-product
-        # outlier weight-column gather reads rows (int8_outlier.hip gather_wt).  Off by default:
-        # measured 3.8 vs 2.9 ms/step for the row-major gather on the 70B --int8 bench.
+        # GPU: keep a transposed [K, N] copy (1 byte/param, affordable in 288 GB) so the
+        # per-product outlier weight-column gather reads contiguous rows (int8_outlier.hip
+        # gather_wt): 1.6 vs 2.9 ms/step on the 70B --int8 bench.  DLI_INT8_WT=0 disables it.
         self.weight_int8_t = q.t().contiguous() if q.is_cuda and os.environ.get(
-            "DLI_INT8_WT", "0") == "1" else None
+            "DLI_INT8_WT", "1") == "1" else None
         self.int8_threshold = float(threshold)
         if not keep_bf16:
             self.weight = nn.Parameter(torch.empty(0, dtype=self.weight.dtype,
