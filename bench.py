@@ -17,13 +17,21 @@ reported.  Prefill and W warmup steps (incl. hipGraph capture) run before the ti
 """
 from __future__ import annotations
 
-import argparse
-import json
 import os
-import random
-import statistics
-import sys
-import time
+
+# Before torch / any HIP call: RCCL's cross-process buffer sharing on this ROCm needs the dmabuf
+# IPC mode (the legacy mode fails with `hipIpcGetMemHandle: invalid argument`); the driver runs this
+# file directly under torchrun, not through distributed_llm_inference.launcher.
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+# per-rank device time per micro-batch step and RCCL receive stalls (HIP events; cheap)
+os.environ.setdefault("DLI_STAGE_TIMING", "1")
+
+import argparse  # noqa: E402
+import json  # noqa: E402
+import random  # noqa: E402
+import statistics  # noqa: E402
+import sys  # noqa: E402
+import time  # noqa: E402
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
@@ -48,6 +56,26 @@ def parse():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
+
+
+def _rank_record(node, rank: int, window_s: float) -> dict:
+    """This rank's share of the timed window (between the last two barriers): stage range,
+    data-plane transport, device compute per micro-batch step, receive stalls, traffic."""
+    from distributed_llm_inference.runtime.faults import snapshot_delta
+    ex = node.ex
+    rec = {"rank": rank, "stage": [ex.stage.start, ex.stage.end], "device": str(ex.device)}
+    rec.update(node.tr.describe())
+    if len(node.snapshots) >= 2:
+        d = snapshot_delta(node.snapshots[-2], node.snapshots[-1])
+        n = max(int(d.get("steps", 0)), 1)
+        rec.update({
+            "mb_steps": int(d.get("steps", 0)),
+            "device_ms_per_mb_step": round(d.get("device_ms", 0.0) / n, 3),
+            "device_busy_frac": round(d.get("device_ms", 0.0) / 1e3 / window_s, 4) if window_s else None,
+            "recv_wait_ms_per_mb_step": round(d.get("recv_wait_ms", 0.0) / n, 3),
+            "bytes_sent": int(d.get("bytes_sent", 0)), "bytes_recv": int(d.get("bytes_recv", 0)),
+        })
+    return rec
 
 
 def main():
@@ -87,6 +115,7 @@ def main():
         interval = obj.barrier_times[-1] - obj.barrier_times[-2] if len(obj.barrier_times) >= 2 else 0.0
         t = torch.tensor([interval], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_gather_object([None] * world, _rank_record(obj, rank, float(t.item())))
         dist.barrier()
         obj.close()
         dist.destroy_process_group()
@@ -129,6 +158,8 @@ def main():
         drv.stop()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, _rank_record(drv, rank, elapsed))
         dist.barrier()
     toks = n1 - n0
     if toks != a.steps * G:
@@ -160,7 +191,7 @@ def main():
                    "parallelism": f"pp{a.gpus}"},
         "p50_token_latency_ms": round(p50, 3),
         "p90_token_latency_ms": round(p90, 3),
-        "transport": type(getattr(drv, "tr", None)).__name__ if world > 1 else "none",
+        "transport": drv.tr.describe()["transport"] if world > 1 else "none",
         "micro_batches": M,
         "batch_per_micro_batch": a.batch_per_mb,
         "prompt_len": a.prompt_len,
@@ -172,6 +203,13 @@ def main():
         "kv_blocks": int(drv.sched.total_blocks),
         "kv_blocks_needed": int(G * drv.sched.blocks_for(a.prompt_len + params.max_tokens)),
     }
+    if world > 1:
+        res["stage_ranges"] = [r["stage"] for r in per_rank]
+        res["per_rank"] = per_rank
+    if a.model != "llama-3-70b":
+        # the headline metric names its model; a run of another model says what it measured
+        res["metric"] = (f"output tokens/sec (whole node) + p50 token latency, "
+                         f"{res['config']['model']} PP={a.gpus}")
     line = json.dumps(res)
     print(line, flush=True)
     if a.json_out:

@@ -253,6 +253,11 @@ PRESETS: Dict[str, ModelSpec] = {
         name="tiny-llama", vocab_size=512, hidden_size=128, intermediate_size=256, num_layers=4,
         num_heads=4, num_kv_heads=2, head_dim=32, max_position_embeddings=2048,
         rope_theta=10000.0, bos_token_id=1, eos_token_id=2),
+    # 8 layers: one per rank in the 8-rank CPU rehearsals of the PP=8 paths
+    "tiny-llama-8l": ModelSpec(
+        name="tiny-llama-8l", vocab_size=512, hidden_size=128, intermediate_size=256, num_layers=8,
+        num_heads=4, num_kv_heads=2, head_dim=32, max_position_embeddings=2048,
+        rope_theta=10000.0, bos_token_id=1, eos_token_id=2),
     "tiny-gpt2": ModelSpec(
         name="tiny-gpt2", arch="gpt2", vocab_size=512, hidden_size=128, intermediate_size=512,
         num_layers=4, num_heads=4, num_kv_heads=4, head_dim=32, max_position_embeddings=512,

@@ -122,13 +122,18 @@ __global__ void __launch_bounds__(kSelThreads) llm_int8_select_kernel(
     for (int i = 0; i < kSelMaxPer; ++i) v[i] = i < n_mine ? __float_as_uint(colmax[k0 + i]) : 0u;
   }
 
-  // the cut t: `threshold`, or -- when more than max_out columns pass it -- the bits of the
-  // (max_out + 1)-th largest column maximum, found by an MSB-first 8-bit radix select
+  // the cut: |x| >= `threshold` (bitsandbytes Linear8bitLt's outlier test), or -- when more than
+  // max_out columns pass it -- strictly above the bits t of the (max_out + 1)-th largest column
+  // maximum, found by an MSB-first 8-bit radix select.  Tie policy: columns tied AT that radix cut
+  // are all dropped (deterministic, <= max_out kept); ops.llm_int8_linear's CPU path applies the
+  // same rule.  Column maxima are >= +0.0, so unsigned bit order is float order.
   unsigned t = __float_as_uint(fmaxf(threshold, 0.f));
+  bool strict = false;
   int c = 0;
 #pragma unroll
-  for (int i = 0; i < kSelMaxPer; ++i) c += v[i] > t;
+  for (int i = 0; i < kSelMaxPer; ++i) c += i < n_mine && v[i] >= t;
   if (block_sum(c, red) > max_out) {
+    strict = true;
     unsigned prefix = 0;
     int r = max_out + 1;   // rank (from the top) of the value being located
     for (int shift = 24; shift >= 0; shift -= 8) {
@@ -180,13 +185,13 @@ __global__ void __launch_bounds__(kSelThreads) llm_int8_select_kernel(
   // compaction in column order (block-wide exclusive scan of per-thread counts)
   int mine = 0;
 #pragma unroll
-  for (int i = 0; i < kSelMaxPer; ++i) mine += i < n_mine && v[i] > t;
+  for (int i = 0; i < kSelMaxPer; ++i) mine += i < n_mine && (strict ? v[i] > t : v[i] >= t);
   int total;
   int pos = block_exclusive_scan(mine, red, total);
 #pragma unroll
   for (int i = 0; i < kSelMaxPer; ++i) {
     if (i < n_mine) {
-      const bool on = v[i] > t;
+      const bool on = strict ? v[i] > t : v[i] >= t;
       flags[k0 + i] = on ? 1 : 0;
       if (on && pos < max_out) {
         idx[pos] = k0 + i;

@@ -53,11 +53,13 @@ class Linear(nn.Module):
         per-channel absmax int8 + bf16 outlier-column decomposition at run time."""
         q, s = ops.quantize_weight_int8(self.weight.data)
         self.weight_int8, self.weight_scale = q, s
-        # GPU: keep a transposed [K, N] copy (1 byte/param, affordable in 288 GB) so the
-        # per-product outlier weight-column gather reads contiguous rows (int8_outlier.hip
-        # gather_wt): 1.6 vs 2.9 ms/step on the 70B --int8 bench.  DLI_INT8_WT=0 disables it.
+        # Optional (DLI_INT8_WT=1): a transposed [K, N] copy so the per-product outlier
+        # weight-column gather reads contiguous rows (int8_outlier.hip gather_wt): 1.6 vs 2.9
+        # ms/step on the 70B --int8 bench (+2.5 % tok/s), but it costs a second byte per weight,
+        # i.e. the memory LLM.int8 exists to save (70B PP=1: KV blocks 9413 -> 6323, -33 %
+        # concurrent sequences).  Off by default; opt in when KV capacity is not the limit.
         self.weight_int8_t = q.t().contiguous() if q.is_cuda and os.environ.get(
-            "DLI_INT8_WT", "1") == "1" else None
+            "DLI_INT8_WT", "0") == "1" else None
         self.int8_threshold = float(threshold)
         if not keep_bf16:
             self.weight = nn.Parameter(torch.empty(0, dtype=self.weight.dtype,
@@ -151,6 +153,9 @@ class AttnMetadata:
     tile_map: Optional[torch.Tensor] = None
     # rows (token index) whose hidden state feeds the LM head, or None = all rows
     logits_rows: Optional[torch.Tensor] = None
+    # caller-supplied pre-inverted additive 4-D mask [B, 1|nh, T, >= L] (LlamaBlock.forward's
+    # reference-compatible path): replaces the in-kernel causal mask
+    custom_mask: Optional[torch.Tensor] = None
 
     @property
     def windowed(self) -> bool:

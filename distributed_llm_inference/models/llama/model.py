@@ -138,7 +138,25 @@ class LlamaBlock(nn.Module):
             raise ValueError("cache is bound to a different layer set")
 
         # which new tokens are real (padding support)
-        if attention_mask is not None:
+        custom = None
+        if attention_mask is not None and attention_mask.dim() == 4:
+            # reference model.py:115-119: a 4-D mask comes pre-inverted (additive, max == 0) and
+            # is used as-is, sliced to the key length (modules.py:92-94); every new token is real
+            if attention_mask.shape[0] != B or attention_mask.shape[2] != T or \
+                    attention_mask.shape[1] not in (1, self.config.num_heads):
+                raise ValueError(f"4-D attention_mask must be [batch={B}, 1 or num_heads, "
+                                 f"seq={T}, key_len], got {tuple(attention_mask.shape)}")
+            if attention_mask.max() != 0:
+                raise ValueError("Custom 4D attention mask should be passed in inverted form "
+                                 "with max==0")
+            if cache.window_length:
+                raise ValueError("4-D attention masks need a full (non-windowed) cache")
+            custom = attention_mask
+            am = torch.ones(B, T, dtype=torch.bool, device=dev)
+        elif attention_mask is not None:
+            if attention_mask.dim() != 2:
+                raise ValueError("attention_mask must be [batch, seq] (1 = token) or a pre-inverted "
+                                 f"4-D mask, got {attention_mask.dim()} dims")
             am = attention_mask[:, -T:].to(torch.bool)
         else:
             am = torch.ones(B, T, dtype=torch.bool, device=dev)
@@ -158,6 +176,12 @@ class LlamaBlock(nn.Module):
         sids = [rows[b] for b in keep]
         qls = [int(q_lens[b]) for b in keep]
         meta = cache.pool.build_metadata(sids, qls)
+        if custom is not None:
+            L_max = int(meta.seq_lens.max())
+            if custom.shape[-1] < L_max:
+                raise ValueError(f"4-D attention_mask key length {custom.shape[-1]} < {L_max} "
+                                 "cached + new tokens")
+            meta.custom_mask = custom.to(dev)
         # explicit positions override the default past_len + arange
         pos_src = position_ids if position_ids is not None else (
             cache_position.unsqueeze(0).expand(B, -1) if cache_position is not None else None)

@@ -81,7 +81,14 @@ class LlamaAttention(nn.Module):
                                    self.num_kv_heads, self.head_dim, k_cache, v_cache,
                                    window=meta.window, want_sink=meta.want_sink,
                                    k_scale=meta.k_scale, v_scale=meta.v_scale)
-        if meta.is_decode:
+        if meta.custom_mask is not None:
+            # reference-API custom 4-D mask (rare, explicit): masked softmax in torch over the
+            # keys gathered from the paged cache the RoPE kernel just wrote
+            from ...ops import reference as ref
+            o = ref.attn_custom_mask(q, k_cache, v_cache, meta.block_tables, meta.seq_lens,
+                                     meta.q_start, self.scale, meta.custom_mask,
+                                     meta.k_scale, meta.v_scale)
+        elif meta.is_decode:
             o = ops.attn_decode(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
                                 self.scale, meta.n_sink, meta.sink_pad, meta.ring, meta.window,
                                 num_splits=meta.num_splits, workspace=meta.workspace,

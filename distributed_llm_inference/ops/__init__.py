@@ -482,6 +482,7 @@ def quant_rowwise_int8(x: torch.Tensor, outlier: Optional[torch.Tensor] = None
 
 
 LLM_INT8_MAX_OUTLIERS = 64   # static outlier-column capacity (graph-capturable shapes)
+LLM_INT8_SELECT_MAX_K = 32768   # int8_outlier.hip select kernel: 1024 threads x 32 columns
 
 
 def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, threshold: float = 6.0,
@@ -503,16 +504,31 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
     flags = None
     if threshold > 0 and M > 0:
         J = min(max_outliers, K)
-        if _gpu(x) and K % 8 == 0:   # int8_outlier.hip: colmax / radix select / two gathers
+        # int8_outlier.hip: colmax / radix select / two gathers (select: K <= 1024 x 32 columns;
+        # the coalesced gather from the transposed copy needs N % 4 == 0)
+        if _gpu(x) and K % 8 == 0 and K <= LLM_INT8_SELECT_MAX_K:
+            if wq_t is not None and N % 4 != 0:
+                wq_t = None
             flags, xo, wo = native().llm_int8_outliers(x.contiguous(), wq, ws.float().contiguous(),
                                                        float(threshold), int(J), wq_t)
         else:
+            # same rule as the kernel: |x| >= threshold; above J such columns, strictly above
+            # the (J+1)-th largest column maximum (ties at that cut dropped)
             colmax = x.abs().amax(0).float()
-            vals, idx = colmax.topk(J)
-            sel = vals > threshold
-            flags = torch.zeros(K, dtype=torch.uint8, device=x.device).scatter_(0, idx, sel.to(torch.uint8))
+            n_pass = int((colmax >= threshold).sum())
+            if n_pass > J:
+                cut = colmax.topk(J + 1).values[-1]
+                on = colmax > cut
+            else:
+                on = colmax >= threshold
+            cols = on.nonzero().flatten()
+            idx = torch.zeros(J, dtype=torch.long, device=x.device)
+            idx[:cols.numel()] = cols
+            sel = torch.zeros(J, dtype=torch.bool, device=x.device)
+            sel[:cols.numel()] = True
+            flags = on.to(torch.uint8)
             xo = x.index_select(1, idx) * sel.to(x.dtype)
-            wo = (wq.index_select(1, idx).float() * ws[:, None]).to(x.dtype)
+            wo = (wq.index_select(1, idx).float() * ws[:, None] * sel).to(x.dtype)
         outl = (xo, wo)
     xq, xs = quant_rowwise_int8(x, flags)
     if _gpu(x) and N % 256 == 0 and K % 128 == 0 and M > 0:

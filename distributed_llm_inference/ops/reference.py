@@ -192,6 +192,32 @@ def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, s
     return out
 
 
+def attn_custom_mask(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale, mask,
+                     k_scale=1.0, v_scale=1.0) -> torch.Tensor:
+    """Attention under a caller-supplied pre-inverted additive mask (reference model.py:115-119,
+    modules.py:92-94): ``scores = q k^T * scale + mask[b, :, :, :L]``, fp32 softmax.  ``mask`` is
+    [B, 1 | nh, T_b, >= L] with 0 = attend, large negative = masked; row b's queries are the last
+    T_b positions of its L cached keys (full, non-windowed cache).  No causal mask is added: the
+    custom mask IS the mask, exactly as in the reference."""
+    out = torch.zeros_like(q)
+    nh = q.shape[1]
+    for b in range(seq_lens.numel()):
+        s0, s1 = int(q_start[b]), int(q_start[b + 1])
+        ql = s1 - s0
+        if ql == 0:
+            continue
+        L = int(seq_lens[b])
+        K, V = _gather_seq(k_cache, v_cache, block_tables[b], L, k_scale, v_scale)
+        G = nh // K.shape[1]
+        Kf = K.float().repeat_interleave(G, dim=1)
+        Vf = V.float().repeat_interleave(G, dim=1)
+        scores = torch.einsum("nhd,shd->hns", q[s0:s1].float(), Kf) * scale    # [nh, ql, L]
+        mb = mask[b, :, -ql:, :L].to(device=q.device, dtype=torch.float32)    # [1|nh, ql, L]
+        p = torch.softmax(scores + mb, dim=-1)
+        out[s0:s1] = torch.einsum("hns,shd->nhd", p, Vf).to(q.dtype)
+    return out
+
+
 # ----------------------------------------------------------------------------- sampling
 def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
            top_k: Optional[torch.Tensor] = None, top_p: Optional[torch.Tensor] = None,

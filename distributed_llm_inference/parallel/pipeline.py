@@ -239,6 +239,7 @@ class DistributedDriver(DriverBase):
         self.faults = FaultInjector(0)
         self.stats = StageStats(0, executor.device)
         self.stats.transport = transport
+        self.snapshots: List[dict] = []   # StageStats.snapshot() at every barrier
 
     def _issue(self, plan: StepPlan) -> None:
         self.ch.ctrl.send(msgpack.packb(plan.to_wire()), self.timeout)
@@ -262,6 +263,7 @@ class DistributedDriver(DriverBase):
             torch.cuda.synchronize()
         if kind == "barrier":
             dist.barrier(group=self.group)
+            self.snapshots.append(self.stats.snapshot())
 
     def close(self) -> None:
         """After :meth:`stop`: wait for every rank to finish, then tear down the RCCL
@@ -281,6 +283,7 @@ class StageFollower:
         self.timeout = timeout
         self.is_last = rank == world - 1
         self.barrier_times: List[float] = []
+        self.snapshots: List[dict] = []   # StageStats.snapshot() at every barrier
         self.faults = FaultInjector(rank)
         self.stats = StageStats(rank, executor.device)
         self.stats.transport = transport
@@ -334,6 +337,7 @@ class StageFollower:
                 self._pub_q.join()
                 dist.barrier(group=self.group)
                 self.barrier_times.append(time.perf_counter())
+                self.snapshots.append(self.stats.snapshot())
                 continue
             plan = StepPlan.from_wire(msg)
             if not plan.seq_ids:
@@ -368,15 +372,17 @@ class StageFollower:
 def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
                    rccl_timeout_s: float = 300.0) -> Transport:
     """RCCL P2P on GPUs (default); ``DLI_TRANSPORT=host`` stages GPU tensors through gloo
-    (several ranks sharing one GPU); gloo on CPU.
+    (several ranks sharing one GPU — an explicit opt-in, never chosen silently); gloo on CPU.
 
     RCCL initialisation is agreed on by all ranks: every rank publishes whether its communicators
     came up (a failure or a peer that never arrives ends in a timeout, not a hang), and if ANY rank
-    failed, every rank falls back to the host-staged transport together and says so on stderr."""
+    failed, EVERY rank raises :class:`TransportInitError` with the failing ranks and the error, so
+    a multi-GPU run either moves hidden states over RCCL or exits non-zero.
+    ``DLI_TRANSPORT=rccl-or-host`` restores the old agreed fallback to the host-staged transport."""
     if world == 1:
         return LoopbackTransport(1)
     kind = os.environ.get("DLI_TRANSPORT", "rccl" if device.type == "cuda" else "gloo")
-    if device.type == "cuda" and kind == "rccl":
+    if device.type == "cuda" and kind in ("rccl", "rccl-or-host"):
         from ..runtime.faults import raw_store
         store = raw_store()
         prefix = f"dli_rccl_{job}"
@@ -385,6 +391,7 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
             tr = RcclTransport(store, rank, world, device, prefix=prefix, timeout_s=rccl_timeout_s)
         except Exception as e:  # noqa: BLE001 - reported and agreed on below
             err = repr(e)
+            store.set(f"{prefix}/err/{rank}", err[:2000])
         store.set(f"{prefix}/ok/{rank}", "1" if tr is not None else "0")
         ok = [store.get(f"{prefix}/ok/{r}") == b"1" for r in range(world)]
         if all(ok):
@@ -392,13 +399,33 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
         if tr is not None:
             tr.abort()
         bad = [r for r, o in enumerate(ok) if not o]
-        msg = (f"[rank {rank}] RCCL transport unavailable (failed on ranks {bad}"
-               + (f": {err}" if err else "") + "); falling back to host-staged transport")
-        log.warning(msg)
+        errs = {r: store.get(f"{prefix}/err/{r}").decode(errors="replace") for r in bad
+                if r != rank and _store_has(store, f"{prefix}/err/{r}")}
+        if err:
+            errs[rank] = err
+        msg = (f"[rank {rank}] RCCL transport unavailable: communicators failed on ranks {bad}"
+               f" (device {device}, HSA_ENABLE_IPC_MODE_LEGACY="
+               f"{os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '<unset>')}); errors: {errs}")
         print(msg, file=sys.stderr, flush=True)
+        if kind != "rccl-or-host":
+            raise TransportInitError(msg)
+        log.warning(msg + "; DLI_TRANSPORT=rccl-or-host: falling back to host-staged transport")
         from .transport import HostStagedTransport
         return HostStagedTransport()
     if device.type == "cuda":
+        if kind != "host":
+            raise ValueError(f"DLI_TRANSPORT={kind!r}: expected rccl, rccl-or-host or host")
         from .transport import HostStagedTransport
         return HostStagedTransport()
     return TorchDistTransport()
+
+
+class TransportInitError(RuntimeError):
+    """The RCCL data plane could not be brought up on every rank."""
+
+
+def _store_has(store, key: str) -> bool:
+    try:
+        return bool(store.check([key]))
+    except Exception:  # noqa: BLE001
+        return False

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import collections
 import os
+import time
 from typing import Dict, Optional
 
 import torch
@@ -33,6 +34,9 @@ class Transport:
     bytes_recv: int = 0
     msgs_sent: int = 0
     msgs_recv: int = 0
+    # time the consumer waited for received data (host-blocking transports: host time; RCCL:
+    # device time the compute stream stalled on the receive, from HIP events, DLI_STAGE_TIMING=1)
+    recv_wait_ms: float = 0.0
 
     def _count(self, t: torch.Tensor, sent: bool) -> None:
         n = t.numel() * t.element_size()
@@ -45,7 +49,12 @@ class Transport:
 
     def traffic(self) -> dict:
         return {"bytes_sent": self.bytes_sent, "bytes_recv": self.bytes_recv,
-                "msgs_sent": self.msgs_sent, "msgs_recv": self.msgs_recv}
+                "msgs_sent": self.msgs_sent, "msgs_recv": self.msgs_recv,
+                "recv_wait_ms": round(self.recv_wait_ms, 3)}
+
+    def describe(self) -> dict:
+        """What carries the data plane (reported by bench.py per rank)."""
+        return {"transport": type(self).__name__}
 
     def send(self, t: torch.Tensor, peer: int) -> None:
         raise NotImplementedError
@@ -70,7 +79,9 @@ class TorchDistTransport(Transport):
         dist.send(t.contiguous(), peer, group=self.group)
 
     def recv(self, t, peer, free_event=None):
+        t0 = time.perf_counter()
         dist.recv(t, peer, group=self.group)
+        self.recv_wait_ms += (time.perf_counter() - t0) * 1e3
         self._count(t, False)
         return t
 
@@ -96,7 +107,9 @@ class HostStagedTransport(Transport):
         if free_event is not None:
             free_event.synchronize()
         host = torch.empty(t.shape, dtype=t.dtype)
+        t0 = time.perf_counter()
         dist.recv(host, peer, group=self.group)
+        self.recv_wait_ms += (time.perf_counter() - t0) * 1e3
         t.copy_(host, non_blocking=False)
         self._count(t, False)
         return t
@@ -132,6 +145,9 @@ class RcclTransport(Transport):
         self.send_stream = torch.cuda.Stream(device=device)
         self.recv_stream = torch.cuda.Stream(device=device)
         self._comms: Dict[int, object] = {}
+        self._rccl_version = int(C.rccl_version())
+        self._timing = os.environ.get("DLI_STAGE_TIMING", "0") == "1"
+        self._waits: collections.deque = collections.deque()
         dev_idx = device.index if device.index is not None else torch.cuda.current_device()
         # pair (i, i+1): the lower rank creates the id; both ends create a 2-rank communicator.
         # (sampled tokens return to the driver over the shm control plane, so no ring closure).
@@ -178,9 +194,32 @@ class RcclTransport(Transport):
             self.recv_stream.wait_stream(cur)
         t.record_stream(self.recv_stream)
         self._comm(peer).recv(t, self._peer_index(peer), self.recv_stream.cuda_stream)
+        if self._timing:
+            a = torch.cuda.Event(enable_timing=True)
+            a.record(cur)
         cur.wait_stream(self.recv_stream)
+        if self._timing:
+            b = torch.cuda.Event(enable_timing=True)
+            b.record(cur)
+            self._waits.append((a, b))
+            self._drain_waits(block=False)
         self._count(t, False)
         return t
+
+    def _drain_waits(self, block: bool) -> None:
+        while self._waits and (block or self._waits[0][1].query()):
+            a, b = self._waits.popleft()
+            b.synchronize()
+            self.recv_wait_ms += a.elapsed_time(b)
+
+    def traffic(self) -> dict:
+        self._drain_waits(block=True)
+        return super().traffic()
+
+    def describe(self) -> dict:
+        return {"transport": "RcclTransport", "rccl_version": self._rccl_version,
+                "pair_comms": {str(p): {"rank": c.rank, "size": c.world}
+                               for p, c in sorted(self._comms.items())}}
 
     def _peer_index(self, peer: int) -> int:
         # inside a 2-rank pair communicator the lower global rank of the pair is index 0

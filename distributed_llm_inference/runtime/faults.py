@@ -66,16 +66,20 @@ class FaultInjector:
 
 
 class StageStats:
-    """EWMA of per-step device time of this rank, published to the torch.distributed store."""
+    """Per-step device time of this rank: an EWMA published to the torch.distributed store
+    (``DLI_PUBLISH_STATS=1``, read by the server's rebalance loop) and cumulative totals that
+    :meth:`snapshot` reports (``DLI_STAGE_TIMING=1``, used by bench.py's per-rank fields)."""
 
     def __init__(self, rank: int, device: torch.device, publish_every: int = 20, alpha: float = 0.1):
         self.rank = rank
         self.device = device
-        self.enabled = os.environ.get("DLI_PUBLISH_STATS", "0") == "1"
+        self.publishing = os.environ.get("DLI_PUBLISH_STATS", "0") == "1"
+        self.enabled = self.publishing or os.environ.get("DLI_STAGE_TIMING", "0") == "1"
         self.every = publish_every
         self.alpha = alpha
         self.ewma: Optional[float] = None
         self.steps = 0
+        self.total_ms = 0.0
         self._pending: Deque[Tuple] = collections.deque()
         self._t0 = 0.0
         self._store = None
@@ -99,15 +103,28 @@ class StageStats:
             self._pending.append((s, e, extra))
         else:
             self._add((time.perf_counter() - s) * 1e3 + extra)
-        while self._pending and self._pending[0][1].query():
+        self._poll(block=False)
+
+    def _poll(self, block: bool) -> None:
+        while self._pending and (block or self._pending[0][1].query()):
             s, e, extra = self._pending.popleft()
+            e.synchronize()
             self._add(s.elapsed_time(e) + extra)
 
     def _add(self, ms: float) -> None:
         self.ewma = ms if self.ewma is None else (1 - self.alpha) * self.ewma + self.alpha * ms
         self.steps += 1
-        if self.steps % self.every == 0:
+        self.total_ms += ms
+        if self.publishing and self.steps % self.every == 0:
             self.publish()
+
+    def snapshot(self) -> dict:
+        """Cumulative counters now (waits for the timing events still in flight)."""
+        self._poll(block=True)
+        rec = {"t": time.perf_counter(), "steps": self.steps, "device_ms": self.total_ms}
+        if self.transport is not None:
+            rec.update(self.transport.traffic())
+        return rec
 
     def publish(self) -> None:
         try:
@@ -119,3 +136,8 @@ class StageStats:
             self._store.set(f"dli_stats/{self.rank}", json.dumps(rec))
         except Exception:
             pass
+
+
+def snapshot_delta(a: dict, b: dict) -> dict:
+    """Counters accumulated between two :meth:`StageStats.snapshot` records."""
+    return {k: b[k] - a[k] for k in b if k in a and isinstance(b[k], (int, float))}

@@ -60,7 +60,15 @@ class Scheduler:
         self.waiting.append(seq)
 
     def abort(self, seq_id: int) -> None:
-        for q in [self.waiting] + self.mbs:
+        # a request still waiting holds no KV and is in no plan: retire it right away, so its
+        # future resolves at the next publish even while admission is blocked on KV capacity
+        for s in list(self.waiting):
+            if s.seq_id == seq_id:
+                self.waiting.remove(s)
+                s.status = SeqStatus.ABORTED
+                s.finish_reason = "abort"
+                self.finished.append(s)
+        for q in self.mbs:
             for s in list(q):
                 if s.seq_id == seq_id:
                     s.status = SeqStatus.ABORTED

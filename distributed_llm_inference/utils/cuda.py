@@ -9,7 +9,7 @@ can never overwrite a result the caller still holds.  ``clone_outputs=False`` op
 zero-copy static-buffer contract.
 
 The runtime does not use this per-op helper on its hot path; it captures the WHOLE per-stage
-decode step per batch bucket (``runtime/graphs.py``).
+decode step per batch bucket (``StageExecutor._capture`` in ``runtime/executor.py``).
 """
 from __future__ import annotations
 

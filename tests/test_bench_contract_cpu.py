@@ -22,13 +22,13 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("n", [2, 4, 8])
 def test_bench_multirank_json_contract(n):
     steps, warmup, bpm = 3, 1, 4
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(REPO, "bench.py"), "--gpus", str(n), "--steps", str(steps),
-           "--warmup", str(warmup), "--model", "tiny-llama", "--batch-per-mb", str(bpm),
+           "--warmup", str(warmup), "--model", "tiny-llama-8l", "--batch-per-mb", str(bpm),
            "--prompt-len", "16", "--max-batched-tokens", "64"]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
@@ -44,3 +44,21 @@ def test_bench_multirank_json_contract(n):
     G = d["config"]["global_batch"]
     assert G == (n + 1) * bpm and d["tokens_timed"] == steps * G
     assert abs(d["value"] - d["tokens_timed"] / (d["ms_per_step"] * steps / 1e3)) < 0.02 * d["value"]
+    # per-rank diagnostics of the multi-rank path (what the 8-GPU driver run is judged on)
+    assert d["transport"] == "TorchDistTransport"   # gloo on the CPU; RCCL on GPUs
+    ranges = d["stage_ranges"]
+    assert len(ranges) == n and ranges[0][0] == 0 and all(
+        ranges[i][1] == ranges[i + 1][0] for i in range(n - 1))
+    pr = d["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(n))
+    for r in pr:
+        assert r["transport"] == "TorchDistTransport"
+        # every rank ran one compute step per micro-batch step of the timed window
+        assert r["mb_steps"] == steps * (n + 1), r
+        assert r["device_ms_per_mb_step"] > 0
+        assert r["recv_wait_ms_per_mb_step"] >= 0
+    H = 128  # tiny-llama-8l hidden size (bf16 activations)
+    mb_bytes = bpm * H * 2
+    for i, r in enumerate(pr):
+        assert r["bytes_sent"] == (steps * (n + 1) * mb_bytes if i < n - 1 else 0), r
+        assert r["bytes_recv"] == (steps * (n + 1) * mb_bytes if i > 0 else 0), r

@@ -189,8 +189,10 @@ def _llm_int8_outliers_ref(x, wq, ws, threshold, J):
     `threshold` (distinct values), in column order, padded with (column 0, weight 0)."""
     colmax = x.float().abs().amax(0)
     vals, _ = colmax.sort(descending=True)
-    t = threshold if (colmax > threshold).sum() <= J else max(threshold, vals[J].item())
-    on = colmax > t
+    if (colmax >= threshold).sum() <= J:
+        on = colmax >= threshold     # bitsandbytes: |A| >= threshold
+    else:
+        on = colmax > vals[J].item()  # strictly above the (J+1)-th largest; ties dropped
     cols = on.nonzero().flatten()
     idx = torch.zeros(J, dtype=torch.long)
     idx[:cols.numel()] = cols
@@ -227,6 +229,39 @@ def test_llm_int8_outlier_kernels_match_reference(gpu, K, n_out, M):
     wq_t = wq.t().contiguous().to(gpu)
     _, _, wo_t = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J, wq_t)
     assert torch.equal(wo_t.cpu(), rw)
+
+
+# the transposed-copy gather's tails: partial 16-column blocks / max_out % 8 != 0 and partial
+# 256-row n-tiles (N % 256 != 0), bit-exact against the reference
+@pytest.mark.parametrize("N,J", [(260, 20), (1028, 40), (512, 64)])
+def test_llm_int8_gather_wt_tails(gpu, N, J):
+    torch.manual_seed(N + J)
+    K, M = 2048, 64
+    xb = (torch.randn(M, K) * 0.5).to(torch.bfloat16)
+    cols = torch.randperm(K)[:J + 7]
+    planted = (torch.randperm(J + 7).to(torch.int16) + 0x4100).view(torch.bfloat16)
+    xb[torch.randint(0, M, (J + 7,)), cols] = planted
+    wq = torch.randint(-127, 128, (N, K), dtype=torch.int8)
+    ws = torch.rand(N) * 0.01 + 1e-3
+    _, _, rw = _llm_int8_outliers_ref(xb, wq, ws, 6.0, J)
+    wq_t = wq.t().contiguous().to(gpu)
+    _, _, wo_t = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J, wq_t)
+    assert torch.equal(wo_t.cpu(), rw)
+
+
+def test_llm_int8_threshold_is_inclusive_and_cpu_gpu_agree(gpu):
+    """|x| == threshold is an outlier (bitsandbytes' >=), on the GPU kernel and the CPU path."""
+    K, N, M = 1024, 256, 8
+    xb = (torch.randn(M, K) * 0.3).to(torch.bfloat16)
+    xb[3, 17] = 6.0        # exactly at the threshold
+    xb[5, 900] = -7.5
+    wq = torch.randint(-127, 128, (N, K), dtype=torch.int8)
+    ws = torch.rand(N) * 0.01 + 1e-3
+    fg, _, _ = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, 64)
+    assert fg.cpu()[17] == 1 and fg.cpu()[900] == 1 and int(fg.sum()) == 2
+    y_cpu = ops.llm_int8_linear(xb, wq, ws, 6.0).float()
+    y_gpu = ops.llm_int8_linear(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0).float().cpu()
+    assert ((y_gpu - y_cpu).norm() / y_cpu.norm()).item() < 5e-3
 
 
 # ------------------------------------------------- stream-K tail (gemm_tile splits = 0, SkArgs)

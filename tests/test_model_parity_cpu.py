@@ -312,3 +312,45 @@ def test_engine_uses_sliding_window_from_config():
     assert eng.executors[0].pool.manager.window_length == 8
     out = eng.generate([list(range(3, 16))], SamplingParams(max_tokens=4, ignore_eos=True))
     assert len(out[0].output) == 4
+
+
+def test_llama_block_4d_custom_mask_matches_hf():
+    """Reference model.py:115-119: a pre-inverted 4-D mask replaces the causal mask.  A prefix-LM
+    mask (first 4 tokens attend bidirectionally) through LlamaBlock.forward equals HF's eager
+    decoder layers under the same additive mask; a 4-D causal mask equals the default path."""
+    from distributed_llm_inference.models.llama import LlamaBlock  # noqa: F401
+    hf = _hf_llama(layers=2, seed=5)
+    hf.config._attn_implementation = "eager"
+    stage = stage_from_hf_model(hf, 0, 2)
+    blk = stage.block
+    torch.manual_seed(0)
+    B, T, P = 2, 9, 4
+    ids = torch.randint(0, 256, (B, T))
+    with torch.no_grad():
+        emb = hf.model.embed_tokens(ids).to(torch.bfloat16).float()
+        neg = torch.finfo(torch.float32).min
+        allowed = torch.tril(torch.ones(T, T, dtype=torch.bool))
+        allowed[:P, :P] = True                                  # prefix-LM block
+        mask = torch.zeros(B, 1, T, T).masked_fill(~allowed, neg)
+        pos = torch.arange(T)[None].expand(B, -1)
+        cos, sin = hf.model.rotary_emb(emb, pos)
+        h = emb
+        for layer in hf.model.layers:
+            h = layer(h, attention_mask=mask, position_ids=pos, position_embeddings=(cos, sin))
+            h = h[0] if isinstance(h, tuple) else h
+        (ours,) = blk("s", emb.to(torch.bfloat16), attention_mask=mask)
+        err = (ours.float() - h).norm() / h.norm()
+        assert err.item() < 2e-2, err.item()
+        # the prefix-LM mask really differs from causal on the prefix rows
+        (causal,) = blk("c", emb.to(torch.bfloat16))
+        assert (causal[:, :P - 1].float() - ours[:, :P - 1].float()).abs().max() > 1e-2
+        # a 4-D causal mask is the default path; T = 1 decode with a 4-D all-zero mask too
+        cm = torch.zeros(B, 1, T, T).masked_fill(~torch.tril(torch.ones(T, T, dtype=torch.bool)), neg)
+        (c4,) = blk("c4", emb.to(torch.bfloat16), attention_mask=cm)
+        assert torch.allclose(c4.float(), causal.float(), atol=2e-2, rtol=2e-2)
+        x1 = torch.randn(B, 1, 128, dtype=torch.bfloat16)
+        (d_plain,) = blk("c", x1)
+        (d_4d,) = blk("c4", x1, attention_mask=torch.zeros(B, 1, 1, T + 1))
+        assert torch.allclose(d_plain.float(), d_4d.float(), atol=2e-2, rtol=2e-2)
+        with pytest.raises(ValueError):
+            blk("bad", emb.to(torch.bfloat16), attention_mask=mask + 1.0)   # not inverted

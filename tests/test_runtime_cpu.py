@@ -160,6 +160,10 @@ def test_scheduler_respects_kv_capacity():
     assert len(p.seq_ids) == 2  # 60 tokens = 2 blocks each; third must wait
     with pytest.raises(ValueError):
         sch.add(Sequence([1] * 200, SamplingParams(max_tokens=1)))
+    # aborting the request that waits for KV retires it at once (admission is still blocked)
+    sch.abort(seqs[2].seq_id)
+    assert not sch.waiting and seqs[2].finish_reason == "abort"
+    assert seqs[2] in sch.pop_finished()
 
 
 # ------------------------------------------------------------------------------ engines
