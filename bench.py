@@ -14,6 +14,12 @@ in flight so all N stages stay busy while tokens return to the driver.  Work per
 fixed as N grows, so the scaling mode is "weak".  A "step" = every in-flight sequence decodes one token.  Timed region:
 barrier + device sync -> exactly K decode steps -> barrier + device sync; the max over ranks is
 reported.  Prefill and W warmup steps (incl. hipGraph capture) run before the timed region.
+
+``--dp D`` (default 1) instead runs D independent pipeline replicas of N/D stages each (DP x PP:
+e.g. dp8 = eight whole-model Llama-3-70B replicas, one per GPU; dp2 x pp4).  Every replica's
+driver plans and times its own sequences; the replicas start and stop the timed window together
+(barrier over the drivers) and ``value`` is the tokens of ALL replicas / the slowest replica's
+window.  The BASELINE headline stays the default PP=N layout.
 """
 from __future__ import annotations
 
@@ -45,6 +51,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="llama-3-70b")
+    ap.add_argument("--dp", type=int, default=1,
+                    help="pipeline replicas (DP x PP, world = dp x pp); default 1 = one PP=N pipeline")
     ap.add_argument("--batch-per-mb", type=int, default=512)
     ap.add_argument("--micro-batches", type=int, default=0, help="0 = N+1 (N=1: 1)")
     ap.add_argument("--prompt-len", type=int, default=512)
@@ -62,8 +70,14 @@ def _rank_record(node, rank: int, window_s: float) -> dict:
     """This rank's share of the timed window (between the last two barriers): stage range,
     data-plane transport, device compute per micro-batch step, receive stalls, traffic."""
     from distributed_llm_inference.runtime.faults import snapshot_delta
-    ex = node.ex
-    rec = {"rank": rank, "stage": [ex.stage.start, ex.stage.end], "device": str(ex.device)}
+    rec = {"rank": rank, "replica": getattr(node, "replica", 0)}
+    ex = getattr(node, "ex", None)
+    if ex is None:   # a single-stage replica (LocalPipeline): the whole model, no transport
+        exs = node.executors
+        rec.update({"stage": [exs[0].stage.start, exs[-1].stage.end], "device": str(exs[0].device),
+                    "transport": "none"})
+        return rec
+    rec.update({"stage": [ex.stage.start, ex.stage.end], "device": str(ex.device)})
     rec.update(node.tr.describe())
     if len(node.snapshots) >= 2:
         d = snapshot_delta(node.snapshots[-2], node.snapshots[-1])
@@ -93,16 +107,19 @@ def main():
         if world == 1 and a.gpus > 1:
             raise SystemExit("for --gpus > 1 launch with torch.distributed.run (one rank per GPU)")
         raise SystemExit(f"WORLD_SIZE={world} != --gpus={a.gpus}")
+    if a.dp < 1 or a.gpus % a.dp:
+        raise SystemExit(f"--dp {a.dp} must divide --gpus {a.gpus}")
+    dp, pp = a.dp, a.gpus // a.dp
     if rank == 0:
         _build.build_all()
     if world > 1:
         dist.init_process_group("gloo")
         dist.barrier()
     spec = resolve_model(a.model)
-    M = a.micro_batches or (a.gpus + 1 if a.gpus > 1 else 1)
+    M = a.micro_batches or (pp + 1 if pp > 1 else 1)
     total_len = a.prompt_len + a.warmup + a.steps + 72
     cfg = EngineConfig(
-        model=a.model, random_init=True, seed=0, quantize="int8" if a.int8 else a.fp8, pp=a.gpus,
+        model=a.model, random_init=True, seed=0, quantize="int8" if a.int8 else a.fp8, pp=pp, dp=dp,
         cache=CacheConfig(block_size=64, gpu_memory_utilization=0.92,
                           dtype="fp8" if a.kv_fp8 else "bf16"),
         serve=ServeConfig(max_batch_size=a.batch_per_mb, max_num_batched_tokens=a.max_batched_tokens,
@@ -110,19 +127,34 @@ def main():
                           graph_batch_sizes=[a.batch_per_mb]))
     t_init = time.perf_counter()
     role, obj = init_pipeline_rank(cfg)
+
+    def world_reduce(elapsed: float, toks: int, rec: dict):
+        """Same collectives on every rank, in the same order: max window, summed tokens, records."""
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n = torch.tensor([toks], dtype=torch.int64)
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        recs = [None] * world
+        dist.all_gather_object(recs, rec)
+        dist.barrier()
+        return float(t.item()), int(n.item()), recs
+
     if role == "follower":
         obj.run()
         interval = obj.barrier_times[-1] - obj.barrier_times[-2] if len(obj.barrier_times) >= 2 else 0.0
-        t = torch.tensor([interval], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_gather_object([None] * world, _rank_record(obj, rank, float(t.item())))
-        dist.barrier()
+        world_reduce(interval, 0, _rank_record(obj, rank, interval))
         obj.close()
         dist.destroy_process_group()
         return
     drv = obj
+    dgroup = getattr(drv, "drivers_group", None)
+
+    def sync_replicas():
+        if dgroup is not None:
+            dist.barrier(group=dgroup)
+
     init_s = time.perf_counter() - t_init
-    rng = random.Random(1234)
+    rng = random.Random(1234 + 7919 * getattr(drv, "replica", 0))
     G = M * a.batch_per_mb
     # generous max_tokens: sequences prefilled early keep decoding during the remaining prefill
     # rounds, and none may finish inside the timed window (constant batch)
@@ -139,8 +171,7 @@ def main():
     for _ in range(a.warmup):
         drv.round()
     drv.barrier()
-    if world > 1:
-        pass  # followers recorded the barrier time
+    sync_replicas()
     n0 = sum(len(s.output) for s in seqs)
     for s in seqs:
         s.token_times.clear()
@@ -150,20 +181,21 @@ def main():
         drv.round()
     drv.barrier()
     t1 = time.perf_counter()
+    sync_replicas()
     driver_busy = (t1 - t0) - (drv.wait_s - w0)
     n1 = sum(len(s.output) for s in seqs)
     elapsed = t1 - t0
+    toks_mine = n1 - n0
+    toks = toks_mine
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
         drv.stop()
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        per_rank = [None] * world
-        dist.all_gather_object(per_rank, _rank_record(drv, rank, elapsed))
-        dist.barrier()
-    toks = n1 - n0
-    if toks != a.steps * G:
-        print(f"WARNING: {toks} tokens in the timed window, expected {a.steps * G} "
+        elapsed, toks, per_rank = world_reduce(elapsed, toks_mine, _rank_record(drv, rank, elapsed))
+    if rank != 0:   # another replica's driver: rank 0 reports for the whole node
+        drv.close()
+        dist.destroy_process_group()
+        return
+    if toks_mine != a.steps * G or toks != a.steps * G * dp:
+        print(f"WARNING: {toks} tokens in the timed window, expected {a.steps * G * dp} "
               "(KV cache too small to run every sequence at once?)", file=sys.stderr, flush=True)
     lat = []
     for s in seqs:
@@ -187,11 +219,11 @@ def main():
                  + ("/fp8-kv" if a.kv_fp8 else ""),
         "data": f"synthetic (random-init {spec.name} weights, random prompt tokens)",
         "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
-                   "global_batch": G, "seq_len": total_len,
-                   "parallelism": f"pp{a.gpus}"},
+                   "global_batch": G * dp, "seq_len": total_len,
+                   "parallelism": f"pp{pp}" if dp == 1 else f"dp{dp}xpp{pp}"},
         "p50_token_latency_ms": round(p50, 3),
         "p90_token_latency_ms": round(p90, 3),
-        "transport": drv.tr.describe()["transport"] if world > 1 else "none",
+        "transport": drv.tr.describe()["transport"] if (world > 1 and pp > 1) else "none",
         "micro_batches": M,
         "batch_per_micro_batch": a.batch_per_mb,
         "prompt_len": a.prompt_len,
@@ -199,6 +231,7 @@ def main():
         "prefill_s": round(prefill_s, 3),
         # host time of the driver rank per micro-batch step NOT spent waiting for results
         "driver_host_ms_per_mb_step": round(driver_busy / (a.steps * M) * 1e3, 3),
+        "replicas": dp, "stages_per_replica": pp,
         "init_s": round(init_s, 1),
         "kv_blocks": int(drv.sched.total_blocks),
         "kv_blocks_needed": int(G * drv.sched.blocks_for(a.prompt_len + params.max_tokens)),
@@ -209,7 +242,7 @@ def main():
     if a.model != "llama-3-70b":
         # the headline metric names its model; a run of another model says what it measured
         res["metric"] = (f"output tokens/sec (whole node) + p50 token latency, "
-                         f"{res['config']['model']} PP={a.gpus}")
+                         f"{res['config']['model']} PP={pp}")
     line = json.dumps(res)
     print(line, flush=True)
     if a.json_out:

@@ -1,13 +1,15 @@
 """``distribute`` — command-line entry point (the reference's ``distribute`` file is empty).
 
-    distribute plan     --model llama-3-70b --gpus 8
+    distribute plan     --model llama-3-70b --gpus 8 [--dp 2]
     distribute generate --model llama-3-8b --gpus 2 --prompt-ids 1,2,3 --max-tokens 32
-    distribute serve    --model llama-3-70b --gpus 8 --port 8000 [--tokenizer DIR]
-    distribute bench    --gpus 8 --steps 20 --warmup 5          (runs bench.py under the launcher)
+    distribute serve    --model llama-3-70b --gpus 8 --port 8000 [--tokenizer DIR] [--dp 8]
+    distribute bench    --gpus 8 --steps 20 --warmup 5 [--dp 2]  (bench.py under the launcher)
 
 One process per GPU (``launcher.launch``); each process owns one pipeline stage (``plan_stages``).
-Rank 0 is the driver (scheduler + stage 0) and hosts the action (generate / serve); the other
-ranks run the stage follower loop until the driver stops them.
+``--dp D`` splits the GPUs into D independent pipeline replicas of gpus/D stages (DP x PP,
+``parallel/replicas.py``): ``generate`` deals the prompts over the replicas, ``serve`` puts one
+HTTP front end (rank 0) over all of them.  The first rank of every replica is its driver
+(scheduler + stage 0); the other ranks run the stage follower loop until their driver stops them.
 """
 from __future__ import annotations
 
@@ -24,7 +26,9 @@ log = logging.getLogger("distribute")
 def _common(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--model", default="llama-3-8b", help="preset name or HF config/checkpoint dir")
     ap.add_argument("--checkpoint", default=None, help="HF safetensors dir (default: random init)")
-    ap.add_argument("--gpus", type=int, default=1, help="pipeline stages = processes = GPUs")
+    ap.add_argument("--gpus", type=int, default=1, help="processes = GPUs (= dp x pipeline stages)")
+    ap.add_argument("--dp", type=int, default=1,
+                    help="pipeline replicas (data parallel); each gets gpus/dp stages")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--fp8", action="store_true", help="fp8-e4m3 weights")
     ap.add_argument("--int8", action="store_true",
@@ -52,7 +56,7 @@ def engine_config(a):
     return EngineConfig(
         model=a.model, checkpoint=a.checkpoint, random_init=a.checkpoint is None, seed=a.seed,
         quantize="fp8" if a.fp8 else ("int8" if a.int8 else False),
-        int8_threshold=a.int8_threshold, pp=a.gpus,
+        int8_threshold=a.int8_threshold, pp=a.gpus // max(1, a.dp), dp=a.dp,
         cache=CacheConfig(block_size=a.block_size, gpu_memory_utilization=a.gpu_mem,
                           window_length=a.window, num_sink_tokens=a.sinks, dtype=a.kv_dtype),
         serve=ServeConfig(max_batch_size=a.max_batch, max_num_batched_tokens=a.max_batched_tokens,
@@ -71,18 +75,29 @@ def load_tokenizer(path: Optional[str]):
 def cmd_plan(a) -> int:
     from .config import plan_stages, resolve_model
     from .models.llama.cache import KVPool
+    from .runtime.engine import ReplicaLayout
     spec = resolve_model(a.checkpoint or a.model)
-    ranges = plan_stages(spec, a.gpus)
+    layout = ReplicaLayout.for_world(a.gpus, a.dp)
+    ranges = plan_stages(spec, layout.pp)
     per_layer = spec.layer_param_count() * (1 if (a.fp8 or a.int8) else 2)
     emb = spec.vocab_size * spec.hidden_size * 2
-    out = []
-    for i, (s, e) in enumerate(ranges):
-        w = (e - s) * per_layer + (emb if i == 0 else 0) + (emb if i == len(ranges) - 1 else 0)
-        free = 288e9 * a.gpu_mem - w
-        kv_tok = KVPool.bytes_per_block(spec, e - s, 1, 1 if a.kv_dtype == "fp8" else 2)
-        out.append(dict(stage=i, gpu=i, layers=[s, e], weights_gb=round(w / 1e9, 2),
-                        kv_capacity_tokens=int(max(0, free) // kv_tok)))
-    print(json.dumps({"model": spec.name, "num_layers": spec.num_layers, "stages": out}, indent=1))
+    replicas = []
+    for r in range(layout.dp):
+        out = []
+        for i, (s, e) in enumerate(ranges):
+            w = (e - s) * per_layer + (emb if i == 0 else 0) + (emb if i == len(ranges) - 1 else 0)
+            free = 288e9 * a.gpu_mem - w
+            kv_tok = KVPool.bytes_per_block(spec, e - s, 1, 1 if a.kv_dtype == "fp8" else 2)
+            out.append(dict(stage=i, rank=r * layout.pp + i, gpu=r * layout.pp + i, layers=[s, e],
+                            weights_gb=round(w / 1e9, 2),
+                            kv_capacity_tokens=int(max(0, free) // kv_tok)))
+        replicas.append(dict(replica=r, driver_rank=r * layout.pp, stages=out))
+    res = {"model": spec.name, "num_layers": spec.num_layers, "dp": layout.dp, "pp": layout.pp,
+           "layout": f"dp{layout.dp}xpp{layout.pp}" if layout.dp > 1 else f"pp{layout.pp}",
+           "stages": replicas[0]["stages"]}
+    if layout.dp > 1:
+        res["replicas"] = replicas
+    print(json.dumps(res, indent=1))
     return 0
 
 
@@ -108,8 +123,12 @@ def cmd_worker(a) -> int:
         return 0
     drv = obj
     tok = load_tokenizer(a.tokenizer)
+    layout = getattr(drv, "layout", None)
+    dp = layout.dp if layout is not None else 1
+    rep = getattr(drv, "replica", 0)
     try:
         if a.action == "generate":
+            from .parallel.replicas import replica_generate
             prompts = []
             if a.prompt_ids:
                 prompts = [[int(x) for x in p.split(",") if x] for p in a.prompt_ids]
@@ -122,8 +141,8 @@ def cmd_worker(a) -> int:
             params = SamplingParams(max_tokens=a.max_tokens, temperature=a.temperature,
                                     top_k=a.top_k, top_p=a.top_p, seed=a.sample_seed,
                                     ignore_eos=a.ignore_eos)
-            outs = drv.generate(prompts, params)
-            for s in outs:
+            outs = replica_generate(drv, prompts, params)
+            for s in outs or []:
                 rec = {"prompt_ids": s.prompt, "output_ids": s.output,
                        "finish_reason": s.finish_reason}
                 if tok is not None:
@@ -134,7 +153,10 @@ def cmd_worker(a) -> int:
             from .server.service import EngineService
             svc = EngineService(drv, eos_token_id=getattr(drv.sched, "eos", None))
             try:
-                serve(svc, a.host, a.port, tok, a.model, a.request_timeout)
+                if dp == 1:
+                    serve(svc, a.host, a.port, tok, a.model, a.request_timeout)
+                else:
+                    _serve_replicas(a, svc, rep, dp, tok)
             finally:
                 svc.shutdown(stop_driver=False)
         else:
@@ -145,6 +167,27 @@ def cmd_worker(a) -> int:
         if dist.is_initialized():
             dist.destroy_process_group()
     return 0
+
+
+def _serve_replicas(a, svc, rep: int, dp: int, tok) -> None:
+    """DP serving: rank 0 hosts the HTTP front end over a :class:`ReplicaRouter`; every other
+    replica driver serves rank 0's requests through a :class:`ReplicaServer`."""
+    import torch.distributed as dist
+    from .parallel.replicas import RemoteReplica, ReplicaRouter, ReplicaServer
+    from .server.http import serve
+    job = dist.distributed_c10d._get_default_store().get("dli_job").decode()
+    if rep == 0:
+        router = ReplicaRouter([svc] + [RemoteReplica(job, r) for r in range(1, dp)])
+        try:
+            serve(router, a.host, a.port, tok, a.model, a.request_timeout)
+        finally:
+            router.shutdown()
+    else:
+        rs = ReplicaServer(svc, job, rep)
+        try:
+            rs.serve_forever()
+        finally:
+            rs.close()
 
 
 def _gen_args(ap):
@@ -180,6 +223,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     _serve_args(s)
     b = sub.add_parser("bench", help="headline benchmark (bench.py) on N GPUs")
     b.add_argument("--gpus", type=int, default=1)
+    b.add_argument("--dp", type=int, default=1, help="pipeline replicas (DP x PP)")
     b.add_argument("rest", nargs=argparse.REMAINDER)
     w = sub.add_parser("worker", help=argparse.SUPPRESS)
     _common(w)
@@ -195,7 +239,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         from .launcher import launch
         bench = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
         rest = [x for x in a.rest if x != "--"]
-        return launch(a.gpus, [bench, "--gpus", str(a.gpus)] + rest)
+        return launch(a.gpus, [bench, "--gpus", str(a.gpus), "--dp", str(a.dp)] + rest)
     # generate / serve: re-run this CLI as `worker` in N processes
     idx = argv.index(a.cmd)
     return _spawn_self(a, a.cmd, argv[:idx] + argv[idx + 1:])

@@ -598,7 +598,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bias", &gelu_bias, "gelu_tanh(x + bias)");
   m.def("add", &add, "out = a + b");
   m.def("rope_cache", &rope_cache, "fused RoPE + paged KV cache write");
-  m.def("attn_decode", &attn_decode, "paged GQA decode attention (split-K)");
+  m.def("attn_decode", &attn_decode, "paged GQA decode attention (split-K)", py::arg("out"),
+        py::arg("q"), py::arg("q_sink"), py::arg("k_cache"), py::arg("v_cache"),
+        py::arg("block_tables"), py::arg("seq_lens"), py::arg("scale"), py::arg("n_sink"),
+        py::arg("sink_pad"), py::arg("ring"), py::arg("window"), py::arg("num_splits"),
+        py::arg("part_o"), py::arg("part_ml"), py::arg("k_scale"), py::arg("v_scale"));
   m.def("attn_prefill", &attn_prefill, "paged causal prefill attention (varlen)");
   m.def("sample", &sample, "greedy / temperature / top-k / top-p sampling");
   m.def("quant_rowwise", &quant_rowwise, "row-wise fp8 e4m3 quantisation (+fused RMSNorm)",

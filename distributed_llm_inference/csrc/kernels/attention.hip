@@ -154,12 +154,20 @@ __device__ __forceinline__ void attn_step(WaveState<D>& st, const bf16x8 (&qf)[D
 }
 
 // ===========================================================================================
-// Decode: one wave per work item (sequence b, kv head, group of 16 q heads, split), 4 independent
-// waves per 256-thread workgroup (no LDS, no barriers).  A wave walks its split's 32-key steps with
-// the loads of step s+1 in flight while step s computes (two register fragment sets; the prefetch
-// index is clamped instead of branched so the loads stay straight-line and hipcc can wait with a
-// counted vmcnt).  With one split the wave writes the normalised output; otherwise unnormalised
-// partials (O, m, l) for attn_combine_kernel.
+// Decode: one wave per work item (sequence b, kv head, group of 16 q heads, split), 4 waves per
+// 256-thread workgroup.  A wave walks its split's 32-key steps with the loads of step s+1 in flight
+// while step s computes (two register fragment sets; the prefetch index is clamped instead of
+// branched so the loads stay straight-line and hipcc can wait with a counted vmcnt).
+//   * one split (large batches): 4 independent waves, no LDS, no barrier; each writes the
+//     normalised output;
+//   * num_splits > 1 (small batches / long contexts: up to hundreds of splits so that even B = 1
+//     puts several waves on every CU): the workgroup's waves hold `gs` (4 or 2) consecutive
+//     splits of one item and merge them through LDS (online-softmax rescale, padded O^T image),
+//     so only num_splits / gs partials per head go to HBM — and none when num_splits == gs;
+//     attn_combine_kernel merges what is left.  (An in-kernel finish by the last-arriving
+//     workgroup — agent-scope release + arrival counter, cdna_hip_programming.md §6 G16 — was
+//     measured 5-75 % SLOWER than this separate merge on every small-batch shape: the per-block
+//     release and the serial read of up to 64 partials by one CU cost more than a launch.)
 // ===========================================================================================
 template <int D, bool WIN>
 __device__ __forceinline__ unsigned step_mask(int u0, int h4, int seg_base, int seg_len, int L,
@@ -178,13 +186,21 @@ __device__ __forceinline__ unsigned step_mask(int u0, int h4, int seg_base, int 
   return vm;
 }
 
-template <int D, bool WIN, bool FP8>
-__global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int items) {
+template <int D, bool WIN, bool FP8, bool GRP>
+__global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int items, int gs) {
+  // GRP (num_splits > 1): the `gs` consecutive splits of one work item that share this
+  // workgroup are merged in LDS, so only num_splits / gs partials per head reach global memory
+  // (none when gs == num_splits: the workgroup writes the normalised output itself)
+  constexpr int LROW = D + 4;  // padded O^T column: conflict-free ds_write_b128
+  __shared__ __attribute__((aligned(16))) float lds[GRP ? 4 * 16 * (LROW + 2) : 1];
+  const int wave = threadIdx.x >> 6;
+  const int item_raw = blockIdx.x * 4 + wave;
+  const bool live = item_raw < items;
+  if (!GRP && !live) return;  // whole wave idle (no barrier in the ungrouped kernel)
   // wave-uniform by construction; readfirstlane tells hipcc so, which turns every index derived
   // from it (seq_lens, block-table entries) into scalar loads that never join the vmcnt queue
   // of the K/V prefetch
-  const int item = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-  if (item >= items) return;  // whole wave idle
+  const int item = __builtin_amdgcn_readfirstlane(live ? item_raw : items - 1);
   const int splits = p.num_splits;
   const int split = item % splits;
   int rest = item / splits;
@@ -198,7 +214,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
   const int col = lane & 15, h4 = lane >> 4;
   const bool col_valid = (g0 + col) < G;
   const int qh = kvh * G + g0 + (col_valid ? col : 0);
-  const int L = p.seq_lens[b];
+  const int L = live ? p.seq_lens[b] : 0;
   const int* bt = p.block_tables + (size_t)b * p.bt_stride;
   const size_t head_stride = (size_t)p.bs * D;  // per (block, kv head)
 
@@ -271,47 +287,128 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
   float lsum = st.l;
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
-  if (!col_valid) return;
-  const int head = kvh * G + g0 + col;
-  if (splits == 1) {
-    const float inv = lsum > 0.f ? vsc / lsum : 0.f;
-    bf16* orow = p.out + ((size_t)b * p.nh + head) * D;
+  const size_t B = (size_t)items / ((size_t)splits * hgroups * p.nkv);
+  if constexpr (!GRP) {
+    if (!col_valid) return;
+    const int head = kvh * G + g0 + col;
+    if (splits == 1) {
+      const float inv = lsum > 0.f ? vsc / lsum : 0.f;
+      bf16* orow = p.out + ((size_t)b * p.nh + head) * D;
 #pragma unroll
-    for (int e = 0; e < D / 16; ++e) {
-      bf16x4 v;
+      for (int e = 0; e < D / 16; ++e) {
+        bf16x4 v;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = (bf16)(st.o[e][r] * inv);
-      *reinterpret_cast<bf16x4*>(orow + 16 * e + 4 * h4) = v;
+        for (int r = 0; r < 4; ++r) v[r] = (bf16)(st.o[e][r] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 16 * e + 4 * h4) = v;
+      }
+    } else {
+      const size_t r0 = ((size_t)split * B + b) * p.nh + head;
+      float* prow = p.part_o + r0 * D;
+#pragma unroll
+      for (int e = 0; e < D / 16; ++e) *reinterpret_cast<f32x4*>(prow + 16 * e + 4 * h4) = st.o[e] * vsc;
+      if (h4 == 0) {
+        p.part_ml[r0 * 2] = st.m;
+        p.part_ml[r0 * 2 + 1] = lsum;
+      }
     }
   } else {
-    const size_t T = (size_t)items / ((size_t)splits * hgroups * p.nkv);  // = B
-    const size_t r0 = ((size_t)split * T + b) * p.nh + head;
-    float* prow = p.part_o + r0 * D;
+    // ---- merge the gs waves of each group in LDS ----
+    float* lo = lds + (wave * 16 + col) * LROW;
+    float* lml = lds + 4 * 16 * LROW;  // [wave][col][m, l]
 #pragma unroll
-    for (int e = 0; e < D / 16; ++e) *reinterpret_cast<f32x4*>(prow + 16 * e + 4 * h4) = st.o[e] * vsc;
+    for (int e = 0; e < D / 16; ++e) *reinterpret_cast<f32x4*>(lo + 16 * e + 4 * h4) = st.o[e];
     if (h4 == 0) {
-      p.part_ml[r0 * 2] = st.m;
-      p.part_ml[r0 * 2 + 1] = lsum;
+      lml[(wave * 16 + col) * 2] = st.m;
+      lml[(wave * 16 + col) * 2 + 1] = lsum;
+    }
+    __syncthreads();
+    const int g = wave / gs;                     // group of this wave
+    const int w0 = g * gs;                       // its first wave
+    const int gitem = blockIdx.x * 4 + w0;       // the group's first work item
+    if (gitem >= items) return;
+    const int S2 = splits / gs;                  // partials per head after the merge
+    const int s2 = (gitem % splits) / gs;
+    const int tg = (wave - w0) * 64 + lane;      // thread index inside the group
+    constexpr int V4 = 16 * D / 4;               // f32x4 units of one group's output
+    for (int u = tg; u < V4; u += gs * 64) {
+      const int c = u / (D / 4), d4 = (u % (D / 4)) * 4;
+      if (g0 + c >= G) continue;
+      float M = -1e30f;
+      for (int w = w0; w < w0 + gs; ++w) M = fmaxf(M, lml[(w * 16 + c) * 2]);
+      float Lt = 0.f;
+      f32x4 O = {0.f, 0.f, 0.f, 0.f};
+      for (int w = w0; w < w0 + gs; ++w) {
+        const float f = __builtin_amdgcn_exp2f(lml[(w * 16 + c) * 2] - M);
+        Lt += f * lml[(w * 16 + c) * 2 + 1];
+        O += f * *reinterpret_cast<const f32x4*>(lds + (w * 16 + c) * LROW + d4);
+      }
+      const int head = kvh * G + g0 + c;
+      if (S2 == 1) {
+        const float inv = Lt > 0.f ? vsc / Lt : 0.f;
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (bf16)(O[r] * inv);
+        *reinterpret_cast<bf16x4*>(p.out + ((size_t)b * p.nh + head) * D + d4) = v;
+      } else {
+        const size_t r0 = ((size_t)s2 * B + b) * p.nh + head;
+        *reinterpret_cast<f32x4*>(p.part_o + r0 * D + d4) = O * vsc;
+        if (d4 == 0) {
+          p.part_ml[r0 * 2] = M;
+          p.part_ml[r0 * 2 + 1] = Lt;
+        }
+      }
     }
   }
 }
 
-// Merge split-K partials: grid (T * nh), D threads.
+// Merge split-K partials: one 256-thread workgroup per (token, head).  D/4 lanes hold one f32x4
+// of O each; the 256 / (D/4) lane groups merge every NG-th split with an online rescale (their
+// loads are independent, so a group keeps several in flight instead of one dependent round trip
+// per split), then the group states merge through LDS.
 template <int D>
-__global__ void __launch_bounds__(128) attn_combine_kernel(AttnParams p, int T) {
+__global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p, int T) {
+  constexpr int LG = D / 4, NG = 256 / LG;
+  __shared__ f32x4 so[NG][LG];
+  __shared__ float sml[NG][2];
   const int th = blockIdx.x;  // t * nh + head
-  const int d = threadIdx.x;
-  float M = -1e30f;
-  for (int s = 0; s < p.num_splits; ++s)
-    M = fmaxf(M, p.part_ml[((size_t)s * T * p.nh + th) * 2]);
-  float O = 0.f, Lt = 0.f;
-  for (int s = 0; s < p.num_splits; ++s) {
-    const float* ml = p.part_ml + ((size_t)s * T * p.nh + th) * 2;
-    const float f = __builtin_amdgcn_exp2f(ml[0] - M);
-    Lt += f * ml[1];
-    O += f * p.part_o[((size_t)s * T * p.nh + th) * D + d];
+  const int grp = threadIdx.x / LG, l = threadIdx.x % LG;
+  const size_t stride = (size_t)T * p.nh;
+  float m = -1e30f, s = 0.f;
+  f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int sp = grp; sp < p.num_splits; sp += NG) {
+    const size_t r = (size_t)sp * stride + th;
+    const float mi = p.part_ml[r * 2], li = p.part_ml[r * 2 + 1];
+    const f32x4 oi = *reinterpret_cast<const f32x4*>(p.part_o + r * D + 4 * l);
+    const float mn = fmaxf(m, mi);
+    const float a = __builtin_amdgcn_exp2f(m - mn), b = __builtin_amdgcn_exp2f(mi - mn);
+    o = o * a + oi * b;
+    s = s * a + li * b;
+    m = mn;
   }
-  p.out[(size_t)th * D + d] = (bf16)(Lt > 0.f ? O / Lt : 0.f);
+  so[grp][l] = o;
+  if (l == 0) {
+    sml[grp][0] = m;
+    sml[grp][1] = s;
+  }
+  __syncthreads();
+  if (grp != 0) return;
+  float M = -1e30f;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) M = fmaxf(M, sml[g][0]);
+  float Lt = 0.f;
+  f32x4 O = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const float f = __builtin_amdgcn_exp2f(sml[g][0] - M);
+    Lt += f * sml[g][1];
+    O += f * so[g][l];
+  }
+  const float inv = Lt > 0.f ? 1.f / Lt : 0.f;
+  bf16x4 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = (bf16)(O[r] * inv);
+  *reinterpret_cast<bf16x4*>(p.out + (size_t)th * D + 4 * l) = v;
 }
 
 // ===========================================================================================
@@ -529,21 +626,35 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw
 }
 
 // ------------------------------------------------------------------------------------------
+template <int D, bool WIN, bool FP8>
+static void decode_grid(const AttnParams& p, int items, int gs, hipStream_t stream) {
+  const int grid = (items + 3) / 4;
+  if (p.num_splits > 1)
+    attn_decode_kernel<D, WIN, FP8, true><<<grid, 256, 0, stream>>>(p, items, gs);
+  else
+    attn_decode_kernel<D, WIN, FP8, false><<<grid, 256, 0, stream>>>(p, items, 1);
+}
+
 template <int D>
 static int launch_decode_d(const AttnParams& p, int B, hipStream_t stream) {
   const int G = p.nh / p.nkv;
   const int hgroups = (G + 15) / 16;
   const long items = (long)B * p.nkv * hgroups * p.num_splits;
   if (items > (1L << 30)) return -3;
-  const int grid = (int)((items + 3) / 4);
+  // splits merged inside a workgroup (its 4 waves hold consecutive splits of one item)
+  const int gs = p.num_splits % 4 == 0 ? 4 : p.num_splits % 2 == 0 ? 2 : 1;
   if (p.ring > 0) {
-    if (p.kv_fp8) attn_decode_kernel<D, true, true><<<grid, 256, 0, stream>>>(p, (int)items);
-    else attn_decode_kernel<D, true, false><<<grid, 256, 0, stream>>>(p, (int)items);
+    if (p.kv_fp8) decode_grid<D, true, true>(p, (int)items, gs, stream);
+    else decode_grid<D, true, false>(p, (int)items, gs, stream);
   } else {
-    if (p.kv_fp8) attn_decode_kernel<D, false, true><<<grid, 256, 0, stream>>>(p, (int)items);
-    else attn_decode_kernel<D, false, false><<<grid, 256, 0, stream>>>(p, (int)items);
+    if (p.kv_fp8) decode_grid<D, false, true>(p, (int)items, gs, stream);
+    else decode_grid<D, false, false>(p, (int)items, gs, stream);
   }
-  if (p.num_splits > 1) attn_combine_kernel<D><<<B * p.nh, D, 0, stream>>>(p, B);
+  if (p.num_splits > gs) {
+    AttnParams pc = p;
+    pc.num_splits = p.num_splits / gs;
+    attn_combine_kernel<D><<<B * p.nh, 256, 0, stream>>>(pc, B);
+  }
   return 0;
 }
 

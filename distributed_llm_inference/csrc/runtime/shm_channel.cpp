@@ -64,6 +64,8 @@ class ShmChannel {
         throw std::runtime_error("ftruncate failed");
       }
     } else {
+      // wait for the creator without the GIL (it may be another thread of this process)
+      py::gil_scoped_release nogil;
       const uint64_t deadline = now_ns() + (uint64_t)(open_timeout_s * 1e9);
       while (true) {
         fd = shm_open(name.c_str(), O_RDWR, 0600);
@@ -95,6 +97,7 @@ class ShmChannel {
       std::atomic_thread_fence(std::memory_order_release);
       reinterpret_cast<std::atomic<uint64_t>*>(&hdr_->magic)->store(kMagic, std::memory_order_release);
     } else {
+      py::gil_scoped_release nogil;
       const uint64_t deadline = now_ns() + (uint64_t)(open_timeout_s * 1e9);
       while (reinterpret_cast<std::atomic<uint64_t>*>(&hdr_->magic)->load(std::memory_order_acquire) != kMagic) {
         if (now_ns() > deadline) throw std::runtime_error("shm channel never initialised");

@@ -183,14 +183,21 @@ def rope_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
 # ----------------------------------------------------------------------------- attention
 def decode_splits(batch: int, nkv: int, group: int, max_len: int, cu: int = 256) -> int:
     """Split-K factor for decode.  The kernel runs one wave per (sequence, kv head, 16-head group,
-    split); aim for ~2 waves per SIMD (8 per CU) while keeping >= 4 key steps per split."""
+    split); aim for ~4 waves per CU (measured best on the 70B head config from B = 1 to 16, 8k-32k
+    contexts: profiles/attn_decode_microbench.json) while keeping >= 1 key step per split.  Splits come
+    in multiples of 4 from 4 up (a workgroup's 4 waves merge theirs in LDS, csrc/kernels/
+    attention.hip), so B = 1 at 8k context runs 256 splits (2048 waves) instead of the 64 the
+    unmerged partial traffic used to allow."""
     waves = batch * nkv * ((group + 15) // 16)
-    target = 8 * cu
-    if waves >= target:
+    if waves >= 8 * cu:
         return 1
+    target = 4 * cu
     want = (target + waves - 1) // waves
-    max_useful = max(1, max_len // 128)
-    return int(max(1, min(want, max_useful, 64)))
+    max_useful = max(1, (max_len + 31) // 32)
+    s = int(max(1, min(want, max_useful, 512)))
+    if s >= 4:
+        return s // 4 * 4
+    return 2 if s == 3 else s
 
 
 def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink=0, sink_pad=0,
@@ -202,16 +209,20 @@ def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_si
     out = torch.empty_like(q) if out is None else out
     part_o = part_ml = None
     if num_splits > 1:
-        B, nh, D = q.shape
         if workspace is None:
-            part_o = torch.empty(num_splits * B * nh * D, dtype=torch.float32, device=q.device)
-            part_ml = torch.empty(num_splits * B * nh * 2, dtype=torch.float32, device=q.device)
-        else:
-            part_o, part_ml = workspace
+            workspace = decode_workspace(q.shape[0], q.shape[1], q.shape[2], num_splits, q.device)
+        part_o, part_ml = workspace
     native().attn_decode(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, float(scale),
                          int(n_sink), int(sink_pad), int(ring), int(window), int(num_splits),
                          part_o, part_ml, float(k_scale), float(v_scale))
     return out
+
+
+def decode_workspace(rows: int, nh: int, head_dim: int, splits: int, device):
+    """Split-K decode workspace: fp32 partial O and (max, sum) per split (sized for the unmerged
+    worst case; the kernel uses splits / 4 of it when its workgroups merge their splits)."""
+    return (torch.empty(splits * rows * nh * head_dim, dtype=torch.float32, device=device),
+            torch.empty(splits * rows * nh * 2, dtype=torch.float32, device=device))
 
 
 def prefill_tile_tokens(nh: int, nkv: int) -> int:

@@ -370,7 +370,7 @@ class StageFollower:
 
 
 def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
-                   rccl_timeout_s: float = 300.0) -> Transport:
+                   rccl_timeout_s: float = 300.0, rank_offset: int = 0) -> Transport:
     """RCCL P2P on GPUs (default); ``DLI_TRANSPORT=host`` stages GPU tensors through gloo
     (several ranks sharing one GPU — an explicit opt-in, never chosen silently); gloo on CPU.
 
@@ -378,7 +378,11 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
     came up (a failure or a peer that never arrives ends in a timeout, not a hang), and if ANY rank
     failed, EVERY rank raises :class:`TransportInitError` with the failing ranks and the error, so
     a multi-GPU run either moves hidden states over RCCL or exits non-zero.
-    ``DLI_TRANSPORT=rccl-or-host`` restores the old agreed fallback to the host-staged transport."""
+    ``DLI_TRANSPORT=rccl-or-host`` restores the old agreed fallback to the host-staged transport.
+
+    ``rank`` / ``world`` are the stage index and stage count of ONE pipeline replica; with several
+    replicas (data parallel) ``rank_offset`` is the replica's first global rank and ``job`` names
+    the replica, so every replica gets its own RCCL pair communicators."""
     if world == 1:
         return LoopbackTransport(1)
     kind = os.environ.get("DLI_TRANSPORT", "rccl" if device.type == "cuda" else "gloo")
@@ -411,13 +415,13 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
             raise TransportInitError(msg)
         log.warning(msg + "; DLI_TRANSPORT=rccl-or-host: falling back to host-staged transport")
         from .transport import HostStagedTransport
-        return HostStagedTransport()
+        return HostStagedTransport(rank_offset=rank_offset)
     if device.type == "cuda":
         if kind != "host":
             raise ValueError(f"DLI_TRANSPORT={kind!r}: expected rccl, rccl-or-host or host")
         from .transport import HostStagedTransport
-        return HostStagedTransport()
-    return TorchDistTransport()
+        return HostStagedTransport(rank_offset=rank_offset)
+    return TorchDistTransport(rank_offset=rank_offset)
 
 
 class TransportInitError(RuntimeError):

@@ -67,20 +67,22 @@ class Transport:
 
 
 class TorchDistTransport(Transport):
-    """Blocking torch.distributed P2P (gloo on CPU)."""
+    """Blocking torch.distributed P2P (gloo on CPU).  Peers are stage indices inside this
+    pipeline replica; ``rank_offset`` (the replica's first global rank) maps them to global ranks."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, rank_offset: int = 0):
         self.group = group
-        self.rank = dist.get_rank()
+        self.offset = rank_offset
+        self.rank = dist.get_rank() - rank_offset
         self.world = dist.get_world_size()
 
     def send(self, t, peer):
         self._count(t, True)
-        dist.send(t.contiguous(), peer, group=self.group)
+        dist.send(t.contiguous(), peer + self.offset)
 
     def recv(self, t, peer, free_event=None):
         t0 = time.perf_counter()
-        dist.recv(t, peer, group=self.group)
+        dist.recv(t, peer + self.offset)
         self.recv_wait_ms += (time.perf_counter() - t0) * 1e3
         self._count(t, False)
         return t
@@ -94,21 +96,22 @@ class HostStagedTransport(Transport):
     single-GPU box.  Never the production path on a multi-GPU node.
     """
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, rank_offset: int = 0):
         self.group = group
-        self.rank = dist.get_rank()
+        self.offset = rank_offset
+        self.rank = dist.get_rank() - rank_offset
         self.world = dist.get_world_size()
 
     def send(self, t, peer):
         self._count(t, True)
-        dist.send(t.detach().to("cpu").contiguous(), peer, group=self.group)
+        dist.send(t.detach().to("cpu").contiguous(), peer + self.offset)
 
     def recv(self, t, peer, free_event=None):
         if free_event is not None:
             free_event.synchronize()
         host = torch.empty(t.shape, dtype=t.dtype)
         t0 = time.perf_counter()
-        dist.recv(host, peer, group=self.group)
+        dist.recv(host, peer + self.offset)
         self.recv_wait_ms += (time.perf_counter() - t0) * 1e3
         t.copy_(host, non_blocking=False)
         self._count(t, False)

@@ -42,6 +42,7 @@ class EngineConfig:
     quantize: object = False        # False | True / "fp8" (e4m3 weights) | "int8" (LLM.int8)
     int8_threshold: float = 6.0     # LLM.int8 outlier threshold (quantize="int8")
     pp: int = 1
+    dp: int = 1                     # pipeline replicas (world = dp x pp in init_pipeline_rank)
     cache: CacheConfig = field(default_factory=CacheConfig)
     serve: ServeConfig = field(default_factory=ServeConfig)
 
@@ -153,14 +154,60 @@ class LLMEngine:
 
 
 # =============================================================================================
+@dataclass(frozen=True)
+class ReplicaLayout:
+    """DP x PP placement of one node's ranks: ``dp`` independent pipeline replicas of ``pp``
+    stages each; replica r owns the consecutive ranks [r*pp, (r+1)*pp) (consecutive GPUs, so every
+    stage hop stays on a direct xGMI link).  The reference's swarm hosts the same blocks on several
+    servers (reference server/server.py:7-8,20; server/worker.py:9-20); on one MI355X node that is a
+    replica of the whole layer range per pipeline."""
+    dp: int
+    pp: int
+
+    @staticmethod
+    def for_world(world: int, dp: int = 1) -> "ReplicaLayout":
+        dp = max(1, int(dp))
+        if world % dp:
+            raise ValueError(f"world size {world} is not a multiple of dp={dp}")
+        return ReplicaLayout(dp, world // dp)
+
+    def replica(self, rank: int) -> int:
+        return rank // self.pp
+
+    def stage(self, rank: int) -> int:
+        return rank % self.pp
+
+    def ranks(self, replica: int) -> List[int]:
+        return list(range(replica * self.pp, (replica + 1) * self.pp))
+
+    def drivers(self) -> List[int]:
+        return [r * self.pp for r in range(self.dp)]
+
+    def describe(self, spec: ModelSpec) -> dict:
+        ranges = plan_stages(spec, self.pp)
+        return {"dp": self.dp, "pp": self.pp,
+                "replicas": [{"replica": r, "driver_rank": r * self.pp,
+                              "stages": [{"rank": r * self.pp + i, "gpu": r * self.pp + i,
+                                          "layers": list(rg)} for i, rg in enumerate(ranges)]}
+                             for r in range(self.dp)]}
+
+
+def _dp_from_env(cfg: EngineConfig) -> int:
+    return int(os.environ.get("DLI_DP", cfg.dp or 1))
+
+
 def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     """Bootstrap this rank of a multi-process pipeline (env: RANK, WORLD_SIZE, LOCAL_RANK,
-    MASTER_ADDR, MASTER_PORT).  Returns ``("driver", DistributedDriver | LocalPipeline)`` on rank 0
-    and ``("follower", StageFollower)`` elsewhere."""
+    MASTER_ADDR, MASTER_PORT; ``DLI_DP`` or ``cfg.dp`` = number of pipeline replicas).  Returns
+    ``("driver", DistributedDriver | LocalPipeline)`` on the first rank of every replica and
+    ``("follower", StageFollower)`` elsewhere.  Every returned object carries ``replica``,
+    ``layout`` and ``drivers_group`` (a gloo group over the replica drivers, None for dp == 1)."""
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", rank))
     spec = resolve_model(cfg.checkpoint or cfg.model)
+    layout = ReplicaLayout.for_world(world, _dp_from_env(cfg))
+    rep, srank, pp = layout.replica(rank), layout.stage(rank), layout.pp
     kv_share = 1.0
     if torch.cuda.is_available():
         # DLI_SHARE_GPU=1: several stage processes on the visible GPUs round-robin (tests on a
@@ -173,29 +220,47 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
+
+    def tag(obj):
+        obj.replica, obj.layout, obj.drivers_group = rep, layout, drivers_group
+        return obj
+
+    drivers_group = None
     if world == 1:
         eng = LLMEngine(cfg.model, pp=1, device=device, cfg=cfg)
-        return "driver", eng.pipeline
+        return "driver", tag(eng.pipeline)
     if not dist.is_initialized():
         dist.init_process_group(backend)
-    group = dist.group.WORLD
+    # every rank creates every group, in the same order (torch.distributed requirement)
+    rep_groups = [dist.new_group(layout.ranks(r)) for r in range(layout.dp)] if layout.dp > 1 \
+        else [dist.group.WORLD]
+    if layout.dp > 1:
+        drivers_group = dist.new_group(layout.drivers())
+    group = rep_groups[rep]
     store = dist.distributed_c10d._get_default_store()
     if rank == 0:
         store.set("dli_job", uuid.uuid4().hex[:12])
     job = store.get("dli_job").decode()
-    ranges = plan_stages(spec, world)
+    if layout.dp > 1:
+        job = f"{job}r{rep}"
+    if pp == 1:
+        # a single-stage replica: its own in-process pipeline on this GPU
+        eng = LLMEngine(cfg.model, pp=1, device=device, cfg=cfg)
+        dist.barrier()
+        return "driver", tag(eng.pipeline)
+    ranges = plan_stages(spec, pp)
     if os.environ.get("DLI_STAGE_RANGES"):  # placement chosen by the server (rebalance)
         import json
         ranges = [tuple(r) for r in json.loads(os.environ["DLI_STAGE_RANGES"])]
-        if len(ranges) != world:
-            raise ValueError("DLI_STAGE_RANGES must have one range per rank")
-    start, end = ranges[rank]
+        if len(ranges) != pp:
+            raise ValueError("DLI_STAGE_RANGES must have one range per pipeline stage")
+    start, end = ranges[srank]
     ex = build_executor(spec, start, end, device, cfg, group=group, kv_share=kv_share)
-    channels = _Channels(job, rank, world)
-    transport = make_transport(rank, world, device, job=job)
-    dist.barrier(group=group)
+    channels = _Channels(job, srank, pp)
+    transport = make_transport(srank, pp, device, job=job, rank_offset=rep * pp)
+    dist.barrier()
     channels.unlink()  # every rank has attached: nothing may be left in /dev/shm after this
-    if rank == 0:
-        sched = make_scheduler(spec, ex, cfg, world)
-        return "driver", DistributedDriver(ex, sched, transport, channels, world, group)
-    return "follower", StageFollower(ex, transport, channels, rank, world, group)
+    if srank == 0:
+        sched = make_scheduler(spec, ex, cfg, pp)
+        return "driver", tag(DistributedDriver(ex, sched, transport, channels, pp, group))
+    return "follower", tag(StageFollower(ex, transport, channels, srank, pp, group))

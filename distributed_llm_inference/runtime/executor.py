@@ -292,9 +292,8 @@ class StageExecutor:
         ws = getattr(self, "_ws", {})
         self._ws = ws
         if key not in ws:
-            nh, D = self.spec.num_heads, self.spec.head_dim
-            ws[key] = (torch.empty(splits * rows * nh * D, dtype=torch.float32, device=self.device),
-                       torch.empty(splits * rows * nh * 2, dtype=torch.float32, device=self.device))
+            ws[key] = ops.decode_workspace(rows, self.spec.num_heads, self.spec.head_dim, splits,
+                                           self.device)
         return ws[key]
 
     def _splits(self, rows: int) -> int:

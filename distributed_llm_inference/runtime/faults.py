@@ -133,7 +133,8 @@ class StageStats:
             rec = {"step_ms": self.ewma, "steps": self.steps}
             if self.transport is not None:
                 rec.update(self.transport.traffic())
-            self._store.set(f"dli_stats/{self.rank}", json.dumps(rec))
+            # keyed by GLOBAL rank: with several pipeline replicas stage indices repeat
+            self._store.set(f"dli_stats/{os.environ.get('RANK', self.rank)}", json.dumps(rec))
         except Exception:
             pass
 

@@ -1,8 +1,10 @@
 """Decode-attention microbenchmark (Llama-3-70B head config) on one MI355X.
 
 KV caches are sized far beyond the 256 MiB Infinity Cache and each call reads a different layer's
-cache (rotating), so every call streams K/V from HBM as in the real decode step.
+cache (rotating), so every call streams K/V from HBM as in the real decode step.  Calls are timed
+from a captured hipGraph replay (as the engine runs them: no host launch cost in the number).
 Prints µs per call and achieved KV bandwidth; writes gpurun_out/attn_bench.json.
+``--sweep`` also times other split counts for the small-batch cases.
 """
 import json
 import os
@@ -16,10 +18,11 @@ from distributed_llm_inference import ops  # noqa: E402
 
 dev = torch.device("cuda:0")
 nh, nkv, D, bs = 64, 8, 128, 64
-CASES = [(256, 590), (256, 2048), (64, 4096), (16, 8192), (1, 8192), (1, 600)]
+CASES = [(512, 600), (256, 2048), (64, 4096), (16, 8192), (16, 32768), (4, 16384), (1, 8192),
+         (1, 32768), (1, 600)]
 
 
-def run(B, L, layers=None):
+def run(B, L, layers=None, splits=None):
     blocks_per_seq = (L + bs - 1) // bs
     nblk = B * blocks_per_seq
     per_layer = 2 * nblk * nkv * bs * D * 2
@@ -29,10 +32,10 @@ def run(B, L, layers=None):
     bt = torch.randperm(nblk, device=dev).to(torch.int32).view(B, blocks_per_seq)
     lens = torch.full((B,), L, dtype=torch.int32, device=dev)
     q = torch.randn(B, nh, D, device=dev, dtype=torch.bfloat16)
-    splits = ops.decode_splits(B, nkv, nh // nkv, L)
+    splits = splits or ops.decode_splits(B, nkv, nh // nkv, L)
     ws = None
     if splits > 1:
-        ws = (torch.empty(splits * B * nh * D, device=dev), torch.empty(splits * B * nh * 2, device=dev))
+        ws = ops.decode_workspace(B, nh, D, splits, dev)
     out = torch.empty_like(q)
 
     def call(i):
@@ -42,12 +45,19 @@ def run(B, L, layers=None):
     for i in range(layers):
         call(i)
     torch.cuda.synchronize()
-    n = 10 * layers
-    t0 = time.perf_counter()
-    for i in range(n):
-        call(i)
+    n = max(layers, 8)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(n):
+            call(i)
+    g.replay()
     torch.cuda.synchronize()
-    us = (time.perf_counter() - t0) / n * 1e6
+    reps = 20
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / (n * reps) * 1e6
     kv_bytes = 2 * B * L * nkv * D * 2
     # numerics spot check against the fp32 reference on a few sequences
     ref = ops.reference.attn_decode(q[:2].cpu(), None, ks[0].cpu(), vs[0].cpu(), bt[:2].cpu(),
@@ -62,9 +72,20 @@ def run(B, L, layers=None):
 
 
 res = []
+for a in sys.argv[1:]:
+    if a.startswith("--cases="):   # e.g. --cases=1x8192,4x16384
+        CASES = [tuple(int(v) for v in c.split("x")) for c in a.split("=", 1)[1].split(",")]
 for B, L in CASES:
     r = run(B, L)
     print(r, flush=True)
     res.append(r)
+if "--sweep" in sys.argv:
+    for B, L in [(1, 8192), (1, 32768), (4, 16384), (16, 8192), (16, 32768), (64, 2048)]:
+        for sp in (4, 8, 16, 32, 64, 128, 256):
+            if sp * 32 <= L:
+                r = run(B, L, splits=sp)
+                r["sweep"] = True
+                print(r, flush=True)
+                res.append(r)
 os.makedirs("gpurun_out", exist_ok=True)
 json.dump(res, open("gpurun_out/attn_bench.json", "w"), indent=1)

@@ -62,3 +62,38 @@ def test_bench_multirank_json_contract(n):
     for i, r in enumerate(pr):
         assert r["bytes_sent"] == (steps * (n + 1) * mb_bytes if i < n - 1 else 0), r
         assert r["bytes_recv"] == (steps * (n + 1) * mb_bytes if i > 0 else 0), r
+
+
+@pytest.mark.parametrize("n,dp", [(4, 2), (2, 2)])
+def test_bench_replicas_json_contract(n, dp):
+    """``--dp``: dp independent pipeline replicas of n/dp stages (dp2 x pp2 over gloo, and two
+    single-stage replicas); one JSON line whose tokens count every replica's sequences."""
+    steps, warmup, bpm = 3, 1, 4
+    pp = n // dp
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", str(n), "--dp", str(dp), "--steps", str(steps),
+           "--warmup", str(warmup), "--model", "tiny-llama-8l", "--batch-per-mb", str(bpm),
+           "--prompt-len", "16", "--max-batched-tokens", "64"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    for k in REQUIRED:
+        assert k in d, k
+    assert d["config"]["parallelism"] == f"dp{dp}xpp{pp}"
+    assert d["replicas"] == dp and d["stages_per_replica"] == pp
+    M = pp + 1 if pp > 1 else 1
+    assert d["micro_batches"] == M
+    G = d["config"]["global_batch"]
+    assert G == dp * M * bpm and d["tokens_timed"] == steps * G
+    assert abs(d["value"] - d["tokens_timed"] / (d["ms_per_step"] * steps / 1e3)) < 0.02 * d["value"]
+    pr = d["per_rank"]
+    assert [r["rank"] for r in pr] == list(range(n))
+    assert [r["replica"] for r in pr] == [i // pp for i in range(n)]
+    for rep in range(dp):
+        rr = [r["stage"] for r in pr if r["replica"] == rep]
+        assert rr[0][0] == 0 and rr[-1][1] == 8 and all(
+            rr[i][1] == rr[i + 1][0] for i in range(len(rr) - 1))

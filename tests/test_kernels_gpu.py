@@ -153,6 +153,51 @@ def test_attn_decode_window(gpu, splits):
     _close(out, out_r, 2e-2, 2e-2, "decode-window")
 
 
+@pytest.mark.parametrize("splits", [1, 2, 4, 12, 64, 256, 6, 3])
+def test_attn_decode_long_context(gpu, splits):
+    """16k-32k contexts (70B head config) through every split path: one split, workgroup-merged
+    splits with nothing left to merge (2, 4), groups of 4 merged in LDS whose partials the combine
+    kernel finishes (12, 64, 256), pairs merged in LDS then combined (6), unmerged splits (3)."""
+    torch.manual_seed(21)
+    nh, nkv, D, bs = 64, 8, 128, 64
+    lens = torch.tensor([16384, 32768 - 5, 20001], dtype=torch.int32)
+    B = lens.numel()
+    max_blocks = (int(lens.max()) + bs - 1) // bs
+    nblocks = B * max_blocks
+    kc, vc = _make_cache(nblocks, nkv, bs, D, gpu)
+    bt = _tables(B, max_blocks, nblocks, gpu, seed=7)
+    q = torch.randn(B, nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    out = ops.attn_decode(q, None, kc, vc, bt, lens.to(gpu), scale, num_splits=splits)
+    out_r = ref.attn_decode(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, scale)
+    _close(out, out_r, 1e-2, 2e-2, f"decode-long-s{splits}")
+
+
+@pytest.mark.parametrize("splits", [1, 8, 64])
+def test_attn_decode_window_multi_wrap(gpu, splits):
+    """StreamingLLM ring at a realistic window (W = 4096, 4 sinks) after several wraps of the
+    ring, scored in slot space against the re-rotation-free reference."""
+    torch.manual_seed(22)
+    nh, nkv, D, bs = 64, 8, 128, 64
+    n_sink, sink_pad, window = 4, 64, 4096
+    ring = window - n_sink + 60   # ring rounded up to whole 32-slot steps (>= window - sinks)
+    ring = (ring + 31) // 32 * 32
+    lens = torch.tensor([3, 4000, 4097, 9000, 13001], dtype=torch.int32)
+    B = lens.numel()
+    max_blocks = (sink_pad + ring + bs - 1) // bs
+    nblocks = B * max_blocks
+    kc, vc = _make_cache(nblocks, nkv, bs, D, gpu)
+    bt = _tables(B, max_blocks, nblocks, gpu, seed=8)
+    q = torch.randn(B, nh, D, device=gpu, dtype=BF)
+    qs = torch.randn(B, nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    out = ops.attn_decode(q, qs, kc, vc, bt, lens.to(gpu), scale, n_sink, sink_pad, ring, window,
+                          num_splits=splits)
+    out_r = ref.attn_decode(q.cpu(), qs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), lens, scale, n_sink,
+                            sink_pad, ring, window)
+    _close(out, out_r, 1e-2, 2e-2, f"decode-window-wrap-s{splits}")
+
+
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (8, 8, 64), (4, 2, 32)])
 @pytest.mark.parametrize("tiles", [False, True])
 def test_attn_prefill(gpu, nh, nkv, D, tiles):

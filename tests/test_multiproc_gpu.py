@@ -4,7 +4,8 @@ On a ONE-GPU box stage processes share the card (``DLI_SHARE_GPU=1``).  RCCL ref
 the same device, so there the full driver/follower GPU path (graphs, shm control plane, token
 feedback, micro-batching) runs over the host-staged transport, the RCCL binding is exercised with
 a 1-rank communicator, and the RCCL-failure path (all ranks agree, fall back together) is tested
-by asking for RCCL on a shared GPU.  With two or more GPUs the RCCL P2P transport and a PP=2
+by asking for RCCL on a shared GPU: by default every rank fails loudly, and only the explicit
+``DLI_TRANSPORT=rccl-or-host`` opt-in falls back.  With two or more GPUs the RCCL P2P transport and a PP=2
 RCCL pipeline are tested for real.
 """
 import multiprocessing as mp
@@ -89,25 +90,42 @@ def test_multiprocess_pipeline_on_gpu(gpu, world, mbs):
     assert got == ref
 
 
-def test_rccl_failure_falls_back_to_host_transport(gpu):
-    """Two ranks on ONE GPU with the default RCCL transport: RCCL rejects the duplicate device,
-    every rank must agree on the failure (non-blocking init, no hang) and fall back together to
-    the host-staged transport, producing the same tokens as PP=1."""
+def _run_pair(transport, timeout=600):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_pipeline_worker, args=(r, 2, port, 3, q, transport)) for r in range(2)]
+    for p in ps:
+        p.start()
+    msgs = [q.get(timeout=timeout)]
+    for p in ps:
+        p.join(120)
+    while not q.empty():
+        msgs.append(q.get(timeout=5))
+    return msgs, ps
+
+
+def test_rccl_failure_is_loud_by_default(gpu):
+    """Two ranks on ONE GPU with the default RCCL transport: RCCL rejects the duplicate device and
+    EVERY rank must raise TransportInitError (agreed through the store: no hang, no silent
+    host-staged fallback, non-zero exit codes)."""
+    msgs, ps = _run_pair("rccl")
+    assert msgs and all(m[0] == "err" for m in msgs), msgs
+    assert any("TransportInitError" in m[1] and "RCCL transport unavailable" in m[1] for m in msgs)
+    assert all(p.exitcode not in (0, None) for p in ps), [p.exitcode for p in ps]
+
+
+def test_rccl_failure_falls_back_with_opt_in(gpu):
+    """``DLI_TRANSPORT=rccl-or-host``: the same RCCL failure, agreed on by all ranks, falls back
+    together to the host-staged transport, producing the same tokens as PP=1."""
     from distributed_llm_inference.runtime.engine import LLMEngine
     from distributed_llm_inference.runtime.sequence import SamplingParams
     os.environ["DLI_TUNABLEOP"] = "0"
     spec, cfg = _cfg(1, 3)
     ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
         PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    ps = [ctx.Process(target=_pipeline_worker, args=(r, 2, port, 3, q, "rccl")) for r in range(2)]
-    for p in ps:
-        p.start()
-    status, got, *rest = q.get(timeout=600)
-    for p in ps:
-        p.join(120)
+    msgs, ps = _run_pair("rccl-or-host")
+    status, got, *rest = msgs[0]
     assert status == "ok", got
     assert all(p.exitcode == 0 for p in ps)
     assert got == ref
