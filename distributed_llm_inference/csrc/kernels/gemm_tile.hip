@@ -129,7 +129,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // FP8 / INT8: A and B are 1-byte elements (K counted in elements = bytes) with fp32 a_scale[M]
 // (per row) and b_scale[N] (per output channel).  Staging is byte-identical to bf16: a k-tile is
 // 128 bytes of every row (64 bf16, 128 fp8 / int8).
-template <int EPI, int PREC>
+template <int EPI, int PREC, bool SKT>
 __global__ void __launch_bounds__(kThreads, 1)
 gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __restrict__ C,
                  const float* __restrict__ a_scale, const float* __restrict__ b_scale,
@@ -149,8 +149,11 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
     const int x = b & 7, q = n >> 3, r = n & 7;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
   };
-  // (bf16 only: in the 1-byte variants the hand-off code pushes the allocator into spilling)
-  constexpr bool kSk = PREC == kBf16 && EPI != kStoreF32;
+  // the stream-K hand-off is a separate instantiation: compiled into the whole-tile kernels it
+  // pushed the allocator to 256 VGPRs + 104 B/lane of scratch spills in the main loop (bf16 store
+  // and SwiGLU variants), which cost the plain kernels ~10 % (bf16 only: in the 1-byte variants
+  // the hand-off code spills even on its own)
+  constexpr bool kSk = SKT && PREC == kBf16 && EPI != kStoreF32;
   const bool is_sk = kSk && (int)blockIdx.x >= sk.n_dp;
   const int lid = is_sk ? remap(blockIdx.x - sk.n_dp, sk.sk_wgs) : remap(blockIdx.x, sk.n_dp);
 
@@ -515,8 +518,9 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
   const int tiles_m = (M + kTM - 1) / kTM, tiles_n = N / kTN;
   const int tiles = tiles_m * tiles_n;
   SkArgs sk{0, 0, nullptr, nullptr, nullptr};
-    if (splits == 0) {
-    if (PREC != kBf16) return -10;   // the stream-K tail is compiled for bf16 operands only
+  if constexpr (PREC != kBf16) {
+    if (splits == 0) return -10;   // the stream-K tail is compiled for bf16 operands only
+  } else if (splits == 0) {
     const int cus = device_cus();
     if (cus <= 0 || cus > kSkMaxWgs) return -7;
     if (workspace == nullptr || epilogue == kStoreF32) return -3;
@@ -531,11 +535,11 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
     if (hipMemsetAsync(workspace, 0, ((size_t)cus * 4 + 15) / 16 * 16, stream) != hipSuccess) return -9;
     const int grid = sk.n_dp + sk.sk_wgs;
     if (epilogue == kSwiGLU)
-      gemm_tile_kernel<kSwiGLU, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
-                                                                    tiles_m, tiles_n, kt, sk);
+      gemm_tile_kernel<kSwiGLU, PREC, true><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
+                                                                          tiles_m, tiles_n, kt, sk);
     else if (epilogue == kStoreBf16)
-      gemm_tile_kernel<kStoreBf16, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
-                                                                       tiles_m, tiles_n, kt, sk);
+      gemm_tile_kernel<kStoreBf16, PREC, true><<<grid, kThreads, 0, stream>>>(
+          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kt, sk);
     else
       return -4;
     return 0;
@@ -548,8 +552,8 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
   const int grid = tiles * splits;
   sk.n_dp = grid;
   if (splits > 1) {
-    gemm_tile_kernel<kStoreF32, PREC><<<grid, kThreads, 0, stream>>>(A, B, workspace, sa, sb, M, N,
-                                                                    K, tiles_m, tiles_n, kps, sk);
+    gemm_tile_kernel<kStoreF32, PREC, false><<<grid, kThreads, 0, stream>>>(
+        A, B, workspace, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk);
     if (epilogue == kStoreF32) return 0;
     const size_t MN = (size_t)M * N;
     size_t blocks = (MN / 8 + 255) / 256;
@@ -557,11 +561,11 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
     tile_splitk_reduce_kernel<<<(int)blocks, 256, 0, stream>>>(reinterpret_cast<bf16*>(C),
                                                                workspace, splits, MN);
   } else if (epilogue == kSwiGLU) {
-    gemm_tile_kernel<kSwiGLU, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K, tiles_m,
-                                                                  tiles_n, kps, sk);
+    gemm_tile_kernel<kSwiGLU, PREC, false><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
+                                                                         tiles_m, tiles_n, kps, sk);
   } else if (epilogue == kStoreBf16) {
-    gemm_tile_kernel<kStoreBf16, PREC><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
-                                                                     tiles_m, tiles_n, kps, sk);
+    gemm_tile_kernel<kStoreBf16, PREC, false><<<grid, kThreads, 0, stream>>>(
+        A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk);
   } else {
     return -4;
   }
