@@ -78,14 +78,17 @@ def cmd_plan(a) -> int:
     from .runtime.engine import ReplicaLayout
     spec = resolve_model(a.checkpoint or a.model)
     layout = ReplicaLayout.for_world(a.gpus, a.dp)
-    ranges = plan_stages(spec, layout.pp)
+    rotate = layout.pp > 1 and os.environ.get("DLI_HEAD_ROTATION", "1") == "1"
+    ranges = plan_stages(spec, layout.pp, head_rotation=rotate)
     per_layer = spec.layer_param_count() * (1 if (a.fp8 or a.int8) else 2)
     emb = spec.vocab_size * spec.hidden_size * 2
     replicas = []
     for r in range(layout.dp):
         out = []
         for i, (s, e) in enumerate(ranges):
-            w = (e - s) * per_layer + (emb if i == 0 else 0) + (emb if i == len(ranges) - 1 else 0)
+            # every rank holds the LM head when it rotates (runtime/head.py)
+            w = (e - s) * per_layer + (emb if i == 0 else 0) + (
+                emb if (i == len(ranges) - 1 or rotate) else 0)
             free = 288e9 * a.gpu_mem - w
             kv_tok = KVPool.bytes_per_block(spec, e - s, 1, 1 if a.kv_dtype == "fp8" else 2)
             out.append(dict(stage=i, rank=r * layout.pp + i, gpu=r * layout.pp + i, layers=[s, e],
@@ -93,6 +96,7 @@ def cmd_plan(a) -> int:
                             kv_capacity_tokens=int(max(0, free) // kv_tok)))
         replicas.append(dict(replica=r, driver_rank=r * layout.pp, stages=out))
     res = {"model": spec.name, "num_layers": spec.num_layers, "dp": layout.dp, "pp": layout.pp,
+           "lm_head": "rotating over the pipeline ranks (decode)" if rotate else "last stage",
            "layout": f"dp{layout.dp}xpp{layout.pp}" if layout.dp > 1 else f"pp{layout.pp}",
            "stages": replicas[0]["stages"]}
     if layout.dp > 1:

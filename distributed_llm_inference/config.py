@@ -290,11 +290,14 @@ def resolve_model(model: Any) -> ModelSpec:
 # equivalent layer cost.
 # ---------------------------------------------------------------------------------------------
 def plan_stages(spec: ModelSpec, num_stages: int,
-                weights: Optional[Sequence[float]] = None) -> List[Tuple[int, int]]:
+                weights: Optional[Sequence[float]] = None,
+                head_rotation: bool = False) -> List[Tuple[int, int]]:
     """Split ``spec.num_layers`` into ``num_stages`` contiguous ``[start, end)`` ranges.
 
     ``weights`` (optional, one per stage) expresses relative stage speed (e.g. for a degraded GPU
-    during rebalancing); the default is uniform hardware.
+    during rebalancing); the default is uniform hardware.  ``head_rotation``: the decode steps'
+    LM head runs on every rank in turn (runtime/head.py), so its cost is shared evenly instead of
+    trimming the last stage.
     """
     L = spec.num_layers
     if num_stages < 1:
@@ -312,7 +315,10 @@ def plan_stages(spec: ModelSpec, num_stages: int,
     head_cost = 0.6 * spec.vocab_size * spec.hidden_size / max(1, spec.layer_param_count())
     extra = [0.0] * num_stages
     if num_stages > 1:
-        extra[-1] += head_cost
+        if head_rotation:
+            extra = [head_cost / num_stages] * num_stages
+        else:
+            extra[-1] += head_cost
     total = (L + sum(extra))
     tw = sum(w)
     # start below the proportional target, then hand out the remaining layers one at a time to
@@ -378,5 +384,8 @@ class ServeConfig:
     num_micro_batches: int = 0  # 0 -> num_stages (+0) for a full pipeline
     max_seq_len: int = 8192
     use_graphs: bool = True
+    # decode steps' LM head + sampling on every pipeline rank in turn (runtime/head.py) instead of
+    # the last stage only; env DLI_HEAD_ROTATION=0/1 overrides
+    head_rotation: bool = True
     graph_batch_sizes: List[int] = field(default_factory=lambda: [1, 2, 4, 8, 16, 32, 64, 96, 128,
                                                                   160, 192, 224, 256])

@@ -342,7 +342,7 @@ void attn_prefill(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache,
 // ------------------------------------------------------------------------------ sampling
 void sample(Tensor out_tokens, optional<Tensor> out_logprobs, Tensor logits,
             optional<Tensor> temperature, optional<Tensor> top_k, optional<Tensor> top_p,
-            optional<Tensor> seeds, optional<Tensor> step) {
+            optional<Tensor> seeds, optional<Tensor> step, optional<Tensor> ctr) {
   CHECK_DEV(logits);
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [B, V] row-major");
   TORCH_CHECK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat,
@@ -376,6 +376,11 @@ void sample(Tensor out_tokens, optional<Tensor> out_logprobs, Tensor logits,
   if (step.has_value()) {
     CHECK_IN(*step); CHECK_I64(*step);
     p.step = reinterpret_cast<const long*>(step->data_ptr<int64_t>());
+  }
+  if (ctr.has_value()) {
+    CHECK_IN(*ctr); CHECK_I64(*ctr);
+    TORCH_CHECK(ctr->numel() == B, "ctr must have B entries");
+    p.ctr = reinterpret_cast<const long*>(ctr->data_ptr<int64_t>());
   }
   p.out_tokens = out_tokens.data_ptr<int>();
   if (out_logprobs.has_value()) {
@@ -604,7 +609,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sink_pad"), py::arg("ring"), py::arg("window"), py::arg("num_splits"),
         py::arg("part_o"), py::arg("part_ml"), py::arg("k_scale"), py::arg("v_scale"));
   m.def("attn_prefill", &attn_prefill, "paged causal prefill attention (varlen)");
-  m.def("sample", &sample, "greedy / temperature / top-k / top-p sampling");
+  m.def("sample", &sample, "greedy / temperature / top-k / top-p sampling", py::arg("out_tokens"),
+        py::arg("out_logprobs"), py::arg("logits"), py::arg("temperature"), py::arg("top_k"),
+        py::arg("top_p"), py::arg("seeds"), py::arg("step"), py::arg("ctr") = py::none());
   m.def("quant_rowwise", &quant_rowwise, "row-wise fp8 e4m3 quantisation (+fused RMSNorm)",
         py::arg("q_out"), py::arg("scale"), py::arg("x"), py::arg("residual"), py::arg("norm_w"),
         py::arg("eps"), py::arg("residual_out") = py::none());

@@ -58,6 +58,8 @@ struct SampleParams {
   const float* top_p;       // [B] (>=1: disabled)
   const unsigned long long* seeds;  // [B]
   const long* step;         // [1] device counter (read only) or nullptr
+  const long* ctr;          // [B] per-row counters (the sampled token's position in its
+                            // sequence) or nullptr: then (step, row) key the randomness
   int* out_tokens;          // [B]
   float* out_logprobs;      // [B] or nullptr
 };

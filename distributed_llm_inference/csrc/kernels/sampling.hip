@@ -8,8 +8,10 @@
 //     probability mass for top-p), and finally Gumbel-max over the kept set:
 //     argmax(x_i + g_i), g_i = -log(-log(u_i)) — an exact sample of the renormalised softmax with
 //     no sort and no normalisation pass.  u_i comes from a counter-based hash of
-//     (seed, step, row, i) so a replayed graph produces fresh randomness via the device-side step
-//     counter.
+//     (seed, ctr[row], i), ctr = the sampled token's position in its sequence: a seeded request
+//     draws the same tokens whatever batch, micro-batch, pipeline depth or rank samples it, and a
+//     replayed graph gets fresh randomness from the device-side counters.  Without per-row
+//     counters (seed, step, row, i) are used.
 //   * optional log-probability of the chosen token under softmax(x).
 #include "kernels.h"
 
@@ -174,7 +176,9 @@ __global__ void __launch_bounds__(1024) sample_kernel(SampleParams p) {
   // ---------------- Gumbel-max over the kept set ----------------
   const unsigned long long seed = p.seeds ? p.seeds[row] : 0x1234ull;
   const unsigned long long st = p.step ? (unsigned long long)p.step[0] : 0ull;
-  const unsigned long long base = (st * 0x100000001B3ull) ^ ((unsigned long long)row << 40);
+  const unsigned long long base =
+      p.ctr ? (unsigned long long)p.ctr[row] * 0x100000001B3ull
+            : (st * 0x100000001B3ull) ^ ((unsigned long long)row << 40);
   float best = -INFINITY;
   int bi = 0x7fffffff;
   for (int i = threadIdx.x; i < V; i += blockDim.x) {

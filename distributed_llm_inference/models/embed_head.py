@@ -70,6 +70,12 @@ class LMHead(nn.Module):
                 rows: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``hidden``/``residual`` are the last layer's (out, residual) pair (residual may be None
         when ``hidden`` already is the full hidden state).  Only ``rows`` produce logits."""
+        return self.project(self.norm(hidden, residual, rows))
+
+    def norm(self, hidden: torch.Tensor, residual: Optional[torch.Tensor] = None,
+             rows: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The final norm alone (what the last pipeline stage sends when another rank runs the
+        vocabulary projection: runtime/head.py)."""
         if rows is not None:
             hidden = hidden.index_select(0, rows)
             if residual is not None:
@@ -81,6 +87,10 @@ class LMHead(nn.Module):
         else:
             normed, _ = ops.layer_norm(hidden, self.norm_weight, self.norm_bias,
                                        self.spec.rms_norm_eps, residual)
+        return normed
+
+    def project(self, normed: torch.Tensor) -> torch.Tensor:
+        """Vocabulary projection of final-normed hidden states -> logits."""
         if self.proj is None:
             return F.linear(normed, self._tied.weight)
         return self.proj(normed)

@@ -94,14 +94,19 @@ class CausalLMStage(nn.Module):
         return KVPool(self.spec, self.num_layers, num_blocks, block_size, self.device,
                       kv_dtype, window_length, num_sink_tokens, max_chunk, k_scale, v_scale)
 
-    def forward(self, inputs: torch.Tensor, meta: AttnMetadata, pool: KVPool) -> torch.Tensor:
+    def forward(self, inputs: torch.Tensor, meta: AttnMetadata, pool: KVPool,
+                project: bool = True) -> torch.Tensor:
         """``inputs``: token ids [T] (stage 0) or hidden states [T, H].  Returns hidden [T, H]
-        (non-last stage) or logits [R, V] for the rows in ``meta.logits_rows`` (last stage)."""
+        (non-last stage) or logits [R, V] for the rows in ``meta.logits_rows`` (last stage);
+        ``project=False`` on the last stage stops after the final norm (normed hidden [R, H]) for a
+        vocabulary projection that runs on another rank (runtime/head.py)."""
         if self.has_embed:
             hidden = self.embed(inputs, meta.positions)
         else:
             hidden = inputs
         out, res = self.block.forward_tokens(hidden, meta, pool)
         if self.has_head:
+            if not project:
+                return self.head.norm(out, res, meta.logits_rows)
             return self.head(out, res, meta.logits_rows)
         return ops.add(out, res)

@@ -269,13 +269,18 @@ def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
            top_k: Optional[torch.Tensor] = None, top_p: Optional[torch.Tensor] = None,
            seeds: Optional[torch.Tensor] = None, step: Optional[torch.Tensor] = None,
            out: Optional[torch.Tensor] = None, logprobs: Optional[torch.Tensor] = None,
-           generator: Optional[torch.Generator] = None) -> torch.Tensor:
+           generator: Optional[torch.Generator] = None,
+           counters: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``seeds`` + ``counters`` (int64 per row: the sampled token's position in its sequence) key
+    each row's randomness, so a seeded request samples the same tokens in any batch / pipeline;
+    without ``counters`` the device ``step`` and the row index do."""
     if not _gpu(logits):
-        y = ref.sample(logits, temperature, top_k, top_p, generator, seeds=seeds, step=step)
+        y = ref.sample(logits, temperature, top_k, top_p, generator, seeds=seeds, step=step,
+                       counters=counters)
         return out.copy_(y) if out is not None else y
     if out is None:
         out = torch.empty(logits.shape[0], dtype=torch.int32, device=logits.device)
-    native().sample(out, logprobs, logits, temperature, top_k, top_p, seeds, step)
+    native().sample(out, logprobs, logits, temperature, top_k, top_p, seeds, step, counters)
     return out
 
 

@@ -222,18 +222,21 @@ def attn_custom_mask(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale
 def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
            top_k: Optional[torch.Tensor] = None, top_p: Optional[torch.Tensor] = None,
            generator: Optional[torch.Generator] = None, seeds: Optional[torch.Tensor] = None,
-           step: Optional[torch.Tensor] = None) -> torch.Tensor:
+           step: Optional[torch.Tensor] = None,
+           counters: Optional[torch.Tensor] = None) -> torch.Tensor:
     """With ``seeds`` (one per row) each row draws from its own generator seeded by
-    (seed, step), like the HIP kernel's counter-based hash: a sequence's samples do not depend on
-    which other rows share the batch.  (The random streams differ from the kernel's.)"""
+    (seed, counter) — ``counters[b]`` (the token's position in its sequence) or else ``step`` —
+    like the HIP kernel's counter-based hash: a sequence's samples do not depend on which other
+    rows share the batch.  (The random streams differ from the kernel's.)"""
     B, V = logits.shape
     out = torch.empty(B, dtype=torch.int32, device=logits.device)
     st = int(step.reshape(-1)[0]) if step is not None else 0
     for b in range(B):
         g = generator
         if seeds is not None:
+            c = int(counters[b]) if counters is not None else st
             g = torch.Generator(device=logits.device)
-            g.manual_seed((int(seeds[b]) * 0x9E3779B97F4A7C15 + st * 0xBF58476D1CE4E5B9)
+            g.manual_seed((int(seeds[b]) * 0x9E3779B97F4A7C15 + c * 0xBF58476D1CE4E5B9)
                           & 0x7FFFFFFFFFFFFFFF)
         x = logits[b].float()
         t = float(temperature[b]) if temperature is not None else 0.0

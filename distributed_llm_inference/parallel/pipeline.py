@@ -4,7 +4,9 @@ Topology (one node, one process per GPU, launched by ``distribute`` / torchrun):
 
   rank 0 (driver)  : scheduler + stage 0 (embedding + first layers)
   rank i (0<i<N-1) : middle layers
-  rank N-1         : last layers + final norm + LM head + sampling kernel
+  rank N-1         : last layers + final norm [+ LM head + sampling kernel]
+  every rank       : with the rotating head (runtime/head.py), the vocabulary projection +
+                     sampling of the decode steps whose turn it is (step % N)
 
 Per micro-batch step:
   * the driver publishes the step plan (sequence ids, new-token counts, frees, sampling params) on
@@ -198,28 +200,33 @@ class LocalPipeline(DriverBase):
 # multi-process pipeline
 # =============================================================================================
 class _Channels:
-    """Shared-memory control (driver -> all) and token (last -> driver) channels."""
+    """Shared-memory control (driver -> all) and token (rank r -> driver) channels.  Tokens come
+    from the last rank only, or from every rank r >= 1 when the LM head rotates
+    (runtime/head.py): ``toks[r]`` on the driver, ``tok`` on a producing rank."""
 
-    def __init__(self, job: str, rank: int, world: int, slot_size: int = 1 << 20):
+    def __init__(self, job: str, rank: int, world: int, slot_size: int = 1 << 20,
+                 head_rotation: bool = False):
         R = _runtime()
         self.ctrl = None
         self.tok = None
+        self.toks: Dict[int, object] = {}
         if world == 1:
             return
         ctrl_name = f"/dli_{job}_ctrl"
-        tok_name = f"/dli_{job}_tok"
+        producers = list(range(1, world)) if head_rotation else [world - 1]
         if rank == 0:
             self.ctrl = R.ShmChannel(ctrl_name, -1, 64, slot_size, world - 1, True)
-            self.tok = R.ShmChannel(tok_name, 0, 64, slot_size, 1, False, 120.0)
+            for r in producers:
+                self.toks[r] = R.ShmChannel(f"/dli_{job}_tok{r}", 0, 64, slot_size, 1, False, 120.0)
+            self.tok = self.toks[world - 1]
         else:
             self.ctrl = R.ShmChannel(ctrl_name, rank - 1, 64, slot_size, world - 1, False, 120.0)
-            if rank == world - 1:
-                self.tok = R.ShmChannel(tok_name, -1, 64, slot_size, 1, True)
-
+            if rank in producers:
+                self.tok = R.ShmChannel(f"/dli_{job}_tok{rank}", -1, 64, slot_size, 1, True)
 
     def unlink(self) -> None:
         """Drop the /dev/shm names once every rank has attached (mappings stay valid)."""
-        for ch in (self.ctrl, self.tok):
+        for ch in [self.ctrl, self.tok] + list(self.toks.values()):
             if ch is not None:
                 ch.unlink()
 
@@ -228,7 +235,8 @@ class DistributedDriver(DriverBase):
     """Rank 0 of a multi-process pipeline."""
 
     def __init__(self, executor: StageExecutor, scheduler: Scheduler, transport: Transport,
-                 channels: _Channels, world: int, ctrl_group=None, timeout: float = 300.0):
+                 channels: _Channels, world: int, ctrl_group=None, timeout: float = 300.0,
+                 policy=None, heads=None):
         super().__init__(scheduler)
         self.ex = executor
         self.tr = transport
@@ -240,6 +248,16 @@ class DistributedDriver(DriverBase):
         self.stats = StageStats(0, executor.device)
         self.stats.transport = transport
         self.snapshots: List[dict] = []   # StageStats.snapshot() at every barrier
+        self.policy = policy              # runtime.head.HeadPolicy (None: head on the last rank)
+        self.heads = heads                # runtime.head.HeadJobs of this rank (rotating head)
+        self._head_results: Dict[int, tuple] = {}
+
+    def _head_rank(self, plan: StepPlan) -> int:
+        return self.policy.rank_for(plan) if self.policy is not None else self.world - 1
+
+    def publish_local(self, plan: StepPlan, pinned, ev) -> None:
+        """HeadJobs callback: tokens of a step whose head ran on this (the driver's) rank."""
+        self._head_results[plan.step] = (pinned, ev)
 
     def _issue(self, plan: StepPlan) -> None:
         self.ch.ctrl.send(msgpack.packb(plan.to_wire()), self.timeout)
@@ -250,11 +268,26 @@ class DistributedDriver(DriverBase):
         self.stats.end(tok)
         if plan.seq_ids:
             self.tr.send(out, 1)
+            if self.heads is not None:
+                self.heads.tick()
+                if self._head_rank(plan) == 0:
+                    self.heads.submit(plan)
+        if self.heads is not None:
+            self.heads.poll()
 
     def _collect(self, plan: StepPlan) -> List[int]:
-        msg = msgpack.unpackb(self.ch.tok.recv(self.timeout))
+        hr = self._head_rank(plan)
+        if hr == 0:
+            while plan.step not in self._head_results:
+                self.heads.poll(block=True)   # (enqueues any deferred GPU job first)
+            pinned, ev = self._head_results.pop(plan.step)
+            if ev is not None:
+                ev.synchronize()
+            return pinned.tolist()
+        msg = msgpack.unpackb(self.ch.toks.get(hr, self.ch.tok).recv(self.timeout))
         if msg["step"] != plan.step:
-            raise RuntimeError(f"token stream out of order: got step {msg['step']}, want {plan.step}")
+            raise RuntimeError(f"token stream of rank {hr} out of order: got step {msg['step']}, "
+                               f"want {plan.step}")
         return list(msg["tokens"])
 
     def _broadcast_control(self, kind: str) -> None:
@@ -276,7 +309,8 @@ class StageFollower:
     """Ranks 1..N-1: execute plans as they are published."""
 
     def __init__(self, executor: StageExecutor, transport: Transport, channels: _Channels,
-                 rank: int, world: int, ctrl_group=None, timeout: float = 300.0):
+                 rank: int, world: int, ctrl_group=None, timeout: float = 300.0, policy=None,
+                 heads=None):
         self.ex, self.tr, self.ch = executor, transport, channels
         self.rank, self.world = rank, world
         self.group = ctrl_group
@@ -287,11 +321,43 @@ class StageFollower:
         self.faults = FaultInjector(rank)
         self.stats = StageStats(rank, executor.device)
         self.stats.transport = transport
+        self.policy = policy              # runtime.head.HeadPolicy (None: head on the last rank)
+        self.heads = heads                # runtime.head.HeadJobs (rotating head, non-last ranks)
         self._pub_q: "queue.Queue" = queue.Queue()
         self._pub_thread = None
-        if self.is_last:
+        if self.is_last or heads is not None:
+            self._start_publisher()
+
+    def _start_publisher(self) -> None:
+        if self._pub_thread is None:
             self._pub_thread = threading.Thread(target=self._publisher, daemon=True)
             self._pub_thread.start()
+
+    def publish(self, plan: StepPlan, pinned, ev) -> None:
+        """Queue a step's sampled tokens for the driver (HeadJobs callback / last stage)."""
+        self._pub_q.put((plan.step, plan.mb, pinned, ev))
+
+    def _head_rank(self, plan: StepPlan) -> int:
+        return self.policy.rank_for(plan) if self.policy is not None else self.world - 1
+
+    def _next_msg(self) -> bytes:
+        """The next control message; a CPU rank with queued head jobs keeps running them while it
+        waits (the driver may be waiting for exactly those tokens)."""
+        if self.heads is None:
+            return self.ch.ctrl.recv(self.timeout)
+        if self.heads.gpu:
+            if self.heads.deferred and not self.ch.ctrl.poll():
+                self.heads.flush()   # idle: the driver may be waiting for these tokens
+            return self.ch.ctrl.recv(self.timeout)
+        t0 = time.perf_counter()
+        while not self.ch.ctrl.poll():
+            if self.heads.pending:
+                self.heads.run_oldest()   # idle: the driver may be waiting for these tokens
+                continue
+            if time.perf_counter() - t0 > self.timeout:
+                return self.ch.ctrl.recv(1e-3)   # raises the channel's TimeoutError
+            time.sleep(2e-4)
+        return self.ch.ctrl.recv(self.timeout)
 
     # ring of receive buffers: the receive of micro-batch m+1 only waits until the compute that
     # READ the slot (two steps earlier) is done, not for everything queued on the compute stream
@@ -327,11 +393,13 @@ class StageFollower:
 
     def run(self) -> None:
         while True:
-            msg = msgpack.unpackb(self.ch.ctrl.recv(self.timeout))
+            msg = msgpack.unpackb(self._next_msg())
             kind = msg.get("kind", "run")
             if kind == "stop":
                 break
             if kind == "barrier":
+                if self.heads is not None:
+                    self.heads.drain()
                 if self.ex.device.type == "cuda":
                     torch.cuda.synchronize()
                 self._pub_q.join()
@@ -343,20 +411,32 @@ class StageFollower:
             if not plan.seq_ids:
                 self.ex.execute(plan, None)  # frees only
                 continue
+            hr = self._head_rank(plan)
             buf, free_ev = self._recv_slot(plan.num_tokens)
             x = self.tr.recv(buf, self.rank - 1, free_event=free_ev)
             if self.faults.active:
                 self.faults.on_step()
             tok = self.stats.begin(self.faults.delay_ms)
-            out = self.ex.execute(plan, x)
+            out = self.ex.execute(plan, x, project=(hr == self.rank))
             self.stats.end(tok)
             self._release_slot()
             if self.is_last:
-                pinned, ev = _sample_tokens_to_host(out)
-                self._pub_q.put((plan.step, plan.mb, pinned, ev))
+                if hr == self.rank:
+                    pinned, ev = _sample_tokens_to_host(out)
+                    self.publish(plan, pinned, ev)
+                else:   # rotating head: normed hidden states to the rank whose turn it is
+                    self.tr.send_head(out, hr)
             else:
                 self.tr.send(out, self.rank + 1)
-        if self.is_last:
+                if self.heads is not None:
+                    self.heads.tick()
+                    if hr == self.rank:
+                        self.heads.submit(plan)
+            if self.heads is not None:
+                self.heads.poll()
+        if self.heads is not None:
+            self.heads.drain()
+        if self._pub_thread is not None:
             self._pub_q.join()
             self._pub_q.put(None)
             self._pub_thread.join()
@@ -370,7 +450,8 @@ class StageFollower:
 
 
 def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
-                   rccl_timeout_s: float = 300.0, rank_offset: int = 0) -> Transport:
+                   rccl_timeout_s: float = 300.0, rank_offset: int = 0,
+                   head_pairs: bool = False) -> Transport:
     """RCCL P2P on GPUs (default); ``DLI_TRANSPORT=host`` stages GPU tensors through gloo
     (several ranks sharing one GPU — an explicit opt-in, never chosen silently); gloo on CPU.
 
@@ -392,7 +473,8 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
         prefix = f"dli_rccl_{job}"
         tr, err = None, ""
         try:
-            tr = RcclTransport(store, rank, world, device, prefix=prefix, timeout_s=rccl_timeout_s)
+            tr = RcclTransport(store, rank, world, device, prefix=prefix, timeout_s=rccl_timeout_s,
+                               head_pairs=head_pairs)
         except Exception as e:  # noqa: BLE001 - reported and agreed on below
             err = repr(e)
             store.set(f"{prefix}/err/{rank}", err[:2000])

@@ -29,6 +29,7 @@ import torch.distributed as dist
 class Transport:
     rank: int
     world: int
+    supports_head = False   # can carry the rotating LM head's hidden states (runtime/head.py)
     # traffic counters (SURVEY §5.5 "comm bytes per stage"); published with the stage stats
     bytes_sent: int = 0
     bytes_recv: int = 0
@@ -87,6 +88,18 @@ class TorchDistTransport(Transport):
         self._count(t, False)
         return t
 
+    # rotating LM head (runtime/head.py): last stage -> the rank whose turn it is; tag 1 keeps
+    # these apart from the stage-to-stage stream between the same two ranks
+    supports_head = True
+
+    def send_head(self, t, peer):
+        self._count(t, True)
+        dist.send(t.contiguous(), peer + self.offset, tag=1)
+
+    def irecv_head(self, t, peer):
+        self._count(t, False)
+        return dist.irecv(t, peer + self.offset, tag=1)
+
 
 class HostStagedTransport(Transport):
     """GPU tensors over torch.distributed (gloo) through host memory.
@@ -140,8 +153,10 @@ class LoopbackTransport(Transport):
 class RcclTransport(Transport):
     """RCCL P2P over xGMI with dedicated send/recv streams (see module docstring)."""
 
+    supports_head = True
+
     def __init__(self, store: "dist.Store", rank: int, world: int, device: torch.device,
-                 prefix: str = "dli_rccl", timeout_s: float = 300.0):
+                 prefix: str = "dli_rccl", timeout_s: float = 300.0, head_pairs: bool = False):
         from .. import ops
         C = ops.native()
         self.rank, self.world, self.device = rank, world, device
@@ -169,6 +184,26 @@ class RcclTransport(Transport):
             peer = b if rank == a else a
             self._comms[peer] = C.RcclComm(bytes(uid), 0 if rank == a else 1, 2, dev_idx,
                                            timeout_s)
+        # rotating LM head: one more 2-rank communicator between the last stage and every other
+        # rank (last -> r only), separate from the stage pair so the stage traffic and the head
+        # traffic never share a communicator across streams.  Initialised after every stage pair
+        # (all ranks) in increasing r on the last rank: no cycle in the blocking inits.
+        self._hcomms: Dict[int, object] = {}
+        last = world - 1
+        if head_pairs and world > 1:
+            for r in range(world - 1):
+                if rank not in (r, last):
+                    continue
+                key = f"{prefix}/h{r}"
+                if rank == last:
+                    uid = C.rccl_unique_id()
+                    store.set(key, uid)
+                else:
+                    uid = store.get(key)
+                peer = r if rank == last else last
+                # index 0 = the sender (last stage), 1 = the head rank
+                self._hcomms[peer] = C.RcclComm(bytes(uid), 0 if rank == last else 1, 2, dev_idx,
+                                                timeout_s)
 
     def _comm(self, peer: int):
         c = self._comms.get(peer)
@@ -209,6 +244,21 @@ class RcclTransport(Transport):
         self._count(t, False)
         return t
 
+    def send_head(self, t: torch.Tensor, peer: int) -> None:
+        """Last stage -> head rank ``peer``: the normed hidden states of an offloaded decode step
+        (asynchronous, on the send stream, ordered after the work queued so far)."""
+        cur = torch.cuda.current_stream(self.device)
+        self.send_stream.wait_stream(cur)
+        t.record_stream(self.send_stream)
+        self._hcomms[peer].send(t, 1, self.send_stream.cuda_stream)
+        self._count(t, True)
+
+    def recv_head(self, t: torch.Tensor, peer: int, stream: "torch.cuda.Stream") -> torch.Tensor:
+        """Head rank: receive into ``t`` on ``stream`` (the head side stream)."""
+        self._hcomms[peer].recv(t, 0, stream.cuda_stream)
+        self._count(t, False)
+        return t
+
     def _drain_waits(self, block: bool) -> None:
         while self._waits and (block or self._waits[0][1].query()):
             a, b = self._waits.popleft()
@@ -220,9 +270,12 @@ class RcclTransport(Transport):
         return super().traffic()
 
     def describe(self) -> dict:
-        return {"transport": "RcclTransport", "rccl_version": self._rccl_version,
-                "pair_comms": {str(p): {"rank": c.rank, "size": c.world}
-                               for p, c in sorted(self._comms.items())}}
+        d = {"transport": "RcclTransport", "rccl_version": self._rccl_version,
+             "pair_comms": {str(p): {"rank": c.rank, "size": c.world}
+                            for p, c in sorted(self._comms.items())}}
+        if self._hcomms:
+            d["head_comms"] = sorted(self._hcomms)
+        return d
 
     def _peer_index(self, peer: int) -> int:
         # inside a 2-rank pair communicator the lower global rank of the pair is index 0
@@ -230,11 +283,13 @@ class RcclTransport(Transport):
         return 0 if peer < self.rank else 1
 
     def close(self) -> None:
-        for c in self._comms.values():
+        for c in list(self._comms.values()) + list(self._hcomms.values()):
             c.destroy()
         self._comms.clear()
+        self._hcomms.clear()
 
     def abort(self) -> None:
-        for c in self._comms.values():
+        for c in list(self._comms.values()) + list(self._hcomms.values()):
             c.abort()
         self._comms.clear()
+        self._hcomms.clear()

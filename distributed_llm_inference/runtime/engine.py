@@ -26,6 +26,7 @@ from ..parallel.pipeline import (DistributedDriver, LocalPipeline, StageFollower
                                  make_transport)
 from ..utils.model import build_stage
 from .executor import StageExecutor
+from .head import HeadJobs, HeadPolicy, HeadRunner
 from .scheduler import Scheduler
 from .sequence import SamplingParams, Sequence as Seq
 
@@ -183,8 +184,8 @@ class ReplicaLayout:
     def drivers(self) -> List[int]:
         return [r * self.pp for r in range(self.dp)]
 
-    def describe(self, spec: ModelSpec) -> dict:
-        ranges = plan_stages(spec, self.pp)
+    def describe(self, spec: ModelSpec, head_rotation: bool = True) -> dict:
+        ranges = plan_stages(spec, self.pp, head_rotation=head_rotation)
         return {"dp": self.dp, "pp": self.pp,
                 "replicas": [{"replica": r, "driver_rank": r * self.pp,
                               "stages": [{"rank": r * self.pp + i, "gpu": r * self.pp + i,
@@ -248,7 +249,8 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         eng = LLMEngine(cfg.model, pp=1, device=device, cfg=cfg)
         dist.barrier()
         return "driver", tag(eng.pipeline)
-    ranges = plan_stages(spec, pp)
+    rotate = head_rotation_wanted(cfg, pp, device)
+    ranges = plan_stages(spec, pp, head_rotation=rotate)
     if os.environ.get("DLI_STAGE_RANGES"):  # placement chosen by the server (rebalance)
         import json
         ranges = [tuple(r) for r in json.loads(os.environ["DLI_STAGE_RANGES"])]
@@ -256,11 +258,41 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
             raise ValueError("DLI_STAGE_RANGES must have one range per pipeline stage")
     start, end = ranges[srank]
     ex = build_executor(spec, start, end, device, cfg, group=group, kv_share=kv_share)
-    channels = _Channels(job, srank, pp)
-    transport = make_transport(srank, pp, device, job=job, rank_offset=rep * pp)
+    transport = make_transport(srank, pp, device, job=job, rank_offset=rep * pp, head_pairs=rotate)
+    # the fallback transport (agreed on by every rank) cannot carry the head: then nobody rotates
+    rotate = rotate and transport.supports_head
+    channels = _Channels(job, srank, pp, head_rotation=rotate)
+    policy = HeadPolicy(pp, rotate, ex.max_num_seqs)
     dist.barrier()
     channels.unlink()  # every rank has attached: nothing may be left in /dev/shm after this
+    heads_runner = None
+    if rotate and srank != pp - 1:
+        from ..utils.model import build_head
+        head = build_head(cfg.checkpoint or spec, device=device,
+                          random_init=cfg.random_init and cfg.checkpoint is None, seed=cfg.seed,
+                          checkpoint=cfg.checkpoint)
+        heads_runner = HeadRunner(head, device, ex.max_num_seqs, cfg.serve.use_graphs,
+                                  ex.graph_sizes)
     if srank == 0:
         sched = make_scheduler(spec, ex, cfg, pp)
-        return "driver", tag(DistributedDriver(ex, sched, transport, channels, pp, group))
-    return "follower", tag(StageFollower(ex, transport, channels, srank, pp, group))
+        drv = DistributedDriver(ex, sched, transport, channels, pp, group, policy=policy)
+        if heads_runner is not None:
+            drv.heads = HeadJobs(heads_runner, transport, pp - 1, drv.publish_local, delay=pp)
+        return "driver", tag(drv)
+    fol = StageFollower(ex, transport, channels, srank, pp, group, policy=policy)
+    if heads_runner is not None:
+        fol.heads = HeadJobs(heads_runner, transport, pp - 1, fol.publish, delay=pp - srank)
+        fol._start_publisher()
+    return "follower", tag(fol)
+
+
+def head_rotation_wanted(cfg: EngineConfig, pp: int, device: torch.device) -> bool:
+    """Rotate the decode LM head over the pipeline ranks (runtime/head.py)?  On by default for
+    PP > 1 over RCCL (GPUs) or gloo (CPU); the host-staged rehearsal transport keeps it on the
+    last stage.  ``DLI_HEAD_ROTATION=0/1`` overrides the config."""
+    env = os.environ.get("DLI_HEAD_ROTATION")
+    want = cfg.serve.head_rotation if env is None else env == "1"
+    if not want or pp < 2:
+        return False
+    kind = os.environ.get("DLI_TRANSPORT", "rccl" if device.type == "cuda" else "gloo")
+    return kind in ("rccl", "rccl-or-host", "gloo")

@@ -53,6 +53,7 @@ class StepPlan:
     top_k: List[int] = field(default_factory=list)
     top_p: List[float] = field(default_factory=list)
     seeds: List[int] = field(default_factory=list)
+    sample_pos: List[int] = field(default_factory=list)     # sampled token's position (RNG key)
     kind: str = "run"                                       # run | barrier | stop
     tokens: Optional[List[int]] = None                      # stage-0 input (not broadcast)
 
@@ -73,12 +74,21 @@ class StepPlan:
         d = dict(step=self.step, mb=self.mb, seq_ids=self.seq_ids, q_lens=self.q_lens,
                  free_ids=self.free_ids, sample_rows=self.sample_rows,
                  temperature=self.temperature, top_k=self.top_k, top_p=self.top_p,
-                 seeds=self.seeds, kind=self.kind)
+                 seeds=self.seeds, sample_pos=self.sample_pos, kind=self.kind)
         return d
 
     @classmethod
     def from_wire(cls, d: dict) -> "StepPlan":
         return cls(**d)
+
+
+def _fill_pos(dst: torch.Tensor, plan: StepPlan, n: int) -> None:
+    """Per-sample-row RNG counters (the sampled token's position); plans without them (built by
+    hand) fall back to the step number, which keeps them distinct across steps."""
+    if len(plan.sample_pos) == n:
+        dst[:n] = torch.as_tensor(plan.sample_pos, dtype=torch.int64)
+    else:
+        dst[:n] = plan.step
 
 
 class _Staging:
@@ -88,6 +98,7 @@ class _Staging:
         self.max_tokens, self.max_seqs, self.max_blocks = max_tokens, max_seqs, max_blocks
         specs = [("slot_mapping", torch.int64, (max_tokens,)),
                  ("seeds", torch.int64, (max_seqs,)),
+                 ("sample_pos", torch.int64, (max_seqs,)),
                  ("logits_rows", torch.int64, (max_seqs,)),
                  ("step", torch.int64, (1,)),
                  ("positions", torch.int32, (max_tokens,)),
@@ -244,11 +255,13 @@ class StageExecutor:
                 h["top_k"][:B] = torch.as_tensor(plan.top_k, dtype=torch.int32)
                 h["top_p"][:B] = torch.as_tensor(plan.top_p, dtype=torch.float32)
                 h["seeds"][:B] = torch.as_tensor(plan.seeds, dtype=torch.int64)
+                _fill_pos(h["sample_pos"], plan, B)
                 if rows > B:
                     h["temperature"][B:rows] = 0.0
                     h["top_k"][B:rows] = 0
                     h["top_p"][B:rows] = 1.0
                     h["seeds"][B:rows] = 0
+                    h["sample_pos"][B:rows] = 0
                 n = rows
             else:
                 qs = h["q_start"]
@@ -258,12 +271,14 @@ class StageExecutor:
                 h["top_k"][:ns] = torch.as_tensor(plan.top_k, dtype=torch.int32)
                 h["top_p"][:ns] = torch.as_tensor(plan.top_p, dtype=torch.float32)
                 h["seeds"][:ns] = torch.as_tensor(plan.seeds, dtype=torch.int64)
+                _fill_pos(h["sample_pos"], plan, ns)
                 st.upload("logits_rows", ns)
                 n = ns
             st.upload("temperature", n)
             st.upload("top_k", n)
             st.upload("top_p", n)
             st.upload("seeds", n)
+            st.upload("sample_pos", n)
             h["step"][0] = plan.step
             st.upload("step", 1)
         st.release()
@@ -303,15 +318,16 @@ class StageExecutor:
                                  self.max_seq_len)
 
     # ------------------------------------------------------------------ forward
-    def _forward(self, meta: AttnMetadata, inputs: torch.Tensor, n_sample: int) -> torch.Tensor:
-        out = self.stage(inputs, meta, self.pool)
-        if not self.stage.has_head:
+    def _forward(self, meta: AttnMetadata, inputs: torch.Tensor, n_sample: int,
+                 project: bool = True) -> torch.Tensor:
+        out = self.stage(inputs, meta, self.pool, project=project)
+        if not self.stage.has_head or not project:
             return out
         d = self.staging.d
         tokens = self._sample_out[:n_sample]
         ops.sample(out, temperature=d["temperature"][:n_sample], top_k=d["top_k"][:n_sample],
                    top_p=d["top_p"][:n_sample], seeds=d["seeds"][:n_sample], step=d["step"],
-                   out=tokens)
+                   out=tokens, counters=d["sample_pos"][:n_sample])
         return tokens
 
     def input_buffer(self, plan: StepPlan) -> Optional[torch.Tensor]:
@@ -331,18 +347,20 @@ class StageExecutor:
 
     @torch.inference_mode()
     def execute(self, plan: StepPlan, inputs: Optional[torch.Tensor] = None,
-                token_src: Optional[torch.Tensor] = None) -> torch.Tensor:
+                token_src: Optional[torch.Tensor] = None, project: bool = True) -> torch.Tensor:
         """Run one step.  ``inputs``: hidden states [T, H] for non-first stages (ignored on stage 0,
         which embeds ``plan.tokens``).  Returns hidden [T, H] or sampled tokens [n_sample] int32
-        (device tensors; the caller decides when to synchronise)."""
+        (device tensors; the caller decides when to synchronise).  ``project=False`` (last stage,
+        decode steps whose vocabulary projection + sampling run on another rank): returns the
+        final-normed hidden states [B, H] instead of tokens."""
         if not (_TRACE or _DEBUG):
-            return self._execute(plan, inputs, token_src)
+            return self._execute(plan, inputs, token_src, project)
         tag = f"stage[{self.stage.start},{self.stage.end}) step={plan.step} mb={plan.mb} " \
               f"{'decode' if plan.is_decode else 'prefill'} B={len(plan.seq_ids)} T={plan.num_tokens}"
         if _TRACE and self.device.type == "cuda":
             torch.cuda.nvtx.range_push(tag)  # roctx range on ROCm (rocprofv3 --marker-trace)
         try:
-            out = self._execute(plan, inputs, token_src)
+            out = self._execute(plan, inputs, token_src, project)
         finally:
             if _TRACE and self.device.type == "cuda":
                 torch.cuda.nvtx.range_pop()
@@ -356,7 +374,7 @@ class StageExecutor:
         return out
 
     def _execute(self, plan: StepPlan, inputs: Optional[torch.Tensor],
-                 token_src: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 token_src: Optional[torch.Tensor] = None, project: bool = True) -> torch.Tensor:
         self.apply_frees(plan.free_ids)
         if not plan.seq_ids:
             return torch.empty(0, device=self.device)
@@ -374,28 +392,35 @@ class StageExecutor:
             self.staging.d["tokens"][:B].copy_(token_src[:B], non_blocking=True)
         n_sample = len(plan.sample_rows)
         all_sample = decode and n_sample == B
+        project = project or not self.stage.has_head
+        if not project and not all_sample:
+            raise ValueError("project=False needs a decode step in which every row samples")
         if grows is not None and (not self.stage.has_head or all_sample):
             if not self.stage.has_embed:
                 src = inputs[:B]
                 if src.data_ptr() != self._hidden_in.data_ptr():
                     self._hidden_in[:B].copy_(src)
-            g = self._graphs.get(grows)
+            key = grows if project else (grows, "norm")
+            g = self._graphs.get(key)
             if g is None:
-                g = self._capture(grows)
+                g = self._capture(grows, project)
             g.graph.replay()
-            return g.out[:n_sample] if self.stage.has_head else g.out[:B].clone()
+            if self.stage.has_head and project:
+                return g.out[:n_sample]
+            return g.out[:B].clone()
         splits = self._splits(rows) if decode else 1
         meta = self._metadata(plan, rows, splits, decode)
         if self.stage.has_embed:
             x = self.staging.d["tokens"][: meta.num_tokens]
         else:
             x = inputs
-        out = self._forward(meta, x, n_sample if self.stage.has_head else 0)
-        return out
+        out = self._forward(meta, x, n_sample if self.stage.has_head else 0, project)
+        return out if project else out[:B]
 
     # ------------------------------------------------------------------ graphs
-    def _capture(self, rows: int) -> "_GraphEntry":
-        """Capture the decode step for ``rows`` sequences (buffers already staged by the caller)."""
+    def _capture(self, rows: int, project: bool = True) -> "_GraphEntry":
+        """Capture the decode step for ``rows`` sequences (buffers already staged by the caller);
+        ``project=False``: the last stage's variant that ends at the final norm."""
         splits = self._splits(rows)
         plan_like = StepPlan(0, 0, list(range(rows)), [1] * rows,
                              sample_rows=list(range(rows)))
@@ -407,17 +432,17 @@ class StageExecutor:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
-                self._forward(meta, x, n_sample)
+                self._forward(meta, x, n_sample, project)
         torch.cuda.current_stream().wait_stream(s)
         graph = torch.cuda.CUDAGraph()
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
         with torch.cuda.graph(graph, pool=self._graph_pool):
-            out = self._forward(meta, x, n_sample)
+            out = self._forward(meta, x, n_sample, project)
         entry = _GraphEntry(graph, out)
-        self._graphs[rows] = entry
-        log.info("captured decode graph rows=%d splits=%d stage=[%d,%d)", rows, splits,
-                 self.stage.start, self.stage.end)
+        self._graphs[rows if project else (rows, "norm")] = entry
+        log.info("captured decode graph rows=%d splits=%d stage=[%d,%d)%s", rows, splits,
+                 self.stage.start, self.stage.end, "" if project else " (ends at the final norm)")
         # (the captured run did not execute; the caller replays the graph for the real step)
         return entry
 
@@ -440,9 +465,10 @@ class StageExecutor:
             h["top_k"][:r] = 0
             h["top_p"][:r] = 1
             h["seeds"][:r] = 0
+            h["sample_pos"][:r] = 0
             for k, n in (("seq_lens", r), ("slot_mapping", r), ("positions", r), ("block_tables", r),
                          ("q_start", r + 1), ("tokens", r), ("temperature", r), ("top_k", r),
-                         ("top_p", r), ("seeds", r)):
+                         ("top_p", r), ("seeds", r), ("sample_pos", r)):
                 self.staging.upload(k, n)
             self.staging.release()
             if self._hidden_in is not None:

@@ -126,7 +126,7 @@ class Scheduler:
             return self._decode_plan(mb)
         budget = self.max_tokens - decode_n
         seq_ids, q_lens, tokens, sample_rows = [], [], [], []
-        temps, topk, topp, seeds = [], [], [], []
+        temps, topk, topp, seeds, spos = [], [], [], [], []
         for s in m:
             pend = s.pending_tokens()
             if s.num_computed >= len(s.prompt):
@@ -148,13 +148,14 @@ class Scheduler:
                 topk.append(int(s.params.top_k))
                 topp.append(float(s.params.top_p))
                 seeds.append(int(s.seed))
+                spos.append(s.num_computed + take)   # the sampled token's position
         free_ids = self.pending_free[mb]
         self.pending_free[mb] = []
         if not seq_ids and not free_ids:
             return None
         plan = StepPlan(step=self.step, mb=mb, seq_ids=seq_ids, q_lens=q_lens, free_ids=free_ids,
                         sample_rows=sample_rows, temperature=temps, top_k=topk, top_p=topp,
-                        seeds=seeds, tokens=tokens)
+                        seeds=seeds, sample_pos=spos, tokens=tokens)
         self.step += 1
         # the tokens are (about to be) in the cache on every stage
         byid = {s.seq_id: s for s in m}
@@ -194,7 +195,8 @@ class Scheduler:
             s.num_computed += 1
         plan = StepPlan(step=self.step, mb=mb, seq_ids=c["seq_ids"], q_lens=c["q_lens"],
                         free_ids=[], sample_rows=c["sample_rows"], temperature=c["temperature"],
-                        top_k=c["top_k"], top_p=c["top_p"], seeds=c["seeds"], tokens=None)
+                        top_k=c["top_k"], top_p=c["top_p"], seeds=c["seeds"],
+                        sample_pos=[s.num_computed for s in rows], tokens=None)
         self.step += 1
         self.lookahead[mb] = plan
         return plan
@@ -211,7 +213,8 @@ class Scheduler:
         plan = StepPlan(step=self.step, mb=mb, seq_ids=c["seq_ids"], q_lens=c["q_lens"],
                         free_ids=free_ids, sample_rows=c["sample_rows"],
                         temperature=c["temperature"], top_k=c["top_k"], top_p=c["top_p"],
-                        seeds=c["seeds"], tokens=tokens)
+                        seeds=c["seeds"], sample_pos=[s.num_computed for s in rows],
+                        tokens=tokens)
         self.step += 1
         self.inflight[mb] = plan
         return plan

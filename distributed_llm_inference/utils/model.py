@@ -196,6 +196,38 @@ def load_stage_extras(stage: CausalLMStage, sd: Dict[str, torch.Tensor]) -> None
                     stage.head.proj.weight.copy_(w)
 
 
+def build_head(model, device=None, dtype=torch.bfloat16, random_init: bool = True, seed: int = 0,
+               checkpoint: Optional[str] = None):
+    """Final norm + LM head alone (plus the embedding it is tied to, if any) for a rank that runs
+    the rotating head's vocabulary projection (runtime/head.py) without owning the last layers.
+    Random init uses the same per-parameter seeds as the last stage's, so every rank holds the
+    identical head; checkpoints load the same HF keys ``load_stage_weights`` does."""
+    from types import SimpleNamespace
+    from ..models.embed_head import Embedding, LMHead
+    spec = _load_config(checkpoint or model)
+    embed = Embedding(spec, device, dtype) if spec.tie_word_embeddings else None
+    head = LMHead(spec, device, dtype, tied=embed)
+    if random_init and checkpoint is None:
+        if embed is not None:
+            embed.init_random(seed)
+        head.init_random(seed)
+        return head
+    files = _weight_files(checkpoint or model, None, False)
+    if spec.arch == "gpt2":
+        want = ["transformer.ln_f.weight", "transformer.ln_f.bias", "transformer.wte.weight"]
+    else:
+        want = ["model.norm.weight", "lm_head.weight", "model.embed_tokens.weight"]
+    sd = {}
+    from safetensors import safe_open
+    for f in sorted({files[k] for k in want if k in files}):
+        with safe_open(f, framework="pt", device="cpu") as fh:
+            for k in want:
+                if k in fh.keys():
+                    sd[k] = fh.get_tensor(k)
+    load_stage_extras(SimpleNamespace(spec=spec, embed=embed, head=head), sd)
+    return head
+
+
 def stage_from_hf_model(hf_model, start: int, end: int, device=None,
                         dtype=torch.bfloat16) -> CausalLMStage:
     """Build a stage from an in-memory HF ``*ForCausalLM`` (tests / conversions)."""

@@ -59,9 +59,23 @@ def test_bench_multirank_json_contract(n):
         assert r["recv_wait_ms_per_mb_step"] >= 0
     H = 128  # tiny-llama-8l hidden size (bf16 activations)
     mb_bytes = bpm * H * 2
+    T = steps * (n + 1)   # decode micro-batch steps in the window
+    head = []             # rotating LM head (runtime/head.py): normed hidden states last -> r
     for i, r in enumerate(pr):
-        assert r["bytes_sent"] == (steps * (n + 1) * mb_bytes if i < n - 1 else 0), r
-        assert r["bytes_recv"] == (steps * (n + 1) * mb_bytes if i > 0 else 0), r
+        stage_sent = T * mb_bytes if i < n - 1 else 0
+        stage_recv = T * mb_bytes if i > 0 else 0
+        if i < n - 1:
+            assert r["bytes_sent"] == stage_sent, r
+            extra = r["bytes_recv"] - stage_recv
+            assert extra >= 0 and extra % mb_bytes == 0, r
+            head.append(extra // mb_bytes)
+        else:
+            assert r["bytes_recv"] == stage_recv, r
+            assert r["bytes_sent"] % mb_bytes == 0, r
+            assert r["bytes_sent"] // mb_bytes == sum(head), (r, head)
+            head.append(T - sum(head))   # steps whose head stayed on the last stage
+    # every rank projected + sampled its 1/n share of the steps (step % n)
+    assert all(T // n <= h <= -(-T // n) for h in head), head
 
 
 @pytest.mark.parametrize("n,dp", [(4, 2), (2, 2)])

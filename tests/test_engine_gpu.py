@@ -294,3 +294,42 @@ def test_reference_llama_block_api_on_gpu(gpu):
     assert cache.get_seq_length(0, "g1") == 40 and cache.get_seq_length(0, "g2") == 5
     cache.close_session("g1")
     assert cache.get_seq_length(0, "g1") == 0
+
+
+@pytest.mark.parametrize("temperature", [0.0, 0.8])
+def test_rotating_head_split_matches_local_head(gpu, temperature):
+    """The rotating LM head's two halves on the GPU (runtime/head.py): the last stage's decode
+    graph that ends at the final norm, then HeadRunner's projection + sampling graph replayed on a
+    side stream, produce exactly the tokens of the fused last-stage head (greedy and seeded
+    top-k sampling)."""
+    from distributed_llm_inference.parallel.pipeline import _sample_tokens_to_host
+    from distributed_llm_inference.runtime.head import HeadRunner
+    p = SamplingParams(max_tokens=8, temperature=temperature, top_k=30, seed=11, ignore_eos=True)
+    ref = [s.output for s in _engine(pp=2, mbs=3).generate(PROMPTS, p)]
+    eng = _engine(pp=2, mbs=3)
+    pipe = eng.pipeline
+    last = pipe.executors[-1]
+    runner = HeadRunner(last.stage.head, last.device, last.max_num_seqs, True, last.graph_sizes)
+    side = torch.cuda.Stream()
+    orig, split = pipe._issue, []
+
+    def issue(plan):
+        if not (plan.seq_ids and plan.is_decode and len(plan.sample_rows) == len(plan.seq_ids)):
+            return orig(plan)
+        x = None
+        for ex in pipe.executors[:-1]:
+            x = ex.execute(plan, x)
+        h = last.execute(plan, x, project=False)
+        assert h.shape == (len(plan.seq_ids), SPEC.hidden_size)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            tok = runner.run(plan, h).clone()
+        torch.cuda.current_stream().wait_stream(side)
+        pipe._last_tokens = tok
+        pipe._results[plan.step] = _sample_tokens_to_host(tok)
+        split.append(plan.step)
+
+    pipe._issue = issue
+    got = [s.output for s in eng.generate(PROMPTS, p)]
+    assert len(split) >= 6 and runner._graphs   # decode steps took the split path, graphed
+    assert got == ref

@@ -233,16 +233,16 @@ def _free_port():
     return port
 
 
-def _mp_worker(rank, world, port, q):
+def _mp_worker(rank, world, port, q, params=None, rotation="1"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_HEAD_ROTATION=rotation)
     import torch.distributed as dist
     from distributed_llm_inference.runtime.engine import init_pipeline_rank
     cfg = _cfg(pp=world)
     cfg.model = SPEC  # type: ignore[assignment]
     role, obj = init_pipeline_rank(cfg)
     if role == "driver":
-        out = obj.generate(PROMPTS, SamplingParams(max_tokens=6, ignore_eos=True))
+        out = obj.generate(PROMPTS, params or SamplingParams(max_tokens=6, ignore_eos=True))
         obj.stop()
         obj.close()
         q.put([s.output for s in out])
@@ -250,6 +250,28 @@ def _mp_worker(rank, world, port, q):
         obj.run()
         obj.close()
     dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,rotation", [(3, "0"), (4, "1")])
+def test_multiprocess_rotating_head_sampling(world, rotation):
+    """Seeded top-k / temperature sampling through the multi-process pipeline with the LM head
+    rotating over the ranks (and, for contrast, pinned to the last rank): identical tokens to the
+    single-stage engine (the sampler's RNG is keyed by seed and step, not by rank)."""
+    p = SamplingParams(max_tokens=7, temperature=0.9, top_k=40, top_p=0.95, seed=3,
+                       ignore_eos=True)
+    ref = [s.output for s in LLMEngine(SPEC, cfg=_cfg()).generate(PROMPTS, p)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_mp_worker, args=(r, world, port, q, p, rotation))
+          for r in range(world)]
+    for pr in ps:
+        pr.start()
+    got = q.get(timeout=240)
+    for pr in ps:
+        pr.join(60)
+        assert pr.exitcode == 0
+    assert got == ref
 
 
 @pytest.mark.parametrize("world", [2, 3, 4])
