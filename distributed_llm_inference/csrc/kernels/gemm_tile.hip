@@ -253,6 +253,9 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
           bf[j][kk] = *reinterpret_cast<const bf16x8*>(buf + (2 + h) * kHalf + b_lane + j * 16 * 128 + sch[kk]);
     };
     auto quadrant = [&](int mq, int nq, const bf16x8 (&bf)[2][2]) {
+      // the computing wave outranks its SIMD partner for the segment: 13-15 % faster than a
+      // static priority for the lagging group or none; triple-buffering the weight half-tiles
+      // (160 KB LDS, twice the DMA lead) buys nothing (profiles/gemm_variants_ab.txt)
       __builtin_amdgcn_s_setprio(1);
       if (FP8) {
         // one K=128 MFMA per fragment pair: the two 16-B chunks (g, g+4) of the 128-B k-tile row
