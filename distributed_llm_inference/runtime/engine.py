@@ -257,6 +257,13 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         if len(ranges) != pp:
             raise ValueError("DLI_STAGE_RANGES must have one range per pipeline stage")
     start, end = ranges[srank]
+    head = None
+    if rotate and srank != pp - 1:
+        # built before the KV pool is sized from the free HBM that is left
+        from ..utils.model import build_head
+        head = build_head(cfg.checkpoint or spec, device=device,
+                          random_init=cfg.random_init and cfg.checkpoint is None, seed=cfg.seed,
+                          checkpoint=cfg.checkpoint)
     ex = build_executor(spec, start, end, device, cfg, group=group, kv_share=kv_share)
     transport = make_transport(srank, pp, device, job=job, rank_offset=rep * pp, head_pairs=rotate)
     # the fallback transport (agreed on by every rank) cannot carry the head: then nobody rotates
@@ -266,11 +273,7 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     dist.barrier()
     channels.unlink()  # every rank has attached: nothing may be left in /dev/shm after this
     heads_runner = None
-    if rotate and srank != pp - 1:
-        from ..utils.model import build_head
-        head = build_head(cfg.checkpoint or spec, device=device,
-                          random_init=cfg.random_init and cfg.checkpoint is None, seed=cfg.seed,
-                          checkpoint=cfg.checkpoint)
+    if rotate and head is not None:
         heads_runner = HeadRunner(head, device, ex.max_num_seqs, cfg.serve.use_graphs,
                                   ex.graph_sizes)
     if srank == 0:
