@@ -126,6 +126,13 @@ struct SkArgs {
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
+#ifdef DLI_GEMM_STAMPS
+// Diagnostic builds only (scripts/experiments/gemm_stamps.hip, gemm_w4_bench.hip): per-workgroup
+// clock stamps (begin / end shader cycles and 100 MHz wall ticks, end of the main loop).  Never
+// compiled into the extension.
+__device__ unsigned long long* g_stamp_blk;   // [grid][8]
+#endif
+
 // FP8 / INT8: A and B are 1-byte elements (K counted in elements = bytes) with fp32 a_scale[M]
 // (per row) and b_scale[N] (per output channel).  Staging is byte-identical to bf16: a k-tile is
 // 128 bytes of every row (64 bf16, 128 fp8 / int8).
@@ -143,6 +150,13 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
   __shared__ __attribute__((aligned(1024))) char smem[kLds];
 
   const int tid0 = threadIdx.x;
+#ifdef DLI_GEMM_STAMPS
+  if (tid0 == 0) {
+    unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
+    st[0] = __builtin_amdgcn_s_memrealtime();
+    st[1] = __builtin_amdgcn_s_memtime();
+  }
+#endif
 
   // ---- XCD-aware, bijective block remap (consecutive logical ids share an XCD / its L2) ----
   auto remap = [](int b, int n) {
@@ -339,6 +353,13 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
       barrier();
     }
     if (wr == 0) barrier();
+#ifdef DLI_GEMM_STAMPS
+    if (tid0 == 0) {
+      unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
+      st[6] = __builtin_amdgcn_s_memrealtime();
+      st[7] = __builtin_amdgcn_s_memtime();
+    }
+#endif
 
     // ---- stream-K hand-off ----
     if (kSk && publish) {
@@ -472,6 +493,13 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
       }
     }
   }
+#ifdef DLI_GEMM_STAMPS
+  if (tid0 == 0) {
+    unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
+    st[2] = __builtin_amdgcn_s_memrealtime();
+    st[3] = __builtin_amdgcn_s_memtime();
+  }
+#endif
 }
 
 __global__ void __launch_bounds__(256) tile_splitk_reduce_kernel(bf16* __restrict__ C,
