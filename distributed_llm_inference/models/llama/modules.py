@@ -117,25 +117,44 @@ class LlamaMLP(nn.Module):
         self.fused_swiglu = False
 
     def set_fused_swiglu(self, on: bool) -> None:
-        """Permute gate_up_proj's rows in place to / from the fused-SwiGLU tile order."""
+        """Permute gate_up_proj's rows in place to / from the fused-SwiGLU tile order (bf16
+        weights, or fp8 weights + their per-channel scales when the fp8 tile path is on)."""
         w = self.gate_up_proj
         if on == self.fused_swiglu:
             return
-        if w.is_fp8 or w.is_int8 or w.bias is not None or w.out_features % 256:
+        if w.is_int8 or w.bias is not None or w.out_features % 256:
             return
+        if w.is_fp8 and on and not ops.fp8_tile_all():
+            return
+        perm = ops.swiglu_interleave if on else ops.swiglu_deinterleave
         with torch.no_grad():
-            perm = ops.swiglu_interleave if on else ops.swiglu_deinterleave
-            w.weight.data.copy_(perm(w.weight.data))
+            if w.is_fp8:
+                # per-output-channel quantisation commutes with the row permutation
+                w.weight_fp8.copy_(perm(w.weight_fp8.view(torch.uint8)).view(w.weight_fp8.dtype))
+                w.weight_scale.copy_(perm(w.weight_scale.reshape(-1, 1)).reshape(w.weight_scale.shape))
+            else:
+                w.weight.data.copy_(perm(w.weight.data))
         self.fused_swiglu = on
 
     def forward(self, normed: Optional[torch.Tensor], x_q=None, defer_reduce: bool = False):
-        if self.fused_swiglu:
-            if self.gate_up_proj.tile_splits(normed):
-                h = ops.gemm_tile(normed, self.gate_up_proj.weight, swiglu=True)
+        gp = self.gate_up_proj
+        if self.fused_swiglu and gp.is_fp8:
+            xq, xs = x_q if x_q is not None else ops.quant_rowwise(normed)
+            if xq.is_cuda and ops.tile_gemm_splits_fp8(xq.shape[0], gp.out_features,
+                                                        gp.in_features):
+                # fp8 gate|up on the block-scaled tile kernel, SwiGLU in its epilogue (bf16 out;
+                # down_proj quantises it: one [M, I] pass instead of silu_mul_quant's [M, 2I])
+                h = ops.gemm_tile_fp8(xq, xs, gp.weight_fp8, gp.weight_scale, swiglu=True)
             else:
-                h = ops.swiglu_interleaved(self.gate_up_proj(normed))
+                h = ops.swiglu_interleaved(gp(None, (xq, xs)))
             return self.down_proj(h, defer_reduce=defer_reduce)
-        gu = self.gate_up_proj(normed, x_q)
+        if self.fused_swiglu:
+            if gp.tile_splits(normed):
+                h = ops.gemm_tile(normed, gp.weight, swiglu=True)
+            else:
+                h = ops.swiglu_interleaved(gp(normed))
+            return self.down_proj(h, defer_reduce=defer_reduce)
+        gu = gp(normed, x_q)
         if self.down_proj.is_fp8:  # SwiGLU fused with the fp8 quantisation of down_proj's input
             return self.down_proj(None, ops.silu_mul_quant(gu), defer_reduce=defer_reduce)
         return self.down_proj(ops.silu_mul(gu), defer_reduce=defer_reduce)
@@ -184,7 +203,8 @@ class LlamaDecoderLayer(nn.Module):
             xq = ops.quant_rowwise(hidden, norm_w=ln1.weight, eps=ln1.eps)
         else:
             xq = ops.quant_rowwise(hidden, residual, ln1.weight, ln1.eps)
-        attn = self.self_attn(None, meta, k_cache, v_cache, cos_sin, x_q=xq)
+        # the O projection's split-K partials (tile path) are summed inside the quantiser
+        attn = self.self_attn(None, meta, k_cache, v_cache, cos_sin, x_q=xq, defer_reduce=True)
         res_out = torch.empty_like(residual) if first else residual
         xq = ops.quant_rowwise(attn, residual, ln2.weight, ln2.eps, residual_out=res_out)
         # defer_out: the down projection's split-K partials go into the next layer's quantiser

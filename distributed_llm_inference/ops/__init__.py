@@ -592,11 +592,20 @@ def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torc
     return out
 
 
+def fp8_tile_all() -> bool:
+    """``DLI_FP8_TILE=all`` (default): every fp8 decode projection runs on the hand-written
+    block-scaled MFMA tile kernel — QKV / O / down with split-K partials reduced by their consumer
+    kernels and gate|up with the fused SwiGLU epilogue.  ``long``: only long-K products (the down
+    projection) do; the K = 8192 ones go to hipBLASLt's row-scaled fp8 GEMM, which is faster on
+    those shapes in isolation (profiles/gemm_fp8_probe.json)."""
+    return os.environ.get("DLI_FP8_TILE", "all") != "long"
+
+
 def tile_gemm_splits_fp8(M: int, N: int, K: int) -> int:
-    """``tile_gemm_splits`` for the fp8 kernel.  Measured on the 70B shapes at M = 512 it beats
-    hipBLASLt's row-wise scaled fp8 GEMM only on the long-K down projection (131 vs 148 us,
-    K = 28672); at K = 8192 the split-K pass costs more than it saves (O 52 vs 41 us)."""
-    if K < 16384:
+    """``tile_gemm_splits`` for the fp8 kernel under the :func:`fp8_tile_all` policy (``long``:
+    K >= 16384 only — on the 70B shapes at M = 512 the long-K down projection is 131 vs 148 us
+    against hipBLASLt; at K = 8192 hipBLASLt wins in isolation, O 41 vs 52 us)."""
+    if K < 16384 and not fp8_tile_all():
         return 0
     return tile_gemm_splits(M, N, K, elem_bytes=1)
 

@@ -65,7 +65,7 @@ def build_executor(spec: ModelSpec, start: int, end: int, device: torch.device, 
     cc, sc = cfg.cache, cfg.serve
     nlayers = end - start
     if device.type == "cuda" and hasattr(stage.block, "set_fused_swiglu"):
-        # bf16 gate|up weights in the tile GEMM's SwiGLU order (fp8 stages keep theirs)
+        # gate|up weights in the tile GEMM's SwiGLU order (bf16, or fp8 on the fp8 tile path)
         stage.block.set_fused_swiglu(True)
     if device.type == "cuda" and sc.use_graphs:
         from .gemm_tuning import tune_decode_gemms

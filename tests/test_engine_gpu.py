@@ -134,6 +134,60 @@ def test_fp8_stage_gpu_matches_cpu(gpu):
     assert rel < 0.05, rel
 
 
+def test_fp8_tile_path_fused_swiglu_matches_cpu(gpu, monkeypatch):
+    """fp8 weights on the hand-written tile GEMMs (DLI_FP8_TILE=all): QKV partials into the RoPE
+    kernel, O partials into the fused norm + quantiser, gate|up with the SwiGLU epilogue on
+    pairwise-interleaved fp8 rows + scales, down partials into the next layer's quantiser — against
+    the CPU dequantised reference with identical fp8 weights (prefill of 384 tokens) and the
+    hipBLASLt fp8 path (+ a 128-sequence decode step; both take the tile path)."""
+    monkeypatch.setenv("DLI_FP8_TILE", "all")
+    spec = SPEC.replace(hidden_size=512, intermediate_size=1024, num_heads=8, num_kv_heads=2,
+                        head_dim=64)
+    prompts = [[(7 * i + j) % 997 + 1 for j in range(3)] for i in range(128)]
+    cpu = CausalLMStage(spec, 0, 3).init_random(4)
+    g = CausalLMStage(spec, 0, 3, device=gpu).init_random(4)
+    g.load_state_dict({k: v.to(gpu) for k, v in cpu.state_dict().items()})
+    cpu.quantize_fp8()
+    g.quantize_fp8()
+    wq0 = g.block.layers[0].mlp.gate_up_proj.weight_fp8.clone()
+    g.block.set_fused_swiglu(True)
+    assert all(l.mlp.fused_swiglu for l in g.block.layers)
+    assert not torch.equal(g.block.layers[0].mlp.gate_up_proj.weight_fp8.view(torch.uint8),
+                           wq0.view(torch.uint8))
+    a = _stage_logits(cpu, prompts, 0)[0]
+
+    def prefill_then_decode(stage):
+        pool = stage.make_pool(256, block_size=64)
+        sids = list(range(len(prompts)))
+        for sid, p in zip(sids, prompts):
+            pool.manager.append(sid, len(p))
+        meta = pool.build_metadata(sids, [len(p) for p in prompts])
+        meta.logits_rows = (torch.cumsum(torch.tensor([len(p) for p in prompts]), 0) - 1).to(gpu)
+        ids = torch.tensor([t for p in prompts for t in p], dtype=torch.int32, device=gpu)
+        pre = stage(ids, meta, pool).float().cpu()
+        for sid in sids:
+            pool.manager.append(sid, 1)
+        meta = pool.build_metadata(sids, [1] * len(sids))
+        toks = torch.tensor([(13 * i) % 997 + 1 for i in sids], dtype=torch.int32, device=gpu)
+        return pre, stage(toks, meta, pool).float().cpu()
+
+    b = prefill_then_decode(g)
+    rel = ((a - b[0]).norm() / a.norm()).item()
+    assert rel < 0.05, rel
+    # the decode step against the hipBLASLt fp8 path (unfused SwiGLU, reduce passes)
+    g.block.set_fused_swiglu(False)
+    monkeypatch.setenv("DLI_FP8_TILE", "long")
+    c = prefill_then_decode(g)
+    for x, y in zip(c, b):
+        rel = ((x - y).norm() / x.norm()).item()
+        assert rel < 0.05, rel
+    monkeypatch.setenv("DLI_FP8_TILE", "all")
+    g.block.set_fused_swiglu(True)
+    g.block.set_fused_swiglu(False)   # round trip restores the quantised rows exactly
+    assert torch.equal(g.block.layers[0].mlp.gate_up_proj.weight_fp8.view(torch.uint8),
+                       wq0.view(torch.uint8))
+
+
 def test_sampling_params_in_engine(gpu):
     p = SamplingParams(max_tokens=10, temperature=0.8, top_k=50, top_p=0.9, seed=1, ignore_eos=True)
     a = [s.output for s in _engine().generate(PROMPTS, p)]
