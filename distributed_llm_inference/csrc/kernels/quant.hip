@@ -11,6 +11,17 @@ namespace dli {
 
 constexpr float kFp8Max = 448.f;
 
+// One workgroup per row; threads chosen so each holds <= 4 bf16x8 vectors (<= 1024 threads): a
+// 28672-wide row (70B down-projection input) gets 896 threads x 4 vectors instead of 256 x 14,
+// ~4x the loads in flight per CU at a quarter of the registers.  Rows up to 8192 wide keep 256
+// threads (the same block shape, so the same reduction order, as before).
+static inline int row_threads(int nvec) {
+  int t = (nvec + 3) / 4;
+  t = (t + 63) / 64 * 64;
+  if (t < 256) t = ((nvec + 63) / 64) * 64 < 256 ? ((nvec + 63) / 64) * 64 : 256;
+  return t > 1024 ? 1024 : t;
+}
+
 // Row amax -> scale, then quantise the VPT x 8 register-resident values of each thread (vector
 // index threadIdx.x + i * blockDim.x) and store them as 8-byte fp8 groups.
 template <int VPT>
@@ -48,11 +59,11 @@ __device__ __forceinline__ void store_fp8_row(float (&v)[VPT][8], uint8_t* __res
 // x_parts (optional): x given as fp32 split-K partials [splits, rows, K] of the tile GEMM that
 // produced it, summed and rounded to bf16 on load (bit-identical to the reduce pass).
 template <int VPT, int NS>
-__global__ void __launch_bounds__(256) quant_rowwise_kernel(
+__global__ void __launch_bounds__(1024) quant_rowwise_kernel(
     uint8_t* __restrict__ q, float* __restrict__ scale, const bf16* __restrict__ x,
     const bf16* residual_in, bf16* residual_out, const bf16* __restrict__ norm_w, float eps,
     int K, const float* __restrict__ x_parts, size_t split_stride) {
-  __shared__ float scratch[8];
+  __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = K >> 3;
   const bool add_residual = residual_in != nullptr;
@@ -109,10 +120,10 @@ __global__ void __launch_bounds__(256) quant_rowwise_kernel(
 // The activation is rounded to bf16 before quantisation, exactly as silu_mul_kernel would store
 // it, so the fp8 path differs from the bf16 path only by the quantisation step.
 template <int VPT>
-__global__ void __launch_bounds__(512) silu_mul_quant_kernel(uint8_t* __restrict__ q,
+__global__ void __launch_bounds__(1024) silu_mul_quant_kernel(uint8_t* __restrict__ q,
                                                              float* __restrict__ scale,
                                                              const bf16* __restrict__ x, int I) {
-  __shared__ float scratch[8];
+  __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = I >> 3;
   const bf16x8* g = reinterpret_cast<const bf16x8*>(x + (size_t)row * 2 * I);
@@ -138,10 +149,10 @@ __global__ void __launch_bounds__(512) silu_mul_quant_kernel(uint8_t* __restrict
 // columns.  Columns flagged in `outlier` (nullable) are zeroed here: they are multiplied in bf16
 // by the caller (the mixed-precision decomposition of LLM.int8).
 template <int VPT>
-__global__ void __launch_bounds__(256) quant_rowwise_int8_kernel(
+__global__ void __launch_bounds__(1024) quant_rowwise_int8_kernel(
     int8_t* __restrict__ q, float* __restrict__ scale, const bf16* __restrict__ x,
     const uint8_t* __restrict__ outlier, int K) {
-  __shared__ float scratch[8];
+  __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = K >> 3;
   const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * K);
@@ -191,8 +202,7 @@ int launch_quant_rowwise_int8(int8_t* q, float* scale, const bf16* x, const uint
   if (K % 8 != 0) return -1;
   if (rows == 0) return 0;
   const int nvec = K / 8;
-  int threads = ((nvec + 63) / 64) * 64;
-  if (threads > 256) threads = 256;
+  const int threads = row_threads(nvec);
   const int vpt = (nvec + threads - 1) / threads;
 #define DLI_QI8(V) \
   quant_rowwise_int8_kernel<V><<<rows, threads, 0, stream>>>(q, scale, x, outlier, K)
@@ -215,8 +225,7 @@ int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* re
   if (residual_in != nullptr && residual_out == nullptr) return -2;
   if (rows == 0) return 0;
   const int nvec = K / 8;
-  int threads = ((nvec + 63) / 64) * 64;
-  if (threads > 256) threads = 256;
+  const int threads = row_threads(nvec);
   const int vpt = (nvec + threads - 1) / threads;
   const int ns = x_parts != nullptr ? splits : 0;
 #define DLI_QUANT(V, NS)                                                                    \
@@ -243,8 +252,7 @@ int launch_silu_mul_quant(uint8_t* q, float* scale, const bf16* x, int rows, int
   if (inter % 8 != 0) return -1;
   if (rows == 0) return 0;
   const int nvec = inter / 8;
-  int threads = ((nvec + 63) / 64) * 64;
-  if (threads > 512) threads = 512;
+  const int threads = row_threads(nvec);
   const int vpt = (nvec + threads - 1) / threads;
 #define DLI_SMQ(V) silu_mul_quant_kernel<V><<<rows, threads, 0, stream>>>(q, scale, x, inter)
   if (vpt <= 1) DLI_SMQ(1);
