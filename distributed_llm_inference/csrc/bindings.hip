@@ -521,7 +521,8 @@ void silu_mul_quant(Tensor q_out, Tensor scale, Tensor x) {
 // workspace of splits * M * N.  fp8: A, B are e4m3 bytes with a_scale [M] and b_scale [N] (fp32,
 // both required); out = (A . B^T) * a_scale[:, None] * b_scale[None, :].
 void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
-               optional<Tensor> workspace, optional<Tensor> a_scale, optional<Tensor> b_scale) {
+               optional<Tensor> workspace, optional<Tensor> a_scale, optional<Tensor> b_scale,
+               optional<Tensor> x_out, optional<Tensor> w_out) {
   CHECK_IN(out); CHECK_IN(a); CHECK_IN(b); CHECK_BF16(out);
   const bool fp8 = a.element_size() == 1;   // 1-byte operands: fp8 e4m3 or int8
   TORCH_CHECK(a.scalar_type() == b.scalar_type(), "gemm_tile: a and b must share a dtype");
@@ -562,9 +563,26 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
     TORCH_CHECK(workspace->numel() >= splits * M * N, "gemm_tile: workspace too small");
     ws = workspace->data_ptr<float>();
   }
+  // LLM.int8 outlier columns (int8 only): out += x_out [M, J] . w_out [N, J]^T in the epilogue
+  const dli::bf16* xo = nullptr;
+  const dli::bf16* wo = nullptr;
+  int J = 0;
+  TORCH_CHECK(x_out.has_value() == w_out.has_value(), "gemm_tile: x_out and w_out go together");
+  if (x_out.has_value()) {
+    TORCH_CHECK(precision == 2, "gemm_tile: outlier columns are an int8 (LLM.int8) feature");
+    CHECK_IN(*x_out); CHECK_IN(*w_out); CHECK_BF16(*x_out); CHECK_BF16(*w_out);
+    TORCH_CHECK(x_out->dim() == 2 && w_out->dim() == 2 && x_out->size(0) == M &&
+                w_out->size(0) == N && x_out->size(1) == w_out->size(1),
+                "gemm_tile: x_out [M, J], w_out [N, J]");
+    J = (int)x_out->size(1);
+    TORCH_CHECK(J % 32 == 0, "gemm_tile: J (outlier columns) must be a multiple of 32");
+    xo = bp(*x_out);
+    wo = bp(*w_out);
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
   check_rc(dli::launch_gemm_tile(out.data_ptr(), a.data_ptr(), b.data_ptr(), sa, sb, ws, (int)M,
-                                 (int)N, (int)K, (int)splits, (int)epilogue, precision, cur_stream()),
+                                 (int)N, (int)K, (int)splits, (int)epilogue, precision, cur_stream(),
+                                 xo, wo, J),
            "gemm_tile");
 }
 
@@ -625,7 +643,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tile", &gemm_tile, "C = A . B^T, 256x256 LDS-DMA 8-phase MFMA tile GEMM",
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
         py::arg("epilogue") = 0, py::arg("workspace") = py::none(),
-        py::arg("a_scale") = py::none(), py::arg("b_scale") = py::none());
+        py::arg("a_scale") = py::none(), py::arg("b_scale") = py::none(),
+        py::arg("x_out") = py::none(), py::arg("w_out") = py::none());
   m.def("rms_norm_splitk", &rms_norm_splitk, "residual add + RMSNorm over un-reduced split-K partials",
         py::arg("out"), py::arg("parts"), py::arg("residual"), py::arg("w"), py::arg("eps"),
         py::arg("residual_out") = py::none());

@@ -123,6 +123,16 @@ struct SkArgs {
   float* slabs;      // [sk_wgs][256 * 256] fp32 partials in accumulator (register) order
 };
 
+// LLM.int8 outlier columns (int8 precision only): the bf16 product x_out [M, J] . w_out [N, J]^T
+// of the J feature columns held out of the int8 quantisation is added to the dequantised tile in
+// the epilogue (split 0 only, so a split-K sum counts it once), one bf16 MFMA k-step per 32
+// columns with the fragments loaded straight from global memory (J <= 64: a few KB per tile).
+struct OutlierArgs {
+  const bf16* x;   // [M, J] activations of the outlier columns (zero-padded past the used ones)
+  const bf16* w;   // [N, J] dequantised weight columns (zero-padded likewise)
+  int J;           // multiple of 32; 0 = none
+};
+
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
@@ -140,7 +150,8 @@ template <int EPI, int PREC, bool SKT>
 __global__ void __launch_bounds__(kThreads, 1)
 gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __restrict__ C,
                  const float* __restrict__ a_scale, const float* __restrict__ b_scale,
-                 int M, int N, int K, int tiles_m, int tiles_n, int k_tiles_per_split, SkArgs sk) {
+                 int M, int N, int K, int tiles_m, int tiles_n, int k_tiles_per_split, SkArgs sk,
+                 OutlierArgs ol) {
   constexpr bool FP8 = PREC == kFp8;
   constexpr bool BYTES = PREC != kBf16;   // 1-byte operands
   const char* A = reinterpret_cast<const char*>(Av);
@@ -446,6 +457,27 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
         }
       }
     }
+    if constexpr (PREC == kInt8) {
+      if (ol.J > 0 && split == 0) {
+        // weight fragment = MFMA A operand, as in the main loop: lane l holds w_out row
+        // n0 + 64 wc + 16 j + (l & 15) and x_out row crow + 16 i, k = 8 (l >> 4) .. + 7
+        for (int kk = 0; kk < ol.J; kk += 32) {
+          bf16x8 wf[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            wf[j] = *reinterpret_cast<const bf16x8*>(
+                ol.w + (size_t)(n0 + wc * 64 + j * 16 + fr) * ol.J + kk + 8 * (lane >> 4));
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int m = min(crow + i * 16, M - 1);
+            const bf16x8 xf = *reinterpret_cast<const bf16x8*>(ol.x + (size_t)m * ol.J + kk +
+                                                               8 * (lane >> 4));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma(wf[j], xf, acc[i][j]);
+          }
+        }
+      }
+    }
     if (EPI == kSwiGLU) {
       // n-fragments (2p, 2p+1) = (gate, up) of output columns n0/2 + wc*32 + p*16 + cq + e
       bf16* out = reinterpret_cast<bf16*>(C);
@@ -540,7 +572,7 @@ int device_cus() {
 template <int PREC>
 int launch_tile(void* C, const void* A, const void* B, const float* sa, const float* sb,
                 float* workspace, int M, int N, int K, int splits, int epilogue,
-                hipStream_t stream) {
+                hipStream_t stream, OutlierArgs ol) {
   constexpr int esz = PREC == kBf16 ? 2 : 1;
   const int kt = (int)((size_t)K * esz / 128);
   if (M <= 0 || N % kTN != 0 || (size_t)K * esz % 128 != 0 || splits < 0) return -1;
@@ -567,10 +599,10 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
     const int grid = sk.n_dp + sk.sk_wgs;
     if (epilogue == kSwiGLU)
       gemm_tile_kernel<kSwiGLU, PREC, true><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
-                                                                          tiles_m, tiles_n, kt, sk);
+                                                                          tiles_m, tiles_n, kt, sk, ol);
     else if (epilogue == kStoreBf16)
       gemm_tile_kernel<kStoreBf16, PREC, true><<<grid, kThreads, 0, stream>>>(
-          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kt, sk);
+          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kt, sk, ol);
     else
       return -4;
     return 0;
@@ -584,7 +616,7 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
   sk.n_dp = grid;
   if (splits > 1) {
     gemm_tile_kernel<kStoreF32, PREC, false><<<grid, kThreads, 0, stream>>>(
-        A, B, workspace, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk);
+        A, B, workspace, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol);
     if (epilogue == kStoreF32) return 0;
     const size_t MN = (size_t)M * N;
     size_t blocks = (MN / 8 + 255) / 256;
@@ -593,10 +625,10 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
                                                                workspace, splits, MN);
   } else if (epilogue == kSwiGLU) {
     gemm_tile_kernel<kSwiGLU, PREC, false><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
-                                                                         tiles_m, tiles_n, kps, sk);
+                                                                         tiles_m, tiles_n, kps, sk, ol);
   } else if (epilogue == kStoreBf16) {
     gemm_tile_kernel<kStoreBf16, PREC, false><<<grid, kThreads, 0, stream>>>(
-        A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk);
+        A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol);
   } else {
     return -4;
   }
@@ -621,17 +653,20 @@ long long gemm_tile_sk_workspace_floats() {
 
 int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale,
                      const float* b_scale, float* workspace, int M, int N, int K, int splits,
-                     int epilogue, int precision, hipStream_t stream) {
+                     int epilogue, int precision, hipStream_t stream, const bf16* x_out,
+                     const bf16* w_out, int J) {
+  if (J < 0 || J % 32 != 0 || (J > 0 && (precision != kInt8 || !x_out || !w_out))) return -12;
+  const OutlierArgs ol{x_out, w_out, J};
   switch (precision) {
     case kBf16:
       return launch_tile<kBf16>(C, A, B, nullptr, nullptr, workspace, M, N, K, splits, epilogue,
-                                stream);
+                                stream, ol);
     case kFp8:
       return launch_tile<kFp8>(C, A, B, a_scale, b_scale, workspace, M, N, K, splits, epilogue,
-                               stream);
+                               stream, ol);
     case kInt8:
       return launch_tile<kInt8>(C, A, B, a_scale, b_scale, workspace, M, N, K, splits, epilogue,
-                                stream);
+                                stream, ol);
   }
   return -6;
 }

@@ -90,7 +90,10 @@ class Linear(nn.Module):
         if self.weight_int8 is not None:
             y = ops.llm_int8_linear(x.reshape(-1, self.in_features), self.weight_int8,
                                     self.weight_scale, self.int8_threshold,
-                                    wq_t=self.weight_int8_t)
+                                    wq_t=self.weight_int8_t,
+                                    defer_reduce=defer_reduce and self.bias is None)
+            if isinstance(y, ops.SplitKPartials):   # the consumer reduces (rms_norm / rope_cache)
+                return y
             y = y.reshape(*x.shape[:-1], self.out_features)
             return y + self.bias if self.bias is not None else y
         if self.weight_fp8 is None:

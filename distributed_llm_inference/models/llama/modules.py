@@ -122,13 +122,22 @@ class LlamaMLP(nn.Module):
         w = self.gate_up_proj
         if on == self.fused_swiglu:
             return
-        if w.is_int8 or w.bias is not None or w.out_features % 256:
+        if w.bias is not None or w.out_features % 256:
             return
         if w.is_fp8 and on and not ops.fp8_tile_all():
             return
+        if w.is_int8 and on and not ops.int8_fused_outliers():
+            return
         perm = ops.swiglu_interleave if on else ops.swiglu_deinterleave
         with torch.no_grad():
-            if w.is_fp8:
+            if w.is_int8:
+                # LLM.int8: rows of the int8 weight and its per-channel scale, columns of the
+                # transposed copy; the outlier columns are gathered from these per product
+                w.weight_int8.copy_(perm(w.weight_int8))
+                w.weight_scale.copy_(perm(w.weight_scale.reshape(-1, 1)).reshape(w.weight_scale.shape))
+                if w.weight_int8_t is not None:
+                    w.weight_int8_t.copy_(perm(w.weight_int8_t.t()).t())
+            elif w.is_fp8:
                 # per-output-channel quantisation commutes with the row permutation
                 w.weight_fp8.copy_(perm(w.weight_fp8.view(torch.uint8)).view(w.weight_fp8.dtype))
                 w.weight_scale.copy_(perm(w.weight_scale.reshape(-1, 1)).reshape(w.weight_scale.shape))
@@ -138,6 +147,11 @@ class LlamaMLP(nn.Module):
 
     def forward(self, normed: Optional[torch.Tensor], x_q=None, defer_reduce: bool = False):
         gp = self.gate_up_proj
+        if self.fused_swiglu and gp.is_int8:
+            # SwiGLU in the int8 tile GEMM's epilogue, after the fused bf16 outlier product
+            h = ops.llm_int8_linear(normed, gp.weight_int8, gp.weight_scale, gp.int8_threshold,
+                                    wq_t=gp.weight_int8_t, swiglu=True)
+            return self.down_proj(h, defer_reduce=defer_reduce)
         if self.fused_swiglu and gp.is_fp8:
             xq, xs = x_q if x_q is not None else ops.quant_rowwise(normed)
             if xq.is_cuda and ops.tile_gemm_splits_fp8(xq.shape[0], gp.out_features,

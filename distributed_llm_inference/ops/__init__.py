@@ -501,19 +501,30 @@ LLM_INT8_MAX_OUTLIERS = 64   # static outlier-column capacity (graph-capturable 
 LLM_INT8_SELECT_MAX_K = 32768   # int8_outlier.hip select kernel: 1024 threads x 32 columns
 
 
+def int8_fused_outliers() -> bool:
+    """``DLI_INT8_FUSED=1`` (default): the LLM.int8 outlier product runs in the int8 tile GEMM's
+    epilogue, split-K partials go to their consumers and gate|up fuses SwiGLU; ``0`` = the
+    previous path (hipBLASLt addmm for the outliers, reduce passes, separate silu_mul) for A/B."""
+    return os.environ.get("DLI_INT8_FUSED", "1") == "1"
+
+
 def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, threshold: float = 6.0,
                     max_outliers: int = LLM_INT8_MAX_OUTLIERS,
-                    wq_t: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    wq_t: Optional[torch.Tensor] = None, swiglu: bool = False,
+                    defer_reduce: bool = False):
     """LLM.int8 matmul ``x [M, K] @ W^T`` with ``W ~= wq * ws[:, None]`` (int8, per-channel).
 
     Mixed-precision decomposition as in bitsandbytes ``Linear8bitLt(threshold=...)``: feature
     columns whose magnitude exceeds ``threshold`` anywhere in the batch are multiplied in bf16
     (with the dequantised weight columns); every other column goes through per-row int8
-    quantisation and the int8 MFMA tile GEMM (``gemm_tile.hip``, v_mfma_i32_16x16x64_i8).  To keep
+    quantisation and the int8 MFMA tile GEMM (``gemm_tile.hip``, v_mfma_i32_16x16x64_i8), whose
+    epilogue adds the bf16 outlier product (one bf16 MFMA k-step per 32 outlier columns).  To keep
     shapes static (hipGraph decode) the outlier set is the ``max_outliers`` largest columns that
     pass the threshold; ``threshold <= 0`` disables the decomposition.  ``wq_t``: optional
     transposed copy ``[K, N]`` of ``wq`` (GPU) that makes the outlier weight-column gather
-    coalesced."""
+    coalesced.  ``swiglu``: ``wq`` / ``ws`` rows in ``swiglu_interleave`` order, returns
+    ``silu(gate) * up`` ([M, N/2]).  ``defer_reduce``: a split-K product returns its fp32 partials
+    (:class:`SplitKPartials`, the outlier product inside split 0's) for a consumer to reduce."""
     M, K = x.shape
     N = wq.shape[0]
     outl = None   # (x_out [M, J], w_out [N, J]) bf16: the outlier product
@@ -549,17 +560,42 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
     xq, xs = quant_rowwise_int8(x, flags)
     if _gpu(x) and N % 256 == 0 and K % 128 == 0 and M > 0:
         sp = tile_gemm_splits(max(M, TILE_GEMM_MIN_M), N, K, elem_bytes=1) or 1
-        y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+        if swiglu:
+            sp = 1
+        xo = wo = None
+        if outl is not None:
+            xo, wo = outl
+            J = xo.shape[1]
+            if J % 32:   # the epilogue's bf16 MFMA k-step: zero-pad to a multiple of 32
+                pad = 32 - J % 32
+                xo = torch.nn.functional.pad(xo, (0, pad))
+                wo = torch.nn.functional.pad(wo, (0, pad))
+            xo, wo = xo.contiguous(), wo.contiguous()
+        if not int8_fused_outliers():
+            # A/B baseline: int8 GEMM (+ reduce pass), then the outlier product by one hipBLASLt
+            # addmm and SwiGLU as a separate pass
+            y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+            ws_ = torch.empty(sp * M * N, dtype=torch.float32, device=x.device) if sp > 1 else None
+            native().gemm_tile(y, xq, wq, int(sp), 0, ws_, xs, ws)
+            if outl is not None:
+                y.addmm_(outl[0], outl[1].t())
+            return swiglu_interleaved(y) if swiglu else y
+        if (defer_reduce and sp > 1 and not swiglu
+                and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
+            parts = torch.empty(sp, M, N, dtype=torch.float32, device=x.device)
+            dummy = torch.empty(M, 0, dtype=torch.bfloat16, device=x.device)   # C is unused
+            native().gemm_tile(dummy, xq, wq, int(sp), 1, parts.view(-1), xs, ws, xo, wo)
+            return SplitKPartials(parts)
+        y = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
         ws_ = torch.empty(sp * M * N, dtype=torch.float32, device=x.device) if sp > 1 else None
-        native().gemm_tile(y, xq, wq, int(sp), 0, ws_, xs, ws)
-        if outl is not None:   # y += x_out . w_out^T in one hipBLASLt call (bf16 C input)
-            y.addmm_(outl[0], outl[1].t())
+        native().gemm_tile(y, xq, wq, int(sp), 2 if swiglu else 0, ws_, xs, ws, xo, wo)
         return y
     # CPU / untileable shapes: dequantised reference
     y = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()
     if outl is not None:
         y = y + outl[0].float() @ outl[1].float().t()
-    return y.to(torch.bfloat16)
+    y = y.to(torch.bfloat16)
+    return swiglu_interleaved(y) if swiglu else y
 
 
 def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,

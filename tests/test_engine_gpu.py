@@ -262,6 +262,45 @@ def test_int8_weights_close_to_bf16(gpu):
     assert rel < 0.1, rel
 
 
+def test_int8_fused_path_matches_unfused(gpu, monkeypatch):
+    """LLM.int8 stage on the fused path (outlier product in the tile epilogue, SwiGLU on
+    interleaved int8 rows, QKV / O / down partials into their consumers) vs the unfused path
+    (separate reduce passes, silu_mul), at a 128-sequence decode batch and a 384-token prefill."""
+    spec = SPEC.replace(hidden_size=512, intermediate_size=1024, num_heads=8, num_kv_heads=2,
+                        head_dim=64)
+    g = CausalLMStage(spec, 0, 3, device=gpu).init_random(12)
+    g.quantize("int8", threshold=3.0)
+    prompts = [[(5 * i + j) % 997 + 1 for j in range(3)] for i in range(128)]
+
+    def run():
+        pool = g.make_pool(256, block_size=64)
+        sids = list(range(len(prompts)))
+        for sid, p in zip(sids, prompts):
+            pool.manager.append(sid, len(p))
+        meta = pool.build_metadata(sids, [len(p) for p in prompts])
+        meta.logits_rows = (torch.cumsum(torch.tensor([len(p) for p in prompts]), 0) - 1).to(gpu)
+        ids = torch.tensor([t for p in prompts for t in p], dtype=torch.int32, device=gpu)
+        pre = g(ids, meta, pool).float().cpu()
+        for sid in sids:
+            pool.manager.append(sid, 1)
+        meta = pool.build_metadata(sids, [1] * len(sids))
+        toks = torch.tensor([(11 * i) % 997 + 1 for i in sids], dtype=torch.int32, device=gpu)
+        return pre, g(toks, meta, pool).float().cpu()
+
+    monkeypatch.setenv("DLI_SPLITK_DEFER", "0")
+    a = run()
+    monkeypatch.setenv("DLI_SPLITK_DEFER", "1")
+    wq0 = g.block.layers[0].mlp.gate_up_proj.weight_int8.clone()
+    g.block.set_fused_swiglu(True)
+    assert g.block.layers[0].mlp.fused_swiglu
+    b = run()
+    for x, y in zip(a, b):
+        rel = ((x - y).norm() / x.norm()).item()
+        assert rel < 0.02, rel
+    g.block.set_fused_swiglu(False)
+    assert torch.equal(g.block.layers[0].mlp.gate_up_proj.weight_int8, wq0)
+
+
 def test_deferred_splitk_reduce_is_bit_identical(gpu, monkeypatch):
     """Split-K partials reduced inside the next RMSNorm (default) vs the separate reduce pass
     (DLI_SPLITK_DEFER=0): same bf16 rounding points, so the stage output is bit-identical."""

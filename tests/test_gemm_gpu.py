@@ -184,6 +184,34 @@ def test_llm_int8_linear_gpu_matches_cpu_and_bf16(gpu):
     assert ((y_gpu - ref).norm() / ref.norm()).item() < 0.02
 
 
+@pytest.mark.parametrize("M,K,N,n_out", [(512, 1024, 1024, 5), (300, 2048, 512, 80), (7, 1024, 256, 3),
+                                         (130, 4096, 768, 0)])
+def test_llm_int8_fused_outlier_epilogue_swiglu_and_partials(gpu, M, K, N, n_out):
+    """The bf16 outlier product runs inside the int8 tile GEMM's epilogue: plain store, fused
+    SwiGLU (pairwise-interleaved int8 rows + scales) and deferred split-K partials (the outlier
+    term in split 0 only) all match the dequantised CPU reference."""
+    torch.manual_seed(M + K + n_out)
+    x = torch.randn(M, K)
+    if n_out:
+        x[:, torch.randperm(K)[:n_out]] *= 40.0
+    xb = x.to(torch.bfloat16)
+    w = (torch.randn(N, K) / K ** 0.5).to(torch.bfloat16)
+    wq, ws = ops.quantize_weight_int8(w)
+    ref = ops.llm_int8_linear(xb, wq, ws, 6.0).float()                 # CPU reference path
+    y = ops.llm_int8_linear(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0).float().cpu()
+    assert ((y - ref).norm() / ref.norm()).item() < 5e-3
+    p = ops.llm_int8_linear(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, defer_reduce=True)
+    if isinstance(p, ops.SplitKPartials):
+        assert p.parts.shape[0] > 1
+        yp = p.parts.sum(0).cpu()
+        assert ((yp - ref).norm() / ref.norm()).item() < 5e-3
+    wqi = ops.swiglu_interleave(wq.to(gpu))
+    wsi = ops.swiglu_interleave(ws.to(gpu).reshape(-1, 1)).reshape(-1)
+    h = ops.llm_int8_linear(xb.to(gpu), wqi, wsi, 6.0, swiglu=True).float().cpu()
+    href = ops.silu_mul(ref.to(torch.bfloat16)).float()
+    assert ((h - href).norm() / href.norm()).item() < 1e-2
+
+
 def _llm_int8_outliers_ref(x, wq, ws, threshold, J):
     """fp32 PyTorch reference of int8_outlier.hip: the <= J largest column maxima above
     `threshold` (distinct values), in column order, padded with (column 0, weight 0)."""
