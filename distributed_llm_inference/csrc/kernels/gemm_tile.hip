@@ -290,6 +290,13 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
           for (int j = 0; j < 2; ++j)
             acc[mq * 4 + i][nq * 2 + j] = mfma_fp8(bf[j][0], bf[j][1], af[i][0], af[i][1],
                                                    acc[mq * 4 + i][nq * 2 + j]);
+        // pin the segment here: without a use the compiler sank all 32 MFMAs of the k-tile past
+        // the phase barriers to the loop's end, which serialised them against the partner wave's
+        // reads (one 1024-cycle MFMA burst per wave instead of four interleaved segments)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[mq * 4 + i][nq * 2 + j]));
       } else if (PREC == kInt8) {
         // two K=64 int8 MFMAs per k-tile (16-B chunks g and g+4), like the two bf16 k-steps
 #pragma unroll

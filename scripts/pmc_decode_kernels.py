@@ -1,6 +1,6 @@
 """Workload for PMC passes over the decode-step kernels at the 70B / 512-sequence shapes:
-gate|up tile GEMM with the SwiGLU epilogue, the split-K O projection (partials only), and the
-paged decode attention at ~590 keys.  Cold weights (rotating set > Infinity Cache).
+gate|up tile GEMM with the SwiGLU epilogue, the split-K O projection (partials only) — bf16 and
+fp8 weights — and the paged decode attention at ~590 keys.  Cold weights (rotating set > Infinity Cache).
 
     rocprofv3 --pmc <counters> --kernel-trace --output-format csv -d DIR -- python3 scripts/pmc_decode_kernels.py
 """
@@ -24,6 +24,15 @@ sp = ops.tile_gemm_splits(M, H, H)
 for i in range(6):
     ops.gemm_tile(x, gu[i % 2], swiglu=True)
     ops.gemm_tile(x, wo[i % 4], splits=sp, defer_reduce=True)
+# fp8 weights: the same two products on the block-scaled fp8 MFMA (rows / scales interleaved for
+# the SwiGLU epilogue as the engine does)
+xq, xs = ops.quant_rowwise(x)
+gq = [ops.quantize_weight_fp8(ops.swiglu_interleave(g)) for g in gu]
+oq = [ops.quantize_weight_fp8(w) for w in wo]
+spf = ops.tile_gemm_splits_fp8(M, H, H)
+for i in range(6):
+    ops.gemm_tile_fp8(xq, xs, gq[i % 2][0], gq[i % 2][1], swiglu=True)
+    ops.gemm_tile_fp8(xq, xs, oq[i % 4][0], oq[i % 4][1], splits=spf, defer_reduce=True)
 # decode attention: 512 sequences x 590 keys, 64 q heads / 8 kv heads, D = 128
 B, L, nh, nkv, D, bs = 512, 590, 64, 8, 128, 64
 nb_per = (L + bs - 1) // bs
