@@ -70,15 +70,53 @@ struct KVFrag {
   bf16x8 v[D / 16];
 };
 
+// fp8 decode with D % 64 == 0 reads K and V^T with 16-byte loads (like bf16) by permuting the
+// head dimension d, which both products are free to do as long as every operand agrees:
+//   * S^T = K . Q^T sums over d: lane (col, h4) takes d = 64c' + 16h4 + [0, 16) of a chunk pair
+//     (2c', 2c'+1) — one 16-byte K load — and Q is loaded with the same map (q_dofs);
+//   * O^T rows are d: row i of V^T blocks (2e', 2e'+1) is d = 32e' + 2i + {0, 1}, one 16-byte
+//     load of two adjacent d's 8 keys each, so a lane's accumulators hold d = 32e' + 8h4 + [0, 8)
+//     (o_dofs) and the output is written with that map.
+template <int D, bool FP8>
+struct DPerm {
+  static constexpr bool on = FP8 && D % 64 == 0;
+};
+
+// element offset of the 8 q values of chunk c held by lane group h4
+template <int D, bool FP8>
+__device__ __forceinline__ int q_dofs(int c, int h4) {
+  return DPerm<D, FP8>::on ? 64 * (c >> 1) + 16 * h4 + 8 * (c & 1) : 32 * c + 8 * h4;
+}
+
 //   kc/vc: the K / V^T caches, hb: element offset of this kv head's page, offk: slot offset of the
-//   step inside the page.  fp8 caches load 8 bytes per fragment and widen to bf16 in registers
-//   (exact), so both MFMA products stay bf16 x bf16.
+//   step inside the page.  fp8 caches widen to bf16 in registers (exact), so both MFMA products
+//   stay bf16 x bf16.
 template <int D, bool FP8>
 __device__ __forceinline__ void attn_load(KVFrag<D>& f, const void* __restrict__ kc,
                                           const void* __restrict__ vc, size_t hb, int offk) {
   const int lane = threadIdx.x & 63;
   const int col = lane & 15, h4 = lane >> 4;
   const int krow0 = offk + 8 * (col >> 2) + (col & 3);
+  if constexpr (DPerm<D, FP8>::on) {
+    const uint8_t* k8 = static_cast<const uint8_t*>(kc);
+    const uint8_t* v8 = static_cast<const uint8_t*>(vc);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int c2 = 0; c2 < D / 64; ++c2) {
+        const uint4 r = *reinterpret_cast<const uint4*>(k8 + hb + (size_t)(krow0 + 4 * t) * D + 64 * c2 + 16 * h4);
+        f.k[t][2 * c2] = fp8x8_to_bf16x8(make_uint2(r.x, r.y));
+        f.k[t][2 * c2 + 1] = fp8x8_to_bf16x8(make_uint2(r.z, r.w));
+      }
+#pragma unroll
+    for (int e2 = 0; e2 < D / 32; ++e2) {
+      const uint4 r = *reinterpret_cast<const uint4*>(
+          v8 + hb + ((size_t)((offk >> 3) + h4) * D + 32 * e2 + 2 * col) * 8);
+      f.v[2 * e2] = fp8x8_to_bf16x8(make_uint2(r.x, r.y));
+      f.v[2 * e2 + 1] = fp8x8_to_bf16x8(make_uint2(r.z, r.w));
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -96,6 +134,19 @@ __device__ __forceinline__ void attn_load(KVFrag<D>& f, const void* __restrict__
       f.v[e] = fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(vc) + o));
     else
       f.v[e] = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(vc) + o);
+  }
+}
+
+// The D/16 f32x4 units of O^T a lane holds (query column col): unit u -> first d and values.
+template <int D, bool FP8>
+__device__ __forceinline__ void o_unit(const WaveState<D>& st, int u, int h4, int& d, f32x4& v) {
+  if constexpr (DPerm<D, FP8>::on) {
+    const int e2 = u >> 1, r0 = (u & 1) * 2;
+    d = 32 * e2 + 8 * h4 + 4 * (u & 1);
+    v = f32x4{st.o[2 * e2][r0], st.o[2 * e2 + 1][r0], st.o[2 * e2][r0 + 1], st.o[2 * e2 + 1][r0 + 1]};
+  } else {
+    d = 16 * u + 4 * h4;
+    v = st.o[u];
   }
 }
 
@@ -228,7 +279,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
     const bf16* qrow = p.q + ((size_t)b * p.nh + qh) * D;
 #pragma unroll
     for (int c = 0; c < D / 32; ++c)
-      qf[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qrow + 32 * c + 8 * h4) : zero8();
+      qf[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qrow + q_dofs<D, FP8>(c, h4)) : zero8();
     // ---- rolling / full segment ----
     int seg_base, seg_len;
     if (WIN) {
@@ -271,7 +322,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
       const bf16* qsrow = p.q_sink + ((size_t)b * p.nh + qh) * D;
 #pragma unroll
       for (int c = 0; c < D / 32; ++c)
-        qs[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qsrow + 32 * c + 8 * h4) : zero8();
+        qs[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qsrow + q_dofs<D, FP8>(c, h4)) : zero8();
       const int nS = min(p.n_sink, L);
       for (int u0 = 0; u0 < nS; u0 += 32) {
         const int page = bt[u0 / p.bs];
@@ -283,7 +334,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
       }
     }
   }
-  // ---- write: lane (col, h4) holds O^T rows d = 16e + 4h4 + r of query column col ----
+  // ---- write: lane (col, h4) holds the O^T units o_unit() of query column col ----
   float lsum = st.l;
   lsum += __shfl_xor(lsum, 16, 64);
   lsum += __shfl_xor(lsum, 32, 64);
@@ -295,17 +346,25 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
       const float inv = lsum > 0.f ? vsc / lsum : 0.f;
       bf16* orow = p.out + ((size_t)b * p.nh + head) * D;
 #pragma unroll
-      for (int e = 0; e < D / 16; ++e) {
+      for (int u = 0; u < D / 16; ++u) {
+        int d;
+        f32x4 o;
+        o_unit<D, FP8>(st, u, h4, d, o);
         bf16x4 v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (bf16)(st.o[e][r] * inv);
-        *reinterpret_cast<bf16x4*>(orow + 16 * e + 4 * h4) = v;
+        for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[r] * inv);
+        *reinterpret_cast<bf16x4*>(orow + d) = v;
       }
     } else {
       const size_t r0 = ((size_t)split * B + b) * p.nh + head;
       float* prow = p.part_o + r0 * D;
 #pragma unroll
-      for (int e = 0; e < D / 16; ++e) *reinterpret_cast<f32x4*>(prow + 16 * e + 4 * h4) = st.o[e] * vsc;
+      for (int u = 0; u < D / 16; ++u) {
+        int d;
+        f32x4 o;
+        o_unit<D, FP8>(st, u, h4, d, o);
+        *reinterpret_cast<f32x4*>(prow + d) = o * vsc;
+      }
       if (h4 == 0) {
         p.part_ml[r0 * 2] = st.m;
         p.part_ml[r0 * 2 + 1] = lsum;
@@ -316,7 +375,12 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
     float* lo = lds + (wave * 16 + col) * LROW;
     float* lml = lds + 4 * 16 * LROW;  // [wave][col][m, l]
 #pragma unroll
-    for (int e = 0; e < D / 16; ++e) *reinterpret_cast<f32x4*>(lo + 16 * e + 4 * h4) = st.o[e];
+    for (int u = 0; u < D / 16; ++u) {
+      int d;
+      f32x4 o;
+      o_unit<D, FP8>(st, u, h4, d, o);
+      *reinterpret_cast<f32x4*>(lo + d) = o;
+    }
     if (h4 == 0) {
       lml[(wave * 16 + col) * 2] = st.m;
       lml[(wave * 16 + col) * 2 + 1] = lsum;

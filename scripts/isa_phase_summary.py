@@ -10,7 +10,7 @@ between their barriers (it sank all of them to the loop's end in the fp8 kernel 
 import re
 import sys
 
-KEEP = ("v_mfma", "s_barrier", "ds_read", "global_load_lds", "buffer_load", "s_waitcnt", "s_setprio",
+KEEP = ("v_mfma", "s_barrier", "ds_read", "global_load", "buffer_load", "v_cvt_scalef32_pk_bf16_fp8", "v_cvt_pk_bf16", "s_waitcnt", "s_setprio",
         "s_cbranch")
 
 
