@@ -114,7 +114,8 @@ class KVPool:
         if num_splits is None:
             max_len = int(sl.max()) if B else 1
             num_splits = ops.decode_splits(B, self.spec.num_kv_heads, self.spec.group_size,
-                                           max_len) if (is_decode and dev.type == "cuda") else 1
+                                           max_len, kv_fp8=self.dtype != torch.bfloat16
+                                           ) if (is_decode and dev.type == "cuda") else 1
         tile_map = None
         if not is_decode and dev.type == "cuda" and B:
             tile_map = ops.prefill_tiles(q_lens, self.spec.num_heads,

@@ -181,13 +181,17 @@ def rope_cache(qkv: torch.Tensor, positions: Optional[torch.Tensor],
 
 
 # ----------------------------------------------------------------------------- attention
-def decode_splits(batch: int, nkv: int, group: int, max_len: int, cu: int = 256) -> int:
+def decode_splits(batch: int, nkv: int, group: int, max_len: int, cu: int = 256,
+                  kv_fp8: bool = False) -> int:
     """Split-K factor for decode.  The kernel runs one wave per (sequence, kv head, 16-head group,
     split); aim for ~4 waves per CU (measured best on the 70B head config from B = 1 to 16, 8k-32k
     contexts: profiles/attn_decode_microbench.json) while keeping >= 1 key step per split.  Splits come
     in multiples of 4 from 4 up (a workgroup's 4 waves merge theirs in LDS, csrc/kernels/
     attention.hip), so B = 1 at 8k context runs 256 splits (2048 waves) instead of the 64 the
-    unmerged partial traffic used to allow."""
+    unmerged partial traffic used to allow.  An fp8 cache streams half the bytes per key step, so
+    where the bf16 rule already splits (2-16) it takes twice the splits (B = 64 at 4k: 104 -> 98 us,
+    B = 16 at 8k: 58 -> 56 us; one split stays best at large batch and 128 at B = 1:
+    profiles/attn_fp8kv_split_sweep.json)."""
     waves = batch * nkv * ((group + 15) // 16)
     if waves >= 8 * cu:
         return 1
@@ -195,6 +199,8 @@ def decode_splits(batch: int, nkv: int, group: int, max_len: int, cu: int = 256)
     want = (target + waves - 1) // waves
     max_useful = max(1, (max_len + 31) // 32)
     s = int(max(1, min(want, max_useful, 512)))
+    if kv_fp8 and 2 <= s <= 16:
+        s = min(2 * s, max_useful)
     if s >= 4:
         return s // 4 * 4
     return 2 if s == 3 else s

@@ -315,7 +315,7 @@ class StageExecutor:
         if self.device.type != "cuda":
             return 1
         return ops.decode_splits(rows, self.spec.num_kv_heads, self.spec.group_size,
-                                 self.max_seq_len)
+                                 self.max_seq_len, kv_fp8=self.pool.dtype != torch.bfloat16)
 
     # ------------------------------------------------------------------ forward
     def _forward(self, meta: AttnMetadata, inputs: torch.Tensor, n_sample: int,

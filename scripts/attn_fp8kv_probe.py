@@ -1,6 +1,7 @@
 """Decode attention with a bf16 vs an fp8 (e4m3fn) KV cache: µs per call and effective KV read
 bandwidth (bytes actually stored) at the Llama-3-70B head config, graph replay, rotating layers.
-    python scripts/attn_fp8kv_probe.py  -> gpurun_out/attn_fp8kv_probe.json"""
+    python scripts/attn_fp8kv_probe.py [--sweep]  -> gpurun_out/attn_fp8kv_probe.json
+--sweep also times 2x and 4x the decode_splits() choice (split heuristic check)."""
 import json
 import os
 import sys
@@ -14,6 +15,40 @@ from distributed_llm_inference import ops  # noqa: E402
 dev = torch.device("cuda:0")
 nh, nkv, D, bs = 64, 8, 128, 64
 res = []
+
+
+def timed(B, L, fp8, esz, layers, ks, vs, bt, lens, q, splits, chosen):
+    ws = ops.decode_workspace(B, nh, D, splits, dev) if splits > 1 else None
+    out = torch.empty_like(q)
+
+    def call(i):
+        ops.attn_decode(q, None, ks[i % layers], vs[i % layers], bt, lens, D ** -0.5,
+                        num_splits=splits, workspace=ws, out=out, k_scale=0.5, v_scale=0.5)
+    for i in range(layers):
+        call(i)
+    torch.cuda.synchronize()
+    n = max(layers, 8)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(n):
+            call(i)
+    g.replay()
+    torch.cuda.synchronize()
+    reps = 20
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    us = (time.perf_counter() - t0) / (n * reps) * 1e6
+    kv = 2 * B * L * nkv * D * esz
+    r = {"B": B, "L": L, "kv": "fp8" if fp8 else "bf16", "splits": splits, "us": round(us, 1),
+         "TBps": round(kv / us / 1e6, 2)}
+    if not chosen:
+        r["sweep"] = True
+    print(json.dumps(r), flush=True)
+    res.append(r)
+
+
 for B, L in [(512, 600), (64, 4096), (16, 8192), (1, 8192)]:
     for fp8 in (False, True):
         bps = (L + bs - 1) // bs
@@ -27,34 +62,12 @@ for B, L in [(512, 600), (64, 4096), (16, 8192), (1, 8192)]:
         bt = torch.randperm(nblk, device=dev).to(torch.int32).view(B, bps)
         lens = torch.full((B,), L, dtype=torch.int32, device=dev)
         q = torch.randn(B, nh, D, device=dev, dtype=torch.bfloat16)
-        splits = ops.decode_splits(B, nkv, nh // nkv, L)
-        ws = ops.decode_workspace(B, nh, D, splits, dev) if splits > 1 else None
-        out = torch.empty_like(q)
-
-        def call(i):
-            ops.attn_decode(q, None, ks[i % layers], vs[i % layers], bt, lens, D ** -0.5,
-                            num_splits=splits, workspace=ws, out=out, k_scale=0.5, v_scale=0.5)
-        for i in range(layers):
-            call(i)
-        torch.cuda.synchronize()
-        n = max(layers, 8)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for i in range(n):
-                call(i)
-        g.replay()
-        torch.cuda.synchronize()
-        reps = 20
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            g.replay()
-        torch.cuda.synchronize()
-        us = (time.perf_counter() - t0) / (n * reps) * 1e6
-        kv = 2 * B * L * nkv * D * esz
-        r = {"B": B, "L": L, "kv": "fp8" if fp8 else "bf16", "splits": splits, "us": round(us, 1),
-             "TBps": round(kv / us / 1e6, 2)}
-        print(json.dumps(r), flush=True)
-        res.append(r)
+        s0 = ops.decode_splits(B, nkv, nh // nkv, L)
+        cands = [s0]
+        if "--sweep" in sys.argv:
+            cands += [c for c in ([2, 4] if s0 == 1 else [2 * s0, 4 * s0]) if c <= min(512, L // 32)]
+        for splits in cands:
+            timed(B, L, fp8, esz, layers, ks, vs, bt, lens, q, splits, splits == s0)
         del ks, vs
         torch.cuda.empty_cache()
 os.makedirs("gpurun_out", exist_ok=True)
