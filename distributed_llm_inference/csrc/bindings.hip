@@ -522,18 +522,41 @@ void silu_mul_quant(Tensor q_out, Tensor scale, Tensor x) {
 // both required); out = (A . B^T) * a_scale[:, None] * b_scale[None, :].
 void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
                optional<Tensor> workspace, optional<Tensor> a_scale, optional<Tensor> b_scale,
-               optional<Tensor> x_out, optional<Tensor> w_out) {
-  CHECK_IN(out); CHECK_IN(a); CHECK_IN(b); CHECK_BF16(out);
+               optional<Tensor> x_out, optional<Tensor> w_out, optional<Tensor> a_mx,
+               optional<Tensor> out_mx) {
+  CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
+  TORCH_CHECK(epilogue == 3 ? out.element_size() == 1 : out.scalar_type() == at::kBFloat16,
+              "gemm_tile: bf16 output (fp8 bytes for epilogue 3)");
   const bool fp8 = a.element_size() == 1;   // 1-byte operands: fp8 e4m3 or int8
   TORCH_CHECK(a.scalar_type() == b.scalar_type(), "gemm_tile: a and b must share a dtype");
   TORCH_CHECK(fp8 || a.scalar_type() == at::kBFloat16, "gemm_tile: bf16, fp8 (e4m3) or int8 operands");
-  const int precision = !fp8 ? 0 : (a.scalar_type() == at::kChar ? 2 : 1);
+  int precision = !fp8 ? 0 : (a.scalar_type() == at::kChar ? 2 : 1);
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_tile: 2-D tensors");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K && out.size(0) == M, "gemm_tile: shape mismatch");
-  TORCH_CHECK(epilogue >= 0 && epilogue <= 2,
-              "gemm_tile: epilogue must be 0 (store), 1 (split-K partials only) or 2 (swiglu)");
-  TORCH_CHECK(epilogue == 1 || out.size(1) == (epilogue == 2 ? N / 2 : N), "gemm_tile: output columns");
+  TORCH_CHECK(epilogue >= 0 && epilogue <= 3,
+              "gemm_tile: epilogue must be 0 (store), 1 (split-K partials only), 2 (swiglu) or 3 "
+              "(swiglu -> fp8 with MX scales)");
+  TORCH_CHECK(epilogue == 1 || out.size(1) == (epilogue >= 2 ? N / 2 : N), "gemm_tile: output columns");
+  // fp8 MX activations: e8m0 scale per (row, 128-column block), layout of gemm_tile.hip mx_off
+  const int64_t nb = (M + 63) / 64;
+  const uint8_t* amx = nullptr;
+  uint8_t* omx = nullptr;
+  if (a_mx.has_value()) {
+    CHECK_IN(*a_mx);
+    TORCH_CHECK(precision == 1 && a_mx->element_size() == 1 && a_mx->numel() == (K / 128) * nb * 64,
+                "gemm_tile: a_mx = fp8 A's e8m0 scales [K / 128][ceil(M / 64) * 64]");
+    amx = static_cast<const uint8_t*>(a_mx->data_ptr());
+    precision = 3;
+  }
+  if (epilogue == 3) {
+    TORCH_CHECK(precision == 1 && splits == 1 && out_mx.has_value(),
+                "gemm_tile: epilogue 3 needs fp8 operands with per-row scales, splits 1, out_mx");
+    CHECK_IN(*out_mx);
+    TORCH_CHECK(out_mx->element_size() == 1 && out_mx->numel() == (N / 2 / 128) * nb * 64,
+                "gemm_tile: out_mx = [N / 256][ceil(M / 64) * 64] bytes");
+    omx = static_cast<uint8_t*>(out_mx->data_ptr());
+  }
   TORCH_CHECK(epilogue != 1 || splits > 1, "gemm_tile: epilogue 1 (partials only) needs splits > 1");
   const int64_t kt = K * a.element_size() / 128;
   TORCH_CHECK(M >= 1 && M <= (1 << 20) && N % 256 == 0 && (K * a.element_size()) % 128 == 0 && K > 0,
@@ -542,11 +565,16 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
   const float* sa = nullptr;
   const float* sb = nullptr;
   if (fp8) {
-    TORCH_CHECK(a_scale.has_value() && b_scale.has_value(), "gemm_tile: 8-bit needs a_scale, b_scale");
-    CHECK_IN(*a_scale); CHECK_IN(*b_scale); CHECK_F32(*a_scale); CHECK_F32(*b_scale);
-    TORCH_CHECK(a_scale->numel() == M && b_scale->numel() == N, "gemm_tile: scale sizes");
-    sa = a_scale->data_ptr<float>();
+    TORCH_CHECK((a_scale.has_value() || precision == 3) && b_scale.has_value(),
+                "gemm_tile: 8-bit needs a_scale (or a_mx) and b_scale");
+    CHECK_IN(*b_scale); CHECK_F32(*b_scale);
+    TORCH_CHECK(b_scale->numel() == N, "gemm_tile: scale sizes");
     sb = b_scale->data_ptr<float>();
+    if (precision != 3) {
+      CHECK_IN(*a_scale); CHECK_F32(*a_scale);
+      TORCH_CHECK(a_scale->numel() == M, "gemm_tile: scale sizes");
+      sa = a_scale->data_ptr<float>();
+    }
   }
   float* ws = nullptr;
   if (splits == 0) {
@@ -582,7 +610,7 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
   const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
   check_rc(dli::launch_gemm_tile(out.data_ptr(), a.data_ptr(), b.data_ptr(), sa, sb, ws, (int)M,
                                  (int)N, (int)K, (int)splits, (int)epilogue, precision, cur_stream(),
-                                 xo, wo, J),
+                                 xo, wo, J, amx, omx),
            "gemm_tile");
 }
 
@@ -644,7 +672,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
         py::arg("epilogue") = 0, py::arg("workspace") = py::none(),
         py::arg("a_scale") = py::none(), py::arg("b_scale") = py::none(),
-        py::arg("x_out") = py::none(), py::arg("w_out") = py::none());
+        py::arg("x_out") = py::none(), py::arg("w_out") = py::none(),
+        py::arg("a_mx") = py::none(), py::arg("out_mx") = py::none());
   m.def("rms_norm_splitk", &rms_norm_splitk, "residual add + RMSNorm over un-reduced split-K partials",
         py::arg("out"), py::arg("parts"), py::arg("residual"), py::arg("w"), py::arg("eps"),
         py::arg("residual_out") = py::none());

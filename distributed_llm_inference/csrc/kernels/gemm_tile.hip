@@ -41,7 +41,14 @@
 //   * epilogues: bf16 store, fp32 split-K slab (summed by `splitk_reduce`), or fused SwiGLU:
 //     with B's rows interleaved by `swiglu_interleave` (gate and up rows of the same output
 //     column land in n-fragments 2p and 2p+1 of one wave) the wave holds gate and up of an output
-//     element in the same lane and register, and stores silu(gate) * up directly.
+//     element in the same lane and register, and stores silu(gate) * up directly;
+//   * fp8 MX activations (kSwiGLUMx -> kFp8Mx): the fp8 gate|up SwiGLU epilogue quantises its
+//     output itself, with one power-of-two (e8m0) scale per (row, 128-column block) — a block is
+//     exactly one workgroup's 128 output columns, so the amax needs only an LDS reduction over its
+//     4 n-waves — and the down projection feeds those scales to the block-scaled MFMA's per-lane
+//     scale operand (each lane scales the 32 K-values it holds, opsel picks the byte), since a
+//     128-column block is exactly one of its k-tiles.  That removes the separate per-row
+//     quantisation pass over h and halves the epilogue's store bytes (fp8 instead of bf16).
 #include "kernels.h"
 
 namespace dli {
@@ -53,7 +60,7 @@ constexpr int kHalf = 128 * 128;       // bytes of one half-tile (128 rows x 64 
 constexpr int kBuf = 4 * kHalf;        // A0 A1 B0 B1
 constexpr int kLds = 2 * kBuf;         // double buffer: 128 KB
 
-enum Epilogue { kStoreBf16 = 0, kStoreF32 = 1, kSwiGLU = 2 };
+enum Epilogue { kStoreBf16 = 0, kStoreF32 = 1, kSwiGLU = 2, kSwiGLUMx = 3 };
 
 // stream-K workspace header: flags [0, kSkMaxWgs), error counter at kSkErrWord, slabs after
 constexpr int kSkMaxWgs = 1020, kSkErrWord = 1023, kSkHeaderFloats = 1024;
@@ -101,7 +108,35 @@ __device__ __forceinline__ f32x4 mfma_i8(const bf16x8& a, const bf16x8& b, const
       __builtin_bit_cast(i32x4_t, c), 0, 0, 0));
 }
 
-enum Prec { kBf16 = 0, kFp8 = 1, kInt8 = 2 };
+enum Prec { kBf16 = 0, kFp8 = 1, kInt8 = 2, kFp8Mx = 3 };
+
+// fp8 x fp8 with per-lane e8m0 scales on the activation operand: lane l's byte SEL of `sc` scales
+// the 32 K-values it holds (row l & 15, K-block l >> 4) — mx_scale_probe.hip pins that mapping
+template <int SEL>
+__device__ __forceinline__ f32x4 mfma_fp8_mx(const bf16x8& a0, const bf16x8& a1, const bf16x8& b0,
+                                             const bf16x8& b1, const f32x4& c, int sc) {
+  typedef int i32x4_t __attribute__((ext_vector_type(4)));
+  const i32x4_t al = __builtin_bit_cast(i32x4_t, a0), ah = __builtin_bit_cast(i32x4_t, a1);
+  const i32x4_t bl = __builtin_bit_cast(i32x4_t, b0), bh = __builtin_bit_cast(i32x4_t, b1);
+  const i32x8 a = {al[0], al[1], al[2], al[3], ah[0], ah[1], ah[2], ah[3]};
+  const i32x8 b = {bl[0], bl[1], bl[2], bl[3], bh[0], bh[1], bh[2], bh[3]};
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, SEL, sc);
+}
+
+// e8m0 activation scales (MX): byte of (row r, k-tile kt) at ((kt * nb + r / 64) * 64 +
+// (r % 16) * 4 + (r % 64) / 16), nb = ceil(M / 64): a lane's 4 rows r0 + 16 i (i = 0..3) of one
+// 64-row block are one dword
+__device__ __forceinline__ size_t mx_off(int kt, int r, int nb) {
+  return ((size_t)kt * nb + (r >> 6)) * 64 + (r & 15) * 4 + ((r & 63) >> 4);
+}
+constexpr int kMxMaxKt = 64;             // k-tiles of scales a kFp8Mx workgroup keeps in LDS
+constexpr int kMxLds = kMxMaxKt * 256;   // [k-tile][256 tile rows] bytes
+
+struct MxArgs {
+  const uint8_t* a_sc;   // kFp8Mx: the A operand's scales (mx_off layout)
+  uint8_t* out_sc;       // kSwiGLUMx: scales of the quantised output (mx_off layout, kt = n-tile)
+  int nb;                // ceil(M / 64)
+};
 
 // Stream-K tail (splits == 1, bf16 / SwiGLU epilogues).  With more tiles than CUs the last wave
 // of whole tiles leaves CUs idle (Llama-3-70B gate|up at M = 512: 448 tiles = 1.75 waves on 256
@@ -151,14 +186,15 @@ __global__ void __launch_bounds__(kThreads, 1)
 gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __restrict__ C,
                  const float* __restrict__ a_scale, const float* __restrict__ b_scale,
                  int M, int N, int K, int tiles_m, int tiles_n, int k_tiles_per_split, SkArgs sk,
-                 OutlierArgs ol) {
-  constexpr bool FP8 = PREC == kFp8;
+                 OutlierArgs ol, MxArgs mx) {
+  constexpr bool MX = PREC == kFp8Mx;
+  constexpr bool FP8 = PREC == kFp8 || MX;
   constexpr bool BYTES = PREC != kBf16;   // 1-byte operands
   const char* A = reinterpret_cast<const char*>(Av);
   const char* B = reinterpret_cast<const char*>(Bv);
   const size_t Kb = (size_t)K * (BYTES ? 1 : 2);   // row stride in bytes
   const int kt_all = (int)(Kb / 128);              // k-tiles of a whole tile
-  __shared__ __attribute__((aligned(1024))) char smem[kLds];
+  __shared__ __attribute__((aligned(1024))) char smem[kLds + (MX ? kMxLds : 0)];
 
   const int tid0 = threadIdx.x;
 #ifdef DLI_GEMM_STAMPS
@@ -263,12 +299,17 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     bf16x8 af[4][2], b0[2][2], b1[2][2];
+    int s_mx[2] = {0, 0};   // kFp8Mx: this lane's 4 row scales of A-half 0 / 1, current k-tile
+    const char* sls = smem + kLds;   // kFp8Mx: [k-tile][256 rows] e8m0 scales
+    int mx_t = 0;                    // kFp8Mx: k-tile (within this split) read_a is reading
     auto read_a = [&](const char* buf, int h) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
           af[i][kk] = *reinterpret_cast<const bf16x8*>(buf + h * kHalf + a_lane + i * 16 * 128 + sch[kk]);
+      if constexpr (MX)
+        s_mx[h] = *reinterpret_cast<const int*>(sls + mx_t * 256 + wr * 128 + h * 64 + fr * 4);
     };
     auto read_b = [&](const char* buf, int h, bf16x8 (&bf)[2][2]) {
 #pragma unroll
@@ -282,7 +323,21 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
       // static priority for the lagging group or none; triple-buffering the weight half-tiles
       // (160 KB LDS, twice the DMA lead) buys nothing (profiles/gemm_variants_ab.txt)
       __builtin_amdgcn_s_setprio(1);
-      if (FP8) {
+      if constexpr (MX) {
+        // per-lane e8m0 activation scales: byte i of the half's dword = row block i
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int sc = s_mx[mq];
+          acc[mq * 4 + 0][nq * 2 + j] = mfma_fp8_mx<0>(bf[j][0], bf[j][1], af[0][0], af[0][1], acc[mq * 4 + 0][nq * 2 + j], sc);
+          acc[mq * 4 + 1][nq * 2 + j] = mfma_fp8_mx<1>(bf[j][0], bf[j][1], af[1][0], af[1][1], acc[mq * 4 + 1][nq * 2 + j], sc);
+          acc[mq * 4 + 2][nq * 2 + j] = mfma_fp8_mx<2>(bf[j][0], bf[j][1], af[2][0], af[2][1], acc[mq * 4 + 2][nq * 2 + j], sc);
+          acc[mq * 4 + 3][nq * 2 + j] = mfma_fp8_mx<3>(bf[j][0], bf[j][1], af[3][0], af[3][1], acc[mq * 4 + 3][nq * 2 + j], sc);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[mq * 4 + i][nq * 2 + j]));
+      } else if (FP8) {
         // one K=128 MFMA per fragment pair: the two 16-B chunks (g, g+4) of the 128-B k-tile row
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -318,6 +373,18 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
       __builtin_amdgcn_s_setprio(0);
     };
 
+    if constexpr (MX) {
+      // this split's activation scales -> LDS, before any LDS-DMA is in flight (plain loads):
+      // k-tile t, 64-row block w >> 2 of the tile (clamped: rows past M are never stored)
+      for (int u = tid; u < T * 16; u += kThreads) {
+        const int t = u >> 4, w = u & 15;
+        const int blk = min((m0 >> 6) + (w >> 2), mx.nb - 1);
+        const uint4 v = *reinterpret_cast<const uint4*>(
+            mx.a_sc + ((size_t)(kt0 + t) * mx.nb + blk) * 64 + (w & 3) * 16);
+        *reinterpret_cast<uint4*>(smem + kLds + t * 256 + w * 16) = v;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     // ---- prologue: tile 0 complete, three halves of tile 1 in flight ----
     // (LDS is free here: every wave passed the realigning barrier after its last ds_read)
     if (T > 0) {
@@ -336,6 +403,7 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
     if (wr == 1) barrier();
     for (int t = 0; t < T; ++t) {
       const char* buf = smem + (t & 1) * kBuf;
+      mx_t = t;
       const bool more1 = t + 1 < T, more2 = t + 2 < T;
       // phase 0: quadrant (0, 0)
       read_a(buf, 0);
@@ -450,7 +518,7 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
     if (BYTES) {  // dequantise: per-row activation scale x per-output-channel weight scale
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float sa = a_scale[min(crow + i * 16, M - 1)];
+        const float sa = MX ? 1.f : a_scale[min(crow + i * 16, M - 1)];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const f32x4 sb = *reinterpret_cast<const f32x4*>(b_scale + n0 + wc * 64 + j * 16 + cq);
@@ -485,7 +553,60 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
         }
       }
     }
-    if (EPI == kSwiGLU) {
+    if constexpr (EPI == kSwiGLUMx) {
+      // h = silu(gate) * up rounded to bf16 (what the bf16 epilogue stores), kept in the gate
+      // fragments; amax per row over the wave's 32 columns (shuffles), then over the 4 n-waves
+      // of the workgroup = the row's 128-column block (LDS; free: every wave is past the loop)
+      float* red = reinterpret_cast<float*>(smem);   // [wr][wc][128 rows]
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float a = 0.f;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float g = (float)(bf16)acc[i][2 * p][e];
+            const float u = (float)(bf16)acc[i][2 * p + 1][e];
+            const float h = (float)(bf16)(silu(g) * u);
+            acc[i][2 * p][e] = h;
+            a = fmaxf(a, fabsf(h));
+          }
+        a = fmaxf(a, __shfl_xor(a, 16, 64));
+        a = fmaxf(a, __shfl_xor(a, 32, 64));
+        if (lane < 16) red[(wr * 4 + wc) * 128 + i * 16 + fr] = a;
+      }
+      __syncthreads();
+      uint8_t* out = reinterpret_cast<uint8_t*>(C);
+      const int I = N >> 1;
+      const int tn = n0 / kTN;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = crow + i * 16;
+        float a = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) a = fmaxf(a, red[(wr * 4 + w) * 128 + i * 16 + fr]);
+        // the smallest 2^k with amax / 2^k <= 448 (e4m3's largest finite value)
+        int k = 0;
+        if (a > 0.f) {
+          const unsigned bits = __float_as_uint(a / 448.f);
+          k = (int)((bits >> 23) & 0xff) - 127 + ((bits & 0x7fffff) ? 1 : 0);
+          k = min(max(k, -126), 126);
+        }
+        const float inv = __uint_as_float((unsigned)(127 - k) << 23);   // 2^-k, exact
+        if (row < M) {
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const f32x4 v = acc[i][2 * p] * inv;
+            *reinterpret_cast<unsigned*>(out + (size_t)row * I + (n0 >> 1) + wc * 32 + p * 16 + cq) =
+                pack4_fp8(v[0], v[1], v[2], v[3]);
+          }
+        }
+        // one byte per (row, block); rows in [M, 64 nb) get 2^0 so the consumer's dword loads
+        // never read an unwritten scale
+        if (wc == 0 && lane < 16 && row < mx.nb * 64)
+          mx.out_sc[mx_off(tn, row, mx.nb)] = (uint8_t)(row < M ? k + 127 : 127);
+      }
+    } else if (EPI == kSwiGLU) {
       // n-fragments (2p, 2p+1) = (gate, up) of output columns n0/2 + wc*32 + p*16 + cq + e
       bf16* out = reinterpret_cast<bf16*>(C);
       const int I = N >> 1;
@@ -579,12 +700,16 @@ int device_cus() {
 template <int PREC>
 int launch_tile(void* C, const void* A, const void* B, const float* sa, const float* sb,
                 float* workspace, int M, int N, int K, int splits, int epilogue,
-                hipStream_t stream, OutlierArgs ol) {
+                hipStream_t stream, OutlierArgs ol, MxArgs mx) {
   constexpr int esz = PREC == kBf16 ? 2 : 1;
   const int kt = (int)((size_t)K * esz / 128);
   if (M <= 0 || N % kTN != 0 || (size_t)K * esz % 128 != 0 || splits < 0) return -1;
   if (splits > kt) return -2;
-  if (PREC != kBf16 && (sa == nullptr || sb == nullptr)) return -5;
+  if (PREC != kBf16 && ((sa == nullptr && PREC != kFp8Mx) || sb == nullptr)) return -5;
+  if (PREC == kFp8Mx && (mx.a_sc == nullptr || mx.nb != (M + 63) / 64)) return -13;
+  if (epilogue == kSwiGLUMx && (PREC != kFp8 || mx.out_sc == nullptr || mx.nb != (M + 63) / 64 ||
+                                splits != 1))
+    return -14;
   const int tiles_m = (M + kTM - 1) / kTM, tiles_n = N / kTN;
   const int tiles = tiles_m * tiles_n;
   SkArgs sk{0, 0, nullptr, nullptr, nullptr};
@@ -606,16 +731,17 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
     const int grid = sk.n_dp + sk.sk_wgs;
     if (epilogue == kSwiGLU)
       gemm_tile_kernel<kSwiGLU, PREC, true><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
-                                                                          tiles_m, tiles_n, kt, sk, ol);
+                                                                          tiles_m, tiles_n, kt, sk, ol, mx);
     else if (epilogue == kStoreBf16)
       gemm_tile_kernel<kStoreBf16, PREC, true><<<grid, kThreads, 0, stream>>>(
-          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kt, sk, ol);
+          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kt, sk, ol, mx);
     else
       return -4;
     return 0;
   }
   const int kps = (kt + splits - 1) / splits;
   if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
+  if (PREC == kFp8Mx && kps > kMxMaxKt) return -15;   // its scales must fit the LDS slot
   // kStoreF32 with splits > 1: partials only, the consumer reduces them (rms_norm_splitk)
   if (splits > 1 && (workspace == nullptr || epilogue == kSwiGLU)) return -3;
   if (splits == 1 && epilogue == kStoreF32) return -3;
@@ -623,19 +749,25 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
   sk.n_dp = grid;
   if (splits > 1) {
     gemm_tile_kernel<kStoreF32, PREC, false><<<grid, kThreads, 0, stream>>>(
-        A, B, workspace, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol);
+        A, B, workspace, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
     if (epilogue == kStoreF32) return 0;
     const size_t MN = (size_t)M * N;
     size_t blocks = (MN / 8 + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     tile_splitk_reduce_kernel<<<(int)blocks, 256, 0, stream>>>(reinterpret_cast<bf16*>(C),
                                                                workspace, splits, MN);
+  } else if (epilogue == kSwiGLUMx) {
+    if constexpr (PREC == kFp8)
+      gemm_tile_kernel<kSwiGLUMx, PREC, false><<<grid, kThreads, 0, stream>>>(
+          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
   } else if (epilogue == kSwiGLU) {
-    gemm_tile_kernel<kSwiGLU, PREC, false><<<grid, kThreads, 0, stream>>>(A, B, C, sa, sb, M, N, K,
-                                                                         tiles_m, tiles_n, kps, sk, ol);
+    if constexpr (PREC == kFp8Mx) return -4;   // MX activations come from the SwiGLU epilogue
+    else
+      gemm_tile_kernel<kSwiGLU, PREC, false><<<grid, kThreads, 0, stream>>>(
+          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
   } else if (epilogue == kStoreBf16) {
     gemm_tile_kernel<kStoreBf16, PREC, false><<<grid, kThreads, 0, stream>>>(
-        A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol);
+        A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
   } else {
     return -4;
   }
@@ -661,19 +793,23 @@ long long gemm_tile_sk_workspace_floats() {
 int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale,
                      const float* b_scale, float* workspace, int M, int N, int K, int splits,
                      int epilogue, int precision, hipStream_t stream, const bf16* x_out,
-                     const bf16* w_out, int J) {
+                     const bf16* w_out, int J, const uint8_t* a_mx, uint8_t* out_mx) {
   if (J < 0 || J % 32 != 0 || (J > 0 && (precision != kInt8 || !x_out || !w_out))) return -12;
   const OutlierArgs ol{x_out, w_out, J};
+  const MxArgs mx{a_mx, out_mx, (M + 63) / 64};
   switch (precision) {
     case kBf16:
       return launch_tile<kBf16>(C, A, B, nullptr, nullptr, workspace, M, N, K, splits, epilogue,
-                                stream, ol);
+                                stream, ol, mx);
     case kFp8:
       return launch_tile<kFp8>(C, A, B, a_scale, b_scale, workspace, M, N, K, splits, epilogue,
-                               stream, ol);
+                               stream, ol, mx);
+    case kFp8Mx:
+      return launch_tile<kFp8Mx>(C, A, B, a_scale, b_scale, workspace, M, N, K, splits, epilogue,
+                                 stream, ol, mx);
     case kInt8:
       return launch_tile<kInt8>(C, A, B, a_scale, b_scale, workspace, M, N, K, splits, epilogue,
-                                stream, ol);
+                                stream, ol, mx);
   }
   return -6;
 }

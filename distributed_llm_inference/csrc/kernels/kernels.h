@@ -82,7 +82,8 @@ int launch_sample(const SampleParams& p, int B, hipStream_t stream);
 int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale,
                      const float* b_scale, float* workspace, int M, int N, int K, int splits,
                      int epilogue, int precision, hipStream_t stream,
-                     const bf16* x_out = nullptr, const bf16* w_out = nullptr, int J = 0);
+                     const bf16* x_out = nullptr, const bf16* w_out = nullptr, int J = 0,
+                     const uint8_t* a_mx = nullptr, uint8_t* out_mx = nullptr);
 // C[MN] (bf16) = sum over `splits` fp32 partial products parts[splits][MN]
 int launch_splitk_reduce(bf16* C, const float* parts, int splits, size_t MN, hipStream_t stream);
 // fp32 elements of the workspace gemm_tile needs for splits == 0 (stream-K tail) on this device

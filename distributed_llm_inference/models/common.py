@@ -106,6 +106,16 @@ class Linear(nn.Module):
             if sp:  # decode micro-batches: 256x256 MFMA tile kernel (csrc/kernels/gemm_tile.hip)
                 return ops.gemm_tile(x, self.weight, splits=sp, defer_reduce=defer_reduce)
             return F.linear(x, self.weight, self.bias)
+        if isinstance(x_q, ops.MxFp8):
+            # MX activations from the fp8 SwiGLU epilogue: their e8m0 block scales go to the
+            # block-scaled MFMA (gemm_tile.hip kFp8Mx); the MLP only hands these over when the
+            # product is tileable (LlamaMLP.forward)
+            sp = ops.tile_gemm_splits_fp8(x_q.q.shape[0], self.out_features, self.in_features)
+            y = ops.gemm_tile_fp8_mx(x_q, self.weight_fp8, self.weight_scale, sp or 1,
+                                     defer_reduce=defer_reduce and self.bias is None)
+            if self.bias is not None:
+                y = y + self.bias
+            return y
         if x_q is None:
             x_q = ops.quant_rowwise(x)
         xq, xs = x_q

@@ -156,6 +156,15 @@ class LlamaMLP(nn.Module):
             xq, xs = x_q if x_q is not None else ops.quant_rowwise(normed)
             if xq.is_cuda and ops.tile_gemm_splits_fp8(xq.shape[0], gp.out_features,
                                                         gp.in_features):
+                dp = self.down_proj
+                dsp = ops.tile_gemm_splits_fp8(xq.shape[0], dp.out_features, dp.in_features)
+                if ops.fp8_mx() and dsp and dp.bias is None and ops.mx_tileable(dp.in_features, dsp):
+                    # SwiGLU output quantised in the epilogue with per-(row, 128-column) e8m0
+                    # scales, consumed by the down projection's block-scaled MFMA: no bf16 h,
+                    # no per-row quantisation pass
+                    h = ops.gemm_tile_fp8(xq, xs, gp.weight_fp8, gp.weight_scale, swiglu=True,
+                                          mx_out=True)
+                    return dp(None, x_q=h, defer_reduce=defer_reduce)
                 # fp8 gate|up on the block-scaled tile kernel, SwiGLU in its epilogue (bf16 out;
                 # down_proj quantises it: one [M, I] pass instead of silu_mul_quant's [M, 2I])
                 h = ops.gemm_tile_fp8(xq, xs, gp.weight_fp8, gp.weight_scale, swiglu=True)

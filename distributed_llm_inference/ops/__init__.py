@@ -606,12 +606,26 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
 
 def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
                   splits: int = 1, swiglu: bool = False, out: Optional[torch.Tensor] = None,
-                  workspace: Optional[torch.Tensor] = None, defer_reduce: bool = False):
+                  workspace: Optional[torch.Tensor] = None, defer_reduce: bool = False,
+                  mx_out: bool = False):
     """fp8 e4m3 tile GEMM: ``(xq [M, K] @ wq[N, K]^T) * xs[M] * ws[N]`` -> bf16, on the
     block-scaled K=128 MFMA (2x the bf16 MFMA rate; unit block scales, per-row / per-channel
     scales applied in the epilogue).  ``swiglu``: ``wq`` / ``ws`` rows in swiglu_interleave order.
-    ``defer_reduce`` (split-K): return :class:`SplitKPartials` (scaled fp32 partials)."""
+    ``defer_reduce`` (split-K): return :class:`SplitKPartials` (scaled fp32 partials).
+    ``mx_out`` (with ``swiglu``): return the SwiGLU output as :class:`MxFp8`, quantised in the
+    epilogue (needs N % 256 == 0)."""
     M, N = xq.shape[0], wq.shape[0]
+    if mx_out:
+        if not swiglu:
+            raise ValueError("gemm_tile_fp8: mx_out is an output of the SwiGLU epilogue")
+        if not _gpu(xq):
+            return mx_quantize(gemm_tile_fp8(xq, xs, wq, ws, swiglu=True))
+        I = N // 2
+        q = torch.empty(M, I, dtype=torch.float8_e4m3fn, device=xq.device)
+        sc = torch.empty(I // 128 * ((M + 63) // 64) * 64, dtype=torch.uint8, device=xq.device)
+        native().gemm_tile(q, xq, wq, 1, 3, None, xs.reshape(-1).contiguous(),
+                           ws.reshape(-1).contiguous(), out_mx=sc)
+        return MxFp8(q, sc)
     if (defer_reduce and splits > 1 and _gpu(xq) and not swiglu
             and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
         parts = torch.empty(splits, M, N, dtype=torch.float32, device=xq.device)
@@ -631,6 +645,95 @@ def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torc
         workspace = torch.empty(splits * M * N, dtype=torch.float32, device=xq.device)
     native().gemm_tile(out, xq, wq, int(splits), 2 if swiglu else 0, workspace,
                        xs.reshape(-1).contiguous(), ws.reshape(-1).contiguous())
+    return out
+
+
+class MxFp8:
+    """fp8 e4m3 activations with one power-of-two (e8m0) scale per (row, 128-column block), as
+    the fp8 gate|up tile GEMM's SwiGLU epilogue writes them (gemm_tile.hip kSwiGLUMx) and the down
+    projection consumes them on the block-scaled MFMA's per-lane scale operand (kFp8Mx).
+    ``sc`` is uint8 in gemm_tile.hip's ``mx_off`` layout: byte of (row r, block kt) at
+    ``(kt * nb + r // 64) * 64 + (r % 16) * 4 + (r % 64) // 16``, ``nb = ceil(M / 64)``."""
+
+    __slots__ = ("q", "sc")
+
+    def __init__(self, q: torch.Tensor, sc: torch.Tensor):
+        self.q, self.sc = q, sc
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    def exponents(self) -> torch.Tensor:
+        """int32 [M, K / 128]: the scale exponents (value = q * 2 ** e)."""
+        M, K = self.q.shape
+        nb = (M + 63) // 64
+        r = torch.arange(M, device=self.sc.device)
+        idx = (r // 64) * 64 + (r % 16) * 4 + (r % 64) // 16
+        return self.sc.view(K // 128, nb * 64)[:, idx].t().to(torch.int32) - 127
+
+    def dequantize(self) -> torch.Tensor:
+        e = self.exponents().float()
+        return self.q.float() * torch.exp2(e).repeat_interleave(128, dim=1)
+
+
+def mx_quantize(h: torch.Tensor) -> MxFp8:
+    """Reference MX quantiser (same rule as the kSwiGLUMx epilogue): per (row, 128-column block)
+    the smallest 2^k with amax / 2^k <= 448, q = e4m3(h / 2^k)."""
+    M, K = h.shape
+    nb = (M + 63) // 64
+    hf = h.float().view(M, K // 128, 128)
+    am = hf.abs().amax(-1)
+    ratio = am / 448.0
+    m, e = torch.frexp(ratio)                       # ratio = m * 2^e, m in [0.5, 1)
+    k = torch.where(m == 0.5, e - 1, e)             # exact powers of two: 2^(e-1) == ratio
+    k = torch.where(am > 0, k, torch.zeros_like(k)).clamp(-126, 126)
+    q = (hf * torch.exp2(-k.float())[..., None]).clamp(-448, 448).view(M, K).to(torch.float8_e4m3fn)
+    sc = torch.full((K // 128, nb * 64), 127, dtype=torch.uint8, device=h.device)
+    r = torch.arange(M, device=h.device)
+    idx = (r // 64) * 64 + (r % 16) * 4 + (r % 64) // 16
+    sc[:, idx] = (k + 127).to(torch.uint8).t()
+    return MxFp8(q, sc.view(-1))
+
+
+def fp8_mx() -> bool:
+    """``DLI_FP8_MX=1`` (default): the fp8 gate|up tile GEMM hands its SwiGLU output to the down
+    projection as :class:`MxFp8` (no separate per-row quantisation pass over h); ``0`` keeps the
+    bf16 h + per-row quantiser path."""
+    return os.environ.get("DLI_FP8_MX", "1") != "0"
+
+
+MX_MAX_KTILES = 64   # k-tiles of scales one kFp8Mx workgroup keeps in LDS (gemm_tile.hip kMxMaxKt)
+
+
+def mx_tileable(K: int, splits: int) -> bool:
+    """Whether a kFp8Mx tile GEMM over K with this split count fits its LDS scale slot."""
+    kt = K // 128
+    return splits >= 1 and K % 128 == 0 and -(-kt // splits) <= MX_MAX_KTILES
+
+
+def gemm_tile_fp8_mx(a: MxFp8, wq: torch.Tensor, ws: torch.Tensor, splits: int = 1,
+                     defer_reduce: bool = False):
+    """fp8 tile GEMM on MX activations: ``(q * 2^e) @ (wq * ws)^T`` with the e8m0 scales applied
+    by the MFMA itself (kFp8Mx); bf16 out, or :class:`SplitKPartials` when deferring."""
+    xq = a.q
+    M, N = xq.shape[0], wq.shape[0]
+    if not _gpu(xq):
+        y = a.dequantize() @ (wq.float() * ws.reshape(-1, 1).float()).t()
+        return y.to(torch.bfloat16)
+    if not mx_tileable(xq.shape[1], splits):
+        raise ValueError(f"gemm_tile_fp8_mx: K={xq.shape[1]} with {splits} splits exceeds the "
+                         f"{MX_MAX_KTILES}-k-tile scale slot")
+    ws = ws.reshape(-1).contiguous()
+    if defer_reduce and splits > 1 and os.environ.get("DLI_SPLITK_DEFER", "1") == "1":
+        parts = torch.empty(splits, M, N, dtype=torch.float32, device=xq.device)
+        dummy = torch.empty(M, 0, dtype=torch.bfloat16, device=xq.device)   # C is unused
+        native().gemm_tile(dummy, xq, wq, int(splits), 1, parts.view(-1), None, ws, a_mx=a.sc)
+        return SplitKPartials(parts)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=xq.device)
+    workspace = (torch.empty(splits * M * N, dtype=torch.float32, device=xq.device)
+                 if splits > 1 else None)
+    native().gemm_tile(out, xq, wq, int(splits), 0, workspace, None, ws, a_mx=a.sc)
     return out
 
 

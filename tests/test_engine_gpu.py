@@ -3,6 +3,7 @@ eager, in-process PP=2/4 vs PP=1, attention-sink window mode, fp8 weights."""
 import pytest
 import torch
 
+from distributed_llm_inference import ops
 from distributed_llm_inference.config import CacheConfig, ModelSpec, ServeConfig
 from distributed_llm_inference.models import CausalLMStage
 from distributed_llm_inference.runtime.engine import EngineConfig, LLMEngine
@@ -186,6 +187,56 @@ def test_fp8_tile_path_fused_swiglu_matches_cpu(gpu, monkeypatch):
     g.block.set_fused_swiglu(False)   # round trip restores the quantised rows exactly
     assert torch.equal(g.block.layers[0].mlp.gate_up_proj.weight_fp8.view(torch.uint8),
                        wq0.view(torch.uint8))
+
+
+def test_fp8_mx_down_projection_engages_and_matches_per_row_path(gpu, monkeypatch):
+    """fp8 decode with the SwiGLU output handed to the down projection as MX (e8m0 per row and
+    128-column block, quantised in the gate|up epilogue) vs the bf16 h + per-row quantiser path
+    (DLI_FP8_MX=0): the MX kernels run for every layer, and against the bf16-weight logits the MX
+    path is no less accurate than the per-row one."""
+    monkeypatch.setenv("DLI_FP8_TILE", "all")
+    spec = SPEC.replace(hidden_size=512, intermediate_size=1024, num_heads=8, num_kv_heads=2,
+                        head_dim=64)
+    prompts = [[(5 * i + j) % 991 + 1 for j in range(4)] for i in range(256)]
+    g = CausalLMStage(spec, 0, 3, device=gpu).init_random(6)
+    calls = []
+    real = ops.gemm_tile_fp8_mx
+
+    def counted(*a, **k):
+        calls.append(1)
+        return real(*a, **k)
+    monkeypatch.setattr(ops, "gemm_tile_fp8_mx", counted)
+
+    def decode(stage):
+        pool = stage.make_pool(256, block_size=64)
+        sids = list(range(len(prompts)))
+        for sid, p in zip(sids, prompts):
+            pool.manager.append(sid, len(p))
+        meta = pool.build_metadata(sids, [len(p) for p in prompts])
+        meta.logits_rows = (torch.cumsum(torch.tensor([len(p) for p in prompts]), 0) - 1).to(gpu)
+        ids = torch.tensor([t for p in prompts for t in p], dtype=torch.int32, device=gpu)
+        stage(ids, meta, pool)
+        for sid in sids:
+            pool.manager.append(sid, 1)
+        meta = pool.build_metadata(sids, [1] * len(sids))
+        toks = torch.tensor([(11 * i) % 991 + 1 for i in sids], dtype=torch.int32, device=gpu)
+        return stage(toks, meta, pool).float().cpu()
+
+    ref = decode(g)   # bf16 weights
+    g.quantize_fp8()
+    g.block.set_fused_swiglu(True)
+    monkeypatch.setenv("DLI_FP8_MX", "1")
+    a = decode(g)
+    n = len(calls)
+    assert n >= 3, calls   # at least one MX down projection per layer (the decode step)
+    monkeypatch.setenv("DLI_FP8_MX", "0")
+    b = decode(g)
+    assert len(calls) == n
+    # two fp8 quantisations of h differ by ~fp8 resolution; against the bf16 model the MX path
+    # (finer, per-block scales) is no worse than the per-row one
+    rel_mx = ((a - ref).norm() / ref.norm()).item()
+    rel_row = ((b - ref).norm() / ref.norm()).item()
+    assert rel_mx < 0.1 and rel_mx < 1.1 * rel_row + 0.005, (rel_mx, rel_row)
 
 
 def test_sampling_params_in_engine(gpu):

@@ -138,6 +138,57 @@ def test_gemm_tile_fp8_exact_integers_and_swiglu(gpu):
     assert (y - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
 
 
+# ------------------------------------------------------------------ fp8 MX activations (kSwiGLUMx -> kFp8Mx)
+@pytest.mark.parametrize("M", [512, 300, 64, 1])
+def test_gemm_tile_fp8_swiglu_mx_epilogue_matches_reference_quantiser(gpu, M):
+    # same main loop as the bf16-output SwiGLU epilogue: its h, quantised by the reference MX rule,
+    # must give the kernel's fp8 bytes and e8m0 scales bit for bit (pad rows of the last 64-row
+    # block carry scale 127)
+    torch.manual_seed(M)
+    K, I = 1024, 768
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    w = (torch.randn(2 * I, K, device=gpu) / 32 * torch.rand(2 * I, 1, device=gpu) * 4).to(torch.bfloat16)
+    xq, xs = ops.quant_rowwise(x)
+    wq, ws = ops.quantize_weight_fp8(w)
+    wqi = ops.swiglu_interleave(wq.view(torch.uint8)).view(wq.dtype)
+    wsi = ops.swiglu_interleave(ws.reshape(-1, 1)).reshape(-1)
+    h = ops.gemm_tile_fp8(xq, xs, wqi, wsi, swiglu=True)
+    a = ops.gemm_tile_fp8(xq, xs, wqi, wsi, swiglu=True, mx_out=True)
+    ref = ops.mx_quantize(h)
+    assert torch.equal(a.sc, ref.sc)
+    assert torch.equal(a.q.view(torch.uint8), ref.q.view(torch.uint8))
+    # and the MX representation stays within fp8 resolution of h
+    err = (a.dequantize() - h.float()).abs()
+    bmax = h.float().abs().view(M, -1, 128).amax(-1).repeat_interleave(128, 1)
+    assert (err <= h.float().abs() * 2 ** -4 + bmax * 2 ** -17).all()
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(512, 1024, 8192, 1), (512, 8192, 28672, 4),
+                                          (300, 512, 4096, 2), (77, 256, 1024, 1)])
+def test_gemm_tile_fp8_mx_matches_dequantised_fp32(gpu, M, N, K, splits):
+    torch.manual_seed(M + N + K)
+    # rows and 128-column blocks of very different magnitudes: per-block scales matter
+    h = (torch.randn(M, K, device=gpu) * torch.exp2(torch.randint(-6, 7, (M, K // 128), device=gpu)
+                                                    ).repeat_interleave(128, 1).float()).to(torch.bfloat16)
+    a = ops.mx_quantize(h)
+    w = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    wq, ws = ops.quantize_weight_fp8(w)
+    ref = a.dequantize() @ (wq.float() * ws.reshape(-1, 1)).t()
+    y = ops.gemm_tile_fp8_mx(a, wq, ws, splits).float()
+    assert (y - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
+    if splits > 1:
+        parts = ops.gemm_tile_fp8_mx(a, wq, ws, splits, defer_reduce=True)
+        assert isinstance(parts, ops.SplitKPartials)
+        assert (parts.parts.sum(0) - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
+
+
+def test_gemm_tile_fp8_mx_rejects_oversized_k_split(gpu):
+    a = ops.mx_quantize(torch.randn(256, 128 * 65, device=gpu).to(torch.bfloat16))
+    wq, ws = ops.quantize_weight_fp8(torch.randn(256, 128 * 65, device=gpu).to(torch.bfloat16))
+    with pytest.raises(ValueError):
+        ops.gemm_tile_fp8_mx(a, wq, ws, 1)
+
+
 # ------------------------------------------------------------------ LLM.int8 (int8 MFMA tile GEMM)
 def test_gemm_tile_int8_exact_and_random(gpu):
     xi = torch.zeros(256, 128, device=gpu)

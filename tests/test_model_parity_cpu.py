@@ -10,6 +10,7 @@ import math
 import pytest
 import torch
 
+from distributed_llm_inference import ops
 from distributed_llm_inference.config import ModelSpec
 from distributed_llm_inference.models import CausalLMStage
 from distributed_llm_inference.ops.reference import build_cos_sin
@@ -133,6 +134,35 @@ def test_fp8_stage_close_to_bf16_cpu():
     b = _run_stage(st, prompts, decode_steps=1)
     for x, y in zip(a, b):
         assert ((x - y).norm() / x.norm()).item() < 0.1
+
+
+def test_mx_fp8_quantiser_layout_and_linear_cpu():
+    """MX activations (fp8 + e8m0 per (row, 128-column block)): exponent layout, dequantisation
+    error, and the Linear path that consumes them (CPU reference of gemm_tile.hip kFp8Mx)."""
+    from distributed_llm_inference.models.common import Linear
+    torch.manual_seed(3)
+    M, K = 70, 384
+    mag = torch.exp2(torch.randint(-8, 9, (M, K // 128)).float()).repeat_interleave(128, 1)
+    h = (torch.randn(M, K) * mag).to(torch.bfloat16)
+    a = ops.mx_quantize(h)
+    nb = (M + 63) // 64
+    assert a.sc.numel() == (K // 128) * nb * 64 and a.q.dtype == torch.float8_e4m3fn
+    e = a.exponents()
+    am = h.float().abs().view(M, K // 128, 128).amax(-1)
+    # smallest power of two that brings every block under 448
+    assert ((am / torch.exp2(e.float())) <= 448).all()
+    assert ((am / torch.exp2(e.float() - 1)) > 448).all()
+    # byte of (row r, block kt) sits at (kt * nb + r // 64) * 64 + (r % 16) * 4 + (r % 64) // 16
+    r, kt = 37, 2
+    assert int(a.sc[(kt * nb + r // 64) * 64 + (r % 16) * 4 + (r % 64) // 16]) == int(e[r, kt]) + 127
+    err = (a.dequantize() - h.float()).abs()
+    assert (err <= h.float().abs() / 16 + am.repeat_interleave(128, 1) * 2 ** -17).all()
+    lin = Linear(K, 256)
+    torch.nn.init.normal_(lin.weight, std=0.05)
+    lin.quantize_fp8()
+    y = lin(None, x_q=a).float()
+    ref = a.dequantize() @ (lin.weight_fp8.float() * lin.weight_scale.reshape(-1, 1)).t()
+    assert (y - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
 
 
 def test_gpt2_matches_hf():
