@@ -70,7 +70,7 @@ static int check(const Shape& c) {
       CK(hipMalloc(&W0, (size_t)c.splits * M * N * 4));
       CK(hipMalloc(&W1, (size_t)c.splits * M * N * 4));
     }
-    int r0 = dli_old::launch_gemm_tile(C0, A, B, nullptr, nullptr, W0, M, N, K, c.splits, sk ? 1 : 0, 0, 0);
+    int r0 = dli_old::launch_gemm_tile(C0, A, B, nullptr, nullptr, W0, M, N, K, c.splits, sk ? 1 : 0, 0, 0, nullptr, nullptr, 0, nullptr, nullptr);
     int r1 = dli::launch_gemm_tile(C1, A, B, nullptr, nullptr, W1, M, N, K, c.splits, sk ? 1 : 0, 0, 0, 256);
     CK(hipDeviceSynchronize());
     if (r0 || r1) { printf("launch rc %d %d\n", r0, r1); return 1; }
@@ -122,7 +122,7 @@ int main(int argc, char** argv) {
     const int epi = c.splits > 1 ? 1 : c.epi;
     auto run = [&](int v, int i) {
       int rc = v == 0 ? dli_old::launch_gemm_tile(C, A, B[i % sets], nullptr, nullptr, ws, c.M, c.N,
-                                                  c.K, c.splits, epi, 0, 0)
+                                                  c.K, c.splits, epi, 0, 0, nullptr, nullptr, 0, nullptr, nullptr)
                       : dli::launch_gemm_tile(C, A, B[i % sets], nullptr, nullptr, ws, c.M, c.N, c.K,
                                               c.splits, epi, 0, 0, 256);
       if (rc) { fprintf(stderr, "rc %d\n", rc); exit(1); }
