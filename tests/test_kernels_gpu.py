@@ -371,10 +371,14 @@ def test_rope_cache_fp8(gpu, window):
     assert torch.equal(v1.cpu().view(torch.uint8), v2.view(torch.uint8))
 
 
-@pytest.mark.parametrize("splits", [1, 3])
-def test_attn_decode_fp8_kv(gpu, splits):
+@pytest.mark.parametrize("splits,D", [(1, 128), (3, 128), (4, 128), (8, 128), (12, 128),
+                                      (64, 128), (6, 128), (4, 64), (1, 64), (4, 32), (3, 32)])
+def test_attn_decode_fp8_kv(gpu, splits, D):
+    """fp8 KV decode through every split path (ungrouped 1 / 3, workgroup-merged 4 / 8, merged +
+    combined 12 / 64, pairs 6) with the head-dim-permuted 16-byte loads (D % 64 == 0) and the
+    8-byte path (D = 32)."""
     torch.manual_seed(12)
-    nh, nkv, D, bs, B = 64, 8, 128, 64, 5
+    nh, nkv, bs, B = 64, 8, 64, 5
     lens = torch.tensor([1, 33, 64, 257, 700], dtype=torch.int32)
     max_blocks = (int(lens.max()) + bs - 1) // bs
     nblocks = B * max_blocks
@@ -388,6 +392,31 @@ def test_attn_decode_fp8_kv(gpu, splits):
     out_r = ref.attn_decode(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, scale,
                             k_scale=ks, v_scale=vs)
     _close(out, out_r, 2e-2, 2e-2, "decode-fp8")
+
+
+@pytest.mark.parametrize("splits", [1, 4, 12])
+def test_attn_decode_fp8_kv_window_sinks(gpu, splits):
+    """fp8 KV in StreamingLLM window mode: the sink segment is scored with q_sink, which must
+    follow the same permuted head-dim map as q."""
+    torch.manual_seed(23)
+    nh, nkv, D, bs = 64, 8, 128, 64
+    n_sink, sink_pad, window = 4, 64, 512
+    ring = (window - n_sink + 31) // 32 * 32
+    lens = torch.tensor([3, 300, 513, 2000], dtype=torch.int32)
+    B = lens.numel()
+    max_blocks = (sink_pad + ring + bs - 1) // bs
+    nblocks = B * max_blocks
+    ks, vs = 0.5, 2.0
+    kc, vc = _make_cache_fp8(nblocks, nkv, bs, D, gpu, ks, vs)
+    bt = _tables(B, max_blocks, nblocks, gpu, seed=9)
+    q = torch.randn(B, nh, D, device=gpu, dtype=BF)
+    qs = torch.randn(B, nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    out = ops.attn_decode(q, qs, kc, vc, bt, lens.to(gpu), scale, n_sink, sink_pad, ring, window,
+                          num_splits=splits, k_scale=ks, v_scale=vs)
+    out_r = ref.attn_decode(q.cpu(), qs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), lens, scale, n_sink,
+                            sink_pad, ring, window, k_scale=ks, v_scale=vs)
+    _close(out, out_r, 2e-2, 2e-2, f"decode-fp8-window-s{splits}")
 
 
 def test_attn_prefill_fp8_kv(gpu):
