@@ -321,7 +321,7 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
 void attn_prefill(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, Tensor v_cache,
                   Tensor block_tables, Tensor seq_lens, Tensor q_start, int64_t max_q,
                   double scale, int64_t n_sink, int64_t sink_pad, int64_t ring, int64_t window,
-                  double k_scale, double v_scale, optional<Tensor> tile_map) {
+                  double k_scale, double v_scale, optional<Tensor> tile_map, int64_t qb) {
   int64_t D = 0;
   auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
                        sink_pad, ring, window, k_scale, v_scale, D);
@@ -335,6 +335,8 @@ void attn_prefill(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache,
     p.tile_map = tile_map->data_ptr<int>();
     p.n_tiles = (int)tile_map->size(0);
   }
+  TORCH_CHECK(qb == 1 || qb == 2, "attn_prefill: qb (query blocks per wave) must be 1 or 2");
+  p.prefill_qb = (int)qb;
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   check_rc(dli::launch_attn_prefill(p, (int)B, (int)max_q, (int)D, cur_stream()), "attn_prefill");
 }

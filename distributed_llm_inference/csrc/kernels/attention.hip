@@ -152,6 +152,9 @@ __device__ __forceinline__ void o_unit(const WaveState<D>& st, int u, int h4, in
 
 // One 32-key step of online-softmax attention for the 16 query columns held by this wave.
 // valid_mask bit j decides visibility of key 8h+j (h = lane>>4) for this lane's column.
+// (Skipping the O rescale when no running max moved, or a mask-free path for steps below the
+// diagonal, cut the prefill loop's VALU count but raised its VGPRs past 128: fewer workgroups
+// per CU, measured slower.)
 template <int D>
 __device__ __forceinline__ void attn_compute(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
                                              const KVFrag<D>& f, float scale_log2,
@@ -499,8 +502,13 @@ __device__ __forceinline__ int kswz(int row) {
   return ((row & 3) | (((row >> 3) & 3) << 2)) & (CH - 1);
 }
 
-template <int D, bool WIN, bool FP8>
-__global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw) {
+template <int D, bool WIN, bool FP8, int QB>
+__global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_kernel(AttnParams p, int hpw) {
+  // QB = 16-token query blocks per wave: every K / V fragment read from LDS feeds QB blocks'
+  // MFMAs.  Measured (profiles/attn_prefill_qb_ab.json): QB = 2 is +2 % on 2k-4k chunks and -25 %
+  // on 16-token ones, so QB = 1 is the default; what paid was occupancy — the 2-waves-per-SIMD
+  // bound lets the QB = 1 kernel settle at ~120 VGPRs (4 workgroups per CU instead of 2):
+  // 508 -> 633 TFLOP/s on a 4k causal chunk
   constexpr int CH = D / 8;            // 16-B units per K row
   constexpr int UNITS = 32 * CH;       // 16-B units per K tile (= per V^T tile)
   constexpr int UPT = (UNITS + 255) / 256;
@@ -538,24 +546,34 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw
   const int qh = h0 + (w % hpw);
   const int qs0 = p.q_start[b];
   const int qlen = p.q_start[b + 1] - qs0;
-  const int wg_tok0 = tile * 16 * tpw;
+  const int wg_tok0 = tile * 16 * tpw * QB;
   if (wg_tok0 >= qlen) return;  // whole workgroup idle (uniform: before any barrier)
-  const int tok0 = wg_tok0 + (w / hpw) * 16;
+  const int tok0 = wg_tok0 + (w / hpw) * 16 * QB;
   const int L = p.seq_lens[b];
-  const int tok = tok0 + col;
-  const bool col_valid = tok < qlen;
-  const int pq = L - qlen + (col_valid ? tok : qlen - 1);  // this column's absolute position
-  const int pq_max = L - qlen + min(qlen - 1, wg_tok0 + 16 * tpw - 1);  // workgroup's last token
+  int tok[QB], pq[QB];
+  bool col_valid[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) {
+    tok[qb] = tok0 + 16 * qb + col;
+    col_valid[qb] = tok[qb] < qlen;
+    pq[qb] = L - qlen + (col_valid[qb] ? tok[qb] : qlen - 1);  // the column's absolute position
+  }
+  const int pq_max = L - qlen + min(qlen - 1, wg_tok0 + 16 * tpw * QB - 1);  // workgroup's last token
   const int* bt = p.block_tables + (size_t)b * p.bt_stride;
   const size_t head_stride = (size_t)p.bs * D;
 
-  bf16x8 qf[D / 32], qsf[D / 32];
-  const size_t qoff = ((size_t)(qs0 + (col_valid ? tok : 0)) * p.nh + qh) * D;
+  bf16x8 qf[QB][D / 32], qsf[WIN ? QB : 1][D / 32];
 #pragma unroll
-  for (int c = 0; c < D / 32; ++c) {
-    qf[c] = col_valid ? *reinterpret_cast<const bf16x8*>(p.q + qoff + 32 * c + 8 * h4) : zero8();
-    qsf[c] = (WIN && p.n_sink > 0 && col_valid)
-                 ? *reinterpret_cast<const bf16x8*>(p.q_sink + qoff + 32 * c + 8 * h4) : zero8();
+  for (int qb = 0; qb < QB; ++qb) {
+    const size_t qoff = ((size_t)(qs0 + (col_valid[qb] ? tok[qb] : 0)) * p.nh + qh) * D;
+#pragma unroll
+    for (int c = 0; c < D / 32; ++c) {
+      qf[qb][c] = col_valid[qb] ? *reinterpret_cast<const bf16x8*>(p.q + qoff + 32 * c + 8 * h4)
+                                : zero8();
+      if constexpr (WIN)
+        qsf[qb][c] = (p.n_sink > 0 && col_valid[qb])
+                         ? *reinterpret_cast<const bf16x8*>(p.q_sink + qoff + 32 * c + 8 * h4) : zero8();
+    }
   }
 
   // virtual steps: [0, n_main) = full cache / ring segment, [n_main, n_main + n_sinkst) = sinks
@@ -621,8 +639,9 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw
   const float sl2 = FP8 ? p.scale_log2 * p.k_scale : p.scale_log2;
   const float vsc = FP8 ? p.v_scale : 1.f;
 
-  WaveState<D> st;
-  st.init();
+  WaveState<D> st[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) st[qb].init();
   if (nsteps > 0) {
     gload(0);
     swrite(0);
@@ -645,46 +664,55 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnParams p, int hpw
 #pragma unroll
     for (int e = 0; e < D / 16; ++e)
       f.v[e] = *reinterpret_cast<const bf16x8*>(&smem[buf][1][(h4 * D + 16 * e + col) * 8]);
-    // ---- visibility of keys 8h4 .. 8h4+7 for this lane's query column ----
+    // ---- visibility of keys 8h4 .. 8h4+7 for this lane's query column, per query block ----
     const int u0 = slot0(sidx);
-    unsigned vm = 0;
     const bool sink_step = WIN && sidx >= n_main;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int u = u0 + 8 * h4 + j;
-      bool ok;
-      if (!WIN) {
-        ok = u <= pq;
-      } else if (sink_step) {
-        ok = u < nS && u <= pq;
-      } else {
-        ok = (u - p.sink_pad) < seg_len;
-        if (ok) {
-          const int a = ring_abs(u, L, p);
-          ok = a >= p.n_sink && a <= pq && (pq - a) < (p.window - p.n_sink);
+    for (int qb = 0; qb < QB; ++qb) {
+      unsigned vm = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int u = u0 + 8 * h4 + j;
+        bool ok;
+        if (!WIN) {
+          ok = u <= pq[qb];
+        } else if (sink_step) {
+          ok = u < nS && u <= pq[qb];
+        } else {
+          ok = (u - p.sink_pad) < seg_len;
+          if (ok) {
+            const int a = ring_abs(u, L, p);
+            ok = a >= p.n_sink && a <= pq[qb] && (pq[qb] - a) < (p.window - p.n_sink);
+          }
+        }
+        vm |= (ok ? 1u : 0u) << j;
+      }
+      if constexpr (WIN) {
+        if (sink_step) {
+          attn_compute<D>(st[qb], qsf[qb], f, sl2, vm);
+          continue;
         }
       }
-      vm |= (ok ? 1u : 0u) << j;
+      attn_compute<D>(st[qb], qf[qb], f, sl2, vm);
     }
-    if (sink_step)
-      attn_compute<D>(st, qsf, f, sl2, vm);
-    else
-      attn_compute<D>(st, qf, f, sl2, vm);
     if (sidx + 1 < nsteps) swrite(buf ^ 1);
     __syncthreads();
   }
-  float lsum = st.l;
-  lsum += __shfl_xor(lsum, 16, 64);
-  lsum += __shfl_xor(lsum, 32, 64);
-  if (col_valid) {
-    const float inv = lsum > 0.f ? vsc / lsum : 0.f;
-    bf16* orow = p.out + ((size_t)(qs0 + tok) * p.nh + qh) * D;
 #pragma unroll
-    for (int e = 0; e < D / 16; ++e) {
-      bf16x4 v;
+  for (int qb = 0; qb < QB; ++qb) {
+    float lsum = st[qb].l;
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    if (col_valid[qb]) {
+      const float inv = lsum > 0.f ? vsc / lsum : 0.f;
+      bf16* orow = p.out + ((size_t)(qs0 + tok[qb]) * p.nh + qh) * D;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = (bf16)(st.o[e][r] * inv);
-      *reinterpret_cast<bf16x4*>(orow + 16 * e + 4 * h4) = v;
+      for (int e = 0; e < D / 16; ++e) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (bf16)(st[qb].o[e][r] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 16 * e + 4 * h4) = v;
+      }
     }
   }
 }
@@ -733,12 +761,21 @@ int launch_attn_decode(const AttnParams& p, int B, int D, hipStream_t stream) {
   }
 }
 
+template <int D, bool WIN, bool FP8>
+static void prefill_grid(const AttnParams& p, dim3 grid, int hpw, hipStream_t stream) {
+  if (p.prefill_qb == 2)
+    attn_prefill_kernel<D, WIN, FP8, 2><<<grid, 256, 0, stream>>>(p, hpw);
+  else
+    attn_prefill_kernel<D, WIN, FP8, 1><<<grid, 256, 0, stream>>>(p, hpw);
+}
+
 template <int D>
 static int launch_prefill_d(const AttnParams& p, int B, int max_q, hipStream_t stream) {
   const int G = p.nh / p.nkv;
   const int hpw = (G % 4 == 0) ? 4 : (G % 2 == 0 ? 2 : 1);  // q heads sharing each K/V tile
   const int tpw = 4 / hpw;
-  dim3 grid((max_q + 16 * tpw - 1) / (16 * tpw), p.nkv * (G / hpw), B);
+  const int tt = 16 * tpw * p.prefill_qb;                      // query tokens per workgroup tile
+  dim3 grid((max_q + tt - 1) / tt, p.nkv * (G / hpw), B);
   if (p.tile_map) {
     // XCD-aware 1-D grid over (group, tile) work items (see attn_prefill_kernel)
     const long total = (long)p.n_tiles * p.nkv * (G / hpw);
@@ -746,17 +783,18 @@ static int launch_prefill_d(const AttnParams& p, int B, int max_q, hipStream_t s
   }
   if (grid.x == 0) return 0;
   if (p.ring > 0) {
-    if (p.kv_fp8) attn_prefill_kernel<D, true, true><<<grid, 256, 0, stream>>>(p, hpw);
-    else attn_prefill_kernel<D, true, false><<<grid, 256, 0, stream>>>(p, hpw);
+    if (p.kv_fp8) prefill_grid<D, true, true>(p, grid, hpw, stream);
+    else prefill_grid<D, true, false>(p, grid, hpw, stream);
   } else {
-    if (p.kv_fp8) attn_prefill_kernel<D, false, true><<<grid, 256, 0, stream>>>(p, hpw);
-    else attn_prefill_kernel<D, false, false><<<grid, 256, 0, stream>>>(p, hpw);
+    if (p.kv_fp8) prefill_grid<D, false, true>(p, grid, hpw, stream);
+    else prefill_grid<D, false, false>(p, grid, hpw, stream);
   }
   return 0;
 }
 
 int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_t stream) {
   if (B == 0 || max_q == 0) return 0;
+  if (p.prefill_qb != 1 && p.prefill_qb != 2) return -3;
   if (p.bs % 32 != 0 || (p.ring > 0 && (p.sink_pad % 32 != 0 || p.ring % 32 != 0))) return -2;
   switch (D) {
     case 32: return launch_prefill_d<32>(p, B, max_q, stream);

@@ -18,6 +18,7 @@ struct AttnParams {
   const int* q_start;   // [B+1] prefill token offsets; nullptr for decode (token b == seq b)
   const int* tile_map;  // prefill: [n_tiles, 2] (sequence, token tile) work list, or nullptr
   int n_tiles;          //   (nullptr: dense grid over max_q x B)
+  int prefill_qb = 1;   // prefill: 16-token query blocks per wave (1 or 2); a tile = 16 TPW QB tokens
   float scale_log2;     // softmax scale * log2(e)
   int nh, nkv, bs;
   int n_sink, sink_pad, ring, window;  // window mode iff ring > 0

@@ -231,11 +231,18 @@ def decode_workspace(rows: int, nh: int, head_dim: int, splits: int, device):
             torch.empty(splits * rows * nh * 2, dtype=torch.float32, device=device))
 
 
+def prefill_qb() -> int:
+    """16-token query blocks per prefill wave (attention.hip QB): ``DLI_PREFILL_QB`` = 1 (default)
+    or 2 (each K / V fragment read from LDS feeds two query blocks' MFMAs: +2 % on 2k-4k chunks,
+    -25 % on 16-token chunks, twice the VGPRs; profiles/attn_prefill_qb_ab.json)."""
+    return 2 if os.environ.get("DLI_PREFILL_QB", "1") == "2" else 1
+
+
 def prefill_tile_tokens(nh: int, nkv: int) -> int:
-    """Query tokens per prefill workgroup tile (attention.hip: 16 * TPW, TPW = 4 / HPW)."""
+    """Query tokens per prefill workgroup tile (attention.hip: 16 * TPW * QB, TPW = 4 / HPW)."""
     G = nh // nkv
     hpw = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
-    return 16 * (4 // hpw)
+    return 16 * (4 // hpw) * prefill_qb()
 
 
 def prefill_tiles(q_lens, nh: int, nkv: int, out=None) -> torch.Tensor:
@@ -266,7 +273,7 @@ def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, m
     out = torch.empty_like(q) if out is None else out
     native().attn_prefill(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start,
                           int(max_q), float(scale), int(n_sink), int(sink_pad), int(ring),
-                          int(window), float(k_scale), float(v_scale), tile_map)
+                          int(window), float(k_scale), float(v_scale), tile_map, prefill_qb())
     return out
 
 

@@ -55,4 +55,4 @@ for c in CASES:
     print(r, flush=True)
     res.append(r)
 os.makedirs("gpurun_out", exist_ok=True)
-json.dump(res, open("gpurun_out/attn_prefill_bench.json", "w"), indent=1)
+json.dump(res, open("gpurun_out/attn_prefill_bench_qb%s.json" % ops.prefill_qb(), "w"), indent=1)

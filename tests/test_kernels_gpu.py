@@ -200,7 +200,9 @@ def test_attn_decode_window_multi_wrap(gpu, splits):
 
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (8, 8, 64), (4, 2, 32)])
 @pytest.mark.parametrize("tiles", [False, True])
-def test_attn_prefill(gpu, nh, nkv, D, tiles):
+@pytest.mark.parametrize("qb", ["1", "2"])
+def test_attn_prefill(gpu, nh, nkv, D, tiles, qb, monkeypatch):
+    monkeypatch.setenv("DLI_PREFILL_QB", qb)   # 16-token query blocks per wave
     torch.manual_seed(4)
     bs = 64
     q_lens = [5, 64, 130, 1, 1, 1]  # mixed batch: prefill chunks and decode rows
@@ -222,7 +224,9 @@ def test_attn_prefill(gpu, nh, nkv, D, tiles):
     _close(out, out_r, 2e-2, 2e-2, "prefill")
 
 
-def test_attn_prefill_window(gpu):
+@pytest.mark.parametrize("qb", ["1", "2"])
+def test_attn_prefill_window(gpu, qb, monkeypatch):
+    monkeypatch.setenv("DLI_PREFILL_QB", qb)
     torch.manual_seed(5)
     nh, nkv, D, bs = 8, 2, 64, 64
     n_sink, sink_pad, window, ring = 4, 32, 96, 192
@@ -417,6 +421,29 @@ def test_attn_decode_fp8_kv_window_sinks(gpu, splits):
     out_r = ref.attn_decode(q.cpu(), qs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), lens, scale, n_sink,
                             sink_pad, ring, window, k_scale=ks, v_scale=vs)
     _close(out, out_r, 2e-2, 2e-2, f"decode-fp8-window-s{splits}")
+
+
+@pytest.mark.parametrize("qb", ["1", "2"])
+def test_attn_prefill_long_chunks(gpu, qb, monkeypatch):
+    """70B head config, long causal chunks on top of cached context (multi-tile workgroups, the
+    diagonal inside a two-block wave tile, a chunk length that is not a tile multiple)."""
+    monkeypatch.setenv("DLI_PREFILL_QB", qb)
+    torch.manual_seed(24)
+    nh, nkv, D, bs = 64, 8, 128, 64
+    q_lens, ctx = [1000, 77, 2048], [0, 900, 64]
+    lens = torch.tensor([a + b for a, b in zip(q_lens, ctx)], dtype=torch.int32)
+    B = len(q_lens)
+    q_start = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
+    max_blocks = (int(lens.max()) + bs - 1) // bs
+    kc, vc = _make_cache(B * max_blocks, nkv, bs, D, gpu)
+    bt = _tables(B, max_blocks, B * max_blocks, gpu, seed=6)
+    q = torch.randn(int(q_start[-1]), nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    tm = ops.prefill_tiles(q_lens, nh, nkv).to(gpu)
+    out = ops.attn_prefill(q, None, kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens), scale,
+                           tile_map=tm)
+    out_r = ref.attn_prefill(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale)
+    _close(out, out_r, 2e-2, 2e-2, f"prefill-long-qb{qb}")
 
 
 def test_attn_prefill_fp8_kv(gpu):
