@@ -594,10 +594,35 @@ __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_ke
   };
 
   typedef int i32x4v __attribute__((ext_vector_type(4)));
+  // bf16 caches: K / V^T tiles go global -> LDS by LDS-DMA (global_load_lds_dwordx4: LDS slot =
+  // wave base + 16 lane, so the K swizzle is applied to the per-lane GLOBAL chunk instead); no
+  // staging registers or ds_writes, ~16 fewer VGPRs.  fp8 caches stage through registers: the
+  // 8-byte units are widened to bf16 on the way into LDS.
+  constexpr bool DMA = !FP8 && UNITS % 256 == 0;
+  auto dma = [&](int sidx, int buf) {
+    const int u0 = slot0(sidx);
+    const int page = bt[u0 / p.bs];
+    const int offk = u0 % p.bs;
+    const size_t e0 = ((size_t)page * p.nkv + kvh) * head_stride + (size_t)offk * D;
+    const bf16* kg = static_cast<const bf16*>(p.k_cache) + e0;
+    const bf16* vg = static_cast<const bf16*>(p.v_cache) + e0;
+#pragma unroll
+    for (int i = 0; i < UPT; ++i) {
+      const int u = threadIdx.x + i * 256;
+      const int row = u / CH, slot = u % CH;
+      // LDS unit u = (row, slot) holds global chunk slot ^ kswz(row)
+      __builtin_amdgcn_global_load_lds(
+          (__attribute__((address_space(1))) void*)(kg + (row * CH + (slot ^ kswz<D>(row))) * 8),
+          (__attribute__((address_space(3))) void*)&smem[buf][0][(w * 64 + i * 256) * 8], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          (__attribute__((address_space(1))) void*)(vg + (size_t)u * 8),
+          (__attribute__((address_space(3))) void*)&smem[buf][1][(w * 64 + i * 256) * 8], 16, 0, 0);
+    }
+  };
   // staging registers: one 8-element unit per tile unit (16 B bf16, or 8 B fp8 widened to bf16
   // when written to LDS, so the LDS tiles and everything after them are bf16 either way)
   typedef typename std::conditional<FP8, uint2, i32x4v>::type Unit;
-  Unit rk[UPT], rv[UPT];
+  Unit rk[DMA ? 1 : UPT], rv[DMA ? 1 : UPT];
   auto gload = [&](int sidx) {
     const int u0 = slot0(sidx);
     const int page = bt[u0 / p.bs];
@@ -643,13 +668,21 @@ __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_ke
 #pragma unroll
   for (int qb = 0; qb < QB; ++qb) st[qb].init();
   if (nsteps > 0) {
-    gload(0);
-    swrite(0);
+    if constexpr (DMA) {
+      dma(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      gload(0);
+      swrite(0);
+    }
   }
   __syncthreads();
   for (int sidx = 0; sidx < nsteps; ++sidx) {
     const int buf = sidx & 1;
-    if (sidx + 1 < nsteps) gload(sidx + 1);
+    if (sidx + 1 < nsteps) {
+      if constexpr (DMA) dma(sidx + 1, buf ^ 1);   // buf ^ 1 was last read before the barrier
+      else gload(sidx + 1);
+    }
     // ---- fragments from LDS ----
     KVFrag<D> f;
     const int krow0 = 8 * (col >> 2) + (col & 3);
@@ -695,7 +728,11 @@ __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_ke
       }
       attn_compute<D>(st[qb], qf[qb], f, sl2, vm);
     }
-    if (sidx + 1 < nsteps) swrite(buf ^ 1);
+    if constexpr (DMA) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step s+1 landed
+    } else {
+      if (sidx + 1 < nsteps) swrite(buf ^ 1);
+    }
     __syncthreads();
   }
 #pragma unroll
