@@ -151,14 +151,15 @@ __device__ __forceinline__ void o_unit(const WaveState<D>& st, int u, int h4, in
 }
 
 // One 32-key step of online-softmax attention for the 16 query columns held by this wave.
-// valid_mask bit j decides visibility of key 8h+j (h = lane>>4) for this lane's column.
-// (Skipping the O rescale when no running max moved, or a mask-free path for steps below the
-// diagonal, cut the prefill loop's VALU count but raised its VGPRs past 128: fewer workgroups
+// visible(j) decides visibility of key 8h+j (h = lane>>4) for this lane's column.  The softmax
+// scale is folded into the exponent's FMA (exp2(s * scale - m)), so a masked key costs one select
+// and the scores are never scaled on their own.
+// (Skipping the O rescale when no running max moved, or a mask-free copy of this step for keys
+// below the diagonal, cut the prefill loop's VALU count but raised its VGPRs: fewer workgroups
 // per CU, measured slower.)
-template <int D>
-__device__ __forceinline__ void attn_compute(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
-                                             const KVFrag<D>& f, float scale_log2,
-                                             unsigned valid_mask) {
+template <int D, typename Visible>
+__device__ __forceinline__ void attn_core(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
+                                          const KVFrag<D>& f, float scale_log2, Visible visible) {
   // ---- S^T = K . Q^T ----
   f32x4 s[2];
 #pragma unroll
@@ -167,24 +168,23 @@ __device__ __forceinline__ void attn_compute(WaveState<D>& st, const bf16x8 (&qf
 #pragma unroll
     for (int c = 0; c < D / 32; ++c) s[t] = mfma16(f.k[t][c], qf[c], s[t]);
   }
-  // ---- online softmax over the 8 keys 8h..8h+7 of this lane ----
+  // ---- online softmax over the 8 keys 8h..8h+7 of this lane (log2 domain) ----
   float x[8];
   float mx = -INFINITY;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float v = s[j >> 2][j & 3] * scale_log2;
-    x[j] = ((valid_mask >> j) & 1u) ? v : -INFINITY;
+    x[j] = visible(j) ? s[j >> 2][j & 3] : -INFINITY;
     mx = fmaxf(mx, x[j]);
   }
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  const float m_new = fmaxf(st.m, mx);
+  const float m_new = fmaxf(st.m, mx * scale_log2);
   const float alpha = __builtin_amdgcn_exp2f(st.m - m_new);
   bf16x8 pb;
   float ps = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float pj = __builtin_amdgcn_exp2f(x[j] - m_new);
+    const float pj = __builtin_amdgcn_exp2f(fmaf(x[j], scale_log2, -m_new));
     ps += pj;
     pb[j] = (bf16)pj;
   }
@@ -196,6 +196,21 @@ __device__ __forceinline__ void attn_compute(WaveState<D>& st, const bf16x8 (&qf
     st.o[e] *= alpha;
     st.o[e] = mfma16(f.v[e], pb, st.o[e]);
   }
+}
+
+// valid_mask bit j = visibility of key 8h+j
+template <int D>
+__device__ __forceinline__ void attn_compute(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
+                                             const KVFrag<D>& f, float scale_log2,
+                                             unsigned valid_mask) {
+  attn_core<D>(st, qf, f, scale_log2, [&](int j) { return ((valid_mask >> j) & 1u) != 0; });
+}
+
+// causal: keys 8h+j with j <= lim are visible (lim = the column's position - the lane's first key)
+template <int D>
+__device__ __forceinline__ void attn_compute_causal(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
+                                                    const KVFrag<D>& f, float scale_log2, int lim) {
+  attn_core<D>(st, qf, f, scale_log2, [&](int j) { return j <= lim; });
 }
 
 template <int D, bool FP8>
@@ -702,6 +717,10 @@ __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_ke
     const bool sink_step = WIN && sidx >= n_main;
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
+      if constexpr (!WIN) {
+        attn_compute_causal<D>(st[qb], qf[qb], f, sl2, pq[qb] - (u0 + 8 * h4));
+        continue;
+      }
       unsigned vm = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
