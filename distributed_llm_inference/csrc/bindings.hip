@@ -179,8 +179,10 @@ void rope_cache(Tensor qkv, optional<Tensor> positions, optional<Tensor> slot_ma
                 int64_t window, Tensor k_cache, Tensor v_cache, int64_t nh, int64_t nkv,
                 double k_scale, double v_scale) {
   CHECK_DEV(qkv);
-  // qkv: the bf16 GEMM output [T, *], or its un-reduced fp32 split-K partials [S, T, N]
-  const bool parts = qkv.scalar_type() == at::kFloat;
+  // qkv: the bf16 GEMM output [T, *], or its un-reduced split-K partials [S, T, N] (fp32, or
+  // bf16 from the fp8 path's gemm_tile epilogue 4)
+  const bool parts_bf16 = qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 3;
+  const bool parts = qkv.scalar_type() == at::kFloat || parts_bf16;
   if (parts) {
     TORCH_CHECK(qkv.dim() == 3 && qkv.is_contiguous(), "qkv partials must be contiguous [S, T, N]");
   } else {
@@ -200,7 +202,8 @@ void rope_cache(Tensor qkv, optional<Tensor> positions, optional<Tensor> slot_ma
   p.v_inv_scale = (float)(1.0 / v_scale);
   if (parts) {
     p.qkv = nullptr;
-    p.qkv_parts = qkv.data_ptr<float>();
+    p.qkv_parts = qkv.data_ptr();
+    p.parts_bf16 = parts_bf16 ? 1 : 0;
     p.splits = (int)qkv.size(0);
     p.qkv_stride = qkv.size(2);
     p.split_stride = (long)(T * qkv.size(2));
@@ -398,8 +401,10 @@ void sample(Tensor out_tokens, optional<Tensor> out_logprobs, Tensor logits,
 void quant_rowwise(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> residual,
                    optional<Tensor> norm_w, double eps, optional<Tensor> residual_out) {
   CHECK_IN(q_out); CHECK_IN(scale); CHECK_IN(x); CHECK_F32(scale);
-  // x: bf16 [rows, K], or fp32 split-K partials [S, rows, K] (summed on load)
-  const bool parts = x.scalar_type() == at::kFloat;
+  // x: bf16 [rows, K], or split-K partials [S, rows, K] summed on load (fp32, or bf16 from the
+  // fp8 path's gemm_tile epilogue 4)
+  const bool parts_bf16 = x.scalar_type() == at::kBFloat16 && x.dim() == 3;
+  const bool parts = x.scalar_type() == at::kFloat || parts_bf16;
   if (parts) {
     TORCH_CHECK(x.dim() == 3, "quant: partials must be [S, rows, K]");
   } else {
@@ -433,8 +438,8 @@ void quant_rowwise(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> residu
   check_rc(dli::launch_quant_rowwise(reinterpret_cast<uint8_t*>(q_out.data_ptr()),
                                      scale.data_ptr<float>(), parts ? nullptr : bp(x), ri, ro, w,
                                      (float)eps, (int)rows, (int)K, cur_stream(),
-                                     parts ? x.data_ptr<float>() : nullptr,
-                                     parts ? (int)x.size(0) : 0),
+                                     parts ? x.data_ptr() : nullptr,
+                                     parts ? (int)x.size(0) : 0, parts_bf16),
            "quant_rowwise");
 }
 
@@ -529,17 +534,22 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
   CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
   TORCH_CHECK(epilogue == 3 ? out.element_size() == 1 : out.scalar_type() == at::kBFloat16,
               "gemm_tile: bf16 output (fp8 bytes for epilogue 3)");
+  const bool bf16_parts = epilogue == 4;   // fp8 operands: bf16 split-K partials into out [S, M, N]
   const bool fp8 = a.element_size() == 1;   // 1-byte operands: fp8 e4m3 or int8
   TORCH_CHECK(a.scalar_type() == b.scalar_type(), "gemm_tile: a and b must share a dtype");
   TORCH_CHECK(fp8 || a.scalar_type() == at::kBFloat16, "gemm_tile: bf16, fp8 (e4m3) or int8 operands");
   int precision = !fp8 ? 0 : (a.scalar_type() == at::kChar ? 2 : 1);
-  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && out.dim() == 2, "gemm_tile: 2-D tensors");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && (out.dim() == 2 || bf16_parts), "gemm_tile: 2-D tensors");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
-  TORCH_CHECK(b.size(1) == K && out.size(0) == M, "gemm_tile: shape mismatch");
-  TORCH_CHECK(epilogue >= 0 && epilogue <= 3,
-              "gemm_tile: epilogue must be 0 (store), 1 (split-K partials only), 2 (swiglu) or 3 "
-              "(swiglu -> fp8 with MX scales)");
-  TORCH_CHECK(epilogue == 1 || out.size(1) == (epilogue >= 2 ? N / 2 : N), "gemm_tile: output columns");
+  TORCH_CHECK(b.size(1) == K && (bf16_parts || out.size(0) == M), "gemm_tile: shape mismatch");
+  TORCH_CHECK(epilogue >= 0 && epilogue <= 4,
+              "gemm_tile: epilogue must be 0 (store), 1 (split-K partials only), 2 (swiglu), 3 "
+              "(swiglu -> fp8 with MX scales) or 4 (bf16 split-K partials, fp8)");
+  TORCH_CHECK(epilogue == 1 || bf16_parts || out.size(1) == (epilogue >= 2 ? N / 2 : N),
+              "gemm_tile: output columns");
+  TORCH_CHECK(!bf16_parts || (fp8 && a.scalar_type() != at::kChar && splits > 1 &&
+                              out.is_contiguous() && out.numel() == splits * M * N),
+              "gemm_tile: epilogue 4 = fp8 operands, splits > 1, out [splits, M, N] bf16");
   // fp8 MX activations: e8m0 scale per (row, 128-column block), layout of gemm_tile.hip mx_off
   const int64_t nb = (M + 63) / 64;
   const uint8_t* amx = nullptr;
@@ -586,7 +596,7 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
     TORCH_CHECK(workspace->numel() >= dli::gemm_tile_sk_workspace_floats(),
                 "gemm_tile: stream-K workspace too small");
     ws = workspace->data_ptr<float>();
-  } else if (splits > 1) {
+  } else if (splits > 1 && !bf16_parts) {
     TORCH_CHECK(epilogue != 2, "gemm_tile: split-K only with the store / partials epilogues");
     TORCH_CHECK(workspace.has_value(), "gemm_tile: split-K needs a workspace");
     CHECK_IN(*workspace); CHECK_F32(*workspace);

@@ -89,6 +89,44 @@ __device__ __forceinline__ bf16 sum_parts1(const float* p, size_t stride) {
   return (bf16)s;
 }
 
+// bf16 partials (the fp8 path's gemm_tile epilogue 4: half the partial bytes; the fp8 activations
+// already carry far more error than rounding each partial to bf16 adds): summed in fp32
+template <int NS>
+__device__ __forceinline__ void sum_parts8(const bf16* p, size_t stride, bf16x8& out) {
+  bf16x8 a[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) a[k] = *reinterpret_cast<const bf16x8*>(p + k * stride);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float s = (float)a[0][j];
+#pragma unroll
+    for (int k = 1; k < NS; ++k) s += (float)a[k][j];
+    out[j] = (bf16)s;
+  }
+}
+
+template <int NS>
+__device__ __forceinline__ void sum_parts4(const bf16* p, size_t stride, bf16x4& out) {
+  bf16x4 a[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) a[k] = *reinterpret_cast<const bf16x4*>(p + k * stride);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float s = (float)a[0][j];
+#pragma unroll
+    for (int k = 1; k < NS; ++k) s += (float)a[k][j];
+    out[j] = (bf16)s;
+  }
+}
+
+template <int NS>
+__device__ __forceinline__ bf16 sum_parts1(const bf16* p, size_t stride) {
+  float s = (float)p[0];
+#pragma unroll
+  for (int k = 1; k < NS; ++k) s += (float)p[k * stride];
+  return (bf16)s;
+}
+
 // dispatch a runtime split count 1..8 to a compile-time NS (0 = no partials)
 #define DLI_SPLITS_SWITCH(splits, MACRO) \
   switch (splits) {                      \

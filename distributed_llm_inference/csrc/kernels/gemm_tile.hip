@@ -60,7 +60,9 @@ constexpr int kHalf = 128 * 128;       // bytes of one half-tile (128 rows x 64 
 constexpr int kBuf = 4 * kHalf;        // A0 A1 B0 B1
 constexpr int kLds = 2 * kBuf;         // double buffer: 128 KB
 
-enum Epilogue { kStoreBf16 = 0, kStoreF32 = 1, kSwiGLU = 2, kSwiGLUMx = 3 };
+// kStoreBf16Part: split-K partials rounded to bf16 (fp8 operands only: half the partial bytes of
+// kStoreF32 for the consumers that sum them; the fp8 activations carry far more error)
+enum Epilogue { kStoreBf16 = 0, kStoreF32 = 1, kSwiGLU = 2, kSwiGLUMx = 3, kStoreBf16Part = 4 };
 
 // stream-K workspace header: flags [0, kSkMaxWgs), error counter at kSkErrWord, slabs after
 constexpr int kSkMaxWgs = 1020, kSkErrWord = 1023, kSkHeaderFloats = 1024;
@@ -627,6 +629,20 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
           *reinterpret_cast<bf16x4*>(out + (size_t)row * I + (n0 >> 1) + wc * 32 + p * 16 + cq) = o;
         }
       }
+    } else if (EPI == kStoreBf16Part) {
+      bf16* out = reinterpret_cast<bf16*>(C) + (size_t)split * M * N;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = crow + i * 16;
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (bf16)acc[i][j][e];
+          *reinterpret_cast<bf16x4*>(out + (size_t)row * N + n0 + wc * 64 + j * 16 + cq) = o;
+        }
+      }
     } else if (EPI == kStoreF32) {
       float* out = reinterpret_cast<float*>(C) + (size_t)split * M * N;
 #pragma unroll
@@ -742,6 +758,17 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
   const int kps = (kt + splits - 1) / splits;
   if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
   if (PREC == kFp8Mx && kps > kMxMaxKt) return -15;   // its scales must fit the LDS slot
+  if (epilogue == kStoreBf16Part) {   // bf16 partials into C [splits, M, N]; the consumer sums
+    if constexpr (PREC == kFp8 || PREC == kFp8Mx) {
+      if (splits < 2) return -3;
+      sk.n_dp = tiles * splits;   // the block remap covers the whole grid
+      gemm_tile_kernel<kStoreBf16Part, PREC, false><<<tiles * splits, kThreads, 0, stream>>>(
+          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
+      return 0;
+    } else {
+      return -4;
+    }
+  }
   // kStoreF32 with splits > 1: partials only, the consumer reduces them (rms_norm_splitk)
   if (splits > 1 && (workspace == nullptr || epilogue == kSwiGLU)) return -3;
   if (splits == 1 && epilogue == kStoreF32) return -3;

@@ -44,7 +44,8 @@ struct RopeCacheParams {
   int nh, nkv, D, bs;
   // optional: qkv given as un-reduced fp32 split-K partials [splits, T, qkv_stride] of the QKV
   // tile GEMM (summed and rounded to bf16 on load, as the reduce pass would); qkv is unused then
-  const float* qkv_parts;
+  const void* qkv_parts;  // fp32, or bf16 with parts_bf16 (the fp8 path's gemm_tile epilogue 4)
+  int parts_bf16;
   int splits;
   long split_stride;      // elements between consecutive partials (T * qkv_stride)
 };
@@ -93,7 +94,8 @@ int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, 
                        int K, hipStream_t stream);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
                          bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,
-                         hipStream_t stream, const float* x_parts = nullptr, int splits = 0);
+                         hipStream_t stream, const void* x_parts = nullptr, int splits = 0,
+                         bool parts_bf16 = false);
 int launch_quant_rowwise_int8(int8_t* q, float* scale, const bf16* x, const uint8_t* outlier,
                               int rows, int K, hipStream_t stream);
 // LLM.int8 outlier bookkeeping (int8_outlier.hip)

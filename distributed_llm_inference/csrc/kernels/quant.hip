@@ -56,13 +56,14 @@ __device__ __forceinline__ void store_fp8_row(float (&v)[VPT][8], uint8_t* __res
 // If `residual_in` is given, x + residual_in is quantised and also written to `residual_out`
 // (which may alias residual_in; like rms_norm_kernel).  If `norm_w` is given the row is
 // RMS-normalised first, so "add residual -> RMSNorm -> fp8" is one HBM pass.
-// x_parts (optional): x given as fp32 split-K partials [splits, rows, K] of the tile GEMM that
-// produced it, summed and rounded to bf16 on load (bit-identical to the reduce pass).
+// x_parts (optional): x given as split-K partials [splits, rows, K] of the tile GEMM that
+// produced it, summed and rounded to bf16 on load: fp32 (bit-identical to the reduce pass) or,
+// with parts_bf16, bf16 partials (fp8 path)
 template <int VPT, int NS>
 __global__ void __launch_bounds__(1024) quant_rowwise_kernel(
     uint8_t* __restrict__ q, float* __restrict__ scale, const bf16* __restrict__ x,
     const bf16* residual_in, bf16* residual_out, const bf16* __restrict__ norm_w, float eps,
-    int K, const float* __restrict__ x_parts, size_t split_stride) {
+    int K, const void* __restrict__ x_parts, size_t split_stride, bool parts_bf16) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = K >> 3;
@@ -80,9 +81,13 @@ __global__ void __launch_bounds__(1024) quant_rowwise_kernel(
     if (idx < nvec) {
       if (norm_w) wv[i] = wr[idx];
       bf16x8 a;
-      if constexpr (NS > 0)
-        sum_parts8<NS>(x_parts + (size_t)row * K + (size_t)idx * 8, split_stride, a);
-      else
+      if constexpr (NS > 0) {
+        const size_t off = (size_t)row * K + (size_t)idx * 8;
+        if (parts_bf16)
+          sum_parts8<NS>(static_cast<const bf16*>(x_parts) + off, split_stride, a);
+        else
+          sum_parts8<NS>(static_cast<const float*>(x_parts) + off, split_stride, a);
+      } else
         a = xr[idx];
       if (add_residual) {
         bf16x8 r = ri[idx];
@@ -218,7 +223,7 @@ int launch_quant_rowwise_int8(int8_t* q, float* scale, const bf16* x, const uint
 
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
                          bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,
-                         hipStream_t stream, const float* x_parts, int splits) {
+                         hipStream_t stream, const void* x_parts, int splits, bool parts_bf16) {
   if (K % 8 != 0) return -1;
   if (x_parts != nullptr && splits < 1) return -3;
   const size_t split_stride = (size_t)rows * K;
@@ -231,7 +236,7 @@ int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* re
 #define DLI_QUANT(V, NS)                                                                    \
   quant_rowwise_kernel<V, NS><<<rows, threads, 0, stream>>>(q, scale, x, residual_in,       \
                                                             residual_out, norm_w, eps, K,   \
-                                                            x_parts, split_stride)
+                                                            x_parts, split_stride, parts_bf16)
 #define DLI_QUANT_NS(NS)                       \
   do {                                         \
     if (vpt <= 1) DLI_QUANT(1, NS);            \

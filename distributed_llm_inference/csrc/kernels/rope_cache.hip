@@ -45,7 +45,11 @@ __device__ __forceinline__ bf16x4 load_qkv4(const RopeCacheParams& p, const bf16
     return *reinterpret_cast<const bf16x4*>(row + c);
   } else {
     bf16x4 o;
-    sum_parts4<NS>(p.qkv_parts + (size_t)t * p.qkv_stride + c, p.split_stride, o);
+    const size_t off = (size_t)t * p.qkv_stride + c;
+    if (p.parts_bf16)
+      sum_parts4<NS>(static_cast<const bf16*>(p.qkv_parts) + off, p.split_stride, o);
+    else
+      sum_parts4<NS>(static_cast<const float*>(p.qkv_parts) + off, p.split_stride, o);
     return o;
   }
 }
@@ -56,7 +60,11 @@ __device__ __forceinline__ bf16 load_qkv1(const RopeCacheParams& p, const bf16* 
   if constexpr (NS == 0)
     return row[c];
   else
-    return sum_parts1<NS>(p.qkv_parts + (size_t)t * p.qkv_stride + c, p.split_stride);
+    return p.parts_bf16
+               ? sum_parts1<NS>(static_cast<const bf16*>(p.qkv_parts) + (size_t)t * p.qkv_stride + c,
+                                p.split_stride)
+               : sum_parts1<NS>(static_cast<const float*>(p.qkv_parts) + (size_t)t * p.qkv_stride + c,
+                                p.split_stride);
 }
 
 // grid (T, ceil(total_heads / kHeadsPerWG)): one workgroup per (token, group of 8 heads) so a

@@ -179,6 +179,11 @@ class LlamaMLP(nn.Module):
             return self.down_proj(h, defer_reduce=defer_reduce)
         gu = gp(normed, x_q)
         if self.down_proj.is_fp8:  # SwiGLU fused with the fp8 quantisation of down_proj's input
+            if not gu.is_cuda and ops.fp8_mx() and self.down_proj.bias is None:
+                # CPU reference of the GPU tile path: h handed over in MX form (per-(row,
+                # 128-column) e8m0 scales), as the fused SwiGLU epilogue quantises it
+                return self.down_proj(None, x_q=ops.mx_quantize(ops.silu_mul(gu)),
+                                      defer_reduce=defer_reduce)
             return self.down_proj(None, ops.silu_mul_quant(gu), defer_reduce=defer_reduce)
         return self.down_proj(ops.silu_mul(gu), defer_reduce=defer_reduce)
 

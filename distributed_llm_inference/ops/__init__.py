@@ -48,7 +48,8 @@ def _gpu(t: torch.Tensor) -> bool:
 
 # ----------------------------------------------------------------------------- normalisation
 class SplitKPartials:
-    """The un-reduced output of a split-K tile GEMM: fp32 partial products ``parts [S, M, N]``.
+    """The un-reduced output of a split-K tile GEMM: fp32 partial products ``parts [S, M, N]``
+    (bf16 on the fp8 path, :func:`fp8_bf16_partials`).
 
     ``gemm_tile(..., defer_reduce=True)`` returns this instead of running the reduction pass;
     ``rms_norm`` sums the partials while it reads them (norm.hip ``x_parts``), so the reduce
@@ -72,9 +73,19 @@ class SplitKPartials:
     is_cuda = True
 
     def materialize(self) -> torch.Tensor:
+        if self.parts.dtype != torch.float32:   # bf16 partials (fp8 path): summed in fp32
+            return self.parts.float().sum(0).to(torch.bfloat16)
         out = torch.empty(self.parts.shape[1:], dtype=torch.bfloat16, device=self.parts.device)
         native().splitk_reduce(out, self.parts)
         return out
+
+
+def fp8_bf16_partials() -> bool:
+    """``DLI_FP8_BF16_PARTS=1`` (default): the fp8 tile GEMMs' split-K partials (QKV, O, down) are
+    stored as bf16 (gemm_tile epilogue 4) and summed in fp32 by their consumers — half the partial
+    bytes written and read.  Rounding each partial to bf16 adds ~2^-9 relative error, far below
+    what the fp8 activations carry; the bf16 path keeps fp32 partials."""
+    return os.environ.get("DLI_FP8_BF16_PARTS", "1") != "0"
 
 
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
@@ -82,6 +93,8 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[to
              ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """``r = x + residual`` written to ``residual_out`` (default: in place into ``residual``);
     ``out = RMSNorm(r or x) * w``.  Returns ``(out, r)``.  ``x`` may be :class:`SplitKPartials`."""
+    if isinstance(x, SplitKPartials) and x.parts.dtype != torch.float32:
+        x = x.materialize()   # bf16 partials (fp8 path; the stage's final norm only)
     if isinstance(x, SplitKPartials):
         out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if out is None else out
         native().rms_norm_splitk(out, x.parts, residual, w, float(eps), residual_out)
@@ -635,6 +648,11 @@ def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torc
         return MxFp8(q, sc)
     if (defer_reduce and splits > 1 and _gpu(xq) and not swiglu
             and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
+        if fp8_bf16_partials():
+            parts = torch.empty(splits, M, N, dtype=torch.bfloat16, device=xq.device)
+            native().gemm_tile(parts, xq, wq, int(splits), 4, None,
+                               xs.reshape(-1).contiguous(), ws.reshape(-1).contiguous())
+            return SplitKPartials(parts)
         parts = torch.empty(splits, M, N, dtype=torch.float32, device=xq.device)
         dummy = torch.empty(M, 0, dtype=torch.bfloat16, device=xq.device)   # C is unused
         native().gemm_tile(dummy, xq, wq, int(splits), 1, parts.view(-1),
@@ -733,6 +751,10 @@ def gemm_tile_fp8_mx(a: MxFp8, wq: torch.Tensor, ws: torch.Tensor, splits: int =
                          f"{MX_MAX_KTILES}-k-tile scale slot")
     ws = ws.reshape(-1).contiguous()
     if defer_reduce and splits > 1 and os.environ.get("DLI_SPLITK_DEFER", "1") == "1":
+        if fp8_bf16_partials():
+            parts = torch.empty(splits, M, N, dtype=torch.bfloat16, device=xq.device)
+            native().gemm_tile(parts, xq, wq, int(splits), 4, None, None, ws, a_mx=a.sc)
+            return SplitKPartials(parts)
         parts = torch.empty(splits, M, N, dtype=torch.float32, device=xq.device)
         dummy = torch.empty(M, 0, dtype=torch.bfloat16, device=xq.device)   # C is unused
         native().gemm_tile(dummy, xq, wq, int(splits), 1, parts.view(-1), None, ws, a_mx=a.sc)

@@ -174,14 +174,18 @@ def test_fp8_tile_path_fused_swiglu_matches_cpu(gpu, monkeypatch):
 
     b = prefill_then_decode(g)
     rel = ((a - b[0]).norm() / a.norm()).item()
-    assert rel < 0.05, rel
+    # two fp8 pipelines that round anything differently (here: bf16 split-K partials, MX block
+    # scales) land ~5 % apart on this random-init stack, while a layout bug lands near 100 %
+    # (test_fp8_bf16_splitk_partials_close_to_fp32_partials measures both at the same 10 % from
+    # the bf16-weight model)
+    assert rel < 0.08, rel
     # the decode step against the hipBLASLt fp8 path (unfused SwiGLU, reduce passes)
     g.block.set_fused_swiglu(False)
     monkeypatch.setenv("DLI_FP8_TILE", "long")
     c = prefill_then_decode(g)
     for x, y in zip(c, b):
         rel = ((x - y).norm() / x.norm()).item()
-        assert rel < 0.05, rel
+        assert rel < 0.08, rel
     monkeypatch.setenv("DLI_FP8_TILE", "all")
     g.block.set_fused_swiglu(True)
     g.block.set_fused_swiglu(False)   # round trip restores the quantised rows exactly
@@ -373,10 +377,67 @@ def test_deferred_splitk_reduce_is_bit_identical_fp8(gpu, monkeypatch):
     g = CausalLMStage(spec, 0, 3, device=gpu).init_random(6)
     g.quantize_fp8()
     prompts = [list(range(1, 200)), list(range(3, 150))]
+    monkeypatch.setenv("DLI_FP8_BF16_PARTS", "0")   # fp32 partials: the bit-identity claim
     a = _stage_logits(g, prompts, 0)[0]
     monkeypatch.setenv("DLI_SPLITK_DEFER", "0")
     b = _stage_logits(g, prompts, 0)[0]
     assert torch.equal(a, b)
+
+
+def test_fp8_bf16_splitk_partials_close_to_fp32_partials(gpu, monkeypatch):
+    """fp8 weights with bf16 split-K partials (gemm_tile epilogue 4, summed in fp32 by the RoPE
+    kernel and the fused norm + quantiser) vs fp32 partials: a 256-sequence decode step through
+    QKV / O / down split-K agrees far inside the fp8 error."""
+    monkeypatch.setenv("DLI_FP8_TILE", "all")
+    spec = SPEC.replace(hidden_size=512, intermediate_size=2048, num_heads=8, num_kv_heads=2,
+                        head_dim=64)
+    g = CausalLMStage(spec, 0, 3, device=gpu).init_random(8)
+    prompts = [[(3 * i + j) % 983 + 1 for j in range(5)] for i in range(256)]
+    calls = []
+    mod = ops.native()
+
+    def spy(out, a, b, splits=1, epilogue=0, *args, **kw):
+        calls.append(epilogue)
+        return mod.gemm_tile(out, a, b, splits, epilogue, *args, **kw)
+
+    class _N:
+        def __getattr__(self, k):
+            return spy if k == "gemm_tile" else getattr(mod, k)
+    nat = _N()
+
+    def decode(parts):
+        monkeypatch.setenv("DLI_FP8_BF16_PARTS", parts)
+        pool = g.make_pool(256, block_size=64)
+        sids = list(range(len(prompts)))
+        for sid, p in zip(sids, prompts):
+            pool.manager.append(sid, len(p))
+        meta = pool.build_metadata(sids, [len(p) for p in prompts])
+        meta.logits_rows = (torch.cumsum(torch.tensor([len(p) for p in prompts]), 0) - 1).to(gpu)
+        ids = torch.tensor([t for p in prompts for t in p], dtype=torch.int32, device=gpu)
+        g(ids, meta, pool)
+        for sid in sids:
+            pool.manager.append(sid, 1)
+        meta = pool.build_metadata(sids, [1] * len(sids))
+        toks = torch.tensor([(7 * i) % 983 + 1 for i in sids], dtype=torch.int32, device=gpu)
+        calls.clear()
+        with monkeypatch.context() as m:
+            m.setattr(ops, "native", lambda: nat)
+            y = g(toks, meta, pool).float().cpu()
+        return y, list(calls)
+
+    ref, _ = decode("1")   # bf16 weights: fp32 partials throughout
+    g.quantize_fp8()
+    g.block.set_fused_swiglu(True)
+    a, ca = decode("1")
+    b, cb = decode("0")
+    assert 4 in ca and 4 not in cb and 1 in cb   # the decode step's split-K GEMMs took each path
+    # against the bf16-weight model, bf16 partials are as accurate as fp32 ones (their difference
+    # to each other is of the same order as each one's fp8 error: a random-init stack amplifies
+    # any perturbation, so the two are compared through the reference, not to each other)
+    rel_b = ((a - ref).norm() / ref.norm()).item()
+    rel_f = ((b - ref).norm() / ref.norm()).item()
+    print("fp8 logits vs bf16 model: bf16 partials", rel_b, "fp32 partials", rel_f)
+    assert rel_b < 1.15 * rel_f + 0.005, (rel_b, rel_f)
 
 
 @pytest.mark.parametrize("preset", ["qwen2-7b", "mistral-7b"])

@@ -109,6 +109,54 @@ def test_rope_cache_from_splitk_partials_bit_identical(gpu, nh, nkv, D, S, fp8):
     assert torch.equal(v1.view(torch.uint8), v2.view(torch.uint8))
 
 
+@pytest.mark.parametrize("fp8", [False, True])
+def test_rope_cache_bf16_partials_match_fp32_partials(gpu, fp8):
+    """bf16 split-K partials (fp8 path, gemm_tile epilogue 4) are summed in fp32 in split order:
+    bit-identical to the same values given as fp32 partials."""
+    torch.manual_seed(14)
+    nh, nkv, D, S, T, bs, nblocks = 64, 8, 128, 3, 29, 64, 8
+    pb = torch.randn(S, T, (nh + 2 * nkv) * D, device=gpu).to(torch.bfloat16)
+    pos = torch.randint(0, 300, (T,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(nblocks * bs, device=gpu)[:T].to(torch.int64)
+    cs = ref.build_cos_sin(D, 512, 500000.0, device=gpu)
+    k1, v1 = _make_cache(nblocks, nkv, bs, D, gpu)
+    if fp8:
+        k1, v1 = k1.to(torch.float8_e4m3fn), v1.to(torch.float8_e4m3fn)
+    k2, v2 = k1.clone(), v1.clone()
+    q1, _ = ops.rope_cache(ops.SplitKPartials(pb.float()), pos, slots, cs, nh, nkv, D, k1, v1)
+    q2, _ = ops.rope_cache(ops.SplitKPartials(pb), pos, slots, cs, nh, nkv, D, k2, v2)
+    assert torch.equal(q1, q2)
+    assert torch.equal(k1.view(torch.uint8), k2.view(torch.uint8))
+    assert torch.equal(v1.view(torch.uint8), v2.view(torch.uint8))
+
+
+@pytest.mark.parametrize("S,rows,K", [(4, 512, 8192), (3, 33, 1024)])
+def test_quant_rowwise_bf16_partials_match_fp32_partials(gpu, S, rows, K):
+    torch.manual_seed(S + rows + 1)
+    pb = torch.randn(S, rows, K, device=gpu).to(torch.bfloat16)
+    res = torch.randn(rows, K, device=gpu, dtype=BF)
+    w = torch.randn(K, device=gpu, dtype=BF)
+    r1, r2 = res.clone(), res.clone()
+    q1, s1 = ops.quant_rowwise(ops.SplitKPartials(pb.float()), r1, w, 1e-5)
+    q2, s2 = ops.quant_rowwise(ops.SplitKPartials(pb), r2, w, 1e-5)
+    assert torch.equal(q1.view(torch.uint8), q2.view(torch.uint8))
+    assert torch.equal(s1, s2) and torch.equal(r1, r2)
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(512, 1024, 8192, 4), (300, 768, 2048, 3)])
+def test_gemm_tile_fp8_bf16_partials(gpu, M, N, K, splits, monkeypatch):
+    """gemm_tile epilogue 4 (fp8, split-K partials rounded to bf16) against the fp32 partials."""
+    torch.manual_seed(M + K)
+    xq, xs = ops.quant_rowwise(torch.randn(M, K, device=gpu).to(BF))
+    wq, ws = ops.quantize_weight_fp8((torch.randn(N, K, device=gpu) / K ** 0.5).to(BF))
+    monkeypatch.setenv("DLI_FP8_BF16_PARTS", "0")
+    pf = ops.gemm_tile_fp8(xq, xs, wq, ws, splits, defer_reduce=True).parts
+    monkeypatch.setenv("DLI_FP8_BF16_PARTS", "1")
+    pb = ops.gemm_tile_fp8(xq, xs, wq, ws, splits, defer_reduce=True).parts
+    assert pb.dtype == BF and pf.dtype == torch.float32
+    assert torch.equal(pb, pf.to(BF))
+
+
 def _tables(B, max_blocks, nblocks, dev, seed=0):
     g = torch.Generator().manual_seed(seed)
     perm = torch.randperm(nblocks, generator=g)[: B * max_blocks]
