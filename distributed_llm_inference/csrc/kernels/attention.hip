@@ -137,6 +137,48 @@ __device__ __forceinline__ void attn_load(KVFrag<D>& f, const void* __restrict__
   }
 }
 
+// fp8 decode (DPerm on): the raw bytes of one 32-key step — half the registers of the widened
+// fragments, so the loop can keep three steps in flight and widen each just before its MFMAs.
+template <int D>
+struct KVRaw {
+  uint4 k[2][D / 64];
+  uint4 v[D / 32];
+};
+
+template <int D>
+__device__ __forceinline__ void attn_load_raw(KVRaw<D>& r, const void* __restrict__ kc,
+                                              const void* __restrict__ vc, size_t hb, int offk) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 15, h4 = lane >> 4;
+  const int krow0 = offk + 8 * (col >> 2) + (col & 3);
+  const uint8_t* k8 = static_cast<const uint8_t*>(kc);
+  const uint8_t* v8 = static_cast<const uint8_t*>(vc);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int c2 = 0; c2 < D / 64; ++c2)
+      r.k[t][c2] = *reinterpret_cast<const uint4*>(k8 + hb + (size_t)(krow0 + 4 * t) * D + 64 * c2 + 16 * h4);
+#pragma unroll
+  for (int e2 = 0; e2 < D / 32; ++e2)
+    r.v[e2] = *reinterpret_cast<const uint4*>(v8 + hb + ((size_t)((offk >> 3) + h4) * D + 32 * e2 + 2 * col) * 8);
+}
+
+template <int D>
+__device__ __forceinline__ void attn_widen(KVFrag<D>& f, const KVRaw<D>& r) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int c2 = 0; c2 < D / 64; ++c2) {
+      f.k[t][2 * c2] = fp8x8_to_bf16x8(make_uint2(r.k[t][c2].x, r.k[t][c2].y));
+      f.k[t][2 * c2 + 1] = fp8x8_to_bf16x8(make_uint2(r.k[t][c2].z, r.k[t][c2].w));
+    }
+#pragma unroll
+  for (int e2 = 0; e2 < D / 32; ++e2) {
+    f.v[2 * e2] = fp8x8_to_bf16x8(make_uint2(r.v[e2].x, r.v[e2].y));
+    f.v[2 * e2 + 1] = fp8x8_to_bf16x8(make_uint2(r.v[e2].z, r.v[e2].w));
+  }
+}
+
 // The D/16 f32x4 units of O^T a lane holds (query column col): unit u -> first d and values.
 template <int D, bool FP8>
 __device__ __forceinline__ void o_unit(const WaveState<D>& st, int u, int h4, int& d, f32x4& v) {
@@ -318,6 +360,35 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
         const size_t hb = ((size_t)page * p.nkv + kvh) * head_stride;
         attn_load<D, FP8>(f, p.k_cache, p.v_cache, hb, u0 % p.bs);
       };
+      if constexpr (DPerm<D, FP8>::on) {
+        // three raw steps in flight, each widened right before its MFMAs
+        auto rload = [&](KVRaw<D>& r, int sidx) {
+          const int u0 = seg_base + sidx * 32;
+          const int page = bt[u0 / p.bs];
+          const size_t hb = ((size_t)page * p.nkv + kvh) * head_stride;
+          attn_load_raw<D>(r, p.k_cache, p.v_cache, hb, u0 % p.bs);
+        };
+        auto step = [&](const KVRaw<D>& r, int sidx) {
+          KVFrag<D> f;
+          attn_widen<D>(f, r);
+          attn_compute<D>(st, qf, f, sl2,
+                          step_mask<D, WIN>(seg_base + sidx * 32, h4, seg_base, seg_len, L, p));
+        };
+        KVRaw<D> r0, r1, r2;
+        rload(r0, s_lo);
+        rload(r1, min(s_lo + 1, s_hi - 1));
+        for (int sidx = s_lo; sidx < s_hi; sidx += 3) {
+          rload(r2, min(sidx + 2, s_hi - 1));
+          __builtin_amdgcn_sched_barrier(0);
+          step(r0, sidx);
+          rload(r0, min(sidx + 3, s_hi - 1));
+          __builtin_amdgcn_sched_barrier(0);
+          if (sidx + 1 < s_hi) step(r1, sidx + 1);
+          rload(r1, min(sidx + 4, s_hi - 1));
+          __builtin_amdgcn_sched_barrier(0);
+          if (sidx + 2 < s_hi) step(r2, sidx + 2);
+        }
+      } else {
       KVFrag<D> fa, fb;
       load(fa, s_lo);
       // sched_barrier(0): keep each prefetch group issued ahead of the previous step's MFMAs
@@ -332,6 +403,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
         if (sidx + 1 < s_hi)
           attn_compute<D>(st, qf, fb, sl2,
                           step_mask<D, WIN>(seg_base + (sidx + 1) * 32, h4, seg_base, seg_len, L, p));
+      }
       }
     }
     // ---- sink segment (window mode): scored with q_sink by the split-0 wave ----
