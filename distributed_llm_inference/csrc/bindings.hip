@@ -71,7 +71,10 @@ void splitk_reduce(Tensor out, Tensor parts) {
 void rms_norm_splitk(Tensor out, Tensor parts, optional<Tensor> residual, Tensor w, double eps,
                      optional<Tensor> residual_out) {
   CHECK_IN(out); CHECK_IN(parts); CHECK_IN(w);
-  CHECK_BF16(out); CHECK_F32(parts); CHECK_BF16(w);
+  CHECK_BF16(out); CHECK_BF16(w);
+  // fp32 partials, or bf16 ones (8-bit weight modes: gemm_tile epilogue 4)
+  const bool parts_bf16 = parts.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(parts_bf16 || parts.scalar_type() == at::kFloat, "rms_norm_splitk: fp32 or bf16 parts");
   TORCH_CHECK(parts.dim() == 3, "rms_norm_splitk: parts must be [splits, rows, hidden]");
   const int64_t splits = parts.size(0), rows = parts.size(1), hidden = parts.size(2);
   TORCH_CHECK(splits >= 1 && w.numel() == hidden && out.numel() == rows * hidden,
@@ -91,7 +94,8 @@ void rms_norm_splitk(Tensor out, Tensor parts, optional<Tensor> residual, Tensor
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(parts.device());
   check_rc(dli::launch_rms_norm(bp(out), nullptr, r, ro, bp(w), (float)eps, (int)rows,
-                                (int)hidden, cur_stream(), parts.data_ptr<float>(), (int)splits),
+                                (int)hidden, cur_stream(), parts.data_ptr(), (int)splits,
+                                parts_bf16),
            "rms_norm_splitk");
 }
 
@@ -547,9 +551,9 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
               "(swiglu -> fp8 with MX scales) or 4 (bf16 split-K partials, fp8)");
   TORCH_CHECK(epilogue == 1 || bf16_parts || out.size(1) == (epilogue >= 2 ? N / 2 : N),
               "gemm_tile: output columns");
-  TORCH_CHECK(!bf16_parts || (fp8 && a.scalar_type() != at::kChar && splits > 1 &&
-                              out.is_contiguous() && out.numel() == splits * M * N),
-              "gemm_tile: epilogue 4 = fp8 operands, splits > 1, out [splits, M, N] bf16");
+  TORCH_CHECK(!bf16_parts || (fp8 && splits > 1 && out.is_contiguous() &&
+                              out.numel() == splits * M * N),
+              "gemm_tile: epilogue 4 = 8-bit operands, splits > 1, out [splits, M, N] bf16");
   // fp8 MX activations: e8m0 scale per (row, 128-column block), layout of gemm_tile.hip mx_off
   const int64_t nb = (M + 63) / 64;
   const uint8_t* amx = nullptr;

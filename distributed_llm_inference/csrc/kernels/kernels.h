@@ -68,7 +68,7 @@ struct SampleParams {
 
 int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* residual_out,
                     const bf16* w, float eps, int rows, int hidden, hipStream_t stream,
-                    const float* x_parts = nullptr, int splits = 0);
+                    const void* x_parts = nullptr, int splits = 0, bool parts_bf16 = false);
 int launch_layer_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* residual_out,
                       const bf16* w, const bf16* b, float eps, int rows, int hidden,
                       hipStream_t stream);

@@ -22,8 +22,8 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
                                                        const bf16* residual_in, bf16* residual_out,
                                                        const bf16* __restrict__ w, float eps,
                                                        int hidden, int add_residual,
-                                                       const float* __restrict__ x_parts,
-                                                       size_t split_stride) {
+                                                       const void* __restrict__ x_parts,
+                                                       size_t split_stride, bool parts_bf16) {
   __shared__ float scratch[8];
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
@@ -42,9 +42,14 @@ __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
     if (idx < nvec) {
       wv[i] = wr[idx];
       bf16x8 a;
-      if constexpr (NS > 0)
-        sum_parts8<NS>(x_parts + (size_t)row * hidden + (size_t)idx * 8, split_stride, a);
-      else
+      if constexpr (NS > 0) {
+        // fp32 partials, or bf16 ones (8-bit weight modes, gemm_tile epilogue 4)
+        const size_t off = (size_t)row * hidden + (size_t)idx * 8;
+        if (parts_bf16)
+          sum_parts8<NS>(static_cast<const bf16*>(x_parts) + off, split_stride, a);
+        else
+          sum_parts8<NS>(static_cast<const float*>(x_parts) + off, split_stride, a);
+      } else
         a = xr[idx];
       if (add_residual) {
         bf16x8 r = ri[idx];
@@ -173,7 +178,7 @@ static inline int norm_threads(int hidden) {
 // Returns 0 on success, -1 if `hidden` is unsupported (must be a multiple of 8, <= 16384).
 int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* residual_out,
                     const bf16* w, float eps, int rows, int hidden, hipStream_t stream,
-                    const float* x_parts, int splits) {
+                    const void* x_parts, int splits, bool parts_bf16) {
   if (hidden % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -1;
   if (x_parts != nullptr && splits < 1) return -2;
   const int add = residual_in != nullptr ? 1 : 0;
@@ -185,13 +190,13 @@ int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* res
     const int threads = norm_threads(hidden);                                                \
     const int vpt = (nvec + threads - 1) / threads;                                          \
     if (vpt <= 1) rms_norm_kernel<1, NS><<<rows, threads, 0, stream>>>(                      \
-        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride);           \
+        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride, parts_bf16);           \
     else if (vpt <= 2) rms_norm_kernel<2, NS><<<rows, threads, 0, stream>>>(                 \
-        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride);           \
+        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride, parts_bf16);           \
     else if (vpt <= 4) rms_norm_kernel<4, NS><<<rows, threads, 0, stream>>>(                 \
-        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride);           \
+        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride, parts_bf16);           \
     else if (vpt <= 8) rms_norm_kernel<8, NS><<<rows, threads, 0, stream>>>(                 \
-        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride);           \
+        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride, parts_bf16);           \
     else return -1;                                                                          \
   } while (0)
   DLI_SPLITS_SWITCH(ns, DLI_RMS)

@@ -81,10 +81,10 @@ class SplitKPartials:
 
 
 def fp8_bf16_partials() -> bool:
-    """``DLI_FP8_BF16_PARTS=1`` (default): the fp8 tile GEMMs' split-K partials (QKV, O, down) are
-    stored as bf16 (gemm_tile epilogue 4) and summed in fp32 by their consumers — half the partial
-    bytes written and read.  Rounding each partial to bf16 adds ~2^-9 relative error, far below
-    what the fp8 activations carry; the bf16 path keeps fp32 partials."""
+    """``DLI_FP8_BF16_PARTS=1`` (default): the 8-bit (fp8 / LLM.int8) tile GEMMs' split-K partials
+    (QKV, O, down) are stored as bf16 (gemm_tile epilogue 4) and summed in fp32 by their consumers
+    — half the partial bytes written and read.  Rounding each partial to bf16 adds ~2^-9 relative
+    error, far below what the 8-bit activations carry; the bf16 path keeps fp32 partials."""
     return os.environ.get("DLI_FP8_BF16_PARTS", "1") != "0"
 
 
@@ -93,8 +93,6 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[to
              ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """``r = x + residual`` written to ``residual_out`` (default: in place into ``residual``);
     ``out = RMSNorm(r or x) * w``.  Returns ``(out, r)``.  ``x`` may be :class:`SplitKPartials`."""
-    if isinstance(x, SplitKPartials) and x.parts.dtype != torch.float32:
-        x = x.materialize()   # bf16 partials (fp8 path; the stage's final norm only)
     if isinstance(x, SplitKPartials):
         out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if out is None else out
         native().rms_norm_splitk(out, x.parts, residual, w, float(eps), residual_out)
@@ -608,6 +606,10 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
             return swiglu_interleaved(y) if swiglu else y
         if (defer_reduce and sp > 1 and not swiglu
                 and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
+            if fp8_bf16_partials():   # bf16 partials (epilogue 4), as on the fp8 path
+                parts = torch.empty(sp, M, N, dtype=torch.bfloat16, device=x.device)
+                native().gemm_tile(parts, xq, wq, int(sp), 4, None, xs, ws, xo, wo)
+                return SplitKPartials(parts)
             parts = torch.empty(sp, M, N, dtype=torch.float32, device=x.device)
             dummy = torch.empty(M, 0, dtype=torch.bfloat16, device=x.device)   # C is unused
             native().gemm_tile(dummy, xq, wq, int(sp), 1, parts.view(-1), xs, ws, xo, wo)

@@ -342,6 +342,9 @@ def test_int8_fused_path_matches_unfused(gpu, monkeypatch):
         toks = torch.tensor([(11 * i) % 997 + 1 for i in sids], dtype=torch.int32, device=gpu)
         return pre, g(toks, meta, pool).float().cpu()
 
+    # fp32 partials on both sides: this compares the fused epilogue with the unfused path (bf16
+    # partials are checked against the bf16 model in test_8bit_bf16_splitk_partials_*)
+    monkeypatch.setenv("DLI_FP8_BF16_PARTS", "0")
     monkeypatch.setenv("DLI_SPLITK_DEFER", "0")
     a = run()
     monkeypatch.setenv("DLI_SPLITK_DEFER", "1")
@@ -384,10 +387,11 @@ def test_deferred_splitk_reduce_is_bit_identical_fp8(gpu, monkeypatch):
     assert torch.equal(a, b)
 
 
-def test_fp8_bf16_splitk_partials_close_to_fp32_partials(gpu, monkeypatch):
-    """fp8 weights with bf16 split-K partials (gemm_tile epilogue 4, summed in fp32 by the RoPE
-    kernel and the fused norm + quantiser) vs fp32 partials: a 256-sequence decode step through
-    QKV / O / down split-K agrees far inside the fp8 error."""
+@pytest.mark.parametrize("mode", ["fp8", "int8"])
+def test_8bit_bf16_splitk_partials_as_accurate_as_fp32(gpu, monkeypatch, mode):
+    """8-bit weights with bf16 split-K partials (gemm_tile epilogue 4, summed in fp32 by the RoPE
+    kernel and the fused norm (+ quantiser) consumers) vs fp32 partials, a 256-sequence decode step
+    through QKV / O / down split-K: both equally far from the bf16-weight model."""
     monkeypatch.setenv("DLI_FP8_TILE", "all")
     spec = SPEC.replace(hidden_size=512, intermediate_size=2048, num_heads=8, num_kv_heads=2,
                         head_dim=64)
@@ -426,7 +430,10 @@ def test_fp8_bf16_splitk_partials_close_to_fp32_partials(gpu, monkeypatch):
         return y, list(calls)
 
     ref, _ = decode("1")   # bf16 weights: fp32 partials throughout
-    g.quantize_fp8()
+    if mode == "fp8":
+        g.quantize_fp8()
+    else:
+        g.quantize("int8", threshold=3.0)
     g.block.set_fused_swiglu(True)
     a, ca = decode("1")
     b, cb = decode("0")
@@ -436,7 +443,7 @@ def test_fp8_bf16_splitk_partials_close_to_fp32_partials(gpu, monkeypatch):
     # any perturbation, so the two are compared through the reference, not to each other)
     rel_b = ((a - ref).norm() / ref.norm()).item()
     rel_f = ((b - ref).norm() / ref.norm()).item()
-    print("fp8 logits vs bf16 model: bf16 partials", rel_b, "fp32 partials", rel_f)
+    print(mode, "logits vs bf16 model: bf16 partials", rel_b, "fp32 partials", rel_f)
     assert rel_b < 1.15 * rel_f + 0.005, (rel_b, rel_f)
 
 

@@ -254,7 +254,7 @@ def test_llm_int8_fused_outlier_epilogue_swiglu_and_partials(gpu, M, K, N, n_out
     p = ops.llm_int8_linear(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, defer_reduce=True)
     if isinstance(p, ops.SplitKPartials):
         assert p.parts.shape[0] > 1
-        yp = p.parts.sum(0).cpu()
+        yp = p.parts.float().sum(0).cpu()
         assert ((yp - ref).norm() / ref.norm()).item() < 5e-3
     wqi = ops.swiglu_interleave(wq.to(gpu))
     wsi = ops.swiglu_interleave(ws.to(gpu).reshape(-1, 1)).reshape(-1)
