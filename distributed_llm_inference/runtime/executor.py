@@ -28,6 +28,7 @@ from .. import ops
 from ..models.common import AttnMetadata
 from ..models.llama.cache import KVPool
 from ..models.stage import CausalLMStage
+from ..utils.cuda import prime_graph_rng
 
 log = logging.getLogger(__name__)
 
@@ -434,6 +435,7 @@ class StageExecutor:
             for _ in range(2):
                 self._forward(meta, x, n_sample, project)
         torch.cuda.current_stream().wait_stream(s)
+        prime_graph_rng(self.device)
         graph = torch.cuda.CUDAGraph()
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()

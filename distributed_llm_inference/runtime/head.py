@@ -29,6 +29,7 @@ import torch
 
 from .. import ops
 from ..models.embed_head import LMHead
+from ..utils.cuda import prime_graph_rng
 from .executor import StepPlan, _Staging, _fill_pos
 
 log = logging.getLogger(__name__)
@@ -140,6 +141,7 @@ class HeadRunner:
             for _ in range(2):
                 self._forward(rows)
         cur.wait_stream(s)
+        prime_graph_rng(torch.cuda.current_device())
         g = torch.cuda.CUDAGraph()
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()

@@ -19,6 +19,35 @@ import torch
 from torch.utils._pytree import tree_flatten, tree_unflatten
 
 
+_RNG_PRIMED: dict = {}
+
+
+def prime_graph_rng(device=None) -> None:
+    """Create the device generator's graph-safe RNG state outside inference mode.
+
+    ``capture_begin`` registers the default generator with the graph and lazily allocates its
+    seed/offset tensors on first use. If that first capture runs under ``torch.inference_mode``
+    (the runtime's decode graphs do) they become inference tensors, and every later capture
+    OUTSIDE inference mode fails with "Inplace update to inference tensor". One empty capture
+    with inference mode off makes them ordinary tensors; later in-place updates are then legal
+    in both modes. The generator re-allocates that state whenever its set of registered graphs
+    becomes empty, so the priming graph is kept alive for the life of the process."""
+    dev = torch.device(device if device is not None else "cuda")
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx in _RNG_PRIMED:
+        return
+    with torch.inference_mode(False), torch.cuda.device(idx):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                torch.empty(1, device=f"cuda:{idx}").fill_(0)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize(idx)
+    _RNG_PRIMED[idx] = g
+
+
 def make_inference_graphed_callable(callable: Callable, sample_args, num_warmup_iters: int = 3,
                                     clone_outputs: bool = True, pool=None) -> Callable:
     assert not isinstance(callable, torch.nn.Module), "pass a function, not an nn.Module"
@@ -38,6 +67,7 @@ def make_inference_graphed_callable(callable: Callable, sample_args, num_warmup_
             callable(*sample_args)
     torch.cuda.current_stream().wait_stream(s)
 
+    prime_graph_rng()
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph, pool=pool):
         outputs = callable(*sample_args)
