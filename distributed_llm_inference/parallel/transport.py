@@ -204,6 +204,31 @@ class RcclTransport(Transport):
                 # index 0 = the sender (last stage), 1 = the head rank
                 self._hcomms[peer] = C.RcclComm(bytes(uid), 0 if rank == last else 1, 2, dev_idx,
                                                 timeout_s)
+        self.connect_ms = self._connect()
+
+    def _connect(self) -> float:
+        """Bring up every P2P connection now, in the direction the runtime uses it, instead of at
+        the first decode step: RCCL connects a pair lazily at its first send/recv, so a link that
+        cannot come up fails here, inside the agreed init of ``make_transport``, with all ranks
+        still in lockstep.  Same order as the data flow (recv from r-1, send to r+1, then the
+        head pairs last -> r in increasing r), so the chain of blocking connects resolves from
+        rank 0 upwards without a cycle."""
+        t0 = time.perf_counter()
+        probe = torch.zeros(64, dtype=torch.bfloat16, device=self.device)
+        with torch.cuda.device(self.device):
+            if self.rank > 0:
+                self._comm(self.rank - 1).recv(probe, 0, self.recv_stream.cuda_stream)
+            if self.rank < self.world - 1:
+                self._comm(self.rank + 1).send(probe, 1, self.send_stream.cuda_stream)
+            last = self.world - 1
+            for r in sorted(self._hcomms):
+                if self.rank == last:
+                    self._hcomms[r].send(probe, 1, self.send_stream.cuda_stream)
+                else:
+                    self._hcomms[r].recv(probe, 0, self.recv_stream.cuda_stream)
+            self.send_stream.synchronize()
+            self.recv_stream.synchronize()
+        return (time.perf_counter() - t0) * 1e3
 
     def _comm(self, peer: int):
         c = self._comms.get(peer)
@@ -271,6 +296,7 @@ class RcclTransport(Transport):
 
     def describe(self) -> dict:
         d = {"transport": "RcclTransport", "rccl_version": self._rccl_version,
+             "connect_ms": round(self.connect_ms, 1),
              "pair_comms": {str(p): {"rank": c.rank, "size": c.world}
                             for p, c in sorted(self._comms.items())}}
         if self._hcomms:
