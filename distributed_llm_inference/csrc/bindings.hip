@@ -470,8 +470,11 @@ void quant_rowwise_int8(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> o
 // LLM.int8 outlier columns of x [M, K] against int8 weights wq [N, K] (scale ws [N]): returns
 // (flags uint8 [K], x_out bf16 [M, max_out], w_out bf16 [N, max_out]) with x_out . w_out^T the
 // bf16 outlier product (padding columns are zero).  Four kernels, static shapes, no host sync.
+// Returns (flags [K] u8, x_out [M, max_out], w_out [N, max_out], cnt [1] i32 = columns kept).
+// dynamic: the gathers write only the first ceil(cnt / 32) 32-column chunks of x_out / w_out (the
+// rest is left unwritten) -- for the int8 tile GEMM, which given `cnt` reads no further.
 std::vector<Tensor> llm_int8_outliers(Tensor x, Tensor wq, Tensor ws, double threshold,
-                                      int64_t max_out, optional<Tensor> wq_t) {
+                                      int64_t max_out, optional<Tensor> wq_t, bool dynamic) {
   CHECK_IN(x); CHECK_BF16(x); CHECK_IN(wq); CHECK_IN(ws); CHECK_F32(ws);
   TORCH_CHECK(wq.scalar_type() == at::kChar, "llm_int8_outliers: wq must be int8");
   TORCH_CHECK(x.dim() == 2 && wq.dim() == 2 && wq.size(1) == x.size(1) && ws.numel() == wq.size(0),
@@ -486,15 +489,18 @@ std::vector<Tensor> llm_int8_outliers(Tensor x, Tensor wq, Tensor ws, double thr
   Tensor flags = at::empty({K}, o.dtype(at::kByte));
   Tensor xo = at::empty({M, max_out}, o);
   Tensor wo = at::empty({N, max_out}, o);
+  Tensor cnt = at::empty({1}, o.dtype(at::kInt));
+  const int* dyn = dynamic ? cnt.data_ptr<int>() : nullptr;
   hipStream_t st = cur_stream();
   check_rc(dli::launch_llm_int8_colmax(colmax.data_ptr<float>(), bp(x), (int)M, (int)K, st),
            "llm_int8_colmax");
   check_rc(dli::launch_llm_int8_select(colmax.data_ptr<float>(), (int)K, (float)threshold,
                                        (int)max_out, idx.data_ptr<int64_t>(), sel.data_ptr<float>(),
-                                       flags.data_ptr<uint8_t>(), st),
+                                       flags.data_ptr<uint8_t>(), st, cnt.data_ptr<int>()),
            "llm_int8_select");
   check_rc(dli::launch_llm_int8_gather_x(bp(xo), bp(x), idx.data_ptr<int64_t>(),
-                                         sel.data_ptr<float>(), (int)M, (int)K, (int)max_out, st),
+                                         sel.data_ptr<float>(), (int)M, (int)K, (int)max_out, st,
+                                         dyn),
            "llm_int8_gather_x");
   if (wq_t.has_value()) {   // transposed copy [K, N]: coalesced column gather
     CHECK_IN((*wq_t));
@@ -502,15 +508,16 @@ std::vector<Tensor> llm_int8_outliers(Tensor x, Tensor wq, Tensor ws, double thr
                     wq_t->size(1) == N, "llm_int8_outliers: wq_t must be int8 [K, N]");
     check_rc(dli::launch_llm_int8_gather_wt(bp(wo), reinterpret_cast<const int8_t*>(wq_t->data_ptr()),
                                             ws.data_ptr<float>(), idx.data_ptr<int64_t>(),
-                                            sel.data_ptr<float>(), (int)N, (int)max_out, st),
+                                            sel.data_ptr<float>(), (int)N, (int)max_out, st, dyn),
              "llm_int8_gather_wt");
   } else {
     check_rc(dli::launch_llm_int8_gather_w(bp(wo), reinterpret_cast<const int8_t*>(wq.data_ptr()),
                                            ws.data_ptr<float>(), idx.data_ptr<int64_t>(),
-                                           sel.data_ptr<float>(), (int)N, (int)K, (int)max_out, st),
+                                           sel.data_ptr<float>(), (int)N, (int)K, (int)max_out, st,
+                                           dyn),
              "llm_int8_gather_w");
   }
-  return {flags, xo, wo};
+  return {flags, xo, wo, cnt};
 }
 
 void silu_mul_quant(Tensor q_out, Tensor scale, Tensor x) {
@@ -534,7 +541,7 @@ void silu_mul_quant(Tensor q_out, Tensor scale, Tensor x) {
 void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
                optional<Tensor> workspace, optional<Tensor> a_scale, optional<Tensor> b_scale,
                optional<Tensor> x_out, optional<Tensor> w_out, optional<Tensor> a_mx,
-               optional<Tensor> out_mx) {
+               optional<Tensor> out_mx, optional<Tensor> ol_cnt) {
   CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
   TORCH_CHECK(epilogue == 3 ? out.element_size() == 1 : out.scalar_type() == at::kBFloat16,
               "gemm_tile: bf16 output (fp8 bytes for epilogue 3)");
@@ -623,10 +630,17 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
     xo = bp(*x_out);
     wo = bp(*w_out);
   }
+  const int* olc = nullptr;   // live outlier columns (llm_int8_outliers(..., dynamic=True))
+  if (ol_cnt.has_value()) {
+    CHECK_IN(*ol_cnt);
+    TORCH_CHECK(x_out.has_value() && ol_cnt->scalar_type() == at::kInt && ol_cnt->numel() == 1,
+                "gemm_tile: ol_cnt = int32 [1] count of the live outlier columns (with x_out)");
+    olc = ol_cnt->data_ptr<int>();
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
   check_rc(dli::launch_gemm_tile(out.data_ptr(), a.data_ptr(), b.data_ptr(), sa, sb, ws, (int)M,
                                  (int)N, (int)K, (int)splits, (int)epilogue, precision, cur_stream(),
-                                 xo, wo, J, amx, omx),
+                                 xo, wo, J, amx, omx, olc),
            "gemm_tile");
 }
 
@@ -680,16 +694,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("quant_rowwise_int8", &quant_rowwise_int8, "LLM.int8 row-wise int8 quantisation (outlier columns zeroed)",
         py::arg("q_out"), py::arg("scale"), py::arg("x"), py::arg("outlier") = py::none());
   m.def("llm_int8_outliers", &llm_int8_outliers,
-        "LLM.int8 outlier columns: (flags, x_out, w_out) for the bf16 outlier product",
+        "LLM.int8 outlier columns: (flags, x_out, w_out, cnt) for the bf16 outlier product",
         py::arg("x"), py::arg("wq"), py::arg("ws"), py::arg("threshold"), py::arg("max_out"),
-        py::arg("wq_t") = py::none());
+        py::arg("wq_t") = py::none(), py::arg("dynamic") = false);
   m.def("silu_mul_quant", &silu_mul_quant, "SwiGLU fused with row-wise fp8 quantisation");
   m.def("gemm_tile", &gemm_tile, "C = A . B^T, 256x256 LDS-DMA 8-phase MFMA tile GEMM",
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
         py::arg("epilogue") = 0, py::arg("workspace") = py::none(),
         py::arg("a_scale") = py::none(), py::arg("b_scale") = py::none(),
         py::arg("x_out") = py::none(), py::arg("w_out") = py::none(),
-        py::arg("a_mx") = py::none(), py::arg("out_mx") = py::none());
+        py::arg("a_mx") = py::none(), py::arg("out_mx") = py::none(),
+        py::arg("ol_cnt") = py::none());
   m.def("rms_norm_splitk", &rms_norm_splitk, "residual add + RMSNorm over un-reduced split-K partials",
         py::arg("out"), py::arg("parts"), py::arg("residual"), py::arg("w"), py::arg("eps"),
         py::arg("residual_out") = py::none());

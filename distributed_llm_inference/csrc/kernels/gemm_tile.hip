@@ -168,6 +168,9 @@ struct OutlierArgs {
   const bf16* x;   // [M, J] activations of the outlier columns (zero-padded past the used ones)
   const bf16* w;   // [N, J] dequantised weight columns (zero-padded likewise)
   int J;           // multiple of 32; 0 = none
+  // optional device count of the outlier columns actually selected (llm_int8_select): only the
+  // first ceil(cnt / 32) k-steps are multiplied; columns past them may hold stale data
+  const int* cnt;
 };
 
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -538,7 +541,8 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
       if (ol.J > 0 && split == 0) {
         // weight fragment = MFMA A operand, as in the main loop: lane l holds w_out row
         // n0 + 64 wc + 16 j + (l & 15) and x_out row crow + 16 i, k = 8 (l >> 4) .. + 7
-        for (int kk = 0; kk < ol.J; kk += 32) {
+        const int jl = ol.cnt ? min(ol.J, (*ol.cnt + 31) & ~31) : ol.J;
+        for (int kk = 0; kk < jl; kk += 32) {
           bf16x8 wf[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j)
@@ -820,9 +824,10 @@ long long gemm_tile_sk_workspace_floats() {
 int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale,
                      const float* b_scale, float* workspace, int M, int N, int K, int splits,
                      int epilogue, int precision, hipStream_t stream, const bf16* x_out,
-                     const bf16* w_out, int J, const uint8_t* a_mx, uint8_t* out_mx) {
+                     const bf16* w_out, int J, const uint8_t* a_mx, uint8_t* out_mx,
+                     const int* ol_cnt) {
   if (J < 0 || J % 32 != 0 || (J > 0 && (precision != kInt8 || !x_out || !w_out))) return -12;
-  const OutlierArgs ol{x_out, w_out, J};
+  const OutlierArgs ol{x_out, w_out, J, ol_cnt};
   const MxArgs mx{a_mx, out_mx, (M + 63) / 64};
   switch (precision) {
     case kBf16:

@@ -10,9 +10,18 @@
 //   * llm_int8_gather_w_kernel   w_out[n, j] = bf16(wq[n, idx[j]] * ws[n]) * sel[j]
 //   * llm_int8_gather_wt_kernel  same from the transposed copy wqT [K, N] (coalesced)
 //   * llm_int8_gather_x_kernel   x_out[m, j] = x[m, idx[j]] * sel[j]
+// The select kernel also stores the number of columns it kept (`cnt`, optional).  Given it, the
+// gathers write only the first ceil(cnt / 32) 32-column chunks and the int8 tile GEMM's epilogue
+// multiplies only those (gemm_tile.hip OutlierArgs::cnt): the outlier work follows the columns
+// actually found (none on most rows of most layers) instead of the static cap.
 #include "kernels.h"
 
 namespace dli {
+
+// columns of the static [*, max_out] outlier buffers that are live for this product
+__device__ __forceinline__ int live_cols(const int* cnt, int max_out) {
+  return cnt ? min(max_out, (*cnt + 31) & ~31) : max_out;
+}
 
 // One workgroup per 64 columns: 256 threads = 8 column vectors (8 bf16 each) x 32 row lanes.  A
 // wave reads 8 rows x 128 contiguous bytes per load; the 32 row-lane maxima are folded in LDS and
@@ -102,7 +111,7 @@ __device__ __forceinline__ int block_exclusive_scan(int x, int* wsum, int& total
 
 __global__ void __launch_bounds__(kSelThreads) llm_int8_select_kernel(
     const float* __restrict__ colmax, int K, float threshold, int max_out, long* __restrict__ idx,
-    float* __restrict__ sel, uint8_t* __restrict__ flags) {
+    float* __restrict__ sel, uint8_t* __restrict__ flags, int* __restrict__ cnt) {
   __shared__ int red[kSelThreads / 64];
   __shared__ int hist[256];
   __shared__ unsigned s_prefix;
@@ -188,6 +197,7 @@ __global__ void __launch_bounds__(kSelThreads) llm_int8_select_kernel(
   for (int i = 0; i < kSelMaxPer; ++i) mine += i < n_mine && (strict ? v[i] > t : v[i] >= t);
   int total;
   int pos = block_exclusive_scan(mine, red, total);
+  if (cnt != nullptr && threadIdx.x == 0) *cnt = min(total, max_out);
 #pragma unroll
   for (int i = 0; i < kSelMaxPer; ++i) {
     if (i < n_mine) {
@@ -206,23 +216,32 @@ __global__ void __launch_bounds__(kSelThreads) llm_int8_select_kernel(
   }
 }
 
+// Row-major gathers: one thread per output element, numbered chunk-major (32-column chunk, then
+// row, then column in the chunk) so a wave covers 2 rows x 32 columns (64-byte store runs) and the
+// threads of a chunk past the live columns return at once -- the launch stays as wide as the
+// one-element-per-thread form (measured faster than looping rows per thread at ~2 workgroups/CU).
 __global__ void __launch_bounds__(256) llm_int8_gather_w_kernel(
     bf16* __restrict__ w_out, const int8_t* __restrict__ wq, const float* __restrict__ ws,
-    const long* __restrict__ idx, const float* __restrict__ sel, int N, int K, int max_out) {
+    const long* __restrict__ idx, const float* __restrict__ sel, int N, int K, int max_out,
+    const int* __restrict__ cnt) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long)N * max_out) return;
-  const int n = (int)(e / max_out), j = (int)(e % max_out);
+  const long per_chunk = (long)N * 32;
+  const int chunk = (int)(e / per_chunk);
+  const int n = (int)((e % per_chunk) >> 5), j = chunk * 32 + (int)(e & 31);
+  if (chunk * 32 >= live_cols(cnt, max_out) || j >= max_out) return;
   const float v = (float)wq[(size_t)n * K + idx[j]] * ws[n];
-  w_out[e] = (bf16)(v * sel[j]);
+  w_out[(size_t)n * max_out + j] = (bf16)(v * sel[j]);
 }
 
 __global__ void __launch_bounds__(256) llm_int8_gather_x_kernel(
     bf16* __restrict__ x_out, const bf16* __restrict__ x, const long* __restrict__ idx,
-    const float* __restrict__ sel, int M, int K, int max_out) {
+    const float* __restrict__ sel, int M, int K, int max_out, const int* __restrict__ cnt) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (long)M * max_out) return;
-  const int m = (int)(e / max_out), j = (int)(e % max_out);
-  x_out[e] = (bf16)((float)x[(size_t)m * K + idx[j]] * sel[j]);
+  const long per_chunk = (long)M * 32;
+  const int chunk = (int)(e / per_chunk);
+  const int m = (int)((e % per_chunk) >> 5), j = chunk * 32 + (int)(e & 31);
+  if (chunk * 32 >= live_cols(cnt, max_out) || j >= max_out) return;
+  x_out[(size_t)m * max_out + j] = (bf16)((float)x[(size_t)m * K + idx[j]] * sel[j]);
 }
 
 int launch_llm_int8_colmax(float* colmax, const bf16* x, int rows, int K, hipStream_t stream) {
@@ -234,9 +253,10 @@ int launch_llm_int8_colmax(float* colmax, const bf16* x, int rows, int K, hipStr
 }
 
 int launch_llm_int8_select(const float* colmax, int K, float threshold, int max_out, long* idx,
-                           float* sel, uint8_t* flags, hipStream_t stream) {
+                           float* sel, uint8_t* flags, hipStream_t stream, int* cnt) {
   if (K <= 0 || K > kSelThreads * kSelMaxPer || max_out <= 0 || max_out > K) return -1;
-  llm_int8_select_kernel<<<1, kSelThreads, 0, stream>>>(colmax, K, threshold, max_out, idx, sel, flags);
+  llm_int8_select_kernel<<<1, kSelThreads, 0, stream>>>(colmax, K, threshold, max_out, idx, sel,
+                                                         flags, cnt);
   return 0;
 }
 
@@ -246,10 +266,12 @@ int launch_llm_int8_select(const float* colmax, int K, float threshold, int max_
 // Requires N % 4 == 0 (launcher).
 __global__ void __launch_bounds__(256) llm_int8_gather_wt_kernel(
     bf16* __restrict__ w_out, const int8_t* __restrict__ wqT, const float* __restrict__ ws,
-    const long* __restrict__ idx, const float* __restrict__ sel, int N, int max_out) {
+    const long* __restrict__ idx, const float* __restrict__ sel, int N, int max_out,
+    const int* __restrict__ cnt) {
   __shared__ float tile[16][257];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n0 = blockIdx.x * 256, j0 = blockIdx.y * 16;
+  if (j0 >= live_cols(cnt, max_out)) return;   // uniform: the whole workgroup leaves
   const int nl = n0 + 4 * lane;
   unsigned q[4];
 #pragma unroll
@@ -283,29 +305,33 @@ __global__ void __launch_bounds__(256) llm_int8_gather_wt_kernel(
 }
 
 int launch_llm_int8_gather_w(bf16* w_out, const int8_t* wq, const float* ws, const long* idx,
-                             const float* sel, int N, int K, int max_out, hipStream_t stream) {
-  const long total = (long)N * max_out;
-  if (total == 0) return 0;
+                             const float* sel, int N, int K, int max_out, hipStream_t stream,
+                             const int* cnt) {
+  if (N < 0 || max_out < 0) return -1;
+  if ((long)N * max_out == 0) return 0;
+  const long total = (long)((max_out + 31) / 32) * N * 32;
   llm_int8_gather_w_kernel<<<(int)((total + 255) / 256), 256, 0, stream>>>(w_out, wq, ws, idx, sel,
-                                                                          N, K, max_out);
+                                                                          N, K, max_out, cnt);
   return 0;
 }
 
 int launch_llm_int8_gather_wt(bf16* w_out, const int8_t* wqT, const float* ws, const long* idx,
-                              const float* sel, int N, int max_out, hipStream_t stream) {
+                              const float* sel, int N, int max_out, hipStream_t stream,
+                              const int* cnt) {
   if (N % 4 != 0) return -1;
   if ((long)N * max_out == 0) return 0;
   dim3 grid((N + 255) / 256, (max_out + 15) / 16);
-  llm_int8_gather_wt_kernel<<<grid, 256, 0, stream>>>(w_out, wqT, ws, idx, sel, N, max_out);
+  llm_int8_gather_wt_kernel<<<grid, 256, 0, stream>>>(w_out, wqT, ws, idx, sel, N, max_out, cnt);
   return 0;
 }
 
 int launch_llm_int8_gather_x(bf16* x_out, const bf16* x, const long* idx, const float* sel, int M,
-                             int K, int max_out, hipStream_t stream) {
-  const long total = (long)M * max_out;
-  if (total == 0) return 0;
+                             int K, int max_out, hipStream_t stream, const int* cnt) {
+  if (M < 0 || max_out < 0) return -1;
+  if ((long)M * max_out == 0) return 0;
+  const long total = (long)((max_out + 31) / 32) * M * 32;
   llm_int8_gather_x_kernel<<<(int)((total + 255) / 256), 256, 0, stream>>>(x_out, x, idx, sel, M,
-                                                                          K, max_out);
+                                                                          K, max_out, cnt);
   return 0;
 }
 

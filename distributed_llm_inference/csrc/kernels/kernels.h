@@ -85,7 +85,8 @@ int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale
                      const float* b_scale, float* workspace, int M, int N, int K, int splits,
                      int epilogue, int precision, hipStream_t stream,
                      const bf16* x_out = nullptr, const bf16* w_out = nullptr, int J = 0,
-                     const uint8_t* a_mx = nullptr, uint8_t* out_mx = nullptr);
+                     const uint8_t* a_mx = nullptr, uint8_t* out_mx = nullptr,
+                     const int* ol_cnt = nullptr);
 // C[MN] (bf16) = sum over `splits` fp32 partial products parts[splits][MN]
 int launch_splitk_reduce(bf16* C, const float* parts, int splits, size_t MN, hipStream_t stream);
 // fp32 elements of the workspace gemm_tile needs for splits == 0 (stream-K tail) on this device
@@ -101,13 +102,17 @@ int launch_quant_rowwise_int8(int8_t* q, float* scale, const bf16* x, const uint
 // LLM.int8 outlier bookkeeping (int8_outlier.hip)
 int launch_llm_int8_colmax(float* colmax, const bf16* x, int rows, int K, hipStream_t stream);
 int launch_llm_int8_select(const float* colmax, int K, float threshold, int max_out, long* idx,
-                           float* sel, uint8_t* flags, hipStream_t stream);
+                           float* sel, uint8_t* flags, hipStream_t stream, int* cnt = nullptr);
+// gathers: `cnt` (optional, written by the select kernel) = only the first ceil(cnt / 32) * 32
+// columns are written (the rest keep stale data: for consumers that read no further)
 int launch_llm_int8_gather_w(bf16* w_out, const int8_t* wq, const float* ws, const long* idx,
-                             const float* sel, int N, int K, int max_out, hipStream_t stream);
+                             const float* sel, int N, int K, int max_out, hipStream_t stream,
+                             const int* cnt = nullptr);
 int launch_llm_int8_gather_wt(bf16* w_out, const int8_t* wqT, const float* ws, const long* idx,
-                              const float* sel, int N, int max_out, hipStream_t stream);
+                              const float* sel, int N, int max_out, hipStream_t stream,
+                              const int* cnt = nullptr);
 int launch_llm_int8_gather_x(bf16* x_out, const bf16* x, const long* idx, const float* sel, int M,
-                             int K, int max_out, hipStream_t stream);
+                             int K, int max_out, hipStream_t stream, const int* cnt = nullptr);
 int launch_silu_mul_quant(uint8_t* q, float* scale, const bf16* x, int rows, int inter,
                           hipStream_t stream);
 

@@ -553,6 +553,8 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
     N = wq.shape[0]
     outl = None   # (x_out [M, J], w_out [N, J]) bf16: the outlier product
     flags = None
+    ol_cnt = None   # device int32 [1]: outlier columns kept (dynamic gathers, fused epilogue)
+    tile_ok = _gpu(x) and N % 256 == 0 and K % 128 == 0 and M > 0
     if threshold > 0 and M > 0:
         J = min(max_outliers, K)
         # int8_outlier.hip: colmax / radix select / two gathers (select: K <= 1024 x 32 columns;
@@ -560,8 +562,14 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
         if _gpu(x) and K % 8 == 0 and K <= LLM_INT8_SELECT_MAX_K:
             if wq_t is not None and N % 4 != 0:
                 wq_t = None
-            flags, xo, wo = native().llm_int8_outliers(x.contiguous(), wq, ws.float().contiguous(),
-                                                       float(threshold), int(J), wq_t)
+            # fused epilogue: it reads only the ceil(cnt / 32) live 32-column chunks, so the
+            # gathers skip the rest (no outliers -> no gather traffic, no outlier MFMA steps)
+            dynamic = (tile_ok and int8_fused_outliers()
+                       and os.environ.get("DLI_INT8_DYNAMIC", "1") == "1")
+            flags, xo, wo, cnt = native().llm_int8_outliers(
+                x.contiguous(), wq, ws.float().contiguous(), float(threshold), int(J), wq_t,
+                dynamic)
+            ol_cnt = cnt if dynamic else None
         else:
             # same rule as the kernel: |x| >= threshold; above J such columns, strictly above
             # the (J+1)-th largest column maximum (ties at that cut dropped)
@@ -582,7 +590,7 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
             wo = (wq.index_select(1, idx).float() * ws[:, None] * sel).to(x.dtype)
         outl = (xo, wo)
     xq, xs = quant_rowwise_int8(x, flags)
-    if _gpu(x) and N % 256 == 0 and K % 128 == 0 and M > 0:
+    if tile_ok:
         sp = tile_gemm_splits(max(M, TILE_GEMM_MIN_M), N, K, elem_bytes=1) or 1
         if swiglu:
             sp = 1
@@ -608,15 +616,18 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
                 and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
             if fp8_bf16_partials():   # bf16 partials (epilogue 4), as on the fp8 path
                 parts = torch.empty(sp, M, N, dtype=torch.bfloat16, device=x.device)
-                native().gemm_tile(parts, xq, wq, int(sp), 4, None, xs, ws, xo, wo)
+                native().gemm_tile(parts, xq, wq, int(sp), 4, None, xs, ws, xo, wo,
+                                   ol_cnt=ol_cnt)
                 return SplitKPartials(parts)
             parts = torch.empty(sp, M, N, dtype=torch.float32, device=x.device)
             dummy = torch.empty(M, 0, dtype=torch.bfloat16, device=x.device)   # C is unused
-            native().gemm_tile(dummy, xq, wq, int(sp), 1, parts.view(-1), xs, ws, xo, wo)
+            native().gemm_tile(dummy, xq, wq, int(sp), 1, parts.view(-1), xs, ws, xo, wo,
+                               ol_cnt=ol_cnt)
             return SplitKPartials(parts)
         y = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
         ws_ = torch.empty(sp * M * N, dtype=torch.float32, device=x.device) if sp > 1 else None
-        native().gemm_tile(y, xq, wq, int(sp), 2 if swiglu else 0, ws_, xs, ws, xo, wo)
+        native().gemm_tile(y, xq, wq, int(sp), 2 if swiglu else 0, ws_, xs, ws, xo, wo,
+                           ol_cnt=ol_cnt)
         return y
     # CPU / untileable shapes: dequantised reference
     y = (xq.float() * xs[:, None]) @ (wq.float() * ws[:, None]).t()

@@ -263,6 +263,34 @@ def test_llm_int8_fused_outlier_epilogue_swiglu_and_partials(gpu, M, K, N, n_out
     assert ((h - href).norm() / href.norm()).item() < 1e-2
 
 
+def test_llm_int8_dynamic_outlier_chunks_ignore_stale_columns(gpu):
+    """The fused path gathers only the live 32-column outlier chunks and the epilogue multiplies
+    only those: a product with few outliers right after one with many (same shapes, so the
+    caching allocator hands back buffers still holding the previous call's columns) and one with
+    none must match the CPU reference, for the store, split-K partial and SwiGLU epilogues."""
+    M, K, N = 256, 4096, 1024
+    torch.manual_seed(7)
+    w = (torch.randn(N, K) / K ** 0.5).to(torch.bfloat16)
+    wq, ws = ops.quantize_weight_int8(w)
+    wqg, wsg = wq.to(gpu), ws.to(gpu)
+    wqi = ops.swiglu_interleave(wqg)
+    wsi = ops.swiglu_interleave(wsg.reshape(-1, 1)).reshape(-1)
+    for n_out in (70, 3, 40, 0, 64):
+        x = torch.randn(M, K)
+        if n_out:
+            x[:, torch.randperm(K)[:n_out]] *= 40.0
+        xb = x.to(torch.bfloat16)
+        ref = ops.llm_int8_linear(xb, wq, ws, 6.0).float()
+        y = ops.llm_int8_linear(xb.to(gpu), wqg, wsg, 6.0).float().cpu()
+        assert ((y - ref).norm() / ref.norm()).item() < 5e-3, n_out
+        p = ops.llm_int8_linear(xb.to(gpu), wqg, wsg, 6.0, defer_reduce=True)
+        yp = p.parts.float().sum(0).cpu() if isinstance(p, ops.SplitKPartials) else p.float().cpu()
+        assert ((yp - ref).norm() / ref.norm()).item() < 5e-3, n_out
+        h = ops.llm_int8_linear(xb.to(gpu), wqi, wsi, 6.0, swiglu=True).float().cpu()
+        href = ops.silu_mul(ref.to(torch.bfloat16)).float()
+        assert ((h - href).norm() / href.norm()).item() < 1e-2, n_out
+
+
 def _llm_int8_outliers_ref(x, wq, ws, threshold, J):
     """fp32 PyTorch reference of int8_outlier.hip: the <= J largest column maxima above
     `threshold` (distinct values), in column order, padded with (column 0, weight 0)."""
@@ -298,16 +326,24 @@ def test_llm_int8_outlier_kernels_match_reference(gpu, K, n_out, M):
     xb[torch.randint(0, M, (n_out,)), cols] = planted
     wq = torch.randint(-127, 128, (N, K), dtype=torch.int8)
     ws = torch.rand(N) * 0.01 + 1e-3
-    flags, xo, wo = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J)
+    flags, xo, wo, cnt = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J)
     rf, rx, rw = _llm_int8_outliers_ref(xb, wq, ws, 6.0, J)
-    assert int(flags.sum()) == min(n_out, J)
+    assert int(flags.sum()) == min(n_out, J) == int(cnt.item())
     assert torch.equal(flags.cpu(), rf)
     assert torch.equal(xo.cpu(), rx)
     assert torch.equal(wo.cpu(), rw)
     # the coalesced gather from the transposed weight copy gives the same bits
     wq_t = wq.t().contiguous().to(gpu)
-    _, _, wo_t = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J, wq_t)
+    _, _, wo_t, _ = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J, wq_t)
     assert torch.equal(wo_t.cpu(), rw)
+    # dynamic: only the live 32-column chunks are written, and those bit-exactly
+    live = min(J, (min(n_out, J) + 31) // 32 * 32)
+    for wt in (None, wq_t):
+        _, xd, wd, c = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J,
+                                                      wt, True)
+        assert int(c.item()) == min(n_out, J)
+        assert torch.equal(xd[:, :live].cpu(), rx[:, :live])
+        assert torch.equal(wd[:, :live].cpu(), rw[:, :live])
 
 
 # the transposed-copy gather's tails: partial 16-column blocks / max_out % 8 != 0 and partial
@@ -324,7 +360,7 @@ def test_llm_int8_gather_wt_tails(gpu, N, J):
     ws = torch.rand(N) * 0.01 + 1e-3
     _, _, rw = _llm_int8_outliers_ref(xb, wq, ws, 6.0, J)
     wq_t = wq.t().contiguous().to(gpu)
-    _, _, wo_t = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J, wq_t)
+    _, _, wo_t, _ = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J, wq_t)
     assert torch.equal(wo_t.cpu(), rw)
 
 
@@ -336,7 +372,7 @@ def test_llm_int8_threshold_is_inclusive_and_cpu_gpu_agree(gpu):
     xb[5, 900] = -7.5
     wq = torch.randint(-127, 128, (N, K), dtype=torch.int8)
     ws = torch.rand(N) * 0.01 + 1e-3
-    fg, _, _ = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, 64)
+    fg, _, _, _ = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, 64)
     assert fg.cpu()[17] == 1 and fg.cpu()[900] == 1 and int(fg.sum()) == 2
     y_cpu = ops.llm_int8_linear(xb, wq, ws, 6.0).float()
     y_gpu = ops.llm_int8_linear(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0).float().cpu()
