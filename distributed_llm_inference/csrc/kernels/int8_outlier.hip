@@ -115,7 +115,7 @@ __global__ void __launch_bounds__(kSelThreads) llm_int8_select_kernel(
   __shared__ int red[kSelThreads / 64];
   __shared__ int hist[256];
   __shared__ unsigned s_prefix;
-  __shared__ int s_rank;
+  __shared__ int s_rank, s_bincnt;
   const int per = (K + kSelThreads - 1) / kSelThreads;
   const int k0 = threadIdx.x * per, n_mine = max(0, min(per, K - k0));
   unsigned v[kSelMaxPer];   // padding = +0.0, never above a positive cut
@@ -181,12 +181,21 @@ __global__ void __launch_bounds__(kSelThreads) llm_int8_select_kernel(
           for (; q < 3 && cum + h[q] < r; ++q) cum += h[q];
           s_prefix = prefix | ((unsigned)(255 - 4 * l - q) << shift);
           s_rank = r - cum;
+          s_bincnt = h[q];
         }
       }
       __syncthreads();
       prefix = s_prefix;
       r = s_rank;
+      const int bincnt = s_bincnt;
       __syncthreads();
+      if (bincnt == 1) {
+        // the located value is the only one with this prefix: every value above it has a larger
+        // prefix, so cutting at prefix | (unresolved bits all ones) keeps exactly the same set
+        // (and there is no tie to drop) -- the remaining passes are skipped
+        prefix |= (1u << shift) - 1u;
+        break;
+      }
     }
     t = prefix;
   }

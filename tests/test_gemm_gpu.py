@@ -346,6 +346,26 @@ def test_llm_int8_outlier_kernels_match_reference(gpu, K, n_out, M):
         assert torch.equal(wd[:, :live].cpu(), rw[:, :live])
 
 
+def test_llm_int8_select_ties_at_the_cut_and_early_exit(gpu):
+    """More than J columns pass the threshold: distinct maxima end the radix select early (the
+    located value alone in its bin), tied maxima at the cut run every pass and drop the whole tie;
+    both must pick the reference's set exactly."""
+    K, M, N, J = 4096, 64, 256, 64
+    wq = torch.randint(-127, 128, (N, K), dtype=torch.int8)
+    ws = torch.rand(N) * 0.01 + 1e-3
+    for vals in ([9.0] * 40 + [8.0] * 60, [float(v) for v in torch.linspace(7.0, 500.0, 150)],
+                 [7.5] * 100):
+        torch.manual_seed(len(vals))
+        xb = (torch.randn(M, K) * 0.5).to(torch.bfloat16)
+        cols = torch.randperm(K)[:len(vals)]
+        xb[torch.randint(0, M, (len(vals),)), cols] = torch.tensor(vals).to(torch.bfloat16)
+        flags, xo, wo, cnt = ops.native().llm_int8_outliers(xb.to(gpu), wq.to(gpu), ws.to(gpu), 6.0, J)
+        rf, rx, rw = _llm_int8_outliers_ref(xb, wq, ws, 6.0, J)
+        assert torch.equal(flags.cpu(), rf), vals[:3]
+        assert int(cnt.item()) == int(rf.sum())
+        assert torch.equal(xo.cpu(), rx) and torch.equal(wo.cpu(), rw)
+
+
 # the transposed-copy gather's tails: partial 16-column blocks / max_out % 8 != 0 and partial
 # 256-row n-tiles (N % 256 != 0), bit-exact against the reference
 @pytest.mark.parametrize("N,J", [(260, 20), (1028, 40), (512, 64)])
