@@ -122,6 +122,21 @@ def _compile_many(jobs, verbose: bool, workers: int) -> None:
             f.result()
 
 
+def _check_own_symbols(so: str) -> None:
+    """A shared object may link with undefined symbols; one of our own (namespace ``dli``) left
+    undefined means a launcher was declared but not compiled in, and would only fail at import on
+    the GPU box -- fail the build here instead."""
+    nm = shutil.which("nm") or os.path.join(ROCM, "lib", "llvm", "bin", "llvm-nm")
+    if not os.path.exists(nm):
+        return
+    r = subprocess.run([nm, "-D", "--undefined-only", "-C", so], capture_output=True, text=True)
+    missing = [l.split(None, 1)[-1] for l in r.stdout.splitlines() if " dli::" in f" {l.split(None, 1)[-1]}"]
+    if missing:
+        os.remove(so)
+        raise RuntimeError("native kernels: undefined dli symbols (declared, never defined): "
+                           + "; ".join(missing[:8]))
+
+
 def build_kernels(force: bool = False, verbose: bool = False, workers: Optional[int] = None) -> str:
     """Compile the gfx950 kernels + torch bindings into ``_C``; returns the .so path."""
     hipcc = shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
@@ -149,6 +164,7 @@ def build_kernels(force: bool = False, verbose: bool = False, workers: Optional[
     _compile_many(jobs, verbose, workers or min(8, os.cpu_count() or 4))
     tmp = out + ".tmp"
     _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs + ldflags, verbose)
+    _check_own_symbols(tmp)
     os.replace(tmp, out)
     _record(out, deps, ARCH)
     return out
