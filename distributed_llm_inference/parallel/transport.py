@@ -20,7 +20,7 @@ from __future__ import annotations
 import collections
 import os
 import time
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -150,6 +150,26 @@ class LoopbackTransport(Transport):
         return x
 
 
+def connect_plan(rank: int, world: int, head_pairs: bool) -> List[tuple]:
+    """The P2P operations ``RcclTransport._connect`` issues on ``rank``, in order, as
+    ``(op, comm kind, peer)``: receive from the previous stage, send to the next, then (rotating
+    head) the last stage sends to every other rank in increasing order while each of them
+    receives once.  Each is blocking until the peer posts its match, so the plans of all ranks
+    must resolve without a cycle (``tests/test_runtime_cpu.py`` simulates every world size)."""
+    ops: List[tuple] = []
+    if rank > 0:
+        ops.append(("recv", "stage", rank - 1))
+    if rank < world - 1:
+        ops.append(("send", "stage", rank + 1))
+    if head_pairs and world > 1:
+        last = world - 1
+        if rank == last:
+            ops += [("send", "head", r) for r in range(world - 1)]
+        else:
+            ops.append(("recv", "head", last))
+    return ops
+
+
 class RcclTransport(Transport):
     """RCCL P2P over xGMI with dedicated send/recv streams (see module docstring)."""
 
@@ -216,16 +236,12 @@ class RcclTransport(Transport):
         t0 = time.perf_counter()
         probe = torch.zeros(64, dtype=torch.bfloat16, device=self.device)
         with torch.cuda.device(self.device):
-            if self.rank > 0:
-                self._comm(self.rank - 1).recv(probe, 0, self.recv_stream.cuda_stream)
-            if self.rank < self.world - 1:
-                self._comm(self.rank + 1).send(probe, 1, self.send_stream.cuda_stream)
-            last = self.world - 1
-            for r in sorted(self._hcomms):
-                if self.rank == last:
-                    self._hcomms[r].send(probe, 1, self.send_stream.cuda_stream)
+            for op, kind, peer in connect_plan(self.rank, self.world, bool(self._hcomms)):
+                comm = self._comm(peer) if kind == "stage" else self._hcomms[peer]
+                if op == "send":   # index of the receiving end inside the 2-rank communicator
+                    comm.send(probe, 1, self.send_stream.cuda_stream)
                 else:
-                    self._hcomms[r].recv(probe, 0, self.recv_stream.cuda_stream)
+                    comm.recv(probe, 0, self.recv_stream.cuda_stream)
             self.send_stream.synchronize()
             self.recv_stream.synchronize()
         return (time.perf_counter() - t0) * 1e3

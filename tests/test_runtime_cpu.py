@@ -442,3 +442,37 @@ def test_swiglu_interleave_roundtrip_and_tile_splits():
     assert ops.tile_gemm_splits(64, 8192, 8192) == 0      # too few rows
     assert ops.tile_gemm_splits(512, 100, 8192) == 0      # N not a multiple of 256
     assert ops.tile_gemm_splits(512, 128256, 8192) == 0   # LM head stays on hipBLASLt
+
+
+@pytest.mark.parametrize("head", [False, True])
+def test_rccl_connect_plan_resolves_without_a_cycle(head):
+    """RcclTransport brings every P2P link up at init with blocking, matched send/recv pairs
+    (parallel/transport.py connect_plan).  Simulate all ranks for every world size up to 16: each
+    op completes only when the peer's current op is its match; every rank must finish, and every
+    link the runtime uses (stage i -> i+1, head last -> r) must be connected exactly once."""
+    from distributed_llm_inference.parallel.transport import connect_plan
+    for world in range(1, 17):
+        plans = [connect_plan(r, world, head) for r in range(world)]
+        pos = [0] * world
+        links = []
+        progress = True
+        while progress:
+            progress = False
+            for r in range(world):
+                if pos[r] >= len(plans[r]):
+                    continue
+                op, kind, peer = plans[r][pos[r]]
+                if pos[peer] >= len(plans[peer]):
+                    continue
+                pop, pkind, ppeer = plans[peer][pos[peer]]
+                if ppeer == r and pkind == kind and {op, pop} == {"send", "recv"}:
+                    src, dst = (r, peer) if op == "send" else (peer, r)
+                    links.append((kind, src, dst))
+                    pos[r] += 1
+                    pos[peer] += 1
+                    progress = True
+        assert all(pos[r] == len(plans[r]) for r in range(world)), (world, head, pos)
+        want = [("stage", i, i + 1) for i in range(world - 1)]
+        if head and world > 1:
+            want += [("head", world - 1, r) for r in range(world - 1)]
+        assert sorted(links) == sorted(want), (world, head)
