@@ -100,9 +100,11 @@ def test_shm_channel_broadcast_multiprocess():
     for p in ps:
         p.start()
     msgs = [f"m{i}".encode() * (i % 5 + 1) for i in range(50)]
-    for m in msgs:  # more messages than slots: exercises back-pressure
-        prod.send(m, 10.0)
-    res = dict(q.get(timeout=30) for _ in ps)
+    # more messages than slots: exercises back-pressure.  Generous timeouts: the spawned
+    # consumers import this module (and torch) before they attach, slow on a loaded machine
+    for m in msgs:
+        prod.send(m, 180.0)
+    res = dict(q.get(timeout=240) for _ in ps)
     for p in ps:
         p.join(10)
     assert res[0] == msgs and res[1] == msgs
