@@ -305,7 +305,7 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
                  Tensor block_tables, Tensor seq_lens, double scale, int64_t n_sink,
                  int64_t sink_pad, int64_t ring, int64_t window, int64_t num_splits,
                  optional<Tensor> part_o, optional<Tensor> part_ml, double k_scale,
-                 double v_scale) {
+                 double v_scale, optional<Tensor> out_q, optional<Tensor> out_mx) {
   int64_t D = 0;
   auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
                        sink_pad, ring, window, k_scale, v_scale, D);
@@ -313,6 +313,17 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
   TORCH_CHECK(seq_lens.numel() == B, "decode: one token per sequence (seq_lens must have T entries)");
   TORCH_CHECK(num_splits >= 1, "num_splits >= 1");
   p.num_splits = (int)num_splits;
+  TORCH_CHECK(out_q.has_value() == out_mx.has_value(), "attn_decode: out_q and out_mx go together");
+  if (out_q.has_value()) {   // MX fp8 output for the fp8 O projection
+    CHECK_IN(*out_q); CHECK_IN(*out_mx);
+    TORCH_CHECK(D == 128 && num_splits == 1, "attn_decode: MX output needs head_dim 128, one split");
+    TORCH_CHECK(out_q->element_size() == 1 && out_q->numel() == B * p.nh * D,
+                "attn_decode: out_q = fp8 [T, nh * D]");
+    TORCH_CHECK(out_mx->element_size() == 1 && out_mx->numel() == p.nh * ((B + 63) / 64) * 64,
+                "attn_decode: out_mx = e8m0 [nh][ceil(T / 64) * 64]");
+    p.out_q = static_cast<uint8_t*>(out_q->data_ptr());
+    p.out_mx = static_cast<uint8_t*>(out_mx->data_ptr());
+  }
   if (num_splits > 1) {
     TORCH_CHECK(part_o.has_value() && part_ml.has_value(), "split-K needs workspaces");
     CHECK_IN(*part_o); CHECK_IN(*part_ml); CHECK_F32(*part_o); CHECK_F32(*part_ml);
@@ -683,7 +694,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("q"), py::arg("q_sink"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("block_tables"), py::arg("seq_lens"), py::arg("scale"), py::arg("n_sink"),
         py::arg("sink_pad"), py::arg("ring"), py::arg("window"), py::arg("num_splits"),
-        py::arg("part_o"), py::arg("part_ml"), py::arg("k_scale"), py::arg("v_scale"));
+        py::arg("part_o"), py::arg("part_ml"), py::arg("k_scale"), py::arg("v_scale"),
+        py::arg("out_q") = py::none(), py::arg("out_mx") = py::none());
   m.def("attn_prefill", &attn_prefill, "paged causal prefill attention (varlen)");
   m.def("sample", &sample, "greedy / temperature / top-k / top-p sampling", py::arg("out_tokens"),
         py::arg("out_logprobs"), py::arg("logits"), py::arg("temperature"), py::arg("top_k"),

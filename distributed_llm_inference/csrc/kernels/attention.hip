@@ -434,6 +434,43 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
     const int head = kvh * G + g0 + col;
     if (splits == 1) {
       const float inv = lsum > 0.f ? vsc / lsum : 0.f;
+      if constexpr (D == 128) {
+        if (p.out_q != nullptr) {
+          // MX fp8 hand-off to the O projection (ops.attn_decode mx_out): the values the bf16
+          // store would write, one e8m0 scale per head row (= one 128-column block of O's
+          // input), amax over the 4 lanes holding the row (h4 = lane >> 4)
+          f32x4 vals[D / 16];
+          int dd[D / 16];
+          float a = 0.f;
+#pragma unroll
+          for (int u = 0; u < D / 16; ++u) {
+            f32x4 o;
+            o_unit<D, FP8>(st, u, h4, dd[u], o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              vals[u][r] = (float)(bf16)(o[r] * inv);
+              a = fmaxf(a, fabsf(vals[u][r]));
+            }
+          }
+          a = fmaxf(a, __shfl_xor(a, 16, 64));
+          a = fmaxf(a, __shfl_xor(a, 32, 64));
+          const int k = mx_exponent(a);
+          const float si = mx_inv_scale(k);
+          uint8_t* qrow = p.out_q + ((size_t)b * p.nh + head) * D;
+#pragma unroll
+          for (int u = 0; u < D / 16; ++u) {
+            const f32x4 v = vals[u] * si;
+            *reinterpret_cast<unsigned*>(qrow + dd[u]) = pack4_fp8(v[0], v[1], v[2], v[3]);
+          }
+          if (h4 == 0) {
+            const int nb = ((int)B + 63) / 64;
+            p.out_mx[mx_off(head, b, nb)] = (uint8_t)(k + 127);
+            if (b == (int)B - 1)   // padding rows of the last 64-row block: scale 2^0
+              for (int r = (int)B; r < nb * 64; ++r) p.out_mx[mx_off(head, r, nb)] = 127;
+          }
+          return;
+        }
+      }
       bf16* orow = p.out + ((size_t)b * p.nh + head) * D;
 #pragma unroll
       for (int u = 0; u < D / 16; ++u) {

@@ -173,6 +173,29 @@ __device__ __forceinline__ unsigned pack4_fp8(float a, float b, float c, float d
   return (unsigned)r;
 }
 
+// ---- MX (e8m0 block-scaled) fp8 activations: one power-of-two scale per (row, 128 columns) -----
+// Byte of (row r, 128-column block kt) at ((kt * nb + r / 64) * 64 + (r % 16) * 4 + (r % 64) / 16),
+// nb = ceil(M / 64): the 4 rows r0 + 16 i (i = 0..3) of one 64-row block that an MFMA lane
+// scales are one dword (gemm_tile.hip kFp8Mx reads them that way).  Rows in [M, 64 nb) hold 127.
+__device__ __forceinline__ size_t mx_off(int kt, int r, int nb) {
+  return ((size_t)kt * nb + (r >> 6)) * 64 + (r & 15) * 4 + ((r & 63) >> 4);
+}
+
+// the smallest k with amax / 2^k <= 448 (e4m3's largest finite value), clamped to e8m0's range;
+// the stored byte is k + 127 and the quantised value e4m3(x * 2^-k)  (ops.mx_quantize's rule)
+__device__ __forceinline__ int mx_exponent(float amax) {
+  int k = 0;
+  if (amax > 0.f) {
+    const unsigned bits = __float_as_uint(amax / 448.f);
+    k = (int)((bits >> 23) & 0xff) - 127 + ((bits & 0x7fffff) ? 1 : 0);
+    k = min(max(k, -126), 126);
+  }
+  return k;
+}
+__device__ __forceinline__ float mx_inv_scale(int k) {   // 2^-k, exact
+  return __uint_as_float((unsigned)(127 - k) << 23);
+}
+
 // 8 packed fp8 bytes -> 8 bf16 (exact: every e4m3 value is representable in bf16).  gfx950's
 // v_cvt_scalef32_pk_bf16_fp8 widens two bytes straight to packed bf16 (scale 1.0): 4 VALU ops per
 // 8 bytes instead of 4 fp8->f32 pairs + 4 f32->bf16 packs.

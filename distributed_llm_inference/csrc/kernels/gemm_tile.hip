@@ -125,12 +125,7 @@ __device__ __forceinline__ f32x4 mfma_fp8_mx(const bf16x8& a0, const bf16x8& a1,
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, SEL, sc);
 }
 
-// e8m0 activation scales (MX): byte of (row r, k-tile kt) at ((kt * nb + r / 64) * 64 +
-// (r % 16) * 4 + (r % 64) / 16), nb = ceil(M / 64): a lane's 4 rows r0 + 16 i (i = 0..3) of one
-// 64-row block are one dword
-__device__ __forceinline__ size_t mx_off(int kt, int r, int nb) {
-  return ((size_t)kt * nb + (r >> 6)) * 64 + (r & 15) * 4 + ((r & 63) >> 4);
-}
+// e8m0 activation scales (MX): common.h mx_off layout (a k-tile of 128 fp8 = one scale block)
 constexpr int kMxMaxKt = 64;             // k-tiles of scales a kFp8Mx workgroup keeps in LDS
 constexpr int kMxLds = kMxMaxKt * 256;   // [k-tile][256 tile rows] bytes
 
@@ -591,14 +586,8 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
         float a = 0.f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) a = fmaxf(a, red[(wr * 4 + w) * 128 + i * 16 + fr]);
-        // the smallest 2^k with amax / 2^k <= 448 (e4m3's largest finite value)
-        int k = 0;
-        if (a > 0.f) {
-          const unsigned bits = __float_as_uint(a / 448.f);
-          k = (int)((bits >> 23) & 0xff) - 127 + ((bits & 0x7fffff) ? 1 : 0);
-          k = min(max(k, -126), 126);
-        }
-        const float inv = __uint_as_float((unsigned)(127 - k) << 23);   // 2^-k, exact
+        const int k = mx_exponent(a);
+        const float inv = mx_inv_scale(k);
         if (row < M) {
 #pragma unroll
           for (int p = 0; p < 2; ++p) {

@@ -25,6 +25,10 @@ struct AttnParams {
   float* part_o;        // [splits, T, nh, D]     (decode, num_splits > 1)
   float* part_ml;       // [splits, T, nh, 2]
   int num_splits;
+  // decode, one split, D = 128: write the output as MX fp8 for the fp8 O projection instead of
+  // bf16 -- e4m3 bytes [T, nh * D] and one e8m0 scale per (token, head) in mx_off layout
+  uint8_t* out_q = nullptr;
+  uint8_t* out_mx = nullptr;
 };
 
 struct RopeCacheParams {

@@ -89,6 +89,21 @@ class LlamaAttention(nn.Module):
                                      meta.q_start, self.scale, meta.custom_mask,
                                      meta.k_scale, meta.v_scale)
         elif meta.is_decode:
+            op = self.o_proj
+            mx = (op.is_fp8 and op.bias is None and ops.fp8_mx_attn()
+                  and ops.attn_decode_mx_ok(self.head_dim, meta.num_splits))
+            if mx and q.is_cuda:
+                sp = ops.tile_gemm_splits_fp8(T, op.out_features, op.in_features)
+                mx = bool(sp) and ops.mx_tileable(op.in_features, sp)
+            if mx:
+                # fp8 O projection: the attention epilogue quantises its output itself (one e8m0
+                # scale per head row), consumed by the block-scaled MFMA -- no bf16 [T, nh*D]
+                # store and no per-row quantisation pass
+                o = ops.attn_decode(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
+                                    self.scale, meta.n_sink, meta.sink_pad, meta.ring, meta.window,
+                                    num_splits=meta.num_splits, workspace=meta.workspace,
+                                    k_scale=meta.k_scale, v_scale=meta.v_scale, mx_out=True)
+                return op(None, x_q=o, defer_reduce=defer_reduce)
             o = ops.attn_decode(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
                                 self.scale, meta.n_sink, meta.sink_pad, meta.ring, meta.window,
                                 num_splits=meta.num_splits, workspace=meta.workspace,

@@ -217,12 +217,37 @@ def decode_splits(batch: int, nkv: int, group: int, max_len: int, cu: int = 256,
     return 2 if s == 3 else s
 
 
+def attn_decode_mx_ok(head_dim: int, num_splits: int) -> bool:
+    """Whether :func:`attn_decode` can hand its output over as :class:`MxFp8` (one e8m0 scale
+    per head row = one 128-column block of the O projection's input; single-split decode)."""
+    return head_dim == 128 and num_splits == 1
+
+
 def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink=0, sink_pad=0,
-                ring=0, window=0, num_splits=1, workspace=None, out=None, k_scale=1.0, v_scale=1.0):
+                ring=0, window=0, num_splits=1, workspace=None, out=None, k_scale=1.0, v_scale=1.0,
+                mx_out: bool = False):
+    """Paged GQA decode attention -> bf16 ``[T, nh, D]``; ``mx_out`` (needs
+    :func:`attn_decode_mx_ok`): the same values (rounded to bf16) quantised in the kernel's
+    epilogue to :class:`MxFp8` ``[T, nh * D]`` for the fp8 O projection, replacing a separate
+    per-row quantisation pass."""
+    if mx_out and not attn_decode_mx_ok(q.shape[-1], num_splits):
+        raise ValueError("attn_decode(mx_out=True) needs head_dim 128 and one split")
     if not _gpu(q):
         y = ref.attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
                             sink_pad, ring, window, k_scale, v_scale)
+        if mx_out:
+            return mx_quantize(y.to(torch.bfloat16).reshape(q.shape[0], -1))
         return out.copy_(y) if out is not None else y
+    if mx_out:
+        T, nh, D = q.shape
+        nb = (T + 63) // 64
+        q8 = torch.empty(T, nh * D, dtype=torch.float8_e4m3fn, device=q.device)
+        sc = torch.empty(nh * nb * 64, dtype=torch.uint8, device=q.device)
+        dummy = torch.empty_like(q) if out is None else out   # shape-checked, not written
+        native().attn_decode(dummy, q, q_sink, k_cache, v_cache, block_tables, seq_lens,
+                             float(scale), int(n_sink), int(sink_pad), int(ring), int(window), 1,
+                             None, None, float(k_scale), float(v_scale), q8, sc)
+        return MxFp8(q8, sc)
     out = torch.empty_like(q) if out is None else out
     part_o = part_ml = None
     if num_splits > 1:
@@ -739,6 +764,13 @@ def fp8_mx() -> bool:
     projection as :class:`MxFp8` (no separate per-row quantisation pass over h); ``0`` keeps the
     bf16 h + per-row quantiser path."""
     return os.environ.get("DLI_FP8_MX", "1") != "0"
+
+
+def fp8_mx_attn() -> bool:
+    """``DLI_FP8_MX_ATTN=1`` (default, with :func:`fp8_mx`): single-split decode attention hands
+    its output to the fp8 O projection as :class:`MxFp8` (quantised in the attention epilogue);
+    ``0`` keeps the bf16 output + per-row quantiser."""
+    return fp8_mx() and os.environ.get("DLI_FP8_MX_ATTN", "1") != "0"
 
 
 MX_MAX_KTILES = 64   # k-tiles of scales one kFp8Mx workgroup keeps in LDS (gemm_tile.hip kMxMaxKt)

@@ -446,6 +446,43 @@ def test_attn_decode_fp8_kv(gpu, splits, D):
     _close(out, out_r, 2e-2, 2e-2, "decode-fp8")
 
 
+@pytest.mark.parametrize("B", [5, 64, 130])
+@pytest.mark.parametrize("kv_fp8", [False, True])
+def test_attn_decode_mx_output_bit_exact(gpu, B, kv_fp8):
+    """attn_decode(mx_out=True): the epilogue's MX fp8 hand-off (one e8m0 scale per head row)
+    equals ops.mx_quantize of the bf16 output bit for bit, incl. the padding-row scales."""
+    torch.manual_seed(B)
+    nh, nkv, D, bs = 16, 4, 128, 64
+    lens = torch.randint(1, 700, (B,), dtype=torch.int32)
+    nblk = int(((lens + bs - 1) // bs).sum()) + 1
+    q = (torch.randn(B, nh, D) * 2.0).to(torch.bfloat16).to(gpu)
+    kc = (torch.randn(nblk, nkv, bs, D) * 0.5)
+    vc = (torch.randn(nblk, nkv, bs // 8, D, 8) * 3.0)
+    ks = vs = 1.0
+    if kv_fp8:
+        ks, vs = 0.25, 0.5
+        kc = (kc / ks).to(torch.float8_e4m3fn)
+        vc = (vc / vs).to(torch.float8_e4m3fn)
+    else:
+        kc, vc = kc.to(torch.bfloat16), vc.to(torch.bfloat16)
+    kc, vc = kc.to(gpu), vc.to(gpu)
+    maxb = int(((lens + bs - 1) // bs).max())
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    nxt = 1
+    for b in range(B):
+        n = int((lens[b] + bs - 1) // bs)
+        bt[b, :n] = torch.arange(nxt, nxt + n)
+        nxt += n
+    bt, lens_g = bt.to(gpu), lens.to(gpu)
+    scale = D ** -0.5
+    ref_o = ops.attn_decode(q, None, kc, vc, bt, lens_g, scale, num_splits=1, k_scale=ks, v_scale=vs)
+    ref = ops.mx_quantize(ref_o.reshape(B, nh * D))
+    mx = ops.attn_decode(q, None, kc, vc, bt, lens_g, scale, num_splits=1, k_scale=ks, v_scale=vs,
+                         mx_out=True)
+    assert torch.equal(mx.sc.cpu(), ref.sc.cpu())
+    assert torch.equal(mx.q.view(torch.uint8).cpu(), ref.q.view(torch.uint8).cpu())
+
+
 @pytest.mark.parametrize("splits", [1, 4, 12])
 def test_attn_decode_fp8_kv_window_sinks(gpu, splits):
     """fp8 KV in StreamingLLM window mode: the sink segment is scored with q_sink, which must
