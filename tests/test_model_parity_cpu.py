@@ -136,6 +136,37 @@ def test_fp8_stage_close_to_bf16_cpu():
         assert ((x - y).norm() / x.norm()).item() < 0.1
 
 
+def test_fp8_stage_head_dim_128_uses_mx_attention_handoff_cpu(monkeypatch):
+    """head_dim 128 fp8 stages hand the single-split decode attention output to the O projection
+    as MX fp8 (the GPU attention epilogue's format; CPU: ops.mx_quantize of the bf16 output).
+    The MX and per-row paths agree closely, and both stay close to bf16."""
+    spec = ModelSpec(name="t128", vocab_size=300, hidden_size=256, intermediate_size=512,
+                     num_layers=2, num_heads=2, num_kv_heads=1, head_dim=128, rope_theta=10000.0,
+                     max_position_embeddings=2048)
+    assert ops.attn_decode_mx_ok(128, 1) and not ops.attn_decode_mx_ok(64, 1)
+    assert not ops.attn_decode_mx_ok(128, 4)
+    st = CausalLMStage(spec, 0, 2).init_random(5)
+    prompts = [[1, 2, 3, 4, 5, 6], [9, 8, 7]]
+    a = _run_stage(st, prompts, decode_steps=1)
+    st.quantize_fp8()
+    calls = []
+    real = ops.attn_decode
+
+    def spy(*args, **kw):
+        calls.append(kw.get("mx_out", False))
+        return real(*args, **kw)
+    monkeypatch.setattr(ops, "attn_decode", spy)
+    b = _run_stage(st, prompts, decode_steps=1)
+    assert calls and all(calls), calls           # every decode step took the MX hand-off
+    monkeypatch.setenv("DLI_FP8_MX_ATTN", "0")
+    calls.clear()
+    c = _run_stage(st, prompts, decode_steps=1)
+    assert calls and not any(calls)
+    for x, y, z in zip(a, b, c):   # (one decode step: later ones may sample different tokens)
+        assert ((x - y).norm() / x.norm()).item() < 0.15
+        assert ((y - z).norm() / z.norm()).item() < 0.1
+
+
 def test_mx_fp8_quantiser_layout_and_linear_cpu():
     """MX activations (fp8 + e8m0 per (row, 128-column block)): exponent layout, dequantisation
     error, and the Linear path that consumes them (CPU reference of gemm_tile.hip kFp8Mx)."""
