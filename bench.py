@@ -254,4 +254,13 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except BaseException as e:
+        # a failed rank ends every rank promptly, each printing its last pipeline op
+        # (distributed_llm_inference/runtime/watchdog.py); no-op for a single process
+        import traceback
+        traceback.print_exc()
+        from distributed_llm_inference.runtime.watchdog import abort_job
+        abort_job(f"bench.py: {type(e).__name__}: {e}")
+        raise

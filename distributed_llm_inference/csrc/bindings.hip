@@ -677,6 +677,7 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, optional<Tensor> bias) {
 }  // namespace
 
 void register_rccl(pybind11::module_& m);  // comm/rccl_p2p.hip
+void register_streams(pybind11::module_& m);  // comm/streams.hip
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "CDNA4 (gfx950) kernels of distributed_llm_inference";
@@ -726,4 +727,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("skinny_gemm", &skinny_gemm, "y = x . W^T (+ bias) for M <= 4 (weight-streaming GEMV)",
         py::arg("out"), py::arg("x"), py::arg("w"), py::arg("bias") = py::none());
   register_rccl(m);
+  register_streams(m);
 }

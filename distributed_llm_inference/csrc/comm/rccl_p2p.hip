@@ -46,7 +46,8 @@ ncclDataType_t to_nccl(const at::Tensor& t) {
 class RcclComm {
  public:
   RcclComm(const std::string& uid, int rank, int world, int device, double timeout_s)
-      : rank_(rank), world_(world), device_(device) {
+      : rank_(rank), world_(world), device_(device),
+        enqueue_timeout_s_(timeout_s < 60.0 ? timeout_s : 60.0) {
     TORCH_CHECK(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id size");
     ncclUniqueId id;
     memcpy(&id, uid.data(), sizeof(id));
@@ -135,7 +136,7 @@ class RcclComm {
   // A non-blocking communicator may return ncclInProgress from an enqueue call.
   void enq(ncclResult_t r, const char* what) {
     if (r == ncclInProgress) {
-      wait_ready(120.0, what);
+      wait_ready(enqueue_timeout_s_, what);
       return;
     }
     TORCH_CHECK(r == ncclSuccess, "RCCL error ", ncclGetErrorString(r), " in ", what);
@@ -147,6 +148,7 @@ class RcclComm {
   }
   ncclComm_t comm_ = nullptr;
   int rank_, world_, device_;
+  double enqueue_timeout_s_;
 };
 
 pybind11::bytes get_unique_id() {
@@ -169,7 +171,7 @@ void register_rccl(pybind11::module_& m) {
   pybind11::class_<RcclComm>(m, "RcclComm")
       .def(pybind11::init<const std::string&, int, int, int, double>(), pybind11::arg("uid"),
            pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("device"),
-           pybind11::arg("timeout_s") = 300.0)
+           pybind11::arg("timeout_s") = 120.0)
       .def("send", &RcclComm::send, pybind11::arg("t"), pybind11::arg("peer"),
            pybind11::arg("stream") = 0)
       .def("recv", &RcclComm::recv, pybind11::arg("t"), pybind11::arg("peer"),

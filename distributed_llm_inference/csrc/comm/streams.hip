@@ -1,0 +1,251 @@
+// Streams with a hardware queue of their own, device-side signal / wait primitives and
+// cross-process device memory (IPC) for the pipeline transports.
+//
+// Why this exists (round-2 verdict, "hardware-queue hazard"): a pipeline rank keeps kernels that
+// WAIT on other ranks (RCCL send/recv, the rotating head's receive) on side streams next to its
+// compute.  HIP multiplexes streams onto a small pool of HSA hardware queues per priority
+// (GPU_MAX_HW_QUEUES, 4 by default); AQL packets of one queue run in order, so a waiting kernel or
+// a cross-stream barrier packet that lands on the compute stream's queue stalls compute until the
+// peer arrives.  Streams created with a CU mask are given a queue of their own (never shared); with
+// the full mask they run on every CU like an ordinary stream.  ``tests/test_streams_gpu.py`` checks
+// the isolation on the hardware by spinning a kernel on each stream in turn and requiring every
+// other stream to make progress.
+//
+// The signal / wait kernels are the device half of the IPC transport (parallel/ipc_transport.py),
+// used where RCCL cannot run (several ranks on one GPU) and as the spin kernel of the isolation
+// test.  Every wait has a deadline: a peer that never arrives turns into a status word the host
+// reads (and a Python error), never a wave that spins forever.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+#define HIP_OK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    TORCH_CHECK(_e == hipSuccess, #expr, " failed: ", hipGetErrorString(_e));          \
+  } while (0)
+
+inline hipStream_t as_stream(int64_t s) {
+  return s ? reinterpret_cast<hipStream_t>(s)
+           : c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+}
+
+// ------------------------------------------------------------------------------------ streams
+// mode 0: ordinary non-blocking stream (shares the per-priority hardware-queue pool)
+// mode 1: full-CU-mask stream -> a hardware queue of its own
+int64_t stream_create(int device, int mode, int priority) {
+  int prev = 0;
+  HIP_OK(hipGetDevice(&prev));
+  HIP_OK(hipSetDevice(device));
+  hipStream_t s = nullptr;
+  if (mode == 1) {
+    hipDeviceProp_t p;
+    HIP_OK(hipGetDeviceProperties(&p, device));
+    const int ncu = p.multiProcessorCount;
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0xffffffffu);
+    if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
+    HIP_OK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  } else {
+    HIP_OK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority));
+  }
+  HIP_OK(hipSetDevice(prev));
+  return reinterpret_cast<int64_t>(s);
+}
+
+void stream_destroy(int64_t s) {
+  if (s) HIP_OK(hipStreamDestroy(reinterpret_cast<hipStream_t>(s)));
+}
+
+int64_t stream_cu_count(int64_t s) {
+  std::vector<uint32_t> mask(16, 0);
+  HIP_OK(hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(s), (uint32_t)mask.size(), mask.data()));
+  int64_t n = 0;
+  for (uint32_t m : mask) n += __builtin_popcount(m);
+  return n;
+}
+
+double wall_clock_hz(int device) {
+  int khz = 0;
+  HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device));
+  return khz * 1e3;
+}
+
+// ---------------------------------------------------------------------------------- kernels
+// One lane polls; the other lanes of the (single, 64-wide) wave only keep the launch shape legal.
+// ``status`` (host-mapped) receives ``code`` if the deadline passes; the wave always exits.
+__global__ void __launch_bounds__(64) wait_geq_kernel(const uint32_t* flag, uint32_t target,
+                                                      uint64_t max_ticks, uint32_t* status,
+                                                      uint32_t code) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
+    if ((uint64_t)(wall_clock64() - t0) > max_ticks) {
+      if (status) __hip_atomic_store(status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+
+// Release-store ``value`` (every write queued before this kernel on its stream has completed:
+// stream order + the system-scope release make the data visible before the flag).
+__global__ void __launch_bounds__(64) signal_kernel(uint32_t* flag, uint32_t value) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A trivial kernel for progress probes: out[0] += 1.
+__global__ void __launch_bounds__(64) touch_kernel(uint32_t* out) {
+  if (threadIdx.x == 0) out[0] += 1u;
+}
+
+void wait_geq(int64_t flag_ptr, int64_t target, double timeout_s, int64_t status_ptr, int64_t code,
+              int64_t stream, int device) {
+  TORCH_CHECK(flag_ptr != 0, "wait_geq: null flag");
+  TORCH_CHECK(timeout_s > 0 && timeout_s < 3600, "wait_geq: timeout must be in (0, 3600) s");
+  const uint64_t ticks = (uint64_t)(timeout_s * wall_clock_hz(device));
+  hipLaunchKernelGGL(wait_geq_kernel, dim3(1), dim3(64), 0, as_stream(stream),
+                     reinterpret_cast<const uint32_t*>(flag_ptr), (uint32_t)target, ticks,
+                     reinterpret_cast<uint32_t*>(status_ptr), (uint32_t)code);
+  HIP_OK(hipGetLastError());
+}
+
+void signal(int64_t flag_ptr, int64_t value, int64_t stream) {
+  TORCH_CHECK(flag_ptr != 0, "signal: null flag");
+  hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, as_stream(stream),
+                     reinterpret_cast<uint32_t*>(flag_ptr), (uint32_t)value);
+  HIP_OK(hipGetLastError());
+}
+
+void touch(at::Tensor out, int64_t stream) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kInt && out.numel() >= 1, "touch: int32 GPU tensor");
+  hipLaunchKernelGGL(touch_kernel, dim3(1), dim3(64), 0, as_stream(stream),
+                     reinterpret_cast<uint32_t*>(out.data_ptr()));
+  HIP_OK(hipGetLastError());
+}
+
+// ----------------------------------------------------------------------- host-mapped flag words
+// Coherent pinned host memory the GPU reads / writes directly: the host sets a flag the GPU
+// waits on (isolation test) and reads the status words wait kernels leave on a timeout.
+class HostWords {
+ public:
+  explicit HostWords(int64_t n) : n_(n) {
+    TORCH_CHECK(n > 0 && n <= (1 << 20), "HostWords: bad size");
+    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&h_), n * sizeof(uint32_t),
+                         hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+    std::memset(h_, 0, n * sizeof(uint32_t));
+    HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_), h_, 0));
+  }
+  ~HostWords() {
+    if (h_) (void)hipHostFree(h_);
+  }
+  void set(int64_t i, int64_t v) {
+    idx(i);
+    __atomic_store_n(h_ + i, (uint32_t)v, __ATOMIC_SEQ_CST);
+  }
+  int64_t get(int64_t i) const {
+    idx(i);
+    return __atomic_load_n(h_ + i, __ATOMIC_SEQ_CST);
+  }
+  int64_t dev_ptr(int64_t i) const {
+    idx(i);
+    return reinterpret_cast<int64_t>(d_ + i);
+  }
+  int64_t size() const { return n_; }
+
+ private:
+  void idx(int64_t i) const { TORCH_CHECK(i >= 0 && i < n_, "HostWords index out of range"); }
+  int64_t n_;
+  uint32_t* h_ = nullptr;
+  uint32_t* d_ = nullptr;
+};
+
+// ------------------------------------------------------------------------ IPC device memory
+// A device allocation of our own (hipMalloc, not the torch caching allocator) so its IPC handle
+// names exactly this buffer; the peer opens it and gets a pointer into the same memory.
+class IpcBuffer {
+ public:
+  IpcBuffer(int64_t nbytes, int device) : nbytes_(nbytes), device_(device), owner_(true) {
+    TORCH_CHECK(nbytes > 0, "IpcBuffer: size");
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, device));
+    HIP_OK(hipMalloc(&p_, nbytes));
+    HIP_OK(hipMemset(p_, 0, nbytes));
+  }
+  IpcBuffer(const std::string& handle, int64_t nbytes, int device)
+      : nbytes_(nbytes), device_(device), owner_(false) {
+    TORCH_CHECK(handle.size() == sizeof(hipIpcMemHandle_t), "IpcBuffer: bad handle size");
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle.data(), sizeof(h));
+    const c10::hip::HIPGuardMasqueradingAsCUDA g(c10::Device(c10::DeviceType::CUDA, device));
+    HIP_OK(hipIpcOpenMemHandle(&p_, h, hipIpcMemLazyEnablePeerAccess));
+  }
+  ~IpcBuffer() { close(); }
+  void close() {
+    if (!p_) return;
+    if (owner_) (void)hipFree(p_);
+    else (void)hipIpcCloseMemHandle(p_);
+    p_ = nullptr;
+  }
+  pybind11::bytes handle() const {
+    TORCH_CHECK(owner_ && p_, "IpcBuffer: only the owner exports a handle");
+    hipIpcMemHandle_t h;
+    HIP_OK(hipIpcGetMemHandle(&h, p_));
+    return pybind11::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  }
+  int64_t ptr() const { return reinterpret_cast<int64_t>(p_); }
+  int64_t nbytes() const { return nbytes_; }
+  // a non-owning tensor view [offset, offset + numel * itemsize) (the buffer must outlive it)
+  at::Tensor view(int64_t offset, std::vector<int64_t> shape, at::ScalarType dt) const {
+    TORCH_CHECK(p_, "IpcBuffer closed");
+    int64_t n = 1;
+    for (auto s : shape) n *= s;
+    const int64_t bytes = n * (int64_t)c10::elementSize(dt);
+    TORCH_CHECK(offset >= 0 && offset + bytes <= nbytes_, "IpcBuffer.view out of range");
+    auto opts = at::TensorOptions().dtype(dt).device(c10::Device(c10::DeviceType::CUDA, device_));
+    return torch::from_blob(static_cast<char*>(p_) + offset, shape, opts);
+  }
+
+ private:
+  void* p_ = nullptr;
+  int64_t nbytes_;
+  int device_;
+  bool owner_;
+};
+
+}  // namespace
+
+void register_streams(pybind11::module_& m) {
+  m.def("stream_create", &stream_create, pybind11::arg("device"), pybind11::arg("mode") = 1,
+        pybind11::arg("priority") = 0);
+  m.def("stream_destroy", &stream_destroy);
+  m.def("stream_cu_count", &stream_cu_count);
+  m.def("wall_clock_hz", &wall_clock_hz);
+  m.def("wait_geq", &wait_geq, pybind11::arg("flag_ptr"), pybind11::arg("target"),
+        pybind11::arg("timeout_s"), pybind11::arg("status_ptr"), pybind11::arg("code"),
+        pybind11::arg("stream"), pybind11::arg("device"));
+  m.def("signal", &signal, pybind11::arg("flag_ptr"), pybind11::arg("value"),
+        pybind11::arg("stream"));
+  m.def("touch", &touch, pybind11::arg("out"), pybind11::arg("stream") = 0);
+  pybind11::class_<HostWords>(m, "HostWords")
+      .def(pybind11::init<int64_t>())
+      .def("set", &HostWords::set)
+      .def("get", &HostWords::get)
+      .def("dev_ptr", &HostWords::dev_ptr)
+      .def("__len__", &HostWords::size);
+  pybind11::class_<IpcBuffer>(m, "IpcBuffer")
+      .def(pybind11::init<int64_t, int>(), pybind11::arg("nbytes"), pybind11::arg("device"))
+      .def(pybind11::init<const std::string&, int64_t, int>(), pybind11::arg("handle"),
+           pybind11::arg("nbytes"), pybind11::arg("device"))
+      .def("handle", &IpcBuffer::handle)
+      .def("close", &IpcBuffer::close)
+      .def("view", &IpcBuffer::view)
+      .def_property_readonly("ptr", &IpcBuffer::ptr)
+      .def_property_readonly("nbytes", &IpcBuffer::nbytes);
+}

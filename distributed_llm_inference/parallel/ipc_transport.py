@@ -1,0 +1,206 @@
+"""Device-side P2P transport over cross-process GPU memory (HIP IPC) with device signals.
+
+RCCL refuses two ranks on one device, so on a one-GPU box the multi-process pipeline used to run
+over the host-staged transport - which blocks the HOST on every receive and cannot carry the
+rotating LM head.  That left the production stream structure untested: kernels that wait on
+other ranks sitting on side streams next to compute, the head's deferred receive + graph replay on
+its own stream.  This transport reproduces that structure exactly, on one GPU or several:
+
+* every directed channel (stage r -> r+1, and last stage -> r for the rotating head) owns
+  ``slots`` message buffers in the RECEIVER's memory plus a ``ready`` word per slot next to them,
+  and a ``free`` word per slot in the SENDER's memory; both ends open the other's allocation with
+  ``hipIpcOpenMemHandle`` (handles exchanged through the job's TCP store);
+* message n uses slot s = n % slots, round u = n // slots.  Sender, on its send stream (after the
+  compute that produced the data): wait ``free[s] >= u`` -> copy into the peer's slot -> release
+  ``ready[s] = u + 1``.  Receiver, on its receive (or head) stream: wait ``ready[s] >= u + 1`` ->
+  copy out -> release ``free[s] = u + 1`` in the sender's memory;
+* the waits are spinning kernels (csrc/comm/streams.hip), like RCCL's: they hold their stream -
+  and, if it were shared, that stream's hardware queue - until the peer arrives.  That is the
+  point: the GPU tests run the real HeadJobs / executor stream schedule against them.  Each wait
+  has a deadline; an expired one leaves a code in a host-mapped status word and :meth:`check`
+  raises with the channel and message number, instead of a wave spinning forever.
+
+Not the production data plane on a multi-GPU node (RcclTransport is), but it works across GPUs
+as well (the copy then crosses xGMI).
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from .transport import Transport
+
+_FLAG_BYTES = 256   # ready / free words region (64 slots max)
+
+
+class _Channel:
+    def __init__(self, cid: int, kind: str, src: int, dst: int, slot_bytes: int, slots: int):
+        self.cid, self.kind, self.src, self.dst = cid, kind, src, dst
+        self.slot_bytes, self.slots = slot_bytes, slots
+        self.n = 0            # messages issued on this end
+        self.data = None      # receiver's slots (owned by the receiver, opened by the sender)
+        self.peer_flags = None  # the other end's flag words (ready at the receiver / free at the sender)
+        self.own = None       # this end's own allocation (kept alive)
+
+    def describe(self) -> str:
+        return f"{self.kind} {self.src}->{self.dst}"
+
+
+class IpcTransport(Transport):
+    """See module docstring.  ``max_bytes``: largest stage message (max tokens x hidden x 2)."""
+
+    supports_head = True
+
+    def __init__(self, store, rank: int, world: int, device: torch.device, streams,
+                 max_bytes: int, head_bytes: int = 0, prefix: str = "dli_ipc",
+                 timeout_s: float = 120.0, slots: int = 2, head_pairs: bool = False):
+        from .. import ops
+        C = ops.native()
+        self.C = C
+        self.rank, self.world, self.device = rank, world, device
+        self.idx = device.index if device.index is not None else torch.cuda.current_device()
+        self.streams = streams
+        self.send_stream = streams.send
+        self.recv_stream = streams.recv
+        self.timeout_s = float(os.environ.get("DLI_P2P_TIMEOUT_S", timeout_s))
+        self.status = C.HostWords(4)   # [0]: code of the first expired wait (0 = none)
+        self.prefix = prefix
+        self._ch: Dict[Tuple[str, int, int], _Channel] = {}
+        edges: List[Tuple[str, int, int, int]] = [("stage", r, r + 1, max_bytes)
+                                                   for r in range(world - 1)]
+        if head_pairs and world > 1:
+            edges += [("head", world - 1, r, head_bytes or max_bytes) for r in range(world - 1)]
+        # every rank publishes its side first, then opens the peers' (the store's get blocks)
+        mine = []
+        for cid, (kind, src, dst, nbytes) in enumerate(edges):
+            if rank not in (src, dst):
+                continue
+            slot_bytes = (int(nbytes) + 255) // 256 * 256
+            ch = _Channel(cid, kind, src, dst, slot_bytes, slots)
+            if rank == dst:   # receiver: slots + ready words
+                ch.own = C.IpcBuffer(slot_bytes * slots + _FLAG_BYTES, self.idx)
+                store.set(f"{prefix}/c{cid}/rx", bytes(ch.own.handle()))
+            else:             # sender: free words
+                ch.own = C.IpcBuffer(_FLAG_BYTES, self.idx)
+                store.set(f"{prefix}/c{cid}/tx", bytes(ch.own.handle()))
+            self._ch[(kind, src, dst)] = ch
+            mine.append(ch)
+        for ch in mine:
+            if rank == ch.dst:
+                h = store.get(f"{prefix}/c{ch.cid}/tx")
+                ch.peer_flags = C.IpcBuffer(bytes(h), _FLAG_BYTES, self.idx)      # sender's free
+            else:
+                h = store.get(f"{prefix}/c{ch.cid}/rx")
+                ch.data = C.IpcBuffer(bytes(h), ch.slot_bytes * ch.slots + _FLAG_BYTES, self.idx)
+        torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ protocol
+    def _flag(self, buf, offset_bytes: int, s: int) -> int:
+        return buf.ptr + offset_bytes + 4 * s
+
+    def _wait(self, ptr: int, target: int, code: int, stream) -> None:
+        self.C.wait_geq(ptr, target, self.timeout_s, self.status.dev_ptr(0), code,
+                        stream.cuda_stream, self.idx)
+
+    def _code(self, ch: _Channel, recv: bool) -> int:
+        return 1 + 2 * ch.cid + (1 if recv else 0)
+
+    def _send_on(self, ch: _Channel, t: torch.Tensor, stream) -> None:
+        nb = t.numel() * t.element_size()
+        if nb > ch.slot_bytes:
+            raise ValueError(f"IPC {ch.describe()}: message of {nb} B > slot of {ch.slot_bytes} B")
+        s, u = ch.n % ch.slots, ch.n // ch.slots
+        ch.n += 1
+        free_ptr = self._flag(ch.own, 0, s)                               # my free words
+        ready_ptr = self._flag(ch.data, ch.slot_bytes * ch.slots, s)      # peer's ready words
+        with torch.cuda.stream(stream):
+            self._wait(free_ptr, u, self._code(ch, False), stream)
+            dst = ch.data.view(s * ch.slot_bytes, [nb], torch.uint8)
+            dst.copy_(t.contiguous().view(-1).view(torch.uint8), non_blocking=True)
+            self.C.signal(ready_ptr, u + 1, stream.cuda_stream)
+
+    def _recv_on(self, ch: _Channel, t: torch.Tensor, stream) -> None:
+        nb = t.numel() * t.element_size()
+        if nb > ch.slot_bytes:
+            raise ValueError(f"IPC {ch.describe()}: message of {nb} B > slot of {ch.slot_bytes} B")
+        s, u = ch.n % ch.slots, ch.n // ch.slots
+        ch.n += 1
+        ready_ptr = self._flag(ch.own, ch.slot_bytes * ch.slots, s)       # my ready words
+        free_ptr = self._flag(ch.peer_flags, 0, s)                         # sender's free words
+        with torch.cuda.stream(stream):
+            self._wait(ready_ptr, u + 1, self._code(ch, True), stream)
+            src = ch.own.view(s * ch.slot_bytes, [nb], torch.uint8)
+            t.view(-1).view(torch.uint8).copy_(src, non_blocking=True)
+            self.C.signal(free_ptr, u + 1, stream.cuda_stream)
+
+    # ------------------------------------------------------------------ Transport API
+    def send(self, t: torch.Tensor, peer: int) -> None:
+        self.check()
+        cur = torch.cuda.current_stream(self.device)
+        self.send_stream.wait_stream(cur)
+        t.record_stream(self.send_stream)
+        self._send_on(self._ch[("stage", self.rank, peer)], t, self.send_stream)
+        self._count(t, True)
+
+    def recv(self, t: torch.Tensor, peer: int, free_event=None) -> torch.Tensor:
+        self.check()
+        cur = torch.cuda.current_stream(self.device)
+        if free_event is not None:
+            self.recv_stream.wait_event(free_event)
+        else:
+            self.recv_stream.wait_stream(cur)
+        t.record_stream(self.recv_stream)
+        self._recv_on(self._ch[("stage", peer, self.rank)], t, self.recv_stream)
+        cur.wait_stream(self.recv_stream)
+        self._count(t, False)
+        return t
+
+    def send_head(self, t: torch.Tensor, peer: int) -> None:
+        self.check()
+        cur = torch.cuda.current_stream(self.device)
+        self.send_stream.wait_stream(cur)
+        t.record_stream(self.send_stream)
+        self._send_on(self._ch[("head", self.rank, peer)], t, self.send_stream)
+        self._count(t, True)
+
+    def recv_head(self, t: torch.Tensor, peer: int, stream) -> torch.Tensor:
+        self.check()
+        self._recv_on(self._ch[("head", peer, self.rank)], t, stream)
+        self._count(t, False)
+        return t
+
+    def check(self) -> None:
+        """Raise if any device-side wait of this rank expired (a peer never arrived)."""
+        code = self.status.get(0)
+        if code:
+            cid, recv = (code - 1) // 2, (code - 1) % 2
+            ch = next((c for c in self._ch.values() if c.cid == cid), None)
+            what = ch.describe() if ch is not None else f"channel {cid}"
+            raise TimeoutError(f"[rank {self.rank}] IPC transport: {'receive' if recv else 'send'} "
+                               f"on {what} waited > {self.timeout_s} s for its peer")
+
+    def describe(self) -> dict:
+        return {"transport": "IpcTransport",
+                "channels": sorted(c.describe() for c in self._ch.values()),
+                "timeout_s": self.timeout_s}
+
+    def close(self) -> None:
+        if not self._ch:
+            return
+        torch.cuda.synchronize(self.device)
+        for ch in self._ch.values():
+            for b in (ch.data, ch.peer_flags):
+                if b is not None:
+                    b.close()
+        # owners free last (peers closed their mappings before the closing barrier)
+        for ch in self._ch.values():
+            ch.own.close()
+        self._ch.clear()
+
+    def abort(self) -> None:
+        """Leaving after a failure: no device synchronisation (a wait kernel may still be
+        spinning towards its deadline); the process exit releases the mappings."""
+        self._ch.clear()

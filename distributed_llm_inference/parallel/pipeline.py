@@ -41,6 +41,7 @@ from ..runtime.executor import StageExecutor, StepPlan
 from ..runtime.faults import FaultInjector, StageStats
 from ..runtime.scheduler import Scheduler
 from ..runtime.sequence import SamplingParams, Sequence as Seq
+from ..runtime.watchdog import TRACKER, abort_job, wait_event
 from .transport import LoopbackTransport, RcclTransport, TorchDistTransport, Transport
 
 log = logging.getLogger(__name__)
@@ -63,6 +64,13 @@ class DriverBase:
         self.collect_times: Dict[int, List[float]] = collections.defaultdict(list)
         self.tokens_generated = 0
         self.wait_s = 0.0  # host time blocked on results (the rest of a round is driver work)
+        self.streams = None  # runtime.streams.RankStreams of a multi-process rank
+
+    def activate_streams(self) -> None:
+        """Make this rank's compute stream current in the calling thread (a serving loop that
+        drives the pipeline from its own thread calls this first)."""
+        if self.streams is not None:
+            self.streams.activate()
 
     # -- to implement
     def _issue(self, plan: StepPlan) -> None:
@@ -235,7 +243,7 @@ class DistributedDriver(DriverBase):
     """Rank 0 of a multi-process pipeline."""
 
     def __init__(self, executor: StageExecutor, scheduler: Scheduler, transport: Transport,
-                 channels: _Channels, world: int, ctrl_group=None, timeout: float = 300.0,
+                 channels: _Channels, world: int, ctrl_group=None, timeout: float = 120.0,
                  policy=None, heads=None):
         super().__init__(scheduler)
         self.ex = executor
@@ -260,13 +268,16 @@ class DistributedDriver(DriverBase):
         self._head_results[plan.step] = (pinned, ev)
 
     def _issue(self, plan: StepPlan) -> None:
+        TRACKER.mark("ctrl-send", plan.step, plan.mb)
         self.ch.ctrl.send(msgpack.packb(plan.to_wire()), self.timeout)
         if plan.seq_ids and self.faults.active:
             self.faults.on_step()
         tok = self.stats.begin(self.faults.delay_ms) if plan.seq_ids else None
+        TRACKER.mark("execute", plan.step, plan.mb, stream="compute")
         out = self.ex.execute(plan, None)
         self.stats.end(tok)
         if plan.seq_ids:
+            TRACKER.mark("send", plan.step, plan.mb, peer=1, stream="send")
             self.tr.send(out, 1)
             if self.heads is not None:
                 self.heads.tick()
@@ -277,14 +288,15 @@ class DistributedDriver(DriverBase):
 
     def _collect(self, plan: StepPlan) -> List[int]:
         hr = self._head_rank(plan)
+        TRACKER.mark("collect", plan.step, plan.mb, peer=hr)
         if hr == 0:
             while plan.step not in self._head_results:
                 self.heads.poll(block=True)   # (enqueues any deferred GPU job first)
             pinned, ev = self._head_results.pop(plan.step)
-            if ev is not None:
-                ev.synchronize()
+            wait_event(ev, "local head tokens", plan.step, plan.mb)
             return pinned.tolist()
-        msg = msgpack.unpackb(self.ch.toks.get(hr, self.ch.tok).recv(self.timeout))
+        with TRACKER.waiting("tokens", plan.step, plan.mb, peer=hr):
+            msg = msgpack.unpackb(self.ch.toks.get(hr, self.ch.tok).recv(self.timeout))
         if msg["step"] != plan.step:
             raise RuntimeError(f"token stream of rank {hr} out of order: got step {msg['step']}, "
                                f"want {plan.step}")
@@ -309,12 +321,13 @@ class StageFollower:
     """Ranks 1..N-1: execute plans as they are published."""
 
     def __init__(self, executor: StageExecutor, transport: Transport, channels: _Channels,
-                 rank: int, world: int, ctrl_group=None, timeout: float = 300.0, policy=None,
+                 rank: int, world: int, ctrl_group=None, timeout: float = 120.0, policy=None,
                  heads=None):
         self.ex, self.tr, self.ch = executor, transport, channels
         self.rank, self.world = rank, world
         self.group = ctrl_group
         self.timeout = timeout
+        self.ctrl_timeout = float(os.environ.get("DLI_CTRL_TIMEOUT_S", "0"))
         self.is_last = rank == world - 1
         self.barrier_times: List[float] = []
         self.snapshots: List[dict] = []   # StageStats.snapshot() at every barrier
@@ -325,6 +338,7 @@ class StageFollower:
         self.heads = heads                # runtime.head.HeadJobs (rotating head, non-last ranks)
         self._pub_q: "queue.Queue" = queue.Queue()
         self._pub_thread = None
+        self.streams = None               # runtime.streams.RankStreams (GPU ranks)
         if self.is_last or heads is not None:
             self._start_publisher()
 
@@ -342,22 +356,27 @@ class StageFollower:
 
     def _next_msg(self) -> bytes:
         """The next control message; a CPU rank with queued head jobs keeps running them while it
-        waits (the driver may be waiting for exactly those tokens)."""
+        waits (the driver may be waiting for exactly those tokens).  Waiting for the driver is
+        idle time, not a stall (a serving pipeline can sit idle for hours): no deadline unless
+        ``DLI_CTRL_TIMEOUT_S`` sets one; a failed driver reaches this rank through the watchdog
+        (runtime/watchdog.py) or the launcher."""
+        TRACKER.mark("ctrl-wait")
+        idle = self.ctrl_timeout
         if self.heads is None:
-            return self.ch.ctrl.recv(self.timeout)
+            return self.ch.ctrl.recv(idle)
         if self.heads.gpu:
             if self.heads.deferred and not self.ch.ctrl.poll():
                 self.heads.flush()   # idle: the driver may be waiting for these tokens
-            return self.ch.ctrl.recv(self.timeout)
+            return self.ch.ctrl.recv(idle)
         t0 = time.perf_counter()
         while not self.ch.ctrl.poll():
             if self.heads.pending:
                 self.heads.run_oldest()   # idle: the driver may be waiting for these tokens
                 continue
-            if time.perf_counter() - t0 > self.timeout:
+            if idle > 0 and time.perf_counter() - t0 > idle:
                 return self.ch.ctrl.recv(1e-3)   # raises the channel's TimeoutError
             time.sleep(2e-4)
-        return self.ch.ctrl.recv(self.timeout)
+        return self.ch.ctrl.recv(idle)
 
     # ring of receive buffers: the receive of micro-batch m+1 only waits until the compute that
     # READ the slot (two steps earlier) is done, not for everything queued on the compute stream
@@ -385,13 +404,22 @@ class StageFollower:
                 self._pub_q.task_done()
                 return
             step, mb, pinned, ev = item
-            if ev is not None:
-                ev.synchronize()
+            wait_event(ev, "sampled tokens on the device", step, mb)
+            TRACKER.mark("publish", step, mb, peer=0)
             self.ch.tok.send(msgpack.packb({"step": step, "mb": mb, "tokens": pinned.tolist()}),
                              self.timeout)
             self._pub_q.task_done()
 
     def run(self) -> None:
+        try:
+            self._run()
+        except BaseException as e:
+            import traceback
+            traceback.print_exc()
+            abort_job(f"{type(e).__name__}: {e}")   # every rank leaves, with its last op
+            raise
+
+    def _run(self) -> None:
         while True:
             msg = msgpack.unpackb(self._next_msg())
             kind = msg.get("kind", "run")
@@ -413,10 +441,12 @@ class StageFollower:
                 continue
             hr = self._head_rank(plan)
             buf, free_ev = self._recv_slot(plan.num_tokens)
+            TRACKER.mark("recv", plan.step, plan.mb, peer=self.rank - 1, stream="recv")
             x = self.tr.recv(buf, self.rank - 1, free_event=free_ev)
             if self.faults.active:
                 self.faults.on_step()
             tok = self.stats.begin(self.faults.delay_ms)
+            TRACKER.mark("execute", plan.step, plan.mb, stream="compute")
             out = self.ex.execute(plan, x, project=(hr == self.rank))
             self.stats.end(tok)
             self._release_slot()
@@ -425,8 +455,10 @@ class StageFollower:
                     pinned, ev = _sample_tokens_to_host(out)
                     self.publish(plan, pinned, ev)
                 else:   # rotating head: normed hidden states to the rank whose turn it is
+                    TRACKER.mark("send_head", plan.step, plan.mb, peer=hr, stream="send")
                     self.tr.send_head(out, hr)
             else:
+                TRACKER.mark("send", plan.step, plan.mb, peer=self.rank + 1, stream="send")
                 self.tr.send(out, self.rank + 1)
                 if self.heads is not None:
                     self.heads.tick()
@@ -450,10 +482,14 @@ class StageFollower:
 
 
 def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
-                   rccl_timeout_s: float = 300.0, rank_offset: int = 0,
-                   head_pairs: bool = False) -> Transport:
-    """RCCL P2P on GPUs (default); ``DLI_TRANSPORT=host`` stages GPU tensors through gloo
-    (several ranks sharing one GPU — an explicit opt-in, never chosen silently); gloo on CPU.
+                   rccl_timeout_s: float = 120.0, rank_offset: int = 0,
+                   head_pairs: bool = False, streams=None, max_bytes: int = 0,
+                   head_bytes: int = 0) -> Transport:
+    """RCCL P2P on GPUs (default); ``DLI_TRANSPORT=ipc`` moves hidden states GPU-side through
+    cross-process device memory with spinning device waits (parallel/ipc_transport.py: several
+    ranks sharing one GPU, with the production stream structure and the rotating head);
+    ``DLI_TRANSPORT=host`` stages GPU tensors through gloo (an explicit opt-in, never chosen
+    silently); gloo on CPU.  ``streams``: the rank's runtime.streams.RankStreams.
 
     RCCL initialisation is agreed on by all ranks: every rank publishes whether its communicators
     came up (a failure or a peer that never arrives ends in a timeout, not a hang), and if ANY rank
@@ -467,6 +503,16 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
     if world == 1:
         return LoopbackTransport(1)
     kind = os.environ.get("DLI_TRANSPORT", "rccl" if device.type == "cuda" else "gloo")
+    if device.type == "cuda" and kind == "ipc":
+        from ..runtime.faults import raw_store
+        from .ipc_transport import IpcTransport
+        if streams is None:
+            from ..runtime.streams import rank_streams
+            streams = rank_streams(device)
+        if max_bytes <= 0:
+            raise ValueError("DLI_TRANSPORT=ipc needs the largest message size (max_bytes)")
+        return IpcTransport(raw_store(), rank, world, device, streams, max_bytes, head_bytes,
+                            prefix=f"dli_ipc_{job}", head_pairs=head_pairs)
     if device.type == "cuda" and kind in ("rccl", "rccl-or-host"):
         from ..runtime.faults import raw_store
         store = raw_store()
@@ -474,7 +520,7 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
         tr, err = None, ""
         try:
             tr = RcclTransport(store, rank, world, device, prefix=prefix, timeout_s=rccl_timeout_s,
-                               head_pairs=head_pairs)
+                               head_pairs=head_pairs, streams=streams)
         except Exception as e:  # noqa: BLE001 - reported and agreed on below
             err = repr(e)
             store.set(f"{prefix}/err/{rank}", err[:2000])
@@ -500,7 +546,7 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
         return HostStagedTransport(rank_offset=rank_offset)
     if device.type == "cuda":
         if kind != "host":
-            raise ValueError(f"DLI_TRANSPORT={kind!r}: expected rccl, rccl-or-host or host")
+            raise ValueError(f"DLI_TRANSPORT={kind!r}: expected rccl, rccl-or-host, ipc or host")
         from .transport import HostStagedTransport
         return HostStagedTransport(rank_offset=rank_offset)
     return TorchDistTransport(rank_offset=rank_offset)

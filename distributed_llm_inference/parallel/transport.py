@@ -176,12 +176,17 @@ class RcclTransport(Transport):
     supports_head = True
 
     def __init__(self, store: "dist.Store", rank: int, world: int, device: torch.device,
-                 prefix: str = "dli_rccl", timeout_s: float = 300.0, head_pairs: bool = False):
+                 prefix: str = "dli_rccl", timeout_s: float = 120.0, head_pairs: bool = False,
+                 streams=None):
         from .. import ops
+        from ..runtime.streams import rank_streams
         C = ops.native()
         self.rank, self.world, self.device = rank, world, device
-        self.send_stream = torch.cuda.Stream(device=device)
-        self.recv_stream = torch.cuda.Stream(device=device)
+        # dedicated streams (hardware queues of their own: runtime/streams.py), shared with the
+        # rank's HeadJobs / executor so every role exists exactly once per process
+        streams = streams or rank_streams(device)
+        self.send_stream = streams.send
+        self.recv_stream = streams.recv
         self._comms: Dict[int, object] = {}
         self._rccl_version = int(C.rccl_version())
         self._timing = os.environ.get("DLI_STAGE_TIMING", "0") == "1"

@@ -242,6 +242,7 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     if rank == 0:
         store.set("dli_job", uuid.uuid4().hex[:12])
     job = store.get("dli_job").decode()
+    base_job = job
     if layout.dp > 1:
         job = f"{job}r{rep}"
     if pp == 1:
@@ -249,6 +250,13 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         eng = LLMEngine(cfg.model, pp=1, device=device, cfg=cfg)
         dist.barrier()
         return "driver", tag(eng.pipeline)
+    streams = None
+    if device.type == "cuda":
+        # every stream this rank will use, each on a hardware queue of its own, made current
+        # before anything is allocated or launched (runtime/streams.py)
+        from .streams import rank_streams
+        streams = rank_streams(device)
+        streams.activate()
     rotate = head_rotation_wanted(cfg, pp, device)
     ranges = plan_stages(spec, pp, head_rotation=rotate)
     if os.environ.get("DLI_STAGE_RANGES"):  # placement chosen by the server (rebalance)
@@ -265,7 +273,15 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
                           random_init=cfg.random_init and cfg.checkpoint is None, seed=cfg.seed,
                           checkpoint=cfg.checkpoint)
     ex = build_executor(spec, start, end, device, cfg, group=group, kv_share=kv_share)
-    transport = make_transport(srank, pp, device, job=job, rank_offset=rep * pp, head_pairs=rotate)
+    if streams is not None:
+        ex.capture_stream = streams.capture
+    H = spec.hidden_size
+    transport = make_transport(srank, pp, device, job=job, rank_offset=rep * pp, head_pairs=rotate,
+                               streams=streams, max_bytes=ex.max_tokens * H * 2,
+                               head_bytes=ex.max_num_seqs * H * 2)
+    # a stalled wait or a failed rank ends the whole job with every rank's last op (watchdog.py)
+    from .watchdog import start_watchdog
+    start_watchdog(base_job, world, on_abort=getattr(transport, "abort", None))
     # the fallback transport (agreed on by every rank) cannot carry the head: then nobody rotates
     rotate = rotate and transport.supports_head
     channels = _Channels(job, srank, pp, head_rotation=rotate)
@@ -275,27 +291,40 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     heads_runner = None
     if rotate and head is not None:
         heads_runner = HeadRunner(head, device, ex.max_num_seqs, cfg.serve.use_graphs,
-                                  ex.graph_sizes)
+                                  ex.graph_sizes,
+                                  capture_stream=streams.capture if streams is not None else None)
+    if device.type == "cuda" and cfg.serve.use_graphs and os.environ.get("DLI_PRECAPTURE", "1") == "1":
+        # capture every decode graph NOW, before any transport traffic: no capture ever runs
+        # next to in-flight receive kernels or the token publisher thread
+        variants = (True, False) if (rotate and srank == pp - 1) else (True,)
+        ex.warmup_graphs(variants=variants)
+        if heads_runner is not None:
+            heads_runner.warmup()
+        dist.barrier(group=group)
     if srank == 0:
         sched = make_scheduler(spec, ex, cfg, pp)
         drv = DistributedDriver(ex, sched, transport, channels, pp, group, policy=policy)
         if heads_runner is not None:
-            drv.heads = HeadJobs(heads_runner, transport, pp - 1, drv.publish_local, delay=pp)
+            drv.heads = HeadJobs(heads_runner, transport, pp - 1, drv.publish_local, delay=pp,
+                                 stream=streams.head if streams is not None else None)
+        drv.streams = streams
         return "driver", tag(drv)
     fol = StageFollower(ex, transport, channels, srank, pp, group, policy=policy)
     if heads_runner is not None:
-        fol.heads = HeadJobs(heads_runner, transport, pp - 1, fol.publish, delay=pp - srank)
+        fol.heads = HeadJobs(heads_runner, transport, pp - 1, fol.publish, delay=pp - srank,
+                             stream=streams.head if streams is not None else None)
         fol._start_publisher()
+    fol.streams = streams
     return "follower", tag(fol)
 
 
 def head_rotation_wanted(cfg: EngineConfig, pp: int, device: torch.device) -> bool:
     """Rotate the decode LM head over the pipeline ranks (runtime/head.py)?  On by default for
-    PP > 1 over RCCL (GPUs) or gloo (CPU); the host-staged rehearsal transport keeps it on the
-    last stage.  ``DLI_HEAD_ROTATION=0/1`` overrides the config."""
+    PP > 1 over RCCL or IPC (GPUs) or gloo (CPU); the host-staged transport keeps it on the last
+    stage.  ``DLI_HEAD_ROTATION=0/1`` overrides the config."""
     env = os.environ.get("DLI_HEAD_ROTATION")
     want = cfg.serve.head_rotation if env is None else env == "1"
     if not want or pp < 2:
         return False
     kind = os.environ.get("DLI_TRANSPORT", "rccl" if device.type == "cuda" else "gloo")
-    return kind in ("rccl", "rccl-or-host", "gloo")
+    return kind in ("rccl", "rccl-or-host", "ipc", "gloo")

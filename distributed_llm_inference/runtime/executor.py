@@ -29,6 +29,7 @@ from ..models.common import AttnMetadata
 from ..models.llama.cache import KVPool
 from ..models.stage import CausalLMStage
 from ..utils.cuda import prime_graph_rng
+from .watchdog import wait_event
 
 log = logging.getLogger(__name__)
 
@@ -140,7 +141,7 @@ class _Staging:
         self.slot = (self.slot + 1) % self.nslots
         ev = self.events[self.slot]
         if ev is not None:
-            ev.synchronize()
+            wait_event(ev, "staging slot (uploads of an earlier step)")
         self.host = self.hosts[self.slot]
         self.h = self.hviews[self.slot]
 
@@ -201,6 +202,8 @@ class StageExecutor:
         self._sample_out = torch.empty(max_num_seqs, dtype=torch.int32, device=self.device)
         self._wp = pool.attn_params()
         self._step_counter = 0
+        # warm-up / capture stream (a pipeline rank passes its dedicated one: runtime/streams.py)
+        self.capture_stream: Optional[torch.cuda.Stream] = None
 
     # ------------------------------------------------------------------ capacity / bookkeeping
     def apply_frees(self, ids: Sequence[int]) -> None:
@@ -429,18 +432,22 @@ class StageExecutor:
         x = self.staging.d["tokens"][:rows] if self.stage.has_embed else self._hidden_in[:rows]
         n_sample = rows if self.stage.has_head else 0
         # warm up on a side stream (hipBLASLt heuristics, allocator) then capture
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
+        s = self.capture_stream or torch.cuda.Stream()
+        cur = torch.cuda.current_stream()
+        s.wait_stream(cur)
         with torch.cuda.stream(s):
             for _ in range(2):
                 self._forward(meta, x, n_sample, project)
-        torch.cuda.current_stream().wait_stream(s)
+        cur.wait_stream(s)
         prime_graph_rng(self.device)
         graph = torch.cuda.CUDAGraph()
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(graph, pool=self._graph_pool):
+        # thread_local: another thread (token publisher) may synchronise events meanwhile
+        with torch.cuda.graph(graph, pool=self._graph_pool, stream=s,
+                              capture_error_mode="thread_local"):
             out = self._forward(meta, x, n_sample, project)
+        cur.wait_stream(s)
         entry = _GraphEntry(graph, out)
         self._graphs[rows if project else (rows, "norm")] = entry
         log.info("captured decode graph rows=%d splits=%d stage=[%d,%d)%s", rows, splits,
@@ -448,13 +455,16 @@ class StageExecutor:
         # (the captured run did not execute; the caller replays the graph for the real step)
         return entry
 
-    def warmup_graphs(self, sizes: Optional[Sequence[int]] = None) -> None:
-        """Pre-capture decode graphs with dummy (empty, seq_len 0) batches."""
+    def warmup_graphs(self, sizes: Optional[Sequence[int]] = None,
+                      variants: Sequence[bool] = (True,)) -> None:
+        """Pre-capture decode graphs with dummy (empty, seq_len 0) batches.  ``variants``: the
+        ``project`` flags to capture (False = the last stage's graph that ends at the final norm,
+        used when the LM head rotates)."""
         if not self.use_graphs:
             return
-        for r in sizes or self.graph_sizes:
-            if r in self._graphs:
-                continue
+        todo = [(r, p) for r in (sizes or self.graph_sizes) for p in variants
+                if (r if p else (r, "norm")) not in self._graphs]
+        for r, project in todo:
             self.staging.acquire()
             h = self.staging.h
             h["seq_lens"][:r] = 0
@@ -475,7 +485,7 @@ class StageExecutor:
             self.staging.release()
             if self._hidden_in is not None:
                 self._hidden_in[:r].zero_()
-            self._capture(r)
+            self._capture(r, project)
         torch.cuda.synchronize()
 
 

@@ -31,6 +31,7 @@ from .. import ops
 from ..models.embed_head import LMHead
 from ..utils.cuda import prime_graph_rng
 from .executor import StepPlan, _Staging, _fill_pos
+from .watchdog import TRACKER
 
 log = logging.getLogger(__name__)
 
@@ -62,8 +63,10 @@ class HeadRunner:
     executor's; the sampling parameters are staged the same way (pinned ring -> device)."""
 
     def __init__(self, head: LMHead, device: torch.device, max_rows: int, use_graphs: bool = True,
-                 graph_sizes: Optional[Sequence[int]] = None):
+                 graph_sizes: Optional[Sequence[int]] = None,
+                 capture_stream: Optional["torch.cuda.Stream"] = None):
         self.head = head
+        self.capture_stream = capture_stream
         self.device = device
         self.max_rows = max_rows
         self.use_graphs = use_graphs and device.type == "cuda"
@@ -133,9 +136,25 @@ class HeadRunner:
         g.replay()
         return self.out[:B]
 
+    @torch.inference_mode()
+    def warmup(self) -> None:
+        """Capture every bucket's graph now (dummy greedy rows), before any traffic."""
+        if not self.use_graphs:
+            return
+        for rows in self.graph_sizes:
+            if rows in self._graphs:
+                continue
+            self.x[:rows].zero_()
+            plan = StepPlan(0, 0, list(range(rows)), [1] * rows, sample_rows=list(range(rows)),
+                            temperature=[0.0] * rows, top_k=[0] * rows, top_p=[1.0] * rows,
+                            seeds=[0] * rows)
+            self._stage(plan, rows)
+            self._capture(rows)
+        torch.cuda.synchronize(self.device)
+
     def _capture(self, rows: int):
         cur = torch.cuda.current_stream()
-        s = torch.cuda.Stream()
+        s = self.capture_stream or torch.cuda.Stream()
         s.wait_stream(cur)
         with torch.cuda.stream(s):
             for _ in range(2):
@@ -168,14 +187,17 @@ class HeadJobs:
     CPU (gloo): the receive is posted at once (``irecv``) and the job runs when this rank is idle
     or its tokens are wanted (``run_oldest`` / ``drain``)."""
 
-    def __init__(self, runner: HeadRunner, transport, last_rank: int, publish, delay: int = 0):
+    def __init__(self, runner: HeadRunner, transport, last_rank: int, publish, delay: int = 0,
+                 stream: Optional["torch.cuda.Stream"] = None):
         self.runner = runner
         self.tr = transport
         self.last = last_rank
         self.publish = publish            # publish(plan, pinned_tokens, event_or_None)
         self.delay = max(0, int(delay))
         self.gpu = runner.device.type == "cuda"
-        self.stream = torch.cuda.Stream(device=runner.device) if self.gpu else None
+        # the rank's dedicated head stream (runtime/streams.py: a hardware queue of its own, so
+        # the waiting receive never sits in front of compute or the stage transfers)
+        self.stream = (stream or torch.cuda.Stream(device=runner.device)) if self.gpu else None
         self._pending: Deque[tuple] = collections.deque()    # CPU: (plan, buf, work)
         self._deferred: Deque[list] = collections.deque()    # GPU: [plan, age]
         self.jobs = 0
@@ -209,6 +231,7 @@ class HeadJobs:
 
     def _enqueue(self, plan: StepPlan) -> None:
         B = len(plan.seq_ids)
+        TRACKER.mark("head-recv", plan.step, plan.mb, peer=self.last, stream="head")
         with torch.cuda.stream(self.stream):
             x = self.runner.x[:B]
             self.tr.recv_head(x, self.last, self.stream)

@@ -1,0 +1,173 @@
+"""Every HIP stream a pipeline rank uses, created once, each on a hardware queue of its own.
+
+A rank keeps kernels that wait on OTHER ranks next to its own compute: the RCCL (or IPC) receive
+of the next micro-batch, the send of the previous one (it completes only once the peer has posted
+its receive), and the rotating LM head's receive (runtime/head.py).  HIP maps streams onto a
+small pool of HSA hardware queues per priority (``GPU_MAX_HW_QUEUES``, 4 by default; PyTorch's
+stream pool alone creates 32 streams per priority, RCCL two internal streams per communicator),
+and the packets of one hardware queue run in order: a waiting kernel - or RCCL's cross-stream
+barrier packet behind it - that lands on the compute stream's queue stalls the stage for as long
+as the peer takes, and at worst closes a wait cycle between ranks.
+
+So the roles that ever hold such work get DEDICATED streams: created with a (full) CU mask, which
+makes HIP give the stream a hardware queue of its own instead of a shared pool queue, while its
+kernels still run on every CU.  Roles:
+
+  ``compute``  every stage kernel and graph replay (made the thread's current stream)
+  ``send``     stage -> stage+1 sends; on the last stage the rotating head's sends
+  ``recv``     stage-1 -> stage receives
+  ``head``     the rotating head's receive + projection + sampling (runtime/head.py)
+  ``capture``  hipGraph warm-up / capture (idle afterwards)
+
+``DLI_STREAMS=pool`` restores ordinary pool streams (the isolation test shows what that risks).
+``tests/test_streams_gpu.py`` proves the isolation on the hardware: a kernel spinning on each
+waiting role in turn must not keep any other role - a decode-graph replay on ``compute``, copies
+on the others - from completing, with RCCL-style barrier packets queued on pool streams as well.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+import torch
+
+ROLES = ("compute", "send", "recv", "head", "capture")
+WAITING_ROLES = ("send", "recv", "head")
+
+
+def _native():
+    from .. import ops
+    return ops.native()
+
+
+class RankStreams:
+    """The streams of one rank on one device (see module docstring)."""
+
+    def __init__(self, device: torch.device, mode: Optional[str] = None):
+        self.device = torch.device(device)
+        self.mode = mode or os.environ.get("DLI_STREAMS", "dedicated")
+        if self.mode not in ("dedicated", "pool"):
+            raise ValueError(f"DLI_STREAMS={self.mode!r}: expected dedicated or pool")
+        self.gpu = self.device.type == "cuda"
+        self._handles = []
+        self.streams: Dict[str, Optional[torch.cuda.Stream]] = {}
+        if not self.gpu:
+            self.streams = {r: None for r in ROLES}
+            return
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.index = idx
+        C = _native()
+        for role in ROLES:
+            if self.mode == "dedicated":
+                h = C.stream_create(idx, 1, 0)
+                self._handles.append(h)
+                self.streams[role] = torch.cuda.ExternalStream(h, device=self.device)
+            else:
+                self.streams[role] = torch.cuda.Stream(device=self.device)
+
+    def __getattr__(self, role: str):
+        if role in ROLES:
+            return self.__dict__["streams"][role]
+        raise AttributeError(role)
+
+    def activate(self) -> None:
+        """Make ``compute`` the calling thread's current stream (torch's current stream is
+        per thread: call this in every thread that launches stage work)."""
+        if self.gpu:
+            torch.cuda.set_stream(self.streams["compute"])
+
+    def describe(self) -> dict:
+        d = {"mode": self.mode}
+        if self.gpu and self.mode == "dedicated":
+            C = _native()
+            d["cu_per_stream"] = {r: int(C.stream_cu_count(s.cuda_stream))
+                                  for r, s in self.streams.items()}
+        return d
+
+    def synchronize(self) -> None:
+        if self.gpu:
+            for s in self.streams.values():
+                s.synchronize()
+
+    def close(self) -> None:
+        """Destroy the dedicated streams (after every stream has drained)."""
+        if not self._handles:
+            return
+        self.synchronize()
+        if torch.cuda.current_stream(self.device).cuda_stream in self._handles:
+            torch.cuda.set_stream(torch.cuda.default_stream(self.device))
+        C = _native()
+        for h in self._handles:
+            C.stream_destroy(h)
+        self._handles.clear()
+
+
+_RANK_STREAMS: Dict[int, RankStreams] = {}
+
+
+def rank_streams(device: torch.device) -> RankStreams:
+    """The process-wide :class:`RankStreams` of ``device`` (created on first use)."""
+    device = torch.device(device)
+    key = device.index if device.index is not None else (
+        torch.cuda.current_device() if device.type == "cuda" else -1)
+    rs = _RANK_STREAMS.get(key)
+    if rs is None:
+        rs = RankStreams(device)
+        _RANK_STREAMS[key] = rs
+    return rs
+
+
+# ------------------------------------------------------------------------------ isolation probe
+def isolation_matrix(streams: Dict[str, torch.cuda.Stream], waiters, device: torch.device,
+                     barrier_streams=(), graph=None, graph_role: str = "compute",
+                     window_s: float = 1.5, spin_timeout_s: float = 20.0) -> Dict[str, Dict[str, bool]]:
+    """For each role in ``waiters``: spin a kernel on it (waiting on a host flag, as a receive
+    waits for its peer), queue RCCL-style barrier packets behind it on ``barrier_streams`` (RCCL
+    makes an internal stream wait on every send / receive it launches), then queue work on every
+    other stream - ``graph`` replayed on ``graph_role``, a small kernel + copy elsewhere - and
+    record whether each completed within ``window_s`` while the spinner still spins.  Returns
+    ``{waiter: {other: progressed}}``.  The spinner always exits (host release or its deadline)."""
+    import time
+    C = _native()
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    names = list(streams)
+    flags = C.HostWords(2)
+    out = torch.zeros(len(names), dtype=torch.int32, device=dev)
+    src = torch.ones(1 << 16, dtype=torch.float32, device=dev)
+    dsts = {n: torch.empty_like(src) for n in names}
+    torch.cuda.synchronize(dev)
+    res: Dict[str, Dict[str, bool]] = {}
+    for w in waiters:
+        flags.set(0, 0)
+        flags.set(1, 0)
+        C.wait_geq(flags.dev_ptr(0), 1, spin_timeout_s, flags.dev_ptr(1), 1,
+                   streams[w].cuda_stream, idx)
+        ev = torch.cuda.Event()
+        ev.record(streams[w])
+        for b in barrier_streams:
+            b.wait_event(ev)
+        evs = {}
+        for i, n in enumerate(names):
+            if n == w:
+                continue
+            s = streams[n]
+            with torch.cuda.stream(s):
+                if graph is not None and n == graph_role:
+                    graph.replay()
+                else:
+                    C.touch(out[i:i + 1], s.cuda_stream)
+                    dsts[n].copy_(src, non_blocking=True)
+            e = torch.cuda.Event()
+            e.record(s)
+            evs[n] = e
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < window_s and not all(e.query() for e in evs.values()):
+            time.sleep(1e-3)
+        res[w] = {n: bool(e.query()) for n, e in evs.items()}
+        flags.set(0, 1)   # release the spinner
+        streams[w].synchronize()
+        torch.cuda.synchronize(dev)
+        if flags.get(1) != 0:
+            raise RuntimeError(f"isolation probe: spinner on {w!r} hit its deadline")
+    return res

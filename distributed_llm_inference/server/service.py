@@ -191,6 +191,9 @@ class EngineService:
 
     def _loop(self) -> None:
         try:
+            act = getattr(self.driver, "activate_streams", None)
+            if act is not None:
+                act()   # the rank's compute stream is per thread (runtime/streams.py)
             while not self._stop.is_set():
                 sched = self.driver.sched
                 self._ingest(block=not sched.has_work())

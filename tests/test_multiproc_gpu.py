@@ -43,11 +43,13 @@ def _cfg(world, mbs):
     return spec, cfg
 
 
-def _pipeline_worker(rank, world, port, mbs, q, transport="host"):
+def _pipeline_worker(rank, world, port, mbs, q, transport="host", rotation=None):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_SHARE_GPU="1",
-                          DLI_TRANSPORT=transport, DLI_TUNABLEOP="0")
+                          DLI_TRANSPORT=transport, DLI_TUNABLEOP="0", DLI_WATCHDOG_S="60")
+        if rotation is not None:
+            os.environ["DLI_HEAD_ROTATION"] = "1" if rotation else "0"
         import torch.distributed as dist
         from distributed_llm_inference.runtime.engine import init_pipeline_rank
         from distributed_llm_inference.runtime.sequence import SamplingParams
@@ -87,6 +89,35 @@ def test_multiprocess_pipeline_on_gpu(gpu, world, mbs):
         p.join(120)
     assert status == "ok", got
     assert all(p.exitcode == 0 for p in ps)
+    assert got == ref
+
+
+@pytest.mark.parametrize("world,mbs,rotation", [(2, 3, True), (4, 5, True), (4, 5, False)])
+def test_multiprocess_pipeline_ipc_transport(gpu, world, mbs, rotation):
+    """Stage processes sharing the GPU over the IPC device transport (parallel/ipc_transport.py):
+    receives are spinning device waits on the rank's dedicated recv / head streams, exactly the
+    production RCCL stream schedule, and with ``rotation`` the rotating LM head's GPU branch runs
+    (HeadJobs deferred enqueue, head-stream receive + graph replay, per-rank token channels).
+    Tokens must equal PP=1's."""
+    from distributed_llm_inference.runtime.engine import LLMEngine
+    from distributed_llm_inference.runtime.sequence import SamplingParams
+    os.environ["DLI_TUNABLEOP"] = "0"
+    spec, cfg = _cfg(1, mbs)
+    ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
+        PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_pipeline_worker, args=(r, world, port, mbs, q, "ipc", rotation))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    status, got, kind = q.get(timeout=600)
+    for p in ps:
+        p.join(120)
+    assert status == "ok", got
+    assert kind == "IpcTransport"
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
     assert got == ref
 
 
