@@ -4,6 +4,7 @@
     distribute generate --model llama-3-8b --gpus 2 --prompt-ids 1,2,3 --max-tokens 32
     distribute serve    --model llama-3-70b --gpus 8 --port 8000 [--tokenizer DIR] [--dp 8]
     distribute bench    --gpus 8 --steps 20 --warmup 5 [--dp 2]  (bench.py under the launcher)
+    distribute block-serve --model llama-3-8b --start 0 --end 16 --port 8100   (swarm block server)
 
 One process per GPU (``launcher.launch``); each process owns one pipeline stage (``plan_stages``).
 ``--dp D`` splits the GPUs into D independent pipeline replicas of gpus/D stages (DP x PP,
@@ -102,6 +103,19 @@ def cmd_plan(a) -> int:
     if layout.dp > 1:
         res["replicas"] = replicas
     print(json.dumps(res, indent=1))
+    return 0
+
+
+def cmd_block_serve(a) -> int:
+    """One block server (reference server/worker.py intent): layers [start, end) behind HTTP."""
+    from .server.block_server import serve_blocks
+    from .server.worker import InferenceWorker
+    logging.basicConfig(level=logging.WARNING)
+    worker = InferenceWorker(a.model, a.start, a.end, layers_per_block=a.layers_per_block,
+                             device=a.device, random_init=a.checkpoint is None,
+                             checkpoint=a.checkpoint, max_batch_size=a.max_batch_size,
+                             window_length=a.window, num_sink_tokens=a.sinks, seed=a.seed)
+    serve_blocks(worker, a.host, a.port)
     return 0
 
 
@@ -229,6 +243,20 @@ def main(argv: Optional[List[str]] = None) -> int:
     b.add_argument("--gpus", type=int, default=1)
     b.add_argument("--dp", type=int, default=1, help="pipeline replicas (DP x PP)")
     b.add_argument("rest", nargs=argparse.REMAINDER)
+    bs = sub.add_parser("block-serve",
+                        help="serve a layer range's hidden-state forward over HTTP (swarm block server)")
+    bs.add_argument("--model", default="llama-3-8b", help="preset name or HF config/checkpoint dir")
+    bs.add_argument("--checkpoint", default=None, help="HF safetensors dir (default: random init)")
+    bs.add_argument("--start", type=int, required=True, help="first layer (inclusive)")
+    bs.add_argument("--end", type=int, required=True, help="last layer (exclusive)")
+    bs.add_argument("--layers-per-block", type=int, default=None)
+    bs.add_argument("--seed", type=int, default=0)
+    bs.add_argument("--device", default=None, help="cuda:N / cpu (default: cuda:0 if present)")
+    bs.add_argument("--max-batch-size", type=int, default=64)
+    bs.add_argument("--window", type=int, default=0)
+    bs.add_argument("--sinks", type=int, default=0)
+    bs.add_argument("--host", default="127.0.0.1")
+    bs.add_argument("--port", type=int, default=8100)
     w = sub.add_parser("worker", help=argparse.SUPPRESS)
     _common(w)
     _gen_args(w)
@@ -239,6 +267,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         return cmd_plan(a)
     if a.cmd == "worker":
         return cmd_worker(a)
+    if a.cmd == "block-serve":
+        return cmd_block_serve(a)
     if a.cmd == "bench":
         from .launcher import launch
         bench = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")

@@ -33,7 +33,7 @@ class InferenceWorker:
                  layers_per_block: Optional[int] = None, device=None, random_init: bool = True,
                  checkpoint: Optional[str] = None, quantize: bool = False,
                  max_batch_size: int = 64, window_length: int = 0, num_sink_tokens: int = 0,
-                 num_blocks: int = 512):
+                 num_blocks: int = 512, seed: int = 0):
         self.model = model
         self.spec = resolve_model(checkpoint or model)
         if not (0 <= block_index_start < block_index_end <= self.spec.num_layers):
@@ -49,7 +49,8 @@ class InferenceWorker:
             e = min(block_index_end, s + n)
             bid = f"{self.spec.name}.{s}-{e}"
             blk = load_block(checkpoint or model, list(range(s, e)), use_quantized=False,
-                             device=self.device, random_init=checkpoint is None and random_init)
+                             device=self.device, random_init=checkpoint is None and random_init,
+                             seed=seed)
             if quantize:
                 blk = convert_to_optimized_block(blk, quantize=True, device=self.device)
             cache = PartialLlamaSinkCache(window_length, num_sink_tokens, num_blocks=num_blocks)
