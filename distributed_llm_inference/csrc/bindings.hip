@@ -254,10 +254,13 @@ void rope_cache(Tensor qkv, optional<Tensor> positions, optional<Tensor> slot_ma
 dli::AttnParams attn_common(Tensor& out, Tensor& q, optional<Tensor>& q_sink, Tensor& k_cache,
                             Tensor& v_cache, Tensor& block_tables, Tensor& seq_lens, double scale,
                             int64_t n_sink, int64_t sink_pad, int64_t ring, int64_t window,
-                            double k_scale, double v_scale, int64_t& D) {
+                            double k_scale, double v_scale, int64_t& D,
+                            bool allow_empty_out = false) {
   CHECK_IN(out); CHECK_IN(q); CHECK_BF16(out); CHECK_BF16(q);
   TORCH_CHECK(q.dim() == 3, "q must be [T, nh, D]");
-  TORCH_CHECK(out.sizes() == q.sizes(), "out must match q");
+  // empty `out`: only for an MX-output decode, whose kernel never touches the bf16 output
+  TORCH_CHECK(out.sizes() == q.sizes() || (allow_empty_out && out.numel() == 0),
+              "out must match q");
   const int64_t nh = q.size(1);
   D = q.size(2);
   const int64_t nkv = k_cache.size(1);
@@ -284,7 +287,7 @@ dli::AttnParams attn_common(Tensor& out, Tensor& q, optional<Tensor>& q_sink, Te
   p.kv_fp8 = fp8 ? 1 : 0;
   p.k_scale = (float)k_scale;
   p.v_scale = (float)v_scale;
-  p.out = bp(out);
+  p.out = out.numel() ? bp(out) : nullptr;
   p.block_tables = block_tables.data_ptr<int>();
   p.bt_stride = (int)block_tables.size(1);
   p.seq_lens = seq_lens.data_ptr<int>();
@@ -308,7 +311,7 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
                  double v_scale, optional<Tensor> out_q, optional<Tensor> out_mx) {
   int64_t D = 0;
   auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
-                       sink_pad, ring, window, k_scale, v_scale, D);
+                       sink_pad, ring, window, k_scale, v_scale, D, out_q.has_value());
   const int64_t B = q.size(0);
   TORCH_CHECK(seq_lens.numel() == B, "decode: one token per sequence (seq_lens must have T entries)");
   TORCH_CHECK(num_splits >= 1, "num_splits >= 1");

@@ -243,7 +243,8 @@ def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_si
         nb = (T + 63) // 64
         q8 = torch.empty(T, nh * D, dtype=torch.float8_e4m3fn, device=q.device)
         sc = torch.empty(nh * nb * 64, dtype=torch.uint8, device=q.device)
-        dummy = torch.empty_like(q) if out is None else out   # shape-checked, not written
+        # the kernel writes only q8 / sc: no bf16 output (nothing held in a graph's pool)
+        dummy = q.new_empty((0, nh, D))
         native().attn_decode(dummy, q, q_sink, k_cache, v_cache, block_tables, seq_lens,
                              float(scale), int(n_sink), int(sink_pad), int(ring), int(window), 1,
                              None, None, float(k_scale), float(v_scale), q8, sc)

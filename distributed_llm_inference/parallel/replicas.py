@@ -108,12 +108,20 @@ class ReplicaServer:
         with self._lock:
             self.evt.send(data, 60.0)
 
-    def _forward_stream(self, rid: int, q: "queue.Queue") -> None:
+    def _forward_stream(self, rid: int, q: "queue.Queue", fut: Future) -> None:
+        """Forward a streaming request's tokens, then its completion - from THIS thread, after
+        the stream's end sentinel, so 'done' can never overtake a token still being forwarded
+        (the proxy ends the stream on 'done')."""
         while True:
             tok = q.get()
             if tok is None:
-                return
+                break
             self._send({"op": "tok", "rid": rid, "tok": int(tok)})
+        try:
+            fut.result()
+        except Exception:  # noqa: BLE001 - reported by _on_done
+            pass
+        self._on_done(rid, fut)
 
     def _on_done(self, rid: int, fut: Future) -> None:
         self._rid2sid.pop(rid, None)
@@ -152,8 +160,10 @@ class ReplicaServer:
                 continue
             self._rid2sid[rid] = fut.seq_id
             if q is not None:
-                threading.Thread(target=self._forward_stream, args=(rid, q), daemon=True).start()
-            fut.add_done_callback(lambda f, rid=rid: self._on_done(rid, f))
+                threading.Thread(target=self._forward_stream, args=(rid, q, fut),
+                                 daemon=True).start()
+            else:
+                fut.add_done_callback(lambda f, rid=rid: self._on_done(rid, f))
 
     def close(self) -> None:
         for ch in (self.req, self.evt):
@@ -271,6 +281,7 @@ class ReplicaRouter:
         self._ids = itertools.count()
         self._lock = threading.Lock()
         self._load = [0] * len(self.services)
+        self._rr = 0   # rotating tie-break: equal loads do not all land on replica 0
 
     @property
     def error(self):
@@ -281,7 +292,9 @@ class ReplicaRouter:
 
     def submit(self, prompt_ids: List[int], params: SamplingParams, stream: bool = False):
         with self._lock:
-            r = min(range(len(self.services)), key=lambda i: (self._load[i], i))
+            n = len(self.services)
+            r = min(range(n), key=lambda i: (self._load[i], (i - self._rr) % n))
+            self._rr = (r + 1) % n
             self._load[r] += 1
         try:
             fut, q = self.services[r].submit(prompt_ids, params, stream=stream)

@@ -137,6 +137,25 @@ def test_router_over_local_and_remote_replica():
             break
         toks.append(t)
     assert toks == fut.result(60).output_ids and len(toks) == 4
+    # streaming straight through the remote replica: every token arrives before the stream ends
+    # ('done' is sent by the forwarding thread after the last token, never ahead of it)
+    for n in (1, 3, 6):
+        fut, q = remote.submit([4, 5, 6, n], SamplingParams(max_tokens=n, ignore_eos=True),
+                               stream=True)
+        toks = []
+        while True:
+            t = q.get(timeout=60)
+            if t is None:
+                break
+            toks.append(t)
+        assert toks == fut.result(60).output_ids and len(toks) == n, (n, toks)
+    # equal loads rotate over the replicas instead of always picking replica 0
+    seen = set()
+    for _ in range(2):
+        f, _ = router.submit([3, 3], SamplingParams(max_tokens=1, ignore_eos=True))
+        f.result(60)
+        seen.add(f.replica)
+    assert seen == {0, 1}
     # abort a long request on whichever replica it landed
     fut, _ = router.submit([9, 9], SamplingParams(max_tokens=250, ignore_eos=True))
     time.sleep(0.2)
