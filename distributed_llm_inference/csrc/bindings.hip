@@ -342,7 +342,8 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
 void attn_prefill(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, Tensor v_cache,
                   Tensor block_tables, Tensor seq_lens, Tensor q_start, int64_t max_q,
                   double scale, int64_t n_sink, int64_t sink_pad, int64_t ring, int64_t window,
-                  double k_scale, double v_scale, optional<Tensor> tile_map, int64_t qb) {
+                  double k_scale, double v_scale, optional<Tensor> tile_map, int64_t qb,
+                  optional<Tensor> mask) {
   int64_t D = 0;
   auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
                        sink_pad, ring, window, k_scale, v_scale, D);
@@ -358,6 +359,18 @@ void attn_prefill(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache,
   }
   TORCH_CHECK(qb == 1 || qb == 2, "attn_prefill: qb (query blocks per wave) must be 1 or 2");
   p.prefill_qb = (int)qb;
+  if (mask.has_value()) {   // reference 4-D additive mask [B, 1 | nh, Tm, Km], fp32
+    CHECK_IN(*mask); CHECK_F32(*mask);
+    TORCH_CHECK(mask->dim() == 4 && mask->size(0) == B &&
+                    (mask->size(1) == 1 || mask->size(1) == q.size(1)),
+                "attn_prefill: mask must be [B, 1 | nh, T, keys]");
+    TORCH_CHECK(ring == 0 && !tile_map.has_value(),
+                "attn_prefill: a custom mask needs a full cache and the dense grid");
+    p.mask = mask->data_ptr<float>();
+    p.mask_heads = (int)mask->size(1);
+    p.mask_q = (int)mask->size(2);
+    p.mask_k = (int)mask->size(3);
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   check_rc(dli::launch_attn_prefill(p, (int)B, (int)max_q, (int)D, cur_stream()), "attn_prefill");
 }
@@ -700,7 +713,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sink_pad"), py::arg("ring"), py::arg("window"), py::arg("num_splits"),
         py::arg("part_o"), py::arg("part_ml"), py::arg("k_scale"), py::arg("v_scale"),
         py::arg("out_q") = py::none(), py::arg("out_mx") = py::none());
-  m.def("attn_prefill", &attn_prefill, "paged causal prefill attention (varlen)");
+  m.def("attn_prefill", &attn_prefill, "paged causal prefill attention (varlen)", py::arg("out"),
+        py::arg("q"), py::arg("q_sink"), py::arg("k_cache"), py::arg("v_cache"),
+        py::arg("block_tables"), py::arg("seq_lens"), py::arg("q_start"), py::arg("max_q"),
+        py::arg("scale"), py::arg("n_sink"), py::arg("sink_pad"), py::arg("ring"),
+        py::arg("window"), py::arg("k_scale"), py::arg("v_scale"), py::arg("tile_map"),
+        py::arg("qb"), py::arg("mask") = py::none());
   m.def("sample", &sample, "greedy / temperature / top-k / top-p sampling", py::arg("out_tokens"),
         py::arg("out_logprobs"), py::arg("logits"), py::arg("temperature"), py::arg("top_k"),
         py::arg("top_p"), py::arg("seeds"), py::arg("step"), py::arg("ctr") = py::none());

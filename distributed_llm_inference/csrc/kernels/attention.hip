@@ -199,9 +199,14 @@ __device__ __forceinline__ void o_unit(const WaveState<D>& st, int u, int h4, in
 // (Skipping the O rescale when no running max moved, or a mask-free copy of this step for keys
 // below the diagonal, cut the prefill loop's VALU count but raised its VGPRs: fewer workgroups
 // per CU, measured slower.)
-template <int D, typename Visible>
+struct NoBias {
+  __device__ __forceinline__ float operator()(int) const { return 0.f; }
+};
+
+template <int D, typename Visible, typename Bias = NoBias>
 __device__ __forceinline__ void attn_core(WaveState<D>& st, const bf16x8 (&qf)[D / 32],
-                                          const KVFrag<D>& f, float scale_log2, Visible visible) {
+                                          const KVFrag<D>& f, float scale_log2, Visible visible,
+                                          Bias bias = Bias()) {
   // ---- S^T = K . Q^T ----
   f32x4 s[2];
 #pragma unroll
@@ -215,7 +220,7 @@ __device__ __forceinline__ void attn_core(WaveState<D>& st, const bf16x8 (&qf)[D
   float mx = -INFINITY;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    x[j] = visible(j) ? s[j >> 2][j & 3] : -INFINITY;
+    x[j] = visible(j) ? s[j >> 2][j & 3] + bias(j) : -INFINITY;
     mx = fmaxf(mx, x[j]);
   }
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
@@ -626,8 +631,9 @@ __device__ __forceinline__ int kswz(int row) {
   return ((row & 3) | (((row >> 3) & 3) << 2)) & (CH - 1);
 }
 
-template <int D, bool WIN, bool FP8, int QB>
+template <int D, bool WIN, bool FP8, int QB, bool MASK = false>
 __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_kernel(AttnParams p, int hpw) {
+  static_assert(!MASK || (!WIN && QB == 1), "custom masks: full cache, one query block per wave");
   // QB = 16-token query blocks per wave: every K / V fragment read from LDS feeds QB blocks'
   // MFMAs.  Measured (profiles/attn_prefill_qb_ab.json): QB = 2 is +2 % on 2k-4k chunks and -25 %
   // on 16-token ones, so QB = 1 is the default; what paid was occupancy — the 2-waves-per-SIMD
@@ -708,10 +714,24 @@ __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_ke
     nS = min(p.n_sink, L);
     n_sinkst = (nS + 31) >> 5;
   } else {
-    seg_len = pq_max + 1;
+    // causal: keys up to the workgroup's last query; a custom mask may open any key < L
+    seg_len = MASK ? L : pq_max + 1;
     n_main = (seg_len + 31) >> 5;
   }
   const int nsteps = n_main + n_sinkst;
+  // custom additive mask row of this lane's query (clamped finite: a fully masked row then
+  // averages V like the reference's fp32 softmax over finfo.min, instead of dividing by 0),
+  // pre-divided by the softmax scale because the scores are scaled inside the exponent
+  const float* mrow = nullptr;
+  float minv = 0.f;
+  int mlen = 0;   // keys [0, mlen) have a mask column (bounds of the caller's tensor)
+  if constexpr (MASK) {
+    const int hsel = p.mask_heads == 1 ? 0 : qh;
+    const int mr = p.mask_q - qlen + (col_valid[0] ? tok[0] : qlen - 1);
+    mlen = mr >= 0 ? min(L, p.mask_k) : 0;   // a row outside the mask: every key masked
+    mrow = p.mask + (((size_t)b * p.mask_heads + hsel) * p.mask_q + max(mr, 0)) * p.mask_k;
+    minv = 1.4426950408889634f / p.scale_log2;   // 1 / scale
+  }
   auto slot0 = [&](int sidx) -> int {  // first cache slot of virtual step sidx
     if (!WIN) return sidx * 32;
     return sidx < n_main ? p.sink_pad + sidx * 32 : (sidx - n_main) * 32;
@@ -826,6 +846,18 @@ __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_ke
     const bool sink_step = WIN && sidx >= n_main;
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
+      if constexpr (MASK) {
+        // keys 8h4 + j < L are candidates; the mask decides (its -inf / finfo.min entries drop out)
+        const int k0 = u0 + 8 * h4;
+        float madd[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          madd[j] = k0 + j < mlen ? fmaxf(mrow[k0 + j], -1e20f) * minv : 0.f;
+        const int lim = mlen - 1 - k0;
+        attn_core<D>(st[qb], qf[qb], f, sl2, [&](int j) { return j <= lim; },
+                     [&](int j) { return madd[j]; });
+        continue;
+      }
       if constexpr (!WIN) {
         attn_compute_causal<D>(st[qb], qf[qb], f, sl2, pq[qb] - (u0 + 8 * h4));
         continue;
@@ -928,6 +960,12 @@ int launch_attn_decode(const AttnParams& p, int B, int D, hipStream_t stream) {
 
 template <int D, bool WIN, bool FP8>
 static void prefill_grid(const AttnParams& p, dim3 grid, int hpw, hipStream_t stream) {
+  if constexpr (!WIN) {
+    if (p.mask) {   // reference 4-D additive mask (rare): one query block per wave
+      attn_prefill_kernel<D, false, FP8, 1, true><<<grid, 256, 0, stream>>>(p, hpw);
+      return;
+    }
+  }
   if (p.prefill_qb == 2)
     attn_prefill_kernel<D, WIN, FP8, 2><<<grid, 256, 0, stream>>>(p, hpw);
   else
@@ -939,7 +977,7 @@ static int launch_prefill_d(const AttnParams& p, int B, int max_q, hipStream_t s
   const int G = p.nh / p.nkv;
   const int hpw = (G % 4 == 0) ? 4 : (G % 2 == 0 ? 2 : 1);  // q heads sharing each K/V tile
   const int tpw = 4 / hpw;
-  const int tt = 16 * tpw * p.prefill_qb;                      // query tokens per workgroup tile
+  const int tt = 16 * tpw * (p.mask ? 1 : p.prefill_qb);      // query tokens per workgroup tile
   dim3 grid((max_q + tt - 1) / tt, p.nkv * (G / hpw), B);
   if (p.tile_map) {
     // XCD-aware 1-D grid over (group, tile) work items (see attn_prefill_kernel)
@@ -961,6 +999,8 @@ int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_
   if (B == 0 || max_q == 0) return 0;
   if (p.prefill_qb != 1 && p.prefill_qb != 2) return -3;
   if (p.bs % 32 != 0 || (p.ring > 0 && (p.sink_pad % 32 != 0 || p.ring % 32 != 0))) return -2;
+  if (p.mask && (p.ring > 0 || p.tile_map || p.mask_heads < 1 || p.mask_q < 1 || p.mask_k < 1))
+    return -4;   // custom masks: full cache, dense grid
   switch (D) {
     case 32: return launch_prefill_d<32>(p, B, max_q, stream);
     case 64: return launch_prefill_d<64>(p, B, max_q, stream);

@@ -29,6 +29,11 @@ struct AttnParams {
   // bf16 -- e4m3 bytes [T, nh * D] and one e8m0 scale per (token, head) in mx_off layout
   uint8_t* out_q = nullptr;
   uint8_t* out_mx = nullptr;
+  // prefill with the reference API's pre-inverted 4-D additive mask (full cache only):
+  // fp32 [B, mask_heads (1 | nh), mask_q, mask_k]; query token t of sequence b uses row
+  // mask_q - qlen_b + t (the last qlen_b rows), key k column k.  No causal mask is added.
+  const float* mask = nullptr;
+  int mask_heads = 0, mask_q = 0, mask_k = 0;
 };
 
 struct RopeCacheParams {

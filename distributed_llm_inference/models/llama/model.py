@@ -181,7 +181,7 @@ class LlamaBlock(nn.Module):
             if custom.shape[-1] < L_max:
                 raise ValueError(f"4-D attention_mask key length {custom.shape[-1]} < {L_max} "
                                  "cached + new tokens")
-            meta.custom_mask = custom.to(dev)
+            meta.custom_mask = (custom if len(keep) == B else custom[keep]).to(dev)
         # explicit positions override the default past_len + arange
         pos_src = position_ids if position_ids is not None else (
             cache_position.unsqueeze(0).expand(B, -1) if cache_position is not None else None)

@@ -82,12 +82,12 @@ class LlamaAttention(nn.Module):
                                    window=meta.window, want_sink=meta.want_sink,
                                    k_scale=meta.k_scale, v_scale=meta.v_scale)
         if meta.custom_mask is not None:
-            # reference-API custom 4-D mask (rare, explicit): masked softmax in torch over the
-            # keys gathered from the paged cache the RoPE kernel just wrote
-            from ...ops import reference as ref
-            o = ref.attn_custom_mask(q, k_cache, v_cache, meta.block_tables, meta.seq_lens,
-                                     meta.q_start, self.scale, meta.custom_mask,
-                                     meta.k_scale, meta.v_scale)
+            # reference-API custom 4-D additive mask (reference model.py:115-119, modules.py:92-94):
+            # the prefill kernel's masked variant (any T, full cache) adds it before the online
+            # softmax in place of the causal mask
+            o = ops.attn_prefill(q, None, k_cache, v_cache, meta.block_tables, meta.seq_lens,
+                                 meta.q_start, meta.max_q, self.scale, k_scale=meta.k_scale,
+                                 v_scale=meta.v_scale, mask=meta.custom_mask)
         elif meta.is_decode:
             op = self.o_proj
             mx = (op.is_fp8 and op.bias is None and ops.fp8_mx_attn()

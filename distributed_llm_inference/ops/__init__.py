@@ -302,15 +302,28 @@ def prefill_tiles(q_lens, nh: int, nkv: int, out=None) -> torch.Tensor:
 
 def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, max_q, scale,
                  n_sink=0, sink_pad=0, ring=0, window=0, out=None, k_scale=1.0, v_scale=1.0,
-                 tile_map=None):
+                 tile_map=None, mask=None):
+    """Paged varlen prefill attention.  ``mask``: the reference API's pre-inverted 4-D additive
+    mask ``[B, 1 | nh, T, >= L]`` (0 = attend, large negative = masked; the last ``q_len_b`` rows
+    of sequence b) - it replaces the causal mask (full cache, any T incl. 1)."""
     if not _gpu(q):
-        y = ref.attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, scale,
-                             n_sink, sink_pad, ring, window, k_scale, v_scale)
+        if mask is not None:
+            y = ref.attn_custom_mask(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale,
+                                     mask, k_scale, v_scale)
+        else:
+            y = ref.attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start,
+                                 scale, n_sink, sink_pad, ring, window, k_scale, v_scale)
         return out.copy_(y) if out is not None else y
     out = torch.empty_like(q) if out is None else out
+    if mask is not None:
+        if ring:
+            raise ValueError("custom 4-D masks need a full (non-windowed) cache")
+        mask = mask.to(device=q.device, dtype=torch.float32).contiguous()
+        tile_map = None   # dense grid: the masked kernel runs one query block per wave
     native().attn_prefill(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start,
                           int(max_q), float(scale), int(n_sink), int(sink_pad), int(ring),
-                          int(window), float(k_scale), float(v_scale), tile_map, prefill_qb())
+                          int(window), float(k_scale), float(v_scale), tile_map, prefill_qb(),
+                          mask)
     return out
 
 

@@ -272,6 +272,52 @@ def test_attn_prefill(gpu, nh, nkv, D, tiles, qb, monkeypatch):
     _close(out, out_r, 2e-2, 2e-2, "prefill")
 
 
+@pytest.mark.parametrize("heads", ["one", "per_head"])
+@pytest.mark.parametrize("D", [64, 128])
+def test_attn_prefill_custom_mask(gpu, heads, D):
+    """The reference API's pre-inverted 4-D additive mask in the HIP prefill kernel (masked
+    variant) against the fp32 oracle ref.attn_custom_mask: ragged lengths, mixed chunk / decode
+    rows, a mask that opens future keys (no causal mask is added), finfo.min and -inf entries,
+    a row open to a single key and a row masked with finfo.min everywhere (mean of V)."""
+    torch.manual_seed(11)
+    nh, nkv, bs = 8, 2, 64
+    q_lens = [9, 1, 40, 3]
+    ctx = [0, 77, 30, 129]
+    lens = [a + b for a, b in zip(q_lens, ctx)]
+    B, Tm, Km = len(q_lens), max(q_lens), max(lens) + 5
+    q_start = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
+    T = int(q_start[-1])
+    max_blocks = (max(lens) + bs - 1) // bs
+    kc, vc = _make_cache(B * max_blocks, nkv, bs, D, gpu)
+    bt = _tables(B, max_blocks, B * max_blocks, gpu, seed=7)
+    q = torch.randn(T, nh, D, device=gpu, dtype=BF)
+    Hm = 1 if heads == "one" else nh
+    neg = torch.finfo(torch.float32).min
+    mask = torch.where(torch.rand(B, Hm, Tm, Km) < 0.3, torch.tensor(neg), torch.tensor(0.0))
+    mask += torch.randn(B, Hm, Tm, Km) * 0.5 * (mask == 0)   # graded biases, max stays ~0
+    mask[0, :, -1, :] = float("-inf")    # -inf everywhere ...
+    mask[0, :, -1, 0] = 0.0              # ... except one key
+    mask[2, :, -5, :] = neg              # a row masked with finfo.min everywhere
+    mask = mask.clamp(max=0.0)
+    scale = 1 / math.sqrt(D)
+    lens_t = torch.tensor(lens, dtype=torch.int32)
+    out = ops.attn_prefill(q, None, kc, vc, bt, lens_t.to(gpu), q_start.to(gpu), max(q_lens),
+                           scale, mask=mask.to(gpu))
+    out_r = ref.attn_custom_mask(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), lens_t, q_start, scale,
+                                 mask)
+    _close(out, out_r, 2e-2, 2e-2, "prefill-custom-mask")
+    # a mask that only re-states causality equals the causal kernel
+    causal = torch.full((B, 1, Tm, Km), neg)
+    for b in range(B):
+        for t in range(q_lens[b]):
+            causal[b, 0, Tm - q_lens[b] + t, : lens[b] - q_lens[b] + t + 1] = 0.0
+    out_c = ops.attn_prefill(q, None, kc, vc, bt, lens_t.to(gpu), q_start.to(gpu), max(q_lens),
+                             scale, mask=causal.to(gpu))
+    out_p = ops.attn_prefill(q, None, kc, vc, bt, lens_t.to(gpu), q_start.to(gpu), max(q_lens),
+                             scale)
+    _close(out_c, out_p.cpu().float(), 1e-2, 1e-2, "custom-causal-vs-causal")
+
+
 @pytest.mark.parametrize("qb", ["1", "2"])
 def test_attn_prefill_window(gpu, qb, monkeypatch):
     monkeypatch.setenv("DLI_PREFILL_QB", qb)
