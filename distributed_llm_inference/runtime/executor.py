@@ -28,7 +28,7 @@ from .. import ops
 from ..models.common import AttnMetadata
 from ..models.llama.cache import KVPool
 from ..models.stage import CausalLMStage
-from ..utils.cuda import prime_graph_rng
+from ..utils.cuda import capture_guard, prime_graph_rng
 from .watchdog import wait_event
 
 log = logging.getLogger(__name__)
@@ -444,8 +444,8 @@ class StageExecutor:
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
         # thread_local: another thread (token publisher) may synchronise events meanwhile
-        with torch.cuda.graph(graph, pool=self._graph_pool, stream=s,
-                              capture_error_mode="thread_local"):
+        with capture_guard(), torch.cuda.graph(graph, pool=self._graph_pool, stream=s,
+                                               capture_error_mode="thread_local"):
             out = self._forward(meta, x, n_sample, project)
         cur.wait_stream(s)
         entry = _GraphEntry(graph, out)

@@ -29,7 +29,7 @@ import torch
 
 from .. import ops
 from ..models.embed_head import LMHead
-from ..utils.cuda import prime_graph_rng
+from ..utils.cuda import capture_guard, prime_graph_rng
 from .executor import StepPlan, _Staging, _fill_pos
 from .watchdog import TRACKER
 
@@ -165,7 +165,8 @@ class HeadRunner:
         if self._pool is None:
             self._pool = torch.cuda.graph_pool_handle()
         # thread_local: publisher threads may synchronise events while this captures
-        with torch.cuda.graph(g, pool=self._pool, stream=s, capture_error_mode="thread_local"):
+        with capture_guard(), torch.cuda.graph(g, pool=self._pool, stream=s,
+                                               capture_error_mode="thread_local"):
             self._forward(rows)
         cur.wait_stream(s)
         self._graphs[rows] = g

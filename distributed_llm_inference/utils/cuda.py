@@ -13,6 +13,8 @@ decode step per batch bucket (``StageExecutor._capture`` in ``runtime/executor.p
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 from typing import Callable
 
 import torch
@@ -20,6 +22,22 @@ from torch.utils._pytree import tree_flatten, tree_unflatten
 
 
 _RNG_PRIMED: dict = {}
+
+
+@contextlib.contextmanager
+def capture_guard():
+    """No Python garbage collection while a graph is being captured: ``torch.cuda.graph`` runs
+    ``gc.collect()`` before capture begins, but an automatic collection triggered by the
+    allocations DURING the capture can destroy an unrelated dead object whose destructor makes a
+    stream-capture-illegal HIP call (freeing another graph's pool, destroying an event) and
+    abort the process.  Collection resumes (and catches up) after the capture."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def prime_graph_rng(device=None) -> None:
@@ -40,7 +58,7 @@ def prime_graph_rng(device=None) -> None:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.stream(s):
+        with torch.cuda.stream(s), capture_guard():
             with torch.cuda.graph(g, stream=s):
                 torch.empty(1, device=f"cuda:{idx}").fill_(0)
         torch.cuda.current_stream().wait_stream(s)
@@ -69,7 +87,7 @@ def make_inference_graphed_callable(callable: Callable, sample_args, num_warmup_
 
     prime_graph_rng()
     graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, pool=pool):
+    with capture_guard(), torch.cuda.graph(graph, pool=pool):
         outputs = callable(*sample_args)
     flat_out, spec = tree_flatten(outputs)
     static_outputs = tuple(flat_out)
