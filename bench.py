@@ -66,6 +66,28 @@ def parse():
     return ap.parse_args()
 
 
+_T0 = time.perf_counter()
+_PHASE = {"phase": "start"}
+
+
+def _progress(msg: str) -> None:
+    """Progress on stderr (a long multi-rank init / prefill must never look hung)."""
+    _PHASE["phase"] = msg
+    print(f"[bench rank {os.environ.get('RANK', '0')} +{time.perf_counter() - _T0:.0f}s] {msg}",
+          file=sys.stderr, flush=True)
+
+
+def _heartbeat(every_s: float = 30.0) -> None:
+    import threading
+
+    def run():
+        while True:
+            time.sleep(every_s)
+            print(f"[bench rank {os.environ.get('RANK', '0')} +{time.perf_counter() - _T0:.0f}s] "
+                  f"alive: {_PHASE['phase']}", file=sys.stderr, flush=True)
+    threading.Thread(target=run, name="bench-heartbeat", daemon=True).start()
+
+
 def _rank_record(node, rank: int, window_s: float) -> dict:
     """This rank's share of the timed window (between the last two barriers): stage range,
     data-plane transport, device compute per micro-batch step, receive stalls, traffic."""
@@ -110,6 +132,8 @@ def main():
     if a.dp < 1 or a.gpus % a.dp:
         raise SystemExit(f"--dp {a.dp} must divide --gpus {a.gpus}")
     dp, pp = a.dp, a.gpus // a.dp
+    os.environ.setdefault("DLI_PROGRESS", "1")   # init phases on stderr (runtime/engine.py)
+    _heartbeat()
     if rank == 0:
         _build.build_all()
     if world > 1:
@@ -126,7 +150,9 @@ def main():
                           num_micro_batches=M, max_seq_len=total_len, use_graphs=not a.no_graphs,
                           graph_batch_sizes=[a.batch_per_mb]))
     t_init = time.perf_counter()
+    _progress("init")
     role, obj = init_pipeline_rank(cfg)
+    _progress(f"init done ({role})")
 
     def world_reduce(elapsed: float, toks: int, rec: dict):
         """Same collectives on every rank, in the same order: max window, summed tokens, records."""
@@ -140,7 +166,9 @@ def main():
         return float(t.item()), int(n.item()), recs
 
     if role == "follower":
+        _progress("serving the driver's steps")
         obj.run()
+        _progress("stopped")
         interval = obj.barrier_times[-1] - obj.barrier_times[-2] if len(obj.barrier_times) >= 2 else 0.0
         world_reduce(interval, 0, _rank_record(obj, rank, interval))
         obj.close()
@@ -165,9 +193,15 @@ def main():
         drv.sched.add(s)
     # prefill: run until every sequence produced its first token
     t_pf = time.perf_counter()
+    _progress(f"prefill of {G} prompts x {a.prompt_len} tokens")
+    n_rounds = 0
     while any(len(s.output) == 0 for s in seqs):
         drv.round()
+        n_rounds += 1
+        if n_rounds % 20 == 0:
+            _progress(f"prefill: {sum(len(s.output) > 0 for s in seqs)}/{G} prompts done")
     prefill_s = time.perf_counter() - t_pf
+    _progress(f"prefill done in {prefill_s:.1f}s; warmup")
     for _ in range(a.warmup):
         drv.round()
     drv.barrier()
@@ -175,12 +209,14 @@ def main():
     n0 = sum(len(s.output) for s in seqs)
     for s in seqs:
         s.token_times.clear()
+    _progress(f"timed: {a.steps} steps")
     t0 = time.perf_counter()
     w0 = drv.wait_s
     for _ in range(a.steps):
         drv.round()
     drv.barrier()
     t1 = time.perf_counter()
+    _progress(f"timed window {t1 - t0:.2f}s")
     sync_replicas()
     driver_busy = (t1 - t0) - (drv.wait_s - w0)
     n1 = sum(len(s.output) for s in seqs)

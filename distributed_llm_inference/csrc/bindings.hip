@@ -572,7 +572,7 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
   CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
   TORCH_CHECK(epilogue == 3 ? out.element_size() == 1 : out.scalar_type() == at::kBFloat16,
               "gemm_tile: bf16 output (fp8 bytes for epilogue 3)");
-  const bool bf16_parts = epilogue == 4;   // fp8 operands: bf16 split-K partials into out [S, M, N]
+  const bool bf16_parts = epilogue == 4;   // bf16 split-K partials into out [S, M, N]
   const bool fp8 = a.element_size() == 1;   // 1-byte operands: fp8 e4m3 or int8
   TORCH_CHECK(a.scalar_type() == b.scalar_type(), "gemm_tile: a and b must share a dtype");
   TORCH_CHECK(fp8 || a.scalar_type() == at::kBFloat16, "gemm_tile: bf16, fp8 (e4m3) or int8 operands");
@@ -582,12 +582,11 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
   TORCH_CHECK(b.size(1) == K && (bf16_parts || out.size(0) == M), "gemm_tile: shape mismatch");
   TORCH_CHECK(epilogue >= 0 && epilogue <= 4,
               "gemm_tile: epilogue must be 0 (store), 1 (split-K partials only), 2 (swiglu), 3 "
-              "(swiglu -> fp8 with MX scales) or 4 (bf16 split-K partials, fp8)");
+              "(swiglu -> fp8 with MX scales) or 4 (bf16 split-K partials)");
   TORCH_CHECK(epilogue == 1 || bf16_parts || out.size(1) == (epilogue >= 2 ? N / 2 : N),
               "gemm_tile: output columns");
-  TORCH_CHECK(!bf16_parts || (fp8 && splits > 1 && out.is_contiguous() &&
-                              out.numel() == splits * M * N),
-              "gemm_tile: epilogue 4 = 8-bit operands, splits > 1, out [splits, M, N] bf16");
+  TORCH_CHECK(!bf16_parts || (splits > 1 && out.is_contiguous() && out.numel() == splits * M * N),
+              "gemm_tile: epilogue 4 = splits > 1, out [splits, M, N] bf16");
   // fp8 MX activations: e8m0 scale per (row, 128-column block), layout of gemm_tile.hip mx_off
   const int64_t nb = (M + 63) / 64;
   const uint8_t* amx = nullptr;

@@ -719,9 +719,12 @@ __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_ke
     n_main = (seg_len + 31) >> 5;
   }
   const int nsteps = n_main + n_sinkst;
-  // custom additive mask row of this lane's query (clamped finite: a fully masked row then
-  // averages V like the reference's fp32 softmax over finfo.min, instead of dividing by 0),
-  // pre-divided by the softmax scale because the scores are scaled inside the exponent
+  // custom additive mask row of this lane's query, pre-divided by the softmax scale because the
+  // scores are scaled inside the exponent.  Entries <= -1e4 (-inf, finfo.min, -1e9 ...) mask the
+  // key outright: exp(-1e4) is 0 in fp32 next to any live score, and keeping such magnitudes out
+  // of the exponent's FMA avoids its rounding residual (half an ulp of ~1e38 is ~1e31).  A row
+  // with no live key outputs zeros (the reference's fp32 softmax over finfo.min would average V;
+  // such rows are padding, ops/reference.py attn_custom_mask defines them the same way).
   const float* mrow = nullptr;
   float minv = 0.f;
   int mlen = 0;   // keys [0, mlen) have a mask column (bounds of the caller's tensor)
@@ -850,11 +853,15 @@ __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_ke
         // keys 8h4 + j < L are candidates; the mask decides (its -inf / finfo.min entries drop out)
         const int k0 = u0 + 8 * h4;
         float madd[8];
+        unsigned vis = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          madd[j] = k0 + j < mlen ? fmaxf(mrow[k0 + j], -1e20f) * minv : 0.f;
-        const int lim = mlen - 1 - k0;
-        attn_core<D>(st[qb], qf[qb], f, sl2, [&](int j) { return j <= lim; },
+        for (int j = 0; j < 8; ++j) {
+          const float mv = k0 + j < mlen ? mrow[k0 + j] : -INFINITY;
+          const bool ok = mv > -1e4f;
+          madd[j] = ok ? mv * minv : 0.f;
+          vis |= (ok ? 1u : 0u) << j;
+        }
+        attn_core<D>(st[qb], qf[qb], f, sl2, [&](int j) { return ((vis >> j) & 1u) != 0; },
                      [&](int j) { return madd[j]; });
         continue;
       }

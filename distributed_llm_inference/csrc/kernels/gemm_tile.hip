@@ -60,8 +60,8 @@ constexpr int kHalf = 128 * 128;       // bytes of one half-tile (128 rows x 64 
 constexpr int kBuf = 4 * kHalf;        // A0 A1 B0 B1
 constexpr int kLds = 2 * kBuf;         // double buffer: 128 KB
 
-// kStoreBf16Part: split-K partials rounded to bf16 (8-bit operands only: half the partial bytes of
-// kStoreF32 for the consumers that sum them; the 8-bit activations carry far more error)
+// kStoreBf16Part: split-K partials rounded to bf16 (half the partial bytes of kStoreF32 for the
+// consumers that sum them; default for 8-bit operands, DLI_BF16_PARTS for bf16 ones)
 enum Epilogue { kStoreBf16 = 0, kStoreF32 = 1, kSwiGLU = 2, kSwiGLUMx = 3, kStoreBf16Part = 4 };
 
 // stream-K workspace header: flags [0, kSkMaxWgs), error counter at kSkErrWord, slabs after
@@ -752,15 +752,11 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
   if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
   if (PREC == kFp8Mx && kps > kMxMaxKt) return -15;   // its scales must fit the LDS slot
   if (epilogue == kStoreBf16Part) {   // bf16 partials into C [splits, M, N]; the consumer sums
-    if constexpr (PREC != kBf16) {
-      if (splits < 2) return -3;
-      sk.n_dp = tiles * splits;   // the block remap covers the whole grid
-      gemm_tile_kernel<kStoreBf16Part, PREC, false><<<tiles * splits, kThreads, 0, stream>>>(
-          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
-      return 0;
-    } else {
-      return -4;
-    }
+    if (splits < 2) return -3;
+    sk.n_dp = tiles * splits;   // the block remap covers the whole grid
+    gemm_tile_kernel<kStoreBf16Part, PREC, false><<<tiles * splits, kThreads, 0, stream>>>(
+        A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
+    return 0;
   }
   // kStoreF32 with splits > 1: partials only, the consumer reduces them (rms_norm_splitk)
   if (splits > 1 && (workspace == nullptr || epilogue == kSwiGLU)) return -3;

@@ -88,6 +88,14 @@ def fp8_bf16_partials() -> bool:
     return os.environ.get("DLI_FP8_BF16_PARTS", "1") != "0"
 
 
+def bf16_bf16_partials() -> bool:
+    """bf16 operands: split-K partials of the deferred projections (QKV, O, down) stored as bf16
+    (``DLI_BF16_PARTS=1``) instead of fp32.  Half the partial traffic of the GEMM epilogue and
+    of the consumer that sums them (RMSNorm / RoPE); each partial carries one extra bf16
+    rounding (~2^-9 relative) before the fp32 sum."""
+    return os.environ.get("DLI_BF16_PARTS", "0") == "1"
+
+
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
              out: Optional[torch.Tensor] = None, residual_out: Optional[torch.Tensor] = None
              ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
@@ -450,6 +458,10 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = 
     M, N = x.shape[0], w.shape[0]
     if (defer_reduce and splits > 1 and _gpu(x) and not swiglu
             and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
+        if bf16_bf16_partials():
+            parts = torch.empty(splits, M, N, dtype=torch.bfloat16, device=x.device)
+            native().gemm_tile(parts, x, w, int(splits), 4)
+            return SplitKPartials(parts)
         parts = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
         dummy = torch.empty(M, 0, dtype=torch.bfloat16, device=x.device)   # C is unused
         native().gemm_tile(dummy, x, w, int(splits), 1, parts.view(-1))

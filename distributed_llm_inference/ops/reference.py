@@ -213,7 +213,12 @@ def attn_custom_mask(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale
         Vf = V.float().repeat_interleave(G, dim=1)
         scores = torch.einsum("nhd,shd->hns", q[s0:s1].float(), Kf) * scale    # [nh, ql, L]
         mb = mask[b, :, -ql:, :L].to(device=q.device, dtype=torch.float32)    # [1|nh, ql, L]
-        p = torch.softmax(scores + mb, dim=-1)
+        # entries <= -1e4 mask the key outright (exactly what exp gives next to any live score);
+        # a query row with no live key outputs zeros (padding rows: the reference's eager
+        # softmax over finfo.min would average V there, HF's SDPA path unmasks such rows)
+        live = mb > -1e4
+        p = torch.softmax((scores + mb).masked_fill(~live, float("-inf")), dim=-1)
+        p = torch.nan_to_num(p, nan=0.0) * live.any(-1, keepdim=True)
         out[s0:s1] = torch.einsum("hns,shd->nhd", p, Vf).to(q.dtype)
     return out
 

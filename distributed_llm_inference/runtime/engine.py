@@ -193,6 +193,16 @@ class ReplicaLayout:
                              for r in range(self.dp)]}
 
 
+def _progress(msg: str) -> None:
+    """``DLI_PROGRESS=1``: rank init phases on stderr (bench.py sets it; a multi-rank init of a
+    70B stage takes minutes and must never look hung)."""
+    if os.environ.get("DLI_PROGRESS") == "1":
+        import sys
+        import time
+        print(f"[dli rank {os.environ.get('RANK', '0')} {time.strftime('%H:%M:%S')}] {msg}",
+              file=sys.stderr, flush=True)
+
+
 def _dp_from_env(cfg: EngineConfig) -> int:
     return int(os.environ.get("DLI_DP", cfg.dp or 1))
 
@@ -272,7 +282,9 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         head = build_head(cfg.checkpoint or spec, device=device,
                           random_init=cfg.random_init and cfg.checkpoint is None, seed=cfg.seed,
                           checkpoint=cfg.checkpoint)
+    _progress(f"building stage [{start},{end}) of {spec.name} on {device}")
     ex = build_executor(spec, start, end, device, cfg, group=group, kv_share=kv_share)
+    _progress(f"stage built: {ex.pool.num_blocks} KV blocks; connecting the transport")
     if streams is not None:
         ex.capture_stream = streams.capture
     H = spec.hidden_size
@@ -297,10 +309,12 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         # capture every decode graph NOW, before any transport traffic: no capture ever runs
         # next to in-flight receive kernels or the token publisher thread
         variants = (True, False) if (rotate and srank == pp - 1) else (True,)
+        _progress(f"transport up ({type(transport).__name__}); capturing decode graphs")
         ex.warmup_graphs(variants=variants)
         if heads_runner is not None:
             heads_runner.warmup()
         dist.barrier(group=group)
+        _progress("graphs captured")
     if srank == 0:
         sched = make_scheduler(spec, ex, cfg, pp)
         drv = DistributedDriver(ex, sched, transport, channels, pp, group, policy=policy)

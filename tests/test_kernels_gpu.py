@@ -157,6 +157,29 @@ def test_gemm_tile_fp8_bf16_partials(gpu, M, N, K, splits, monkeypatch):
     assert torch.equal(pb, pf.to(BF))
 
 
+@pytest.mark.parametrize("M,N,K,splits", [(512, 1024, 8192, 4), (300, 768, 2048, 3)])
+def test_gemm_tile_bf16_operand_bf16_partials(gpu, M, N, K, splits, monkeypatch):
+    """bf16 operands, DLI_BF16_PARTS=1: epilogue 4 writes each split's fp32 partial rounded to
+    bf16 - exactly the fp32 partials' rounding - and RMSNorm over them stays within one bf16
+    ulp-scale of the fp32-partials result."""
+    torch.manual_seed(M + K + 1)
+    x = torch.randn(M, K, device=gpu).to(BF)
+    w = (torch.randn(N, K, device=gpu) / K ** 0.5).to(BF)
+    monkeypatch.setenv("DLI_BF16_PARTS", "0")
+    pf = ops.gemm_tile(x, w, splits, defer_reduce=True).parts
+    monkeypatch.setenv("DLI_BF16_PARTS", "1")
+    pb = ops.gemm_tile(x, w, splits, defer_reduce=True).parts
+    assert pb.dtype == BF and pf.dtype == torch.float32
+    assert torch.equal(pb, pf.to(BF))
+    nw = torch.rand(N, device=gpu).to(BF) + 0.5
+    r1 = torch.randn(M, N, device=gpu).to(BF)
+    r2 = r1.clone()
+    y1, _ = ops.rms_norm(ops.SplitKPartials(pf), nw, 1e-5, r1)
+    y2, _ = ops.rms_norm(ops.SplitKPartials(pb), nw, 1e-5, r2)
+    _close(y2, y1, 2e-2, 2e-2, "rms over bf16 partials")
+    _close(r2, r1, 2e-2, 2e-2, "residual over bf16 partials")
+
+
 def _tables(B, max_blocks, nblocks, dev, seed=0):
     g = torch.Generator().manual_seed(seed)
     perm = torch.randperm(nblocks, generator=g)[: B * max_blocks]
@@ -278,7 +301,7 @@ def test_attn_prefill_custom_mask(gpu, heads, D):
     """The reference API's pre-inverted 4-D additive mask in the HIP prefill kernel (masked
     variant) against the fp32 oracle ref.attn_custom_mask: ragged lengths, mixed chunk / decode
     rows, a mask that opens future keys (no causal mask is added), finfo.min and -inf entries,
-    a row open to a single key and a row masked with finfo.min everywhere (mean of V)."""
+    a row open to a single key and a row masked with finfo.min everywhere (zeros)."""
     torch.manual_seed(11)
     nh, nkv, bs = 8, 2, 64
     q_lens = [9, 1, 40, 3]
@@ -297,7 +320,7 @@ def test_attn_prefill_custom_mask(gpu, heads, D):
     mask += torch.randn(B, Hm, Tm, Km) * 0.5 * (mask == 0)   # graded biases, max stays ~0
     mask[0, :, -1, :] = float("-inf")    # -inf everywhere ...
     mask[0, :, -1, 0] = 0.0              # ... except one key
-    mask[2, :, -5, :] = neg              # a row masked with finfo.min everywhere
+    mask[2, :, -5, :] = neg              # a row masked with finfo.min everywhere (-> zeros)
     mask = mask.clamp(max=0.0)
     scale = 1 / math.sqrt(D)
     lens_t = torch.tensor(lens, dtype=torch.int32)

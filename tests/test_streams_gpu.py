@@ -25,13 +25,13 @@ def _small_stage_graph(dev, capture):
     cur = torch.cuda.current_stream()
     capture.wait_stream(cur)
     with torch.cuda.stream(capture):
-        y = ops.rms_norm(x @ w, nw, 1e-5)
+        y = ops.rms_norm(x @ w, nw, 1e-5)[0]
     cur.wait_stream(capture)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=capture):
         y = x
         for _ in range(6):
-            y = ops.rms_norm(y @ w, nw, 1e-5)
+            y = ops.rms_norm(y @ w, nw, 1e-5)[0]
     torch.cuda.synchronize()
     return g
 
