@@ -8,6 +8,8 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
+#include <cstdlib>
+
 #include "kernels/kernels.h"
 
 using at::Tensor;
@@ -316,6 +318,11 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
   TORCH_CHECK(seq_lens.numel() == B, "decode: one token per sequence (seq_lens must have T entries)");
   TORCH_CHECK(num_splits >= 1, "num_splits >= 1");
   p.num_splits = (int)num_splits;
+  static const int kv_nt = [] {   // DLI_KV_NT=1: non-temporal K/V loads (A/B switch)
+    const char* e = std::getenv("DLI_KV_NT");
+    return e != nullptr && e[0] == '1' ? 1 : 0;
+  }();
+  p.kv_nt = kv_nt;
   TORCH_CHECK(out_q.has_value() == out_mx.has_value(), "attn_decode: out_q and out_mx go together");
   if (out_q.has_value()) {   // MX fp8 output for the fp8 O projection
     CHECK_IN(*out_q); CHECK_IN(*out_mx);

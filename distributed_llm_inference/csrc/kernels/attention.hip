@@ -91,7 +91,18 @@ __device__ __forceinline__ int q_dofs(int c, int h4) {
 //   kc/vc: the K / V^T caches, hb: element offset of this kv head's page, offk: slot offset of the
 //   step inside the page.  fp8 caches widen to bf16 in registers (exact), so both MFMA products
 //   stay bf16 x bf16.
-template <int D, bool FP8>
+// 16-B K/V load; NT = non-temporal (the cache is streamed once per step: no reuse to keep)
+template <bool NT>
+__device__ __forceinline__ bf16x8 kv_ld16(const bf16* p) {
+  if constexpr (NT) {
+    typedef int i32x4_t __attribute__((ext_vector_type(4)));
+    return __builtin_bit_cast(bf16x8, __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(p)));
+  } else {
+    return *reinterpret_cast<const bf16x8*>(p);
+  }
+}
+
+template <int D, bool FP8, bool NT = false>
 __device__ __forceinline__ void attn_load(KVFrag<D>& f, const void* __restrict__ kc,
                                           const void* __restrict__ vc, size_t hb, int offk) {
   const int lane = threadIdx.x & 63;
@@ -125,7 +136,7 @@ __device__ __forceinline__ void attn_load(KVFrag<D>& f, const void* __restrict__
       if (FP8)
         f.k[t][c] = fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(kc) + e));
       else
-        f.k[t][c] = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(kc) + e);
+        f.k[t][c] = kv_ld16<NT>(static_cast<const bf16*>(kc) + e);
     }
 #pragma unroll
   for (int e = 0; e < D / 16; ++e) {
@@ -133,7 +144,7 @@ __device__ __forceinline__ void attn_load(KVFrag<D>& f, const void* __restrict__
     if (FP8)
       f.v[e] = fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(vc) + o));
     else
-      f.v[e] = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(vc) + o);
+      f.v[e] = kv_ld16<NT>(static_cast<const bf16*>(vc) + o);
   }
 }
 
@@ -302,7 +313,7 @@ __device__ __forceinline__ unsigned step_mask(int u0, int h4, int seg_base, int 
   return vm;
 }
 
-template <int D, bool WIN, bool FP8, bool GRP>
+template <int D, bool WIN, bool FP8, bool GRP, bool NT = false>
 __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int items, int gs) {
   // GRP (num_splits > 1): the `gs` consecutive splits of one work item that share this
   // workgroup are merged in LDS, so only num_splits / gs partials per head reach global memory
@@ -363,7 +374,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
         const int u0 = seg_base + sidx * 32;
         const int page = bt[u0 / p.bs];
         const size_t hb = ((size_t)page * p.nkv + kvh) * head_stride;
-        attn_load<D, FP8>(f, p.k_cache, p.v_cache, hb, u0 % p.bs);
+        attn_load<D, FP8, NT>(f, p.k_cache, p.v_cache, hb, u0 % p.bs);
       };
       if constexpr (DPerm<D, FP8>::on) {
         // three raw steps in flight, each widened right before its MFMAs
@@ -927,6 +938,8 @@ static void decode_grid(const AttnParams& p, int items, int gs, hipStream_t stre
   const int grid = (items + 3) / 4;
   if (p.num_splits > 1)
     attn_decode_kernel<D, WIN, FP8, true><<<grid, 256, 0, stream>>>(p, items, gs);
+  else if (!FP8 && !WIN && p.kv_nt)   // large-batch bf16 full-cache decode: non-temporal stream
+    attn_decode_kernel<D, false, false, false, true><<<grid, 256, 0, stream>>>(p, items, 1);
   else
     attn_decode_kernel<D, WIN, FP8, false><<<grid, 256, 0, stream>>>(p, items, 1);
 }

@@ -34,6 +34,8 @@ struct AttnParams {
   // mask_q - qlen_b + t (the last qlen_b rows), key k column k.  No causal mask is added.
   const float* mask = nullptr;
   int mask_heads = 0, mask_q = 0, mask_k = 0;
+  // decode, bf16 full cache, one split: load K / V non-temporally (streamed once per step)
+  int kv_nt = 0;
 };
 
 struct RopeCacheParams {

@@ -90,10 +90,11 @@ def fp8_bf16_partials() -> bool:
 
 def bf16_bf16_partials() -> bool:
     """bf16 operands: split-K partials of the deferred projections (QKV, O, down) stored as bf16
-    (``DLI_BF16_PARTS=1``) instead of fp32.  Half the partial traffic of the GEMM epilogue and
-    of the consumer that sums them (RMSNorm / RoPE); each partial carries one extra bf16
-    rounding (~2^-9 relative) before the fp32 sum."""
-    return os.environ.get("DLI_BF16_PARTS", "0") == "1"
+    (default; ``DLI_BF16_PARTS=0`` keeps fp32).  Half the partial traffic of the GEMM epilogue
+    and of the consumer that sums them (RMSNorm / RoPE); each partial carries one extra bf16
+    rounding (~2^-9 relative) before the fp32 sum.  Measured on the default bench (same box,
+    interleaved): 6468-6482 -> 6556-6574 tok/s (profiles/bf16_partials_ab.txt)."""
+    return os.environ.get("DLI_BF16_PARTS", "1") == "1"
 
 
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,

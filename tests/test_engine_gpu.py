@@ -366,10 +366,17 @@ def test_deferred_splitk_reduce_is_bit_identical(gpu, monkeypatch):
                         head_dim=128)
     g = CausalLMStage(spec, 0, 4, device=gpu).init_random(5)
     prompts = [list(range(1, 200)), list(range(3, 150))]   # 347 rows: tile GEMMs with split-K
+    monkeypatch.setenv("DLI_BF16_PARTS", "0")   # fp32 partials: the bit-identity claim
     a = _stage_logits(g, prompts, 0)[0]
     monkeypatch.setenv("DLI_SPLITK_DEFER", "0")
     b = _stage_logits(g, prompts, 0)[0]
     assert torch.equal(a, b)
+    # default bf16 partials (one extra bf16 rounding per partial): close, not identical
+    monkeypatch.setenv("DLI_SPLITK_DEFER", "1")
+    monkeypatch.setenv("DLI_BF16_PARTS", "1")
+    c = _stage_logits(g, prompts, 0)[0]
+    rel = ((c.float() - b.float()).norm() / b.float().norm()).item()
+    assert rel < 1e-2, rel
 
 
 def test_deferred_splitk_reduce_is_bit_identical_fp8(gpu, monkeypatch):
