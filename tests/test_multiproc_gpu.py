@@ -121,6 +121,62 @@ def test_multiprocess_pipeline_ipc_transport(gpu, world, mbs, rotation):
     assert got == ref
 
 
+def _ipc_timeout_worker(rank, port, q):
+    try:
+        os.environ.update(RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                          MASTER_PORT=str(port), DLI_P2P_TIMEOUT_S="2")
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        from distributed_llm_inference.parallel.ipc_transport import IpcTransport
+        from distributed_llm_inference.runtime.faults import raw_store
+        from distributed_llm_inference.runtime.streams import RankStreams
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        rs = RankStreams(dev)
+        tr = IpcTransport(raw_store(), rank, 2, dev, rs, max_bytes=1 << 16)
+        if rank == 0:   # one message, then silence
+            tr.send(torch.ones(1024, device=dev, dtype=torch.bfloat16), 1)
+            torch.cuda.synchronize()
+            q.put(("sent", None))
+        else:
+            x = torch.empty(1024, device=dev, dtype=torch.bfloat16)
+            tr.recv(x, 0)
+            torch.cuda.synchronize()
+            ok = bool((x == 1).all())
+            tr.recv(x, 0)            # never sent: the device wait hits its 2 s deadline
+            torch.cuda.synchronize()
+            try:
+                tr.check()
+                q.put(("no-timeout", ok))
+            except TimeoutError as e:
+                q.put(("timeout", (ok, str(e))))
+        dist.barrier()
+        tr.close()
+        dist.destroy_process_group()
+    except Exception:
+        q.put(("err", traceback.format_exc()))
+
+
+def test_ipc_transport_wait_deadline_is_reported(gpu):
+    """A receive whose sender never arrives: the spinning device wait exits at its deadline
+    (DLI_P2P_TIMEOUT_S) and the transport raises TimeoutError naming the channel - no wave is
+    left spinning, the process exits normally."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_ipc_timeout_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert "sent" in res, res
+    assert "timeout" in res, res
+    ok, msg = res["timeout"]
+    assert ok and "stage 0->1" in msg and "receive" in msg, res
+    assert all(p.exitcode == 0 for p in ps)
+
+
 def _run_pair(transport, timeout=600):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
