@@ -182,6 +182,10 @@ class IpcTransport(Transport):
             raise TimeoutError(f"[rank {self.rank}] IPC transport: {'receive' if recv else 'send'} "
                                f"on {what} waited > {self.timeout_s} s for its peer")
 
+    def counters(self) -> dict:
+        """Messages issued per channel on this end (host side; the watchdog's record)."""
+        return {c.describe(): c.n for c in self._ch.values()}
+
     def describe(self) -> dict:
         return {"transport": "IpcTransport",
                 "channels": sorted(c.describe() for c in self._ch.values()),

@@ -344,7 +344,8 @@ class StageFollower:
 
     def _start_publisher(self) -> None:
         if self._pub_thread is None:
-            self._pub_thread = threading.Thread(target=self._publisher, daemon=True)
+            self._pub_thread = threading.Thread(target=self._publisher, name="dli-publisher",
+                                                daemon=True)
             self._pub_thread.start()
 
     def publish(self, plan: StepPlan, pinned, ev) -> None:

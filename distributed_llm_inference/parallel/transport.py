@@ -57,6 +57,10 @@ class Transport:
         """What carries the data plane (reported by bench.py per rank)."""
         return {"transport": type(self).__name__}
 
+    def counters(self) -> dict:
+        """Per-link message counts (the watchdog's abort record)."""
+        return {"msgs_sent": self.msgs_sent, "msgs_recv": self.msgs_recv}
+
     def send(self, t: torch.Tensor, peer: int) -> None:
         raise NotImplementedError
 

@@ -292,8 +292,9 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
                                streams=streams, max_bytes=ex.max_tokens * H * 2,
                                head_bytes=ex.max_num_seqs * H * 2)
     # a stalled wait or a failed rank ends the whole job with every rank's last op (watchdog.py)
-    from .watchdog import start_watchdog
+    from .watchdog import TRACKER, start_watchdog
     start_watchdog(base_job, world, on_abort=getattr(transport, "abort", None))
+    TRACKER.add_state("transport", transport.counters)
     # the fallback transport (agreed on by every rank) cannot carry the head: then nobody rotates
     rotate = rotate and transport.supports_head
     channels = _Channels(job, srank, pp, head_rotation=rotate)
@@ -321,12 +322,15 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         if heads_runner is not None:
             drv.heads = HeadJobs(heads_runner, transport, pp - 1, drv.publish_local, delay=pp,
                                  stream=streams.head if streams is not None else None)
+            TRACKER.add_state("head_jobs", drv.heads.state)
         drv.streams = streams
+        TRACKER.add_state("driver", lambda: {"inflight": [(p.step, p.mb) for p in drv.inflight]})
         return "driver", tag(drv)
     fol = StageFollower(ex, transport, channels, srank, pp, group, policy=policy)
     if heads_runner is not None:
         fol.heads = HeadJobs(heads_runner, transport, pp - 1, fol.publish, delay=pp - srank,
                              stream=streams.head if streams is not None else None)
+        TRACKER.add_state("head_jobs", fol.heads.state)
         fol._start_publisher()
     fol.streams = streams
     return "follower", tag(fol)

@@ -202,6 +202,7 @@ class HeadJobs:
         self._pending: Deque[tuple] = collections.deque()    # CPU: (plan, buf, work)
         self._deferred: Deque[list] = collections.deque()    # GPU: [plan, age]
         self.jobs = 0
+        self.enqueued = 0
 
     def submit(self, plan: StepPlan) -> None:
         self.jobs += 1
@@ -230,9 +231,15 @@ class HeadJobs:
     def deferred(self) -> int:
         return len(self._deferred)
 
+    def state(self) -> dict:
+        """Snapshot for the watchdog's record: jobs submitted, waiting to be enqueued, enqueued."""
+        return {"jobs": self.jobs, "deferred": [(j[0].step, j[1]) for j in self._deferred],
+                "enqueued": self.enqueued, "pending_cpu": len(self._pending), "delay": self.delay}
+
     def _enqueue(self, plan: StepPlan) -> None:
         B = len(plan.seq_ids)
         TRACKER.mark("head-recv", plan.step, plan.mb, peer=self.last, stream="head")
+        self.enqueued += 1
         with torch.cuda.stream(self.stream):
             x = self.runner.x[:B]
             self.tr.recv_head(x, self.last, self.stream)

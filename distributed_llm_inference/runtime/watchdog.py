@@ -32,14 +32,23 @@ class OpTracker:
     def __init__(self):
         self.rank = int(os.environ.get("RANK", "0"))
         self.last = {"op": "init", "step": -1, "mb": -1, "peer": -1, "stream": ""}
+        self.by_thread: dict = {}   # thread name -> its last op (the pipeline loop, publisher...)
         self.t_last = time.monotonic()
         self.ops = 0
         self._wait: Optional[dict] = None
+        self._state: dict = {}      # name -> callable returning a JSON-able snapshot
 
     def mark(self, op: str, step: int = -1, mb: int = -1, peer: int = -1, stream: str = "") -> None:
-        self.last = {"op": op, "step": step, "mb": mb, "peer": peer, "stream": stream}
+        rec = {"op": op, "step": step, "mb": mb, "peer": peer, "stream": stream}
+        self.by_thread[threading.current_thread().name] = rec
+        if threading.current_thread() is threading.main_thread():
+            self.last = rec
         self.t_last = time.monotonic()
         self.ops += 1
+
+    def add_state(self, name: str, fn) -> None:
+        """Register a snapshot provider (transport counters, head-job queue...) for the record."""
+        self._state[name] = fn
 
     @contextlib.contextmanager
     def waiting(self, what: str, step: int = -1, mb: int = -1, peer: int = -1):
@@ -57,10 +66,18 @@ class OpTracker:
         now = time.monotonic()
         r = {"rank": self.rank, "last_op": dict(self.last), "ops": self.ops,
              "s_since_last_op": round(now - self.t_last, 1)}
+        others = {k: v for k, v in self.by_thread.items() if k != threading.main_thread().name}
+        if others:
+            r["threads"] = others
         w = self._wait
         if w is not None:
             r["waiting"] = {k: v for k, v in w.items() if k != "t0"}
             r["waiting"]["for_s"] = round(now - w["t0"], 1)
+        for name, fn in list(self._state.items()):
+            try:
+                r[name] = fn()
+            except Exception as e:  # noqa: BLE001 - a snapshot must never block the abort
+                r[name] = repr(e)
         return r
 
 

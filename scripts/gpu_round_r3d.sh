@@ -13,5 +13,9 @@ for nt in 0 1 0 1; do
       > gpurun_out/bench_nt$nt.log 2>&1 || exit $?
   echo "nt=$nt $(grep '^{' gpurun_out/bench_nt$nt.log | tail -1 | cut -c1-200)" | tee -a gpurun_out/nt_ab.txt
 done
+timeout -k 10 300 python -u -m pytest -v --timeout 200 --timeout-method thread \
+    tests/test_multiproc_gpu.py -k "deadline" > gpurun_out/t_r3d.log 2>&1
+rc=$?; tail -2 gpurun_out/t_r3d.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 bash scripts/rehearsal_pp8_ipc.sh || exit $?
 exit 0
