@@ -21,6 +21,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -81,24 +82,48 @@ double wall_clock_hz(int device) {
 // ---------------------------------------------------------------------------------- kernels
 // One lane polls; the other lanes of the (single, 64-wide) wave only keep the launch shape legal.
 // ``status`` (host-mapped) receives ``code`` if the deadline passes; the wave always exits.
+// ``abort`` (host-mapped, optional): a nonzero word ends the wait at once (the job is leaving);
+// ``progress`` (host-mapped, optional): receives ``target`` once the wait is satisfied, so the
+// host can tell which wait of a stuck pipeline never completed without touching the GPU.
 __global__ void __launch_bounds__(64) wait_geq_kernel(const uint32_t* flag, uint32_t target,
                                                       uint64_t max_ticks, uint32_t* status,
-                                                      uint32_t code) {
+                                                      uint32_t code, const uint32_t* abort,
+                                                      uint32_t* progress) {
   if (threadIdx.x != 0) return;
   const uint64_t t0 = wall_clock64();
   while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
-    if ((uint64_t)(wall_clock64() - t0) > max_ticks) {
+    const bool aborted =
+        abort && __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+    if (aborted || (uint64_t)(wall_clock64() - t0) > max_ticks) {
       if (status) __hip_atomic_store(status, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
     __builtin_amdgcn_s_sleep(8);
   }
+  if (progress) __hip_atomic_store(progress, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Release-store ``value`` (every write queued before this kernel on its stream has completed:
-// stream order + the system-scope release make the data visible before the flag).
-__global__ void __launch_bounds__(64) signal_kernel(uint32_t* flag, uint32_t value) {
-  if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+// stream order + the system-scope release make the data visible before the flag); ``progress``
+// (host-mapped, optional) records the value for the host.
+__global__ void __launch_bounds__(64) signal_kernel(uint32_t* flag, uint32_t value,
+                                                    uint32_t* progress) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (progress) __hip_atomic_store(progress, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Stream-ordered device copy as a KERNEL on the caller's stream.  hipMemcpyAsync between two
+// device pointers may be carried out by an SDMA engine queue that the process's streams share:
+// a copy that must wait for a spinning credit wait on one stream then blocks, in that shared
+// in-order queue, the copy another stream needs to release its peer - a cross-process deadlock
+// the IPC rehearsal hit.  A copy kernel stays on its own stream's hardware queue.
+__global__ void __launch_bounds__(256) dev_copy_kernel(uint4* __restrict__ dst,
+                                                       const uint4* __restrict__ src, size_t n16) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16;
+       i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
 }
 
 // A trivial kernel for progress probes: out[0] += 1.
@@ -107,20 +132,35 @@ __global__ void __launch_bounds__(64) touch_kernel(uint32_t* out) {
 }
 
 void wait_geq(int64_t flag_ptr, int64_t target, double timeout_s, int64_t status_ptr, int64_t code,
-              int64_t stream, int device) {
+              int64_t stream, int device, int64_t abort_ptr, int64_t progress_ptr) {
   TORCH_CHECK(flag_ptr != 0, "wait_geq: null flag");
   TORCH_CHECK(timeout_s > 0 && timeout_s < 3600, "wait_geq: timeout must be in (0, 3600) s");
   const uint64_t ticks = (uint64_t)(timeout_s * wall_clock_hz(device));
   hipLaunchKernelGGL(wait_geq_kernel, dim3(1), dim3(64), 0, as_stream(stream),
                      reinterpret_cast<const uint32_t*>(flag_ptr), (uint32_t)target, ticks,
-                     reinterpret_cast<uint32_t*>(status_ptr), (uint32_t)code);
+                     reinterpret_cast<uint32_t*>(status_ptr), (uint32_t)code,
+                     reinterpret_cast<const uint32_t*>(abort_ptr),
+                     reinterpret_cast<uint32_t*>(progress_ptr));
   HIP_OK(hipGetLastError());
 }
 
-void signal(int64_t flag_ptr, int64_t value, int64_t stream) {
+void signal(int64_t flag_ptr, int64_t value, int64_t stream, int64_t progress_ptr) {
   TORCH_CHECK(flag_ptr != 0, "signal: null flag");
   hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, as_stream(stream),
-                     reinterpret_cast<uint32_t*>(flag_ptr), (uint32_t)value);
+                     reinterpret_cast<uint32_t*>(flag_ptr), (uint32_t)value,
+                     reinterpret_cast<uint32_t*>(progress_ptr));
+  HIP_OK(hipGetLastError());
+}
+
+void dev_copy(int64_t dst, int64_t src, int64_t nbytes, int64_t stream) {
+  TORCH_CHECK(dst && src && nbytes >= 0, "dev_copy: bad arguments");
+  TORCH_CHECK(nbytes % 16 == 0 && dst % 16 == 0 && src % 16 == 0,
+              "dev_copy: 16-byte aligned pointers and sizes");
+  if (nbytes == 0) return;
+  const size_t n16 = (size_t)nbytes / 16;
+  const size_t blocks = std::min<size_t>((n16 + 255) / 256, 2048);
+  hipLaunchKernelGGL(dev_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src), n16);
   HIP_OK(hipGetLastError());
 }
 
@@ -229,10 +269,13 @@ void register_streams(pybind11::module_& m) {
   m.def("wall_clock_hz", &wall_clock_hz);
   m.def("wait_geq", &wait_geq, pybind11::arg("flag_ptr"), pybind11::arg("target"),
         pybind11::arg("timeout_s"), pybind11::arg("status_ptr"), pybind11::arg("code"),
-        pybind11::arg("stream"), pybind11::arg("device"));
+        pybind11::arg("stream"), pybind11::arg("device"), pybind11::arg("abort_ptr") = 0,
+        pybind11::arg("progress_ptr") = 0);
   m.def("signal", &signal, pybind11::arg("flag_ptr"), pybind11::arg("value"),
-        pybind11::arg("stream"));
+        pybind11::arg("stream"), pybind11::arg("progress_ptr") = 0);
   m.def("touch", &touch, pybind11::arg("out"), pybind11::arg("stream") = 0);
+  m.def("dev_copy", &dev_copy, pybind11::arg("dst"), pybind11::arg("src"), pybind11::arg("nbytes"),
+        pybind11::arg("stream"));
   pybind11::class_<HostWords>(m, "HostWords")
       .def(pybind11::init<int64_t>())
       .def("set", &HostWords::set)

@@ -13,7 +13,10 @@ its own stream.  This transport reproduces that structure exactly, on one GPU or
 * message n uses slot s = n % slots, round u = n // slots.  Sender, on its send stream (after the
   compute that produced the data): wait ``free[s] >= u`` -> copy into the peer's slot -> release
   ``ready[s] = u + 1``.  Receiver, on its receive (or head) stream: wait ``ready[s] >= u + 1`` ->
-  copy out -> release ``free[s] = u + 1`` in the sender's memory;
+  copy out -> release ``free[s] = u + 1`` in the sender's memory.  The copies are kernels on the
+  same stream, never hipMemcpyAsync: a memcpy may run on an SDMA queue the process's streams
+  share, and one copy held there behind a spinning wait blocks the copy that would release it
+  (measured: the 8-rank rehearsal deadlocked in its third decode round with torch copies);
 * the waits are spinning kernels (csrc/comm/streams.hip), like RCCL's: they hold their stream -
   and, if it were shared, that stream's hardware queue - until the peer arrives.  That is the
   point: the GPU tests run the real HeadJobs / executor stream schedule against them.  Each wait
@@ -66,7 +69,12 @@ class IpcTransport(Transport):
         self.send_stream = streams.send
         self.recv_stream = streams.recv
         self.timeout_s = float(os.environ.get("DLI_P2P_TIMEOUT_S", timeout_s))
-        self.status = C.HostWords(4)   # [0]: code of the first expired wait (0 = none)
+        # host-mapped words: [0] code of the first expired wait (0 = none), [1] abort (nonzero
+        # ends every pending device wait), then 4 progress words per channel, written by the
+        # device as each wait / release completes: sender (credit seen, ready released),
+        # receiver (ready seen, credit released) - a stuck pipeline's record names the one
+        # wait that never completed, read without any GPU operation
+        self.status = C.HostWords(2 + 4 * 64)
         self.prefix = prefix
         self._ch: Dict[Tuple[str, int, int], _Channel] = {}
         edges: List[Tuple[str, int, int, int]] = [("stage", r, r + 1, max_bytes)
@@ -101,14 +109,19 @@ class IpcTransport(Transport):
     def _flag(self, buf, offset_bytes: int, s: int) -> int:
         return buf.ptr + offset_bytes + 4 * s
 
-    def _wait(self, ptr: int, target: int, code: int, stream) -> None:
+    def _prog(self, ch: _Channel, k: int) -> int:
+        return self.status.dev_ptr(2 + 4 * ch.cid + k)
+
+    def _wait(self, ptr: int, target: int, code: int, stream, progress: int = 0) -> None:
         self.C.wait_geq(ptr, target, self.timeout_s, self.status.dev_ptr(0), code,
-                        stream.cuda_stream, self.idx)
+                        stream.cuda_stream, self.idx, self.status.dev_ptr(1), progress)
 
     def _code(self, ch: _Channel, recv: bool) -> int:
         return 1 + 2 * ch.cid + (1 if recv else 0)
 
     def _send_on(self, ch: _Channel, t: torch.Tensor, stream) -> None:
+        if not t.is_contiguous():
+            t = t.contiguous()
         nb = t.numel() * t.element_size()
         if nb > ch.slot_bytes:
             raise ValueError(f"IPC {ch.describe()}: message of {nb} B > slot of {ch.slot_bytes} B")
@@ -117,12 +130,14 @@ class IpcTransport(Transport):
         free_ptr = self._flag(ch.own, 0, s)                               # my free words
         ready_ptr = self._flag(ch.data, ch.slot_bytes * ch.slots, s)      # peer's ready words
         with torch.cuda.stream(stream):
-            self._wait(free_ptr, u, self._code(ch, False), stream)
-            dst = ch.data.view(s * ch.slot_bytes, [nb], torch.uint8)
-            dst.copy_(t.contiguous().view(-1).view(torch.uint8), non_blocking=True)
-            self.C.signal(ready_ptr, u + 1, stream.cuda_stream)
+            self._wait(free_ptr, u, self._code(ch, False), stream, self._prog(ch, 0))
+            # copy KERNEL on this stream (not hipMemcpyAsync: see csrc/comm/streams.hip dev_copy)
+            self.C.dev_copy(ch.data.ptr + s * ch.slot_bytes, t.data_ptr(), nb, stream.cuda_stream)
+            self.C.signal(ready_ptr, u + 1, stream.cuda_stream, self._prog(ch, 1))
 
     def _recv_on(self, ch: _Channel, t: torch.Tensor, stream) -> None:
+        if not t.is_contiguous():
+            raise ValueError("IPC receive buffers must be contiguous")
         nb = t.numel() * t.element_size()
         if nb > ch.slot_bytes:
             raise ValueError(f"IPC {ch.describe()}: message of {nb} B > slot of {ch.slot_bytes} B")
@@ -131,10 +146,9 @@ class IpcTransport(Transport):
         ready_ptr = self._flag(ch.own, ch.slot_bytes * ch.slots, s)       # my ready words
         free_ptr = self._flag(ch.peer_flags, 0, s)                         # sender's free words
         with torch.cuda.stream(stream):
-            self._wait(ready_ptr, u + 1, self._code(ch, True), stream)
-            src = ch.own.view(s * ch.slot_bytes, [nb], torch.uint8)
-            t.view(-1).view(torch.uint8).copy_(src, non_blocking=True)
-            self.C.signal(free_ptr, u + 1, stream.cuda_stream)
+            self._wait(ready_ptr, u + 1, self._code(ch, True), stream, self._prog(ch, 2))
+            self.C.dev_copy(t.data_ptr(), ch.own.ptr + s * ch.slot_bytes, nb, stream.cuda_stream)
+            self.C.signal(free_ptr, u + 1, stream.cuda_stream, self._prog(ch, 3))
 
     # ------------------------------------------------------------------ Transport API
     def send(self, t: torch.Tensor, peer: int) -> None:
@@ -183,8 +197,18 @@ class IpcTransport(Transport):
                                f"on {what} waited > {self.timeout_s} s for its peer")
 
     def counters(self) -> dict:
-        """Messages issued per channel on this end (host side; the watchdog's record)."""
-        return {c.describe(): c.n for c in self._ch.values()}
+        """Per channel: messages issued on this end (host) and the device's progress words -
+        sender: last credit round seen / last ready value released; receiver: last ready value
+        seen / last credit released (message n of slot s: ready = n // slots + 1)."""
+        out = {}
+        for c in self._ch.values():
+            b = 2 + 4 * c.cid
+            if self.rank == c.src:
+                dev = {"credit_seen": self.status.get(b), "ready_released": self.status.get(b + 1)}
+            else:
+                dev = {"ready_seen": self.status.get(b + 2), "credit_released": self.status.get(b + 3)}
+            out[c.describe()] = {"issued": c.n, **dev}
+        return out
 
     def describe(self) -> dict:
         return {"transport": "IpcTransport",
@@ -205,6 +229,9 @@ class IpcTransport(Transport):
         self._ch.clear()
 
     def abort(self) -> None:
-        """Leaving after a failure: no device synchronisation (a wait kernel may still be
-        spinning towards its deadline); the process exit releases the mappings."""
+        """Leaving after a failure: raise the abort word (every pending device wait of this rank
+        exits at its next poll), no device synchronisation; the process exit releases the
+        mappings."""
+        self.status.set(1, 1)
+        time.sleep(0.05)
         self._ch.clear()

@@ -120,13 +120,19 @@ def rank_streams(device: torch.device) -> RankStreams:
 # ------------------------------------------------------------------------------ isolation probe
 def isolation_matrix(streams: Dict[str, torch.cuda.Stream], waiters, device: torch.device,
                      barrier_streams=(), graph=None, graph_role: str = "compute",
-                     window_s: float = 1.5, spin_timeout_s: float = 20.0) -> Dict[str, Dict[str, bool]]:
+                     window_s: float = 1.5, spin_timeout_s: float = 20.0,
+                     host_copies: bool = False) -> Dict[str, Dict[str, bool]]:
     """For each role in ``waiters``: spin a kernel on it (waiting on a host flag, as a receive
     waits for its peer), queue RCCL-style barrier packets behind it on ``barrier_streams`` (RCCL
     makes an internal stream wait on every send / receive it launches), then queue work on every
     other stream - ``graph`` replayed on ``graph_role``, a small kernel + copy elsewhere - and
     record whether each completed within ``window_s`` while the spinner still spins.  Returns
-    ``{waiter: {other: progressed}}``.  The spinner always exits (host release or its deadline)."""
+    ``{waiter: {other: progressed}}``.  The spinner always exits (host release or its deadline).
+
+    ``host_copies``: the waiting stream also queues a host -> device copy behind its spinner (as
+    the head stream's staging uploads sit behind its receive), and every other stream's work is
+    a host -> device copy too: copies a runtime hands to a copy engine queue shared by the
+    process's streams would then wait behind the spinner's copy."""
     import time
     C = _native()
     dev = torch.device(device)
@@ -136,6 +142,7 @@ def isolation_matrix(streams: Dict[str, torch.cuda.Stream], waiters, device: tor
     out = torch.zeros(len(names), dtype=torch.int32, device=dev)
     src = torch.ones(1 << 16, dtype=torch.float32, device=dev)
     dsts = {n: torch.empty_like(src) for n in names}
+    hsrc = torch.ones(1 << 16, dtype=torch.float32).pin_memory() if host_copies else None
     torch.cuda.synchronize(dev)
     res: Dict[str, Dict[str, bool]] = {}
     for w in waiters:
@@ -143,6 +150,9 @@ def isolation_matrix(streams: Dict[str, torch.cuda.Stream], waiters, device: tor
         flags.set(1, 0)
         C.wait_geq(flags.dev_ptr(0), 1, spin_timeout_s, flags.dev_ptr(1), 1,
                    streams[w].cuda_stream, idx)
+        if host_copies:
+            with torch.cuda.stream(streams[w]):
+                dsts[w].copy_(hsrc, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(streams[w])
         for b in barrier_streams:
@@ -157,7 +167,7 @@ def isolation_matrix(streams: Dict[str, torch.cuda.Stream], waiters, device: tor
                     graph.replay()
                 else:
                     C.touch(out[i:i + 1], s.cuda_stream)
-                    dsts[n].copy_(src, non_blocking=True)
+                    dsts[n].copy_(hsrc if host_copies else src, non_blocking=True)
             e = torch.cuda.Event()
             e.record(s)
             evs[n] = e

@@ -26,6 +26,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="gpurun_out/queue_probe.json")
     ap.add_argument("--log-only", action="store_true")
+    ap.add_argument("--copies-only", action="store_true",
+                    help="only the host->device copy coupling check (run with and without "
+                         "HSA_ENABLE_SDMA=0)")
     a = ap.parse_args()
     import torch
     from distributed_llm_inference import ops
@@ -44,6 +47,18 @@ def main():
         rs.close()
         return
 
+    if a.copies_only:
+        rs = RankStreams(dev, "dedicated")
+        m = isolation_matrix(rs.streams, ("send", "recv", "head"), dev, host_copies=True)
+        ok = all(v for row in m.values() for v in row.values())
+        res = {"HSA_ENABLE_SDMA": os.environ.get("HSA_ENABLE_SDMA", "<unset: SDMA on>"),
+               "isolated": ok, "matrix": m}
+        print(json.dumps(res), flush=True)
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+        rs.close()
+        return
     x = torch.randn(2048, 2048, device=dev, dtype=torch.bfloat16)
     w = torch.randn(2048, 2048, device=dev, dtype=torch.bfloat16)
     out = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES", "<unset: HIP default 4>"),
