@@ -16,6 +16,7 @@
 // test.  Every wait has a deadline: a peer that never arrives turns into a status word the host
 // reads (and a Python error), never a wave that spins forever.
 #include <torch/extension.h>
+#include <pybind11/stl.h>
 #include <ATen/hip/HIPContext.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
@@ -24,6 +25,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace {
@@ -114,16 +116,49 @@ __global__ void __launch_bounds__(64) signal_kernel(uint32_t* flag, uint32_t val
   }
 }
 
-// Stream-ordered device copy as a KERNEL on the caller's stream.  hipMemcpyAsync between two
-// device pointers may be carried out by an SDMA engine queue that the process's streams share:
-// a copy that must wait for a spinning credit wait on one stream then blocks, in that shared
-// in-order queue, the copy another stream needs to release its peer - a cross-process deadlock
-// the IPC rehearsal hit.  A copy kernel stays on its own stream's hardware queue.
+// Stream-ordered device copy as a KERNEL on the caller's stream.  hipMemcpyAsync may be carried
+// out on a copy queue that the process's streams share (see copy_segments below): a copy that
+// must wait for a spinning credit wait on one stream would then block, in that shared in-order
+// queue, the copy another stream needs to release its peer.  A copy kernel stays on its own
+// stream's hardware queue.
 __global__ void __launch_bounds__(256) dev_copy_kernel(uint4* __restrict__ dst,
                                                        const uint4* __restrict__ src, size_t n16) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16;
        i += (size_t)gridDim.x * blockDim.x)
     dst[i] = src[i];
+}
+
+// Up to kMaxSegs (offset, bytes) segments copied src_base + off -> dst_base + off in ONE launch on
+// the caller's stream: the per-step host -> device metadata uploads (the source is coherent,
+// device-mapped host memory, read directly by the kernel) and the device -> host token returns.
+// Measured on MI355X (scripts/queue_probe.py --copies-only, profiles/streams/): a host <-> device
+// hipMemcpyAsync is carried out on a copy queue shared by the process's streams - with SDMA (the
+// default) by an engine queue, with HSA_ENABLE_SDMA=0 by a blit queue - so a copy that a stream
+// orders behind a spinning receive (the rotating head's staging uploads) holds up every other
+// stream's copies, the compute stream's step uploads included.  Kernels run on their own stream.
+constexpr int kMaxSegs = 24;
+struct Segs {
+  long long off[kMaxSegs];
+  long long n[kMaxSegs];
+  int count;
+};
+
+__global__ void __launch_bounds__(256) copy_segments_kernel(char* dst, const char* src, Segs segs) {
+  const int sg = blockIdx.y;
+  if (sg >= segs.count) return;
+  const long long off = segs.off[sg], n = segs.n[sg];
+  char* d = dst + off;
+  const char* s = src + off;
+  const long long tid = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  const long long nth = (long long)gridDim.x * blockDim.x;
+  if ((((unsigned long long)d | (unsigned long long)s) & 15ull) == 0) {
+    const long long n16 = n >> 4;
+    for (long long i = tid; i < n16; i += nth)
+      reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
+    for (long long i = (n16 << 4) + tid; i < n; i += nth) d[i] = s[i];
+  } else {
+    for (long long i = tid; i < n; i += nth) d[i] = s[i];
+  }
 }
 
 // A trivial kernel for progress probes: out[0] += 1.
@@ -164,6 +199,28 @@ void dev_copy(int64_t dst, int64_t src, int64_t nbytes, int64_t stream) {
   HIP_OK(hipGetLastError());
 }
 
+void copy_segments(int64_t dst_base, int64_t src_base, std::vector<std::pair<int64_t, int64_t>> segs,
+                   int64_t stream) {
+  TORCH_CHECK(dst_base && src_base, "copy_segments: null base");
+  TORCH_CHECK((int)segs.size() <= kMaxSegs, "copy_segments: at most ", kMaxSegs, " segments");
+  Segs a{};
+  long long most = 0;
+  for (const auto& sg : segs) {
+    TORCH_CHECK(sg.first >= 0 && sg.second >= 0, "copy_segments: bad segment");
+    if (sg.second == 0) continue;
+    a.off[a.count] = sg.first;
+    a.n[a.count] = sg.second;
+    ++a.count;
+    most = std::max(most, (long long)sg.second);
+  }
+  if (a.count == 0) return;
+  const long long blocks = std::min<long long>((most / 16 + 255) / 256 + 1, 64);
+  hipLaunchKernelGGL(copy_segments_kernel, dim3((unsigned)blocks, (unsigned)a.count), dim3(256), 0,
+                     as_stream(stream), reinterpret_cast<char*>(dst_base),
+                     reinterpret_cast<const char*>(src_base), a);
+  HIP_OK(hipGetLastError());
+}
+
 void touch(at::Tensor out, int64_t stream) {
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kInt && out.numel() >= 1, "touch: int32 GPU tensor");
   hipLaunchKernelGGL(touch_kernel, dim3(1), dim3(64), 0, as_stream(stream),
@@ -174,6 +231,32 @@ void touch(at::Tensor out, int64_t stream) {
 // ----------------------------------------------------------------------- host-mapped flag words
 // Coherent pinned host memory the GPU reads / writes directly: the host sets a flag the GPU
 // waits on (isolation test) and reads the status words wait kernels leave on a timeout.
+// Coherent, device-mapped pinned host buffer: the host fills it through a CPU tensor view, kernels
+// read (or write) it through the device pointer - no copy engine in between.
+class HostBuffer {
+ public:
+  explicit HostBuffer(int64_t nbytes) : n_(nbytes) {
+    TORCH_CHECK(nbytes > 0, "HostBuffer: size");
+    HIP_OK(hipHostMalloc(&h_, nbytes, hipHostMallocMapped | hipHostMallocCoherent |
+                                          hipHostMallocPortable));
+    std::memset(h_, 0, nbytes);
+    HIP_OK(hipHostGetDevicePointer(&d_, h_, 0));
+  }
+  ~HostBuffer() {
+    if (h_) (void)hipHostFree(h_);
+  }
+  at::Tensor tensor() const {   // CPU uint8 view (the buffer must outlive it)
+    return torch::from_blob(h_, {n_}, at::TensorOptions().dtype(at::kByte));
+  }
+  int64_t dev_ptr() const { return reinterpret_cast<int64_t>(d_); }
+  int64_t nbytes() const { return n_; }
+
+ private:
+  int64_t n_;
+  void* h_ = nullptr;
+  void* d_ = nullptr;
+};
+
 class HostWords {
  public:
   explicit HostWords(int64_t n) : n_(n) {
@@ -276,6 +359,13 @@ void register_streams(pybind11::module_& m) {
   m.def("touch", &touch, pybind11::arg("out"), pybind11::arg("stream") = 0);
   m.def("dev_copy", &dev_copy, pybind11::arg("dst"), pybind11::arg("src"), pybind11::arg("nbytes"),
         pybind11::arg("stream"));
+  m.def("copy_segments", &copy_segments, pybind11::arg("dst_base"), pybind11::arg("src_base"),
+        pybind11::arg("segments"), pybind11::arg("stream"));
+  pybind11::class_<HostBuffer>(m, "HostBuffer")
+      .def(pybind11::init<int64_t>())
+      .def("tensor", &HostBuffer::tensor)
+      .def_property_readonly("dev_ptr", &HostBuffer::dev_ptr)
+      .def_property_readonly("nbytes", &HostBuffer::nbytes);
   pybind11::class_<HostWords>(m, "HostWords")
       .def(pybind11::init<int64_t>())
       .def("set", &HostWords::set)

@@ -14,9 +14,11 @@ its own stream.  This transport reproduces that structure exactly, on one GPU or
   compute that produced the data): wait ``free[s] >= u`` -> copy into the peer's slot -> release
   ``ready[s] = u + 1``.  Receiver, on its receive (or head) stream: wait ``ready[s] >= u + 1`` ->
   copy out -> release ``free[s] = u + 1`` in the sender's memory.  The copies are kernels on the
-  same stream, never hipMemcpyAsync: a memcpy may run on an SDMA queue the process's streams
-  share, and one copy held there behind a spinning wait blocks the copy that would release it
-  (measured: the 8-rank rehearsal deadlocked in its third decode round with torch copies);
+  same stream, never hipMemcpyAsync: a memcpy runs on a copy queue the process's streams share
+  (measured, profiles/streams/copies_*.json), where one copy held behind a spinning wait blocks
+  every other stream's copies.  (The 8-rank rehearsal's stall in its third decode round came
+  from exactly that coupling - the executor's host -> device step uploads stuck behind the head
+  stream's; those are copy kernels now as well, runtime/executor.py _Staging);
 * the waits are spinning kernels (csrc/comm/streams.hip), like RCCL's: they hold their stream -
   and, if it were shared, that stream's hardware queue - until the peer arrives.  That is the
   point: the GPU tests run the real HeadJobs / executor stream schedule against them.  Each wait

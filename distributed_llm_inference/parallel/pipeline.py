@@ -144,13 +144,12 @@ class DriverBase:
 
 
 def _sample_tokens_to_host(out: torch.Tensor):
-    """Async D2H of sampled tokens; returns (pinned tensor, event)."""
+    """Async D2H of sampled tokens; returns (host tensor, event).  On the GPU a copy kernel on
+    the current stream writes a device-mapped host ring slot (runtime/streams.py
+    HostTokenRing): no copy engine shared with the other streams."""
     if out.is_cuda:
-        pinned = torch.empty(out.shape, dtype=out.dtype, pin_memory=True)
-        pinned.copy_(out, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        return pinned, ev
+        from ..runtime.streams import token_ring
+        return token_ring(out.device).take(out)
     return out.clone(), None
 
 

@@ -121,14 +121,26 @@ class _Staging:
             nbytes = n * torch.empty((), dtype=dt).element_size()
             self.offsets[name] = (off, dt, shape)
             off += (nbytes + 255) // 256 * 256
-        pin = device.type == "cuda"
-        # a RING of pinned host slots: async H2D copies of step k may still be pending on the
-        # stream when the host already stages step k+1 (the host runs ahead of the GPU), so a
-        # slot is reused only after the event recorded behind its uploads has completed
-        self.nslots = 4 if pin else 1
-        self.hosts = [torch.zeros(off, dtype=torch.uint8, pin_memory=pin) for _ in range(self.nslots)]
+        gpu = device.type == "cuda"
+        # a RING of host slots: the uploads of step k may still be pending on the stream when the
+        # host already stages step k+1 (the host runs ahead of the GPU), so a slot is reused only
+        # after the event recorded behind its uploads has completed.  On the GPU the slots are
+        # coherent, device-mapped host memory and ONE copy kernel per step moves the written
+        # sections on the caller's stream (csrc/comm/streams.hip copy_segments): a host -> device
+        # memcpy would go through a copy queue shared by every stream of the process, where the
+        # rotating head's uploads (ordered behind a spinning receive) hold up the step's uploads
+        self.nslots = 4 if gpu else 1
+        self._hbufs = []
+        if gpu:
+            from .. import ops
+            self._C = ops.native()
+            self._hbufs = [self._C.HostBuffer(off) for _ in range(self.nslots)]
+            self.hosts = [b.tensor() for b in self._hbufs]
+        else:
+            self.hosts = [torch.zeros(off, dtype=torch.uint8) for _ in range(self.nslots)]
         self.hviews = [{k: self._view(h, k) for k in self.offsets} for h in self.hosts]
         self.events: List[Optional[torch.cuda.Event]] = [None] * self.nslots
+        self._pending: List[Tuple[int, int]] = []
         self.slot = 0
         self.host = self.hosts[0]
         self.h = self.hviews[0]
@@ -146,8 +158,14 @@ class _Staging:
         self.h = self.hviews[self.slot]
 
     def release(self) -> None:
-        """Mark the current slot's uploads as enqueued (reusable once this event completes)."""
+        """Enqueue the current slot's uploads (one copy kernel on the current stream) and mark
+        the slot reusable once the event behind them completes."""
         if self.device.type == "cuda":
+            s = torch.cuda.current_stream().cuda_stream
+            for i in range(0, len(self._pending), 24):   # the kernel takes <= 24 segments
+                self._C.copy_segments(self.dev.data_ptr(), self._hbufs[self.slot].dev_ptr,
+                                      self._pending[i:i + 24], s)
+            self._pending = []
             ev = self.events[self.slot] or torch.cuda.Event()
             ev.record()
             self.events[self.slot] = ev
@@ -161,7 +179,8 @@ class _Staging:
         return buf[off: off + n * es].view(dt).view(shape)
 
     def upload(self, name: str, count: int) -> None:
-        """Copy the first ``count`` elements (rows for 2-D) of section ``name`` to the device."""
+        """Copy the first ``count`` elements (rows for 2-D) of section ``name`` to the device
+        (GPU: at :meth:`release`, in one kernel with the slot's other sections)."""
         if count <= 0:
             return
         off, dt, shape = self.offsets[name]
@@ -171,7 +190,7 @@ class _Staging:
         es = torch.empty((), dtype=dt).element_size()
         nb = count * row * es
         if self.device.type == "cuda":
-            self.dev[off: off + nb].copy_(self.host[off: off + nb], non_blocking=True)
+            self._pending.append((off, nb))   # moved by release()'s copy kernel
         else:
             self.dev[off: off + nb].copy_(self.host[off: off + nb])
 

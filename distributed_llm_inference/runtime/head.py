@@ -31,6 +31,7 @@ from .. import ops
 from ..models.embed_head import LMHead
 from ..utils.cuda import capture_guard, prime_graph_rng
 from .executor import StepPlan, _Staging, _fill_pos
+from .streams import token_ring
 from .watchdog import TRACKER
 
 log = logging.getLogger(__name__)
@@ -244,10 +245,8 @@ class HeadJobs:
             x = self.runner.x[:B]
             self.tr.recv_head(x, self.last, self.stream)
             tok = self.runner.run(plan, None)
-            pinned = torch.empty(B, dtype=torch.int32, pin_memory=True)
-            pinned.copy_(tok, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(self.stream)
+            # device -> host by a copy kernel on the head stream (no shared copy engine)
+            pinned, ev = token_ring(self.runner.device).take(tok, self.stream)
         self.publish(plan, pinned, ev)
 
     @property

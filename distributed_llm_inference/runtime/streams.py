@@ -102,6 +102,55 @@ class RankStreams:
         self._handles.clear()
 
 
+class HostTokenRing:
+    """Device -> host returns of sampled token ids without a copy engine: a ring of slots in
+    coherent, device-mapped host memory written by a copy kernel on the caller's stream
+    (``copy_segments``), followed by an event.  (A device -> host ``copy_`` goes through a copy
+    queue shared by the process's streams - see csrc/comm/streams.hip - where it can wait behind
+    another stream's copy that is ordered after a spinning receive.)  A slot is reused after
+    ``slots`` further takes; consumers read a slot once its event completed, well before that."""
+
+    def __init__(self, device: torch.device, max_items: int, slots: int = 64):
+        from .. import ops
+        self.C = ops.native()
+        self.device = torch.device(device)
+        self.item_bytes = (int(max_items) * 4 + 255) // 256 * 256
+        self.slots = slots
+        self.buf = self.C.HostBuffer(self.item_bytes * slots)
+        self.view = self.buf.tensor()
+        self.i = 0
+
+    def take(self, tok: torch.Tensor, stream=None):
+        """Copy ``tok`` (int32 [B], device) into the next slot on ``stream`` (default: current);
+        returns (host int32 view [B], event recorded after the copy)."""
+        if tok.dtype != torch.int32 or not tok.is_contiguous():
+            tok = tok.to(torch.int32).contiguous()
+        nb = tok.numel() * 4
+        if nb > self.item_bytes:
+            raise ValueError(f"{tok.numel()} tokens > ring slot of {self.item_bytes // 4}")
+        off = (self.i % self.slots) * self.item_bytes
+        self.i += 1
+        s = stream or torch.cuda.current_stream(self.device)
+        self.C.copy_segments(self.buf.dev_ptr + off, tok.data_ptr(), [(0, nb)], s.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(s)
+        return self.view[off: off + nb].view(torch.int32), ev
+
+
+_TOKEN_RINGS: Dict[int, HostTokenRing] = {}
+
+
+def token_ring(device: torch.device, max_items: int = 4096) -> HostTokenRing:
+    """The process-wide token ring of ``device`` (sized for up to ``max_items`` tokens a take)."""
+    device = torch.device(device)
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    r = _TOKEN_RINGS.get(key)
+    if r is None or r.item_bytes < max_items * 4:
+        r = HostTokenRing(device, max_items)
+        _TOKEN_RINGS[key] = r
+    return r
+
+
 _RANK_STREAMS: Dict[int, RankStreams] = {}
 
 
@@ -121,7 +170,8 @@ def rank_streams(device: torch.device) -> RankStreams:
 def isolation_matrix(streams: Dict[str, torch.cuda.Stream], waiters, device: torch.device,
                      barrier_streams=(), graph=None, graph_role: str = "compute",
                      window_s: float = 1.5, spin_timeout_s: float = 20.0,
-                     host_copies: bool = False) -> Dict[str, Dict[str, bool]]:
+                     host_copies: bool = False, copy_kernels: bool = False
+                     ) -> Dict[str, Dict[str, bool]]:
     """For each role in ``waiters``: spin a kernel on it (waiting on a host flag, as a receive
     waits for its peer), queue RCCL-style barrier packets behind it on ``barrier_streams`` (RCCL
     makes an internal stream wait on every send / receive it launches), then queue work on every
@@ -132,7 +182,9 @@ def isolation_matrix(streams: Dict[str, torch.cuda.Stream], waiters, device: tor
     ``host_copies``: the waiting stream also queues a host -> device copy behind its spinner (as
     the head stream's staging uploads sit behind its receive), and every other stream's work is
     a host -> device copy too: copies a runtime hands to a copy engine queue shared by the
-    process's streams would then wait behind the spinner's copy."""
+    process's streams would then wait behind the spinner's copy.  ``copy_kernels``: those copies
+    are made the runtime's way instead - a ``copy_segments`` kernel reading device-mapped host
+    memory on the stream itself (executor staging, HostTokenRing)."""
     import time
     C = _native()
     dev = torch.device(device)
@@ -143,6 +195,14 @@ def isolation_matrix(streams: Dict[str, torch.cuda.Stream], waiters, device: tor
     src = torch.ones(1 << 16, dtype=torch.float32, device=dev)
     dsts = {n: torch.empty_like(src) for n in names}
     hsrc = torch.ones(1 << 16, dtype=torch.float32).pin_memory() if host_copies else None
+    hbuf = C.HostBuffer(1 << 18) if copy_kernels else None
+
+    def host_copy(dst: torch.Tensor, s) -> None:
+        if copy_kernels:
+            C.copy_segments(dst.data_ptr(), hbuf.dev_ptr, [(0, dst.numel() * 4)], s.cuda_stream)
+        else:
+            with torch.cuda.stream(s):
+                dst.copy_(hsrc, non_blocking=True)
     torch.cuda.synchronize(dev)
     res: Dict[str, Dict[str, bool]] = {}
     for w in waiters:
@@ -151,8 +211,7 @@ def isolation_matrix(streams: Dict[str, torch.cuda.Stream], waiters, device: tor
         C.wait_geq(flags.dev_ptr(0), 1, spin_timeout_s, flags.dev_ptr(1), 1,
                    streams[w].cuda_stream, idx)
         if host_copies:
-            with torch.cuda.stream(streams[w]):
-                dsts[w].copy_(hsrc, non_blocking=True)
+            host_copy(dsts[w], streams[w])
         ev = torch.cuda.Event()
         ev.record(streams[w])
         for b in barrier_streams:
@@ -167,7 +226,10 @@ def isolation_matrix(streams: Dict[str, torch.cuda.Stream], waiters, device: tor
                     graph.replay()
                 else:
                     C.touch(out[i:i + 1], s.cuda_stream)
-                    dsts[n].copy_(hsrc if host_copies else src, non_blocking=True)
+                    if host_copies:
+                        host_copy(dsts[n], s)
+                    else:
+                        dsts[n].copy_(src, non_blocking=True)
             e = torch.cuda.Event()
             e.record(s)
             evs[n] = e

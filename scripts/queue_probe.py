@@ -49,10 +49,12 @@ def main():
 
     if a.copies_only:
         rs = RankStreams(dev, "dedicated")
-        m = isolation_matrix(rs.streams, ("send", "recv", "head"), dev, host_copies=True)
-        ok = all(v for row in m.values() for v in row.values())
-        res = {"HSA_ENABLE_SDMA": os.environ.get("HSA_ENABLE_SDMA", "<unset: SDMA on>"),
-               "isolated": ok, "matrix": m}
+        res = {"HSA_ENABLE_SDMA": os.environ.get("HSA_ENABLE_SDMA", "<unset: SDMA on>")}
+        for kind, ck in (("memcpy", False), ("copy_kernel", True)):
+            m = isolation_matrix(rs.streams, ("send", "recv", "head"), dev, host_copies=True,
+                                 copy_kernels=ck)
+            res[kind] = {"isolated": all(v for row in m.values() for v in row.values()),
+                         "matrix": m}
         print(json.dumps(res), flush=True)
         os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
         with open(a.out, "w") as f:

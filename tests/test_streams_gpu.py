@@ -59,6 +59,55 @@ def test_dedicated_streams_have_their_own_hardware_queues(gpu):
         rs.close()
 
 
+def test_runtime_host_copies_are_not_coupled_across_streams(gpu):
+    """Host <-> device copies the runtime makes per step (staging uploads, token returns) are
+    copy KERNELS on the issuing stream reading / writing device-mapped host memory: one queued on
+    a stream behind a spinning receive (the rotating head's uploads) must not hold up another
+    stream's copies (a hipMemcpyAsync goes through a copy queue the process's streams share:
+    scripts/queue_probe.py --copies-only, profiles/streams/copies_*.json)."""
+    from distributed_llm_inference.runtime.streams import (WAITING_ROLES, RankStreams,
+                                                           isolation_matrix)
+    dev = torch.device("cuda", 0)
+    rs = RankStreams(dev, "dedicated")
+    try:
+        m = isolation_matrix(rs.streams, WAITING_ROLES, dev, host_copies=True, copy_kernels=True)
+        stuck = {w: [o for o, ok in row.items() if not ok] for w, row in m.items()}
+        assert not any(stuck.values()), f"copies stalled behind a waiting stream's copy: {stuck}"
+    finally:
+        rs.close()
+
+
+def test_staging_and_token_ring_roundtrip(gpu):
+    """The executor's host-mapped staging (one copy kernel per step) and the token ring deliver
+    exactly the bytes written, slot after slot."""
+    from distributed_llm_inference.runtime.executor import _Staging
+    from distributed_llm_inference.runtime.streams import HostTokenRing
+    dev = torch.device("cuda", 0)
+    st = _Staging(64, 16, 4, dev)
+    for it in range(9):
+        st.acquire()
+        st.h["positions"][:7] = torch.arange(7, dtype=torch.int32) + it
+        st.h["seq_lens"][:3] = torch.tensor([it, 2 * it, 3], dtype=torch.int32)
+        st.h["block_tables"][:2] = it
+        st.upload("positions", 7)
+        st.upload("seq_lens", 3)
+        st.upload("block_tables", 2)
+        st.release()
+        torch.cuda.synchronize()
+        assert torch.equal(st.d["positions"][:7].cpu(), torch.arange(7, dtype=torch.int32) + it)
+        assert st.d["seq_lens"][:3].tolist() == [it, 2 * it, 3]
+        assert (st.d["block_tables"][:2] == it).all()
+    ring = HostTokenRing(dev, 512, slots=4)
+    outs = []
+    for it in range(10):
+        tok = torch.arange(300, device=dev, dtype=torch.int32) * (it + 1)
+        outs.append((it, *ring.take(tok)))
+        if len(outs) > 2:   # consume two behind, as the pipeline does
+            j, host, ev = outs.pop(0)
+            ev.synchronize()
+            assert torch.equal(host, torch.arange(300, dtype=torch.int32) * (j + 1))
+
+
 def test_wait_kernel_deadline_reports_instead_of_hanging(gpu):
     """A device wait whose peer never arrives exits at its deadline and leaves its code."""
     from distributed_llm_inference import ops
