@@ -85,13 +85,15 @@ double wall_clock_hz(int device) {
 // One lane polls; the other lanes of the (single, 64-wide) wave only keep the launch shape legal.
 // ``status`` (host-mapped) receives ``code`` if the deadline passes; the wave always exits.
 // ``abort`` (host-mapped, optional): a nonzero word ends the wait at once (the job is leaving);
-// ``progress`` (host-mapped, optional): receives ``target`` once the wait is satisfied, so the
-// host can tell which wait of a stuck pipeline never completed without touching the GPU.
+// ``progress`` (host-mapped, optional, 2 words): [0] receives ``target`` when the wave starts
+// waiting, [1] once the wait is satisfied - the host tells which wait of a stuck pipeline its
+// stream reached and never passed (or never reached) without touching the GPU.
 __global__ void __launch_bounds__(64) wait_geq_kernel(const uint32_t* flag, uint32_t target,
                                                       uint64_t max_ticks, uint32_t* status,
                                                       uint32_t code, const uint32_t* abort,
                                                       uint32_t* progress) {
   if (threadIdx.x != 0) return;
+  if (progress) __hip_atomic_store(progress, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint64_t t0 = wall_clock64();
   while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < target) {
     const bool aborted =
@@ -102,15 +104,21 @@ __global__ void __launch_bounds__(64) wait_geq_kernel(const uint32_t* flag, uint
     }
     __builtin_amdgcn_s_sleep(8);
   }
-  if (progress) __hip_atomic_store(progress, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (progress) __hip_atomic_store(progress + 1, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Release-store ``value`` (every write queued before this kernel on its stream has completed:
 // stream order + the system-scope release make the data visible before the flag); ``progress``
-// (host-mapped, optional) records the value for the host.
+// (host-mapped, optional) records the value for the host.  ``status`` / ``abort`` (host-mapped,
+// optional): when either is nonzero - a wait of this process expired, or the job is leaving -
+// nothing is released, so a failed wait never lets garbage flow on to the peer and every
+// progress word stays where the failure froze it.
 __global__ void __launch_bounds__(64) signal_kernel(uint32_t* flag, uint32_t value,
-                                                    uint32_t* progress) {
+                                                    uint32_t* progress, const uint32_t* status,
+                                                    const uint32_t* abort) {
   if (threadIdx.x == 0) {
+    if (status && __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
+    if (abort && __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) return;
     __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     if (progress) __hip_atomic_store(progress, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -179,11 +187,14 @@ void wait_geq(int64_t flag_ptr, int64_t target, double timeout_s, int64_t status
   HIP_OK(hipGetLastError());
 }
 
-void signal(int64_t flag_ptr, int64_t value, int64_t stream, int64_t progress_ptr) {
+void signal(int64_t flag_ptr, int64_t value, int64_t stream, int64_t progress_ptr,
+            int64_t status_ptr, int64_t abort_ptr) {
   TORCH_CHECK(flag_ptr != 0, "signal: null flag");
   hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, as_stream(stream),
                      reinterpret_cast<uint32_t*>(flag_ptr), (uint32_t)value,
-                     reinterpret_cast<uint32_t*>(progress_ptr));
+                     reinterpret_cast<uint32_t*>(progress_ptr),
+                     reinterpret_cast<const uint32_t*>(status_ptr),
+                     reinterpret_cast<const uint32_t*>(abort_ptr));
   HIP_OK(hipGetLastError());
 }
 
@@ -355,7 +366,8 @@ void register_streams(pybind11::module_& m) {
         pybind11::arg("stream"), pybind11::arg("device"), pybind11::arg("abort_ptr") = 0,
         pybind11::arg("progress_ptr") = 0);
   m.def("signal", &signal, pybind11::arg("flag_ptr"), pybind11::arg("value"),
-        pybind11::arg("stream"), pybind11::arg("progress_ptr") = 0);
+        pybind11::arg("stream"), pybind11::arg("progress_ptr") = 0,
+        pybind11::arg("status_ptr") = 0, pybind11::arg("abort_ptr") = 0);
   m.def("touch", &touch, pybind11::arg("out"), pybind11::arg("stream") = 0);
   m.def("dev_copy", &dev_copy, pybind11::arg("dst"), pybind11::arg("src"), pybind11::arg("nbytes"),
         pybind11::arg("stream"));

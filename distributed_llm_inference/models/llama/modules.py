@@ -187,7 +187,7 @@ class LlamaMLP(nn.Module):
                 h = ops.swiglu_interleaved(gp(None, (xq, xs)))
             return self.down_proj(h, defer_reduce=defer_reduce)
         if self.fused_swiglu:
-            if gp.tile_splits(normed):
+            if gp.tile_splits(normed) and ops.gate_up_on_tile():
                 h = ops.gemm_tile(normed, gp.weight, swiglu=True)
             else:
                 h = ops.swiglu_interleaved(gp(normed))

@@ -97,6 +97,13 @@ def bf16_bf16_partials() -> bool:
     return os.environ.get("DLI_BF16_PARTS", "1") == "1"
 
 
+def gate_up_on_tile() -> bool:
+    """bf16 gate|up with SwiGLU in the tile GEMM's epilogue (default); ``DLI_GATEUP_TILE=0``
+    runs it on hipBLASLt (interleaved weight as-is) followed by ``swiglu_interleaved`` - the A/B
+    for the step's largest GEMM."""
+    return os.environ.get("DLI_GATEUP_TILE", "1") == "1"
+
+
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
              out: Optional[torch.Tensor] = None, residual_out: Optional[torch.Tensor] = None
              ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:

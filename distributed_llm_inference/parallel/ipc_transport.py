@@ -54,6 +54,9 @@ class _Channel:
         return f"{self.kind} {self.src}->{self.dst}"
 
 
+_PROG = 6   # progress words per channel (see IpcTransport.__init__)
+
+
 class IpcTransport(Transport):
     """See module docstring.  ``max_bytes``: largest stage message (max tokens x hidden x 2)."""
 
@@ -72,11 +75,12 @@ class IpcTransport(Transport):
         self.recv_stream = streams.recv
         self.timeout_s = float(os.environ.get("DLI_P2P_TIMEOUT_S", timeout_s))
         # host-mapped words: [0] code of the first expired wait (0 = none), [1] abort (nonzero
-        # ends every pending device wait), then 4 progress words per channel, written by the
-        # device as each wait / release completes: sender (credit seen, ready released),
-        # receiver (ready seen, credit released) - a stuck pipeline's record names the one
-        # wait that never completed, read without any GPU operation
-        self.status = C.HostWords(2 + 4 * 64)
+        # ends every pending device wait and stops every release), then 6 progress words per
+        # channel, written by the device: sender (credit wait entered, credit seen, ready
+        # released), receiver (ready wait entered, ready seen, credit released) - a stuck
+        # pipeline's record names the wait each stream reached and never passed, read without
+        # any GPU operation (releases stop after a failure, so the words stay frozen there)
+        self.status = C.HostWords(2 + _PROG * 64)
         self.prefix = prefix
         self._ch: Dict[Tuple[str, int, int], _Channel] = {}
         edges: List[Tuple[str, int, int, int]] = [("stage", r, r + 1, max_bytes)
@@ -112,7 +116,11 @@ class IpcTransport(Transport):
         return buf.ptr + offset_bytes + 4 * s
 
     def _prog(self, ch: _Channel, k: int) -> int:
-        return self.status.dev_ptr(2 + 4 * ch.cid + k)
+        return self.status.dev_ptr(2 + _PROG * ch.cid + k)
+
+    def _signal(self, ptr: int, value: int, stream, progress: int) -> None:
+        self.C.signal(ptr, value, stream.cuda_stream, progress, self.status.dev_ptr(0),
+                      self.status.dev_ptr(1))
 
     def _wait(self, ptr: int, target: int, code: int, stream, progress: int = 0) -> None:
         self.C.wait_geq(ptr, target, self.timeout_s, self.status.dev_ptr(0), code,
@@ -135,7 +143,7 @@ class IpcTransport(Transport):
             self._wait(free_ptr, u, self._code(ch, False), stream, self._prog(ch, 0))
             # copy KERNEL on this stream (not hipMemcpyAsync: see csrc/comm/streams.hip dev_copy)
             self.C.dev_copy(ch.data.ptr + s * ch.slot_bytes, t.data_ptr(), nb, stream.cuda_stream)
-            self.C.signal(ready_ptr, u + 1, stream.cuda_stream, self._prog(ch, 1))
+            self._signal(ready_ptr, u + 1, stream, self._prog(ch, 2))
 
     def _recv_on(self, ch: _Channel, t: torch.Tensor, stream) -> None:
         if not t.is_contiguous():
@@ -148,9 +156,9 @@ class IpcTransport(Transport):
         ready_ptr = self._flag(ch.own, ch.slot_bytes * ch.slots, s)       # my ready words
         free_ptr = self._flag(ch.peer_flags, 0, s)                         # sender's free words
         with torch.cuda.stream(stream):
-            self._wait(ready_ptr, u + 1, self._code(ch, True), stream, self._prog(ch, 2))
+            self._wait(ready_ptr, u + 1, self._code(ch, True), stream, self._prog(ch, 3))
             self.C.dev_copy(t.data_ptr(), ch.own.ptr + s * ch.slot_bytes, nb, stream.cuda_stream)
-            self.C.signal(free_ptr, u + 1, stream.cuda_stream, self._prog(ch, 3))
+            self._signal(free_ptr, u + 1, stream, self._prog(ch, 5))
 
     # ------------------------------------------------------------------ Transport API
     def send(self, t: torch.Tensor, peer: int) -> None:
@@ -199,16 +207,20 @@ class IpcTransport(Transport):
                                f"on {what} waited > {self.timeout_s} s for its peer")
 
     def counters(self) -> dict:
-        """Per channel: messages issued on this end (host) and the device's progress words -
-        sender: last credit round seen / last ready value released; receiver: last ready value
-        seen / last credit released (message n of slot s: ready = n // slots + 1)."""
+        """Per channel: messages issued on this end (host) and the device's progress words
+        (message n uses slot n % slots, round u = n // slots): sender - credit wait entered /
+        passed (target u), ready released (u + 1); receiver - ready wait entered / passed
+        (target u + 1), credit released (u + 1).  "entered" > "seen" = the stream sits in that
+        wait; "entered" == "seen" with fewer issued = the stream is held up before it."""
         out = {}
         for c in self._ch.values():
-            b = 2 + 4 * c.cid
+            b = 2 + _PROG * c.cid
+            g = self.status.get
             if self.rank == c.src:
-                dev = {"credit_seen": self.status.get(b), "ready_released": self.status.get(b + 1)}
+                dev = {"credit_wait": g(b), "credit_seen": g(b + 1), "ready_released": g(b + 2)}
             else:
-                dev = {"ready_seen": self.status.get(b + 2), "credit_released": self.status.get(b + 3)}
+                dev = {"ready_wait": g(b + 3), "ready_seen": g(b + 4),
+                       "credit_released": g(b + 5)}
             out[c.describe()] = {"issued": c.n, **dev}
         return out
 

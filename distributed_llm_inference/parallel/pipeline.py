@@ -276,8 +276,10 @@ class DistributedDriver(DriverBase):
         out = self.ex.execute(plan, None)
         self.stats.end(tok)
         if plan.seq_ids:
+            _device_mark(self.ex, "compute", plan.step)
             TRACKER.mark("send", plan.step, plan.mb, peer=1, stream="send")
             self.tr.send(out, 1)
+            _device_mark(self.ex, "send", plan.step)
             if self.heads is not None:
                 self.heads.tick()
                 if self._head_rank(plan) == 0:
@@ -443,6 +445,7 @@ class StageFollower:
             buf, free_ev = self._recv_slot(plan.num_tokens)
             TRACKER.mark("recv", plan.step, plan.mb, peer=self.rank - 1, stream="recv")
             x = self.tr.recv(buf, self.rank - 1, free_event=free_ev)
+            _device_mark(self.ex, "recv", plan.step)
             if self.faults.active:
                 self.faults.on_step()
             tok = self.stats.begin(self.faults.delay_ms)
@@ -450,6 +453,7 @@ class StageFollower:
             out = self.ex.execute(plan, x, project=(hr == self.rank))
             self.stats.end(tok)
             self._release_slot()
+            _device_mark(self.ex, "compute", plan.step)
             if self.is_last:
                 if hr == self.rank:
                     pinned, ev = _sample_tokens_to_host(out)
@@ -457,9 +461,11 @@ class StageFollower:
                 else:   # rotating head: normed hidden states to the rank whose turn it is
                     TRACKER.mark("send_head", plan.step, plan.mb, peer=hr, stream="send")
                     self.tr.send_head(out, hr)
+                    _device_mark(self.ex, "send", plan.step)
             else:
                 TRACKER.mark("send", plan.step, plan.mb, peer=self.rank + 1, stream="send")
                 self.tr.send(out, self.rank + 1)
+                _device_mark(self.ex, "send", plan.step)
                 if self.heads is not None:
                     self.heads.tick()
                     if hr == self.rank:
@@ -479,6 +485,16 @@ class StageFollower:
         """Counterpart of :meth:`DistributedDriver.close` (call after :meth:`run` returns)."""
         dist.barrier(group=self.group)
         self.tr.close()
+
+
+def _device_mark(ex, role: str, step: int) -> None:
+    """Device progress mark of ``role``'s stream after this step's work (watchdog record)."""
+    if TRACKER._words is None:
+        return
+    from ..runtime.streams import rank_streams
+    stream = (torch.cuda.current_stream(ex.device) if role == "compute"
+              else rank_streams(ex.device).streams.get(role))
+    TRACKER.device_mark(role, step, stream)
 
 
 def make_transport(rank: int, world: int, device: torch.device, job: str = "0",

@@ -264,9 +264,12 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     if device.type == "cuda":
         # every stream this rank will use, each on a hardware queue of its own, made current
         # before anything is allocated or launched (runtime/streams.py)
-        from .streams import rank_streams
+        from .streams import rank_streams, token_ring
         streams = rank_streams(device)
         streams.activate()
+        # host-mapped allocations now, never in the step loop: allocating pinned / mapped host
+        # memory may synchronise the device, i.e. wait for a stream parked in a peer wait
+        token_ring(device)
     rotate = head_rotation_wanted(cfg, pp, device)
     ranges = plan_stages(spec, pp, head_rotation=rotate)
     if os.environ.get("DLI_STAGE_RANGES"):  # placement chosen by the server (rebalance)
@@ -295,6 +298,8 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     from .watchdog import TRACKER, start_watchdog
     start_watchdog(base_job, world, on_abort=getattr(transport, "abort", None))
     TRACKER.add_state("transport", transport.counters)
+    if device.type == "cuda" and world > 1 and os.environ.get("DLI_DEVICE_MARKS", "1") == "1":
+        TRACKER.enable_device_marks(device)
     # the fallback transport (agreed on by every rank) cannot carry the head: then nobody rotates
     rotate = rotate and transport.supports_head
     channels = _Channels(job, srank, pp, head_rotation=rotate)

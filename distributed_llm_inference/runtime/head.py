@@ -247,6 +247,7 @@ class HeadJobs:
             tok = self.runner.run(plan, None)
             # device -> host by a copy kernel on the head stream (no shared copy engine)
             pinned, ev = token_ring(self.runner.device).take(tok, self.stream)
+        TRACKER.device_mark("head", plan.step, self.stream)
         self.publish(plan, pinned, ev)
 
     @property

@@ -28,6 +28,9 @@ from typing import Callable, List, Optional
 EXIT_CODE = 3
 
 
+_MARK_ROLES = ("compute", "send", "recv", "head")
+
+
 class OpTracker:
     def __init__(self):
         self.rank = int(os.environ.get("RANK", "0"))
@@ -37,6 +40,7 @@ class OpTracker:
         self.ops = 0
         self._wait: Optional[dict] = None
         self._state: dict = {}      # name -> callable returning a JSON-able snapshot
+        self._words = None          # device marks (enable_device_marks)
 
     def mark(self, op: str, step: int = -1, mb: int = -1, peer: int = -1, stream: str = "") -> None:
         rec = {"op": op, "step": step, "mb": mb, "peer": peer, "stream": stream}
@@ -45,6 +49,29 @@ class OpTracker:
             self.last = rec
         self.t_last = time.monotonic()
         self.ops += 1
+
+    def enable_device_marks(self, device) -> None:
+        """Per-stream device progress in the record: after each step's work on a role's stream
+        (compute / send / recv / head) a one-lane kernel stores ``step + 1`` into host-mapped
+        memory, next to the host's count of what it enqueued - a stuck rank then shows which
+        stream is behind, and by how many steps, without any GPU call."""
+        from .. import ops
+        self._C = ops.native()
+        self._words = self._C.HostWords(len(_MARK_ROLES))
+        self._enq = {r: 0 for r in _MARK_ROLES}
+        self.add_state("device", self.device_state)
+
+    def device_mark(self, role: str, step: int, stream) -> None:
+        if self._words is None or stream is None:
+            return
+        i = _MARK_ROLES.index(role)
+        self._enq[role] = step + 1
+        self._C.signal(self._words.dev_ptr(i), step + 1, stream.cuda_stream)
+
+    def device_state(self) -> dict:
+        """{role: [last step enqueued, last step the device finished]} (0 = none yet)."""
+        return {r: [self._enq[r] - 1, self._words.get(i) - 1] for i, r in enumerate(_MARK_ROLES)
+                if self._enq[r]}
 
     def add_state(self, name: str, fn) -> None:
         """Register a snapshot provider (transport counters, head-job queue...) for the record."""
