@@ -89,8 +89,18 @@ class LMHead(nn.Module):
                                        self.spec.rms_norm_eps, residual)
         return normed
 
-    def project(self, normed: torch.Tensor) -> torch.Tensor:
-        """Vocabulary projection of final-normed hidden states -> logits."""
+    def project(self, normed: torch.Tensor, tile: bool = False) -> torch.Tensor:
+        """Vocabulary projection of final-normed hidden states -> logits.  ``tile``: on the GPU
+        take the hand-written tile GEMM even where hipBLASLt is faster (the rotating head's side
+        stream: a library stream-K kernel there may be in flight next to another one on the
+        compute stream, and persistent kernels that wait for each other's workgroups can
+        deadlock - ops.library_gemms)."""
+        w = self._tied.weight if self.proj is None else self.proj.weight
+        if (tile and normed.is_cuda and normed.dim() == 2 and normed.dtype == torch.bfloat16
+                and w.dtype == torch.bfloat16 and w.numel() and w.shape[0] % 256 == 0
+                and (self.proj is None or self.proj.bias is None)
+                and (w.shape[1] * 2) % 128 == 0):
+            return ops.gemm_tile(normed.contiguous(), w, splits=1)
         if self.proj is None:
             return F.linear(normed, self._tied.weight)
         return self.proj(normed)

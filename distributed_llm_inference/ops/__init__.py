@@ -527,6 +527,20 @@ TILE_GEMM_MAX_M = 2048   # above (prefill chunks): hipBLASLt's large-M solutions
 _CUS = 256
 
 
+def library_gemms() -> bool:
+    """Whether products the tile kernel does not take well (M < 128, M > 2048, the wide LM head)
+    may go to hipBLASLt (default).  ``DLI_GEMM_LIB=0`` keeps every tileable product on the tile
+    kernel: hipBLASLt picks stream-K solutions for some of these shapes - persistent kernels
+    sized to the CU count whose workgroups wait for each other's partial tiles - and two of
+    them in flight at once (the head stream next to the compute stream, or ranks sharing one
+    GPU) can each hold CUs the other needs.  Measured: every hipBLASLt kernel torch picks for the
+    70B decode shapes at M = 1..4096 is stream-K (``SK3``, profiles/streams/blaslt_streamk.txt);
+    8 pipeline ranks sharing one GPU at 32 rows per micro-batch stalled in 4 of 4 runs with them
+    and completed with this off.  Off by default when ranks share a GPU (``DLI_SHARE_GPU=1``)."""
+    default = "0" if os.environ.get("DLI_SHARE_GPU", "0") == "1" else "1"
+    return os.environ.get("DLI_GEMM_LIB", default) == "1"
+
+
 def tile_gemm_splits(M: int, N: int, K: int, elem_bytes: int = 2) -> int:
     """Split-K factor for ``gemm_tile`` on an [M, K] x [N, K]^T product, or 0 = not eligible.
 
@@ -535,11 +549,14 @@ def tile_gemm_splits(M: int, N: int, K: int, elem_bytes: int = 2) -> int:
     best per shape, profiles/gemm_tile_bench.json).  ``DLI_TILE_GEMM=0`` disables the kernel."""
     if os.environ.get("DLI_TILE_GEMM", "1") == "0":
         return 0
-    if not (TILE_GEMM_MIN_M <= M <= TILE_GEMM_MAX_M) or N % 256 or (K * elem_bytes) % 128:
+    lib = library_gemms()
+    if N % 256 or (K * elem_bytes) % 128 or M < 1:
+        return 0
+    if lib and not (TILE_GEMM_MIN_M <= M <= TILE_GEMM_MAX_M):
         return 0
     k_tiles = K * elem_bytes // 128
     tiles = ((M + 255) // 256) * (N // 256)
-    if tiles > 2 * _CUS:
+    if lib and tiles > 2 * _CUS:
         return 0  # e.g. the 128256-wide LM head: hipBLASLt's wide-N solutions are faster (690 vs 824 us)
     best, best_util = 1, 0.0
     for s in range(1, int(os.environ.get("DLI_TILE_MAX_SPLITS", "8")) + 1):

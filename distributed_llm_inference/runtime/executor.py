@@ -29,7 +29,7 @@ from ..models.common import AttnMetadata
 from ..models.llama.cache import KVPool
 from ..models.stage import CausalLMStage
 from ..utils.cuda import capture_guard, prime_graph_rng
-from .watchdog import wait_event
+from .watchdog import TRACKER, wait_event
 
 log = logging.getLogger(__name__)
 
@@ -407,6 +407,9 @@ class StageExecutor:
         grows = self._graph_rows(B) if decode else None
         rows = grows if grows is not None else B
         self._stage_metadata(plan, rows)
+        if TRACKER._words is not None:
+            TRACKER.note_plan(plan.step, B=B, T=plan.num_tokens, rows=rows,
+                              max_len=int(self.staging.h["seq_lens"][:B].max()))
         if self.stage.has_embed and plan.tokens is None:
             # lookahead step: this step's input tokens are the previous step's sampler output,
             # still on the device (stream order makes the copy wait for that sampler)
@@ -427,6 +430,7 @@ class StageExecutor:
             g = self._graphs.get(key)
             if g is None:
                 g = self._capture(grows, project)
+            TRACKER.device_mark("compute_in", plan.step, torch.cuda.current_stream())
             g.graph.replay()
             if self.stage.has_head and project:
                 return g.out[:n_sample]

@@ -111,7 +111,7 @@ class HeadRunner:
 
     def _forward(self, rows: int) -> torch.Tensor:
         d = self.staging.d
-        logits = self.head.project(self.x[:rows])
+        logits = self.head.project(self.x[:rows], tile=True)
         return ops.sample(logits, temperature=d["temperature"][:rows], top_k=d["top_k"][:rows],
                           top_p=d["top_p"][:rows], seeds=d["seeds"][:rows], step=d["step"],
                           out=self.out[:rows], counters=d["sample_pos"][:rows])

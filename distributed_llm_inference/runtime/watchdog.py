@@ -17,6 +17,7 @@ publisher), and until then every rank just waits.  Here:
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import json
 import os
@@ -28,7 +29,8 @@ from typing import Callable, List, Optional
 EXIT_CODE = 3
 
 
-_MARK_ROLES = ("compute", "send", "recv", "head")
+# compute_in: this step's inputs uploaded, its graph about to run; compute: graph done
+_MARK_ROLES = ("compute_in", "compute", "send", "recv", "head")
 
 
 class OpTracker:
@@ -38,7 +40,8 @@ class OpTracker:
         self.by_thread: dict = {}   # thread name -> its last op (the pipeline loop, publisher...)
         self.t_last = time.monotonic()
         self.ops = 0
-        self._wait: Optional[dict] = None
+        self._waits: dict = {}      # thread name -> the blocking host wait it is in
+        self.plans: "collections.deque" = collections.deque(maxlen=12)   # recent step shapes
         self._state: dict = {}      # name -> callable returning a JSON-able snapshot
         self._words = None          # device marks (enable_device_marks)
 
@@ -80,14 +83,23 @@ class OpTracker:
     @contextlib.contextmanager
     def waiting(self, what: str, step: int = -1, mb: int = -1, peer: int = -1):
         """A host wait that must end while the job is healthy (the watchdog times it)."""
-        self._wait = {"what": what, "step": step, "mb": mb, "peer": peer, "t0": time.monotonic()}
+        name = threading.current_thread().name
+        self._waits[name] = {"what": what, "step": step, "mb": mb, "peer": peer,
+                             "t0": time.monotonic()}
         try:
             yield
         finally:
-            self._wait = None
+            self._waits.pop(name, None)
 
     def current_wait(self) -> Optional[dict]:
-        return self._wait
+        """The longest-running host wait of any thread (None: no thread is waiting)."""
+        ws = list(self._waits.values())
+        return min(ws, key=lambda w: w["t0"]) if ws else None
+
+    def note_plan(self, step: int, **shape) -> None:
+        """Shape of a step this rank executes (B, T, graph rows, longest sequence) for the
+        record: a step whose kernels never finish can be told apart by its inputs."""
+        self.plans.append({"step": step, **shape})
 
     def record(self) -> dict:
         now = time.monotonic()
@@ -96,10 +108,14 @@ class OpTracker:
         others = {k: v for k, v in self.by_thread.items() if k != threading.main_thread().name}
         if others:
             r["threads"] = others
-        w = self._wait
-        if w is not None:
-            r["waiting"] = {k: v for k, v in w.items() if k != "t0"}
-            r["waiting"]["for_s"] = round(now - w["t0"], 1)
+        waits = {}
+        for name, w in list(self._waits.items()):
+            waits[name] = {k: v for k, v in w.items() if k != "t0"}
+            waits[name]["for_s"] = round(now - w["t0"], 1)
+        if waits:
+            r["waiting"] = waits
+        if self.plans:
+            r["plans"] = list(self.plans)
         for name, fn in list(self._state.items()):
             try:
                 r[name] = fn()

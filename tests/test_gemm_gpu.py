@@ -106,6 +106,35 @@ def test_linear_dispatches_decode_batches_to_tile_gemm(gpu, monkeypatch):
     assert (y.float() - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
 
 
+def test_no_library_gemms_keeps_small_and_wide_products_on_the_tile_kernel(gpu, monkeypatch):
+    """DLI_GEMM_LIB=0 (default when ranks share a GPU): M < 128 and the wide LM head stay on the
+    tile kernel (hipBLASLt's choices there are stream-K persistent kernels); the rotating head's
+    projection always does (LMHead.project(tile=True))."""
+    from distributed_llm_inference.config import PRESETS
+    from distributed_llm_inference.models.common import Linear
+    from distributed_llm_inference.models.embed_head import LMHead
+    monkeypatch.setenv("DLI_GEMM_LIB", "0")
+    calls = []
+    real = ops.gemm_tile
+    monkeypatch.setattr(ops, "gemm_tile", lambda *a, **k: calls.append(a[1].shape) or real(*a, **k))
+    lin = Linear(1024, 2048, device=gpu)
+    torch.nn.init.normal_(lin.weight, std=0.02)
+    for M in (3, 32, 127):
+        x = torch.randn(M, 1024, device=gpu, dtype=torch.bfloat16)
+        ref = x.float() @ lin.weight.float().t()
+        assert (lin(x).float() - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
+    assert len(calls) == 3, calls
+    monkeypatch.setenv("DLI_GEMM_LIB", "1")
+    spec = PRESETS["llama-3-8b"].replace(hidden_size=1024, vocab_size=256 * 300)
+    head = LMHead(spec, device=gpu).init_random(3)
+    x = torch.randn(32, 1024, device=gpu, dtype=torch.bfloat16)
+    calls.clear()
+    y = head.project(x, tile=True)
+    assert calls, "the rotating head's projection did not use the tile GEMM"
+    ref = x.float() @ head.proj.weight.float().t()
+    assert (y.float() - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
+
+
 @pytest.mark.parametrize("M,N,K,splits", [(256, 256, 128, 1), (512, 512, 2048, 1), (100, 768, 1024, 3),
                                           (512, 1024, 8192, 4), (33, 256, 384, 1)])
 def test_gemm_tile_fp8_matches_dequantised_fp32(gpu, M, N, K, splits):

@@ -54,7 +54,7 @@ def test_stalled_rank_ends_the_job_with_every_last_op(fault, culprit):
     assert sorted(rows) == list(range(n)), rows
     # the driver was waiting for tokens of a step in flight
     d = json.loads(rows[0])
-    assert d["waiting"]["what"] == "tokens", d
+    assert d["waiting"]["MainThread"]["what"] == "tokens", d
     for rk, row in rows.items():
         rec = json.loads(row)
         assert rec["last_op"]["op"] and rec["last_op"]["step"] >= 0, rec
