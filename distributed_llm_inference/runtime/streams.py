@@ -131,7 +131,8 @@ class HostTokenRing:
         off = (self.i % self.slots) * self.item_bytes
         self.i += 1
         s = stream or torch.cuda.current_stream(self.device)
-        self.C.copy_segments(self.buf.dev_ptr + off, tok.data_ptr(), [(0, nb)], s.cuda_stream)
+        if nb:   # (an empty step samples nothing: no copy, just the event)
+            self.C.copy_segments(self.buf.dev_ptr + off, tok.data_ptr(), [(0, nb)], s.cuda_stream)
         ev = torch.cuda.Event()
         ev.record(s)
         return self.view[off: off + nb].view(torch.int32), ev
