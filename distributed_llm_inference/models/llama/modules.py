@@ -189,6 +189,8 @@ class LlamaMLP(nn.Module):
         if self.fused_swiglu:
             if gp.tile_splits(normed) and ops.gate_up_on_tile():
                 h = ops.gemm_tile(normed, gp.weight, swiglu=True)
+            elif gp.tile_splits(normed) and ops.gate_up_plain_tile():
+                h = ops.swiglu_interleaved(ops.gemm_tile(normed, gp.weight))
             else:
                 h = ops.swiglu_interleaved(gp(normed))
             return self.down_proj(h, defer_reduce=defer_reduce)

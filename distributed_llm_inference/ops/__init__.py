@@ -99,9 +99,14 @@ def bf16_bf16_partials() -> bool:
 
 def gate_up_on_tile() -> bool:
     """bf16 gate|up with SwiGLU in the tile GEMM's epilogue (default); ``DLI_GATEUP_TILE=0``
-    runs it on hipBLASLt (interleaved weight as-is) followed by ``swiglu_interleaved`` - the A/B
-    for the step's largest GEMM."""
+    runs it on hipBLASLt (interleaved weight as-is) followed by ``swiglu_interleaved``, ``plain``
+    on the tile kernel with the plain bf16 store followed by ``swiglu_interleaved`` - the A/Bs
+    for the step's largest GEMM (hipBLASLt: -1.8 %, profiles/gateup_tile_vs_hipblaslt_ab.txt)."""
     return os.environ.get("DLI_GATEUP_TILE", "1") == "1"
+
+
+def gate_up_plain_tile() -> bool:
+    return os.environ.get("DLI_GATEUP_TILE", "1") == "plain"
 
 
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
