@@ -151,3 +151,37 @@ def test_signal_then_wait_orders_data(gpu):
         assert words.get(0) == 0
         assert torch.all(out == it)
     buf.close()
+
+
+def test_device_marks_report_stream_progress(gpu):
+    """The watchdog's per-stream device marks: a mark queued behind a spinning wait stays at the
+    previous step until the wait is released; marks on other streams are unaffected."""
+    import time
+    from distributed_llm_inference import ops
+    from distributed_llm_inference.runtime.streams import RankStreams
+    from distributed_llm_inference.runtime.watchdog import OpTracker
+    C = ops.native()
+    dev = torch.device("cuda", 0)
+    rs = RankStreams(dev, "dedicated")
+    tr = OpTracker()
+    tr.enable_device_marks(dev)
+    flags = C.HostWords(2)
+    try:
+        tr.device_mark("recv", 0, rs.recv)
+        tr.device_mark("compute", 0, rs.compute)
+        rs.synchronize()
+        assert tr.device_state()["recv"] == [0, 0]
+        C.wait_geq(flags.dev_ptr(0), 1, 10.0, flags.dev_ptr(1), 1, rs.recv.cuda_stream, 0)
+        tr.device_mark("recv", 1, rs.recv)
+        tr.device_mark("compute", 1, rs.compute)
+        rs.compute.synchronize()
+        time.sleep(0.05)
+        st = tr.device_state()
+        assert st["compute"] == [1, 1] and st["recv"] == [1, 0], st
+        flags.set(0, 1)
+        rs.recv.synchronize()
+        assert tr.device_state()["recv"] == [1, 1] and flags.get(1) == 0
+    finally:
+        flags.set(0, 1)
+        torch.cuda.synchronize(dev)
+        rs.close()
