@@ -109,6 +109,40 @@ def test_rope_cache_from_splitk_partials_bit_identical(gpu, nh, nkv, D, S, fp8):
     assert torch.equal(v1.view(torch.uint8), v2.view(torch.uint8))
 
 
+@pytest.mark.parametrize("nh,nkv,D,S", [(64, 8, 128, 3), (8, 8, 64, 0), (4, 2, 32, 2)])
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("parts_bf16", [False, True])
+def test_rope_cache_v8_bit_identical_to_v4(gpu, monkeypatch, nh, nkv, D, S, fp8, parts_bf16):
+    """The 16-byte kernel (default for D % 16 == 0) computes every element exactly as the
+    4-element kernel (DLI_ROPE_V8=0): q, q_sink, K and V^T caches, bf16 / fp32 / bf16 partials."""
+    if S == 0 and parts_bf16:
+        pytest.skip("no partials")
+    torch.manual_seed(21)
+    T, bs, nblocks = 41, 64, 8
+    width = (nh + 2 * nkv) * D
+    if S:
+        parts = torch.randn(S, T, width, device=gpu)
+        src = ops.SplitKPartials(parts.to(torch.bfloat16) if parts_bf16 else parts)
+    else:
+        src = torch.randn(T, width, device=gpu, dtype=BF)
+    pos = torch.randint(0, 300, (T,), device=gpu, dtype=torch.int32)
+    slots = torch.randperm(nblocks * bs, device=gpu)[:T].to(torch.int64)
+    slots[7] = -1
+    cs = ref.build_cos_sin(D, 512, 500000.0, device=gpu)
+    k1, v1 = _make_cache(nblocks, nkv, bs, D, gpu)
+    if fp8:
+        k1, v1 = k1.to(torch.float8_e4m3fn), v1.to(torch.float8_e4m3fn)
+    k2, v2 = k1.clone(), v1.clone()
+    outs = []
+    for v8, (k, v) in (("1", (k1, v1)), ("0", (k2, v2))):
+        monkeypatch.setenv("DLI_ROPE_V8", v8)
+        outs.append(ops.rope_cache(src, pos, slots, cs, nh, nkv, D, k, v, window=100,
+                                   want_sink=True, k_scale=0.5, v_scale=0.25))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(k1.view(torch.uint8), k2.view(torch.uint8))
+    assert torch.equal(v1.view(torch.uint8), v2.view(torch.uint8))
+
+
 @pytest.mark.parametrize("fp8", [False, True])
 def test_rope_cache_bf16_partials_match_fp32_partials(gpu, fp8):
     """bf16 split-K partials (fp8 path, gemm_tile epilogue 4) are summed in fp32 in split order:
