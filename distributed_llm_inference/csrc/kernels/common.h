@@ -127,6 +127,87 @@ __device__ __forceinline__ bf16 sum_parts1(const bf16* p, size_t stride) {
   return (bf16)s;
 }
 
+// One row of a row-per-workgroup kernel (RMSNorm, the fp8 row quantiser): VPT 16-byte vectors per
+// lane at vector index lane + i * blockDim.x, the row's global loads issued before any is used -
+// one memory round trip per row (per ~64 VGPRs of split-K partials).  (Loads guarded per vector by `idx < nvec` made hipcc wait
+// for each vector's loads before issuing the next vector's: VPT serial round trips per row, plus
+// one more for the residual.)  Lanes past the row's end load its last vector and must discard
+// what they get (`row_valid`).  NS > 0: the vector is the sum of NS split-K partials (PB: bf16
+// partials), summed in split order and rounded once, exactly as sum_parts8.
+__device__ __forceinline__ int row_vec_idx(int i, int nvec) {
+  const int idx = (int)threadIdx.x + i * (int)blockDim.x;
+  return idx < nvec ? idx : nvec - 1;
+}
+__device__ __forceinline__ bool row_valid(int i, int nvec) {
+  return (int)threadIdx.x + i * (int)blockDim.x < nvec;
+}
+
+template <int VPT, int NS, bool PB>
+__device__ __forceinline__ void load_row_vecs(bf16x8 (&a)[VPT], const bf16* x, const void* parts,
+                                              size_t row_off, size_t stride, int nvec) {
+  if constexpr (NS == 0) {
+    const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + row_off);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) a[i] = xr[row_vec_idx(i, nvec)];
+  } else {
+    // partial vectors in flight per lane: ~64 VGPRs of them (a bf16 vector is 4, an fp32 one 8),
+    // so at most CH vectors' partials per round trip
+    constexpr int CH0 = PB ? 16 / NS : 8 / NS;
+    constexpr int CH = CH0 < 1 ? 1 : (CH0 > VPT ? VPT : CH0);
+#pragma unroll
+    for (int c = 0; c < VPT; c += CH) {
+      if constexpr (PB) {
+        const bf16* pp = static_cast<const bf16*>(parts) + row_off;
+        bf16x8 r[CH][NS];
+#pragma unroll
+        for (int i = 0; i < CH; ++i)
+#pragma unroll
+          for (int k = 0; k < NS; ++k)
+            if (c + i < VPT)
+              r[i][k] = *reinterpret_cast<const bf16x8*>(
+                  pp + k * stride + (size_t)row_vec_idx(c + i, nvec) * 8);
+#pragma unroll
+        for (int i = 0; i < CH; ++i)
+          if (c + i < VPT)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              float sm = (float)r[i][0][j];
+#pragma unroll
+              for (int k = 1; k < NS; ++k) sm += (float)r[i][k][j];
+              a[c + i][j] = (bf16)sm;
+            }
+      } else {
+        const float* pp = static_cast<const float*>(parts) + row_off;
+        f32x4 r0[CH][NS], r1[CH][NS];
+#pragma unroll
+        for (int i = 0; i < CH; ++i)
+#pragma unroll
+          for (int k = 0; k < NS; ++k)
+            if (c + i < VPT) {
+              const float* q = pp + k * stride + (size_t)row_vec_idx(c + i, nvec) * 8;
+              r0[i][k] = *reinterpret_cast<const f32x4*>(q);
+              r1[i][k] = *reinterpret_cast<const f32x4*>(q + 4);
+            }
+#pragma unroll
+        for (int i = 0; i < CH; ++i)
+          if (c + i < VPT) {
+            f32x4 s0 = r0[i][0], s1 = r1[i][0];
+#pragma unroll
+            for (int k = 1; k < NS; ++k) {
+              s0 += r0[i][k];
+              s1 += r1[i][k];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              a[c + i][j] = (bf16)s0[j];
+              a[c + i][j + 4] = (bf16)s1[j];
+            }
+          }
+      }
+    }
+  }
+}
+
 // dispatch a runtime split count 1..8 to a compile-time NS (0 = no partials)
 #define DLI_SPLITS_SWITCH(splits, MACRO) \
   switch (splits) {                      \

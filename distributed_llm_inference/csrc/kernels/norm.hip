@@ -16,70 +16,61 @@ namespace dli {
 // of the tile GEMM that produced it (gemm_tile.hip kStoreF32); they are summed and rounded to bf16
 // here, exactly as tile_splitk_reduce_kernel would, so the reduction pass and its bf16 round trip
 // through HBM disappear while the numerics stay bit-identical.
-template <int VPT, int NS>  // bf16x8 vectors per thread; NS > 0: x is NS fp32 partials
+template <int VPT, int NS, bool PB>  // bf16x8 vectors per thread; NS > 0: x is NS partials
 __global__ void __launch_bounds__(256) rms_norm_kernel(bf16* __restrict__ out,
                                                        const bf16* __restrict__ x,
                                                        const bf16* residual_in, bf16* residual_out,
                                                        const bf16* __restrict__ w, float eps,
                                                        int hidden, int add_residual,
                                                        const void* __restrict__ x_parts,
-                                                       size_t split_stride, bool parts_bf16) {
+                                                       size_t split_stride) {
   __shared__ float scratch[8];
   const int row = blockIdx.x;
   const int nvec = hidden >> 3;
-  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * hidden);
-  const bf16x8* ri = reinterpret_cast<const bf16x8*>(residual_in + (size_t)row * hidden);
-  bf16x8* ro = reinterpret_cast<bf16x8*>(residual_out + (size_t)row * hidden);
+  const size_t row_off = (size_t)row * hidden;
+  const bf16x8* ri = reinterpret_cast<const bf16x8*>(residual_in + row_off);
+  bf16x8* ro = reinterpret_cast<bf16x8*>(residual_out + row_off);
   const bf16x8* wr = reinterpret_cast<const bf16x8*>(w);
-  bf16x8* outr = reinterpret_cast<bf16x8*>(out + (size_t)row * hidden);
+  bf16x8* outr = reinterpret_cast<bf16x8*>(out + row_off);
+
+  // every load of the row first (common.h load_row_vecs): weights, residual, x / partials
+  bf16x8 wv[VPT], rv[VPT], a[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) wv[i] = wr[row_vec_idx(i, nvec)];
+  if (add_residual) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) rv[i] = ri[row_vec_idx(i, nvec)];
+  }
+  load_row_vecs<VPT, NS, PB>(a, x, x_parts, row_off, split_stride, nvec);
 
   float v[VPT][8];
-  bf16x8 wv[VPT];  // weights loaded with the row: no dependent L2 round trip after the reduction
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
-    const int idx = threadIdx.x + i * blockDim.x;
-    if (idx < nvec) {
-      wv[i] = wr[idx];
-      bf16x8 a;
-      if constexpr (NS > 0) {
-        // fp32 partials, or bf16 ones (8-bit weight modes, gemm_tile epilogue 4)
-        const size_t off = (size_t)row * hidden + (size_t)idx * 8;
-        if (parts_bf16)
-          sum_parts8<NS>(static_cast<const bf16*>(x_parts) + off, split_stride, a);
-        else
-          sum_parts8<NS>(static_cast<const float*>(x_parts) + off, split_stride, a);
-      } else
-        a = xr[idx];
-      if (add_residual) {
-        bf16x8 r = ri[idx];
-        bf16x8 s;
+    const bool ok = row_valid(i, nvec);
+    if (add_residual) {
+      bf16x8 s;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s[j] = (bf16)((float)a[j] + (float)r[j]);
-        ro[idx] = s;
-        a = s;
-      }
+      for (int j = 0; j < 8; ++j) s[j] = (bf16)((float)a[i][j] + (float)rv[i][j]);
+      if (ok) ro[threadIdx.x + i * blockDim.x] = s;
+      a[i] = s;
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[i][j] = (float)a[j];
-        ss = __builtin_fmaf(v[i][j], v[i][j], ss);   // explicit: same rounding in every instantiation
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    for (int j = 0; j < 8; ++j) {
+      v[i][j] = ok ? (float)a[i][j] : 0.f;
+      ss = __builtin_fmaf(v[i][j], v[i][j], ss);   // explicit: same rounding in every instantiation
     }
   }
   ss = block_reduce_sum(ss, scratch);
   const float rstd = rsqrtf(ss / (float)hidden + eps);
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
-    const int idx = threadIdx.x + i * blockDim.x;
-    if (idx < nvec) {
+    if (row_valid(i, nvec)) {
       const bf16x8 ww = wv[i];
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[i][j] * rstd * (float)ww[j]);
-      outr[idx] = o;
+      outr[threadIdx.x + i * blockDim.x] = o;
     }
   }
 }
@@ -184,23 +175,29 @@ int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* res
   const int add = residual_in != nullptr ? 1 : 0;
   const size_t stride = (size_t)rows * hidden;
   const int ns = x_parts != nullptr ? splits : 0;
-#define DLI_RMS(NS)                                                                          \
-  do {                                                                                       \
-    const int nvec = hidden / 8;                                                             \
-    const int threads = norm_threads(hidden);                                                \
-    const int vpt = (nvec + threads - 1) / threads;                                          \
-    if (vpt <= 1) rms_norm_kernel<1, NS><<<rows, threads, 0, stream>>>(                      \
-        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride, parts_bf16);           \
-    else if (vpt <= 2) rms_norm_kernel<2, NS><<<rows, threads, 0, stream>>>(                 \
-        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride, parts_bf16);           \
-    else if (vpt <= 4) rms_norm_kernel<4, NS><<<rows, threads, 0, stream>>>(                 \
-        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride, parts_bf16);           \
-    else if (vpt <= 8) rms_norm_kernel<8, NS><<<rows, threads, 0, stream>>>(                 \
-        out, x, residual_in, residual_out, w, eps, hidden, add, x_parts, stride, parts_bf16);           \
-    else return -1;                                                                          \
+  const int nvec = hidden / 8;
+  const int threads = norm_threads(hidden);
+  const int vpt = (nvec + threads - 1) / threads;
+  if (vpt > 8) return -1;
+#define DLI_RMS_V(V, NS, PB)                                                           \
+  rms_norm_kernel<V, NS, PB><<<rows, threads, 0, stream>>>(out, x, residual_in, residual_out, \
+                                                           w, eps, hidden, add, x_parts, stride)
+#define DLI_RMS_PB(NS, PB)                      \
+  do {                                          \
+    if (vpt <= 1) DLI_RMS_V(1, NS, PB);         \
+    else if (vpt <= 2) DLI_RMS_V(2, NS, PB);    \
+    else if (vpt <= 4) DLI_RMS_V(4, NS, PB);    \
+    else DLI_RMS_V(8, NS, PB);                  \
+  } while (0)
+#define DLI_RMS(NS)                                                   \
+  do {                                                                \
+    if (NS > 0 && parts_bf16) DLI_RMS_PB(NS, true);                   \
+    else DLI_RMS_PB(NS, false);                                       \
   } while (0)
   DLI_SPLITS_SWITCH(ns, DLI_RMS)
 #undef DLI_RMS
+#undef DLI_RMS_PB
+#undef DLI_RMS_V
   return 0;
 }
 

@@ -59,50 +59,44 @@ __device__ __forceinline__ void store_fp8_row(float (&v)[VPT][8], uint8_t* __res
 // x_parts (optional): x given as split-K partials [splits, rows, K] of the tile GEMM that
 // produced it, summed and rounded to bf16 on load: fp32 (bit-identical to the reduce pass) or,
 // with parts_bf16, bf16 partials (fp8 path)
-template <int VPT, int NS>
+template <int VPT, int NS, bool PB>
 __global__ void __launch_bounds__(1024) quant_rowwise_kernel(
     uint8_t* __restrict__ q, float* __restrict__ scale, const bf16* __restrict__ x,
     const bf16* residual_in, bf16* residual_out, const bf16* __restrict__ norm_w, float eps,
-    int K, const void* __restrict__ x_parts, size_t split_stride, bool parts_bf16) {
+    int K, const void* __restrict__ x_parts, size_t split_stride) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nvec = K >> 3;
   const bool add_residual = residual_in != nullptr;
-  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)row * K);
-  const bf16x8* ri = reinterpret_cast<const bf16x8*>(residual_in + (size_t)row * K);
-  bf16x8* ro = reinterpret_cast<bf16x8*>(residual_out + (size_t)row * K);
-  float v[VPT][8];
-  bf16x8 wv[VPT];  // norm weights loaded with the row (no dependent load after the reduction)
+  const size_t row_off = (size_t)row * K;
+  const bf16x8* ri = reinterpret_cast<const bf16x8*>(residual_in + row_off);
+  bf16x8* ro = reinterpret_cast<bf16x8*>(residual_out + row_off);
   const bf16x8* wr = reinterpret_cast<const bf16x8*>(norm_w);
+  // the row's loads first (common.h load_row_vecs): norm weights, residual, x / partials
+  bf16x8 wv[VPT], rv[VPT], a[VPT];
+  if (norm_w) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) wv[i] = wr[row_vec_idx(i, nvec)];
+  }
+  if (add_residual) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) rv[i] = ri[row_vec_idx(i, nvec)];
+  }
+  load_row_vecs<VPT, NS, PB>(a, x, x_parts, row_off, split_stride, nvec);
+  float v[VPT][8];
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
-    const int idx = threadIdx.x + i * blockDim.x;
-    if (idx < nvec) {
-      if (norm_w) wv[i] = wr[idx];
-      bf16x8 a;
-      if constexpr (NS > 0) {
-        const size_t off = (size_t)row * K + (size_t)idx * 8;
-        if (parts_bf16)
-          sum_parts8<NS>(static_cast<const bf16*>(x_parts) + off, split_stride, a);
-        else
-          sum_parts8<NS>(static_cast<const float*>(x_parts) + off, split_stride, a);
-      } else
-        a = xr[idx];
-      if (add_residual) {
-        bf16x8 r = ri[idx];
+    const bool ok = row_valid(i, nvec);
+    if (add_residual) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = (bf16)((float)a[j] + (float)r[j]);
-        ro[idx] = a;
-      }
+      for (int j = 0; j < 8; ++j) a[i][j] = (bf16)((float)a[i][j] + (float)rv[i][j]);
+      if (ok) ro[threadIdx.x + i * blockDim.x] = a[i];
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[i][j] = (float)a[j];
-        ss = __builtin_fmaf(v[i][j], v[i][j], ss);   // explicit: same rounding in every instantiation
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    for (int j = 0; j < 8; ++j) {
+      v[i][j] = ok ? (float)a[i][j] : 0.f;
+      ss = __builtin_fmaf(v[i][j], v[i][j], ss);   // explicit: same rounding in every instantiation
     }
   }
   if (norm_w) {
@@ -110,8 +104,7 @@ __global__ void __launch_bounds__(1024) quant_rowwise_kernel(
     const float rstd = rsqrtf(ss / (float)K + eps);
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
-      const int idx = threadIdx.x + i * blockDim.x;
-      if (idx < nvec) {
+      if (row_valid(i, nvec)) {
         const bf16x8 ww = wv[i];
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[i][j] = (float)(bf16)(v[i][j] * rstd * (float)ww[j]);
@@ -233,10 +226,15 @@ int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* re
   const int threads = row_threads(nvec);
   const int vpt = (nvec + threads - 1) / threads;
   const int ns = x_parts != nullptr ? splits : 0;
-#define DLI_QUANT(V, NS)                                                                    \
-  quant_rowwise_kernel<V, NS><<<rows, threads, 0, stream>>>(q, scale, x, residual_in,       \
-                                                            residual_out, norm_w, eps, K,   \
-                                                            x_parts, split_stride, parts_bf16)
+#define DLI_QUANT(V, NS)                                                                     \
+  do {                                                                                       \
+    if (NS > 0 && parts_bf16)                                                                \
+      quant_rowwise_kernel<V, NS, true><<<rows, threads, 0, stream>>>(                       \
+          q, scale, x, residual_in, residual_out, norm_w, eps, K, x_parts, split_stride);    \
+    else                                                                                     \
+      quant_rowwise_kernel<V, NS, false><<<rows, threads, 0, stream>>>(                      \
+          q, scale, x, residual_in, residual_out, norm_w, eps, K, x_parts, split_stride);    \
+  } while (0)
 #define DLI_QUANT_NS(NS)                       \
   do {                                         \
     if (vpt <= 1) DLI_QUANT(1, NS);            \

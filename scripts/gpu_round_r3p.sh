@@ -1,0 +1,14 @@
+# Round-3 GPU round P: refresh the README results table (first half of scripts/results_sweep.sh).
+set -u
+mkdir -p gpurun_out/results
+export TMPDIR=/tmp
+run() {  # name, args...
+  local name=$1; shift
+  timeout -k 10 400 python -u bench.py "$@" --json-out gpurun_out/results/$name.json > gpurun_out/results/$name.log 2>&1 || { echo "$name failed"; tail -5 gpurun_out/results/$name.log; exit 1; }
+  echo "$name $(python -c "import json;d=json.load(open('gpurun_out/results/$name.json'));print(d['value'], 'tok/s', d['ms_per_step'], 'ms/step p50', d['p50_token_latency_ms'])")"
+}
+run bf16_b512
+run fp8_b512 --fp8
+run fp8_fp8kv_b512 --fp8 --kv-fp8
+run bf16_fp8kv_b512 --kv-fp8
+run int8_b512 --int8

@@ -1,0 +1,14 @@
+# Round-3 GPU round Q: second half of the README results sweep.
+set -u
+mkdir -p gpurun_out/results
+export TMPDIR=/tmp
+run() {  # name, args...
+  local name=$1; shift
+  timeout -k 10 400 python -u bench.py "$@" --json-out gpurun_out/results/$name.json > gpurun_out/results/$name.log 2>&1 || { echo "$name failed"; tail -5 gpurun_out/results/$name.log; exit 1; }
+  echo "$name $(python -c "import json;d=json.load(open('gpurun_out/results/$name.json'));print(d['value'], 'tok/s', d['ms_per_step'], 'ms/step p50', d['p50_token_latency_ms'])")"
+}
+run bf16_b512_again
+run llama3_8b_bf16_b512 --model llama-3-8b
+run bf16_b1 --batch-per-mb 1 --steps 20
+run bf16_b1_ctx8k --batch-per-mb 1 --prompt-len 8192 --steps 20
+run bf16_b16_ctx8k --batch-per-mb 16 --prompt-len 8192 --steps 10
