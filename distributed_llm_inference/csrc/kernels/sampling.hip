@@ -84,7 +84,31 @@ __global__ void __launch_bounds__(1024) sample_kernel(SampleParams p) {
   if (!(temp > 0.f)) {
     float best = -INFINITY;
     int bi = 0x7fffffff;
-    for (int i = threadIdx.x; i < V; i += blockDim.x) argmax_pair(best, bi, load_logit(p, row, i), i);
+    if (!p.logits_is_f32 && V % 8 == 0 && p.row_stride % 8 == 0) {
+      // bf16 rows: 16-byte loads, 4 in flight per lane (a 128256-wide row is ~16 vectors per
+      // lane instead of ~125 dependent 2-byte loads); the argmax is order-independent
+      // (lower index wins ties), so the result equals the element-wise loop's
+      const bf16x8* r8 = reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(p.logits) +
+                                                         (size_t)row * p.row_stride);
+      const int n8 = V >> 3;
+      for (int base = threadIdx.x; base < n8; base += 4 * blockDim.x) {
+        bf16x8 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i8 = base + u * blockDim.x;
+          v[u] = r8[i8 < n8 ? i8 : n8 - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i8 = base + u * blockDim.x;
+          if (i8 < n8)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) argmax_pair(best, bi, (float)v[u][j], i8 * 8 + j);
+        }
+      }
+    } else {
+      for (int i = threadIdx.x; i < V; i += blockDim.x) argmax_pair(best, bi, load_logit(p, row, i), i);
+    }
     block_argmax(best, bi, s_f, s_i);
     if (p.out_logprobs) {
       float s = 0.f;

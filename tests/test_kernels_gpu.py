@@ -416,6 +416,21 @@ def test_sample_greedy_and_topk1(gpu):
     _close(lp, lp_ref, 1e-3, 1e-3, "logprob")
 
 
+@pytest.mark.parametrize("V", [128256, 1000, 1003])
+def test_sample_greedy_ties_take_the_lowest_index(gpu, V):
+    """16-byte greedy path (bf16, V % 8 == 0) and the element-wise one agree with torch's argmax,
+    ties included (the lowest index wins)."""
+    torch.manual_seed(V)
+    B = 5
+    logits = torch.randn(B, V, device=gpu).clamp(-4, 4).to(BF)
+    logits[:, V // 3] = 9.0
+    logits[:, V - 2] = 9.0
+    logits[1, 0] = 9.0
+    out = ops.sample(logits)
+    assert torch.equal(out.cpu().long(), logits.float().argmax(-1).cpu())
+    assert out[1].item() == 0 and out[0].item() == V // 3
+
+
 def test_sample_distribution(gpu):
     # V small, many rows with the same logits -> empirical frequencies ~ softmax
     V, B = 16, 4096
