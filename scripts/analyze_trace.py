@@ -26,6 +26,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=4, help="decode micro-batch steps to aggregate")
     ap.add_argument("--marker", default="sample_kernel")
+    ap.add_argument("--cycle", default="", help="KERNEL:N - per-position means of KERNEL's calls")
     a = ap.parse_args()
     if a.trace.endswith(".db"):  # rocprofv3 rocpd (SQLite) output
         import sqlite3
@@ -56,6 +57,23 @@ def main():
     print(f"{'kernel':<60} {'calls/step':>10} {'us/step':>10} {'share':>7}")
     for k, v in busy.most_common():
         print(f"{k:<60} {calls[k]/a.steps:>10.1f} {v/1e3/a.steps:>10.1f} {100*v/total_busy:>6.1f}%")
+    # per-position split of a kernel that serves several projections of a layer (the split-K tile
+    # GEMM runs QKV, O and down in that order): mean duration of the i-th call in each cycle
+    if a.cycle:
+        name, n = a.cycle.rsplit(":", 1)
+        n = int(n)
+        pos = [[] for _ in range(n)]
+        step_bounds = marks[-a.steps - 1:]
+        for s0, s1 in zip(step_bounds[:-1], step_bounds[1:]):   # cycles restart every step
+            durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                    for r in rows[s0 + 1:s1 + 1] if short(r["Kernel_Name"]) == name]
+            for j, d in enumerate(durs[:len(durs) - len(durs) % n]):
+                pos[j % n].append(d)
+        print(f"\n{name}: mean us per position in cycles of {n} (per step, {len(pos[0])} cycles)")
+        for i in range(n):
+            d = pos[i]
+            if d:
+                print(f"  position {i}: {sum(d) / len(d) / 1e3:8.1f} us  (min {min(d) / 1e3:.1f})")
 
 
 if __name__ == "__main__":
