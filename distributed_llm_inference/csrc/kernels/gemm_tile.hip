@@ -74,6 +74,11 @@ __device__ __forceinline__ void dma16(const void* g, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
+// non-temporal (cache policy NT): data streamed through once
+__device__ __forceinline__ void dma16_nt(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 2);
+}
+
 __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -181,7 +186,12 @@ __device__ unsigned long long* g_stamp_blk;   // [grid][8]
 // FP8 / INT8: A and B are 1-byte elements (K counted in elements = bytes) with fp32 a_scale[M]
 // (per row) and b_scale[N] (per output channel).  Staging is byte-identical to bf16: a k-tile is
 // 128 bytes of every row (64 bf16, 128 fp8 / int8).
-template <int EPI, int PREC, bool SKT>
+// VAR bit 0 (whole-tile / split-K launches with tiles_m <= 2, i.e. decode micro-batches of
+// <= 512 rows): the weight (B) half-tiles are loaded non-temporal — each weight byte is read by
+// at most the two M-tiles of its panel, so keep the L2 for the re-read activation panels
+// (down projection 203 -> 194 us, gate|up -0.6 %; at 8192^3, where B is re-read by 32 M-tiles,
+// it costs 3 %: profiles/gemm_var_nt_group_ab.json)
+template <int EPI, int PREC, bool SKT, int VAR = 0>
 __global__ void __launch_bounds__(kThreads, 1)
 gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __restrict__ C,
                  const float* __restrict__ a_scale, const float* __restrict__ b_scale,
@@ -260,8 +270,15 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
       finish = !publish && s0 > tile_k0; // ends the tile but did not start it: add predecessors'
       tile = sk.n_dp + t;
     }
-    const int tm = tile % tiles_m;              // the M tiles of one N panel are neighbours:
-    const int tn = tile / tiles_m;              // they share the streamed weight panel via L2
+    // grouped tile order: groups of (up to) 8 M-tiles x all N panels, M fastest inside a group,
+    // so the 32 consecutive tiles an XCD runs share 8 activation and 4 weight panels through its
+    // L2 (the M tiles of one N panel stay neighbours).  Identical to M-fastest order for
+    // tiles_m <= 8 (every decode shape); 8192^3: 1296 -> 1386 TF (profiles/gemm_var_nt_group_ab.json)
+    constexpr int GM = 8;
+    const int gper = GM * tiles_n, grp = tile / gper, grem = tile % gper;
+    const int gm = min(GM, tiles_m - grp * GM);
+    const int tm = grp * GM + grem % gm;
+    const int tn = grem / gm;
     const int m0 = tm * kTM, n0 = tn * kTN;
 
     // ---- DMA source rows: thread stages LDS units u = j*512 + tid (j = 0, 1) of each half-tile ----
@@ -288,7 +305,10 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const char* src = which < 2 ? srcA[which][j] : srcB[which - 2][j];
-        dma16(src + koff, dst + j * 8192);
+        if ((VAR & 1) != 0 && which >= 2)
+          dma16_nt(src + koff, dst + j * 8192);
+        else
+          dma16(src + koff, dst + j * 8192);
       }
     };
 
@@ -704,6 +724,58 @@ int device_cus() {
   return cus[dev];
 }
 
+template <int VAR, int PREC>
+int launch_whole_impl(void* C, const void* A, const void* B, const float* sa, const float* sb,
+                      float* workspace, int M, int N, int K, int splits, int kps, int epilogue,
+                      int tiles, int tiles_m, int tiles_n, hipStream_t stream, OutlierArgs ol,
+                      MxArgs mx) {
+  SkArgs sk{0, 0, nullptr, nullptr, nullptr};
+  if (epilogue == kStoreBf16Part) {   // bf16 partials into C [splits, M, N]; the consumer sums
+    if (splits < 2) return -3;
+    sk.n_dp = tiles * splits;   // the block remap covers the whole grid
+    gemm_tile_kernel<kStoreBf16Part, PREC, false, VAR><<<tiles * splits, kThreads, 0, stream>>>(
+        A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
+    return 0;
+  }
+  // kStoreF32 with splits > 1: partials only, the consumer reduces them (rms_norm_splitk)
+  if (splits > 1 && (workspace == nullptr || epilogue == kSwiGLU)) return -3;
+  if (splits == 1 && epilogue == kStoreF32) return -3;
+  const int grid = tiles * splits;
+  sk.n_dp = grid;
+  if (splits > 1) {
+    gemm_tile_kernel<kStoreF32, PREC, false, VAR><<<grid, kThreads, 0, stream>>>(
+        A, B, workspace, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
+    if (epilogue == kStoreF32) return 0;
+    const size_t MN = (size_t)M * N;
+    size_t blocks = (MN / 8 + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    tile_splitk_reduce_kernel<<<(int)blocks, 256, 0, stream>>>(reinterpret_cast<bf16*>(C),
+                                                               workspace, splits, MN);
+  } else if (epilogue == kSwiGLUMx) {
+    if constexpr (PREC == kFp8)
+      gemm_tile_kernel<kSwiGLUMx, PREC, false, VAR><<<grid, kThreads, 0, stream>>>(
+          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
+  } else if (epilogue == kSwiGLU) {
+    if constexpr (PREC == kFp8Mx) return -4;   // MX activations come from the SwiGLU epilogue
+    else
+      gemm_tile_kernel<kSwiGLU, PREC, false, VAR><<<grid, kThreads, 0, stream>>>(
+          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
+  } else if (epilogue == kStoreBf16) {
+    gemm_tile_kernel<kStoreBf16, PREC, false, VAR><<<grid, kThreads, 0, stream>>>(
+        A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
+  } else {
+    return -4;
+  }
+  return 0;
+}
+
+// non-temporal weight loads (gemm_tile_kernel VAR bit 0) for tiles_m <= 2; DLI_GEMM_BNT=0 turns
+// them off (read per launch, so a captured graph keeps the choice it was captured with)
+bool weights_nt(int tiles_m) {
+  const char* e = getenv("DLI_GEMM_BNT");
+  return tiles_m <= 2 && !(e != nullptr && e[0] == '0');
+}
+
 // splits == 0: data-parallel whole tiles + stream-K tail (SkArgs); workspace = the
 // gemm_tile_sk_workspace_floats() layout: [flags | err | pad] 4 KB, then sk_wgs fp32 slabs.
 template <int PREC>
@@ -751,44 +823,11 @@ int launch_tile(void* C, const void* A, const void* B, const float* sa, const fl
   const int kps = (kt + splits - 1) / splits;
   if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
   if (PREC == kFp8Mx && kps > kMxMaxKt) return -15;   // its scales must fit the LDS slot
-  if (epilogue == kStoreBf16Part) {   // bf16 partials into C [splits, M, N]; the consumer sums
-    if (splits < 2) return -3;
-    sk.n_dp = tiles * splits;   // the block remap covers the whole grid
-    gemm_tile_kernel<kStoreBf16Part, PREC, false><<<tiles * splits, kThreads, 0, stream>>>(
-        A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
-    return 0;
-  }
-  // kStoreF32 with splits > 1: partials only, the consumer reduces them (rms_norm_splitk)
-  if (splits > 1 && (workspace == nullptr || epilogue == kSwiGLU)) return -3;
-  if (splits == 1 && epilogue == kStoreF32) return -3;
-  const int grid = tiles * splits;
-  sk.n_dp = grid;
-  if (splits > 1) {
-    gemm_tile_kernel<kStoreF32, PREC, false><<<grid, kThreads, 0, stream>>>(
-        A, B, workspace, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
-    if (epilogue == kStoreF32) return 0;
-    const size_t MN = (size_t)M * N;
-    size_t blocks = (MN / 8 + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    tile_splitk_reduce_kernel<<<(int)blocks, 256, 0, stream>>>(reinterpret_cast<bf16*>(C),
-                                                               workspace, splits, MN);
-  } else if (epilogue == kSwiGLUMx) {
-    if constexpr (PREC == kFp8)
-      gemm_tile_kernel<kSwiGLUMx, PREC, false><<<grid, kThreads, 0, stream>>>(
-          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
-  } else if (epilogue == kSwiGLU) {
-    if constexpr (PREC == kFp8Mx) return -4;   // MX activations come from the SwiGLU epilogue
-    else
-      gemm_tile_kernel<kSwiGLU, PREC, false><<<grid, kThreads, 0, stream>>>(
-          A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
-  } else if (epilogue == kStoreBf16) {
-    gemm_tile_kernel<kStoreBf16, PREC, false><<<grid, kThreads, 0, stream>>>(
-        A, B, C, sa, sb, M, N, K, tiles_m, tiles_n, kps, sk, ol, mx);
-  } else {
-    return -4;
-  }
-  return 0;
+  if (weights_nt(tiles_m))
+    return launch_whole_impl<1, PREC>(C, A, B, sa, sb, workspace, M, N, K, splits, kps, epilogue, tiles, tiles_m, tiles_n, stream, ol, mx);
+  return launch_whole_impl<0, PREC>(C, A, B, sa, sb, workspace, M, N, K, splits, kps, epilogue, tiles, tiles_m, tiles_n, stream, ol, mx);
 }
+
 
 }  // namespace
 
