@@ -224,10 +224,15 @@ class IpcTransport(Transport):
             out[c.describe()] = {"issued": c.n, **dev}
         return out
 
+    fallback_from = ""   # set by make_transport when the agreed RCCL bring-up failed
+
     def describe(self) -> dict:
-        return {"transport": "IpcTransport",
-                "channels": sorted(c.describe() for c in self._ch.values()),
-                "timeout_s": self.timeout_s}
+        d = {"transport": "IpcTransport",
+             "channels": sorted(c.describe() for c in self._ch.values()),
+             "timeout_s": self.timeout_s}
+        if self.fallback_from:
+            d["fallback_from"] = self.fallback_from
+        return d
 
     def close(self) -> None:
         if not self._ch:

@@ -512,13 +512,19 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
     failed, EVERY rank raises :class:`TransportInitError` with the failing ranks and the error, so
     a multi-GPU run either moves hidden states over RCCL or exits non-zero.
     ``DLI_TRANSPORT=rccl-or-host`` restores the old agreed fallback to the host-staged transport.
+    With ``DLI_TRANSPORT`` unset (``rccl-or-ipc``) an agreed RCCL failure falls back to the IPC
+    device transport instead (same stream structure, rotating head, device-side waits; hidden
+    states cross xGMI as peer-memory copies), announced on stderr and in ``describe()`` — an
+    explicit ``DLI_TRANSPORT=rccl`` keeps the strict fail-loud behaviour.
 
     ``rank`` / ``world`` are the stage index and stage count of ONE pipeline replica; with several
     replicas (data parallel) ``rank_offset`` is the replica's first global rank and ``job`` names
     the replica, so every replica gets its own RCCL pair communicators."""
     if world == 1:
         return LoopbackTransport(1)
-    kind = os.environ.get("DLI_TRANSPORT", "rccl" if device.type == "cuda" else "gloo")
+    kind = os.environ.get("DLI_TRANSPORT", "rccl-or-ipc" if device.type == "cuda" else "gloo")
+    if kind == "rccl-or-ipc" and max_bytes <= 0:
+        kind = "rccl"   # no message size to size the IPC channels with: strict RCCL
     if device.type == "cuda" and kind == "ipc":
         from ..runtime.faults import raw_store
         from .ipc_transport import IpcTransport
@@ -529,7 +535,7 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
             raise ValueError("DLI_TRANSPORT=ipc needs the largest message size (max_bytes)")
         return IpcTransport(raw_store(), rank, world, device, streams, max_bytes, head_bytes,
                             prefix=f"dli_ipc_{job}", head_pairs=head_pairs)
-    if device.type == "cuda" and kind in ("rccl", "rccl-or-host"):
+    if device.type == "cuda" and kind in ("rccl", "rccl-or-host", "rccl-or-ipc"):
         from ..runtime.faults import raw_store
         store = raw_store()
         prefix = f"dli_rccl_{job}"
@@ -555,6 +561,17 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
                f" (device {device}, HSA_ENABLE_IPC_MODE_LEGACY="
                f"{os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '<unset>')}); errors: {errs}")
         print(msg, file=sys.stderr, flush=True)
+        if kind == "rccl-or-ipc":
+            print(f"[rank {rank}] falling back to the IPC device transport (agreed by every rank)",
+                  file=sys.stderr, flush=True)
+            from .ipc_transport import IpcTransport
+            if streams is None:
+                from ..runtime.streams import rank_streams
+                streams = rank_streams(device)
+            tr = IpcTransport(store, rank, world, device, streams, max_bytes, head_bytes,
+                              prefix=f"dli_ipc_{job}", head_pairs=head_pairs)
+            tr.fallback_from = f"RcclTransport failed on ranks {bad}"
+            return tr
         if kind != "rccl-or-host":
             raise TransportInitError(msg)
         log.warning(msg + "; DLI_TRANSPORT=rccl-or-host: falling back to host-staged transport")
@@ -562,7 +579,8 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
         return HostStagedTransport(rank_offset=rank_offset)
     if device.type == "cuda":
         if kind != "host":
-            raise ValueError(f"DLI_TRANSPORT={kind!r}: expected rccl, rccl-or-host, ipc or host")
+            raise ValueError(f"DLI_TRANSPORT={kind!r}: expected rccl, rccl-or-ipc, rccl-or-host, "
+                             "ipc or host")
         from .transport import HostStagedTransport
         return HostStagedTransport(rank_offset=rank_offset)
     return TorchDistTransport(rank_offset=rank_offset)

@@ -4,8 +4,9 @@ On a ONE-GPU box stage processes share the card (``DLI_SHARE_GPU=1``).  RCCL ref
 the same device, so there the full driver/follower GPU path (graphs, shm control plane, token
 feedback, micro-batching) runs over the host-staged transport, the RCCL binding is exercised with
 a 1-rank communicator, and the RCCL-failure path (all ranks agree, fall back together) is tested
-by asking for RCCL on a shared GPU: by default every rank fails loudly, and only the explicit
-``DLI_TRANSPORT=rccl-or-host`` opt-in falls back.  With two or more GPUs the RCCL P2P transport and a PP=2
+by asking for RCCL on a shared GPU: with an explicit ``DLI_TRANSPORT=rccl`` every rank fails
+loudly, ``DLI_TRANSPORT=rccl-or-host`` falls back to host staging, and the default (unset:
+``rccl-or-ipc``) falls back, agreed, to the IPC device transport.  With two or more GPUs the RCCL P2P transport and a PP=2
 RCCL pipeline are tested for real.
 """
 import multiprocessing as mp
@@ -47,7 +48,11 @@ def _pipeline_worker(rank, world, port, mbs, q, transport="host", rotation=None)
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_SHARE_GPU="1",
-                          DLI_TRANSPORT=transport, DLI_TUNABLEOP="0", DLI_WATCHDOG_S="60")
+                          DLI_TUNABLEOP="0", DLI_WATCHDOG_S="60")
+        if transport is None:   # the default
+            os.environ.pop("DLI_TRANSPORT", None)
+        else:
+            os.environ["DLI_TRANSPORT"] = transport
         if rotation is not None:
             os.environ["DLI_HEAD_ROTATION"] = "1" if rotation else "0"
         import torch.distributed as dist
@@ -192,8 +197,8 @@ def _run_pair(transport, timeout=600):
     return msgs, ps
 
 
-def test_rccl_failure_is_loud_by_default(gpu):
-    """Two ranks on ONE GPU with the default RCCL transport: RCCL rejects the duplicate device and
+def test_rccl_failure_is_loud_when_strict(gpu):
+    """Two ranks on ONE GPU with ``DLI_TRANSPORT=rccl``: RCCL rejects the duplicate device and
     EVERY rank must raise TransportInitError (agreed through the store: no hang, no silent
     host-staged fallback, non-zero exit codes)."""
     msgs, ps = _run_pair("rccl")
@@ -217,6 +222,23 @@ def test_rccl_failure_falls_back_with_opt_in(gpu):
     assert all(p.exitcode == 0 for p in ps)
     assert got == ref
     assert rest and rest[0] == "HostStagedTransport", rest
+
+
+def test_rccl_failure_falls_back_to_ipc_by_default(gpu):
+    """``DLI_TRANSPORT`` unset: RCCL fails on the shared GPU on both ranks, they agree and bring up
+    the IPC device transport instead (rotating head kept), producing the same tokens as PP=1."""
+    from distributed_llm_inference.runtime.engine import LLMEngine
+    from distributed_llm_inference.runtime.sequence import SamplingParams
+    os.environ["DLI_TUNABLEOP"] = "0"
+    spec, cfg = _cfg(1, 3)
+    ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
+        PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
+    msgs, ps = _run_pair(None)
+    status, got, *rest = msgs[0]
+    assert status == "ok", got
+    assert all(p.exitcode == 0 for p in ps)
+    assert got == ref
+    assert rest and rest[0] == "IpcTransport", rest
 
 
 def _rccl_worker(rank, port, q):
