@@ -58,3 +58,23 @@ for rows in (1, 64, 512):
     print(rows, res[rows], flush=True)
 os.makedirs("gpurun_out", exist_ok=True)
 json.dump(res, open("gpurun_out/sample_probe.json", "w"), indent=1)
+
+# the decode step's order: LM-head GEMM (hipBLASLt) writes the logits, the sampler reads them next
+rows, H = 512, 8192
+x = torch.randn(rows, H, device=dev, dtype=torch.bfloat16)
+w = (torch.randn(V, H, device=dev) * 0.02).to(torch.bfloat16)
+logits = torch.empty(rows, V, device=dev, dtype=torch.bfloat16)
+temp = torch.zeros(rows, device=dev)
+topk = torch.zeros(rows, dtype=torch.int32, device=dev)
+topp = torch.ones(rows, device=dev)
+seeds = torch.arange(rows, dtype=torch.int64, device=dev)
+step = torch.zeros(1, dtype=torch.int64, device=dev)
+out = torch.empty(rows, dtype=torch.int32, device=dev)
+gemm = lambda: torch.matmul(x, w.t(), out=logits)
+both = lambda: (gemm(), ops.sample(logits, temperature=temp, top_k=topk, top_p=topp, seeds=seeds,
+                                   step=step, out=out))
+t_g, t_b = timed(gemm), timed(both)
+res["after_gemm_512"] = {"gemm_us": round(t_g, 1), "gemm_plus_greedy_us": round(t_b, 1),
+                         "greedy_after_gemm_us": round(t_b - t_g, 1)}
+print("after_gemm_512", res["after_gemm_512"], flush=True)
+json.dump(res, open("gpurun_out/sample_probe.json", "w"), indent=1)
