@@ -32,7 +32,11 @@ def test_bench_multirank_json_contract(n):
            "--prompt-len", "16", "--max-batched-tokens", "64"]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
-    assert r.returncode == 0, r.stderr[-3000:]
+    if r.returncode != 0:   # the ranks' own errors first: torchrun's summary hides them
+        keys = ("Error", "error", "Traceback", "terminate", "abort", "Abort", "watchdog", "File ")
+        own = [l for l in r.stderr.splitlines() if any(k in l for k in keys)
+               and "elastic" not in l and "ChildFailedError" not in l]
+        pytest.fail("\n".join(own[-60:]) + "\n---- tail ----\n" + r.stderr[-2000:])
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
@@ -91,7 +95,11 @@ def test_bench_replicas_json_contract(n, dp):
            "--prompt-len", "16", "--max-batched-tokens", "64"]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
-    assert r.returncode == 0, r.stderr[-3000:]
+    if r.returncode != 0:   # the ranks' own errors first: torchrun's summary hides them
+        keys = ("Error", "error", "Traceback", "terminate", "abort", "Abort", "watchdog", "File ")
+        own = [l for l in r.stderr.splitlines() if any(k in l for k in keys)
+               and "elastic" not in l and "ChildFailedError" not in l]
+        pytest.fail("\n".join(own[-60:]) + "\n---- tail ----\n" + r.stderr[-2000:])
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
