@@ -546,6 +546,7 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
         except Exception as e:  # noqa: BLE001 - reported and agreed on below
             err = repr(e)
             store.set(f"{prefix}/err/{rank}", err[:2000])
+            store.set(f"{prefix}/failed", f"rank {rank}: {err[:500]}")   # peers stop early
         store.set(f"{prefix}/ok/{rank}", "1" if tr is not None else "0")
         ok = [store.get(f"{prefix}/ok/{r}") == b"1" for r in range(world)]
         if all(ok):

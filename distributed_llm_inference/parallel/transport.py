@@ -191,48 +191,43 @@ class RcclTransport(Transport):
         streams = streams or rank_streams(device)
         self.send_stream = streams.send
         self.recv_stream = streams.recv
-        self._comms: Dict[int, object] = {}
         self._rccl_version = int(C.rccl_version())
         self._timing = os.environ.get("DLI_STAGE_TIMING", "0") == "1"
         self._waits: collections.deque = collections.deque()
         dev_idx = device.index if device.index is not None else torch.cuda.current_device()
         # pair (i, i+1): the lower rank creates the id; both ends create a 2-rank communicator.
         # (sampled tokens return to the driver over the shm control plane, so no ring closure).
-        # Init order: every rank initialises its lower pair first, so the chain of blocking
-        # ncclCommInitRank calls resolves from rank 0 upwards without a cycle.
-        pairs = [(r, r + 1) for r in range(world - 1)]
-        for (a, b) in pairs:
-            if rank not in (a, b):
-                continue
-            key = f"{prefix}/{a}-{b}"
-            if rank == a:
-                uid = C.rccl_unique_id()
-                store.set(key, uid)
-            else:
-                uid = store.get(key)
-            peer = b if rank == a else a
-            self._comms[peer] = C.RcclComm(bytes(uid), 0 if rank == a else 1, 2, dev_idx,
-                                           timeout_s)
         # rotating LM head: one more 2-rank communicator between the last stage and every other
         # rank (last -> r only), separate from the stage pair so the stage traffic and the head
-        # traffic never share a communicator across streams.  Initialised after every stage pair
-        # (all ranks) in increasing r on the last rank: no cycle in the blocking inits.
-        self._hcomms: Dict[int, object] = {}
+        # traffic never share a communicator across streams.
         last = world - 1
+        plan = [("stage", a, a + 1, f"{prefix}/{a}-{a + 1}") for a in range(world - 1)]
         if head_pairs and world > 1:
-            for r in range(world - 1):
-                if rank not in (r, last):
-                    continue
-                key = f"{prefix}/h{r}"
-                if rank == last:
-                    uid = C.rccl_unique_id()
-                    store.set(key, uid)
-                else:
-                    uid = store.get(key)
-                peer = r if rank == last else last
-                # index 0 = the sender (last stage), 1 = the head rank
-                self._hcomms[peer] = C.RcclComm(bytes(uid), 0 if rank == last else 1, 2, dev_idx,
-                                                timeout_s)
+            plan += [("head", last, r, f"{prefix}/h{r}") for r in range(world - 1)]
+        plan = [e for e in plan if rank in (e[1], e[2])]
+        # 1) publish every unique id this rank owns BEFORE initialising any communicator: a rank
+        #    whose first init fails must not leave a later peer blocked on an id it never set
+        #    (with > 2 ranks that turned an RCCL failure into a hang in the store)
+        for kind, a, b, key in plan:
+            if rank == a:
+                store.set(key, C.rccl_unique_id())
+        # 2) initialise in order: every rank its lower stage pair first, the head pairs after all
+        #    stage pairs in increasing r, so the chain of blocking inits resolves from rank 0
+        #    upwards without a cycle.  A failure already published by any rank ends the bring-up
+        #    here instead of after this rank's own init deadlines.
+        self._comms: Dict[int, object] = {}
+        self._hcomms: Dict[int, object] = {}
+        fail_key = f"{prefix}/failed"
+        self._store, self._fail_key, self._timeout_s = store, fail_key, float(timeout_s)
+        for kind, a, b, key in plan:
+            if store.check([fail_key]):
+                raise RuntimeError(f"RCCL bring-up abandoned: another rank failed "
+                                   f"({store.get(fail_key).decode(errors='replace')[:200]})")
+            uid = store.get(key)
+            peer = b if rank == a else a
+            # index 0 = the pair's first member (stage: lower rank; head: the last stage)
+            comm = C.RcclComm(bytes(uid), 0 if rank == a else 1, 2, dev_idx, timeout_s)
+            (self._comms if kind == "stage" else self._hcomms)[peer] = comm
         self.connect_ms = self._connect()
 
     def _connect(self) -> float:
@@ -251,8 +246,20 @@ class RcclTransport(Transport):
                     comm.send(probe, 1, self.send_stream.cuda_stream)
                 else:
                     comm.recv(probe, 0, self.recv_stream.cuda_stream)
-            self.send_stream.synchronize()
-            self.recv_stream.synchronize()
+            # bounded wait: a peer that failed after this rank's communicators came up never
+            # posts its side, and the RCCL kernel waiting for it would spin forever; poll, watch
+            # for a published failure, and abort the communicators (their kernels exit) instead
+            evs = [torch.cuda.Event(), torch.cuda.Event()]
+            evs[0].record(self.send_stream)
+            evs[1].record(self.recv_stream)
+            deadline = time.monotonic() + self._timeout_s
+            while not all(e.query() for e in evs):
+                if self._store.check([self._fail_key]) or time.monotonic() > deadline:
+                    why = ("another rank failed" if self._store.check([self._fail_key])
+                           else f"no peer within {self._timeout_s:.0f} s")
+                    self.abort()
+                    raise RuntimeError(f"RCCL connect of rank {self.rank} abandoned: {why}")
+                time.sleep(0.005)
         return (time.perf_counter() - t0) * 1e3
 
     def _comm(self, peer: int):

@@ -1,0 +1,99 @@
+"""RCCL bring-up failure handling with more than two ranks (parallel/transport.py RcclTransport),
+simulated on the CPU: one thread per rank, a blocking in-memory store, and a fake native module
+whose 2-rank communicator init blocks until both members arrive (like ncclCommInitRank) or its
+deadline passes, and fails immediately on a chosen rank.
+
+The failure path used to hang with > 2 ranks: a rank whose first communicator init raised never
+published the unique id of its next pair, so that peer blocked in ``store.get`` forever (seen as
+a 900 s hang of an 8-rank bench on a shared GPU).  Now every rank publishes the ids it owns before
+initialising anything, and stops at the next init once any rank has published a failure."""
+import threading
+import time
+
+import pytest
+import torch
+
+from distributed_llm_inference.parallel import transport as tmod
+
+
+class _Store:
+    def __init__(self):
+        self.d, self.cv = {}, threading.Condition()
+
+    def set(self, k, v):
+        with self.cv:
+            self.d[k] = v if isinstance(v, bytes) else str(v).encode()
+            self.cv.notify_all()
+
+    def get(self, k):
+        with self.cv:
+            if not self.cv.wait_for(lambda: k in self.d, timeout=10.0):
+                raise TimeoutError(f"store.get({k!r}) blocked")   # the old hang
+            return self.d[k]
+
+    def check(self, keys):
+        with self.cv:
+            return all(k in self.d for k in keys)
+
+
+class _Native:
+    """ncclGetUniqueId / 2-rank ncclCommInitRank stand-ins."""
+
+    def __init__(self, fail_rank):
+        self.fail_rank, self.lock, self.arrived, self.n = fail_rank, threading.Lock(), {}, 0
+
+    def rccl_version(self):
+        return 22606
+
+    def rccl_unique_id(self):
+        with self.lock:
+            self.n += 1
+            return f"uid{self.n}".encode()
+
+    def RcclComm(self, uid, idx, world, dev, timeout_s):
+        me = threading.current_thread().name
+        if me == f"rank{self.fail_rank}":
+            raise RuntimeError("RCCL error: invalid usage (duplicate GPU)")
+        with self.lock:
+            ev = self.arrived.setdefault(uid, [threading.Event(), threading.Event()])
+        ev[idx].set()
+        if not ev[1 - idx].wait(timeout=min(timeout_s, 1.0)):
+            raise RuntimeError("ncclCommInitRankConfig timed out")
+        return object()
+
+
+class _Streams:
+    send = recv = None
+
+
+@pytest.mark.parametrize("world,fail_rank,head", [(4, 1, False), (8, 1, True), (8, 6, True),
+                                                   (8, 7, True), (8, 0, False)])
+def test_rccl_bringup_failure_never_blocks_peers(monkeypatch, world, fail_rank, head):
+    nat = _Native(fail_rank)
+    from distributed_llm_inference import ops
+    monkeypatch.setattr(ops, "native", lambda: nat)
+    store = _Store()
+    errs = {}
+
+    def rank_main(r):
+        try:
+            tmod.RcclTransport(store, r, world, torch.device("cuda", 0), prefix="t",
+                               timeout_s=1.0, head_pairs=head, streams=_Streams())
+            errs[r] = None
+        except Exception as e:  # noqa: BLE001
+            errs[r] = e
+            store.set("t/failed", f"rank {r}")   # what make_transport publishes
+
+    th = [threading.Thread(target=rank_main, args=(r,), name=f"rank{r}") for r in range(world)]
+    t0 = time.monotonic()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(30.0)
+    assert not any(t.is_alive() for t in th), "a rank is still blocked"
+    assert time.monotonic() - t0 < 20.0
+    assert not any(isinstance(e, TimeoutError) for e in errs.values()), errs
+    assert isinstance(errs[fail_rank], RuntimeError) and "duplicate" in str(errs[fail_rank])
+    # nobody completes a transport when a rank failed: every other rank either stopped at a
+    # published failure, timed out on the failed peer, or (CPU box) failed its CUDA connect probe
+    assert len(errs) == world
