@@ -6,7 +6,7 @@ set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 unset DLI_TRANSPORT
-DLI_SHARE_GPU=1 DLI_WATCHDOG_S=${DLI_WATCHDOG_S:-120} timeout -k 10 900 python -m torch.distributed.run \
+DLI_SHARE_GPU=1 DLI_WATCHDOG_S=${DLI_WATCHDOG_S:-120} timeout -k 10 700 python -m torch.distributed.run \
     --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29617 \
     bench.py --gpus 8 --steps 5 --warmup 2 --batch-per-mb 32 --prompt-len 256 > gpurun_out/rehearsal_pp8_default.log 2>&1
 rc=$?; grep '^{' gpurun_out/rehearsal_pp8_default.log | tail -1 > gpurun_out/rehearsal_pp8_default.json
