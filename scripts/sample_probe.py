@@ -50,11 +50,23 @@ for rows in (1, 64, 512):
     am = timed(lambda: logits.argmax(-1))
     temp2 = torch.full((rows,), 0.8, device=dev)
     topp2 = torch.full((rows,), 0.9, device=dev)
-    us_p = timed(lambda: ops.sample(logits, temperature=temp2, top_k=topk, top_p=topp2, seeds=seeds,
-                                    step=step, out=out))
+    topk2 = torch.full((rows,), 50, dtype=torch.int32, device=dev)
+    r = {}
+    toks = {}
+    for path in ("1", "0"):   # DLI_SAMPLE_REGS: register path / radix-histogram path
+        os.environ["DLI_SAMPLE_REGS"] = path
+        r[f"top_p_us_regs{path}"] = round(timed(lambda: ops.sample(
+            logits, temperature=temp2, top_k=topk, top_p=topp2, seeds=seeds, step=step, out=out)), 1)
+        r[f"top_k_top_p_us_regs{path}"] = round(timed(lambda: ops.sample(
+            logits, temperature=temp2, top_k=topk2, top_p=topp2, seeds=seeds, step=step, out=out)), 1)
+        ops.sample(logits, temperature=temp2, top_k=topk2, top_p=topp2, seeds=seeds, step=step, out=out)
+        torch.cuda.synchronize()
+        toks[path] = out.clone()
+    os.environ.pop("DLI_SAMPLE_REGS")
+    r["same_tokens_frac"] = round((toks["1"] == toks["0"]).float().mean().item(), 4)
     gb = rows * V * 2 / 1e9
     res[rows] = {"greedy_us": round(us, 1), "greedy_TBps": round(gb / us * 1e3, 2), "argmax_equal": ok,
-                 "torch_argmax_us": round(am, 1), "top_p_us": round(us_p, 1)}
+                 "torch_argmax_us": round(am, 1), **r}
     print(rows, res[rows], flush=True)
 os.makedirs("gpurun_out", exist_ok=True)
 json.dump(res, open("gpurun_out/sample_probe.json", "w"), indent=1)
