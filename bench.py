@@ -300,3 +300,16 @@ if __name__ == "__main__":
         from distributed_llm_inference.runtime.watchdog import abort_job
         abort_job(f"bench.py: {type(e).__name__}: {e}")
         raise
+    # done (rank 0's JSON line is out): leave without interpreter finalisation — daemon threads
+    # (watchdog, heartbeat, transport pollers) may still sit in C++ store / gloo calls, and tearing
+    # their objects down under them ended a finished rank with SIGABRT ("terminate called without
+    # an active exception") now and then on a loaded machine
+    try:
+        import torch
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+    except Exception:  # noqa: BLE001
+        pass
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(0)
