@@ -300,10 +300,13 @@ if __name__ == "__main__":
         from distributed_llm_inference.runtime.watchdog import abort_job
         abort_job(f"bench.py: {type(e).__name__}: {e}")
         raise
-    # done (rank 0's JSON line is out): leave without interpreter finalisation — daemon threads
-    # (watchdog, heartbeat, transport pollers) may still sit in C++ store / gloo calls, and tearing
-    # their objects down under them ended a finished rank with SIGABRT ("terminate called without
-    # an active exception") now and then on a loaded machine
+    # multi-rank runs, done (rank 0's JSON line is out): leave without interpreter finalisation —
+    # daemon threads (watchdog, heartbeat, transport pollers) may still sit in C++ store / gloo
+    # calls, and tearing their objects down under them ended a finished rank with SIGABRT
+    # ("terminate called without an active exception") now and then on a loaded machine.  A
+    # single process exits normally (a profiler's exit hooks write its trace then).
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        sys.exit(0)
     try:
         import torch
         if torch.cuda.is_initialized():
