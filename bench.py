@@ -292,6 +292,8 @@ def main():
 if __name__ == "__main__":
     try:
         main()
+    except SystemExit:   # argparse (--help, bad flags) and explicit exits: no abort broadcast
+        raise
     except BaseException as e:
         # a failed rank ends every rank promptly, each printing its last pipeline op
         # (distributed_llm_inference/runtime/watchdog.py); no-op for a single process
