@@ -158,6 +158,7 @@ struct SkArgs {
   unsigned* flags;   // [sk_wgs] publish flags, zeroed by a memset node before every launch
   unsigned* err;     // spin-timeout counter (diagnostic; tests zero it once)
   float* slabs;      // [sk_wgs][256 * 256] fp32 partials in accumulator (register) order
+  int gm = 8;        // M-tiles per group of the grouped tile order (DLI_GEMM_GM, experiments)
 };
 
 // LLM.int8 outlier columns (int8 precision only): the bf16 product x_out [M, J] . w_out [N, J]^T
@@ -274,7 +275,7 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
     // so the 32 consecutive tiles an XCD runs share 8 activation and 4 weight panels through its
     // L2 (the M tiles of one N panel stay neighbours).  Identical to M-fastest order for
     // tiles_m <= 8 (every decode shape); 8192^3: 1296 -> 1386 TF (profiles/gemm_var_nt_group_ab.json)
-    constexpr int GM = 8;
+    const int GM = sk.gm;
     const int gper = GM * tiles_n, grp = tile / gper, grem = tile % gper;
     const int gm = min(GM, tiles_m - grp * GM);
     const int tm = grp * GM + grem % gm;
@@ -730,6 +731,7 @@ int launch_whole_impl(void* C, const void* A, const void* B, const float* sa, co
                       int tiles, int tiles_m, int tiles_n, hipStream_t stream, OutlierArgs ol,
                       MxArgs mx) {
   SkArgs sk{0, 0, nullptr, nullptr, nullptr};
+  if (const char* g = getenv("DLI_GEMM_GM")) sk.gm = atoi(g) > 0 ? atoi(g) : 8;
   if (epilogue == kStoreBf16Part) {   // bf16 partials into C [splits, M, N]; the consumer sums
     if (splits < 2) return -3;
     sk.n_dp = tiles * splits;   // the block remap covers the whole grid
