@@ -682,3 +682,27 @@ def test_quant_rowwise_from_splitk_partials_bit_identical(gpu, S, rows, K, with_
     q2, s2 = ops.quant_rowwise(ops.SplitKPartials(parts), r2, w, 1e-5)
     assert torch.equal(q1.view(torch.uint8), q2.view(torch.uint8))
     assert torch.equal(s1, s2) and torch.equal(r1, r2)
+
+
+@pytest.mark.parametrize("V", [128256, 32000, 50304])
+def test_sample_register_path_matches_radix_path(gpu, V, monkeypatch):
+    """The register-resident top-k / top-p search (sampling.hip sample_row_regs) keeps the same
+    set as the radix-histogram path and draws the same Gumbel sample: identical tokens for
+    seeded rows over temperatures, top-k and top-p values (bf16 logits, V % 8 == 0)."""
+    torch.manual_seed(V)
+    B = 24
+    logits = (torch.randn(B, V, device=gpu) * torch.linspace(0.5, 6, B, device=gpu)[:, None]).to(BF)
+    t = torch.linspace(0.3, 1.5, B, device=gpu)
+    ks = torch.tensor([0, 1, 2, 5, 40, 1000, V - 1, V] * 3, dtype=torch.int32, device=gpu)
+    ps = torch.tensor([1.0, 0.9, 0.5, 0.99, 0.1, 0.7] * 4, device=gpu)
+    seeds = torch.arange(B, device=gpu) * 7919 + 3
+    ctr = torch.arange(B, device=gpu, dtype=torch.int64) + 100
+    out = {}
+    for path in ("1", "0"):
+        monkeypatch.setenv("DLI_SAMPLE_REGS", path)
+        lp = torch.empty(B, device=gpu)
+        tok = ops.sample(logits, temperature=t, top_k=ks, top_p=ps, seeds=seeds, counters=ctr,
+                         logprobs=lp)
+        out[path] = (tok.cpu(), lp.cpu())
+    assert torch.equal(out["1"][0], out["0"][0]), (out["1"][0], out["0"][0])
+    _close(out["1"][1], out["0"][1], 1e-4, 1e-4, "logprobs")
