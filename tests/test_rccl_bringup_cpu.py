@@ -97,3 +97,65 @@ def test_rccl_bringup_failure_never_blocks_peers(monkeypatch, world, fail_rank, 
     # nobody completes a transport when a rank failed: every other rank either stopped at a
     # published failure, timed out on the failed peer, or (CPU box) failed its CUDA connect probe
     assert len(errs) == world
+
+
+@pytest.mark.parametrize("env,expect", [(None, "ipc"), ("rccl-or-ipc", "ipc"), ("rccl", "raise"),
+                                        ("rccl-or-host", "host")])
+def test_make_transport_agreed_fallback(monkeypatch, env, expect):
+    """make_transport on a GPU device when RCCL fails on one rank of two: every rank agrees, and
+    the default (`rccl-or-ipc`) brings up the IPC device transport, `rccl` raises
+    TransportInitError, `rccl-or-host` falls back to host staging.  Both ranks run as threads
+    over one in-memory store; the transports are stand-ins (no GPU needed)."""
+    from distributed_llm_inference.parallel import ipc_transport, pipeline
+    from distributed_llm_inference.runtime import faults
+
+    store = _Store()
+    monkeypatch.setattr(faults, "raw_store", lambda: store)
+
+    class FakeRccl:
+        def __init__(self, store, rank, world, device, **kw):
+            if rank == 1:
+                raise RuntimeError("RCCL error: invalid usage")
+
+        def abort(self):
+            pass
+
+    class FakeIpc:
+        def __init__(self, store, rank, world, device, streams, max_bytes, head_bytes, **kw):
+            self.rank = rank
+
+    class FakeHost:
+        def __init__(self, rank_offset=0):
+            pass
+
+    monkeypatch.setattr(pipeline, "RcclTransport", FakeRccl)
+    monkeypatch.setattr(ipc_transport, "IpcTransport", FakeIpc)
+    monkeypatch.setattr(tmod, "HostStagedTransport", FakeHost)
+    if env is None:
+        monkeypatch.delenv("DLI_TRANSPORT", raising=False)
+    else:
+        monkeypatch.setenv("DLI_TRANSPORT", env)
+    res = {}
+
+    def rank_main(r):
+        try:
+            res[r] = pipeline.make_transport(r, 2, torch.device("cuda", 0), job="j",
+                                             streams=_Streams(), max_bytes=1 << 20,
+                                             head_bytes=1 << 16)
+        except Exception as e:  # noqa: BLE001
+            res[r] = e
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(20.0)
+    assert not any(t.is_alive() for t in th)
+    for r in range(2):
+        if expect == "ipc":
+            assert isinstance(res[r], FakeIpc), res
+            assert "failed on ranks [1]" in res[r].fallback_from
+        elif expect == "host":
+            assert isinstance(res[r], FakeHost), res
+        else:
+            assert isinstance(res[r], pipeline.TransportInitError), res
