@@ -21,6 +21,7 @@ namespace dli {
 namespace {
 
 constexpr int kRows = 2;
+typedef unsigned u32x4n __attribute__((ext_vector_type(4)));   // nontemporal-loadable 16 B
 constexpr int kUnroll = 4;
 
 template <int M>
@@ -88,7 +89,113 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
     }
 }
 
+// fp8 e4m3 weights [N, K] with one fp32 scale per output row: the same weight stream at half
+// the bytes.  A lane takes 16 consecutive k (one 16-B load per row), widens them to bf16 with
+// v_cvt_scalef32_pk_bf16_fp8 (exact) and accumulates with v_dot2c_f32_bf16 against the
+// activations — bf16, or (XF8) the fp8 rows + per-row scales the fused RMSNorm quantiser already
+// produced, widened the same way; the scales are applied once to the reduced sum:
+// y = wscale[n] * (xscale[m]) * sum_k x[m, k] * w8[n, k].
+template <int M, bool XF8>
+__global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __restrict__ xv_,
+                                                              const float* __restrict__ xscale,
+                                                              const uint8_t* __restrict__ W,
+                                                              const float* __restrict__ wscale,
+                                                              const bf16* __restrict__ bias,
+                                                              bf16* __restrict__ y, int N, int K) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+  const int n0 = wave * kRows;
+  if (n0 >= N) return;
+  float acc[M][kRows];
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) acc[m][r] = 0.f;
+  const uint8_t* wrow[kRows];
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(n0 + r, N - 1) * K;
+
+  constexpr int kStep = 64 * 16;  // elements per wave instruction
+  for (int k0 = lane * 16; k0 < K; k0 += kStep * kUnroll) {
+    u32x4n wv[kUnroll][kRows];
+    bf16x8 xv[kUnroll][M][2];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int k = k0 + u * kStep;
+      if (k < K) {
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+          wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(wrow[r] + k));
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          if constexpr (XF8) {
+            const uint4 xb = *reinterpret_cast<const uint4*>(
+                static_cast<const uint8_t*>(xv_) + (size_t)m * K + k);
+            xv[u][m][0] = fp8x8_to_bf16x8(uint2{xb.x, xb.y});
+            xv[u][m][1] = fp8x8_to_bf16x8(uint2{xb.z, xb.w});
+          } else {
+            const bf16* x = static_cast<const bf16*>(xv_);
+            xv[u][m][0] = *reinterpret_cast<const bf16x8*>(x + (size_t)m * K + k);
+            xv[u][m][1] = *reinterpret_cast<const bf16x8*>(x + (size_t)m * K + k + 8);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) wv[u][r] = u32x4n{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int m = 0; m < M; ++m) xv[u][m][0] = xv[u][m][1] = bf16x8{};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        const bf16x8 w0 = fp8x8_to_bf16x8(uint2{wv[u][r][0], wv[u][r][1]});
+        const bf16x8 w1 = fp8x8_to_bf16x8(uint2{wv[u][r][2], wv[u][r][3]});
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int m = 0; m < M; ++m) {
+            const bf16x2 x0 = {xv[u][m][0][2 * j], xv[u][m][0][2 * j + 1]};
+            const bf16x2 x1 = {xv[u][m][1][2 * j], xv[u][m][1][2 * j + 1]};
+            acc[m][r] = __builtin_amdgcn_fdot2_f32_bf16(x0, bf16x2{w0[2 * j], w0[2 * j + 1]},
+                                                        acc[m][r], false);
+            acc[m][r] = __builtin_amdgcn_fdot2_f32_bf16(x1, bf16x2{w1[2 * j], w1[2 * j + 1]},
+                                                        acc[m][r], false);
+          }
+      }
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const float v = wave_reduce_sum(acc[m][r]);
+      const int n = n0 + r;
+      if (lane == 0 && n < N)
+        y[(size_t)m * N + n] =
+            (bf16)(v * wscale[n] * (XF8 ? xscale[m] : 1.f) + (bias ? (float)bias[n] : 0.f));
+    }
+}
+
 }  // namespace
+
+int launch_skinny_gemm_fp8(bf16* y, const void* x, const float* xscale, const uint8_t* W,
+                           const float* wscale, const bf16* bias, int M, int N, int K,
+                           hipStream_t stream) {
+  if (M < 1 || M > 2 || K % 16 != 0 || N < 1) return -1;
+  const int waves = (N + kRows - 1) / kRows;
+  const int grid = (waves + 3) / 4;
+  const bool xf8 = xscale != nullptr;
+  if (M == 1 && xf8)
+    skinny_gemm_fp8_kernel<1, true><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+  else if (M == 1)
+    skinny_gemm_fp8_kernel<1, false><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+  else if (xf8)
+    skinny_gemm_fp8_kernel<2, true><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+  else
+    skinny_gemm_fp8_kernel<2, false><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+  return 0;
+}
 
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
                        int K, hipStream_t stream) {

@@ -102,6 +102,9 @@ int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale
 int launch_splitk_reduce(bf16* C, const float* parts, int splits, size_t MN, hipStream_t stream);
 // fp32 elements of the workspace gemm_tile needs for splits == 0 (stream-K tail) on this device
 long long gemm_tile_sk_workspace_floats();
+int launch_skinny_gemm_fp8(bf16* y, const void* x, const float* xscale, const uint8_t* W,
+                           const float* wscale, const bf16* bias, int M, int N, int K,
+                           hipStream_t stream);
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
                        int K, hipStream_t stream);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,

@@ -116,9 +116,20 @@ class Linear(nn.Module):
             if self.bias is not None:
                 y = y + self.bias
             return y
+        if (x_q is None and x is not None and x.is_cuda and x.dim() == 2
+                and 1 <= x.shape[0] <= ops.SKINNY_DISPATCH_M and x.dtype == torch.bfloat16
+                and self.in_features % 16 == 0):
+            # 1-2 row decode: fp8 weight-streaming GEMV on the bf16 rows (no quantisation pass)
+            return ops.skinny_gemm_fp8(x, self.weight_fp8, self.weight_scale, None, self.bias)
         if x_q is None:
             x_q = ops.quant_rowwise(x)
         xq, xs = x_q
+        if (xq.is_cuda and xq.dim() == 2 and 1 <= xq.shape[0] <= ops.SKINNY_DISPATCH_M
+                and self.in_features % 16 == 0):
+            # 1-2 row decode on the fused quantiser's fp8 rows: half the weight bytes of bf16
+            # streamed by the GEMV kernel (hipBLASLt's fp8 GEMM at M = 1 streamed them slower
+            # than the bf16 GEMV: Llama-3.1-70B batch-1 decode ran at the bf16 speed)
+            return ops.skinny_gemm_fp8(xq, self.weight_fp8, self.weight_scale, xs, self.bias)
         if xq.is_cuda and self.bias is None and xq.dim() == 2:
             sp = ops.tile_gemm_splits_fp8(xq.shape[0], self.out_features, self.in_features)
             if sp:  # long-K fp8 products: block-scaled MFMA tile kernel (csrc/kernels/gemm_tile.hip)

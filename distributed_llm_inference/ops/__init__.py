@@ -905,6 +905,26 @@ SKINNY_DISPATCH_M = 2   # Linear uses it up to here: measured faster than hipBLA
                         # every Llama-3-70B decode shape (5.3-6.9 vs 4.3-6.0 TB/s), slower at M = 4
 
 
+def skinny_gemm_fp8(x: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor,
+                    x_scale: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None
+                    ) -> torch.Tensor:
+    """``y = (x . w8^T) * w_scale (* x_scale)`` for 1-2 decode rows: fp8 e4m3 weights [N, K]
+    with one scale per output row, activations bf16 or fp8 with one scale per row (the fused
+    RMSNorm quantiser's output), weight-streaming GEMV (csrc/kernels/gemv.hip)."""
+    M, N = x.shape[0], w8.shape[0]
+    if not _gpu(x):
+        xf = x.float() * x_scale.reshape(-1, 1) if x_scale is not None else x.float()
+        y = (xf @ (w8.float() * w_scale.reshape(-1, 1)).t())
+        if bias is not None:
+            y = y + bias.float()
+        return y.to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    native().skinny_gemm_fp8(out, x.contiguous(),
+                             None if x_scale is None else x_scale.reshape(-1).contiguous(), w8,
+                             w_scale.reshape(-1).contiguous(), bias)
+    return out
+
+
 def skinny_gemm(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``x [M, K] @ w[N, K]^T (+ bias)`` for M <= 4 with the weight-streaming HIP kernel."""

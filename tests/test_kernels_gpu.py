@@ -706,3 +706,26 @@ def test_sample_register_path_matches_radix_path(gpu, V, monkeypatch):
         out[path] = (tok.cpu(), lp.cpu())
     assert torch.equal(out["1"][0], out["0"][0]), (out["1"][0], out["0"][0])
     _close(out["1"][1], out["0"][1], 1e-4, 1e-4, "logprobs")
+
+
+@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("fp8_act", [False, True])
+def test_skinny_gemm_fp8(gpu, M, fp8_act):
+    """fp8-weight GEMV (gemv.hip skinny_gemm_fp8_kernel) against the fp32 product of the same
+    dequantised operands: bf16 rows, or fp8 rows with per-row scales (quant_rowwise's output)."""
+    torch.manual_seed(M + 2 * fp8_act)
+    N, K = 2050, 8192
+    w = torch.randn(N, K, device=gpu) * 0.02
+    wq, ws = ops.quantize_weight_fp8(w.to(BF))
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    bias = torch.randn(N, device=gpu, dtype=BF)
+    wd = wq.float() * ws.reshape(-1, 1)
+    if fp8_act:
+        xq, xs = ops.quant_rowwise(x)
+        y = ops.skinny_gemm_fp8(xq, wq, ws, xs, bias)
+        xd = xq.float() * xs.reshape(-1, 1)
+    else:
+        y = ops.skinny_gemm_fp8(x, wq, ws, None, bias)
+        xd = x.float()
+    ref = xd @ wd.t() + bias.float()
+    _close(y.float(), ref, 2e-2, 2e-2, "skinny fp8")
