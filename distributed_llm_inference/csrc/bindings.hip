@@ -696,6 +696,28 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, optional<Tensor> bias) {
                                    cur_stream()), "skinny_gemm");
 }
 
+// int8 weights [N, K] with fp32 per-row scales [N], bf16 activations (weight-only dequantisation)
+void skinny_gemm_int8(Tensor out, Tensor x, Tensor w, Tensor wscale, optional<Tensor> bias) {
+  CHECK_IN(out); CHECK_IN(x); CHECK_IN(w); CHECK_IN(wscale);
+  CHECK_BF16(out); CHECK_BF16(x); CHECK_F32(wscale);
+  TORCH_CHECK(w.scalar_type() == at::kChar, "skinny_gemm_int8: int8 weights");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm_int8: 2-D tensors");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N && wscale.numel() == N,
+              "skinny_gemm_int8: shape mismatch");
+  TORCH_CHECK(M >= 1 && M <= 2 && K % 16 == 0, "skinny_gemm_int8: M in [1, 2], K % 16 == 0");
+  const dli::bf16* b = nullptr;
+  if (bias.has_value()) {
+    CHECK_IN(*bias); CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() == N, "skinny_gemm_int8: bias must have N entries");
+    b = bp(*bias);
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  check_rc(dli::launch_skinny_gemm_int8(bp(out), bp(x), w.data_ptr<int8_t>(),
+                                        wscale.data_ptr<float>(), b, (int)M, (int)N, (int)K,
+                                        cur_stream()), "skinny_gemm_int8");
+}
+
 // fp8 e4m3 weights [N, K] (1-byte storage), fp32 per-row scales [N]; activations bf16, or fp8
 // [M, K] with fp32 per-row scales xscale [M] (the fused RMSNorm quantiser's output)
 void skinny_gemm_fp8(Tensor out, Tensor x, optional<Tensor> xscale, Tensor w, Tensor wscale,
@@ -785,6 +807,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_reduce", &splitk_reduce, "bf16 out = sum of fp32 split-K partials [S, M, N]");
   m.def("gemm_tile_sk_workspace_floats", []() { return dli::gemm_tile_sk_workspace_floats(); },
         "fp32 workspace elements gemm_tile(splits=0) needs on the current device");
+  m.def("skinny_gemm_int8", &skinny_gemm_int8,
+        "y = (x . W8^T) * scale (+ bias), int8 weights, bf16 rows, M <= 2 (weight-streaming GEMV)",
+        py::arg("out"), py::arg("x"), py::arg("w"), py::arg("wscale"), py::arg("bias") = py::none());
   m.def("skinny_gemm_fp8", &skinny_gemm_fp8,
         "y = (x . W8^T) * scale (+ bias), fp8 e4m3 weights, M <= 2 (weight-streaming GEMV)",
         py::arg("out"), py::arg("x"), py::arg("xscale"), py::arg("w"), py::arg("wscale"),

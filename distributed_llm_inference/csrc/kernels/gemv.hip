@@ -95,7 +95,18 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
 // activations — bf16, or (XF8) the fp8 rows + per-row scales the fused RMSNorm quantiser already
 // produced, widened the same way; the scales are applied once to the reduced sum:
 // y = wscale[n] * (xscale[m]) * sum_k x[m, k] * w8[n, k].
-template <int M, bool XF8>
+// WI8: int8 weights instead (LLM.int8 mode's [N, K] int8 + per-row scale), widened exactly to bf16
+__device__ __forceinline__ bf16x8 i8x8_to_bf16x8(uint2 v) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = (bf16)(float)(int)(signed char)((v.x >> (8 * j)) & 0xFFu);
+    o[4 + j] = (bf16)(float)(int)(signed char)((v.y >> (8 * j)) & 0xFFu);
+  }
+  return o;
+}
+
+template <int M, bool XF8, bool WI8 = false>
 __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __restrict__ xv_,
                                                               const float* __restrict__ xscale,
                                                               const uint8_t* __restrict__ W,
@@ -150,8 +161,10 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
     for (int u = 0; u < kUnroll; ++u)
 #pragma unroll
       for (int r = 0; r < kRows; ++r) {
-        const bf16x8 w0 = fp8x8_to_bf16x8(uint2{wv[u][r][0], wv[u][r][1]});
-        const bf16x8 w1 = fp8x8_to_bf16x8(uint2{wv[u][r][2], wv[u][r][3]});
+        const bf16x8 w0 = WI8 ? i8x8_to_bf16x8(uint2{wv[u][r][0], wv[u][r][1]})
+                              : fp8x8_to_bf16x8(uint2{wv[u][r][0], wv[u][r][1]});
+        const bf16x8 w1 = WI8 ? i8x8_to_bf16x8(uint2{wv[u][r][2], wv[u][r][3]})
+                              : fp8x8_to_bf16x8(uint2{wv[u][r][2], wv[u][r][3]});
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -194,6 +207,19 @@ int launch_skinny_gemm_fp8(bf16* y, const void* x, const float* xscale, const ui
     skinny_gemm_fp8_kernel<2, true><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
   else
     skinny_gemm_fp8_kernel<2, false><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+  return 0;
+}
+
+int launch_skinny_gemm_int8(bf16* y, const bf16* x, const int8_t* W, const float* wscale,
+                            const bf16* bias, int M, int N, int K, hipStream_t stream) {
+  if (M < 1 || M > 2 || K % 16 != 0 || N < 1) return -1;
+  const int waves = (N + kRows - 1) / kRows;
+  const int grid = (waves + 3) / 4;
+  const uint8_t* w = reinterpret_cast<const uint8_t*>(W);
+  if (M == 1)
+    skinny_gemm_fp8_kernel<1, false, true><<<grid, 256, 0, stream>>>(x, nullptr, w, wscale, bias, y, N, K);
+  else
+    skinny_gemm_fp8_kernel<2, false, true><<<grid, 256, 0, stream>>>(x, nullptr, w, wscale, bias, y, N, K);
   return 0;
 }
 

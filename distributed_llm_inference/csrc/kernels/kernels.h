@@ -105,6 +105,8 @@ long long gemm_tile_sk_workspace_floats();
 int launch_skinny_gemm_fp8(bf16* y, const void* x, const float* xscale, const uint8_t* W,
                            const float* wscale, const bf16* bias, int M, int N, int K,
                            hipStream_t stream);
+int launch_skinny_gemm_int8(bf16* y, const bf16* x, const int8_t* W, const float* wscale,
+                            const bf16* bias, int M, int N, int K, hipStream_t stream);
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
                        int K, hipStream_t stream);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,

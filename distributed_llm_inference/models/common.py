@@ -88,6 +88,12 @@ class Linear(nn.Module):
         be None (fp8 weights only).  ``defer_reduce``: a split-K tile GEMM returns its fp32
         partials (``ops.SplitKPartials``) for an RMSNorm consumer to reduce."""
         if self.weight_int8 is not None:
+            if (x.is_cuda and x.dim() == 2 and 1 <= x.shape[0] <= ops.SKINNY_DISPATCH_M
+                    and x.dtype == torch.bfloat16 and self.in_features % 16 == 0
+                    and os.environ.get("DLI_INT8_GEMV", "1") == "1"):
+                # 1-2 row decode: int8 weight-streaming GEMV on the bf16 rows (the weights are
+                # the whole cost; bf16 activations need no outlier decomposition)
+                return ops.skinny_gemm_int8(x, self.weight_int8, self.weight_scale, self.bias)
             y = ops.llm_int8_linear(x.reshape(-1, self.in_features), self.weight_int8,
                                     self.weight_scale, self.int8_threshold,
                                     wq_t=self.weight_int8_t,

@@ -905,6 +905,22 @@ SKINNY_DISPATCH_M = 2   # Linear uses it up to here: measured faster than hipBLA
                         # every Llama-3-70B decode shape (5.3-6.9 vs 4.3-6.0 TB/s), slower at M = 4
 
 
+def skinny_gemm_int8(x: torch.Tensor, wq: torch.Tensor, w_scale: torch.Tensor,
+                     bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``y = (x . wq^T) * w_scale`` for 1-2 bf16 decode rows with LLM.int8 weights (int8 [N, K],
+    per-row scale): the weight stream at 1 byte per weight, activations kept in bf16 (no
+    activation quantisation, so no outlier split is needed: every column is exact bf16 x int8)."""
+    M, N = x.shape[0], wq.shape[0]
+    if not _gpu(x):
+        y = x.float() @ (wq.float() * w_scale.reshape(-1, 1)).t()
+        if bias is not None:
+            y = y + bias.float()
+        return y.to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    native().skinny_gemm_int8(out, x.contiguous(), wq, w_scale.reshape(-1).contiguous(), bias)
+    return out
+
+
 def skinny_gemm_fp8(x: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor,
                     x_scale: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None
                     ) -> torch.Tensor:

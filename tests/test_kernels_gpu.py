@@ -729,3 +729,17 @@ def test_skinny_gemm_fp8(gpu, M, fp8_act):
         xd = x.float()
     ref = xd @ wd.t() + bias.float()
     _close(y.float(), ref, 2e-2, 2e-2, "skinny fp8")
+
+
+@pytest.mark.parametrize("M", [1, 2])
+def test_skinny_gemm_int8(gpu, M):
+    """int8-weight GEMV (LLM.int8 weights, bf16 rows) against the fp32 product of the same
+    dequantised weights."""
+    torch.manual_seed(M)
+    N, K = 2050, 8192
+    w = torch.randn(N, K, device=gpu) * 0.02
+    wq, ws = ops.quantize_weight_int8(w)
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    y = ops.skinny_gemm_int8(x, wq, ws)
+    ref = x.float() @ (wq.float() * ws.reshape(-1, 1)).t()
+    _close(y.float(), ref, 2e-2, 2e-2, "skinny int8")
