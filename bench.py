@@ -92,7 +92,8 @@ def _rank_record(node, rank: int, window_s: float) -> dict:
     """This rank's share of the timed window (between the last two barriers): stage range,
     data-plane transport, device compute per micro-batch step, receive stalls, traffic."""
     from distributed_llm_inference.runtime.faults import snapshot_delta
-    rec = {"rank": rank, "replica": getattr(node, "replica", 0)}
+    rec = {"rank": rank, "replica": getattr(node, "replica", 0),
+           "head_rotation": bool(getattr(node, "head_rotation", False))}
     ex = getattr(node, "ex", None)
     if ex is None:   # a single-stage replica (LocalPipeline): the whole model, no transport
         exs = node.executors

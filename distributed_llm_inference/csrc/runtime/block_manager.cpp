@@ -118,6 +118,31 @@ class BlockManager {
     return true;
   }
 
+  // Undo the last reservation of n tokens: shrink the length and return the blocks the shorter
+  // sequence no longer covers to the free list (in the reverse order they were taken, so the LIFO
+  // allocation order -- and every stage's block tables -- stay what they were).  A sequence that
+  // shrinks to zero tokens is dropped, as if it had never been appended to.  With a sink window
+  // the ring slots the undone tokens wrapped onto are not restored: callers roll back before any
+  // KV is written (validation failures) or accept that the overwritten window tokens are lost.
+  void rollback(int64_t sid, int64_t n) {
+    auto it = seqs_.find(sid);
+    if (it == seqs_.end()) throw std::out_of_range("unknown sequence " + std::to_string(sid));
+    SeqState& s = it->second;
+    if (n < 0 || n > s.length) throw std::invalid_argument("rollback beyond the sequence start");
+    s.length -= n;
+    const int64_t keep = blocks_for(s.length);
+    while ((int64_t)s.blocks.size() > keep) {
+      free_.push_back(s.blocks.back());
+      s.blocks.pop_back();
+    }
+    if (s.length == 0) seqs_.erase(it);
+  }
+
+  void rollback_batch(const std::vector<int64_t>& sids, const std::vector<int64_t>& ns) {
+    if (sids.size() != ns.size()) throw std::invalid_argument("rollback_batch: size mismatch");
+    for (size_t i = sids.size(); i-- > 0;) rollback(sids[i], ns[i]);  // reverse of append order
+  }
+
   int64_t slot_of(int64_t sid, int64_t a) const {
     const SeqState& s = get(sid);
     return physical(s, logical_slot(a));
@@ -227,6 +252,8 @@ void register_block_manager(py::module_& m) {
       .def("can_append", &BlockManager::can_append)
       .def("append", &BlockManager::append)
       .def("append_batch", &BlockManager::append_batch)
+      .def("rollback", &BlockManager::rollback)
+      .def("rollback_batch", &BlockManager::rollback_batch)
       .def("slot_of", &BlockManager::slot_of)
       .def("block_table", &BlockManager::block_table)
       .def("prepare", &BlockManager::prepare, py::arg("sids"), py::arg("q_lens"),

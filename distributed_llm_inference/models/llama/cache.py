@@ -206,13 +206,35 @@ class PartialLlamaSinkCache:
 
     def reserve(self, generation_id: str, batch: int, n_new: int) -> List[int]:
         rows = self.session_rows(generation_id, batch)
-        m = self.pool.manager
-        if not m.can_append(rows, [n_new] * len(rows)):
-            raise MemoryError("KV pool exhausted: close sessions or enlarge num_blocks")
-        for r in rows:
-            m.append(r, n_new)
-        self._seen_tokens[generation_id] += n_new
+        self.reserve_rows(generation_id, rows, [n_new] * len(rows), n_new)
         return rows
+
+    def reserve_rows(self, generation_id: str, rows: Sequence[int], q_lens: Sequence[int],
+                     seen: int) -> None:
+        """All-or-nothing reservation of ``q_lens[i]`` new tokens on each of the session's rows
+        (and ``seen`` more tokens on its seen-token counter).  On pool exhaustion nothing changes
+        -- a session created for this call is dropped again -- and ``MemoryError`` is raised."""
+        m = self.pool.manager
+        if not m.append_batch(list(rows), [int(q) for q in q_lens]):
+            if self._seen_tokens.get(generation_id, 0) == 0 and not any(
+                    m.has_sequence(r) for r in rows):
+                self._sessions.pop(generation_id, None)
+                self._seen_tokens.pop(generation_id, None)
+            raise MemoryError("KV pool exhausted: close sessions or enlarge num_blocks")
+        self._seen_tokens[generation_id] += int(seen)
+
+    def unreserve_rows(self, generation_id: str, rows: Sequence[int], q_lens: Sequence[int],
+                       seen: int) -> None:
+        """Undo :meth:`reserve_rows` after a failed forward: the session is as long as before the
+        call (a session the call created disappears)."""
+        m = self.pool.manager
+        m.rollback_batch(list(rows), [int(q) for q in q_lens])
+        left = self._seen_tokens.get(generation_id, 0) - int(seen)
+        if left <= 0 and not any(m.has_sequence(r) for r in rows):
+            self._sessions.pop(generation_id, None)
+            self._seen_tokens.pop(generation_id, None)
+        else:
+            self._seen_tokens[generation_id] = left
 
     def update(self, key_states: torch.Tensor, value_states: torch.Tensor, layer_idx: int,
                cache_kwargs: Optional[Dict[str, Any]] = None) -> Tuple[torch.Tensor, torch.Tensor]:

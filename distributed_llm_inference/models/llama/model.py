@@ -160,38 +160,49 @@ class LlamaBlock(nn.Module):
             am = attention_mask[:, -T:].to(torch.bool)
         else:
             am = torch.ones(B, T, dtype=torch.bool, device=dev)
-        q_lens = am.sum(-1).tolist()
-        rows = cache.session_rows(generation_id, B)
-        m = cache.pool.manager
-        if not m.can_append(rows, q_lens):
-            raise MemoryError("KV pool exhausted")
-        for sid, q in zip(rows, q_lens):
-            m.append(sid, int(q))
-        cache._seen_tokens[generation_id] += T
-        keep = [b for b in range(B) if q_lens[b] > 0]
-        out_full = torch.zeros_like(hidden_states)
-        all_hs = None
-        if not keep:
-            return (out_full,) if not output_hidden_states else (out_full, ())
-        sids = [rows[b] for b in keep]
-        qls = [int(q_lens[b]) for b in keep]
-        meta = cache.pool.build_metadata(sids, qls)
-        if custom is not None:
-            L_max = int(meta.seq_lens.max())
-            if custom.shape[-1] < L_max:
-                raise ValueError(f"4-D attention_mask key length {custom.shape[-1]} < {L_max} "
-                                 "cached + new tokens")
-            meta.custom_mask = (custom if len(keep) == B else custom[keep]).to(dev)
+        q_lens = [int(q) for q in am.sum(-1).tolist()]
         # explicit positions override the default past_len + arange
         pos_src = position_ids if position_ids is not None else (
             cache_position.unsqueeze(0).expand(B, -1) if cache_position is not None else None)
-        if pos_src is not None:
-            # rows with no real token contribute nothing to am, so the packing order matches
-            meta.positions = pos_src.to(dev)[:, -T:][am].to(torch.int32).contiguous()
-        x = hidden_states[am].to(torch.bfloat16).contiguous()  # [T_total, H] packed
-        collect = [] if output_hidden_states else None
-        out, res = self.forward_tokens(x, meta, cache.pool, collect=collect)
-        y = ops.add(out, res)
+        if pos_src is not None and (pos_src.dim() != 2 or pos_src.shape[0] not in (1, B)
+                                    or pos_src.shape[1] < T):
+            raise ValueError(f"position_ids must be [batch={B} or 1, >= {T}], "
+                             f"got {tuple(pos_src.shape)}")
+        m = cache.pool.manager
+        # Everything that can be checked is checked before the session grows: a rejected call
+        # leaves the cache exactly as it was.
+        prev = cache._sessions.get(generation_id)
+        if prev is not None and len(prev) != B:
+            raise ValueError(f"session {generation_id!r} has batch {len(prev)}, got {B}")
+        if custom is not None:
+            past = [m.length(r) if m.has_sequence(r) else 0 for r in prev] if prev else [0] * B
+            L_max = max([p + q for p, q in zip(past, q_lens) if q > 0] + [0])
+            if custom.shape[-1] < L_max:
+                raise ValueError(f"4-D attention_mask key length {custom.shape[-1]} < {L_max} "
+                                 "cached + new tokens")
+        rows = cache.session_rows(generation_id, B)
+        cache.reserve_rows(generation_id, rows, q_lens, T)   # all or nothing, MemoryError
+        try:
+            keep = [b for b in range(B) if q_lens[b] > 0]
+            out_full = torch.zeros_like(hidden_states)
+            if not keep:
+                return (out_full,) if not output_hidden_states else (out_full, ())
+            sids = [rows[b] for b in keep]
+            qls = [q_lens[b] for b in keep]
+            meta = cache.pool.build_metadata(sids, qls)
+            if custom is not None:
+                meta.custom_mask = (custom if len(keep) == B else custom[keep]).to(dev)
+            if pos_src is not None:
+                # rows with no real token contribute nothing to am, so the packing order matches
+                meta.positions = pos_src.to(dev).expand(B, -1)[:, -T:][am].to(
+                    torch.int32).contiguous()
+            x = hidden_states[am].to(torch.bfloat16).contiguous()  # [T_total, H] packed
+            collect = [] if output_hidden_states else None
+            out, res = self.forward_tokens(x, meta, cache.pool, collect=collect)
+            y = ops.add(out, res)
+        except BaseException:
+            cache.unreserve_rows(generation_id, rows, q_lens, T)
+            raise
         out_full[am] = y.to(out_full.dtype)
         if output_hidden_states:
             all_hs = []

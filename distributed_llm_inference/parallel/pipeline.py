@@ -522,7 +522,8 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
     the replica, so every replica gets its own RCCL pair communicators."""
     if world == 1:
         return LoopbackTransport(1)
-    kind = os.environ.get("DLI_TRANSPORT", "rccl-or-ipc" if device.type == "cuda" else "gloo")
+    from .transport import transport_kind
+    kind = transport_kind(device)
     if kind == "rccl-or-ipc" and max_bytes <= 0:
         kind = "rccl"   # no message size to size the IPC channels with: strict RCCL
     if device.type == "cuda" and kind == "ipc":
@@ -578,10 +579,7 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
         log.warning(msg + "; DLI_TRANSPORT=rccl-or-host: falling back to host-staged transport")
         from .transport import HostStagedTransport
         return HostStagedTransport(rank_offset=rank_offset)
-    if device.type == "cuda":
-        if kind != "host":
-            raise ValueError(f"DLI_TRANSPORT={kind!r}: expected rccl, rccl-or-ipc, rccl-or-host, "
-                             "ipc or host")
+    if device.type == "cuda":   # kind == "host" (transport_kind validated it)
         from .transport import HostStagedTransport
         return HostStagedTransport(rank_offset=rank_offset)
     return TorchDistTransport(rank_offset=rank_offset)

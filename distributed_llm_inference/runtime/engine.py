@@ -232,8 +232,11 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     else:
         device = torch.device("cpu")
 
+    head_rotation = False
+
     def tag(obj):
         obj.replica, obj.layout, obj.drivers_group = rep, layout, drivers_group
+        obj.head_rotation = head_rotation
         return obj
 
     drivers_group = None
@@ -302,6 +305,7 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         TRACKER.enable_device_marks(device)
     # the fallback transport (agreed on by every rank) cannot carry the head: then nobody rotates
     rotate = rotate and transport.supports_head
+    head_rotation = rotate   # recorded on the returned driver / follower (bench per-rank records)
     channels = _Channels(job, srank, pp, head_rotation=rotate)
     policy = HeadPolicy(pp, rotate, ex.max_num_seqs)
     dist.barrier()
@@ -349,5 +353,5 @@ def head_rotation_wanted(cfg: EngineConfig, pp: int, device: torch.device) -> bo
     want = cfg.serve.head_rotation if env is None else env == "1"
     if not want or pp < 2:
         return False
-    kind = os.environ.get("DLI_TRANSPORT", "rccl" if device.type == "cuda" else "gloo")
-    return kind in ("rccl", "rccl-or-host", "ipc", "gloo")
+    from ..parallel.transport import HEAD_ROTATING_KINDS, transport_kind
+    return transport_kind(device) in HEAD_ROTATING_KINDS

@@ -103,33 +103,77 @@ class InferenceBackend:
 
     @torch.inference_mode()
     def _process_tasks(self, tasks: List[Task]) -> List[Any]:
-        """Pack every pending session step into one varlen forward through the block."""
+        """Pack every pending session step into one varlen forward through the block.
+
+        Several steps of one session in the same batch run in submission order: the k-th step of
+        every session goes into the k-th packed forward ("wave")."""
         blk = self.module
-        cache = self.cache
-        dev = self._device()
-        cache.bind(blk.config, blk.layer_ids, dev, torch.bfloat16)
-        m = cache.pool.manager
-        sids, qlens, xs, spans = [], [], [], []
-        for t in tasks:
-            (h,) = t.args[:1]
-            gid = t.meta["generation_id"]
-            B, T, H = h.shape
-            rows = cache.session_rows(gid, B)
-            for r in rows:
-                m.append(r, T)
-            cache._seen_tokens[gid] += T
-            spans.append((len(sids), B, T))
+        self.cache.bind(blk.config, blk.layer_ids, self._device(), torch.bfloat16)
+        results: List[Any] = [None] * len(tasks)
+        waves: List[List[int]] = []
+        count: Dict[Any, int] = {}
+        for i, t in enumerate(tasks):
+            k = count.get(t.meta.get("generation_id"), 0)
+            count[t.meta.get("generation_id")] = k + 1
+            if k == len(waves):
+                waves.append([])
+            waves[k].append(i)
+        for k, wave in enumerate(waves):
+            # a later step of a session whose earlier step failed in this batch fails too
+            failed = {tasks[i].meta.get("generation_id") for w in waves[:k] for i in w
+                      if isinstance(results[i], BaseException)}
+            for i in wave:
+                if tasks[i].meta.get("generation_id") in failed:
+                    results[i] = RuntimeError("an earlier step of this session failed")
+            wave = [i for i in wave if results[i] is None]
+            try:
+                self._run_wave(tasks, wave, results)
+            except Exception as e:  # noqa: BLE001 - the whole wave failed (reservations undone)
+                for i in wave:
+                    if results[i] is None:
+                        results[i] = e
+        return results
+
+    def _run_wave(self, tasks: List[Task], wave: List[int], results: List[Any]) -> None:
+        blk, cache, dev = self.module, self.cache, self._device()
+        # Each task reserves its rows all-or-nothing: a task that does not fit (or is malformed)
+        # fails alone and leaves its session untouched; the tasks that fit still run.  If the
+        # packed forward itself raises, every reservation of the wave is rolled back.
+        sids, qlens, xs, spans, done = [], [], [], [], []
+        for i in wave:
+            t = tasks[i]
+            try:
+                (h,) = t.args[:1]
+                gid = t.meta["generation_id"]
+                if gid is None:
+                    raise ValueError("block backends need a generation_id")
+                if h.dim() != 3:
+                    raise ValueError("hidden_states must be [batch, seq, hidden]")
+                B, T, H = h.shape
+                rows = cache.session_rows(gid, B)
+                cache.reserve_rows(gid, rows, [T] * B, T)
+            except Exception as e:  # noqa: BLE001 - delivered to this task's waiter only
+                results[i] = e
+                continue
+            done.append((gid, rows, T))
+            spans.append((i, B, T))
             sids += rows
             qlens += [T] * B
             xs.append(h.reshape(B * T, H).to(dev, torch.bfloat16))
-        meta = cache.pool.build_metadata(sids, qlens)
-        out, res = blk.forward_tokens(torch.cat(xs, 0), meta, cache.pool)
-        y = out + res
-        results, off = [], 0
-        for (_, B, T) in spans:
-            results.append((y[off: off + B * T].view(B, T, -1),))
+        if not spans:
+            return
+        try:
+            meta = cache.pool.build_metadata(sids, qlens)
+            out, res = blk.forward_tokens(torch.cat(xs, 0), meta, cache.pool)
+            y = out + res
+        except BaseException:
+            for gid, rows, T in reversed(done):
+                cache.unreserve_rows(gid, rows, [T] * len(rows), T)
+            raise
+        off = 0
+        for (i, B, T) in spans:
+            results[i] = (y[off: off + B * T].view(B, T, -1),)
             off += B * T
-        return results
 
     def submit(self, *inputs, generation_id: Optional[str] = None):
         return self.inference_pool.submit_task(*inputs, generation_id=generation_id)

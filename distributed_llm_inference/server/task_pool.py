@@ -126,9 +126,14 @@ class TaskPool:
                         res = tuple(p[j] for p in pieces)
                         t.future.set_result(res if isinstance(out, (tuple, list)) else res[0])
                 else:
+                    # a result that is an exception fails that task alone (e.g. a session whose
+                    # KV reservation did not fit); the rest of the batch completes
                     results = self.process_func(batch)
                     for t, r in zip(batch, results):
-                        t.future.set_result(r)
+                        if isinstance(r, BaseException):
+                            t.future.set_exception(r)
+                        else:
+                            t.future.set_result(r)
                 self.batches_processed += 1
                 self.tasks_processed += len(batch)
             except BaseException as e:  # deliver the failure to every waiter

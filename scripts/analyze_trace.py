@@ -54,6 +54,18 @@ def main():
     print(f"decode window: {a.steps} micro-batch steps, wall {wall/1e6:.3f} ms "
           f"({wall/1e6/a.steps:.3f} ms/step), kernel busy {total_busy/1e6:.3f} ms "
           f"({100*total_busy/wall:.1f}% of wall), kernels {len(seg)}")
+    # idle time between consecutive kernels (end of one -> start of the next; overlaps count 0)
+    gaps = []
+    end = int(seg[0]["End_Timestamp"])
+    for r in seg[1:]:
+        s = int(r["Start_Timestamp"])
+        gaps.append(max(0, s - end))
+        end = max(end, int(r["End_Timestamp"]))
+    if gaps:
+        gs = sorted(gaps)
+        print(f"inter-kernel gaps: {sum(gaps)/1e3/a.steps:.1f} us/step over {len(gaps)/a.steps:.0f} gaps/step, "
+              f"median {gs[len(gs)//2]/1e3:.2f} us, p90 {gs[int(len(gs)*0.9)]/1e3:.2f} us, "
+              f"max {gs[-1]/1e3:.1f} us")
     print(f"{'kernel':<60} {'calls/step':>10} {'us/step':>10} {'share':>7}")
     for k, v in busy.most_common():
         print(f"{k:<60} {calls[k]/a.steps:>10.1f} {v/1e3/a.steps:>10.1f} {100*v/total_busy:>6.1f}%")
