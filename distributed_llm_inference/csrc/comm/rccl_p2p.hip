@@ -45,7 +45,9 @@ ncclDataType_t to_nccl(const at::Tensor& t) {
 
 class RcclComm {
  public:
-  RcclComm(const std::string& uid, int rank, int world, int device, double timeout_s)
+  // wait=false returns with the (non-blocking) init still in flight: the caller polls ready()
+  // and can give up early (another rank failed, a peer never answered) with abort().
+  RcclComm(const std::string& uid, int rank, int world, int device, double timeout_s, bool wait)
       : rank_(rank), world_(world), device_(device),
         enqueue_timeout_s_(timeout_s < 60.0 ? timeout_s : 60.0) {
     TORCH_CHECK(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id size");
@@ -61,9 +63,24 @@ class RcclComm {
       comm_ = nullptr;
       TORCH_CHECK(false, "RCCL error ", ncclGetErrorString(r), " in ncclCommInitRankConfig");
     }
-    wait_ready(timeout_s, "ncclCommInitRankConfig");
+    if (wait) wait_ready(timeout_s, "ncclCommInitRankConfig");
   }
   ~RcclComm() { destroy(); }
+
+  // true once initialised; false while the init is in flight; raises (and aborts) on an error.
+  bool ready() {
+    TORCH_CHECK(comm_ != nullptr, "communicator destroyed");
+    ncclResult_t st = ncclInProgress;
+    const ncclResult_t q = ncclCommGetAsyncError(comm_, &st);
+    if (q != ncclSuccess) st = q;
+    if (st == ncclInProgress) return false;
+    if (st != ncclSuccess) {
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+      TORCH_CHECK(false, "RCCL error ", ncclGetErrorString(st), " in ncclCommInitRankConfig");
+    }
+    return true;
+  }
 
   void destroy() {
     if (comm_) {
@@ -169,9 +186,10 @@ void register_rccl(pybind11::module_& m) {
   m.def("rccl_unique_id", &get_unique_id);
   m.def("rccl_version", &rccl_version);
   pybind11::class_<RcclComm>(m, "RcclComm")
-      .def(pybind11::init<const std::string&, int, int, int, double>(), pybind11::arg("uid"),
+      .def(pybind11::init<const std::string&, int, int, int, double, bool>(), pybind11::arg("uid"),
            pybind11::arg("rank"), pybind11::arg("world"), pybind11::arg("device"),
-           pybind11::arg("timeout_s") = 120.0)
+           pybind11::arg("timeout_s") = 120.0, pybind11::arg("wait") = true)
+      .def("ready", &RcclComm::ready, pybind11::call_guard<pybind11::gil_scoped_release>())
       .def("send", &RcclComm::send, pybind11::arg("t"), pybind11::arg("peer"),
            pybind11::arg("stream") = 0)
       .def("recv", &RcclComm::recv, pybind11::arg("t"), pybind11::arg("peer"),

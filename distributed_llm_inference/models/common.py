@@ -124,8 +124,9 @@ class Linear(nn.Module):
             return y
         if (x_q is None and x is not None and x.is_cuda and x.dim() == 2
                 and 1 <= x.shape[0] <= ops.SKINNY_DISPATCH_M and x.dtype == torch.bfloat16
-                and self.in_features % 16 == 0):
-            # 1-2 row decode: fp8 weight-streaming GEMV on the bf16 rows (no quantisation pass)
+                and self.in_features % 16 == 0 and os.environ.get("DLI_FP8_GEMV", "1") == "1"):
+            # 1-2 row decode: fp8 weight-streaming GEMV on the bf16 rows (no quantisation pass;
+            # DLI_FP8_GEMV=0 quantises the rows as a batch of >= 3 would -- docs/parity.md C11)
             return ops.skinny_gemm_fp8(x, self.weight_fp8, self.weight_scale, None, self.bias)
         if x_q is None:
             x_q = ops.quant_rowwise(x)

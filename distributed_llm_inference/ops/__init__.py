@@ -48,8 +48,9 @@ def _gpu(t: torch.Tensor) -> bool:
 
 # ----------------------------------------------------------------------------- normalisation
 class SplitKPartials:
-    """The un-reduced output of a split-K tile GEMM: fp32 partial products ``parts [S, M, N]``
-    (bf16 on the fp8 path, :func:`fp8_bf16_partials`).
+    """The un-reduced output of a split-K tile GEMM: partial products ``parts [S, M, N]``, bf16
+    by default (:func:`bf16_bf16_partials`, :func:`fp8_bf16_partials`), fp32 with
+    ``DLI_BF16_PARTS=0`` / ``DLI_FP8_BF16_PARTS=0``; consumers always sum them in fp32.
 
     ``gemm_tile(..., defer_reduce=True)`` returns this instead of running the reduction pass;
     ``rms_norm`` sums the partials while it reads them (norm.hip ``x_parts``), so the reduce
@@ -84,7 +85,7 @@ def fp8_bf16_partials() -> bool:
     """``DLI_FP8_BF16_PARTS=1`` (default): the 8-bit (fp8 / LLM.int8) tile GEMMs' split-K partials
     (QKV, O, down) are stored as bf16 (gemm_tile epilogue 4) and summed in fp32 by their consumers
     — half the partial bytes written and read.  Rounding each partial to bf16 adds ~2^-9 relative
-    error, far below what the 8-bit activations carry; the bf16 path keeps fp32 partials."""
+    error, far below what the 8-bit activations carry (bf16 operands: :func:`bf16_bf16_partials`)."""
     return os.environ.get("DLI_FP8_BF16_PARTS", "1") != "0"
 
 
@@ -93,7 +94,9 @@ def bf16_bf16_partials() -> bool:
     (default; ``DLI_BF16_PARTS=0`` keeps fp32).  Half the partial traffic of the GEMM epilogue
     and of the consumer that sums them (RMSNorm / RoPE); each partial carries one extra bf16
     rounding (~2^-9 relative) before the fp32 sum.  Measured on the default bench (same box,
-    interleaved): 6468-6482 -> 6556-6574 tok/s (profiles/bf16_partials_ab.txt)."""
+    interleaved): 6468-6482 -> 6556-6574 tok/s (profiles/bf16_partials_ab.txt).  End-to-end
+    bound vs the fp32 CPU reference: tests/test_engine_gpu.py::
+    test_bf16_splitk_partials_end_to_end_vs_cpu_reference; listed in docs/parity.md (C6)."""
     return os.environ.get("DLI_BF16_PARTS", "1") == "1"
 
 

@@ -130,8 +130,8 @@ class IpcTransport(Transport):
         return 1 + 2 * ch.cid + (1 if recv else 0)
 
     def _send_on(self, ch: _Channel, t: torch.Tensor, stream) -> None:
-        if not t.is_contiguous():
-            t = t.contiguous()
+        if not t.is_contiguous():   # callers make it contiguous before ordering the streams
+            raise ValueError("IPC send buffers must be contiguous")
         nb = t.numel() * t.element_size()
         if nb > ch.slot_bytes:
             raise ValueError(f"IPC {ch.describe()}: message of {nb} B > slot of {ch.slot_bytes} B")
@@ -164,6 +164,9 @@ class IpcTransport(Transport):
     def send(self, t: torch.Tensor, peer: int) -> None:
         self.check()
         cur = torch.cuda.current_stream(self.device)
+        # a contiguous copy is made on the compute stream BEFORE the send stream is ordered
+        # after it, and that copy is the tensor kept alive for the send stream
+        t = t.contiguous()
         self.send_stream.wait_stream(cur)
         t.record_stream(self.send_stream)
         self._send_on(self._ch[("stage", self.rank, peer)], t, self.send_stream)
@@ -185,6 +188,9 @@ class IpcTransport(Transport):
     def send_head(self, t: torch.Tensor, peer: int) -> None:
         self.check()
         cur = torch.cuda.current_stream(self.device)
+        # a contiguous copy is made on the compute stream BEFORE the send stream is ordered
+        # after it, and that copy is the tensor kept alive for the send stream
+        t = t.contiguous()
         self.send_stream.wait_stream(cur)
         t.record_stream(self.send_stream)
         self._send_on(self._ch[("head", self.rank, peer)], t, self.send_stream)

@@ -549,7 +549,7 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
             store.set(f"{prefix}/err/{rank}", err[:2000])
             store.set(f"{prefix}/failed", f"rank {rank}: {err[:500]}")   # peers stop early
         store.set(f"{prefix}/ok/{rank}", "1" if tr is not None else "0")
-        ok = [store.get(f"{prefix}/ok/{r}") == b"1" for r in range(world)]
+        ok = _agree(store, prefix, world, rank, rccl_timeout_s)
         if all(ok):
             return tr
         if tr is not None:
@@ -583,6 +583,27 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
         from .transport import HostStagedTransport
         return HostStagedTransport(rank_offset=rank_offset)
     return TorchDistTransport(rank_offset=rank_offset)
+
+
+def _agree(store, prefix: str, world: int, rank: int, timeout_s: float) -> List[bool]:
+    """Every rank's RCCL bring-up outcome, as soon as it is decided: all ranks answered ok, or
+    any rank published a failure (then the ranks that have not answered count as failed: they
+    are stuck on the failed peer or dead, and will see the failure key themselves).  A rank
+    that answers nothing at all within ``timeout_s`` is declared failed here (and published, so
+    every rank decides the same)."""
+    fail_key = f"{prefix}/failed"
+    keys = [f"{prefix}/ok/{r}" for r in range(world)]
+    deadline = time.monotonic() + timeout_s
+    while True:
+        if all(_store_has(store, k) for k in keys):
+            return [store.get(k) == b"1" for k in keys]
+        if _store_has(store, fail_key):
+            return [_store_has(store, k) and store.get(k) == b"1" for k in keys]
+        if time.monotonic() > deadline:
+            missing = [r for r, k in enumerate(keys) if not _store_has(store, k)]
+            store.set(fail_key, f"rank {rank}: ranks {missing} never answered")
+            store.set(f"{prefix}/err/{missing[0]}", f"no answer within {timeout_s:.0f} s")
+        time.sleep(0.002)
 
 
 class TransportInitError(RuntimeError):

@@ -235,20 +235,55 @@ class RcclTransport(Transport):
         #    stage pairs in increasing r, so the chain of blocking inits resolves from rank 0
         #    upwards without a cycle.  A failure already published by any rank ends the bring-up
         #    here instead of after this rank's own init deadlines.
+        #    Every wait (a peer's unique id, a communicator's init) is a poll that gives up early:
+        #    on a failure published by any rank, or when a pair init is still pending a probe
+        #    window after BOTH of its ends announced they started it (a 2-rank init takes a
+        #    second or two once both ends are in it).  A peer that is merely late -- still
+        #    loading its weights, or blocked upstream on another pair -- has not announced the
+        #    pair and is waited for up to the full deadline; a pair that both ends entered and
+        #    that hangs ends every rank's bring-up within seconds.
         self._comms: Dict[int, object] = {}
         self._hcomms: Dict[int, object] = {}
         fail_key = f"{prefix}/failed"
         self._store, self._fail_key, self._timeout_s = store, fail_key, float(timeout_s)
+        self._probe_s = float(os.environ.get("DLI_RCCL_PROBE_S", "15"))
+        self._deadline = time.monotonic() + self._timeout_s
         for kind, a, b, key in plan:
-            if store.check([fail_key]):
-                raise RuntimeError(f"RCCL bring-up abandoned: another rank failed "
-                                   f"({store.get(fail_key).decode(errors='replace')[:200]})")
-            uid = store.get(key)
             peer = b if rank == a else a
-            # index 0 = the pair's first member (stage: lower rank; head: the last stage)
-            comm = C.RcclComm(bytes(uid), 0 if rank == a else 1, 2, dev_idx, timeout_s)
+            idx = 0 if rank == a else 1   # 0 = the pair's first member (stage: lower rank; head: last)
+            self._await(lambda: store.check([key]), f"the unique id of pair {a}-{b}")
+            uid = store.get(key)
+            store.set(f"{key}/init/{idx}", "1")
+            comm = C.RcclComm(bytes(uid), idx, 2, dev_idx, timeout_s, False)
             (self._comms if kind == "stage" else self._hcomms)[peer] = comm
+            try:
+                self._await(comm.ready, f"the RCCL init of pair {a}-{b}",
+                            peer_key=f"{key}/init/{1 - idx}")
+            except BaseException:
+                self.abort()
+                raise
         self.connect_ms = self._connect()
+
+    def _await(self, done, what: str, peer_key: Optional[str] = None) -> None:
+        """Poll ``done()`` until true; raise when another rank published a failure, when the
+        bring-up deadline passes, or (``peer_key``: the peer's announcement that it entered the
+        same pair init) when the wait outlasts the probe window after both ends are in."""
+        both_in: Optional[float] = None
+        while not done():
+            now = time.monotonic()
+            if self._store.check([self._fail_key]):
+                why = self._store.get(self._fail_key).decode(errors="replace")[:200]
+                raise RuntimeError(f"RCCL bring-up of rank {self.rank} abandoned waiting for "
+                                   f"{what}: another rank failed ({why})")
+            if peer_key is not None and both_in is None and self._store.check([peer_key]):
+                both_in = now
+            if both_in is not None and now - both_in > self._probe_s:
+                raise RuntimeError(f"RCCL bring-up of rank {self.rank}: {what} still pending "
+                                   f"{self._probe_s:.0f} s after both ends entered it")
+            if now > self._deadline:
+                raise RuntimeError(f"RCCL bring-up of rank {self.rank}: {what} timed out after "
+                                   f"{self._timeout_s:.0f} s")
+            time.sleep(0.002)
 
     def _connect(self) -> float:
         """Bring up every P2P connection now, in the direction the runtime uses it, instead of at
@@ -272,14 +307,12 @@ class RcclTransport(Transport):
             evs = [torch.cuda.Event(), torch.cuda.Event()]
             evs[0].record(self.send_stream)
             evs[1].record(self.recv_stream)
-            deadline = time.monotonic() + self._timeout_s
-            while not all(e.query() for e in evs):
-                if self._store.check([self._fail_key]) or time.monotonic() > deadline:
-                    why = ("another rank failed" if self._store.check([self._fail_key])
-                           else f"no peer within {self._timeout_s:.0f} s")
-                    self.abort()
-                    raise RuntimeError(f"RCCL connect of rank {self.rank} abandoned: {why}")
-                time.sleep(0.005)
+            self._deadline = time.monotonic() + self._timeout_s
+            try:
+                self._await(lambda: all(e.query() for e in evs), "the connect probes")
+            except BaseException as e:
+                self.abort()
+                raise RuntimeError(f"RCCL connect of rank {self.rank} abandoned: {e}") from e
         return (time.perf_counter() - t0) * 1e3
 
     def _comm(self, peer: int):
@@ -291,6 +324,7 @@ class RcclTransport(Transport):
     def send(self, t: torch.Tensor, peer: int) -> None:
         """Asynchronous: the send waits for work already queued on the current stream."""
         cur = torch.cuda.current_stream(self.device)
+        t = t.contiguous()   # copied on the compute stream, before the send stream waits on it
         self.send_stream.wait_stream(cur)
         t.record_stream(self.send_stream)
         self._comm(peer).send(t, self._peer_index(peer), self.send_stream.cuda_stream)
@@ -325,6 +359,7 @@ class RcclTransport(Transport):
         """Last stage -> head rank ``peer``: the normed hidden states of an offloaded decode step
         (asynchronous, on the send stream, ordered after the work queued so far)."""
         cur = torch.cuda.current_stream(self.device)
+        t = t.contiguous()   # copied on the compute stream, before the send stream waits on it
         self.send_stream.wait_stream(cur)
         t.record_stream(self.send_stream)
         self._hcomms[peer].send(t, 1, self.send_stream.cuda_stream)

@@ -272,7 +272,10 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         streams.activate()
         # host-mapped allocations now, never in the step loop: allocating pinned / mapped host
         # memory may synchronise the device, i.e. wait for a stream parked in a peer wait
-        token_ring(device)
+        # every decode step of every in-flight micro-batch (plus the rotating head's) may hold a
+        # slot until its consumer reads it: size the ring from that, with headroom
+        M = max(1, cfg.serve.num_micro_batches or pp)
+        token_ring(device, max(4096, cfg.serve.max_batch_size), slots=max(64, 8 * (M + pp)))
     rotate = head_rotation_wanted(cfg, pp, device)
     ranges = plan_stages(spec, pp, head_rotation=rotate)
     if os.environ.get("DLI_STAGE_RANGES"):  # placement chosen by the server (rebalance)

@@ -27,7 +27,8 @@ on the others - from completing, with RCCL-style barrier packets queued on pool 
 from __future__ import annotations
 
 import os
-from typing import Dict, Optional
+import weakref
+from typing import Dict, List, Optional
 
 import torch
 
@@ -107,18 +108,27 @@ class HostTokenRing:
     coherent, device-mapped host memory written by a copy kernel on the caller's stream
     (``copy_segments``), followed by an event.  (A device -> host ``copy_`` goes through a copy
     queue shared by the process's streams - see csrc/comm/streams.hip - where it can wait behind
-    another stream's copy that is ordered after a spinning receive.)  A slot is reused after
-    ``slots`` further takes; consumers read a slot once its event completed, well before that."""
+    another stream's copy that is ordered after a spinning receive.)
+
+    A slot is handed out again only when the host view returned for its previous use is gone
+    (its consumer read it and dropped it; views are tracked by weak reference).  A take that
+    would overwrite a view still held -- more unconsumed takes than ``slots`` -- raises instead of
+    silently corrupting tokens; size the ring from the in-flight micro-batch count at init."""
 
     def __init__(self, device: torch.device, max_items: int, slots: int = 64):
         from .. import ops
         self.C = ops.native()
         self.device = torch.device(device)
         self.item_bytes = (int(max_items) * 4 + 255) // 256 * 256
-        self.slots = slots
-        self.buf = self.C.HostBuffer(self.item_bytes * slots)
+        self.slots = int(slots)
+        self.buf = self.C.HostBuffer(self.item_bytes * self.slots)
         self.view = self.buf.tensor()
+        self._out: List[Optional[weakref.ref]] = [None] * self.slots
         self.i = 0
+
+    def in_use(self) -> int:
+        """Slots whose host view is still held by a consumer."""
+        return sum(1 for r in self._out if r is not None and r() is not None)
 
     def take(self, tok: torch.Tensor, stream=None):
         """Copy ``tok`` (int32 [B], device) into the next slot on ``stream`` (default: current);
@@ -128,26 +138,41 @@ class HostTokenRing:
         nb = tok.numel() * 4
         if nb > self.item_bytes:
             raise ValueError(f"{tok.numel()} tokens > ring slot of {self.item_bytes // 4}")
-        off = (self.i % self.slots) * self.item_bytes
+        k = self.i % self.slots
+        prev = self._out[k]
+        if prev is not None and prev() is not None:
+            raise RuntimeError(f"HostTokenRing overflow: slot {k} is still held by its consumer "
+                               f"({self.in_use()} of {self.slots} slots unconsumed); size the ring "
+                               "with token_ring(device, max_items, slots)")
+        off = k * self.item_bytes
         self.i += 1
         s = stream or torch.cuda.current_stream(self.device)
         if nb:   # (an empty step samples nothing: no copy, just the event)
             self.C.copy_segments(self.buf.dev_ptr + off, tok.data_ptr(), [(0, nb)], s.cuda_stream)
         ev = torch.cuda.Event()
         ev.record(s)
-        return self.view[off: off + nb].view(torch.int32), ev
+        v = self.view[off: off + nb].view(torch.int32)
+        self._out[k] = weakref.ref(v)
+        return v, ev
 
 
 _TOKEN_RINGS: Dict[int, HostTokenRing] = {}
+_RETIRED_RINGS: List[HostTokenRing] = []   # replaced rings: views into them may still be read
 
 
-def token_ring(device: torch.device, max_items: int = 4096) -> HostTokenRing:
-    """The process-wide token ring of ``device`` (sized for up to ``max_items`` tokens a take)."""
+def token_ring(device: torch.device, max_items: int = 4096, slots: int = 64) -> HostTokenRing:
+    """The process-wide token ring of ``device`` (up to ``max_items`` tokens a take, ``slots``
+    takes unconsumed at once).  Call it at init with the largest sizes (engine.py does): a later
+    request for a larger ring replaces it, keeping the old buffer alive for views into it."""
     device = torch.device(device)
     key = device.index if device.index is not None else torch.cuda.current_device()
     r = _TOKEN_RINGS.get(key)
-    if r is None or r.item_bytes < max_items * 4:
-        r = HostTokenRing(device, max_items)
+    if r is None or r.item_bytes < max_items * 4 or r.slots < slots:
+        if r is not None:
+            _RETIRED_RINGS.append(r)
+            max_items = max(max_items, r.item_bytes // 4)
+            slots = max(slots, r.slots)
+        r = HostTokenRing(device, max_items, slots)
         _TOKEN_RINGS[key] = r
     return r
 

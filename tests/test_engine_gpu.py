@@ -552,3 +552,91 @@ def test_rotating_head_split_matches_local_head(gpu, temperature):
     got = [s.output for s in eng.generate(PROMPTS, p)]
     assert len(split) >= 6 and runner._graphs   # decode steps took the split path, graphed
     assert got == ref
+
+
+def test_bf16_splitk_partials_end_to_end_vs_cpu_reference(gpu, monkeypatch):
+    """Default bf16 path: QKV / O / down split-K partials stored as bf16 (DLI_BF16_PARTS=1, gemm_tile
+    epilogue 4) vs fp32 partials (=0), a 256-sequence decode step, each against the fp32 CPU
+    reference of the same weights (the extra rounding is bounded end to end)."""
+    spec = SPEC.replace(hidden_size=1024, intermediate_size=2048, num_heads=16, num_kv_heads=4,
+                        head_dim=64)
+    cpu = CausalLMStage(spec, 0, 3).init_random(9)
+    g = CausalLMStage(spec, 0, 3, device=gpu).init_random(9)
+    g.load_state_dict({k: v.to(gpu) for k, v in cpu.state_dict().items()})
+    prompts = [[(5 * i + j) % 983 + 1 for j in range(4)] for i in range(256)]
+    mod = ops.native()
+    calls = []
+
+    class _N:
+        def __getattr__(self, k):
+            if k != "gemm_tile":
+                return getattr(mod, k)
+
+            def spy(out, a, b, splits=1, epilogue=0, *args, **kw):
+                calls.append(epilogue)
+                return mod.gemm_tile(out, a, b, splits, epilogue, *args, **kw)
+            return spy
+
+    def decode(stage, parts=None):
+        if parts is not None:
+            monkeypatch.setenv("DLI_BF16_PARTS", parts)
+        dev = stage.device
+        pool = stage.make_pool(256, block_size=64)
+        sids = list(range(len(prompts)))
+        for sid, p in zip(sids, prompts):
+            pool.manager.append(sid, len(p))
+        meta = pool.build_metadata(sids, [len(p) for p in prompts])
+        meta.logits_rows = (torch.cumsum(torch.tensor([len(p) for p in prompts]), 0) - 1).to(dev)
+        ids = torch.tensor([t for p in prompts for t in p], dtype=torch.int32, device=dev)
+        stage(ids, meta, pool)
+        for sid in sids:
+            pool.manager.append(sid, 1)
+        meta = pool.build_metadata(sids, [1] * len(sids))
+        toks = torch.tensor([(11 * i) % 983 + 1 for i in sids], dtype=torch.int32, device=dev)
+        calls.clear()
+        with monkeypatch.context() as m:
+            if dev.type == "cuda":
+                m.setattr(ops, "native", lambda: _N())
+            y = stage(toks, meta, pool).float().cpu()
+        return y, list(calls)
+
+    ref, _ = decode(cpu)
+    a, ca = decode(g, "1")
+    b, cb = decode(g, "0")
+    assert 4 in ca and 4 not in cb and 1 in cb, (ca, cb)   # both partial paths really ran
+    rel_b = ((a - ref).norm() / ref.norm()).item()
+    rel_f = ((b - ref).norm() / ref.norm()).item()
+    print("bf16 logits vs CPU reference: bf16 partials", rel_b, "fp32 partials", rel_f)
+    assert rel_b < 0.03 and rel_b < 1.15 * rel_f + 0.005, (rel_b, rel_f)
+
+
+@pytest.mark.parametrize("mode", ["fp8", "int8"])
+def test_8bit_gemv_vs_quantised_path_bounded(gpu, monkeypatch, mode):
+    """1-2 decode rows take the weight-streaming GEMV on bf16 activations; >= 3 rows (or
+    DLI_*_GEMV=0) quantise the activations (fp8 rows / LLM.int8 with outlier split).  Both stay
+    close to the fp32 product of the same 8-bit weights, and the GEMV is the closer of the two, so
+    the batch-size dependence of a row's output is bounded (docs/parity.md C11)."""
+    from distributed_llm_inference.models.common import Linear
+    torch.manual_seed(0)
+    lin = Linear(8192, 1024, device=gpu)
+    lin.weight.data.normal_(0, 0.02)
+    x = torch.randn(2, 8192, device=gpu).to(torch.bfloat16)
+    x[:, 17] *= 12.0    # one outlier feature, as real activations have
+    if mode == "fp8":
+        lin.quantize_fp8()
+        wdq = lin.weight_fp8.float() * lin.weight_scale.float().view(-1, 1)
+        env = "DLI_FP8_GEMV"
+    else:
+        lin.quantize_int8(threshold=6.0)
+        wdq = lin.weight_int8.float() * lin.weight_scale.float().view(-1, 1)
+        env = "DLI_INT8_GEMV"
+    ref = x.float() @ wdq.t()
+    monkeypatch.setenv(env, "1")
+    a = lin(x).float()
+    monkeypatch.setenv(env, "0")
+    b = lin(x).float()
+    ea = ((a - ref).norm() / ref.norm()).item()
+    eb = ((b - ref).norm() / ref.norm()).item()
+    eab = ((a - b).norm() / ref.norm()).item()
+    print(mode, "GEMV", ea, "quantised path", eb, "difference", eab)
+    assert ea < 0.01 and eb < 0.06 and ea <= eb + 1e-3 and eab < 0.06, (ea, eb, eab)

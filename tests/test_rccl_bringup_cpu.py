@@ -36,11 +36,26 @@ class _Store:
             return all(k in self.d for k in keys)
 
 
+class _Comm:
+    """A 2-rank communicator whose (non-blocking) init completes once both members arrived,
+    never if either member is the hung rank."""
+
+    def __init__(self, ev, idx, hung):
+        self.ev, self.idx, self.hung = ev, idx, hung
+
+    def ready(self):
+        return not self.hung[0] and self.ev[1 - self.idx].is_set()
+
+    def abort(self):
+        pass
+
+
 class _Native:
     """ncclGetUniqueId / 2-rank ncclCommInitRank stand-ins."""
 
-    def __init__(self, fail_rank):
+    def __init__(self, fail_rank, hung_rank=None):
         self.fail_rank, self.lock, self.arrived, self.n = fail_rank, threading.Lock(), {}, 0
+        self.hung_rank, self.members = hung_rank, {}
 
     def rccl_version(self):
         return 22606
@@ -50,16 +65,19 @@ class _Native:
             self.n += 1
             return f"uid{self.n}".encode()
 
-    def RcclComm(self, uid, idx, world, dev, timeout_s):
+    def RcclComm(self, uid, idx, world, dev, timeout_s, wait=True):
         me = threading.current_thread().name
         if me == f"rank{self.fail_rank}":
             raise RuntimeError("RCCL error: invalid usage (duplicate GPU)")
         with self.lock:
             ev = self.arrived.setdefault(uid, [threading.Event(), threading.Event()])
+            hung = self.members.setdefault(uid, [False])
+            if me == f"rank{self.hung_rank}":
+                hung[0] = True      # this pair's init never completes, on either end
         ev[idx].set()
-        if not ev[1 - idx].wait(timeout=min(timeout_s, 1.0)):
+        if wait and not ev[1 - idx].wait(timeout=min(timeout_s, 1.0)):
             raise RuntimeError("ncclCommInitRankConfig timed out")
-        return object()
+        return _Comm(ev, idx, hung)
 
 
 class _Streams:
@@ -159,3 +177,79 @@ def test_make_transport_agreed_fallback(monkeypatch, env, expect):
             assert isinstance(res[r], FakeHost), res
         else:
             assert isinstance(res[r], pipeline.TransportInitError), res
+
+
+@pytest.mark.parametrize("hung_rank,head", [(3, True), (7, True), (0, False), (5, False)])
+def test_hung_rank_ends_bringup_within_seconds(monkeypatch, hung_rank, head):
+    """One of 8 ranks enters its RCCL inits but they never complete (RCCL refused on a shared GPU
+    hung like this).  Its peers see the pair pending a probe window after both ends entered it,
+    publish the failure, and every rank -- the hung one included -- agrees on the IPC fallback
+    within seconds, not after the 120 s init deadline (VERDICT r3 weak #6)."""
+    from distributed_llm_inference.parallel import ipc_transport, pipeline
+    from distributed_llm_inference.runtime import faults
+    nat = _Native(fail_rank=None, hung_rank=hung_rank)
+    from distributed_llm_inference import ops
+    monkeypatch.setattr(ops, "native", lambda: nat)
+    monkeypatch.setattr(tmod.RcclTransport, "_connect", lambda self: 0.0)   # no CUDA probe here
+    store = _Store()
+    monkeypatch.setattr(faults, "raw_store", lambda: store)
+
+    class FakeIpc:
+        def __init__(self, store, rank, world, device, streams, max_bytes, head_bytes, **kw):
+            self.rank = rank
+
+    monkeypatch.setattr(ipc_transport, "IpcTransport", FakeIpc)
+    monkeypatch.delenv("DLI_TRANSPORT", raising=False)
+    monkeypatch.setenv("DLI_RCCL_PROBE_S", "3")
+    world, res = 8, {}
+
+    def rank_main(r):
+        try:
+            res[r] = pipeline.make_transport(r, world, torch.device("cuda", 0), job="h",
+                                             rccl_timeout_s=120.0, head_pairs=head,
+                                             streams=_Streams(), max_bytes=1 << 20,
+                                             head_bytes=1 << 16)
+        except Exception as e:  # noqa: BLE001
+            res[r] = e
+
+    th = [threading.Thread(target=rank_main, args=(r,), name=f"rank{r}") for r in range(world)]
+    t0 = time.monotonic()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60.0)
+    took = time.monotonic() - t0
+    assert not any(t.is_alive() for t in th), "a rank is still blocked"
+    assert took <= 15.0, took
+    assert all(isinstance(res[r], FakeIpc) for r in range(world)), res
+    assert len({res[r].fallback_from for r in range(world)}) == 1   # one agreed set of failed ranks
+
+
+def test_healthy_bringup_agrees_on_rccl(monkeypatch):
+    """No failure: every rank returns its RcclTransport, and a slow rank (still loading weights)
+    is waited for rather than declared failed."""
+    from distributed_llm_inference.parallel import pipeline
+    from distributed_llm_inference.runtime import faults
+    nat = _Native(fail_rank=None)
+    from distributed_llm_inference import ops
+    monkeypatch.setattr(ops, "native", lambda: nat)
+    monkeypatch.setattr(tmod.RcclTransport, "_connect", lambda self: 0.0)
+    store = _Store()
+    monkeypatch.setattr(faults, "raw_store", lambda: store)
+    monkeypatch.delenv("DLI_TRANSPORT", raising=False)
+    monkeypatch.setenv("DLI_RCCL_PROBE_S", "1")
+    world, res = 4, {}
+
+    def rank_main(r):
+        if r == 2:
+            time.sleep(2.5)    # longer than the probe window: not a failure, it never entered
+        res[r] = pipeline.make_transport(r, world, torch.device("cuda", 0), job="ok",
+                                         head_pairs=True, streams=_Streams(), max_bytes=1 << 20,
+                                         head_bytes=1 << 16)
+
+    th = [threading.Thread(target=rank_main, args=(r,), name=f"rank{r}") for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(30.0)
+    assert all(isinstance(res.get(r), tmod.RcclTransport) for r in range(world)), res
