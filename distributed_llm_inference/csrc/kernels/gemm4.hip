@@ -1,0 +1,342 @@
+// Projection GEMM for CDNA4, one wave per SIMD:  C[M, N] = A[M, K] . B[N, K]^T  (bf16, fp32 acc)
+//
+// Same contract as gemm_tile.hip (256 x 256 x 64 tiles, NT operands, the weight fragment as the
+// MFMA A operand so every lane owns 4 consecutive output columns, the same SwiGLU interleave and
+// split-K partial layouts), different machine shape:
+//
+//   * workgroup = 4 waves as 2 (M) x 2 (N), ONE wave per SIMD; wave tile 128 x 128 = 8 x 8
+//     fragments of v_mfma_f32_16x16x32_bf16, 256 fp32 accumulators per lane in AGPRs.  Per
+//     k-tile a wave reads 16 + 16 fragments (32 KB per wave, 128 KB per CU) for 128 MFMAs -- a
+//     third less LDS traffic per FLOP than the 8-wave kernel's 128 x 64 wave tiles (192 KB per
+//     CU per k-tile).  The decode GEMMs run at the power cap, so LDS energy is clock;
+//   * the k-loop is written instruction by instruction: every MFMA, fragment read, barrier and
+//     wait is an `asm volatile` statement (the LDS-DMA issues are builtins pinned between them
+//     by the statements' memory clobbers), so the source order IS the issue order, and the
+//     compiler only allocates registers.  The schedule is the one hipBLASLt's hand-written
+//     MT256x256x64 MI16x16 kernel uses (profiles/gemm4_isa_vs_hipblaslt.md):
+//
+//       seg 1 (64 MFMAs of k-step 0, fragments P):  read k-step 1 fragments Q of tile t, one
+//             ds_read_b128 per 2 MFMAs; lgkmcnt(0) + barrier B1 (stage t&1 is free);
+//       seg 2 (64 MFMAs of k-step 1, fragments Q):  LDS-DMA tile t+2 into stage t&1, one
+//             buffer_load ... lds per 2 MFMAs; after 8 of them vmcnt(8) + barrier B2 (tile t+1
+//             has landed in stage (t+1)&1 for every wave); read k-step 0 fragments P of tile
+//             t+1, one per 2 MFMAs; lgkmcnt(0) at the segment's end.
+//
+//     Two barriers per k-tile, no wait on a fragment inside a segment (each segment's
+//     fragments were read and retired during the previous one), the DMA of a tile has one
+//     whole k-tile of MFMAs to land;
+//   * LDS: two stages of A [256][128 B] + B [256][128 B] = 128 KB; XOR swizzle chunk ^ ((row >> 1)
+//     & 7) on the DMA source address (LDS-DMA writes lane-linearly) and on the fragment reads
+//     (conflict-free ds_read_b128, docs/kernels.md).  Rows of A past M are clamped to row M-1
+//     (computed, never stored), so no load leaves the tensor;
+//   * persistent grid: with more tiles than CUs each workgroup runs several whole tiles in turn
+//     (gate|up at M = 512: 448 tiles on 224 workgroups, 2 each -- at the power cap fewer busy CUs
+//     clock higher, which is why hipBLASLt picks that grid); blockIdx is remapped so the
+//     workgroups of one XCD take neighbouring work items (shared A / B panels in its L2).
+#include "kernels.h"
+
+namespace dli {
+
+namespace {
+
+constexpr int kG4Threads = 256;
+constexpr int kG4Stage = 65536;   // A [256][128 B] | B [256][128 B]
+
+enum G4Epi { kG4Bf16 = 0, kG4F32 = 1, kG4SwiGLU = 2, kG4Bf16Part = 4 };
+
+typedef __attribute__((address_space(3))) void g4_lds_t;
+
+template <bool V>
+struct G4B { static constexpr bool value = V; };
+
+__device__ __forceinline__ float g4_silu(float x) { return x / (1.f + __expf(-x)); }
+
+__device__ __forceinline__ void g4_mfma(f32x4& acc, const bf16x8& w, const bf16x8& x) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(w), "v"(x) : "memory");
+}
+
+template <int OFF>
+__device__ __forceinline__ void g4_read(bf16x8& dst, int addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF) : "memory");
+}
+
+__device__ __forceinline__ void g4_sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void g4_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int N>
+__device__ __forceinline__ void g4_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" :: "i"(N) : "memory");
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t g4_rsrc(const void* base, int bytes) {
+  const unsigned long long p = (unsigned long long)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)p);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(p >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(kG4Threads, 1)
+gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __restrict__ C,
+             int M, int N, int K, int tiles_m, int tiles_n, int kps, int splits) {
+  __shared__ __attribute__((aligned(1024))) char smem[2 * kG4Stage];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 1, wc = w & 1, fr = lane & 15;
+  const int Kb = K * 2;
+  const int kt_all = Kb / 128;
+  const int items = tiles_m * tiles_n * splits;
+  const int lds0 = (int)(size_t)smem;
+
+  // XCD-aware bijective remap of the workgroup index: blocks b, b+8, ... share an XCD
+  const int G = gridDim.x, bx = blockIdx.x, x8 = bx & 7, q8 = G >> 3, r8 = G & 7;
+  const int lid = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (bx >> 3);
+
+  // per-lane constants: fragment read addresses of (operand, k-step, stage) and DMA offsets
+  const int sw = fr >> 1;   // (row >> 1) & 7 of every row this lane reads
+  int rdA[2][2], rdB[2][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = ((kk * 4 + (lane >> 4)) ^ sw) << 4;
+      rdA[kk][s] = lds0 + s * kG4Stage + (wr * 128 + fr) * 128 + ch;
+      rdB[kk][s] = lds0 + s * kG4Stage + 32768 + (wc * 128 + fr) * 128 + ch;
+    }
+  // DMA: wave-load q = 4j + w covers tile rows 8q .. 8q+7; lane -> row 8q + (lane >> 3), LDS
+  // slot lane & 7 holding global chunk (lane & 7) ^ ((row >> 1) & 7) = .. ^ ((q & 1) * 4 + (lane >> 4))
+  const int dchunk = ((lane & 7) ^ (((w & 1) * 4 + (lane >> 4)) & 7)) << 4;
+  const int drow = 8 * w + (lane >> 3);
+
+  for (int item = lid; item < items; item += G) {
+    const int tile = item % (tiles_m * tiles_n), split = item / (tiles_m * tiles_n);
+    const int tm = tile % tiles_m, tn = tile / tiles_m;   // M tiles of one weight panel adjacent
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int kt0 = split * kps;
+    const int T = __builtin_amdgcn_readfirstlane(min(kps, kt_all - kt0));
+    const int mrows = min(256, M - m0);
+    const auto rsA = g4_rsrc(A + (size_t)m0 * K, mrows * Kb);
+    const auto rsB = g4_rsrc(B + (size_t)n0 * K, 256 * Kb);
+    int voA[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) voA[j] = min(drow + 32 * j, mrows - 1) * Kb + dchunk;
+    const int voB = drow * Kb + dchunk;
+
+    // stage DMA piece j (0..15: A rows 32j' .. for j < 8, B for j >= 8) of k-tile t
+    auto dma = [&](int t, int j) {
+      const int s = t & 1;
+      const int koff = __builtin_amdgcn_readfirstlane((kt0 + t) * 128);
+      if (j < 8) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsA, (g4_lds_t*)(smem + s * kG4Stage + (4 * j + w) * 1024), 16, voA[j], koff, 0, 0);
+      } else {
+        const int jb = j - 8;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsB, (g4_lds_t*)(smem + s * kG4Stage + 32768 + (4 * jb + w) * 1024), 16, voB,
+            __builtin_amdgcn_readfirstlane(koff + jb * 32 * Kb), 0, 0);
+      }
+    };
+
+    f32x4 acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // fragment sets: P = k-step 0, Q = k-step 1 ([0..7] weight fragments, [8..15] activation)
+    bf16x8 P[16], Q[16];
+    // read fragment n of k-step kk of stage s: n < 8 weight rows wc*128 + 16n, else activation
+    // rows wr*128 + 16(n-8)
+    auto rd = [&](bf16x8 (&F)[16], int n, int kk, int s) {
+      switch (n) {
+        case 0: g4_read<0 * 2048>(F[0], rdB[kk][s]); break;
+        case 1: g4_read<1 * 2048>(F[1], rdB[kk][s]); break;
+        case 2: g4_read<2 * 2048>(F[2], rdB[kk][s]); break;
+        case 3: g4_read<3 * 2048>(F[3], rdB[kk][s]); break;
+        case 4: g4_read<4 * 2048>(F[4], rdB[kk][s]); break;
+        case 5: g4_read<5 * 2048>(F[5], rdB[kk][s]); break;
+        case 6: g4_read<6 * 2048>(F[6], rdB[kk][s]); break;
+        case 7: g4_read<7 * 2048>(F[7], rdB[kk][s]); break;
+        case 8: g4_read<0 * 2048>(F[8], rdA[kk][s]); break;
+        case 9: g4_read<1 * 2048>(F[9], rdA[kk][s]); break;
+        case 10: g4_read<2 * 2048>(F[10], rdA[kk][s]); break;
+        case 11: g4_read<3 * 2048>(F[11], rdA[kk][s]); break;
+        case 12: g4_read<4 * 2048>(F[12], rdA[kk][s]); break;
+        case 13: g4_read<5 * 2048>(F[13], rdA[kk][s]); break;
+        case 14: g4_read<6 * 2048>(F[14], rdA[kk][s]); break;
+        default: g4_read<7 * 2048>(F[15], rdA[kk][s]); break;
+      }
+    };
+    // MFMA number k (0..63) of a segment: activation row-block k / 8, weight block k % 8
+    auto mf = [&](const bf16x8 (&F)[16], int k) {
+      g4_mfma(acc[k >> 3][k & 7], F[k & 7], F[8 + (k >> 3)]);
+    };
+
+    // ---- prologue: tiles 0 and 1 in flight, tile 0 landed, k-step 0 fragments of tile 0 read ----
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dma(0, j);
+    if (T > 1) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) dma(1, j);
+      g4_vmcnt<16>();
+    } else {
+      g4_vmcnt<0>();
+    }
+    g4_barrier();
+#pragma unroll
+    for (int n = 0; n < 16; ++n) rd(P, n, 0, 0);
+    g4_sync_lds();
+
+    // one k-tile.  DMA: issue tile t+2 into stage t&1; NEXT: read k-step 0 of tile t+1
+    auto ktile = [&](int t, auto dma_c, auto next_c) {
+      constexpr bool DMA = decltype(dma_c)::value, NEXT = decltype(next_c)::value;
+      const int s = t & 1;
+      // seg 1: k-step 0 MFMAs; k-step 1 fragments of this tile -> Q
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        mf(P, k);
+        if (k >= 2 && k < 34 && (k & 1) == 0) rd(Q, (k - 2) >> 1, 1, s);
+        if (k == 47) {   // this wave's reads of stage s are done -> after B1 every wave's are
+          g4_sync_lds();
+          if (DMA) g4_barrier();
+        }
+      }
+      // seg 2: k-step 1 MFMAs; DMA of tile t+2 into stage s; k-step 0 of tile t+1 -> P
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        mf(Q, k);
+        if (DMA && k < 32 && (k & 1) == 0) dma(t + 2, k >> 1);
+        if (NEXT) {
+          if (k == 15) {   // own DMA of tile t+1 landed (all but the 8 pieces just issued)
+            if (DMA) g4_vmcnt<8>(); else g4_vmcnt<0>();
+            g4_barrier();
+          }
+          if (k >= 17 && k < 49 && (k & 1) == 1) rd(P, (k - 17) >> 1, 0, s ^ 1);
+        }
+      }
+      if (NEXT) g4_sync_lds();
+    };
+    int t = 0;
+    for (; t + 2 < T; ++t) ktile(t, G4B<true>{}, G4B<true>{});
+    if (t + 1 < T) ktile(t++, G4B<false>{}, G4B<true>{});
+    ktile(t, G4B<false>{}, G4B<false>{});
+
+    // the last MFMAs' results -> compiler-issued AGPR reads: 12+ wait states for an 8-pass XDL
+    // write; the fence takes every accumulator "+a" so no read is hoisted above it
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]),
+                   "+a"(acc[i][4]), "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+
+    // ---- epilogue: fragment (i, j) element e of lane l is
+    //      C[m0 + wr*128 + 16i + (l & 15)][n0 + wc*128 + 16j + 4(l >> 4) + e] ----
+    const int crow = m0 + wr * 128 + fr;
+    const int cq = 4 * (lane >> 4);
+    if constexpr (EPI == kG4SwiGLU) {
+      // n-fragments (2p, 2p+1) = (gate, up) of output columns n0/2 + wc*64 + 16p + cq + e
+      bf16* out = reinterpret_cast<bf16*>(C);
+      const int I = N >> 1;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = crow + i * 16;
+        if (row >= M) continue;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float g = (float)(bf16)acc[i][2 * p][e];   // round like GEMM -> silu_mul
+            const float u = (float)(bf16)acc[i][2 * p + 1][e];
+            o[e] = (bf16)(g4_silu(g) * u);
+          }
+          *reinterpret_cast<bf16x4*>(out + (size_t)row * I + (n0 >> 1) + wc * 64 + p * 16 + cq) = o;
+        }
+      }
+    } else if constexpr (EPI == kG4F32) {
+      float* out = reinterpret_cast<float*>(C) + (size_t)split * M * N;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = crow + i * 16;
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          *reinterpret_cast<f32x4*>(out + (size_t)row * N + n0 + wc * 128 + j * 16 + cq) = acc[i][j];
+      }
+    } else {
+      bf16* out = reinterpret_cast<bf16*>(C) + (EPI == kG4Bf16Part ? (size_t)split * M * N : 0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = crow + i * 16;
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          bf16x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = (bf16)acc[i][j][e];
+          *reinterpret_cast<bf16x4*>(out + (size_t)row * N + n0 + wc * 128 + j * 16 + cq) = o;
+        }
+      }
+    }
+    // the next item's prologue re-stages both LDS stages: every wave's last reads are retired
+    // (lgkmcnt(0) in the last k-tile), the barrier makes that hold for all of them
+    g4_barrier();
+  }
+}
+
+int g4_cus() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    return 256;
+  return n;
+}
+
+}  // namespace
+
+// Persistent grid for `items` work items on `cus` CUs: all of them if they fit, else the
+// smallest grid that needs the same number of rounds (448 items on 256 CUs -> 224 x 2).
+int gemm4_grid(int items, int cus) {
+  if (items <= cus) return items;
+  const int rounds = (items + cus - 1) / cus;
+  return (items + rounds - 1) / rounds;
+}
+
+// C = A . B^T on the one-wave-per-SIMD kernel.  epilogue 0: bf16 [M, N]; 2: fused SwiGLU ([M,
+// N/2], B rows in swiglu_interleave order); with splits > 1: 1 = fp32 partials [splits, M, N],
+// 4 = bf16 partials [splits, M, N] (into C; the consumer sums them).  grid <= 0: automatic.
+int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int splits,
+                 int epilogue, int grid, hipStream_t stream) {
+  if (M <= 0 || N % 256 != 0 || (K * 2) % 128 != 0 || splits < 1) return -1;
+  const int kt = K * 2 / 128;
+  if (splits > kt) return -2;
+  const int kps = (kt + splits - 1) / splits;
+  if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
+  if ((splits > 1) != (epilogue == kG4F32 || epilogue == kG4Bf16Part)) return -3;
+  const int tiles_m = (M + 255) / 256, tiles_n = N / 256;
+  const int items = tiles_m * tiles_n * splits;
+  if (grid <= 0) grid = gemm4_grid(items, g4_cus());
+  if (grid > items) grid = items;
+  const bf16* a = reinterpret_cast<const bf16*>(A);
+  const bf16* b = reinterpret_cast<const bf16*>(B);
+  switch (epilogue) {
+    case kG4Bf16:
+      gemm4_kernel<kG4Bf16><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      break;
+    case kG4F32:
+      gemm4_kernel<kG4F32><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      break;
+    case kG4SwiGLU:
+      gemm4_kernel<kG4SwiGLU><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      break;
+    case kG4Bf16Part:
+      gemm4_kernel<kG4Bf16Part><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      break;
+    default:
+      return -4;
+  }
+  return 0;
+}
+
+}  // namespace dli

@@ -11,7 +11,9 @@ Reference: /root/reference/distributed_llm_inference/utils/model.py —
     with per-channel scales (CDNA4 fp8 MFMA) by default, or ``"int8"`` = LLM.int8 (int8 MFMA tile
     GEMM + bf16 outlier columns above ``threshold``);
   * a random-init path builds any config without a checkpoint (``random_init=True``).
-Weights are read with ``safetensors`` (memory-mapped, no pickle execution).
+Weights are read with ``safetensors`` (memory-mapped, no pickle execution), or -- for the
+``pytorch_model.bin`` formats the reference also lists (utils/model.py:13) -- with
+``torch.load(..., weights_only=True, mmap=True)``: tensors only, nothing from the file is executed.
 """
 from __future__ import annotations
 
@@ -28,7 +30,43 @@ from ..models.stage import CausalLMStage, apply_quantization, make_block
 
 log = logging.getLogger(__name__)
 
-INDEX_FILE_PATTERNS = ["model.safetensors.index.json", "model.safetensors"]
+# searched in this order (reference utils/model.py:13 lists the same four names)
+INDEX_FILE_PATTERNS = ["model.safetensors.index.json", "model.safetensors",
+                       "pytorch_model.bin.index.json", "pytorch_model.bin"]
+
+
+class _BinShard:
+    """A ``pytorch_model*.bin`` shard opened with the weights-only unpickler (tensors and plain
+    containers only; anything else in the file is refused, never executed), memory-mapped."""
+
+    def __init__(self, path: str):
+        try:
+            sd = torch.load(path, map_location="cpu", weights_only=True, mmap=True)
+        except RuntimeError:   # legacy (non-zip) serialisation cannot be memory-mapped
+            sd = torch.load(path, map_location="cpu", weights_only=True)
+        if not isinstance(sd, dict):
+            raise ValueError(f"{path}: expected a state dict, got {type(sd).__name__}")
+        self._sd = sd
+
+    def keys(self):
+        return list(self._sd.keys())
+
+    def get_tensor(self, key: str) -> torch.Tensor:
+        return self._sd[key]
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+def _open_shard(path: str):
+    """Context manager with ``keys()`` / ``get_tensor(k)`` over a safetensors or .bin shard."""
+    if path.endswith(".bin"):
+        return _BinShard(path)
+    from safetensors import safe_open
+    return safe_open(path, framework="pt", device="cpu")
 
 
 def _resolve_file(repo: str, filename: str, cache_dir: Optional[str] = None,
@@ -47,9 +85,8 @@ def _resolve_file(repo: str, filename: str, cache_dir: Optional[str] = None,
 
 def get_sharded_block_state_from_file(file: str, block_prefix: str) -> Dict[str, torch.Tensor]:
     """All tensors of ``file`` whose key starts with ``block_prefix`` (prefix stripped)."""
-    from safetensors import safe_open
     out = {}
-    with safe_open(file, framework="pt", device="cpu") as f:
+    with _open_shard(file) as f:
         for key in f.keys():
             if key.startswith(block_prefix):
                 out[key[len(block_prefix):]] = f.get_tensor(key)
@@ -57,28 +94,29 @@ def get_sharded_block_state_from_file(file: str, block_prefix: str) -> Dict[str,
 
 
 def _weight_files(repo: str, cache_dir=None, token=False) -> Dict[str, str]:
-    """Map tensor name -> local shard path."""
-    idx = _resolve_file(repo, "model.safetensors.index.json", cache_dir, token)
-    if idx is not None:
-        with open(idx) as f:
-            index = json.load(f)
-        if "weight_map" not in index:
-            raise ValueError("Index file does not contain a weight map")
-        out = {}
-        for k, shard in index["weight_map"].items():
-            p = _resolve_file(repo, shard, cache_dir, token)
-            if p is None:
-                raise FileNotFoundError(f"shard {shard} of {repo} is not available locally")
-            out[k] = p
-        return out
-    single = _resolve_file(repo, "model.safetensors", cache_dir, token)
-    if single is not None:
-        from safetensors import safe_open
-        with safe_open(single, framework="pt", device="cpu") as f:
-            return {k: single for k in f.keys()}
+    """Map tensor name -> local shard path (safetensors preferred, then pytorch_model*.bin)."""
+    for index_name, single_name in (("model.safetensors.index.json", "model.safetensors"),
+                                    ("pytorch_model.bin.index.json", "pytorch_model.bin")):
+        idx = _resolve_file(repo, index_name, cache_dir, token)
+        if idx is not None:
+            with open(idx) as f:
+                index = json.load(f)
+            if "weight_map" not in index:
+                raise ValueError("Index file does not contain a weight map")
+            out = {}
+            for k, shard in index["weight_map"].items():
+                p = _resolve_file(repo, shard, cache_dir, token)
+                if p is None:
+                    raise FileNotFoundError(f"shard {shard} of {repo} is not available locally")
+                out[k] = p
+            return out
+        single = _resolve_file(repo, single_name, cache_dir, token)
+        if single is not None:
+            with _open_shard(single) as f:
+                return {k: single for k in f.keys()}
     raise FileNotFoundError(
-        f"no safetensors checkpoint found for {repo!r} (local dir or local HF cache); "
-        "use random_init=True to build the architecture without weights")
+        f"no checkpoint ({', '.join(INDEX_FILE_PATTERNS)}) found for {repo!r} (local dir or "
+        "local HF cache); use random_init=True to build the architecture without weights")
 
 
 def get_block_state_dict(repo: str, block_idx: int, cache_dir: Optional[str] = None,
@@ -166,8 +204,7 @@ def load_stage_weights(stage: CausalLMStage, model_name: str, cache_dir=None, to
         want += extra["head"]
     sd = {}
     for f in sorted({files[k] for k in want if k in files}):
-        from safetensors import safe_open
-        with safe_open(f, framework="pt", device="cpu") as fh:
+        with _open_shard(f) as fh:
             for k in want:
                 if k in fh.keys():
                     sd[k] = fh.get_tensor(k)
@@ -218,9 +255,8 @@ def build_head(model, device=None, dtype=torch.bfloat16, random_init: bool = Tru
     else:
         want = ["model.norm.weight", "lm_head.weight", "model.embed_tokens.weight"]
     sd = {}
-    from safetensors import safe_open
     for f in sorted({files[k] for k in want if k in files}):
-        with safe_open(f, framework="pt", device="cpu") as fh:
+        with _open_shard(f) as fh:
             for k in want:
                 if k in fh.keys():
                     sd[k] = fh.get_tensor(k)
@@ -256,9 +292,18 @@ def build_stage(model: str, start: int, end: int, device=None, dtype=torch.bfloa
     return stage
 
 
-def save_random_checkpoint(spec: ModelSpec, path: str, seed: int = 0, shard_layers: int = 2) -> None:
-    """Write a random-init HF-format sharded checkpoint (config.json + safetensors + index)."""
-    from safetensors.torch import save_file
+def save_random_checkpoint(spec: ModelSpec, path: str, seed: int = 0, shard_layers: int = 2,
+                           fmt: str = "safetensors") -> None:
+    """Write a random-init HF-format sharded checkpoint: config.json + shards + index, as
+    safetensors (``model-*.safetensors``) or ``fmt="bin"`` (``pytorch_model-*.bin``, plain
+    tensor dicts written by ``torch.save``)."""
+    if fmt not in ("safetensors", "bin"):
+        raise ValueError(f"unknown checkpoint format {fmt!r}")
+    if fmt == "bin":
+        def save_file(tensors, file):
+            torch.save(tensors, file)
+    else:
+        from safetensors.torch import save_file
     os.makedirs(path, exist_ok=True)
     with open(os.path.join(path, "config.json"), "w") as f:
         json.dump(spec.to_hf_dict(), f)
@@ -283,9 +328,11 @@ def save_random_checkpoint(spec: ModelSpec, path: str, seed: int = 0, shard_laye
         if stage.head.proj is not None:
             extra["lm_head.weight"] = stage.head.proj.weight.data.clone()
     shards.append(extra)
+    stem, ext = ("model", "safetensors") if fmt == "safetensors" else ("pytorch_model", "bin")
     for i, sh in enumerate(shards):
-        name = f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors"
+        name = f"{stem}-{i + 1:05d}-of-{len(shards):05d}.{ext}"
         save_file(sh, os.path.join(path, name))
         weight_map.update({k: name for k in sh})
-    with open(os.path.join(path, "model.safetensors.index.json"), "w") as f:
+    index = "model.safetensors.index.json" if fmt == "safetensors" else "pytorch_model.bin.index.json"
+    with open(os.path.join(path, index), "w") as f:
         json.dump({"metadata": {}, "weight_map": weight_map}, f)
