@@ -5,6 +5,8 @@
     distribute serve    --model llama-3-70b --gpus 8 --port 8000 [--tokenizer DIR] [--dp 8]
     distribute bench    --gpus 8 --steps 20 --warmup 5 [--dp 2]  (bench.py under the launcher)
     distribute block-serve --model llama-3-8b --start 0 --end 16 --port 8100   (swarm block server)
+    distribute registry --port 8099                                           (swarm block registry)
+    distribute block-serve --model llama-3-8b --registry http://h:8099 --max-layers 16 --port 8100
 
 One process per GPU (``launcher.launch``); each process owns one pipeline stage (``plan_stages``).
 ``--dp D`` splits the GPUs into D independent pipeline replicas of gpus/D stages (DP x PP,
@@ -107,15 +109,40 @@ def cmd_plan(a) -> int:
 
 
 def cmd_block_serve(a) -> int:
-    """One block server (reference server/worker.py intent): layers [start, end) behind HTTP."""
+    """One block server (reference server/worker.py intent): layers [start, end) behind HTTP.
+    With ``--registry`` the range is claimed from the block registry (the least-served layers,
+    reference server/server.py:7-8) instead of given."""
     from .server.block_server import serve_blocks
     from .server.worker import InferenceWorker
     logging.basicConfig(level=logging.WARNING)
-    worker = InferenceWorker(a.model, a.start, a.end, layers_per_block=a.layers_per_block,
+    registry, url = None, None
+    start, end = a.start, a.end
+    if a.registry:
+        from .config import resolve_model
+        from .server.registry import RegistryClient
+        spec = resolve_model(a.checkpoint or a.model)
+        registry = RegistryClient(a.registry)
+        url = a.public_url or f"http://{a.host}:{a.port}"
+        start, end = registry.claim(spec.name, spec.num_layers,
+                                    a.max_layers or spec.num_layers, url)
+        print(f"block-serve: registry {a.registry} assigned layers [{start}, {end}) to {url}",
+              file=sys.stderr, flush=True)
+    elif start is None or end is None:
+        print("block-serve: give --start and --end, or --registry", file=sys.stderr)
+        return 2
+    worker = InferenceWorker(a.model, start, end, layers_per_block=a.layers_per_block,
                              device=a.device, random_init=a.checkpoint is None,
                              checkpoint=a.checkpoint, max_batch_size=a.max_batch_size,
                              window_length=a.window, num_sink_tokens=a.sinks, seed=a.seed)
-    serve_blocks(worker, a.host, a.port)
+    serve_blocks(worker, a.host, a.port, registry=registry, url=url)
+    return 0
+
+
+def cmd_registry(a) -> int:
+    """The block registry (server/registry.py): block servers claim layers, clients find chains."""
+    from .server.registry import serve_registry
+    logging.basicConfig(level=logging.WARNING)
+    serve_registry(a.host, a.port)
     return 0
 
 
@@ -247,8 +274,14 @@ def main(argv: Optional[List[str]] = None) -> int:
                         help="serve a layer range's hidden-state forward over HTTP (swarm block server)")
     bs.add_argument("--model", default="llama-3-8b", help="preset name or HF config/checkpoint dir")
     bs.add_argument("--checkpoint", default=None, help="HF safetensors dir (default: random init)")
-    bs.add_argument("--start", type=int, required=True, help="first layer (inclusive)")
-    bs.add_argument("--end", type=int, required=True, help="last layer (exclusive)")
+    bs.add_argument("--start", type=int, default=None, help="first layer (inclusive)")
+    bs.add_argument("--end", type=int, default=None, help="last layer (exclusive)")
+    bs.add_argument("--registry", default=None,
+                    help="block registry URL: claim the least-served layers instead of --start/--end")
+    bs.add_argument("--max-layers", type=int, default=None,
+                    help="with --registry: most layers this server holds (default: all)")
+    bs.add_argument("--public-url", default=None,
+                    help="with --registry: URL clients reach this server at (default http://host:port)")
     bs.add_argument("--layers-per-block", type=int, default=None)
     bs.add_argument("--seed", type=int, default=0)
     bs.add_argument("--device", default=None, help="cuda:N / cpu (default: cuda:0 if present)")
@@ -257,6 +290,9 @@ def main(argv: Optional[List[str]] = None) -> int:
     bs.add_argument("--sinks", type=int, default=0)
     bs.add_argument("--host", default="127.0.0.1")
     bs.add_argument("--port", type=int, default=8100)
+    rg = sub.add_parser("registry", help="block registry: servers claim layer ranges, clients find chains")
+    rg.add_argument("--host", default="127.0.0.1")
+    rg.add_argument("--port", type=int, default=8099)
     w = sub.add_parser("worker", help=argparse.SUPPRESS)
     _common(w)
     _gen_args(w)
@@ -267,6 +303,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         return cmd_plan(a)
     if a.cmd == "worker":
         return cmd_worker(a)
+    if a.cmd == "registry":
+        return cmd_registry(a)
     if a.cmd == "block-serve":
         return cmd_block_serve(a)
     if a.cmd == "bench":

@@ -19,7 +19,8 @@ Server (``distribute block-serve --model M --start a --end b --port P``)::
 
 Client: :class:`RemoteBlocks` (one server) and :class:`RemoteSequential` (a chain of servers
 whose ranges tile [0, L) - the client side of the swarm: ``forward(gid, hidden)`` walks the
-chain, ``close_session(gid)`` frees the session everywhere).
+chain, ``close_session(gid)`` frees the session everywhere; ``from_registry`` finds the chain in
+a block registry, server/registry.py, where ``block-serve --registry`` servers claim their layers).
 """
 from __future__ import annotations
 
@@ -102,10 +103,30 @@ def build_block_app(worker):
     return app
 
 
-def serve_blocks(worker, host: str = "127.0.0.1", port: int = 8100) -> None:
+def serve_blocks(worker, host: str = "127.0.0.1", port: int = 8100, registry=None,
+                 url: Optional[str] = None, ttl: float = 30.0) -> None:
+    """Serve ``worker`` over HTTP.  With ``registry`` (a :class:`RegistryClient`) the server is
+    announced under ``url`` while its /health answers, and withdrawn when it stops."""
     import uvicorn
     worker.run()
-    uvicorn.run(build_block_app(worker), host=host, port=port, log_level="warning")
+    stop = None
+    if registry is not None:
+        import threading
+        from .registry import heartbeat_loop
+        url = url or f"http://{host}:{port}"
+        probe = RemoteBlocks(url, timeout=5.0)
+        stop = threading.Event()
+        heartbeat_loop(registry, worker.spec.name, url, worker.start, worker.end,
+                       worker.spec.num_layers, probe.healthy, ttl=ttl, stop=stop)
+    try:
+        uvicorn.run(build_block_app(worker), host=host, port=port, log_level="warning")
+    finally:
+        if registry is not None:
+            stop.set()
+            try:
+                registry.withdraw(url)
+            except Exception:  # noqa: BLE001 - best effort: the entry also expires after ttl
+                pass
 
 
 class RemoteBlocks:
@@ -163,6 +184,33 @@ class RemoteSequential:
                 raise ValueError(f"layer ranges do not chain: [{a['start']},{a['end']}) then "
                                  f"[{b['start']},{b['end']})")
         self.start, self.end = infos[0]["start"], infos[-1]["end"]
+
+    @classmethod
+    def from_registry(cls, registry_url: str, model: str, timeout: float = 120.0,
+                      wait_s: float = 0.0) -> "RemoteSequential":
+        """The chain of ready servers listed by a block registry (server/registry.py) that
+        covers ``model`` from layer 0 to its last layer; ``wait_s``: keep polling that long
+        for the swarm to cover it."""
+        import time
+        from ..config import resolve_model
+        from .registry import RegistryClient, find_chain
+        reg = RegistryClient(registry_url)
+        try:
+            name = resolve_model(model).name
+        except ValueError:
+            name = model
+        deadline = time.monotonic() + wait_s
+        while True:
+            entries = reg.servers(name)
+            L = max([int(e["num_layers"]) for e in entries] + [0])
+            chain = find_chain(entries, L) if L else []
+            if chain or time.monotonic() >= deadline:
+                break
+            time.sleep(0.5)
+        if not chain:
+            raise LookupError(f"registry {registry_url} lists no chain of ready servers covering "
+                              f"{name} (servers: {[(e['start'], e['end']) for e in entries]})")
+        return cls([e["url"] for e in chain], timeout=timeout)
 
     def forward(self, generation_id: str, hidden: torch.Tensor) -> torch.Tensor:
         for s in self.servers:

@@ -1,0 +1,217 @@
+"""Block registry: which server serves which layers, and which layers a new server should take.
+
+Reference: the server loop is meant to "choose optimal block ids" against what the swarm already
+serves (/root/reference/distributed_llm_inference/server/server.py:7-8), through hivemind's DHT
+(imported at server/backend.py:4-7).  Here the swarm's shared state is one small HTTP service:
+
+    POST /claim     {"model", "num_layers", "max_layers", "url"} -> {"start", "end"}
+                    picks the range for a new block server and records it at once (under one
+                    lock, so servers starting together never pick the same gap)
+    POST /announce  {"model", "url", "start", "end", "num_layers", "ttl"}: the server is up
+                    (sent again every ttl / 3 as a heartbeat; an entry that misses its ttl is
+                    dropped, a claim that never turns ready after ``claim_ttl`` too)
+    POST /withdraw  {"url"}
+    GET  /servers?model=M   [{"url", "start", "end", "num_layers", "ready"}]
+
+``distribute registry`` runs it; ``distribute block-serve --registry URL --max-layers N`` claims
+a range instead of taking ``--start/--end``, and ``RemoteSequential.from_registry(URL, model)``
+builds the client's chain from the registry alone.
+"""
+from __future__ import annotations
+
+import threading
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+
+def choose_range(num_layers: int, max_layers: int,
+                 served: Sequence[Tuple[int, int]]) -> Tuple[int, int]:
+    """The layer range a new server holding at most ``max_layers`` layers should serve.
+
+    Uncovered layers come first: the first maximal run of layers nobody serves, capped at
+    ``max_layers``.  With every layer covered, the window of ``max_layers`` layers with the
+    lowest (max coverage, total coverage) -- the least-served part of the model, where one more
+    replica adds the most throughput; the lowest start breaks ties."""
+    if num_layers <= 0 or max_layers <= 0:
+        raise ValueError("num_layers and max_layers must be positive")
+    span = min(max_layers, num_layers)
+    cov = [0] * num_layers
+    for s, e in served:
+        for i in range(max(0, s), min(num_layers, e)):
+            cov[i] += 1
+    if 0 in cov:
+        s = cov.index(0)
+        e = s
+        while e < num_layers and cov[e] == 0 and e - s < span:
+            e += 1
+        return s, e
+    best = min(range(num_layers - span + 1),
+               key=lambda s: (max(cov[s:s + span]), sum(cov[s:s + span]), s))
+    return best, best + span
+
+
+def find_chain(entries: Sequence[dict], num_layers: int) -> List[dict]:
+    """Servers whose ranges chain exactly from layer 0 to ``num_layers`` (fewest hops; among
+    equals the earliest-listed servers), or [] if the ready servers do not cover the model."""
+    by_start: Dict[int, List[dict]] = {}
+    for e in entries:
+        by_start.setdefault(int(e["start"]), []).append(e)
+    # breadth-first over layer boundaries: the first path that reaches num_layers has fewest hops
+    prev: Dict[int, Tuple[int, dict]] = {}
+    frontier = [0]
+    seen = {0}
+    while frontier:
+        nxt = []
+        for b in frontier:
+            for e in by_start.get(b, []):
+                end = int(e["end"])
+                if end not in seen and end <= num_layers:
+                    seen.add(end)
+                    prev[end] = (b, e)
+                    nxt.append(end)
+        if num_layers in seen:
+            break
+        frontier = nxt
+    if num_layers not in seen:
+        return []
+    chain, b = [], num_layers
+    while b != 0:
+        b0, e = prev[b]
+        chain.append(e)
+        b = b0
+    return chain[::-1]
+
+
+class Registry:
+    """In-memory registry state (the service wraps it; tests use it directly)."""
+
+    def __init__(self, claim_ttl: float = 900.0):
+        self.claim_ttl = claim_ttl
+        self._lock = threading.Lock()
+        self._entries: Dict[str, dict] = {}   # url -> entry
+
+    def _expire(self, now: float) -> None:
+        for url in [u for u, e in self._entries.items() if e["expires"] < now]:
+            del self._entries[url]
+
+    def claim(self, model: str, num_layers: int, max_layers: int, url: str) -> Tuple[int, int]:
+        with self._lock:
+            now = time.monotonic()
+            self._expire(now)
+            self._entries.pop(url, None)   # a restarted server re-claims
+            served = [(e["start"], e["end"]) for e in self._entries.values() if e["model"] == model]
+            s, e = choose_range(num_layers, max_layers, served)
+            self._entries[url] = {"url": url, "model": model, "start": s, "end": e,
+                                  "num_layers": num_layers, "ready": False,
+                                  "expires": now + self.claim_ttl}
+            return s, e
+
+    def announce(self, model: str, url: str, start: int, end: int, num_layers: int,
+                 ttl: float) -> None:
+        with self._lock:
+            self._entries[url] = {"url": url, "model": model, "start": int(start),
+                                  "end": int(end), "num_layers": int(num_layers), "ready": True,
+                                  "expires": time.monotonic() + float(ttl)}
+
+    def withdraw(self, url: str) -> None:
+        with self._lock:
+            self._entries.pop(url, None)
+
+    def servers(self, model: Optional[str] = None) -> List[dict]:
+        with self._lock:
+            self._expire(time.monotonic())
+            return [{k: v for k, v in e.items() if k != "expires"}
+                    for e in self._entries.values() if model is None or e["model"] == model]
+
+
+def build_registry_app(reg: Optional[Registry] = None):
+    from fastapi import FastAPI, HTTPException
+    reg = reg or Registry()
+    app = FastAPI(title="distributed_llm_inference block registry")
+
+    @app.post("/claim")
+    async def claim(body: dict):
+        try:
+            s, e = reg.claim(body["model"], int(body["num_layers"]), int(body["max_layers"]),
+                             body["url"])
+        except (KeyError, ValueError) as ex:
+            raise HTTPException(400, f"bad claim: {ex}")
+        return {"start": s, "end": e}
+
+    @app.post("/announce")
+    async def announce(body: dict):
+        try:
+            reg.announce(body["model"], body["url"], body["start"], body["end"],
+                         body["num_layers"], body.get("ttl", 30.0))
+        except KeyError as ex:
+            raise HTTPException(400, f"bad announce: missing {ex}")
+        return {"ok": True}
+
+    @app.post("/withdraw")
+    async def withdraw(body: dict):
+        reg.withdraw(body["url"])
+        return {"ok": True}
+
+    @app.get("/servers")
+    async def servers(model: Optional[str] = None):
+        return reg.servers(model)
+
+    return app
+
+
+def serve_registry(host: str = "127.0.0.1", port: int = 8099) -> None:
+    import uvicorn
+    uvicorn.run(build_registry_app(), host=host, port=port, log_level="warning")
+
+
+class RegistryClient:
+    def __init__(self, url: str, timeout: float = 30.0):
+        import requests
+        self.url = url.rstrip("/")
+        self.timeout = timeout
+        self._s = requests.Session()
+
+    def _post(self, path: str, body: dict) -> dict:
+        r = self._s.post(self.url + path, json=body, timeout=self.timeout)
+        if r.status_code != 200:
+            raise RuntimeError(f"{self.url}{path}: HTTP {r.status_code}: {r.text[:300]}")
+        return r.json()
+
+    def claim(self, model: str, num_layers: int, max_layers: int, url: str) -> Tuple[int, int]:
+        d = self._post("/claim", {"model": model, "num_layers": num_layers,
+                                  "max_layers": max_layers, "url": url})
+        return int(d["start"]), int(d["end"])
+
+    def announce(self, model: str, url: str, start: int, end: int, num_layers: int,
+                 ttl: float = 30.0) -> None:
+        self._post("/announce", {"model": model, "url": url, "start": start, "end": end,
+                                 "num_layers": num_layers, "ttl": ttl})
+
+    def withdraw(self, url: str) -> None:
+        self._post("/withdraw", {"url": url})
+
+    def servers(self, model: Optional[str] = None, ready_only: bool = True) -> List[dict]:
+        r = self._s.get(self.url + "/servers", params={"model": model} if model else None,
+                        timeout=self.timeout)
+        r.raise_for_status()
+        return [e for e in r.json() if e["ready"] or not ready_only]
+
+
+def heartbeat_loop(client: RegistryClient, model: str, url: str, start: int, end: int,
+                   num_layers: int, healthy, ttl: float = 30.0,
+                   stop: Optional[threading.Event] = None) -> threading.Thread:
+    """Background thread: announce this server while ``healthy()`` holds, every ttl / 3."""
+    stop = stop or threading.Event()
+
+    def run():
+        while not stop.is_set():
+            try:
+                if healthy():
+                    client.announce(model, url, start, end, num_layers, ttl)
+            except Exception:  # noqa: BLE001 - the registry may be restarting; keep trying
+                pass
+            stop.wait(ttl / 3)
+
+    th = threading.Thread(target=run, name="registry-heartbeat", daemon=True)
+    th.start()
+    return th
