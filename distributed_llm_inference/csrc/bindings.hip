@@ -677,13 +677,43 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
            "gemm_tile");
 }
 
+// one-wave-per-SIMD tile GEMM (gemm4.hip), bf16: epilogue 0 = bf16 [M, N], 2 = SwiGLU [M, N/2]
+// (splits 1); 1 = fp32 partials, 4 = bf16 partials [splits, M, N] (splits > 1)
+void gemm4(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue, int64_t grid) {
+  CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
+  CHECK_BF16(a); CHECK_BF16(b);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm4: 2-D operands");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "gemm4: shape mismatch");
+  int64_t want = 0;
+  if (epilogue == 0) want = M * N;
+  else if (epilogue == 2) want = M * (N / 2);
+  else if (epilogue == 1 || epilogue == 4) want = splits * M * N;
+  else TORCH_CHECK(false, "gemm4: epilogue 0, 1, 2 or 4");
+  TORCH_CHECK(out.is_contiguous() && out.numel() == want &&
+              out.scalar_type() == (epilogue == 1 ? at::kFloat : at::kBFloat16),
+              "gemm4: output size / dtype");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
+  check_rc(dli::launch_gemm4(out.data_ptr(), a.data_ptr(), b.data_ptr(), (int)M, (int)N, (int)K,
+                             (int)splits, (int)epilogue, (int)grid, cur_stream()),
+           "gemm4");
+}
+
 // ------------------------------------------------------------------------------ skinny GEMM
-void skinny_gemm(Tensor out, Tensor x, Tensor w, optional<Tensor> bias) {
+// swiglu: w is a swiglu_interleave'd gate|up weight [2I, K]; out = silu(gate) * up [M, I]
+static int64_t gemv_out_cols(int64_t N, bool swiglu, const char* what) {
+  TORCH_CHECK(!swiglu || N % 32 == 0, what, ": swiglu needs 32 | N");
+  return swiglu ? N / 2 : N;
+}
+
+void skinny_gemm(Tensor out, Tensor x, Tensor w, optional<Tensor> bias, bool swiglu) {
   CHECK_IN(out); CHECK_IN(x); CHECK_IN(w);
   CHECK_BF16(out); CHECK_BF16(x); CHECK_BF16(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm: 2-D tensors");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N, "skinny_gemm: shape mismatch");
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == gemv_out_cols(N, swiglu, "skinny_gemm"),
+              "skinny_gemm: shape mismatch");
+  TORCH_CHECK(!swiglu || M <= 2, "skinny_gemm: swiglu for M <= 2");
   TORCH_CHECK(M >= 1 && M <= 4 && K % 8 == 0, "skinny_gemm: M in [1, 4], K % 8 == 0");
   const dli::bf16* b = nullptr;
   if (bias.has_value()) {
@@ -693,17 +723,19 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, optional<Tensor> bias) {
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_rc(dli::launch_skinny_gemm(bp(out), bp(x), bp(w), b, (int)M, (int)N, (int)K,
-                                   cur_stream()), "skinny_gemm");
+                                   cur_stream(), swiglu), "skinny_gemm");
 }
 
 // int8 weights [N, K] with fp32 per-row scales [N], bf16 activations (weight-only dequantisation)
-void skinny_gemm_int8(Tensor out, Tensor x, Tensor w, Tensor wscale, optional<Tensor> bias) {
+void skinny_gemm_int8(Tensor out, Tensor x, Tensor w, Tensor wscale, optional<Tensor> bias,
+                      bool swiglu) {
   CHECK_IN(out); CHECK_IN(x); CHECK_IN(w); CHECK_IN(wscale);
   CHECK_BF16(out); CHECK_BF16(x); CHECK_F32(wscale);
   TORCH_CHECK(w.scalar_type() == at::kChar, "skinny_gemm_int8: int8 weights");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm_int8: 2-D tensors");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N && wscale.numel() == N,
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M &&
+              out.size(1) == gemv_out_cols(N, swiglu, "skinny_gemm_int8") && wscale.numel() == N,
               "skinny_gemm_int8: shape mismatch");
   TORCH_CHECK(M >= 1 && M <= 2 && K % 16 == 0, "skinny_gemm_int8: M in [1, 2], K % 16 == 0");
   const dli::bf16* b = nullptr;
@@ -715,19 +747,20 @@ void skinny_gemm_int8(Tensor out, Tensor x, Tensor w, Tensor wscale, optional<Te
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_rc(dli::launch_skinny_gemm_int8(bp(out), bp(x), w.data_ptr<int8_t>(),
                                         wscale.data_ptr<float>(), b, (int)M, (int)N, (int)K,
-                                        cur_stream()), "skinny_gemm_int8");
+                                        cur_stream(), swiglu), "skinny_gemm_int8");
 }
 
 // fp8 e4m3 weights [N, K] (1-byte storage), fp32 per-row scales [N]; activations bf16, or fp8
 // [M, K] with fp32 per-row scales xscale [M] (the fused RMSNorm quantiser's output)
 void skinny_gemm_fp8(Tensor out, Tensor x, optional<Tensor> xscale, Tensor w, Tensor wscale,
-                     optional<Tensor> bias) {
+                     optional<Tensor> bias, bool swiglu) {
   CHECK_IN(out); CHECK_IN(x); CHECK_IN(w); CHECK_IN(wscale);
   CHECK_BF16(out); CHECK_F32(wscale);
   TORCH_CHECK(w.element_size() == 1, "skinny_gemm_fp8: 1-byte (fp8 e4m3) weights");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm_fp8: 2-D tensors");
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && out.size(0) == M && out.size(1) == N && wscale.numel() == N,
+  TORCH_CHECK(w.size(1) == K && out.size(0) == M &&
+              out.size(1) == gemv_out_cols(N, swiglu, "skinny_gemm_fp8") && wscale.numel() == N,
               "skinny_gemm_fp8: shape mismatch");
   TORCH_CHECK(M >= 1 && M <= 2 && K % 16 == 0, "skinny_gemm_fp8: M in [1, 2], K % 16 == 0");
   const float* xs = nullptr;
@@ -749,7 +782,7 @@ void skinny_gemm_fp8(Tensor out, Tensor x, optional<Tensor> xscale, Tensor w, Te
   check_rc(dli::launch_skinny_gemm_fp8(bp(out), x.data_ptr(), xs,
                                        static_cast<const uint8_t*>(w.data_ptr()),
                                        wscale.data_ptr<float>(), b, (int)M, (int)N, (int)K,
-                                       cur_stream()), "skinny_gemm_fp8");
+                                       cur_stream(), swiglu), "skinny_gemm_fp8");
 }
 
 }  // namespace
@@ -807,15 +840,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_reduce", &splitk_reduce, "bf16 out = sum of fp32 split-K partials [S, M, N]");
   m.def("gemm_tile_sk_workspace_floats", []() { return dli::gemm_tile_sk_workspace_floats(); },
         "fp32 workspace elements gemm_tile(splits=0) needs on the current device");
+  m.def("gemm4", &gemm4, "C = A . B^T, one-wave-per-SIMD 256x256 MFMA tile GEMM (gemm4.hip)",
+        py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
+        py::arg("epilogue") = 0, py::arg("grid") = 0);
   m.def("skinny_gemm_int8", &skinny_gemm_int8,
         "y = (x . W8^T) * scale (+ bias), int8 weights, bf16 rows, M <= 2 (weight-streaming GEMV)",
-        py::arg("out"), py::arg("x"), py::arg("w"), py::arg("wscale"), py::arg("bias") = py::none());
+        py::arg("out"), py::arg("x"), py::arg("w"), py::arg("wscale"), py::arg("bias") = py::none(),
+        py::arg("swiglu") = false);
   m.def("skinny_gemm_fp8", &skinny_gemm_fp8,
         "y = (x . W8^T) * scale (+ bias), fp8 e4m3 weights, M <= 2 (weight-streaming GEMV)",
         py::arg("out"), py::arg("x"), py::arg("xscale"), py::arg("w"), py::arg("wscale"),
-        py::arg("bias") = py::none());
+        py::arg("bias") = py::none(), py::arg("swiglu") = false);
   m.def("skinny_gemm", &skinny_gemm, "y = x . W^T (+ bias) for M <= 4 (weight-streaming GEMV)",
-        py::arg("out"), py::arg("x"), py::arg("w"), py::arg("bias") = py::none());
+        py::arg("out"), py::arg("x"), py::arg("w"), py::arg("bias") = py::none(),
+        py::arg("swiglu") = false);
   register_rccl(m);
   register_streams(m);
 }

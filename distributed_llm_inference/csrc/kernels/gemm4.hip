@@ -82,6 +82,15 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
              int M, int N, int K, int tiles_m, int tiles_n, int kps, int splits) {
   __shared__ __attribute__((aligned(1024))) char smem[2 * kG4Stage];
   const int tid = threadIdx.x, lane = tid & 63;
+#ifdef DLI_GEMM_STAMPS
+  // diagnostic builds only (scripts/experiments/gemm4_bench.hip): begin / end-of-last-k-loop /
+  // end stamps per workgroup, shader cycles and 100 MHz wall ticks (g_stamp_blk: gemm_tile.hip)
+  unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
+  if (tid == 0) {
+    st[0] = __builtin_amdgcn_s_memrealtime();
+    st[1] = __builtin_amdgcn_s_memtime();
+  }
+#endif
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1, fr = lane & 15;
   const int Kb = K * 2;
@@ -222,6 +231,12 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
     if (t + 1 < T) ktile(t++, G4B<false>{}, G4B<true>{});
     ktile(t, G4B<false>{}, G4B<false>{});
 
+#ifdef DLI_GEMM_STAMPS
+    if (tid == 0) {
+      st[6] = __builtin_amdgcn_s_memrealtime();
+      st[7] = __builtin_amdgcn_s_memtime();
+    }
+#endif
     // the last MFMAs' results -> compiler-issued AGPR reads: 12+ wait states for an 8-pass XDL
     // write; the fence takes every accumulator "+a" so no read is hoisted above it
     asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
@@ -283,6 +298,12 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
     // (lgkmcnt(0) in the last k-tile), the barrier makes that hold for all of them
     g4_barrier();
   }
+#ifdef DLI_GEMM_STAMPS
+  if (tid == 0) {
+    st[2] = __builtin_amdgcn_s_memrealtime();
+    st[3] = __builtin_amdgcn_s_memtime();
+  }
+#endif
 }
 
 int g4_cus() {

@@ -24,7 +24,16 @@ constexpr int kRows = 2;
 typedef unsigned u32x4n __attribute__((ext_vector_type(4)));   // nontemporal-loadable 16 B
 constexpr int kUnroll = 4;
 
-template <int M>
+// Weight rows of a wave.  Plain: rows 2w, 2w+1.  SW (fused SwiGLU over a swiglu_interleave'd
+// gate|up weight, N = 2I rows): output column o = w, its gate row 32 (o / 16) + o % 16 and up
+// row 16 further, so the wave holds both factors of silu(gate) * up.
+template <bool SW>
+__device__ __forceinline__ int gemv_row(int wave, int r) {
+  if constexpr (SW) return 32 * (wave >> 4) + (wave & 15) + 16 * r;
+  return wave * kRows + r;
+}
+
+template <int M, bool SW = false>
 __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict__ x,
                                                           const bf16* __restrict__ W,
                                                           const bf16* __restrict__ bias,
@@ -32,7 +41,7 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int n0 = wave * kRows;
-  if (n0 >= N) return;
+  if ((SW ? 2 * wave : n0) >= N) return;
   float acc[M][kRows];
 #pragma unroll
   for (int m = 0; m < M; ++m)
@@ -41,7 +50,7 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
 
   const bf16* wrow[kRows];
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(n0 + r, N - 1) * K;
+  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<SW>(wave, r), N - 1) * K;
 
   constexpr int kStep = 64 * 8;  // elements per wave instruction
   for (int k0 = lane * 8; k0 < K; k0 += kStep * kUnroll) {
@@ -80,13 +89,19 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
         }
   }
 #pragma unroll
-  for (int m = 0; m < M; ++m)
+  for (int m = 0; m < M; ++m) {
+    float v[kRows];
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
-      const float v = wave_reduce_sum(acc[m][r]);
-      const int n = n0 + r;
-      if (lane == 0 && n < N) y[(size_t)m * N + n] = (bf16)(v + (bias ? (float)bias[n] : 0.f));
+      const int n = gemv_row<SW>(wave, r);
+      v[r] = wave_reduce_sum(acc[m][r]) + (bias ? (float)bias[n] : 0.f);
+      if (!SW && lane == 0 && n < N) y[(size_t)m * N + n] = (bf16)v[r];
     }
+    if (SW && lane == 0) {   // gate and up rounded to bf16 first, as the unfused path does
+      const float g = (float)(bf16)v[0], u = (float)(bf16)v[1];
+      y[(size_t)m * (N >> 1) + wave] = (bf16)(g / (1.f + __expf(-g)) * u);
+    }
+  }
 }
 
 // fp8 e4m3 weights [N, K] with one fp32 scale per output row: the same weight stream at half
@@ -95,18 +110,21 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
 // activations — bf16, or (XF8) the fp8 rows + per-row scales the fused RMSNorm quantiser already
 // produced, widened the same way; the scales are applied once to the reduced sum:
 // y = wscale[n] * (xscale[m]) * sum_k x[m, k] * w8[n, k].
-// WI8: int8 weights instead (LLM.int8 mode's [N, K] int8 + per-row scale), widened exactly to bf16
-__device__ __forceinline__ bf16x8 i8x8_to_bf16x8(uint2 v) {
-  bf16x8 o;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    o[j] = (bf16)(float)(int)(signed char)((v.x >> (8 * j)) & 0xFFu);
-    o[4 + j] = (bf16)(float)(int)(signed char)((v.y >> (8 * j)) & 0xFFu);
-  }
-  return o;
+// WI8: int8 weights instead (LLM.int8 mode's [N, K] int8 + per-row scale).  Each byte is biased
+// to unsigned (one v_xor_b32 per 4 bytes: b ^ 0x80 = b + 128), converted by v_cvt_f32_ubyteN
+// (exact; an integer below 256 has its bf16 in the top half of its fp32), and two top halves are
+// packed into one bf16 pair by v_perm_b32 -- 2.25 VALU per weight byte instead of a per-byte
+// sign-extend / convert / round chain.  The bias is removed once from the reduced sum:
+// sum x * w = sum x * (w + 128) - 128 * sum x, with sum x accumulated by one extra dot per pair.
+__device__ __forceinline__ bf16x2 u8pair_to_bf16x2(unsigned u, int j) {
+  const float lo = (float)((u >> (16 * j)) & 0xFFu);
+  const float hi = (float)((u >> (16 * j + 8)) & 0xFFu);
+  const unsigned p = __builtin_amdgcn_perm(__builtin_bit_cast(unsigned, hi),
+                                           __builtin_bit_cast(unsigned, lo), 0x07060302u);
+  return __builtin_bit_cast(bf16x2, p);
 }
 
-template <int M, bool XF8, bool WI8 = false>
+template <int M, bool XF8, bool WI8 = false, bool SW = false>
 __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __restrict__ xv_,
                                                               const float* __restrict__ xscale,
                                                               const uint8_t* __restrict__ W,
@@ -116,15 +134,18 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int n0 = wave * kRows;
-  if (n0 >= N) return;
+  if ((SW ? 2 * wave : n0) >= N) return;
   float acc[M][kRows];
 #pragma unroll
   for (int m = 0; m < M; ++m)
 #pragma unroll
     for (int r = 0; r < kRows; ++r) acc[m][r] = 0.f;
+  float sx[M];   // WI8: sum of this lane's x (the unsigned-bias correction)
+#pragma unroll
+  for (int m = 0; m < M; ++m) sx[m] = 0.f;
   const uint8_t* wrow[kRows];
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(n0 + r, N - 1) * K;
+  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<SW>(wave, r), N - 1) * K;
 
   constexpr int kStep = 64 * 16;  // elements per wave instruction
   for (int k0 = lane * 16; k0 < K; k0 += kStep * kUnroll) {
@@ -157,77 +178,129 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
         for (int m = 0; m < M; ++m) xv[u][m][0] = xv[u][m][1] = bf16x8{};
       }
     }
+    if constexpr (WI8) {
+      // sum x of this lane's k (once per row m, shared by the kRows weight rows)
+      const bf16x2 ones = {(bf16)1.f, (bf16)1.f};
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u)
+      for (int u = 0; u < kUnroll; ++u)
 #pragma unroll
-      for (int r = 0; r < kRows; ++r) {
-        const bf16x8 w0 = WI8 ? i8x8_to_bf16x8(uint2{wv[u][r][0], wv[u][r][1]})
-                              : fp8x8_to_bf16x8(uint2{wv[u][r][0], wv[u][r][1]});
-        const bf16x8 w1 = WI8 ? i8x8_to_bf16x8(uint2{wv[u][r][2], wv[u][r][3]})
-                              : fp8x8_to_bf16x8(uint2{wv[u][r][2], wv[u][r][3]});
+        for (int m = 0; m < M; ++m)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+          for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int m = 0; m < M; ++m) {
-            const bf16x2 x0 = {xv[u][m][0][2 * j], xv[u][m][0][2 * j + 1]};
-            const bf16x2 x1 = {xv[u][m][1][2 * j], xv[u][m][1][2 * j + 1]};
-            acc[m][r] = __builtin_amdgcn_fdot2_f32_bf16(x0, bf16x2{w0[2 * j], w0[2 * j + 1]},
-                                                        acc[m][r], false);
-            acc[m][r] = __builtin_amdgcn_fdot2_f32_bf16(x1, bf16x2{w1[2 * j], w1[2 * j + 1]},
-                                                        acc[m][r], false);
+            for (int j = 0; j < 4; ++j)
+              sx[m] = __builtin_amdgcn_fdot2_f32_bf16(
+                  bf16x2{xv[u][m][h][2 * j], xv[u][m][h][2 * j + 1]}, ones, sx[m], false);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+#pragma unroll
+          for (int d = 0; d < 4; ++d) {   // dword d = bytes 4d .. 4d+3 = x pairs (2d, 2d+1)
+            const unsigned ub = wv[u][r][d] ^ 0x80808080u;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const bf16x2 wp = u8pair_to_bf16x2(ub, j);
+              const int e = (d & 1) * 4 + 2 * j;   // element of the 8-wide x half d >> 1
+#pragma unroll
+              for (int m = 0; m < M; ++m)
+                acc[m][r] = __builtin_amdgcn_fdot2_f32_bf16(
+                    bf16x2{xv[u][m][d >> 1][e], xv[u][m][d >> 1][e + 1]}, wp, acc[m][r], false);
+            }
           }
-      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+          const bf16x8 w0 = fp8x8_to_bf16x8(uint2{wv[u][r][0], wv[u][r][1]});
+          const bf16x8 w1 = fp8x8_to_bf16x8(uint2{wv[u][r][2], wv[u][r][3]});
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+              const bf16x2 x0 = {xv[u][m][0][2 * j], xv[u][m][0][2 * j + 1]};
+              const bf16x2 x1 = {xv[u][m][1][2 * j], xv[u][m][1][2 * j + 1]};
+              acc[m][r] = __builtin_amdgcn_fdot2_f32_bf16(x0, bf16x2{w0[2 * j], w0[2 * j + 1]},
+                                                          acc[m][r], false);
+              acc[m][r] = __builtin_amdgcn_fdot2_f32_bf16(x1, bf16x2{w1[2 * j], w1[2 * j + 1]},
+                                                          acc[m][r], false);
+            }
+        }
+    }
+  }
+  if constexpr (WI8) {
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) acc[m][r] -= 128.f * sx[m];
   }
 #pragma unroll
-  for (int m = 0; m < M; ++m)
+  for (int m = 0; m < M; ++m) {
+    float v[kRows];
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
-      const float v = wave_reduce_sum(acc[m][r]);
-      const int n = n0 + r;
-      if (lane == 0 && n < N)
-        y[(size_t)m * N + n] =
-            (bf16)(v * wscale[n] * (XF8 ? xscale[m] : 1.f) + (bias ? (float)bias[n] : 0.f));
+      const int n = min(gemv_row<SW>(wave, r), N - 1);
+      v[r] = wave_reduce_sum(acc[m][r]) * wscale[n] * (XF8 ? xscale[m] : 1.f) +
+             (bias ? (float)bias[n] : 0.f);
+      if (!SW && lane == 0 && n0 + r < N) y[(size_t)m * N + n0 + r] = (bf16)v[r];
     }
+    if (SW && lane == 0) {   // gate and up rounded to bf16 first, as the unfused path does
+      const float g = (float)(bf16)v[0], u = (float)(bf16)v[1];
+      y[(size_t)m * (N >> 1) + wave] = (bf16)(g / (1.f + __expf(-g)) * u);
+    }
+  }
 }
 
 }  // namespace
 
+// swiglu: W is a swiglu_interleave'd gate|up weight [N = 2I, K], y is silu(gate) * up [M, I]
+template <bool XF8, bool WI8>
+static void launch_fp8_m(bf16* y, const void* x, const float* xscale, const uint8_t* W,
+                         const float* wscale, const bf16* bias, int M, int N, int K, bool swiglu,
+                         hipStream_t stream) {
+  const int waves = swiglu ? N / 2 : (N + kRows - 1) / kRows;
+  const int grid = (waves + 3) / 4;
+  if (M == 1 && swiglu)
+    skinny_gemm_fp8_kernel<1, XF8, WI8, true><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+  else if (M == 1)
+    skinny_gemm_fp8_kernel<1, XF8, WI8, false><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+  else if (swiglu)
+    skinny_gemm_fp8_kernel<2, XF8, WI8, true><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+  else
+    skinny_gemm_fp8_kernel<2, XF8, WI8, false><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+}
+
 int launch_skinny_gemm_fp8(bf16* y, const void* x, const float* xscale, const uint8_t* W,
                            const float* wscale, const bf16* bias, int M, int N, int K,
-                           hipStream_t stream) {
-  if (M < 1 || M > 2 || K % 16 != 0 || N < 1) return -1;
-  const int waves = (N + kRows - 1) / kRows;
-  const int grid = (waves + 3) / 4;
-  const bool xf8 = xscale != nullptr;
-  if (M == 1 && xf8)
-    skinny_gemm_fp8_kernel<1, true><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
-  else if (M == 1)
-    skinny_gemm_fp8_kernel<1, false><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
-  else if (xf8)
-    skinny_gemm_fp8_kernel<2, true><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+                           hipStream_t stream, bool swiglu) {
+  if (M < 1 || M > 2 || K % 16 != 0 || N < 1 || (swiglu && N % 32 != 0)) return -1;
+  if (xscale != nullptr)
+    launch_fp8_m<true, false>(y, x, xscale, W, wscale, bias, M, N, K, swiglu, stream);
   else
-    skinny_gemm_fp8_kernel<2, false><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+    launch_fp8_m<false, false>(y, x, xscale, W, wscale, bias, M, N, K, swiglu, stream);
   return 0;
 }
 
 int launch_skinny_gemm_int8(bf16* y, const bf16* x, const int8_t* W, const float* wscale,
-                            const bf16* bias, int M, int N, int K, hipStream_t stream) {
-  if (M < 1 || M > 2 || K % 16 != 0 || N < 1) return -1;
-  const int waves = (N + kRows - 1) / kRows;
-  const int grid = (waves + 3) / 4;
-  const uint8_t* w = reinterpret_cast<const uint8_t*>(W);
-  if (M == 1)
-    skinny_gemm_fp8_kernel<1, false, true><<<grid, 256, 0, stream>>>(x, nullptr, w, wscale, bias, y, N, K);
-  else
-    skinny_gemm_fp8_kernel<2, false, true><<<grid, 256, 0, stream>>>(x, nullptr, w, wscale, bias, y, N, K);
+                            const bf16* bias, int M, int N, int K, hipStream_t stream,
+                            bool swiglu) {
+  if (M < 1 || M > 2 || K % 16 != 0 || N < 1 || (swiglu && N % 32 != 0)) return -1;
+  launch_fp8_m<false, true>(y, x, nullptr, reinterpret_cast<const uint8_t*>(W), wscale, bias, M,
+                            N, K, swiglu, stream);
   return 0;
 }
 
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
-                       int K, hipStream_t stream) {
-  if (M < 1 || M > 4 || K % 8 != 0 || N < 1) return -1;
-  const int waves = (N + kRows - 1) / kRows;
+                       int K, hipStream_t stream, bool swiglu) {
+  if (M < 1 || M > 4 || K % 8 != 0 || N < 1 || (swiglu && (N % 32 != 0 || M > 2))) return -1;
+  const int waves = swiglu ? N / 2 : (N + kRows - 1) / kRows;
   const int grid = (waves + 3) / 4;
+  if (swiglu) {
+    if (M == 1) skinny_gemm_kernel<1, true><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K);
+    else skinny_gemm_kernel<2, true><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K);
+    return 0;
+  }
   switch (M) {
     case 1: skinny_gemm_kernel<1><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K); break;
     case 2: skinny_gemm_kernel<2><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K); break;

@@ -102,13 +102,21 @@ int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale
 int launch_splitk_reduce(bf16* C, const float* parts, int splits, size_t MN, hipStream_t stream);
 // fp32 elements of the workspace gemm_tile needs for splits == 0 (stream-K tail) on this device
 long long gemm_tile_sk_workspace_floats();
+// skinny GEMMs (gemv.hip); swiglu: W is a swiglu_interleave'd gate|up weight [2I, K] and y is
+// silu(gate) * up [M, I]
 int launch_skinny_gemm_fp8(bf16* y, const void* x, const float* xscale, const uint8_t* W,
                            const float* wscale, const bf16* bias, int M, int N, int K,
-                           hipStream_t stream);
+                           hipStream_t stream, bool swiglu = false);
 int launch_skinny_gemm_int8(bf16* y, const bf16* x, const int8_t* W, const float* wscale,
-                            const bf16* bias, int M, int N, int K, hipStream_t stream);
+                            const bf16* bias, int M, int N, int K, hipStream_t stream,
+                            bool swiglu = false);
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
-                       int K, hipStream_t stream);
+                       int K, hipStream_t stream, bool swiglu = false);
+// one-wave-per-SIMD 256x256 GEMM (gemm4.hip); epilogue 0 bf16, 1 fp32 partials, 2 SwiGLU,
+// 4 bf16 partials; grid <= 0: automatic persistent grid
+int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int splits,
+                 int epilogue, int grid, hipStream_t stream);
+int gemm4_grid(int items, int cus);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
                          bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,
                          hipStream_t stream, const void* x_parts = nullptr, int splits = 0,

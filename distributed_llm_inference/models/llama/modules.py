@@ -20,6 +20,8 @@ mathematically identical to the unsliced projection; it is accepted and ignored.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional, Tuple
 
 import torch
@@ -162,6 +164,11 @@ class LlamaMLP(nn.Module):
 
     def forward(self, normed: Optional[torch.Tensor], x_q=None, defer_reduce: bool = False):
         gp = self.gate_up_proj
+        if self.fused_swiglu and os.environ.get("DLI_GEMV_SWIGLU", "1") == "1":
+            # 1-2 decode rows: SwiGLU in the weight-streaming GEMV's epilogue (any weight dtype)
+            h = gp.gemv_swiglu(normed, x_q)
+            if h is not None:
+                return self.down_proj(h, defer_reduce=defer_reduce)
         if self.fused_swiglu and gp.is_int8:
             # SwiGLU in the int8 tile GEMM's epilogue, after the fused bf16 outlier product
             h = ops.llm_int8_linear(normed, gp.weight_int8, gp.weight_scale, gp.int8_threshold,

@@ -908,25 +908,32 @@ SKINNY_DISPATCH_M = 2   # Linear uses it up to here: measured faster than hipBLA
                         # every Llama-3-70B decode shape (5.3-6.9 vs 4.3-6.0 TB/s), slower at M = 4
 
 
+def _swiglu_ref(y: torch.Tensor) -> torch.Tensor:
+    """CPU reference of the fused-SwiGLU GEMV epilogue: bf16 gate / up, interleaved columns."""
+    return swiglu_interleaved(y.to(torch.bfloat16))
+
+
 def skinny_gemm_int8(x: torch.Tensor, wq: torch.Tensor, w_scale: torch.Tensor,
-                     bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     bias: Optional[torch.Tensor] = None, swiglu: bool = False) -> torch.Tensor:
     """``y = (x . wq^T) * w_scale`` for 1-2 bf16 decode rows with LLM.int8 weights (int8 [N, K],
     per-row scale): the weight stream at 1 byte per weight, activations kept in bf16 (no
-    activation quantisation, so no outlier split is needed: every column is exact bf16 x int8)."""
+    activation quantisation, so no outlier split is needed: every column is exact bf16 x int8).
+    ``swiglu``: ``wq`` is a swiglu_interleave'd gate|up weight; returns silu(gate) * up."""
     M, N = x.shape[0], wq.shape[0]
     if not _gpu(x):
         y = x.float() @ (wq.float() * w_scale.reshape(-1, 1)).t()
         if bias is not None:
             y = y + bias.float()
-        return y.to(torch.bfloat16)
-    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-    native().skinny_gemm_int8(out, x.contiguous(), wq, w_scale.reshape(-1).contiguous(), bias)
+        return _swiglu_ref(y) if swiglu else y.to(torch.bfloat16)
+    out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
+    native().skinny_gemm_int8(out, x.contiguous(), wq, w_scale.reshape(-1).contiguous(), bias,
+                              swiglu)
     return out
 
 
 def skinny_gemm_fp8(x: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor,
-                    x_scale: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None
-                    ) -> torch.Tensor:
+                    x_scale: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
+                    swiglu: bool = False) -> torch.Tensor:
     """``y = (x . w8^T) * w_scale (* x_scale)`` for 1-2 decode rows: fp8 e4m3 weights [N, K]
     with one scale per output row, activations bf16 or fp8 with one scale per row (the fused
     RMSNorm quantiser's output), weight-streaming GEMV (csrc/kernels/gemv.hip)."""
@@ -936,22 +943,25 @@ def skinny_gemm_fp8(x: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor,
         y = (xf @ (w8.float() * w_scale.reshape(-1, 1)).t())
         if bias is not None:
             y = y + bias.float()
-        return y.to(torch.bfloat16)
-    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+        return _swiglu_ref(y) if swiglu else y.to(torch.bfloat16)
+    out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
     native().skinny_gemm_fp8(out, x.contiguous(),
                              None if x_scale is None else x_scale.reshape(-1).contiguous(), w8,
-                             w_scale.reshape(-1).contiguous(), bias)
+                             w_scale.reshape(-1).contiguous(), bias, swiglu)
     return out
 
 
 def skinny_gemm(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``x [M, K] @ w[N, K]^T (+ bias)`` for M <= 4 with the weight-streaming HIP kernel."""
+                out: Optional[torch.Tensor] = None, swiglu: bool = False) -> torch.Tensor:
+    """``x [M, K] @ w[N, K]^T (+ bias)`` for M <= 4 with the weight-streaming HIP kernel;
+    ``swiglu`` (M <= 2): ``w`` is a swiglu_interleave'd gate|up weight, returns silu(gate) * up."""
     if not _gpu(x):
-        y = (x.float() @ w.float().t() + (bias.float() if bias is not None else 0.0)).to(x.dtype)
+        y = x.float() @ w.float().t() + (bias.float() if bias is not None else 0.0)
+        y = _swiglu_ref(y) if swiglu else y.to(x.dtype)
         return out.copy_(y) if out is not None else y
     if out is None:
-        out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-    native().skinny_gemm(out, x, w, bias)
+        out = torch.empty(x.shape[0], w.shape[0] // 2 if swiglu else w.shape[0], dtype=x.dtype,
+                          device=x.device)
+    native().skinny_gemm(out, x, w, bias, swiglu)
     return out
 

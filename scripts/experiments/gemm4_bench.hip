@@ -9,6 +9,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I distributed_llm_inference/csrc/kernels \
 //         scripts/experiments/gemm4_bench.hip -o tools_bin/gemm4_bench
 //   tools_bin/gemm4_bench [rounds] [gate|up grid override]
+#define DLI_GEMM_STAMPS 1
 #include "../../distributed_llm_inference/csrc/kernels/gemm_tile.hip"
 #include "../../distributed_llm_inference/csrc/kernels/gemm4.hip"
 
@@ -133,6 +134,10 @@ int main(int argc, char** argv) {
   };
   const int rounds = argc > 1 ? atoi(argv[1]) : 7;
   if (argc > 2) g_grid = atoi(argv[2]);
+  // every launch of this build writes per-workgroup stamps: point them at a buffer first
+  unsigned long long* sb;
+  CK(hipMalloc(&sb, (size_t)8192 * 64));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(dli::g_stamp_blk), &sb, sizeof(sb)));
   int bad = 0;
   for (auto& c : shapes)
     if (c.M <= 512) bad += check(c);
@@ -182,6 +187,36 @@ int main(int argc, char** argv) {
         t[v].push_back(ms * 1e3 / iters);
       }
     for (auto& x : t) std::sort(x.begin(), x.end());
+    // one stamped launch of each: per-workgroup cycles of the k-loops and the clock
+    for (int v = 0; v < 2; ++v) {
+      const int tiles = ((c.M + 255) / 256) * (c.N / 256);
+      const int items = tiles * c.splits;
+      const bool sk0 = v == 0 && tile_sk;
+      int wgs = v == 0 ? (sk0 ? tiles / 256 * 256 + 256 : items)
+                       : (grid > 0 ? grid : dli::gemm4_grid(items, 256));
+      CK(hipMemset(sb, 0, (size_t)8192 * 64));
+      run(v, 0);
+      CK(hipDeviceSynchronize());
+      std::vector<unsigned long long> h((size_t)wgs * 8);
+      CK(hipMemcpy(h.data(), sb, h.size() * 8, hipMemcpyDeviceToHost));
+      std::vector<double> cyc, clk;
+      for (int b = 0; b < wgs; ++b) {
+        const unsigned long long* q = &h[(size_t)b * 8];
+        if (q[3] <= q[1]) continue;
+        cyc.push_back((double)(q[3] - q[1]));
+        const double us = (q[2] - q[0]) / 100.0;
+        if (us > 0) clk.push_back((q[3] - q[1]) / us / 1e3);
+      }
+      std::sort(cyc.begin(), cyc.end());
+      std::sort(clk.begin(), clk.end());
+      // k-tiles per workgroup: gemm_tile = one item each (stream-K: ~ the same), gemm4 = items / grid
+      const double kt_item = (double)c.K * 2 / 128 / c.splits;
+      const double per_wg = v == 0 ? kt_item * (double)items / wgs : kt_item * ((double)items / wgs);
+      if (!cyc.empty())
+        printf("%-16s %s stamps: %d wgs, med %.0f cyc/wg = %.0f per k-tile, clock %.2f GHz\n",
+               c.name, v == 0 ? "gemm_tile" : "gemm4    ", wgs, cyc[cyc.size() / 2],
+               cyc[cyc.size() / 2] / per_wg, clk.empty() ? 0.0 : clk[clk.size() / 2]);
+    }
     const double fl = 2.0 * c.M * c.N * c.K;
     printf("%-16s M=%d N=%d K=%d s=%d | gemm_tile %.1f us (min %.1f, %.0f TF) | gemm4 %.1f us "
            "(min %.1f, %.0f TF) | gemm4/tile %.3f\n",

@@ -542,3 +542,34 @@ def test_gemm_tile_defer_reduce_feeds_rms_norm(gpu, monkeypatch, bf16_parts):
         assert (p.materialize().float() - y_ref.float()).abs().max().item() < tol
         assert (rb.float() - ra.float()).abs().max().item() < tol
         assert (b.float() - a.float()).abs().max().item() < 2e-2 * a.float().abs().max().item()
+
+
+@pytest.mark.parametrize("M", [512, 300, 40])
+@pytest.mark.parametrize("N,K,splits,epi", [(2048, 1024, 1, 0), (4096, 2048, 1, 2),
+                                            (1024, 4096, 3, 1), (1024, 4096, 4, 4),
+                                            (7680, 512, 1, 0)])
+def test_gemm4_bit_identical_to_gemm_tile(gpu, M, N, K, splits, epi):
+    """gemm4.hip (one wave per SIMD, asm-ordered k-loop) runs the same MFMA over the same k order
+    as gemm_tile: bf16 store, SwiGLU and fp32 / bf16 split-K partials must match it bit for bit,
+    for full and partial M tiles and persistent grids (7680 / 256 x 2 = 60 tiles, few CUs)."""
+    torch.manual_seed(M + N + splits)
+    a = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    b = (torch.randn(N, K, device=gpu) * 0.05).to(torch.bfloat16)
+    nat = ops.native()
+    if epi in (1, 4):
+        ref = torch.empty(splits, M, N, device=gpu, dtype=torch.float32)
+        nat.gemm_tile(torch.empty(M, 0, device=gpu, dtype=torch.bfloat16), a, b, splits, 1,
+                      ref.view(-1))
+        if epi == 4:
+            ref = ref.to(torch.bfloat16)
+        out = torch.empty(splits, M, N, device=gpu, dtype=ref.dtype)
+    else:
+        cols = N // 2 if epi == 2 else N
+        ref = torch.empty(M, cols, device=gpu, dtype=torch.bfloat16)
+        nat.gemm_tile(ref, a, b, 1, epi)
+        out = torch.empty_like(ref)
+    for grid in (0, 7):   # automatic persistent grid, and a small grid that loops over tiles
+        out.fill_(7.0)
+        nat.gemm4(out, a, b, splits, epi, grid)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), (grid, (out.float() - ref.float()).abs().max().item())

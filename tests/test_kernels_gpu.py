@@ -743,3 +743,35 @@ def test_skinny_gemm_int8(gpu, M):
     y = ops.skinny_gemm_int8(x, wq, ws)
     ref = x.float() @ (wq.float() * ws.reshape(-1, 1)).t()
     _close(y.float(), ref, 2e-2, 2e-2, "skinny int8")
+
+
+@pytest.mark.parametrize("wdtype", ["bf16", "fp8", "fp8-act", "int8"])
+@pytest.mark.parametrize("M", [1, 2])
+def test_skinny_gemm_swiglu(gpu, M, wdtype):
+    """Fused-SwiGLU GEMV epilogue (gemv.hip SW variants) on a swiglu_interleave'd gate|up
+    weight against silu(gate) * up of the fp32 product of the same dequantised operands."""
+    torch.manual_seed(7 * M + len(wdtype))
+    I, K = 1024, 4096
+    w = torch.randn(2 * I, K, device=gpu) * 0.02
+    wi = ops.swiglu_interleave(w.to(BF))
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    if wdtype == "bf16":
+        y = ops.skinny_gemm(x, wi, swiglu=True)
+        gu = x.float() @ wi.float().t()
+    elif wdtype == "int8":
+        wq, ws = ops.quantize_weight_int8(wi.float())
+        y = ops.skinny_gemm_int8(x, wq, ws, swiglu=True)
+        gu = x.float() @ (wq.float() * ws.reshape(-1, 1)).t()
+    else:
+        wq, ws = ops.quantize_weight_fp8(wi)
+        wd = wq.float() * ws.reshape(-1, 1)
+        if wdtype == "fp8-act":
+            xq, xs = ops.quant_rowwise(x)
+            y = ops.skinny_gemm_fp8(xq, wq, ws, xs, swiglu=True)
+            gu = (xq.float() * xs.reshape(-1, 1)) @ wd.t()
+        else:
+            y = ops.skinny_gemm_fp8(x, wq, ws, swiglu=True)
+            gu = x.float() @ wd.t()
+    ref = ops.swiglu_interleaved(gu.to(BF).cpu()).float()
+    assert y.shape == (M, I)
+    _close(y.float().cpu(), ref, 2e-2, 2e-2, f"skinny swiglu {wdtype}")
