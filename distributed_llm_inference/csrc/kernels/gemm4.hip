@@ -49,6 +49,26 @@ typedef __attribute__((address_space(3))) void g4_lds_t;
 template <bool V>
 struct G4B { static constexpr bool value = V; };
 
+// k-loop schedules (MFMA positions 0..127 of a k-tile): Q reads at q0 + qs*n, lgkmcnt(0) + B1
+// after MFMA b1, DMA piece j at d0 + ds*j, vmcnt(vm) + B2 after b2 (vm = DMA pieces issued
+// before b2), P reads at p0 + ps*n.  Constraints: Q reads < b1 < d0, pieces before b2 == vm,
+// b2 < p0, the last P read leaves the tail of the k-tile to retire it.
+template <int V> struct G4Sched;
+template <> struct G4Sched<0> {   // DMA in k-step 1, early wait (lead ~0.9 k-tile)
+  static constexpr int q0 = 2, qs = 2, b1 = 47, d0 = 64, ds = 2, b2 = 79, vm = 8, p0 = 81, ps = 2;
+};
+template <> struct G4Sched<1> {   // DMA right after B1 in k-step 0, wait in k-step 1 (lead ~1.25)
+  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 2, b2 = 88, vm = 16, p0 = 89, ps = 2;
+};
+template <> struct G4Sched<2> {   // hipBLASLt-like: late wait, dense P reads (lead ~1.4)
+  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 3, b2 = 104, vm = 16, p0 = 105, ps = 1;
+};
+template <> struct G4Sched<3> {   // dense Q reads, early DMA
+  static constexpr int q0 = 0, qs = 1, b1 = 24, d0 = 25, ds = 2, b2 = 80, vm = 16, p0 = 81, ps = 2;
+};
+constexpr int kG4Variants = 4;
+constexpr int kG4Default = 0;
+
 __device__ __forceinline__ float g4_silu(float x) { return x / (1.f + __expf(-x)); }
 
 __device__ __forceinline__ void g4_mfma(f32x4& acc, const bf16x8& w, const bf16x8& x) {
@@ -76,7 +96,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t g4_rsrc(const void* base, int 
                                            __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-template <int EPI>
+template <int EPI, int VAR>
 __global__ void __launch_bounds__(kG4Threads, 1)
 gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __restrict__ C,
              int M, int N, int K, int tiles_m, int tiles_n, int kps, int splits) {
@@ -200,28 +220,29 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
     // one k-tile.  DMA: issue tile t+2 into stage t&1; NEXT: read k-step 0 of tile t+1
     auto ktile = [&](int t, auto dma_c, auto next_c) {
       constexpr bool DMA = decltype(dma_c)::value, NEXT = decltype(next_c)::value;
+      using S = G4Sched<VAR>;
       const int s = t & 1;
-      // seg 1: k-step 0 MFMAs; k-step 1 fragments of this tile -> Q
+      // MFMA g of the k-tile (g < 64: k-step 0 on P, else k-step 1 on Q), and after it: the k-step
+      // 1 reads of this tile -> Q, B1, the DMA of tile t+2 into stage s, B2, the k-step 0 reads of
+      // tile t+1 -> P, at the positions the schedule S gives
 #pragma unroll
-      for (int k = 0; k < 64; ++k) {
-        mf(P, k);
-        if (k >= 2 && k < 34 && (k & 1) == 0) rd(Q, (k - 2) >> 1, 1, s);
-        if (k == 47) {   // this wave's reads of stage s are done -> after B1 every wave's are
+      for (int g = 0; g < 128; ++g) {
+        if (g < 64) mf(P, g); else mf(Q, g - 64);
+        if (g >= S::q0 && g < S::q0 + 16 * S::qs && (g - S::q0) % S::qs == 0)
+          rd(Q, (g - S::q0) / S::qs, 1, s);
+        if (g == S::b1) {   // this wave's reads of stage s are done -> after B1 every wave's are
           g4_sync_lds();
           if (DMA) g4_barrier();
         }
-      }
-      // seg 2: k-step 1 MFMAs; DMA of tile t+2 into stage s; k-step 0 of tile t+1 -> P
-#pragma unroll
-      for (int k = 0; k < 64; ++k) {
-        mf(Q, k);
-        if (DMA && k < 32 && (k & 1) == 0) dma(t + 2, k >> 1);
+        if (DMA && g >= S::d0 && g < S::d0 + 16 * S::ds && (g - S::d0) % S::ds == 0)
+          dma(t + 2, (g - S::d0) / S::ds);
         if (NEXT) {
-          if (k == 15) {   // own DMA of tile t+1 landed (all but the 8 pieces just issued)
-            if (DMA) g4_vmcnt<8>(); else g4_vmcnt<0>();
+          if (g == S::b2) {   // own DMA of tile t+1 landed (all but the pieces of t+2 since)
+            if (DMA) g4_vmcnt<S::vm>(); else g4_vmcnt<0>();
             g4_barrier();
           }
-          if (k >= 17 && k < 49 && (k & 1) == 1) rd(P, (k - 17) >> 1, 0, s ^ 1);
+          if (g >= S::p0 && g < S::p0 + 16 * S::ps && (g - S::p0) % S::ps == 0)
+            rd(P, (g - S::p0) / S::ps, 0, s ^ 1);
         }
       }
       if (NEXT) g4_sync_lds();
@@ -327,8 +348,35 @@ int gemm4_grid(int items, int cus) {
 // C = A . B^T on the one-wave-per-SIMD kernel.  epilogue 0: bf16 [M, N]; 2: fused SwiGLU ([M,
 // N/2], B rows in swiglu_interleave order); with splits > 1: 1 = fp32 partials [splits, M, N],
 // 4 = bf16 partials [splits, M, N] (into C; the consumer sums them).  grid <= 0: automatic.
+template <int VAR>
+static int launch_gemm4_v(void* C, const bf16* a, const bf16* b, int M, int N, int K, int tiles_m,
+                          int tiles_n, int kps, int splits, int epilogue, int grid,
+                          hipStream_t stream) {
+  switch (epilogue) {
+    case kG4Bf16:
+      gemm4_kernel<kG4Bf16, VAR><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      break;
+    case kG4F32:
+      gemm4_kernel<kG4F32, VAR><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      break;
+    case kG4SwiGLU:
+      gemm4_kernel<kG4SwiGLU, VAR><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      break;
+    case kG4Bf16Part:
+      gemm4_kernel<kG4Bf16Part, VAR><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      break;
+    default:
+      return -4;
+  }
+  return 0;
+}
+
+// C = A . B^T on the one-wave-per-SIMD kernel.  epilogue 0: bf16 [M, N]; 2: fused SwiGLU ([M,
+// N/2], B rows in swiglu_interleave order); with splits > 1: 1 = fp32 partials [splits, M, N],
+// 4 = bf16 partials [splits, M, N] (into C; the consumer sums them).  grid <= 0: automatic.
+// variant < 0: the default k-loop schedule (G4Sched), else that one (A/B experiments).
 int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int splits,
-                 int epilogue, int grid, hipStream_t stream) {
+                 int epilogue, int grid, hipStream_t stream, int variant) {
   if (M <= 0 || N % 256 != 0 || (K * 2) % 128 != 0 || splits < 1) return -1;
   const int kt = K * 2 / 128;
   if (splits > kt) return -2;
@@ -341,23 +389,14 @@ int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int
   if (grid > items) grid = items;
   const bf16* a = reinterpret_cast<const bf16*>(A);
   const bf16* b = reinterpret_cast<const bf16*>(B);
-  switch (epilogue) {
-    case kG4Bf16:
-      gemm4_kernel<kG4Bf16><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
-      break;
-    case kG4F32:
-      gemm4_kernel<kG4F32><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
-      break;
-    case kG4SwiGLU:
-      gemm4_kernel<kG4SwiGLU><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
-      break;
-    case kG4Bf16Part:
-      gemm4_kernel<kG4Bf16Part><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
-      break;
-    default:
-      return -4;
+  if (variant < 0) variant = kG4Default;
+  switch (variant) {
+    case 0: return launch_gemm4_v<0>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
+    case 1: return launch_gemm4_v<1>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
+    case 2: return launch_gemm4_v<2>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
+    case 3: return launch_gemm4_v<3>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
   }
-  return 0;
+  return -5;
 }
 
 }  // namespace dli

@@ -113,9 +113,9 @@ int launch_skinny_gemm_int8(bf16* y, const bf16* x, const int8_t* W, const float
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
                        int K, hipStream_t stream, bool swiglu = false);
 // one-wave-per-SIMD 256x256 GEMM (gemm4.hip); epilogue 0 bf16, 1 fp32 partials, 2 SwiGLU,
-// 4 bf16 partials; grid <= 0: automatic persistent grid
+// 4 bf16 partials; grid <= 0: automatic persistent grid; variant < 0: default k-loop schedule
 int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int splits,
-                 int epilogue, int grid, hipStream_t stream);
+                 int epilogue, int grid, hipStream_t stream, int variant = -1);
 int gemm4_grid(int items, int cus);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
                          bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,

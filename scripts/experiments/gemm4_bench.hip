@@ -43,6 +43,8 @@ static float bf2f(__bf16 v) { return (float)v; }
 struct Shape { const char* name; int M, N, K, splits, epi; };
 
 static int g_grid = 0;
+static int g_var = 0;   // gemm4 schedule variant under check
+constexpr int kVars = 4;
 
 static int check(const Shape& c) {
   int bad = 0;
@@ -64,7 +66,7 @@ static int check(const Shape& c) {
     int r0 = dli::launch_gemm_tile(C0, A, B, nullptr, nullptr, W0, M, N, K, c.splits, sk ? 1 : 0,
                                    0, 0, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
     int r1 = dli::launch_gemm4(sk ? (void*)W1 : (void*)C1, A, B, M, N, K, c.splits, sk ? 1 : 0,
-                               0, 0);
+                               0, 0, g_var);
     CK(hipDeviceSynchronize());
     if (r0 || r1) { printf("launch rc %d %d\n", r0, r1); return 1; }
     size_t nbytes = sk ? (size_t)c.splits * M * N * 4 : (size_t)M * N * 2;
@@ -73,13 +75,13 @@ static int check(const Shape& c) {
     CK(hipMemcpy(h1.data(), sk ? (void*)W1 : (void*)C1, nbytes, hipMemcpyDeviceToHost));
     size_t diff = 0;
     for (size_t i = 0; i < nbytes; ++i) diff += h0[i] != h1[i];
-    printf("check %-16s M=%d %s: %zu differing bytes of %zu\n", c.name, M,
+    printf("check v%d %-16s M=%d %s: %zu differing bytes of %zu\n", g_var, c.name, M,
            sk ? "fp32 partials" : "bf16 store", diff, nbytes);
     bad += diff != 0;
     if (sk) {   // bf16 partials: the same sums rounded
       __bf16* P1;
       CK(hipMalloc(&P1, (size_t)c.splits * M * N * 2));
-      int r2 = dli::launch_gemm4(P1, A, B, M, N, K, c.splits, 4, 0, 0);
+      int r2 = dli::launch_gemm4(P1, A, B, M, N, K, c.splits, 4, 0, 0, g_var);
       CK(hipDeviceSynchronize());
       if (r2) { printf("bf16 parts rc %d\n", r2); return 1; }
       std::vector<__bf16> hp((size_t)c.splits * M * N);
@@ -94,7 +96,7 @@ static int check(const Shape& c) {
     if (!sk && c.epi == 2) {
       __bf16* S;
       CK(hipMalloc(&S, (size_t)M * N));
-      int r2 = dli::launch_gemm4(S, A, B, M, N, K, 1, 2, 0, 0);
+      int r2 = dli::launch_gemm4(S, A, B, M, N, K, 1, 2, 0, 0, g_var);
       CK(hipDeviceSynchronize());
       if (r2) { printf("swiglu rc %d\n", r2); return 1; }
       std::vector<__bf16> hs((size_t)M * N / 2), hp((size_t)M * N);
@@ -139,8 +141,9 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&sb, (size_t)8192 * 64));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(dli::g_stamp_blk), &sb, sizeof(sb)));
   int bad = 0;
-  for (auto& c : shapes)
-    if (c.M <= 512) bad += check(c);
+  for (g_var = 0; g_var < kVars; ++g_var)
+    for (auto& c : shapes)
+      if (c.M <= 512) bad += check(c);
   if (bad) { printf("CHECK FAILED\n"); return 2; }
   for (auto& c : shapes) {
     const size_t wbytes = (size_t)c.N * c.K * 2;
@@ -166,18 +169,18 @@ int main(int argc, char** argv) {
                                               tile_sk ? 0 : c.splits, epi, 0, 0, nullptr, nullptr,
                                               0, nullptr, nullptr, nullptr)
                       : dli::launch_gemm4(c.splits > 1 ? (void*)ws : (void*)C, A, B[i % sets],
-                                          c.M, c.N, c.K, c.splits, epi, grid, 0);
+                                          c.M, c.N, c.K, c.splits, epi, grid, 0, v - 1);
       if (rc) { fprintf(stderr, "rc %d\n", rc); exit(1); }
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    std::vector<double> t[2];
+    std::vector<double> t[1 + kVars];
     const int iters = c.M > 512 ? 5 : 20;
-    for (int v = 0; v < 2; ++v) for (int i = 0; i < 5; ++i) run(v, i);
+    for (int v = 0; v <= kVars; ++v) for (int i = 0; i < 5; ++i) run(v, i);
     for (int r = 0; r < rounds; ++r)
-      for (int vv = 0; vv < 2; ++vv) {
-        const int v = (r & 1) ? 1 - vv : vv;
+      for (int vv = 0; vv <= kVars; ++vv) {
+        const int v = (r & 1) ? kVars - vv : vv;
         CK(hipEventRecord(e0));
         for (int i = 0; i < iters; ++i) run(v, i);
         CK(hipEventRecord(e1));
@@ -188,7 +191,7 @@ int main(int argc, char** argv) {
       }
     for (auto& x : t) std::sort(x.begin(), x.end());
     // one stamped launch of each: per-workgroup cycles of the k-loops and the clock
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v <= kVars; ++v) {
       const int tiles = ((c.M + 255) / 256) * (c.N / 256);
       const int items = tiles * c.splits;
       const bool sk0 = v == 0 && tile_sk;
@@ -213,16 +216,17 @@ int main(int argc, char** argv) {
       const double kt_item = (double)c.K * 2 / 128 / c.splits;
       const double per_wg = v == 0 ? kt_item * (double)items / wgs : kt_item * ((double)items / wgs);
       if (!cyc.empty())
-        printf("%-16s %s stamps: %d wgs, med %.0f cyc/wg = %.0f per k-tile, clock %.2f GHz\n",
-               c.name, v == 0 ? "gemm_tile" : "gemm4    ", wgs, cyc[cyc.size() / 2],
+        printf("%-16s %s%d stamps: %d wgs, med %.0f cyc/wg = %.0f per k-tile, clock %.2f GHz\n",
+               c.name, v == 0 ? "gemm_tile" : "gemm4 v", v - 1, wgs, cyc[cyc.size() / 2],
                cyc[cyc.size() / 2] / per_wg, clk.empty() ? 0.0 : clk[clk.size() / 2]);
     }
     const double fl = 2.0 * c.M * c.N * c.K;
-    printf("%-16s M=%d N=%d K=%d s=%d | gemm_tile %.1f us (min %.1f, %.0f TF) | gemm4 %.1f us "
-           "(min %.1f, %.0f TF) | gemm4/tile %.3f\n",
-           c.name, c.M, c.N, c.K, c.splits, t[0][t[0].size() / 2], t[0][0],
-           fl / t[0][t[0].size() / 2] / 1e6, t[1][t[1].size() / 2], t[1][0],
-           fl / t[1][t[1].size() / 2] / 1e6, t[1][t[1].size() / 2] / t[0][t[0].size() / 2]);
+    printf("%-16s M=%d N=%d K=%d s=%d | gemm_tile %.1f us (min %.1f, %.0f TF)", c.name, c.M, c.N,
+           c.K, c.splits, t[0][t[0].size() / 2], t[0][0], fl / t[0][t[0].size() / 2] / 1e6);
+    for (int v = 1; v <= kVars; ++v)
+      printf(" | v%d %.1f us (%.0f TF, %.3f)", v - 1, t[v][t[v].size() / 2],
+             fl / t[v][t[v].size() / 2] / 1e6, t[v][t[v].size() / 2] / t[0][t[0].size() / 2]);
+    printf("\n");
     fflush(stdout);
     CK(hipFree(A));
     for (auto& b : B) CK(hipFree(b));
