@@ -275,6 +275,10 @@ def main():
     }
     if world > 1:
         res["stage_ranges"] = [r["stage"] for r in per_rank]
+        res["head_rotation"] = any(r.get("head_rotation") for r in per_rank)
+        fb = sorted({r["fallback_from"] for r in per_rank if r.get("fallback_from")})
+        if fb:   # the data plane is NOT RCCL: say so at the top level, not only per rank
+            res["transport_fallback_from"] = fb
         res["per_rank"] = per_rank
     if a.model != "llama-3-70b":
         # the headline metric names its model; a run of another model says what it measured

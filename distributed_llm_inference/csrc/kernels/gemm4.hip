@@ -35,6 +35,8 @@
 //     workgroups of one XCD take neighbouring work items (shared A / B panels in its L2).
 #include "kernels.h"
 
+#include <utility>
+
 namespace dli {
 
 namespace {
@@ -48,6 +50,13 @@ typedef __attribute__((address_space(3))) void g4_lds_t;
 
 template <bool V>
 struct G4B { static constexpr bool value = V; };
+
+// compile-time loop: f(std::integral_constant<int, i>) for i in the sequence, fully unrolled
+// (a 128-step #pragma unroll loop of this size is not unrolled by the compiler)
+template <typename F, int... I>
+__device__ __forceinline__ void g4_static_for(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
 
 // k-loop schedules (MFMA positions 0..127 of a k-tile): Q reads at q0 + qs*n, lgkmcnt(0) + B1
 // after MFMA b1, DMA piece j at d0 + ds*j, vmcnt(vm) + B2 after b2 (vm = DMA pieces issued
@@ -225,26 +234,24 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
       // MFMA g of the k-tile (g < 64: k-step 0 on P, else k-step 1 on Q), and after it: the k-step
       // 1 reads of this tile -> Q, B1, the DMA of tile t+2 into stage s, B2, the k-step 0 reads of
       // tile t+1 -> P, at the positions the schedule S gives
-#pragma unroll
-      for (int g = 0; g < 128; ++g) {
-        if (g < 64) mf(P, g); else mf(Q, g - 64);
-        if (g >= S::q0 && g < S::q0 + 16 * S::qs && (g - S::q0) % S::qs == 0)
+      g4_static_for(std::make_integer_sequence<int, 128>{}, [&](auto G) {
+        constexpr int g = decltype(G)::value;
+        if constexpr (g < 64) mf(P, g); else mf(Q, g - 64);
+        if constexpr (g >= S::q0 && g < S::q0 + 16 * S::qs && (g - S::q0) % S::qs == 0)
           rd(Q, (g - S::q0) / S::qs, 1, s);
-        if (g == S::b1) {   // this wave's reads of stage s are done -> after B1 every wave's are
+        if constexpr (g == S::b1) {   // this wave's reads of stage s done -> after B1 every wave's
           g4_sync_lds();
           if (DMA) g4_barrier();
         }
-        if (DMA && g >= S::d0 && g < S::d0 + 16 * S::ds && (g - S::d0) % S::ds == 0)
+        if constexpr (DMA && g >= S::d0 && g < S::d0 + 16 * S::ds && (g - S::d0) % S::ds == 0)
           dma(t + 2, (g - S::d0) / S::ds);
-        if (NEXT) {
-          if (g == S::b2) {   // own DMA of tile t+1 landed (all but the pieces of t+2 since)
-            if (DMA) g4_vmcnt<S::vm>(); else g4_vmcnt<0>();
-            g4_barrier();
-          }
-          if (g >= S::p0 && g < S::p0 + 16 * S::ps && (g - S::p0) % S::ps == 0)
-            rd(P, (g - S::p0) / S::ps, 0, s ^ 1);
+        if constexpr (NEXT && g == S::b2) {   // own DMA of tile t+1 landed (all but t+2's since)
+          if (DMA) g4_vmcnt<S::vm>(); else g4_vmcnt<0>();
+          g4_barrier();
         }
-      }
+        if constexpr (NEXT && g >= S::p0 && g < S::p0 + 16 * S::ps && (g - S::p0) % S::ps == 0)
+          rd(P, (g - S::p0) / S::ps, 0, s ^ 1);
+      });
       if (NEXT) g4_sync_lds();
     };
     int t = 0;
