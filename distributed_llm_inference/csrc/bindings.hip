@@ -700,13 +700,48 @@ void gemm4(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue, int
 }
 
 // ------------------------------------------------------------------------------ skinny GEMM
+// fused input RMSNorm of a skinny GEMM's rows: norm_w given -> x' = rmsnorm(x + res_in) * norm_w
+struct GemvNormArgs {
+  dli::GemvNorm nm{};
+  bool on = false;
+};
+static GemvNormArgs gemv_norm_args(const Tensor& x, const optional<Tensor>& norm_w,
+                                   const optional<Tensor>& res_in, const optional<Tensor>& res_out,
+                                   double eps, const char* what) {
+  GemvNormArgs a;
+  if (!norm_w.has_value()) {
+    TORCH_CHECK(!res_in.has_value() && !res_out.has_value(), what, ": residuals need norm_w");
+    return a;
+  }
+  CHECK_IN(*norm_w); CHECK_BF16(*norm_w); CHECK_BF16(x);
+  TORCH_CHECK(norm_w->numel() == x.size(1) && x.size(0) <= 2, what, ": norm_w [K], M <= 2");
+  a.on = true;
+  a.nm.w = bp(*norm_w);
+  a.nm.eps = (float)eps;
+  if (res_in.has_value()) {
+    CHECK_IN(*res_in); CHECK_BF16(*res_in);
+    TORCH_CHECK(res_in->sizes() == x.sizes(), what, ": res_in shape");
+    a.nm.res_in = bp(*res_in);
+  }
+  if (res_out.has_value()) {
+    CHECK_IN(*res_out); CHECK_BF16(*res_out);
+    TORCH_CHECK(res_out->sizes() == x.sizes() && res_in.has_value(), what, ": res_out needs res_in");
+    TORCH_CHECK(res_out->data_ptr() != res_in->data_ptr(), what, ": res_out must not alias res_in");
+    a.nm.res_out = bp(*res_out);
+  }
+  return a;
+}
+
 // swiglu: w is a swiglu_interleave'd gate|up weight [2I, K]; out = silu(gate) * up [M, I]
 static int64_t gemv_out_cols(int64_t N, bool swiglu, const char* what) {
   TORCH_CHECK(!swiglu || N % 32 == 0, what, ": swiglu needs 32 | N");
   return swiglu ? N / 2 : N;
 }
 
-void skinny_gemm(Tensor out, Tensor x, Tensor w, optional<Tensor> bias, bool swiglu) {
+void skinny_gemm(Tensor out, Tensor x, Tensor w, optional<Tensor> bias, bool swiglu,
+                 optional<Tensor> norm_w, optional<Tensor> res_in, optional<Tensor> res_out,
+                 double eps) {
+  const GemvNormArgs na = gemv_norm_args(x, norm_w, res_in, res_out, eps, "skinny_gemm");
   CHECK_IN(out); CHECK_IN(x); CHECK_IN(w);
   CHECK_BF16(out); CHECK_BF16(x); CHECK_BF16(w);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm: 2-D tensors");
@@ -723,12 +758,14 @@ void skinny_gemm(Tensor out, Tensor x, Tensor w, optional<Tensor> bias, bool swi
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_rc(dli::launch_skinny_gemm(bp(out), bp(x), bp(w), b, (int)M, (int)N, (int)K,
-                                   cur_stream(), swiglu), "skinny_gemm");
+                                   cur_stream(), swiglu, na.on ? &na.nm : nullptr), "skinny_gemm");
 }
 
 // int8 weights [N, K] with fp32 per-row scales [N], bf16 activations (weight-only dequantisation)
 void skinny_gemm_int8(Tensor out, Tensor x, Tensor w, Tensor wscale, optional<Tensor> bias,
-                      bool swiglu) {
+                      bool swiglu, optional<Tensor> norm_w, optional<Tensor> res_in,
+                      optional<Tensor> res_out, double eps) {
+  const GemvNormArgs na = gemv_norm_args(x, norm_w, res_in, res_out, eps, "skinny_gemm_int8");
   CHECK_IN(out); CHECK_IN(x); CHECK_IN(w); CHECK_IN(wscale);
   CHECK_BF16(out); CHECK_BF16(x); CHECK_F32(wscale);
   TORCH_CHECK(w.scalar_type() == at::kChar, "skinny_gemm_int8: int8 weights");
@@ -747,13 +784,17 @@ void skinny_gemm_int8(Tensor out, Tensor x, Tensor w, Tensor wscale, optional<Te
   const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
   check_rc(dli::launch_skinny_gemm_int8(bp(out), bp(x), w.data_ptr<int8_t>(),
                                         wscale.data_ptr<float>(), b, (int)M, (int)N, (int)K,
-                                        cur_stream(), swiglu), "skinny_gemm_int8");
+                                        cur_stream(), swiglu, na.on ? &na.nm : nullptr),
+           "skinny_gemm_int8");
 }
 
 // fp8 e4m3 weights [N, K] (1-byte storage), fp32 per-row scales [N]; activations bf16, or fp8
 // [M, K] with fp32 per-row scales xscale [M] (the fused RMSNorm quantiser's output)
 void skinny_gemm_fp8(Tensor out, Tensor x, optional<Tensor> xscale, Tensor w, Tensor wscale,
-                     optional<Tensor> bias, bool swiglu) {
+                     optional<Tensor> bias, bool swiglu, optional<Tensor> norm_w,
+                     optional<Tensor> res_in, optional<Tensor> res_out, double eps) {
+  const GemvNormArgs na = gemv_norm_args(x, norm_w, res_in, res_out, eps, "skinny_gemm_fp8");
+  TORCH_CHECK(!na.on || !xscale.has_value(), "skinny_gemm_fp8: the fused norm takes bf16 rows");
   CHECK_IN(out); CHECK_IN(x); CHECK_IN(w); CHECK_IN(wscale);
   CHECK_BF16(out); CHECK_F32(wscale);
   TORCH_CHECK(w.element_size() == 1, "skinny_gemm_fp8: 1-byte (fp8 e4m3) weights");
@@ -782,7 +823,8 @@ void skinny_gemm_fp8(Tensor out, Tensor x, optional<Tensor> xscale, Tensor w, Te
   check_rc(dli::launch_skinny_gemm_fp8(bp(out), x.data_ptr(), xs,
                                        static_cast<const uint8_t*>(w.data_ptr()),
                                        wscale.data_ptr<float>(), b, (int)M, (int)N, (int)K,
-                                       cur_stream(), swiglu), "skinny_gemm_fp8");
+                                       cur_stream(), swiglu, na.on ? &na.nm : nullptr),
+           "skinny_gemm_fp8");
 }
 
 }  // namespace
@@ -846,14 +888,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("skinny_gemm_int8", &skinny_gemm_int8,
         "y = (x . W8^T) * scale (+ bias), int8 weights, bf16 rows, M <= 2 (weight-streaming GEMV)",
         py::arg("out"), py::arg("x"), py::arg("w"), py::arg("wscale"), py::arg("bias") = py::none(),
-        py::arg("swiglu") = false);
+        py::arg("swiglu") = false, py::arg("norm_w") = py::none(), py::arg("res_in") = py::none(),
+        py::arg("res_out") = py::none(), py::arg("eps") = 1e-5);
   m.def("skinny_gemm_fp8", &skinny_gemm_fp8,
         "y = (x . W8^T) * scale (+ bias), fp8 e4m3 weights, M <= 2 (weight-streaming GEMV)",
         py::arg("out"), py::arg("x"), py::arg("xscale"), py::arg("w"), py::arg("wscale"),
-        py::arg("bias") = py::none(), py::arg("swiglu") = false);
+        py::arg("bias") = py::none(), py::arg("swiglu") = false, py::arg("norm_w") = py::none(),
+        py::arg("res_in") = py::none(), py::arg("res_out") = py::none(), py::arg("eps") = 1e-5);
   m.def("skinny_gemm", &skinny_gemm, "y = x . W^T (+ bias) for M <= 4 (weight-streaming GEMV)",
         py::arg("out"), py::arg("x"), py::arg("w"), py::arg("bias") = py::none(),
-        py::arg("swiglu") = false);
+        py::arg("swiglu") = false, py::arg("norm_w") = py::none(), py::arg("res_in") = py::none(),
+        py::arg("res_out") = py::none(), py::arg("eps") = 1e-5);
   register_rccl(m);
   register_streams(m);
 }

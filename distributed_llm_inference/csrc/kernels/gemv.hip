@@ -24,6 +24,56 @@ constexpr int kRows = 2;
 typedef unsigned u32x4n __attribute__((ext_vector_type(4)));   // nontemporal-loadable 16 B
 constexpr int kUnroll = 4;
 
+// NORM (fused input RMSNorm, 1-2 decode rows): the GEMV's x is rmsnorm(x + res_in) * w, computed
+// once per workgroup into LDS by the same arithmetic as norm.hip's rms_norm_kernel (same
+// per-thread vector assignment, fma order and block reduction at 256 threads), so the normalised
+// row is bit-identical to the separate kernel's; workgroup 0 also writes res_out = x + res_in
+// (the residual stream; it must not alias res_in, which every workgroup reads).  Saves one
+// launch per norm in the 1-2 row decode step, where every launch costs its dispatch latency.
+extern __shared__ __attribute__((aligned(16))) char gemv_lds[];
+
+template <int M>
+__device__ __forceinline__ void gemv_norm_prologue(const bf16* __restrict__ x, const GemvNorm& nm,
+                                                   int K) {
+  __shared__ float scratch[8];
+  const int nvec = K >> 3;
+  bf16* xs = reinterpret_cast<bf16*>(gemv_lds);
+  const bf16x8* w8 = reinterpret_cast<const bf16x8*>(nm.w);
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (size_t)m * K);
+    const bf16x8* rr = nm.res_in ? reinterpret_cast<const bf16x8*>(nm.res_in + (size_t)m * K) : nullptr;
+    bf16x8* ro = nm.res_out ? reinterpret_cast<bf16x8*>(nm.res_out + (size_t)m * K) : nullptr;
+    bf16x8* xo = reinterpret_cast<bf16x8*>(xs + (size_t)m * K);
+    float ss = 0.f;
+    for (int idx = threadIdx.x; idx < nvec; idx += blockDim.x) {
+      bf16x8 a = xr[idx];
+      if (rr != nullptr) {
+        const bf16x8 r = rr[idx];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = (bf16)((float)a[j] + (float)r[j]);
+        if (ro != nullptr && blockIdx.x == 0) ro[idx] = a;
+      }
+      xo[idx] = a;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = (float)a[j];
+        ss = __builtin_fmaf(v, v, ss);
+      }
+    }
+    ss = block_reduce_sum(ss, scratch);
+    const float rstd = rsqrtf(ss / (float)K + nm.eps);
+    for (int idx = threadIdx.x; idx < nvec; idx += blockDim.x) {   // own elements only
+      const bf16x8 a = xo[idx], ww = w8[idx];
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)a[j] * rstd * (float)ww[j]);
+      xo[idx] = o;
+    }
+  }
+  __syncthreads();
+}
+
 // Weight rows of a wave.  Plain: rows 2w, 2w+1.  SW (fused SwiGLU over a swiglu_interleave'd
 // gate|up weight, N = 2I rows): output column o = w, its gate row 32 (o / 16) + o % 16 and up
 // row 16 further, so the wave holds both factors of silu(gate) * up.
@@ -33,14 +83,17 @@ __device__ __forceinline__ int gemv_row(int wave, int r) {
   return wave * kRows + r;
 }
 
-template <int M, bool SW = false>
-__global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict__ x,
+template <int M, bool SW = false, bool NORM = false>
+__global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict__ x_in,
                                                           const bf16* __restrict__ W,
                                                           const bf16* __restrict__ bias,
-                                                          bf16* __restrict__ y, int N, int K) {
+                                                          bf16* __restrict__ y, int N, int K,
+                                                          GemvNorm nm) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int n0 = wave * kRows;
+  if constexpr (NORM) gemv_norm_prologue<M>(x_in, nm, K);   // every thread, before any exit
+  const bf16* x = NORM ? reinterpret_cast<const bf16*>(gemv_lds) : x_in;
   if ((SW ? 2 * wave : n0) >= N) return;
   float acc[M][kRows];
 #pragma unroll
@@ -124,16 +177,20 @@ __device__ __forceinline__ bf16x2 u8pair_to_bf16x2(unsigned u, int j) {
   return __builtin_bit_cast(bf16x2, p);
 }
 
-template <int M, bool XF8, bool WI8 = false, bool SW = false>
-__global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __restrict__ xv_,
+template <int M, bool XF8, bool WI8 = false, bool SW = false, bool NORM = false>
+__global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __restrict__ x_in,
                                                               const float* __restrict__ xscale,
                                                               const uint8_t* __restrict__ W,
                                                               const float* __restrict__ wscale,
                                                               const bf16* __restrict__ bias,
-                                                              bf16* __restrict__ y, int N, int K) {
+                                                              bf16* __restrict__ y, int N, int K,
+                                                              GemvNorm nm) {
+  static_assert(!(NORM && XF8), "the fused norm feeds bf16 rows");
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int n0 = wave * kRows;
+  if constexpr (NORM) gemv_norm_prologue<M>(static_cast<const bf16*>(x_in), nm, K);
+  const void* xv_ = NORM ? static_cast<const void*>(gemv_lds) : x_in;
   if ((SW ? 2 * wave : n0) >= N) return;
   float acc[M][kRows];
 #pragma unroll
@@ -254,58 +311,87 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
 
 }  // namespace
 
-// swiglu: W is a swiglu_interleave'd gate|up weight [N = 2I, K], y is silu(gate) * up [M, I]
+// swiglu: W is a swiglu_interleave'd gate|up weight [N = 2I, K], y is silu(gate) * up [M, I];
+// nm (optional): the fused input RMSNorm (x is then the un-normalised row, bf16)
+template <bool XF8, bool WI8, int M, bool SW>
+static void launch_fp8_t(bf16* y, const void* x, const float* xscale, const uint8_t* W,
+                         const float* wscale, const bf16* bias, int N, int K, const GemvNorm* nm,
+                         int grid, hipStream_t stream) {
+  if constexpr (!XF8) {
+    if (nm != nullptr) {
+      skinny_gemm_fp8_kernel<M, XF8, WI8, SW, true><<<grid, 256, (size_t)M * K * 2, stream>>>(
+          x, xscale, W, wscale, bias, y, N, K, *nm);
+      return;
+    }
+  }
+  skinny_gemm_fp8_kernel<M, XF8, WI8, SW, false><<<grid, 256, 0, stream>>>(
+      x, xscale, W, wscale, bias, y, N, K, GemvNorm{});
+}
+
 template <bool XF8, bool WI8>
 static void launch_fp8_m(bf16* y, const void* x, const float* xscale, const uint8_t* W,
                          const float* wscale, const bf16* bias, int M, int N, int K, bool swiglu,
-                         hipStream_t stream) {
+                         const GemvNorm* nm, hipStream_t stream) {
   const int waves = swiglu ? N / 2 : (N + kRows - 1) / kRows;
   const int grid = (waves + 3) / 4;
-  if (M == 1 && swiglu)
-    skinny_gemm_fp8_kernel<1, XF8, WI8, true><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
-  else if (M == 1)
-    skinny_gemm_fp8_kernel<1, XF8, WI8, false><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
-  else if (swiglu)
-    skinny_gemm_fp8_kernel<2, XF8, WI8, true><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
-  else
-    skinny_gemm_fp8_kernel<2, XF8, WI8, false><<<grid, 256, 0, stream>>>(x, xscale, W, wscale, bias, y, N, K);
+  if (M == 1 && swiglu) launch_fp8_t<XF8, WI8, 1, true>(y, x, xscale, W, wscale, bias, N, K, nm, grid, stream);
+  else if (M == 1) launch_fp8_t<XF8, WI8, 1, false>(y, x, xscale, W, wscale, bias, N, K, nm, grid, stream);
+  else if (swiglu) launch_fp8_t<XF8, WI8, 2, true>(y, x, xscale, W, wscale, bias, N, K, nm, grid, stream);
+  else launch_fp8_t<XF8, WI8, 2, false>(y, x, xscale, W, wscale, bias, N, K, nm, grid, stream);
+}
+
+static bool gemv_norm_ok(const GemvNorm* nm, int M, int K) {
+  return nm == nullptr || (nm->w != nullptr && M <= 2 && (size_t)M * K * 2 <= 65536 &&
+                           (nm->res_out == nullptr || nm->res_out != nm->res_in));
 }
 
 int launch_skinny_gemm_fp8(bf16* y, const void* x, const float* xscale, const uint8_t* W,
                            const float* wscale, const bf16* bias, int M, int N, int K,
-                           hipStream_t stream, bool swiglu) {
+                           hipStream_t stream, bool swiglu, const GemvNorm* nm) {
   if (M < 1 || M > 2 || K % 16 != 0 || N < 1 || (swiglu && N % 32 != 0)) return -1;
+  if (!gemv_norm_ok(nm, M, K) || (nm != nullptr && xscale != nullptr)) return -2;
   if (xscale != nullptr)
-    launch_fp8_m<true, false>(y, x, xscale, W, wscale, bias, M, N, K, swiglu, stream);
+    launch_fp8_m<true, false>(y, x, xscale, W, wscale, bias, M, N, K, swiglu, nullptr, stream);
   else
-    launch_fp8_m<false, false>(y, x, xscale, W, wscale, bias, M, N, K, swiglu, stream);
+    launch_fp8_m<false, false>(y, x, xscale, W, wscale, bias, M, N, K, swiglu, nm, stream);
   return 0;
 }
 
 int launch_skinny_gemm_int8(bf16* y, const bf16* x, const int8_t* W, const float* wscale,
                             const bf16* bias, int M, int N, int K, hipStream_t stream,
-                            bool swiglu) {
+                            bool swiglu, const GemvNorm* nm) {
   if (M < 1 || M > 2 || K % 16 != 0 || N < 1 || (swiglu && N % 32 != 0)) return -1;
+  if (!gemv_norm_ok(nm, M, K)) return -2;
   launch_fp8_m<false, true>(y, x, nullptr, reinterpret_cast<const uint8_t*>(W), wscale, bias, M,
-                            N, K, swiglu, stream);
+                            N, K, swiglu, nm, stream);
   return 0;
 }
 
+template <int M, bool SW>
+static void launch_bf16_t(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int N, int K,
+                          const GemvNorm* nm, int grid, hipStream_t stream) {
+  if (nm != nullptr && M <= 2)
+    skinny_gemm_kernel<M, SW, true><<<grid, 256, (size_t)M * K * 2, stream>>>(x, W, bias, y, N, K, *nm);
+  else
+    skinny_gemm_kernel<M, SW, false><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K, GemvNorm{});
+}
+
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
-                       int K, hipStream_t stream, bool swiglu) {
+                       int K, hipStream_t stream, bool swiglu, const GemvNorm* nm) {
   if (M < 1 || M > 4 || K % 8 != 0 || N < 1 || (swiglu && (N % 32 != 0 || M > 2))) return -1;
+  if (!gemv_norm_ok(nm, M, K)) return -2;
   const int waves = swiglu ? N / 2 : (N + kRows - 1) / kRows;
   const int grid = (waves + 3) / 4;
   if (swiglu) {
-    if (M == 1) skinny_gemm_kernel<1, true><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K);
-    else skinny_gemm_kernel<2, true><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K);
+    if (M == 1) launch_bf16_t<1, true>(y, x, W, bias, N, K, nm, grid, stream);
+    else launch_bf16_t<2, true>(y, x, W, bias, N, K, nm, grid, stream);
     return 0;
   }
   switch (M) {
-    case 1: skinny_gemm_kernel<1><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K); break;
-    case 2: skinny_gemm_kernel<2><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K); break;
-    case 3: skinny_gemm_kernel<3><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K); break;
-    case 4: skinny_gemm_kernel<4><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K); break;
+    case 1: launch_bf16_t<1, false>(y, x, W, bias, N, K, nm, grid, stream); break;
+    case 2: launch_bf16_t<2, false>(y, x, W, bias, N, K, nm, grid, stream); break;
+    case 3: launch_bf16_t<3, false>(y, x, W, bias, N, K, nullptr, grid, stream); break;
+    case 4: launch_bf16_t<4, false>(y, x, W, bias, N, K, nullptr, grid, stream); break;
   }
   return 0;
 }

@@ -103,15 +103,23 @@ int launch_splitk_reduce(bf16* C, const float* parts, int splits, size_t MN, hip
 // fp32 elements of the workspace gemm_tile needs for splits == 0 (stream-K tail) on this device
 long long gemm_tile_sk_workspace_floats();
 // skinny GEMMs (gemv.hip); swiglu: W is a swiglu_interleave'd gate|up weight [2I, K] and y is
-// silu(gate) * up [M, I]
+// silu(gate) * up [M, I].  nm: fused input RMSNorm of x (M <= 2, bf16 rows): x' = rmsnorm(x +
+// res_in) * w, res_out = x + res_in (written once; must not alias res_in)
+struct GemvNorm {
+  const bf16* res_in;   // nullptr: no residual add
+  bf16* res_out;        // nullptr: not written
+  const bf16* w;        // [K]
+  float eps;
+};
 int launch_skinny_gemm_fp8(bf16* y, const void* x, const float* xscale, const uint8_t* W,
                            const float* wscale, const bf16* bias, int M, int N, int K,
-                           hipStream_t stream, bool swiglu = false);
+                           hipStream_t stream, bool swiglu = false, const GemvNorm* nm = nullptr);
 int launch_skinny_gemm_int8(bf16* y, const bf16* x, const int8_t* W, const float* wscale,
                             const bf16* bias, int M, int N, int K, hipStream_t stream,
-                            bool swiglu = false);
+                            bool swiglu = false, const GemvNorm* nm = nullptr);
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
-                       int K, hipStream_t stream, bool swiglu = false);
+                       int K, hipStream_t stream, bool swiglu = false,
+                       const GemvNorm* nm = nullptr);
 // one-wave-per-SIMD 256x256 GEMM (gemm4.hip); epilogue 0 bf16, 1 fp32 partials, 2 SwiGLU,
 // 4 bf16 partials; grid <= 0: automatic persistent grid; variant < 0: default k-loop schedule
 int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int splits,

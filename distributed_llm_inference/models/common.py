@@ -81,35 +81,53 @@ class Linear(nn.Module):
             return 0
         return ops.tile_gemm_splits(x.shape[0], self.out_features, self.in_features)
 
+    def gemv_ok(self, rows: int, swiglu: bool = False, bf16_rows: bool = True) -> bool:
+        """Whether :meth:`gemv` takes a product of ``rows`` GPU rows (bf16 rows, or with
+        ``bf16_rows=False`` the fused quantiser's fp8 rows for fp8 weights)."""
+        if not 1 <= rows <= ops.SKINNY_DISPATCH_M:
+            return False
+        if swiglu and (self.bias is not None or self.out_features % 32):
+            return False
+        if self.weight_int8 is not None:
+            return bf16_rows and self.in_features % 16 == 0 and \
+                os.environ.get("DLI_INT8_GEMV", "1") == "1"
+        if self.weight_fp8 is not None:
+            return self.in_features % 16 == 0
+        return bf16_rows and self.in_features % 8 == 0
+
+    def gemv(self, x: Optional[torch.Tensor], x_q: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+             swiglu: bool = False, norm: Optional["ops.RowNorm"] = None) -> Optional[torch.Tensor]:
+        """The weight-streaming GEMV (1-2 decode rows on the GPU) of this Linear, with its
+        optional fused epilogue (``swiglu``: this is a swiglu_interleave'd gate|up projection,
+        silu(gate) * up is returned) and fused prologue (``norm``: x is the un-normalised row and
+        the GEMV applies the input RMSNorm itself).  None when the GEMV does not take the
+        product (more rows, CPU, shapes it does not cover) -- the caller falls back."""
+        src = x if x is not None else (x_q[0] if x_q is not None else None)
+        if (src is None or not src.is_cuda or src.dim() != 2 or isinstance(x_q, ops.MxFp8)
+                or not self.gemv_ok(src.shape[0], swiglu, bf16_rows=x is not None)):
+            return None
+        if x is not None and (x.dtype != torch.bfloat16 or not x.is_contiguous()):
+            return None
+        if norm is not None and x is None:
+            return None
+        if self.weight_int8 is not None:
+            return ops.skinny_gemm_int8(x, self.weight_int8, self.weight_scale, self.bias,
+                                        swiglu=swiglu, norm=norm)
+        if self.weight_fp8 is not None:
+            if norm is not None or (x_q is None and x is not None and
+                                    os.environ.get("DLI_FP8_GEMV", "1") == "1"):
+                return ops.skinny_gemm_fp8(x, self.weight_fp8, self.weight_scale, None, self.bias,
+                                           swiglu=swiglu, norm=norm)
+            xq, xs = x_q if x_q is not None else ops.quant_rowwise(x)
+            return ops.skinny_gemm_fp8(xq, self.weight_fp8, self.weight_scale, xs, self.bias,
+                                       swiglu=swiglu)
+        return ops.skinny_gemm(x, self.weight, self.bias, swiglu=swiglu, norm=norm)
+
     def gemv_swiglu(self, x: Optional[torch.Tensor],
                     x_q: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
                     ) -> Optional[torch.Tensor]:
-        """silu(gate) * up straight from the weight-streaming GEMV (1-2 decode rows on the GPU,
-        this Linear being a swiglu_interleave'd gate|up projection): the GEMV's epilogue applies
-        SwiGLU, so no [M, 2I] intermediate and no silu_mul launch.  None when the GEMV does not
-        take the product (more rows, CPU, shapes it does not cover) -- the caller falls back."""
-        if self.bias is not None or self.out_features % 32:
-            return None
-        src = x if x is not None else (x_q[0] if x_q is not None else None)
-        if (src is None or not src.is_cuda or src.dim() != 2 or isinstance(x_q, ops.MxFp8)
-                or not 1 <= src.shape[0] <= ops.SKINNY_DISPATCH_M):
-            return None
-        if self.weight_int8 is not None:
-            if (x is None or x.dtype != torch.bfloat16 or self.in_features % 16
-                    or os.environ.get("DLI_INT8_GEMV", "1") != "1"):
-                return None
-            return ops.skinny_gemm_int8(x, self.weight_int8, self.weight_scale, swiglu=True)
-        if self.weight_fp8 is not None:
-            if self.in_features % 16:
-                return None
-            if x_q is None and x is not None and x.dtype == torch.bfloat16 and \
-                    os.environ.get("DLI_FP8_GEMV", "1") == "1":
-                return ops.skinny_gemm_fp8(x, self.weight_fp8, self.weight_scale, swiglu=True)
-            xq, xs = x_q if x_q is not None else ops.quant_rowwise(x)
-            return ops.skinny_gemm_fp8(xq, self.weight_fp8, self.weight_scale, xs, swiglu=True)
-        if x is None or x.dtype != torch.bfloat16 or not x.is_contiguous() or self.in_features % 8:
-            return None
-        return ops.skinny_gemm(x, self.weight, swiglu=True)
+        """silu(gate) * up straight from the GEMV's epilogue (see :meth:`gemv`)."""
+        return self.gemv(x, x_q, swiglu=True)
 
     def forward(self, x: Optional[torch.Tensor],
                 x_q: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,

@@ -75,9 +75,17 @@ class LlamaAttention(nn.Module):
                              device=device)
 
     def forward(self, normed: Optional[torch.Tensor], meta: AttnMetadata, k_cache: torch.Tensor,
-                v_cache: torch.Tensor, cos_sin: torch.Tensor, x_q=None, defer_reduce: bool = False):
-        # split-K partials of the QKV GEMM are summed inside the RoPE / KV-write kernel
-        qkv = self.qkv_proj(normed, x_q, defer_reduce=True)
+                v_cache: torch.Tensor, cos_sin: torch.Tensor, x_q=None, defer_reduce: bool = False,
+                norm: Optional[ops.RowNorm] = None):
+        """``norm``: ``normed`` is the UN-normalised row and the QKV GEMV applies the input
+        RMSNorm itself (1-2 decode rows, LlamaDecoderLayer._forward_gemv)."""
+        if norm is not None:
+            qkv = self.qkv_proj.gemv(normed, norm=norm)
+            if qkv is None:
+                raise RuntimeError("fused-norm QKV: the GEMV does not take this product")
+        else:
+            # split-K partials of the QKV GEMM are summed inside the RoPE / KV-write kernel
+            qkv = self.qkv_proj(normed, x_q, defer_reduce=True)
         T = qkv.shape[0]
         q, q_sink = ops.rope_cache(qkv, meta.positions, meta.slot_mapping, cos_sin, self.num_heads,
                                    self.num_kv_heads, self.head_dim, k_cache, v_cache,
@@ -162,8 +170,14 @@ class LlamaMLP(nn.Module):
                 w.weight.data.copy_(perm(w.weight.data))
         self.fused_swiglu = on
 
-    def forward(self, normed: Optional[torch.Tensor], x_q=None, defer_reduce: bool = False):
+    def forward(self, normed: Optional[torch.Tensor], x_q=None, defer_reduce: bool = False,
+                norm: Optional[ops.RowNorm] = None):
         gp = self.gate_up_proj
+        if norm is not None:   # un-normalised rows: the gate|up GEMV applies the RMSNorm itself
+            h = gp.gemv(normed, swiglu=True, norm=norm)
+            if h is None:
+                raise RuntimeError("fused-norm gate|up: the GEMV does not take this product")
+            return self.down_proj(h, defer_reduce=defer_reduce)
         if self.fused_swiglu and os.environ.get("DLI_GEMV_SWIGLU", "1") == "1":
             # 1-2 decode rows: SwiGLU in the weight-streaming GEMV's epilogue (any weight dtype)
             h = gp.gemv_swiglu(normed, x_q)
@@ -230,6 +244,8 @@ class LlamaDecoderLayer(nn.Module):
         """``defer_out``: the returned hidden state may be ``ops.SplitKPartials`` (the next
         layer's input RMSNorm reduces them); the O projection's partials always go straight
         into the post-attention RMSNorm."""
+        if self._gemv_norms(hidden):
+            return self._forward_gemv(hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out)
         if self.self_attn.qkv_proj.is_fp8:
             return self._forward_fp8(hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out)
         first = residual is None
@@ -244,6 +260,36 @@ class LlamaDecoderLayer(nn.Module):
         normed, residual = self.post_attention_layernorm(
             attn, residual, residual_out=torch.empty_like(residual) if first else None)
         return self.mlp(normed, defer_reduce=defer_out), residual
+
+    def _gemv_norms(self, hidden) -> bool:
+        """1-2 decode rows whose four projections all run on the weight-streaming GEMV: the two
+        RMSNorms then run inside the QKV and gate|up GEMVs (``_forward_gemv``)."""
+        if (not isinstance(hidden, torch.Tensor) or not hidden.is_cuda or hidden.dim() != 2
+                or hidden.dtype != torch.bfloat16 or not hidden.is_contiguous()
+                or os.environ.get("DLI_GEMV_NORM", "1") != "1"):
+            return False
+        M = hidden.shape[0]
+        a, m = self.self_attn, self.mlp
+        return (M * self.hidden_size * 2 <= 65536 and m.fused_swiglu
+                and a.qkv_proj.gemv_ok(M) and a.o_proj.gemv_ok(M)
+                and m.gate_up_proj.gemv_ok(M, swiglu=True) and m.down_proj.gemv_ok(M))
+
+    def _forward_gemv(self, hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out=False):
+        """1-2 decode rows: input RMSNorm fused into the QKV GEMV, post-attention RMSNorm into the
+        gate|up GEMV (which also applies SwiGLU): per layer QKV, RoPE/KV, attention, O, gate|up,
+        down -- two launches fewer than the unfused order, same normalised rows (bit-identical
+        norm arithmetic, gemv.hip).  The residual stream moves to fresh buffers (the GEMV writes
+        it once while every workgroup still reads the old one)."""
+        ln1, ln2 = self.input_layernorm, self.post_attention_layernorm
+        if residual is None:   # first layer of the stage: the input IS the residual
+            n1, res = ops.RowNorm(ln1.weight, ln1.eps), hidden
+        else:
+            res = torch.empty_like(residual)
+            n1 = ops.RowNorm(ln1.weight, ln1.eps, residual, res)
+        attn = self.self_attn(hidden, meta, k_cache, v_cache, cos_sin, norm=n1)
+        res2 = torch.empty_like(res)
+        n2 = ops.RowNorm(ln2.weight, ln2.eps, res, res2)
+        return self.mlp(attn, norm=n2, defer_reduce=defer_out), res2
 
     def _forward_fp8(self, hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out=False):
         """fp8 weights: every RMSNorm is fused with the fp8 quantisation of the GEMM input that

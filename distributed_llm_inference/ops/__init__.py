@@ -908,37 +908,68 @@ SKINNY_DISPATCH_M = 2   # Linear uses it up to here: measured faster than hipBLA
                         # every Llama-3-70B decode shape (5.3-6.9 vs 4.3-6.0 TB/s), slower at M = 4
 
 
+class RowNorm:
+    """The input RMSNorm a skinny GEMM applies to its rows itself (1-2 decode rows, GPU): the
+    GEMV multiplies ``rmsnorm(x + res_in) * w`` (bit-identical to :func:`rms_norm`'s output) and
+    writes ``res_out = x + res_in`` once -- one launch instead of two.  ``res_out`` must be a
+    different buffer than ``res_in``; ``res_in=None``: no residual add (x itself is normalised)."""
+
+    __slots__ = ("w", "eps", "res_in", "res_out")
+
+    def __init__(self, w: torch.Tensor, eps: float, res_in: Optional[torch.Tensor] = None,
+                 res_out: Optional[torch.Tensor] = None):
+        if res_out is not None and (res_in is None or res_out.data_ptr() == res_in.data_ptr()):
+            raise ValueError("RowNorm: res_out needs res_in and must not alias it")
+        self.w, self.eps, self.res_in, self.res_out = w, float(eps), res_in, res_out
+
+    def apply(self, x: torch.Tensor) -> torch.Tensor:
+        """The normalised rows (CPU reference path; also writes res_out)."""
+        y, _ = rms_norm(x, self.w, self.eps, residual=self.res_in,
+                        residual_out=self.res_out if self.res_in is not None else None)
+        return y
+
+    def kwargs(self) -> dict:
+        return dict(norm_w=self.w, res_in=self.res_in, res_out=self.res_out, eps=self.eps)
+
+
 def _swiglu_ref(y: torch.Tensor) -> torch.Tensor:
     """CPU reference of the fused-SwiGLU GEMV epilogue: bf16 gate / up, interleaved columns."""
     return swiglu_interleaved(y.to(torch.bfloat16))
 
 
 def skinny_gemm_int8(x: torch.Tensor, wq: torch.Tensor, w_scale: torch.Tensor,
-                     bias: Optional[torch.Tensor] = None, swiglu: bool = False) -> torch.Tensor:
+                     bias: Optional[torch.Tensor] = None, swiglu: bool = False,
+                     norm: Optional[RowNorm] = None) -> torch.Tensor:
     """``y = (x . wq^T) * w_scale`` for 1-2 bf16 decode rows with LLM.int8 weights (int8 [N, K],
     per-row scale): the weight stream at 1 byte per weight, activations kept in bf16 (no
     activation quantisation, so no outlier split is needed: every column is exact bf16 x int8).
     ``swiglu``: ``wq`` is a swiglu_interleave'd gate|up weight; returns silu(gate) * up."""
     M, N = x.shape[0], wq.shape[0]
     if not _gpu(x):
+        if norm is not None:
+            x = norm.apply(x)
         y = x.float() @ (wq.float() * w_scale.reshape(-1, 1)).t()
         if bias is not None:
             y = y + bias.float()
         return _swiglu_ref(y) if swiglu else y.to(torch.bfloat16)
     out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
     native().skinny_gemm_int8(out, x.contiguous(), wq, w_scale.reshape(-1).contiguous(), bias,
-                              swiglu)
+                              swiglu, **(norm.kwargs() if norm is not None else {}))
     return out
 
 
 def skinny_gemm_fp8(x: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor,
                     x_scale: Optional[torch.Tensor] = None, bias: Optional[torch.Tensor] = None,
-                    swiglu: bool = False) -> torch.Tensor:
+                    swiglu: bool = False, norm: Optional[RowNorm] = None) -> torch.Tensor:
     """``y = (x . w8^T) * w_scale (* x_scale)`` for 1-2 decode rows: fp8 e4m3 weights [N, K]
     with one scale per output row, activations bf16 or fp8 with one scale per row (the fused
     RMSNorm quantiser's output), weight-streaming GEMV (csrc/kernels/gemv.hip)."""
     M, N = x.shape[0], w8.shape[0]
+    if norm is not None and x_scale is not None:
+        raise ValueError("skinny_gemm_fp8: the fused norm takes bf16 rows")
     if not _gpu(x):
+        if norm is not None:
+            x = norm.apply(x)
         xf = x.float() * x_scale.reshape(-1, 1) if x_scale is not None else x.float()
         y = (xf @ (w8.float() * w_scale.reshape(-1, 1)).t())
         if bias is not None:
@@ -947,21 +978,25 @@ def skinny_gemm_fp8(x: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor,
     out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
     native().skinny_gemm_fp8(out, x.contiguous(),
                              None if x_scale is None else x_scale.reshape(-1).contiguous(), w8,
-                             w_scale.reshape(-1).contiguous(), bias, swiglu)
+                             w_scale.reshape(-1).contiguous(), bias, swiglu,
+                             **(norm.kwargs() if norm is not None else {}))
     return out
 
 
 def skinny_gemm(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
-                out: Optional[torch.Tensor] = None, swiglu: bool = False) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, swiglu: bool = False,
+                norm: Optional[RowNorm] = None) -> torch.Tensor:
     """``x [M, K] @ w[N, K]^T (+ bias)`` for M <= 4 with the weight-streaming HIP kernel;
     ``swiglu`` (M <= 2): ``w`` is a swiglu_interleave'd gate|up weight, returns silu(gate) * up."""
     if not _gpu(x):
+        if norm is not None:
+            x = norm.apply(x)
         y = x.float() @ w.float().t() + (bias.float() if bias is not None else 0.0)
         y = _swiglu_ref(y) if swiglu else y.to(x.dtype)
         return out.copy_(y) if out is not None else y
     if out is None:
         out = torch.empty(x.shape[0], w.shape[0] // 2 if swiglu else w.shape[0], dtype=x.dtype,
                           device=x.device)
-    native().skinny_gemm(out, x, w, bias, swiglu)
+    native().skinny_gemm(out, x, w, bias, swiglu, **(norm.kwargs() if norm is not None else {}))
     return out
 

@@ -775,3 +775,37 @@ def test_skinny_gemm_swiglu(gpu, M, wdtype):
     ref = ops.swiglu_interleaved(gu.to(BF).cpu()).float()
     assert y.shape == (M, I)
     _close(y.float().cpu(), ref, 2e-2, 2e-2, f"skinny swiglu {wdtype}")
+
+
+@pytest.mark.parametrize("wdtype", ["bf16", "fp8", "int8"])
+@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("swiglu", [False, True])
+@pytest.mark.parametrize("resid", [False, True])
+def test_skinny_gemm_fused_norm_bit_identical(gpu, M, wdtype, swiglu, resid):
+    """The GEMV's fused input RMSNorm (gemv.hip gemv_norm_prologue) reproduces rms_norm's
+    normalised rows bit for bit, so fused == rms_norm -> GEMV exactly; res_out = x + res_in."""
+    torch.manual_seed(M * 31 + swiglu * 7 + resid)
+    N, K = (2048 if swiglu else 1536), 8192
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    res = torch.randn(M, K, device=gpu, dtype=BF) if resid else None
+    res0 = res.clone() if resid else None
+    nw = (1 + 0.1 * torch.randn(K, device=gpu)).to(BF)
+    w = (torch.randn(N, K, device=gpu) * 0.02).to(BF)
+    if wdtype == "fp8":
+        wq, ws = ops.quantize_weight_fp8(w)
+        f = lambda xx, **kw: ops.skinny_gemm_fp8(xx, wq, ws, None, swiglu=swiglu, **kw)  # noqa: E731
+    elif wdtype == "int8":
+        wq, ws = ops.quantize_weight_int8(w.float())
+        f = lambda xx, **kw: ops.skinny_gemm_int8(xx, wq, ws, swiglu=swiglu, **kw)  # noqa: E731
+    else:
+        f = lambda xx, **kw: ops.skinny_gemm(xx, w, swiglu=swiglu, **kw)  # noqa: E731
+    r_sep = res.clone() if resid else None
+    normed, _ = ops.rms_norm(x, nw, 1e-5, residual=r_sep)      # r_sep <- x + res in place
+    ref = f(normed)
+    r_out = torch.empty_like(x) if resid else None
+    got = f(x, norm=ops.RowNorm(nw, 1e-5, res, r_out))
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), (got.float() - ref.float()).abs().max().item()
+    if resid:
+        assert torch.equal(r_out, r_sep)
+        assert torch.equal(res, res0)   # res_in untouched (not aliased)
