@@ -640,3 +640,24 @@ def test_8bit_gemv_vs_quantised_path_bounded(gpu, monkeypatch, mode):
     eab = ((a - b).norm() / ref.norm()).item()
     print(mode, "GEMV", ea, "quantised path", eb, "difference", eab)
     assert ea < 0.01 and eb < 0.06 and ea <= eb + 1e-3 and eab < 0.06, (ea, eb, eab)
+
+
+@pytest.mark.parametrize("quantize", [False, "fp8", "int8"])
+def test_gemv_fused_norm_path_matches_unfused_decode(gpu, monkeypatch, quantize):
+    """1-2 row decode with the RMSNorms fused into the QKV / gate|up GEMVs (DLI_GEMV_NORM=1,
+    default) against the unfused order: bf16 weights give identical greedy tokens; 8-bit
+    weights (the fused path feeds bf16 rows instead of quantised ones) stay close."""
+    prompts = [list(range(3, 40))]
+
+    def run(flag):
+        monkeypatch.setenv("DLI_GEMV_NORM", flag)
+        eng = _engine(graphs=False, quantize=quantize)
+        outs = eng.generate(prompts, SamplingParams(max_tokens=12, temperature=0.0))
+        return [o.output for o in outs]
+
+    a, b = run("1"), run("0")
+    if not quantize:
+        assert a == b
+    else:
+        agree = sum(x == y for x, y in zip(a[0], b[0])) / len(a[0])
+        assert agree >= 0.5, (a, b)
