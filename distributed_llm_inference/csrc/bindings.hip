@@ -827,6 +827,82 @@ void skinny_gemm_fp8(Tensor out, Tensor x, optional<Tensor> xscale, Tensor w, Te
            "skinny_gemm_fp8");
 }
 
+// 1-2 decode rows: the fused QKV GEMV whose epilogue does rope_cache's work (q rotated into q_out,
+// k rotated and v written into the paged caches), optionally with the fused input RMSNorm.
+// w: bf16 [N, K], fp8 e4m3 / int8 [N, K] with fp32 per-row wscale; N = (nh + 2 nkv) D.
+void skinny_gemm_qkv_rope(Tensor q_out, Tensor x, Tensor w, optional<Tensor> wscale,
+                          optional<Tensor> bias, optional<Tensor> positions,
+                          optional<Tensor> slot_mapping, optional<Tensor> cos_sin, Tensor k_cache,
+                          Tensor v_cache, int64_t nh, int64_t nkv, double k_scale, double v_scale,
+                          optional<Tensor> norm_w, optional<Tensor> res_in,
+                          optional<Tensor> res_out, double eps) {
+  CHECK_IN(q_out); CHECK_IN(x); CHECK_IN(w);
+  CHECK_BF16(q_out); CHECK_BF16(x);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && q_out.dim() == 3, "skinny_gemm_qkv_rope: shapes");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0), D = q_out.size(2);
+  TORCH_CHECK(M >= 1 && M <= 2 && w.size(1) == K && q_out.size(0) == M && q_out.size(1) == nh &&
+                  N == (nh + 2 * nkv) * D,
+              "skinny_gemm_qkv_rope: x [M <= 2, K], w [(nh + 2 nkv) D, K], q_out [M, nh, D]");
+  const bool fp8 = check_cache(k_cache, v_cache, nkv, D);
+  TORCH_CHECK(k_scale > 0 && v_scale > 0, "KV scales must be positive");
+  dli::GemvRope rp{};
+  rp.kv_fp8 = fp8 ? 1 : 0;
+  rp.k_inv_scale = (float)(1.0 / k_scale);
+  rp.v_inv_scale = (float)(1.0 / v_scale);
+  if (positions.has_value()) {
+    CHECK_IN(*positions); CHECK_I32(*positions);
+    TORCH_CHECK(positions->numel() == M, "positions must have M entries");
+    rp.positions = positions->data_ptr<int>();
+  }
+  if (slot_mapping.has_value()) {
+    CHECK_IN(*slot_mapping); CHECK_I64(*slot_mapping);
+    TORCH_CHECK(slot_mapping->numel() == M, "slot_mapping must have M entries");
+    rp.slot_mapping = reinterpret_cast<const long*>(slot_mapping->data_ptr<int64_t>());
+  }
+  if (cos_sin.has_value()) {
+    CHECK_IN(*cos_sin); CHECK_F32(*cos_sin);
+    TORCH_CHECK(cos_sin->dim() == 2 && cos_sin->size(1) == D && positions.has_value(),
+                "cos_sin must be [max_pos, D] (with positions)");
+    rp.cos_sin = cos_sin->data_ptr<float>();
+    rp.max_pos = (int)cos_sin->size(0);
+  }
+  rp.q_out = bp(q_out);
+  rp.k_cache = k_cache.data_ptr();
+  rp.v_cache = v_cache.data_ptr();
+  rp.nh = (int)nh;
+  rp.nkv = (int)nkv;
+  rp.D = (int)D;
+  rp.bs = (int)k_cache.size(2);
+  const GemvNormArgs na = gemv_norm_args(x, norm_w, res_in, res_out, eps, "skinny_gemm_qkv_rope");
+  const dli::GemvNorm* nm = na.on ? &na.nm : nullptr;
+  const dli::bf16* b = nullptr;
+  if (bias.has_value()) {
+    CHECK_IN(*bias); CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() == N, "skinny_gemm_qkv_rope: bias must have N entries");
+    b = bp(*bias);
+  }
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  int rc;
+  if (w.scalar_type() == at::kBFloat16) {
+    rc = dli::launch_skinny_gemm(nullptr, bp(x), bp(w), b, (int)M, (int)N, (int)K, cur_stream(),
+                                 false, nm, &rp);
+  } else {
+    TORCH_CHECK(wscale.has_value() && w.element_size() == 1, "8-bit weights need wscale");
+    CHECK_IN(*wscale); CHECK_F32(*wscale);
+    TORCH_CHECK(wscale->numel() == N, "wscale must have N entries");
+    if (w.scalar_type() == at::kChar)
+      rc = dli::launch_skinny_gemm_int8(nullptr, bp(x), w.data_ptr<int8_t>(),
+                                        wscale->data_ptr<float>(), b, (int)M, (int)N, (int)K,
+                                        cur_stream(), false, nm, &rp);
+    else
+      rc = dli::launch_skinny_gemm_fp8(nullptr, x.data_ptr(), nullptr,
+                                       static_cast<const uint8_t*>(w.data_ptr()),
+                                       wscale->data_ptr<float>(), b, (int)M, (int)N, (int)K,
+                                       cur_stream(), false, nm, &rp);
+  }
+  check_rc(rc, "skinny_gemm_qkv_rope");
+}
+
 }  // namespace
 
 void register_rccl(pybind11::module_& m);  // comm/rccl_p2p.hip
@@ -882,6 +958,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("splitk_reduce", &splitk_reduce, "bf16 out = sum of fp32 split-K partials [S, M, N]");
   m.def("gemm_tile_sk_workspace_floats", []() { return dli::gemm_tile_sk_workspace_floats(); },
         "fp32 workspace elements gemm_tile(splits=0) needs on the current device");
+  m.def("skinny_gemm_qkv_rope", &skinny_gemm_qkv_rope,
+        "1-2 row fused QKV GEMV with RoPE + paged KV write in its epilogue (+ fused input RMSNorm)",
+        py::arg("q_out"), py::arg("x"), py::arg("w"), py::arg("wscale"), py::arg("bias"),
+        py::arg("positions"), py::arg("slot_mapping"), py::arg("cos_sin"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("nh"), py::arg("nkv"), py::arg("k_scale") = 1.0,
+        py::arg("v_scale") = 1.0, py::arg("norm_w") = py::none(), py::arg("res_in") = py::none(),
+        py::arg("res_out") = py::none(), py::arg("eps") = 1e-5);
   m.def("gemm4", &gemm4, "C = A . B^T, one-wave-per-SIMD 256x256 MFMA tile GEMM (gemm4.hip)",
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
         py::arg("epilogue") = 0, py::arg("grid") = 0);

@@ -74,27 +74,106 @@ __device__ __forceinline__ void gemv_norm_prologue(const bf16* __restrict__ x, c
   __syncthreads();
 }
 
-// Weight rows of a wave.  Plain: rows 2w, 2w+1.  SW (fused SwiGLU over a swiglu_interleave'd
-// gate|up weight, N = 2I rows): output column o = w, its gate row 32 (o / 16) + o % 16 and up
-// row 16 further, so the wave holds both factors of silu(gate) * up.
-template <bool SW>
-__device__ __forceinline__ int gemv_row(int wave, int r) {
-  if constexpr (SW) return 32 * (wave >> 4) + (wave & 15) + 16 * r;
+// Epilogues.  kEpPlain: y[m, n] for rows n = 2w, 2w+1.  kEpSwiGLU (over a swiglu_interleave'd
+// gate|up weight, N = 2I rows): the wave takes output column o = w, its gate row 32 (o / 16) +
+// o % 16 and the up row 16 further, and stores silu(gate) * up.  kEpRope (the fused QKV weight
+// [(nh + 2 nkv) D, K]): a wave of the q / k part takes rows (h D + d, h D + d + D/2) -- both
+// rotation partners -- applies RoPE at the row's position and stores q packed [M, nh, D] or k
+// into the paged K cache; a wave of the v part takes two consecutive rows and scatters them into
+// the paged V^T cache: rope_cache.hip's arithmetic, element for element, minus its launch.
+enum GemvEp { kEpPlain = 0, kEpSwiGLU = 1, kEpRope = 2 };
+
+template <int EP>
+__device__ __forceinline__ int gemv_row(int wave, int r, const GemvRope& rp) {
+  if constexpr (EP == kEpSwiGLU) return 32 * (wave >> 4) + (wave & 15) + 16 * r;
+  if constexpr (EP == kEpRope) {
+    const int half = rp.D >> 1, nqk = rp.nh + rp.nkv;
+    if (wave < nqk * half) {
+      const int h = wave / half;
+      return h * rp.D + (wave - h * half) + r * half;
+    }
+    return nqk * rp.D + 2 * (wave - nqk * half) + r;
+  }
   return wave * kRows + r;
 }
 
-template <int M, bool SW = false, bool NORM = false>
+// outputs of a wave: kRows values per row m (final fp32, every lane holds them), lane 0 stores
+template <int EP, int M>
+__device__ __forceinline__ void gemv_store(const float (&v)[M][kRows], int wave, int lane, int N,
+                                           bf16* __restrict__ y, const GemvRope& rp) {
+  if (lane != 0) return;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    if constexpr (EP == kEpPlain) {
+#pragma unroll
+      for (int r = 0; r < kRows; ++r)
+        if (wave * kRows + r < N) y[(size_t)m * N + wave * kRows + r] = (bf16)v[m][r];
+    } else if constexpr (EP == kEpSwiGLU) {   // gate and up rounded to bf16 first (unfused path)
+      const float g = (float)(bf16)v[m][0], u = (float)(bf16)v[m][1];
+      y[(size_t)m * (N >> 1) + wave] = (bf16)(g / (1.f + __expf(-g)) * u);
+    } else {
+      const int D = rp.D, half = D >> 1, nqk = rp.nh + rp.nkv;
+      const bf16 b0 = (bf16)v[m][0], b1 = (bf16)v[m][1];   // the GEMM output, rounded
+      const long slot = rp.slot_mapping ? rp.slot_mapping[m] : -1;
+      const long blk = slot >= 0 ? slot / rp.bs : 0;
+      const int off = slot >= 0 ? (int)(slot % rp.bs) : 0;
+      if (wave < nqk * half) {
+        const int h = wave / half, d = wave - h * half;
+        bf16 o0 = b0, o1 = b1;
+        if (rp.cos_sin) {
+          int pc = rp.positions ? rp.positions[m] : 0;
+          pc = pc < 0 ? 0 : (pc >= rp.max_pos ? rp.max_pos - 1 : pc);
+          const float c = rp.cos_sin[(size_t)pc * D + d], sn = rp.cos_sin[(size_t)pc * D + half + d];
+          const float x0 = (float)b0, x1 = (float)b1;
+          o0 = (bf16)__builtin_fmaf(x0, c, -(x1 * sn));
+          o1 = (bf16)__builtin_fmaf(x1, c, x0 * sn);
+        }
+        if (h < rp.nh) {
+          bf16* q = rp.q_out + ((size_t)m * rp.nh + h) * D;
+          q[d] = o0;
+          q[d + half] = o1;
+        } else if (slot >= 0) {
+          const size_t base = (((size_t)blk * rp.nkv + (h - rp.nh)) * rp.bs + off) * D;
+          if (rp.kv_fp8) {
+            uint8_t* kc = static_cast<uint8_t*>(rp.k_cache) + base;
+            kc[d] = f32_to_fp8((float)o0 * rp.k_inv_scale);
+            kc[d + half] = f32_to_fp8((float)o1 * rp.k_inv_scale);
+          } else {
+            bf16* kc = static_cast<bf16*>(rp.k_cache) + base;
+            kc[d] = o0;
+            kc[d + half] = o1;
+          }
+        }
+      } else if (slot >= 0) {
+        const int e = 2 * (wave - nqk * half), kh = e / D, dd = e - kh * D;
+        const size_t grp = ((size_t)blk * rp.nkv + kh) * (rp.bs >> 3) + (off >> 3);
+        const size_t i0 = (grp * D + dd) * 8 + (off & 7);
+        if (rp.kv_fp8) {
+          uint8_t* vc = static_cast<uint8_t*>(rp.v_cache);
+          vc[i0] = f32_to_fp8((float)b0 * rp.v_inv_scale);
+          vc[i0 + 8] = f32_to_fp8((float)b1 * rp.v_inv_scale);
+        } else {
+          bf16* vc = static_cast<bf16*>(rp.v_cache);
+          vc[i0] = b0;
+          vc[i0 + 8] = b1;
+        }
+      }
+    }
+  }
+}
+
+template <int M, int EP = kEpPlain, bool NORM = false>
 __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict__ x_in,
                                                           const bf16* __restrict__ W,
                                                           const bf16* __restrict__ bias,
                                                           bf16* __restrict__ y, int N, int K,
-                                                          GemvNorm nm) {
+                                                          GemvNorm nm, GemvRope rp) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int n0 = wave * kRows;
   if constexpr (NORM) gemv_norm_prologue<M>(x_in, nm, K);   // every thread, before any exit
   const bf16* x = NORM ? reinterpret_cast<const bf16*>(gemv_lds) : x_in;
-  if ((SW ? 2 * wave : n0) >= N) return;
+  if ((EP != kEpPlain ? 2 * wave : n0) >= N) return;
   float acc[M][kRows];
 #pragma unroll
   for (int m = 0; m < M; ++m)
@@ -103,7 +182,7 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
 
   const bf16* wrow[kRows];
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<SW>(wave, r), N - 1) * K;
+  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<EP>(wave, r, rp), N - 1) * K;
 
   constexpr int kStep = 64 * 8;  // elements per wave instruction
   for (int k0 = lane * 8; k0 < K; k0 += kStep * kUnroll) {
@@ -141,20 +220,15 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
           }
         }
   }
+  float v[M][kRows];
 #pragma unroll
-  for (int m = 0; m < M; ++m) {
-    float v[kRows];
+  for (int m = 0; m < M; ++m)
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
-      const int n = gemv_row<SW>(wave, r);
-      v[r] = wave_reduce_sum(acc[m][r]) + (bias ? (float)bias[n] : 0.f);
-      if (!SW && lane == 0 && n < N) y[(size_t)m * N + n] = (bf16)v[r];
+      const int n = min(gemv_row<EP>(wave, r, rp), N - 1);
+      v[m][r] = wave_reduce_sum(acc[m][r]) + (bias ? (float)bias[n] : 0.f);
     }
-    if (SW && lane == 0) {   // gate and up rounded to bf16 first, as the unfused path does
-      const float g = (float)(bf16)v[0], u = (float)(bf16)v[1];
-      y[(size_t)m * (N >> 1) + wave] = (bf16)(g / (1.f + __expf(-g)) * u);
-    }
-  }
+  gemv_store<EP, M>(v, wave, lane, N, y, rp);
 }
 
 // fp8 e4m3 weights [N, K] with one fp32 scale per output row: the same weight stream at half
@@ -177,21 +251,21 @@ __device__ __forceinline__ bf16x2 u8pair_to_bf16x2(unsigned u, int j) {
   return __builtin_bit_cast(bf16x2, p);
 }
 
-template <int M, bool XF8, bool WI8 = false, bool SW = false, bool NORM = false>
+template <int M, bool XF8, bool WI8 = false, int EP = kEpPlain, bool NORM = false>
 __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __restrict__ x_in,
                                                               const float* __restrict__ xscale,
                                                               const uint8_t* __restrict__ W,
                                                               const float* __restrict__ wscale,
                                                               const bf16* __restrict__ bias,
                                                               bf16* __restrict__ y, int N, int K,
-                                                              GemvNorm nm) {
+                                                              GemvNorm nm, GemvRope rp) {
   static_assert(!(NORM && XF8), "the fused norm feeds bf16 rows");
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int n0 = wave * kRows;
   if constexpr (NORM) gemv_norm_prologue<M>(static_cast<const bf16*>(x_in), nm, K);
   const void* xv_ = NORM ? static_cast<const void*>(gemv_lds) : x_in;
-  if ((SW ? 2 * wave : n0) >= N) return;
+  if ((EP != kEpPlain ? 2 * wave : n0) >= N) return;
   float acc[M][kRows];
 #pragma unroll
   for (int m = 0; m < M; ++m)
@@ -202,7 +276,7 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
   for (int m = 0; m < M; ++m) sx[m] = 0.f;
   const uint8_t* wrow[kRows];
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<SW>(wave, r), N - 1) * K;
+  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<EP>(wave, r, rp), N - 1) * K;
 
   constexpr int kStep = 64 * 16;  // elements per wave instruction
   for (int k0 = lane * 16; k0 < K; k0 += kStep * kUnroll) {
@@ -292,52 +366,61 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
 #pragma unroll
       for (int r = 0; r < kRows; ++r) acc[m][r] -= 128.f * sx[m];
   }
+  float v[M][kRows];
 #pragma unroll
-  for (int m = 0; m < M; ++m) {
-    float v[kRows];
+  for (int m = 0; m < M; ++m)
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
-      const int n = min(gemv_row<SW>(wave, r), N - 1);
-      v[r] = wave_reduce_sum(acc[m][r]) * wscale[n] * (XF8 ? xscale[m] : 1.f) +
-             (bias ? (float)bias[n] : 0.f);
-      if (!SW && lane == 0 && n0 + r < N) y[(size_t)m * N + n0 + r] = (bf16)v[r];
+      const int n = min(gemv_row<EP>(wave, r, rp), N - 1);
+      v[m][r] = wave_reduce_sum(acc[m][r]) * wscale[n] * (XF8 ? xscale[m] : 1.f) +
+                (bias ? (float)bias[n] : 0.f);
     }
-    if (SW && lane == 0) {   // gate and up rounded to bf16 first, as the unfused path does
-      const float g = (float)(bf16)v[0], u = (float)(bf16)v[1];
-      y[(size_t)m * (N >> 1) + wave] = (bf16)(g / (1.f + __expf(-g)) * u);
-    }
-  }
+  gemv_store<EP, M>(v, wave, lane, N, y, rp);
 }
 
 }  // namespace
 
 // swiglu: W is a swiglu_interleave'd gate|up weight [N = 2I, K], y is silu(gate) * up [M, I];
+// rp (optional): W is the fused QKV weight, the epilogue applies RoPE and writes q / the caches;
 // nm (optional): the fused input RMSNorm (x is then the un-normalised row, bf16)
-template <bool XF8, bool WI8, int M, bool SW>
+static int gemv_ep(bool swiglu, const GemvRope* rp) {
+  return rp != nullptr ? kEpRope : swiglu ? kEpSwiGLU : kEpPlain;
+}
+
+template <bool XF8, bool WI8, int M, int EP>
 static void launch_fp8_t(bf16* y, const void* x, const float* xscale, const uint8_t* W,
                          const float* wscale, const bf16* bias, int N, int K, const GemvNorm* nm,
-                         int grid, hipStream_t stream) {
+                         const GemvRope& rp, int grid, hipStream_t stream) {
   if constexpr (!XF8) {
     if (nm != nullptr) {
-      skinny_gemm_fp8_kernel<M, XF8, WI8, SW, true><<<grid, 256, (size_t)M * K * 2, stream>>>(
-          x, xscale, W, wscale, bias, y, N, K, *nm);
+      skinny_gemm_fp8_kernel<M, XF8, WI8, EP, true><<<grid, 256, (size_t)M * K * 2, stream>>>(
+          x, xscale, W, wscale, bias, y, N, K, *nm, rp);
       return;
     }
   }
-  skinny_gemm_fp8_kernel<M, XF8, WI8, SW, false><<<grid, 256, 0, stream>>>(
-      x, xscale, W, wscale, bias, y, N, K, GemvNorm{});
+  skinny_gemm_fp8_kernel<M, XF8, WI8, EP, false><<<grid, 256, 0, stream>>>(
+      x, xscale, W, wscale, bias, y, N, K, GemvNorm{}, rp);
+}
+
+template <bool XF8, bool WI8, int M>
+static void launch_fp8_ep(bf16* y, const void* x, const float* xscale, const uint8_t* W,
+                          const float* wscale, const bf16* bias, int N, int K, int ep,
+                          const GemvNorm* nm, const GemvRope* rp, int grid, hipStream_t stream) {
+  const GemvRope r = rp ? *rp : GemvRope{};
+  if (ep == kEpRope) launch_fp8_t<XF8, WI8, M, kEpRope>(y, x, xscale, W, wscale, bias, N, K, nm, r, grid, stream);
+  else if (ep == kEpSwiGLU) launch_fp8_t<XF8, WI8, M, kEpSwiGLU>(y, x, xscale, W, wscale, bias, N, K, nm, r, grid, stream);
+  else launch_fp8_t<XF8, WI8, M, kEpPlain>(y, x, xscale, W, wscale, bias, N, K, nm, r, grid, stream);
 }
 
 template <bool XF8, bool WI8>
 static void launch_fp8_m(bf16* y, const void* x, const float* xscale, const uint8_t* W,
                          const float* wscale, const bf16* bias, int M, int N, int K, bool swiglu,
-                         const GemvNorm* nm, hipStream_t stream) {
-  const int waves = swiglu ? N / 2 : (N + kRows - 1) / kRows;
+                         const GemvNorm* nm, const GemvRope* rp, hipStream_t stream) {
+  const int ep = gemv_ep(swiglu, rp);
+  const int waves = ep != kEpPlain ? N / 2 : (N + kRows - 1) / kRows;
   const int grid = (waves + 3) / 4;
-  if (M == 1 && swiglu) launch_fp8_t<XF8, WI8, 1, true>(y, x, xscale, W, wscale, bias, N, K, nm, grid, stream);
-  else if (M == 1) launch_fp8_t<XF8, WI8, 1, false>(y, x, xscale, W, wscale, bias, N, K, nm, grid, stream);
-  else if (swiglu) launch_fp8_t<XF8, WI8, 2, true>(y, x, xscale, W, wscale, bias, N, K, nm, grid, stream);
-  else launch_fp8_t<XF8, WI8, 2, false>(y, x, xscale, W, wscale, bias, N, K, nm, grid, stream);
+  if (M == 1) launch_fp8_ep<XF8, WI8, 1>(y, x, xscale, W, wscale, bias, N, K, ep, nm, rp, grid, stream);
+  else launch_fp8_ep<XF8, WI8, 2>(y, x, xscale, W, wscale, bias, N, K, ep, nm, rp, grid, stream);
 }
 
 static bool gemv_norm_ok(const GemvNorm* nm, int M, int K) {
@@ -345,53 +428,70 @@ static bool gemv_norm_ok(const GemvNorm* nm, int M, int K) {
                            (nm->res_out == nullptr || nm->res_out != nm->res_in));
 }
 
+static bool gemv_rope_ok(const GemvRope* rp, bool swiglu, int M, int N) {
+  return rp == nullptr ||
+         (!swiglu && M <= 2 && rp->D % 2 == 0 && rp->bs % 8 == 0 && rp->q_out != nullptr &&
+          N == (rp->nh + 2 * rp->nkv) * rp->D && (rp->cos_sin == nullptr || rp->max_pos > 0));
+}
+
 int launch_skinny_gemm_fp8(bf16* y, const void* x, const float* xscale, const uint8_t* W,
                            const float* wscale, const bf16* bias, int M, int N, int K,
-                           hipStream_t stream, bool swiglu, const GemvNorm* nm) {
+                           hipStream_t stream, bool swiglu, const GemvNorm* nm,
+                           const GemvRope* rp) {
   if (M < 1 || M > 2 || K % 16 != 0 || N < 1 || (swiglu && N % 32 != 0)) return -1;
   if (!gemv_norm_ok(nm, M, K) || (nm != nullptr && xscale != nullptr)) return -2;
+  if (!gemv_rope_ok(rp, swiglu, M, N)) return -3;
   if (xscale != nullptr)
-    launch_fp8_m<true, false>(y, x, xscale, W, wscale, bias, M, N, K, swiglu, nullptr, stream);
+    launch_fp8_m<true, false>(y, x, xscale, W, wscale, bias, M, N, K, swiglu, nullptr, rp, stream);
   else
-    launch_fp8_m<false, false>(y, x, xscale, W, wscale, bias, M, N, K, swiglu, nm, stream);
+    launch_fp8_m<false, false>(y, x, xscale, W, wscale, bias, M, N, K, swiglu, nm, rp, stream);
   return 0;
 }
 
 int launch_skinny_gemm_int8(bf16* y, const bf16* x, const int8_t* W, const float* wscale,
                             const bf16* bias, int M, int N, int K, hipStream_t stream,
-                            bool swiglu, const GemvNorm* nm) {
+                            bool swiglu, const GemvNorm* nm, const GemvRope* rp) {
   if (M < 1 || M > 2 || K % 16 != 0 || N < 1 || (swiglu && N % 32 != 0)) return -1;
   if (!gemv_norm_ok(nm, M, K)) return -2;
+  if (!gemv_rope_ok(rp, swiglu, M, N)) return -3;
   launch_fp8_m<false, true>(y, x, nullptr, reinterpret_cast<const uint8_t*>(W), wscale, bias, M,
-                            N, K, swiglu, nm, stream);
+                            N, K, swiglu, nm, rp, stream);
   return 0;
 }
 
-template <int M, bool SW>
+template <int M, int EP>
 static void launch_bf16_t(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int N, int K,
-                          const GemvNorm* nm, int grid, hipStream_t stream) {
+                          const GemvNorm* nm, const GemvRope& rp, int grid, hipStream_t stream) {
   if (nm != nullptr && M <= 2)
-    skinny_gemm_kernel<M, SW, true><<<grid, 256, (size_t)M * K * 2, stream>>>(x, W, bias, y, N, K, *nm);
+    skinny_gemm_kernel<M, EP, true><<<grid, 256, (size_t)M * K * 2, stream>>>(x, W, bias, y, N, K, *nm, rp);
   else
-    skinny_gemm_kernel<M, SW, false><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K, GemvNorm{});
+    skinny_gemm_kernel<M, EP, false><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K, GemvNorm{}, rp);
+}
+
+template <int M>
+static void launch_bf16_ep(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int N, int K,
+                           int ep, const GemvNorm* nm, const GemvRope* rp, int grid,
+                           hipStream_t stream) {
+  const GemvRope r = rp ? *rp : GemvRope{};
+  if (ep == kEpRope) launch_bf16_t<M, kEpRope>(y, x, W, bias, N, K, nm, r, grid, stream);
+  else if (ep == kEpSwiGLU) launch_bf16_t<M, kEpSwiGLU>(y, x, W, bias, N, K, nm, r, grid, stream);
+  else launch_bf16_t<M, kEpPlain>(y, x, W, bias, N, K, nm, r, grid, stream);
 }
 
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
-                       int K, hipStream_t stream, bool swiglu, const GemvNorm* nm) {
+                       int K, hipStream_t stream, bool swiglu, const GemvNorm* nm,
+                       const GemvRope* rp) {
   if (M < 1 || M > 4 || K % 8 != 0 || N < 1 || (swiglu && (N % 32 != 0 || M > 2))) return -1;
   if (!gemv_norm_ok(nm, M, K)) return -2;
-  const int waves = swiglu ? N / 2 : (N + kRows - 1) / kRows;
+  if (!gemv_rope_ok(rp, swiglu, M, N)) return -3;
+  const int ep = gemv_ep(swiglu, rp);
+  const int waves = ep != kEpPlain ? N / 2 : (N + kRows - 1) / kRows;
   const int grid = (waves + 3) / 4;
-  if (swiglu) {
-    if (M == 1) launch_bf16_t<1, true>(y, x, W, bias, N, K, nm, grid, stream);
-    else launch_bf16_t<2, true>(y, x, W, bias, N, K, nm, grid, stream);
-    return 0;
-  }
   switch (M) {
-    case 1: launch_bf16_t<1, false>(y, x, W, bias, N, K, nm, grid, stream); break;
-    case 2: launch_bf16_t<2, false>(y, x, W, bias, N, K, nm, grid, stream); break;
-    case 3: launch_bf16_t<3, false>(y, x, W, bias, N, K, nullptr, grid, stream); break;
-    case 4: launch_bf16_t<4, false>(y, x, W, bias, N, K, nullptr, grid, stream); break;
+    case 1: launch_bf16_ep<1>(y, x, W, bias, N, K, ep, nm, rp, grid, stream); break;
+    case 2: launch_bf16_ep<2>(y, x, W, bias, N, K, ep, nm, rp, grid, stream); break;
+    case 3: skinny_gemm_kernel<3><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K, GemvNorm{}, GemvRope{}); break;
+    case 4: skinny_gemm_kernel<4><<<grid, 256, 0, stream>>>(x, W, bias, y, N, K, GemvNorm{}, GemvRope{}); break;
   }
   return 0;
 }

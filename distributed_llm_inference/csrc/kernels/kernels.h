@@ -111,15 +111,31 @@ struct GemvNorm {
   const bf16* w;        // [K]
   float eps;
 };
+// rp: W is the fused QKV weight [(nh + 2 nkv) D, K] and the GEMV's epilogue does rope_cache's
+// work (q rotated into q_out [M, nh, D], k rotated and v into the paged caches); y is unused
+struct GemvRope {
+  const int* positions;       // [M]
+  const long* slot_mapping;   // [M] (-1: no cache write)
+  const float* cos_sin;       // [max_pos, D] (cos | sin), nullptr: no rotation
+  int max_pos;
+  bf16* q_out;                // [M, nh, D]
+  void* k_cache;              // [blocks, nkv, bs, D]
+  void* v_cache;              // [blocks, nkv, bs/8, D, 8]
+  int kv_fp8;
+  float k_inv_scale, v_inv_scale;
+  int nh, nkv, D, bs;
+};
 int launch_skinny_gemm_fp8(bf16* y, const void* x, const float* xscale, const uint8_t* W,
                            const float* wscale, const bf16* bias, int M, int N, int K,
-                           hipStream_t stream, bool swiglu = false, const GemvNorm* nm = nullptr);
+                           hipStream_t stream, bool swiglu = false, const GemvNorm* nm = nullptr,
+                           const GemvRope* rp = nullptr);
 int launch_skinny_gemm_int8(bf16* y, const bf16* x, const int8_t* W, const float* wscale,
                             const bf16* bias, int M, int N, int K, hipStream_t stream,
-                            bool swiglu = false, const GemvNorm* nm = nullptr);
+                            bool swiglu = false, const GemvNorm* nm = nullptr,
+                            const GemvRope* rp = nullptr);
 int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, int M, int N,
                        int K, hipStream_t stream, bool swiglu = false,
-                       const GemvNorm* nm = nullptr);
+                       const GemvNorm* nm = nullptr, const GemvRope* rp = nullptr);
 // one-wave-per-SIMD 256x256 GEMM (gemm4.hip); epilogue 0 bf16, 1 fp32 partials, 2 SwiGLU,
 // 4 bf16 partials; grid <= 0: automatic persistent grid; variant < 0: default k-loop schedule
 int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int splits,

@@ -123,6 +123,29 @@ class Linear(nn.Module):
                                        swiglu=swiglu)
         return ops.skinny_gemm(x, self.weight, self.bias, swiglu=swiglu, norm=norm)
 
+    def gemv_qkv_rope(self, x: torch.Tensor, meta: "AttnMetadata", k_cache: torch.Tensor,
+                      v_cache: torch.Tensor, cos_sin: torch.Tensor, nh: int, nkv: int,
+                      head_dim: int, norm: Optional["ops.RowNorm"] = None
+                      ) -> Optional[torch.Tensor]:
+        """This Linear as the fused QKV projection of 1-2 decode rows with RoPE and the paged
+        KV write in the GEMV's epilogue (see :func:`ops.skinny_gemm_qkv_rope`): returns q
+        [M, nh, D], or None when that path does not apply (window mode's sink query, more rows,
+        CPU) -- the caller then runs the GEMV and rope_cache separately."""
+        if (x is None or not x.is_cuda or x.dim() != 2 or x.dtype != torch.bfloat16
+                or not self.gemv_ok(x.shape[0]) or meta.want_sink or meta.custom_mask is not None
+                or self.out_features != (nh + 2 * nkv) * head_dim
+                or os.environ.get("DLI_GEMV_ROPE", "1") != "1"):
+            return None
+        if self.weight_int8 is not None:
+            w, ws = self.weight_int8, self.weight_scale
+        elif self.weight_fp8 is not None:
+            w, ws = self.weight_fp8, self.weight_scale
+        else:
+            w, ws = self.weight, None
+        return ops.skinny_gemm_qkv_rope(x, w, ws, self.bias, meta.positions, meta.slot_mapping,
+                                        cos_sin, nh, nkv, head_dim, k_cache, v_cache,
+                                        meta.k_scale, meta.v_scale, norm=norm)
+
     def gemv_swiglu(self, x: Optional[torch.Tensor],
                     x_q: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
                     ) -> Optional[torch.Tensor]:

@@ -79,18 +79,26 @@ class LlamaAttention(nn.Module):
                 norm: Optional[ops.RowNorm] = None):
         """``norm``: ``normed`` is the UN-normalised row and the QKV GEMV applies the input
         RMSNorm itself (1-2 decode rows, LlamaDecoderLayer._forward_gemv)."""
+        q = None
         if norm is not None:
-            qkv = self.qkv_proj.gemv(normed, norm=norm)
-            if qkv is None:
-                raise RuntimeError("fused-norm QKV: the GEMV does not take this product")
+            # 1-2 rows: RMSNorm -> QKV -> RoPE / KV write in one GEMV launch when it applies
+            q = self.qkv_proj.gemv_qkv_rope(normed, meta, k_cache, v_cache, cos_sin,
+                                            self.num_heads, self.num_kv_heads, self.head_dim,
+                                            norm=norm)
+            q_sink = None
+            if q is None:
+                qkv = self.qkv_proj.gemv(normed, norm=norm)
+                if qkv is None:
+                    raise RuntimeError("fused-norm QKV: the GEMV does not take this product")
         else:
             # split-K partials of the QKV GEMM are summed inside the RoPE / KV-write kernel
             qkv = self.qkv_proj(normed, x_q, defer_reduce=True)
-        T = qkv.shape[0]
-        q, q_sink = ops.rope_cache(qkv, meta.positions, meta.slot_mapping, cos_sin, self.num_heads,
-                                   self.num_kv_heads, self.head_dim, k_cache, v_cache,
-                                   window=meta.window, want_sink=meta.want_sink,
-                                   k_scale=meta.k_scale, v_scale=meta.v_scale)
+        if q is None:
+            q, q_sink = ops.rope_cache(qkv, meta.positions, meta.slot_mapping, cos_sin,
+                                       self.num_heads, self.num_kv_heads, self.head_dim, k_cache,
+                                       v_cache, window=meta.window, want_sink=meta.want_sink,
+                                       k_scale=meta.k_scale, v_scale=meta.v_scale)
+        T = q.shape[0]
         if meta.custom_mask is not None:
             # reference-API custom 4-D additive mask (reference model.py:115-119, modules.py:92-94):
             # the prefill kernel's masked variant (any T, full cache) adds it before the online

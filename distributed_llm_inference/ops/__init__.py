@@ -983,6 +983,36 @@ def skinny_gemm_fp8(x: torch.Tensor, w8: torch.Tensor, w_scale: torch.Tensor,
     return out
 
 
+def skinny_gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, w_scale: Optional[torch.Tensor],
+                         bias: Optional[torch.Tensor], positions: Optional[torch.Tensor],
+                         slot_mapping: Optional[torch.Tensor], cos_sin: Optional[torch.Tensor],
+                         nh: int, nkv: int, head_dim: int, k_cache: torch.Tensor,
+                         v_cache: torch.Tensor, k_scale: float = 1.0, v_scale: float = 1.0,
+                         norm: Optional[RowNorm] = None) -> torch.Tensor:
+    """1-2 decode rows: the fused QKV projection (bf16, fp8 or int8 weights ``w`` [(nh + 2 nkv) D,
+    K], per-row ``w_scale`` for 8-bit) with :func:`rope_cache`'s work in the GEMV epilogue --
+    returns q [M, nh, D] rotated, k (rotated) and v written to the paged caches -- and the
+    input RMSNorm in its prologue when ``norm`` is given.  One launch instead of three."""
+    M = x.shape[0]
+    if not _gpu(x):
+        if norm is not None:
+            x = norm.apply(x)
+        wf = w.float() if w_scale is None else w.float() * w_scale.reshape(-1, 1)
+        qkv = x.float() @ wf.t()
+        if bias is not None:
+            qkv = qkv + bias.float()
+        q, _ = rope_cache(qkv.to(torch.bfloat16), positions, slot_mapping, cos_sin, nh, nkv,
+                          head_dim, k_cache, v_cache, k_scale=k_scale, v_scale=v_scale)
+        return q
+    q = torch.empty(M, nh, head_dim, dtype=torch.bfloat16, device=x.device)
+    native().skinny_gemm_qkv_rope(q, x.contiguous(), w,
+                                  None if w_scale is None else w_scale.reshape(-1).contiguous(),
+                                  bias, positions, slot_mapping, cos_sin, k_cache, v_cache,
+                                  int(nh), int(nkv), float(k_scale), float(v_scale),
+                                  **(norm.kwargs() if norm is not None else {}))
+    return q
+
+
 def skinny_gemm(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
                 out: Optional[torch.Tensor] = None, swiglu: bool = False,
                 norm: Optional[RowNorm] = None) -> torch.Tensor:

@@ -809,3 +809,49 @@ def test_skinny_gemm_fused_norm_bit_identical(gpu, M, wdtype, swiglu, resid):
     if resid:
         assert torch.equal(r_out, r_sep)
         assert torch.equal(res, res0)   # res_in untouched (not aliased)
+
+
+@pytest.mark.parametrize("wdtype", ["bf16", "fp8", "int8"])
+@pytest.mark.parametrize("kv_fp8", [False, True])
+@pytest.mark.parametrize("M", [1, 2])
+def test_skinny_gemm_qkv_rope_matches_gemv_then_rope_cache(gpu, wdtype, kv_fp8, M):
+    """The fused QKV GEMV with RoPE + paged KV write in its epilogue (gemv.hip kEpRope) produces
+    the same q and the same cache bytes as the GEMV followed by rope_cache (one slot skipped
+    with -1 when M = 2), with and without the fused input RMSNorm."""
+    torch.manual_seed(11 * M + kv_fp8 + len(wdtype))
+    nh, nkv, D, bs, K, nblk = 8, 2, 128, 64, 2048, 4
+    N = (nh + 2 * nkv) * D
+    x = torch.randn(M, K, device=gpu, dtype=BF)
+    w = (torch.randn(N, K, device=gpu) * 0.02).to(BF)
+    if wdtype == "fp8":
+        wq, ws = ops.quantize_weight_fp8(w)
+    elif wdtype == "int8":
+        wq, ws = ops.quantize_weight_int8(w.float())
+    else:
+        wq, ws = w, None
+    cs = ops.reference.build_cos_sin(D, 4096, 500000.0, None, device=gpu)
+    pos = torch.tensor([37, 4000][:M], device=gpu, dtype=torch.int32)
+    slots = torch.tensor([5, -1][:M] if M == 2 else [70], device=gpu, dtype=torch.int64)
+    kdt = torch.float8_e4m3fn if kv_fp8 else BF
+    nw = (1 + 0.1 * torch.randn(K, device=gpu)).to(BF)
+    for norm in (None, ops.RowNorm(nw, 1e-5)):
+        caches = []
+        for _ in range(2):
+            kc = torch.zeros(nblk, nkv, bs, D, device=gpu).to(kdt)
+            vc = torch.zeros(nblk, nkv, bs // 8, D, 8, device=gpu).to(kdt)
+            caches.append((kc, vc))
+        xin = x if norm is None else norm.apply(x)
+        if wdtype == "bf16":
+            qkv = ops.skinny_gemm(xin, wq)
+        elif wdtype == "fp8":
+            qkv = ops.skinny_gemm_fp8(xin, wq, ws)
+        else:
+            qkv = ops.skinny_gemm_int8(xin, wq, ws)
+        q_ref, _ = ops.rope_cache(qkv, pos, slots, cs, nh, nkv, D, *caches[0], k_scale=0.5,
+                                  v_scale=0.25)
+        q = ops.skinny_gemm_qkv_rope(x, wq, ws, None, pos, slots, cs, nh, nkv, D, *caches[1],
+                                     k_scale=0.5, v_scale=0.25, norm=norm)
+        torch.cuda.synchronize()
+        assert torch.equal(q, q_ref)
+        for a, b in zip(caches[0], caches[1]):
+            assert torch.equal(a.view(torch.uint8), b.view(torch.uint8))
