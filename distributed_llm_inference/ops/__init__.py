@@ -472,6 +472,8 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = 
     ``silu(x @ gate^T) * (x @ up^T)`` ([M, N/2]).  ``defer_reduce`` (split-K only): return the
     fp32 partials as :class:`SplitKPartials` for a consumer that reduces them (``rms_norm``)."""
     M, N = x.shape[0], w.shape[0]
+    if _gpu(x) and gemm4_enabled():
+        return _gemm4(x, w, splits, swiglu, out, defer_reduce)
     if (defer_reduce and splits > 1 and _gpu(x) and not swiglu
             and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
         if bf16_bf16_partials():
@@ -499,6 +501,38 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = 
     if splits > 1 and workspace is None:
         workspace = torch.empty(splits * M * N, dtype=torch.float32, device=x.device)
     native().gemm_tile(out, x, w, int(splits), 2 if swiglu else 0, workspace)
+    return out
+
+
+def gemm4_enabled() -> bool:
+    """bf16 decode projections on the one-wave-per-SIMD kernel (csrc/kernels/gemm4.hip) instead
+    of gemm_tile: ``DLI_GEMM4=1`` (read per call, so a captured graph keeps its choice)."""
+    return os.environ.get("DLI_GEMM4", "0") == "1"
+
+
+def _gemm4(x: torch.Tensor, w: torch.Tensor, splits: int, swiglu: bool,
+           out: Optional[torch.Tensor], defer_reduce: bool):
+    """:func:`gemm_tile`'s contract on gemm4: same epilogues (bf16 store, fused SwiGLU, split-K
+    partials handed to the consumer or reduced here), bit-identical results."""
+    M, N = x.shape[0], w.shape[0]
+    splits = max(1, int(splits))
+    if splits > 1 and defer_reduce and not swiglu and \
+            os.environ.get("DLI_SPLITK_DEFER", "1") == "1":
+        bf = bf16_bf16_partials()
+        parts = torch.empty(splits, M, N, dtype=torch.bfloat16 if bf else torch.float32,
+                            device=x.device)
+        native().gemm4(parts, x, w, splits, 4 if bf else 1)
+        return SplitKPartials(parts)
+    if out is None:
+        out = torch.empty(M, N // 2 if swiglu else N, dtype=x.dtype, device=x.device)
+    if splits == 1:
+        native().gemm4(out, x, w, 1, 2 if swiglu else 0)
+        return out
+    if swiglu:
+        raise ValueError("gemm4: fused SwiGLU takes whole-K tiles (splits = 1)")
+    parts = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+    native().gemm4(parts, x, w, splits, 1)
+    native().splitk_reduce(out, parts)
     return out
 
 
