@@ -75,7 +75,13 @@ template <> struct G4Sched<2> {   // hipBLASLt-like: late wait, dense P reads (l
 template <> struct G4Sched<3> {   // dense Q reads, early DMA
   static constexpr int q0 = 0, qs = 1, b1 = 24, d0 = 25, ds = 2, b2 = 80, vm = 16, p0 = 81, ps = 2;
 };
-constexpr int kG4Variants = 4;
+template <> struct G4Sched<4> {   // late wait, DMA spread thin (1 per 4 MFMAs), dense P reads
+  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 4, b2 = 104, vm = 16, p0 = 105, ps = 1;
+};
+template <> struct G4Sched<5> {   // dense Q reads, early B1, DMA 1 per 3, late wait
+  static constexpr int q0 = 0, qs = 1, b1 = 20, d0 = 21, ds = 3, b2 = 96, vm = 16, p0 = 97, ps = 1;
+};
+constexpr int kG4Variants = 6;
 constexpr int kG4Default = 0;
 
 __device__ __forceinline__ float g4_silu(float x) { return x / (1.f + __expf(-x)); }
@@ -402,6 +408,8 @@ int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int
     case 1: return launch_gemm4_v<1>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
     case 2: return launch_gemm4_v<2>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
     case 3: return launch_gemm4_v<3>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
+    case 4: return launch_gemm4_v<4>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
+    case 5: return launch_gemm4_v<5>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
   }
   return -5;
 }

@@ -1,4 +1,4 @@
-# One-GPU results sweep behind README's table (each config its own process, back to back)
+# One-GPU results sweep behind README's table (each config its own process, back to back, one box)
 set -u
 mkdir -p gpurun_out/results
 export TMPDIR=/tmp
@@ -13,6 +13,8 @@ run fp8_fp8kv_b512 --fp8 --kv-fp8
 run bf16_fp8kv_b512 --kv-fp8
 run llama3_8b_bf16_b512 --model llama-3-8b
 run bf16_b1 --batch-per-mb 1 --steps 20
+run fp8_b1 --fp8 --batch-per-mb 1 --steps 20
+run int8_b1 --int8 --batch-per-mb 1 --steps 20
 run int8_b512 --int8
 run bf16_b1_ctx8k --batch-per-mb 1 --prompt-len 8192 --steps 20
 run bf16_b16_ctx8k --batch-per-mb 16 --prompt-len 8192 --steps 10
