@@ -679,9 +679,24 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
 
 // one-wave-per-SIMD tile GEMM (gemm4.hip), bf16: epilogue 0 = bf16 [M, N], 2 = SwiGLU [M, N/2]
 // (splits 1); 1 = fp32 partials, 4 = bf16 partials [splits, M, N] (splits > 1)
-void gemm4(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue, int64_t grid) {
+// fp8 e4m3 operands (1-byte a / b) take per-row a_scale [M] and per-channel b_scale [N] (fp32)
+void gemm4(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue, int64_t grid,
+           optional<Tensor> a_scale, optional<Tensor> b_scale, int64_t variant) {
   CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
-  CHECK_BF16(a); CHECK_BF16(b);
+  const bool fp8 = a.element_size() == 1;
+  TORCH_CHECK(a.scalar_type() == b.scalar_type() && a.scalar_type() != at::kChar,
+              "gemm4: bf16 or fp8 e4m3 operands of one dtype");
+  if (!fp8) { CHECK_BF16(a); }
+  const float* sa = nullptr;
+  const float* sb = nullptr;
+  if (fp8) {
+    TORCH_CHECK(a_scale.has_value() && b_scale.has_value(), "gemm4: fp8 needs a_scale and b_scale");
+    CHECK_IN(*a_scale); CHECK_IN(*b_scale); CHECK_F32(*a_scale); CHECK_F32(*b_scale);
+    TORCH_CHECK(a_scale->numel() == a.size(0) && b_scale->numel() == b.size(0),
+                "gemm4: a_scale [M], b_scale [N]");
+    sa = a_scale->data_ptr<float>();
+    sb = b_scale->data_ptr<float>();
+  }
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm4: 2-D operands");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K, "gemm4: shape mismatch");
@@ -695,7 +710,8 @@ void gemm4(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue, int
               "gemm4: output size / dtype");
   const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
   check_rc(dli::launch_gemm4(out.data_ptr(), a.data_ptr(), b.data_ptr(), (int)M, (int)N, (int)K,
-                             (int)splits, (int)epilogue, (int)grid, cur_stream()),
+                             (int)splits, (int)epilogue, (int)grid, cur_stream(), (int)variant,
+                             fp8 ? 1 : 0, sa, sb),
            "gemm4");
 }
 
@@ -967,7 +983,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("res_out") = py::none(), py::arg("eps") = 1e-5);
   m.def("gemm4", &gemm4, "C = A . B^T, one-wave-per-SIMD 256x256 MFMA tile GEMM (gemm4.hip)",
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
-        py::arg("epilogue") = 0, py::arg("grid") = 0);
+        py::arg("epilogue") = 0, py::arg("grid") = 0, py::arg("a_scale") = py::none(),
+        py::arg("b_scale") = py::none(), py::arg("variant") = -1);
   m.def("skinny_gemm_int8", &skinny_gemm_int8,
         "y = (x . W8^T) * scale (+ bias), int8 weights, bf16 rows, M <= 2 (weight-streaming GEMV)",
         py::arg("out"), py::arg("x"), py::arg("w"), py::arg("wscale"), py::arg("bias") = py::none(),

@@ -81,13 +81,40 @@ template <> struct G4Sched<4> {   // late wait, DMA spread thin (1 per 4 MFMAs),
 template <> struct G4Sched<5> {   // dense Q reads, early B1, DMA 1 per 3, late wait
   static constexpr int q0 = 0, qs = 1, b1 = 20, d0 = 21, ds = 3, b2 = 96, vm = 16, p0 = 97, ps = 1;
 };
-constexpr int kG4Variants = 6;
-constexpr int kG4Default = 0;
+template <> struct G4Sched<6> {   // v4 with the DMA spread over B2 (1 per 6 MFMAs, 12 before it)
+  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 6, b2 = 104, vm = 12, p0 = 105, ps = 1;
+};
+template <> struct G4Sched<7> {   // v4 with the DMA 1 per 5 MFMAs (14 before B2)
+  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 5, b2 = 104, vm = 14, p0 = 105, ps = 1;
+};
+constexpr int kG4Variants = 8;
+// measured fastest on every decode shape and 8192^3 (profiles/r4/gemm4_ab_v0-5.txt)
+constexpr int kG4Default = 4;
 
 __device__ __forceinline__ float g4_silu(float x) { return x / (1.f + __expf(-x)); }
 
 __device__ __forceinline__ void g4_mfma(f32x4& acc, const bf16x8& w, const bf16x8& x) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(w), "v"(x) : "memory");
+}
+
+typedef int g4_i32x4 __attribute__((ext_vector_type(4)));
+typedef int g4_i32x8 __attribute__((ext_vector_type(8)));
+typedef float g4_f32x16 __attribute__((ext_vector_type(16)));
+
+// fp8 e4m3 x fp8 e4m3 -> fp32, 32 x 32 x 64, block scales 1.0 (e8m0 127 in `sc`): the per-row /
+// per-channel scales are applied in the epilogue.  The two 16-B halves of each operand come from
+// two ds_read_b128 into adjacent registers (the register coalescer places them; no copies).
+__device__ __forceinline__ void g4_mfma8(g4_f32x16& acc, const g4_i32x4& w0, const g4_i32x4& w1,
+                                         const g4_i32x4& x0, const g4_i32x4& x1, int sc) {
+  const g4_i32x8 w = __builtin_shufflevector(w0, w1, 0, 1, 2, 3, 4, 5, 6, 7);
+  const g4_i32x8 x = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+  asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+               : "+a"(acc) : "v"(w), "v"(x), "v"(sc) : "memory");
+}
+
+template <int OFF>
+__device__ __forceinline__ void g4_read8(g4_i32x4& dst, int addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF) : "memory");
 }
 
 template <int OFF>
@@ -111,10 +138,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t g4_rsrc(const void* base, int 
                                            __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-template <int EPI, int VAR>
+// PREC 0: bf16 operands (16x16x32 MFMAs, 128 per wave per k-tile).  PREC 1: fp8 e4m3 operands
+// (a k-tile = 128 bytes = 128 elements of every row, the same LDS image and DMA): 32x32x64
+// block-scaled MFMAs, 32 per wave per k-tile, each as long as four bf16 ones, so the k-loop
+// schedule (in 16-cycle slots, one bf16 MFMA or a quarter fp8 MFMA each) is shared; fragments of
+// 32 rows x 64 bytes (two ds_read_b128 per lane); per-row a_scale x per-channel b_scale in the
+// epilogue, as gemm_tile.hip's fp8 path.
+template <int EPI, int VAR, int PREC = 0>
 __global__ void __launch_bounds__(kG4Threads, 1)
-gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __restrict__ C,
-             int M, int N, int K, int tiles_m, int tiles_n, int kps, int splits) {
+gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __restrict__ C,
+             int M, int N, int K, int tiles_m, int tiles_n, int kps, int splits,
+             const float* __restrict__ a_scale, const float* __restrict__ b_scale) {
+  constexpr bool F8 = PREC == 1;
+  const char* A = reinterpret_cast<const char*>(Av);
+  const char* B = reinterpret_cast<const char*>(Bv);
   __shared__ __attribute__((aligned(1024))) char smem[2 * kG4Stage];
   const int tid = threadIdx.x, lane = tid & 63;
 #ifdef DLI_GEMM_STAMPS
@@ -128,7 +165,7 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
 #endif
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1, fr = lane & 15;
-  const int Kb = K * 2;
+  const int Kb = K * (F8 ? 1 : 2);
   const int kt_all = Kb / 128;
   const int items = tiles_m * tiles_n * splits;
   const int lds0 = (int)(size_t)smem;
@@ -148,6 +185,22 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
       rdA[kk][s] = lds0 + s * kG4Stage + (wr * 128 + fr) * 128 + ch;
       rdB[kk][s] = lds0 + s * kG4Stage + 32768 + (wc * 128 + fr) * 128 + ch;
     }
+  // fp8 fragments: lane l reads row 32 i + (l & 31) of its wave's A / B half, 16-B chunks
+  // kk*4 + 2 (l >> 5) + h (h = 0, 1) of the 128-B k-tile row, swizzled like the DMA wrote them
+  int rdA8[2][2][2], rdB8[2][2][2];
+  if constexpr (F8) {
+    const int r32 = lane & 31, sw8 = (r32 >> 1) & 7;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ch = ((kk * 4 + 2 * (lane >> 5) + h) ^ sw8) << 4;
+          rdA8[kk][st][h] = lds0 + st * kG4Stage + (wr * 128 + r32) * 128 + ch;
+          rdB8[kk][st][h] = lds0 + st * kG4Stage + 32768 + (wc * 128 + r32) * 128 + ch;
+        }
+  }
   // DMA: wave-load q = 4j + w covers tile rows 8q .. 8q+7; lane -> row 8q + (lane >> 3), LDS
   // slot lane & 7 holding global chunk (lane & 7) ^ ((row >> 1) & 7) = .. ^ ((q & 1) * 4 + (lane >> 4))
   const int dchunk = ((lane & 7) ^ (((w & 1) * 4 + (lane >> 4)) & 7)) << 4;
@@ -160,8 +213,8 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
     const int kt0 = split * kps;
     const int T = __builtin_amdgcn_readfirstlane(min(kps, kt_all - kt0));
     const int mrows = min(256, M - m0);
-    const auto rsA = g4_rsrc(A + (size_t)m0 * K, mrows * Kb);
-    const auto rsB = g4_rsrc(B + (size_t)n0 * K, 256 * Kb);
+    const auto rsA = g4_rsrc(A + (size_t)m0 * Kb, mrows * Kb);
+    const auto rsB = g4_rsrc(B + (size_t)n0 * Kb, 256 * Kb);
     int voA[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) voA[j] = min(drow + 32 * j, mrows - 1) * Kb + dchunk;
@@ -187,6 +240,35 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // fp8: 4 x 4 tiles of 32 x 32 (acc8[mi][ni]: activation block mi, weight block ni)
+    g4_f32x16 acc8[4][4];
+    if constexpr (F8) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc8[i][j][e] = 0.f;
+    }
+    const int sc127 = 127;
+    // fp8 fragment sets ([2 ni + h] weight halves, [8 + 2 mi + h] activation halves)
+    g4_i32x4 P8[16], Q8[16];
+    auto rd8 = [&](g4_i32x4 (&F)[16], int n, int kk, int s) {
+      const int h = n & 1, blk = (n >> 1) & 3;
+      const int base = n < 8 ? rdB8[kk][s][h] : rdA8[kk][s][h];
+      switch (blk) {
+        case 0: g4_read8<0 * 4096>(F[n], base); break;
+        case 1: g4_read8<1 * 4096>(F[n], base); break;
+        case 2: g4_read8<2 * 4096>(F[n], base); break;
+        default: g4_read8<3 * 4096>(F[n], base); break;
+      }
+    };
+    // fp8 MFMA number k (0..15) of a k-step: activation block k / 4, weight block k % 4
+    auto mf8 = [&](const g4_i32x4 (&F)[16], int k) {
+      const int mi = k >> 2, ni = k & 3;
+      g4_mfma8(acc8[mi][ni], F[2 * ni], F[2 * ni + 1], F[8 + 2 * mi], F[9 + 2 * mi], sc127);
+    };
 
     // fragment sets: P = k-step 0, Q = k-step 1 ([0..7] weight fragments, [8..15] activation)
     bf16x8 P[16], Q[16];
@@ -229,7 +311,9 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
     }
     g4_barrier();
 #pragma unroll
-    for (int n = 0; n < 16; ++n) rd(P, n, 0, 0);
+    for (int n = 0; n < 16; ++n) {
+      if constexpr (F8) rd8(P8, n, 0, 0); else rd(P, n, 0, 0);
+    }
     g4_sync_lds();
 
     // one k-tile.  DMA: issue tile t+2 into stage t&1; NEXT: read k-step 0 of tile t+1
@@ -242,9 +326,16 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
       // tile t+1 -> P, at the positions the schedule S gives
       g4_static_for(std::make_integer_sequence<int, 128>{}, [&](auto G) {
         constexpr int g = decltype(G)::value;
-        if constexpr (g < 64) mf(P, g); else mf(Q, g - 64);
-        if constexpr (g >= S::q0 && g < S::q0 + 16 * S::qs && (g - S::q0) % S::qs == 0)
-          rd(Q, (g - S::q0) / S::qs, 1, s);
+        if constexpr (F8) {   // one 32x32x64 MFMA per 4 slots
+          if constexpr (g % 4 == 0) {
+            if constexpr (g < 64) mf8(P8, g / 4); else mf8(Q8, (g - 64) / 4);
+          }
+        } else {
+          if constexpr (g < 64) mf(P, g); else mf(Q, g - 64);
+        }
+        if constexpr (g >= S::q0 && g < S::q0 + 16 * S::qs && (g - S::q0) % S::qs == 0) {
+          if constexpr (F8) rd8(Q8, (g - S::q0) / S::qs, 1, s); else rd(Q, (g - S::q0) / S::qs, 1, s);
+        }
         if constexpr (g == S::b1) {   // this wave's reads of stage s done -> after B1 every wave's
           g4_sync_lds();
           if (DMA) g4_barrier();
@@ -255,8 +346,10 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
           if (DMA) g4_vmcnt<S::vm>(); else g4_vmcnt<0>();
           g4_barrier();
         }
-        if constexpr (NEXT && g >= S::p0 && g < S::p0 + 16 * S::ps && (g - S::p0) % S::ps == 0)
-          rd(P, (g - S::p0) / S::ps, 0, s ^ 1);
+        if constexpr (NEXT && g >= S::p0 && g < S::p0 + 16 * S::ps && (g - S::p0) % S::ps == 0) {
+          if constexpr (F8) rd8(P8, (g - S::p0) / S::ps, 0, s ^ 1);
+          else rd(P, (g - S::p0) / S::ps, 0, s ^ 1);
+        }
       });
       if (NEXT) g4_sync_lds();
     };
@@ -274,13 +367,72 @@ gemm4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __res
     // the last MFMAs' results -> compiler-issued AGPR reads: 12+ wait states for an 8-pass XDL
     // write; the fence takes every accumulator "+a" so no read is hoisted above it
     asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    if constexpr (F8) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-      asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]),
-                   "+a"(acc[i][4]), "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+      for (int i = 0; i < 4; ++i)
+        asm volatile("" : "+a"(acc8[i][0]), "+a"(acc8[i][1]), "+a"(acc8[i][2]), "+a"(acc8[i][3]));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]),
+                     "+a"(acc[i][4]), "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
+    }
 
     // ---- epilogue: fragment (i, j) element e of lane l is
     //      C[m0 + wr*128 + 16i + (l & 15)][n0 + wc*128 + 16j + 4(l >> 4) + e] ----
+    if constexpr (F8) {
+      // 32x32 tile (mi, ni) element r of lane l: row m0 + wr*128 + 32 mi + (l & 31), column
+      // n0 + wc*128 + 32 ni + 8 (r >> 2) + 4 (l >> 5) + (r & 3): 4 consecutive columns per group
+      const int c4 = 4 * (lane >> 5);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int row = m0 + wr * 128 + 32 * mi + (lane & 31);
+        if (row >= M) continue;
+        const float sa = a_scale[row];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int nb = n0 + wc * 128 + 32 * ni + c4;
+          if constexpr (EPI == kG4SwiGLU) {
+            // groups 0, 1 = gate of output columns 16 q + 8 g + c4 + e (q = wc*4 + ni), 2, 3 = up
+            bf16* out = reinterpret_cast<bf16*>(C);
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+              const f32x4 sg = *reinterpret_cast<const f32x4*>(b_scale + nb + 8 * g);
+              const f32x4 su = *reinterpret_cast<const f32x4*>(b_scale + nb + 8 * g + 16);
+              bf16x4 o;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float gv = (float)(bf16)(acc8[mi][ni][4 * g + e] * sg[e] * sa);
+                const float uv = (float)(bf16)(acc8[mi][ni][4 * g + 8 + e] * su[e] * sa);
+                o[e] = (bf16)(g4_silu(gv) * uv);
+              }
+              *reinterpret_cast<bf16x4*>(out + (size_t)row * (N >> 1) + (n0 >> 1) + wc * 64 +
+                                         16 * ni + 8 * g + c4) = o;
+            }
+          } else {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const f32x4 sb = *reinterpret_cast<const f32x4*>(b_scale + nb + 8 * g);
+              f32x4 v;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = acc8[mi][ni][4 * g + e] * sb[e] * sa;
+              const size_t idx = (size_t)row * N + nb + 8 * g;
+              if constexpr (EPI == kG4F32) {
+                *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + (size_t)split * M * N + idx) = v;
+              } else {
+                bf16x4 o;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+                bf16* out = reinterpret_cast<bf16*>(C) + (EPI == kG4Bf16Part ? (size_t)split * M * N : 0);
+                *reinterpret_cast<bf16x4*>(out + idx) = o;
+              }
+            }
+          }
+        }
+      }
+      g4_barrier();
+      continue;
+    }
     const int crow = m0 + wr * 128 + fr;
     const int cq = 4 * (lane >> 4);
     if constexpr (EPI == kG4SwiGLU) {
@@ -361,22 +513,22 @@ int gemm4_grid(int items, int cus) {
 // C = A . B^T on the one-wave-per-SIMD kernel.  epilogue 0: bf16 [M, N]; 2: fused SwiGLU ([M,
 // N/2], B rows in swiglu_interleave order); with splits > 1: 1 = fp32 partials [splits, M, N],
 // 4 = bf16 partials [splits, M, N] (into C; the consumer sums them).  grid <= 0: automatic.
-template <int VAR>
-static int launch_gemm4_v(void* C, const bf16* a, const bf16* b, int M, int N, int K, int tiles_m,
+template <int VAR, int PREC>
+static int launch_gemm4_v(void* C, const void* a, const void* b, int M, int N, int K, int tiles_m,
                           int tiles_n, int kps, int splits, int epilogue, int grid,
-                          hipStream_t stream) {
+                          hipStream_t stream, const float* sa, const float* sb) {
   switch (epilogue) {
     case kG4Bf16:
-      gemm4_kernel<kG4Bf16, VAR><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      gemm4_kernel<kG4Bf16, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb);
       break;
     case kG4F32:
-      gemm4_kernel<kG4F32, VAR><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      gemm4_kernel<kG4F32, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb);
       break;
     case kG4SwiGLU:
-      gemm4_kernel<kG4SwiGLU, VAR><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      gemm4_kernel<kG4SwiGLU, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb);
       break;
     case kG4Bf16Part:
-      gemm4_kernel<kG4Bf16Part, VAR><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits);
+      gemm4_kernel<kG4Bf16Part, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb);
       break;
     default:
       return -4;
@@ -384,14 +536,41 @@ static int launch_gemm4_v(void* C, const bf16* a, const bf16* b, int M, int N, i
   return 0;
 }
 
+template <int PREC>
+static int launch_gemm4_p(void* C, const void* a, const void* b, int M, int N, int K, int tiles_m,
+                          int tiles_n, int kps, int splits, int epilogue, int grid,
+                          hipStream_t stream, int variant, const float* sa, const float* sb) {
+#ifndef DLI_GEMM4_ALL_VARIANTS   // the library carries the default schedule only
+  if (variant != kG4Default) return -5;
+  return launch_gemm4_v<kG4Default, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+#else
+  switch (variant) {
+    case 0: return launch_gemm4_v<0, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+    case 1: return launch_gemm4_v<1, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+    case 2: return launch_gemm4_v<2, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+    case 3: return launch_gemm4_v<3, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+    case 4: return launch_gemm4_v<4, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+    case 5: return launch_gemm4_v<5, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+    case 6: return launch_gemm4_v<6, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+    case 7: return launch_gemm4_v<7, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+  }
+  return -5;
+#endif
+}
+
 // C = A . B^T on the one-wave-per-SIMD kernel.  epilogue 0: bf16 [M, N]; 2: fused SwiGLU ([M,
 // N/2], B rows in swiglu_interleave order); with splits > 1: 1 = fp32 partials [splits, M, N],
 // 4 = bf16 partials [splits, M, N] (into C; the consumer sums them).  grid <= 0: automatic.
 // variant < 0: the default k-loop schedule (G4Sched), else that one (A/B experiments).
+// precision 1: fp8 e4m3 A [M, K] / B [N, K] (1-byte), results scaled by a_scale[M] * b_scale[N].
 int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int splits,
-                 int epilogue, int grid, hipStream_t stream, int variant) {
-  if (M <= 0 || N % 256 != 0 || (K * 2) % 128 != 0 || splits < 1) return -1;
-  const int kt = K * 2 / 128;
+                 int epilogue, int grid, hipStream_t stream, int variant, int precision,
+                 const float* a_scale, const float* b_scale) {
+  const int esz = precision == 1 ? 1 : 2;
+  if (precision != 0 && precision != 1) return -6;
+  if (precision == 1 && (a_scale == nullptr || b_scale == nullptr)) return -7;
+  if (M <= 0 || N % 256 != 0 || (K * esz) % 128 != 0 || splits < 1) return -1;
+  const int kt = K * esz / 128;
   if (splits > kt) return -2;
   const int kps = (kt + splits - 1) / splits;
   if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
@@ -400,18 +579,12 @@ int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int
   const int items = tiles_m * tiles_n * splits;
   if (grid <= 0) grid = gemm4_grid(items, g4_cus());
   if (grid > items) grid = items;
-  const bf16* a = reinterpret_cast<const bf16*>(A);
-  const bf16* b = reinterpret_cast<const bf16*>(B);
   if (variant < 0) variant = kG4Default;
-  switch (variant) {
-    case 0: return launch_gemm4_v<0>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
-    case 1: return launch_gemm4_v<1>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
-    case 2: return launch_gemm4_v<2>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
-    case 3: return launch_gemm4_v<3>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
-    case 4: return launch_gemm4_v<4>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
-    case 5: return launch_gemm4_v<5>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream);
-  }
-  return -5;
+  if (precision == 1)
+    return launch_gemm4_p<1>(C, A, B, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid,
+                             stream, variant, a_scale, b_scale);
+  return launch_gemm4_p<0>(C, A, B, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream,
+                           variant, nullptr, nullptr);
 }
 
 }  // namespace dli

@@ -138,8 +138,10 @@ int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, 
                        const GemvNorm* nm = nullptr, const GemvRope* rp = nullptr);
 // one-wave-per-SIMD 256x256 GEMM (gemm4.hip); epilogue 0 bf16, 1 fp32 partials, 2 SwiGLU,
 // 4 bf16 partials; grid <= 0: automatic persistent grid; variant < 0: default k-loop schedule
+// precision 1: fp8 e4m3 operands with per-row a_scale [M] and per-channel b_scale [N]
 int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int splits,
-                 int epilogue, int grid, hipStream_t stream, int variant = -1);
+                 int epilogue, int grid, hipStream_t stream, int variant = -1, int precision = 0,
+                 const float* a_scale = nullptr, const float* b_scale = nullptr);
 int gemm4_grid(int items, int cus);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
                          bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,

@@ -511,27 +511,31 @@ def gemm4_enabled() -> bool:
 
 
 def _gemm4(x: torch.Tensor, w: torch.Tensor, splits: int, swiglu: bool,
-           out: Optional[torch.Tensor], defer_reduce: bool):
+           out: Optional[torch.Tensor], defer_reduce: bool,
+           xs: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None):
     """:func:`gemm_tile`'s contract on gemm4: same epilogues (bf16 store, fused SwiGLU, split-K
-    partials handed to the consumer or reduced here), bit-identical results."""
+    partials handed to the consumer or reduced here), bit-identical results for bf16.  fp8 e4m3
+    operands (``xs`` [M] / ``ws`` [N] scales) run the block-scaled 32x32x64 MFMA
+    (:func:`gemm_tile_fp8`'s contract, bf16 output)."""
     M, N = x.shape[0], w.shape[0]
     splits = max(1, int(splits))
+    fp8 = xs is not None
     if splits > 1 and defer_reduce and not swiglu and \
             os.environ.get("DLI_SPLITK_DEFER", "1") == "1":
-        bf = bf16_bf16_partials()
+        bf = fp8_bf16_partials() if fp8 else bf16_bf16_partials()
         parts = torch.empty(splits, M, N, dtype=torch.bfloat16 if bf else torch.float32,
                             device=x.device)
-        native().gemm4(parts, x, w, splits, 4 if bf else 1)
+        native().gemm4(parts, x, w, splits, 4 if bf else 1, 0, xs, ws)
         return SplitKPartials(parts)
     if out is None:
-        out = torch.empty(M, N // 2 if swiglu else N, dtype=x.dtype, device=x.device)
+        out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
     if splits == 1:
-        native().gemm4(out, x, w, 1, 2 if swiglu else 0)
+        native().gemm4(out, x, w, 1, 2 if swiglu else 0, 0, xs, ws)
         return out
     if swiglu:
         raise ValueError("gemm4: fused SwiGLU takes whole-K tiles (splits = 1)")
     parts = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
-    native().gemm4(parts, x, w, splits, 1)
+    native().gemm4(parts, x, w, splits, 1, 0, xs, ws)
     native().splitk_reduce(out, parts)
     return out
 
@@ -777,6 +781,9 @@ def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torc
         native().gemm_tile(q, xq, wq, 1, 3, None, xs.reshape(-1).contiguous(),
                            ws.reshape(-1).contiguous(), out_mx=sc)
         return MxFp8(q, sc)
+    if _gpu(xq) and gemm4_enabled() and xq.shape[1] % 128 == 0:
+        return _gemm4(xq, wq, splits, swiglu, out, defer_reduce,
+                      xs.reshape(-1).contiguous(), ws.reshape(-1).contiguous())
     if (defer_reduce and splits > 1 and _gpu(xq) and not swiglu
             and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
         if fp8_bf16_partials():

@@ -10,6 +10,7 @@
 //         scripts/experiments/gemm4_bench.hip -o tools_bin/gemm4_bench
 //   tools_bin/gemm4_bench [rounds] [gate|up grid override]
 #define DLI_GEMM_STAMPS 1
+#define DLI_GEMM4_ALL_VARIANTS 1
 #include "../../distributed_llm_inference/csrc/kernels/gemm_tile.hip"
 #include "../../distributed_llm_inference/csrc/kernels/gemm4.hip"
 
@@ -44,7 +45,7 @@ struct Shape { const char* name; int M, N, K, splits, epi; };
 
 static int g_grid = 0;
 static int g_var = 0;   // gemm4 schedule variant under check
-constexpr int kVars = 6;
+constexpr int kVars = 8;
 
 static int check(const Shape& c) {
   int bad = 0;

@@ -573,3 +573,45 @@ def test_gemm4_bit_identical_to_gemm_tile(gpu, M, N, K, splits, epi):
         nat.gemm4(out, a, b, splits, epi, grid)
         torch.cuda.synchronize()
         assert torch.equal(out, ref), (grid, (out.float() - ref.float()).abs().max().item())
+
+
+def _q8(x):
+    s = (x.float().abs().amax(1) / 448.0).clamp_min(1e-12)
+    return (x.float() / s[:, None]).to(torch.float8_e4m3fn), s.contiguous()
+
+
+@pytest.mark.parametrize("M", [512, 300, 40])
+@pytest.mark.parametrize("N,K,splits,epi", [(2048, 1024, 1, 0), (4096, 2048, 1, 2),
+                                            (1024, 4096, 3, 1), (1024, 4096, 4, 4),
+                                            (7680, 512, 1, 0)])
+def test_gemm4_fp8_matches_gemm_tile_fp8(gpu, M, N, K, splits, epi):
+    """fp8 gemm4 (block-scaled 32x32x64 MFMA, unit block scales, per-row x per-channel scales in
+    the epilogue) against gemm_tile's fp8 path on the same quantised operands and against the fp32
+    product of the dequantised operands."""
+    torch.manual_seed(M + N + splits + 1)
+    a, sa = _q8(torch.randn(M, K, device=gpu))
+    b, sb = _q8(torch.randn(N, K, device=gpu) * 0.05)
+    nat = ops.native()
+    full = (a.float() * sa[:, None]) @ (b.float() * sb[:, None]).t()
+    if epi in (1, 4):
+        ref = torch.empty(splits, M, N, device=gpu, dtype=torch.float32)
+        nat.gemm_tile(torch.empty(M, 0, device=gpu, dtype=torch.bfloat16), a, b, splits, 1,
+                      ref.view(-1), sa, sb)
+        out = torch.empty(splits, M, N, device=gpu,
+                          dtype=torch.bfloat16 if epi == 4 else torch.float32)
+        f32 = full
+    else:
+        cols = N // 2 if epi == 2 else N
+        ref = torch.empty(M, cols, device=gpu, dtype=torch.bfloat16)
+        nat.gemm_tile(ref, a, b, 1, epi, None, sa, sb)
+        out = torch.empty_like(ref)
+        f32 = ops.swiglu_interleaved(full) if epi == 2 else full
+    scale = f32.abs().max().item()
+    for grid in (0, 7):
+        out.fill_(7.0)
+        nat.gemm4(out, a, b, splits, epi, grid, sa, sb)
+        torch.cuda.synchronize()
+        got = out.float().sum(0) if epi in (1, 4) else out.float()
+        want = ref.float().sum(0) if epi in (1, 4) else ref.float()
+        assert (got - want).abs().max().item() < 2e-2 * scale, grid
+        assert (got - f32).abs().max().item() < 2e-2 * scale, grid
