@@ -88,8 +88,11 @@ template <> struct G4Sched<7> {   // v4 with the DMA 1 per 5 MFMAs (14 before B2
   static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 5, b2 = 104, vm = 14, p0 = 105, ps = 1;
 };
 constexpr int kG4Variants = 8;
-// measured fastest on every decode shape and 8192^3 (profiles/r4/gemm4_ab_v0-5.txt)
-constexpr int kG4Default = 4;
+// Default schedules (profiles/r4/gemm4_ab_v0-7.txt): decode-sized M (<= 2 row tiles, the
+// activations stay L2 / MALL-resident and only the weight stream misses) takes v6, whose DMA runs
+// the latest and thinnest (gate|up 377 vs 415 us gemm_tile, down 187 vs 199); larger M, where
+// both operands stream from HBM and a short DMA lead stalls (8192^3: v6 1074 us), takes v4.
+constexpr int kG4Default = 4, kG4DecodeDefault = 6;
 
 __device__ __forceinline__ float g4_silu(float x) { return x / (1.f + __expf(-x)); }
 
@@ -540,7 +543,9 @@ template <int PREC>
 static int launch_gemm4_p(void* C, const void* a, const void* b, int M, int N, int K, int tiles_m,
                           int tiles_n, int kps, int splits, int epilogue, int grid,
                           hipStream_t stream, int variant, const float* sa, const float* sb) {
-#ifndef DLI_GEMM4_ALL_VARIANTS   // the library carries the default schedule only
+#ifndef DLI_GEMM4_ALL_VARIANTS   // the library carries the default schedules only
+  if (variant == kG4DecodeDefault)
+    return launch_gemm4_v<kG4DecodeDefault, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
   if (variant != kG4Default) return -5;
   return launch_gemm4_v<kG4Default, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
 #else
@@ -579,7 +584,7 @@ int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int
   const int items = tiles_m * tiles_n * splits;
   if (grid <= 0) grid = gemm4_grid(items, g4_cus());
   if (grid > items) grid = items;
-  if (variant < 0) variant = kG4Default;
+  if (variant < 0) variant = tiles_m <= 2 ? kG4DecodeDefault : kG4Default;
   if (precision == 1)
     return launch_gemm4_p<1>(C, A, B, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid,
                              stream, variant, a_scale, b_scale);

@@ -605,7 +605,7 @@ def test_gemm4_fp8_matches_gemm_tile_fp8(gpu, M, N, K, splits, epi):
         ref = torch.empty(M, cols, device=gpu, dtype=torch.bfloat16)
         nat.gemm_tile(ref, a, b, 1, epi, None, sa, sb)
         out = torch.empty_like(ref)
-        f32 = ops.swiglu_interleaved(full) if epi == 2 else full
+        f32 = ops.swiglu_interleaved(full.cpu()).to(gpu) if epi == 2 else full   # fp32 reference
     scale = f32.abs().max().item()
     for grid in (0, 7):
         out.fill_(7.0)
