@@ -504,10 +504,15 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = 
     return out
 
 
-def gemm4_enabled() -> bool:
-    """bf16 decode projections on the one-wave-per-SIMD kernel (csrc/kernels/gemm4.hip) instead
-    of gemm_tile: ``DLI_GEMM4=1`` (read per call, so a captured graph keeps its choice)."""
-    return os.environ.get("DLI_GEMM4", "0") == "1"
+def gemm4_enabled(fp8: bool = False) -> bool:
+    """Decode projections on the one-wave-per-SIMD kernel (csrc/kernels/gemm4.hip) instead of
+    gemm_tile (read per call, so a captured graph keeps its choice).  bf16: ``DLI_GEMM4=1``
+    (default; 70B decode step 75.0 vs 77.7 ms, profiles/r4/gemm4_step_ab.txt).  fp8:
+    ``DLI_GEMM4_FP8=1`` (default off: the K = 8192 QKV / O products it takes measured 0.8 %
+    slower in-step; gate|up and down stay on gemm_tile's MX epilogues either way)."""
+    if fp8:
+        return os.environ.get("DLI_GEMM4_FP8", "0") == "1"
+    return os.environ.get("DLI_GEMM4", "1") == "1"
 
 
 def _gemm4(x: torch.Tensor, w: torch.Tensor, splits: int, swiglu: bool,
@@ -781,7 +786,7 @@ def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torc
         native().gemm_tile(q, xq, wq, 1, 3, None, xs.reshape(-1).contiguous(),
                            ws.reshape(-1).contiguous(), out_mx=sc)
         return MxFp8(q, sc)
-    if _gpu(xq) and gemm4_enabled() and xq.shape[1] % 128 == 0:
+    if _gpu(xq) and gemm4_enabled(fp8=True) and xq.shape[1] % 128 == 0:
         return _gemm4(xq, wq, splits, swiglu, out, defer_reduce,
                       xs.reshape(-1).contiguous(), ws.reshape(-1).contiguous())
     if (defer_reduce and splits > 1 and _gpu(xq) and not swiglu

@@ -39,7 +39,17 @@ __global__ void fill_rand(__bf16* p, size_t n, unsigned seed, float scale) {
   }
 }
 
+__global__ void fill_fp8(unsigned char* p, size_t n, unsigned seed) {   // finite e4m3, |x| < 256
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    unsigned x = (unsigned)i * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    p[i] = (unsigned char)(x & 0xF7u);   // exponent field <= 14
+  }
+}
+
 static float bf2f(__bf16 v) { return (float)v; }
+static bool g_fp8 = false;   // argv[3] == "fp8": time the fp8 e4m3 paths (checks: tests/test_gemm_gpu.py)
 
 struct Shape { const char* name; int M, N, K, splits, epi; };
 
@@ -137,40 +147,58 @@ int main(int argc, char** argv) {
   };
   const int rounds = argc > 1 ? atoi(argv[1]) : 7;
   if (argc > 2) g_grid = atoi(argv[2]);
+  g_fp8 = argc > 3 && strcmp(argv[3], "fp8") == 0;
   // every launch of this build writes per-workgroup stamps: point them at a buffer first
   unsigned long long* sb;
   CK(hipMalloc(&sb, (size_t)8192 * 64));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(dli::g_stamp_blk), &sb, sizeof(sb)));
   int bad = 0;
-  for (g_var = 0; g_var < kVars; ++g_var)
+  for (g_var = 0; g_var < kVars && !g_fp8; ++g_var)
     for (auto& c : shapes)
       if (c.M <= 512) bad += check(c);
   if (bad) { printf("CHECK FAILED\n"); return 2; }
   for (auto& c : shapes) {
-    const size_t wbytes = (size_t)c.N * c.K * 2;
+    const int esz = g_fp8 ? 1 : 2;
+    const size_t wbytes = (size_t)c.N * c.K * esz;
     const int sets = (int)std::max<size_t>(2, std::min<size_t>(6, 1200000000ull / wbytes + 1));
     __bf16 *A, *C;
     std::vector<__bf16*> B(sets);
     float* ws = nullptr;
-    CK(hipMalloc(&A, (size_t)c.M * c.K * 2));
+    float *sa, *sb8;
+    CK(hipMalloc(&sa, (size_t)c.M * 4));
+    CK(hipMalloc(&sb8, (size_t)c.N * 4));
+    {
+      std::vector<float> ones((size_t)std::max(c.M, c.N), 1.f / 64);
+      CK(hipMemcpy(sa, ones.data(), (size_t)c.M * 4, hipMemcpyHostToDevice));
+      CK(hipMemcpy(sb8, ones.data(), (size_t)c.N * 4, hipMemcpyHostToDevice));
+    }
+    CK(hipMalloc(&A, (size_t)c.M * c.K * esz));
     for (auto& b : B) CK(hipMalloc(&b, wbytes));
     CK(hipMalloc(&C, (size_t)c.M * c.N * 2));
     if (c.splits > 1) CK(hipMalloc(&ws, (size_t)c.splits * c.M * c.N * 4));
     // the production gate|up launch of the 8-wave kernel: whole tiles + stream-K tail
-    const bool tile_sk = c.epi == 2 && dli::gemm_tile_sk_workspace_floats() > 0;
+    const bool tile_sk = !g_fp8 && c.epi == 2 && dli::gemm_tile_sk_workspace_floats() > 0;
     float* sk_ws = nullptr;
     if (tile_sk) CK(hipMalloc(&sk_ws, (size_t)dli::gemm_tile_sk_workspace_floats() * 4));
-    fill_rand<<<1024, 256>>>(A, (size_t)c.M * c.K, 1, 1.f);
-    for (int i = 0; i < sets; ++i) fill_rand<<<4096, 256>>>(B[i], (size_t)c.N * c.K, 7 + i, 0.02f);
+    if (g_fp8) {
+      fill_fp8<<<1024, 256>>>((unsigned char*)A, (size_t)c.M * c.K, 1);
+      for (int i = 0; i < sets; ++i) fill_fp8<<<4096, 256>>>((unsigned char*)B[i], (size_t)c.N * c.K, 7 + i);
+    } else {
+      fill_rand<<<1024, 256>>>(A, (size_t)c.M * c.K, 1, 1.f);
+      for (int i = 0; i < sets; ++i) fill_rand<<<4096, 256>>>(B[i], (size_t)c.N * c.K, 7 + i, 0.02f);
+    }
     const int epi = c.splits > 1 ? 1 : c.epi;
     const int grid = (c.epi == 2 && g_grid > 0) ? g_grid : 0;
     auto run = [&](int v, int i) {
-      int rc = v == 0 ? dli::launch_gemm_tile(C, A, B[i % sets], nullptr, nullptr,
-                                              tile_sk ? sk_ws : ws, c.M, c.N, c.K,
-                                              tile_sk ? 0 : c.splits, epi, 0, 0, nullptr, nullptr,
-                                              0, nullptr, nullptr, nullptr)
+      int rc = v == 0 ? dli::launch_gemm_tile(C, A, B[i % sets], g_fp8 ? sa : nullptr,
+                                              g_fp8 ? sb8 : nullptr, tile_sk ? sk_ws : ws, c.M,
+                                              c.N, c.K, tile_sk ? 0 : c.splits, epi,
+                                              g_fp8 ? dli::kFp8 : 0, 0, nullptr, nullptr, 0,
+                                              nullptr, nullptr, nullptr)
                       : dli::launch_gemm4(c.splits > 1 ? (void*)ws : (void*)C, A, B[i % sets],
-                                          c.M, c.N, c.K, c.splits, epi, grid, 0, v - 1);
+                                          c.M, c.N, c.K, c.splits, epi, grid, 0, v - 1,
+                                          g_fp8 ? 1 : 0, g_fp8 ? sa : nullptr,
+                                          g_fp8 ? sb8 : nullptr);
       if (rc) { fprintf(stderr, "rc %d\n", rc); exit(1); }
     };
     hipEvent_t e0, e1;
@@ -214,7 +242,7 @@ int main(int argc, char** argv) {
       std::sort(cyc.begin(), cyc.end());
       std::sort(clk.begin(), clk.end());
       // k-tiles per workgroup: gemm_tile = one item each (stream-K: ~ the same), gemm4 = items / grid
-      const double kt_item = (double)c.K * 2 / 128 / c.splits;
+      const double kt_item = (double)c.K * esz / 128 / c.splits;
       const double per_wg = v == 0 ? kt_item * (double)items / wgs : kt_item * ((double)items / wgs);
       if (!cyc.empty())
         printf("%-16s %s%d stamps: %d wgs, med %.0f cyc/wg = %.0f per k-tile, clock %.2f GHz\n",
@@ -222,14 +250,14 @@ int main(int argc, char** argv) {
                cyc[cyc.size() / 2] / per_wg, clk.empty() ? 0.0 : clk[clk.size() / 2]);
     }
     const double fl = 2.0 * c.M * c.N * c.K;
-    printf("%-16s M=%d N=%d K=%d s=%d | gemm_tile %.1f us (min %.1f, %.0f TF)", c.name, c.M, c.N,
+    printf("%s%-16s M=%d N=%d K=%d s=%d | gemm_tile %.1f us (min %.1f, %.0f TF)", g_fp8 ? "fp8 " : "", c.name, c.M, c.N,
            c.K, c.splits, t[0][t[0].size() / 2], t[0][0], fl / t[0][t[0].size() / 2] / 1e6);
     for (int v = 1; v <= kVars; ++v)
       printf(" | v%d %.1f us (%.0f TF, %.3f)", v - 1, t[v][t[v].size() / 2],
              fl / t[v][t[v].size() / 2] / 1e6, t[v][t[v].size() / 2] / t[0][t[0].size() / 2]);
     printf("\n");
     fflush(stdout);
-    CK(hipFree(A));
+    CK(hipFree(A)); CK(hipFree(sa)); CK(hipFree(sb8));
     for (auto& b : B) CK(hipFree(b));
     CK(hipFree(C));
     if (ws) CK(hipFree(ws));

@@ -1,5 +1,5 @@
 #!/bin/bash
-# In-step A/B of the bf16 decode projections: gemm_tile (default) vs gemm4 (DLI_GEMM4=1),
+# In-step A/B of the decode projections: gemm_tile (DLI_GEMM4=0) vs gemm4 (DLI_GEMM4=1, default),
 # bench.py back to back, interleaved twice; extra bench.py arguments (e.g. --fp8) in $1
 set -u
 mkdir -p gpurun_out/ab

@@ -68,7 +68,7 @@ for fmt in (sys.argv[1:] or ["bf16", "fp8", "int8"]):
         ws = weights(fmt, N, K)
         sc = torch.rand(N, device=dev) * 1e-2 + 1e-3
         x = torch.randn(1, K, device=dev, dtype=torch.bfloat16)
-        fns = [(lambda w=w: call(fmt, x, w, sc, sw)) for w in ws]
+        fns = [(lambda w=w, x=x, sc=sc, sw=sw: call(fmt, x, w, sc, sw)) for w in ws]
         us = timed_graph(fns) / L
         b = N * K * esz
         out[name] = {"us": round(us, 2), "TBps": round(b / us / 1e6, 2)}
