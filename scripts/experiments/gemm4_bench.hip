@@ -231,16 +231,26 @@ int main(int argc, char** argv) {
       CK(hipDeviceSynchronize());
       std::vector<unsigned long long> h((size_t)wgs * 8);
       CK(hipMemcpy(h.data(), sb, h.size() * 8, hipMemcpyDeviceToHost));
-      std::vector<double> cyc, clk;
+      std::vector<double> cyc, clk, life;
+      unsigned long long t0 = ~0ull, s1 = 0, e1 = 0;
       for (int b = 0; b < wgs; ++b) {
         const unsigned long long* q = &h[(size_t)b * 8];
         if (q[3] <= q[1]) continue;
+        t0 = std::min(t0, q[0]);
+        s1 = std::max(s1, q[0]);
+        e1 = std::max(e1, q[2]);
+        life.push_back((q[2] - q[0]) / 100.0);
         cyc.push_back((double)(q[3] - q[1]));
         const double us = (q[2] - q[0]) / 100.0;
         if (us > 0) clk.push_back((q[3] - q[1]) / us / 1e3);
       }
       std::sort(cyc.begin(), cyc.end());
       std::sort(clk.begin(), clk.end());
+      std::sort(life.begin(), life.end());
+      if (!life.empty())   // dispatch skew and the slowest workgroup, wall-clock (100 MHz ticks)
+        printf("%-16s %s%d wall: start skew %.1f us, WG life med %.1f / max %.1f us, span %.1f us\n",
+               c.name, v == 0 ? "gemm_tile" : "gemm4 v", v - 1, (s1 - t0) / 100.0,
+               life[life.size() / 2], life.back(), (e1 - t0) / 100.0);
       // k-tiles per workgroup: gemm_tile = one item each (stream-K: ~ the same), gemm4 = items / grid
       const double kt_item = (double)c.K * esz / 128 / c.splits;
       const double per_wg = v == 0 ? kt_item * (double)items / wgs : kt_item * ((double)items / wgs);
