@@ -676,7 +676,7 @@ def test_gemm4_dispatch_bit_identical_in_a_decode_step(gpu, monkeypatch):
 
     def step(flag):
         monkeypatch.setenv("DLI_GEMM4", flag)
-        pool = g.make_pool(64, block_size=64)
+        pool = g.make_pool(320, block_size=64)   # one block per sequence
         sids = list(range(len(prompts)))
         for sid, p in zip(sids, prompts):
             pool.manager.append(sid, len(p))
