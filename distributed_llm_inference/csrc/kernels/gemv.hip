@@ -32,11 +32,70 @@ constexpr int kUnroll = 4;
 // launch per norm in the 1-2 row decode step, where every launch costs its dispatch latency.
 extern __shared__ __attribute__((aligned(16))) char gemv_lds[];
 
+// rows of K <= 8 * 4 * 256 (every Llama hidden size up to 8192): each thread's 4 vectors of every
+// row (and the norm weight) are loaded in one burst and kept in registers through the reduction --
+// one L2 round trip instead of the generic loop's one per vector and a second pass for w.  Same
+// vector assignment and fma order as the generic loop, so the same bits.
+template <int M>
+__device__ __forceinline__ void gemv_norm_prologue_regs(const bf16* __restrict__ x,
+                                                        const GemvNorm& nm, int K,
+                                                        float* scratch) {
+  constexpr int VPT = 4;
+  const int nvec = K >> 3;
+  bf16x8* xs = reinterpret_cast<bf16x8*>(gemv_lds);
+  const bf16x8* w8 = reinterpret_cast<const bf16x8*>(nm.w);
+  bf16x8 wv[VPT], a[M][VPT], rv[M][VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) wv[i] = w8[row_vec_idx(i, nvec)];
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      a[m][i] = reinterpret_cast<const bf16x8*>(x + (size_t)m * K)[row_vec_idx(i, nvec)];
+      if (nm.res_in != nullptr)
+        rv[m][i] = reinterpret_cast<const bf16x8*>(nm.res_in + (size_t)m * K)[row_vec_idx(i, nvec)];
+    }
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    bf16x8* ro = nm.res_out ? reinterpret_cast<bf16x8*>(nm.res_out + (size_t)m * K) : nullptr;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      if (!row_valid(i, nvec)) continue;
+      if (nm.res_in != nullptr) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[m][i][j] = (bf16)((float)a[m][i][j] + (float)rv[m][i][j]);
+        if (ro != nullptr && blockIdx.x == 0) ro[threadIdx.x + i * blockDim.x] = a[m][i];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = (float)a[m][i][j];
+        ss = __builtin_fmaf(v, v, ss);
+      }
+    }
+    ss = block_reduce_sum(ss, scratch);
+    const float rstd = rsqrtf(ss / (float)K + nm.eps);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      if (!row_valid(i, nvec)) continue;
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)a[m][i][j] * rstd * (float)wv[i][j]);
+      xs[(size_t)m * nvec + threadIdx.x + i * blockDim.x] = o;
+    }
+  }
+  __syncthreads();
+}
+
 template <int M>
 __device__ __forceinline__ void gemv_norm_prologue(const bf16* __restrict__ x, const GemvNorm& nm,
                                                    int K) {
   __shared__ float scratch[8];
   const int nvec = K >> 3;
+  if (nvec <= 4 * (int)blockDim.x) {
+    gemv_norm_prologue_regs<M>(x, nm, K, scratch);
+    return;
+  }
   bf16* xs = reinterpret_cast<bf16*>(gemv_lds);
   const bf16x8* w8 = reinterpret_cast<const bf16x8*>(nm.w);
 #pragma unroll
@@ -171,6 +230,24 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int n0 = wave * kRows;
+  const bf16* wrow[kRows];   // rows clamped: the loads below never leave W, even for idle waves
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<EP>(wave, r, rp), N - 1) * K;
+  constexpr int kStep = 64 * 8;  // elements per wave instruction
+  bf16x8 wv[kUnroll][kRows];
+  auto load_w = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int k = k0 + u * kStep;
+#pragma unroll
+      for (int r = 0; r < kRows; ++r)
+        wv[u][r] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wrow[r] + k))
+                         : bf16x8{};
+    }
+  };
+  // the first k-group of weights does not depend on x: in flight before the norm prologue
+  const int kfirst = lane * 8;
+  load_w(kfirst);
   if constexpr (NORM) gemv_norm_prologue<M>(x_in, nm, K);   // every thread, before any exit
   const bf16* x = NORM ? reinterpret_cast<const bf16*>(gemv_lds) : x_in;
   if ((EP != kEpPlain ? 2 * wave : n0) >= N) return;
@@ -180,30 +257,15 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
 #pragma unroll
     for (int r = 0; r < kRows; ++r) acc[m][r] = 0.f;
 
-  const bf16* wrow[kRows];
-#pragma unroll
-  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<EP>(wave, r, rp), N - 1) * K;
-
-  constexpr int kStep = 64 * 8;  // elements per wave instruction
-  for (int k0 = lane * 8; k0 < K; k0 += kStep * kUnroll) {
-    bf16x8 wv[kUnroll][kRows];
+  for (int k0 = kfirst; k0 < K; k0 += kStep * kUnroll) {
+    if (k0 != kfirst) load_w(k0);
     bf16x8 xv[kUnroll][M];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int k = k0 + u * kStep;
-      if (k < K) {
 #pragma unroll
-        for (int r = 0; r < kRows; ++r)
-          wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wrow[r] + k));
-#pragma unroll
-        for (int m = 0; m < M; ++m)
-          xv[u][m] = *reinterpret_cast<const bf16x8*>(x + (size_t)m * K + k);
-      } else {
-#pragma unroll
-        for (int r = 0; r < kRows; ++r) wv[u][r] = bf16x8{};
-#pragma unroll
-        for (int m = 0; m < M; ++m) xv[u][m] = bf16x8{};
-      }
+      for (int m = 0; m < M; ++m)
+        xv[u][m] = k < K ? *reinterpret_cast<const bf16x8*>(x + (size_t)m * K + k) : bf16x8{};
     }
     // v_dot2c_f32_bf16: two bf16 products accumulated in fp32 per instruction, no conversions
 #pragma unroll
@@ -263,6 +325,24 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
   const int n0 = wave * kRows;
+  const uint8_t* wrow[kRows];   // rows clamped: the loads below never leave W, even for idle waves
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<EP>(wave, r, rp), N - 1) * K;
+  constexpr int kStep = 64 * 16;  // elements per wave instruction
+  u32x4n wv[kUnroll][kRows];
+  auto load_w = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int k = k0 + u * kStep;
+#pragma unroll
+      for (int r = 0; r < kRows; ++r)
+        wv[u][r] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(wrow[r] + k))
+                         : u32x4n{0u, 0u, 0u, 0u};
+    }
+  };
+  // the first k-group of weights does not depend on x: in flight before the norm prologue
+  const int kfirst = lane * 16;
+  load_w(kfirst);
   if constexpr (NORM) gemv_norm_prologue<M>(static_cast<const bf16*>(x_in), nm, K);
   const void* xv_ = NORM ? static_cast<const void*>(gemv_lds) : x_in;
   if ((EP != kEpPlain ? 2 * wave : n0) >= N) return;
@@ -274,21 +354,14 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
   float sx[M];   // WI8: sum of this lane's x (the unsigned-bias correction)
 #pragma unroll
   for (int m = 0; m < M; ++m) sx[m] = 0.f;
-  const uint8_t* wrow[kRows];
-#pragma unroll
-  for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<EP>(wave, r, rp), N - 1) * K;
 
-  constexpr int kStep = 64 * 16;  // elements per wave instruction
-  for (int k0 = lane * 16; k0 < K; k0 += kStep * kUnroll) {
-    u32x4n wv[kUnroll][kRows];
+  for (int k0 = kfirst; k0 < K; k0 += kStep * kUnroll) {
+    if (k0 != kfirst) load_w(k0);
     bf16x8 xv[kUnroll][M][2];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int k = k0 + u * kStep;
       if (k < K) {
-#pragma unroll
-        for (int r = 0; r < kRows; ++r)
-          wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(wrow[r] + k));
 #pragma unroll
         for (int m = 0; m < M; ++m) {
           if constexpr (XF8) {
@@ -303,8 +376,6 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
           }
         }
       } else {
-#pragma unroll
-        for (int r = 0; r < kRows; ++r) wv[u][r] = u32x4n{0u, 0u, 0u, 0u};
 #pragma unroll
         for (int m = 0; m < M; ++m) xv[u][m][0] = xv[u][m][1] = bf16x8{};
       }

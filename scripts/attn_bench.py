@@ -87,5 +87,13 @@ if "--sweep" in sys.argv:
                 r["sweep"] = True
                 print(r, flush=True)
                 res.append(r)
+if "--short" in sys.argv:   # batch-1 short contexts: latency-bound, fewer splits skip the merge
+    for B, L in [(1, 600), (1, 1100), (1, 2048), (2, 600)]:
+        for sp in (1, 2, 4, 8, 16):
+            if sp * 32 <= L:
+                r = run(B, L, splits=sp)
+                r["short"] = True
+                print(r, flush=True)
+                res.append(r)
 os.makedirs("gpurun_out", exist_ok=True)
 json.dump(res, open("gpurun_out/attn_bench.json", "w"), indent=1)
