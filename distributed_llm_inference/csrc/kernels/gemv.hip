@@ -235,20 +235,20 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
   for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<EP>(wave, r, rp), N - 1) * K;
   constexpr int kStep = 64 * 8;  // elements per wave instruction
   bf16x8 wv[kUnroll][kRows];
-  auto load_w = [&](int k0) {
+  auto load_w = [&](int u, int k) {
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const int k = k0 + u * kStep;
-#pragma unroll
-      for (int r = 0; r < kRows; ++r)
-        wv[u][r] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wrow[r] + k))
-                         : bf16x8{};
-    }
+    for (int r = 0; r < kRows; ++r)
+      wv[u][r] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wrow[r] + k))
+                       : bf16x8{};
   };
-  // the first k-group of weights does not depend on x: in flight before the norm prologue
   const int kfirst = lane * 8;
-  load_w(kfirst);
-  if constexpr (NORM) gemv_norm_prologue<M>(x_in, nm, K);   // every thread, before any exit
+  if constexpr (NORM) {
+    // the first k-group of weights does not depend on x: in flight during the norm prologue
+    // (only here: with x from global memory the per-step weight / x interleave below is faster)
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) load_w(u, kfirst + u * kStep);
+    gemv_norm_prologue<M>(x_in, nm, K);   // every thread, before any exit
+  }
   const bf16* x = NORM ? reinterpret_cast<const bf16*>(gemv_lds) : x_in;
   if ((EP != kEpPlain ? 2 * wave : n0) >= N) return;
   float acc[M][kRows];
@@ -258,11 +258,12 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
     for (int r = 0; r < kRows; ++r) acc[m][r] = 0.f;
 
   for (int k0 = kfirst; k0 < K; k0 += kStep * kUnroll) {
-    if (k0 != kfirst) load_w(k0);
+    const bool pre = NORM && k0 == kfirst;
     bf16x8 xv[kUnroll][M];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int k = k0 + u * kStep;
+      if (!pre) load_w(u, k);
 #pragma unroll
       for (int m = 0; m < M; ++m)
         xv[u][m] = k < K ? *reinterpret_cast<const bf16x8*>(x + (size_t)m * K + k) : bf16x8{};
@@ -330,20 +331,20 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
   for (int r = 0; r < kRows; ++r) wrow[r] = W + (size_t)min(gemv_row<EP>(wave, r, rp), N - 1) * K;
   constexpr int kStep = 64 * 16;  // elements per wave instruction
   u32x4n wv[kUnroll][kRows];
-  auto load_w = [&](int k0) {
+  auto load_w = [&](int u, int k) {
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) {
-      const int k = k0 + u * kStep;
-#pragma unroll
-      for (int r = 0; r < kRows; ++r)
-        wv[u][r] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(wrow[r] + k))
-                         : u32x4n{0u, 0u, 0u, 0u};
-    }
+    for (int r = 0; r < kRows; ++r)
+      wv[u][r] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(wrow[r] + k))
+                       : u32x4n{0u, 0u, 0u, 0u};
   };
-  // the first k-group of weights does not depend on x: in flight before the norm prologue
   const int kfirst = lane * 16;
-  load_w(kfirst);
-  if constexpr (NORM) gemv_norm_prologue<M>(static_cast<const bf16*>(x_in), nm, K);
+  if constexpr (NORM) {
+    // the first k-group of weights does not depend on x: in flight during the norm prologue
+    // (only here: with x from global memory the per-step weight / x interleave below is faster)
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) load_w(u, kfirst + u * kStep);
+    gemv_norm_prologue<M>(static_cast<const bf16*>(x_in), nm, K);
+  }
   const void* xv_ = NORM ? static_cast<const void*>(gemv_lds) : x_in;
   if ((EP != kEpPlain ? 2 * wave : n0) >= N) return;
   float acc[M][kRows];
@@ -356,11 +357,12 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
   for (int m = 0; m < M; ++m) sx[m] = 0.f;
 
   for (int k0 = kfirst; k0 < K; k0 += kStep * kUnroll) {
-    if (k0 != kfirst) load_w(k0);
+    const bool pre = NORM && k0 == kfirst;
     bf16x8 xv[kUnroll][M][2];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int k = k0 + u * kStep;
+      if (!pre) load_w(u, k);
       if (k < K) {
 #pragma unroll
         for (int m = 0; m < M; ++m) {
