@@ -1,0 +1,487 @@
+// One Llama decoder layer for ONE decode row in ONE launch (batch-1 / single-session decode).
+//
+// At batch 1 a layer is a pure weight stream (70B fp8: 0.86 GB per layer, ~125 us at HBM rate)
+// cut into six dependent kernels (QKV + RoPE, attention, merge, O, gate|up + SwiGLU, down); each
+// boundary costs a launch plus the latency ramp of the next kernel's first loads (~3.5 us
+// measured per GEMV, scripts/gemv_bw.py) -- ~15 % of the fp8 step.  Here the six phases run in
+// one persistent grid (one 512-thread workgroup per CU, all co-resident) separated by grid
+// barriers, and every wave issues its first weight loads of the next phase BEFORE it waits at the
+// barrier, so the barrier's latency hides under the weight fetch instead of adding to it.
+//
+//   P1  x = rmsnorm(h + r) * w1 (LDS, per workgroup); QKV GEMV, RoPE, k / v -> paged cache, q
+//   P2  attention: 4-wave groups run attn_decode_item over consecutive splits and merge them
+//       in LDS (attention.hip's grouped path), partials -> part_o / part_ml
+//   P3  merge of the partials per head (attn_combine_kernel's arithmetic) -> attn [nh * D]
+//   P4  O GEMV -> o_out
+//   P5  res2 = o_out + (h + r); x = rmsnorm(res2) * w2 (LDS); gate|up GEMV + SwiGLU -> act
+//   P6  down GEMV -> out
+//
+// Every phase uses the arithmetic of the kernel it replaces (GEMV per-lane k order and wave
+// reduction, the 256-thread norm reduction, the grouped attention merge and the combine), so the
+// layer output is bit-identical to the six-kernel path (tests/test_decode_layer_gpu.py).
+//
+// Grid barrier: one 64-bit arrival counter per stream of layer launches, never reset: a launch's
+// base is the counter rounded down to a multiple of kDlBarriers * grid (every earlier launch
+// added exactly that many), read before the first arrival.  Arrivals are agent-scope atomics
+// after a release fence; waiting is a bounded spin (an error count, never a hang: co-residency
+// of all workgroups is required, so the host launches grid = CUs and only when no other kernel
+// can hold CUs -- ops.decode_layer_ok).
+#include "kernels.h"
+#include "attn_core.h"
+#include "gemv_core.h"
+
+namespace dli {
+
+namespace {
+
+constexpr int kDlThreads = 512;   // 8 waves, 2 per SIMD: 256 VGPRs for the attention phase
+constexpr int kDlWaves = kDlThreads / 64;
+constexpr int kDlBarriers = 5;
+constexpr int kDlUnroll = 4;      // k-steps of weight loads in flight per GEMV wave (8 spills)
+
+__device__ __forceinline__ void dl_grid_sync(unsigned long long* bar, unsigned long long target,
+                                             unsigned* err) {
+  __threadfence();   // release: this wave's global stores (outputs, cache writes) device-visible
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins == (1u << 22)) {   // ~0.2 s: count it and go on (never hang the GPU)
+        atomicAdd(err, 1u);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __threadfence();   // acquire: no stale line of another workgroup's output in this CU's caches
+}
+
+// x staging: rmsnorm(a + b) * w for one row of K <= 8192 (b optional), by threads 0..255 with
+// gemv_norm_prologue_regs' vector assignment and fma order (the other waves contribute 0 to the
+// block sum, which leaves it unchanged): bit-identical to the 256-thread fused norm.  `sum_out`
+// (optional, workgroup 0 only): a + b.
+__device__ __forceinline__ void dl_norm_stage(bf16x8* xs, const bf16* a, const bf16* b,
+                                              const bf16* w, float eps, int K, bf16* sum_out,
+                                              float* scratch) {
+  constexpr int VPT = 4;
+  const int nvec = K >> 3;
+  const int t = threadIdx.x;
+  const bool act = t < 256;
+  auto vidx = [&](int i) { const int idx = t + i * 256; return idx < nvec ? idx : nvec - 1; };
+  auto vok = [&](int i) { return act && t + i * 256 < nvec; };
+  bf16x8 wv[VPT], av[VPT], rv[VPT];
+  if (act) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      wv[i] = reinterpret_cast<const bf16x8*>(w)[vidx(i)];
+      av[i] = reinterpret_cast<const bf16x8*>(a)[vidx(i)];
+      if (b != nullptr) rv[i] = reinterpret_cast<const bf16x8*>(b)[vidx(i)];
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    if (!vok(i)) continue;
+    if (b != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) av[i][j] = (bf16)((float)av[i][j] + (float)rv[i][j]);
+      if (sum_out != nullptr) reinterpret_cast<bf16x8*>(sum_out)[t + i * 256] = av[i];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = (float)av[i][j];
+      ss = __builtin_fmaf(v, v, ss);
+    }
+  }
+  ss = block_reduce_sum(ss, scratch);
+  const float rstd = rsqrtf(ss / (float)K + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    if (!vok(i)) continue;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)av[i][j] * rstd * (float)wv[i][j]);
+    xs[t + i * 256] = o;
+  }
+}
+
+// plain x staging (global -> LDS), K % 8 == 0
+__device__ __forceinline__ void dl_copy_stage(bf16x8* xs, const bf16* x, int K) {
+  for (int i = threadIdx.x; i < (K >> 3); i += kDlThreads) xs[i] = reinterpret_cast<const bf16x8*>(x)[i];
+}
+
+// One GEMV phase over tasks (2 weight rows each) t = gw, gw + nw, ...: the per-lane k order,
+// dot order, wave reduction and scaling of skinny_gemm_kernel / skinny_gemm_fp8_kernel (M = 1,
+// bf16 activations), so each output is bit-identical to the standalone GEMV.  x in LDS.  The
+// first weight group of the wave's first task may have been issued already (pre).
+template <int WQ>   // 0 bf16, 1 fp8 e4m3, 2 int8
+struct DlGemv {
+  static constexpr int E = WQ == 0 ? 8 : 16;        // elements per lane per k-step (16 B)
+  static constexpr int kStep = 64 * E;
+  u32x4n wv[kDlUnroll][kRows];
+  const unsigned char* wrow[kRows];
+
+  template <int EP>
+  __device__ __forceinline__ int ntask(const DecodeProj& g) const {
+    return EP != kEpPlain ? g.N / 2 : (g.N + kRows - 1) / kRows;
+  }
+  template <int EP>
+  __device__ __forceinline__ void rows(const DecodeProj& g, int t, const GemvRope& rp) {
+    const int esz = WQ == 0 ? 2 : 1;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r)
+      wrow[r] = static_cast<const unsigned char*>(g.w) +
+                (size_t)min(gemv_row<EP>(t, r, rp), g.N - 1) * g.K * esz;
+  }
+  __device__ __forceinline__ void load(const DecodeProj& g, int u, int k) {
+    const int esz = WQ == 0 ? 2 : 1;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r)
+      wv[u][r] = k < g.K ? __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(wrow[r] + (size_t)k * esz))
+                         : u32x4n{0u, 0u, 0u, 0u};
+  }
+  // the first weight group of this wave's first task (before a barrier)
+  template <int EP>
+  __device__ __forceinline__ void prefetch(const DecodeProj& g, int gw, const GemvRope& rp) {
+    if (gw >= ntask<EP>(g)) return;
+    rows<EP>(g, gw, rp);
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < kDlUnroll; ++u) load(g, u, lane * E + u * kStep);
+  }
+
+  template <int EP>
+  __device__ __forceinline__ void run(const DecodeProj& g, const bf16* xs, bf16* y, int gw, int nw,
+                                      const GemvRope& rp, bool pre) {
+    const int lane = threadIdx.x & 63;
+    const int K = g.K, N = g.N;
+    for (int t = gw; t < ntask<EP>(g); t += nw) {
+      if (!pre) rows<EP>(g, t, rp);
+      float acc[kRows] = {0.f, 0.f};
+      float sx = 0.f;
+      for (int k0 = lane * E; k0 < K; k0 += kStep * kDlUnroll) {
+        if (!pre) {
+#pragma unroll
+          for (int u = 0; u < kDlUnroll; ++u) load(g, u, k0 + u * kStep);
+        }
+        pre = false;
+        if constexpr (WQ == 0) {
+          bf16x8 xv[kDlUnroll];
+#pragma unroll
+          for (int u = 0; u < kDlUnroll; ++u) {
+            const int k = k0 + u * kStep;
+            xv[u] = k < K ? *reinterpret_cast<const bf16x8*>(xs + k) : bf16x8{};
+          }
+#pragma unroll
+          for (int u = 0; u < kDlUnroll; ++u) {
+            const bf16x8 w0 = __builtin_bit_cast(bf16x8, wv[u][0]);
+            const bf16x8 w1 = __builtin_bit_cast(bf16x8, wv[u][1]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const bf16x2 xp = {xv[u][2 * j], xv[u][2 * j + 1]};
+              acc[0] = __builtin_amdgcn_fdot2_f32_bf16(xp, bf16x2{w0[2 * j], w0[2 * j + 1]}, acc[0], false);
+              acc[1] = __builtin_amdgcn_fdot2_f32_bf16(xp, bf16x2{w1[2 * j], w1[2 * j + 1]}, acc[1], false);
+            }
+          }
+        } else {
+          bf16x8 xv[kDlUnroll][2];
+#pragma unroll
+          for (int u = 0; u < kDlUnroll; ++u) {
+            const int k = k0 + u * kStep;
+            if (k < K) {
+              xv[u][0] = *reinterpret_cast<const bf16x8*>(xs + k);
+              xv[u][1] = *reinterpret_cast<const bf16x8*>(xs + k + 8);
+            } else {
+              xv[u][0] = xv[u][1] = bf16x8{};
+            }
+          }
+          if constexpr (WQ == 2) {
+            const bf16x2 ones = {(bf16)1.f, (bf16)1.f};
+#pragma unroll
+            for (int u = 0; u < kDlUnroll; ++u)
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                  sx = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{xv[u][h][2 * j], xv[u][h][2 * j + 1]},
+                                                       ones, sx, false);
+#pragma unroll
+            for (int u = 0; u < kDlUnroll; ++u)
+#pragma unroll
+              for (int r = 0; r < kRows; ++r)
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                  const unsigned ub = wv[u][r][d] ^ 0x80808080u;
+#pragma unroll
+                  for (int j = 0; j < 2; ++j) {
+                    const bf16x2 wp = u8pair_to_bf16x2(ub, j);
+                    const int e = (d & 1) * 4 + 2 * j;
+                    acc[r] = __builtin_amdgcn_fdot2_f32_bf16(
+                        bf16x2{xv[u][d >> 1][e], xv[u][d >> 1][e + 1]}, wp, acc[r], false);
+                  }
+                }
+          } else {
+#pragma unroll
+            for (int u = 0; u < kDlUnroll; ++u)
+#pragma unroll
+              for (int r = 0; r < kRows; ++r) {
+                const bf16x8 w0 = fp8x8_to_bf16x8(uint2{wv[u][r][0], wv[u][r][1]});
+                const bf16x8 w1 = fp8x8_to_bf16x8(uint2{wv[u][r][2], wv[u][r][3]});
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                  const bf16x2 x0 = {xv[u][0][2 * j], xv[u][0][2 * j + 1]};
+                  const bf16x2 x1 = {xv[u][1][2 * j], xv[u][1][2 * j + 1]};
+                  acc[r] = __builtin_amdgcn_fdot2_f32_bf16(x0, bf16x2{w0[2 * j], w0[2 * j + 1]}, acc[r], false);
+                  acc[r] = __builtin_amdgcn_fdot2_f32_bf16(x1, bf16x2{w1[2 * j], w1[2 * j + 1]}, acc[r], false);
+                }
+              }
+          }
+        }
+      }
+      if constexpr (WQ == 2) {
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) acc[r] -= 128.f * sx;
+      }
+      float v[1][kRows];
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        const int n = min(gemv_row<EP>(t, r, rp), N - 1);
+        const float s = wave_reduce_sum(acc[r]);
+        v[0][r] = WQ == 0 ? s + (g.bias ? (float)g.bias[n] : 0.f)
+                          : s * g.ws[n] + (g.bias ? (float)g.bias[n] : 0.f);
+      }
+      gemv_store<EP, 1>(v, t, lane, N, y, rp);
+    }
+  }
+};
+
+
+template <int WQ, bool KV8>
+__global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerParams a) {
+  constexpr int D = 128;
+  constexpr int LROW = D + 4;
+  // LDS: the staged x of the current GEMV phase (<= 64 KB: I <= 32768), the attention groups'
+  // merge images, reduction scratch
+  __shared__ __attribute__((aligned(16))) bf16x8 xs[4096];
+  __shared__ __attribute__((aligned(16))) float alds[2][4 * 16 * (LROW + 2)];
+  __shared__ float scratch[kDlWaves];
+  const int G = gridDim.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kDlWaves + wave);
+  const int nw = G * kDlWaves;
+  const bf16* xsb = reinterpret_cast<const bf16*>(xs);
+
+  // this launch's barrier base (see the header)
+  __shared__ unsigned long long base_s;
+  if (threadIdx.x == 0) {
+    const unsigned long long v = __hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long per = (unsigned long long)kDlBarriers * G;
+    base_s = v / per * per;
+  }
+  // (the norm stage's block reduction below synchronises the workgroup before base_s is read)
+
+  DlGemv<WQ> gv;
+  // ---- P1: norm 1 + QKV GEMV + RoPE / cache write ----
+  gv.template prefetch<kEpRope>(a.qkv, gw, a.rp);
+  dl_norm_stage(xs, a.h, a.r, a.ln1, a.eps1, a.qkv.K, blockIdx.x == 0 ? a.res1 : nullptr, scratch);
+  __syncthreads();
+  const unsigned long long base = base_s;
+  gv.template run<kEpRope>(a.qkv, xsb, nullptr, gw, nw, a.rp, true);
+  dl_grid_sync(a.bar, base + 1ull * G, a.err);
+
+  // ---- P2: attention partials (4-wave groups, attention.hip's grouped merge) ----
+  const AttnParams& p = a.ap;
+  const int items = p.nkv * ((p.nh / p.nkv + 15) >> 4) * p.num_splits;   // B = 1
+  if (blockIdx.x * kDlWaves < items) {   // workgroup-uniform: 2 groups of 4 waves each
+    const int grp = wave >> 2, wig = wave & 3;
+    const int gidx = blockIdx.x * 2 + grp;   // the standalone kernel's blockIdx
+    const int item_raw = gidx * 4 + wig;
+    const bool live = item_raw < items;
+    const int item = __builtin_amdgcn_readfirstlane(live ? item_raw : items - 1);
+    WaveState<D> st;
+    const DecodeItem di = attn_decode_item<D, false, KV8, false>(p, item, live, st);
+    const int col = lane & 15, h4 = lane >> 4;
+    float lsum = st.l;
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    float* lds = alds[grp];
+    float* lo = lds + (wig * 16 + col) * LROW;
+    float* lml = lds + 4 * 16 * LROW;
+#pragma unroll
+    for (int u = 0; u < D / 16; ++u) {
+      int d;
+      f32x4 o;
+      o_unit<D, KV8>(st, u, h4, d, o);
+      *reinterpret_cast<f32x4*>(lo + d) = o;
+    }
+    if (h4 == 0) {
+      lml[(wig * 16 + col) * 2] = st.m;
+      lml[(wig * 16 + col) * 2 + 1] = lsum;
+    }
+    __syncthreads();
+    const int gs = a.gs;
+    const int gq = wig / gs, w0 = gq * gs;   // merge group of this wave inside its 4-wave group
+    const int gitem = gidx * 4 + w0;
+    if (gitem < items) {
+      const int S2 = p.num_splits / gs;
+      const int s2 = (gitem % p.num_splits) / gs;
+      const int tg = (wig - w0) * 64 + lane;
+      constexpr int V4 = 16 * D / 4;
+      const int Gq = di.G;
+      for (int u = tg; u < V4; u += gs * 64) {
+        const int c = u / (D / 4), d4 = (u % (D / 4)) * 4;
+        if (di.g0 + c >= Gq) continue;
+        float M = -1e30f;
+        for (int w = w0; w < w0 + gs; ++w) M = fmaxf(M, lml[(w * 16 + c) * 2]);
+        float Lt = 0.f;
+        f32x4 O = {0.f, 0.f, 0.f, 0.f};
+        for (int w = w0; w < w0 + gs; ++w) {
+          const float f = __builtin_amdgcn_exp2f(lml[(w * 16 + c) * 2] - M);
+          Lt += f * lml[(w * 16 + c) * 2 + 1];
+          O += f * *reinterpret_cast<const f32x4*>(lds + (w * 16 + c) * LROW + d4);
+        }
+        const int head = di.kvh * Gq + di.g0 + c;
+        if (S2 == 1) {
+          const float inv = Lt > 0.f ? di.vsc / Lt : 0.f;
+          bf16x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (bf16)(O[r] * inv);
+          *reinterpret_cast<bf16x4*>(a.attn + (size_t)head * D + d4) = v;
+        } else {
+          const size_t r0 = (size_t)s2 * p.nh + head;
+          *reinterpret_cast<f32x4*>(p.part_o + r0 * D + d4) = O * di.vsc;
+          if (d4 == 0) {
+            p.part_ml[r0 * 2] = M;
+            p.part_ml[r0 * 2 + 1] = Lt;
+          }
+        }
+      }
+    }
+  }
+  gv.template prefetch<kEpPlain>(a.o, gw, a.rp);   // O weights in flight across two barriers
+  dl_grid_sync(a.bar, base + 2ull * G, a.err);
+
+  // ---- P3: merge the partials per head (attn_combine_kernel's arithmetic, B = 1) ----
+  const int S2 = p.num_splits / a.gs;
+  if (S2 > 1) {
+    // one wave per head: lanes 0..31 hold 4 consecutive d; the combine kernel's 8 lane groups
+    // take partials g, g + 8, ... -- its per-group running merge and the final in-order merge
+    // of the 8 group states are reproduced here with the same operations
+    for (int head = gw; head < p.nh; head += nw) {
+      if (lane < D / 4) {
+        constexpr int NG = 256 / (D / 4);
+        float gm[NG], gsum[NG];
+        f32x4 go[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          float m = -1e30f, s = 0.f;
+          f32x4 o = {0.f, 0.f, 0.f, 0.f};
+          for (int sp = g; sp < S2; sp += NG) {
+            const size_t r = (size_t)sp * p.nh + head;
+            const float mi = p.part_ml[r * 2], li = p.part_ml[r * 2 + 1];
+            const f32x4 oi = *reinterpret_cast<const f32x4*>(p.part_o + r * D + 4 * lane);
+            const float mn = fmaxf(m, mi);
+            const float e0 = __builtin_amdgcn_exp2f(m - mn), e1 = __builtin_amdgcn_exp2f(mi - mn);
+            o = o * e0 + oi * e1;
+            s = s * e0 + li * e1;
+            m = mn;
+          }
+          gm[g] = m;
+          gsum[g] = s;
+          go[g] = o;
+        }
+        float M = -1e30f;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) M = fmaxf(M, gm[g]);
+        float Lt = 0.f;
+        f32x4 O = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          const float f = __builtin_amdgcn_exp2f(gm[g] - M);
+          Lt += f * gsum[g];
+          O += f * go[g];
+        }
+        const float inv = Lt > 0.f ? 1.f / Lt : 0.f;
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (bf16)(O[r] * inv);
+        *reinterpret_cast<bf16x4*>(a.attn + (size_t)head * D + 4 * lane) = v;
+      }
+    }
+  }
+  dl_grid_sync(a.bar, base + 3ull * G, a.err);
+
+  // ---- P4: O GEMV ----
+  dl_copy_stage(xs, a.attn, a.o.K);
+  __syncthreads();
+  gv.template run<kEpPlain>(a.o, xsb, a.o_out, gw, nw, a.rp, true);
+  gv.template prefetch<kEpSwiGLU>(a.gu, gw, a.rp);
+  dl_grid_sync(a.bar, base + 4ull * G, a.err);
+
+  // ---- P5: residual + norm 2 + gate|up GEMV + SwiGLU ----
+  dl_norm_stage(xs, a.o_out, a.res1, a.ln2, a.eps2, a.gu.K, blockIdx.x == 0 ? a.res2 : nullptr,
+                scratch);
+  __syncthreads();
+  gv.template run<kEpSwiGLU>(a.gu, xsb, a.act, gw, nw, a.rp, true);
+  gv.template prefetch<kEpPlain>(a.down, gw, a.rp);
+  dl_grid_sync(a.bar, base + 5ull * G, a.err);
+
+  // ---- P6: down GEMV ----
+  dl_copy_stage(xs, a.act, a.down.K);
+  __syncthreads();
+  gv.template run<kEpPlain>(a.down, xsb, a.out, gw, nw, a.rp, true);
+}
+
+template <int WQ, bool KV8>
+int launch_dl(const DecodeLayerParams& p, hipStream_t stream) {
+  const int grid = decode_layer_grid();
+  if (grid <= 0) return -20;
+  static int fits = -1;   // every workgroup must be co-resident (grid barriers)
+  if (fits < 0) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, decode_layer_kernel<WQ, KV8>, kDlThreads, 0) != hipSuccess)
+      return -21;
+    fits = n >= 1 ? 1 : 0;
+  }
+  if (!fits) return -22;
+  decode_layer_kernel<WQ, KV8><<<grid, kDlThreads, 0, stream>>>(p);
+  return 0;
+}
+
+}  // namespace
+
+int decode_layer_grid() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+  return n;
+}
+
+// wq: 0 bf16, 1 fp8 e4m3, 2 int8 weights (per-row scales in DecodeProj::ws)
+int launch_decode_layer(const DecodeLayerParams& p, int wq, hipStream_t stream) {
+  const int K = p.qkv.K;
+  if (K % 8 != 0 || K > 8 * 4 * 256) return -1;                 // norm staging: 4 vectors / thread
+  if (p.o.N != K || p.gu.K != K || p.down.N != K || p.o.K != p.ap.nh * 128) return -2;
+  if (p.gu.N != 2 * p.down.K || p.down.K % 8 != 0 || p.down.K > 8 * 4096) return -3;   // LDS x
+  if (p.rp.D != 128 || p.ap.num_splits < 1 || p.gs < 1 || p.ap.num_splits % p.gs != 0 ||
+      4 % p.gs != 0)
+    return -4;
+  if (p.ap.n_sink != 0 || p.ap.ring != 0) return -5;             // full cache only
+  if (wq != 0 && (p.qkv.ws == nullptr || p.o.ws == nullptr || p.gu.ws == nullptr || p.down.ws == nullptr))
+    return -6;
+  if (p.bar == nullptr || p.err == nullptr || p.attn == nullptr || p.o_out == nullptr ||
+      p.act == nullptr || p.res2 == nullptr || p.res1 == nullptr || p.out == nullptr)
+    return -7;
+  if (p.ap.num_splits / p.gs > 1 && (p.ap.part_o == nullptr || p.ap.part_ml == nullptr)) return -8;
+  const bool kv8 = p.ap.kv_fp8 != 0;
+  switch (wq) {
+    case 0: return kv8 ? launch_dl<0, true>(p, stream) : launch_dl<0, false>(p, stream);
+    case 1: return kv8 ? launch_dl<1, true>(p, stream) : launch_dl<1, false>(p, stream);
+    case 2: return kv8 ? launch_dl<2, true>(p, stream) : launch_dl<2, false>(p, stream);
+  }
+  return -9;
+}
+
+}  // namespace dli

@@ -73,6 +73,15 @@ class Linear(nn.Module):
             self.weight = nn.Parameter(torch.empty(0, dtype=self.weight.dtype,
                                                    device=self.weight.device), requires_grad=False)
 
+    def stream_weights(self):
+        """(weight, per-row scale or None, bias or None) in the format the weight-streaming
+        kernels read: bf16 [N, K], fp8 e4m3 [N, K] or int8 [N, K] with fp32 scales [N]."""
+        if self.weight_fp8 is not None:
+            return self.weight_fp8, self.weight_scale.reshape(-1), self.bias
+        if self.weight_int8 is not None:
+            return self.weight_int8, self.weight_scale.reshape(-1), self.bias
+        return self.weight, None, self.bias
+
     def tile_splits(self, x: torch.Tensor) -> int:
         """Split-K factor if ``gemm_tile`` takes this product on the GPU, else 0."""
         if (self.bias is not None or not x.is_cuda or x.dim() != 2 or x.dtype != torch.bfloat16

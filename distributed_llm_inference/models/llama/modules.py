@@ -253,6 +253,8 @@ class LlamaDecoderLayer(nn.Module):
         layer's input RMSNorm reduces them); the O projection's partials always go straight
         into the post-attention RMSNorm."""
         if self._gemv_norms(hidden):
+            if self._layer_kernel_ok(hidden, residual, meta):
+                return self._forward_layer_kernel(hidden, residual, meta, k_cache, v_cache, cos_sin)
             return self._forward_gemv(hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out)
         if self.self_attn.qkv_proj.is_fp8:
             return self._forward_fp8(hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out)
@@ -281,6 +283,59 @@ class LlamaDecoderLayer(nn.Module):
         return (M * self.hidden_size * 2 <= 65536 and m.fused_swiglu
                 and a.qkv_proj.gemv_ok(M) and a.o_proj.gemv_ok(M)
                 and m.gate_up_proj.gemv_ok(M, swiglu=True) and m.down_proj.gemv_ok(M))
+
+    def _layer_kernel_ok(self, hidden, residual, meta) -> bool:
+        """One decode row whose layer the persistent decode-layer kernel takes (full cache, head
+        dim 128, one weight format, hidden <= 8192, intermediate <= 32768, fused RoPE path)."""
+        a, m = self.self_attn, self.mlp
+        if (hidden.shape[0] != 1 or not meta.is_decode or meta.custom_mask is not None
+                or meta.window or meta.ring or meta.n_sink or a.head_dim != 128
+                or self.hidden_size > 8192 or m.down_proj.in_features > 32768
+                or not ops.decode_layer_enabled()
+                or os.environ.get("DLI_GEMV_ROPE", "1") != "1"
+                or (residual is not None and not isinstance(residual, torch.Tensor))):
+            return False
+        fmts = {(p.is_fp8, p.is_int8) for p in (a.qkv_proj, a.o_proj, m.gate_up_proj, m.down_proj)}
+        return len(fmts) == 1
+
+    def _forward_layer_kernel(self, hidden, residual, meta, k_cache, v_cache, cos_sin):
+        """The fused-norm GEMV path's six launches (QKV + RoPE, attention, merge, O, gate|up +
+        SwiGLU, down) as one persistent kernel with grid barriers between them
+        (csrc/kernels/decode_layer.hip): same results bit for bit, five launch-and-ramp gaps
+        fewer per layer."""
+        a, m = self.self_attn, self.mlp
+        ln1, ln2 = self.input_layernorm, self.post_attention_layernorm
+        dev = hidden.device
+        bar = getattr(self, "_dl_bar", None)
+        if bar is None or bar.device != dev:
+            # grid-barrier arrival counter of this layer's launches (never reset; see the kernel)
+            bar = self._dl_bar = torch.zeros(2, dtype=torch.int64, device=dev)
+        nh, D = a.num_heads, a.head_dim
+        h = hidden.reshape(-1)
+        first = residual is None
+        res1 = h if first else torch.empty_like(h)
+        res2, out = torch.empty_like(h), torch.empty_like(h)
+        q = torch.empty(1, nh, D, dtype=hidden.dtype, device=dev)
+        attn = torch.empty(nh * D, dtype=hidden.dtype, device=dev)
+        o_out = torch.empty_like(h)
+        act = torch.empty(m.down_proj.in_features, dtype=hidden.dtype, device=dev)
+        ws = meta.workspace if meta.num_splits > 1 else None
+        if meta.num_splits > 1 and ws is None:
+            ws = ops.decode_workspace(1, nh, D, meta.num_splits, dev)
+        ops.native().decode_layer(
+            h, None if first else residual.reshape(-1), res1, res2, out, ln1.weight, ln2.weight,
+            float(ln1.eps), float(ln2.eps), *a.qkv_proj.stream_weights(),
+            *a.o_proj.stream_weights(), *m.gate_up_proj.stream_weights(),
+            *m.down_proj.stream_weights(), meta.positions, meta.slot_mapping, cos_sin, q, k_cache,
+            v_cache, float(meta.k_scale), float(meta.v_scale), meta.block_tables, meta.seq_lens,
+            float(a.scale), int(meta.num_splits), ws[0] if ws else None, ws[1] if ws else None,
+            attn, o_out, act, bar)
+        return out.view(1, -1), res2.view(1, -1)
+
+    def decode_layer_errors(self) -> int:
+        """Grid-barrier spin timeouts of this layer's persistent launches (0 = all completed)."""
+        bar = getattr(self, "_dl_bar", None)
+        return 0 if bar is None else int(bar[1].item() & 0xFFFFFFFF)
 
     def _forward_gemv(self, hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out=False):
         """1-2 decode rows: input RMSNorm fused into the QKV GEMV, post-attention RMSNorm into the

@@ -504,6 +504,26 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = 
     return out
 
 
+_DECODE_LAYER_BLOCKED = False
+
+
+def block_decode_layer(blocked: bool = True) -> None:
+    """Keep batch-1 decode off the persistent decode-layer kernel in this process (the engine
+    calls this when other kernels run next to the stage's layers -- the rotating LM head's side
+    stream): its grid barriers need every workgroup of the launch resident at once."""
+    global _DECODE_LAYER_BLOCKED
+    _DECODE_LAYER_BLOCKED = bool(blocked)
+
+
+def decode_layer_enabled() -> bool:
+    """Single-row decode runs each Llama layer as ONE persistent launch (csrc/kernels/
+    decode_layer.hip: the six GEMV / attention kernels of the fused-norm path as phases between
+    grid barriers, bit-identical results).  ``DLI_DECODE_LAYER=0`` turns it off; it is off when
+    ranks share a GPU (``DLI_SHARE_GPU=1``) or after :func:`block_decode_layer`."""
+    return (not _DECODE_LAYER_BLOCKED and os.environ.get("DLI_DECODE_LAYER", "1") == "1"
+            and os.environ.get("DLI_SHARE_GPU", "0") != "1")
+
+
 def gemm4_enabled(fp8: bool = False) -> bool:
     """Decode projections on the one-wave-per-SIMD kernel (csrc/kernels/gemm4.hip) instead of
     gemm_tile (read per call, so a captured graph keeps its choice).  bf16: ``DLI_GEMM4=1``

@@ -308,6 +308,11 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         TRACKER.enable_device_marks(device)
     # the fallback transport (agreed on by every rank) cannot carry the head: then nobody rotates
     rotate = rotate and transport.supports_head
+    if rotate:
+        # the head's side stream runs kernels next to the stage's layers: keep batch-1 decode off
+        # the grid-barrier decode-layer kernel (it needs every workgroup resident at once)
+        from .. import ops
+        ops.block_decode_layer(True)
     head_rotation = rotate   # recorded on the returned driver / follower (bench per-rank records)
     channels = _Channels(job, srank, pp, head_rotation=rotate)
     policy = HeadPolicy(pp, rotate, ex.max_num_seqs)
