@@ -38,11 +38,11 @@ def _decode(stage, flag, monkeypatch, kv_dtype, steps, prompt_len):
 def test_decode_layer_kernel_bit_identical(gpu, monkeypatch, quant, kv):
     kv_dtype = torch.float8_e4m3fn if kv == "fp8" else torch.bfloat16
     stage = CausalLMStage(SPEC, 0, 3, device=gpu).init_random(11)
-    stage.block.set_fused_swiglu(True)
     if quant == "fp8":
         stage.block.quantize_fp8()
     elif quant == "int8":
         stage.block.quantize_int8()
+    stage.block.set_fused_swiglu(True)   # after quantising, as the engine does
     # 40-token prompt + 60 steps: crosses 32-key steps, cache blocks and split-count changes
     ref = _decode(stage, "0", monkeypatch, kv_dtype, 60, 40)
     got = _decode(stage, "1", monkeypatch, kv_dtype, 60, 40)
