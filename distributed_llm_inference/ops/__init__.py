@@ -633,6 +633,8 @@ def tile_gemm_splits(M: int, N: int, K: int, elem_bytes: int = 2) -> int:
     for s in range(1, int(os.environ.get("DLI_TILE_MAX_SPLITS", "8")) + 1):
         if s > k_tiles or (s > 1 and tiles * s > 2 * _CUS):
             break
+        if (s - 1) * (-(-k_tiles // s)) >= k_tiles:
+            continue   # the kernels give every split >= 1 k-tile (16 k-tiles can't go 7 ways)
         work = tiles * s
         util = work / (_CUS * ((work + _CUS - 1) // _CUS))
         if util > best_util + 1e-9:
