@@ -41,21 +41,24 @@ constexpr int kDlUnroll = 4;      // k-steps of weight loads in flight per GEMV 
 
 __device__ __forceinline__ void dl_grid_sync(unsigned long long* bar, unsigned long long target,
                                              unsigned* err) {
-  __threadfence();   // release: this wave's global stores (outputs, cache writes) device-visible
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores have reached L2
   __syncthreads();
   if (threadIdx.x == 0) {
+    // one L2 write-back (release) and one invalidate (acquire) per workgroup and barrier: the
+    // L2s of the 8 XCDs are not coherent with each other for ordinary stores
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
     while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins == (1u << 22)) {   // ~0.2 s: count it and go on (never hang the GPU)
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins == (1u << 21)) {   // ~0.2 s: count it and go on (never hang the GPU)
         atomicAdd(err, 1u);
         break;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
-  __threadfence();   // acquire: no stale line of another workgroup's output in this CU's caches
 }
 
 // x staging: rmsnorm(a + b) * w for one row of K <= 8192 (b optional), by threads 0..255 with
@@ -112,151 +115,161 @@ __device__ __forceinline__ void dl_copy_stage(bf16x8* xs, const bf16* x, int K) 
   for (int i = threadIdx.x; i < (K >> 3); i += kDlThreads) xs[i] = reinterpret_cast<const bf16x8*>(x)[i];
 }
 
-// One GEMV phase over tasks (2 weight rows each) t = gw, gw + nw, ...: the per-lane k order,
-// dot order, wave reduction and scaling of skinny_gemm_kernel / skinny_gemm_fp8_kernel (M = 1,
-// bf16 activations), so each output is bit-identical to the standalone GEMV.  x in LDS.  The
-// first weight group of the wave's first task may have been issued already (pre).
-template <int WQ>   // 0 bf16, 1 fp8 e4m3, 2 int8
+// One GEMV phase over tasks (2 weight rows each): a wave runs TP tasks at once (t, t + nw, ...)
+// so that TP x 4 k-steps x 2 rows of 16-B weight loads per lane are in flight (the 8 waves of a
+// CU have to cover the HBM latency that ~20 resident waves cover in the standalone kernel).  Each
+// task's per-lane k order, dot order, wave reduction and scaling are skinny_gemm_kernel's /
+// skinny_gemm_fp8_kernel's (M = 1, bf16 activations): every output is bit-identical to the
+// standalone GEMV.  x in LDS, read once per k-step for all TP tasks.  The first weight group of
+// the wave's first TP tasks may have been issued before the phase's barrier (pre).
+template <int WQ, int TP>   // WQ: 0 bf16, 1 fp8 e4m3, 2 int8
 struct DlGemv {
   static constexpr int E = WQ == 0 ? 8 : 16;        // elements per lane per k-step (16 B)
   static constexpr int kStep = 64 * E;
-  u32x4n wv[kDlUnroll][kRows];
-  const unsigned char* wrow[kRows];
+  static constexpr int U = kDlUnroll;
+  u32x4n wv[TP][U][kRows];
+  const unsigned char* wrow[TP][kRows];
 
   template <int EP>
-  __device__ __forceinline__ int ntask(const DecodeProj& g) const {
+  __device__ __forceinline__ static int ntask(const DecodeProj& g) {
     return EP != kEpPlain ? g.N / 2 : (g.N + kRows - 1) / kRows;
   }
   template <int EP>
-  __device__ __forceinline__ void rows(const DecodeProj& g, int t, const GemvRope& rp) {
+  __device__ __forceinline__ void rows(const DecodeProj& g, int t0, int nw, const GemvRope& rp) {
+    const int esz = WQ == 0 ? 2 : 1;
+    const int nt = ntask<EP>(g);
+#pragma unroll
+    for (int i = 0; i < TP; ++i) {
+      const int t = min(t0 + i * nw, nt - 1);   // idle slots re-read a valid task (never stored)
+#pragma unroll
+      for (int r = 0; r < kRows; ++r)
+        wrow[i][r] = static_cast<const unsigned char*>(g.w) +
+                     (size_t)min(gemv_row<EP>(t, r, rp), g.N - 1) * g.K * esz;
+    }
+  }
+  __device__ __forceinline__ void load(const DecodeProj& g, int k0) {
     const int esz = WQ == 0 ? 2 : 1;
 #pragma unroll
-    for (int r = 0; r < kRows; ++r)
-      wrow[r] = static_cast<const unsigned char*>(g.w) +
-                (size_t)min(gemv_row<EP>(t, r, rp), g.N - 1) * g.K * esz;
-  }
-  __device__ __forceinline__ void load(const DecodeProj& g, int u, int k) {
-    const int esz = WQ == 0 ? 2 : 1;
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u * kStep;
 #pragma unroll
-    for (int r = 0; r < kRows; ++r)
-      wv[u][r] = k < g.K ? __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(wrow[r] + (size_t)k * esz))
-                         : u32x4n{0u, 0u, 0u, 0u};
+      for (int i = 0; i < TP; ++i)
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+          wv[i][u][r] = k < g.K ? __builtin_nontemporal_load(
+                                      reinterpret_cast<const u32x4n*>(wrow[i][r] + (size_t)k * esz))
+                                : u32x4n{0u, 0u, 0u, 0u};
+    }
   }
-  // the first weight group of this wave's first task (before a barrier)
+  // the first weight group of this wave's first TP tasks (before a barrier)
   template <int EP>
-  __device__ __forceinline__ void prefetch(const DecodeProj& g, int gw, const GemvRope& rp) {
+  __device__ __forceinline__ void prefetch(const DecodeProj& g, int gw, int nw, const GemvRope& rp) {
     if (gw >= ntask<EP>(g)) return;
-    rows<EP>(g, gw, rp);
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int u = 0; u < kDlUnroll; ++u) load(g, u, lane * E + u * kStep);
+    rows<EP>(g, gw, nw, rp);
+    load(g, (threadIdx.x & 63) * E);
   }
 
   template <int EP>
   __device__ __forceinline__ void run(const DecodeProj& g, const bf16* xs, bf16* y, int gw, int nw,
                                       const GemvRope& rp, bool pre) {
     const int lane = threadIdx.x & 63;
-    const int K = g.K, N = g.N;
-    for (int t = gw; t < ntask<EP>(g); t += nw) {
-      if (!pre) rows<EP>(g, t, rp);
-      float acc[kRows] = {0.f, 0.f};
+    const int K = g.K, N = g.N, nt = ntask<EP>(g);
+    for (int t0 = gw; t0 < nt; t0 += nw * TP) {
+      if (!pre) rows<EP>(g, t0, nw, rp);
+      float acc[TP][kRows];
+#pragma unroll
+      for (int i = 0; i < TP; ++i) acc[i][0] = acc[i][1] = 0.f;
       float sx = 0.f;
-      for (int k0 = lane * E; k0 < K; k0 += kStep * kDlUnroll) {
-        if (!pre) {
-#pragma unroll
-          for (int u = 0; u < kDlUnroll; ++u) load(g, u, k0 + u * kStep);
-        }
+      for (int k0 = lane * E; k0 < K; k0 += kStep * U) {
+        if (!pre) load(g, k0);
         pre = false;
-        if constexpr (WQ == 0) {
-          bf16x8 xv[kDlUnroll];
 #pragma unroll
-          for (int u = 0; u < kDlUnroll; ++u) {
-            const int k = k0 + u * kStep;
-            xv[u] = k < K ? *reinterpret_cast<const bf16x8*>(xs + k) : bf16x8{};
-          }
+        for (int u = 0; u < U; ++u) {
+          const int k = k0 + u * kStep;
+          if constexpr (WQ == 0) {
+            const bf16x8 xv = k < K ? *reinterpret_cast<const bf16x8*>(xs + k) : bf16x8{};
 #pragma unroll
-          for (int u = 0; u < kDlUnroll; ++u) {
-            const bf16x8 w0 = __builtin_bit_cast(bf16x8, wv[u][0]);
-            const bf16x8 w1 = __builtin_bit_cast(bf16x8, wv[u][1]);
+            for (int i = 0; i < TP; ++i) {
+              const bf16x8 w0 = __builtin_bit_cast(bf16x8, wv[i][u][0]);
+              const bf16x8 w1 = __builtin_bit_cast(bf16x8, wv[i][u][1]);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const bf16x2 xp = {xv[u][2 * j], xv[u][2 * j + 1]};
-              acc[0] = __builtin_amdgcn_fdot2_f32_bf16(xp, bf16x2{w0[2 * j], w0[2 * j + 1]}, acc[0], false);
-              acc[1] = __builtin_amdgcn_fdot2_f32_bf16(xp, bf16x2{w1[2 * j], w1[2 * j + 1]}, acc[1], false);
+              for (int j = 0; j < 4; ++j) {
+                const bf16x2 xp = {xv[2 * j], xv[2 * j + 1]};
+                acc[i][0] = __builtin_amdgcn_fdot2_f32_bf16(xp, bf16x2{w0[2 * j], w0[2 * j + 1]}, acc[i][0], false);
+                acc[i][1] = __builtin_amdgcn_fdot2_f32_bf16(xp, bf16x2{w1[2 * j], w1[2 * j + 1]}, acc[i][1], false);
+              }
             }
-          }
-        } else {
-          bf16x8 xv[kDlUnroll][2];
-#pragma unroll
-          for (int u = 0; u < kDlUnroll; ++u) {
-            const int k = k0 + u * kStep;
+          } else {
+            bf16x8 xv[2];
             if (k < K) {
-              xv[u][0] = *reinterpret_cast<const bf16x8*>(xs + k);
-              xv[u][1] = *reinterpret_cast<const bf16x8*>(xs + k + 8);
+              xv[0] = *reinterpret_cast<const bf16x8*>(xs + k);
+              xv[1] = *reinterpret_cast<const bf16x8*>(xs + k + 8);
             } else {
-              xv[u][0] = xv[u][1] = bf16x8{};
+              xv[0] = xv[1] = bf16x8{};
             }
-          }
-          if constexpr (WQ == 2) {
-            const bf16x2 ones = {(bf16)1.f, (bf16)1.f};
-#pragma unroll
-            for (int u = 0; u < kDlUnroll; ++u)
+            if constexpr (WQ == 2) {
+              const bf16x2 ones = {(bf16)1.f, (bf16)1.f};
 #pragma unroll
               for (int h = 0; h < 2; ++h)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                  sx = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{xv[u][h][2 * j], xv[u][h][2 * j + 1]},
-                                                       ones, sx, false);
+                  sx = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{xv[h][2 * j], xv[h][2 * j + 1]}, ones,
+                                                       sx, false);
 #pragma unroll
-            for (int u = 0; u < kDlUnroll; ++u)
+              for (int i = 0; i < TP; ++i)
 #pragma unroll
-              for (int r = 0; r < kRows; ++r)
+                for (int r = 0; r < kRows; ++r)
 #pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                  const unsigned ub = wv[u][r][d] ^ 0x80808080u;
+                  for (int d = 0; d < 4; ++d) {
+                    const unsigned ub = wv[i][u][r][d] ^ 0x80808080u;
 #pragma unroll
-                  for (int j = 0; j < 2; ++j) {
-                    const bf16x2 wp = u8pair_to_bf16x2(ub, j);
-                    const int e = (d & 1) * 4 + 2 * j;
-                    acc[r] = __builtin_amdgcn_fdot2_f32_bf16(
-                        bf16x2{xv[u][d >> 1][e], xv[u][d >> 1][e + 1]}, wp, acc[r], false);
+                    for (int j = 0; j < 2; ++j) {
+                      const bf16x2 wp = u8pair_to_bf16x2(ub, j);
+                      const int e = (d & 1) * 4 + 2 * j;
+                      acc[i][r] = __builtin_amdgcn_fdot2_f32_bf16(
+                          bf16x2{xv[d >> 1][e], xv[d >> 1][e + 1]}, wp, acc[i][r], false);
+                    }
+                  }
+            } else {
+#pragma unroll
+              for (int i = 0; i < TP; ++i)
+#pragma unroll
+                for (int r = 0; r < kRows; ++r) {
+                  const bf16x8 w0 = fp8x8_to_bf16x8(uint2{wv[i][u][r][0], wv[i][u][r][1]});
+                  const bf16x8 w1 = fp8x8_to_bf16x8(uint2{wv[i][u][r][2], wv[i][u][r][3]});
+#pragma unroll
+                  for (int j = 0; j < 4; ++j) {
+                    const bf16x2 x0 = {xv[0][2 * j], xv[0][2 * j + 1]};
+                    const bf16x2 x1 = {xv[1][2 * j], xv[1][2 * j + 1]};
+                    acc[i][r] = __builtin_amdgcn_fdot2_f32_bf16(x0, bf16x2{w0[2 * j], w0[2 * j + 1]}, acc[i][r], false);
+                    acc[i][r] = __builtin_amdgcn_fdot2_f32_bf16(x1, bf16x2{w1[2 * j], w1[2 * j + 1]}, acc[i][r], false);
                   }
                 }
-          } else {
-#pragma unroll
-            for (int u = 0; u < kDlUnroll; ++u)
-#pragma unroll
-              for (int r = 0; r < kRows; ++r) {
-                const bf16x8 w0 = fp8x8_to_bf16x8(uint2{wv[u][r][0], wv[u][r][1]});
-                const bf16x8 w1 = fp8x8_to_bf16x8(uint2{wv[u][r][2], wv[u][r][3]});
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                  const bf16x2 x0 = {xv[u][0][2 * j], xv[u][0][2 * j + 1]};
-                  const bf16x2 x1 = {xv[u][1][2 * j], xv[u][1][2 * j + 1]};
-                  acc[r] = __builtin_amdgcn_fdot2_f32_bf16(x0, bf16x2{w0[2 * j], w0[2 * j + 1]}, acc[r], false);
-                  acc[r] = __builtin_amdgcn_fdot2_f32_bf16(x1, bf16x2{w1[2 * j], w1[2 * j + 1]}, acc[r], false);
-                }
-              }
+            }
           }
         }
       }
-      if constexpr (WQ == 2) {
 #pragma unroll
-        for (int r = 0; r < kRows; ++r) acc[r] -= 128.f * sx;
-      }
-      float v[1][kRows];
+      for (int i = 0; i < TP; ++i) {
+        const int t = t0 + i * nw;
+        if (t >= nt) break;
+        if constexpr (WQ == 2) {
 #pragma unroll
-      for (int r = 0; r < kRows; ++r) {
-        const int n = min(gemv_row<EP>(t, r, rp), N - 1);
-        const float s = wave_reduce_sum(acc[r]);
-        v[0][r] = WQ == 0 ? s + (g.bias ? (float)g.bias[n] : 0.f)
-                          : s * g.ws[n] + (g.bias ? (float)g.bias[n] : 0.f);
+          for (int r = 0; r < kRows; ++r) acc[i][r] -= 128.f * sx;
+        }
+        float v[1][kRows];
+#pragma unroll
+        for (int r = 0; r < kRows; ++r) {
+          const int n = min(gemv_row<EP>(t, r, rp), N - 1);
+          const float s = wave_reduce_sum(acc[i][r]);
+          v[0][r] = WQ == 0 ? s + (g.bias ? (float)g.bias[n] : 0.f)
+                            : s * g.ws[n] + (g.bias ? (float)g.bias[n] : 0.f);
+        }
+        gemv_store<EP, 1>(v, t, lane, N, y, rp);
       }
-      gemv_store<EP, 1>(v, t, lane, N, y, rp);
     }
   }
 };
-
 
 template <int WQ, bool KV8>
 __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerParams a) {
@@ -282,13 +295,13 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   }
   // (the norm stage's block reduction below synchronises the workgroup before base_s is read)
 
-  DlGemv<WQ> gv;
   // ---- P1: norm 1 + QKV GEMV + RoPE / cache write ----
-  gv.template prefetch<kEpRope>(a.qkv, gw, a.rp);
+  DlGemv<WQ, 2> g1;
+  g1.template prefetch<kEpRope>(a.qkv, gw, nw, a.rp);
   dl_norm_stage(xs, a.h, a.r, a.ln1, a.eps1, a.qkv.K, blockIdx.x == 0 ? a.res1 : nullptr, scratch);
   __syncthreads();
   const unsigned long long base = base_s;
-  gv.template run<kEpRope>(a.qkv, xsb, nullptr, gw, nw, a.rp, true);
+  g1.template run<kEpRope>(a.qkv, xsb, nullptr, gw, nw, a.rp, true);
   dl_grid_sync(a.bar, base + 1ull * G, a.err);
 
   // ---- P2: attention partials (4-wave groups, attention.hip's grouped merge) ----
@@ -360,7 +373,8 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
       }
     }
   }
-  gv.template prefetch<kEpPlain>(a.o, gw, a.rp);   // O weights in flight across two barriers
+  DlGemv<WQ, 2> g4;
+  g4.template prefetch<kEpPlain>(a.o, gw, nw, a.rp);   // O weights in flight across two barriers
   dl_grid_sync(a.bar, base + 2ull * G, a.err);
 
   // ---- P3: merge the partials per head (attn_combine_kernel's arithmetic, B = 1) ----
@@ -416,22 +430,24 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   // ---- P4: O GEMV ----
   dl_copy_stage(xs, a.attn, a.o.K);
   __syncthreads();
-  gv.template run<kEpPlain>(a.o, xsb, a.o_out, gw, nw, a.rp, true);
-  gv.template prefetch<kEpSwiGLU>(a.gu, gw, a.rp);
+  g4.template run<kEpPlain>(a.o, xsb, a.o_out, gw, nw, a.rp, true);
+  DlGemv<WQ, 4> g5;
+  g5.template prefetch<kEpSwiGLU>(a.gu, gw, nw, a.rp);
   dl_grid_sync(a.bar, base + 4ull * G, a.err);
 
   // ---- P5: residual + norm 2 + gate|up GEMV + SwiGLU ----
   dl_norm_stage(xs, a.o_out, a.res1, a.ln2, a.eps2, a.gu.K, blockIdx.x == 0 ? a.res2 : nullptr,
                 scratch);
   __syncthreads();
-  gv.template run<kEpSwiGLU>(a.gu, xsb, a.act, gw, nw, a.rp, true);
-  gv.template prefetch<kEpPlain>(a.down, gw, a.rp);
+  g5.template run<kEpSwiGLU>(a.gu, xsb, a.act, gw, nw, a.rp, true);
+  DlGemv<WQ, 2> g6;
+  g6.template prefetch<kEpPlain>(a.down, gw, nw, a.rp);
   dl_grid_sync(a.bar, base + 5ull * G, a.err);
 
   // ---- P6: down GEMV ----
   dl_copy_stage(xs, a.act, a.down.K);
   __syncthreads();
-  gv.template run<kEpPlain>(a.down, xsb, a.out, gw, nw, a.rp, true);
+  g6.template run<kEpPlain>(a.down, xsb, a.out, gw, nw, a.rp, true);
 }
 
 template <int WQ, bool KV8>
