@@ -955,7 +955,8 @@ void decode_layer(Tensor h, optional<Tensor> r, Tensor res1, Tensor res2, Tensor
                   Tensor slot_mapping, optional<Tensor> cos_sin, Tensor q_out, Tensor k_cache,
                   Tensor v_cache, double k_scale, double v_scale, Tensor block_tables,
                   Tensor seq_lens, double scale, int64_t num_splits, optional<Tensor> part_o,
-                  optional<Tensor> part_ml, Tensor attn, Tensor o_out, Tensor act, Tensor bar) {
+                  optional<Tensor> part_ml, Tensor attn, Tensor o_out, Tensor act, Tensor bar,
+                  optional<Tensor> stamps) {
   for (const Tensor* t : {&h, &res1, &res2, &out, &ln1, &ln2, &attn, &o_out, &act, &q_out}) {
     CHECK_IN(*t); CHECK_BF16(*t);
   }
@@ -1044,6 +1045,12 @@ void decode_layer(Tensor h, optional<Tensor> r, Tensor res1, Tensor res2, Tensor
   p.act = bp(act);
   p.bar = reinterpret_cast<unsigned long long*>(bar.data_ptr<int64_t>());
   p.err = reinterpret_cast<unsigned*>(bar.data_ptr<int64_t>() + 1);
+  if (stamps.has_value()) {
+    CHECK_IN(*stamps);
+    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->numel() >= 16 * dli::decode_layer_grid(),
+                "decode_layer: stamps = int64 [grid * 16]");
+    p.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
   check_rc(dli::launch_decode_layer(p, wq, cur_stream()), "decode_layer");
 }

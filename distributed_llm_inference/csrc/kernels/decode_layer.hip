@@ -39,10 +39,16 @@ constexpr int kDlWaves = kDlThreads / 64;
 constexpr int kDlBarriers = 5;
 constexpr int kDlUnroll = 4;      // k-steps of weight loads in flight per GEMV wave (8 spills)
 
+// diagnostics (DecodeLayerParams::stamps): slot 2k-1 = arrival at barrier k, 2k = its release
+__device__ __forceinline__ void dl_stamp(unsigned long long* st, int slot) {
+  if (st != nullptr && threadIdx.x == 0) st[(size_t)blockIdx.x * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
 __device__ __forceinline__ void dl_grid_sync(unsigned long long* bar, unsigned long long target,
-                                             unsigned* err) {
+                                             unsigned* err, unsigned long long* st, int k) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores have reached L2
   __syncthreads();
+  dl_stamp(st, 2 * k - 1);
   if (threadIdx.x == 0) {
     // one L2 write-back (release) and one invalidate (acquire) per workgroup and barrier: the
     // L2s of the 8 XCDs are not coherent with each other for ordinary stores
@@ -58,6 +64,7 @@ __device__ __forceinline__ void dl_grid_sync(unsigned long long* bar, unsigned l
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
+  dl_stamp(st, 2 * k);
   __syncthreads();
 }
 
@@ -295,6 +302,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   }
   // (the norm stage's block reduction below synchronises the workgroup before base_s is read)
 
+  dl_stamp(a.stamps, 0);
   // ---- P1: norm 1 + QKV GEMV + RoPE / cache write ----
   DlGemv<WQ, 2> g1;
   g1.template prefetch<kEpRope>(a.qkv, gw, nw, a.rp);
@@ -302,7 +310,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   __syncthreads();
   const unsigned long long base = base_s;
   g1.template run<kEpRope>(a.qkv, xsb, nullptr, gw, nw, a.rp, true);
-  dl_grid_sync(a.bar, base + 1ull * G, a.err);
+  dl_grid_sync(a.bar, base + 1ull * G, a.err, a.stamps, 1);
 
   // ---- P2: attention partials (4-wave groups, attention.hip's grouped merge) ----
   const AttnParams& p = a.ap;
@@ -375,7 +383,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   }
   DlGemv<WQ, 2> g4;
   g4.template prefetch<kEpPlain>(a.o, gw, nw, a.rp);   // O weights in flight across two barriers
-  dl_grid_sync(a.bar, base + 2ull * G, a.err);
+  dl_grid_sync(a.bar, base + 2ull * G, a.err, a.stamps, 2);
 
   // ---- P3: merge the partials per head (attn_combine_kernel's arithmetic, B = 1) ----
   const int S2 = p.num_splits / a.gs;
@@ -425,7 +433,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
       }
     }
   }
-  dl_grid_sync(a.bar, base + 3ull * G, a.err);
+  dl_grid_sync(a.bar, base + 3ull * G, a.err, a.stamps, 3);
 
   // ---- P4: O GEMV ----
   dl_copy_stage(xs, a.attn, a.o.K);
@@ -433,7 +441,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   g4.template run<kEpPlain>(a.o, xsb, a.o_out, gw, nw, a.rp, true);
   DlGemv<WQ, 4> g5;
   g5.template prefetch<kEpSwiGLU>(a.gu, gw, nw, a.rp);
-  dl_grid_sync(a.bar, base + 4ull * G, a.err);
+  dl_grid_sync(a.bar, base + 4ull * G, a.err, a.stamps, 4);
 
   // ---- P5: residual + norm 2 + gate|up GEMV + SwiGLU ----
   dl_norm_stage(xs, a.o_out, a.res1, a.ln2, a.eps2, a.gu.K, blockIdx.x == 0 ? a.res2 : nullptr,
@@ -442,12 +450,15 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   g5.template run<kEpSwiGLU>(a.gu, xsb, a.act, gw, nw, a.rp, true);
   DlGemv<WQ, 2> g6;
   g6.template prefetch<kEpPlain>(a.down, gw, nw, a.rp);
-  dl_grid_sync(a.bar, base + 5ull * G, a.err);
+  dl_grid_sync(a.bar, base + 5ull * G, a.err, a.stamps, 5);
 
   // ---- P6: down GEMV ----
   dl_copy_stage(xs, a.act, a.down.K);
   __syncthreads();
   g6.template run<kEpPlain>(a.down, xsb, a.out, gw, nw, a.rp, true);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  dl_stamp(a.stamps, 11);
 }
 
 template <int WQ, bool KV8>

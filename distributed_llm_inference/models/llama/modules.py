@@ -329,8 +329,19 @@ class LlamaDecoderLayer(nn.Module):
             *m.down_proj.stream_weights(), meta.positions, meta.slot_mapping, cos_sin, q, k_cache,
             v_cache, float(meta.k_scale), float(meta.v_scale), meta.block_tables, meta.seq_lens,
             float(a.scale), int(meta.num_splits), ws[0] if ws else None, ws[1] if ws else None,
-            attn, o_out, act, bar)
+            attn, o_out, act, bar, self._dl_stamp_buffer(dev))
         return out.view(1, -1), res2.view(1, -1)
+
+    def _dl_stamp_buffer(self, dev):
+        """``DLI_DL_STAMPS=1`` (diagnostics, scripts/decode_layer_probe.py): per-workgroup wall
+        stamps of the decode-layer kernel's phases, overwritten by every launch."""
+        if os.environ.get("DLI_DL_STAMPS", "0") != "1":
+            return None
+        st = getattr(self, "_dl_stamps", None)
+        if st is None or st.device != dev:
+            st = self._dl_stamps = torch.zeros(16 * ops.native().decode_layer_grid(),
+                                               dtype=torch.int64, device=dev)
+        return st
 
     def decode_layer_errors(self) -> int:
         """Grid-barrier spin timeouts of this layer's persistent launches (0 = all completed)."""
