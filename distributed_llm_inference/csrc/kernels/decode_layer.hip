@@ -44,16 +44,26 @@ __device__ __forceinline__ void dl_stamp(unsigned long long* st, int slot) {
   if (st != nullptr && threadIdx.x == 0) st[(size_t)blockIdx.x * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
+// Grid barrier k.  Order inside: every wave's stores complete (vmcnt(0): nothing else is in
+// flight yet), one L2 write-back by thread 0, its arrival; THEN the next phase's first weight
+// loads (`prefetch`) go out, so they overlap the wait instead of delaying the arrival (vmcnt is
+// in order on CDNA: a wait for the stores would also wait for loads issued before it); the
+// acquire is a bare L2 / L1 invalidate, which waits for nothing.
+template <typename F>
 __device__ __forceinline__ void dl_grid_sync(unsigned long long* bar, unsigned long long target,
-                                             unsigned* err, unsigned long long* st, int k) {
+                                             unsigned* err, unsigned long long* st, int k,
+                                             F&& prefetch) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores have reached L2
   __syncthreads();
   dl_stamp(st, 2 * k - 1);
   if (threadIdx.x == 0) {
-    // one L2 write-back (release) and one invalidate (acquire) per workgroup and barrier: the
-    // L2s of the 8 XCDs are not coherent with each other for ordinary stores
+    // the L2s of the 8 XCDs are not coherent with each other for ordinary stores: one
+    // write-back (release) and one invalidate (acquire) per workgroup and barrier
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  prefetch();
+  if (threadIdx.x == 0) {
     unsigned spins = 0;
     while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(2);
@@ -62,7 +72,7 @@ __device__ __forceinline__ void dl_grid_sync(unsigned long long* bar, unsigned l
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("buffer_inv sc1" ::: "memory");
   }
   dl_stamp(st, 2 * k);
   __syncthreads();
@@ -304,13 +314,13 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
 
   dl_stamp(a.stamps, 0);
   // ---- P1: norm 1 + QKV GEMV + RoPE / cache write ----
-  DlGemv<WQ, 2> g1;
+  DlGemv<WQ, 3> g1;   // ~2.5 QKV tasks per wave on 70B: all of them in one round
   g1.template prefetch<kEpRope>(a.qkv, gw, nw, a.rp);
   dl_norm_stage(xs, a.h, a.r, a.ln1, a.eps1, a.qkv.K, blockIdx.x == 0 ? a.res1 : nullptr, scratch);
   __syncthreads();
   const unsigned long long base = base_s;
   g1.template run<kEpRope>(a.qkv, xsb, nullptr, gw, nw, a.rp, true);
-  dl_grid_sync(a.bar, base + 1ull * G, a.err, a.stamps, 1);
+  dl_grid_sync(a.bar, base + 1ull * G, a.err, a.stamps, 1, [] {});
 
   // ---- P2: attention partials (4-wave groups, attention.hip's grouped merge) ----
   const AttnParams& p = a.ap;
@@ -382,8 +392,9 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
     }
   }
   DlGemv<WQ, 2> g4;
-  g4.template prefetch<kEpPlain>(a.o, gw, nw, a.rp);   // O weights in flight across two barriers
-  dl_grid_sync(a.bar, base + 2ull * G, a.err, a.stamps, 2);
+  // O weights: in flight from the merge barrier on (issued at the attention barrier, the
+  // workgroups that have no attention work would flood HBM while the attention runs)
+  dl_grid_sync(a.bar, base + 2ull * G, a.err, a.stamps, 2, [] {});
 
   // ---- P3: merge the partials per head (attn_combine_kernel's arithmetic, B = 1) ----
   const int S2 = p.num_splits / a.gs;
@@ -433,15 +444,16 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
       }
     }
   }
-  dl_grid_sync(a.bar, base + 3ull * G, a.err, a.stamps, 3);
+  dl_grid_sync(a.bar, base + 3ull * G, a.err, a.stamps, 3,
+               [&] { g4.template prefetch<kEpPlain>(a.o, gw, nw, a.rp); });
 
   // ---- P4: O GEMV ----
   dl_copy_stage(xs, a.attn, a.o.K);
   __syncthreads();
   g4.template run<kEpPlain>(a.o, xsb, a.o_out, gw, nw, a.rp, true);
   DlGemv<WQ, 4> g5;
-  g5.template prefetch<kEpSwiGLU>(a.gu, gw, nw, a.rp);
-  dl_grid_sync(a.bar, base + 4ull * G, a.err, a.stamps, 4);
+  dl_grid_sync(a.bar, base + 4ull * G, a.err, a.stamps, 4,
+               [&] { g5.template prefetch<kEpSwiGLU>(a.gu, gw, nw, a.rp); });
 
   // ---- P5: residual + norm 2 + gate|up GEMV + SwiGLU ----
   dl_norm_stage(xs, a.o_out, a.res1, a.ln2, a.eps2, a.gu.K, blockIdx.x == 0 ? a.res2 : nullptr,
@@ -449,8 +461,8 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   __syncthreads();
   g5.template run<kEpSwiGLU>(a.gu, xsb, a.act, gw, nw, a.rp, true);
   DlGemv<WQ, 2> g6;
-  g6.template prefetch<kEpPlain>(a.down, gw, nw, a.rp);
-  dl_grid_sync(a.bar, base + 5ull * G, a.err, a.stamps, 5);
+  dl_grid_sync(a.bar, base + 5ull * G, a.err, a.stamps, 5,
+               [&] { g6.template prefetch<kEpPlain>(a.down, gw, nw, a.rp); });
 
   // ---- P6: down GEMV ----
   dl_copy_stage(xs, a.act, a.down.K);
