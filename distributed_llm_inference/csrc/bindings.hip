@@ -1047,8 +1047,8 @@ void decode_layer(Tensor h, optional<Tensor> r, Tensor res1, Tensor res2, Tensor
   p.err = reinterpret_cast<unsigned*>(bar.data_ptr<int64_t>() + 1);
   if (stamps.has_value()) {
     CHECK_IN(*stamps);
-    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->numel() >= 16 * dli::decode_layer_grid(),
-                "decode_layer: stamps = int64 [grid * 16]");
+    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->numel() >= 24 * dli::decode_layer_grid(),
+                "decode_layer: stamps = int64 [grid * 24]");
     p.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());

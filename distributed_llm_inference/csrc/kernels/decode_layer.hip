@@ -39,9 +39,10 @@ constexpr int kDlWaves = kDlThreads / 64;
 constexpr int kDlBarriers = 5;
 constexpr int kDlUnroll = 4;      // k-steps of weight loads in flight per GEMV wave (8 spills)
 
-// diagnostics (DecodeLayerParams::stamps): slot 2k-1 = arrival at barrier k, 2k = its release
+// diagnostics (DecodeLayerParams::stamps, [grid][24]): slot 0 = start, 2k-1 = arrival at barrier
+// k, 12+k = its L2 write-back done, 2k = its release, 11 = end
 __device__ __forceinline__ void dl_stamp(unsigned long long* st, int slot) {
-  if (st != nullptr && threadIdx.x == 0) st[(size_t)blockIdx.x * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+  if (st != nullptr && threadIdx.x == 0) st[(size_t)blockIdx.x * 24 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Grid barrier k.  Order inside: every wave's stores complete (vmcnt(0): nothing else is in
@@ -60,6 +61,7 @@ __device__ __forceinline__ void dl_grid_sync(unsigned long long* bar, unsigned l
     // the L2s of the 8 XCDs are not coherent with each other for ordinary stores: one
     // write-back (release) and one invalidate (acquire) per workgroup and barrier
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    dl_stamp(st, 12 + k);   // after the L2 write-back
     __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   prefetch();
@@ -132,158 +134,184 @@ __device__ __forceinline__ void dl_copy_stage(bf16x8* xs, const bf16* x, int K) 
   for (int i = threadIdx.x; i < (K >> 3); i += kDlThreads) xs[i] = reinterpret_cast<const bf16x8*>(x)[i];
 }
 
-// One GEMV phase over tasks (2 weight rows each): a wave runs TP tasks at once (t, t + nw, ...)
-// so that TP x 4 k-steps x 2 rows of 16-B weight loads per lane are in flight (the 8 waves of a
-// CU have to cover the HBM latency that ~20 resident waves cover in the standalone kernel).  Each
-// task's per-lane k order, dot order, wave reduction and scaling are skinny_gemm_kernel's /
-// skinny_gemm_fp8_kernel's (M = 1, bf16 activations): every output is bit-identical to the
-// standalone GEMV.  x in LDS, read once per k-step for all TP tasks.  The first weight group of
-// the wave's first TP tasks may have been issued before the phase's barrier (pre).
+// One GEMV phase over tasks (2 weight rows each).  A wave runs TP tasks at once (t, t + nw, ...)
+// and walks them in chunks of 4 k-steps (TP x 4 x 2 rows of 16-B weight loads per lane); the
+// loads of chunk c + 1 are issued before chunk c is consumed (two register sets), so every wave
+// keeps a full chunk in flight without a bubble -- the 8 waves of a CU have to cover the HBM
+// latency that ~20 resident waves cover in the standalone kernel.  Each task's per-lane k order,
+// dot order, wave reduction and scaling are skinny_gemm_kernel's / skinny_gemm_fp8_kernel's
+// (M = 1, bf16 activations): every output is bit-identical to the standalone GEMV.  x in LDS.
+// Chunk 0 may have been issued before the phase's barrier (prefetch / pre).
 template <int WQ, int TP>   // WQ: 0 bf16, 1 fp8 e4m3, 2 int8
 struct DlGemv {
   static constexpr int E = WQ == 0 ? 8 : 16;        // elements per lane per k-step (16 B)
   static constexpr int kStep = 64 * E;
   static constexpr int U = kDlUnroll;
-  u32x4n wv[TP][U][kRows];
-  const unsigned char* wrow[TP][kRows];
+  u32x4n wv[2][TP][U][kRows];
+  const unsigned char* wrow[2][TP][kRows];
 
   template <int EP>
   __device__ __forceinline__ static int ntask(const DecodeProj& g) {
     return EP != kEpPlain ? g.N / 2 : (g.N + kRows - 1) / kRows;
   }
-  template <int EP>
-  __device__ __forceinline__ void rows(const DecodeProj& g, int t0, int nw, const GemvRope& rp) {
+  __device__ __forceinline__ static int iters(const DecodeProj& g) {
+    return (g.K + kStep * U - 1) / (kStep * U);
+  }
+  // issue chunk c (round c / iters, k-chunk c % iters) into register set B
+  template <int EP, int B>
+  __device__ __forceinline__ void issue(const DecodeProj& g, int gw, int nw, const GemvRope& rp,
+                                        int c) {
     const int esz = WQ == 0 ? 2 : 1;
+    const int it = iters(g), r = c / it, kc = c - r * it;
     const int nt = ntask<EP>(g);
+    const int t0 = gw + r * nw * TP;
 #pragma unroll
     for (int i = 0; i < TP; ++i) {
       const int t = min(t0 + i * nw, nt - 1);   // idle slots re-read a valid task (never stored)
 #pragma unroll
-      for (int r = 0; r < kRows; ++r)
-        wrow[i][r] = static_cast<const unsigned char*>(g.w) +
-                     (size_t)min(gemv_row<EP>(t, r, rp), g.N - 1) * g.K * esz;
+      for (int q = 0; q < kRows; ++q)
+        wrow[B][i][q] = static_cast<const unsigned char*>(g.w) +
+                        (size_t)min(gemv_row<EP>(t, q, rp), g.N - 1) * g.K * esz;
     }
-  }
-  __device__ __forceinline__ void load(const DecodeProj& g, int k0) {
-    const int esz = WQ == 0 ? 2 : 1;
+    const int k0 = (threadIdx.x & 63) * E + kc * kStep * U;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = k0 + u * kStep;
 #pragma unroll
       for (int i = 0; i < TP; ++i)
 #pragma unroll
-        for (int r = 0; r < kRows; ++r)
-          wv[i][u][r] = k < g.K ? __builtin_nontemporal_load(
-                                      reinterpret_cast<const u32x4n*>(wrow[i][r] + (size_t)k * esz))
-                                : u32x4n{0u, 0u, 0u, 0u};
+        for (int q = 0; q < kRows; ++q)
+          wv[B][i][u][q] = k < g.K ? __builtin_nontemporal_load(
+                                         reinterpret_cast<const u32x4n*>(wrow[B][i][q] + (size_t)k * esz))
+                                   : u32x4n{0u, 0u, 0u, 0u};
     }
   }
-  // the first weight group of this wave's first TP tasks (before a barrier)
+  template <int EP>
+  __device__ __forceinline__ int chunks(const DecodeProj& g, int gw, int nw) const {
+    const int nt = ntask<EP>(g);
+    return gw < nt ? (nt - gw + nw * TP - 1) / (nw * TP) * iters(g) : 0;
+  }
+  // chunk 0 of this wave (before a barrier)
   template <int EP>
   __device__ __forceinline__ void prefetch(const DecodeProj& g, int gw, int nw, const GemvRope& rp) {
-    if (gw >= ntask<EP>(g)) return;
-    rows<EP>(g, gw, nw, rp);
-    load(g, (threadIdx.x & 63) * E);
+    if (chunks<EP>(g, gw, nw) > 0) issue<EP, 0>(g, gw, nw, rp, 0);
+  }
+
+  float acc[TP][kRows];
+  float sx;
+
+  // consume chunk c from register set B; the last chunk of a round reduces and stores its tasks
+  template <int EP, int B>
+  __device__ __forceinline__ void consume(const DecodeProj& g, const bf16* xs, bf16* y, int gw,
+                                          int nw, const GemvRope& rp, int c) {
+    const int lane = threadIdx.x & 63;
+    const int K = g.K, N = g.N, nt = ntask<EP>(g);
+    const int it = iters(g), r = c / it, kc = c - r * it;
+    if (kc == 0) {
+#pragma unroll
+      for (int i = 0; i < TP; ++i) acc[i][0] = acc[i][1] = 0.f;
+      sx = 0.f;
+    }
+    const int k0 = lane * E + kc * kStep * U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u * kStep;
+      if constexpr (WQ == 0) {
+        const bf16x8 xv = k < K ? *reinterpret_cast<const bf16x8*>(xs + k) : bf16x8{};
+#pragma unroll
+        for (int i = 0; i < TP; ++i) {
+          const bf16x8 w0 = __builtin_bit_cast(bf16x8, wv[B][i][u][0]);
+          const bf16x8 w1 = __builtin_bit_cast(bf16x8, wv[B][i][u][1]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bf16x2 xp = {xv[2 * j], xv[2 * j + 1]};
+            acc[i][0] = __builtin_amdgcn_fdot2_f32_bf16(xp, bf16x2{w0[2 * j], w0[2 * j + 1]}, acc[i][0], false);
+            acc[i][1] = __builtin_amdgcn_fdot2_f32_bf16(xp, bf16x2{w1[2 * j], w1[2 * j + 1]}, acc[i][1], false);
+          }
+        }
+      } else {
+        bf16x8 xv[2];
+        if (k < K) {
+          xv[0] = *reinterpret_cast<const bf16x8*>(xs + k);
+          xv[1] = *reinterpret_cast<const bf16x8*>(xs + k + 8);
+        } else {
+          xv[0] = xv[1] = bf16x8{};
+        }
+        if constexpr (WQ == 2) {
+          const bf16x2 ones = {(bf16)1.f, (bf16)1.f};
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              sx = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{xv[h][2 * j], xv[h][2 * j + 1]}, ones,
+                                                   sx, false);
+#pragma unroll
+          for (int i = 0; i < TP; ++i)
+#pragma unroll
+            for (int q = 0; q < kRows; ++q)
+#pragma unroll
+              for (int d = 0; d < 4; ++d) {
+                const unsigned ub = wv[B][i][u][q][d] ^ 0x80808080u;
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                  const bf16x2 wp = u8pair_to_bf16x2(ub, j);
+                  const int e = (d & 1) * 4 + 2 * j;
+                  acc[i][q] = __builtin_amdgcn_fdot2_f32_bf16(
+                      bf16x2{xv[d >> 1][e], xv[d >> 1][e + 1]}, wp, acc[i][q], false);
+                }
+              }
+        } else {
+#pragma unroll
+          for (int i = 0; i < TP; ++i)
+#pragma unroll
+            for (int q = 0; q < kRows; ++q) {
+              const bf16x8 w0 = fp8x8_to_bf16x8(uint2{wv[B][i][u][q][0], wv[B][i][u][q][1]});
+              const bf16x8 w1 = fp8x8_to_bf16x8(uint2{wv[B][i][u][q][2], wv[B][i][u][q][3]});
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const bf16x2 x0 = {xv[0][2 * j], xv[0][2 * j + 1]};
+                const bf16x2 x1 = {xv[1][2 * j], xv[1][2 * j + 1]};
+                acc[i][q] = __builtin_amdgcn_fdot2_f32_bf16(x0, bf16x2{w0[2 * j], w0[2 * j + 1]}, acc[i][q], false);
+                acc[i][q] = __builtin_amdgcn_fdot2_f32_bf16(x1, bf16x2{w1[2 * j], w1[2 * j + 1]}, acc[i][q], false);
+              }
+            }
+        }
+      }
+    }
+    if (kc != it - 1) return;
+    const int t0 = gw + r * nw * TP;
+#pragma unroll
+    for (int i = 0; i < TP; ++i) {
+      const int t = t0 + i * nw;
+      if (t >= nt) break;
+      if constexpr (WQ == 2) {
+#pragma unroll
+        for (int q = 0; q < kRows; ++q) acc[i][q] -= 128.f * sx;
+      }
+      float v[1][kRows];
+#pragma unroll
+      for (int q = 0; q < kRows; ++q) {
+        const int n = min(gemv_row<EP>(t, q, rp), N - 1);
+        const float sm = wave_reduce_sum(acc[i][q]);
+        v[0][q] = WQ == 0 ? sm + (g.bias ? (float)g.bias[n] : 0.f)
+                          : sm * g.ws[n] + (g.bias ? (float)g.bias[n] : 0.f);
+      }
+      gemv_store<EP, 1>(v, t, lane, N, y, rp);
+    }
   }
 
   template <int EP>
   __device__ __forceinline__ void run(const DecodeProj& g, const bf16* xs, bf16* y, int gw, int nw,
                                       const GemvRope& rp, bool pre) {
-    const int lane = threadIdx.x & 63;
-    const int K = g.K, N = g.N, nt = ntask<EP>(g);
-    for (int t0 = gw; t0 < nt; t0 += nw * TP) {
-      if (!pre) rows<EP>(g, t0, nw, rp);
-      float acc[TP][kRows];
-#pragma unroll
-      for (int i = 0; i < TP; ++i) acc[i][0] = acc[i][1] = 0.f;
-      float sx = 0.f;
-      for (int k0 = lane * E; k0 < K; k0 += kStep * U) {
-        if (!pre) load(g, k0);
-        pre = false;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int k = k0 + u * kStep;
-          if constexpr (WQ == 0) {
-            const bf16x8 xv = k < K ? *reinterpret_cast<const bf16x8*>(xs + k) : bf16x8{};
-#pragma unroll
-            for (int i = 0; i < TP; ++i) {
-              const bf16x8 w0 = __builtin_bit_cast(bf16x8, wv[i][u][0]);
-              const bf16x8 w1 = __builtin_bit_cast(bf16x8, wv[i][u][1]);
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const bf16x2 xp = {xv[2 * j], xv[2 * j + 1]};
-                acc[i][0] = __builtin_amdgcn_fdot2_f32_bf16(xp, bf16x2{w0[2 * j], w0[2 * j + 1]}, acc[i][0], false);
-                acc[i][1] = __builtin_amdgcn_fdot2_f32_bf16(xp, bf16x2{w1[2 * j], w1[2 * j + 1]}, acc[i][1], false);
-              }
-            }
-          } else {
-            bf16x8 xv[2];
-            if (k < K) {
-              xv[0] = *reinterpret_cast<const bf16x8*>(xs + k);
-              xv[1] = *reinterpret_cast<const bf16x8*>(xs + k + 8);
-            } else {
-              xv[0] = xv[1] = bf16x8{};
-            }
-            if constexpr (WQ == 2) {
-              const bf16x2 ones = {(bf16)1.f, (bf16)1.f};
-#pragma unroll
-              for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                  sx = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{xv[h][2 * j], xv[h][2 * j + 1]}, ones,
-                                                       sx, false);
-#pragma unroll
-              for (int i = 0; i < TP; ++i)
-#pragma unroll
-                for (int r = 0; r < kRows; ++r)
-#pragma unroll
-                  for (int d = 0; d < 4; ++d) {
-                    const unsigned ub = wv[i][u][r][d] ^ 0x80808080u;
-#pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                      const bf16x2 wp = u8pair_to_bf16x2(ub, j);
-                      const int e = (d & 1) * 4 + 2 * j;
-                      acc[i][r] = __builtin_amdgcn_fdot2_f32_bf16(
-                          bf16x2{xv[d >> 1][e], xv[d >> 1][e + 1]}, wp, acc[i][r], false);
-                    }
-                  }
-            } else {
-#pragma unroll
-              for (int i = 0; i < TP; ++i)
-#pragma unroll
-                for (int r = 0; r < kRows; ++r) {
-                  const bf16x8 w0 = fp8x8_to_bf16x8(uint2{wv[i][u][r][0], wv[i][u][r][1]});
-                  const bf16x8 w1 = fp8x8_to_bf16x8(uint2{wv[i][u][r][2], wv[i][u][r][3]});
-#pragma unroll
-                  for (int j = 0; j < 4; ++j) {
-                    const bf16x2 x0 = {xv[0][2 * j], xv[0][2 * j + 1]};
-                    const bf16x2 x1 = {xv[1][2 * j], xv[1][2 * j + 1]};
-                    acc[i][r] = __builtin_amdgcn_fdot2_f32_bf16(x0, bf16x2{w0[2 * j], w0[2 * j + 1]}, acc[i][r], false);
-                    acc[i][r] = __builtin_amdgcn_fdot2_f32_bf16(x1, bf16x2{w1[2 * j], w1[2 * j + 1]}, acc[i][r], false);
-                  }
-                }
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < TP; ++i) {
-        const int t = t0 + i * nw;
-        if (t >= nt) break;
-        if constexpr (WQ == 2) {
-#pragma unroll
-          for (int r = 0; r < kRows; ++r) acc[i][r] -= 128.f * sx;
-        }
-        float v[1][kRows];
-#pragma unroll
-        for (int r = 0; r < kRows; ++r) {
-          const int n = min(gemv_row<EP>(t, r, rp), N - 1);
-          const float s = wave_reduce_sum(acc[i][r]);
-          v[0][r] = WQ == 0 ? s + (g.bias ? (float)g.bias[n] : 0.f)
-                            : s * g.ws[n] + (g.bias ? (float)g.bias[n] : 0.f);
-        }
-        gemv_store<EP, 1>(v, t, lane, N, y, rp);
-      }
+    const int C = chunks<EP>(g, gw, nw);
+    if (C == 0) return;
+    if (!pre) issue<EP, 0>(g, gw, nw, rp, 0);
+    for (int c = 0; c < C; c += 2) {
+      if (c + 1 < C) issue<EP, 1>(g, gw, nw, rp, c + 1);
+      consume<EP, 0>(g, xs, y, gw, nw, rp, c);
+      if (c + 1 >= C) break;
+      if (c + 2 < C) issue<EP, 0>(g, gw, nw, rp, c + 2);
+      consume<EP, 1>(g, xs, y, gw, nw, rp, c + 1);
     }
   }
 };
@@ -295,7 +323,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   // LDS: the staged x of the current GEMV phase (<= 64 KB: I <= 32768), the attention groups'
   // merge images, reduction scratch
   __shared__ __attribute__((aligned(16))) bf16x8 xs[4096];
-  __shared__ __attribute__((aligned(16))) float alds[2][4 * 16 * (LROW + 2)];
+  __shared__ __attribute__((aligned(16))) float alds[4 * 16 * (LROW + 2)];
   __shared__ float scratch[kDlWaves];
   const int G = gridDim.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -314,7 +342,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
 
   dl_stamp(a.stamps, 0);
   // ---- P1: norm 1 + QKV GEMV + RoPE / cache write ----
-  DlGemv<WQ, 3> g1;   // ~2.5 QKV tasks per wave on 70B: all of them in one round
+  DlGemv<WQ, 3> g1;   // 70B: ~2.5 QKV tasks per wave, one round
   g1.template prefetch<kEpRope>(a.qkv, gw, nw, a.rp);
   dl_norm_stage(xs, a.h, a.r, a.ln1, a.eps1, a.qkv.K, blockIdx.x == 0 ? a.res1 : nullptr, scratch);
   __syncthreads();
@@ -325,37 +353,44 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   // ---- P2: attention partials (4-wave groups, attention.hip's grouped merge) ----
   const AttnParams& p = a.ap;
   const int items = p.nkv * ((p.nh / p.nkv + 15) >> 4) * p.num_splits;   // B = 1
-  if (blockIdx.x * kDlWaves < items) {   // workgroup-uniform: 2 groups of 4 waves each
-    const int grp = wave >> 2, wig = wave & 3;
-    const int gidx = blockIdx.x * 2 + grp;   // the standalone kernel's blockIdx
+  // one 4-wave group (the standalone kernel's workgroup) per workgroup, on as many CUs as there
+  // are groups: the latency-bound key loop runs one wave per SIMD, as it does standalone; waves
+  // 4..7 only join the merge barrier
+  for (int gidx = blockIdx.x; gidx * 4 < items; gidx += G) {   // workgroup-uniform
+    const bool aw = wave < 4;
+    const int wig = wave & 3;
+    // gidx: the standalone kernel's blockIdx
     const int item_raw = gidx * 4 + wig;
     const bool live = item_raw < items;
     const int item = __builtin_amdgcn_readfirstlane(live ? item_raw : items - 1);
     WaveState<D> st;
-    const DecodeItem di = attn_decode_item<D, false, KV8, false>(p, item, live, st);
+    DecodeItem di{};
     const int col = lane & 15, h4 = lane >> 4;
-    float lsum = st.l;
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
-    float* lds = alds[grp];
-    float* lo = lds + (wig * 16 + col) * LROW;
+    float* lds = alds;
     float* lml = lds + 4 * 16 * LROW;
+    if (aw) {
+      di = attn_decode_item<D, false, KV8, false>(p, item, live, st);
+      float lsum = st.l;
+      lsum += __shfl_xor(lsum, 16, 64);
+      lsum += __shfl_xor(lsum, 32, 64);
+      float* lo = lds + (wig * 16 + col) * LROW;
 #pragma unroll
-    for (int u = 0; u < D / 16; ++u) {
-      int d;
-      f32x4 o;
-      o_unit<D, KV8>(st, u, h4, d, o);
-      *reinterpret_cast<f32x4*>(lo + d) = o;
-    }
-    if (h4 == 0) {
-      lml[(wig * 16 + col) * 2] = st.m;
-      lml[(wig * 16 + col) * 2 + 1] = lsum;
+      for (int u = 0; u < D / 16; ++u) {
+        int d;
+        f32x4 o;
+        o_unit<D, KV8>(st, u, h4, d, o);
+        *reinterpret_cast<f32x4*>(lo + d) = o;
+      }
+      if (h4 == 0) {
+        lml[(wig * 16 + col) * 2] = st.m;
+        lml[(wig * 16 + col) * 2 + 1] = lsum;
+      }
     }
     __syncthreads();
     const int gs = a.gs;
     const int gq = wig / gs, w0 = gq * gs;   // merge group of this wave inside its 4-wave group
     const int gitem = gidx * 4 + w0;
-    if (gitem < items) {
+    if (aw && gitem < items) {
       const int S2 = p.num_splits / gs;
       const int s2 = (gitem % p.num_splits) / gs;
       const int tg = (wig - w0) * 64 + lane;
@@ -390,6 +425,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
         }
       }
     }
+    __syncthreads();   // the LDS images are rewritten by the next group of this workgroup
   }
   DlGemv<WQ, 2> g4;
   // O weights: in flight from the merge barrier on (issued at the attention barrier, the
@@ -451,7 +487,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   dl_copy_stage(xs, a.attn, a.o.K);
   __syncthreads();
   g4.template run<kEpPlain>(a.o, xsb, a.o_out, gw, nw, a.rp, true);
-  DlGemv<WQ, 4> g5;
+  DlGemv<WQ, 2> g5;   // 70B: 14 gate|up tasks per wave, 7 full rounds
   dl_grid_sync(a.bar, base + 4ull * G, a.err, a.stamps, 4,
                [&] { g5.template prefetch<kEpSwiGLU>(a.gu, gw, nw, a.rp); });
 

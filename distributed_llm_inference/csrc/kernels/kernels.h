@@ -150,7 +150,7 @@ struct DecodeLayerParams {
   bf16* act;            // [I] scratch
   unsigned long long* bar;   // grid-barrier arrival counter (zero once, then never reset)
   unsigned* err;        // barrier spin-timeout count (0 = every barrier completed)
-  unsigned long long* stamps = nullptr;   // diagnostics: [grid][16] 100 MHz wall ticks per phase
+  unsigned long long* stamps = nullptr;   // diagnostics: [grid][24] 100 MHz wall ticks per phase
 };
 int launch_decode_layer(const DecodeLayerParams& p, int wq, hipStream_t stream);
 int decode_layer_grid();

@@ -339,7 +339,7 @@ class LlamaDecoderLayer(nn.Module):
             return None
         st = getattr(self, "_dl_stamps", None)
         if st is None or st.device != dev:
-            st = self._dl_stamps = torch.zeros(16 * ops.native().decode_layer_grid(),
+            st = self._dl_stamps = torch.zeros(24 * ops.native().decode_layer_grid(),
                                                dtype=torch.int64, device=dev)
         return st
 
