@@ -516,11 +516,12 @@ def block_decode_layer(blocked: bool = True) -> None:
 
 
 def decode_layer_enabled() -> bool:
-    """Single-row decode runs each Llama layer as ONE persistent launch (csrc/kernels/
-    decode_layer.hip: the six GEMV / attention kernels of the fused-norm path as phases between
-    grid barriers, bit-identical results).  ``DLI_DECODE_LAYER=0`` turns it off; it is off when
-    ranks share a GPU (``DLI_SHARE_GPU=1``) or after :func:`block_decode_layer`."""
-    return (not _DECODE_LAYER_BLOCKED and os.environ.get("DLI_DECODE_LAYER", "1") == "1"
+    """``DLI_DECODE_LAYER=1``: single-row decode runs each Llama layer as ONE persistent launch
+    (csrc/kernels/decode_layer.hip: the six GEMV / attention kernels of the fused-norm path as
+    phases between grid barriers, bit-identical results).  Off by default until it beats the
+    six-launch path (scripts/decode_layer_probe.py); never when ranks share a GPU
+    (``DLI_SHARE_GPU=1``) or after :func:`block_decode_layer`."""
+    return (not _DECODE_LAYER_BLOCKED and os.environ.get("DLI_DECODE_LAYER", "0") == "1"
             and os.environ.get("DLI_SHARE_GPU", "0") != "1")
 
 
