@@ -956,7 +956,7 @@ void decode_layer(Tensor h, optional<Tensor> r, Tensor res1, Tensor res2, Tensor
                   Tensor v_cache, double k_scale, double v_scale, Tensor block_tables,
                   Tensor seq_lens, double scale, int64_t num_splits, optional<Tensor> part_o,
                   optional<Tensor> part_ml, Tensor attn, Tensor o_out, Tensor act, Tensor bar,
-                  optional<Tensor> stamps) {
+                  optional<Tensor> stamps, int64_t flags) {
   for (const Tensor* t : {&h, &res1, &res2, &out, &ln1, &ln2, &attn, &o_out, &act, &q_out}) {
     CHECK_IN(*t); CHECK_BF16(*t);
   }
@@ -1051,6 +1051,7 @@ void decode_layer(Tensor h, optional<Tensor> r, Tensor res1, Tensor res2, Tensor
                 "decode_layer: stamps = int64 [grid * 24]");
     p.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
   }
+  p.flags = (int)flags;
   const c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
   check_rc(dli::launch_decode_layer(p, wq, cur_stream()), "decode_layer");
 }

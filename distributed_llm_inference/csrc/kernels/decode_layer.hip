@@ -11,8 +11,8 @@
 //   P1  x = rmsnorm(h + r) * w1 (LDS, per workgroup); QKV GEMV, RoPE, k / v -> paged cache, q
 //   P2  attention: 4-wave groups run attn_decode_item over consecutive splits and merge them
 //       in LDS (attention.hip's grouped path), partials -> part_o / part_ml
-//   P3  merge of the partials per head (attn_combine_kernel's arithmetic) -> attn [nh * D]
-//   P4  O GEMV -> o_out
+//   P4  every workgroup merges the partials into its LDS x (attn_combine_kernel's arithmetic);
+//       O GEMV -> o_out
 //   P5  res2 = o_out + (h + r); x = rmsnorm(res2) * w2 (LDS); gate|up GEMV + SwiGLU -> act
 //   P6  down GEMV -> out
 //
@@ -36,11 +36,11 @@ namespace {
 
 constexpr int kDlThreads = 512;   // 8 waves, 2 per SIMD: 256 VGPRs for the attention phase
 constexpr int kDlWaves = kDlThreads / 64;
-constexpr int kDlBarriers = 5;
+constexpr int kDlBarriers = 4;
 constexpr int kDlUnroll = 4;      // k-steps of weight loads in flight per GEMV wave (8 spills)
 
 // diagnostics (DecodeLayerParams::stamps, [grid][24]): slot 0 = start, 2k-1 = arrival at barrier
-// k, 12+k = its L2 write-back done, 2k = its release, 11 = end
+// k, 12+k = its L2 write-back done, 2k = its release, 9 = end
 __device__ __forceinline__ void dl_stamp(unsigned long long* st, int slot) {
   if (st != nullptr && threadIdx.x == 0) st[(size_t)blockIdx.x * 24 + slot] = __builtin_amdgcn_s_memrealtime();
 }
@@ -428,67 +428,66 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
     __syncthreads();   // the LDS images are rewritten by the next group of this workgroup
   }
   DlGemv<WQ, 2> g4;
-  // O weights: in flight from the merge barrier on (issued at the attention barrier, the
-  // workgroups that have no attention work would flood HBM while the attention runs)
-  dl_grid_sync(a.bar, base + 2ull * G, a.err, a.stamps, 2, [] {});
+  const bool o_early = (a.flags & 1) != 0;   // O weights in flight during the attention tail
+  dl_grid_sync(a.bar, base + 2ull * G, a.err, a.stamps, 2, [&] {
+    if (o_early) g4.template prefetch<kEpPlain>(a.o, gw, nw, a.rp);
+  });
 
-  // ---- P3: merge the partials per head (attn_combine_kernel's arithmetic, B = 1) ----
+  // ---- P3 + P4: merge the partials into the O GEMV's x (LDS), O GEMV ----
   const int S2 = p.num_splits / a.gs;
   if (S2 > 1) {
-    // one wave per head: lanes 0..31 hold 4 consecutive d; the combine kernel's 8 lane groups
-    // take partials g, g + 8, ... -- its per-group running merge and the final in-order merge
-    // of the 8 group states are reproduced here with the same operations
-    for (int head = gw; head < p.nh; head += nw) {
-      if (lane < D / 4) {
-        constexpr int NG = 256 / (D / 4);
-        float gm[NG], gsum[NG];
-        f32x4 go[NG];
+    // every workgroup merges all heads itself (the partials are a few tens of KB, L2-resident
+    // after the first reader of each XCD) instead of a merge phase and a barrier; thread ->
+    // (head, 4 consecutive d); attn_combine_kernel's 8 lane groups take partials g, g + 8, ...:
+    // its per-group running merge and the in-order merge of the 8 group states are reproduced
+    // with the same operations
+    constexpr int NG = 256 / (D / 4);
+    for (int idx = threadIdx.x; idx < p.nh * (D / 4); idx += kDlThreads) {
+      const int head = idx / (D / 4), l4 = idx % (D / 4);
+      float gm[NG], gsum[NG];
+      f32x4 go[NG];
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          float m = -1e30f, s = 0.f;
-          f32x4 o = {0.f, 0.f, 0.f, 0.f};
-          for (int sp = g; sp < S2; sp += NG) {
-            const size_t r = (size_t)sp * p.nh + head;
-            const float mi = p.part_ml[r * 2], li = p.part_ml[r * 2 + 1];
-            const f32x4 oi = *reinterpret_cast<const f32x4*>(p.part_o + r * D + 4 * lane);
-            const float mn = fmaxf(m, mi);
-            const float e0 = __builtin_amdgcn_exp2f(m - mn), e1 = __builtin_amdgcn_exp2f(mi - mn);
-            o = o * e0 + oi * e1;
-            s = s * e0 + li * e1;
-            m = mn;
-          }
-          gm[g] = m;
-          gsum[g] = s;
-          go[g] = o;
+      for (int g = 0; g < NG; ++g) {
+        float m = -1e30f, s = 0.f;
+        f32x4 o = {0.f, 0.f, 0.f, 0.f};
+        for (int sp = g; sp < S2; sp += NG) {
+          const size_t r = (size_t)sp * p.nh + head;
+          const float mi = p.part_ml[r * 2], li = p.part_ml[r * 2 + 1];
+          const f32x4 oi = *reinterpret_cast<const f32x4*>(p.part_o + r * D + 4 * l4);
+          const float mn = fmaxf(m, mi);
+          const float e0 = __builtin_amdgcn_exp2f(m - mn), e1 = __builtin_amdgcn_exp2f(mi - mn);
+          o = o * e0 + oi * e1;
+          s = s * e0 + li * e1;
+          m = mn;
         }
-        float M = -1e30f;
-#pragma unroll
-        for (int g = 0; g < NG; ++g) M = fmaxf(M, gm[g]);
-        float Lt = 0.f;
-        f32x4 O = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          const float f = __builtin_amdgcn_exp2f(gm[g] - M);
-          Lt += f * gsum[g];
-          O += f * go[g];
-        }
-        const float inv = Lt > 0.f ? 1.f / Lt : 0.f;
-        bf16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (bf16)(O[r] * inv);
-        *reinterpret_cast<bf16x4*>(a.attn + (size_t)head * D + 4 * lane) = v;
+        gm[g] = m;
+        gsum[g] = s;
+        go[g] = o;
       }
+      float M = -1e30f;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) M = fmaxf(M, gm[g]);
+      float Lt = 0.f;
+      f32x4 O = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        const float f = __builtin_amdgcn_exp2f(gm[g] - M);
+        Lt += f * gsum[g];
+        O += f * go[g];
+      }
+      const float inv = Lt > 0.f ? 1.f / Lt : 0.f;
+      bf16x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = (bf16)(O[q] * inv);
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(xs) + (size_t)head * D + 4 * l4) = v;
     }
+  } else {
+    dl_copy_stage(xs, a.attn, a.o.K);
   }
-  dl_grid_sync(a.bar, base + 3ull * G, a.err, a.stamps, 3,
-               [&] { g4.template prefetch<kEpPlain>(a.o, gw, nw, a.rp); });
-
-  // ---- P4: O GEMV ----
-  dl_copy_stage(xs, a.attn, a.o.K);
   __syncthreads();
-  g4.template run<kEpPlain>(a.o, xsb, a.o_out, gw, nw, a.rp, true);
+  g4.template run<kEpPlain>(a.o, xsb, a.o_out, gw, nw, a.rp, o_early);
   DlGemv<WQ, 2> g5;   // 70B: 14 gate|up tasks per wave, 7 full rounds
-  dl_grid_sync(a.bar, base + 4ull * G, a.err, a.stamps, 4,
+  dl_grid_sync(a.bar, base + 3ull * G, a.err, a.stamps, 3,
                [&] { g5.template prefetch<kEpSwiGLU>(a.gu, gw, nw, a.rp); });
 
   // ---- P5: residual + norm 2 + gate|up GEMV + SwiGLU ----
@@ -497,7 +496,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   __syncthreads();
   g5.template run<kEpSwiGLU>(a.gu, xsb, a.act, gw, nw, a.rp, true);
   DlGemv<WQ, 2> g6;
-  dl_grid_sync(a.bar, base + 5ull * G, a.err, a.stamps, 5,
+  dl_grid_sync(a.bar, base + 4ull * G, a.err, a.stamps, 4,
                [&] { g6.template prefetch<kEpPlain>(a.down, gw, nw, a.rp); });
 
   // ---- P6: down GEMV ----
@@ -506,7 +505,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   g6.template run<kEpPlain>(a.down, xsb, a.out, gw, nw, a.rp, true);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  dl_stamp(a.stamps, 11);
+  dl_stamp(a.stamps, 9);
 }
 
 template <int WQ, bool KV8>

@@ -329,7 +329,8 @@ class LlamaDecoderLayer(nn.Module):
             *m.down_proj.stream_weights(), meta.positions, meta.slot_mapping, cos_sin, q, k_cache,
             v_cache, float(meta.k_scale), float(meta.v_scale), meta.block_tables, meta.seq_lens,
             float(a.scale), int(meta.num_splits), ws[0] if ws else None, ws[1] if ws else None,
-            attn, o_out, act, bar, self._dl_stamp_buffer(dev))
+            attn, o_out, act, bar, self._dl_stamp_buffer(dev),
+            int(os.environ.get("DLI_DL_FLAGS", "0")))
         return out.view(1, -1), res2.view(1, -1)
 
     def _dl_stamp_buffer(self, dev):

@@ -58,18 +58,18 @@ step("1", 2)
 st = stage.block.layers[1]._dl_stamps.view(-1, 24).cpu().double()
 t0 = st[:, 0].min()
 rel = (st - t0) / 100.0   # us
-names = ["P1 norm+QKV+RoPE", "P2 attention", "P3 merge", "P4 O", "P5 norm+gate|up", "P6 down"]
+names = ["P1 norm+QKV+RoPE", "P2 attention", "P4 merge+O", "P5 norm+gate|up", "P6 down"]
 prev_release = 0.0
 print(f"{fmt} ctx {ctx}: step with {L} layers (+ head): decode-layer kernel {t_mk:.3f} ms, "
       f"six-kernel path {t_six:.3f} ms")
-for k in range(1, 6):
+for k in range(1, 5):
     arr, rls = rel[:, 2 * k - 1], rel[:, 2 * k]
     print(f"  {names[k - 1]:18s} ends {arr.max():7.1f} us (median arrival {arr.median():7.1f}) "
           f"-> {arr.max() - prev_release:6.1f} us;  barrier {k}: release {rls.min():7.1f}..{rls.max():7.1f}"
           f" (latency {rls.min() - arr.max():5.1f} us, L2 write-back med "
           f"{(rel[:, 12 + k] - arr).median():4.1f} max {(rel[:, 12 + k] - arr).max():4.1f} us)")
     prev_release = rls.min().item()
-end = rel[:, 11]
-print(f"  {names[5]:18s} ends {end.max():7.1f} us -> {end.max() - prev_release:6.1f} us;  "
+end = rel[:, 9]
+print(f"  {names[4]:18s} ends {end.max():7.1f} us -> {end.max() - prev_release:6.1f} us;  "
       f"kernel start skew {rel[:, 0].max():.1f} us")
 print("errors", sum(l.decode_layer_errors() for l in stage.block.layers))
