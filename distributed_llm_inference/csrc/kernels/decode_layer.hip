@@ -58,10 +58,11 @@ __device__ __forceinline__ void dl_grid_sync(unsigned long long* bar, unsigned l
   __syncthreads();
   dl_stamp(st, 2 * k - 1);
   if (threadIdx.x == 0) {
-    // the L2s of the 8 XCDs are not coherent with each other for ordinary stores: one
-    // write-back (release) and one invalidate (acquire) per workgroup and barrier
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    dl_stamp(st, 12 + k);   // after the L2 write-back
+    // every cross-workgroup value of a phase is stored write-through at device scope (gst<true>),
+    // so its completion (vmcnt(0) above) is the release: no L2 write-back (measured 1.3-3.4 us
+    // median per workgroup and barrier when it was one); the acquire below invalidates this CU's
+    // L1 / the XCD's L2 (no stale line of a buffer another workgroup wrote this launch)
+    dl_stamp(st, 12 + k);
     __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   prefetch();
@@ -109,7 +110,7 @@ __device__ __forceinline__ void dl_norm_stage(bf16x8* xs, const bf16* a, const b
     if (b != nullptr) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) av[i][j] = (bf16)((float)av[i][j] + (float)rv[i][j]);
-      if (sum_out != nullptr) reinterpret_cast<bf16x8*>(sum_out)[t + i * 256] = av[i];
+      if (sum_out != nullptr) gst<true>(reinterpret_cast<bf16x8*>(sum_out) + t + i * 256, av[i]);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -165,9 +166,11 @@ struct DlGemv {
     const int it = iters(g), r = c / it, kc = c - r * it;
     const int nt = ntask<EP>(g);
     const int t0 = gw + r * nw * TP;
+    bool live[TP];
 #pragma unroll
     for (int i = 0; i < TP; ++i) {
-      const int t = min(t0 + i * nw, nt - 1);   // idle slots re-read a valid task (never stored)
+      live[i] = t0 + i * nw < nt;   // idle slots load nothing (their results are never stored)
+      const int t = min(t0 + i * nw, nt - 1);
 #pragma unroll
       for (int q = 0; q < kRows; ++q)
         wrow[B][i][q] = static_cast<const unsigned char*>(g.w) +
@@ -181,9 +184,10 @@ struct DlGemv {
       for (int i = 0; i < TP; ++i)
 #pragma unroll
         for (int q = 0; q < kRows; ++q)
-          wv[B][i][u][q] = k < g.K ? __builtin_nontemporal_load(
-                                         reinterpret_cast<const u32x4n*>(wrow[B][i][q] + (size_t)k * esz))
-                                   : u32x4n{0u, 0u, 0u, 0u};
+          wv[B][i][u][q] = live[i] && k < g.K
+                               ? __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(
+                                     wrow[B][i][q] + (size_t)k * esz))
+                               : u32x4n{0u, 0u, 0u, 0u};
     }
   }
   template <int EP>
@@ -296,7 +300,7 @@ struct DlGemv {
         v[0][q] = WQ == 0 ? sm + (g.bias ? (float)g.bias[n] : 0.f)
                           : sm * g.ws[n] + (g.bias ? (float)g.bias[n] : 0.f);
       }
-      gemv_store<EP, 1>(v, t, lane, N, y, rp);
+      gemv_store<EP, 1, true>(v, t, lane, N, y, rp);
     }
   }
 
@@ -414,13 +418,13 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
           bf16x4 v;
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = (bf16)(O[r] * inv);
-          *reinterpret_cast<bf16x4*>(a.attn + (size_t)head * D + d4) = v;
+          gst<true>(reinterpret_cast<bf16x4*>(a.attn + (size_t)head * D + d4), v);
         } else {
           const size_t r0 = (size_t)s2 * p.nh + head;
-          *reinterpret_cast<f32x4*>(p.part_o + r0 * D + d4) = O * di.vsc;
+          gst<true>(reinterpret_cast<f32x4*>(p.part_o + r0 * D + d4), O * di.vsc);
           if (d4 == 0) {
-            p.part_ml[r0 * 2] = M;
-            p.part_ml[r0 * 2 + 1] = Lt;
+            gst<true>(p.part_ml + r0 * 2, M);
+            gst<true>(p.part_ml + r0 * 2 + 1, Lt);
           }
         }
       }
@@ -485,6 +489,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
     dl_copy_stage(xs, a.attn, a.o.K);
   }
   __syncthreads();
+  dl_stamp(a.stamps, 20);   // merge / staging done
   g4.template run<kEpPlain>(a.o, xsb, a.o_out, gw, nw, a.rp, o_early);
   DlGemv<WQ, 2> g5;   // 70B: 14 gate|up tasks per wave, 7 full rounds
   dl_grid_sync(a.bar, base + 3ull * G, a.err, a.stamps, 3,

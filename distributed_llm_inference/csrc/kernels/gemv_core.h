@@ -33,7 +33,29 @@ __device__ __forceinline__ int gemv_row(int wave, int r, const GemvRope& rp) {
 }
 
 // outputs of a wave: kRows values per row m (final fp32, every lane holds them), lane 0 stores
-template <int EP, int M>
+// store; WT (the batch-1 decode-layer kernel): device-scope write-through (sc1), so the value is
+// visible to every XCD once the store completes -- no L2 write-back before the grid barrier
+template <bool WT, typename T>
+__device__ __forceinline__ void gst(T* p, T v) {
+  if constexpr (!WT) {
+    *p = v;
+  } else if constexpr (sizeof(T) == 1) {
+    asm volatile("global_store_byte %0, %1, off sc1" :: "v"(p), "v"((unsigned)__builtin_bit_cast(unsigned char, v)) : "memory");
+  } else if constexpr (sizeof(T) == 2) {
+    asm volatile("global_store_short %0, %1, off sc1" :: "v"(p), "v"((unsigned)__builtin_bit_cast(unsigned short, v)) : "memory");
+  } else if constexpr (sizeof(T) == 4) {
+    asm volatile("global_store_dword %0, %1, off sc1" :: "v"(p), "v"(__builtin_bit_cast(unsigned, v)) : "memory");
+  } else if constexpr (sizeof(T) == 8) {
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+    asm volatile("global_store_dwordx2 %0, %1, off sc1" :: "v"(p), "v"(__builtin_bit_cast(u32x2_t, v)) : "memory");
+  } else {
+    static_assert(sizeof(T) == 16, "gst: 1, 2, 4, 8 or 16 bytes");
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(__builtin_bit_cast(u32x4_t, v)) : "memory");
+  }
+}
+
+template <int EP, int M, bool WT = false>
 __device__ __forceinline__ void gemv_store(const float (&v)[M][kRows], int wave, int lane, int N,
                                            bf16* __restrict__ y, const GemvRope& rp) {
   if (lane != 0) return;
@@ -42,10 +64,10 @@ __device__ __forceinline__ void gemv_store(const float (&v)[M][kRows], int wave,
     if constexpr (EP == kEpPlain) {
 #pragma unroll
       for (int r = 0; r < kRows; ++r)
-        if (wave * kRows + r < N) y[(size_t)m * N + wave * kRows + r] = (bf16)v[m][r];
+        if (wave * kRows + r < N) gst<WT>(y + (size_t)m * N + wave * kRows + r, (bf16)v[m][r]);
     } else if constexpr (EP == kEpSwiGLU) {   // gate and up rounded to bf16 first (unfused path)
       const float g = (float)(bf16)v[m][0], u = (float)(bf16)v[m][1];
-      y[(size_t)m * (N >> 1) + wave] = (bf16)(g / (1.f + __expf(-g)) * u);
+      gst<WT>(y + (size_t)m * (N >> 1) + wave, (bf16)(g / (1.f + __expf(-g)) * u));
     } else {
       const int D = rp.D, half = D >> 1, nqk = rp.nh + rp.nkv;
       const bf16 b0 = (bf16)v[m][0], b1 = (bf16)v[m][1];   // the GEMM output, rounded
@@ -65,18 +87,18 @@ __device__ __forceinline__ void gemv_store(const float (&v)[M][kRows], int wave,
         }
         if (h < rp.nh) {
           bf16* q = rp.q_out + ((size_t)m * rp.nh + h) * D;
-          q[d] = o0;
-          q[d + half] = o1;
+          gst<WT>(q + d, o0);
+          gst<WT>(q + d + half, o1);
         } else if (slot >= 0) {
           const size_t base = (((size_t)blk * rp.nkv + (h - rp.nh)) * rp.bs + off) * D;
           if (rp.kv_fp8) {
             uint8_t* kc = static_cast<uint8_t*>(rp.k_cache) + base;
-            kc[d] = f32_to_fp8((float)o0 * rp.k_inv_scale);
-            kc[d + half] = f32_to_fp8((float)o1 * rp.k_inv_scale);
+            gst<WT>(kc + d, (uint8_t)f32_to_fp8((float)o0 * rp.k_inv_scale));
+            gst<WT>(kc + d + half, (uint8_t)f32_to_fp8((float)o1 * rp.k_inv_scale));
           } else {
             bf16* kc = static_cast<bf16*>(rp.k_cache) + base;
-            kc[d] = o0;
-            kc[d + half] = o1;
+            gst<WT>(kc + d, o0);
+            gst<WT>(kc + d + half, o1);
           }
         }
       } else if (slot >= 0) {
@@ -85,12 +107,12 @@ __device__ __forceinline__ void gemv_store(const float (&v)[M][kRows], int wave,
         const size_t i0 = (grp * D + dd) * 8 + (off & 7);
         if (rp.kv_fp8) {
           uint8_t* vc = static_cast<uint8_t*>(rp.v_cache);
-          vc[i0] = f32_to_fp8((float)b0 * rp.v_inv_scale);
-          vc[i0 + 8] = f32_to_fp8((float)b1 * rp.v_inv_scale);
+          gst<WT>(vc + i0, (uint8_t)f32_to_fp8((float)b0 * rp.v_inv_scale));
+          gst<WT>(vc + i0 + 8, (uint8_t)f32_to_fp8((float)b1 * rp.v_inv_scale));
         } else {
           bf16* vc = static_cast<bf16*>(rp.v_cache);
-          vc[i0] = b0;
-          vc[i0 + 8] = b1;
+          gst<WT>(vc + i0, b0);
+          gst<WT>(vc + i0 + 8, b1);
         }
       }
     }

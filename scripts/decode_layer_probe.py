@@ -69,6 +69,8 @@ for k in range(1, 5):
           f" (latency {rls.min() - arr.max():5.1f} us, L2 write-back med "
           f"{(rel[:, 12 + k] - arr).median():4.1f} max {(rel[:, 12 + k] - arr).max():4.1f} us)")
     prev_release = rls.min().item()
+print(f"  (merge + staging of the O input: median {(rel[:, 20] - rel[:, 4]).median():.1f} us, "
+      f"max {(rel[:, 20] - rel[:, 4]).max():.1f} us after barrier 2)")
 end = rel[:, 9]
 print(f"  {names[4]:18s} ends {end.max():7.1f} us -> {end.max() - prev_release:6.1f} us;  "
       f"kernel start skew {rel[:, 0].max():.1f} us")
