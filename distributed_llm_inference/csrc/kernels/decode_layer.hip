@@ -331,7 +331,9 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   __shared__ float scratch[kDlWaves];
   const int G = gridDim.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int gw = __builtin_amdgcn_readfirstlane(blockIdx.x * kDlWaves + wave);
+  // GEMV task order: wave-major across workgroups, so a phase whose task count is not a multiple
+  // of the wave count (70B QKV: 2.5 per wave) gives every CU the same number of tasks
+  const int gw = __builtin_amdgcn_readfirstlane(wave * (int)gridDim.x + (int)blockIdx.x);
   const int nw = G * kDlWaves;
   const bf16* xsb = reinterpret_cast<const bf16*>(xs);
 
@@ -452,21 +454,34 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
       f32x4 go[NG];
 #pragma unroll
       for (int g = 0; g < NG; ++g) {
-        float m = -1e30f, s = 0.f;
-        f32x4 o = {0.f, 0.f, 0.f, 0.f};
-        for (int sp = g; sp < S2; sp += NG) {
-          const size_t r = (size_t)sp * p.nh + head;
-          const float mi = p.part_ml[r * 2], li = p.part_ml[r * 2 + 1];
-          const f32x4 oi = *reinterpret_cast<const f32x4*>(p.part_o + r * D + 4 * l4);
-          const float mn = fmaxf(m, mi);
-          const float e0 = __builtin_amdgcn_exp2f(m - mn), e1 = __builtin_amdgcn_exp2f(mi - mn);
-          o = o * e0 + oi * e1;
-          s = s * e0 + li * e1;
-          m = mn;
+        gm[g] = -1e30f;
+        gsum[g] = 0.f;
+        go[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      // partials base + g go to group g (the combine kernel's order); each round's loads are
+      // issued together, then merged
+      for (int base = 0; base < S2; base += NG) {
+        float mi[NG], li[NG];
+        f32x4 oi[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          if (base + g < S2) {
+            const size_t r = (size_t)(base + g) * p.nh + head;
+            mi[g] = p.part_ml[r * 2];
+            li[g] = p.part_ml[r * 2 + 1];
+            oi[g] = *reinterpret_cast<const f32x4*>(p.part_o + r * D + 4 * l4);
+          }
         }
-        gm[g] = m;
-        gsum[g] = s;
-        go[g] = o;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          if (base + g < S2) {
+            const float mn = fmaxf(gm[g], mi[g]);
+            const float e0 = __builtin_amdgcn_exp2f(gm[g] - mn), e1 = __builtin_amdgcn_exp2f(mi[g] - mn);
+            go[g] = go[g] * e0 + oi[g] * e1;
+            gsum[g] = gsum[g] * e0 + li[g] * e1;
+            gm[g] = mn;
+          }
+        }
       }
       float M = -1e30f;
 #pragma unroll
