@@ -26,7 +26,8 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=4, help="decode micro-batch steps to aggregate")
     ap.add_argument("--marker", default="sample_kernel")
-    ap.add_argument("--cycle", default="", help="KERNEL:N - per-position means of KERNEL's calls")
+    ap.add_argument("--cycle", default="", help="KERNEL:N - per-position means of KERNEL's calls "
+                    "(~TEXT:N: every kernel whose name contains TEXT)")
     a = ap.parse_args()
     if a.trace.endswith(".db"):  # rocprofv3 rocpd (SQLite) output
         import sqlite3
@@ -78,7 +79,9 @@ def main():
         step_bounds = marks[-a.steps - 1:]
         for s0, s1 in zip(step_bounds[:-1], step_bounds[1:]):   # cycles restart every step
             durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-                    for r in rows[s0 + 1:s1 + 1] if short(r["Kernel_Name"]) == name]
+                    for r in rows[s0 + 1:s1 + 1]
+                    if (name[1:] in short(r["Kernel_Name"]) if name.startswith("~")
+                        else short(r["Kernel_Name"]) == name)]
             for j, d in enumerate(durs[:len(durs) - len(durs) % n]):
                 pos[j % n].append(d)
         print(f"\n{name}: mean us per position in cycles of {n} (per step, {len(pos[0])} cycles)")

@@ -9,7 +9,7 @@ for cfg in bf16 fp8; do
   f=$(find /tmp/prof_$cfg -name "*kernel_trace.csv" | head -1)
   s=$(find /tmp/prof_$cfg -name "*kernel_stats.csv" | head -1)
   cp "$s" gpurun_out/prof_${cfg}_kernel_stats.csv
-  cyc="dli::gemm_tile_kernel<4, 0, false, 1>:3"; [ $cfg = fp8 ] && cyc="dli::gemm_tile_kernel<4, 3, false, 1>:2"
+  cyc="~gemm4_kernel<4,:3"; [ $cfg = fp8 ] && cyc="dli::gemm_tile_kernel<4, 3, false, 1>:2"
   python3 scripts/analyze_trace.py "$f" --steps 3 --cycle "$cyc" > gpurun_out/prof_${cfg}_breakdown.txt || exit $?
   cat gpurun_out/prof_${cfg}_breakdown.txt
 done
