@@ -20,8 +20,8 @@
 // reduction, the 256-thread norm reduction, the grouped attention merge and the combine), so the
 // layer output is bit-identical to the six-kernel path (tests/test_decode_layer_gpu.py).
 //
-// Grid barrier: one 64-bit arrival counter per stream of layer launches, never reset: a launch's
-// base is the counter rounded down to a multiple of kDlBarriers * grid (every earlier launch
+// Grid barrier: 64-bit arrival counters (8, summed) per stream of layer launches, never reset: a
+// launch's base is their sum rounded down to a multiple of kDlBarriers * grid (every earlier launch
 // added exactly that many), read before the first arrival.  Arrivals are agent-scope atomics
 // after a release fence; waiting is a bounded spin (an error count, never a hang: co-residency
 // of all workgroups is required, so the host launches grid = CUs and only when no other kernel
@@ -38,6 +38,19 @@ constexpr int kDlThreads = 512;   // 8 waves, 2 per SIMD: 256 VGPRs for the atte
 constexpr int kDlWaves = kDlThreads / 64;
 constexpr int kDlBarriers = 4;
 constexpr int kDlUnroll = 4;      // k-steps of weight loads in flight per GEMV wave (8 spills)
+
+constexpr int kDlCounters = 8, kDlCounterStride = 16;   // u64s: one 128-B line per counter
+
+__device__ __forceinline__ unsigned long long dl_arrivals(unsigned long long* bar) {
+  unsigned long long v[kDlCounters];
+#pragma unroll
+  for (int i = 0; i < kDlCounters; ++i)
+    v[i] = __hip_atomic_load(bar + i * kDlCounterStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned long long t = 0;
+#pragma unroll
+  for (int i = 0; i < kDlCounters; ++i) t += v[i];
+  return t;
+}
 
 // diagnostics (DecodeLayerParams::stamps, [grid][24]): slot 0 = start, 2k-1 = arrival at barrier
 // k, 12+k = its L2 write-back done, 2k = its release, 9 = end
@@ -58,17 +71,21 @@ __device__ __forceinline__ void dl_grid_sync(unsigned long long* bar, unsigned l
   __syncthreads();
   dl_stamp(st, 2 * k - 1);
   if (threadIdx.x == 0) {
-    // every cross-workgroup value of a phase is stored write-through at device scope (gst<true>),
+    // arrivals spread over kDlCounters counters in separate 128-B lines (workgroup b -> counter
+    // b % kDlCounters): 256 arrivals on ONE address serialise (~6 us measured when they all come
+    // at once); pollers sum the counters.
+    // Every cross-workgroup value of a phase is stored write-through at device scope (gst<true>),
     // so its completion (vmcnt(0) above) is the release: no L2 write-back (measured 1.3-3.4 us
     // median per workgroup and barrier when it was one); the acquire below invalidates this CU's
     // L1 / the XCD's L2 (no stale line of a buffer another workgroup wrote this launch)
     dl_stamp(st, 12 + k);
-    __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(bar + (blockIdx.x % kDlCounters) * kDlCounterStride, 1ull,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   prefetch();
   if (threadIdx.x == 0) {
     unsigned spins = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (dl_arrivals(bar) < target) {
       __builtin_amdgcn_s_sleep(2);
       if (++spins == (1u << 21)) {   // ~0.2 s: count it and go on (never hang the GPU)
         atomicAdd(err, 1u);
@@ -340,7 +357,7 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   // this launch's barrier base (see the header)
   __shared__ unsigned long long base_s;
   if (threadIdx.x == 0) {
-    const unsigned long long v = __hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long v = dl_arrivals(a.bar);
     const unsigned long long per = (unsigned long long)kDlBarriers * G;
     base_s = v / per * per;
   }
@@ -441,7 +458,68 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
 
   // ---- P3 + P4: merge the partials into the O GEMV's x (LDS), O GEMV ----
   const int S2 = p.num_splits / a.gs;
-  if (S2 > 1) {
+  if (S2 > 1 && S2 <= 4 && p.nh * (D / 4) <= 4 * kDlThreads) {
+    // short contexts (<= 4 partials per head, every item of the workgroup in one pass): all
+    // loads of a thread's 4 items first, one round trip; the combine kernel's groups 4..7 are
+    // empty here (their merge terms are exact zeros) and are skipped
+    constexpr int IPT = 4;
+    float mi[IPT][4], li[IPT][4];
+    f32x4 oi[IPT][4];
+#pragma unroll
+    for (int it = 0; it < IPT; ++it) {
+      const int idx = threadIdx.x + it * kDlThreads;
+      const int head = idx / (D / 4), l4 = idx % (D / 4);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (g < S2 && idx < p.nh * (D / 4)) {
+          const size_t r = (size_t)g * p.nh + head;
+          mi[it][g] = p.part_ml[r * 2];
+          li[it][g] = p.part_ml[r * 2 + 1];
+          oi[it][g] = *reinterpret_cast<const f32x4*>(p.part_o + r * D + 4 * l4);
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < IPT; ++it) {
+      const int idx = threadIdx.x + it * kDlThreads;
+      if (idx >= p.nh * (D / 4)) break;
+      const int head = idx / (D / 4), l4 = idx % (D / 4);
+      float gm[4], gsum[4];
+      f32x4 go[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {   // the combine kernel's first merge into an empty group
+        if (g >= S2) break;
+        // its running state is a loop-carried value there, not a constant: keep it opaque so the
+        // same multiply-adds (and contractions) are emitted
+        float m0 = -1e30f, s0 = 0.f;
+        f32x4 o0 = {0.f, 0.f, 0.f, 0.f};
+        asm volatile("" : "+v"(m0), "+v"(s0), "+v"(o0));
+        const float mn = fmaxf(m0, mi[it][g]);
+        const float e0 = __builtin_amdgcn_exp2f(m0 - mn), e1 = __builtin_amdgcn_exp2f(mi[it][g] - mn);
+        go[g] = o0 * e0 + oi[it][g] * e1;
+        gsum[g] = s0 * e0 + li[it][g] * e1;
+        gm[g] = mn;
+      }
+      float M = -1e30f;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        if (g < S2) M = fmaxf(M, gm[g]);
+      float Lt = 0.f;
+      f32x4 O = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (g >= S2) break;
+        const float f = __builtin_amdgcn_exp2f(gm[g] - M);
+        Lt += f * gsum[g];
+        O += f * go[g];
+      }
+      const float inv = Lt > 0.f ? 1.f / Lt : 0.f;
+      bf16x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = (bf16)(O[q] * inv);
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(xs) + (size_t)head * D + 4 * l4) = v;
+    }
+  } else if (S2 > 1) {
     // every workgroup merges all heads itself (the partials are a few tens of KB, L2-resident
     // after the first reader of each XCD) instead of a merge phase and a barrier; thread ->
     // (head, 4 consecutive d); attn_combine_kernel's 8 lane groups take partials g, g + 8, ...:

@@ -148,7 +148,7 @@ struct DecodeLayerParams {
   bf16* attn;           // [nh * D] scratch
   bf16* o_out;          // [K] scratch
   bf16* act;            // [I] scratch
-  unsigned long long* bar;   // grid-barrier arrival counter (zero once, then never reset)
+  unsigned long long* bar;   // grid-barrier arrival counters [8][16] (zero once, never reset)
   unsigned* err;        // barrier spin-timeout count (0 = every barrier completed)
   unsigned long long* stamps = nullptr;   // diagnostics: [grid][24] 100 MHz wall ticks per phase
   int flags = 0;        // bit 0: issue the O weights' first chunk at the attention barrier

@@ -309,7 +309,7 @@ class LlamaDecoderLayer(nn.Module):
         bar = getattr(self, "_dl_bar", None)
         if bar is None or bar.device != dev:
             # grid-barrier arrival counter of this layer's launches (never reset; see the kernel)
-            bar = self._dl_bar = torch.zeros(2, dtype=torch.int64, device=dev)
+            bar = self._dl_bar = torch.zeros(136, dtype=torch.int64, device=dev)
         nh, D = a.num_heads, a.head_dim
         h = hidden.reshape(-1)
         first = residual is None
@@ -347,7 +347,7 @@ class LlamaDecoderLayer(nn.Module):
     def decode_layer_errors(self) -> int:
         """Grid-barrier spin timeouts of this layer's persistent launches (0 = all completed)."""
         bar = getattr(self, "_dl_bar", None)
-        return 0 if bar is None else int(bar[1].item() & 0xFFFFFFFF)
+        return 0 if bar is None else int(bar[128].item() & 0xFFFFFFFF)
 
     def _forward_gemv(self, hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out=False):
         """1-2 decode rows: input RMSNorm fused into the QKV GEMV, post-attention RMSNorm into the
