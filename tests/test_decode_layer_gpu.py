@@ -62,3 +62,17 @@ def test_decode_layer_kernel_long_context_many_splits(gpu, monkeypatch):
     got = _decode(stage, "1", monkeypatch, torch.bfloat16, 4, 1500)
     assert torch.equal(ref, got), (ref - got).abs().max().item()
     assert sum(l.decode_layer_errors() for l in stage.block.layers) == 0
+
+
+@pytest.mark.parametrize("quant", [None, "fp8"])
+def test_decode_layer_kernel_merge_fast_path(gpu, monkeypatch, quant):
+    """560-600 token contexts: 8-16 splits merged 4 at a time in the attention groups, so the
+    O phase's staging merges 2-4 partials per head (its single-round path)."""
+    stage = CausalLMStage(SPEC, 0, 2, device=gpu).init_random(7)
+    if quant == "fp8":
+        stage.block.quantize_fp8()
+    stage.block.set_fused_swiglu(True)
+    ref = _decode(stage, "0", monkeypatch, torch.bfloat16, 40, 560)
+    got = _decode(stage, "1", monkeypatch, torch.bfloat16, 40, 560)
+    assert torch.equal(ref, got), (ref - got).abs().max().item()
+    assert sum(l.decode_layer_errors() for l in stage.block.layers) == 0
