@@ -35,6 +35,7 @@
 //     workgroups of one XCD take neighbouring work items (shared A / B panels in its L2).
 #include "kernels.h"
 
+#include <type_traits>
 #include <utility>
 
 namespace dli {
@@ -87,7 +88,22 @@ template <> struct G4Sched<6> {   // v4 with the DMA spread over B2 (1 per 6 MFM
 template <> struct G4Sched<7> {   // v4 with the DMA 1 per 5 MFMAs (14 before B2)
   static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 5, b2 = 104, vm = 14, p0 = 105, ps = 1;
 };
-constexpr int kG4Variants = 8;
+// bfirst: the weight (B) pieces of a stage go out before the activation (A) pieces -- at decode M
+// the activations are L2-resident and the weights stream from HBM, so the HBM loads get the
+// longest lead before the barrier that waits for them
+template <> struct G4Sched<8> {   // v6, weights first
+  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 6, b2 = 104, vm = 12, p0 = 105, ps = 1;
+  static constexpr bool bfirst = true;
+};
+template <> struct G4Sched<9> {   // v4, weights first
+  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 4, b2 = 104, vm = 16, p0 = 105, ps = 1;
+  static constexpr bool bfirst = true;
+};
+template <typename S, typename = void> struct G4BFirst { static constexpr bool value = false; };
+template <typename S> struct G4BFirst<S, std::void_t<decltype(S::bfirst)>> {
+  static constexpr bool value = S::bfirst;
+};
+constexpr int kG4Variants = 10;
 // Default schedules (profiles/r4/gemm4_ab_v0-7.txt): decode-sized M (<= 2 row tiles, the
 // activations stay L2 / MALL-resident and only the weight stream misses) takes v6, whose DMA runs
 // the latest and thinnest (gate|up 377 vs 415 us gemm_tile, down 187 vs 199); larger M, where
@@ -344,7 +360,7 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
           if (DMA) g4_barrier();
         }
         if constexpr (DMA && g >= S::d0 && g < S::d0 + 16 * S::ds && (g - S::d0) % S::ds == 0)
-          dma(t + 2, (g - S::d0) / S::ds);
+          dma(t + 2, G4BFirst<S>::value ? (((g - S::d0) / S::ds) + 8) & 15 : (g - S::d0) / S::ds);
         if constexpr (NEXT && g == S::b2) {   // own DMA of tile t+1 landed (all but t+2's since)
           if (DMA) g4_vmcnt<S::vm>(); else g4_vmcnt<0>();
           g4_barrier();
@@ -558,6 +574,8 @@ static int launch_gemm4_p(void* C, const void* a, const void* b, int M, int N, i
     case 5: return launch_gemm4_v<5, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
     case 6: return launch_gemm4_v<6, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
     case 7: return launch_gemm4_v<7, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+    case 8: return launch_gemm4_v<8, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+    case 9: return launch_gemm4_v<9, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
   }
   return -5;
 #endif

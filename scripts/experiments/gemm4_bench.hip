@@ -55,7 +55,7 @@ struct Shape { const char* name; int M, N, K, splits, epi; };
 
 static int g_grid = 0;
 static int g_var = 0;   // gemm4 schedule variant under check
-constexpr int kVars = 8;
+constexpr int kVars = 10;
 
 static int check(const Shape& c) {
   int bad = 0;
