@@ -51,6 +51,32 @@ def step(flag, n=10):
     return ts[len(ts) // 2] * 1e3
 
 
+def graph_step(flag, reps=20):
+    """the same decode step replayed from a hipGraph (as the engine runs it)"""
+    os.environ["DLI_DECODE_LAYER"] = flag
+    pool.manager.append(0, 1)
+    m = pool.build_metadata([0], [1])
+    tok = torch.tensor([5], dtype=torch.int32, device=dev)
+    s_ = torch.cuda.Stream()
+    with torch.cuda.stream(s_):
+        for _ in range(2):
+            stage(tok, m, pool)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s_):
+        stage(tok, m, pool)
+    g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+g_mk = graph_step("1")
+g_six = graph_step("0")
+print(f"graph replay, {L} layers: decode-layer kernel {g_mk:.3f} ms, six-kernel path {g_six:.3f} ms")
 os.environ["DLI_DL_STAMPS"] = "1"
 t_mk = step("1")
 t_six = step("0")
