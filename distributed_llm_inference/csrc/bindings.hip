@@ -974,8 +974,9 @@ void decode_layer(Tensor h, optional<Tensor> r, Tensor res1, Tensor res2, Tensor
   }
   TORCH_CHECK(res2.data_ptr() != res1.data_ptr(), "decode_layer: res2 must not alias res1");
   CHECK_IN(bar);
-  TORCH_CHECK(bar.scalar_type() == at::kLong && bar.numel() >= 136,
-              "decode_layer: bar = int64 [136] (8 counters x 16, error word at 128)");
+  TORCH_CHECK(bar.scalar_type() == at::kLong && bar.numel() >= 168,
+              "decode_layer: bar = int64 [168] (8 counters x 16, error word at 128, merge "
+              "counters from 136)");
   int wq = -1;
   dli::DecodeLayerParams p{};
   p.qkv = decode_proj(w_qkv, s_qkv, b_qkv, wq, "decode_layer qkv");
@@ -1046,6 +1047,7 @@ void decode_layer(Tensor h, optional<Tensor> r, Tensor res1, Tensor res2, Tensor
   p.act = bp(act);
   p.bar = reinterpret_cast<unsigned long long*>(bar.data_ptr<int64_t>());
   p.err = reinterpret_cast<unsigned*>(bar.data_ptr<int64_t>() + 128);
+  p.merge_cnt = (flags & 2) ? nullptr : reinterpret_cast<unsigned*>(bar.data_ptr<int64_t>() + 136);
   if (stamps.has_value()) {
     CHECK_IN(*stamps);
     TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->numel() >= 24 * dli::decode_layer_grid(),

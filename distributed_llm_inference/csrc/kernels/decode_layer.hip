@@ -40,6 +40,7 @@ constexpr int kDlBarriers = 4;
 constexpr int kDlUnroll = 4;      // k-steps of weight loads in flight per GEMV wave (8 spills)
 
 constexpr int kDlCounters = 8, kDlCounterStride = 16;   // u64s: one 128-B line per counter
+constexpr int kDlMergeCounters = 64;   // attention merge arrivals, one per (kv head, head group)
 
 __device__ __forceinline__ unsigned long long dl_arrivals(unsigned long long* bar) {
   unsigned long long v[kDlCounters];
@@ -371,11 +372,15 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
   __syncthreads();
   const unsigned long long base = base_s;
   g1.template run<kEpRope>(a.qkv, xsb, nullptr, gw, nw, a.rp, true);
+  if (blockIdx.x == 0 && threadIdx.x < kDlMergeCounters && a.merge_cnt != nullptr)   // P2's merge
+    __hip_atomic_store(a.merge_cnt + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   dl_grid_sync(a.bar, base + 1ull * G, a.err, a.stamps, 1, [] {});
 
   // ---- P2: attention partials (4-wave groups, attention.hip's grouped merge) ----
   const AttnParams& p = a.ap;
   const int items = p.nkv * ((p.nh / p.nkv + 15) >> 4) * p.num_splits;   // B = 1
+  const bool last_merge = a.merge_cnt != nullptr && a.gs == 4 &&
+                          p.nkv * ((p.nh / p.nkv + 15) >> 4) <= kDlMergeCounters;
   // one 4-wave group (the standalone kernel's workgroup) per workgroup, on as many CUs as there
   // are groups: the latency-bound key loop runs one wave per SIMD, as it does standalone; waves
   // 4..7 only join the merge barrier
@@ -448,6 +453,86 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
         }
       }
     }
+    // The last of the S2 merge groups of a (kv head, head group) to finish merges all S2
+    // partials into the attention output itself (gs == 4: one merge group per workgroup; the
+    // counter was zeroed by workgroup 0 before barrier 1): no merge phase after the barrier.
+    // Partials are stored write-through and the arrival follows their completion; the merging
+    // group reads them at device scope (sc1), past any stale L2 line.
+    const int S2g = p.num_splits / a.gs;
+    if (last_merge && S2g > 1 && gidx * 4 < items) {   // workgroup-uniform
+      __shared__ int is_last;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int hg = (gidx * 4 / p.num_splits);   // (kv head, head group) index of this group
+      if (threadIdx.x == 0)
+        is_last = __hip_atomic_fetch_add(a.merge_cnt + hg, 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S2g - 1);
+      __syncthreads();
+      if (is_last) {
+        const int Gq = p.nh / p.nkv, hgroups = (Gq + 15) >> 4;
+        const int kvh = hg / hgroups, g0 = (hg % hgroups) * 16;
+        const int nheads = min(16, Gq - g0);
+        constexpr int NG = 256 / (D / 4);
+        const auto rso = __builtin_amdgcn_make_buffer_rsrc(p.part_o, 0, 0x7fffffff, 0x00020000);
+        const auto rsm = __builtin_amdgcn_make_buffer_rsrc(p.part_ml, 0, 0x7fffffff, 0x00020000);
+        for (int idx = threadIdx.x; idx < nheads * (D / 4); idx += kDlThreads) {
+          const int head = kvh * Gq + g0 + idx / (D / 4), l4 = idx % (D / 4);
+          float gm[NG], gsum[NG];
+          f32x4 go[NG];
+#pragma unroll
+          for (int g = 0; g < NG; ++g) {
+            gm[g] = -1e30f;
+            gsum[g] = 0.f;
+            go[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+          for (int base = 0; base < S2g; base += NG) {
+#pragma unroll
+            for (int half = 0; half < NG; half += 4) {   // 4 partials in flight at a time
+              float mi[4], li[4];
+              f32x4 oi[4];
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                if (base + half + j < S2g) {
+                  const int r = (base + half + j) * p.nh + head;
+                  // sc1 (device scope): the value another workgroup stored write-through
+                  mi[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsm, r * 8, 0, 16));
+                  li[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsm, r * 8 + 4, 0, 16));
+                  oi[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                        rso, (r * D + 4 * l4) * 4, 0, 16));
+                }
+              }
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int g = half + j;
+                if (base + g < S2g) {
+                  const float mn = fmaxf(gm[g], mi[j]);
+                  const float e0 = __builtin_amdgcn_exp2f(gm[g] - mn), e1 = __builtin_amdgcn_exp2f(mi[j] - mn);
+                  go[g] = go[g] * e0 + oi[j] * e1;
+                  gsum[g] = gsum[g] * e0 + li[j] * e1;
+                  gm[g] = mn;
+                }
+              }
+            }
+          }
+          float M = -1e30f;
+#pragma unroll
+          for (int g = 0; g < NG; ++g) M = fmaxf(M, gm[g]);
+          float Lt = 0.f;
+          f32x4 O = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int g = 0; g < NG; ++g) {
+            const float f = __builtin_amdgcn_exp2f(gm[g] - M);
+            Lt += f * gsum[g];
+            O += f * go[g];
+          }
+          const float inv = Lt > 0.f ? 1.f / Lt : 0.f;
+          bf16x4 v;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = (bf16)(O[q] * inv);
+          gst<true>(reinterpret_cast<bf16x4*>(a.attn + (size_t)head * D + 4 * l4), v);
+        }
+      }
+    }
     __syncthreads();   // the LDS images are rewritten by the next group of this workgroup
   }
   DlGemv<WQ, 2> g4;
@@ -458,7 +543,9 @@ __global__ void __launch_bounds__(kDlThreads) decode_layer_kernel(DecodeLayerPar
 
   // ---- P3 + P4: merge the partials into the O GEMV's x (LDS), O GEMV ----
   const int S2 = p.num_splits / a.gs;
-  if (S2 > 1 && S2 <= 4 && p.nh * (D / 4) <= 4 * kDlThreads) {
+  if (S2 > 1 && last_merge) {
+    dl_copy_stage(xs, a.attn, a.o.K);   // merged by the last attention group of each head group
+  } else if (S2 > 1 && S2 <= 4 && p.nh * (D / 4) <= 4 * kDlThreads) {
     // short contexts (<= 4 partials per head, every item of the workgroup in one pass): all
     // loads of a thread's 4 items first, one round trip; the combine kernel's groups 4..7 are
     // empty here (their merge terms are exact zeros) and are skipped

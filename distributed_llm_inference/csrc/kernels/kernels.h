@@ -152,6 +152,7 @@ struct DecodeLayerParams {
   unsigned* err;        // barrier spin-timeout count (0 = every barrier completed)
   unsigned long long* stamps = nullptr;   // diagnostics: [grid][24] 100 MHz wall ticks per phase
   int flags = 0;        // bit 0: issue the O weights' first chunk at the attention barrier
+  unsigned* merge_cnt = nullptr;   // [64] attention-merge arrival counters (zeroed in-kernel)
 };
 int launch_decode_layer(const DecodeLayerParams& p, int wq, hipStream_t stream);
 int decode_layer_grid();

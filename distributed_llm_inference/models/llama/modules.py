@@ -309,7 +309,7 @@ class LlamaDecoderLayer(nn.Module):
         bar = getattr(self, "_dl_bar", None)
         if bar is None or bar.device != dev:
             # grid-barrier arrival counter of this layer's launches (never reset; see the kernel)
-            bar = self._dl_bar = torch.zeros(136, dtype=torch.int64, device=dev)
+            bar = self._dl_bar = torch.zeros(168, dtype=torch.int64, device=dev)
         nh, D = a.num_heads, a.head_dim
         h = hidden.reshape(-1)
         first = residual is None
