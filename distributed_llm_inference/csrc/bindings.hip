@@ -310,7 +310,8 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
                  Tensor block_tables, Tensor seq_lens, double scale, int64_t n_sink,
                  int64_t sink_pad, int64_t ring, int64_t window, int64_t num_splits,
                  optional<Tensor> part_o, optional<Tensor> part_ml, double k_scale,
-                 double v_scale, optional<Tensor> out_q, optional<Tensor> out_mx) {
+                 double v_scale, optional<Tensor> out_q, optional<Tensor> out_mx,
+                 optional<Tensor> merge_cnt) {
   int64_t D = 0;
   auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
                        sink_pad, ring, window, k_scale, v_scale, D, out_q.has_value());
@@ -341,6 +342,11 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
     TORCH_CHECK(part_ml->numel() >= num_splits * B * p.nh * 2, "part_ml workspace too small");
     p.part_o = part_o->data_ptr<float>();
     p.part_ml = part_ml->data_ptr<float>();
+    if (merge_cnt.has_value()) {   // last-arrival merge instead of the combine kernel
+      CHECK_IN(*merge_cnt); CHECK_I32(*merge_cnt);
+      TORCH_CHECK(merge_cnt->numel() >= B * p.nh, "attn_decode: merge_cnt = int32 [B * nh], zeros");
+      p.merge_cnt = reinterpret_cast<unsigned*>(merge_cnt->data_ptr<int>());
+    }
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   check_rc(dli::launch_attn_decode(p, (int)B, (int)D, cur_stream()), "attn_decode");
@@ -1081,7 +1087,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("block_tables"), py::arg("seq_lens"), py::arg("scale"), py::arg("n_sink"),
         py::arg("sink_pad"), py::arg("ring"), py::arg("window"), py::arg("num_splits"),
         py::arg("part_o"), py::arg("part_ml"), py::arg("k_scale"), py::arg("v_scale"),
-        py::arg("out_q") = py::none(), py::arg("out_mx") = py::none());
+        py::arg("out_q") = py::none(), py::arg("out_mx") = py::none(),
+        py::arg("merge_cnt") = py::none());
   m.def("attn_prefill", &attn_prefill, "paged causal prefill attention (varlen)", py::arg("out"),
         py::arg("q"), py::arg("q_sink"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("block_tables"), py::arg("seq_lens"), py::arg("q_start"), py::arg("max_q"),

@@ -184,6 +184,14 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = (bf16)(O[r] * inv);
         *reinterpret_cast<bf16x4*>(p.out + ((size_t)b * p.nh + head) * D + d4) = v;
+      } else if (D == 128 && p.merge_cnt != nullptr && gs == 4) {   // write-through: the merging
+        // group may be on another XCD
+        const size_t r0 = ((size_t)s2 * B + b) * p.nh + head;
+        gst<true>(reinterpret_cast<f32x4*>(p.part_o + r0 * D + d4), O * vsc);
+        if (d4 == 0) {
+          gst<true>(p.part_ml + r0 * 2, M);
+          gst<true>(p.part_ml + r0 * 2 + 1, Lt);
+        }
       } else {
         const size_t r0 = ((size_t)s2 * B + b) * p.nh + head;
         *reinterpret_cast<f32x4*>(p.part_o + r0 * D + d4) = O * vsc;
@@ -192,6 +200,84 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
           p.part_ml[r0 * 2 + 1] = Lt;
         }
       }
+    }
+    // ---- last arrival merges (merge_cnt, gs == 4: the whole workgroup is one group) ----
+    const int S2m = splits / gs;
+    if (D == 128 && p.merge_cnt != nullptr && gs == 4 && S2m > 1) {   // (D < 128: 16-32 lane
+      // groups in the combine, too many registers for the merge's per-group state)
+      __shared__ int is_last;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's partial stores completed
+      __syncthreads();
+      const int ctr = ((int)b * p.nkv + kvh) * hgroups + g0 / 16;
+      if (threadIdx.x == 0)
+        is_last = __hip_atomic_fetch_add(p.merge_cnt + ctr, 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S2m - 1);
+      __syncthreads();
+      if (!is_last) return;
+      // attn_combine_kernel's arithmetic: its 256 / (D / 4) lane groups take partials g, g + NG,
+      // ...; each group's running merge, then the in-order merge of the group states.  Partials
+      // are read at device scope (sc1): written write-through by workgroups on other XCDs
+      constexpr int NG = 256 / (D / 4);
+      const auto rso = __builtin_amdgcn_make_buffer_rsrc(p.part_o, 0, 0x7fffffff, 0x00020000);
+      const auto rsm = __builtin_amdgcn_make_buffer_rsrc(p.part_ml, 0, 0x7fffffff, 0x00020000);
+      const int nheads = min(16, G - g0);
+      for (int idx = threadIdx.x; idx < nheads * (D / 4); idx += blockDim.x) {
+        const int head = kvh * G + g0 + idx / (D / 4), l4 = idx % (D / 4);
+        float gm[NG], gsum[NG];
+        f32x4 go[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          gm[g] = -1e30f;
+          gsum[g] = 0.f;
+          go[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        for (int base = 0; base < S2m; base += NG) {
+#pragma unroll
+          for (int half = 0; half < NG; half += 4) {
+            float mi[4], li[4];
+            f32x4 oi[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              if (base + half + j < S2m) {
+                const int r = (int)(((size_t)(base + half + j) * B + b) * p.nh + head);
+                mi[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsm, r * 8, 0, 16));
+                li[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsm, r * 8 + 4, 0, 16));
+                oi[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      rso, (r * D + 4 * l4) * 4, 0, 16));
+              }
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int g = half + j;
+              if (base + g < S2m) {
+                const float mn = fmaxf(gm[g], mi[j]);
+                const float e0 = __builtin_amdgcn_exp2f(gm[g] - mn), e1 = __builtin_amdgcn_exp2f(mi[j] - mn);
+                go[g] = go[g] * e0 + oi[j] * e1;
+                gsum[g] = gsum[g] * e0 + li[j] * e1;
+                gm[g] = mn;
+              }
+            }
+          }
+        }
+        float Mx = -1e30f;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) Mx = fmaxf(Mx, gm[g]);
+        float Lx = 0.f;
+        f32x4 Ox = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          const float f = __builtin_amdgcn_exp2f(gm[g] - Mx);
+          Lx += f * gsum[g];
+          Ox += f * go[g];
+        }
+        const float inv = Lx > 0.f ? 1.f / Lx : 0.f;
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (bf16)(Ox[r] * inv);
+        *reinterpret_cast<bf16x4*>(p.out + ((size_t)b * p.nh + head) * D + 4 * l4) = v;
+      }
+      if (threadIdx.x == 0)   // ready for the next launch (every group of this counter arrived)
+        __hip_atomic_store(p.merge_cnt + ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -587,7 +673,7 @@ static int launch_decode_d(const AttnParams& p, int B, hipStream_t stream) {
     if (p.kv_fp8) decode_grid<D, false, true>(p, (int)items, gs, stream);
     else decode_grid<D, false, false>(p, (int)items, gs, stream);
   }
-  if (p.num_splits > gs) {
+  if (p.num_splits > gs && !(D == 128 && p.merge_cnt != nullptr && gs == 4)) {
     AttnParams pc = p;
     pc.num_splits = p.num_splits / gs;
     attn_combine_kernel<D><<<B * p.nh, 256, 0, stream>>>(pc, B);

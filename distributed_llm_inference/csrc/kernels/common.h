@@ -40,6 +40,28 @@ __device__ __forceinline__ T wave_reduce_max(T v) {
   return v;
 }
 
+// store; WT: device-scope write-through (sc1), so the value is visible to every XCD once the
+// store completes (no L2 write-back before a grid barrier / arrival counter)
+template <bool WT, typename T>
+__device__ __forceinline__ void gst(T* p, T v) {
+  if constexpr (!WT) {
+    *p = v;
+  } else if constexpr (sizeof(T) == 1) {
+    asm volatile("global_store_byte %0, %1, off sc1" :: "v"(p), "v"((unsigned)__builtin_bit_cast(unsigned char, v)) : "memory");
+  } else if constexpr (sizeof(T) == 2) {
+    asm volatile("global_store_short %0, %1, off sc1" :: "v"(p), "v"((unsigned)__builtin_bit_cast(unsigned short, v)) : "memory");
+  } else if constexpr (sizeof(T) == 4) {
+    asm volatile("global_store_dword %0, %1, off sc1" :: "v"(p), "v"(__builtin_bit_cast(unsigned, v)) : "memory");
+  } else if constexpr (sizeof(T) == 8) {
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+    asm volatile("global_store_dwordx2 %0, %1, off sc1" :: "v"(p), "v"(__builtin_bit_cast(u32x2_t, v)) : "memory");
+  } else {
+    static_assert(sizeof(T) == 16, "gst: 1, 2, 4, 8 or 16 bytes");
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(__builtin_bit_cast(u32x4_t, v)) : "memory");
+  }
+}
+
 // Block-wide sum of one float per thread.  `scratch` must hold >= blockDim.x/64 floats.
 // Split-K partials consumed in place of a reduce pass (gemm_tile.hip kStoreF32 slabs).  NS
 // partials of N consecutive fp32 elements, all loads issued before the adds (NS is a compile-time

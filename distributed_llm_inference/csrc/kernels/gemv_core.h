@@ -33,28 +33,6 @@ __device__ __forceinline__ int gemv_row(int wave, int r, const GemvRope& rp) {
 }
 
 // outputs of a wave: kRows values per row m (final fp32, every lane holds them), lane 0 stores
-// store; WT (the batch-1 decode-layer kernel): device-scope write-through (sc1), so the value is
-// visible to every XCD once the store completes -- no L2 write-back before the grid barrier
-template <bool WT, typename T>
-__device__ __forceinline__ void gst(T* p, T v) {
-  if constexpr (!WT) {
-    *p = v;
-  } else if constexpr (sizeof(T) == 1) {
-    asm volatile("global_store_byte %0, %1, off sc1" :: "v"(p), "v"((unsigned)__builtin_bit_cast(unsigned char, v)) : "memory");
-  } else if constexpr (sizeof(T) == 2) {
-    asm volatile("global_store_short %0, %1, off sc1" :: "v"(p), "v"((unsigned)__builtin_bit_cast(unsigned short, v)) : "memory");
-  } else if constexpr (sizeof(T) == 4) {
-    asm volatile("global_store_dword %0, %1, off sc1" :: "v"(p), "v"(__builtin_bit_cast(unsigned, v)) : "memory");
-  } else if constexpr (sizeof(T) == 8) {
-    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-    asm volatile("global_store_dwordx2 %0, %1, off sc1" :: "v"(p), "v"(__builtin_bit_cast(u32x2_t, v)) : "memory");
-  } else {
-    static_assert(sizeof(T) == 16, "gst: 1, 2, 4, 8 or 16 bytes");
-    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(__builtin_bit_cast(u32x4_t, v)) : "memory");
-  }
-}
-
 template <int EP, int M, bool WT = false>
 __device__ __forceinline__ void gemv_store(const float (&v)[M][kRows], int wave, int lane, int N,
                                            bf16* __restrict__ y, const GemvRope& rp) {

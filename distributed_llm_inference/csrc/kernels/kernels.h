@@ -36,6 +36,10 @@ struct AttnParams {
   int mask_heads = 0, mask_q = 0, mask_k = 0;
   // decode, bf16 full cache, one split: load K / V non-temporally (streamed once per step)
   int kv_nt = 0;
+  // decode with 4-split groups and more partials than groups: per (sequence, kv head, head
+  // group) arrival counters [B * nkv * hgroups], zero between launches; the last group to store
+  // its partial merges them all (no attn_combine_kernel launch).  nullptr: combine kernel
+  unsigned* merge_cnt = nullptr;
 };
 
 struct RopeCacheParams {

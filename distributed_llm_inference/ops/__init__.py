@@ -274,22 +274,35 @@ def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_si
                              None, None, float(k_scale), float(v_scale), q8, sc)
         return MxFp8(q8, sc)
     out = torch.empty_like(q) if out is None else out
-    part_o = part_ml = None
+    part_o = part_ml = cnt = None
     if num_splits > 1:
         if workspace is None:
             workspace = decode_workspace(q.shape[0], q.shape[1], q.shape[2], num_splits, q.device)
-        part_o, part_ml = workspace
+        part_o, part_ml = workspace[0], workspace[1]
+        if len(workspace) > 2 and attn_last_merge():
+            cnt = workspace[2]
     native().attn_decode(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, float(scale),
                          int(n_sink), int(sink_pad), int(ring), int(window), int(num_splits),
-                         part_o, part_ml, float(k_scale), float(v_scale))
+                         part_o, part_ml, float(k_scale), float(v_scale), merge_cnt=cnt)
     return out
+
+
+def attn_last_merge() -> bool:
+    """``DLI_ATTN_MERGE=1`` (default): split-K decode attention (head dim 128, 4-split groups)
+    merges its partials in the last-arriving workgroup of each head group (write-through
+    partials, an arrival counter per head group, device-scope reads) instead of launching
+    attn_combine_kernel; ``0``: the combine kernel.  Same arithmetic either way."""
+    return os.environ.get("DLI_ATTN_MERGE", "1") == "1"
 
 
 def decode_workspace(rows: int, nh: int, head_dim: int, splits: int, device):
     """Split-K decode workspace: fp32 partial O and (max, sum) per split (sized for the unmerged
-    worst case; the kernel uses splits / 4 of it when its workgroups merge their splits)."""
+    worst case; the kernel uses splits / 4 of it when its workgroups merge their splits), and the
+    last-arrival merge's counters (int32, zero between launches: the merging workgroup resets
+    its own)."""
     return (torch.empty(splits * rows * nh * head_dim, dtype=torch.float32, device=device),
-            torch.empty(splits * rows * nh * 2, dtype=torch.float32, device=device))
+            torch.empty(splits * rows * nh * 2, dtype=torch.float32, device=device),
+            torch.zeros(rows * nh, dtype=torch.int32, device=device))
 
 
 def prefill_qb() -> int:

@@ -855,3 +855,35 @@ def test_skinny_gemm_qkv_rope_matches_gemv_then_rope_cache(gpu, wdtype, kv_fp8, 
         assert torch.equal(q, q_ref)
         for a, b in zip(caches[0], caches[1]):
             assert torch.equal(a.view(torch.uint8), b.view(torch.uint8))
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("splits,lens", [(8, [600]), (16, [600, 1100]), (64, [8192, 3000, 17]),
+                                         (128, [16384, 2, 600, 9000])])
+def test_attn_decode_last_merge_matches_combine(gpu, monkeypatch, fp8, splits, lens):
+    """The last-arriving workgroup's in-kernel merge (DLI_ATTN_MERGE=1, head dim 128) uses the
+    combine kernel's arithmetic: bit-identical outputs, with one workspace reused across launches
+    (its counters must come back to zero)."""
+    torch.manual_seed(splits)
+    nh, nkv, D, bs = 64, 8, 128, 64
+    lens_t = torch.tensor(lens, dtype=torch.int32)
+    B = lens_t.numel()
+    max_blocks = (int(lens_t.max()) + bs - 1) // bs
+    nblocks = B * max_blocks
+    if fp8:
+        kc, vc = _make_cache_fp8(nblocks, nkv, bs, D, gpu, 0.5, 2.0)
+    else:
+        kc, vc = _make_cache(nblocks, nkv, bs, D, gpu)
+    bt = _tables(B, max_blocks, nblocks, gpu, seed=3)
+    q = torch.randn(B, nh, D, device=gpu, dtype=BF)
+    ws = ops.decode_workspace(B, nh, D, splits, gpu)
+    kw = dict(num_splits=splits, workspace=ws, k_scale=0.5 if fp8 else 1.0,
+              v_scale=2.0 if fp8 else 1.0)
+    monkeypatch.setenv("DLI_ATTN_MERGE", "0")
+    ref_out = ops.attn_decode(q, None, kc, vc, bt, lens_t.to(gpu), D ** -0.5, **kw).clone()
+    monkeypatch.setenv("DLI_ATTN_MERGE", "1")
+    for _ in range(3):
+        got = ops.attn_decode(q, None, kc, vc, bt, lens_t.to(gpu), D ** -0.5, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref_out), (got.float() - ref_out.float()).abs().max().item()
+    assert int(ws[2].abs().sum().item()) == 0   # every counter reset by its merging workgroup
