@@ -41,12 +41,14 @@ namespace dli {
 //     puts several waves on every CU): the workgroup's waves hold `gs` (4 or 2) consecutive
 //     splits of one item and merge them through LDS (online-softmax rescale, padded O^T image),
 //     so only num_splits / gs partials per head go to HBM — and none when num_splits == gs;
-//     attn_combine_kernel merges what is left — or (round 4, head dim 128, DLI_ATTN_MERGE=1,
-//     default) the last-arriving workgroup of each head group does, with the combine kernel's
+//     attn_combine_kernel merges what is left — or (round 4, head dim 128, opt-in
+//     DLI_ATTN_MERGE=1) the last-arriving workgroup of each head group does, with the combine kernel's
 //     arithmetic: partials are stored write-through at device scope (no L2 write-back, which is
 //     what made round 2's agent-scope-release version 5-75 % slower than the launch), one
 //     relaxed arrival counter per head group after the stores complete, and the merging
-//     workgroup reads the partials with device-scope loads and resets its counter.
+//     workgroup reads the partials with device-scope loads and resets its counter.  Measured
+//     still slower than the launch at B = 1 (600 keys 11.3 vs 10.6 us, 8k keys 28.1 vs 15.0 us:
+//     one workgroup merging up to 32 partials serially), hence opt-in.
 // ===========================================================================================
 template <int D, bool WIN, bool FP8, bool GRP, bool NT = false>
 __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int items, int gs) {

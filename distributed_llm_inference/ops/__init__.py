@@ -288,11 +288,14 @@ def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_si
 
 
 def attn_last_merge() -> bool:
-    """``DLI_ATTN_MERGE=1`` (default): split-K decode attention (head dim 128, 4-split groups)
-    merges its partials in the last-arriving workgroup of each head group (write-through
-    partials, an arrival counter per head group, device-scope reads) instead of launching
-    attn_combine_kernel; ``0``: the combine kernel.  Same arithmetic either way."""
-    return os.environ.get("DLI_ATTN_MERGE", "1") == "1"
+    """``DLI_ATTN_MERGE=1``: split-K decode attention (head dim 128, 4-split groups) merges its
+    partials in the last-arriving workgroup of each head group (write-through partials, an
+    arrival counter per head group, device-scope reads) instead of launching
+    attn_combine_kernel.  Same arithmetic (bit-identical, tests/test_kernels_gpu.py).  Off by
+    default: measured slower (B=1: 600 keys 11.3 vs 10.6 us, 8k keys 28.1 vs 15.0 us -- one
+    workgroup reading up to 32 partials serially costs more than the launch;
+    profiles/r4/attn_last_merge_bench.txt)."""
+    return os.environ.get("DLI_ATTN_MERGE", "0") == "1"
 
 
 def decode_workspace(rows: int, nh: int, head_dim: int, splits: int, device):
