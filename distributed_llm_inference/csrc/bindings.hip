@@ -155,6 +155,14 @@ void gelu_bias(Tensor out, Tensor x, optional<Tensor> bias) {
   check_rc(dli::launch_gelu_bias(bp(out), bp(x), bb, (int)rows, (int)cols, cur_stream()), "gelu");
 }
 
+void l3_prefetch(Tensor t, int64_t nwg) {
+  CHECK_IN(t);
+  const size_t nb = (size_t)t.numel() * t.element_size();
+  TORCH_CHECK(nwg > 0 && nwg <= 4096, "l3_prefetch: 1 <= nwg <= 4096");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(t.device());
+  check_rc(dli::launch_l3_prefetch(t.data_ptr(), nb, (int)nwg, cur_stream()), "l3_prefetch");
+}
+
 void add(Tensor out, Tensor a, Tensor b) {
   CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
   CHECK_BF16(out); CHECK_BF16(a); CHECK_BF16(b);
@@ -311,7 +319,8 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
                  int64_t sink_pad, int64_t ring, int64_t window, int64_t num_splits,
                  optional<Tensor> part_o, optional<Tensor> part_ml, double k_scale,
                  double v_scale, optional<Tensor> out_q, optional<Tensor> out_mx,
-                 optional<Tensor> merge_cnt) {
+                 optional<Tensor> merge_cnt, optional<Tensor> prefetch, int64_t pf_split,
+                 int64_t pf_wgs) {
   int64_t D = 0;
   auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
                        sink_pad, ring, window, k_scale, v_scale, D, out_q.has_value());
@@ -347,6 +356,18 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
       TORCH_CHECK(merge_cnt->numel() >= B * p.nh, "attn_decode: merge_cnt = int32 [B * nh], zeros");
       p.merge_cnt = reinterpret_cast<unsigned*>(merge_cnt->data_ptr<int>());
     }
+  }
+  if (prefetch.has_value() && pf_wgs > 0) {   // L3 warm-up of the next projection's weights
+    CHECK_IN(*prefetch);
+    const size_t nb = (size_t)prefetch->numel() * prefetch->element_size();
+    TORCH_CHECK(nb % 16 == 0 && reinterpret_cast<uintptr_t>(prefetch->data_ptr()) % 16 == 0,
+                "attn_decode: prefetch range must be 16-byte aligned");
+    TORCH_CHECK(pf_split >= 0 && pf_split % 16 == 0, "attn_decode: pf_split % 16 == 0");
+    TORCH_CHECK(pf_wgs <= 4096, "attn_decode: pf_wgs <= 4096");
+    p.pf_src = prefetch->data_ptr();
+    p.pf_bytes = nb;
+    p.pf_split = (size_t)pf_split;
+    p.pf_wgs = (int)pf_wgs;
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   check_rc(dli::launch_attn_decode(p, (int)B, (int)D, cur_stream()), "attn_decode");
@@ -1088,7 +1109,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sink_pad"), py::arg("ring"), py::arg("window"), py::arg("num_splits"),
         py::arg("part_o"), py::arg("part_ml"), py::arg("k_scale"), py::arg("v_scale"),
         py::arg("out_q") = py::none(), py::arg("out_mx") = py::none(),
-        py::arg("merge_cnt") = py::none());
+        py::arg("merge_cnt") = py::none(), py::arg("prefetch") = py::none(),
+        py::arg("pf_split") = 0, py::arg("pf_wgs") = 0);
+  m.def("l3_prefetch", &l3_prefetch, "read a tensor on nwg workgroups and discard it "
+        "(Infinity-Cache warm-up)", py::arg("t"), py::arg("nwg"));
   m.def("attn_prefill", &attn_prefill, "paged causal prefill attention (varlen)", py::arg("out"),
         py::arg("q"), py::arg("q_sink"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("block_tables"), py::arg("seq_lens"), py::arg("q_start"), py::arg("max_q"),

@@ -57,6 +57,10 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
   // (none when gs == num_splits: the workgroup writes the normalised output itself)
   constexpr int LROW = D + 4;  // padded O^T column: conflict-free ds_write_b128
   __shared__ __attribute__((aligned(16))) float lds[GRP ? 4 * 16 * (LROW + 2) : 1];
+  if (p.pf_wgs > 0 && (int)blockIdx.x >= (int)gridDim.x - p.pf_wgs) {   // L3 warm-up workgroups
+    l3_touch(p.pf_src, p.pf_bytes, blockIdx.x - (gridDim.x - p.pf_wgs), p.pf_wgs, p.pf_never, nullptr);
+    return;
+  }
   const int wave = threadIdx.x >> 6;
   const int item_raw = blockIdx.x * 4 + wave;
   const bool live = item_raw < items;
@@ -295,6 +299,10 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p, int T) 
   constexpr int LG = D / 4, NG = 256 / LG;
   __shared__ f32x4 so[NG][LG];
   __shared__ float sml[NG][2];
+  if (p.pf_wgs > 0 && (int)blockIdx.x >= (int)gridDim.x - p.pf_wgs) {   // L3 warm-up workgroups
+    l3_touch(p.pf_src, p.pf_bytes, blockIdx.x - (gridDim.x - p.pf_wgs), p.pf_wgs, p.pf_never, nullptr);
+    return;
+  }
   const int th = blockIdx.x;  // t * nh + head
   const int grp = threadIdx.x / LG, l = threadIdx.x % LG;
   const size_t stride = (size_t)T * p.nh;
@@ -653,7 +661,7 @@ __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_ke
 // ------------------------------------------------------------------------------------------
 template <int D, bool WIN, bool FP8>
 static void decode_grid(const AttnParams& p, int items, int gs, hipStream_t stream) {
-  const int grid = (items + 3) / 4;
+  const int grid = (items + 3) / 4 + p.pf_wgs;
   if (p.num_splits > 1)
     attn_decode_kernel<D, WIN, FP8, true><<<grid, 256, 0, stream>>>(p, items, gs);
   else if (!FP8 && !WIN && p.kv_nt)   // large-batch bf16 full-cache decode: non-temporal stream
@@ -670,17 +678,25 @@ static int launch_decode_d(const AttnParams& p, int B, hipStream_t stream) {
   if (items > (1L << 30)) return -3;
   // splits merged inside a workgroup (its 4 waves hold consecutive splits of one item)
   const int gs = p.num_splits % 4 == 0 ? 4 : p.num_splits % 2 == 0 ? 2 : 1;
+  const bool combine = p.num_splits > gs && !(D == 128 && p.merge_cnt != nullptr && gs == 4);
+  AttnParams pa = p;   // L3 warm-up share of the attention launch (all of it without a combine)
+  if (p.pf_bytes == 0) pa.pf_wgs = 0;
+  else if (combine) pa.pf_bytes = p.pf_split < p.pf_bytes ? p.pf_split : p.pf_bytes;
+  if (pa.pf_bytes == 0) pa.pf_wgs = 0;
   if (p.ring > 0) {
-    if (p.kv_fp8) decode_grid<D, true, true>(p, (int)items, gs, stream);
-    else decode_grid<D, true, false>(p, (int)items, gs, stream);
+    if (p.kv_fp8) decode_grid<D, true, true>(pa, (int)items, gs, stream);
+    else decode_grid<D, true, false>(pa, (int)items, gs, stream);
   } else {
-    if (p.kv_fp8) decode_grid<D, false, true>(p, (int)items, gs, stream);
-    else decode_grid<D, false, false>(p, (int)items, gs, stream);
+    if (p.kv_fp8) decode_grid<D, false, true>(pa, (int)items, gs, stream);
+    else decode_grid<D, false, false>(pa, (int)items, gs, stream);
   }
-  if (p.num_splits > gs && !(D == 128 && p.merge_cnt != nullptr && gs == 4)) {
+  if (combine) {
     AttnParams pc = p;
     pc.num_splits = p.num_splits / gs;
-    attn_combine_kernel<D><<<B * p.nh, 256, 0, stream>>>(pc, B);
+    pc.pf_src = static_cast<const char*>(p.pf_src) + pa.pf_bytes;
+    pc.pf_bytes = p.pf_bytes - pa.pf_bytes;
+    if (pc.pf_bytes == 0) pc.pf_wgs = 0;
+    attn_combine_kernel<D><<<B * p.nh + pc.pf_wgs, 256, 0, stream>>>(pc, B);
   }
   return 0;
 }

@@ -40,6 +40,13 @@ struct AttnParams {
   // group) arrival counters [B * nkv * hgroups], zero between launches; the last group to store
   // its partial merges them all (no attn_combine_kernel launch).  nullptr: combine kernel
   unsigned* merge_cnt = nullptr;
+  // decode: Infinity-Cache warm-up of the next projection's weights while HBM is otherwise idle
+  // (batch-1 attention reads a few MB of K/V): pf_wgs extra workgroups per launch read
+  // [pf_src, pf_src + pf_bytes) and discard it -- the first pf_split bytes in the attention launch,
+  // the rest in the combine launch when there is one.  pf_never is 0 (keeps the loads alive).
+  const void* pf_src = nullptr;
+  size_t pf_bytes = 0, pf_split = 0;
+  int pf_wgs = 0, pf_never = 0;
 };
 
 struct RopeCacheParams {
@@ -92,6 +99,8 @@ int launch_silu_mul(bf16* out, const bf16* x, int rows, int inter, bool interlea
 int launch_gelu_bias(bf16* out, const bf16* x, const bf16* bias, int rows, int cols,
                      hipStream_t stream);
 int launch_add(bf16* out, const bf16* a, const bf16* b, size_t n, hipStream_t stream);
+// read [src, src + bytes) on nwg workgroups and discard it (Infinity-Cache warm-up)
+int launch_l3_prefetch(const void* src, size_t bytes, int nwg, hipStream_t stream);
 int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stream);
 int launch_attn_decode(const AttnParams& p, int B, int D, hipStream_t stream);
 int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_t stream);

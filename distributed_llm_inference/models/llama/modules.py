@@ -122,10 +122,13 @@ class LlamaAttention(nn.Module):
                                     num_splits=meta.num_splits, workspace=meta.workspace,
                                     k_scale=meta.k_scale, v_scale=meta.v_scale, mx_out=True)
                 return op(None, x_q=o, defer_reduce=defer_reduce)
+            pf = None
+            if T <= 2 and q.is_cuda and ops.l3_prefetch_enabled() and op.gemv_ok(T):
+                pf = op.stream_weights()[0]   # the O GEMV's weights, into L3 during attention
             o = ops.attn_decode(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
                                 self.scale, meta.n_sink, meta.sink_pad, meta.ring, meta.window,
                                 num_splits=meta.num_splits, workspace=meta.workspace,
-                                k_scale=meta.k_scale, v_scale=meta.v_scale)
+                                k_scale=meta.k_scale, v_scale=meta.v_scale, prefetch=pf)
         else:
             o = ops.attn_prefill(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
                                  meta.q_start, meta.max_q, self.scale, meta.n_sink, meta.sink_pad,

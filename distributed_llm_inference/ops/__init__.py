@@ -249,11 +249,13 @@ def attn_decode_mx_ok(head_dim: int, num_splits: int) -> bool:
 
 def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink=0, sink_pad=0,
                 ring=0, window=0, num_splits=1, workspace=None, out=None, k_scale=1.0, v_scale=1.0,
-                mx_out: bool = False):
+                mx_out: bool = False, prefetch=None):
     """Paged GQA decode attention -> bf16 ``[T, nh, D]``; ``mx_out`` (needs
     :func:`attn_decode_mx_ok`): the same values (rounded to bf16) quantised in the kernel's
     epilogue to :class:`MxFp8` ``[T, nh * D]`` for the fp8 O projection, replacing a separate
-    per-row quantisation pass."""
+    per-row quantisation pass.  ``prefetch``: a tensor (the next GEMV's weight) that extra
+    workgroups of the attention / combine launches read into the Infinity Cache meanwhile
+    (:func:`l3_prefetch_cfg`); no effect on the result."""
     if mx_out and not attn_decode_mx_ok(q.shape[-1], num_splits):
         raise ValueError("attn_decode(mx_out=True) needs head_dim 128 and one split")
     if not _gpu(q):
@@ -281,10 +283,40 @@ def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_si
         part_o, part_ml = workspace[0], workspace[1]
         if len(workspace) > 2 and attn_last_merge():
             cnt = workspace[2]
+    pf_split = pf_wgs = 0
+    if prefetch is not None:
+        share, pf_wgs = l3_prefetch_cfg()
+        nb = prefetch.numel() * prefetch.element_size()
+        pf_split = int(nb * share) // 16 * 16
     native().attn_decode(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, float(scale),
                          int(n_sink), int(sink_pad), int(ring), int(window), int(num_splits),
-                         part_o, part_ml, float(k_scale), float(v_scale), merge_cnt=cnt)
+                         part_o, part_ml, float(k_scale), float(v_scale), merge_cnt=cnt,
+                         prefetch=prefetch if pf_wgs else None, pf_split=pf_split, pf_wgs=pf_wgs)
     return out
+
+
+def l3_prefetch_enabled() -> bool:
+    """``DLI_L3_PF=1``: batch-1 decode attention reads the O projection's weights into the
+    256 MiB Infinity Cache while it runs (HBM is otherwise idle: a few MB of K/V per layer), so
+    the O GEMV streams them from L3 (scripts/l3_prefetch_probe.py).  Off by default: a warm O
+    GEMV is only 1.4-2.8 us faster (13.4 -> 11.7 us fp8, 23.7 -> 20.9 us bf16: L3 serves this
+    stream at 5.7-6.4 TB/s) and the batch-1 step did not change (fp8 77.45 vs 77.42 tok/s;
+    profiles/r4/l3_prefetch_ab.txt)."""
+    return os.environ.get("DLI_L3_PF", "0") == "1"
+
+
+def l3_prefetch_cfg():
+    """(share of the bytes read by the attention launch -- the rest by the combine launch when
+    there is one --, warm-up workgroups per launch): ``DLI_L3_PF_SPLIT`` (default 1.0),
+    ``DLI_L3_PF_WGS`` (default 224)."""
+    share = min(max(float(os.environ.get("DLI_L3_PF_SPLIT", "1.0")), 0.0), 1.0)
+    return share, max(0, min(4096, int(os.environ.get("DLI_L3_PF_WGS", "224"))))
+
+
+def l3_prefetch(t: torch.Tensor, nwg: int = 224) -> None:
+    """Read ``t`` on ``nwg`` workgroups and discard it (Infinity-Cache warm-up); GPU only."""
+    if _gpu(t):
+        native().l3_prefetch(t, int(nwg))
 
 
 def attn_last_merge() -> bool:

@@ -887,3 +887,30 @@ def test_attn_decode_last_merge_matches_combine(gpu, monkeypatch, fp8, splits, l
         torch.cuda.synchronize()
         assert torch.equal(got, ref_out), (got.float() - ref_out.float()).abs().max().item()
     assert int(ws[2].abs().sum().item()) == 0   # every counter reset by its merging workgroup
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("splits,share", [(1, 1.0), (16, 1.0), (16, 0.5), (16, 0.0)])
+def test_attn_decode_l3_prefetch_leaves_output_unchanged(gpu, monkeypatch, splits, share):
+    """Warm-up workgroups appended to the attention / combine launches (DLI_L3_PF) read a weight
+    and discard it: bit-identical attention output for every split of the bytes between the two
+    launches, the weight untouched, and ops.l3_prefetch alone is a no-op on its tensor."""
+    torch.manual_seed(splits)
+    nh, nkv, D, bs = 64, 8, 128, 64
+    lens_t = torch.tensor([600], dtype=torch.int32)
+    max_blocks = (600 + bs - 1) // bs
+    kc, vc = _make_cache(max_blocks, nkv, bs, D, gpu)
+    bt = _tables(1, max_blocks, max_blocks, gpu, seed=5)
+    q = torch.randn(1, nh, D, device=gpu, dtype=BF)
+    w = torch.randn(8192, 8192, device=gpu, dtype=BF)
+    w_ref = w.clone()
+    ws = ops.decode_workspace(1, nh, D, splits, gpu)
+    kw = dict(num_splits=splits, workspace=ws if splits > 1 else None)
+    ref_out = ops.attn_decode(q, None, kc, vc, bt, lens_t.to(gpu), D ** -0.5, **kw).clone()
+    monkeypatch.setenv("DLI_L3_PF_SPLIT", str(share))
+    monkeypatch.setenv("DLI_L3_PF_WGS", "200")
+    got = ops.attn_decode(q, None, kc, vc, bt, lens_t.to(gpu), D ** -0.5, prefetch=w, **kw)
+    ops.l3_prefetch(w, 96)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref_out)
+    assert torch.equal(w, w_ref)
