@@ -518,7 +518,8 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = 
     """``x [M, K] @ w[N, K]^T`` with the 256x256 LDS-DMA MFMA kernel (N % 256 == 0, K % 64 == 0).
     ``swiglu=True``: ``w`` is a ``swiglu_interleave``d [gate; up] weight and the result is
     ``silu(x @ gate^T) * (x @ up^T)`` ([M, N/2]).  ``defer_reduce`` (split-K only): return the
-    fp32 partials as :class:`SplitKPartials` for a consumer that reduces them (``rms_norm``)."""
+    partials as :class:`SplitKPartials` for a consumer that reduces them (``rms_norm``): bf16
+    under :func:`bf16_bf16_partials` (the default), else fp32."""
     M, N = x.shape[0], w.shape[0]
     if _gpu(x) and gemm4_enabled():
         return _gemm4(x, w, splits, swiglu, out, defer_reduce)
@@ -745,7 +746,7 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
     pass the threshold; ``threshold <= 0`` disables the decomposition.  ``wq_t``: optional
     transposed copy ``[K, N]`` of ``wq`` (GPU) that makes the outlier weight-column gather
     coalesced.  ``swiglu``: ``wq`` / ``ws`` rows in ``swiglu_interleave`` order, returns
-    ``silu(gate) * up`` ([M, N/2]).  ``defer_reduce``: a split-K product returns its fp32 partials
+    ``silu(gate) * up`` ([M, N/2]).  ``defer_reduce``: a split-K product returns its partials
     (:class:`SplitKPartials`, the outlier product inside split 0's) for a consumer to reduce."""
     M, K = x.shape
     N = wq.shape[0]
@@ -842,7 +843,8 @@ def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torc
     """fp8 e4m3 tile GEMM: ``(xq [M, K] @ wq[N, K]^T) * xs[M] * ws[N]`` -> bf16, on the
     block-scaled K=128 MFMA (2x the bf16 MFMA rate; unit block scales, per-row / per-channel
     scales applied in the epilogue).  ``swiglu``: ``wq`` / ``ws`` rows in swiglu_interleave order.
-    ``defer_reduce`` (split-K): return :class:`SplitKPartials` (scaled fp32 partials).
+    ``defer_reduce`` (split-K): return :class:`SplitKPartials` (scaled partials, bf16 under
+    :func:`fp8_bf16_partials`).
     ``mx_out`` (with ``swiglu``): return the SwiGLU output as :class:`MxFp8`, quantised in the
     epilogue (needs N % 256 == 0)."""
     M, N = xq.shape[0], wq.shape[0]
