@@ -8,6 +8,18 @@ namespace dli {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+// Block-table entry of a wave-uniform index, by a scalar load waited on in place.  A plain
+// bt[i] inside the decode loop compiles to a VECTOR load (the loop's sched_barrier is a memory
+// side effect to the clobber analysis, so the load is not proven read-only-so-far), and its
+// vmcnt(0) wait drained the prefetched K/V of the next step every step.  The scalar load joins
+// only the lgkm queue: the K/V loads in flight stay in flight.
+__device__ __forceinline__ int bt_entry(const int* bt, int i) {
+  const int* a = bt + __builtin_amdgcn_readfirstlane(i);
+  int v;
+  asm volatile("s_load_dword %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(a));
+  return v;
+}
+
 __device__ __forceinline__ bf16x8 zero8() {
   i32x4 z = {0, 0, 0, 0};
   return __builtin_bit_cast(bf16x8, z);
@@ -108,32 +120,31 @@ __device__ __forceinline__ void attn_load(KVFrag<D>& f, const void* __restrict__
     }
     return;
   }
+  // Keys past the sequence end (nvalid >= 1 of this step's 32) are not fetched: their rows /
+  // 8-key groups are clamped to the last valid one, a line already being read, so every load is
+  // issued unconditionally (no exec-masked branches: hipcc then counts the vmcnt waits and the
+  // next step's prefetch stays in flight through this step's MFMAs).  The clamped keys are
+  // invisible to the softmax (p = 0 exactly) and their finite V values add exact zeros.
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const bool kin = krow0 - offk + 4 * t < nvalid;
+    const int kr = min(krow0 + 4 * t, offk + nvalid - 1);
 #pragma unroll
     for (int c = 0; c < D / 32; ++c) {
-      const size_t e = hb + (size_t)(krow0 + 4 * t) * D + 32 * c + 8 * h4;
-      f.k[t][c] = zero8();
-      if (kin) {
-        if (FP8)
-          f.k[t][c] = fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(kc) + e));
-        else
-          f.k[t][c] = kv_ld16<NT>(static_cast<const bf16*>(kc) + e);
-      }
+      const size_t e = hb + (size_t)kr * D + 32 * c + 8 * h4;
+      if (FP8)
+        f.k[t][c] = fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(kc) + e));
+      else
+        f.k[t][c] = kv_ld16<NT>(static_cast<const bf16*>(kc) + e);
     }
   }
-  const bool vin = 8 * h4 < nvalid;
+  const int vg = min(h4, (nvalid - 1) >> 3);
 #pragma unroll
   for (int e = 0; e < D / 16; ++e) {
-    const size_t o = hb + ((size_t)((offk >> 3) + h4) * D + 16 * e + col) * 8;
-    f.v[e] = zero8();
-    if (vin) {
-      if (FP8)
-        f.v[e] = fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(vc) + o));
-      else
-        f.v[e] = kv_ld16<NT>(static_cast<const bf16*>(vc) + o);
-    }
+    const size_t o = hb + ((size_t)((offk >> 3) + vg) * D + 16 * e + col) * 8;
+    if (FP8)
+      f.v[e] = fp8x8_to_bf16x8(*reinterpret_cast<const uint2*>(static_cast<const uint8_t*>(vc) + o));
+    else
+      f.v[e] = kv_ld16<NT>(static_cast<const bf16*>(vc) + o);
   }
 }
 
@@ -341,7 +352,7 @@ __device__ __forceinline__ DecodeItem attn_decode_item(const AttnParams& p, int 
     if (s_lo < s_hi) {
       auto load = [&](KVFrag<D>& f, int sidx) {
         const int u0 = seg_base + sidx * 32;
-        const int page = bt[u0 / p.bs];
+        const int page = bt_entry(bt, u0 / p.bs);
         const size_t hb = ((size_t)page * p.nkv + kvh) * head_stride;
         // full-cache mode: keys past the sequence end are not fetched (ring mode: all 32, its
         // validity is positional)
@@ -352,7 +363,7 @@ __device__ __forceinline__ DecodeItem attn_decode_item(const AttnParams& p, int 
         // three raw steps in flight, each widened right before its MFMAs
         auto rload = [&](KVRaw<D>& r, int sidx) {
           const int u0 = seg_base + sidx * 32;
-          const int page = bt[u0 / p.bs];
+          const int page = bt_entry(bt, u0 / p.bs);
           const size_t hb = ((size_t)page * p.nkv + kvh) * head_stride;
           attn_load_raw<D>(r, p.k_cache, p.v_cache, hb, u0 % p.bs);
         };
@@ -403,7 +414,7 @@ __device__ __forceinline__ DecodeItem attn_decode_item(const AttnParams& p, int 
         qs[c] = col_valid ? *reinterpret_cast<const bf16x8*>(qsrow + q_dofs<D, FP8>(c, h4)) : zero8();
       const int nS = min(p.n_sink, L);
       for (int u0 = 0; u0 < nS; u0 += 32) {
-        const int page = bt[u0 / p.bs];
+        const int page = bt_entry(bt, u0 / p.bs);
         const size_t hb = ((size_t)page * p.nkv + kvh) * head_stride;
         unsigned vm = 0;
 #pragma unroll
