@@ -35,10 +35,16 @@ extern __shared__ __attribute__((aligned(16))) char gemv_lds[];
 // row (and the norm weight) are loaded in one burst and kept in registers through the reduction --
 // one L2 round trip instead of the generic loop's one per vector and a second pass for w.  Same
 // vector assignment and fma order as the generic loop, so the same bits.
-template <int M>
+//
+// `issue` (the caller's first weight group, which does not depend on x) runs right after the
+// prologue's own loads: vmcnt retires loads in order, so a weight group issued BEFORE them would
+// have to land before the norm could start (measured: at 8 k-steps per group the fused-norm
+// GEMVs ran 30-40 % slower, profiles/r4/gemv_unroll8_ab.txt); issued after, it stays in flight
+// through the reduction.
+template <int M, typename F>
 __device__ __forceinline__ void gemv_norm_prologue_regs(const bf16* __restrict__ x,
                                                         const GemvNorm& nm, int K,
-                                                        float* scratch) {
+                                                        float* scratch, F&& issue) {
   constexpr int VPT = 4;
   const int nvec = K >> 3;
   bf16x8* xs = reinterpret_cast<bf16x8*>(gemv_lds);
@@ -54,6 +60,9 @@ __device__ __forceinline__ void gemv_norm_prologue_regs(const bf16* __restrict__
       if (nm.res_in != nullptr)
         rv[m][i] = reinterpret_cast<const bf16x8*>(nm.res_in + (size_t)m * K)[row_vec_idx(i, nvec)];
     }
+  __builtin_amdgcn_sched_barrier(0);
+  issue();
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     bf16x8* ro = nm.res_out ? reinterpret_cast<bf16x8*>(nm.res_out + (size_t)m * K) : nullptr;
@@ -86,15 +95,16 @@ __device__ __forceinline__ void gemv_norm_prologue_regs(const bf16* __restrict__
   __syncthreads();
 }
 
-template <int M>
+template <int M, typename F>
 __device__ __forceinline__ void gemv_norm_prologue(const bf16* __restrict__ x, const GemvNorm& nm,
-                                                   int K) {
+                                                   int K, F&& issue) {
   __shared__ float scratch[8];
   const int nvec = K >> 3;
   if (nvec <= 4 * (int)blockDim.x) {
-    gemv_norm_prologue_regs<M>(x, nm, K, scratch);
+    gemv_norm_prologue_regs<M>(x, nm, K, scratch, issue);
     return;
   }
+  issue();
   bf16* xs = reinterpret_cast<bf16*>(gemv_lds);
   const bf16x8* w8 = reinterpret_cast<const bf16x8*>(nm.w);
 #pragma unroll
@@ -152,13 +162,17 @@ __global__ void __launch_bounds__(256) skinny_gemm_kernel(const bf16* __restrict
       wv[u][r] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(wrow[r] + k))
                        : bf16x8{};
   };
+
   const int kfirst = lane * 8;
   if constexpr (NORM) {
     // the first k-group of weights does not depend on x: in flight during the norm prologue
     // (only here: with x from global memory the per-step weight / x interleave below is faster)
+    // (the unconditional-load form of skinny_gemm_fp8_kernel's load_w_pre measured -0.4 % on
+    // the bf16 batch-1 step, profiles/r4/gemv_prologue_ab.txt: not used here)
+    gemv_norm_prologue<M>(x_in, nm, K, [&] {   // every thread, before any exit
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) load_w(u, kfirst + u * kStep);
-    gemv_norm_prologue<M>(x_in, nm, K);   // every thread, before any exit
+      for (int u = 0; u < kUnroll; ++u) load_w(u, kfirst + u * kStep);
+    });
   }
   const bf16* x = NORM ? reinterpret_cast<const bf16*>(gemv_lds) : x_in;
   if ((EP != kEpPlain ? 2 * wave : n0) >= N) return;
@@ -240,13 +254,26 @@ __global__ void __launch_bounds__(256) skinny_gemm_fp8_kernel(const void* __rest
       wv[u][r] = k < K ? __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(wrow[r] + k))
                        : u32x4n{0u, 0u, 0u, 0u};
   };
+  // the weight group issued during the norm prologue: loads past the row end (k >= K, only when
+  // K is not a multiple of the group) re-read the row's last 16 bytes instead of branching around
+  // the load, so every load is unconditional and hipcc counts the prologue's vmcnt waits (with
+  // exec-masked loads it waited for the whole group: measured 30-40 % slower fused-norm GEMVs at
+  // 8 k-steps per group).  Their x is zero, so they add exact zeros (finite weights).  The loop's
+  // own loads keep the branch: its interleaved schedule measured faster (O 13.2 vs 15.0 us).
+  auto load_w_pre = [&](int u, int k) {
+    const int kc = k < K ? k : K - 16;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r)
+      wv[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4n*>(wrow[r] + kc));
+  };
   const int kfirst = lane * 16;
   if constexpr (NORM) {
     // the first k-group of weights does not depend on x: in flight during the norm prologue
     // (only here: with x from global memory the per-step weight / x interleave below is faster)
+    gemv_norm_prologue<M>(static_cast<const bf16*>(x_in), nm, K, [&] {
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) load_w(u, kfirst + u * kStep);
-    gemv_norm_prologue<M>(static_cast<const bf16*>(x_in), nm, K);
+      for (int u = 0; u < kUnroll; ++u) load_w_pre(u, kfirst + u * kStep);
+    });
   }
   const void* xv_ = NORM ? static_cast<const void*>(gemv_lds) : x_in;
   if ((EP != kEpPlain ? 2 * wave : n0) >= N) return;
