@@ -62,6 +62,10 @@ def parse():
                     help="LLM.int8 weights (the reference's 8-bit mode: int8 MFMA + bf16 outliers)")
     ap.add_argument("--kv-fp8", action="store_true", help="fp8-e4m3 KV cache")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--num-layers", type=int, default=0,
+                    help="REHEARSAL ONLY: the model's width with this many layers (e.g. 16 = 2 per "
+                         "stage at PP=8, so 8 ranks x 9 micro-batches x 512 rows fit one GPU); the "
+                         "result names the reduced model and is not a headline number")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -103,8 +107,10 @@ def _rank_record(node, rank: int, window_s: float) -> dict:
     rec.update({"stage": [ex.stage.start, ex.stage.end], "device": str(ex.device)})
     rec.update(node.tr.describe())
     if len(node.snapshots) >= 2:
+        from distributed_llm_inference.runtime.hostclock import per_step
         d = snapshot_delta(node.snapshots[-2], node.snapshots[-1])
         n = max(int(d.get("steps", 0)), 1)
+        rec.update(per_step(d, n))
         rec.update({
             "mb_steps": int(d.get("steps", 0)),
             "device_ms_per_mb_step": round(d.get("device_ms", 0.0) / n, 3),
@@ -141,10 +147,21 @@ def main():
         dist.init_process_group("gloo")
         dist.barrier()
     spec = resolve_model(a.model)
+    model = a.model
+    if a.num_layers:
+        # host-path rehearsal at the real width / row count with fewer layers (never a headline)
+        spec = spec.replace(num_layers=a.num_layers, name=f"{spec.name}-{a.num_layers}L")
+        model = spec
     M = a.micro_batches or (pp + 1 if pp > 1 else 1)
-    total_len = a.prompt_len + a.warmup + a.steps + 72
+    G = M * a.batch_per_mb
+    # sequences prefilled in the first prefill round keep decoding through the remaining ones
+    # (each round admits up to M x max_batched_tokens prompt tokens): none may reach max_tokens
+    # before the end of the timed window
+    prefill_rounds = -(-G * a.prompt_len // (M * a.max_batched_tokens))
+    max_tokens = a.warmup + a.steps + 64 + prefill_rounds
+    total_len = a.prompt_len + max_tokens + 8
     cfg = EngineConfig(
-        model=a.model, random_init=True, seed=0, quantize="int8" if a.int8 else a.fp8, pp=pp, dp=dp,
+        model=model, random_init=True, seed=0, quantize="int8" if a.int8 else a.fp8, pp=pp, dp=dp,
         cache=CacheConfig(block_size=64, gpu_memory_utilization=0.92,
                           dtype="fp8" if a.kv_fp8 else "bf16"),
         serve=ServeConfig(max_batch_size=a.batch_per_mb, max_num_batched_tokens=a.max_batched_tokens,
@@ -184,10 +201,8 @@ def main():
 
     init_s = time.perf_counter() - t_init
     rng = random.Random(1234 + 7919 * getattr(drv, "replica", 0))
-    G = M * a.batch_per_mb
-    # generous max_tokens: sequences prefilled early keep decoding during the remaining prefill
-    # rounds, and none may finish inside the timed window (constant batch)
-    params = SamplingParams(max_tokens=a.warmup + a.steps + 64, ignore_eos=True)
+    # generous max_tokens (above): none may finish inside the timed window (constant batch)
+    params = SamplingParams(max_tokens=max_tokens, ignore_eos=True)
     seqs = [Sequence([rng.randrange(spec.vocab_size) for _ in range(a.prompt_len)], params)
             for _ in range(G)]
     for s in seqs:
@@ -211,12 +226,15 @@ def main():
     for s in seqs:
         s.token_times.clear()
     _progress(f"timed: {a.steps} steps")
+    from distributed_llm_inference.runtime.hostclock import HOST, per_step
+    h0 = HOST.snapshot()
     t0 = time.perf_counter()
     w0 = drv.wait_s
     for _ in range(a.steps):
         drv.round()
     drv.barrier()
     t1 = time.perf_counter()
+    h1 = HOST.snapshot()
     _progress(f"timed window {t1 - t0:.2f}s")
     sync_replicas()
     driver_busy = (t1 - t0) - (drv.wait_s - w0)
@@ -255,7 +273,8 @@ def main():
         "dtype": ("int8-weights/bf16-act" if a.int8 else "fp8-weights/bf16-act" if a.fp8 else "bf16")
                  + ("/fp8-kv" if a.kv_fp8 else ""),
         "data": f"synthetic (random-init {spec.name} weights, random prompt tokens)",
-        "config": {"model": "Llama-3-70B" if a.model == "llama-3-70b" else a.model,
+        "config": {"model": "Llama-3-70B" if (a.model == "llama-3-70b" and not a.num_layers)
+                   else spec.name,
                    "global_batch": G * dp, "seq_len": total_len,
                    "parallelism": f"pp{pp}" if dp == 1 else f"dp{dp}xpp{pp}"},
         "p50_token_latency_ms": round(p50, 3),
@@ -268,6 +287,8 @@ def main():
         "prefill_s": round(prefill_s, 3),
         # host time of the driver rank per micro-batch step NOT spent waiting for results
         "driver_host_ms_per_mb_step": round(driver_busy / (a.steps * M) * 1e3, 3),
+        # ... and by phase (runtime/hostclock.py; waits on the device / token channel apart)
+        "driver_host_phases": per_step({k: h1[k] - h0.get(k, 0.0) for k in h1}, a.steps * M),
         "replicas": dp, "stages_per_replica": pp,
         "init_s": round(init_s, 1),
         "kv_blocks": int(drv.sched.total_blocks),
@@ -280,7 +301,10 @@ def main():
         if fb:   # the data plane is NOT RCCL: say so at the top level, not only per rank
             res["transport_fallback_from"] = fb
         res["per_rank"] = per_rank
-    if a.model != "llama-3-70b":
+    if a.num_layers:
+        res["rehearsal"] = f"{a.num_layers} of {resolve_model(a.model).num_layers} layers"
+        res["vs_baseline"] = None
+    if a.model != "llama-3-70b" or a.num_layers:
         # the headline metric names its model; a run of another model says what it measured
         res["metric"] = (f"output tokens/sec (whole node) + p50 token latency, "
                          f"{res['config']['model']} PP={pp}")

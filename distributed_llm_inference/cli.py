@@ -121,7 +121,7 @@ def cmd_block_serve(a) -> int:
         from .config import resolve_model
         from .server.registry import RegistryClient
         spec = resolve_model(a.checkpoint or a.model)
-        registry = RegistryClient(a.registry)
+        registry = RegistryClient(a.registry, token=a.registry_token)
         url = a.public_url or f"http://{a.host}:{a.port}"
         start, end = registry.claim(spec.name, spec.num_layers,
                                     a.max_layers or spec.num_layers, url)
@@ -142,7 +142,7 @@ def cmd_registry(a) -> int:
     """The block registry (server/registry.py): block servers claim layers, clients find chains."""
     from .server.registry import serve_registry
     logging.basicConfig(level=logging.WARNING)
-    serve_registry(a.host, a.port)
+    serve_registry(a.host, a.port, token=a.token)
     return 0
 
 
@@ -280,6 +280,8 @@ def main(argv: Optional[List[str]] = None) -> int:
                     help="block registry URL: claim the least-served layers instead of --start/--end")
     bs.add_argument("--max-layers", type=int, default=None,
                     help="with --registry: most layers this server holds (default: all)")
+    bs.add_argument("--registry-token", default=None,
+                    help="shared secret of a registry started with --token")
     bs.add_argument("--public-url", default=None,
                     help="with --registry: URL clients reach this server at (default http://host:port)")
     bs.add_argument("--layers-per-block", type=int, default=None)
@@ -293,6 +295,9 @@ def main(argv: Optional[List[str]] = None) -> int:
     rg = sub.add_parser("registry", help="block registry: servers claim layer ranges, clients find chains")
     rg.add_argument("--host", default="127.0.0.1")
     rg.add_argument("--port", type=int, default=8099)
+    rg.add_argument("--token", default=None,
+                    help="shared secret required by /claim, /announce and /withdraw (Bearer); "
+                         "without it the registry must only be reachable from a trusted network")
     w = sub.add_parser("worker", help=argparse.SUPPRESS)
     _common(w)
     _gen_args(w)

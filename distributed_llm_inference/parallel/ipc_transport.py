@@ -230,7 +230,7 @@ class IpcTransport(Transport):
             out[c.describe()] = {"issued": c.n, **dev}
         return out
 
-    fallback_from = ""   # set by make_transport when the agreed RCCL bring-up failed
+    fallback_from = ""   # set by make_transport: why the default kind took IPC (a shared GPU)
 
     def describe(self) -> dict:
         d = {"transport": "IpcTransport",

@@ -39,6 +39,7 @@ import torch.distributed as dist
 
 from ..runtime.executor import StageExecutor, StepPlan
 from ..runtime.faults import FaultInjector, StageStats
+from ..runtime.hostclock import HOST
 from ..runtime.scheduler import Scheduler
 from ..runtime.sequence import SamplingParams, Sequence as Seq
 from ..runtime.watchdog import TRACKER, abort_job, wait_event
@@ -64,6 +65,7 @@ class DriverBase:
         self.collect_times: Dict[int, List[float]] = collections.defaultdict(list)
         self.tokens_generated = 0
         self.wait_s = 0.0  # host time blocked on results (the rest of a round is driver work)
+        self._tok_wait_ms = 0.0  # of the current _collect: blocked on the tokens
         self.streams = None  # runtime.streams.RankStreams of a multi-process rank
 
     def activate_streams(self) -> None:
@@ -86,12 +88,16 @@ class DriverBase:
     def _collect_front(self) -> None:
         p = self.inflight.popleft()
         t0 = time.perf_counter()
+        self._tok_wait_ms = 0.0
         toks = self._collect(p)
         now = time.perf_counter()
         self.wait_s += now - t0
         self.collect_times[p.mb].append(now)
         self.tokens_generated += len(toks)
         self.sched.on_tokens(p.mb, toks, now)
+        # host phases (runtime/hostclock.py): blocked on the tokens vs reading / applying them
+        HOST.add("tokens_wait", self._tok_wait_ms)
+        HOST.add("tokens", (time.perf_counter() - t0) * 1e3 - self._tok_wait_ms)
 
     def round(self) -> bool:
         """Give every micro-batch one step (collecting results as needed).  Returns False when
@@ -100,7 +106,9 @@ class DriverBase:
         for mb in range(self.sched.M):
             while self.sched.inflight[mb] is not None:
                 self._collect_front()
+            t0 = time.perf_counter()
             plan = self.sched.plan(mb)
+            HOST.since("plan", t0)
             if plan is None:
                 continue
             self._issue(plan)
@@ -192,7 +200,9 @@ class LocalPipeline(DriverBase):
     def _collect(self, plan: StepPlan) -> List[int]:
         pinned, ev = self._results.pop(plan.step)
         if ev is not None:
+            t0 = time.perf_counter()
             ev.synchronize()
+            self._tok_wait_ms += (time.perf_counter() - t0) * 1e3
         return pinned.tolist()
 
     def _broadcast_control(self, kind: str) -> None:
@@ -267,37 +277,47 @@ class DistributedDriver(DriverBase):
         self._head_results[plan.step] = (pinned, ev)
 
     def _issue(self, plan: StepPlan) -> None:
+        t = time.perf_counter()
         TRACKER.mark("ctrl-send", plan.step, plan.mb)
         self.ch.ctrl.send(msgpack.packb(plan.to_wire()), self.timeout)
+        t = HOST.since("ctrl", t)
         if plan.seq_ids and self.faults.active:
             self.faults.on_step()
         tok = self.stats.begin(self.faults.delay_ms) if plan.seq_ids else None
         TRACKER.mark("execute", plan.step, plan.mb, stream="compute")
-        out = self.ex.execute(plan, None)
+        out = self.ex.execute(plan, None)   # charges stage / staging_wait / launch itself
         self.stats.end(tok)
+        t = time.perf_counter()
         if plan.seq_ids:
             _device_mark(self.ex, "compute", plan.step)
             TRACKER.mark("send", plan.step, plan.mb, peer=1, stream="send")
             self.tr.send(out, 1)
             _device_mark(self.ex, "send", plan.step)
+            t = HOST.since("send", t)
             if self.heads is not None:
                 self.heads.tick()
                 if self._head_rank(plan) == 0:
                     self.heads.submit(plan)
         if self.heads is not None:
             self.heads.poll()
+            HOST.since("head", t)
 
     def _collect(self, plan: StepPlan) -> List[int]:
         hr = self._head_rank(plan)
         TRACKER.mark("collect", plan.step, plan.mb, peer=hr)
         if hr == 0:
+            t0 = time.perf_counter()
             while plan.step not in self._head_results:
                 self.heads.poll(block=True)   # (enqueues any deferred GPU job first)
             pinned, ev = self._head_results.pop(plan.step)
             wait_event(ev, "local head tokens", plan.step, plan.mb)
+            self._tok_wait_ms += (time.perf_counter() - t0) * 1e3
             return pinned.tolist()
+        t0 = time.perf_counter()
         with TRACKER.waiting("tokens", plan.step, plan.mb, peer=hr):
-            msg = msgpack.unpackb(self.ch.toks.get(hr, self.ch.tok).recv(self.timeout))
+            raw = self.ch.toks.get(hr, self.ch.tok).recv(self.timeout)
+        self._tok_wait_ms += (time.perf_counter() - t0) * 1e3
+        msg = msgpack.unpackb(raw)
         if msg["step"] != plan.step:
             raise RuntimeError(f"token stream of rank {hr} out of order: got step {msg['step']}, "
                                f"want {plan.step}")
@@ -423,7 +443,10 @@ class StageFollower:
 
     def _run(self) -> None:
         while True:
-            msg = msgpack.unpackb(self._next_msg())
+            t = time.perf_counter()
+            raw = self._next_msg()
+            t = HOST.since("ctrl_wait", t)
+            msg = msgpack.unpackb(raw)
             kind = msg.get("kind", "run")
             if kind == "stop":
                 break
@@ -438,6 +461,7 @@ class StageFollower:
                 self.snapshots.append(self.stats.snapshot())
                 continue
             plan = StepPlan.from_wire(msg)
+            t = HOST.since("unpack", t)
             if not plan.seq_ids:
                 self.ex.execute(plan, None)  # frees only
                 continue
@@ -446,12 +470,14 @@ class StageFollower:
             TRACKER.mark("recv", plan.step, plan.mb, peer=self.rank - 1, stream="recv")
             x = self.tr.recv(buf, self.rank - 1, free_event=free_ev)
             _device_mark(self.ex, "recv", plan.step)
+            HOST.since("recv", t)
             if self.faults.active:
                 self.faults.on_step()
             tok = self.stats.begin(self.faults.delay_ms)
             TRACKER.mark("execute", plan.step, plan.mb, stream="compute")
             out = self.ex.execute(plan, x, project=(hr == self.rank))
             self.stats.end(tok)
+            t = time.perf_counter()
             self._release_slot()
             _device_mark(self.ex, "compute", plan.step)
             if self.is_last:
@@ -470,8 +496,10 @@ class StageFollower:
                     self.heads.tick()
                     if hr == self.rank:
                         self.heads.submit(plan)
+            t = HOST.since("send", t)
             if self.heads is not None:
                 self.heads.poll()
+                HOST.since("head", t)
         if self.heads is not None:
             self.heads.drain()
         if self._pub_thread is not None:
@@ -497,25 +525,70 @@ def _device_mark(ex, role: str, step: int) -> None:
     TRACKER.device_mark(role, step, stream)
 
 
+def device_identity(device: torch.device) -> str:
+    """A string naming the physical device ``device`` is on, equal for two processes exactly when
+    they drive the same GPU: host name + PCI domain:bus:device + the device UUID (CPU ranks: the
+    host and process)."""
+    import socket
+    host = socket.gethostname()
+    if device.type != "cuda":
+        return f"{host}/cpu/{os.getpid()}"
+    p = torch.cuda.get_device_properties(device)
+    return f"{host}/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}/{p.uuid}"
+
+
+def choose_data_plane(kind: str, device_ids: Sequence[str]) -> tuple:
+    """``(plane, reason)`` for a ``DLI_TRANSPORT`` kind and every stage's :func:`device_identity`.
+
+    ``rccl-or-ipc`` (the default) is RCCL whenever every stage has a GPU of its own - then an RCCL
+    failure fails the job loudly, it never silently becomes another transport - and the IPC device
+    transport only when two stages share a GPU (RCCL refuses two ranks on one device; that is the
+    one-GPU rehearsal of a pipeline).  Every other kind is taken as given: ``rccl`` (strict),
+    ``rccl-or-host`` (RCCL, agreed fallback to host staging), ``ipc``, ``host``."""
+    if kind != "rccl-or-ipc":
+        return kind, ""
+    seen: Dict[str, List[int]] = collections.defaultdict(list)
+    for r, d in enumerate(device_ids):
+        seen[d].append(r)
+    shared = [rs for rs in seen.values() if len(rs) > 1]
+    if shared:
+        return "ipc", f"stages share a GPU (ranks {shared}): RCCL needs one device per rank"
+    return "rccl", ""
+
+
+def _exchange_device_ids(store, key: str, rank: int, world: int, device: torch.device,
+                         timeout_s: float) -> List[str]:
+    store.set(f"{key}/{rank}", device_identity(device))
+    keys = [f"{key}/{r}" for r in range(world)]
+    deadline = time.monotonic() + timeout_s
+    while not all(_store_has(store, k) for k in keys):
+        if time.monotonic() > deadline:
+            missing = [r for r, k in enumerate(keys) if not _store_has(store, k)]
+            raise TransportInitError(f"[rank {rank}] ranks {missing} never published their "
+                                     f"device within {timeout_s:.0f} s")
+        time.sleep(0.002)
+    return [store.get(k).decode() for k in keys]
+
+
 def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
                    rccl_timeout_s: float = 120.0, rank_offset: int = 0,
                    head_pairs: bool = False, streams=None, max_bytes: int = 0,
                    head_bytes: int = 0) -> Transport:
-    """RCCL P2P on GPUs (default); ``DLI_TRANSPORT=ipc`` moves hidden states GPU-side through
-    cross-process device memory with spinning device waits (parallel/ipc_transport.py: several
-    ranks sharing one GPU, with the production stream structure and the rotating head);
-    ``DLI_TRANSPORT=host`` stages GPU tensors through gloo (an explicit opt-in, never chosen
-    silently); gloo on CPU.  ``streams``: the rank's runtime.streams.RankStreams.
+    """The data plane of one pipeline replica (``DLI_TRANSPORT``, see :func:`choose_data_plane`):
 
-    RCCL initialisation is agreed on by all ranks: every rank publishes whether its communicators
-    came up (a failure or a peer that never arrives ends in a timeout, not a hang), and if ANY rank
-    failed, EVERY rank raises :class:`TransportInitError` with the failing ranks and the error, so
-    a multi-GPU run either moves hidden states over RCCL or exits non-zero.
-    ``DLI_TRANSPORT=rccl-or-host`` restores the old agreed fallback to the host-staged transport.
-    With ``DLI_TRANSPORT`` unset (``rccl-or-ipc``) an agreed RCCL failure falls back to the IPC
-    device transport instead (same stream structure, rotating head, device-side waits; hidden
-    states cross xGMI as peer-memory copies), announced on stderr and in ``describe()`` — an
-    explicit ``DLI_TRANSPORT=rccl`` keeps the strict fail-loud behaviour.
+    * RCCL P2P on GPUs, one 2-rank communicator per stage pair (+ head pairs) — the production
+      path whenever every stage has its own GPU;
+    * the IPC device transport (parallel/ipc_transport.py: cross-process device memory with
+      spinning device waits, the production stream structure and the rotating head) when stages
+      share a GPU — chosen by comparing every rank's published PCI device, never as the fallback of
+      a failed RCCL bring-up on distinct GPUs;
+    * host staging through gloo (``DLI_TRANSPORT=host`` / ``rccl-or-host``, explicit opt-ins);
+    * gloo on the CPU (tests).
+
+    RCCL initialisation is agreed on by all ranks (:func:`_agree`): every rank publishes whether
+    its communicators came up (a failure or a peer that never arrives ends in a timeout, not a
+    hang), and if ANY rank failed, EVERY rank raises :class:`TransportInitError` with the failing
+    ranks and the error (``rccl-or-host``: every rank switches to host staging instead).
 
     ``rank`` / ``world`` are the stage index and stage count of ONE pipeline replica; with several
     replicas (data parallel) ``rank_offset`` is the replica's first global rank and ``job`` names
@@ -524,85 +597,116 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
         return LoopbackTransport(1)
     from .transport import transport_kind
     kind = transport_kind(device)
-    if kind == "rccl-or-ipc" and max_bytes <= 0:
-        kind = "rccl"   # no message size to size the IPC channels with: strict RCCL
-    if device.type == "cuda" and kind == "ipc":
-        from ..runtime.faults import raw_store
-        from .ipc_transport import IpcTransport
-        if streams is None:
-            from ..runtime.streams import rank_streams
-            streams = rank_streams(device)
+    if kind == "gloo":
+        return TorchDistTransport(rank_offset=rank_offset)
+    from ..runtime.faults import raw_store
+    if kind == "rccl-or-ipc":
+        ids = _exchange_device_ids(raw_store(), f"dli_dev_{job}", rank, world, device,
+                                   rccl_timeout_s)
+        kind, why = choose_data_plane(kind, ids)
+        if kind == "ipc" and max_bytes <= 0:
+            raise ValueError(f"{why}; the IPC transport needs the largest message size (max_bytes)")
+        if kind == "ipc":
+            print(f"[rank {rank}] data plane: IPC device transport ({why})", file=sys.stderr,
+                  flush=True)
+            tr = _ipc(raw_store(), rank, world, device, streams, max_bytes, head_bytes, job,
+                      head_pairs)
+            tr.fallback_from = why
+            return tr
+    if kind == "ipc":
         if max_bytes <= 0:
             raise ValueError("DLI_TRANSPORT=ipc needs the largest message size (max_bytes)")
-        return IpcTransport(raw_store(), rank, world, device, streams, max_bytes, head_bytes,
-                            prefix=f"dli_ipc_{job}", head_pairs=head_pairs)
-    if device.type == "cuda" and kind in ("rccl", "rccl-or-host", "rccl-or-ipc"):
-        from ..runtime.faults import raw_store
-        store = raw_store()
-        prefix = f"dli_rccl_{job}"
-        tr, err = None, ""
-        try:
-            tr = RcclTransport(store, rank, world, device, prefix=prefix, timeout_s=rccl_timeout_s,
-                               head_pairs=head_pairs, streams=streams)
-        except Exception as e:  # noqa: BLE001 - reported and agreed on below
-            err = repr(e)
-            store.set(f"{prefix}/err/{rank}", err[:2000])
-            store.set(f"{prefix}/failed", f"rank {rank}: {err[:500]}")   # peers stop early
-        store.set(f"{prefix}/ok/{rank}", "1" if tr is not None else "0")
-        ok = _agree(store, prefix, world, rank, rccl_timeout_s)
-        if all(ok):
-            return tr
-        if tr is not None:
-            tr.abort()
-        bad = [r for r, o in enumerate(ok) if not o]
-        errs = {r: store.get(f"{prefix}/err/{r}").decode(errors="replace") for r in bad
-                if r != rank and _store_has(store, f"{prefix}/err/{r}")}
-        if err:
-            errs[rank] = err
-        msg = (f"[rank {rank}] RCCL transport unavailable: communicators failed on ranks {bad}"
-               f" (device {device}, HSA_ENABLE_IPC_MODE_LEGACY="
-               f"{os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '<unset>')}); errors: {errs}")
-        print(msg, file=sys.stderr, flush=True)
-        if kind == "rccl-or-ipc":
-            print(f"[rank {rank}] falling back to the IPC device transport (agreed by every rank)",
-                  file=sys.stderr, flush=True)
-            from .ipc_transport import IpcTransport
-            if streams is None:
-                from ..runtime.streams import rank_streams
-                streams = rank_streams(device)
-            tr = IpcTransport(store, rank, world, device, streams, max_bytes, head_bytes,
-                              prefix=f"dli_ipc_{job}", head_pairs=head_pairs)
-            tr.fallback_from = f"RcclTransport failed on ranks {bad}"
-            return tr
-        if kind != "rccl-or-host":
-            raise TransportInitError(msg)
-        log.warning(msg + "; DLI_TRANSPORT=rccl-or-host: falling back to host-staged transport")
+        return _ipc(raw_store(), rank, world, device, streams, max_bytes, head_bytes, job,
+                    head_pairs)
+    if kind == "host":
         from .transport import HostStagedTransport
         return HostStagedTransport(rank_offset=rank_offset)
-    if device.type == "cuda":   # kind == "host" (transport_kind validated it)
-        from .transport import HostStagedTransport
-        return HostStagedTransport(rank_offset=rank_offset)
-    return TorchDistTransport(rank_offset=rank_offset)
+    # kind in ("rccl", "rccl-or-host")
+    store = raw_store()
+    prefix = f"dli_rccl_{job}"
+    tr, err = None, ""
+    try:
+        tr = RcclTransport(store, rank, world, device, prefix=prefix, timeout_s=rccl_timeout_s,
+                           head_pairs=head_pairs, streams=streams)
+    except Exception as e:  # noqa: BLE001 - reported and agreed on below
+        err = repr(e)
+        store.set(f"{prefix}/err/{rank}", err[:2000])
+        store.set(f"{prefix}/failed", f"rank {rank}: {err[:500]}")   # peers stop early
+    mine = _publish_ok(store, f"{prefix}/ok/{rank}", tr is not None)
+    if not mine and tr is not None:   # declared dead by a peer's deadline before answering
+        store.set(f"{prefix}/failed", f"rank {rank}: answered after the agreement deadline")
+    ok = _agree(store, prefix, world, rank, rccl_timeout_s)
+    if all(ok):
+        return tr
+    if tr is not None:
+        tr.abort()
+    bad = [r for r, o in enumerate(ok) if not o]
+    errs = {r: store.get(f"{prefix}/err/{r}").decode(errors="replace") for r in bad
+            if r != rank and _store_has(store, f"{prefix}/err/{r}")}
+    if err:
+        errs[rank] = err
+    msg = (f"[rank {rank}] RCCL transport unavailable: communicators failed on ranks {bad}"
+           f" (device {device}, HSA_ENABLE_IPC_MODE_LEGACY="
+           f"{os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '<unset>')}); errors: {errs}")
+    print(msg, file=sys.stderr, flush=True)
+    if kind != "rccl-or-host":
+        raise TransportInitError(msg)
+    log.warning(msg + "; DLI_TRANSPORT=rccl-or-host: falling back to host-staged transport")
+    from .transport import HostStagedTransport
+    return HostStagedTransport(rank_offset=rank_offset)
+
+
+def _ipc(store, rank, world, device, streams, max_bytes, head_bytes, job, head_pairs):
+    from .ipc_transport import IpcTransport
+    if streams is None:
+        from ..runtime.streams import rank_streams
+        streams = rank_streams(device)
+    return IpcTransport(store, rank, world, device, streams, max_bytes, head_bytes,
+                        prefix=f"dli_ipc_{job}", head_pairs=head_pairs)
+
+
+def _publish_ok(store, key: str, ok: bool) -> bool:
+    """Publish this rank's bring-up outcome unless a peer already declared it failed (a
+    ``compare_set`` on the missing key, see :func:`_agree`); returns the value that stands."""
+    return _compare_set(store, key, "1" if ok else "0") == b"1"
+
+
+def _compare_set(store, key: str, value: str) -> bytes:
+    """Set ``key`` to ``value`` if it does not exist; returns the value the key holds."""
+    return bytes(store.compare_set(key, "", value))
 
 
 def _agree(store, prefix: str, world: int, rank: int, timeout_s: float) -> List[bool]:
-    """Every rank's RCCL bring-up outcome, as soon as it is decided: all ranks answered ok, or
-    any rank published a failure (then the ranks that have not answered count as failed: they
-    are stuck on the failed peer or dead, and will see the failure key themselves).  A rank
-    that answers nothing at all within ``timeout_s`` is declared failed here (and published, so
-    every rank decides the same)."""
+    """Every rank's RCCL bring-up outcome; every rank decides the same.
+
+    * no failure published and every rank answered: their answers;
+    * a failure published (by a failing rank, or by a rank whose deadline passed): each rank that
+      has not answered is declared failed with a ``compare_set`` of its key to "0" - whichever
+      of that and the rank's own ``compare_set`` comes first stands, for every reader, so a late
+      rank can never turn "1" after another rank decided without it."""
     fail_key = f"{prefix}/failed"
     keys = [f"{prefix}/ok/{r}" for r in range(world)]
     deadline = time.monotonic() + timeout_s
+    failed_at: Optional[float] = None
     while True:
-        if all(_store_has(store, k) for k in keys):
-            return [store.get(k) == b"1" for k in keys]
-        if _store_has(store, fail_key):
-            return [_store_has(store, k) and store.get(k) == b"1" for k in keys]
+        if failed_at is None and _store_has(store, fail_key):
+            failed_at = time.monotonic()
+        # after a failure, live ranks answer within milliseconds (their bring-up stops at the
+        # published failure): give them a short grace so the reported set is the ranks that
+        # really failed, then settle every missing answer as failed - sticky, the same everywhere
+        if failed_at is not None and (all(_store_has(store, k) for k in keys)
+                                      or time.monotonic() - failed_at > min(timeout_s, 5.0)):
+            return [_compare_set(store, k, "0") == b"1" for k in keys]
+        if failed_at is None and all(_store_has(store, k) for k in keys):
+            vals = [store.get(k) == b"1" for k in keys]
+            if all(vals):
+                return vals
+            # a "0" is always preceded by its rank's failure key: decide on the sticky path
+            continue
         if time.monotonic() > deadline:
             missing = [r for r, k in enumerate(keys) if not _store_has(store, k)]
-            store.set(fail_key, f"rank {rank}: ranks {missing} never answered")
             store.set(f"{prefix}/err/{missing[0]}", f"no answer within {timeout_s:.0f} s")
+            store.set(fail_key, f"rank {rank}: ranks {missing} never answered")
         time.sleep(0.002)
 
 

@@ -14,6 +14,11 @@ link, so the MI355X-native transport is RCCL point-to-point:
   multi-process CPU tests).
 * :class:`LoopbackTransport` — all stages in one process (tests, single-GPU PP rehearsal):
   a stream-ordered hand-off through a per-pair queue.
+
+:class:`RcclTransport` also runs host-synchronously on CPU tensors (stream handle 0, no events):
+that is how its data path - pair and head communicators, peer indices inside each 2-rank pair,
+the connect plan - is exercised end to end by the CPU tests with a simulated communicator
+(``tests/test_rccl_dataplane_cpu.py``), since a one-GPU box cannot run two RCCL ranks.
 """
 from __future__ import annotations
 
@@ -194,6 +199,21 @@ def connect_plan(rank: int, world: int, head_pairs: bool) -> List[tuple]:
     return ops
 
 
+class _HostRecv:
+    """Deferred host-synchronous receive (the CPU path's stand-in for a gloo ``Work``)."""
+
+    def __init__(self, fn):
+        self._fn, self._done = fn, False
+
+    def is_completed(self) -> bool:
+        return self._done
+
+    def wait(self) -> None:
+        if not self._done:
+            self._fn()
+            self._done = True
+
+
 class RcclTransport(Transport):
     """RCCL P2P over xGMI with dedicated send/recv streams (see module docstring)."""
 
@@ -206,6 +226,7 @@ class RcclTransport(Transport):
         from ..runtime.streams import rank_streams
         C = ops.native()
         self.rank, self.world, self.device = rank, world, device
+        self._gpu = device.type == "cuda"   # CPU: host-synchronous (simulated communicators)
         # dedicated streams (hardware queues of their own: runtime/streams.py), shared with the
         # rank's HeadJobs / executor so every role exists exactly once per process
         streams = streams or rank_streams(device)
@@ -214,7 +235,8 @@ class RcclTransport(Transport):
         self._rccl_version = int(C.rccl_version())
         self._timing = os.environ.get("DLI_STAGE_TIMING", "0") == "1"
         self._waits: collections.deque = collections.deque()
-        dev_idx = device.index if device.index is not None else torch.cuda.current_device()
+        dev_idx = (-1 if not self._gpu else
+                   device.index if device.index is not None else torch.cuda.current_device())
         # pair (i, i+1): the lower rank creates the id; both ends create a 2-rank communicator.
         # (sampled tokens return to the driver over the shm control plane, so no ring closure).
         # rotating LM head: one more 2-rank communicator between the last stage and every other
@@ -294,13 +316,21 @@ class RcclTransport(Transport):
         rank 0 upwards without a cycle."""
         t0 = time.perf_counter()
         probe = torch.zeros(64, dtype=torch.bfloat16, device=self.device)
+        if not self._gpu:   # host-synchronous: each probe completes before the next is issued
+            for op, kind, peer in connect_plan(self.rank, self.world, bool(self._hcomms)):
+                comm = self._comm(peer) if kind == "stage" else self._hcomms[peer]
+                if op == "send":
+                    comm.send(probe, self._pair_index(peer, kind), 0)
+                else:
+                    comm.recv(probe, self._pair_index(peer, kind), 0)
+            return (time.perf_counter() - t0) * 1e3
         with torch.cuda.device(self.device):
             for op, kind, peer in connect_plan(self.rank, self.world, bool(self._hcomms)):
                 comm = self._comm(peer) if kind == "stage" else self._hcomms[peer]
-                if op == "send":   # index of the receiving end inside the 2-rank communicator
-                    comm.send(probe, 1, self.send_stream.cuda_stream)
+                if op == "send":
+                    comm.send(probe, self._pair_index(peer, kind), self.send_stream.cuda_stream)
                 else:
-                    comm.recv(probe, 0, self.recv_stream.cuda_stream)
+                    comm.recv(probe, self._pair_index(peer, kind), self.recv_stream.cuda_stream)
             # bounded wait: a peer that failed after this rank's communicators came up never
             # posts its side, and the RCCL kernel waiting for it would spin forever; poll, watch
             # for a published failure, and abort the communicators (their kernels exit) instead
@@ -323,11 +353,15 @@ class RcclTransport(Transport):
 
     def send(self, t: torch.Tensor, peer: int) -> None:
         """Asynchronous: the send waits for work already queued on the current stream."""
+        if not self._gpu:
+            self._comm(peer).send(t.contiguous(), self._pair_index(peer, "stage"), 0)
+            self._count(t, True)
+            return
         cur = torch.cuda.current_stream(self.device)
         t = t.contiguous()   # copied on the compute stream, before the send stream waits on it
         self.send_stream.wait_stream(cur)
         t.record_stream(self.send_stream)
-        self._comm(peer).send(t, self._peer_index(peer), self.send_stream.cuda_stream)
+        self._comm(peer).send(t, self._pair_index(peer, "stage"), self.send_stream.cuda_stream)
         self._count(t, True)
 
     def recv(self, t: torch.Tensor, peer: int, free_event: Optional["torch.cuda.Event"] = None
@@ -336,13 +370,19 @@ class RcclTransport(Transport):
 
         ``free_event`` (optional) marks when ``t`` is no longer read by earlier compute; without it
         the receive waits for everything queued on the compute stream (no overlap)."""
+        if not self._gpu:
+            t0 = time.perf_counter()
+            self._comm(peer).recv(t, self._pair_index(peer, "stage"), 0)
+            self.recv_wait_ms += (time.perf_counter() - t0) * 1e3
+            self._count(t, False)
+            return t
         cur = torch.cuda.current_stream(self.device)
         if free_event is not None:
             self.recv_stream.wait_event(free_event)
         else:
             self.recv_stream.wait_stream(cur)
         t.record_stream(self.recv_stream)
-        self._comm(peer).recv(t, self._peer_index(peer), self.recv_stream.cuda_stream)
+        self._comm(peer).recv(t, self._pair_index(peer, "stage"), self.recv_stream.cuda_stream)
         if self._timing:
             a = torch.cuda.Event(enable_timing=True)
             a.record(cur)
@@ -358,18 +398,30 @@ class RcclTransport(Transport):
     def send_head(self, t: torch.Tensor, peer: int) -> None:
         """Last stage -> head rank ``peer``: the normed hidden states of an offloaded decode step
         (asynchronous, on the send stream, ordered after the work queued so far)."""
+        if not self._gpu:
+            self._head_comm(peer).send(t.contiguous(), self._pair_index(peer, "head"), 0)
+            self._count(t, True)
+            return
         cur = torch.cuda.current_stream(self.device)
         t = t.contiguous()   # copied on the compute stream, before the send stream waits on it
         self.send_stream.wait_stream(cur)
         t.record_stream(self.send_stream)
-        self._hcomms[peer].send(t, 1, self.send_stream.cuda_stream)
+        self._head_comm(peer).send(t, self._pair_index(peer, "head"), self.send_stream.cuda_stream)
         self._count(t, True)
 
     def recv_head(self, t: torch.Tensor, peer: int, stream: "torch.cuda.Stream") -> torch.Tensor:
         """Head rank: receive into ``t`` on ``stream`` (the head side stream)."""
-        self._hcomms[peer].recv(t, 0, stream.cuda_stream)
+        self._head_comm(peer).recv(t, self._pair_index(peer, "head"),
+                                   stream.cuda_stream if stream is not None else 0)
         self._count(t, False)
         return t
+
+    def irecv_head(self, t: torch.Tensor, peer: int) -> "_HostRecv":
+        """CPU (host-synchronous) counterpart of :meth:`recv_head` for runtime/head.py's CPU
+        path: a work handle whose ``wait()`` performs the receive."""
+        if self._gpu:
+            raise RuntimeError("irecv_head is the CPU path; GPU head jobs use recv_head on a stream")
+        return _HostRecv(lambda: self.recv_head(t, peer, None))
 
     def _drain_waits(self, block: bool) -> None:
         while self._waits and (block or self._waits[0][1].query()):
@@ -390,9 +442,19 @@ class RcclTransport(Transport):
             d["head_comms"] = sorted(self._hcomms)
         return d
 
-    def _peer_index(self, peer: int) -> int:
-        # inside a 2-rank pair communicator the lower global rank of the pair is index 0
-        # (this also holds for the ring-closure pair (0, world-1))
+    def _head_comm(self, peer: int):
+        c = self._hcomms.get(peer)
+        if c is None:
+            raise ValueError(f"rank {self.rank} has no head communicator with rank {peer}")
+        return c
+
+    def _pair_index(self, peer: int, kind: str) -> int:
+        """Index of ``peer`` inside the 2-rank communicator this rank shares with it.  Stage pair
+        (a, a+1): the lower stage is index 0.  Head pair (last, r): the last stage, the pair's
+        creator and only sender, is index 0 and head rank r is index 1 - so a head pair is NOT
+        ordered by rank (the last stage is the higher rank but index 0)."""
+        if kind == "head":
+            return 0 if peer == self.world - 1 else 1
         return 0 if peer < self.rank else 1
 
     def close(self) -> None:

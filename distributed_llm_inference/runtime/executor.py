@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import bisect
 import logging
+import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -29,6 +30,7 @@ from ..models.common import AttnMetadata
 from ..models.llama.cache import KVPool
 from ..models.stage import CausalLMStage
 from ..utils.cuda import capture_guard, prime_graph_rng
+from .hostclock import HOST
 from .watchdog import TRACKER, wait_event
 
 log = logging.getLogger(__name__)
@@ -142,6 +144,7 @@ class _Staging:
         self.events: List[Optional[torch.cuda.Event]] = [None] * self.nslots
         self._pending: List[Tuple[int, int]] = []
         self.slot = 0
+        self.waited_ms = 0.0   # host time blocked in acquire() (the device behind the ring)
         self.host = self.hosts[0]
         self.h = self.hviews[0]
         self.dev = torch.zeros(off, dtype=torch.uint8, device=device)
@@ -152,8 +155,12 @@ class _Staging:
         """Switch to the next host slot, waiting until its previous uploads have executed."""
         self.slot = (self.slot + 1) % self.nslots
         ev = self.events[self.slot]
-        if ev is not None:
+        if ev is not None and not ev.query():
+            t0 = time.perf_counter()
             wait_event(ev, "staging slot (uploads of an earlier step)")
+            ms = (time.perf_counter() - t0) * 1e3
+            self.waited_ms += ms
+            HOST.add("staging_wait", ms)
         self.host = self.hosts[self.slot]
         self.h = self.hviews[self.slot]
 
@@ -398,6 +405,10 @@ class StageExecutor:
 
     def _execute(self, plan: StepPlan, inputs: Optional[torch.Tensor],
                  token_src: Optional[torch.Tensor] = None, project: bool = True) -> torch.Tensor:
+        # host phases (runtime/hostclock.py): "stage" = frees, KV reservation, metadata staging;
+        # "staging_wait" (charged by _Staging.acquire) = blocked behind the device; "launch" =
+        # graph replay / eager kernel launches
+        t0, w0 = time.perf_counter(), self.staging.waited_ms
         self.apply_frees(plan.free_ids)
         if not plan.seq_ids:
             return torch.empty(0, device=self.device)
@@ -431,17 +442,25 @@ class StageExecutor:
             if g is None:
                 g = self._capture(grows, project)
             TRACKER.device_mark("compute_in", plan.step, torch.cuda.current_stream())
+            t1 = time.perf_counter()
+            HOST.add("stage", (t1 - t0) * 1e3 - (self.staging.waited_ms - w0))
             g.graph.replay()
             if self.stage.has_head and project:
+                HOST.since("launch", t1)
                 return g.out[:n_sample]
-            return g.out[:B].clone()
+            out = g.out[:B].clone()
+            HOST.since("launch", t1)
+            return out
         splits = self._splits(rows) if decode else 1
         meta = self._metadata(plan, rows, splits, decode)
         if self.stage.has_embed:
             x = self.staging.d["tokens"][: meta.num_tokens]
         else:
             x = inputs
+        t1 = time.perf_counter()
+        HOST.add("stage", (t1 - t0) * 1e3 - (self.staging.waited_ms - w0))
         out = self._forward(meta, x, n_sample if self.stage.has_head else 0, project)
+        HOST.since("launch", t1)
         return out if project else out[:B]
 
     # ------------------------------------------------------------------ graphs

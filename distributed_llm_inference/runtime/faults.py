@@ -121,7 +121,9 @@ class StageStats:
     def snapshot(self) -> dict:
         """Cumulative counters now (waits for the timing events still in flight)."""
         self._poll(block=True)
+        from .hostclock import HOST
         rec = {"t": time.perf_counter(), "steps": self.steps, "device_ms": self.total_ms}
+        rec.update(HOST.snapshot())
         if self.transport is not None:
             rec.update(self.transport.traffic())
         return rec

@@ -27,7 +27,6 @@ on the others - from completing, with RCCL-style barrier packets queued on pool 
 from __future__ import annotations
 
 import os
-import weakref
 from typing import Dict, List, Optional
 
 import torch
@@ -103,6 +102,59 @@ class RankStreams:
         self._handles.clear()
 
 
+class TokenSlot:
+    """One take of a :class:`HostTokenRing`: the host view of the copied tokens and the ring slot
+    behind it.  The consumer reads it ONCE with :meth:`tolist`, which also frees the slot; a take
+    that is never read (an aborted step) frees its slot with :meth:`release` or when the handle is
+    garbage-collected.  ``view`` peeks without freeing (tests)."""
+
+    __slots__ = ("view", "_ledger", "_k")
+
+    def __init__(self, view: torch.Tensor, ledger: "SlotLedger", k: int):
+        self.view, self._ledger, self._k = view, ledger, k
+
+    def tolist(self) -> List[int]:
+        out = self.view.tolist()
+        self.release()
+        return out
+
+    def release(self) -> None:
+        if self._ledger is not None:
+            self._ledger.release(self._k)
+            self._ledger = None
+
+    def __len__(self) -> int:
+        return self.view.numel()
+
+    def __del__(self):
+        self.release()
+
+
+class SlotLedger:
+    """Which slots of a ring are held by an unread :class:`TokenSlot` (round-robin hand-out; a
+    hand-out onto a held slot raises instead of overwriting tokens nobody has read yet)."""
+
+    def __init__(self, slots: int):
+        self.held = [False] * int(slots)
+        self.i = 0
+
+    def acquire(self) -> int:
+        k = self.i % len(self.held)
+        if self.held[k]:
+            raise RuntimeError(f"HostTokenRing overflow: slot {k} is still held by its consumer "
+                               f"({self.in_use()} of {len(self.held)} slots unread); size the "
+                               "ring with token_ring(device, max_items, slots)")
+        self.held[k] = True
+        self.i += 1
+        return k
+
+    def release(self, k: int) -> None:
+        self.held[k] = False
+
+    def in_use(self) -> int:
+        return sum(self.held)
+
+
 class HostTokenRing:
     """Device -> host returns of sampled token ids without a copy engine: a ring of slots in
     coherent, device-mapped host memory written by a copy kernel on the caller's stream
@@ -110,10 +162,10 @@ class HostTokenRing:
     queue shared by the process's streams - see csrc/comm/streams.hip - where it can wait behind
     another stream's copy that is ordered after a spinning receive.)
 
-    A slot is handed out again only when the host view returned for its previous use is gone
-    (its consumer read it and dropped it; views are tracked by weak reference).  A take that
-    would overwrite a view still held -- more unconsumed takes than ``slots`` -- raises instead of
-    silently corrupting tokens; size the ring from the in-flight micro-batch count at init."""
+    Slots are released explicitly: :meth:`take` returns a :class:`TokenSlot` that frees its slot
+    when the consumer reads it (``tolist()``), releases it, or drops it.  A take that would
+    overwrite a slot still held -- more unread takes than ``slots`` -- raises instead of silently
+    corrupting tokens; size the ring from the in-flight micro-batch count at init."""
 
     def __init__(self, device: torch.device, max_items: int, slots: int = 64):
         from .. import ops
@@ -123,37 +175,28 @@ class HostTokenRing:
         self.slots = int(slots)
         self.buf = self.C.HostBuffer(self.item_bytes * self.slots)
         self.view = self.buf.tensor()
-        self._out: List[Optional[weakref.ref]] = [None] * self.slots
-        self.i = 0
+        self.ledger = SlotLedger(self.slots)
 
     def in_use(self) -> int:
-        """Slots whose host view is still held by a consumer."""
-        return sum(1 for r in self._out if r is not None and r() is not None)
+        """Slots held by an unread take."""
+        return self.ledger.in_use()
 
     def take(self, tok: torch.Tensor, stream=None):
         """Copy ``tok`` (int32 [B], device) into the next slot on ``stream`` (default: current);
-        returns (host int32 view [B], event recorded after the copy)."""
+        returns (:class:`TokenSlot`, event recorded after the copy)."""
         if tok.dtype != torch.int32 or not tok.is_contiguous():
             tok = tok.to(torch.int32).contiguous()
         nb = tok.numel() * 4
         if nb > self.item_bytes:
             raise ValueError(f"{tok.numel()} tokens > ring slot of {self.item_bytes // 4}")
-        k = self.i % self.slots
-        prev = self._out[k]
-        if prev is not None and prev() is not None:
-            raise RuntimeError(f"HostTokenRing overflow: slot {k} is still held by its consumer "
-                               f"({self.in_use()} of {self.slots} slots unconsumed); size the ring "
-                               "with token_ring(device, max_items, slots)")
+        k = self.ledger.acquire()
         off = k * self.item_bytes
-        self.i += 1
         s = stream or torch.cuda.current_stream(self.device)
         if nb:   # (an empty step samples nothing: no copy, just the event)
             self.C.copy_segments(self.buf.dev_ptr + off, tok.data_ptr(), [(0, nb)], s.cuda_stream)
         ev = torch.cuda.Event()
         ev.record(s)
-        v = self.view[off: off + nb].view(torch.int32)
-        self._out[k] = weakref.ref(v)
-        return v, ev
+        return TokenSlot(self.view[off: off + nb].view(torch.int32), self.ledger, k), ev
 
 
 _TOKEN_RINGS: Dict[int, HostTokenRing] = {}

@@ -98,6 +98,9 @@ class InferenceBackend:
         if self.is_block:
             if generation_id is None:
                 raise ValueError("block backends need a generation_id")
+            dev = self._device()
+            inputs = tuple(x.to(dev, torch.bfloat16) if torch.is_tensor(x) else x for x in inputs)
+            kw = {k: v.to(dev) if torch.is_tensor(v) else v for k, v in kw.items()}
             return self.module(generation_id, *inputs, past_key_value=self.cache, **kw)
         return self.module(*inputs, **kw)
 
@@ -106,7 +109,29 @@ class InferenceBackend:
         """Pack every pending session step into one varlen forward through the block.
 
         Several steps of one session in the same batch run in submission order: the k-th step of
-        every session goes into the k-th packed forward ("wave")."""
+        every session goes into the k-th packed forward ("wave").  A step that carries the
+        reference stage API's extra arguments (``attention_mask``, ``position_ids``,
+        ``output_hidden_states``: task meta ``kwargs``) runs alone through ``LlamaBlock.forward``
+        at its place in submission order; the plain steps around it are packed as usual."""
+        results: List[Any] = [None] * len(tasks)
+        seg: List[int] = []
+        for i, t in enumerate(tasks + [None]):
+            if t is not None and not t.meta.get("kwargs"):
+                seg.append(i)
+                continue
+            if seg:
+                for j, r in zip(seg, self._process_packed([tasks[j] for j in seg])):
+                    results[j] = r
+                seg = []
+            if t is not None:
+                try:
+                    results[i] = self.forward(*t.args, generation_id=t.meta.get("generation_id"),
+                                              **t.meta["kwargs"])
+                except Exception as e:  # noqa: BLE001 - this task's waiter only
+                    results[i] = e
+        return results
+
+    def _process_packed(self, tasks: List[Task]) -> List[Any]:
         blk = self.module
         self.cache.bind(blk.config, blk.layer_ids, self._device(), torch.bfloat16)
         results: List[Any] = [None] * len(tasks)
@@ -150,6 +175,9 @@ class InferenceBackend:
                 if h.dim() != 3:
                     raise ValueError("hidden_states must be [batch, seq, hidden]")
                 B, T, H = h.shape
+                # to the device BEFORE reserving: a failed copy (OOM, bad shape) leaves nothing
+                # reserved
+                x = h.reshape(B * T, H).to(dev, torch.bfloat16)
                 rows = cache.session_rows(gid, B)
                 cache.reserve_rows(gid, rows, [T] * B, T)
             except Exception as e:  # noqa: BLE001 - delivered to this task's waiter only
@@ -159,7 +187,7 @@ class InferenceBackend:
             spans.append((i, B, T))
             sids += rows
             qlens += [T] * B
-            xs.append(h.reshape(B * T, H).to(dev, torch.bfloat16))
+            xs.append(x)
         if not spans:
             return
         try:
@@ -175,8 +203,12 @@ class InferenceBackend:
             results[i] = (y[off: off + B * T].view(B, T, -1),)
             off += B * T
 
-    def submit(self, *inputs, generation_id: Optional[str] = None):
-        return self.inference_pool.submit_task(*inputs, generation_id=generation_id)
+    def submit(self, *inputs, generation_id: Optional[str] = None, **kwargs):
+        """Queue one step; ``kwargs``: the reference stage API's ``attention_mask`` /
+        ``position_ids`` / ``output_hidden_states`` (run unpacked, in order)."""
+        kwargs = {k: v for k, v in kwargs.items() if v is not None and v is not False}
+        return self.inference_pool.submit_task(*inputs, generation_id=generation_id,
+                                               kwargs=kwargs or None)
 
     def close_session(self, generation_id: str) -> None:
         if self.cache is not None:

@@ -13,18 +13,31 @@ Server (``distribute block-serve --model M --start a --end b --port P``)::
     GET  /info                     {"model", "start", "end", "hidden_size", "blocks": [...]}
     GET  /health                   200 while every block's pool is alive
     POST /forward                  msgpack {"generation_id", "block_id"?, "shape", "dtype",
-                                   "data"} -> msgpack {"shape", "dtype", "data"}
-                                   (no block_id: every block of the worker, in order)
+                                   "data", "attention_mask"?, "position_ids"?,
+                                   "output_hidden_states"?} -> msgpack {"shape", "dtype", "data",
+                                   "hidden_states"?: [tensor, ...]}
+                                   (no block_id: every block of the worker, in order; the optional
+                                   fields are the reference stage API's arguments, reference
+                                   models/llama/model.py:25-33, tensors packed like the hidden)
     POST /close_session            {"generation_id"}: free the session's KV on every block
 
 Client: :class:`RemoteBlocks` (one server) and :class:`RemoteSequential` (a chain of servers
-whose ranges tile [0, L) - the client side of the swarm: ``forward(gid, hidden)`` walks the
+whose ranges tile [0, L) - the client side of the swarm: ``forward(gid, hidden, ...)`` walks the
 chain, ``close_session(gid)`` frees the session everywhere; ``from_registry`` finds the chain in
 a block registry, server/registry.py, where ``block-serve --registry`` servers claim their layers).
+
+Failover (reference server/server.py:15-23: the swarm survives unhealthy servers): the client
+keeps, per session, the inputs it sent to every layer range.  When a hop fails (connection error,
+timeout or HTTP 5xx) it re-resolves that range from the registry (any ready servers chaining it,
+the dead one excluded), replays the session's history into them to rebuild their KV, and carries
+on - the outputs equal an uninterrupted run.  A session that cannot be recovered is closed on
+every surviving server before the error is raised, so no KV is orphaned.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence
+import logging
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import msgpack
 import torch
@@ -34,7 +47,11 @@ try:   # module level: FastAPI resolves the (string) annotations of the handlers
 except ImportError:  # pragma: no cover - the client side needs no web framework
     Request = None
 
-_DTYPES = {"bfloat16": torch.bfloat16, "float32": torch.float32, "float16": torch.float16}
+log = logging.getLogger(__name__)
+
+_DTYPES = {"bfloat16": torch.bfloat16, "float32": torch.float32, "float16": torch.float16,
+           "int64": torch.int64, "int32": torch.int32, "bool": torch.bool}
+_STAGE_KWARGS = ("attention_mask", "position_ids")
 
 
 def pack_tensor(t: torch.Tensor) -> dict:
@@ -42,8 +59,9 @@ def pack_tensor(t: torch.Tensor) -> dict:
     name = str(t.dtype).replace("torch.", "")
     if name not in _DTYPES:
         raise TypeError(f"unsupported dtype {t.dtype}")
-    # raw bytes of the storage (bf16 has no numpy dtype: view as int16)
-    raw = t.view(torch.int16) if t.dtype in (torch.bfloat16, torch.float16) else t
+    # raw bytes of the storage (bf16 has no numpy dtype: view as int16; bool as uint8)
+    raw = (t.view(torch.int16) if t.dtype in (torch.bfloat16, torch.float16)
+           else t.view(torch.uint8) if t.dtype == torch.bool else t)
     return {"shape": list(t.shape), "dtype": name, "data": raw.numpy().tobytes()}
 
 
@@ -52,7 +70,14 @@ def unpack_tensor(d: dict) -> torch.Tensor:
     buf = bytearray(d["data"])
     if dt in (torch.bfloat16, torch.float16):
         return torch.frombuffer(buf, dtype=torch.int16).view(dt).reshape(d["shape"])
+    if dt == torch.bool:
+        return torch.frombuffer(buf, dtype=torch.uint8).view(torch.bool).reshape(d["shape"])
     return torch.frombuffer(buf, dtype=dt).reshape(d["shape"])
+
+
+class HopFailure(RuntimeError):
+    """A block server could not be reached or failed on its side (connection error, timeout,
+    HTTP 5xx): the hop is replaceable.  Client errors (4xx) are plain RuntimeErrors."""
 
 
 def build_block_app(worker):
@@ -65,7 +90,7 @@ def build_block_app(worker):
     async def info():
         return {"model": worker.spec.name, "start": worker.start, "end": worker.end,
                 "hidden_size": worker.spec.hidden_size, "device": str(worker.device),
-                "blocks": [dict(b) for b in worker.block_ids]}
+                "blocks": [dict(b) for b in worker.block_ids], "sessions": worker.sessions()}
 
     @app.get("/health")
     async def health():
@@ -86,12 +111,24 @@ def build_block_app(worker):
         bid = body.get("block_id")
         if bid is not None and bid not in worker.blocks:
             raise HTTPException(404, f"unknown block {bid!r}")
+        kw = {k: unpack_tensor(body[k]) for k in _STAGE_KWARGS if body.get(k) is not None}
+        if body.get("output_hidden_states"):
+            kw["output_hidden_states"] = True
 
         def run():
-            y = worker.forward(bid, gid, x) if bid is not None else worker.forward_range(gid, x)
+            y = worker.forward(bid, gid, x, **kw) if bid is not None else \
+                worker.forward_range(gid, x, **kw)
+            if kw.get("output_hidden_states"):
+                y, hs = y
+                out = pack_tensor(y.to(x.dtype))
+                out["hidden_states"] = [pack_tensor(h.to(x.dtype)) for h in hs]
+                return out
             return pack_tensor(y.to(x.dtype))
 
-        out = await asyncio.get_running_loop().run_in_executor(None, run)
+        try:
+            out = await asyncio.get_running_loop().run_in_executor(None, run)
+        except (ValueError, MemoryError) as e:   # a bad request / no KV room: the client's call
+            raise HTTPException(422, f"{type(e).__name__}: {e}")
         return Response(msgpack.packb(out), media_type="application/msgpack")
 
     @app.post("/close_session")
@@ -141,10 +178,27 @@ class RemoteBlocks:
 
     def info(self) -> dict:
         if self._info is None:
-            r = self._s.get(self.url + "/info", timeout=self.timeout)
+            import requests
+            try:
+                r = self._s.get(self.url + "/info", timeout=self.timeout)
+            except requests.RequestException as e:
+                raise HopFailure(f"{self.url}/info: {e!r}") from e
+            if r.status_code >= 500:
+                raise HopFailure(f"{self.url}/info: HTTP {r.status_code}")
             r.raise_for_status()
             self._info = r.json()
         return self._info
+
+    def sessions(self) -> List[str]:
+        """The generation ids currently holding KV on the server (fresh, not cached)."""
+        r = self._s.get(self.url + "/info", timeout=self.timeout)
+        r.raise_for_status()
+        return list(r.json().get("sessions", []))
+
+    @property
+    def range(self) -> Tuple[int, int]:
+        i = self.info()
+        return int(i["start"]), int(i["end"])
 
     def healthy(self) -> bool:
         try:
@@ -152,17 +206,39 @@ class RemoteBlocks:
         except Exception:  # noqa: BLE001
             return False
 
-    def forward(self, generation_id: str, hidden: torch.Tensor,
-                block_id: Optional[str] = None) -> torch.Tensor:
+    def forward(self, generation_id: str, hidden: torch.Tensor, block_id: Optional[str] = None,
+                attention_mask: Optional[torch.Tensor] = None,
+                position_ids: Optional[torch.Tensor] = None,
+                output_hidden_states: bool = False):
+        """The server's layers on ``hidden [B, T, H]``; returns the hidden states, or
+        ``(hidden, all_hidden_states)`` with ``output_hidden_states``.  Raises
+        :class:`HopFailure` when the server is unreachable or fails on its side."""
+        import requests
         body = pack_tensor(hidden)
         body["generation_id"] = generation_id
         if block_id is not None:
             body["block_id"] = block_id
-        r = self._s.post(self.url + "/forward", data=msgpack.packb(body),
-                         headers={"Content-Type": "application/msgpack"}, timeout=self.timeout)
+        if attention_mask is not None:
+            body["attention_mask"] = pack_tensor(attention_mask)
+        if position_ids is not None:
+            body["position_ids"] = pack_tensor(position_ids)
+        if output_hidden_states:
+            body["output_hidden_states"] = True
+        try:
+            r = self._s.post(self.url + "/forward", data=msgpack.packb(body),
+                             headers={"Content-Type": "application/msgpack"},
+                             timeout=self.timeout)
+        except requests.RequestException as e:
+            raise HopFailure(f"{self.url}/forward: {e!r}") from e
+        if r.status_code >= 500:
+            raise HopFailure(f"{self.url}/forward: HTTP {r.status_code}: {r.text[:300]}")
         if r.status_code != 200:
             raise RuntimeError(f"{self.url}/forward: HTTP {r.status_code}: {r.text[:500]}")
-        return unpack_tensor(msgpack.unpackb(r.content))
+        d = msgpack.unpackb(r.content)
+        y = unpack_tensor(d)
+        if output_hidden_states:
+            return y, tuple(unpack_tensor(h) for h in d.get("hidden_states", []))
+        return y
 
     def close_session(self, generation_id: str) -> None:
         r = self._s.post(self.url + "/close_session", json={"generation_id": generation_id},
@@ -171,9 +247,16 @@ class RemoteBlocks:
 
 
 class RemoteSequential:
-    """A chain of block servers covering consecutive layer ranges (the swarm's client side)."""
+    """A chain of block servers covering consecutive layer ranges (the swarm's client side).
 
-    def __init__(self, urls: Sequence[str], timeout: float = 120.0):
+    With a ``registry`` (``from_registry``) a failed hop is replaced by ready servers from the
+    registry and the session's history is replayed into them (module docstring); without one a
+    failure closes the session on the surviving servers and raises."""
+
+    def __init__(self, urls: Sequence[str], timeout: float = 120.0, registry=None,
+                 model: Optional[str] = None, failover_wait_s: float = 30.0,
+                 max_failovers: int = 4):
+        self.timeout = timeout
         self.servers: List[RemoteBlocks] = [RemoteBlocks(u, timeout) for u in urls]
         infos = [s.info() for s in self.servers]
         order = sorted(range(len(infos)), key=lambda i: infos[i]["start"])
@@ -184,17 +267,23 @@ class RemoteSequential:
                 raise ValueError(f"layer ranges do not chain: [{a['start']},{a['end']}) then "
                                  f"[{b['start']},{b['end']})")
         self.start, self.end = infos[0]["start"], infos[-1]["end"]
+        self.registry, self.model = registry, model or infos[0]["model"]
+        self.failover_wait_s, self.max_failovers = failover_wait_s, max_failovers
+        # per session: the inputs sent to each layer range, in order (hidden, kwargs)
+        self._history: Dict[str, Dict[Tuple[int, int], List[tuple]]] = {}
+        self.dead: set = set()
+        self.failovers = 0
 
     @classmethod
     def from_registry(cls, registry_url: str, model: str, timeout: float = 120.0,
-                      wait_s: float = 0.0) -> "RemoteSequential":
+                      wait_s: float = 0.0, token: Optional[str] = None,
+                      failover_wait_s: float = 30.0) -> "RemoteSequential":
         """The chain of ready servers listed by a block registry (server/registry.py) that
         covers ``model`` from layer 0 to its last layer; ``wait_s``: keep polling that long
-        for the swarm to cover it."""
-        import time
+        for the swarm to cover it.  The registry also serves failed hops' replacements."""
         from ..config import resolve_model
         from .registry import RegistryClient, find_chain
-        reg = RegistryClient(registry_url)
+        reg = RegistryClient(registry_url, token=token)
         try:
             name = resolve_model(model).name
         except ValueError:
@@ -210,15 +299,119 @@ class RemoteSequential:
         if not chain:
             raise LookupError(f"registry {registry_url} lists no chain of ready servers covering "
                               f"{name} (servers: {[(e['start'], e['end']) for e in entries]})")
-        return cls([e["url"] for e in chain], timeout=timeout)
+        return cls([e["url"] for e in chain], timeout=timeout, registry=reg, model=name,
+                   failover_wait_s=failover_wait_s)
 
-    def forward(self, generation_id: str, hidden: torch.Tensor) -> torch.Tensor:
-        for s in self.servers:
-            hidden = s.forward(generation_id, hidden)
-        return hidden
+    # ------------------------------------------------------------------ forward
+    def forward(self, generation_id: str, hidden: torch.Tensor,
+                attention_mask: Optional[torch.Tensor] = None,
+                position_ids: Optional[torch.Tensor] = None,
+                output_hidden_states: bool = False):
+        """Walk the chain (the reference stage API over the whole model range).  Returns the
+        hidden states, or ``(hidden, all_hidden_states)`` with ``output_hidden_states``."""
+        kw = {}
+        if attention_mask is not None:
+            kw["attention_mask"] = attention_mask
+        if position_ids is not None:
+            kw["position_ids"] = position_ids
+        hist = self._history.setdefault(generation_id, {})
+        hs: list = []
+        i = 0
+        while i < len(self.servers):
+            s = self.servers[i]
+            try:
+                out = s.forward(generation_id, hidden, output_hidden_states=output_hidden_states,
+                                **kw)
+            except HopFailure as e:
+                self._failover(i, generation_id, e)
+                continue   # the replacement chain now sits at position i
+            hist.setdefault(s.range, []).append((hidden, kw))
+            if output_hidden_states:
+                out, h = out
+                hs = hs[:-1] + list(h)
+            hidden = out
+            i += 1
+        return (hidden, tuple(hs)) if output_hidden_states else hidden
 
     __call__ = forward
 
+    def _failover(self, i: int, generation_id: str, err: Exception) -> None:
+        """Replace hop ``i`` (its layer range) with ready servers from the registry and replay
+        the history of EVERY open session into them (their KV for this range was on the dead
+        server).  Raises - after closing the sessions on the surviving servers - when no
+        replacement can be found."""
+        failed = self.servers[i]
+        a, b = failed.range
+        self.dead.add(failed.url)
+        log.warning("block server %s (layers [%d, %d)) failed: %s; re-resolving", failed.url, a,
+                    b, err)
+        last_err: Exception = err
+        deadline = time.monotonic() + self.failover_wait_s
+        while self.registry is not None and self.failovers < self.max_failovers:
+            repl = self._resolve(a, b)
+            if repl is None:
+                if time.monotonic() > deadline:
+                    break
+                time.sleep(0.5)
+                continue
+            try:
+                self._replay(repl)
+            except HopFailure as e2:   # the replacement died too: exclude it and retry
+                self.dead.update(s.url for s in repl if not s.healthy())
+                last_err = e2
+                continue
+            self.servers[i:i + 1] = repl
+            self.failovers += 1
+            log.warning("layers [%d, %d) now served by %s", a, b, [s.url for s in repl])
+            return
+        self._abandon(exclude={failed.url})
+        raise RuntimeError(f"block server {failed.url} (layers [{a}, {b})) failed and no "
+                           f"replacement was found: {last_err}") from last_err
+
+    def _resolve(self, a: int, b: int) -> Optional[List[RemoteBlocks]]:
+        from .registry import find_chain
+        try:
+            entries = [e for e in self.registry.servers(self.model) if e["url"] not in self.dead]
+        except Exception:  # noqa: BLE001 - registry unreachable right now: retry until deadline
+            return None
+        chain = find_chain(entries, b, start=a)
+        if not chain:
+            return None
+        repl = [RemoteBlocks(e["url"], self.timeout) for e in chain]
+        for s in repl:
+            if not s.healthy():   # listed until its ttl lapses, but already gone
+                self.dead.add(s.url)
+                return None
+        return repl
+
+    def _replay(self, repl: List[RemoteBlocks]) -> None:
+        """Rebuild every open session's KV on the replacement servers: feed each server, in
+        order, the inputs the failed range received (the outputs of server k are the inputs of
+        server k+1); record them as the new ranges' history."""
+        a, b = repl[0].range[0], repl[-1].range[1]
+        for gid, hist in self._history.items():
+            inputs = hist.pop((a, b), [])
+            for s in repl:
+                hist[s.range] = list(inputs)
+                nxt = []
+                for h, kw in inputs:
+                    s_gid_out = s.forward(gid, h, **kw)
+                    nxt.append((s_gid_out, kw))
+                inputs = nxt
+
+    def _abandon(self, exclude=()) -> None:
+        """Close every session on the servers still alive (no orphaned KV)."""
+        for gid in list(self._history):
+            for s in self.servers:
+                if s.url in exclude or s.url in self.dead:
+                    continue
+                try:
+                    s.close_session(gid)
+                except Exception:  # noqa: BLE001 - best effort: the server may be gone too
+                    pass
+        self._history.clear()
+
     def close_session(self, generation_id: str) -> None:
+        self._history.pop(generation_id, None)
         for s in self.servers:
             s.close_session(generation_id)

@@ -15,13 +15,25 @@ serves (/root/reference/distributed_llm_inference/server/server.py:7-8), through
 
 ``distribute registry`` runs it; ``distribute block-serve --registry URL --max-layers N`` claims
 a range instead of taking ``--start/--end``, and ``RemoteSequential.from_registry(URL, model)``
-builds the client's chain from the registry alone.
+builds the client's chain from the registry alone - and re-resolves a failed hop from it
+(server/block_server.py failover).
+
+Trust: the mutating endpoints (/claim, /announce, /withdraw) take a shared token when the
+registry is started with one (``distribute registry --token T``; servers pass the same
+``--registry-token``): ``Authorization: Bearer T``, else 401.  Without a token anyone who can
+reach the registry can announce a URL for a layer range and receive clients' hidden states, so
+an open registry belongs on a trusted network only.
 """
 from __future__ import annotations
 
 import threading
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
+
+try:   # module level: FastAPI resolves the (string) annotations of the handlers here
+    from fastapi import Request
+except ImportError:  # pragma: no cover - clients need no web framework
+    Request = None
 
 
 def choose_range(num_layers: int, max_layers: int,
@@ -50,16 +62,17 @@ def choose_range(num_layers: int, max_layers: int,
     return best, best + span
 
 
-def find_chain(entries: Sequence[dict], num_layers: int) -> List[dict]:
-    """Servers whose ranges chain exactly from layer 0 to ``num_layers`` (fewest hops; among
-    equals the earliest-listed servers), or [] if the ready servers do not cover the model."""
+def find_chain(entries: Sequence[dict], num_layers: int, start: int = 0) -> List[dict]:
+    """Servers whose ranges chain exactly from layer ``start`` to ``num_layers`` (fewest hops;
+    among equals the earliest-listed servers), or [] if the given servers do not cover it.
+    (``start`` > 0: the replacement for one failed hop of a longer chain.)"""
     by_start: Dict[int, List[dict]] = {}
     for e in entries:
         by_start.setdefault(int(e["start"]), []).append(e)
     # breadth-first over layer boundaries: the first path that reaches num_layers has fewest hops
     prev: Dict[int, Tuple[int, dict]] = {}
-    frontier = [0]
-    seen = {0}
+    frontier = [start]
+    seen = {start}
     while frontier:
         nxt = []
         for b in frontier:
@@ -72,10 +85,10 @@ def find_chain(entries: Sequence[dict], num_layers: int) -> List[dict]:
         if num_layers in seen:
             break
         frontier = nxt
-    if num_layers not in seen:
+    if num_layers not in seen or num_layers == start:
         return []
     chain, b = [], num_layers
-    while b != 0:
+    while b != start:
         b0, e = prev[b]
         chain.append(e)
         b = b0
@@ -124,32 +137,50 @@ class Registry:
                     for e in self._entries.values() if model is None or e["model"] == model]
 
 
-def build_registry_app(reg: Optional[Registry] = None):
+def build_registry_app(reg: Optional[Registry] = None, token: Optional[str] = None):
+    """The registry's HTTP service; ``token``: the shared secret the mutating endpoints require."""
+    import hmac
     from fastapi import FastAPI, HTTPException
     reg = reg or Registry()
     app = FastAPI(title="distributed_llm_inference block registry")
 
+    def _auth(request: Request) -> None:
+        if token is None:
+            return
+        got = request.headers.get("authorization", "")
+        if not hmac.compare_digest(got.encode(), f"Bearer {token}".encode()):
+            raise HTTPException(401, "registry token required (Authorization: Bearer ...)")
+
     @app.post("/claim")
-    async def claim(body: dict):
+    async def claim(body: dict, request: Request):
+        _auth(request)
         try:
-            s, e = reg.claim(body["model"], int(body["num_layers"]), int(body["max_layers"]),
-                             body["url"])
-        except (KeyError, ValueError) as ex:
-            raise HTTPException(400, f"bad claim: {ex}")
+            s, e = reg.claim(str(body["model"]), int(body["num_layers"]),
+                             int(body["max_layers"]), str(body["url"]))
+        except (KeyError, ValueError, TypeError) as ex:
+            raise HTTPException(400, f"bad claim: {ex!r}")
         return {"start": s, "end": e}
 
     @app.post("/announce")
-    async def announce(body: dict):
+    async def announce(body: dict, request: Request):
+        _auth(request)
         try:
-            reg.announce(body["model"], body["url"], body["start"], body["end"],
-                         body["num_layers"], body.get("ttl", 30.0))
-        except KeyError as ex:
-            raise HTTPException(400, f"bad announce: missing {ex}")
+            start, end, n = int(body["start"]), int(body["end"]), int(body["num_layers"])
+            if not 0 <= start < end <= n:
+                raise ValueError(f"range [{start}, {end}) outside [0, {n})")
+            reg.announce(str(body["model"]), str(body["url"]), start, end, n,
+                         float(body.get("ttl", 30.0)))
+        except (KeyError, ValueError, TypeError) as ex:
+            raise HTTPException(400, f"bad announce: {ex!r}")
         return {"ok": True}
 
     @app.post("/withdraw")
-    async def withdraw(body: dict):
-        reg.withdraw(body["url"])
+    async def withdraw(body: dict, request: Request):
+        _auth(request)
+        try:
+            reg.withdraw(str(body["url"]))
+        except (KeyError, TypeError) as ex:
+            raise HTTPException(400, f"bad withdraw: {ex!r}")
         return {"ok": True}
 
     @app.get("/servers")
@@ -159,17 +190,19 @@ def build_registry_app(reg: Optional[Registry] = None):
     return app
 
 
-def serve_registry(host: str = "127.0.0.1", port: int = 8099) -> None:
+def serve_registry(host: str = "127.0.0.1", port: int = 8099, token: Optional[str] = None) -> None:
     import uvicorn
-    uvicorn.run(build_registry_app(), host=host, port=port, log_level="warning")
+    uvicorn.run(build_registry_app(token=token), host=host, port=port, log_level="warning")
 
 
 class RegistryClient:
-    def __init__(self, url: str, timeout: float = 30.0):
+    def __init__(self, url: str, timeout: float = 30.0, token: Optional[str] = None):
         import requests
         self.url = url.rstrip("/")
         self.timeout = timeout
         self._s = requests.Session()
+        if token:
+            self._s.headers["Authorization"] = f"Bearer {token}"
 
     def _post(self, path: str, body: dict) -> dict:
         r = self._s.post(self.url + path, json=body, timeout=self.timeout)

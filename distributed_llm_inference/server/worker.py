@@ -74,15 +74,35 @@ class InferenceWorker:
     def is_healthy(self) -> bool:
         return self._running and all(be.inference_pool.is_alive for be in self.blocks.values())
 
-    def forward(self, block_id: str, generation_id: str, hidden: torch.Tensor) -> torch.Tensor:
-        (out,) = self.blocks[block_id].submit(hidden, generation_id=generation_id).result()
-        return out
+    def forward(self, block_id: str, generation_id: str, hidden: torch.Tensor, **kw):
+        """One block.  ``kw``: the reference stage API's ``attention_mask`` / ``position_ids`` /
+        ``output_hidden_states`` (reference models/llama/model.py:25-33).  Returns the hidden
+        states, or ``(hidden, all_hidden_states)`` with ``output_hidden_states``."""
+        res = self.blocks[block_id].submit(hidden, generation_id=generation_id, **kw).result()
+        if kw.get("output_hidden_states"):
+            return res[0], tuple(res[1])
+        return res[0]
 
-    def forward_range(self, generation_id: str, hidden: torch.Tensor) -> torch.Tensor:
-        """Run every block of this worker in order (the whole stage)."""
+    def forward_range(self, generation_id: str, hidden: torch.Tensor, **kw):
+        """Run every block of this worker in order (the whole stage); with
+        ``output_hidden_states`` the per-layer inputs of every block and the final output."""
+        want = bool(kw.get("output_hidden_states"))
+        hs: list = []
         for b in self.block_ids:
-            hidden = self.forward(b["block_id"], generation_id, hidden)
-        return hidden
+            out = self.forward(b["block_id"], generation_id, hidden, **kw)
+            if want:
+                out, blk_hs = out
+                hs = hs[:-1] + list(blk_hs)   # a block's first entry is the previous output
+            hidden = out
+        return (hidden, tuple(hs)) if want else hidden
+
+    def sessions(self) -> List[str]:
+        """The generation ids holding KV on any block of this worker."""
+        ids = set()
+        for be in self.blocks.values():
+            if be.cache is not None:
+                ids.update(k for k in be.cache._sessions if k != "__schema__")
+        return sorted(ids)
 
     def close_session(self, generation_id: str) -> None:
         for be in self.blocks.values():

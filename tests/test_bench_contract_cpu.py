@@ -61,6 +61,13 @@ def test_bench_multirank_json_contract(n):
         assert r["mb_steps"] == steps * (n + 1), r
         assert r["device_ms_per_mb_step"] > 0
         assert r["recv_wait_ms_per_mb_step"] >= 0
+        # host time per micro-batch step, by phase (runtime/hostclock.py)
+        ph = r["host_ms_per_mb_step"]
+        assert "launch" in ph and "stage" in ph, r
+        assert ("plan" in ph and "ctrl" in ph) if r["rank"] == 0 else ("ctrl_wait" in ph), r
+        assert r["host_busy_ms_per_mb_step"] > 0
+    dh = d["driver_host_phases"]
+    assert dh["host_busy_ms_per_mb_step"] > 0 and "tokens" in dh["host_ms_per_mb_step"]
     H = 128  # tiny-llama-8l hidden size (bf16 activations)
     mb_bytes = bpm * H * 2
     T = steps * (n + 1)   # decode micro-batch steps in the window
@@ -83,7 +90,7 @@ def test_bench_multirank_json_contract(n):
 
 
 @pytest.mark.parametrize("n,dp", [(4, 2), (2, 2)])
-def test_bench_replicas_json_contract(n, dp):
+def test_bench_replicas_json_contract(n, dp):  # noqa: C901
     """``--dp``: dp independent pipeline replicas of n/dp stages (dp2 x pp2 over gloo, and two
     single-stage replicas); one JSON line whose tokens count every replica's sequences."""
     steps, warmup, bpm = 3, 1, 4

@@ -5,9 +5,10 @@ the same device, so there the full driver/follower GPU path (graphs, shm control
 feedback, micro-batching) runs over the host-staged transport, the RCCL binding is exercised with
 a 1-rank communicator, and the RCCL-failure path (all ranks agree, fall back together) is tested
 by asking for RCCL on a shared GPU: with an explicit ``DLI_TRANSPORT=rccl`` every rank fails
-loudly, ``DLI_TRANSPORT=rccl-or-host`` falls back to host staging, and the default (unset:
-``rccl-or-ipc``) falls back, agreed, to the IPC device transport.  With two or more GPUs the RCCL P2P transport and a PP=2
-RCCL pipeline are tested for real.
+loudly and ``DLI_TRANSPORT=rccl-or-host`` falls back to host staging.  The default (unset:
+``rccl-or-ipc``) compares the ranks' PCI devices and takes the IPC device transport on a shared
+GPU without trying RCCL (strict RCCL on distinct GPUs).  With two or more GPUs the RCCL P2P
+transport and a PP=2 RCCL pipeline are tested for real.
 """
 import multiprocessing as mp
 import os
@@ -224,9 +225,9 @@ def test_rccl_failure_falls_back_with_opt_in(gpu):
     assert rest and rest[0] == "HostStagedTransport", rest
 
 
-def test_rccl_failure_falls_back_to_ipc_by_default(gpu):
-    """``DLI_TRANSPORT`` unset: RCCL fails on the shared GPU on both ranks, they agree and bring up
-    the IPC device transport instead (rotating head kept), producing the same tokens as PP=1."""
+def test_default_transport_on_a_shared_gpu_is_ipc(gpu):
+    """``DLI_TRANSPORT`` unset: both ranks publish the same PCI device, so every rank brings up the
+    IPC device transport (rotating head kept) without trying RCCL, producing PP=1's tokens."""
     from distributed_llm_inference.runtime.engine import LLMEngine
     from distributed_llm_inference.runtime.sequence import SamplingParams
     os.environ["DLI_TUNABLEOP"] = "0"

@@ -1,0 +1,198 @@
+"""Swarm client failover and the full stage API over the wire (VERDICT r4 missing #2-#3), CPU.
+
+Three registry block servers tile tiny-llama-8l's 8 layers ([0,3) [3,6) [6,8)) and a fourth, the
+spare, claims the least-served range.  The client builds its chain from the registry, and the
+server of its first hop is killed (SIGKILL) in the middle of two sessions' generations.  The client
+re-resolves that range from the registry, replays each session's history into the replacement and
+carries on: every output equals the same session run with no failure, bit for bit.  A chain with
+no replacement closes the session on the surviving servers before raising (no orphaned KV).
+
+Reference: the server loop's health / restart intent (/root/reference/distributed_llm_inference/
+server/server.py:15-23) and the stage signature (models/llama/model.py:25-33)."""
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MODEL = "tiny-llama-8l"
+TOKEN = "s3cret"
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _start_server(reg_url, env, max_layers=3):
+    port = _port()
+    p = subprocess.Popen(
+        [sys.executable, os.path.join(REPO, "distribute"), "block-serve", "--model", MODEL,
+         "--registry", reg_url, "--registry-token", TOKEN, "--max-layers", str(max_layers),
+         "--port", str(port), "--device", "cpu", "--seed", "3"],
+        env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    return p, f"http://127.0.0.1:{port}"
+
+
+def _wait_ready(client, n, procs, timeout=240):
+    deadline = time.time() + timeout
+    while len(client.servers(MODEL)) < n:
+        for p in procs:
+            if p.poll() is not None and p.returncode not in (0, -9, -15):
+                raise RuntimeError(p.stderr.read().decode()[-3000:])
+        if time.time() > deadline:
+            raise TimeoutError(f"servers: {client.servers(MODEL, ready_only=False)}")
+        time.sleep(0.3)
+
+
+@pytest.fixture(scope="module")
+def swarm():
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    rport = _port()
+    reg_url = f"http://127.0.0.1:{rport}"
+    reg = subprocess.Popen([sys.executable, os.path.join(REPO, "distribute"), "registry",
+                            "--port", str(rport), "--token", TOKEN],
+                           env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    from distributed_llm_inference.server.registry import RegistryClient
+    client = RegistryClient(reg_url, timeout=5, token=TOKEN)
+    deadline = time.time() + 120
+    while True:
+        try:
+            client.servers()
+            break
+        except Exception:  # noqa: BLE001
+            if reg.poll() is not None:
+                raise RuntimeError(reg.stderr.read().decode()[-3000:])
+            if time.time() > deadline:
+                raise TimeoutError("registry did not come up")
+            time.sleep(0.3)
+    procs = {}
+    for _ in range(3):
+        p, u = _start_server(reg_url, env)
+        procs[u] = p
+    _wait_ready(client, 3, list(procs.values()))
+    p, u = _start_server(reg_url, env)        # the spare: every layer covered once -> [0, 3)
+    procs[u] = p
+    _wait_ready(client, 4, list(procs.values()))
+    yield reg_url, client, procs
+    for p in list(procs.values()) + [reg]:
+        if p.poll() is None:
+            p.terminate()
+    for p in list(procs.values()) + [reg]:
+        p.wait(30)
+
+
+def test_registry_requires_the_token(swarm):
+    reg_url, client, _ = swarm
+    from distributed_llm_inference.server.registry import RegistryClient
+    anon = RegistryClient(reg_url, timeout=5)
+    with pytest.raises(RuntimeError, match="401"):
+        anon.announce(MODEL, "http://evil:1", 0, 8, 8)
+    with pytest.raises(RuntimeError, match="401"):
+        anon.withdraw(next(iter(e["url"] for e in client.servers(MODEL))))
+    with pytest.raises(RuntimeError, match="400"):   # malformed range: a 400, not a 500
+        client.announce(MODEL, "http://x:1", 5, 2, 8)
+    assert all(e["url"] != "http://evil:1" for e in client.servers(MODEL))
+    assert anon.servers(MODEL)   # reading needs no token
+
+
+def test_stage_api_over_the_wire(swarm):
+    """position_ids, a 2-D attention_mask and output_hidden_states through the chain equal one
+    local LlamaBlock over every layer called the same way."""
+    reg_url, _, _ = swarm
+    from distributed_llm_inference.config import resolve_model
+    from distributed_llm_inference.models import LlamaBlock
+    from distributed_llm_inference.server.block_server import RemoteSequential
+    spec = resolve_model(MODEL)
+    chain = RemoteSequential.from_registry(reg_url, MODEL, token=TOKEN)
+    ref = LlamaBlock(spec, list(range(spec.num_layers))).init_random(3)
+    cache = ref.new_cache(num_blocks=64)
+    g = torch.Generator().manual_seed(5)
+    H = spec.hidden_size
+
+    def close(a, b):
+        assert a.shape == b.shape
+        assert torch.allclose(a.float(), b.float(), atol=5e-2, rtol=5e-2), \
+            (a.float() - b.float()).abs().max()
+
+    with torch.inference_mode():
+        x = (torch.randn(2, 5, H, generator=g) * 0.5).to(torch.bfloat16)
+        am = torch.tensor([[1, 1, 1, 1, 1], [0, 0, 1, 1, 1]])
+        pos = torch.tensor([[10, 11, 12, 13, 14], [0, 0, 20, 21, 22]])
+        y, hs = chain.forward("api", x, attention_mask=am, position_ids=pos,
+                              output_hidden_states=True)
+        r, rhs = ref("api", x, attention_mask=am, position_ids=pos, past_key_value=cache,
+                     output_hidden_states=True)
+        close(y, r)
+        assert len(hs) == len(rhs) == spec.num_layers + 1
+        for a, b in zip(hs, rhs):
+            close(a, b)
+        x1 = (torch.randn(2, 1, H, generator=g) * 0.5).to(torch.bfloat16)
+        close(chain.forward("api", x1), ref("api", x1, past_key_value=cache)[0])
+    chain.close_session("api")
+
+
+def test_failover_replays_history_into_the_spare(swarm):
+    reg_url, client, procs = swarm
+    from distributed_llm_inference.config import resolve_model
+    from distributed_llm_inference.server.block_server import RemoteSequential
+    spec = resolve_model(MODEL)
+    H = spec.hidden_size
+    chain = RemoteSequential.from_registry(reg_url, MODEL, token=TOKEN, failover_wait_s=30)
+    assert [s.range for s in chain.servers] == [(0, 3), (3, 6), (6, 8)]
+    g = torch.Generator().manual_seed(9)
+    prompts = {"a": 6, "b": 3}
+    steps = [(gid, T) for gid, T in prompts.items()] + [(gid, 1) for _ in range(4)
+                                                         for gid in ("b", "a")]
+    inputs = [(gid, (torch.randn(1, T, H, generator=g) * 0.5).to(torch.bfloat16))
+              for gid, T in steps]
+    with torch.inference_mode():
+        # the same sessions with no failure ("ref-" ids, run first, sequentially)
+        ref = [chain.forward("ref-" + gid, x) for gid, x in inputs]
+        for gid in prompts:
+            chain.close_session("ref-" + gid)
+        victim = chain.servers[0].url
+        out = []
+        for k, (gid, x) in enumerate(inputs):
+            if k == 4:   # mid-generation: both sessions prefilled and decoding
+                procs[victim].send_signal(signal.SIGKILL)
+                procs[victim].wait(10)
+            out.append(chain.forward(gid, x))
+    assert chain.failovers == 1 and victim in chain.dead
+    assert chain.servers[0].url != victim and chain.servers[0].range == (0, 3)
+    for k, (o, r) in enumerate(zip(out, ref)):
+        assert torch.equal(o, r), (k, (o.float() - r.float()).abs().max())
+    # the replacement holds both sessions; closing frees them everywhere
+    assert chain.servers[0].sessions() == ["a", "b"]
+    for gid in prompts:
+        chain.close_session(gid)
+    assert all(s.sessions() == [] for s in chain.servers)
+
+
+def test_unrecoverable_failure_frees_the_survivors(swarm):
+    """No registry to find a replacement: the client closes the session on the servers that are
+    still alive, then raises."""
+    _, client, procs = swarm
+    from distributed_llm_inference.server.block_server import RemoteSequential
+    from distributed_llm_inference.config import resolve_model
+    live = {e["url"]: e for e in client.servers(MODEL) if procs[e["url"]].poll() is None}
+    by_range = {(e["start"], e["end"]): u for u, e in live.items()}
+    urls = [by_range[(0, 3)], by_range[(3, 6)], by_range[(6, 8)]]
+    chain = RemoteSequential(urls)      # no registry
+    H = resolve_model(MODEL).hidden_size
+    with torch.inference_mode():
+        chain.forward("z", torch.zeros(1, 4, H, dtype=torch.bfloat16))
+        assert all(s.sessions() == ["z"] for s in chain.servers)
+        procs[urls[2]].send_signal(signal.SIGKILL)
+        procs[urls[2]].wait(10)
+        with pytest.raises(RuntimeError, match="no replacement"):
+            chain.forward("z", torch.zeros(1, 1, H, dtype=torch.bfloat16))
+    assert chain.servers[0].sessions() == [] and chain.servers[1].sessions() == []
