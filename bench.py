@@ -62,6 +62,8 @@ def parse():
                     help="LLM.int8 weights (the reference's 8-bit mode: int8 MFMA + bf16 outliers)")
     ap.add_argument("--kv-fp8", action="store_true", help="fp8-e4m3 KV cache")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--kernels", default="",
+                    help="kernel policy overrides (config.KernelPolicy), e.g. fp8_gemm4=gate_up")
     ap.add_argument("--num-layers", type=int, default=0,
                     help="REHEARSAL ONLY: the model's width with this many layers (e.g. 16 = 2 per "
                          "stage at PP=8, so 8 ranks x 9 micro-batches x 512 rows fit one GPU); the "
@@ -126,7 +128,8 @@ def main():
     import torch
     import torch.distributed as dist
     from distributed_llm_inference import _build
-    from distributed_llm_inference.config import CacheConfig, ServeConfig, resolve_model
+    from distributed_llm_inference.config import (CacheConfig, KernelPolicy, ServeConfig,
+                                                  resolve_model)
     from distributed_llm_inference.runtime.engine import EngineConfig, init_pipeline_rank
     from distributed_llm_inference.runtime.sequence import SamplingParams, Sequence
 
@@ -162,6 +165,7 @@ def main():
     total_len = a.prompt_len + max_tokens + 8
     cfg = EngineConfig(
         model=model, random_init=True, seed=0, quantize="int8" if a.int8 else a.fp8, pp=pp, dp=dp,
+        kernels=KernelPolicy().with_overrides(a.kernels),
         cache=CacheConfig(block_size=64, gpu_memory_utilization=0.92,
                           dtype="fp8" if a.kv_fp8 else "bf16"),
         serve=ServeConfig(max_batch_size=a.batch_per_mb, max_num_batched_tokens=a.max_batched_tokens,
@@ -280,6 +284,7 @@ def main():
         "p50_token_latency_ms": round(p50, 3),
         "p90_token_latency_ms": round(p90, 3),
         "transport": drv.tr.describe()["transport"] if (world > 1 and pp > 1) else "none",
+        "kernel_policy": a.kernels or "default",
         "micro_batches": M,
         "batch_per_micro_batch": a.batch_per_mb,
         "prompt_len": a.prompt_len,

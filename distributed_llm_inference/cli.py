@@ -49,14 +49,24 @@ def _common(ap: argparse.ArgumentParser) -> None:
     ap.add_argument("--max-seq-len", type=int, default=8192)
     ap.add_argument("--micro-batches", type=int, default=0)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--kernels", default="",
+                    help="kernel policy overrides, e.g. gemm4=0,fp8_gemm4=gate_up "
+                         "(config.KernelPolicy fields)")
+    ap.add_argument("--transport", default=None,
+                    choices=["rccl-or-ipc", "rccl", "rccl-or-host", "ipc", "host"],
+                    help="pipeline data plane (default rccl-or-ipc: RCCL on distinct GPUs, IPC "
+                         "when stages share one)")
     ap.add_argument("--tokenizer", default=None, help="HF tokenizer dir (local files only)")
     ap.add_argument("-v", "--verbose", action="store_true")
 
 
 def engine_config(a):
-    from .config import CacheConfig, ServeConfig
+    from .config import CacheConfig, KernelPolicy, ServeConfig
     from .runtime.engine import EngineConfig
+    if getattr(a, "transport", None):
+        os.environ["DLI_TRANSPORT"] = a.transport   # read by every rank's make_transport
     return EngineConfig(
+        kernels=KernelPolicy().with_overrides(getattr(a, "kernels", "")),
         model=a.model, checkpoint=a.checkpoint, random_init=a.checkpoint is None, seed=a.seed,
         quantize="fp8" if a.fp8 else ("int8" if a.int8 else False),
         int8_threshold=a.int8_threshold, pp=a.gpus // max(1, a.dp), dp=a.dp,

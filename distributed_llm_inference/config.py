@@ -378,6 +378,84 @@ class CacheConfig:
 
 
 @dataclass
+class KernelPolicy:
+    """Which hand-written kernel takes each hot-path product (read by ``ops`` at every call, so a
+    captured hipGraph keeps the choice it was captured with).  The defaults are the measured
+    winners; the fields exist for the trade-offs that are real and for A/B runs.  Set from
+    ``EngineConfig.kernels`` / ``distribute --kernels k=v,...`` / ``bench.py --kernels``; the
+    ``DLI_KERNELS`` environment variable (same syntax) overrides them."""
+
+    # bf16 decode projections on the one-wave-per-SIMD gemm4 kernel (else the 8-wave gemm_tile):
+    # 70B decode step 75.0 vs 77.7 ms (profiles/r4/gemm4_step_ab.txt)
+    gemm4: bool = True
+    # fp8 decode projections on gemm4 (block-scaled MFMA, fp8 k-loop schedule) instead of
+    # gemm_tile: "all", "none", or a "+"-separated subset of qkv / o / gate_up / down
+    fp8_gemm4: str = "none"
+    # split-K partials of the deferred projections (QKV, O, down) stored as bf16 (else fp32);
+    # consumers always sum in fp32 (profiles/bf16_partials_ab.txt, docs/parity.md C6)
+    bf16_partials: bool = True
+    # split-K partials summed by their consumer kernel (RMSNorm / RoPE / quantiser) instead of a
+    # reduce pass; with fp32 partials both are bit-identical (the tests' reference path)
+    defer_splitk: bool = True
+    # fp8: SwiGLU / attention outputs handed to the next projection as MX (e8m0 per 128-column
+    # block, quantised in the producer's epilogue) instead of bf16 + a per-row quantiser pass
+    fp8_mx: bool = True
+    # hand-written tile GEMMs for the decode projections at all (False: hipBLASLt everywhere)
+    tile_gemms: bool = True
+    # hipBLASLt for the products the tile kernels do not take well (M < 128, M > 2048, the LM
+    # head).  None = automatic: off when pipeline ranks share a GPU (DLI_SHARE_GPU), because its
+    # stream-K kernels wait on each other's workgroups (README "What else couples streams")
+    library_gemms: Optional[bool] = None
+    # run the partial last wave of whole-K bf16 gemm_tile products stream-K (neutral in-step)
+    stream_k_tail: bool = False
+    # 1-2 decode rows on the weight-streaming GEMVs, with the input RMSNorm, RoPE/KV write and
+    # SwiGLU fused into them (else the batch path)
+    gemv: bool = True
+    # ... with the RMSNorms fused into the QKV / gate|up GEMVs (bit-identical norm arithmetic)
+    gemv_norm: bool = True
+    # LLM.int8: a resident transposed int8 copy of every weight for the outlier-column gather
+    # (1.6 vs 2.9 ms per 70B step, but one more byte per weight: a third less KV capacity)
+    int8_transposed: bool = False
+
+    _FP8_SHAPES = ("qkv", "o", "gate_up", "down")
+
+    def __post_init__(self):
+        sel = self.fp8_gemm4
+        if sel not in ("all", "none") and any(
+                x not in self._FP8_SHAPES for x in sel.split("+")):
+            raise ValueError(f"fp8_gemm4={sel!r}: 'all', 'none' or a '+' list of "
+                             f"{'/'.join(self._FP8_SHAPES)}")
+
+    def fp8_on_gemm4(self, shape: str) -> bool:
+        return self.fp8_gemm4 == "all" or shape in self.fp8_gemm4.split("+")
+
+    def with_overrides(self, spec: str) -> "KernelPolicy":
+        """``"gemm4=0,library_gemms=auto"`` applied on top of this policy."""
+        if not spec or not spec.strip():
+            return self
+        kw: Dict[str, Any] = {}
+        names = {f.name: f for f in dataclasses.fields(self)}
+        for item in spec.split(","):
+            if not item.strip():
+                continue
+            k, _, v = item.partition("=")
+            k, v = k.strip(), v.strip()
+            if k not in names:
+                raise ValueError(f"unknown kernel policy field {k!r} (known: {sorted(names)})")
+            if k == "fp8_gemm4":
+                kw[k] = v
+            elif k == "library_gemms" and v.lower() in ("auto", "none", ""):
+                kw[k] = None
+            elif v.lower() in ("1", "true", "on", "yes"):
+                kw[k] = True
+            elif v.lower() in ("0", "false", "off", "no"):
+                kw[k] = False
+            else:
+                raise ValueError(f"kernel policy {k}={v!r}: expected 0/1")
+        return dataclasses.replace(self, **kw)
+
+
+@dataclass
 class ServeConfig:
     max_batch_size: int = 256
     max_num_batched_tokens: int = 8192

@@ -155,14 +155,6 @@ void gelu_bias(Tensor out, Tensor x, optional<Tensor> bias) {
   check_rc(dli::launch_gelu_bias(bp(out), bp(x), bb, (int)rows, (int)cols, cur_stream()), "gelu");
 }
 
-void l3_prefetch(Tensor t, int64_t nwg) {
-  CHECK_IN(t);
-  const size_t nb = (size_t)t.numel() * t.element_size();
-  TORCH_CHECK(nwg > 0 && nwg <= 4096, "l3_prefetch: 1 <= nwg <= 4096");
-  const c10::hip::HIPGuardMasqueradingAsCUDA g(t.device());
-  check_rc(dli::launch_l3_prefetch(t.data_ptr(), nb, (int)nwg, cur_stream()), "l3_prefetch");
-}
-
 void add(Tensor out, Tensor a, Tensor b) {
   CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
   CHECK_BF16(out); CHECK_BF16(a); CHECK_BF16(b);
@@ -318,9 +310,7 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
                  Tensor block_tables, Tensor seq_lens, double scale, int64_t n_sink,
                  int64_t sink_pad, int64_t ring, int64_t window, int64_t num_splits,
                  optional<Tensor> part_o, optional<Tensor> part_ml, double k_scale,
-                 double v_scale, optional<Tensor> out_q, optional<Tensor> out_mx,
-                 optional<Tensor> merge_cnt, optional<Tensor> prefetch, int64_t pf_split,
-                 int64_t pf_wgs) {
+                 double v_scale, optional<Tensor> out_q, optional<Tensor> out_mx) {
   int64_t D = 0;
   auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
                        sink_pad, ring, window, k_scale, v_scale, D, out_q.has_value());
@@ -328,11 +318,6 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
   TORCH_CHECK(seq_lens.numel() == B, "decode: one token per sequence (seq_lens must have T entries)");
   TORCH_CHECK(num_splits >= 1, "num_splits >= 1");
   p.num_splits = (int)num_splits;
-  static const int kv_nt = [] {   // DLI_KV_NT=1: non-temporal K/V loads (A/B switch)
-    const char* e = std::getenv("DLI_KV_NT");
-    return e != nullptr && e[0] == '1' ? 1 : 0;
-  }();
-  p.kv_nt = kv_nt;
   TORCH_CHECK(out_q.has_value() == out_mx.has_value(), "attn_decode: out_q and out_mx go together");
   if (out_q.has_value()) {   // MX fp8 output for the fp8 O projection
     CHECK_IN(*out_q); CHECK_IN(*out_mx);
@@ -351,23 +336,6 @@ void attn_decode(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache, 
     TORCH_CHECK(part_ml->numel() >= num_splits * B * p.nh * 2, "part_ml workspace too small");
     p.part_o = part_o->data_ptr<float>();
     p.part_ml = part_ml->data_ptr<float>();
-    if (merge_cnt.has_value()) {   // last-arrival merge instead of the combine kernel
-      CHECK_IN(*merge_cnt); CHECK_I32(*merge_cnt);
-      TORCH_CHECK(merge_cnt->numel() >= B * p.nh, "attn_decode: merge_cnt = int32 [B * nh], zeros");
-      p.merge_cnt = reinterpret_cast<unsigned*>(merge_cnt->data_ptr<int>());
-    }
-  }
-  if (prefetch.has_value() && pf_wgs > 0) {   // L3 warm-up of the next projection's weights
-    CHECK_IN(*prefetch);
-    const size_t nb = (size_t)prefetch->numel() * prefetch->element_size();
-    TORCH_CHECK(nb % 16 == 0 && reinterpret_cast<uintptr_t>(prefetch->data_ptr()) % 16 == 0,
-                "attn_decode: prefetch range must be 16-byte aligned");
-    TORCH_CHECK(pf_split >= 0 && pf_split % 16 == 0, "attn_decode: pf_split % 16 == 0");
-    TORCH_CHECK(pf_wgs <= 4096, "attn_decode: pf_wgs <= 4096");
-    p.pf_src = prefetch->data_ptr();
-    p.pf_bytes = nb;
-    p.pf_split = (size_t)pf_split;
-    p.pf_wgs = (int)pf_wgs;
   }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   check_rc(dli::launch_attn_decode(p, (int)B, (int)D, cur_stream()), "attn_decode");
@@ -947,145 +915,6 @@ void skinny_gemm_qkv_rope(Tensor q_out, Tensor x, Tensor w, optional<Tensor> wsc
 }
 
 
-// one Llama decoder layer for a single decode row, one persistent launch (decode_layer.hip)
-dli::DecodeProj decode_proj(const Tensor& w, const optional<Tensor>& ws, const optional<Tensor>& b,
-                            int& wq, const char* what) {
-  CHECK_IN(w);
-  TORCH_CHECK(w.dim() == 2, what, ": weight must be [N, K]");
-  const int q = w.scalar_type() == at::kBFloat16 ? 0 : w.scalar_type() == at::kChar ? 2
-                : w.element_size() == 1 ? 1 : -1;
-  TORCH_CHECK(q >= 0 && (wq < 0 || wq == q), what, ": bf16 / fp8 / int8 weights, one format per layer");
-  wq = q;
-  dli::DecodeProj d{};
-  d.w = w.data_ptr();
-  d.N = (int)w.size(0);
-  d.K = (int)w.size(1);
-  if (q != 0) {
-    TORCH_CHECK(ws.has_value(), what, ": 8-bit weights need their per-row scales");
-    CHECK_IN(*ws); CHECK_F32(*ws);
-    TORCH_CHECK(ws->numel() == d.N, what, ": scale must have N entries");
-    d.ws = ws->data_ptr<float>();
-  }
-  if (b.has_value()) {
-    CHECK_IN(*b); CHECK_BF16(*b);
-    TORCH_CHECK(b->numel() == d.N, what, ": bias must have N entries");
-    d.bias = bp(*b);
-  }
-  return d;
-}
-
-void decode_layer(Tensor h, optional<Tensor> r, Tensor res1, Tensor res2, Tensor out, Tensor ln1,
-                  Tensor ln2, double eps1, double eps2, Tensor w_qkv, optional<Tensor> s_qkv,
-                  optional<Tensor> b_qkv, Tensor w_o, optional<Tensor> s_o, optional<Tensor> b_o,
-                  Tensor w_gu, optional<Tensor> s_gu, optional<Tensor> b_gu, Tensor w_down,
-                  optional<Tensor> s_down, optional<Tensor> b_down, Tensor positions,
-                  Tensor slot_mapping, optional<Tensor> cos_sin, Tensor q_out, Tensor k_cache,
-                  Tensor v_cache, double k_scale, double v_scale, Tensor block_tables,
-                  Tensor seq_lens, double scale, int64_t num_splits, optional<Tensor> part_o,
-                  optional<Tensor> part_ml, Tensor attn, Tensor o_out, Tensor act, Tensor bar,
-                  optional<Tensor> stamps, int64_t flags) {
-  for (const Tensor* t : {&h, &res1, &res2, &out, &ln1, &ln2, &attn, &o_out, &act, &q_out}) {
-    CHECK_IN(*t); CHECK_BF16(*t);
-  }
-  const int64_t K = h.numel();
-  TORCH_CHECK(res1.numel() == K && res2.numel() == K && out.numel() == K && ln1.numel() == K &&
-                  ln2.numel() == K && o_out.numel() == K,
-              "decode_layer: hidden-size vectors");
-  if (r.has_value()) {
-    CHECK_IN(*r); CHECK_BF16(*r);
-    TORCH_CHECK(r->numel() == K, "decode_layer: residual size");
-    TORCH_CHECK(res1.data_ptr() != r->data_ptr() && res1.data_ptr() != h.data_ptr(),
-                "decode_layer: res1 must not alias the inputs");
-  } else {
-    TORCH_CHECK(res1.data_ptr() == h.data_ptr(), "decode_layer: first layer passes res1 = h");
-  }
-  TORCH_CHECK(res2.data_ptr() != res1.data_ptr(), "decode_layer: res2 must not alias res1");
-  CHECK_IN(bar);
-  TORCH_CHECK(bar.scalar_type() == at::kLong && bar.numel() >= 168,
-              "decode_layer: bar = int64 [168] (8 counters x 16, error word at 128, merge "
-              "counters from 136)");
-  int wq = -1;
-  dli::DecodeLayerParams p{};
-  p.qkv = decode_proj(w_qkv, s_qkv, b_qkv, wq, "decode_layer qkv");
-  p.o = decode_proj(w_o, s_o, b_o, wq, "decode_layer o");
-  p.gu = decode_proj(w_gu, s_gu, b_gu, wq, "decode_layer gate_up");
-  p.down = decode_proj(w_down, s_down, b_down, wq, "decode_layer down");
-  TORCH_CHECK(p.qkv.K == K && act.numel() == p.down.K, "decode_layer: projection shapes");
-  TORCH_CHECK(q_out.dim() == 3 && q_out.size(0) == 1, "decode_layer: q_out [1, nh, D]");
-  const int64_t nh = q_out.size(1), D = q_out.size(2);
-  TORCH_CHECK(attn.numel() == nh * D, "decode_layer: attn [nh * D]");
-  const int64_t nkv = (p.qkv.N / D - nh) / 2;
-  TORCH_CHECK(p.qkv.N == (nh + 2 * nkv) * D && nkv >= 1, "decode_layer: qkv rows");
-  // attention (B = 1) over q_out
-  Tensor qv = q_out.view({1, nh, D});
-  Tensor qo = qv;
-  optional<Tensor> no_sink = c10::nullopt;
-  int64_t Dq = 0;
-  dli::AttnParams ap = attn_common(qo, qv, no_sink, k_cache, v_cache, block_tables, seq_lens,
-                                   scale, 0, 0, 0, 0, k_scale, v_scale, Dq, false);
-  ap.out = nullptr;
-  TORCH_CHECK(seq_lens.numel() == 1 && num_splits >= 1, "decode_layer: one sequence");
-  ap.num_splits = (int)num_splits;
-  const int gs = num_splits % 4 == 0 ? 4 : num_splits % 2 == 0 ? 2 : 1;
-  if (num_splits / gs > 1) {
-    TORCH_CHECK(part_o.has_value() && part_ml.has_value(), "decode_layer: split workspaces");
-    CHECK_IN(*part_o); CHECK_IN(*part_ml); CHECK_F32(*part_o); CHECK_F32(*part_ml);
-    TORCH_CHECK(part_o->numel() >= num_splits / gs * nh * D && part_ml->numel() >= num_splits / gs * nh * 2,
-                "decode_layer: split workspaces too small");
-    ap.part_o = part_o->data_ptr<float>();
-    ap.part_ml = part_ml->data_ptr<float>();
-  }
-  // QKV epilogue
-  dli::GemvRope rp{};
-  rp.kv_fp8 = ap.kv_fp8;
-  rp.k_inv_scale = (float)(1.0 / k_scale);
-  rp.v_inv_scale = (float)(1.0 / v_scale);
-  CHECK_IN(positions); CHECK_I32(positions); CHECK_IN(slot_mapping); CHECK_I64(slot_mapping);
-  TORCH_CHECK(positions.numel() == 1 && slot_mapping.numel() == 1, "decode_layer: one row");
-  rp.positions = positions.data_ptr<int>();
-  rp.slot_mapping = reinterpret_cast<const long*>(slot_mapping.data_ptr<int64_t>());
-  if (cos_sin.has_value()) {
-    CHECK_IN(*cos_sin); CHECK_F32(*cos_sin);
-    TORCH_CHECK(cos_sin->dim() == 2 && cos_sin->size(1) == D, "cos_sin must be [max_pos, D]");
-    rp.cos_sin = cos_sin->data_ptr<float>();
-    rp.max_pos = (int)cos_sin->size(0);
-  }
-  rp.q_out = bp(q_out);
-  rp.k_cache = k_cache.data_ptr();
-  rp.v_cache = v_cache.data_ptr();
-  rp.nh = (int)nh;
-  rp.nkv = (int)nkv;
-  rp.D = (int)D;
-  rp.bs = (int)k_cache.size(2);
-  p.h = bp(h);
-  p.r = r.has_value() ? bp(*r) : nullptr;
-  p.res1 = bp(res1);
-  p.res2 = bp(res2);
-  p.out = bp(out);
-  p.ln1 = bp(ln1);
-  p.ln2 = bp(ln2);
-  p.eps1 = (float)eps1;
-  p.eps2 = (float)eps2;
-  p.rp = rp;
-  p.ap = ap;
-  p.gs = gs;
-  p.attn = bp(attn);
-  p.o_out = bp(o_out);
-  p.act = bp(act);
-  p.bar = reinterpret_cast<unsigned long long*>(bar.data_ptr<int64_t>());
-  p.err = reinterpret_cast<unsigned*>(bar.data_ptr<int64_t>() + 128);
-  p.merge_cnt = (flags & 2) ? nullptr : reinterpret_cast<unsigned*>(bar.data_ptr<int64_t>() + 136);
-  if (stamps.has_value()) {
-    CHECK_IN(*stamps);
-    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->numel() >= 24 * dli::decode_layer_grid(),
-                "decode_layer: stamps = int64 [grid * 24]");
-    p.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
-  }
-  p.flags = (int)flags;
-  const c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
-  check_rc(dli::launch_decode_layer(p, wq, cur_stream()), "decode_layer");
-}
-
 }  // namespace
 
 void register_rccl(pybind11::module_& m);  // comm/rccl_p2p.hip
@@ -1108,11 +937,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("block_tables"), py::arg("seq_lens"), py::arg("scale"), py::arg("n_sink"),
         py::arg("sink_pad"), py::arg("ring"), py::arg("window"), py::arg("num_splits"),
         py::arg("part_o"), py::arg("part_ml"), py::arg("k_scale"), py::arg("v_scale"),
-        py::arg("out_q") = py::none(), py::arg("out_mx") = py::none(),
-        py::arg("merge_cnt") = py::none(), py::arg("prefetch") = py::none(),
-        py::arg("pf_split") = 0, py::arg("pf_wgs") = 0);
-  m.def("l3_prefetch", &l3_prefetch, "read a tensor on nwg workgroups and discard it "
-        "(Infinity-Cache warm-up)", py::arg("t"), py::arg("nwg"));
+        py::arg("out_q") = py::none(), py::arg("out_mx") = py::none());
   m.def("attn_prefill", &attn_prefill, "paged causal prefill attention (varlen)", py::arg("out"),
         py::arg("q"), py::arg("q_sink"), py::arg("k_cache"), py::arg("v_cache"),
         py::arg("block_tables"), py::arg("seq_lens"), py::arg("q_start"), py::arg("max_q"),
@@ -1152,9 +977,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("v_cache"), py::arg("nh"), py::arg("nkv"), py::arg("k_scale") = 1.0,
         py::arg("v_scale") = 1.0, py::arg("norm_w") = py::none(), py::arg("res_in") = py::none(),
         py::arg("res_out") = py::none(), py::arg("eps") = 1e-5);
-  m.def("decode_layer", &decode_layer,
-        "one Llama decoder layer for a single decode row in one persistent launch (decode_layer.hip)");
-  m.def("decode_layer_grid", &dli::decode_layer_grid, "workgroups of a decode_layer launch (CUs)");
   m.def("gemm4", &gemm4, "C = A . B^T, one-wave-per-SIMD 256x256 MFMA tile GEMM (gemm4.hip)",
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
         py::arg("epilogue") = 0, py::arg("grid") = 0, py::arg("a_scale") = py::none(),

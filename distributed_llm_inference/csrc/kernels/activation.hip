@@ -101,18 +101,6 @@ int launch_gelu_bias(bf16* out, const bf16* x, const bf16* bias, int rows, int c
   return 0;
 }
 
-__global__ void __launch_bounds__(256) l3_prefetch_kernel(const void* src, size_t bytes, int never,
-                                                          unsigned* sink) {
-  l3_touch(src, bytes, blockIdx.x, gridDim.x, never, sink);
-}
-
-int launch_l3_prefetch(const void* src, size_t bytes, int nwg, hipStream_t stream) {
-  if (bytes % 16 != 0 || reinterpret_cast<uintptr_t>(src) % 16 != 0 || nwg <= 0) return -1;
-  if (bytes == 0) return 0;
-  l3_prefetch_kernel<<<nwg, 256, 0, stream>>>(src, bytes, 0, nullptr);
-  return 0;
-}
-
 int launch_add(bf16* out, const bf16* a, const bf16* b, size_t n, hipStream_t stream) {
   if (n % 8 != 0) return -1;
   if (n == 0) return 0;

@@ -41,26 +41,18 @@ namespace dli {
 //     puts several waves on every CU): the workgroup's waves hold `gs` (4 or 2) consecutive
 //     splits of one item and merge them through LDS (online-softmax rescale, padded O^T image),
 //     so only num_splits / gs partials per head go to HBM — and none when num_splits == gs;
-//     attn_combine_kernel merges what is left — or (round 4, head dim 128, opt-in
-//     DLI_ATTN_MERGE=1) the last-arriving workgroup of each head group does, with the combine kernel's
-//     arithmetic: partials are stored write-through at device scope (no L2 write-back, which is
-//     what made round 2's agent-scope-release version 5-75 % slower than the launch), one
-//     relaxed arrival counter per head group after the stores complete, and the merging
-//     workgroup reads the partials with device-scope loads and resets its counter.  Measured
-//     still slower than the launch at B = 1 (600 keys 11.3 vs 10.6 us, 8k keys 28.1 vs 15.0 us:
-//     one workgroup merging up to 32 partials serially), hence opt-in.
+//     attn_combine_kernel merges what is left.  (A last-arrival merge inside this kernel was
+//     measured slower than the combine launch at B = 1 - 600 keys 11.3 vs 10.6 us, 8k keys
+//     28.1 vs 15.0 us, one workgroup merging up to 32 partials serially - and lives in
+//     scripts/experiments/.)
 // ===========================================================================================
-template <int D, bool WIN, bool FP8, bool GRP, bool NT = false>
+template <int D, bool WIN, bool FP8, bool GRP>
 __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int items, int gs) {
   // GRP (num_splits > 1): the `gs` consecutive splits of one work item that share this
   // workgroup are merged in LDS, so only num_splits / gs partials per head reach global memory
   // (none when gs == num_splits: the workgroup writes the normalised output itself)
   constexpr int LROW = D + 4;  // padded O^T column: conflict-free ds_write_b128
   __shared__ __attribute__((aligned(16))) float lds[GRP ? 4 * 16 * (LROW + 2) : 1];
-  if (p.pf_wgs > 0 && (int)blockIdx.x >= (int)gridDim.x - p.pf_wgs) {   // L3 warm-up workgroups
-    l3_touch(p.pf_src, p.pf_bytes, blockIdx.x - (gridDim.x - p.pf_wgs), p.pf_wgs, p.pf_never, nullptr);
-    return;
-  }
   const int wave = threadIdx.x >> 6;
   const int item_raw = blockIdx.x * 4 + wave;
   const bool live = item_raw < items;
@@ -70,7 +62,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
   // of the K/V prefetch
   const int item = __builtin_amdgcn_readfirstlane(live ? item_raw : items - 1);
   WaveState<D> st;
-  const DecodeItem di = attn_decode_item<D, WIN, FP8, NT>(p, item, live, st);
+  const DecodeItem di = attn_decode_item<D, WIN, FP8, false>(p, item, live, st);
   const int splits = p.num_splits, split = di.split, G = di.G, hgroups = di.hgroups;
   const int g0 = di.g0, kvh = di.kvh, b = di.b;
   const int lane = threadIdx.x & 63, col = lane & 15, h4 = lane >> 4;
@@ -192,14 +184,6 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = (bf16)(O[r] * inv);
         *reinterpret_cast<bf16x4*>(p.out + ((size_t)b * p.nh + head) * D + d4) = v;
-      } else if (D == 128 && p.merge_cnt != nullptr && gs == 4) {   // write-through: the merging
-        // group may be on another XCD
-        const size_t r0 = ((size_t)s2 * B + b) * p.nh + head;
-        gst<true>(reinterpret_cast<f32x4*>(p.part_o + r0 * D + d4), O * vsc);
-        if (d4 == 0) {
-          gst<true>(p.part_ml + r0 * 2, M);
-          gst<true>(p.part_ml + r0 * 2 + 1, Lt);
-        }
       } else {
         const size_t r0 = ((size_t)s2 * B + b) * p.nh + head;
         *reinterpret_cast<f32x4*>(p.part_o + r0 * D + d4) = O * vsc;
@@ -208,84 +192,6 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
           p.part_ml[r0 * 2 + 1] = Lt;
         }
       }
-    }
-    // ---- last arrival merges (merge_cnt, gs == 4: the whole workgroup is one group) ----
-    const int S2m = splits / gs;
-    if (D == 128 && p.merge_cnt != nullptr && gs == 4 && S2m > 1) {   // (D < 128: 16-32 lane
-      // groups in the combine, too many registers for the merge's per-group state)
-      __shared__ int is_last;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's partial stores completed
-      __syncthreads();
-      const int ctr = ((int)b * p.nkv + kvh) * hgroups + g0 / 16;
-      if (threadIdx.x == 0)
-        is_last = __hip_atomic_fetch_add(p.merge_cnt + ctr, 1u, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S2m - 1);
-      __syncthreads();
-      if (!is_last) return;
-      // attn_combine_kernel's arithmetic: its 256 / (D / 4) lane groups take partials g, g + NG,
-      // ...; each group's running merge, then the in-order merge of the group states.  Partials
-      // are read at device scope (sc1): written write-through by workgroups on other XCDs
-      constexpr int NG = 256 / (D / 4);
-      const auto rso = __builtin_amdgcn_make_buffer_rsrc(p.part_o, 0, 0x7fffffff, 0x00020000);
-      const auto rsm = __builtin_amdgcn_make_buffer_rsrc(p.part_ml, 0, 0x7fffffff, 0x00020000);
-      const int nheads = min(16, G - g0);
-      for (int idx = threadIdx.x; idx < nheads * (D / 4); idx += blockDim.x) {
-        const int head = kvh * G + g0 + idx / (D / 4), l4 = idx % (D / 4);
-        float gm[NG], gsum[NG];
-        f32x4 go[NG];
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          gm[g] = -1e30f;
-          gsum[g] = 0.f;
-          go[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        for (int base = 0; base < S2m; base += NG) {
-#pragma unroll
-          for (int half = 0; half < NG; half += 4) {
-            float mi[4], li[4];
-            f32x4 oi[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              if (base + half + j < S2m) {
-                const int r = (int)(((size_t)(base + half + j) * B + b) * p.nh + head);
-                mi[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsm, r * 8, 0, 16));
-                li[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsm, r * 8 + 4, 0, 16));
-                oi[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      rso, (r * D + 4 * l4) * 4, 0, 16));
-              }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int g = half + j;
-              if (base + g < S2m) {
-                const float mn = fmaxf(gm[g], mi[j]);
-                const float e0 = __builtin_amdgcn_exp2f(gm[g] - mn), e1 = __builtin_amdgcn_exp2f(mi[j] - mn);
-                go[g] = go[g] * e0 + oi[j] * e1;
-                gsum[g] = gsum[g] * e0 + li[j] * e1;
-                gm[g] = mn;
-              }
-            }
-          }
-        }
-        float Mx = -1e30f;
-#pragma unroll
-        for (int g = 0; g < NG; ++g) Mx = fmaxf(Mx, gm[g]);
-        float Lx = 0.f;
-        f32x4 Ox = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          const float f = __builtin_amdgcn_exp2f(gm[g] - Mx);
-          Lx += f * gsum[g];
-          Ox += f * go[g];
-        }
-        const float inv = Lx > 0.f ? 1.f / Lx : 0.f;
-        bf16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (bf16)(Ox[r] * inv);
-        *reinterpret_cast<bf16x4*>(p.out + ((size_t)b * p.nh + head) * D + 4 * l4) = v;
-      }
-      if (threadIdx.x == 0)   // ready for the next launch (every group of this counter arrived)
-        __hip_atomic_store(p.merge_cnt + ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -299,10 +205,6 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(AttnParams p, int T) 
   constexpr int LG = D / 4, NG = 256 / LG;
   __shared__ f32x4 so[NG][LG];
   __shared__ float sml[NG][2];
-  if (p.pf_wgs > 0 && (int)blockIdx.x >= (int)gridDim.x - p.pf_wgs) {   // L3 warm-up workgroups
-    l3_touch(p.pf_src, p.pf_bytes, blockIdx.x - (gridDim.x - p.pf_wgs), p.pf_wgs, p.pf_never, nullptr);
-    return;
-  }
   const int th = blockIdx.x;  // t * nh + head
   const int grp = threadIdx.x / LG, l = threadIdx.x % LG;
   const size_t stride = (size_t)T * p.nh;
@@ -661,11 +563,9 @@ __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_ke
 // ------------------------------------------------------------------------------------------
 template <int D, bool WIN, bool FP8>
 static void decode_grid(const AttnParams& p, int items, int gs, hipStream_t stream) {
-  const int grid = (items + 3) / 4 + p.pf_wgs;
+  const int grid = (items + 3) / 4;
   if (p.num_splits > 1)
     attn_decode_kernel<D, WIN, FP8, true><<<grid, 256, 0, stream>>>(p, items, gs);
-  else if (!FP8 && !WIN && p.kv_nt)   // large-batch bf16 full-cache decode: non-temporal stream
-    attn_decode_kernel<D, false, false, false, true><<<grid, 256, 0, stream>>>(p, items, 1);
   else
     attn_decode_kernel<D, WIN, FP8, false><<<grid, 256, 0, stream>>>(p, items, 1);
 }
@@ -678,25 +578,17 @@ static int launch_decode_d(const AttnParams& p, int B, hipStream_t stream) {
   if (items > (1L << 30)) return -3;
   // splits merged inside a workgroup (its 4 waves hold consecutive splits of one item)
   const int gs = p.num_splits % 4 == 0 ? 4 : p.num_splits % 2 == 0 ? 2 : 1;
-  const bool combine = p.num_splits > gs && !(D == 128 && p.merge_cnt != nullptr && gs == 4);
-  AttnParams pa = p;   // L3 warm-up share of the attention launch (all of it without a combine)
-  if (p.pf_bytes == 0) pa.pf_wgs = 0;
-  else if (combine) pa.pf_bytes = p.pf_split < p.pf_bytes ? p.pf_split : p.pf_bytes;
-  if (pa.pf_bytes == 0) pa.pf_wgs = 0;
   if (p.ring > 0) {
-    if (p.kv_fp8) decode_grid<D, true, true>(pa, (int)items, gs, stream);
-    else decode_grid<D, true, false>(pa, (int)items, gs, stream);
+    if (p.kv_fp8) decode_grid<D, true, true>(p, (int)items, gs, stream);
+    else decode_grid<D, true, false>(p, (int)items, gs, stream);
   } else {
-    if (p.kv_fp8) decode_grid<D, false, true>(pa, (int)items, gs, stream);
-    else decode_grid<D, false, false>(pa, (int)items, gs, stream);
+    if (p.kv_fp8) decode_grid<D, false, true>(p, (int)items, gs, stream);
+    else decode_grid<D, false, false>(p, (int)items, gs, stream);
   }
-  if (combine) {
+  if (p.num_splits > gs) {
     AttnParams pc = p;
     pc.num_splits = p.num_splits / gs;
-    pc.pf_src = static_cast<const char*>(p.pf_src) + pa.pf_bytes;
-    pc.pf_bytes = p.pf_bytes - pa.pf_bytes;
-    if (pc.pf_bytes == 0) pc.pf_wgs = 0;
-    attn_combine_kernel<D><<<B * p.nh + pc.pf_wgs, 256, 0, stream>>>(pc, B);
+    attn_combine_kernel<D><<<B * p.nh, 256, 0, stream>>>(pc, B);
   }
   return 0;
 }

@@ -62,34 +62,6 @@ __device__ __forceinline__ void gst(T* p, T v) {
   }
 }
 
-// Infinity-Cache (L3) warm-up: workgroup `wg` of `nwg` reads its contiguous share of
-// [src, src + bytes) (16-byte aligned, bytes % 16 == 0) and discards it, so that a later kernel
-// streaming the range (a batch-1 GEMV's weights) reads it from the 256 MiB L3 instead of HBM.
-// 16 x 16-B loads in flight per lane (64 KiB per 256-thread workgroup).  The xor of what was read
-// is stored only when `never` is nonzero -- it never is; that keeps the loads alive.
-__device__ __forceinline__ void l3_touch(const void* src, size_t bytes, int wg, int nwg, int never,
-                                         unsigned* sink) {
-  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-  const u32x4_t* s = reinterpret_cast<const u32x4_t*>(src);
-  const size_t n = bytes >> 4;
-  const size_t per = (n + nwg - 1) / nwg;
-  const size_t lo = (size_t)wg * per;
-  const size_t hi = lo + per < n ? lo + per : n;
-  constexpr int U = 16;
-  u32x4_t acc = {0u, 0u, 0u, 0u};
-  for (size_t i = lo + threadIdx.x; i < hi; i += (size_t)U * blockDim.x) {
-    u32x4_t v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const size_t j = i + (size_t)u * blockDim.x;
-      v[u] = j < hi ? s[j] : u32x4_t{0u, 0u, 0u, 0u};
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) acc ^= v[u];
-  }
-  if (never) sink[threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
-}
-
 // Block-wide sum of one float per thread.  `scratch` must hold >= blockDim.x/64 floats.
 // Split-K partials consumed in place of a reduce pass (gemm_tile.hip kStoreF32 slabs).  NS
 // partials of N consecutive fp32 elements, all loads issued before the adds (NS is a compile-time
@@ -259,7 +231,7 @@ __device__ __forceinline__ void load_row_vecs(bf16x8 (&a)[VPT], const bf16* x, c
 }
 
 // dispatch a runtime split count 1..8 to a compile-time NS (0 = no partials)
-#define DLI_SPLITS_SWITCH(splits, MACRO) \
+#define SPLITS_SWITCH(splits, MACRO) \
   switch (splits) {                      \
     case 0: MACRO(0); break;             \
     case 1: MACRO(1); break;             \
@@ -355,7 +327,7 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 
 }  // namespace dli
 
-#define DLI_HIP_CHECK(expr)                                                         \
+#define CHECK_HIP(expr)                                                         \
   do {                                                                              \
     hipError_t _e = (expr);                                                         \
     if (_e != hipSuccess) {                                                         \

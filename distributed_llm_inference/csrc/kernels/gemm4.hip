@@ -64,46 +64,18 @@ __device__ __forceinline__ void g4_static_for(std::integer_sequence<int, I...>, 
 // before b2), P reads at p0 + ps*n.  Constraints: Q reads < b1 < d0, pieces before b2 == vm,
 // b2 < p0, the last P read leaves the tail of the k-tile to retire it.
 template <int V> struct G4Sched;
-template <> struct G4Sched<0> {   // DMA in k-step 1, early wait (lead ~0.9 k-tile)
-  static constexpr int q0 = 2, qs = 2, b1 = 47, d0 = 64, ds = 2, b2 = 79, vm = 8, p0 = 81, ps = 2;
-};
-template <> struct G4Sched<1> {   // DMA right after B1 in k-step 0, wait in k-step 1 (lead ~1.25)
-  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 2, b2 = 88, vm = 16, p0 = 89, ps = 2;
-};
-template <> struct G4Sched<2> {   // hipBLASLt-like: late wait, dense P reads (lead ~1.4)
-  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 3, b2 = 104, vm = 16, p0 = 105, ps = 1;
-};
-template <> struct G4Sched<3> {   // dense Q reads, early DMA
-  static constexpr int q0 = 0, qs = 1, b1 = 24, d0 = 25, ds = 2, b2 = 80, vm = 16, p0 = 81, ps = 2;
-};
 template <> struct G4Sched<4> {   // late wait, DMA spread thin (1 per 4 MFMAs), dense P reads
   static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 4, b2 = 104, vm = 16, p0 = 105, ps = 1;
-};
-template <> struct G4Sched<5> {   // dense Q reads, early B1, DMA 1 per 3, late wait
-  static constexpr int q0 = 0, qs = 1, b1 = 20, d0 = 21, ds = 3, b2 = 96, vm = 16, p0 = 97, ps = 1;
 };
 template <> struct G4Sched<6> {   // v4 with the DMA spread over B2 (1 per 6 MFMAs, 12 before it)
   static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 6, b2 = 104, vm = 12, p0 = 105, ps = 1;
 };
-template <> struct G4Sched<7> {   // v4 with the DMA 1 per 5 MFMAs (14 before B2)
-  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 5, b2 = 104, vm = 14, p0 = 105, ps = 1;
-};
-// bfirst: the weight (B) pieces of a stage go out before the activation (A) pieces -- at decode M
-// the activations are L2-resident and the weights stream from HBM, so the HBM loads get the
-// longest lead before the barrier that waits for them
-template <> struct G4Sched<8> {   // v6, weights first
-  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 6, b2 = 104, vm = 12, p0 = 105, ps = 1;
-  static constexpr bool bfirst = true;
-};
-template <> struct G4Sched<9> {   // v4, weights first
-  static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 4, b2 = 104, vm = 16, p0 = 105, ps = 1;
-  static constexpr bool bfirst = true;
-};
+// (the other eight schedules of the round-4 A/B, profiles/r4/gemm4_ab_v0-7.txt, are in
+// scripts/experiments/gemm4_sched_variants.h)
 template <typename S, typename = void> struct G4BFirst { static constexpr bool value = false; };
 template <typename S> struct G4BFirst<S, std::void_t<decltype(S::bfirst)>> {
   static constexpr bool value = S::bfirst;
 };
-constexpr int kG4Variants = 10;
 // Default schedules (profiles/r4/gemm4_ab_v0-7.txt): decode-sized M (<= 2 row tiles, the
 // activations stay L2 / MALL-resident and only the weight stream misses) takes v6, whose DMA runs
 // the latest and thinnest (gate|up 377 vs 415 us gemm_tile, down 187 vs 199); larger M, where
@@ -173,7 +145,7 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
   const char* B = reinterpret_cast<const char*>(Bv);
   __shared__ __attribute__((aligned(1024))) char smem[2 * kG4Stage];
   const int tid = threadIdx.x, lane = tid & 63;
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
   // diagnostic builds only (scripts/experiments/gemm4_bench.hip): begin / end-of-last-k-loop /
   // end stamps per workgroup, shader cycles and 100 MHz wall ticks (g_stamp_blk: gemm_tile.hip)
   unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
@@ -377,7 +349,7 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
     if (t + 1 < T) ktile(t++, G4B<false>{}, G4B<true>{});
     ktile(t, G4B<false>{}, G4B<false>{});
 
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
     if (tid == 0) {
       st[6] = __builtin_amdgcn_s_memrealtime();
       st[7] = __builtin_amdgcn_s_memtime();
@@ -503,7 +475,7 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
     // (lgkmcnt(0) in the last k-tile), the barrier makes that hold for all of them
     g4_barrier();
   }
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
   if (tid == 0) {
     st[2] = __builtin_amdgcn_s_memrealtime();
     st[3] = __builtin_amdgcn_s_memtime();
@@ -559,26 +531,10 @@ template <int PREC>
 static int launch_gemm4_p(void* C, const void* a, const void* b, int M, int N, int K, int tiles_m,
                           int tiles_n, int kps, int splits, int epilogue, int grid,
                           hipStream_t stream, int variant, const float* sa, const float* sb) {
-#ifndef DLI_GEMM4_ALL_VARIANTS   // the library carries the default schedules only
   if (variant == kG4DecodeDefault)
     return launch_gemm4_v<kG4DecodeDefault, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
   if (variant != kG4Default) return -5;
   return launch_gemm4_v<kG4Default, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
-#else
-  switch (variant) {
-    case 0: return launch_gemm4_v<0, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
-    case 1: return launch_gemm4_v<1, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
-    case 2: return launch_gemm4_v<2, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
-    case 3: return launch_gemm4_v<3, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
-    case 4: return launch_gemm4_v<4, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
-    case 5: return launch_gemm4_v<5, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
-    case 6: return launch_gemm4_v<6, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
-    case 7: return launch_gemm4_v<7, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
-    case 8: return launch_gemm4_v<8, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
-    case 9: return launch_gemm4_v<9, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
-  }
-  return -5;
-#endif
 }
 
 // C = A . B^T on the one-wave-per-SIMD kernel.  epilogue 0: bf16 [M, N]; 2: fused SwiGLU ([M,

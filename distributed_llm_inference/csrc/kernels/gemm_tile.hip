@@ -61,7 +61,7 @@ constexpr int kBuf = 4 * kHalf;        // A0 A1 B0 B1
 constexpr int kLds = 2 * kBuf;         // double buffer: 128 KB
 
 // kStoreBf16Part: split-K partials rounded to bf16 (half the partial bytes of kStoreF32 for the
-// consumers that sum them; default for 8-bit operands, DLI_BF16_PARTS for bf16 ones)
+// consumers that sum them; the default for every precision)
 enum Epilogue { kStoreBf16 = 0, kStoreF32 = 1, kSwiGLU = 2, kSwiGLUMx = 3, kStoreBf16Part = 4 };
 
 // stream-K workspace header: flags [0, kSkMaxWgs), error counter at kSkErrWord, slabs after
@@ -158,7 +158,7 @@ struct SkArgs {
   unsigned* flags;   // [sk_wgs] publish flags, zeroed by a memset node before every launch
   unsigned* err;     // spin-timeout counter (diagnostic; tests zero it once)
   float* slabs;      // [sk_wgs][256 * 256] fp32 partials in accumulator (register) order
-  int gm = 8;        // M-tiles per group of the grouped tile order (DLI_GEMM_GM, experiments)
+  int gm = 8;        // M-tiles per group of the grouped tile order (measured best: 4-8)
 };
 
 // LLM.int8 outlier columns (int8 precision only): the bf16 product x_out [M, J] . w_out [N, J]^T
@@ -177,7 +177,7 @@ struct OutlierArgs {
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
 // Diagnostic builds only (scripts/experiments/gemm_stamps.hip, gemm_w4_bench.hip): per-workgroup
 // clock stamps (begin / end shader cycles and 100 MHz wall ticks, end of the main loop).  Never
 // compiled into the extension.
@@ -208,7 +208,7 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
   __shared__ __attribute__((aligned(1024))) char smem[kLds + (MX ? kMxLds : 0)];
 
   const int tid0 = threadIdx.x;
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
   if (tid0 == 0) {
     unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
     st[0] = __builtin_amdgcn_s_memrealtime();
@@ -460,7 +460,7 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
       barrier();
     }
     if (wr == 0) barrier();
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
     if (tid0 == 0) {
       unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
       st[6] = __builtin_amdgcn_s_memrealtime();
@@ -683,7 +683,7 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
       }
     }
   }
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
   if (tid0 == 0) {
     unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
     st[2] = __builtin_amdgcn_s_memrealtime();
@@ -731,7 +731,6 @@ int launch_whole_impl(void* C, const void* A, const void* B, const float* sa, co
                       int tiles, int tiles_m, int tiles_n, hipStream_t stream, OutlierArgs ol,
                       MxArgs mx) {
   SkArgs sk{0, 0, nullptr, nullptr, nullptr};
-  if (const char* g = getenv("DLI_GEMM_GM")) sk.gm = atoi(g) > 0 ? atoi(g) : 8;
   if (epilogue == kStoreBf16Part) {   // bf16 partials into C [splits, M, N]; the consumer sums
     if (splits < 2) return -3;
     sk.n_dp = tiles * splits;   // the block remap covers the whole grid
@@ -771,12 +770,9 @@ int launch_whole_impl(void* C, const void* A, const void* B, const float* sa, co
   return 0;
 }
 
-// non-temporal weight loads (gemm_tile_kernel VAR bit 0) for tiles_m <= 2; DLI_GEMM_BNT=0 turns
-// them off (read per launch, so a captured graph keeps the choice it was captured with)
-bool weights_nt(int tiles_m) {
-  const char* e = getenv("DLI_GEMM_BNT");
-  return tiles_m <= 2 && !(e != nullptr && e[0] == '0');
-}
+// non-temporal weight loads (gemm_tile_kernel VAR bit 0) for tiles_m <= 2: each weight byte is
+// read at most twice (profiles/gemm_var_nt_group_ab.json)
+bool weights_nt(int tiles_m) { return tiles_m <= 2; }
 
 // splits == 0: data-parallel whole tiles + stream-K tail (SkArgs); workspace = the
 // gemm_tile_sk_workspace_floats() layout: [flags | err | pad] 4 KB, then sk_wgs fp32 slabs.

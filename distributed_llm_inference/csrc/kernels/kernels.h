@@ -34,19 +34,6 @@ struct AttnParams {
   // mask_q - qlen_b + t (the last qlen_b rows), key k column k.  No causal mask is added.
   const float* mask = nullptr;
   int mask_heads = 0, mask_q = 0, mask_k = 0;
-  // decode, bf16 full cache, one split: load K / V non-temporally (streamed once per step)
-  int kv_nt = 0;
-  // decode with 4-split groups and more partials than groups: per (sequence, kv head, head
-  // group) arrival counters [B * nkv * hgroups], zero between launches; the last group to store
-  // its partial merges them all (no attn_combine_kernel launch).  nullptr: combine kernel
-  unsigned* merge_cnt = nullptr;
-  // decode: Infinity-Cache warm-up of the next projection's weights while HBM is otherwise idle
-  // (batch-1 attention reads a few MB of K/V): pf_wgs extra workgroups per launch read
-  // [pf_src, pf_src + pf_bytes) and discard it -- the first pf_split bytes in the attention launch,
-  // the rest in the combine launch when there is one.  pf_never is 0 (keeps the loads alive).
-  const void* pf_src = nullptr;
-  size_t pf_bytes = 0, pf_split = 0;
-  int pf_wgs = 0, pf_never = 0;
 };
 
 struct RopeCacheParams {
@@ -99,8 +86,6 @@ int launch_silu_mul(bf16* out, const bf16* x, int rows, int inter, bool interlea
 int launch_gelu_bias(bf16* out, const bf16* x, const bf16* bias, int rows, int cols,
                      hipStream_t stream);
 int launch_add(bf16* out, const bf16* a, const bf16* b, size_t n, hipStream_t stream);
-// read [src, src + bytes) on nwg workgroups and discard it (Infinity-Cache warm-up)
-int launch_l3_prefetch(const void* src, size_t bytes, int nwg, hipStream_t stream);
 int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stream);
 int launch_attn_decode(const AttnParams& p, int B, int D, hipStream_t stream);
 int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_t stream);
@@ -138,37 +123,6 @@ struct GemvRope {
   float k_inv_scale, v_inv_scale;
   int nh, nkv, D, bs;
 };
-// One Llama decoder layer for a single decode row in one persistent launch (decode_layer.hip).
-struct DecodeProj {
-  const void* w;       // [N, K]: bf16, fp8 e4m3 or int8
-  const float* ws;     // [N] per-row scale (8-bit weights) or nullptr
-  const bf16* bias;    // [N] or nullptr
-  int N, K;
-};
-struct DecodeLayerParams {
-  const bf16* h;        // [K] layer input (previous down output, or the embedding)
-  const bf16* r;        // [K] residual stream, or nullptr (first layer: h is the residual)
-  bf16* res1;           // [K] h + r (== h when r is nullptr: not written then)
-  bf16* res2;           // [K] o_out + res1 (the layer's residual output)
-  bf16* out;            // [K] down output (the layer's hidden output)
-  const bf16* ln1;
-  const bf16* ln2;
-  float eps1, eps2;
-  DecodeProj qkv, o, gu, down;   // gu: swiglu_interleave'd gate|up
-  GemvRope rp;          // QKV epilogue: q -> rp.q_out, k / v -> the paged caches
-  AttnParams ap;        // decode attention over rp.q_out (B = 1), split partials
-  int gs;               // splits merged per 4-wave group
-  bf16* attn;           // [nh * D] scratch
-  bf16* o_out;          // [K] scratch
-  bf16* act;            // [I] scratch
-  unsigned long long* bar;   // grid-barrier arrival counters [8][16] (zero once, never reset)
-  unsigned* err;        // barrier spin-timeout count (0 = every barrier completed)
-  unsigned long long* stamps = nullptr;   // diagnostics: [grid][24] 100 MHz wall ticks per phase
-  int flags = 0;        // bit 0: issue the O weights' first chunk at the attention barrier
-  unsigned* merge_cnt = nullptr;   // [64] attention-merge arrival counters (zeroed in-kernel)
-};
-int launch_decode_layer(const DecodeLayerParams& p, int wq, hipStream_t stream);
-int decode_layer_grid();
 int launch_skinny_gemm_fp8(bf16* y, const void* x, const float* xscale, const uint8_t* W,
                            const float* wscale, const bf16* bias, int M, int N, int K,
                            hipStream_t stream, bool swiglu = false, const GemvNorm* nm = nullptr,

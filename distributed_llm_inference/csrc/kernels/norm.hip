@@ -154,7 +154,7 @@ static inline int norm_threads(int hidden) {
   return t > 256 ? 256 : t;
 }
 
-#define DLI_NORM_DISPATCH(KERNEL, ...)                                                    \
+#define NORM_DISPATCH(KERNEL, ...)                                                    \
   do {                                                                                    \
     const int nvec = hidden / 8;                                                          \
     const int threads = norm_threads(hidden);                                             \
@@ -179,25 +179,25 @@ int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* res
   const int threads = norm_threads(hidden);
   const int vpt = (nvec + threads - 1) / threads;
   if (vpt > 8) return -1;
-#define DLI_RMS_V(V, NS, PB)                                                           \
+#define RMS_LAUNCH_V(V, NS, PB)                                                           \
   rms_norm_kernel<V, NS, PB><<<rows, threads, 0, stream>>>(out, x, residual_in, residual_out, \
                                                            w, eps, hidden, add, x_parts, stride)
-#define DLI_RMS_PB(NS, PB)                      \
+#define RMS_LAUNCH_PB(NS, PB)                      \
   do {                                          \
-    if (vpt <= 1) DLI_RMS_V(1, NS, PB);         \
-    else if (vpt <= 2) DLI_RMS_V(2, NS, PB);    \
-    else if (vpt <= 4) DLI_RMS_V(4, NS, PB);    \
-    else DLI_RMS_V(8, NS, PB);                  \
+    if (vpt <= 1) RMS_LAUNCH_V(1, NS, PB);         \
+    else if (vpt <= 2) RMS_LAUNCH_V(2, NS, PB);    \
+    else if (vpt <= 4) RMS_LAUNCH_V(4, NS, PB);    \
+    else RMS_LAUNCH_V(8, NS, PB);                  \
   } while (0)
-#define DLI_RMS(NS)                                                   \
+#define RMS_LAUNCH(NS)                                                   \
   do {                                                                \
-    if (NS > 0 && parts_bf16) DLI_RMS_PB(NS, true);                   \
-    else DLI_RMS_PB(NS, false);                                       \
+    if (NS > 0 && parts_bf16) RMS_LAUNCH_PB(NS, true);                   \
+    else RMS_LAUNCH_PB(NS, false);                                       \
   } while (0)
-  DLI_SPLITS_SWITCH(ns, DLI_RMS)
-#undef DLI_RMS
-#undef DLI_RMS_PB
-#undef DLI_RMS_V
+  SPLITS_SWITCH(ns, RMS_LAUNCH)
+#undef RMS_LAUNCH
+#undef RMS_LAUNCH_PB
+#undef RMS_LAUNCH_V
   return 0;
 }
 
@@ -206,7 +206,7 @@ int launch_layer_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* r
                       hipStream_t stream) {
   if (hidden % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -1;
   const int add = residual_in != nullptr ? 1 : 0;
-  DLI_NORM_DISPATCH(layer_norm_kernel, out, x, residual_in, residual_out, w, b, eps, hidden, add);
+  NORM_DISPATCH(layer_norm_kernel, out, x, residual_in, residual_out, w, b, eps, hidden, add);
   return 0;
 }
 

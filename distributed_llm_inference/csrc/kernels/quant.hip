@@ -202,15 +202,15 @@ int launch_quant_rowwise_int8(int8_t* q, float* scale, const bf16* x, const uint
   const int nvec = K / 8;
   const int threads = row_threads(nvec);
   const int vpt = (nvec + threads - 1) / threads;
-#define DLI_QI8(V) \
+#define QI8_LAUNCH(V) \
   quant_rowwise_int8_kernel<V><<<rows, threads, 0, stream>>>(q, scale, x, outlier, K)
-  if (vpt <= 1) DLI_QI8(1);
-  else if (vpt <= 2) DLI_QI8(2);
-  else if (vpt <= 4) DLI_QI8(4);
-  else if (vpt <= 8) DLI_QI8(8);
-  else if (vpt <= 16) DLI_QI8(16);
+  if (vpt <= 1) QI8_LAUNCH(1);
+  else if (vpt <= 2) QI8_LAUNCH(2);
+  else if (vpt <= 4) QI8_LAUNCH(4);
+  else if (vpt <= 8) QI8_LAUNCH(8);
+  else if (vpt <= 16) QI8_LAUNCH(16);
   else return -1;
-#undef DLI_QI8
+#undef QI8_LAUNCH
   return 0;
 }
 
@@ -226,7 +226,7 @@ int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* re
   const int threads = row_threads(nvec);
   const int vpt = (nvec + threads - 1) / threads;
   const int ns = x_parts != nullptr ? splits : 0;
-#define DLI_QUANT(V, NS)                                                                     \
+#define QUANT_LAUNCH(V, NS)                                                                     \
   do {                                                                                       \
     if (NS > 0 && parts_bf16)                                                                \
       quant_rowwise_kernel<V, NS, true><<<rows, threads, 0, stream>>>(                       \
@@ -235,18 +235,18 @@ int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* re
       quant_rowwise_kernel<V, NS, false><<<rows, threads, 0, stream>>>(                      \
           q, scale, x, residual_in, residual_out, norm_w, eps, K, x_parts, split_stride);    \
   } while (0)
-#define DLI_QUANT_NS(NS)                       \
+#define QUANT_LAUNCH_NS(NS)                       \
   do {                                         \
-    if (vpt <= 1) DLI_QUANT(1, NS);            \
-    else if (vpt <= 2) DLI_QUANT(2, NS);       \
-    else if (vpt <= 4) DLI_QUANT(4, NS);       \
-    else if (vpt <= 8) DLI_QUANT(8, NS);       \
-    else if (vpt <= 16) DLI_QUANT(16, NS);     \
+    if (vpt <= 1) QUANT_LAUNCH(1, NS);            \
+    else if (vpt <= 2) QUANT_LAUNCH(2, NS);       \
+    else if (vpt <= 4) QUANT_LAUNCH(4, NS);       \
+    else if (vpt <= 8) QUANT_LAUNCH(8, NS);       \
+    else if (vpt <= 16) QUANT_LAUNCH(16, NS);     \
     else return -1;                            \
   } while (0)
-  DLI_SPLITS_SWITCH(ns, DLI_QUANT_NS)
-#undef DLI_QUANT_NS
-#undef DLI_QUANT
+  SPLITS_SWITCH(ns, QUANT_LAUNCH_NS)
+#undef QUANT_LAUNCH_NS
+#undef QUANT_LAUNCH
   return 0;
 }
 
@@ -257,14 +257,14 @@ int launch_silu_mul_quant(uint8_t* q, float* scale, const bf16* x, int rows, int
   const int nvec = inter / 8;
   const int threads = row_threads(nvec);
   const int vpt = (nvec + threads - 1) / threads;
-#define DLI_SMQ(V) silu_mul_quant_kernel<V><<<rows, threads, 0, stream>>>(q, scale, x, inter)
-  if (vpt <= 1) DLI_SMQ(1);
-  else if (vpt <= 2) DLI_SMQ(2);
-  else if (vpt <= 4) DLI_SMQ(4);
-  else if (vpt <= 8) DLI_SMQ(8);
-  else if (vpt <= 16) DLI_SMQ(16);
+#define SMQ_LAUNCH(V) silu_mul_quant_kernel<V><<<rows, threads, 0, stream>>>(q, scale, x, inter)
+  if (vpt <= 1) SMQ_LAUNCH(1);
+  else if (vpt <= 2) SMQ_LAUNCH(2);
+  else if (vpt <= 4) SMQ_LAUNCH(4);
+  else if (vpt <= 8) SMQ_LAUNCH(8);
+  else if (vpt <= 16) SMQ_LAUNCH(16);
   else return -1;
-#undef DLI_SMQ
+#undef SMQ_LAUNCH
   return 0;
 }
 

@@ -282,12 +282,10 @@ int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stre
   dim3 grid(num_tokens, (heads + kHeadsPerWG - 1) / kHeadsPerWG);
   const int ns = p.qkv_parts != nullptr ? p.splits : 0;
   // 16-byte path: both rotation halves and every head start on 16-byte boundaries of every
-  // partial (DLI_ROPE_V8=0 keeps the 4-element kernel, for A/B)
-  const char* v8e = getenv("DLI_ROPE_V8");   // read per launch (a graph captures the choice)
-  const bool v8_env = !(v8e && v8e[0] == '0');
-  const bool v8 = v8_env && p.D % 16 == 0 && p.qkv_stride % 8 == 0 &&
+  // partial (otherwise the 4-element kernel)
+  const bool v8 = p.D % 16 == 0 && p.qkv_stride % 8 == 0 &&
                   (p.qkv_parts == nullptr || p.split_stride % 8 == 0);
-#define DLI_ROPE(NS)                                                   \
+#define ROPE_LAUNCH(NS)                                                   \
   do {                                                                 \
     if (v8) {                                                          \
       if (p.kv_fp8)                                                    \
@@ -299,8 +297,8 @@ int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stre
     else                                                               \
       rope_cache_kernel<false, NS><<<grid, 128, 0, stream>>>(p);       \
   } while (0)
-  DLI_SPLITS_SWITCH(ns, DLI_ROPE)
-#undef DLI_ROPE
+  SPLITS_SWITCH(ns, ROPE_LAUNCH)
+#undef ROPE_LAUNCH
   return 0;
 }
 

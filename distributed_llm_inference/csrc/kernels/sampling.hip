@@ -7,7 +7,7 @@
 //     the top-k / top-p thresholds come from a 4-ary search over 16-bit value keys with block
 //     reductions — same kept set and Gumbel draw as below, deterministic, 2.2-2.9x faster
 //     (profiles/sample_probe.json: top-p over 512 x 128256 1.02 ms -> 0.38 ms, one row 365 ->
-//     161 us, identical tokens); DLI_SAMPLE_REGS=0 keeps the radix path.
+//     161 us, identical tokens); the radix path remains for fp32 logits and odd vocabularies.
 //   * otherwise x = logits / T, then optional top-k and top-p filtering by *radix select* on the
 //     order-preserving uint32 image of x (4 passes of 8 bits, LDS histograms: counts for top-k,
 //     probability mass for top-p), and finally Gumbel-max over the kept set:
@@ -421,9 +421,7 @@ __global__ void __launch_bounds__(1024) sample_kernel(SampleParams p) {
 int launch_sample(const SampleParams& p, int B, hipStream_t stream) {
   if (B == 0) return 0;
   const int n8 = p.V / 8;
-  const char* e = getenv("DLI_SAMPLE_REGS");   // =0: radix-histogram path (A/B)
-  const bool regs = !p.logits_is_f32 && p.V % 8 == 0 && p.row_stride % 8 == 0 &&
-                    !(e != nullptr && e[0] == '0');
+  const bool regs = !p.logits_is_f32 && p.V % 8 == 0 && p.row_stride % 8 == 0;
   if (regs && n8 <= 4 * 1024)
     sample_kernel<4><<<B, 1024, 0, stream>>>(p);
   else if (regs && n8 <= 8 * 1024)

@@ -12,7 +12,6 @@
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -39,6 +38,9 @@ class Linear(nn.Module):
         self.register_buffer("weight_int8", None, persistent=False)
         self.register_buffer("weight_int8_t", None, persistent=False)
         self.int8_threshold = 0.0
+        # which projection of its layer this is ("qkv" / "o" / "gate_up" / "down", set by the
+        # model): KernelPolicy.fp8_gemm4 routes fp8 products per role
+        self.role = ""
 
     @property
     def is_fp8(self) -> bool:
@@ -53,13 +55,13 @@ class Linear(nn.Module):
         per-channel absmax int8 + bf16 outlier-column decomposition at run time."""
         q, s = ops.quantize_weight_int8(self.weight.data)
         self.weight_int8, self.weight_scale = q, s
-        # Optional (DLI_INT8_WT=1): a transposed [K, N] copy so the per-product outlier
+        # Optional (KernelPolicy.int8_transposed): a transposed [K, N] copy so the per-product outlier
         # weight-column gather reads contiguous rows (int8_outlier.hip gather_wt): 1.6 vs 2.9
         # ms/step on the 70B --int8 bench (+2.5 % tok/s), but it costs a second byte per weight,
         # i.e. the memory LLM.int8 exists to save (70B PP=1: KV blocks 9413 -> 6323, -33 %
         # concurrent sequences).  Off by default; opt in when KV capacity is not the limit.
-        self.weight_int8_t = q.t().contiguous() if q.is_cuda and os.environ.get(
-            "DLI_INT8_WT", "0") == "1" else None
+        self.weight_int8_t = (q.t().contiguous() if q.is_cuda and ops.policy().int8_transposed
+                              else None)
         self.int8_threshold = float(threshold)
         if not keep_bf16:
             self.weight = nn.Parameter(torch.empty(0, dtype=self.weight.dtype,
@@ -98,11 +100,10 @@ class Linear(nn.Module):
         if swiglu and (self.bias is not None or self.out_features % 32):
             return False
         if self.weight_int8 is not None:
-            return bf16_rows and self.in_features % 16 == 0 and \
-                os.environ.get("DLI_INT8_GEMV", "1") == "1"
+            return bf16_rows and self.in_features % 16 == 0 and ops.policy().gemv
         if self.weight_fp8 is not None:
-            return self.in_features % 16 == 0
-        return bf16_rows and self.in_features % 8 == 0
+            return self.in_features % 16 == 0 and ops.policy().gemv
+        return bf16_rows and self.in_features % 8 == 0 and ops.policy().gemv
 
     def gemv(self, x: Optional[torch.Tensor], x_q: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
              swiglu: bool = False, norm: Optional["ops.RowNorm"] = None) -> Optional[torch.Tensor]:
@@ -123,8 +124,7 @@ class Linear(nn.Module):
             return ops.skinny_gemm_int8(x, self.weight_int8, self.weight_scale, self.bias,
                                         swiglu=swiglu, norm=norm)
         if self.weight_fp8 is not None:
-            if norm is not None or (x_q is None and x is not None and
-                                    os.environ.get("DLI_FP8_GEMV", "1") == "1"):
+            if norm is not None or (x_q is None and x is not None):
                 return ops.skinny_gemm_fp8(x, self.weight_fp8, self.weight_scale, None, self.bias,
                                            swiglu=swiglu, norm=norm)
             xq, xs = x_q if x_q is not None else ops.quant_rowwise(x)
@@ -142,8 +142,7 @@ class Linear(nn.Module):
         CPU) -- the caller then runs the GEMV and rope_cache separately."""
         if (x is None or not x.is_cuda or x.dim() != 2 or x.dtype != torch.bfloat16
                 or not self.gemv_ok(x.shape[0]) or meta.want_sink or meta.custom_mask is not None
-                or self.out_features != (nh + 2 * nkv) * head_dim
-                or os.environ.get("DLI_GEMV_ROPE", "1") != "1"):
+                or self.out_features != (nh + 2 * nkv) * head_dim):
             return None
         if self.weight_int8 is not None:
             w, ws = self.weight_int8, self.weight_scale
@@ -170,7 +169,7 @@ class Linear(nn.Module):
         if self.weight_int8 is not None:
             if (x.is_cuda and x.dim() == 2 and 1 <= x.shape[0] <= ops.SKINNY_DISPATCH_M
                     and x.dtype == torch.bfloat16 and self.in_features % 16 == 0
-                    and os.environ.get("DLI_INT8_GEMV", "1") == "1"):
+                    and ops.policy().gemv):
                 # 1-2 row decode: int8 weight-streaming GEMV on the bf16 rows (the weights are
                 # the whole cost; bf16 activations need no outlier decomposition)
                 return ops.skinny_gemm_int8(x, self.weight_int8, self.weight_scale, self.bias)
@@ -185,7 +184,7 @@ class Linear(nn.Module):
         if self.weight_fp8 is None:
             if (x.is_cuda and x.dim() == 2 and 1 <= x.shape[0] <= ops.SKINNY_DISPATCH_M
                     and x.dtype == torch.bfloat16 and x.is_contiguous()
-                    and self.in_features % 8 == 0):
+                    and self.in_features % 8 == 0 and ops.policy().gemv):
                 # 1-2 row decode batches: weight-streaming HIP kernel (csrc/kernels/gemv.hip)
                 return ops.skinny_gemm(x, self.weight, self.bias)
             sp = self.tile_splits(x)
@@ -198,21 +197,23 @@ class Linear(nn.Module):
             # product is tileable (LlamaMLP.forward)
             sp = ops.tile_gemm_splits_fp8(x_q.q.shape[0], self.out_features, self.in_features)
             y = ops.gemm_tile_fp8_mx(x_q, self.weight_fp8, self.weight_scale, sp or 1,
-                                     defer_reduce=defer_reduce and self.bias is None)
+                                     defer_reduce=defer_reduce and self.bias is None,
+                                     gemm4=ops.policy().fp8_on_gemm4(self.role))
             if self.bias is not None:
                 y = y + self.bias
             return y
         if (x_q is None and x is not None and x.is_cuda and x.dim() == 2
                 and 1 <= x.shape[0] <= ops.SKINNY_DISPATCH_M and x.dtype == torch.bfloat16
-                and self.in_features % 16 == 0 and os.environ.get("DLI_FP8_GEMV", "1") == "1"):
+                and self.in_features % 16 == 0 and ops.policy().gemv):
             # 1-2 row decode: fp8 weight-streaming GEMV on the bf16 rows (no quantisation pass;
-            # DLI_FP8_GEMV=0 quantises the rows as a batch of >= 3 would -- docs/parity.md C11)
+            # KernelPolicy.gemv=False quantises the rows as a batch of >= 3 would --
+            # docs/parity.md C11)
             return ops.skinny_gemm_fp8(x, self.weight_fp8, self.weight_scale, None, self.bias)
         if x_q is None:
             x_q = ops.quant_rowwise(x)
         xq, xs = x_q
         if (xq.is_cuda and xq.dim() == 2 and 1 <= xq.shape[0] <= ops.SKINNY_DISPATCH_M
-                and self.in_features % 16 == 0):
+                and self.in_features % 16 == 0 and ops.policy().gemv):
             # 1-2 row decode on the fused quantiser's fp8 rows: half the weight bytes of bf16
             # streamed by the GEMV kernel (hipBLASLt's fp8 GEMM at M = 1 streamed them slower
             # than the bf16 GEMV: Llama-3.1-70B batch-1 decode ran at the bf16 speed)
@@ -221,7 +222,8 @@ class Linear(nn.Module):
             sp = ops.tile_gemm_splits_fp8(xq.shape[0], self.out_features, self.in_features)
             if sp:  # long-K fp8 products: block-scaled MFMA tile kernel (csrc/kernels/gemm_tile.hip)
                 return ops.gemm_tile_fp8(xq, xs, self.weight_fp8, self.weight_scale, sp,
-                                         defer_reduce=defer_reduce)
+                                         defer_reduce=defer_reduce,
+                                         gemm4=ops.policy().fp8_on_gemm4(self.role))
         if xq.is_cuda:
             y = torch._scaled_mm(xq, self.weight_fp8.t(), scale_a=xs, scale_b=self.weight_scale,
                                  out_dtype=torch.bfloat16)

@@ -20,8 +20,6 @@ mathematically identical to the unsliced projection; it is accepted and ignored.
 """
 from __future__ import annotations
 
-import os
-
 from typing import Optional, Tuple
 
 import torch
@@ -73,6 +71,7 @@ class LlamaAttention(nn.Module):
                                dtype=dtype, device=device)
         self.o_proj = Linear(spec.q_size, spec.hidden_size, bias=spec.has_o_proj_bias, dtype=dtype,
                              device=device)
+        self.qkv_proj.role, self.o_proj.role = "qkv", "o"
 
     def forward(self, normed: Optional[torch.Tensor], meta: AttnMetadata, k_cache: torch.Tensor,
                 v_cache: torch.Tensor, cos_sin: torch.Tensor, x_q=None, defer_reduce: bool = False,
@@ -108,7 +107,7 @@ class LlamaAttention(nn.Module):
                                  v_scale=meta.v_scale, mask=meta.custom_mask)
         elif meta.is_decode:
             op = self.o_proj
-            mx = (op.is_fp8 and op.bias is None and ops.fp8_mx_attn()
+            mx = (op.is_fp8 and op.bias is None and ops.policy().fp8_mx
                   and ops.attn_decode_mx_ok(self.head_dim, meta.num_splits))
             if mx and q.is_cuda:
                 sp = ops.tile_gemm_splits_fp8(T, op.out_features, op.in_features)
@@ -122,13 +121,10 @@ class LlamaAttention(nn.Module):
                                     num_splits=meta.num_splits, workspace=meta.workspace,
                                     k_scale=meta.k_scale, v_scale=meta.v_scale, mx_out=True)
                 return op(None, x_q=o, defer_reduce=defer_reduce)
-            pf = None
-            if T <= 2 and q.is_cuda and ops.l3_prefetch_enabled() and op.gemv_ok(T):
-                pf = op.stream_weights()[0]   # the O GEMV's weights, into L3 during attention
             o = ops.attn_decode(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
                                 self.scale, meta.n_sink, meta.sink_pad, meta.ring, meta.window,
                                 num_splits=meta.num_splits, workspace=meta.workspace,
-                                k_scale=meta.k_scale, v_scale=meta.v_scale, prefetch=pf)
+                                k_scale=meta.k_scale, v_scale=meta.v_scale)
         else:
             o = ops.attn_prefill(q, q_sink, k_cache, v_cache, meta.block_tables, meta.seq_lens,
                                  meta.q_start, meta.max_q, self.scale, meta.n_sink, meta.sink_pad,
@@ -148,6 +144,7 @@ class LlamaMLP(nn.Module):
                                    dtype=dtype, device=device)
         self.down_proj = Linear(spec.intermediate_size, spec.hidden_size, bias=spec.mlp_bias,
                                 dtype=dtype, device=device)
+        self.gate_up_proj.role, self.down_proj.role = "gate_up", "down"
         # True once gate_up_proj.weight's rows are in ops.swiglu_interleave order, so the tile
         # GEMM's epilogue can apply SwiGLU itself (no [M, 2I] intermediate, no silu_mul launch)
         self.fused_swiglu = False
@@ -159,10 +156,6 @@ class LlamaMLP(nn.Module):
         if on == self.fused_swiglu:
             return
         if w.bias is not None or w.out_features % 256:
-            return
-        if w.is_fp8 and on and not ops.fp8_tile_all():
-            return
-        if w.is_int8 and on and not ops.int8_fused_outliers():
             return
         perm = ops.swiglu_interleave if on else ops.swiglu_deinterleave
         with torch.no_grad():
@@ -189,7 +182,7 @@ class LlamaMLP(nn.Module):
             if h is None:
                 raise RuntimeError("fused-norm gate|up: the GEMV does not take this product")
             return self.down_proj(h, defer_reduce=defer_reduce)
-        if self.fused_swiglu and os.environ.get("DLI_GEMV_SWIGLU", "1") == "1":
+        if self.fused_swiglu and ops.policy().gemv:
             # 1-2 decode rows: SwiGLU in the weight-streaming GEMV's epilogue (any weight dtype)
             h = gp.gemv_swiglu(normed, x_q)
             if h is not None:
@@ -205,30 +198,31 @@ class LlamaMLP(nn.Module):
                                                         gp.in_features):
                 dp = self.down_proj
                 dsp = ops.tile_gemm_splits_fp8(xq.shape[0], dp.out_features, dp.in_features)
-                if ops.fp8_mx() and dsp and dp.bias is None and ops.mx_tileable(dp.in_features, dsp):
+                g4 = ops.policy().fp8_on_gemm4("gate_up")
+                if (ops.policy().fp8_mx and dsp and dp.bias is None
+                        and ops.mx_tileable(dp.in_features, dsp)):
                     # SwiGLU output quantised in the epilogue with per-(row, 128-column) e8m0
                     # scales, consumed by the down projection's block-scaled MFMA: no bf16 h,
                     # no per-row quantisation pass
                     h = ops.gemm_tile_fp8(xq, xs, gp.weight_fp8, gp.weight_scale, swiglu=True,
-                                          mx_out=True)
+                                          mx_out=True, gemm4=g4)
                     return dp(None, x_q=h, defer_reduce=defer_reduce)
                 # fp8 gate|up on the block-scaled tile kernel, SwiGLU in its epilogue (bf16 out;
                 # down_proj quantises it: one [M, I] pass instead of silu_mul_quant's [M, 2I])
-                h = ops.gemm_tile_fp8(xq, xs, gp.weight_fp8, gp.weight_scale, swiglu=True)
+                h = ops.gemm_tile_fp8(xq, xs, gp.weight_fp8, gp.weight_scale, swiglu=True,
+                                      gemm4=g4)
             else:
                 h = ops.swiglu_interleaved(gp(None, (xq, xs)))
             return self.down_proj(h, defer_reduce=defer_reduce)
         if self.fused_swiglu:
-            if gp.tile_splits(normed) and ops.gate_up_on_tile():
+            if gp.tile_splits(normed):
                 h = ops.gemm_tile(normed, gp.weight, swiglu=True)
-            elif gp.tile_splits(normed) and ops.gate_up_plain_tile():
-                h = ops.swiglu_interleaved(ops.gemm_tile(normed, gp.weight))
             else:
                 h = ops.swiglu_interleaved(gp(normed))
             return self.down_proj(h, defer_reduce=defer_reduce)
         gu = gp(normed, x_q)
         if self.down_proj.is_fp8:  # SwiGLU fused with the fp8 quantisation of down_proj's input
-            if not gu.is_cuda and ops.fp8_mx() and self.down_proj.bias is None:
+            if not gu.is_cuda and ops.policy().fp8_mx and self.down_proj.bias is None:
                 # CPU reference of the GPU tile path: h handed over in MX form (per-(row,
                 # 128-column) e8m0 scales), as the fused SwiGLU epilogue quantises it
                 return self.down_proj(None, x_q=ops.mx_quantize(ops.silu_mul(gu)),
@@ -256,8 +250,6 @@ class LlamaDecoderLayer(nn.Module):
         layer's input RMSNorm reduces them); the O projection's partials always go straight
         into the post-attention RMSNorm."""
         if self._gemv_norms(hidden):
-            if self._layer_kernel_ok(hidden, residual, meta):
-                return self._forward_layer_kernel(hidden, residual, meta, k_cache, v_cache, cos_sin)
             return self._forward_gemv(hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out)
         if self.self_attn.qkv_proj.is_fp8:
             return self._forward_fp8(hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out)
@@ -279,78 +271,13 @@ class LlamaDecoderLayer(nn.Module):
         RMSNorms then run inside the QKV and gate|up GEMVs (``_forward_gemv``)."""
         if (not isinstance(hidden, torch.Tensor) or not hidden.is_cuda or hidden.dim() != 2
                 or hidden.dtype != torch.bfloat16 or not hidden.is_contiguous()
-                or os.environ.get("DLI_GEMV_NORM", "1") != "1"):
+                or not (ops.policy().gemv and ops.policy().gemv_norm)):
             return False
         M = hidden.shape[0]
         a, m = self.self_attn, self.mlp
         return (M * self.hidden_size * 2 <= 65536 and m.fused_swiglu
                 and a.qkv_proj.gemv_ok(M) and a.o_proj.gemv_ok(M)
                 and m.gate_up_proj.gemv_ok(M, swiglu=True) and m.down_proj.gemv_ok(M))
-
-    def _layer_kernel_ok(self, hidden, residual, meta) -> bool:
-        """One decode row whose layer the persistent decode-layer kernel takes (full cache, head
-        dim 128, one weight format, hidden <= 8192, intermediate <= 32768, fused RoPE path)."""
-        a, m = self.self_attn, self.mlp
-        if (hidden.shape[0] != 1 or not meta.is_decode or meta.custom_mask is not None
-                or meta.window or meta.ring or meta.n_sink or a.head_dim != 128
-                or self.hidden_size > 8192 or m.down_proj.in_features > 32768
-                or not ops.decode_layer_enabled()
-                or os.environ.get("DLI_GEMV_ROPE", "1") != "1"
-                or (residual is not None and not isinstance(residual, torch.Tensor))):
-            return False
-        fmts = {(p.is_fp8, p.is_int8) for p in (a.qkv_proj, a.o_proj, m.gate_up_proj, m.down_proj)}
-        return len(fmts) == 1
-
-    def _forward_layer_kernel(self, hidden, residual, meta, k_cache, v_cache, cos_sin):
-        """The fused-norm GEMV path's six launches (QKV + RoPE, attention, merge, O, gate|up +
-        SwiGLU, down) as one persistent kernel with grid barriers between them
-        (csrc/kernels/decode_layer.hip): same results bit for bit, five launch-and-ramp gaps
-        fewer per layer."""
-        a, m = self.self_attn, self.mlp
-        ln1, ln2 = self.input_layernorm, self.post_attention_layernorm
-        dev = hidden.device
-        bar = getattr(self, "_dl_bar", None)
-        if bar is None or bar.device != dev:
-            # grid-barrier arrival counter of this layer's launches (never reset; see the kernel)
-            bar = self._dl_bar = torch.zeros(168, dtype=torch.int64, device=dev)
-        nh, D = a.num_heads, a.head_dim
-        h = hidden.reshape(-1)
-        first = residual is None
-        res1 = h if first else torch.empty_like(h)
-        res2, out = torch.empty_like(h), torch.empty_like(h)
-        q = torch.empty(1, nh, D, dtype=hidden.dtype, device=dev)
-        attn = torch.empty(nh * D, dtype=hidden.dtype, device=dev)
-        o_out = torch.empty_like(h)
-        act = torch.empty(m.down_proj.in_features, dtype=hidden.dtype, device=dev)
-        ws = meta.workspace if meta.num_splits > 1 else None
-        if meta.num_splits > 1 and ws is None:
-            ws = ops.decode_workspace(1, nh, D, meta.num_splits, dev)
-        ops.native().decode_layer(
-            h, None if first else residual.reshape(-1), res1, res2, out, ln1.weight, ln2.weight,
-            float(ln1.eps), float(ln2.eps), *a.qkv_proj.stream_weights(),
-            *a.o_proj.stream_weights(), *m.gate_up_proj.stream_weights(),
-            *m.down_proj.stream_weights(), meta.positions, meta.slot_mapping, cos_sin, q, k_cache,
-            v_cache, float(meta.k_scale), float(meta.v_scale), meta.block_tables, meta.seq_lens,
-            float(a.scale), int(meta.num_splits), ws[0] if ws else None, ws[1] if ws else None,
-            attn, o_out, act, bar, self._dl_stamp_buffer(dev),
-            int(os.environ.get("DLI_DL_FLAGS", "0")))
-        return out.view(1, -1), res2.view(1, -1)
-
-    def _dl_stamp_buffer(self, dev):
-        """``DLI_DL_STAMPS=1`` (diagnostics, scripts/decode_layer_probe.py): per-workgroup wall
-        stamps of the decode-layer kernel's phases, overwritten by every launch."""
-        if os.environ.get("DLI_DL_STAMPS", "0") != "1":
-            return None
-        st = getattr(self, "_dl_stamps", None)
-        if st is None or st.device != dev:
-            st = self._dl_stamps = torch.zeros(24 * ops.native().decode_layer_grid(),
-                                               dtype=torch.int64, device=dev)
-        return st
-
-    def decode_layer_errors(self) -> int:
-        """Grid-barrier spin timeouts of this layer's persistent launches (0 = all completed)."""
-        bar = getattr(self, "_dl_bar", None)
-        return 0 if bar is None else int(bar[128].item() & 0xFFFFFFFF)
 
     def _forward_gemv(self, hidden, residual, meta, k_cache, v_cache, cos_sin, defer_out=False):
         """1-2 decode rows: input RMSNorm fused into the QKV GEMV, post-attention RMSNorm into the

@@ -5,15 +5,47 @@ There is deliberately no silent fallback: a GPU tensor with the native extension
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from typing import Optional, Tuple
 
 import torch
 
+from ..config import KernelPolicy
 from . import reference as ref
 
 _C = None
+_POLICY: Optional[KernelPolicy] = None
+
+
+def policy() -> KernelPolicy:
+    """The process's :class:`~config.KernelPolicy` (``DLI_KERNELS`` applied on top)."""
+    global _POLICY
+    if _POLICY is None:
+        _POLICY = KernelPolicy().with_overrides(os.environ.get("DLI_KERNELS", ""))
+    return _POLICY
+
+
+def set_policy(p: KernelPolicy) -> KernelPolicy:
+    """Install ``p`` (``DLI_KERNELS`` still overrides it); returns the previous policy."""
+    global _POLICY
+    prev = policy()
+    _POLICY = p.with_overrides(os.environ.get("DLI_KERNELS", ""))
+    return prev
+
+
+@contextlib.contextmanager
+def kernel_policy(**fields):
+    """Temporarily change policy fields (tests, A/B probes): ``with kernel_policy(gemm4=False):``."""
+    import dataclasses
+    prev = policy()
+    global _POLICY
+    _POLICY = dataclasses.replace(prev, **fields)
+    try:
+        yield _POLICY
+    finally:
+        _POLICY = prev
 
 
 class NativeKernelsMissing(RuntimeError):
@@ -49,8 +81,8 @@ def _gpu(t: torch.Tensor) -> bool:
 # ----------------------------------------------------------------------------- normalisation
 class SplitKPartials:
     """The un-reduced output of a split-K tile GEMM: partial products ``parts [S, M, N]``, bf16
-    by default (:func:`bf16_bf16_partials`, :func:`fp8_bf16_partials`), fp32 with
-    ``DLI_BF16_PARTS=0`` / ``DLI_FP8_BF16_PARTS=0``; consumers always sum them in fp32.
+    by default (:func:`bf16_partials`), fp32 with ``KernelPolicy.bf16_partials=False``;
+    consumers always sum them in fp32.
 
     ``gemm_tile(..., defer_reduce=True)`` returns this instead of running the reduction pass;
     ``rms_norm`` sums the partials while it reads them (norm.hip ``x_parts``), so the reduce
@@ -81,35 +113,16 @@ class SplitKPartials:
         return out
 
 
-def fp8_bf16_partials() -> bool:
-    """``DLI_FP8_BF16_PARTS=1`` (default): the 8-bit (fp8 / LLM.int8) tile GEMMs' split-K partials
-    (QKV, O, down) are stored as bf16 (gemm_tile epilogue 4) and summed in fp32 by their consumers
-    — half the partial bytes written and read.  Rounding each partial to bf16 adds ~2^-9 relative
-    error, far below what the 8-bit activations carry (bf16 operands: :func:`bf16_bf16_partials`)."""
-    return os.environ.get("DLI_FP8_BF16_PARTS", "1") != "0"
-
-
-def bf16_bf16_partials() -> bool:
-    """bf16 operands: split-K partials of the deferred projections (QKV, O, down) stored as bf16
-    (default; ``DLI_BF16_PARTS=0`` keeps fp32).  Half the partial traffic of the GEMM epilogue
-    and of the consumer that sums them (RMSNorm / RoPE); each partial carries one extra bf16
-    rounding (~2^-9 relative) before the fp32 sum.  Measured on the default bench (same box,
-    interleaved): 6468-6482 -> 6556-6574 tok/s (profiles/bf16_partials_ab.txt).  End-to-end
-    bound vs the fp32 CPU reference: tests/test_engine_gpu.py::
-    test_bf16_splitk_partials_end_to_end_vs_cpu_reference; listed in docs/parity.md (C6)."""
-    return os.environ.get("DLI_BF16_PARTS", "1") == "1"
-
-
-def gate_up_on_tile() -> bool:
-    """bf16 gate|up with SwiGLU in the tile GEMM's epilogue (default); ``DLI_GATEUP_TILE=0``
-    runs it on hipBLASLt (interleaved weight as-is) followed by ``swiglu_interleaved``, ``plain``
-    on the tile kernel with the plain bf16 store followed by ``swiglu_interleaved`` - the A/Bs
-    for the step's largest GEMM (hipBLASLt: -1.8 %, profiles/gateup_tile_vs_hipblaslt_ab.txt)."""
-    return os.environ.get("DLI_GATEUP_TILE", "1") == "1"
-
-
-def gate_up_plain_tile() -> bool:
-    return os.environ.get("DLI_GATEUP_TILE", "1") == "plain"
+def bf16_partials() -> bool:
+    """Split-K partials of the deferred projections (QKV, O, down) stored as bf16
+    (``KernelPolicy.bf16_partials``, default) for every operand precision: half the partial
+    traffic of the GEMM epilogue and of the consumer that sums them (RMSNorm / RoPE); each
+    partial carries one extra bf16 rounding (~2^-9 relative) before the fp32 sum.  Measured on the
+    default bench (same box, interleaved): 6468-6482 -> 6556-6574 tok/s
+    (profiles/bf16_partials_ab.txt).  End-to-end bound vs the fp32 CPU reference:
+    tests/test_engine_gpu.py::test_bf16_splitk_partials_end_to_end_vs_cpu_reference; listed in
+    docs/parity.md (C6)."""
+    return policy().bf16_partials
 
 
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
@@ -249,13 +262,11 @@ def attn_decode_mx_ok(head_dim: int, num_splits: int) -> bool:
 
 def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink=0, sink_pad=0,
                 ring=0, window=0, num_splits=1, workspace=None, out=None, k_scale=1.0, v_scale=1.0,
-                mx_out: bool = False, prefetch=None):
+                mx_out: bool = False):
     """Paged GQA decode attention -> bf16 ``[T, nh, D]``; ``mx_out`` (needs
     :func:`attn_decode_mx_ok`): the same values (rounded to bf16) quantised in the kernel's
     epilogue to :class:`MxFp8` ``[T, nh * D]`` for the fp8 O projection, replacing a separate
-    per-row quantisation pass.  ``prefetch``: a tensor (the next GEMV's weight) that extra
-    workgroups of the attention / combine launches read into the Infinity Cache meanwhile
-    (:func:`l3_prefetch_cfg`); no effect on the result."""
+    per-row quantisation pass."""
     if mx_out and not attn_decode_mx_ok(q.shape[-1], num_splits):
         raise ValueError("attn_decode(mx_out=True) needs head_dim 128 and one split")
     if not _gpu(q):
@@ -276,90 +287,41 @@ def attn_decode(q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_si
                              None, None, float(k_scale), float(v_scale), q8, sc)
         return MxFp8(q8, sc)
     out = torch.empty_like(q) if out is None else out
-    part_o = part_ml = cnt = None
+    part_o = part_ml = None
     if num_splits > 1:
         if workspace is None:
             workspace = decode_workspace(q.shape[0], q.shape[1], q.shape[2], num_splits, q.device)
         part_o, part_ml = workspace[0], workspace[1]
-        if len(workspace) > 2 and attn_last_merge():
-            cnt = workspace[2]
-    pf_split = pf_wgs = 0
-    if prefetch is not None:
-        share, pf_wgs = l3_prefetch_cfg()
-        nb = prefetch.numel() * prefetch.element_size()
-        pf_split = int(nb * share) // 16 * 16
     native().attn_decode(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, float(scale),
                          int(n_sink), int(sink_pad), int(ring), int(window), int(num_splits),
-                         part_o, part_ml, float(k_scale), float(v_scale), merge_cnt=cnt,
-                         prefetch=prefetch if pf_wgs else None, pf_split=pf_split, pf_wgs=pf_wgs)
+                         part_o, part_ml, float(k_scale), float(v_scale))
     return out
-
-
-def l3_prefetch_enabled() -> bool:
-    """``DLI_L3_PF=1``: batch-1 decode attention reads the O projection's weights into the
-    256 MiB Infinity Cache while it runs (HBM is otherwise idle: a few MB of K/V per layer), so
-    the O GEMV streams them from L3 (scripts/l3_prefetch_probe.py).  Off by default: a warm O
-    GEMV is only 1.4-2.8 us faster (13.4 -> 11.7 us fp8, 23.7 -> 20.9 us bf16: L3 serves this
-    stream at 5.7-6.4 TB/s) and the batch-1 step did not change (fp8 77.45 vs 77.42 tok/s;
-    profiles/r4/l3_prefetch_ab.txt)."""
-    return os.environ.get("DLI_L3_PF", "0") == "1"
-
-
-def l3_prefetch_cfg():
-    """(share of the bytes read by the attention launch -- the rest by the combine launch when
-    there is one --, warm-up workgroups per launch): ``DLI_L3_PF_SPLIT`` (default 1.0),
-    ``DLI_L3_PF_WGS`` (default 224)."""
-    share = min(max(float(os.environ.get("DLI_L3_PF_SPLIT", "1.0")), 0.0), 1.0)
-    return share, max(0, min(4096, int(os.environ.get("DLI_L3_PF_WGS", "224"))))
-
-
-def l3_prefetch(t: torch.Tensor, nwg: int = 224) -> None:
-    """Read ``t`` on ``nwg`` workgroups and discard it (Infinity-Cache warm-up); GPU only."""
-    if _gpu(t):
-        native().l3_prefetch(t, int(nwg))
-
-
-def attn_last_merge() -> bool:
-    """``DLI_ATTN_MERGE=1``: split-K decode attention (head dim 128, 4-split groups) merges its
-    partials in the last-arriving workgroup of each head group (write-through partials, an
-    arrival counter per head group, device-scope reads) instead of launching
-    attn_combine_kernel.  Same arithmetic (bit-identical, tests/test_kernels_gpu.py).  Off by
-    default: measured slower (B=1: 600 keys 11.3 vs 10.6 us, 8k keys 28.1 vs 15.0 us -- one
-    workgroup reading up to 32 partials serially costs more than the launch;
-    profiles/r4/attn_last_merge_bench.txt)."""
-    return os.environ.get("DLI_ATTN_MERGE", "0") == "1"
 
 
 def decode_workspace(rows: int, nh: int, head_dim: int, splits: int, device):
     """Split-K decode workspace: fp32 partial O and (max, sum) per split (sized for the unmerged
-    worst case; the kernel uses splits / 4 of it when its workgroups merge their splits), and the
-    last-arrival merge's counters (int32, zero between launches: the merging workgroup resets
-    its own)."""
+    worst case; the kernel uses splits / 4 of it when its workgroups merge their splits)."""
     return (torch.empty(splits * rows * nh * head_dim, dtype=torch.float32, device=device),
-            torch.empty(splits * rows * nh * 2, dtype=torch.float32, device=device),
-            torch.zeros(rows * nh, dtype=torch.int32, device=device))
+            torch.empty(splits * rows * nh * 2, dtype=torch.float32, device=device))
 
 
-def prefill_qb() -> int:
-    """16-token query blocks per prefill wave (attention.hip QB): ``DLI_PREFILL_QB`` = 1 (default)
-    or 2 (each K / V fragment read from LDS feeds two query blocks' MFMAs: +2 % on 2k-4k chunks,
-    -25 % on 16-token chunks, twice the VGPRs; profiles/attn_prefill_qb_ab.json)."""
-    return 2 if os.environ.get("DLI_PREFILL_QB", "1") == "2" else 1
+PREFILL_QB = 1   # 16-token query blocks per prefill wave (attention.hip QB; 2 was +2 % on 2k-4k
+                 # chunks but -25 % on 16-token ones: profiles/attn_prefill_qb_ab.json)
 
 
-def prefill_tile_tokens(nh: int, nkv: int) -> int:
+def prefill_tile_tokens(nh: int, nkv: int, qb: int = PREFILL_QB) -> int:
     """Query tokens per prefill workgroup tile (attention.hip: 16 * TPW * QB, TPW = 4 / HPW)."""
     G = nh // nkv
     hpw = 4 if G % 4 == 0 else (2 if G % 2 == 0 else 1)
-    return 16 * (4 // hpw) * prefill_qb()
+    return 16 * (4 // hpw) * qb
 
 
-def prefill_tiles(q_lens, nh: int, nkv: int, out=None) -> torch.Tensor:
+def prefill_tiles(q_lens, nh: int, nkv: int, out=None, qb: int = PREFILL_QB) -> torch.Tensor:
     """Compact (sequence, token-tile) work list of the prefill kernel: one row per tile that
     holds query tokens.  A 1-token decode row mixed into a prefill batch gets a single tile
     instead of ``max_q / tile`` empty workgroups.  Returns int32 [n_tiles, 2] (or fills ``out``)."""
     import numpy as np
-    tt = prefill_tile_tokens(nh, nkv)
+    tt = prefill_tile_tokens(nh, nkv, qb)
     ql = np.asarray(q_lens, dtype=np.int64)
     nt = (ql + tt - 1) // tt
     b = np.repeat(np.arange(len(ql), dtype=np.int32), nt)
@@ -374,10 +336,11 @@ def prefill_tiles(q_lens, nh: int, nkv: int, out=None) -> torch.Tensor:
 
 def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, max_q, scale,
                  n_sink=0, sink_pad=0, ring=0, window=0, out=None, k_scale=1.0, v_scale=1.0,
-                 tile_map=None, mask=None):
+                 tile_map=None, mask=None, qb: int = PREFILL_QB):
     """Paged varlen prefill attention.  ``mask``: the reference API's pre-inverted 4-D additive
     mask ``[B, 1 | nh, T, >= L]`` (0 = attend, large negative = masked; the last ``q_len_b`` rows
-    of sequence b) - it replaces the causal mask (full cache, any T incl. 1)."""
+    of sequence b) - it replaces the causal mask (full cache, any T incl. 1).  ``qb``: 16-token
+    query blocks per wave (1 or 2; ``tile_map`` must be built with the same value)."""
     if not _gpu(q):
         if mask is not None:
             y = ref.attn_custom_mask(q, k_cache, v_cache, block_tables, seq_lens, q_start, scale,
@@ -394,8 +357,7 @@ def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, m
         tile_map = None   # dense grid: the masked kernel runs one query block per wave
     native().attn_prefill(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start,
                           int(max_q), float(scale), int(n_sink), int(sink_pad), int(ring),
-                          int(window), float(k_scale), float(v_scale), tile_map, prefill_qb(),
-                          mask)
+                          int(window), float(k_scale), float(v_scale), tile_map, int(qb), mask)
     return out
 
 
@@ -519,13 +481,12 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = 
     ``swiglu=True``: ``w`` is a ``swiglu_interleave``d [gate; up] weight and the result is
     ``silu(x @ gate^T) * (x @ up^T)`` ([M, N/2]).  ``defer_reduce`` (split-K only): return the
     partials as :class:`SplitKPartials` for a consumer that reduces them (``rms_norm``): bf16
-    under :func:`bf16_bf16_partials` (the default), else fp32."""
+    under :func:`bf16_partials` (the default), else fp32."""
     M, N = x.shape[0], w.shape[0]
-    if _gpu(x) and gemm4_enabled():
+    if _gpu(x) and policy().gemm4:
         return _gemm4(x, w, splits, swiglu, out, defer_reduce)
-    if (defer_reduce and splits > 1 and _gpu(x) and not swiglu
-            and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
-        if bf16_bf16_partials():
+    if defer_reduce and splits > 1 and _gpu(x) and not swiglu and policy().defer_splitk:
+        if bf16_partials():
             parts = torch.empty(splits, M, N, dtype=torch.bfloat16, device=x.device)
             native().gemm_tile(parts, x, w, int(splits), 4)
             return SplitKPartials(parts)
@@ -553,38 +514,6 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = 
     return out
 
 
-_DECODE_LAYER_BLOCKED = False
-
-
-def block_decode_layer(blocked: bool = True) -> None:
-    """Keep batch-1 decode off the persistent decode-layer kernel in this process (the engine
-    calls this when other kernels run next to the stage's layers -- the rotating LM head's side
-    stream): its grid barriers need every workgroup of the launch resident at once."""
-    global _DECODE_LAYER_BLOCKED
-    _DECODE_LAYER_BLOCKED = bool(blocked)
-
-
-def decode_layer_enabled() -> bool:
-    """``DLI_DECODE_LAYER=1``: single-row decode runs each Llama layer as ONE persistent launch
-    (csrc/kernels/decode_layer.hip: the six GEMV / attention kernels of the fused-norm path as
-    phases between grid barriers, bit-identical results).  Off by default until it beats the
-    six-launch path (scripts/decode_layer_probe.py); never when ranks share a GPU
-    (``DLI_SHARE_GPU=1``) or after :func:`block_decode_layer`."""
-    return (not _DECODE_LAYER_BLOCKED and os.environ.get("DLI_DECODE_LAYER", "0") == "1"
-            and os.environ.get("DLI_SHARE_GPU", "0") != "1")
-
-
-def gemm4_enabled(fp8: bool = False) -> bool:
-    """Decode projections on the one-wave-per-SIMD kernel (csrc/kernels/gemm4.hip) instead of
-    gemm_tile (read per call, so a captured graph keeps its choice).  bf16: ``DLI_GEMM4=1``
-    (default; 70B decode step 75.0 vs 77.7 ms, profiles/r4/gemm4_step_ab.txt).  fp8:
-    ``DLI_GEMM4_FP8=1`` (default off: the K = 8192 QKV / O products it takes measured 0.8 %
-    slower in-step; gate|up and down stay on gemm_tile's MX epilogues either way)."""
-    if fp8:
-        return os.environ.get("DLI_GEMM4_FP8", "0") == "1"
-    return os.environ.get("DLI_GEMM4", "1") == "1"
-
-
 def _gemm4(x: torch.Tensor, w: torch.Tensor, splits: int, swiglu: bool,
            out: Optional[torch.Tensor], defer_reduce: bool,
            xs: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None):
@@ -595,9 +524,8 @@ def _gemm4(x: torch.Tensor, w: torch.Tensor, splits: int, swiglu: bool,
     M, N = x.shape[0], w.shape[0]
     splits = max(1, int(splits))
     fp8 = xs is not None
-    if splits > 1 and defer_reduce and not swiglu and \
-            os.environ.get("DLI_SPLITK_DEFER", "1") == "1":
-        bf = fp8_bf16_partials() if fp8 else bf16_bf16_partials()
+    if splits > 1 and defer_reduce and not swiglu and policy().defer_splitk:
+        bf = bf16_partials()
         parts = torch.empty(splits, M, N, dtype=torch.bfloat16 if bf else torch.float32,
                             device=x.device)
         native().gemm4(parts, x, w, splits, 4 if bf else 1, 0, xs, ws)
@@ -630,13 +558,14 @@ def tile_gemm_stream_k(M: int, N: int, device) -> bool:
     """Whether a whole-K (splits = 1) bf16 ``gemm_tile`` should run its last, partial wave of tiles
     as a stream-K tail: more tiles than CUs and a remainder of at least half the CUs (Llama-3-70B
     gate|up at M = 512: 448 tiles = 256 whole + 192 shared k-wise by 256 workgroups, instead of a
-    second wave with 64 idle CUs).  Opt-in (``DLI_TILE_SK=1``): in isolation (back-to-back
+    second wave with 64 idle CUs).  Opt-in: in isolation (back-to-back
     launches) it is 6-12 % faster (profiles/gemm_sk_bench.json), but inside the decode step the
     gate|up GEMM runs at the same ~386 us either way (rocprofv3, profiles/stream_k_decode_ab.txt),
     and bench.py is unchanged within noise.  In the decode step the whole-tile kernel already runs
     25 % faster than in the isolated loop (386 vs 480 us), so the idle-CU tail is not what bounds
-    it there; a GRBM_GUI_ACTIVE pass shows the stream-K variant at a ~1 % lower clock."""
-    if os.environ.get("DLI_TILE_SK", "0") != "1":
+    it there; a GRBM_GUI_ACTIVE pass shows the stream-K variant at a ~1 % lower clock.
+    (``KernelPolicy.stream_k_tail``.)"""
+    if not policy().stream_k_tail:
         return False
     cus = device_cus(device)
     tiles = ((M + 255) // 256) * (N // 256)
@@ -645,21 +574,25 @@ def tile_gemm_stream_k(M: int, N: int, device) -> bool:
 
 TILE_GEMM_MIN_M = 128    # below: too few rows to fill a 256-row tile (hipBLASLt / skinny path)
 TILE_GEMM_MAX_M = 2048   # above (prefill chunks): hipBLASLt's large-M solutions
+TILE_MAX_SPLITS = 8      # norm / quant / rope consumers sum up to 8 partials (SPLITS_SWITCH)
 _CUS = 256
 
 
 def library_gemms() -> bool:
     """Whether products the tile kernel does not take well (M < 128, M > 2048, the wide LM head)
-    may go to hipBLASLt (default).  ``DLI_GEMM_LIB=0`` keeps every tileable product on the tile
+    may go to hipBLASLt (default).  Off, every tileable product stays on the tile
     kernel: hipBLASLt picks stream-K solutions for some of these shapes - persistent kernels
     sized to the CU count whose workgroups wait for each other's partial tiles - and two of
     them in flight at once (the head stream next to the compute stream, or ranks sharing one
     GPU) can each hold CUs the other needs.  Measured: every hipBLASLt kernel torch picks for the
     70B decode shapes at M = 1..4096 is stream-K (``SK3``, profiles/streams/blaslt_streamk.txt);
     8 pipeline ranks sharing one GPU at 32 rows per micro-batch stalled in 4 of 4 runs with them
-    and completed with this off.  Off by default when ranks share a GPU (``DLI_SHARE_GPU=1``)."""
-    default = "0" if os.environ.get("DLI_SHARE_GPU", "0") == "1" else "1"
-    return os.environ.get("DLI_GEMM_LIB", default) == "1"
+    and completed with this off.  ``KernelPolicy.library_gemms``; automatic (None): off when
+    ranks share a GPU (``DLI_SHARE_GPU=1``)."""
+    lib = policy().library_gemms
+    if lib is None:
+        return os.environ.get("DLI_SHARE_GPU", "0") != "1"
+    return bool(lib)
 
 
 def tile_gemm_splits(M: int, N: int, K: int, elem_bytes: int = 2) -> int:
@@ -667,8 +600,9 @@ def tile_gemm_splits(M: int, N: int, K: int, elem_bytes: int = 2) -> int:
 
     Picks the split that best fills the 256 CUs with whole waves of 256x256 tiles (ties -> fewer
     splits), e.g. 70B at M = 512: QKV 80 tiles x 3, O / down 64 x 4, gate|up 448 x 1 (measured
-    best per shape, profiles/gemm_tile_bench.json).  ``DLI_TILE_GEMM=0`` disables the kernel."""
-    if os.environ.get("DLI_TILE_GEMM", "1") == "0":
+    best per shape, profiles/gemm_tile_bench.json).  ``KernelPolicy.tile_gemms=False`` disables
+    the tile kernels (hipBLASLt everywhere)."""
+    if not policy().tile_gemms:
         return 0
     lib = library_gemms()
     if N % 256 or (K * elem_bytes) % 128 or M < 1:
@@ -680,7 +614,7 @@ def tile_gemm_splits(M: int, N: int, K: int, elem_bytes: int = 2) -> int:
     if lib and tiles > 2 * _CUS:
         return 0  # e.g. the 128256-wide LM head: hipBLASLt's wide-N solutions are faster (690 vs 824 us)
     best, best_util = 1, 0.0
-    for s in range(1, int(os.environ.get("DLI_TILE_MAX_SPLITS", "8")) + 1):
+    for s in range(1, TILE_MAX_SPLITS + 1):
         if s > k_tiles or (s > 1 and tiles * s > 2 * _CUS):
             break
         if (s - 1) * (-(-k_tiles // s)) >= k_tiles:
@@ -724,13 +658,6 @@ LLM_INT8_MAX_OUTLIERS = 64   # static outlier-column capacity (graph-capturable 
 LLM_INT8_SELECT_MAX_K = 32768   # int8_outlier.hip select kernel: 1024 threads x 32 columns
 
 
-def int8_fused_outliers() -> bool:
-    """``DLI_INT8_FUSED=1`` (default): the LLM.int8 outlier product runs in the int8 tile GEMM's
-    epilogue, split-K partials go to their consumers and gate|up fuses SwiGLU; ``0`` = the
-    previous path (hipBLASLt addmm for the outliers, reduce passes, separate silu_mul) for A/B."""
-    return os.environ.get("DLI_INT8_FUSED", "1") == "1"
-
-
 def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, threshold: float = 6.0,
                     max_outliers: int = LLM_INT8_MAX_OUTLIERS,
                     wq_t: Optional[torch.Tensor] = None, swiglu: bool = False,
@@ -763,8 +690,7 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
                 wq_t = None
             # fused epilogue: it reads only the ceil(cnt / 32) live 32-column chunks, so the
             # gathers skip the rest (no outliers -> no gather traffic, no outlier MFMA steps)
-            dynamic = (tile_ok and int8_fused_outliers()
-                       and os.environ.get("DLI_INT8_DYNAMIC", "1") == "1")
+            dynamic = tile_ok
             flags, xo, wo, cnt = native().llm_int8_outliers(
                 x.contiguous(), wq, ws.float().contiguous(), float(threshold), int(J), wq_t,
                 dynamic)
@@ -802,18 +728,8 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
                 xo = torch.nn.functional.pad(xo, (0, pad))
                 wo = torch.nn.functional.pad(wo, (0, pad))
             xo, wo = xo.contiguous(), wo.contiguous()
-        if not int8_fused_outliers():
-            # A/B baseline: int8 GEMM (+ reduce pass), then the outlier product by one hipBLASLt
-            # addmm and SwiGLU as a separate pass
-            y = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-            ws_ = torch.empty(sp * M * N, dtype=torch.float32, device=x.device) if sp > 1 else None
-            native().gemm_tile(y, xq, wq, int(sp), 0, ws_, xs, ws)
-            if outl is not None:
-                y.addmm_(outl[0], outl[1].t())
-            return swiglu_interleaved(y) if swiglu else y
-        if (defer_reduce and sp > 1 and not swiglu
-                and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
-            if fp8_bf16_partials():   # bf16 partials (epilogue 4), as on the fp8 path
+        if defer_reduce and sp > 1 and not swiglu and policy().defer_splitk:
+            if bf16_partials():   # bf16 partials (epilogue 4), as on the fp8 path
                 parts = torch.empty(sp, M, N, dtype=torch.bfloat16, device=x.device)
                 native().gemm_tile(parts, xq, wq, int(sp), 4, None, xs, ws, xo, wo,
                                    ol_cnt=ol_cnt)
@@ -839,14 +755,15 @@ def llm_int8_linear(x: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, thresho
 def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor,
                   splits: int = 1, swiglu: bool = False, out: Optional[torch.Tensor] = None,
                   workspace: Optional[torch.Tensor] = None, defer_reduce: bool = False,
-                  mx_out: bool = False):
+                  mx_out: bool = False, gemm4: bool = False):
     """fp8 e4m3 tile GEMM: ``(xq [M, K] @ wq[N, K]^T) * xs[M] * ws[N]`` -> bf16, on the
     block-scaled K=128 MFMA (2x the bf16 MFMA rate; unit block scales, per-row / per-channel
     scales applied in the epilogue).  ``swiglu``: ``wq`` / ``ws`` rows in swiglu_interleave order.
     ``defer_reduce`` (split-K): return :class:`SplitKPartials` (scaled partials, bf16 under
-    :func:`fp8_bf16_partials`).
+    :func:`bf16_partials`).
     ``mx_out`` (with ``swiglu``): return the SwiGLU output as :class:`MxFp8`, quantised in the
-    epilogue (needs N % 256 == 0)."""
+    epilogue (needs N % 256 == 0).  ``gemm4``: run on the one-wave-per-SIMD kernel (the caller
+    decides per shape: ``KernelPolicy.fp8_on_gemm4``)."""
     M, N = xq.shape[0], wq.shape[0]
     if mx_out:
         if not swiglu:
@@ -859,12 +776,11 @@ def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torc
         native().gemm_tile(q, xq, wq, 1, 3, None, xs.reshape(-1).contiguous(),
                            ws.reshape(-1).contiguous(), out_mx=sc)
         return MxFp8(q, sc)
-    if _gpu(xq) and gemm4_enabled(fp8=True) and xq.shape[1] % 128 == 0:
+    if _gpu(xq) and gemm4 and xq.shape[1] % 128 == 0:
         return _gemm4(xq, wq, splits, swiglu, out, defer_reduce,
                       xs.reshape(-1).contiguous(), ws.reshape(-1).contiguous())
-    if (defer_reduce and splits > 1 and _gpu(xq) and not swiglu
-            and os.environ.get("DLI_SPLITK_DEFER", "1") == "1"):
-        if fp8_bf16_partials():
+    if defer_reduce and splits > 1 and _gpu(xq) and not swiglu and policy().defer_splitk:
+        if bf16_partials():
             parts = torch.empty(splits, M, N, dtype=torch.bfloat16, device=xq.device)
             native().gemm_tile(parts, xq, wq, int(splits), 4, None,
                                xs.reshape(-1).contiguous(), ws.reshape(-1).contiguous())
@@ -937,20 +853,6 @@ def mx_quantize(h: torch.Tensor) -> MxFp8:
     return MxFp8(q, sc.view(-1))
 
 
-def fp8_mx() -> bool:
-    """``DLI_FP8_MX=1`` (default): the fp8 gate|up tile GEMM hands its SwiGLU output to the down
-    projection as :class:`MxFp8` (no separate per-row quantisation pass over h); ``0`` keeps the
-    bf16 h + per-row quantiser path."""
-    return os.environ.get("DLI_FP8_MX", "1") != "0"
-
-
-def fp8_mx_attn() -> bool:
-    """``DLI_FP8_MX_ATTN=1`` (default, with :func:`fp8_mx`): single-split decode attention hands
-    its output to the fp8 O projection as :class:`MxFp8` (quantised in the attention epilogue);
-    ``0`` keeps the bf16 output + per-row quantiser."""
-    return fp8_mx() and os.environ.get("DLI_FP8_MX_ATTN", "1") != "0"
-
-
 MX_MAX_KTILES = 64   # k-tiles of scales one kFp8Mx workgroup keeps in LDS (gemm_tile.hip kMxMaxKt)
 
 
@@ -961,7 +863,7 @@ def mx_tileable(K: int, splits: int) -> bool:
 
 
 def gemm_tile_fp8_mx(a: MxFp8, wq: torch.Tensor, ws: torch.Tensor, splits: int = 1,
-                     defer_reduce: bool = False):
+                     defer_reduce: bool = False, gemm4: bool = False):
     """fp8 tile GEMM on MX activations: ``(q * 2^e) @ (wq * ws)^T`` with the e8m0 scales applied
     by the MFMA itself (kFp8Mx); bf16 out, or :class:`SplitKPartials` when deferring."""
     xq = a.q
@@ -973,8 +875,8 @@ def gemm_tile_fp8_mx(a: MxFp8, wq: torch.Tensor, ws: torch.Tensor, splits: int =
         raise ValueError(f"gemm_tile_fp8_mx: K={xq.shape[1]} with {splits} splits exceeds the "
                          f"{MX_MAX_KTILES}-k-tile scale slot")
     ws = ws.reshape(-1).contiguous()
-    if defer_reduce and splits > 1 and os.environ.get("DLI_SPLITK_DEFER", "1") == "1":
-        if fp8_bf16_partials():
+    if defer_reduce and splits > 1 and policy().defer_splitk:
+        if bf16_partials():
             parts = torch.empty(splits, M, N, dtype=torch.bfloat16, device=xq.device)
             native().gemm_tile(parts, xq, wq, int(splits), 4, None, None, ws, a_mx=a.sc)
             return SplitKPartials(parts)
@@ -989,21 +891,11 @@ def gemm_tile_fp8_mx(a: MxFp8, wq: torch.Tensor, ws: torch.Tensor, splits: int =
     return out
 
 
-def fp8_tile_all() -> bool:
-    """``DLI_FP8_TILE=all`` (default): every fp8 decode projection runs on the hand-written
-    block-scaled MFMA tile kernel — QKV / O / down with split-K partials reduced by their consumer
-    kernels and gate|up with the fused SwiGLU epilogue.  ``long``: only long-K products (the down
-    projection) do; the K = 8192 ones go to hipBLASLt's row-scaled fp8 GEMM, which is faster on
-    those shapes in isolation (profiles/gemm_fp8_probe.json)."""
-    return os.environ.get("DLI_FP8_TILE", "all") != "long"
-
-
 def tile_gemm_splits_fp8(M: int, N: int, K: int) -> int:
-    """``tile_gemm_splits`` for the fp8 kernel under the :func:`fp8_tile_all` policy (``long``:
-    K >= 16384 only — on the 70B shapes at M = 512 the long-K down projection is 131 vs 148 us
-    against hipBLASLt; at K = 8192 hipBLASLt wins in isolation, O 41 vs 52 us)."""
-    if K < 16384 and not fp8_tile_all():
-        return 0
+    """``tile_gemm_splits`` for the fp8 kernels (every fp8 decode projection runs on the
+    hand-written block-scaled MFMA tile kernels: QKV / O / down split-K with their partials
+    reduced by the consumer kernels, gate|up with the fused SwiGLU epilogue;
+    profiles/fp8_tile_all_vs_long.json)."""
     return tile_gemm_splits(M, N, K, elem_bytes=1)
 
 

@@ -20,7 +20,8 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
-from ..config import CacheConfig, ModelSpec, ServeConfig, plan_stages, resolve_model
+from .. import ops
+from ..config import CacheConfig, KernelPolicy, ModelSpec, ServeConfig, plan_stages, resolve_model
 from ..models.llama.cache import KVPool
 from ..parallel.pipeline import (DistributedDriver, LocalPipeline, StageFollower, _Channels,
                                  make_transport)
@@ -46,6 +47,8 @@ class EngineConfig:
     dp: int = 1                     # pipeline replicas (world = dp x pp in init_pipeline_rank)
     cache: CacheConfig = field(default_factory=CacheConfig)
     serve: ServeConfig = field(default_factory=ServeConfig)
+    # hot-path kernel choices; None keeps the process's current policy (ops.policy())
+    kernels: Optional[KernelPolicy] = None
 
 
 def _activation_reserve(spec: ModelSpec, serve: ServeConfig) -> int:
@@ -58,6 +61,8 @@ def _activation_reserve(spec: ModelSpec, serve: ServeConfig) -> int:
 def build_executor(spec: ModelSpec, start: int, end: int, device: torch.device, cfg: EngineConfig,
                    group=None, num_blocks: Optional[int] = None,
                    kv_share: float = 1.0) -> StageExecutor:
+    if cfg.kernels is not None:   # before any weight conversion reads it (int8_transposed)
+        ops.set_policy(cfg.kernels)
     stage = build_stage(cfg.checkpoint or spec, start, end, device=device,
                         random_init=cfg.random_init and cfg.checkpoint is None, seed=cfg.seed,
                         quantize=cfg.quantize, checkpoint=cfg.checkpoint,
@@ -304,15 +309,10 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     from .watchdog import TRACKER, start_watchdog
     start_watchdog(base_job, world, on_abort=getattr(transport, "abort", None))
     TRACKER.add_state("transport", transport.counters)
-    if device.type == "cuda" and world > 1 and os.environ.get("DLI_DEVICE_MARKS", "1") == "1":
+    if device.type == "cuda" and world > 1:
         TRACKER.enable_device_marks(device)
     # the fallback transport (agreed on by every rank) cannot carry the head: then nobody rotates
     rotate = rotate and transport.supports_head
-    if rotate:
-        # the head's side stream runs kernels next to the stage's layers: keep batch-1 decode off
-        # the grid-barrier decode-layer kernel (it needs every workgroup resident at once)
-        from .. import ops
-        ops.block_decode_layer(True)
     head_rotation = rotate   # recorded on the returned driver / follower (bench per-rank records)
     channels = _Channels(job, srank, pp, head_rotation=rotate)
     policy = HeadPolicy(pp, rotate, ex.max_num_seqs)
@@ -323,7 +323,7 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
         heads_runner = HeadRunner(head, device, ex.max_num_seqs, cfg.serve.use_graphs,
                                   ex.graph_sizes,
                                   capture_stream=streams.capture if streams is not None else None)
-    if device.type == "cuda" and cfg.serve.use_graphs and os.environ.get("DLI_PRECAPTURE", "1") == "1":
+    if device.type == "cuda" and cfg.serve.use_graphs:
         # capture every decode graph NOW, before any transport traffic: no capture ever runs
         # next to in-flight receive kernels or the token publisher thread
         variants = (True, False) if (rotate and srank == pp - 1) else (True,)

@@ -37,10 +37,11 @@ log = logging.getLogger(__name__)
 
 import os as _os  # noqa: E402
 
-# DLI_TRACE=1: roctx range per stage step (visible with rocprofv3 --marker-trace / torch profiler)
-# DLI_DEBUG_SYNC=1: synchronise after every stage step and check outputs (NaN/Inf, token range)
-_TRACE = _os.environ.get("DLI_TRACE", "0") == "1"
-_DEBUG = _os.environ.get("DLI_DEBUG_SYNC", "0") == "1"
+# DLI_DEBUG (comma list): "trace" = roctx range per stage step (rocprofv3 --marker-trace / torch
+# profiler); "sync" = synchronise after every stage step and check outputs (NaN/Inf, token range)
+_DEBUG_FLAGS = {f.strip() for f in _os.environ.get("DLI_DEBUG", "").split(",")}
+_TRACE = "trace" in _DEBUG_FLAGS
+_DEBUG = "sync" in _DEBUG_FLAGS
 
 
 @dataclass

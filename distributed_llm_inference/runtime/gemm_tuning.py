@@ -56,8 +56,8 @@ def tune_decode_gemms(stage, batch_sizes: Iterable[int], results_file: Optional[
                       max_duration_ms: int = 60) -> None:
     if not torch.cuda.is_available() or stage.device.type != "cuda":
         return
-    if os.environ.get("DLI_TUNABLEOP", "1") == "0":
-        return
+    if os.environ.get("DLI_TUNING_DIR", "") == "off":
+        return   # DLI_TUNING_DIR=off: no TunableOp at all (tests, short runs)
     t = torch.cuda.tunable
     t.enable(True)
     for f in (SHIPPED, results_file):

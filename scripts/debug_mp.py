@@ -25,7 +25,7 @@ def cfgs(world, mbs, graphs):
 def worker(rank, world, port, mbs, graphs, q):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_SHARE_GPU="1",
-                      DLI_TRANSPORT="host", DLI_TUNABLEOP="0")
+                      DLI_TRANSPORT="host", DLI_TUNING_DIR="off")
     import torch.distributed as dist
     from distributed_llm_inference.runtime.engine import init_pipeline_rank
     from distributed_llm_inference.runtime.sequence import SamplingParams
@@ -41,7 +41,7 @@ def worker(rank, world, port, mbs, graphs, q):
 
 
 def main():
-    os.environ["DLI_TUNABLEOP"] = "0"
+    os.environ["DLI_TUNING_DIR"] = "off"
     from distributed_llm_inference.runtime.engine import LLMEngine
     from distributed_llm_inference.runtime.sequence import SamplingParams
     ctx = mp.get_context("spawn")

@@ -9,7 +9,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I distributed_llm_inference/csrc/kernels \
 //         scripts/experiments/gemm4_bench.hip -o tools_bin/gemm4_bench
 //   tools_bin/gemm4_bench [rounds] [gate|up grid override]
-#define DLI_GEMM_STAMPS 1
+#define GEMM_STAMPS 1
 #define DLI_GEMM4_ALL_VARIANTS 1
 #include "../../distributed_llm_inference/csrc/kernels/gemm_tile.hip"
 #include "../../distributed_llm_inference/csrc/kernels/gemm4.hip"

@@ -6,7 +6,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I distributed_llm_inference/csrc/kernels \
 //         -I scripts/experiments scripts/experiments/gemm_bn_bench.hip -o tools_bin/gemm_bn_bench
-#define DLI_GEMM_STAMPS 1
+#define GEMM_STAMPS 1
 #include "gemm_tile_bn.hip"   // scripts/experiments: the generalized (rejected) kernel
 
 #include <algorithm>

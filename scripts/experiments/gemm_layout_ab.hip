@@ -14,7 +14,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I distributed_llm_inference/csrc/kernels \
 //         -I scripts/experiments scripts/experiments/gemm_layout_ab.hip -o tools_bin/gemm_layout_ab
-#define DLI_GEMM_STAMPS 1
+#define GEMM_STAMPS 1
 #include "gemm_tile_bn.hip"
 namespace dli_old { using namespace dli; }
 #define dli dli_old

@@ -1,6 +1,6 @@
 // Clock-stamp diagnostic of the tile GEMM (standalone, no torch): where does a decode-shape
-// GEMM spend its time?  Builds gemm_tile.hip with DLI_GEMM_STAMPS (per-workgroup begin/end
-// shader-cycle + wall stamps, HW ids) and optionally DLI_GEMM_STAMPS_KT_REMOVED (per-k-tile stamps of
+// GEMM spend its time?  Builds gemm_tile.hip with GEMM_STAMPS (per-workgroup begin/end
+// shader-cycle + wall stamps, HW ids) and optionally GEMM_STAMPS_KT_REMOVED (per-k-tile stamps of
 // wave 0), runs the 70B decode shapes at M = 512 on random operands with the weights rotated past
 // the Infinity Cache, and prints per case: wall us (events), per-workgroup duration (us, cycles),
 // clock, round structure (workgroups starting in the first vs later rounds and their durations),
@@ -10,7 +10,7 @@
 //         scripts/experiments/gemm_stamps.hip -o tools_bin/gemm_stamps && tools_bin/gemm_stamps
 // (the per-k-tile stamps of the profiles/gemm_clock_stamps.txt second half came from a wave-0
 // stamp at the top of every k-tile, since removed from the kernel: it perturbed the loop)
-#define DLI_GEMM_STAMPS 1
+#define GEMM_STAMPS 1
 #include "gemm_tile.hip"
 
 #include <algorithm>

@@ -109,7 +109,7 @@ __device__ __forceinline__ f32x4 mfma_i8(const bf16x8& a, const bf16x8& b, const
 
 enum Prec { kBf16 = 0, kFp8 = 1, kInt8 = 2 };
 
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
 // Diagnostic build only (scripts/gemm_stamps.hip, scripts/gemm_w4_bench.hip): per-workgroup clock
 // stamps (begin/end shader cycles and 100 MHz wall ticks, end of the main loop).  Never compiled
 // into the extension.
@@ -138,7 +138,7 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
   __shared__ __attribute__((aligned(1024))) char smem[kLds];
 
   const int tid = threadIdx.x;
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
   if (tid == 0) {
     unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
     st[0] = __builtin_amdgcn_s_memrealtime();
@@ -318,7 +318,7 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
     barrier();
   }
   if (grp == 0) barrier();
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
   if (tid == 0) {
     unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
     st[6] = __builtin_amdgcn_s_memrealtime();
@@ -396,7 +396,7 @@ gemm_tile_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void*
       }
     }
   }
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
   if (tid == 0) {
     unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
     st[2] = __builtin_amdgcn_s_memrealtime();

@@ -67,7 +67,7 @@ gemm_w4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __r
                int M, int N, int K, int tiles_m, int tiles_n, int kps) {
   __shared__ __attribute__((aligned(1024))) char smem[NS == 2 ? 2 * kW4Stage : NS * 32768];
   const int tid = threadIdx.x, lane = tid & 63;
-#ifdef DLI_GEMM_STAMPS   // diagnostic build only (g_stamp_blk: gemm_tile.hip, scripts/gemm_w4_bench.hip)
+#ifdef GEMM_STAMPS   // diagnostic build only (g_stamp_blk: gemm_tile.hip, scripts/gemm_w4_bench.hip)
   if (tid == 0) {
     unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
     st[0] = __builtin_amdgcn_s_memrealtime();
@@ -251,7 +251,7 @@ gemm_w4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __r
     asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]),
                  "+a"(acc[i][4]), "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
 
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
   if (tid == 0) {
     unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
     st[6] = __builtin_amdgcn_s_memrealtime();
@@ -306,7 +306,7 @@ gemm_w4_kernel(const bf16* __restrict__ A, const bf16* __restrict__ B, void* __r
       }
     }
   }
-#ifdef DLI_GEMM_STAMPS
+#ifdef GEMM_STAMPS
   if (tid == 0) {
     unsigned long long* st = g_stamp_blk + (size_t)blockIdx.x * 8;
     st[2] = __builtin_amdgcn_s_memrealtime();

@@ -8,7 +8,7 @@
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I distributed_llm_inference/csrc/kernels \
 //         -I scripts/experiments scripts/experiments/gemm_w4_bench.hip -o tools_bin/gemm_w4_bench
-#define DLI_GEMM_STAMPS 1
+#define GEMM_STAMPS 1
 #include "gemm_tile.hip"
 #include "gemm_w4.hip"
 

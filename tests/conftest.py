@@ -21,6 +21,16 @@ def _native_runtime():
     yield
 
 
+@pytest.fixture(autouse=True)
+def _restore_kernel_policy():
+    """A test may change the process's kernel policy (ops.kernel_policy / set_policy): every
+    test starts from, and leaves, the policy it found."""
+    from distributed_llm_inference import ops
+    saved = ops._POLICY
+    yield
+    ops._POLICY = saved
+
+
 def gpu_available():
     try:
         import torch

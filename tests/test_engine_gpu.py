@@ -135,13 +135,12 @@ def test_fp8_stage_gpu_matches_cpu(gpu):
     assert rel < 0.05, rel
 
 
-def test_fp8_tile_path_fused_swiglu_matches_cpu(gpu, monkeypatch):
-    """fp8 weights on the hand-written tile GEMMs (DLI_FP8_TILE=all): QKV partials into the RoPE
-    kernel, O partials into the fused norm + quantiser, gate|up with the SwiGLU epilogue on
-    pairwise-interleaved fp8 rows + scales, down partials into the next layer's quantiser — against
-    the CPU dequantised reference with identical fp8 weights (prefill of 384 tokens) and the
-    hipBLASLt fp8 path (+ a 128-sequence decode step; both take the tile path)."""
-    monkeypatch.setenv("DLI_FP8_TILE", "all")
+def test_fp8_tile_path_fused_swiglu_matches_cpu(gpu):
+    """fp8 weights on the hand-written tile GEMMs: QKV partials into the RoPE kernel, O partials
+    into the fused norm + quantiser, gate|up with the SwiGLU epilogue on pairwise-interleaved fp8
+    rows + scales, down partials into the next layer's quantiser — against the CPU dequantised
+    reference with identical fp8 weights (prefill of 384 tokens), and (+ a 128-sequence decode
+    step) against the unfused order (reduce passes, SwiGLU as a separate pass)."""
     spec = SPEC.replace(hidden_size=512, intermediate_size=1024, num_heads=8, num_kv_heads=2,
                         head_dim=64)
     prompts = [[(7 * i + j) % 997 + 1 for j in range(3)] for i in range(128)]
@@ -179,14 +178,13 @@ def test_fp8_tile_path_fused_swiglu_matches_cpu(gpu, monkeypatch):
     # (test_fp8_bf16_splitk_partials_close_to_fp32_partials measures both at the same 10 % from
     # the bf16-weight model)
     assert rel < 0.08, rel
-    # the decode step against the hipBLASLt fp8 path (unfused SwiGLU, reduce passes)
+    # the decode step against the unfused order (SwiGLU pass, reduce passes)
     g.block.set_fused_swiglu(False)
-    monkeypatch.setenv("DLI_FP8_TILE", "long")
-    c = prefill_then_decode(g)
+    with ops.kernel_policy(defer_splitk=False, fp8_mx=False):
+        c = prefill_then_decode(g)
     for x, y in zip(c, b):
         rel = ((x - y).norm() / x.norm()).item()
         assert rel < 0.08, rel
-    monkeypatch.setenv("DLI_FP8_TILE", "all")
     g.block.set_fused_swiglu(True)
     g.block.set_fused_swiglu(False)   # round trip restores the quantised rows exactly
     assert torch.equal(g.block.layers[0].mlp.gate_up_proj.weight_fp8.view(torch.uint8),
@@ -196,9 +194,8 @@ def test_fp8_tile_path_fused_swiglu_matches_cpu(gpu, monkeypatch):
 def test_fp8_mx_down_projection_engages_and_matches_per_row_path(gpu, monkeypatch):
     """fp8 decode with the SwiGLU output handed to the down projection as MX (e8m0 per row and
     128-column block, quantised in the gate|up epilogue) vs the bf16 h + per-row quantiser path
-    (DLI_FP8_MX=0): the MX kernels run for every layer, and against the bf16-weight logits the MX
-    path is no less accurate than the per-row one."""
-    monkeypatch.setenv("DLI_FP8_TILE", "all")
+    (KernelPolicy.fp8_mx=False): the MX kernels run for every layer, and against the bf16-weight
+    logits the MX path is no less accurate than the per-row one."""
     spec = SPEC.replace(hidden_size=512, intermediate_size=1024, num_heads=8, num_kv_heads=2,
                         head_dim=64)
     prompts = [[(5 * i + j) % 991 + 1 for j in range(4)] for i in range(256)]
@@ -229,12 +226,11 @@ def test_fp8_mx_down_projection_engages_and_matches_per_row_path(gpu, monkeypatc
     ref = decode(g)   # bf16 weights
     g.quantize_fp8()
     g.block.set_fused_swiglu(True)
-    monkeypatch.setenv("DLI_FP8_MX", "1")
     a = decode(g)
     n = len(calls)
     assert n >= 3, calls   # at least one MX down projection per layer (the decode step)
-    monkeypatch.setenv("DLI_FP8_MX", "0")
-    b = decode(g)
+    with ops.kernel_policy(fp8_mx=False):
+        b = decode(g)
     assert len(calls) == n
     # two fp8 quantisations of h differ by ~fp8 resolution; against the bf16 model the MX path
     # (finer, per-block scales) is no worse than the per-row one
@@ -344,14 +340,13 @@ def test_int8_fused_path_matches_unfused(gpu, monkeypatch):
 
     # fp32 partials on both sides: this compares the fused epilogue with the unfused path (bf16
     # partials are checked against the bf16 model in test_8bit_bf16_splitk_partials_*)
-    monkeypatch.setenv("DLI_FP8_BF16_PARTS", "0")
-    monkeypatch.setenv("DLI_SPLITK_DEFER", "0")
-    a = run()
-    monkeypatch.setenv("DLI_SPLITK_DEFER", "1")
+    with ops.kernel_policy(bf16_partials=False, defer_splitk=False):
+        a = run()
     wq0 = g.block.layers[0].mlp.gate_up_proj.weight_int8.clone()
     g.block.set_fused_swiglu(True)
     assert g.block.layers[0].mlp.fused_swiglu
-    b = run()
+    with ops.kernel_policy(bf16_partials=False):
+        b = run()
     for x, y in zip(a, b):
         rel = ((x - y).norm() / x.norm()).item()
         assert rel < 0.02, rel
@@ -359,27 +354,26 @@ def test_int8_fused_path_matches_unfused(gpu, monkeypatch):
     assert torch.equal(g.block.layers[0].mlp.gate_up_proj.weight_int8, wq0)
 
 
-def test_deferred_splitk_reduce_is_bit_identical(gpu, monkeypatch):
+def test_deferred_splitk_reduce_is_bit_identical(gpu):
     """Split-K partials reduced inside the next RMSNorm (default) vs the separate reduce pass
-    (DLI_SPLITK_DEFER=0): same bf16 rounding points, so the stage output is bit-identical."""
+    (KernelPolicy.defer_splitk=False): same bf16 rounding points, so the stage output is
+    bit-identical."""
     spec = SPEC.replace(hidden_size=512, intermediate_size=1024, num_heads=4, num_kv_heads=2,
                         head_dim=128)
     g = CausalLMStage(spec, 0, 4, device=gpu).init_random(5)
     prompts = [list(range(1, 200)), list(range(3, 150))]   # 347 rows: tile GEMMs with split-K
-    monkeypatch.setenv("DLI_BF16_PARTS", "0")   # fp32 partials: the bit-identity claim
-    a = _stage_logits(g, prompts, 0)[0]
-    monkeypatch.setenv("DLI_SPLITK_DEFER", "0")
-    b = _stage_logits(g, prompts, 0)[0]
+    with ops.kernel_policy(bf16_partials=False):   # fp32 partials: the bit-identity claim
+        a = _stage_logits(g, prompts, 0)[0]
+        with ops.kernel_policy(bf16_partials=False, defer_splitk=False):
+            b = _stage_logits(g, prompts, 0)[0]
     assert torch.equal(a, b)
     # default bf16 partials (one extra bf16 rounding per partial): close, not identical
-    monkeypatch.setenv("DLI_SPLITK_DEFER", "1")
-    monkeypatch.setenv("DLI_BF16_PARTS", "1")
     c = _stage_logits(g, prompts, 0)[0]
     rel = ((c.float() - b.float()).norm() / b.float().norm()).item()
     assert rel < 1e-2, rel
 
 
-def test_deferred_splitk_reduce_is_bit_identical_fp8(gpu, monkeypatch):
+def test_deferred_splitk_reduce_is_bit_identical_fp8(gpu):
     """fp8 weights: the long-K down projection (fp8 tile GEMM, split-K) hands its partials to the
     next layer's fused RMSNorm + fp8 quantiser; bit-identical to the separate reduce pass."""
     spec = SPEC.replace(hidden_size=512, intermediate_size=16384, num_heads=4, num_kv_heads=2,
@@ -387,10 +381,10 @@ def test_deferred_splitk_reduce_is_bit_identical_fp8(gpu, monkeypatch):
     g = CausalLMStage(spec, 0, 3, device=gpu).init_random(6)
     g.quantize_fp8()
     prompts = [list(range(1, 200)), list(range(3, 150))]
-    monkeypatch.setenv("DLI_FP8_BF16_PARTS", "0")   # fp32 partials: the bit-identity claim
-    a = _stage_logits(g, prompts, 0)[0]
-    monkeypatch.setenv("DLI_SPLITK_DEFER", "0")
-    b = _stage_logits(g, prompts, 0)[0]
+    with ops.kernel_policy(bf16_partials=False):   # fp32 partials: the bit-identity claim
+        a = _stage_logits(g, prompts, 0)[0]
+    with ops.kernel_policy(bf16_partials=False, defer_splitk=False):
+        b = _stage_logits(g, prompts, 0)[0]
     assert torch.equal(a, b)
 
 
@@ -399,7 +393,6 @@ def test_8bit_bf16_splitk_partials_as_accurate_as_fp32(gpu, monkeypatch, mode):
     """8-bit weights with bf16 split-K partials (gemm_tile epilogue 4, summed in fp32 by the RoPE
     kernel and the fused norm (+ quantiser) consumers) vs fp32 partials, a 256-sequence decode step
     through QKV / O / down split-K: both equally far from the bf16-weight model."""
-    monkeypatch.setenv("DLI_FP8_TILE", "all")
     spec = SPEC.replace(hidden_size=512, intermediate_size=2048, num_heads=8, num_kv_heads=2,
                         head_dim=64)
     g = CausalLMStage(spec, 0, 3, device=gpu).init_random(8)
@@ -417,7 +410,10 @@ def test_8bit_bf16_splitk_partials_as_accurate_as_fp32(gpu, monkeypatch, mode):
     nat = _N()
 
     def decode(parts):
-        monkeypatch.setenv("DLI_FP8_BF16_PARTS", parts)
+        with ops.kernel_policy(bf16_partials=parts == "1"):
+            return _decode()
+
+    def _decode():
         pool = g.make_pool(256, block_size=64)
         sids = list(range(len(prompts)))
         for sid, p in zip(sids, prompts):
@@ -555,8 +551,8 @@ def test_rotating_head_split_matches_local_head(gpu, temperature):
 
 
 def test_bf16_splitk_partials_end_to_end_vs_cpu_reference(gpu, monkeypatch):
-    """Default bf16 path: QKV / O / down split-K partials stored as bf16 (DLI_BF16_PARTS=1, gemm_tile
-    epilogue 4) vs fp32 partials (=0), a 256-sequence decode step, each against the fp32 CPU
+    """Default bf16 path: QKV / O / down split-K partials stored as bf16 (gemm_tile / gemm4
+    epilogue 4) vs fp32 partials, a 256-sequence decode step, each against the fp32 CPU
     reference of the same weights (the extra rounding is bounded end to end)."""
     spec = SPEC.replace(hidden_size=1024, intermediate_size=2048, num_heads=16, num_kv_heads=4,
                         head_dim=64)
@@ -579,8 +575,10 @@ def test_bf16_splitk_partials_end_to_end_vs_cpu_reference(gpu, monkeypatch):
             return spy
 
     def decode(stage, parts=None):
-        if parts is not None:
-            monkeypatch.setenv("DLI_BF16_PARTS", parts)
+        with ops.kernel_policy(bf16_partials=parts != "0"):
+            return _decode(stage)
+
+    def _decode(stage):
         dev = stage.device
         pool = stage.make_pool(256, block_size=64)
         sids = list(range(len(prompts)))
@@ -614,7 +612,7 @@ def test_bf16_splitk_partials_end_to_end_vs_cpu_reference(gpu, monkeypatch):
 @pytest.mark.parametrize("mode", ["fp8", "int8"])
 def test_8bit_gemv_vs_quantised_path_bounded(gpu, monkeypatch, mode):
     """1-2 decode rows take the weight-streaming GEMV on bf16 activations; >= 3 rows (or
-    DLI_*_GEMV=0) quantise the activations (fp8 rows / LLM.int8 with outlier split).  Both stay
+    KernelPolicy.gemv=False) quantise the activations (fp8 rows / LLM.int8 with outlier split).  Both stay
     close to the fp32 product of the same 8-bit weights, and the GEMV is the closer of the two, so
     the batch-size dependence of a row's output is bounded (docs/parity.md C11)."""
     from distributed_llm_inference.models.common import Linear
@@ -626,16 +624,13 @@ def test_8bit_gemv_vs_quantised_path_bounded(gpu, monkeypatch, mode):
     if mode == "fp8":
         lin.quantize_fp8()
         wdq = lin.weight_fp8.float() * lin.weight_scale.float().view(-1, 1)
-        env = "DLI_FP8_GEMV"
     else:
         lin.quantize_int8(threshold=6.0)
         wdq = lin.weight_int8.float() * lin.weight_scale.float().view(-1, 1)
-        env = "DLI_INT8_GEMV"
     ref = x.float() @ wdq.t()
-    monkeypatch.setenv(env, "1")
     a = lin(x).float()
-    monkeypatch.setenv(env, "0")
-    b = lin(x).float()
+    with ops.kernel_policy(gemv=False):
+        b = lin(x).float()
     ea = ((a - ref).norm() / ref.norm()).item()
     eb = ((b - ref).norm() / ref.norm()).item()
     eab = ((a - b).norm() / ref.norm()).item()
@@ -645,15 +640,15 @@ def test_8bit_gemv_vs_quantised_path_bounded(gpu, monkeypatch, mode):
 
 @pytest.mark.parametrize("quantize", [False, "fp8", "int8"])
 def test_gemv_fused_norm_path_matches_unfused_decode(gpu, monkeypatch, quantize):
-    """1-2 row decode with the RMSNorms fused into the QKV / gate|up GEMVs (DLI_GEMV_NORM=1,
+    """1-2 row decode with the RMSNorms fused into the QKV / gate|up GEMVs (KernelPolicy.gemv_norm,
     default) against the unfused order: bf16 weights give identical greedy tokens; 8-bit
     weights (the fused path feeds bf16 rows instead of quantised ones) stay close."""
     prompts = [list(range(3, 40))]
 
     def run(flag):
-        monkeypatch.setenv("DLI_GEMV_NORM", flag)
-        eng = _engine(graphs=False, quantize=quantize)
-        outs = eng.generate(prompts, SamplingParams(max_tokens=12, temperature=0.0))
+        with ops.kernel_policy(gemv_norm=flag == "1"):
+            eng = _engine(graphs=False, quantize=quantize)
+            outs = eng.generate(prompts, SamplingParams(max_tokens=12, temperature=0.0))
         return [o.output for o in outs]
 
     a, b = run("1"), run("0")
@@ -665,7 +660,7 @@ def test_gemv_fused_norm_path_matches_unfused_decode(gpu, monkeypatch, quantize)
 
 
 def test_gemm4_dispatch_bit_identical_in_a_decode_step(gpu, monkeypatch):
-    """DLI_GEMM4=1 routes the bf16 decode projections to gemm4.hip (same epilogues: split-K
+    """KernelPolicy.gemm4 routes the bf16 decode projections to gemm4.hip (same epilogues: split-K
     partials into the norms / RoPE, fused SwiGLU): a 256-sequence decode step's logits are
     bit-identical to the gemm_tile ones."""
     spec = SPEC.replace(hidden_size=512, intermediate_size=1024, num_heads=8, num_kv_heads=4,
@@ -675,7 +670,10 @@ def test_gemm4_dispatch_bit_identical_in_a_decode_step(gpu, monkeypatch):
     prompts = [[(3 * i + j) % 977 + 1 for j in range(3)] for i in range(256)]
 
     def step(flag):
-        monkeypatch.setenv("DLI_GEMM4", flag)
+        with ops.kernel_policy(gemm4=flag == "1"):
+            return _step()
+
+    def _step():
         pool = g.make_pool(320, block_size=64)   # one block per sequence
         sids = list(range(len(prompts)))
         for sid, p in zip(sids, prompts):

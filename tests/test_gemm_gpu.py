@@ -107,13 +107,15 @@ def test_linear_dispatches_decode_batches_to_tile_gemm(gpu, monkeypatch):
 
 
 def test_no_library_gemms_keeps_small_and_wide_products_on_the_tile_kernel(gpu, monkeypatch):
-    """DLI_GEMM_LIB=0 (default when ranks share a GPU): M < 128 and the wide LM head stay on the
+    """KernelPolicy.library_gemms=False (the default when ranks share a GPU): M < 128 and the wide
+    LM head stay on the
     tile kernel (hipBLASLt's choices there are stream-K persistent kernels); the rotating head's
     projection always does (LMHead.project(tile=True))."""
     from distributed_llm_inference.config import PRESETS
     from distributed_llm_inference.models.common import Linear
     from distributed_llm_inference.models.embed_head import LMHead
-    monkeypatch.setenv("DLI_GEMM_LIB", "0")
+    cm = ops.kernel_policy(library_gemms=False)
+    cm.__enter__()
     calls = []
     real = ops.gemm_tile
     monkeypatch.setattr(ops, "gemm_tile", lambda *a, **k: calls.append(a[1].shape) or real(*a, **k))
@@ -124,7 +126,7 @@ def test_no_library_gemms_keeps_small_and_wide_products_on_the_tile_kernel(gpu, 
         ref = x.float() @ lin.weight.float().t()
         assert (lin(x).float() - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
     assert len(calls) == 3, calls
-    monkeypatch.setenv("DLI_GEMM_LIB", "1")
+    cm.__exit__(None, None, None)   # library GEMMs allowed again: the head's tile=True still holds
     spec = PRESETS["llama-3-8b"].replace(hidden_size=1024, vocab_size=256 * 300)
     head = LMHead(spec, device=gpu).init_random(3)
     x = torch.randn(32, 1024, device=gpu, dtype=torch.bfloat16)
@@ -464,9 +466,10 @@ def test_gemm_tile_stream_k_matches_fp32(gpu, M, N, K, swiglu):
 
 
 def test_gemm_tile_stream_k_dispatch_and_graph(gpu, monkeypatch):
-    """With DLI_TILE_SK=1 ops.gemm_tile picks the stream-K tail for the 70B gate|up shape, also
-    under graph replay."""
-    monkeypatch.setenv("DLI_TILE_SK", "1")
+    """With KernelPolicy.stream_k_tail ops.gemm_tile picks the stream-K tail for the 70B gate|up
+    shape, also under graph replay."""
+    cm = ops.kernel_policy(stream_k_tail=True, gemm4=False)
+    cm.__enter__()
     if ops.device_cus(gpu) != 256:
         pytest.skip("shape sized for 256 CUs")
     M, I, K = 512, 28672, 512
@@ -516,9 +519,11 @@ def test_rms_norm_splitk_bit_identical_to_reduce_then_norm(gpu, S, M, H, mode):
 
 @pytest.mark.parametrize("bf16_parts", ["0", "1"])
 def test_gemm_tile_defer_reduce_feeds_rms_norm(gpu, monkeypatch, bf16_parts):
-    """fp32 partials (DLI_BF16_PARTS=0): the consumer's sum is bit-identical to the reduce pass;
-    bf16 partials (default): each partial carries one extra bf16 rounding - close, not equal."""
-    monkeypatch.setenv("DLI_BF16_PARTS", bf16_parts)
+    """fp32 partials (KernelPolicy.bf16_partials=False): the consumer's sum is bit-identical to the
+    reduce pass; bf16 partials (default): each partial carries one extra bf16 rounding - close,
+    not equal."""
+    cm = ops.kernel_policy(bf16_partials=bf16_parts == "1")
+    cm.__enter__()
     torch.manual_seed(11)
     M, N, K = 512, 8192, 8192
     x = torch.randn(M, K, device=gpu, dtype=torch.bfloat16)

@@ -112,9 +112,11 @@ def test_rope_cache_from_splitk_partials_bit_identical(gpu, nh, nkv, D, S, fp8):
 @pytest.mark.parametrize("nh,nkv,D,S", [(64, 8, 128, 3), (8, 8, 64, 0), (4, 2, 32, 2)])
 @pytest.mark.parametrize("fp8", [False, True])
 @pytest.mark.parametrize("parts_bf16", [False, True])
-def test_rope_cache_v8_bit_identical_to_v4(gpu, monkeypatch, nh, nkv, D, S, fp8, parts_bf16):
+def test_rope_cache_v8_bit_identical_to_v4(gpu, nh, nkv, D, S, fp8, parts_bf16):
     """The 16-byte kernel (default for D % 16 == 0) computes every element exactly as the
-    4-element kernel (DLI_ROPE_V8=0): q, q_sink, K and V^T caches, bf16 / fp32 / bf16 partials."""
+    4-element kernel - which runs when a bf16 qkv row stride is not a multiple of 8 - fed the
+    reduced input (split-K partials summed in fp32 in split order, rounded to bf16 once): q,
+    q_sink, K and V^T caches, bf16 / fp32 / bf16 partials."""
     if S == 0 and parts_bf16:
         pytest.skip("no partials")
     torch.manual_seed(21)
@@ -122,9 +124,18 @@ def test_rope_cache_v8_bit_identical_to_v4(gpu, monkeypatch, nh, nkv, D, S, fp8,
     width = (nh + 2 * nkv) * D
     if S:
         parts = torch.randn(S, T, width, device=gpu)
-        src = ops.SplitKPartials(parts.to(torch.bfloat16) if parts_bf16 else parts)
+        parts = parts.to(torch.bfloat16) if parts_bf16 else parts
+        src = ops.SplitKPartials(parts)
+        acc = parts[0].float()
+        for i in range(1, S):
+            acc = acc + parts[i].float()
+        red = acc.to(BF)
     else:
-        src = torch.randn(T, width, device=gpu, dtype=BF)
+        src = red = torch.randn(T, width, device=gpu, dtype=BF)
+    # the same values at a row stride of width + 4 (not a multiple of 8): the 4-element kernel
+    odd = torch.zeros(T, width + 4, device=gpu, dtype=BF)
+    odd[:, :width] = red
+    src_v4 = odd[:, :width]
     pos = torch.randint(0, 300, (T,), device=gpu, dtype=torch.int32)
     slots = torch.randperm(nblocks * bs, device=gpu)[:T].to(torch.int64)
     slots[7] = -1
@@ -134,9 +145,8 @@ def test_rope_cache_v8_bit_identical_to_v4(gpu, monkeypatch, nh, nkv, D, S, fp8,
         k1, v1 = k1.to(torch.float8_e4m3fn), v1.to(torch.float8_e4m3fn)
     k2, v2 = k1.clone(), v1.clone()
     outs = []
-    for v8, (k, v) in (("1", (k1, v1)), ("0", (k2, v2))):
-        monkeypatch.setenv("DLI_ROPE_V8", v8)
-        outs.append(ops.rope_cache(src, pos, slots, cs, nh, nkv, D, k, v, window=100,
+    for x, (k, v) in ((src, (k1, v1)), (src_v4, (k2, v2))):
+        outs.append(ops.rope_cache(x, pos, slots, cs, nh, nkv, D, k, v, window=100,
                                    want_sink=True, k_scale=0.5, v_scale=0.25))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     assert torch.equal(k1.view(torch.uint8), k2.view(torch.uint8))
@@ -178,30 +188,28 @@ def test_quant_rowwise_bf16_partials_match_fp32_partials(gpu, S, rows, K):
 
 
 @pytest.mark.parametrize("M,N,K,splits", [(512, 1024, 8192, 4), (300, 768, 2048, 3)])
-def test_gemm_tile_fp8_bf16_partials(gpu, M, N, K, splits, monkeypatch):
+def test_gemm_tile_fp8_bf16_partials(gpu, M, N, K, splits):
     """gemm_tile epilogue 4 (fp8, split-K partials rounded to bf16) against the fp32 partials."""
     torch.manual_seed(M + K)
     xq, xs = ops.quant_rowwise(torch.randn(M, K, device=gpu).to(BF))
     wq, ws = ops.quantize_weight_fp8((torch.randn(N, K, device=gpu) / K ** 0.5).to(BF))
-    monkeypatch.setenv("DLI_FP8_BF16_PARTS", "0")
-    pf = ops.gemm_tile_fp8(xq, xs, wq, ws, splits, defer_reduce=True).parts
-    monkeypatch.setenv("DLI_FP8_BF16_PARTS", "1")
+    with ops.kernel_policy(bf16_partials=False):
+        pf = ops.gemm_tile_fp8(xq, xs, wq, ws, splits, defer_reduce=True).parts
     pb = ops.gemm_tile_fp8(xq, xs, wq, ws, splits, defer_reduce=True).parts
     assert pb.dtype == BF and pf.dtype == torch.float32
     assert torch.equal(pb, pf.to(BF))
 
 
 @pytest.mark.parametrize("M,N,K,splits", [(512, 1024, 8192, 4), (300, 768, 2048, 3)])
-def test_gemm_tile_bf16_operand_bf16_partials(gpu, M, N, K, splits, monkeypatch):
-    """bf16 operands, DLI_BF16_PARTS=1: epilogue 4 writes each split's fp32 partial rounded to
+def test_gemm_tile_bf16_operand_bf16_partials(gpu, M, N, K, splits):
+    """bf16 operands, bf16 partials (default): epilogue 4 writes each split's fp32 partial rounded to
     bf16 - exactly the fp32 partials' rounding - and RMSNorm over them stays within one bf16
     ulp-scale of the fp32-partials result."""
     torch.manual_seed(M + K + 1)
     x = torch.randn(M, K, device=gpu).to(BF)
     w = (torch.randn(N, K, device=gpu) / K ** 0.5).to(BF)
-    monkeypatch.setenv("DLI_BF16_PARTS", "0")
-    pf = ops.gemm_tile(x, w, splits, defer_reduce=True).parts
-    monkeypatch.setenv("DLI_BF16_PARTS", "1")
+    with ops.kernel_policy(bf16_partials=False):
+        pf = ops.gemm_tile(x, w, splits, defer_reduce=True).parts
     pb = ops.gemm_tile(x, w, splits, defer_reduce=True).parts
     assert pb.dtype == BF and pf.dtype == torch.float32
     assert torch.equal(pb, pf.to(BF))
@@ -306,8 +314,8 @@ def test_attn_decode_window_multi_wrap(gpu, splits):
 @pytest.mark.parametrize("nh,nkv,D", [(32, 8, 128), (8, 8, 64), (4, 2, 32)])
 @pytest.mark.parametrize("tiles", [False, True])
 @pytest.mark.parametrize("qb", ["1", "2"])
-def test_attn_prefill(gpu, nh, nkv, D, tiles, qb, monkeypatch):
-    monkeypatch.setenv("DLI_PREFILL_QB", qb)   # 16-token query blocks per wave
+def test_attn_prefill(gpu, nh, nkv, D, tiles, qb):
+    qb = int(qb)   # 16-token query blocks per wave
     torch.manual_seed(4)
     bs = 64
     q_lens = [5, 64, 130, 1, 1, 1]  # mixed batch: prefill chunks and decode rows
@@ -322,9 +330,9 @@ def test_attn_prefill(gpu, nh, nkv, D, tiles, qb, monkeypatch):
     bt = _tables(B, max_blocks, nblocks, gpu, seed=2)
     q = torch.randn(T, nh, D, device=gpu, dtype=BF)
     scale = 1 / math.sqrt(D)
-    tm = ops.prefill_tiles(q_lens, nh, nkv).to(gpu) if tiles else None
+    tm = ops.prefill_tiles(q_lens, nh, nkv, qb=qb).to(gpu) if tiles else None
     out = ops.attn_prefill(q, None, kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens), scale,
-                           tile_map=tm)
+                           tile_map=tm, qb=qb)
     out_r = ref.attn_prefill(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale)
     _close(out, out_r, 2e-2, 2e-2, "prefill")
 
@@ -376,8 +384,8 @@ def test_attn_prefill_custom_mask(gpu, heads, D):
 
 
 @pytest.mark.parametrize("qb", ["1", "2"])
-def test_attn_prefill_window(gpu, qb, monkeypatch):
-    monkeypatch.setenv("DLI_PREFILL_QB", qb)
+def test_attn_prefill_window(gpu, qb):
+    qb = int(qb)
     torch.manual_seed(5)
     nh, nkv, D, bs = 8, 2, 64, 64
     n_sink, sink_pad, window, ring = 4, 32, 96, 192
@@ -392,7 +400,7 @@ def test_attn_prefill_window(gpu, qb, monkeypatch):
     qs = torch.randn(47, nh, D, device=gpu, dtype=BF)
     scale = 1 / math.sqrt(D)
     out = ops.attn_prefill(q, qs, kc, vc, bt, lens.to(gpu), q_start.to(gpu), 40, scale, n_sink,
-                           sink_pad, ring, window)
+                           sink_pad, ring, window, qb=qb)
     out_r = ref.attn_prefill(q.cpu(), qs.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale,
                              n_sink, sink_pad, ring, window)
     _close(out, out_r, 2e-2, 2e-2, "prefill-window")
@@ -627,10 +635,10 @@ def test_attn_decode_fp8_kv_window_sinks(gpu, splits):
 
 
 @pytest.mark.parametrize("qb", ["1", "2"])
-def test_attn_prefill_long_chunks(gpu, qb, monkeypatch):
+def test_attn_prefill_long_chunks(gpu, qb):
     """70B head config, long causal chunks on top of cached context (multi-tile workgroups, the
     diagonal inside a two-block wave tile, a chunk length that is not a tile multiple)."""
-    monkeypatch.setenv("DLI_PREFILL_QB", qb)
+    qb = int(qb)
     torch.manual_seed(24)
     nh, nkv, D, bs = 64, 8, 128, 64
     q_lens, ctx = [1000, 77, 2048], [0, 900, 64]
@@ -642,9 +650,9 @@ def test_attn_prefill_long_chunks(gpu, qb, monkeypatch):
     bt = _tables(B, max_blocks, B * max_blocks, gpu, seed=6)
     q = torch.randn(int(q_start[-1]), nh, D, device=gpu, dtype=BF)
     scale = 1 / math.sqrt(D)
-    tm = ops.prefill_tiles(q_lens, nh, nkv).to(gpu)
+    tm = ops.prefill_tiles(q_lens, nh, nkv, qb=qb).to(gpu)
     out = ops.attn_prefill(q, None, kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens), scale,
-                           tile_map=tm)
+                           tile_map=tm, qb=qb)
     out_r = ref.attn_prefill(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale)
     _close(out, out_r, 2e-2, 2e-2, f"prefill-long-qb{qb}")
 
@@ -685,10 +693,11 @@ def test_quant_rowwise_from_splitk_partials_bit_identical(gpu, S, rows, K, with_
 
 
 @pytest.mark.parametrize("V", [128256, 32000, 50304])
-def test_sample_register_path_matches_radix_path(gpu, V, monkeypatch):
-    """The register-resident top-k / top-p search (sampling.hip sample_row_regs) keeps the same
-    set as the radix-histogram path and draws the same Gumbel sample: identical tokens for
-    seeded rows over temperatures, top-k and top-p values (bf16 logits, V % 8 == 0)."""
+def test_sample_register_path_matches_radix_path(gpu, V):
+    """The register-resident top-k / top-p search (sampling.hip sample_row_regs, bf16 logits with
+    V % 8 == 0) keeps the same set as the radix-histogram path (the same values as fp32 logits)
+    and draws the same Gumbel sample: identical tokens for seeded rows over temperatures, top-k
+    and top-p values."""
     torch.manual_seed(V)
     B = 24
     logits = (torch.randn(B, V, device=gpu) * torch.linspace(0.5, 6, B, device=gpu)[:, None]).to(BF)
@@ -698,10 +707,9 @@ def test_sample_register_path_matches_radix_path(gpu, V, monkeypatch):
     seeds = torch.arange(B, device=gpu) * 7919 + 3
     ctr = torch.arange(B, device=gpu, dtype=torch.int64) + 100
     out = {}
-    for path in ("1", "0"):
-        monkeypatch.setenv("DLI_SAMPLE_REGS", path)
+    for path, lg in (("1", logits), ("0", logits.float())):
         lp = torch.empty(B, device=gpu)
-        tok = ops.sample(logits, temperature=t, top_k=ks, top_p=ps, seeds=seeds, counters=ctr,
+        tok = ops.sample(lg, temperature=t, top_k=ks, top_p=ps, seeds=seeds, counters=ctr,
                          logprobs=lp)
         out[path] = (tok.cpu(), lp.cpu())
     assert torch.equal(out["1"][0], out["0"][0]), (out["1"][0], out["0"][0])
@@ -855,62 +863,3 @@ def test_skinny_gemm_qkv_rope_matches_gemv_then_rope_cache(gpu, wdtype, kv_fp8, 
         assert torch.equal(q, q_ref)
         for a, b in zip(caches[0], caches[1]):
             assert torch.equal(a.view(torch.uint8), b.view(torch.uint8))
-
-
-@pytest.mark.parametrize("fp8", [False, True])
-@pytest.mark.parametrize("splits,lens", [(8, [600]), (16, [600, 1100]), (64, [8192, 3000, 17]),
-                                         (128, [16384, 2, 600, 9000])])
-def test_attn_decode_last_merge_matches_combine(gpu, monkeypatch, fp8, splits, lens):
-    """The last-arriving workgroup's in-kernel merge (DLI_ATTN_MERGE=1, head dim 128) uses the
-    combine kernel's arithmetic: bit-identical outputs, with one workspace reused across launches
-    (its counters must come back to zero)."""
-    torch.manual_seed(splits)
-    nh, nkv, D, bs = 64, 8, 128, 64
-    lens_t = torch.tensor(lens, dtype=torch.int32)
-    B = lens_t.numel()
-    max_blocks = (int(lens_t.max()) + bs - 1) // bs
-    nblocks = B * max_blocks
-    if fp8:
-        kc, vc = _make_cache_fp8(nblocks, nkv, bs, D, gpu, 0.5, 2.0)
-    else:
-        kc, vc = _make_cache(nblocks, nkv, bs, D, gpu)
-    bt = _tables(B, max_blocks, nblocks, gpu, seed=3)
-    q = torch.randn(B, nh, D, device=gpu, dtype=BF)
-    ws = ops.decode_workspace(B, nh, D, splits, gpu)
-    kw = dict(num_splits=splits, workspace=ws, k_scale=0.5 if fp8 else 1.0,
-              v_scale=2.0 if fp8 else 1.0)
-    monkeypatch.setenv("DLI_ATTN_MERGE", "0")
-    ref_out = ops.attn_decode(q, None, kc, vc, bt, lens_t.to(gpu), D ** -0.5, **kw).clone()
-    monkeypatch.setenv("DLI_ATTN_MERGE", "1")
-    for _ in range(3):
-        got = ops.attn_decode(q, None, kc, vc, bt, lens_t.to(gpu), D ** -0.5, **kw)
-        torch.cuda.synchronize()
-        assert torch.equal(got, ref_out), (got.float() - ref_out.float()).abs().max().item()
-    assert int(ws[2].abs().sum().item()) == 0   # every counter reset by its merging workgroup
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("splits,share", [(1, 1.0), (16, 1.0), (16, 0.5), (16, 0.0)])
-def test_attn_decode_l3_prefetch_leaves_output_unchanged(gpu, monkeypatch, splits, share):
-    """Warm-up workgroups appended to the attention / combine launches (DLI_L3_PF) read a weight
-    and discard it: bit-identical attention output for every split of the bytes between the two
-    launches, the weight untouched, and ops.l3_prefetch alone is a no-op on its tensor."""
-    torch.manual_seed(splits)
-    nh, nkv, D, bs = 64, 8, 128, 64
-    lens_t = torch.tensor([600], dtype=torch.int32)
-    max_blocks = (600 + bs - 1) // bs
-    kc, vc = _make_cache(max_blocks, nkv, bs, D, gpu)
-    bt = _tables(1, max_blocks, max_blocks, gpu, seed=5)
-    q = torch.randn(1, nh, D, device=gpu, dtype=BF)
-    w = torch.randn(8192, 8192, device=gpu, dtype=BF)
-    w_ref = w.clone()
-    ws = ops.decode_workspace(1, nh, D, splits, gpu)
-    kw = dict(num_splits=splits, workspace=ws if splits > 1 else None)
-    ref_out = ops.attn_decode(q, None, kc, vc, bt, lens_t.to(gpu), D ** -0.5, **kw).clone()
-    monkeypatch.setenv("DLI_L3_PF_SPLIT", str(share))
-    monkeypatch.setenv("DLI_L3_PF_WGS", "200")
-    got = ops.attn_decode(q, None, kc, vc, bt, lens_t.to(gpu), D ** -0.5, prefetch=w, **kw)
-    ops.l3_prefetch(w, 96)
-    torch.cuda.synchronize()
-    assert torch.equal(got, ref_out)
-    assert torch.equal(w, w_ref)

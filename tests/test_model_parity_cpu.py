@@ -158,9 +158,9 @@ def test_fp8_stage_head_dim_128_uses_mx_attention_handoff_cpu(monkeypatch):
     monkeypatch.setattr(ops, "attn_decode", spy)
     b = _run_stage(st, prompts, decode_steps=1)
     assert calls and all(calls), calls           # every decode step took the MX hand-off
-    monkeypatch.setenv("DLI_FP8_MX_ATTN", "0")
     calls.clear()
-    c = _run_stage(st, prompts, decode_steps=1)
+    with ops.kernel_policy(fp8_mx=False):
+        c = _run_stage(st, prompts, decode_steps=1)
     assert calls and not any(calls)
     for x, y, z in zip(a, b, c):   # (one decode step: later ones may sample different tokens)
         assert ((x - y).norm() / x.norm()).item() < 0.15

@@ -49,7 +49,7 @@ def _pipeline_worker(rank, world, port, mbs, q, transport="host", rotation=None)
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_SHARE_GPU="1",
-                          DLI_TUNABLEOP="0", DLI_WATCHDOG_S="60")
+                          DLI_TUNING_DIR="off", DLI_WATCHDOG_S="60")
         if transport is None:   # the default
             os.environ.pop("DLI_TRANSPORT", None)
         else:
@@ -80,7 +80,7 @@ def _pipeline_worker(rank, world, port, mbs, q, transport="host", rotation=None)
 def test_multiprocess_pipeline_on_gpu(gpu, world, mbs):
     from distributed_llm_inference.runtime.engine import LLMEngine
     from distributed_llm_inference.runtime.sequence import SamplingParams
-    os.environ["DLI_TUNABLEOP"] = "0"
+    os.environ["DLI_TUNING_DIR"] = "off"
     spec, cfg = _cfg(1, mbs)
     ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
         PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
@@ -107,7 +107,7 @@ def test_multiprocess_pipeline_ipc_transport(gpu, world, mbs, rotation):
     Tokens must equal PP=1's."""
     from distributed_llm_inference.runtime.engine import LLMEngine
     from distributed_llm_inference.runtime.sequence import SamplingParams
-    os.environ["DLI_TUNABLEOP"] = "0"
+    os.environ["DLI_TUNING_DIR"] = "off"
     spec, cfg = _cfg(1, mbs)
     ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
         PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
@@ -213,7 +213,7 @@ def test_rccl_failure_falls_back_with_opt_in(gpu):
     together to the host-staged transport, producing the same tokens as PP=1."""
     from distributed_llm_inference.runtime.engine import LLMEngine
     from distributed_llm_inference.runtime.sequence import SamplingParams
-    os.environ["DLI_TUNABLEOP"] = "0"
+    os.environ["DLI_TUNING_DIR"] = "off"
     spec, cfg = _cfg(1, 3)
     ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
         PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
@@ -230,7 +230,7 @@ def test_default_transport_on_a_shared_gpu_is_ipc(gpu):
     IPC device transport (rotating head kept) without trying RCCL, producing PP=1's tokens."""
     from distributed_llm_inference.runtime.engine import LLMEngine
     from distributed_llm_inference.runtime.sequence import SamplingParams
-    os.environ["DLI_TUNABLEOP"] = "0"
+    os.environ["DLI_TUNING_DIR"] = "off"
     spec, cfg = _cfg(1, 3)
     ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
         PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
@@ -298,7 +298,7 @@ def test_rccl_p2p_two_gpus(gpu):
 def _pipeline_worker_gpus(rank, world, port, q):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
-                          MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_TUNABLEOP="0",
+                          MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_TUNING_DIR="off",
                           DLI_TRANSPORT="rccl")
         os.environ.pop("DLI_SHARE_GPU", None)
         import torch.distributed as dist
@@ -326,7 +326,7 @@ def test_multiprocess_pipeline_rccl_two_gpus(gpu):
     """PP=2 over RCCL P2P between two GPUs equals PP=1 (same micro-batch count)."""
     from distributed_llm_inference.runtime.engine import LLMEngine
     from distributed_llm_inference.runtime.sequence import SamplingParams
-    os.environ["DLI_TUNABLEOP"] = "0"
+    os.environ["DLI_TUNING_DIR"] = "off"
     spec, cfg = _cfg(1, 3)
     ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
         PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
