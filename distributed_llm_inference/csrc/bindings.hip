@@ -676,37 +676,63 @@ void gemm_tile(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue,
 // (splits 1); 1 = fp32 partials, 4 = bf16 partials [splits, M, N] (splits > 1)
 // fp8 e4m3 operands (1-byte a / b) take per-row a_scale [M] and per-channel b_scale [N] (fp32)
 void gemm4(Tensor out, Tensor a, Tensor b, int64_t splits, int64_t epilogue, int64_t grid,
-           optional<Tensor> a_scale, optional<Tensor> b_scale, int64_t variant) {
+           optional<Tensor> a_scale, optional<Tensor> b_scale, int64_t variant,
+           optional<Tensor> a_mx, optional<Tensor> out_mx) {
   CHECK_IN(out); CHECK_IN(a); CHECK_IN(b);
   const bool fp8 = a.element_size() == 1;
   TORCH_CHECK(a.scalar_type() == b.scalar_type() && a.scalar_type() != at::kChar,
               "gemm4: bf16 or fp8 e4m3 operands of one dtype");
   if (!fp8) { CHECK_BF16(a); }
-  const float* sa = nullptr;
-  const float* sb = nullptr;
-  if (fp8) {
-    TORCH_CHECK(a_scale.has_value() && b_scale.has_value(), "gemm4: fp8 needs a_scale and b_scale");
-    CHECK_IN(*a_scale); CHECK_IN(*b_scale); CHECK_F32(*a_scale); CHECK_F32(*b_scale);
-    TORCH_CHECK(a_scale->numel() == a.size(0) && b_scale->numel() == b.size(0),
-                "gemm4: a_scale [M], b_scale [N]");
-    sa = a_scale->data_ptr<float>();
-    sb = b_scale->data_ptr<float>();
-  }
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm4: 2-D operands");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(b.size(1) == K, "gemm4: shape mismatch");
+  const int64_t nb = (M + 63) / 64;
+  const float* sa = nullptr;
+  const float* sb = nullptr;
+  const uint8_t* amx = nullptr;
+  uint8_t* omx = nullptr;
+  int precision = 0;
+  if (fp8) {
+    TORCH_CHECK(b_scale.has_value(), "gemm4: fp8 needs b_scale");
+    CHECK_IN(*b_scale); CHECK_F32(*b_scale);
+    TORCH_CHECK(b_scale->numel() == N, "gemm4: b_scale [N]");
+    sb = b_scale->data_ptr<float>();
+    if (a_mx.has_value()) {   // MX activations: e8m0 per (row, 128-column block)
+      CHECK_IN(*a_mx);
+      TORCH_CHECK(a_mx->element_size() == 1 && a_mx->numel() == (K / 128) * nb * 64,
+                  "gemm4: a_mx = e8m0 [K / 128][ceil(M / 64) * 64] (mx_off layout)");
+      amx = static_cast<const uint8_t*>(a_mx->data_ptr());
+      precision = 2;
+    } else {
+      TORCH_CHECK(a_scale.has_value(), "gemm4: fp8 needs a_scale (or a_mx)");
+      CHECK_IN(*a_scale); CHECK_F32(*a_scale);
+      TORCH_CHECK(a_scale->numel() == M, "gemm4: a_scale [M]");
+      sa = a_scale->data_ptr<float>();
+      precision = 1;
+    }
+  }
   int64_t want = 0;
   if (epilogue == 0) want = M * N;
-  else if (epilogue == 2) want = M * (N / 2);
+  else if (epilogue == 2 || epilogue == 3) want = M * (N / 2);
   else if (epilogue == 1 || epilogue == 4) want = splits * M * N;
-  else TORCH_CHECK(false, "gemm4: epilogue 0, 1, 2 or 4");
+  else TORCH_CHECK(false, "gemm4: epilogue 0, 1, 2, 3 or 4");
+  const auto odt = out.scalar_type();
   TORCH_CHECK(out.is_contiguous() && out.numel() == want &&
-              out.scalar_type() == (epilogue == 1 ? at::kFloat : at::kBFloat16),
+              (epilogue == 3 ? out.element_size() == 1
+                             : odt == (epilogue == 1 ? at::kFloat : at::kBFloat16)),
               "gemm4: output size / dtype");
+  if (epilogue == 3) {
+    TORCH_CHECK(precision == 1 && splits == 1, "gemm4: the MX SwiGLU epilogue takes per-row fp8, one split");
+    TORCH_CHECK(out_mx.has_value(), "gemm4: epilogue 3 needs out_mx");
+    CHECK_IN(*out_mx);
+    TORCH_CHECK(out_mx->element_size() == 1 && out_mx->numel() == (N / 2 / 128) * nb * 64,
+                "gemm4: out_mx = e8m0 [N / 256][ceil(M / 64) * 64]");
+    omx = static_cast<uint8_t*>(out_mx->data_ptr());
+  }
   const c10::hip::HIPGuardMasqueradingAsCUDA g(a.device());
   check_rc(dli::launch_gemm4(out.data_ptr(), a.data_ptr(), b.data_ptr(), (int)M, (int)N, (int)K,
                              (int)splits, (int)epilogue, (int)grid, cur_stream(), (int)variant,
-                             fp8 ? 1 : 0, sa, sb),
+                             precision, sa, sb, amx, omx),
            "gemm4");
 }
 
@@ -980,7 +1006,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm4", &gemm4, "C = A . B^T, one-wave-per-SIMD 256x256 MFMA tile GEMM (gemm4.hip)",
         py::arg("out"), py::arg("a"), py::arg("b"), py::arg("splits") = 1,
         py::arg("epilogue") = 0, py::arg("grid") = 0, py::arg("a_scale") = py::none(),
-        py::arg("b_scale") = py::none(), py::arg("variant") = -1);
+        py::arg("b_scale") = py::none(), py::arg("variant") = -1, py::arg("a_mx") = py::none(),
+        py::arg("out_mx") = py::none());
   m.def("skinny_gemm_int8", &skinny_gemm_int8,
         "y = (x . W8^T) * scale (+ bias), int8 weights, bf16 rows, M <= 2 (weight-streaming GEMV)",
         py::arg("out"), py::arg("x"), py::arg("w"), py::arg("wscale"), py::arg("bias") = py::none(),

@@ -33,6 +33,14 @@
 //     (gate|up at M = 512: 448 tiles on 224 workgroups, 2 each -- at the power cap fewer busy CUs
 //     clock higher, which is why hipBLASLt picks that grid); blockIdx is remapped so the
 //     workgroups of one XCD take neighbouring work items (shared A / B panels in its L2).
+//   * fp8 (e4m3) operands run the block-scaled 32x32x64 MFMA with gemm_tile.hip's fp8 contracts:
+//     per-row activation x per-channel weight scales in the epilogue (PREC 1), or MX activations
+//     (PREC 2: one e8m0 scale per (row, 128-column block), common.h mx_off layout) fed to the
+//     MFMA's per-lane scale operand -- a k-tile is exactly one scale block, so lane l's scale
+//     byte for activation block mi is row 32 mi + (l & 31)'s, read once per k-tile from an LDS
+//     copy of the tile's scales; and the gate|up SwiGLU epilogue can quantise its output to MX
+//     itself (kG4SwiGLUMx: the 128 output columns of a 256-wide weight tile are one block, so
+//     the row amax is a shuffle plus one LDS exchange between the tile's two n-waves).
 #include "kernels.h"
 
 #include <type_traits>
@@ -45,7 +53,17 @@ namespace {
 constexpr int kG4Threads = 256;
 constexpr int kG4Stage = 65536;   // A [256][128 B] | B [256][128 B]
 
-enum G4Epi { kG4Bf16 = 0, kG4F32 = 1, kG4SwiGLU = 2, kG4Bf16Part = 4 };
+enum G4Epi { kG4Bf16 = 0, kG4F32 = 1, kG4SwiGLU = 2, kG4SwiGLUMx = 3, kG4Bf16Part = 4 };
+
+constexpr int kG4MxKt = 64;                // k-tiles of MX scales a workgroup keeps in LDS
+constexpr int kG4MxLds = kG4MxKt * 256;    // [k-tile][256 tile rows] e8m0 bytes
+constexpr int kG4RedLds = 2 * 256 * 4;     // kG4SwiGLUMx row amax exchange [wc][256 rows]
+
+struct G4Mx {
+  const uint8_t* a_sc;   // PREC 2: the activations' e8m0 scales (mx_off layout)
+  uint8_t* out_sc;       // kG4SwiGLUMx: scales of the quantised output (mx_off, kt = n-tile)
+  int nb;                // ceil(M / 64)
+};
 
 typedef __attribute__((address_space(3))) void g4_lds_t;
 
@@ -103,6 +121,35 @@ __device__ __forceinline__ void g4_mfma8(g4_f32x16& acc, const g4_i32x4& w0, con
                : "+a"(acc) : "v"(w), "v"(x), "v"(sc) : "memory");
 }
 
+// MX activations: the weight block scale stays 1.0 (e8m0 127), the activation scale is byte SEL
+// of `sx` (lane l: activation row 32 SEL + (l & 31) of the wave's 128, this k-tile)
+template <int SEL>
+__device__ __forceinline__ void g4_mfma8mx(g4_f32x16& acc, const g4_i32x4& w0, const g4_i32x4& w1,
+                                           const g4_i32x4& x0, const g4_i32x4& x1, int sc, int sx) {
+  const g4_i32x8 w = __builtin_shufflevector(w0, w1, 0, 1, 2, 3, 4, 5, 6, 7);
+  const g4_i32x8 x = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+  if constexpr (SEL == 0)
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]"
+                 : "+a"(acc) : "v"(w), "v"(x), "v"(sc), "v"(sx) : "memory");
+  else if constexpr (SEL == 1)
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,1,0] op_sel_hi:[0,0,0]"
+                 : "+a"(acc) : "v"(w), "v"(x), "v"(sc), "v"(sx) : "memory");
+  else if constexpr (SEL == 2)
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,1,0]"
+                 : "+a"(acc) : "v"(w), "v"(x), "v"(sc), "v"(sx) : "memory");
+  else
+    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,1,0] op_sel_hi:[0,1,0]"
+                 : "+a"(acc) : "v"(w), "v"(x), "v"(sc), "v"(sx) : "memory");
+}
+
+typedef unsigned g4_u32x2 __attribute__((ext_vector_type(2)));
+
+// the two dwords of this lane's MX scales of one k-tile (rows wr*128 + (l & 15) + {0..63 step
+// 16} and + 64: mx_off packs rows r, r+16, r+32, r+48 of a 64-row block in one dword)
+__device__ __forceinline__ void g4_read_mx(g4_u32x2& dst, int addr) {
+  asm volatile("ds_read2_b32 %0, %1 offset1:16" : "=v"(dst) : "v"(addr) : "memory");
+}
+
 template <int OFF>
 __device__ __forceinline__ void g4_read8(g4_i32x4& dst, int addr) {
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(OFF) : "memory");
@@ -134,16 +181,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t g4_rsrc(const void* base, int 
 // block-scaled MFMAs, 32 per wave per k-tile, each as long as four bf16 ones, so the k-loop
 // schedule (in 16-cycle slots, one bf16 MFMA or a quarter fp8 MFMA each) is shared; fragments of
 // 32 rows x 64 bytes (two ds_read_b128 per lane); per-row a_scale x per-channel b_scale in the
-// epilogue, as gemm_tile.hip's fp8 path.
+// epilogue, as gemm_tile.hip's fp8 path.  PREC 2: PREC 1 with MX activation scales (G4Mx) on the
+// MFMA's scale operand instead of a_scale.
 template <int EPI, int VAR, int PREC = 0>
 __global__ void __launch_bounds__(kG4Threads, 1)
 gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __restrict__ C,
              int M, int N, int K, int tiles_m, int tiles_n, int kps, int splits,
-             const float* __restrict__ a_scale, const float* __restrict__ b_scale) {
-  constexpr bool F8 = PREC == 1;
+             const float* __restrict__ a_scale, const float* __restrict__ b_scale, G4Mx mx) {
+  constexpr bool F8 = PREC >= 1;
+  constexpr bool MXIN = PREC == 2;
+  constexpr int kMxOff = 2 * kG4Stage;                              // MX scale slab
+  constexpr int kRedOff = kMxOff + (MXIN ? kG4MxLds : 0);           // kG4SwiGLUMx exchange
+  constexpr int kSmem = kRedOff + (EPI == kG4SwiGLUMx ? kG4RedLds : 0);
   const char* A = reinterpret_cast<const char*>(Av);
   const char* B = reinterpret_cast<const char*>(Bv);
-  __shared__ __attribute__((aligned(1024))) char smem[2 * kG4Stage];
+  __shared__ __attribute__((aligned(1024))) char smem[kSmem];
   const int tid = threadIdx.x, lane = tid & 63;
 #ifdef GEMM_STAMPS
   // diagnostic builds only (scripts/experiments/gemm4_bench.hip): begin / end-of-last-k-loop /
@@ -192,6 +244,10 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
           rdB8[kk][st][h] = lds0 + st * kG4Stage + 32768 + (wc * 128 + r32) * 128 + ch;
         }
   }
+  // MX scales: this lane's two dwords of a k-tile's 256-byte slab (rows wr*128 + (l & 15) + 16 i)
+  // and the byte order that packs the rows it scales, 32 mi + (l & 31), as bytes mi = 0..3
+  const int mxrd = lds0 + kMxOff + wr * 128 + (lane & 15) * 4;
+  const unsigned mxsel = (lane & 16) ? 0x07050301u : 0x06040200u;
   // DMA: wave-load q = 4j + w covers tile rows 8q .. 8q+7; lane -> row 8q + (lane >> 3), LDS
   // slot lane & 7 holding global chunk (lane & 7) ^ ((row >> 1) & 7) = .. ^ ((q & 1) * 4 + (lane >> 4))
   const int dchunk = ((lane & 7) ^ (((w & 1) * 4 + (lane >> 4)) & 7)) << 4;
@@ -210,6 +266,23 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
 #pragma unroll
     for (int j = 0; j < 8; ++j) voA[j] = min(drow + 32 * j, mrows - 1) * Kb + dchunk;
     const int voB = drow * Kb + dchunk;
+
+    if constexpr (MXIN) {
+      // this tile's scales of its k-tiles into LDS, [t][256 rows]; 64-row blocks past the
+      // array (a partial last M tile) read as 2^0 (their rows are computed, never stored)
+      const int vb = min(4, mx.nb - (m0 >> 6));
+      for (int idx = tid; idx < T * 64; idx += kG4Threads) {
+        const int t = idx >> 6, d = idx & 63, blk = d >> 4;
+        unsigned v = 0x7f7f7f7fu;
+        if (blk < vb)
+          v = *reinterpret_cast<const unsigned*>(
+              mx.a_sc + ((size_t)(kt0 + t) * mx.nb + (m0 >> 6) + blk) * 64 + (d & 15) * 4);
+        *reinterpret_cast<unsigned*>(smem + kMxOff + t * 256 + d * 4) = v;
+      }
+      g4_sync_lds();   // written before the prologue's barrier publishes them
+    }
+    g4_u32x2 mxr = {0x7f7f7f7fu, 0x7f7f7f7fu};   // raw scale dwords of the next k-tile
+    int mxs = 0x7f7f7f7f;                        // packed scales of the current k-tile
 
     // stage DMA piece j (0..15: A rows 32j' .. for j < 8, B for j >= 8) of k-tile t
     auto dma = [&](int t, int j) {
@@ -258,7 +331,16 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
     // fp8 MFMA number k (0..15) of a k-step: activation block k / 4, weight block k % 4
     auto mf8 = [&](const g4_i32x4 (&F)[16], int k) {
       const int mi = k >> 2, ni = k & 3;
-      g4_mfma8(acc8[mi][ni], F[2 * ni], F[2 * ni + 1], F[8 + 2 * mi], F[9 + 2 * mi], sc127);
+      if constexpr (MXIN) {
+        switch (mi) {   // (k is a compile-time constant at every call: the switch folds)
+          case 0: g4_mfma8mx<0>(acc8[0][ni], F[2 * ni], F[2 * ni + 1], F[8], F[9], sc127, mxs); break;
+          case 1: g4_mfma8mx<1>(acc8[1][ni], F[2 * ni], F[2 * ni + 1], F[10], F[11], sc127, mxs); break;
+          case 2: g4_mfma8mx<2>(acc8[2][ni], F[2 * ni], F[2 * ni + 1], F[12], F[13], sc127, mxs); break;
+          default: g4_mfma8mx<3>(acc8[3][ni], F[2 * ni], F[2 * ni + 1], F[14], F[15], sc127, mxs); break;
+        }
+      } else {
+        g4_mfma8(acc8[mi][ni], F[2 * ni], F[2 * ni + 1], F[8 + 2 * mi], F[9 + 2 * mi], sc127);
+      }
     };
 
     // fragment sets: P = k-step 0, Q = k-step 1 ([0..7] weight fragments, [8..15] activation)
@@ -301,6 +383,7 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
       g4_vmcnt<0>();
     }
     g4_barrier();
+    if constexpr (MXIN) g4_read_mx(mxr, mxrd);
 #pragma unroll
     for (int n = 0; n < 16; ++n) {
       if constexpr (F8) rd8(P8, n, 0, 0); else rd(P, n, 0, 0);
@@ -312,6 +395,8 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
       constexpr bool DMA = decltype(dma_c)::value, NEXT = decltype(next_c)::value;
       using S = G4Sched<VAR>;
       const int s = t & 1;
+      // this k-tile's MX scales (read with the previous tile's P fragments, retired since)
+      if constexpr (MXIN) mxs = (int)__builtin_amdgcn_perm(mxr[1], mxr[0], mxsel);
       // MFMA g of the k-tile (g < 64: k-step 0 on P, else k-step 1 on Q), and after it: the k-step
       // 1 reads of this tile -> Q, B1, the DMA of tile t+2 into stage s, B2, the k-step 0 reads of
       // tile t+1 -> P, at the positions the schedule S gives
@@ -338,6 +423,7 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
           g4_barrier();
         }
         if constexpr (NEXT && g >= S::p0 && g < S::p0 + 16 * S::ps && (g - S::p0) % S::ps == 0) {
+          if constexpr (MXIN && g == S::p0) g4_read_mx(mxr, mxrd + (t + 1) * 256);
           if constexpr (F8) rd8(P8, (g - S::p0) / S::ps, 0, s ^ 1);
           else rd(P, (g - S::p0) / S::ps, 0, s ^ 1);
         }
@@ -371,6 +457,65 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
 
     // ---- epilogue: fragment (i, j) element e of lane l is
     //      C[m0 + wr*128 + 16i + (l & 15)][n0 + wc*128 + 16j + 4(l >> 4) + e] ----
+    if constexpr (F8 && EPI == kG4SwiGLUMx) {
+      // h = silu(gate) * up rounded to bf16 (what the bf16 SwiGLU epilogue stores), kept in the
+      // gate registers; the row's amax over its 128-column block = the two n-waves' 64 each
+      // (lanes l and l + 32 share a row: one shuffle, then one LDS exchange), then e4m3(h * 2^-k)
+      // and one e8m0 byte per (row, block) -- ops.mx_quantize's rule, gemm_tile's kSwiGLUMx
+      const int c4 = 4 * (lane >> 5), x = lane & 31;
+      float* red = reinterpret_cast<float*>(smem + kRedOff);   // [wc][256 rows]
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int row = m0 + wr * 128 + 32 * mi + x;
+        const float sa = a_scale[min(row, M - 1)];
+        float a = 0.f;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int nb = n0 + wc * 128 + 32 * ni + c4;
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            const f32x4 sg = *reinterpret_cast<const f32x4*>(b_scale + nb + 8 * g);
+            const f32x4 su = *reinterpret_cast<const f32x4*>(b_scale + nb + 8 * g + 16);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float gv = (float)(bf16)(acc8[mi][ni][4 * g + e] * sg[e] * sa);
+              const float uv = (float)(bf16)(acc8[mi][ni][4 * g + 8 + e] * su[e] * sa);
+              const float h = (float)(bf16)(g4_silu(gv) * uv);
+              acc8[mi][ni][4 * g + e] = h;
+              a = fmaxf(a, fabsf(h));
+            }
+          }
+        }
+        a = fmaxf(a, __shfl_xor(a, 32, 64));
+        if (lane < 32) red[wc * 256 + wr * 128 + 32 * mi + x] = a;
+      }
+      g4_sync_lds();
+      g4_barrier();
+      uint8_t* out = reinterpret_cast<uint8_t*>(C);
+      const int I = N >> 1, tn = n0 >> 8;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int r = wr * 128 + 32 * mi + x, row = m0 + r;
+        const int k = mx_exponent(fmaxf(red[r], red[256 + r]));
+        const float inv = mx_inv_scale(k);
+        if (row < M) {
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+              *reinterpret_cast<unsigned*>(out + (size_t)row * I + (n0 >> 1) + wc * 64 + 16 * ni +
+                                           8 * g + c4) =
+                  pack4_fp8(acc8[mi][ni][4 * g] * inv, acc8[mi][ni][4 * g + 1] * inv,
+                            acc8[mi][ni][4 * g + 2] * inv, acc8[mi][ni][4 * g + 3] * inv);
+            }
+        }
+        // one byte per (row, block); rows in [M, 64 nb) get 2^0 (the consumer reads them)
+        if (wc == 0 && lane < 32 && row < mx.nb * 64)
+          mx.out_sc[mx_off(tn, row, mx.nb)] = (uint8_t)(row < M ? k + 127 : 127);
+      }
+      g4_barrier();
+      continue;
+    }
     if constexpr (F8) {
       // 32x32 tile (mi, ni) element r of lane l: row m0 + wr*128 + 32 mi + (l & 31), column
       // n0 + wc*128 + 32 ni + 8 (r >> 2) + 4 (l >> 5) + (r & 3): 4 consecutive columns per group
@@ -379,7 +524,7 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
       for (int mi = 0; mi < 4; ++mi) {
         const int row = m0 + wr * 128 + 32 * mi + (lane & 31);
         if (row >= M) continue;
-        const float sa = a_scale[row];
+        const float sa = MXIN ? 1.f : a_scale[row];
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
           const int nb = n0 + wc * 128 + 32 * ni + c4;
@@ -507,19 +652,24 @@ int gemm4_grid(int items, int cus) {
 template <int VAR, int PREC>
 static int launch_gemm4_v(void* C, const void* a, const void* b, int M, int N, int K, int tiles_m,
                           int tiles_n, int kps, int splits, int epilogue, int grid,
-                          hipStream_t stream, const float* sa, const float* sb) {
+                          hipStream_t stream, const float* sa, const float* sb, G4Mx mx) {
   switch (epilogue) {
     case kG4Bf16:
-      gemm4_kernel<kG4Bf16, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb);
+      gemm4_kernel<kG4Bf16, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb, mx);
       break;
     case kG4F32:
-      gemm4_kernel<kG4F32, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb);
+      gemm4_kernel<kG4F32, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb, mx);
       break;
     case kG4SwiGLU:
-      gemm4_kernel<kG4SwiGLU, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb);
+      if constexpr (PREC == 2) return -4;   // MX activations feed down / O, never gate|up
+      else gemm4_kernel<kG4SwiGLU, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb, mx);
+      break;
+    case kG4SwiGLUMx:
+      if constexpr (PREC != 1) return -4;   // the MX output of the fp8 gate|up projection
+      else gemm4_kernel<kG4SwiGLUMx, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb, mx);
       break;
     case kG4Bf16Part:
-      gemm4_kernel<kG4Bf16Part, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb);
+      gemm4_kernel<kG4Bf16Part, VAR, PREC><<<grid, kG4Threads, 0, stream>>>(a, b, C, M, N, K, tiles_m, tiles_n, kps, splits, sa, sb, mx);
       break;
     default:
       return -4;
@@ -530,40 +680,52 @@ static int launch_gemm4_v(void* C, const void* a, const void* b, int M, int N, i
 template <int PREC>
 static int launch_gemm4_p(void* C, const void* a, const void* b, int M, int N, int K, int tiles_m,
                           int tiles_n, int kps, int splits, int epilogue, int grid,
-                          hipStream_t stream, int variant, const float* sa, const float* sb) {
+                          hipStream_t stream, int variant, const float* sa, const float* sb,
+                          G4Mx mx) {
   if (variant == kG4DecodeDefault)
-    return launch_gemm4_v<kG4DecodeDefault, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+    return launch_gemm4_v<kG4DecodeDefault, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
   if (variant != kG4Default) return -5;
-  return launch_gemm4_v<kG4Default, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb);
+  return launch_gemm4_v<kG4Default, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
 }
 
 // C = A . B^T on the one-wave-per-SIMD kernel.  epilogue 0: bf16 [M, N]; 2: fused SwiGLU ([M,
 // N/2], B rows in swiglu_interleave order); with splits > 1: 1 = fp32 partials [splits, M, N],
 // 4 = bf16 partials [splits, M, N] (into C; the consumer sums them).  grid <= 0: automatic.
 // variant < 0: the default k-loop schedule (G4Sched), else that one (A/B experiments).
-// precision 1: fp8 e4m3 A [M, K] / B [N, K] (1-byte), results scaled by a_scale[M] * b_scale[N].
+// precision 1: fp8 e4m3 A [M, K] / B [N, K] (1-byte), results scaled by a_scale[M] * b_scale[N];
+// precision 2: fp8 with MX activation scales a_mx (mx_off layout, nb = ceil(M / 64)) instead of
+// a_scale.  epilogue 3 (precision 1, one split): SwiGLU quantised to MX fp8 [M, N/2] in C, its
+// scales in out_mx.
 int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int splits,
                  int epilogue, int grid, hipStream_t stream, int variant, int precision,
-                 const float* a_scale, const float* b_scale) {
-  const int esz = precision == 1 ? 1 : 2;
-  if (precision != 0 && precision != 1) return -6;
+                 const float* a_scale, const float* b_scale, const uint8_t* a_mx,
+                 uint8_t* out_mx) {
+  const int esz = precision >= 1 ? 1 : 2;
+  if (precision < 0 || precision > 2) return -6;
   if (precision == 1 && (a_scale == nullptr || b_scale == nullptr)) return -7;
+  if (precision == 2 && (a_mx == nullptr || b_scale == nullptr)) return -7;
+  if (epilogue == kG4SwiGLUMx && (precision != 1 || out_mx == nullptr)) return -8;
   if (M <= 0 || N % 256 != 0 || (K * esz) % 128 != 0 || splits < 1) return -1;
   const int kt = K * esz / 128;
   if (splits > kt) return -2;
   const int kps = (kt + splits - 1) / splits;
   if ((splits - 1) * kps >= kt) return -2;   // every split owns at least one k-tile
+  if (precision == 2 && kps > kG4MxKt) return -9;   // the tile's scales must fit the LDS slab
   if ((splits > 1) != (epilogue == kG4F32 || epilogue == kG4Bf16Part)) return -3;
   const int tiles_m = (M + 255) / 256, tiles_n = N / 256;
   const int items = tiles_m * tiles_n * splits;
   if (grid <= 0) grid = gemm4_grid(items, g4_cus());
   if (grid > items) grid = items;
   if (variant < 0) variant = tiles_m <= 2 ? kG4DecodeDefault : kG4Default;
+  const G4Mx mx{a_mx, out_mx, (M + 63) / 64};
+  if (precision == 2)
+    return launch_gemm4_p<2>(C, A, B, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid,
+                             stream, variant, nullptr, b_scale, mx);
   if (precision == 1)
     return launch_gemm4_p<1>(C, A, B, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid,
-                             stream, variant, a_scale, b_scale);
+                             stream, variant, a_scale, b_scale, mx);
   return launch_gemm4_p<0>(C, A, B, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream,
-                           variant, nullptr, nullptr);
+                           variant, nullptr, nullptr, mx);
 }
 
 }  // namespace dli

@@ -135,11 +135,14 @@ int launch_skinny_gemm(bf16* y, const bf16* x, const bf16* W, const bf16* bias, 
                        int K, hipStream_t stream, bool swiglu = false,
                        const GemvNorm* nm = nullptr, const GemvRope* rp = nullptr);
 // one-wave-per-SIMD 256x256 GEMM (gemm4.hip); epilogue 0 bf16, 1 fp32 partials, 2 SwiGLU,
-// 4 bf16 partials; grid <= 0: automatic persistent grid; variant < 0: default k-loop schedule
-// precision 1: fp8 e4m3 operands with per-row a_scale [M] and per-channel b_scale [N]
+// 3 SwiGLU quantised to MX fp8 (precision 1; scales into out_mx), 4 bf16 partials; grid <= 0:
+// automatic persistent grid; variant < 0: default k-loop schedule.  precision 1: fp8 e4m3
+// operands with per-row a_scale [M] and per-channel b_scale [N]; 2: fp8 with MX activation
+// scales a_mx (mx_off layout) and per-channel b_scale
 int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int splits,
                  int epilogue, int grid, hipStream_t stream, int variant = -1, int precision = 0,
-                 const float* a_scale = nullptr, const float* b_scale = nullptr);
+                 const float* a_scale = nullptr, const float* b_scale = nullptr,
+                 const uint8_t* a_mx = nullptr, uint8_t* out_mx = nullptr);
 int gemm4_grid(int items, int cus);
 int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* residual_in,
                          bf16* residual_out, const bf16* norm_w, float eps, int rows, int K,

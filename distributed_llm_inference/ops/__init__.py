@@ -516,31 +516,38 @@ def gemm_tile(x: torch.Tensor, w: torch.Tensor, splits: int = 1, swiglu: bool = 
 
 def _gemm4(x: torch.Tensor, w: torch.Tensor, splits: int, swiglu: bool,
            out: Optional[torch.Tensor], defer_reduce: bool,
-           xs: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None):
+           xs: Optional[torch.Tensor] = None, ws: Optional[torch.Tensor] = None,
+           x_mx: Optional[torch.Tensor] = None):
     """:func:`gemm_tile`'s contract on gemm4: same epilogues (bf16 store, fused SwiGLU, split-K
     partials handed to the consumer or reduced here), bit-identical results for bf16.  fp8 e4m3
-    operands (``xs`` [M] / ``ws`` [N] scales) run the block-scaled 32x32x64 MFMA
-    (:func:`gemm_tile_fp8`'s contract, bf16 output)."""
+    operands (``xs`` [M] / ``ws`` [N] scales, or ``x_mx``: MX activation scales) run the
+    block-scaled 32x32x64 MFMA (:func:`gemm_tile_fp8` / :func:`gemm_tile_fp8_mx`'s contracts)."""
     M, N = x.shape[0], w.shape[0]
     splits = max(1, int(splits))
-    fp8 = xs is not None
+    fp8 = xs is not None or x_mx is not None
     if splits > 1 and defer_reduce and not swiglu and policy().defer_splitk:
         bf = bf16_partials()
         parts = torch.empty(splits, M, N, dtype=torch.bfloat16 if bf else torch.float32,
                             device=x.device)
-        native().gemm4(parts, x, w, splits, 4 if bf else 1, 0, xs, ws)
+        native().gemm4(parts, x, w, splits, 4 if bf else 1, 0, xs, ws, a_mx=x_mx)
         return SplitKPartials(parts)
     if out is None:
         out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
     if splits == 1:
-        native().gemm4(out, x, w, 1, 2 if swiglu else 0, 0, xs, ws)
+        native().gemm4(out, x, w, 1, 2 if swiglu else 0, 0, xs, ws, a_mx=x_mx)
         return out
     if swiglu:
         raise ValueError("gemm4: fused SwiGLU takes whole-K tiles (splits = 1)")
     parts = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
-    native().gemm4(parts, x, w, splits, 1, 0, xs, ws)
+    native().gemm4(parts, x, w, splits, 1, 0, xs, ws, a_mx=x_mx)
     native().splitk_reduce(out, parts)
     return out
+
+
+def gemm4_mx_ok(K: int, splits: int) -> bool:
+    """Whether gemm4 takes MX activations over K with this split count (its LDS scale slab holds
+    64 k-tiles; csrc/kernels/gemm4.hip kG4MxKt)."""
+    return mx_tileable(K, splits)
 
 
 _CU_COUNT = {}
@@ -773,8 +780,12 @@ def gemm_tile_fp8(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torc
         I = N // 2
         q = torch.empty(M, I, dtype=torch.float8_e4m3fn, device=xq.device)
         sc = torch.empty(I // 128 * ((M + 63) // 64) * 64, dtype=torch.uint8, device=xq.device)
-        native().gemm_tile(q, xq, wq, 1, 3, None, xs.reshape(-1).contiguous(),
+        if gemm4:
+            native().gemm4(q, xq, wq, 1, 3, 0, xs.reshape(-1).contiguous(),
                            ws.reshape(-1).contiguous(), out_mx=sc)
+        else:
+            native().gemm_tile(q, xq, wq, 1, 3, None, xs.reshape(-1).contiguous(),
+                               ws.reshape(-1).contiguous(), out_mx=sc)
         return MxFp8(q, sc)
     if _gpu(xq) and gemm4 and xq.shape[1] % 128 == 0:
         return _gemm4(xq, wq, splits, swiglu, out, defer_reduce,
@@ -875,6 +886,8 @@ def gemm_tile_fp8_mx(a: MxFp8, wq: torch.Tensor, ws: torch.Tensor, splits: int =
         raise ValueError(f"gemm_tile_fp8_mx: K={xq.shape[1]} with {splits} splits exceeds the "
                          f"{MX_MAX_KTILES}-k-tile scale slot")
     ws = ws.reshape(-1).contiguous()
+    if gemm4:
+        return _gemm4(xq, wq, splits, False, None, defer_reduce, None, ws, x_mx=a.sc)
     if defer_reduce and splits > 1 and policy().defer_splitk:
         if bf16_partials():
             parts = torch.empty(splits, M, N, dtype=torch.bfloat16, device=xq.device)

@@ -171,10 +171,12 @@ def test_gemm_tile_fp8_exact_integers_and_swiglu(gpu):
 
 # ------------------------------------------------------------------ fp8 MX activations (kSwiGLUMx -> kFp8Mx)
 @pytest.mark.parametrize("M", [512, 300, 64, 1])
-def test_gemm_tile_fp8_swiglu_mx_epilogue_matches_reference_quantiser(gpu, M):
+@pytest.mark.parametrize("gemm4", [False, True])
+def test_gemm_tile_fp8_swiglu_mx_epilogue_matches_reference_quantiser(gpu, M, gemm4):
     # same main loop as the bf16-output SwiGLU epilogue: its h, quantised by the reference MX rule,
     # must give the kernel's fp8 bytes and e8m0 scales bit for bit (pad rows of the last 64-row
-    # block carry scale 127)
+    # block carry scale 127); for gemm_tile (8 waves, 16x16x128 MFMA) and gemm4 (one wave per
+    # SIMD, 32x32x64 MFMA, kG4SwiGLUMx)
     torch.manual_seed(M)
     K, I = 1024, 768
     x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
@@ -183,8 +185,8 @@ def test_gemm_tile_fp8_swiglu_mx_epilogue_matches_reference_quantiser(gpu, M):
     wq, ws = ops.quantize_weight_fp8(w)
     wqi = ops.swiglu_interleave(wq.view(torch.uint8)).view(wq.dtype)
     wsi = ops.swiglu_interleave(ws.reshape(-1, 1)).reshape(-1)
-    h = ops.gemm_tile_fp8(xq, xs, wqi, wsi, swiglu=True)
-    a = ops.gemm_tile_fp8(xq, xs, wqi, wsi, swiglu=True, mx_out=True)
+    h = ops.gemm_tile_fp8(xq, xs, wqi, wsi, swiglu=True, gemm4=gemm4)
+    a = ops.gemm_tile_fp8(xq, xs, wqi, wsi, swiglu=True, mx_out=True, gemm4=gemm4)
     ref = ops.mx_quantize(h)
     assert torch.equal(a.sc, ref.sc)
     assert torch.equal(a.q.view(torch.uint8), ref.q.view(torch.uint8))
@@ -196,7 +198,8 @@ def test_gemm_tile_fp8_swiglu_mx_epilogue_matches_reference_quantiser(gpu, M):
 
 @pytest.mark.parametrize("M,N,K,splits", [(512, 1024, 8192, 1), (512, 8192, 28672, 4),
                                           (300, 512, 4096, 2), (77, 256, 1024, 1)])
-def test_gemm_tile_fp8_mx_matches_dequantised_fp32(gpu, M, N, K, splits):
+@pytest.mark.parametrize("gemm4", [False, True])
+def test_gemm_tile_fp8_mx_matches_dequantised_fp32(gpu, M, N, K, splits, gemm4):
     torch.manual_seed(M + N + K)
     # rows and 128-column blocks of very different magnitudes: per-block scales matter
     h = (torch.randn(M, K, device=gpu) * torch.exp2(torch.randint(-6, 7, (M, K // 128), device=gpu)
@@ -205,10 +208,13 @@ def test_gemm_tile_fp8_mx_matches_dequantised_fp32(gpu, M, N, K, splits):
     w = (torch.randn(N, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
     wq, ws = ops.quantize_weight_fp8(w)
     ref = a.dequantize() @ (wq.float() * ws.reshape(-1, 1)).t()
-    y = ops.gemm_tile_fp8_mx(a, wq, ws, splits).float()
+    y = ops.gemm_tile_fp8_mx(a, wq, ws, splits, gemm4=gemm4).float()
     assert (y - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
+    if gemm4:   # the two kernels agree to fp32 accumulation-order differences (bf16 output)
+        y0 = ops.gemm_tile_fp8_mx(a, wq, ws, splits).float()
+        assert (y - y0).abs().max().item() < 1e-2 * ref.abs().max().item()
     if splits > 1:
-        parts = ops.gemm_tile_fp8_mx(a, wq, ws, splits, defer_reduce=True)
+        parts = ops.gemm_tile_fp8_mx(a, wq, ws, splits, defer_reduce=True, gemm4=gemm4)
         assert isinstance(parts, ops.SplitKPartials)
         assert (parts.parts.sum(0) - ref).abs().max().item() < 1e-2 * ref.abs().max().item()
 
@@ -620,3 +626,32 @@ def test_gemm4_fp8_matches_gemm_tile_fp8(gpu, M, N, K, splits, epi):
         want = ref.float().sum(0) if epi in (1, 4) else ref.float()
         assert (got - want).abs().max().item() < 2e-2 * scale, grid
         assert (got - f32).abs().max().item() < 2e-2 * scale, grid
+
+
+@pytest.mark.parametrize("M,K,I", [(512, 8192, 28672), (300, 2048, 1536), (40, 1024, 768)])
+def test_gemm4_fp8_mx_chain_gate_up_to_down(gpu, M, K, I):
+    """The fp8 MLP hand-off on gemm4 end to end: gate|up + SwiGLU quantised to MX in gemm4's
+    epilogue, consumed by the down projection on gemm4's MX operand - against the same chain on
+    gemm_tile, and the down product against the fp32 product of the dequantised MX activations
+    (a shared partial M tile, the 70B shape with its 4-way split-K)."""
+    torch.manual_seed(M + I)
+    x = torch.randn(M, K, device=gpu).to(torch.bfloat16)
+    wgu = (torch.randn(2 * I, K, device=gpu) / K ** 0.5).to(torch.bfloat16)
+    wd = (torch.randn(K, I, device=gpu) / I ** 0.5).to(torch.bfloat16)
+    xq, xs = ops.quant_rowwise(x)
+    gq, gs = ops.quantize_weight_fp8(wgu)
+    gqi = ops.swiglu_interleave(gq.view(torch.uint8)).view(gq.dtype)
+    gsi = ops.swiglu_interleave(gs.reshape(-1, 1)).reshape(-1)
+    dq, ds = ops.quantize_weight_fp8(wd)
+    sp = ops.tile_gemm_splits_fp8(M, K, I) or 1
+    outs = {}
+    for g4 in (False, True):
+        h = ops.gemm_tile_fp8(xq, xs, gqi, gsi, swiglu=True, mx_out=True, gemm4=g4)
+        y = ops.gemm_tile_fp8_mx(h, dq, ds, sp, gemm4=g4).float()
+        ref = h.dequantize() @ (dq.float() * ds.reshape(-1, 1)).t()
+        assert (y - ref).abs().max().item() < 1e-2 * ref.abs().max().item(), g4
+        outs[g4] = (h.dequantize(), y)
+    hd = (outs[True][0] - outs[False][0]).abs().max().item()
+    assert hd <= 2 ** -3 * outs[False][0].abs().max().item(), hd   # one fp8 step, at most
+    scale = outs[False][1].abs().max().item()
+    assert (outs[True][1] - outs[False][1]).abs().max().item() < 3e-2 * scale
