@@ -388,9 +388,11 @@ class KernelPolicy:
     # bf16 decode projections on the one-wave-per-SIMD gemm4 kernel (else the 8-wave gemm_tile):
     # 70B decode step 75.0 vs 77.7 ms (profiles/r4/gemm4_step_ab.txt)
     gemm4: bool = True
-    # fp8 decode projections on gemm4 (block-scaled MFMA, fp8 k-loop schedule) instead of
-    # gemm_tile: "all", "none", or a "+"-separated subset of qkv / o / gate_up / down
-    fp8_gemm4: str = "none"
+    # fp8 decode projections on gemm4 (16x16x128 block-scaled MFMA, G4S8 k-loop; bit-identical
+    # to gemm_tile) instead of gemm_tile: "all", "none", or a "+"-separated subset of qkv / o /
+    # gate_up / down.  gate|up: 202 vs 219 us alone, +1.9 % tok/s in-step; the others win 2-7 %
+    # alone but stay within noise in-step (profiles/r5/fp8_gemm4_16x16.md)
+    fp8_gemm4: str = "gate_up"
     # split-K partials of the deferred projections (QKV, O, down) stored as bf16 (else fp32);
     # consumers always sum in fp32 (profiles/bf16_partials_ab.txt, docs/parity.md C6)
     bf16_partials: bool = True
@@ -427,7 +429,7 @@ class KernelPolicy:
                              f"{'/'.join(self._FP8_SHAPES)}")
 
     def fp8_on_gemm4(self, shape: str) -> bool:
-        return self.fp8_gemm4 == "all" or shape in self.fp8_gemm4.split("+")
+        return self.gemm4 and (self.fp8_gemm4 == "all" or shape in self.fp8_gemm4.split("+"))
 
     def with_overrides(self, spec: str) -> "KernelPolicy":
         """``"gemm4=0,library_gemms=auto"`` applied on top of this policy."""

@@ -33,14 +33,18 @@
 //     (gate|up at M = 512: 448 tiles on 224 workgroups, 2 each -- at the power cap fewer busy CUs
 //     clock higher, which is why hipBLASLt picks that grid); blockIdx is remapped so the
 //     workgroups of one XCD take neighbouring work items (shared A / B panels in its L2).
-//   * fp8 (e4m3) operands run the block-scaled 32x32x64 MFMA with gemm_tile.hip's fp8 contracts:
-//     per-row activation x per-channel weight scales in the epilogue (PREC 1), or MX activations
-//     (PREC 2: one e8m0 scale per (row, 128-column block), common.h mx_off layout) fed to the
-//     MFMA's per-lane scale operand -- a k-tile is exactly one scale block, so lane l's scale
-//     byte for activation block mi is row 32 mi + (l & 31)'s, read once per k-tile from an LDS
-//     copy of the tile's scales; and the gate|up SwiGLU epilogue can quantise its output to MX
-//     itself (kG4SwiGLUMx: the 128 output columns of a 256-wide weight tile are one block, so
-//     the row amax is a shuffle plus one LDS exchange between the tile's two n-waves).
+//   * fp8 (e4m3) operands run gemm_tile.hip's block-scaled 16x16x128 MFMA with its fragment
+//     pairing (halves = 16-B chunks g and g+4 of the 128-B k-tile row), so sums, epilogues and
+//     split-K partials are bit-identical to gemm_tile's fp8 path.  A k-tile is 64 MFMAs of 32
+//     cycles (the bf16 k-tile's 2048), but each needs a whole 32-B fragment pair, so the k-loop
+//     has its own schedule (G4S8): weight fragments double-buffered, activation fragments
+//     re-read one row block behind the MFMAs.  Per-row activation x per-channel weight scales in
+//     the epilogue (PREC 1), or MX activations (PREC 2: one e8m0 scale per (row, 128-column
+//     block), common.h mx_off layout) on the MFMA's per-lane scale operand -- a k-tile is exactly
+//     one scale block, read once per k-tile from an LDS copy of the tile's scales; and the
+//     gate|up SwiGLU epilogue can quantise its output to MX itself (kG4SwiGLUMx: the 128 output
+//     columns of a 256-wide weight tile are one block, so the row amax is two shuffles plus one
+//     LDS exchange between the tile's two n-waves).
 #include "kernels.h"
 
 #include <type_traits>
@@ -110,42 +114,81 @@ typedef int g4_i32x4 __attribute__((ext_vector_type(4)));
 typedef int g4_i32x8 __attribute__((ext_vector_type(8)));
 typedef float g4_f32x16 __attribute__((ext_vector_type(16)));
 
-// fp8 e4m3 x fp8 e4m3 -> fp32, 32 x 32 x 64, block scales 1.0 (e8m0 127 in `sc`): the per-row /
-// per-channel scales are applied in the epilogue.  The two 16-B halves of each operand come from
-// two ds_read_b128 into adjacent registers (the register coalescer places them; no copies).
-__device__ __forceinline__ void g4_mfma8(g4_f32x16& acc, const g4_i32x4& w0, const g4_i32x4& w1,
+// fp8 e4m3 x fp8 e4m3 -> fp32, 16 x 16 x 128, block scales 1.0 (e8m0 127 in `sc`): the per-row /
+// per-channel scales are applied in the epilogue -- gemm_tile.hip's mfma_fp8, same operand order
+// (weights = A, activations = B).  The two 16-B halves of each operand come from two
+// ds_read_b128 into adjacent registers (the register coalescer places them; no copies).
+__device__ __forceinline__ void g4_mfma8(f32x4& acc, const g4_i32x4& w0, const g4_i32x4& w1,
                                          const g4_i32x4& x0, const g4_i32x4& x1, int sc) {
   const g4_i32x8 w = __builtin_shufflevector(w0, w1, 0, 1, 2, 3, 4, 5, 6, 7);
   const g4_i32x8 x = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
-  asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
+  asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %3 op_sel_hi:[0,0,0]"
                : "+a"(acc) : "v"(w), "v"(x), "v"(sc) : "memory");
 }
 
 // MX activations: the weight block scale stays 1.0 (e8m0 127), the activation scale is byte SEL
-// of `sx` (lane l: activation row 32 SEL + (l & 31) of the wave's 128, this k-tile)
+// of `sx` (lane l: row l & 15 of activation fragment SEL of a 64-row half, mx_off's byte order)
 template <int SEL>
-__device__ __forceinline__ void g4_mfma8mx(g4_f32x16& acc, const g4_i32x4& w0, const g4_i32x4& w1,
+__device__ __forceinline__ void g4_mfma8mx(f32x4& acc, const g4_i32x4& w0, const g4_i32x4& w1,
                                            const g4_i32x4& x0, const g4_i32x4& x1, int sc, int sx) {
   const g4_i32x8 w = __builtin_shufflevector(w0, w1, 0, 1, 2, 3, 4, 5, 6, 7);
   const g4_i32x8 x = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
   if constexpr (SEL == 0)
-    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]"
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,0,0]"
                  : "+a"(acc) : "v"(w), "v"(x), "v"(sc), "v"(sx) : "memory");
   else if constexpr (SEL == 1)
-    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,1,0] op_sel_hi:[0,0,0]"
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,1,0] op_sel_hi:[0,0,0]"
                  : "+a"(acc) : "v"(w), "v"(x), "v"(sc), "v"(sx) : "memory");
   else if constexpr (SEL == 2)
-    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,1,0]"
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel_hi:[0,1,0]"
                  : "+a"(acc) : "v"(w), "v"(x), "v"(sc), "v"(sx) : "memory");
   else
-    asm volatile("v_mfma_scale_f32_32x32x64_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,1,0] op_sel_hi:[0,1,0]"
+    asm volatile("v_mfma_scale_f32_16x16x128_f8f6f4 %0, %1, %2, %0, %3, %4 op_sel:[0,1,0] op_sel_hi:[0,1,0]"
                  : "+a"(acc) : "v"(w), "v"(x), "v"(sc), "v"(sx) : "memory");
 }
+
+// fp8 k-loop schedules, in MFMA slots 0..63 of a k-tile (32 cycles each; MFMA g = activation
+// fragment g / 8 x weight fragment g % 8).  Activation fragments la..7 of the tile are read at
+// slots 1.. (two halves each), then lgkmcnt(0) + B1 after slot b1; DMA piece j after slot
+// d0 + ds*j; vmcnt(vm) + B2 after b2; then the next tile's reads -- MX dwords with activation
+// fragment 0, weight fragments 0..7 (into the other weight buffer), activation fragments
+// 1..la-1 -- spread evenly over slots p0..63, each at least two MFMAs after its register's last
+// use; lgkmcnt(2 (la - 1)) at the tile's end (weights and fragment 0 landed).  Weights are double
+// buffered (128 VGPRs), activations single (64): with the 256 accumulators in AGPRs a second
+// activation set would not fit.
+template <int V> struct G4S8;
+template <> struct G4S8<0> {   // late activation reads, DMA before B2 (1 per 2 MFMAs)
+  static constexpr int la = 7, b1 = 5, d0 = 6, ds = 2, b2 = 37, vm = 16, p0 = 38;
+};
+template <> struct G4S8<1> {   // three activation fragments read at the tile's start
+  static constexpr int la = 5, b1 = 8, d0 = 9, ds = 2, b2 = 40, vm = 16, p0 = 41;
+};
+template <> struct G4S8<2> {   // v0 with the DMA spread over B2 (1 per 3 MFMAs, 12 before it)
+  static constexpr int la = 7, b1 = 5, d0 = 6, ds = 3, b2 = 40, vm = 12, p0 = 41;
+};
+constexpr int kG8Default = 0, kG8Variants = 3;
+template <typename S> struct G4S8Reads {
+  static constexpr int n = 16 + 2 * S::la;   // post-B2 reads per k-tile
+  static constexpr int len = 64 - S::p0;
+  // first post-B2 read issued after MFMA slot g (reads [lo(g), lo(g + 1)) go there)
+  static constexpr int lo(int g) { return g < S::p0 ? 0 : ((g - S::p0) * n + len - 1) / len; }
+  static constexpr int pos(int r) { return S::p0 + r * len / n; }
+  static constexpr bool ok() {
+    for (int i = 1; i < S::la; ++i)   // activation fragment i's last MFMA is slot 8 i + 7
+      if (pos(18 + 2 * (i - 1)) < 8 * i + 9) return false;
+    return S::b1 >= 2 * (8 - S::la) && S::d0 > S::b1 && S::d0 + (S::vm - 1) * S::ds <= S::b2 &&
+           (S::vm == 16 || S::d0 + S::vm * S::ds > S::b2) && S::p0 > S::b2 &&
+           S::d0 + 15 * S::ds <= 63 && 2 * (S::la - 1) <= 15;
+  }
+};
+static_assert(G4S8Reads<G4S8<0>>::ok() && G4S8Reads<G4S8<1>>::ok() && G4S8Reads<G4S8<2>>::ok(),
+              "fp8 k-loop schedule violates a hazard / count constraint");
 
 typedef unsigned g4_u32x2 __attribute__((ext_vector_type(2)));
 
 // the two dwords of this lane's MX scales of one k-tile (rows wr*128 + (l & 15) + {0..63 step
-// 16} and + 64: mx_off packs rows r, r+16, r+32, r+48 of a 64-row block in one dword)
+// 16} and + 64: mx_off packs rows r, r+16, r+32, r+48 of a 64-row block in one dword; byte i of
+// dword h scales activation fragment 4 h + i)
 __device__ __forceinline__ void g4_read_mx(g4_u32x2& dst, int addr) {
   asm volatile("ds_read2_b32 %0, %1 offset1:16" : "=v"(dst) : "v"(addr) : "memory");
 }
@@ -176,13 +219,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t g4_rsrc(const void* base, int 
                                            __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-// PREC 0: bf16 operands (16x16x32 MFMAs, 128 per wave per k-tile).  PREC 1: fp8 e4m3 operands
-// (a k-tile = 128 bytes = 128 elements of every row, the same LDS image and DMA): 32x32x64
-// block-scaled MFMAs, 32 per wave per k-tile, each as long as four bf16 ones, so the k-loop
-// schedule (in 16-cycle slots, one bf16 MFMA or a quarter fp8 MFMA each) is shared; fragments of
-// 32 rows x 64 bytes (two ds_read_b128 per lane); per-row a_scale x per-channel b_scale in the
-// epilogue, as gemm_tile.hip's fp8 path.  PREC 2: PREC 1 with MX activation scales (G4Mx) on the
-// MFMA's scale operand instead of a_scale.
+// PREC 0: bf16 operands (16x16x32 MFMAs, 128 per wave per k-tile, G4Sched<VAR>).  PREC 1: fp8
+// e4m3 operands (a k-tile = 128 bytes = 128 elements of every row, the same LDS image and DMA):
+// 16x16x128 block-scaled MFMAs, 64 per wave per k-tile (G4S8<VAR>); per-row a_scale x
+// per-channel b_scale in the epilogue, as gemm_tile.hip's fp8 path.  PREC 2: PREC 1 with MX
+// activation scales (G4Mx) on the MFMA's scale operand instead of a_scale.
 template <int EPI, int VAR, int PREC = 0>
 __global__ void __launch_bounds__(kG4Threads, 1)
 gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __restrict__ C,
@@ -228,26 +269,10 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
       rdA[kk][s] = lds0 + s * kG4Stage + (wr * 128 + fr) * 128 + ch;
       rdB[kk][s] = lds0 + s * kG4Stage + 32768 + (wc * 128 + fr) * 128 + ch;
     }
-  // fp8 fragments: lane l reads row 32 i + (l & 31) of its wave's A / B half, 16-B chunks
-  // kk*4 + 2 (l >> 5) + h (h = 0, 1) of the 128-B k-tile row, swizzled like the DMA wrote them
-  int rdA8[2][2][2], rdB8[2][2][2];
-  if constexpr (F8) {
-    const int r32 = lane & 31, sw8 = (r32 >> 1) & 7;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int ch = ((kk * 4 + 2 * (lane >> 5) + h) ^ sw8) << 4;
-          rdA8[kk][st][h] = lds0 + st * kG4Stage + (wr * 128 + r32) * 128 + ch;
-          rdB8[kk][st][h] = lds0 + st * kG4Stage + 32768 + (wc * 128 + r32) * 128 + ch;
-        }
-  }
+  // (fp8: a fragment's two 16-B halves are the bf16 k-step 0 / 1 chunks, rdX[0] / rdX[1]: chunks
+  // l >> 4 and 4 + (l >> 4) of the 128-B row, gemm_tile.hip's fp8 pairing)
   // MX scales: this lane's two dwords of a k-tile's 256-byte slab (rows wr*128 + (l & 15) + 16 i)
-  // and the byte order that packs the rows it scales, 32 mi + (l & 31), as bytes mi = 0..3
   const int mxrd = lds0 + kMxOff + wr * 128 + (lane & 15) * 4;
-  const unsigned mxsel = (lane & 16) ? 0x07050301u : 0x06040200u;
   // DMA: wave-load q = 4j + w covers tile rows 8q .. 8q+7; lane -> row 8q + (lane >> 3), LDS
   // slot lane & 7 holding global chunk (lane & 7) ^ ((row >> 1) & 7) = .. ^ ((q & 1) * 4 + (lane >> 4))
   const int dchunk = ((lane & 7) ^ (((w & 1) * 4 + (lane >> 4)) & 7)) << 4;
@@ -281,8 +306,8 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
       }
       g4_sync_lds();   // written before the prologue's barrier publishes them
     }
-    g4_u32x2 mxr = {0x7f7f7f7fu, 0x7f7f7f7fu};   // raw scale dwords of the next k-tile
-    int mxs = 0x7f7f7f7f;                        // packed scales of the current k-tile
+    g4_u32x2 mxr = {0x7f7f7f7fu, 0x7f7f7f7fu};   // scale dwords of the next k-tile
+    g4_u32x2 mxc = mxr;                          // ... of the current one
 
     // stage DMA piece j (0..15: A rows 32j' .. for j < 8, B for j >= 8) of k-tile t
     auto dma = [&](int t, int j) {
@@ -305,44 +330,99 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // fp8: 4 x 4 tiles of 32 x 32 (acc8[mi][ni]: activation block mi, weight block ni)
-    g4_f32x16 acc8[4][4];
     if constexpr (F8) {
+      // ---- fp8 k-loop (G4S8): 64 16x16x128 MFMAs per wave per k-tile ----
+      using S = G4S8<(VAR >= 0 && VAR < kG8Variants) ? VAR : kG8Default>;
+      using R = G4S8Reads<S>;
+      const int sc127 = 127;
+      g4_i32x4 W8[2][8][2], A8[8][2];   // [buffer][fragment][half], [fragment][half]
+      // prologue: tiles 0 and 1 in flight, tile 0 landed, its weights (buffer 0), activation
+      // fragments 0..la-1 and MX scales read
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 16; ++j) dma(0, j);
+      if (T > 1) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc8[i][j][e] = 0.f;
-    }
-    const int sc127 = 127;
-    // fp8 fragment sets ([2 ni + h] weight halves, [8 + 2 mi + h] activation halves)
-    g4_i32x4 P8[16], Q8[16];
-    auto rd8 = [&](g4_i32x4 (&F)[16], int n, int kk, int s) {
-      const int h = n & 1, blk = (n >> 1) & 3;
-      const int base = n < 8 ? rdB8[kk][s][h] : rdA8[kk][s][h];
-      switch (blk) {
-        case 0: g4_read8<0 * 4096>(F[n], base); break;
-        case 1: g4_read8<1 * 4096>(F[n], base); break;
-        case 2: g4_read8<2 * 4096>(F[n], base); break;
-        default: g4_read8<3 * 4096>(F[n], base); break;
-      }
-    };
-    // fp8 MFMA number k (0..15) of a k-step: activation block k / 4, weight block k % 4
-    auto mf8 = [&](const g4_i32x4 (&F)[16], int k) {
-      const int mi = k >> 2, ni = k & 3;
-      if constexpr (MXIN) {
-        switch (mi) {   // (k is a compile-time constant at every call: the switch folds)
-          case 0: g4_mfma8mx<0>(acc8[0][ni], F[2 * ni], F[2 * ni + 1], F[8], F[9], sc127, mxs); break;
-          case 1: g4_mfma8mx<1>(acc8[1][ni], F[2 * ni], F[2 * ni + 1], F[10], F[11], sc127, mxs); break;
-          case 2: g4_mfma8mx<2>(acc8[2][ni], F[2 * ni], F[2 * ni + 1], F[12], F[13], sc127, mxs); break;
-          default: g4_mfma8mx<3>(acc8[3][ni], F[2 * ni], F[2 * ni + 1], F[14], F[15], sc127, mxs); break;
-        }
+        for (int j = 0; j < 16; ++j) dma(1, j);
+        g4_vmcnt<16>();
       } else {
-        g4_mfma8(acc8[mi][ni], F[2 * ni], F[2 * ni + 1], F[8 + 2 * mi], F[9 + 2 * mi], sc127);
+        g4_vmcnt<0>();
       }
-    };
+      g4_barrier();
+      if constexpr (MXIN) g4_read_mx(mxr, mxrd);
+      g4_static_for(std::make_integer_sequence<int, 16>{}, [&](auto N) {
+        constexpr int n = decltype(N)::value, f = n >> 1, h = n & 1;
+        g4_read8<f * 2048>(W8[0][f][h], rdB[h][0]);
+        if constexpr (f < S::la) g4_read8<f * 2048>(A8[f][h], rdA[h][0]);
+      });
+      g4_sync_lds();
 
+      // one k-tile on stage / weight buffer P (= t & 1).  DMA: issue tile t+2 into stage P; NEXT:
+      // read tile t+1's weights into buffer P ^ 1 and its activation fragments 0..la-1
+      auto ktile8 = [&](int t, auto p_c, auto dma_c, auto next_c, bool dma_rt, bool next_rt) {
+        constexpr int P = decltype(p_c)::value;
+        // DMA / NEXT: compile-time "may", dma_rt / next_rt: whether it does (uniform)
+        constexpr bool DMA = decltype(dma_c)::value, NEXT = decltype(next_c)::value;
+        if constexpr (MXIN) mxc = mxr;
+        g4_static_for(std::make_integer_sequence<int, 64>{}, [&](auto G) {
+          constexpr int g = decltype(G)::value, i = g >> 3, j = g & 7;
+          if constexpr (MXIN)
+            g4_mfma8mx<i & 3>(acc[i][j], W8[P][j][0], W8[P][j][1], A8[i][0], A8[i][1], sc127,
+                              (int)mxc[i >> 2]);
+          else
+            g4_mfma8(acc[i][j], W8[P][j][0], W8[P][j][1], A8[i][0], A8[i][1], sc127);
+          if constexpr (g >= 1 && g <= 2 * (8 - S::la)) {   // this tile's late activation reads
+            constexpr int f = S::la + (g - 1) / 2, h = (g - 1) & 1;
+            g4_read8<f * 2048>(A8[f][h], rdA[h][P]);
+          }
+          if constexpr (g == S::b1) {
+            g4_sync_lds();
+            if (DMA && dma_rt) g4_barrier();
+          }
+          if constexpr (DMA && g >= S::d0 && g <= S::d0 + 15 * S::ds && (g - S::d0) % S::ds == 0)
+            if (dma_rt) dma(t + 2, (g - S::d0) / S::ds);
+          if constexpr (NEXT && g == S::b2) {
+            if (next_rt) {
+              if (DMA && dma_rt) g4_vmcnt<S::vm>(); else g4_vmcnt<0>();
+              g4_barrier();
+            }
+          }
+          if constexpr (NEXT) if (next_rt) {
+            g4_static_for(std::make_integer_sequence<int, 4>{}, [&](auto K) {
+              constexpr int r = R::lo(g) + decltype(K)::value;
+              if constexpr (r < R::lo(g + 1)) {
+                if constexpr (r < 2) {
+                  if constexpr (MXIN && r == 0) g4_read_mx(mxr, mxrd + (t + 1) * 256);
+                  g4_read8<0>(A8[0][r], rdA[r][P ^ 1]);
+                } else if constexpr (r < 18) {
+                  constexpr int f = (r - 2) >> 1, h = r & 1;
+                  g4_read8<f * 2048>(W8[P ^ 1][f][h], rdB[h][P ^ 1]);
+                } else {
+                  constexpr int f = 1 + ((r - 18) >> 1), h = r & 1;
+                  g4_read8<f * 2048>(A8[f][h], rdA[h][P ^ 1]);
+                }
+              }
+            });
+          }
+        });
+        if constexpr (NEXT)
+          if (next_rt) asm volatile("s_waitcnt lgkmcnt(%0)" :: "i"(2 * (S::la - 1)) : "memory");
+      };
+      // tiles in pairs (stage parity = t & 1 is a compile-time argument), then the 1-3 left
+      using B1 = G4B<true>;
+      using B0 = G4B<false>;
+      using P0 = std::integral_constant<int, 0>;
+      using P1 = std::integral_constant<int, 1>;
+      int t = 0;
+      for (; t + 3 < T; t += 2) {
+        ktile8(t, P0{}, B1{}, B1{}, true, true);
+        ktile8(t + 1, P1{}, B1{}, B1{}, true, true);
+      }
+      ktile8(t, P0{}, B1{}, B1{}, t + 2 < T, t + 1 < T);
+      if (t + 1 < T) {
+        ktile8(t + 1, P1{}, B0{}, B1{}, false, t + 2 < T);
+        if (t + 2 < T) ktile8(t + 2, P0{}, B0{}, B0{}, false, false);
+      }
+    } else {
     // fragment sets: P = k-step 0, Q = k-step 1 ([0..7] weight fragments, [8..15] activation)
     bf16x8 P[16], Q[16];
     // read fragment n of k-step kk of stage s: n < 8 weight rows wc*128 + 16n, else activation
@@ -383,11 +463,8 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
       g4_vmcnt<0>();
     }
     g4_barrier();
-    if constexpr (MXIN) g4_read_mx(mxr, mxrd);
 #pragma unroll
-    for (int n = 0; n < 16; ++n) {
-      if constexpr (F8) rd8(P8, n, 0, 0); else rd(P, n, 0, 0);
-    }
+    for (int n = 0; n < 16; ++n) rd(P, n, 0, 0);
     g4_sync_lds();
 
     // one k-tile.  DMA: issue tile t+2 into stage t&1; NEXT: read k-step 0 of tile t+1
@@ -395,23 +472,14 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
       constexpr bool DMA = decltype(dma_c)::value, NEXT = decltype(next_c)::value;
       using S = G4Sched<VAR>;
       const int s = t & 1;
-      // this k-tile's MX scales (read with the previous tile's P fragments, retired since)
-      if constexpr (MXIN) mxs = (int)__builtin_amdgcn_perm(mxr[1], mxr[0], mxsel);
       // MFMA g of the k-tile (g < 64: k-step 0 on P, else k-step 1 on Q), and after it: the k-step
       // 1 reads of this tile -> Q, B1, the DMA of tile t+2 into stage s, B2, the k-step 0 reads of
       // tile t+1 -> P, at the positions the schedule S gives
       g4_static_for(std::make_integer_sequence<int, 128>{}, [&](auto G) {
         constexpr int g = decltype(G)::value;
-        if constexpr (F8) {   // one 32x32x64 MFMA per 4 slots
-          if constexpr (g % 4 == 0) {
-            if constexpr (g < 64) mf8(P8, g / 4); else mf8(Q8, (g - 64) / 4);
-          }
-        } else {
-          if constexpr (g < 64) mf(P, g); else mf(Q, g - 64);
-        }
-        if constexpr (g >= S::q0 && g < S::q0 + 16 * S::qs && (g - S::q0) % S::qs == 0) {
-          if constexpr (F8) rd8(Q8, (g - S::q0) / S::qs, 1, s); else rd(Q, (g - S::q0) / S::qs, 1, s);
-        }
+        if constexpr (g < 64) mf(P, g); else mf(Q, g - 64);
+        if constexpr (g >= S::q0 && g < S::q0 + 16 * S::qs && (g - S::q0) % S::qs == 0)
+          rd(Q, (g - S::q0) / S::qs, 1, s);
         if constexpr (g == S::b1) {   // this wave's reads of stage s done -> after B1 every wave's
           g4_sync_lds();
           if (DMA) g4_barrier();
@@ -422,11 +490,8 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
           if (DMA) g4_vmcnt<S::vm>(); else g4_vmcnt<0>();
           g4_barrier();
         }
-        if constexpr (NEXT && g >= S::p0 && g < S::p0 + 16 * S::ps && (g - S::p0) % S::ps == 0) {
-          if constexpr (MXIN && g == S::p0) g4_read_mx(mxr, mxrd + (t + 1) * 256);
-          if constexpr (F8) rd8(P8, (g - S::p0) / S::ps, 0, s ^ 1);
-          else rd(P, (g - S::p0) / S::ps, 0, s ^ 1);
-        }
+        if constexpr (NEXT && g >= S::p0 && g < S::p0 + 16 * S::ps && (g - S::p0) % S::ps == 0)
+          rd(P, (g - S::p0) / S::ps, 0, s ^ 1);
       });
       if (NEXT) g4_sync_lds();
     };
@@ -434,6 +499,7 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
     for (; t + 2 < T; ++t) ktile(t, G4B<true>{}, G4B<true>{});
     if (t + 1 < T) ktile(t++, G4B<false>{}, G4B<true>{});
     ktile(t, G4B<false>{}, G4B<false>{});
+    }
 
 #ifdef GEMM_STAMPS
     if (tid == 0) {
@@ -442,135 +508,76 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
     }
 #endif
     // the last MFMAs' results -> compiler-issued AGPR reads: 12+ wait states for an 8-pass XDL
-    // write; the fence takes every accumulator "+a" so no read is hoisted above it
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-    if constexpr (F8) {
+    // write (18+ for the 16-pass fp8 one); the fence takes every accumulator "+a" so no read is
+    // hoisted above it
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        asm volatile("" : "+a"(acc8[i][0]), "+a"(acc8[i][1]), "+a"(acc8[i][2]), "+a"(acc8[i][3]));
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]),
-                     "+a"(acc[i][4]), "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
-    }
+    for (int i = 0; i < 8; ++i)
+      asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]),
+                   "+a"(acc[i][4]), "+a"(acc[i][5]), "+a"(acc[i][6]), "+a"(acc[i][7]));
 
     // ---- epilogue: fragment (i, j) element e of lane l is
     //      C[m0 + wr*128 + 16i + (l & 15)][n0 + wc*128 + 16j + 4(l >> 4) + e] ----
-    if constexpr (F8 && EPI == kG4SwiGLUMx) {
+    const int crow = m0 + wr * 128 + fr;
+    const int cq = 4 * (lane >> 4);
+    if constexpr (F8) {   // dequantise as gemm_tile.hip: (acc x channel scale) x row scale
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float sa = MXIN ? 1.f : a_scale[min(crow + i * 16, M - 1)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const f32x4 sb = *reinterpret_cast<const f32x4*>(b_scale + n0 + wc * 128 + j * 16 + cq);
+          acc[i][j] = acc[i][j] * sb * sa;
+        }
+      }
+    }
+    if constexpr (EPI == kG4SwiGLUMx) {
       // h = silu(gate) * up rounded to bf16 (what the bf16 SwiGLU epilogue stores), kept in the
-      // gate registers; the row's amax over its 128-column block = the two n-waves' 64 each
-      // (lanes l and l + 32 share a row: one shuffle, then one LDS exchange), then e4m3(h * 2^-k)
-      // and one e8m0 byte per (row, block) -- ops.mx_quantize's rule, gemm_tile's kSwiGLUMx
-      const int c4 = 4 * (lane >> 5), x = lane & 31;
+      // gate fragments; the row's amax over its 128-column block = the two n-waves' 64 each (the
+      // 4 lanes sharing a row: two shuffles, then one LDS exchange), then e4m3(h * 2^-k) and one
+      // e8m0 byte per (row, block) -- ops.mx_quantize's rule, gemm_tile's kSwiGLUMx
       float* red = reinterpret_cast<float*>(smem + kRedOff);   // [wc][256 rows]
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        const int row = m0 + wr * 128 + 32 * mi + x;
-        const float sa = a_scale[min(row, M - 1)];
+      for (int i = 0; i < 8; ++i) {
         float a = 0.f;
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const int nb = n0 + wc * 128 + 32 * ni + c4;
+        for (int p = 0; p < 4; ++p)
 #pragma unroll
-          for (int g = 0; g < 2; ++g) {
-            const f32x4 sg = *reinterpret_cast<const f32x4*>(b_scale + nb + 8 * g);
-            const f32x4 su = *reinterpret_cast<const f32x4*>(b_scale + nb + 8 * g + 16);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float gv = (float)(bf16)(acc8[mi][ni][4 * g + e] * sg[e] * sa);
-              const float uv = (float)(bf16)(acc8[mi][ni][4 * g + 8 + e] * su[e] * sa);
-              const float h = (float)(bf16)(g4_silu(gv) * uv);
-              acc8[mi][ni][4 * g + e] = h;
-              a = fmaxf(a, fabsf(h));
-            }
+          for (int e = 0; e < 4; ++e) {
+            const float g = (float)(bf16)acc[i][2 * p][e];
+            const float u = (float)(bf16)acc[i][2 * p + 1][e];
+            const float h = (float)(bf16)(g4_silu(g) * u);
+            acc[i][2 * p][e] = h;
+            a = fmaxf(a, fabsf(h));
           }
-        }
+        a = fmaxf(a, __shfl_xor(a, 16, 64));
         a = fmaxf(a, __shfl_xor(a, 32, 64));
-        if (lane < 32) red[wc * 256 + wr * 128 + 32 * mi + x] = a;
+        if (lane < 16) red[wc * 256 + wr * 128 + i * 16 + fr] = a;
       }
       g4_sync_lds();
       g4_barrier();
       uint8_t* out = reinterpret_cast<uint8_t*>(C);
       const int I = N >> 1, tn = n0 >> 8;
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        const int r = wr * 128 + 32 * mi + x, row = m0 + r;
+      for (int i = 0; i < 8; ++i) {
+        const int r = wr * 128 + i * 16 + fr, row = m0 + r;
         const int k = mx_exponent(fmaxf(red[r], red[256 + r]));
         const float inv = mx_inv_scale(k);
         if (row < M) {
 #pragma unroll
-          for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-              *reinterpret_cast<unsigned*>(out + (size_t)row * I + (n0 >> 1) + wc * 64 + 16 * ni +
-                                           8 * g + c4) =
-                  pack4_fp8(acc8[mi][ni][4 * g] * inv, acc8[mi][ni][4 * g + 1] * inv,
-                            acc8[mi][ni][4 * g + 2] * inv, acc8[mi][ni][4 * g + 3] * inv);
-            }
-        }
-        // one byte per (row, block); rows in [M, 64 nb) get 2^0 (the consumer reads them)
-        if (wc == 0 && lane < 32 && row < mx.nb * 64)
-          mx.out_sc[mx_off(tn, row, mx.nb)] = (uint8_t)(row < M ? k + 127 : 127);
-      }
-      g4_barrier();
-      continue;
-    }
-    if constexpr (F8) {
-      // 32x32 tile (mi, ni) element r of lane l: row m0 + wr*128 + 32 mi + (l & 31), column
-      // n0 + wc*128 + 32 ni + 8 (r >> 2) + 4 (l >> 5) + (r & 3): 4 consecutive columns per group
-      const int c4 = 4 * (lane >> 5);
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        const int row = m0 + wr * 128 + 32 * mi + (lane & 31);
-        if (row >= M) continue;
-        const float sa = MXIN ? 1.f : a_scale[row];
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const int nb = n0 + wc * 128 + 32 * ni + c4;
-          if constexpr (EPI == kG4SwiGLU) {
-            // groups 0, 1 = gate of output columns 16 q + 8 g + c4 + e (q = wc*4 + ni), 2, 3 = up
-            bf16* out = reinterpret_cast<bf16*>(C);
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-              const f32x4 sg = *reinterpret_cast<const f32x4*>(b_scale + nb + 8 * g);
-              const f32x4 su = *reinterpret_cast<const f32x4*>(b_scale + nb + 8 * g + 16);
-              bf16x4 o;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float gv = (float)(bf16)(acc8[mi][ni][4 * g + e] * sg[e] * sa);
-                const float uv = (float)(bf16)(acc8[mi][ni][4 * g + 8 + e] * su[e] * sa);
-                o[e] = (bf16)(g4_silu(gv) * uv);
-              }
-              *reinterpret_cast<bf16x4*>(out + (size_t)row * (N >> 1) + (n0 >> 1) + wc * 64 +
-                                         16 * ni + 8 * g + c4) = o;
-            }
-          } else {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const f32x4 sb = *reinterpret_cast<const f32x4*>(b_scale + nb + 8 * g);
-              f32x4 v;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = acc8[mi][ni][4 * g + e] * sb[e] * sa;
-              const size_t idx = (size_t)row * N + nb + 8 * g;
-              if constexpr (EPI == kG4F32) {
-                *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(C) + (size_t)split * M * N + idx) = v;
-              } else {
-                bf16x4 o;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-                bf16* out = reinterpret_cast<bf16*>(C) + (EPI == kG4Bf16Part ? (size_t)split * M * N : 0);
-                *reinterpret_cast<bf16x4*>(out + idx) = o;
-              }
-            }
+          for (int p = 0; p < 4; ++p) {
+            const f32x4 v = acc[i][2 * p] * inv;
+            *reinterpret_cast<unsigned*>(out + (size_t)row * I + (n0 >> 1) + wc * 64 + p * 16 + cq) =
+                pack4_fp8(v[0], v[1], v[2], v[3]);
           }
         }
+        // one byte per (row, block); rows in [M, 64 nb) get 2^0 (the consumer reads them)
+        if (wc == 0 && lane < 16 && row < mx.nb * 64)
+          mx.out_sc[mx_off(tn, row, mx.nb)] = (uint8_t)(row < M ? k + 127 : 127);
       }
-      g4_barrier();
+      g4_barrier();   // the exchange slab is reused by the next item
       continue;
     }
-    const int crow = m0 + wr * 128 + fr;
-    const int cq = 4 * (lane >> 4);
     if constexpr (EPI == kG4SwiGLU) {
       // n-fragments (2p, 2p+1) = (gate, up) of output columns n0/2 + wc*64 + 16p + cq + e
       bf16* out = reinterpret_cast<bf16*>(C);
@@ -682,16 +689,27 @@ static int launch_gemm4_p(void* C, const void* a, const void* b, int M, int N, i
                           int tiles_n, int kps, int splits, int epilogue, int grid,
                           hipStream_t stream, int variant, const float* sa, const float* sb,
                           G4Mx mx) {
-  if (variant == kG4DecodeDefault)
-    return launch_gemm4_v<kG4DecodeDefault, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
-  if (variant != kG4Default) return -5;
-  return launch_gemm4_v<kG4Default, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
+  if constexpr (PREC >= 1) {   // fp8: G4S8 schedules (the others: experiment builds only)
+#ifdef GEMM4_FP8_VARIANTS
+    if (variant == 1)
+      return launch_gemm4_v<1, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
+    if (variant == 2)
+      return launch_gemm4_v<2, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
+#endif
+    if (variant != kG8Default) return -5;
+    return launch_gemm4_v<kG8Default, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
+  } else {
+    if (variant == kG4DecodeDefault)
+      return launch_gemm4_v<kG4DecodeDefault, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
+    if (variant != kG4Default) return -5;
+    return launch_gemm4_v<kG4Default, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
+  }
 }
 
 // C = A . B^T on the one-wave-per-SIMD kernel.  epilogue 0: bf16 [M, N]; 2: fused SwiGLU ([M,
 // N/2], B rows in swiglu_interleave order); with splits > 1: 1 = fp32 partials [splits, M, N],
 // 4 = bf16 partials [splits, M, N] (into C; the consumer sums them).  grid <= 0: automatic.
-// variant < 0: the default k-loop schedule (G4Sched), else that one (A/B experiments).
+// variant < 0: the default k-loop schedule (G4Sched; fp8: G4S8), else that one (A/B experiments).
 // precision 1: fp8 e4m3 A [M, K] / B [N, K] (1-byte), results scaled by a_scale[M] * b_scale[N];
 // precision 2: fp8 with MX activation scales a_mx (mx_off layout, nb = ceil(M / 64)) instead of
 // a_scale.  epilogue 3 (precision 1, one split): SwiGLU quantised to MX fp8 [M, N/2] in C, its
@@ -716,7 +734,8 @@ int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int
   const int items = tiles_m * tiles_n * splits;
   if (grid <= 0) grid = gemm4_grid(items, g4_cus());
   if (grid > items) grid = items;
-  if (variant < 0) variant = tiles_m <= 2 ? kG4DecodeDefault : kG4Default;
+  if (variant < 0)
+    variant = precision >= 1 ? kG8Default : tiles_m <= 2 ? kG4DecodeDefault : kG4Default;
   const G4Mx mx{a_mx, out_mx, (M + 63) / 64};
   if (precision == 2)
     return launch_gemm4_p<2>(C, A, B, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid,

@@ -521,7 +521,8 @@ def _gemm4(x: torch.Tensor, w: torch.Tensor, splits: int, swiglu: bool,
     """:func:`gemm_tile`'s contract on gemm4: same epilogues (bf16 store, fused SwiGLU, split-K
     partials handed to the consumer or reduced here), bit-identical results for bf16.  fp8 e4m3
     operands (``xs`` [M] / ``ws`` [N] scales, or ``x_mx``: MX activation scales) run the
-    block-scaled 32x32x64 MFMA (:func:`gemm_tile_fp8` / :func:`gemm_tile_fp8_mx`'s contracts)."""
+    block-scaled 16x16x128 MFMA with gemm_tile's fragment pairing (:func:`gemm_tile_fp8` /
+    :func:`gemm_tile_fp8_mx`'s contracts, bit-identical results)."""
     M, N = x.shape[0], w.shape[0]
     splits = max(1, int(splits))
     fp8 = xs is not None or x_mx is not None

@@ -49,9 +49,10 @@ def test_env_surface_is_small_and_has_no_stale_docs():
 
 def test_kernel_policy_overrides_parse_and_reject_unknown_fields():
     from distributed_llm_inference.config import KernelPolicy
-    p = KernelPolicy().with_overrides("gemm4=0, library_gemms=auto ,fp8_gemm4=gate_up+down")
-    assert not p.gemm4 and p.library_gemms is None
+    p = KernelPolicy().with_overrides("gemm4=1, library_gemms=auto ,fp8_gemm4=gate_up+down")
+    assert p.gemm4 and p.library_gemms is None
     assert p.fp8_on_gemm4("down") and not p.fp8_on_gemm4("qkv")
+    assert not p.with_overrides("gemm4=0").fp8_on_gemm4("down")   # gemm4 off: nothing on it
     assert KernelPolicy(fp8_gemm4="all").fp8_on_gemm4("o")
     with pytest.raises(ValueError, match="unknown kernel policy field"):
         KernelPolicy().with_overrides("gemm5=1")
