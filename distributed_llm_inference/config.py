@@ -393,6 +393,9 @@ class KernelPolicy:
     # gate_up / down.  gate|up: 202 vs 219 us alone, +1.9 % tok/s in-step; the others win 2-7 %
     # alone but stay within noise in-step (profiles/r5/fp8_gemm4_16x16.md)
     fp8_gemm4: str = "gate_up"
+    # bf16 gemm4 k-loop schedule at decode M (<= 2 row tiles of 256): 6 (DMA spread thin), 4,
+    # or 9 / 8 = 6 / 4 with the weight stream non-temporal (csrc/kernels/gemm4.hip G4Sched)
+    gemm4_decode_sched: int = 6
     # split-K partials of the deferred projections (QKV, O, down) stored as bf16 (else fp32);
     # consumers always sum in fp32 (profiles/bf16_partials_ab.txt, docs/parity.md C6)
     bf16_partials: bool = True
@@ -422,6 +425,8 @@ class KernelPolicy:
     _FP8_SHAPES = ("qkv", "o", "gate_up", "down")
 
     def __post_init__(self):
+        if self.gemm4_decode_sched not in (4, 6, 8, 9):
+            raise ValueError(f"gemm4_decode_sched={self.gemm4_decode_sched}: 4, 6, 8 or 9")
         sel = self.fp8_gemm4
         if sel not in ("all", "none") and any(
                 x not in self._FP8_SHAPES for x in sel.split("+")):
@@ -446,6 +451,8 @@ class KernelPolicy:
                 raise ValueError(f"unknown kernel policy field {k!r} (known: {sorted(names)})")
             if k == "fp8_gemm4":
                 kw[k] = v
+            elif names[k].type in (int, "int"):
+                kw[k] = int(v)
             elif k == "library_gemms" and v.lower() in ("auto", "none", ""):
                 kw[k] = None
             elif v.lower() in ("1", "true", "on", "yes"):

@@ -54,6 +54,14 @@ namespace dli {
 
 namespace {
 
+// cache-policy bits of the activation / weight LDS-DMA (experiment builds override them)
+#ifndef GEMM4_A_AUX
+#define GEMM4_A_AUX 0
+#endif
+#ifndef GEMM4_B_AUX
+#define GEMM4_B_AUX 0
+#endif
+
 constexpr int kG4Threads = 256;
 constexpr int kG4Stage = 65536;   // A [256][128 B] | B [256][128 B]
 
@@ -92,11 +100,19 @@ template <> struct G4Sched<4> {   // late wait, DMA spread thin (1 per 4 MFMAs),
 template <> struct G4Sched<6> {   // v4 with the DMA spread over B2 (1 per 6 MFMAs, 12 before it)
   static constexpr int q0 = 0, qs = 2, b1 = 35, d0 = 36, ds = 6, b2 = 104, vm = 12, p0 = 105, ps = 1;
 };
+// v4 / v6 with the weight DMA non-temporal (cache policy NT, aux 2: gemm_tile's decode weight
+// stream) -- each weight byte is read by at most two workgroups at decode M
+template <> struct G4Sched<8> : G4Sched<4> { static constexpr bool nt = true; };
+template <> struct G4Sched<9> : G4Sched<6> { static constexpr bool nt = true; };
 // (the other eight schedules of the round-4 A/B, profiles/r4/gemm4_ab_v0-7.txt, are in
 // scripts/experiments/gemm4_sched_variants.h)
 template <typename S, typename = void> struct G4BFirst { static constexpr bool value = false; };
 template <typename S> struct G4BFirst<S, std::void_t<decltype(S::bfirst)>> {
   static constexpr bool value = S::bfirst;
+};
+template <int V, typename = void> struct G4Nt { static constexpr bool value = false; };
+template <int V> struct G4Nt<V, std::void_t<decltype(G4Sched<V>::nt)>> {
+  static constexpr bool value = G4Sched<V>::nt;
 };
 // Default schedules (profiles/r4/gemm4_ab_v0-7.txt): decode-sized M (<= 2 row tiles, the
 // activations stay L2 / MALL-resident and only the weight stream misses) takes v6, whose DMA runs
@@ -206,6 +222,21 @@ __device__ __forceinline__ void g4_read(bf16x8& dst, int addr) {
 __device__ __forceinline__ void g4_sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void g4_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
+#ifdef GEMM_PROBE
+// diagnostic builds only (scripts/experiments/gemm4_probe.hip): per wave, shader cycles stalled
+// at the k-loop's waits (s_memtime, an SMEM read, before and after each; the read after B2 is
+// waited for at once -- no LDS read is in flight there -- the others ride the next lgkmcnt(0)).
+// g_probe[(block * 4 + wave) * 8 + k]: k = 0 B1 (lgkmcnt(0) + barrier), 1 B2 (vmcnt + barrier),
+// 2 end-of-tile LDS wait, 3 k-loop cycles, 4 k-tiles
+__device__ unsigned long long* g_probe;
+struct G4Probe {
+  unsigned long long b1 = 0, b2 = 0, ew = 0, t0 = 0, t1 = 0, t4 = 0, t5 = 0, loop0 = 0, loop = 0;
+  unsigned long long kt = 0;
+};
+#define G4P_TIME(v) asm volatile("s_memtime %0" : "=s"(v) :: "memory")
+#define G4P_FENCE(v) asm volatile("" : "+s"(v) :: "memory")
+#endif
+
 template <int N>
 __device__ __forceinline__ void g4_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" :: "i"(N) : "memory");
@@ -231,6 +262,7 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
              const float* __restrict__ a_scale, const float* __restrict__ b_scale, G4Mx mx) {
   constexpr bool F8 = PREC >= 1;
   constexpr bool MXIN = PREC == 2;
+  constexpr int kBAux = (!F8 && G4Nt<VAR>::value) ? 2 : GEMM4_B_AUX;   // weight DMA cache policy
   constexpr int kMxOff = 2 * kG4Stage;                              // MX scale slab
   constexpr int kRedOff = kMxOff + (MXIN ? kG4MxLds : 0);           // kG4SwiGLUMx exchange
   constexpr int kSmem = kRedOff + (EPI == kG4SwiGLUMx ? kG4RedLds : 0);
@@ -253,6 +285,9 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
   const int kt_all = Kb / 128;
   const int items = tiles_m * tiles_n * splits;
   const int lds0 = (int)(size_t)smem;
+#ifdef GEMM_PROBE
+  G4Probe pr;
+#endif
 
   // XCD-aware bijective remap of the workgroup index: blocks b, b+8, ... share an XCD
   const int G = gridDim.x, bx = blockIdx.x, x8 = bx & 7, q8 = G >> 3, r8 = G & 7;
@@ -291,6 +326,9 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
 #pragma unroll
     for (int j = 0; j < 8; ++j) voA[j] = min(drow + 32 * j, mrows - 1) * Kb + dchunk;
     const int voB = drow * Kb + dchunk;
+#ifdef GEMM_PROBE
+    G4P_TIME(pr.loop0);
+#endif
 
     if constexpr (MXIN) {
       // this tile's scales of its k-tiles into LDS, [t][256 rows]; 64-row blocks past the
@@ -311,16 +349,20 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
 
     // stage DMA piece j (0..15: A rows 32j' .. for j < 8, B for j >= 8) of k-tile t
     auto dma = [&](int t, int j) {
+#ifdef GEMM_PROBE_NODMA
+      if (t >= 2) return;   // diagnostic: the k-loop's DMA cost (results are garbage)
+#endif
       const int s = t & 1;
       const int koff = __builtin_amdgcn_readfirstlane((kt0 + t) * 128);
       if (j < 8) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rsA, (g4_lds_t*)(smem + s * kG4Stage + (4 * j + w) * 1024), 16, voA[j], koff, 0, 0);
+            rsA, (g4_lds_t*)(smem + s * kG4Stage + (4 * j + w) * 1024), 16, voA[j], koff, 0,
+            GEMM4_A_AUX);
       } else {
         const int jb = j - 8;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rsB, (g4_lds_t*)(smem + s * kG4Stage + 32768 + (4 * jb + w) * 1024), 16, voB,
-            __builtin_amdgcn_readfirstlane(koff + jb * 32 * Kb), 0, 0);
+            __builtin_amdgcn_readfirstlane(koff + jb * 32 * Kb), 0, kBAux);
       }
     };
 
@@ -375,15 +417,36 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
             g4_read8<f * 2048>(A8[f][h], rdA[h][P]);
           }
           if constexpr (g == S::b1) {
+#ifdef GEMM_PROBE
+            G4P_TIME(pr.t0);
+#endif
             g4_sync_lds();
             if (DMA && dma_rt) g4_barrier();
+#ifdef GEMM_PROBE
+            G4P_FENCE(pr.t4); G4P_FENCE(pr.t5); G4P_FENCE(pr.t0);
+            pr.ew += pr.t5 - pr.t4;
+            pr.t4 = pr.t5 = 0;
+            G4P_TIME(pr.t1);
+#endif
           }
           if constexpr (DMA && g >= S::d0 && g <= S::d0 + 15 * S::ds && (g - S::d0) % S::ds == 0)
             if (dma_rt) dma(t + 2, (g - S::d0) / S::ds);
           if constexpr (NEXT && g == S::b2) {
             if (next_rt) {
+#ifdef GEMM_PROBE
+              unsigned long long t2, t3;
+              G4P_TIME(t2);
+#endif
               if (DMA && dma_rt) g4_vmcnt<S::vm>(); else g4_vmcnt<0>();
               g4_barrier();
+#ifdef GEMM_PROBE
+              G4P_TIME(t3);
+              g4_sync_lds();
+              G4P_FENCE(t2); G4P_FENCE(t3); G4P_FENCE(pr.t1);
+              pr.b2 += t3 - t2;
+              pr.b1 += pr.t1 - pr.t0;
+              pr.t0 = pr.t1 = 0;
+#endif
             }
           }
           if constexpr (NEXT) if (next_rt) {
@@ -404,8 +467,15 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
             });
           }
         });
+#ifdef GEMM_PROBE
+        if constexpr (NEXT) if (next_rt) G4P_TIME(pr.t4);
+#endif
         if constexpr (NEXT)
           if (next_rt) asm volatile("s_waitcnt lgkmcnt(%0)" :: "i"(2 * (S::la - 1)) : "memory");
+#ifdef GEMM_PROBE
+        if constexpr (NEXT) if (next_rt) G4P_TIME(pr.t5);
+        ++pr.kt;
+#endif
       };
       // tiles in pairs (stage parity = t & 1 is a compile-time argument), then the 1-3 left
       using B1 = G4B<true>;
@@ -481,19 +551,47 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
         if constexpr (g >= S::q0 && g < S::q0 + 16 * S::qs && (g - S::q0) % S::qs == 0)
           rd(Q, (g - S::q0) / S::qs, 1, s);
         if constexpr (g == S::b1) {   // this wave's reads of stage s done -> after B1 every wave's
+#ifdef GEMM_PROBE
+          G4P_TIME(pr.t0);
+#endif
           g4_sync_lds();
           if (DMA) g4_barrier();
+#ifdef GEMM_PROBE
+          G4P_FENCE(pr.t4); G4P_FENCE(pr.t5); G4P_FENCE(pr.t0);
+          pr.ew += pr.t5 - pr.t4;
+          pr.t4 = pr.t5 = 0;
+          G4P_TIME(pr.t1);
+#endif
         }
         if constexpr (DMA && g >= S::d0 && g < S::d0 + 16 * S::ds && (g - S::d0) % S::ds == 0)
           dma(t + 2, G4BFirst<S>::value ? (((g - S::d0) / S::ds) + 8) & 15 : (g - S::d0) / S::ds);
         if constexpr (NEXT && g == S::b2) {   // own DMA of tile t+1 landed (all but t+2's since)
+#ifdef GEMM_PROBE
+          unsigned long long t2, t3;
+          G4P_TIME(t2);
+#endif
           if (DMA) g4_vmcnt<S::vm>(); else g4_vmcnt<0>();
           g4_barrier();
+#ifdef GEMM_PROBE
+          G4P_TIME(t3);
+          g4_sync_lds();
+          G4P_FENCE(t2); G4P_FENCE(t3); G4P_FENCE(pr.t1);
+          pr.b2 += t3 - t2;
+          pr.b1 += pr.t1 - pr.t0;
+          pr.t0 = pr.t1 = 0;
+#endif
         }
         if constexpr (NEXT && g >= S::p0 && g < S::p0 + 16 * S::ps && (g - S::p0) % S::ps == 0)
           rd(P, (g - S::p0) / S::ps, 0, s ^ 1);
       });
+#ifdef GEMM_PROBE
+      if (NEXT) G4P_TIME(pr.t4);
+#endif
       if (NEXT) g4_sync_lds();
+#ifdef GEMM_PROBE
+      if (NEXT) G4P_TIME(pr.t5);
+      ++pr.kt;
+#endif
     };
     int t = 0;
     for (; t + 2 < T; ++t) ktile(t, G4B<true>{}, G4B<true>{});
@@ -511,6 +609,15 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
     // write (18+ for the 16-pass fp8 one); the fence takes every accumulator "+a" so no read is
     // hoisted above it
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+#ifdef GEMM_PROBE
+    {
+      unsigned long long e;
+      G4P_TIME(e);
+      g4_sync_lds();
+      G4P_FENCE(e); G4P_FENCE(pr.loop0);
+      pr.loop += e - pr.loop0;
+    }
+#endif
 #pragma unroll
     for (int i = 0; i < 8; ++i)
       asm volatile("" : "+a"(acc[i][0]), "+a"(acc[i][1]), "+a"(acc[i][2]), "+a"(acc[i][3]),
@@ -627,6 +734,12 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
     // (lgkmcnt(0) in the last k-tile), the barrier makes that hold for all of them
     g4_barrier();
   }
+#ifdef GEMM_PROBE
+  if (lane == 0) {
+    unsigned long long* q = g_probe + ((size_t)blockIdx.x * 4 + w) * 8;
+    q[0] = pr.b1; q[1] = pr.b2; q[2] = pr.ew; q[3] = pr.loop; q[4] = pr.kt;
+  }
+#endif
 #ifdef GEMM_STAMPS
   if (tid == 0) {
     st[2] = __builtin_amdgcn_s_memrealtime();
@@ -701,6 +814,10 @@ static int launch_gemm4_p(void* C, const void* a, const void* b, int M, int N, i
   } else {
     if (variant == kG4DecodeDefault)
       return launch_gemm4_v<kG4DecodeDefault, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
+    if (variant == 8)
+      return launch_gemm4_v<8, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
+    if (variant == 9)
+      return launch_gemm4_v<9, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
     if (variant != kG4Default) return -5;
     return launch_gemm4_v<kG4Default, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
   }

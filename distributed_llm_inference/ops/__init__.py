@@ -526,21 +526,23 @@ def _gemm4(x: torch.Tensor, w: torch.Tensor, splits: int, swiglu: bool,
     M, N = x.shape[0], w.shape[0]
     splits = max(1, int(splits))
     fp8 = xs is not None or x_mx is not None
+    # bf16 decode-size schedule from the policy; fp8 and larger M: the kernel's default
+    var = policy().gemm4_decode_sched if (not fp8 and M <= 512) else -1
     if splits > 1 and defer_reduce and not swiglu and policy().defer_splitk:
         bf = bf16_partials()
         parts = torch.empty(splits, M, N, dtype=torch.bfloat16 if bf else torch.float32,
                             device=x.device)
-        native().gemm4(parts, x, w, splits, 4 if bf else 1, 0, xs, ws, a_mx=x_mx)
+        native().gemm4(parts, x, w, splits, 4 if bf else 1, 0, xs, ws, var, a_mx=x_mx)
         return SplitKPartials(parts)
     if out is None:
         out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
     if splits == 1:
-        native().gemm4(out, x, w, 1, 2 if swiglu else 0, 0, xs, ws, a_mx=x_mx)
+        native().gemm4(out, x, w, 1, 2 if swiglu else 0, 0, xs, ws, var, a_mx=x_mx)
         return out
     if swiglu:
         raise ValueError("gemm4: fused SwiGLU takes whole-K tiles (splits = 1)")
     parts = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
-    native().gemm4(parts, x, w, splits, 1, 0, xs, ws, a_mx=x_mx)
+    native().gemm4(parts, x, w, splits, 1, 0, xs, ws, var, a_mx=x_mx)
     native().splitk_reduce(out, parts)
     return out
 

@@ -590,11 +590,13 @@ def test_gemm4_bit_identical_to_gemm_tile(gpu, M, N, K, splits, epi):
         ref = torch.empty(M, cols, device=gpu, dtype=torch.bfloat16)
         nat.gemm_tile(ref, a, b, 1, epi)
         out = torch.empty_like(ref)
-    for grid in (0, 7):   # automatic persistent grid, and a small grid that loops over tiles
+    # automatic persistent grid, and a small grid that loops over tiles; every decode-size
+    # schedule (NT weight streams 8 / 9 included) gives the same bits
+    for grid, var in ((0, -1), (7, -1), (0, 4), (0, 8), (0, 9)):
         out.fill_(7.0)
-        nat.gemm4(out, a, b, splits, epi, grid)
+        nat.gemm4(out, a, b, splits, epi, grid, None, None, var)
         torch.cuda.synchronize()
-        assert torch.equal(out, ref), (grid, (out.float() - ref.float()).abs().max().item())
+        assert torch.equal(out, ref), (grid, var, (out.float() - ref.float()).abs().max().item())
 
 
 def _q8(x):
