@@ -393,9 +393,10 @@ class KernelPolicy:
     # gate_up / down.  gate|up: 202 vs 219 us alone, +1.9 % tok/s in-step; the others win 2-7 %
     # alone but stay within noise in-step (profiles/r5/fp8_gemm4_16x16.md)
     fp8_gemm4: str = "gate_up"
-    # bf16 gemm4 k-loop schedule at decode M (<= 2 row tiles of 256): 6 (DMA spread thin), 4,
-    # or 9 / 8 = 6 / 4 with the weight stream non-temporal (csrc/kernels/gemm4.hip G4Sched)
-    gemm4_decode_sched: int = 6
+    # bf16 gemm4 k-loop schedule at decode M (<= 2 row tiles of 256): 8 / 9 = 4 / 6 with the
+    # weight stream non-temporal, or 4, 6 (csrc/kernels/gemm4.hip G4Sched; 8: +1.4 % tok/s over
+    # 6 in-step, profiles/r5/gemm4_sched_nt.md)
+    gemm4_decode_sched: int = 8
     # split-K partials of the deferred projections (QKV, O, down) stored as bf16 (else fp32);
     # consumers always sum in fp32 (profiles/bf16_partials_ab.txt, docs/parity.md C6)
     bf16_partials: bool = True

@@ -114,11 +114,12 @@ template <int V, typename = void> struct G4Nt { static constexpr bool value = fa
 template <int V> struct G4Nt<V, std::void_t<decltype(G4Sched<V>::nt)>> {
   static constexpr bool value = G4Sched<V>::nt;
 };
-// Default schedules (profiles/r4/gemm4_ab_v0-7.txt): decode-sized M (<= 2 row tiles, the
-// activations stay L2 / MALL-resident and only the weight stream misses) takes v6, whose DMA runs
-// the latest and thinnest (gate|up 377 vs 415 us gemm_tile, down 187 vs 199); larger M, where
-// both operands stream from HBM and a short DMA lead stalls (8192^3: v6 1074 us), takes v4.
-constexpr int kG4Default = 4, kG4DecodeDefault = 6;
+// Default schedules: decode-sized M (<= 2 row tiles, the activations stay L2 / MALL-resident and
+// only the weight stream misses) takes v8 = v4 with the weight stream non-temporal (round 5,
+// profiles/r5/gemm4_sched_nt.md: gate|up 400 vs 431 us for v6, down 191 vs 216, +1.4 % tok/s
+// in-step; round 4 had picked v6 over plain v4, profiles/r4/gemm4_ab_v0-7.txt); larger M, where
+// both operands stream from HBM and are re-read by many row tiles, takes v4 (8192^3: v6 1074 us).
+constexpr int kG4Default = 4, kG4DecodeDefault = 8;
 
 __device__ __forceinline__ float g4_silu(float x) { return x / (1.f + __expf(-x)); }
 

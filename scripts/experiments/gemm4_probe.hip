@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #define CK(x)                                                                  \
@@ -38,18 +39,21 @@ __global__ void fill_bytes(unsigned char* p, size_t n, unsigned seed, unsigned m
 struct Case { const char* name; int M, N, K, splits, epi, prec, var; };
 
 int main() {
-  std::vector<Case> cases = {
-      {"bf16 gate_up swiglu", 512, 57344, 8192, 1, 2, 0, 6},
-      {"bf16 gate_up swiglu", 512, 57344, 8192, 1, 2, 0, 4},
-      {"bf16 down s4 bf16p", 512, 8192, 28672, 4, 4, 0, 6},
-      {"bf16 qkv s3 bf16p", 512, 10240, 8192, 3, 4, 0, 6},
+  std::vector<Case> cases;
+  for (int v : {6, 4, 9, 8}) {   // bf16 decode schedules (8 / 9: 4 / 6 with NT weights)
+    cases.push_back({"bf16 gate_up swiglu", 512, 57344, 8192, 1, 2, 0, v});
+    cases.push_back({"bf16 down s4 bf16p", 512, 8192, 28672, 4, 4, 0, v});
+    cases.push_back({"bf16 qkv s3 bf16p", 512, 10240, 8192, 3, 4, 0, v});
+    cases.push_back({"bf16 o s4 bf16p", 512, 8192, 8192, 4, 4, 0, v});
+  }
+  if (getenv("PROBE_BF16_ONLY") == nullptr) for (Case c : std::vector<Case>{
       {"fp8 gate_up swiglu-mx", 512, 57344, 8192, 1, 3, 1, 0},
       {"fp8 gate_up swiglu-mx", 512, 57344, 8192, 1, 3, 1, 1},
       {"fp8 gate_up swiglu-mx", 512, 57344, 8192, 1, 3, 1, 2},
       {"fp8 down mx s4 bf16p", 512, 8192, 28672, 4, 4, 2, 0},
       {"fp8 down mx s4 bf16p", 512, 8192, 28672, 4, 4, 2, 2},
       {"fp8 qkv s3 bf16p", 512, 10240, 8192, 3, 4, 1, 0},
-  };
+  }) cases.push_back(c);
   unsigned long long* probe;
   const size_t pslots = (size_t)4096 * 4 * 8;
   CK(hipMalloc(&probe, pslots * 8));

@@ -566,7 +566,7 @@ def test_gemm_tile_defer_reduce_feeds_rms_norm(gpu, monkeypatch, bf16_parts):
         assert (b.float() - a.float()).abs().max().item() < 2e-2 * a.float().abs().max().item()
 
 
-@pytest.mark.parametrize("M", [512, 300, 40, 1100])   # <= 512: decode schedule v6; 1100: v4
+@pytest.mark.parametrize("M", [512, 300, 40, 1100])   # <= 512: decode schedule v8 (NT weights); 1100: v4
 @pytest.mark.parametrize("N,K,splits,epi", [(2048, 1024, 1, 0), (4096, 2048, 1, 2),
                                             (1024, 4096, 3, 1), (1024, 4096, 4, 4),
                                             (7680, 512, 1, 0)])
