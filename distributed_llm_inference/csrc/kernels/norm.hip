@@ -174,7 +174,11 @@ int launch_rms_norm(bf16* out, const bf16* x, const bf16* residual_in, bf16* res
   if (x_parts != nullptr && splits < 1) return -2;
   const int add = residual_in != nullptr ? 1 : 0;
   const size_t stride = (size_t)rows * hidden;
+#ifdef PROBE_NS1   // diagnostic (scripts/split_k_upper_bound.sh): read split 0 only
+  const int ns = x_parts != nullptr ? 1 : 0;
+#else
   const int ns = x_parts != nullptr ? splits : 0;
+#endif
   const int nvec = hidden / 8;
   const int threads = norm_threads(hidden);
   const int vpt = (nvec + threads - 1) / threads;

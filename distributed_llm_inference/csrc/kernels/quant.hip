@@ -225,7 +225,11 @@ int launch_quant_rowwise(uint8_t* q, float* scale, const bf16* x, const bf16* re
   const int nvec = K / 8;
   const int threads = row_threads(nvec);
   const int vpt = (nvec + threads - 1) / threads;
+#ifdef PROBE_NS1   // diagnostic (scripts/split_k_upper_bound.sh): read split 0 only
+  const int ns = x_parts != nullptr ? 1 : 0;
+#else
   const int ns = x_parts != nullptr ? splits : 0;
+#endif
 #define QUANT_LAUNCH(V, NS)                                                                     \
   do {                                                                                       \
     if (NS > 0 && parts_bf16)                                                                \

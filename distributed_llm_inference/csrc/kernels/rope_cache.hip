@@ -280,7 +280,11 @@ int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stre
   if (p.qkv_parts != nullptr && (p.splits < 1 || p.split_stride % 4 != 0)) return -2;
   const int heads = p.nh + 2 * p.nkv;
   dim3 grid(num_tokens, (heads + kHeadsPerWG - 1) / kHeadsPerWG);
+#ifdef PROBE_NS1   // diagnostic (scripts/split_k_upper_bound.sh): read split 0 only
+  const int ns = p.qkv_parts != nullptr ? 1 : 0;
+#else
   const int ns = p.qkv_parts != nullptr ? p.splits : 0;
+#endif
   // 16-byte path: both rotation halves and every head start on 16-byte boundaries of every
   // partial (otherwise the 4-element kernel)
   const bool v8 = p.D % 16 == 0 && p.qkv_stride % 8 == 0 &&

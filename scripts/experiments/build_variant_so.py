@@ -4,6 +4,7 @@ gpurun snapshot; ``build/`` does not); ``scripts/so_ab.sh`` swaps it over the in
 runs.
 
     python scripts/experiments/build_variant_so.py depth3 kernels/attention.hip -DATTN_FP8_DEPTH3
+    python scripts/experiments/build_variant_so.py ns1 norm.hip,rope_cache.hip,quant.hip -DPROBE_NS1
 
 Reuses the in-tree build's objects for every other source (build it first: ``__graft_entry__``).
 """
@@ -20,7 +21,8 @@ from distributed_llm_inference import _build as B  # noqa: E402
 
 
 def main() -> None:
-    name, src_rel, flags = sys.argv[1], sys.argv[2], sys.argv[3:]
+    name, flags = sys.argv[1], sys.argv[3:]
+    src_rels = sys.argv[2].split(",")
     B.build_kernels()
     hipcc = shutil.which("hipcc") or os.path.join(B.ROCM, "bin", "hipcc")
     tcflags, ldflags = B._torch_flags()
@@ -36,7 +38,7 @@ def main() -> None:
         fl = base + (tcflags if s in B.TORCH_SOURCES else [])
         key = hashlib.sha1(" ".join(fl).encode()).hexdigest()[:8]
         obj = os.path.join(B.BUILD_DIR, s.replace("/", "_") + f".{key}.o")
-        if s == src_rel or s.endswith("/" + src_rel):
+        if any(s == r or s.endswith("/" + r) for r in src_rels):
             obj = os.path.join(out_dir, os.path.basename(s) + ".o")
             subprocess.run(fl + flags + ["-c", path, "-o", obj], check=True)
         objs.append(obj)
