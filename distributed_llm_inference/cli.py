@@ -133,10 +133,11 @@ def cmd_block_serve(a) -> int:
         spec = resolve_model(a.checkpoint or a.model)
         registry = RegistryClient(a.registry, token=a.registry_token)
         url = a.public_url or f"http://{a.host}:{a.port}"
-        start, end = registry.claim(spec.name, spec.num_layers,
-                                    a.max_layers or spec.num_layers, url)
-        print(f"block-serve: registry {a.registry} assigned layers [{start}, {end}) to {url}",
-              file=sys.stderr, flush=True)
+        if start is None or end is None:
+            start, end = registry.claim(spec.name, spec.num_layers,
+                                        a.max_layers or spec.num_layers, url)
+            print(f"block-serve: registry {a.registry} assigned layers [{start}, {end}) to {url}",
+                  file=sys.stderr, flush=True)
     elif start is None or end is None:
         print("block-serve: give --start and --end, or --registry", file=sys.stderr)
         return 2
@@ -144,7 +145,9 @@ def cmd_block_serve(a) -> int:
                              device=a.device, random_init=a.checkpoint is None,
                              checkpoint=a.checkpoint, max_batch_size=a.max_batch_size,
                              window_length=a.window, num_sink_tokens=a.sinks, seed=a.seed)
-    serve_blocks(worker, a.host, a.port, registry=registry, url=url)
+    serve_blocks(worker, a.host, a.port, registry=registry, url=url,
+                 rebalance_s=a.rebalance_s if registry is not None else 0.0,
+                 max_layers=a.max_layers)
     return 0
 
 
@@ -287,13 +290,17 @@ def main(argv: Optional[List[str]] = None) -> int:
     bs.add_argument("--start", type=int, default=None, help="first layer (inclusive)")
     bs.add_argument("--end", type=int, default=None, help="last layer (exclusive)")
     bs.add_argument("--registry", default=None,
-                    help="block registry URL: claim the least-served layers instead of --start/--end")
+                    help="block registry URL: claim the least-served layers (or announce "
+                         "--start/--end when given)")
     bs.add_argument("--max-layers", type=int, default=None,
                     help="with --registry: most layers this server holds (default: all)")
     bs.add_argument("--registry-token", default=None,
                     help="shared secret of a registry started with --token")
     bs.add_argument("--public-url", default=None,
                     help="with --registry: URL clients reach this server at (default http://host:port)")
+    bs.add_argument("--rebalance-s", type=float, default=0.0,
+                    help="with --registry: every this many seconds, move to less-served layers "
+                         "when that raises the swarm's least-served coverage (0 = never)")
     bs.add_argument("--layers-per-block", type=int, default=None)
     bs.add_argument("--seed", type=int, default=0)
     bs.add_argument("--device", default=None, help="cuda:N / cpu (default: cuda:0 if present)")

@@ -80,11 +80,25 @@ class HopFailure(RuntimeError):
     HTTP 5xx): the hop is replaceable.  Client errors (4xx) are plain RuntimeErrors."""
 
 
-def build_block_app(worker):
+class HopMoved(HopFailure):
+    """The server now serves other layers (swarm rebalancing): re-resolve its old range."""
+
+
+def build_block_app(worker, rebalance=None):
+    """The block server's HTTP service; ``rebalance``: a callable running one rebalancing round
+    (:func:`rebalance_once`) behind POST /rebalance, for operators and tests."""
     from fastapi import FastAPI, HTTPException
     from fastapi.responses import JSONResponse, Response
 
     app = FastAPI(title="distributed_llm_inference block server")
+
+    @app.post("/rebalance")
+    async def rebalance_now():
+        import asyncio
+        if rebalance is None:
+            raise HTTPException(404, "this server has no registry to rebalance against")
+        moved = await asyncio.get_running_loop().run_in_executor(None, rebalance)
+        return {"moved": moved is not None, "start": worker.start, "end": worker.end}
 
     @app.get("/info")
     async def info():
@@ -108,6 +122,11 @@ def build_block_app(worker):
         if x.dim() != 3 or x.shape[-1] != worker.spec.hidden_size:
             raise HTTPException(400, f"hidden must be [B, T, {worker.spec.hidden_size}], "
                                      f"got {list(x.shape)}")
+        want = body.get("expect_range")
+        if want is not None and (int(want[0]), int(want[1])) != (worker.start, worker.end):
+            # the client's chain predates a move of this server (rebalancing): 409, it re-resolves
+            raise HTTPException(409, f"moved: serving [{worker.start}, {worker.end}), "
+                                     f"not [{want[0]}, {want[1]})")
         bid = body.get("block_id")
         if bid is not None and bid not in worker.blocks:
             raise HTTPException(404, f"unknown block {bid!r}")
@@ -129,6 +148,8 @@ def build_block_app(worker):
             out = await asyncio.get_running_loop().run_in_executor(None, run)
         except (ValueError, MemoryError) as e:   # a bad request / no KV room: the client's call
             raise HTTPException(422, f"{type(e).__name__}: {e}")
+        except KeyError as e:   # the worker moved while this request walked its blocks
+            raise HTTPException(409, f"moved: {e!r}")
         return Response(msgpack.packb(out), media_type="application/msgpack")
 
     @app.post("/close_session")
@@ -140,10 +161,57 @@ def build_block_app(worker):
     return app
 
 
+def rebalance_once(worker, registry, url: str, max_layers: int, moving) -> Optional[Tuple[int, int]]:
+    """One rebalancing round: if the worker holds no sessions and the registry says moving to
+    less-served layers helps the swarm (registry.rebalance_target, recorded there as this
+    server's claim), load them, swap them in (InferenceWorker.move_to) and announce the new
+    range.  ``moving`` pauses the heartbeat meanwhile, so it never re-announces the old range
+    over the new claim.  Returns the new range, or None."""
+    if worker.sessions():
+        return None   # a move would drop their KV: wait until the server is idle
+    target = registry.rebalance(worker.spec.name, url, worker.spec.num_layers, max_layers)
+    if target is None:
+        return None
+    moving.set()
+    try:
+        old = (worker.start, worker.end)
+        try:
+            worker.move_to(*target)
+        except Exception:   # noqa: BLE001 - e.g. no memory for the new layers: stay
+            log.exception("move [%d, %d) -> %s failed; staying", old[0], old[1], target)
+        registry.announce(worker.spec.name, url, worker.start, worker.end,
+                          worker.spec.num_layers)
+        log.warning("rebalanced: layers [%d, %d) -> [%d, %d)", old[0], old[1], worker.start,
+                    worker.end)
+        return (worker.start, worker.end) if (worker.start, worker.end) != old else None
+    finally:
+        moving.clear()
+
+
+def rebalance_loop(worker, registry, url: str, max_layers: int, period_s: float,
+                   stop, moving) -> "threading.Thread":
+    """:func:`rebalance_once` every ``period_s`` until ``stop``."""
+    import threading
+
+    def run():
+        while not stop.wait(period_s):
+            try:
+                rebalance_once(worker, registry, url, max_layers, moving)
+            except Exception:   # noqa: BLE001 - the registry may be restarting; keep trying
+                log.debug("rebalance round failed", exc_info=True)
+
+    th = threading.Thread(target=run, name="block-rebalance", daemon=True)
+    th.start()
+    return th
+
+
 def serve_blocks(worker, host: str = "127.0.0.1", port: int = 8100, registry=None,
-                 url: Optional[str] = None, ttl: float = 30.0) -> None:
+                 url: Optional[str] = None, ttl: float = 30.0, rebalance_s: float = 0.0,
+                 max_layers: Optional[int] = None) -> None:
     """Serve ``worker`` over HTTP.  With ``registry`` (a :class:`RegistryClient`) the server is
-    announced under ``url`` while its /health answers, and withdrawn when it stops."""
+    announced under ``url`` while its /health answers, and withdrawn when it stops;
+    ``rebalance_s`` > 0: every that many seconds it may move to less-served layers
+    (:func:`rebalance_loop`, at most ``max_layers`` of them)."""
     import uvicorn
     worker.run()
     stop = None
@@ -153,10 +221,18 @@ def serve_blocks(worker, host: str = "127.0.0.1", port: int = 8100, registry=Non
         url = url or f"http://{host}:{port}"
         probe = RemoteBlocks(url, timeout=5.0)
         stop = threading.Event()
+        moving = threading.Event()
         heartbeat_loop(registry, worker.spec.name, url, worker.start, worker.end,
-                       worker.spec.num_layers, probe.healthy, ttl=ttl, stop=stop)
+                       worker.spec.num_layers, probe.healthy, ttl=ttl, stop=stop,
+                       current_range=lambda: None if moving.is_set() else (worker.start,
+                                                                             worker.end))
+        span = max_layers or (worker.end - worker.start)
+        rebalance = lambda: rebalance_once(worker, registry, url, span, moving)  # noqa: E731
+        if rebalance_s > 0:
+            rebalance_loop(worker, registry, url, span, rebalance_s, stop, moving)
     try:
-        uvicorn.run(build_block_app(worker), host=host, port=port, log_level="warning")
+        uvicorn.run(build_block_app(worker, rebalance if registry is not None else None),
+                    host=host, port=port, log_level="warning")
     finally:
         if registry is not None:
             stop.set()
@@ -224,6 +300,7 @@ class RemoteBlocks:
             body["position_ids"] = pack_tensor(position_ids)
         if output_hidden_states:
             body["output_hidden_states"] = True
+        body["expect_range"] = list(self.range)   # a moved server answers 409
         try:
             r = self._s.post(self.url + "/forward", data=msgpack.packb(body),
                              headers={"Content-Type": "application/msgpack"},
@@ -232,6 +309,8 @@ class RemoteBlocks:
             raise HopFailure(f"{self.url}/forward: {e!r}") from e
         if r.status_code >= 500:
             raise HopFailure(f"{self.url}/forward: HTTP {r.status_code}: {r.text[:300]}")
+        if r.status_code == 409:
+            raise HopMoved(f"{self.url}/forward: {r.text[:300]}")
         if r.status_code != 200:
             raise RuntimeError(f"{self.url}/forward: HTTP {r.status_code}: {r.text[:500]}")
         d = msgpack.unpackb(r.content)
@@ -342,7 +421,8 @@ class RemoteSequential:
         replacement can be found."""
         failed = self.servers[i]
         a, b = failed.range
-        self.dead.add(failed.url)
+        if not isinstance(err, HopMoved):   # a moved server is alive, just elsewhere now
+            self.dead.add(failed.url)
         log.warning("block server %s (layers [%d, %d)) failed: %s; re-resolving", failed.url, a,
                     b, err)
         last_err: Exception = err

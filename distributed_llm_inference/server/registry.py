@@ -11,12 +11,18 @@ serves (/root/reference/distributed_llm_inference/server/server.py:7-8), through
                     (sent again every ttl / 3 as a heartbeat; an entry that misses its ttl is
                     dropped, a claim that never turns ready after ``claim_ttl`` too)
     POST /withdraw  {"url"}
+    POST /rebalance {"model", "url", "num_layers", "max_layers"} -> {"move", "start", "end"}
+                    should this server move to less-served layers (``rebalance_target``)? A move
+                    is recorded at once as the server's new claim, so servers rebalancing
+                    together never pile onto the same gap
     GET  /servers?model=M   [{"url", "start", "end", "num_layers", "ready"}]
 
 ``distribute registry`` runs it; ``distribute block-serve --registry URL --max-layers N`` claims
 a range instead of taking ``--start/--end``, and ``RemoteSequential.from_registry(URL, model)``
 builds the client's chain from the registry alone - and re-resolves a failed hop from it
-(server/block_server.py failover).
+(server/block_server.py failover).  ``block-serve --rebalance-s T`` asks /rebalance every T
+seconds while it holds no sessions and moves when the swarm gains from it (the reference's
+``should_rebalance`` intent, server/server.py:20).
 
 Trust: the mutating endpoints (/claim, /announce, /withdraw) take a shared token when the
 registry is started with one (``distribute registry --token T``; servers pass the same
@@ -28,12 +34,20 @@ from __future__ import annotations
 
 import threading
 import time
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 try:   # module level: FastAPI resolves the (string) annotations of the handlers here
     from fastapi import Request
 except ImportError:  # pragma: no cover - clients need no web framework
     Request = None
+
+
+def _coverage(num_layers: int, served: Sequence[Tuple[int, int]]) -> List[int]:
+    cov = [0] * num_layers
+    for s, e in served:
+        for i in range(max(0, s), min(num_layers, e)):
+            cov[i] += 1
+    return cov
 
 
 def choose_range(num_layers: int, max_layers: int,
@@ -47,10 +61,7 @@ def choose_range(num_layers: int, max_layers: int,
     if num_layers <= 0 or max_layers <= 0:
         raise ValueError("num_layers and max_layers must be positive")
     span = min(max_layers, num_layers)
-    cov = [0] * num_layers
-    for s, e in served:
-        for i in range(max(0, s), min(num_layers, e)):
-            cov[i] += 1
+    cov = _coverage(num_layers, served)
     if 0 in cov:
         s = cov.index(0)
         e = s
@@ -60,6 +71,31 @@ def choose_range(num_layers: int, max_layers: int,
     best = min(range(num_layers - span + 1),
                key=lambda s: (max(cov[s:s + span]), sum(cov[s:s + span]), s))
     return best, best + span
+
+
+def swarm_score(num_layers: int, served: Sequence[Tuple[int, int]]) -> Tuple[int, int]:
+    """How well ``served`` covers the model: every chain passes through every layer, so the
+    swarm's throughput is bounded by its least-served layer -- (that coverage, minus the number
+    of layers at it); larger is better."""
+    cov = _coverage(num_layers, served)
+    lo = min(cov)
+    return lo, -cov.count(lo)
+
+
+def rebalance_target(num_layers: int, max_layers: int, others: Sequence[Tuple[int, int]],
+                     mine: Tuple[int, int]) -> Optional[Tuple[int, int]]:
+    """Where a server now serving ``mine`` should move, given the ranges ``others`` the rest of
+    the swarm serves, or None to stay: the window of ``max_layers`` layers (or
+    :func:`choose_range`'s pick) with the best :func:`swarm_score`, taken only when it strictly
+    beats staying (a move costs a reload and drops sessions); the lowest start breaks ties."""
+    span = min(max_layers, num_layers)
+    cands = {(s, s + span) for s in range(num_layers - span + 1)}
+    cands.add(tuple(choose_range(num_layers, span, others)))
+    here = swarm_score(num_layers, list(others) + [tuple(mine)])
+    best = max(sorted(cands), key=lambda c: (swarm_score(num_layers, list(others) + [c]), -c[0]))
+    if tuple(best) != tuple(mine) and swarm_score(num_layers, list(others) + [best]) > here:
+        return best
+    return None
 
 
 def find_chain(entries: Sequence[dict], num_layers: int, start: int = 0) -> List[dict]:
@@ -130,6 +166,24 @@ class Registry:
         with self._lock:
             self._entries.pop(url, None)
 
+    def rebalance(self, model: str, url: str, num_layers: int,
+                  max_layers: int) -> Optional[Tuple[int, int]]:
+        """The range the ready server ``url`` should move to (recorded as its claim), or None."""
+        with self._lock:
+            now = time.monotonic()
+            self._expire(now)
+            me = self._entries.get(url)
+            if me is None or not me["ready"] or me["model"] != model:
+                return None
+            others = [(e["start"], e["end"]) for u, e in self._entries.items()
+                      if u != url and e["model"] == model]
+            target = rebalance_target(num_layers, max_layers, others, (me["start"], me["end"]))
+            if target is not None:
+                self._entries[url] = {"url": url, "model": model, "start": target[0],
+                                      "end": target[1], "num_layers": num_layers, "ready": False,
+                                      "expires": now + self.claim_ttl}
+            return target
+
     def servers(self, model: Optional[str] = None) -> List[dict]:
         with self._lock:
             self._expire(time.monotonic())
@@ -183,6 +237,16 @@ def build_registry_app(reg: Optional[Registry] = None, token: Optional[str] = No
             raise HTTPException(400, f"bad withdraw: {ex!r}")
         return {"ok": True}
 
+    @app.post("/rebalance")
+    async def rebalance(body: dict, request: Request):
+        _auth(request)
+        try:
+            t = reg.rebalance(str(body["model"]), str(body["url"]), int(body["num_layers"]),
+                              int(body["max_layers"]))
+        except (KeyError, ValueError, TypeError) as ex:
+            raise HTTPException(400, f"bad rebalance: {ex!r}")
+        return {"move": t is not None, "start": t[0] if t else None, "end": t[1] if t else None}
+
     @app.get("/servers")
     async def servers(model: Optional[str] = None):
         return reg.servers(model)
@@ -223,6 +287,12 @@ class RegistryClient:
     def withdraw(self, url: str) -> None:
         self._post("/withdraw", {"url": url})
 
+    def rebalance(self, model: str, url: str, num_layers: int,
+                  max_layers: int) -> Optional[Tuple[int, int]]:
+        d = self._post("/rebalance", {"model": model, "url": url, "num_layers": num_layers,
+                                      "max_layers": max_layers})
+        return (int(d["start"]), int(d["end"])) if d["move"] else None
+
     def servers(self, model: Optional[str] = None, ready_only: bool = True) -> List[dict]:
         r = self._s.get(self.url + "/servers", params={"model": model} if model else None,
                         timeout=self.timeout)
@@ -232,15 +302,20 @@ class RegistryClient:
 
 def heartbeat_loop(client: RegistryClient, model: str, url: str, start: int, end: int,
                    num_layers: int, healthy, ttl: float = 30.0,
-                   stop: Optional[threading.Event] = None) -> threading.Thread:
-    """Background thread: announce this server while ``healthy()`` holds, every ttl / 3."""
+                   stop: Optional[threading.Event] = None,
+                   current_range: Optional[Callable[[], Optional[Tuple[int, int]]]] = None
+                   ) -> threading.Thread:
+    """Background thread: announce this server while ``healthy()`` holds, every ttl / 3.
+    ``current_range``: the range to announce, read at every beat (None: skip the beat -- the
+    server is moving and its new claim must not be overwritten)."""
     stop = stop or threading.Event()
 
     def run():
         while not stop.is_set():
             try:
-                if healthy():
-                    client.announce(model, url, start, end, num_layers, ttl)
+                rng = current_range() if current_range is not None else (start, end)
+                if rng is not None and healthy():
+                    client.announce(model, url, rng[0], rng[1], num_layers, ttl)
             except Exception:  # noqa: BLE001 - the registry may be restarting; keep trying
                 pass
             stop.wait(ttl / 3)
