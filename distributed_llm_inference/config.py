@@ -394,10 +394,9 @@ class KernelPolicy:
     # alone but stay within noise in-step (profiles/r5/fp8_gemm4_16x16.md)
     fp8_gemm4: str = "gate_up"
     # bf16 gemm4 k-loop schedule at decode M (<= 2 row tiles of 256): 8 / 9 = 4 / 6 with the
-    # weight stream non-temporal, or 4, 6 (csrc/kernels/gemm4.hip G4Sched).  -1 = by M: 8 for two
-    # row tiles (+1.4 % tok/s over 6 at 512 rows), 6 for one (-0.5 % for 8 at 16 rows, 8k
-    # context; profiles/r5/gemm4_sched_nt.md)
-    gemm4_decode_sched: int = -1
+    # weight stream non-temporal, or 4, 6 (csrc/kernels/gemm4.hip G4Sched; 8: +1.4 % tok/s over
+    # 6 in-step, profiles/r5/gemm4_sched_nt.md)
+    gemm4_decode_sched: int = 8
     # split-K partials of the deferred projections (QKV, O, down) stored as bf16 (else fp32);
     # consumers always sum in fp32 (profiles/bf16_partials_ab.txt, docs/parity.md C6)
     bf16_partials: bool = True
@@ -427,8 +426,8 @@ class KernelPolicy:
     _FP8_SHAPES = ("qkv", "o", "gate_up", "down")
 
     def __post_init__(self):
-        if self.gemm4_decode_sched not in (-1, 4, 6, 8, 9):
-            raise ValueError(f"gemm4_decode_sched={self.gemm4_decode_sched}: -1, 4, 6, 8 or 9")
+        if self.gemm4_decode_sched not in (4, 6, 8, 9):
+            raise ValueError(f"gemm4_decode_sched={self.gemm4_decode_sched}: 4, 6, 8 or 9")
         sel = self.fp8_gemm4
         if sel not in ("all", "none") and any(
                 x not in self._FP8_SHAPES for x in sel.split("+")):

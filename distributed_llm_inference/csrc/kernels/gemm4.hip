@@ -114,9 +114,8 @@ template <int V, typename = void> struct G4Nt { static constexpr bool value = fa
 template <int V> struct G4Nt<V, std::void_t<decltype(G4Sched<V>::nt)>> {
   static constexpr bool value = G4Sched<V>::nt;
 };
-// Default schedules: decode-sized M (2 row tiles, the activations stay L2 / MALL-resident and
-// only the weight stream misses; one row tile takes v6) takes v8 = v4 with the weight stream
-// non-temporal (round 5,
+// Default schedules: decode-sized M (<= 2 row tiles, the activations stay L2 / MALL-resident and
+// only the weight stream misses) takes v8 = v4 with the weight stream non-temporal (round 5,
 // profiles/r5/gemm4_sched_nt.md: gate|up 400 vs 431 us for v6, down 191 vs 216, +1.4 % tok/s
 // in-step; round 4 had picked v6 over plain v4, profiles/r4/gemm4_ab_v0-7.txt); larger M, where
 // both operands stream from HBM and are re-read by many row tiles, takes v4 (8192^3: v6 1074 us).
@@ -814,8 +813,8 @@ static int launch_gemm4_p(void* C, const void* a, const void* b, int M, int N, i
     if (variant != kG8Default) return -5;
     return launch_gemm4_v<kG8Default, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
   } else {
-    if (variant == kG4DecodeDefault)
-      return launch_gemm4_v<kG4DecodeDefault, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
+    if (variant == 6)
+      return launch_gemm4_v<6, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
     if (variant == 8)
       return launch_gemm4_v<8, PREC>(C, a, b, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid, stream, sa, sb, mx);
     if (variant == 9)
@@ -854,10 +853,7 @@ int launch_gemm4(void* C, const void* A, const void* B, int M, int N, int K, int
   if (grid <= 0) grid = gemm4_grid(items, g4_cus());
   if (grid > items) grid = items;
   if (variant < 0)
-    variant = precision >= 1 ? kG8Default
-              : tiles_m == 2  ? kG4DecodeDefault
-              : tiles_m == 1  ? 6   // one row tile: v6 (NT measured -0.5 % at 16 rows)
-                              : kG4Default;
+    variant = precision >= 1 ? kG8Default : tiles_m <= 2 ? kG4DecodeDefault : kG4Default;
   const G4Mx mx{a_mx, out_mx, (M + 63) / 64};
   if (precision == 2)
     return launch_gemm4_p<2>(C, A, B, M, N, K, tiles_m, tiles_n, kps, splits, epilogue, grid,

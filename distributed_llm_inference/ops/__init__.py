@@ -526,13 +526,8 @@ def _gemm4(x: torch.Tensor, w: torch.Tensor, splits: int, swiglu: bool,
     M, N = x.shape[0], w.shape[0]
     splits = max(1, int(splits))
     fp8 = xs is not None or x_mx is not None
-    # bf16 decode-size schedule from the policy (-1: 8 for two row tiles, 6 for one); fp8 and
-    # larger M: the kernel's default
-    var = -1
-    if not fp8 and M <= 512:
-        var = policy().gemm4_decode_sched
-        if var < 0:
-            var = 8 if M > 256 else 6
+    # bf16 decode-size schedule from the policy; fp8 and larger M: the kernel's default
+    var = policy().gemm4_decode_sched if (not fp8 and M <= 512) else -1
     if splits > 1 and defer_reduce and not swiglu and policy().defer_splitk:
         bf = bf16_partials()
         parts = torch.empty(splits, M, N, dtype=torch.bfloat16 if bf else torch.float32,

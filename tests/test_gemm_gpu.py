@@ -592,7 +592,7 @@ def test_gemm4_bit_identical_to_gemm_tile(gpu, M, N, K, splits, epi):
         out = torch.empty_like(ref)
     # automatic persistent grid, and a small grid that loops over tiles; every decode-size
     # schedule (NT weight streams 8 / 9 included) gives the same bits
-    for grid, var in ((0, -1), (7, -1), (0, 4), (0, 8), (0, 9)):
+    for grid, var in ((0, -1), (7, -1), (0, 4), (0, 6), (0, 8), (0, 9)):
         out.fill_(7.0)
         nat.gemm4(out, a, b, splits, epi, grid, None, None, var)
         torch.cuda.synchronize()
