@@ -498,7 +498,10 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
     bf16x8 P[16], Q[16];
     // read fragment n of k-step kk of stage s: n < 8 weight rows wc*128 + 16n, else activation
     // rows wr*128 + 16(n-8)
-    auto rd = [&](bf16x8 (&F)[16], int n, int kk, int s) {
+    auto rd = [&](bf16x8 (&F)[16], int n, int kk, int s, bool in_loop = true) {
+#ifdef GEMM_PROBE_NOBREAD
+      if (n < 8 && in_loop) return;   // diagnostic: no weight-fragment LDS reads in the loop
+#endif
       switch (n) {
         case 0: g4_read<0 * 2048>(F[0], rdB[kk][s]); break;
         case 1: g4_read<1 * 2048>(F[1], rdB[kk][s]); break;
@@ -535,7 +538,11 @@ gemm4_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, void* __r
     }
     g4_barrier();
 #pragma unroll
-    for (int n = 0; n < 16; ++n) rd(P, n, 0, 0);
+    for (int n = 0; n < 16; ++n) rd(P, n, 0, 0, false);
+#ifdef GEMM_PROBE_NOBREAD
+#pragma unroll
+    for (int n = 0; n < 8; ++n) rd(Q, n, 1, 0, false);   // real (random) weight values throughout
+#endif
     g4_sync_lds();
 
     // one k-tile.  DMA: issue tile t+2 into stage t&1; NEXT: read k-step 0 of tile t+1
