@@ -70,7 +70,10 @@ __device__ __forceinline__ bf16 load_qkv1(const RopeCacheParams& p, const bf16* 
 // grid (T, ceil(total_heads / kHeadsPerWG)): one workgroup per (token, group of 8 heads) so a
 // decode step of B tokens launches B * 10 workgroups (70B) instead of B — the kernel is
 // latency-bound, not bandwidth-bound, at one workgroup per token.
-constexpr int kHeadsPerWG = 8;
+#ifndef ROPE_HPW
+#define ROPE_HPW 8
+#endif
+constexpr int kHeadsPerWG = ROPE_HPW;
 
 template <bool FP8, int NS>
 __global__ void __launch_bounds__(128) rope_cache_kernel(RopeCacheParams p) {
