@@ -569,7 +569,10 @@ def test_gemm_tile_defer_reduce_feeds_rms_norm(gpu, monkeypatch, bf16_parts):
 @pytest.mark.parametrize("M", [512, 300, 40, 1100])   # <= 512: decode schedule v8 (NT weights); 1100: v4
 @pytest.mark.parametrize("N,K,splits,epi", [(2048, 1024, 1, 0), (4096, 2048, 1, 2),
                                             (1024, 4096, 3, 1), (1024, 4096, 4, 4),
-                                            (7680, 512, 1, 0)])
+                                            (7680, 512, 1, 0),
+                                            # 1-3 k-tiles per split: every tail of the k-loop
+                                            (256, 64, 1, 0), (512, 128, 1, 2), (256, 192, 1, 0),
+                                            (768, 320, 2, 1)])
 def test_gemm4_bit_identical_to_gemm_tile(gpu, M, N, K, splits, epi):
     """gemm4.hip (one wave per SIMD, asm-ordered k-loop) runs the same MFMA over the same k order
     as gemm_tile: bf16 store, SwiGLU and fp32 / bf16 split-K partials must match it bit for bit,
@@ -607,7 +610,10 @@ def _q8(x):
 @pytest.mark.parametrize("M", [512, 300, 40])
 @pytest.mark.parametrize("N,K,splits,epi", [(2048, 1024, 1, 0), (4096, 2048, 1, 2),
                                             (1024, 4096, 3, 1), (1024, 4096, 4, 4),
-                                            (7680, 512, 1, 0)])
+                                            (7680, 512, 1, 0),
+                                            # 1-3 k-tiles per split: every tail of the k-loop
+                                            (256, 128, 1, 0), (512, 256, 1, 2), (256, 384, 1, 0),
+                                            (768, 640, 2, 1)])
 def test_gemm4_fp8_bit_identical_to_gemm_tile_fp8(gpu, M, N, K, splits, epi):
     """fp8 gemm4 (block-scaled 16x16x128 MFMA with gemm_tile's fragment pairing, unit block scales,
     per-row x per-channel scales in the epilogue) against gemm_tile's fp8 path on the same
