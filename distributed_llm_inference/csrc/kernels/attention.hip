@@ -46,8 +46,20 @@ namespace dli {
 //     28.1 vs 15.0 us, one workgroup merging up to 32 partials serially - and lives in
 //     scripts/experiments/.)
 // ===========================================================================================
+// bf16 full-cache single-split decode (the large-batch case) walks one key step per wave at 4
+// waves per SIMD (attn_core.h ONE_STEP); the others keep two (fp8: three raw) steps in flight
+template <bool WIN, bool FP8, bool GRP>
+constexpr bool decode_one_step() {
+#ifdef ATTN_DECODE_TWO_STEP   // experiment builds: the round-4 loop everywhere
+  return false;
+#else
+  return !WIN && !FP8 && !GRP;
+#endif
+}
+
 template <int D, bool WIN, bool FP8, bool GRP>
-__global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int items, int gs) {
+__global__ void __launch_bounds__(256, (decode_one_step<WIN, FP8, GRP>() ? 4 : 1))
+attn_decode_kernel(AttnParams p, int items, int gs) {
   // GRP (num_splits > 1): the `gs` consecutive splits of one work item that share this
   // workgroup are merged in LDS, so only num_splits / gs partials per head reach global memory
   // (none when gs == num_splits: the workgroup writes the normalised output itself)
@@ -62,7 +74,8 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnParams p, int item
   // of the K/V prefetch
   const int item = __builtin_amdgcn_readfirstlane(live ? item_raw : items - 1);
   WaveState<D> st;
-  const DecodeItem di = attn_decode_item<D, WIN, FP8, false>(p, item, live, st);
+  const DecodeItem di =
+      attn_decode_item<D, WIN, FP8, false, decode_one_step<WIN, FP8, GRP>()>(p, item, live, st);
   const int splits = p.num_splits, split = di.split, G = di.G, hgroups = di.hgroups;
   const int g0 = di.g0, kvh = di.kvh, b = di.b;
   const int lane = threadIdx.x & 63, col = lane & 15, h4 = lane >> 4;

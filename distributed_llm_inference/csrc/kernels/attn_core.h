@@ -306,7 +306,7 @@ struct DecodeItem {
   float vsc;   // fp8 caches: V's scale, applied to the output
 };
 
-template <int D, bool WIN, bool FP8, bool NT>
+template <int D, bool WIN, bool FP8, bool NT, bool ONE_STEP = false>
 __device__ __forceinline__ DecodeItem attn_decode_item(const AttnParams& p, int item, bool live,
                                                        WaveState<D>& st) {
   const int splits = p.num_splits;
@@ -388,6 +388,18 @@ __device__ __forceinline__ DecodeItem attn_decode_item(const AttnParams& p, int 
           if (sidx + 2 < s_hi) step(r2, sidx + 2);
         }
       } else {
+      if constexpr (ONE_STEP) {
+        // one step per wave in flight and 4 waves per SIMD (96 VGPRs; attn_decode_kernel's
+        // launch bounds) instead of two steps at 2 waves: the same bytes in flight per SIMD,
+        // twice the waves to hide latency, and B = 512 x 8 kv heads = 4096 waves in ONE round
+        // (profiles/r5/attn_one_step.md: 600 keys 213.6 vs 220.7 us, 1100 keys 397 vs 405)
+        for (int sidx = s_lo; sidx < s_hi; ++sidx) {
+          KVFrag<D> f;
+          load(f, sidx);
+          attn_compute<D>(st, qf, f, sl2,
+                          step_mask<D, WIN>(seg_base + sidx * 32, h4, seg_base, seg_len, L, p));
+        }
+      } else {
       KVFrag<D> fa, fb;
       load(fa, s_lo);
       // sched_barrier(0): keep each prefetch group issued ahead of the previous step's MFMAs
@@ -402,6 +414,7 @@ __device__ __forceinline__ DecodeItem attn_decode_item(const AttnParams& p, int 
         if (sidx + 1 < s_hi)
           attn_compute<D>(st, qf, fb, sl2,
                           step_mask<D, WIN>(seg_base + (sidx + 1) * 32, h4, seg_base, seg_len, L, p));
+      }
       }
       }
     }
