@@ -46,14 +46,17 @@ namespace dli {
 //     28.1 vs 15.0 us, one workgroup merging up to 32 partials serially - and lives in
 //     scripts/experiments/.)
 // ===========================================================================================
-// bf16 full-cache single-split decode (the large-batch case) walks one key step per wave at 4
-// waves per SIMD (attn_core.h ONE_STEP); the others keep two (fp8: three raw) steps in flight
+// full-cache single-split decode (the large-batch case), bf16 or fp8 KV, walks one key step
+// per wave at 4 waves per SIMD (attn_core.h ONE_STEP: 96 / 104 VGPRs); the window and split
+// kernels keep two (fp8: three raw) steps in flight at 2 waves
 template <bool WIN, bool FP8, bool GRP>
 constexpr bool decode_one_step() {
-#ifdef ATTN_DECODE_TWO_STEP   // experiment builds: the round-4 loop everywhere
+#if defined(ATTN_DECODE_TWO_STEP)     // experiment builds: the round-4 loops everywhere
   return false;
-#else
+#elif defined(ATTN_FP8_THREE_STEP)    // experiment builds: the round-4 fp8-KV loop
   return !WIN && !FP8 && !GRP;
+#else
+  return !WIN && !GRP;
 #endif
 }
 

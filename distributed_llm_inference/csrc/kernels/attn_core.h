@@ -373,6 +373,13 @@ __device__ __forceinline__ DecodeItem attn_decode_item(const AttnParams& p, int 
           attn_compute<D>(st, qf, f, sl2,
                           step_mask<D, WIN>(seg_base + sidx * 32, h4, seg_base, seg_len, L, p));
         };
+        if constexpr (ONE_STEP) {   // one raw step per wave at 4 waves per SIMD (see below)
+          for (int sidx = s_lo; sidx < s_hi; ++sidx) {
+            KVRaw<D> r;
+            rload(r, sidx);
+            step(r, sidx);
+          }
+        } else {
         KVRaw<D> r0, r1, r2;
         rload(r0, s_lo);
         rload(r1, min(s_lo + 1, s_hi - 1));
@@ -386,6 +393,7 @@ __device__ __forceinline__ DecodeItem attn_decode_item(const AttnParams& p, int 
           rload(r1, min(sidx + 4, s_hi - 1));
           __builtin_amdgcn_sched_barrier(0);
           if (sidx + 2 < s_hi) step(r2, sidx + 2);
+        }
         }
       } else {
       if constexpr (ONE_STEP) {
