@@ -46,22 +46,14 @@ namespace dli {
 //     28.1 vs 15.0 us, one workgroup merging up to 32 partials serially - and lives in
 //     scripts/experiments/.)
 // ===========================================================================================
-// full-cache single-split decode (the large-batch case), bf16 or fp8 KV, walks one key step
-// per wave at 4 waves per SIMD (attn_core.h ONE_STEP: 96 / 104 VGPRs); the window and split
-// kernels keep two (fp8: three raw) steps in flight at 2 waves
-template <bool WIN, bool FP8, bool GRP>
-constexpr bool decode_one_step() {
-#if defined(ATTN_DECODE_TWO_STEP)     // experiment builds: the round-4 loops everywhere
-  return false;
-#elif defined(ATTN_FP8_THREE_STEP)    // experiment builds: the round-4 fp8-KV loop
-  return !WIN && !FP8 && !GRP;
-#else
-  return !WIN && !GRP;
-#endif
-}
-
-template <int D, bool WIN, bool FP8, bool GRP>
-__global__ void __launch_bounds__(256, (decode_one_step<WIN, FP8, GRP>() ? 4 : 1))
+// ONE (full-cache single-split decode of a batch large enough to fill the chip, bf16 or fp8
+// KV): one key step per wave in flight at 4 waves per SIMD (attn_core.h ONE_STEP, 96 / 104
+// VGPRs) instead of two (fp8: three raw) steps at 2 waves -- the same bytes in flight per SIMD,
+// twice the waves, and B = 512 x 8 kv heads = 4096 waves in ONE round.  With fewer waves than
+// the chip holds at 4 per SIMD the deeper prefetch wins (fp8 KV at 1024 waves: 148 vs 99 us),
+// so decode_grid picks ONE by the item count (profiles/r5/attn_one_step.md).
+template <int D, bool WIN, bool FP8, bool GRP, bool ONE = false>
+__global__ void __launch_bounds__(256, (ONE ? 4 : 1))
 attn_decode_kernel(AttnParams p, int items, int gs) {
   // GRP (num_splits > 1): the `gs` consecutive splits of one work item that share this
   // workgroup are merged in LDS, so only num_splits / gs partials per head reach global memory
@@ -77,8 +69,7 @@ attn_decode_kernel(AttnParams p, int items, int gs) {
   // of the K/V prefetch
   const int item = __builtin_amdgcn_readfirstlane(live ? item_raw : items - 1);
   WaveState<D> st;
-  const DecodeItem di =
-      attn_decode_item<D, WIN, FP8, false, decode_one_step<WIN, FP8, GRP>()>(p, item, live, st);
+  const DecodeItem di = attn_decode_item<D, WIN, FP8, false, ONE>(p, item, live, st);
   const int splits = p.num_splits, split = di.split, G = di.G, hgroups = di.hgroups;
   const int g0 = di.g0, kvh = di.kvh, b = di.b;
   const int lane = threadIdx.x & 63, col = lane & 15, h4 = lane >> 4;
@@ -577,13 +568,38 @@ __global__ void __launch_bounds__(256, (WIN && QB == 2) ? 1 : 2) attn_prefill_ke
 }
 
 // ------------------------------------------------------------------------------------------
+static int attn_cus() {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      return 256;
+    return n;
+  }();
+  return cus;
+}
+
 template <int D, bool WIN, bool FP8>
 static void decode_grid(const AttnParams& p, int items, int gs, hipStream_t stream) {
   const int grid = (items + 3) / 4;
-  if (p.num_splits > 1)
+  if (p.num_splits > 1) {
     attn_decode_kernel<D, WIN, FP8, true><<<grid, 256, 0, stream>>>(p, items, gs);
-  else
-    attn_decode_kernel<D, WIN, FP8, false><<<grid, 256, 0, stream>>>(p, items, 1);
+    return;
+  }
+  if constexpr (!WIN) {
+#ifndef ATTN_DECODE_TWO_STEP   // experiment builds: the round-4 loop at every batch
+    // one-step when it fills every SIMD with 4 waves and its last round is no emptier than the
+    // two-step loop's (B = 768: 6144 waves are 1.5 rounds of 4096 but 3 full rounds of 2048 --
+    // one-step measured 358 vs 342 us there)
+    const long s1 = 16L * attn_cus(), s2 = 8L * attn_cus();
+    const long r1 = (items + s1 - 1) / s1, r2 = (items + s2 - 1) / s2;
+    if (items >= s1 && (double)items / (r1 * s1) >= (double)items / (r2 * s2)) {
+      attn_decode_kernel<D, WIN, FP8, false, true><<<grid, 256, 0, stream>>>(p, items, 1);
+      return;
+    }
+#endif
+  }
+  attn_decode_kernel<D, WIN, FP8, false><<<grid, 256, 0, stream>>>(p, items, 1);
 }
 
 template <int D>

@@ -6,7 +6,7 @@ rc=0
 for arm in ${ARMS:-base fp8one base fp8one}; do
   if [ $arm = base ]; then cp /tmp/base.so "$so"; else cp tools_bin/variants/$arm/$(basename "$so") "$so"; fi
   echo "== $arm"
-  timeout -k 10 300 python -u scripts/attn_fp8kv_probe.py 2>&1 | grep '"B"' || { rc=1; break; }
+  timeout -k 10 300 python -u scripts/attn_fp8kv_probe.py ${CASES:+--cases=$CASES} 2>&1 | grep '"B"' || { rc=1; break; }
 done
 cp /tmp/base.so "$so"
 exit $rc

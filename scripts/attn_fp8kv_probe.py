@@ -49,7 +49,11 @@ def timed(B, L, fp8, esz, layers, ks, vs, bt, lens, q, splits, chosen):
     res.append(r)
 
 
-for B, L in [(512, 600), (64, 4096), (16, 8192), (1, 8192)]:
+CASES = [(512, 600), (64, 4096), (16, 8192), (1, 8192)]
+for a in sys.argv[1:]:
+    if a.startswith("--cases="):   # e.g. --cases=256x600,512x600
+        CASES = [tuple(int(v) for v in c.split("x")) for c in a.split("=", 1)[1].split(",")]
+for B, L in CASES:
     for fp8 in (False, True):
         bps = (L + bs - 1) // bs
         nblk = B * bps
