@@ -8,8 +8,12 @@ a device copy of the same bytes is the bandwidth reference.
 Prints one JSON line per kernel (us per call, TB/s of its HBM bytes)."""
 import argparse
 import json
+import os
+import sys
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributed_llm_inference import ops
 
