@@ -192,8 +192,15 @@ __device__ __forceinline__ bf16x8 load_qkv8(const RopeCacheParams& p, const bf16
   }
 }
 
+// One wave per workgroup (ROPE_THREADS): 8 heads' rotation groups are 64 lanes' work, so a
+// 128-thread workgroup left its second wave idle in 9 of every 10 workgroups.  64 threads:
+// 15.1 vs 17.6 us (bf16 KV) and 13.8 vs 15.9 us (fp8 KV) at 70B x 512 rows
+// (scripts/rope_bench.py, profiles/r5/rope_threads/).
+#ifndef ROPE_THREADS
+#define ROPE_THREADS 64
+#endif
 template <bool FP8, int NS>
-__global__ void __launch_bounds__(128) rope_cache_kernel_v8(RopeCacheParams p) {
+__global__ void __launch_bounds__(ROPE_THREADS) rope_cache_kernel_v8(RopeCacheParams p) {
   const int t = blockIdx.x;
   const int h_lo = blockIdx.y * kHeadsPerWG;
   const int D = p.D, half = D >> 1;
@@ -296,9 +303,9 @@ int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stre
   do {                                                                 \
     if (v8) {                                                          \
       if (p.kv_fp8)                                                    \
-        rope_cache_kernel_v8<true, NS><<<grid, 128, 0, stream>>>(p);   \
+        rope_cache_kernel_v8<true, NS><<<grid, ROPE_THREADS, 0, stream>>>(p);   \
       else                                                             \
-        rope_cache_kernel_v8<false, NS><<<grid, 128, 0, stream>>>(p);  \
+        rope_cache_kernel_v8<false, NS><<<grid, ROPE_THREADS, 0, stream>>>(p);  \
     } else if (p.kv_fp8)                                               \
       rope_cache_kernel<true, NS><<<grid, 128, 0, stream>>>(p);        \
     else                                                               \
