@@ -572,6 +572,40 @@ def test_attn_decode_fp8_kv(gpu, splits, D):
     _close(out, out_r, 2e-2, 2e-2, "decode-fp8")
 
 
+@pytest.mark.parametrize("kv_fp8", [False, True])
+@pytest.mark.parametrize("B", [512, 1024])
+def test_attn_decode_one_step_loop_large_batch(gpu, kv_fp8, B):
+    """Large one-split batches (B x 8 kv heads >= 16 waves per CU: attention.hip decode_grid runs
+    the one-step loop at 4 waves per SIMD) against the fp32 reference on sampled sequences, and
+    bit for bit against the same sequences run as small batches (the two-step loop): both
+    loops walk the keys in the same order through the same online-softmax arithmetic."""
+    torch.manual_seed(B + kv_fp8)
+    nh, nkv, D, bs = 64, 8, 128, 64
+    lens = torch.randint(1, 300, (B,), dtype=torch.int32)
+    lens[:3] = torch.tensor([1, 32, 299], dtype=torch.int32)
+    max_blocks = (int(lens.max()) + bs - 1) // bs
+    nblocks = B * max_blocks
+    ks = vs = 1.0
+    if kv_fp8:
+        ks, vs = 0.25, 1.5
+        kc, vc = _make_cache_fp8(nblocks, nkv, bs, D, gpu, ks, vs)
+    else:
+        kc, vc = _make_cache(nblocks, nkv, bs, D, gpu)
+    bt = _tables(B, max_blocks, nblocks, gpu, seed=7)
+    q = torch.randn(B, nh, D, device=gpu, dtype=BF)
+    lg = lens.to(gpu)
+    scale = 1 / math.sqrt(D)
+    out = ops.attn_decode(q, None, kc, vc, bt, lg, scale, num_splits=1, k_scale=ks, v_scale=vs)
+    parts = [ops.attn_decode(q[i:i + 64], None, kc, vc, bt[i:i + 64], lg[i:i + 64], scale,
+                             num_splits=1, k_scale=ks, v_scale=vs) for i in range(0, B, 64)]
+    torch.cuda.synchronize()
+    assert torch.equal(out, torch.cat(parts, 0))
+    idx = torch.tensor([0, 1, 2] + list(range(5, B, B // 29)))
+    out_r = ref.attn_decode(q[idx].cpu(), None, kc.cpu(), vc.cpu(), bt[idx].cpu(), lens[idx],
+                            scale, k_scale=ks, v_scale=vs)
+    _close(out[idx], out_r, 2e-2, 2e-2, "decode one-step")
+
+
 @pytest.mark.parametrize("B", [5, 64, 130])
 @pytest.mark.parametrize("kv_fp8", [False, True])
 def test_attn_decode_mx_output_bit_exact(gpu, B, kv_fp8):
