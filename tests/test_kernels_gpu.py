@@ -573,14 +573,15 @@ def test_attn_decode_fp8_kv(gpu, splits, D):
 
 
 @pytest.mark.parametrize("kv_fp8", [False, True])
-@pytest.mark.parametrize("B", [512, 1024])
-def test_attn_decode_one_step_loop_large_batch(gpu, kv_fp8, B):
+@pytest.mark.parametrize("B,nh,nkv,D", [(512, 64, 8, 128), (1024, 64, 8, 128), (512, 16, 8, 64),
+                                        (512, 8, 8, 32)])
+def test_attn_decode_one_step_loop_large_batch(gpu, kv_fp8, B, nh, nkv, D):
     """Large one-split batches (B x 8 kv heads >= 16 waves per CU: attention.hip decode_grid runs
     the one-step loop at 4 waves per SIMD) against the fp32 reference on sampled sequences, and
     bit for bit against the same sequences run as small batches (the two-step loop): both
     loops walk the keys in the same order through the same online-softmax arithmetic."""
-    torch.manual_seed(B + kv_fp8)
-    nh, nkv, D, bs = 64, 8, 128, 64
+    torch.manual_seed(B + kv_fp8 + D)
+    bs = 64
     lens = torch.randint(1, 300, (B,), dtype=torch.int32)
     lens[:3] = torch.tensor([1, 32, 299], dtype=torch.int32)
     max_blocks = (int(lens.max()) + bs - 1) // bs
