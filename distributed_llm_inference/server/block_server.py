@@ -84,17 +84,23 @@ class HopMoved(HopFailure):
     """The server now serves other layers (swarm rebalancing): re-resolve its old range."""
 
 
-def build_block_app(worker, rebalance=None):
+def build_block_app(worker, rebalance=None, token=None):
     """The block server's HTTP service; ``rebalance``: a callable running one rebalancing round
-    (:func:`rebalance_once`) behind POST /rebalance, for operators and tests."""
-    from fastapi import FastAPI, HTTPException
+    (:func:`rebalance_once`) behind POST /rebalance, for operators and tests.  ``token``: the
+    registry's shared token (``--registry-token``), then required by POST /rebalance as well
+    (``Authorization: Bearer ...``), since a move changes what the swarm serves."""
+    import hmac
+    from fastapi import FastAPI, HTTPException, Request
     from fastapi.responses import JSONResponse, Response
 
     app = FastAPI(title="distributed_llm_inference block server")
 
     @app.post("/rebalance")
-    async def rebalance_now():
+    async def rebalance_now(request: Request):
         import asyncio
+        if token is not None and not hmac.compare_digest(
+                request.headers.get("authorization", "").encode(), f"Bearer {token}".encode()):
+            raise HTTPException(401, "registry token required (Authorization: Bearer ...)")
         if rebalance is None:
             raise HTTPException(404, "this server has no registry to rebalance against")
         moved = await asyncio.get_running_loop().run_in_executor(None, rebalance)
@@ -231,7 +237,8 @@ def serve_blocks(worker, host: str = "127.0.0.1", port: int = 8100, registry=Non
         if rebalance_s > 0:
             rebalance_loop(worker, registry, url, span, rebalance_s, stop, moving)
     try:
-        uvicorn.run(build_block_app(worker, rebalance if registry is not None else None),
+        uvicorn.run(build_block_app(worker, rebalance if registry is not None else None,
+                                    token=getattr(registry, "token", None)),
                     host=host, port=port, log_level="warning")
     finally:
         if registry is not None:

@@ -265,6 +265,7 @@ class RegistryClient:
         self.url = url.rstrip("/")
         self.timeout = timeout
         self._s = requests.Session()
+        self.token = token or None
         if token:
             self._s.headers["Authorization"] = f"Bearer {token}"
 
