@@ -345,7 +345,7 @@ void attn_prefill(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache,
                   Tensor block_tables, Tensor seq_lens, Tensor q_start, int64_t max_q,
                   double scale, int64_t n_sink, int64_t sink_pad, int64_t ring, int64_t window,
                   double k_scale, double v_scale, optional<Tensor> tile_map, int64_t qb,
-                  optional<Tensor> mask) {
+                  optional<Tensor> mask, bool m32) {
   int64_t D = 0;
   auto p = attn_common(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, scale, n_sink,
                        sink_pad, ring, window, k_scale, v_scale, D);
@@ -361,6 +361,7 @@ void attn_prefill(Tensor out, Tensor q, optional<Tensor> q_sink, Tensor k_cache,
   }
   TORCH_CHECK(qb == 1 || qb == 2, "attn_prefill: qb (query blocks per wave) must be 1 or 2");
   p.prefill_qb = (int)qb;
+  p.prefill_m32 = m32 ? 1 : 0;
   if (mask.has_value()) {   // reference 4-D additive mask [B, 1 | nh, Tm, Km], fp32
     CHECK_IN(*mask); CHECK_F32(*mask);
     TORCH_CHECK(mask->dim() == 4 && mask->size(0) == B &&
@@ -969,7 +970,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("block_tables"), py::arg("seq_lens"), py::arg("q_start"), py::arg("max_q"),
         py::arg("scale"), py::arg("n_sink"), py::arg("sink_pad"), py::arg("ring"),
         py::arg("window"), py::arg("k_scale"), py::arg("v_scale"), py::arg("tile_map"),
-        py::arg("qb"), py::arg("mask") = py::none());
+        py::arg("qb"), py::arg("mask") = py::none(), py::arg("m32") = true);
   m.def("sample", &sample, "greedy / temperature / top-k / top-p sampling", py::arg("out_tokens"),
         py::arg("out_logprobs"), py::arg("logits"), py::arg("temperature"), py::arg("top_k"),
         py::arg("top_p"), py::arg("seeds"), py::arg("step"), py::arg("ctr") = py::none());

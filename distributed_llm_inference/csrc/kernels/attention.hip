@@ -679,6 +679,7 @@ int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_
   if (p.bs % 32 != 0 || (p.ring > 0 && (p.sink_pad % 32 != 0 || p.ring % 32 != 0))) return -2;
   if (p.mask && (p.ring > 0 || p.tile_map || p.mask_heads < 1 || p.mask_q < 1 || p.mask_k < 1))
     return -4;   // custom masks: full cache, dense grid
+  if (attn_prefill32_eligible(p, D)) return launch_attn_prefill32(p, B, max_q, stream);
   switch (D) {
     case 32: return launch_prefill_d<32>(p, B, max_q, stream);
     case 64: return launch_prefill_d<64>(p, B, max_q, stream);

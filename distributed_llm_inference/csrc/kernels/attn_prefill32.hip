@@ -1,0 +1,477 @@
+// Causal prefill attention on the 32x32x16 bf16 MFMA: 32 query rows per wave, 64-key steps.
+//
+// Replaces the reference's eager prefill attention (modules.py:87-97: repeat_kv, QK^T/sqrt(D) +
+// additive causal mask, fp32 softmax, PV) for the common case - full (non-windowed) bf16 cache,
+// head_dim 128, GQA group a multiple of 4, no custom mask; attention.hip keeps the general kernel.
+//
+// Why a second kernel: attention.hip's prefill wave holds 16 query rows on the 16x16x32 MFMA, so
+// every K / V^T fragment read from LDS (one ds_read_b128) feeds ONE 16-cycle MFMA: four SIMDs ask
+// the LDS for 4 KB per 16 cycles = its whole 256 B/clk, and the loop sat at 0.7 PF on 4k-token
+// chunks.  Here a wave holds 32 query rows on the 32x32x16 MFMA (32 cycles per fragment read):
+// half the LDS bytes per FLOP, and 64-key steps halve the barriers and online-softmax rescales
+// per FLOP (MI355X_MICROARCH.md "LDS"; cdna_hip_programming.md Appendix B "Fused attention
+// prefill").
+//
+// Layout of one workgroup = GW q heads of ONE kv head (GW = 8, or 4) x TQ query tokens (32, or 16
+// for short chunks), NW = GW * TQ / 32 waves; row R = 32 w + c of the workgroup is token R % TQ
+// of head R / TQ.  All waves share every K / V^T tile (GQA-native, no repeat_kv).
+//   * S^T[key, q] = K[key, d] . Q^T[d, q] (A = K rows from LDS, B = Q^T in registers): lane
+//     (c = l & 31, h = l >> 5) ends holding column c and accumulator rows (r&3) + 8(r>>2) + 4h.
+//     The K tile's LDS row i holds key pi(i) = i with bits 2 and 3 swapped, so register r of lane
+//     half h holds key 16(r>>3) + 8h + (r&7): registers 8s..8s+7, packed to bf16, ARE the P^T
+//     operand of k-step s of the next product (keys 16s + 8h + j), with no lane movement
+//     (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand").
+//   * O^T[d, q] += V^T[d, key] . P^T[key, q]: the cache's V^T 8-key groups [g][d][8] give lane
+//     (d, h) of k-step s group 2s + h as ONE 16-byte LDS read.
+//   * K rows are stored with 16-byte chunk c at c ^ (row & 15): the row reads of one ds_read_b128
+//     lane group (rows {0-3, 12-15, 20-27} or {4-11, 16-19, 28-31}, one chunk) then hit 16
+//     distinct bank slots; the V^T reads (consecutive d) are conflict-free as stored.
+//   * K / V^T tiles (2 x 16 KB per step) go global -> LDS by LDS-DMA into two buffers: the next
+//     step's DMA is issued before this step's MFMAs, one barrier per step.
+//   * online softmax in the log2 domain with a deferred max (cdna_hip_programming.md T13): the
+//     running max (and the O / l rescale) moves only when some column's max grew by more than
+//     THR = 8, so P <= 2^8 (exact-scale fp32 accumulation; bf16 P keeps its relative precision).
+//   * causality from seq_lens / q_start (no mask tensor); steps entirely below the diagonal skip
+//     the mask, the half of a diagonal step past every column's position skips its MFMAs.
+//   * work list: the (sequence, tile) map of attention.hip walked heaviest tile first (the
+//     causal tail), XCD-grouped so consecutive tiles of one kv head share an L2.
+#include "kernels.h"
+#include "attn_core.h"
+
+#include <type_traits>
+
+namespace dli {
+
+namespace {
+
+constexpr int P32_D = 128;
+constexpr float P32_THR = 8.f;   // deferred-max threshold (log2 domain)
+#ifndef P32_PIPE
+#define P32_PIPE 0   // 1: the software-pipelined loop (measured slower, see the A/B in profiles/r6/)
+#endif
+#ifndef P32_EARLYDMA
+#define P32_EARLYDMA 0   // 1: issue the next step's DMA before this step's MFMAs
+#endif
+#ifndef P32_KO
+#define P32_KO 0   // diagnosis builds only: 1 = no softmax (P = S), 2 = no DMA in the loop
+#endif
+#ifndef P32_PRIO
+#define P32_PRIO 0   // 1: static s_setprio 1 for the second half of the waves
+#endif
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int swap23(int i) {   // pi: swap bits 2 and 3 of a 32-row index
+  return (i & ~0xC) | ((i & 4) << 1) | ((i & 8) >> 1);
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x16& s, int base) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)s[base + j];
+  return r;
+}
+
+}  // namespace
+
+template <int TQ, int GW>
+__global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
+  constexpr int D = P32_D;
+  constexpr int CH = D / 8;                 // 16-B chunks per K row
+  constexpr int NW = GW * TQ / 32;          // waves per workgroup
+  constexpr int DPW = 32 / NW;              // LDS-DMA wave-instructions per wave per step
+  // [buf][K | V^T][64 keys x D]: 2 x 2 x 16 KB
+  __shared__ __attribute__((aligned(16))) bf16 smem[2][2][64 * D];
+
+  const int G = p.nh / p.nkv;
+  const int wg_per_kv = G / GW;
+  int b, tile, grp;
+  if (p.tile_map) {
+    const int total = p.n_tiles * p.nkv * wg_per_kv;
+    const int per = (int)gridDim.x >> 3;
+    const int L8 = (int)blockIdx.x;
+    const int w = (L8 & 7) * per + (L8 >> 3);
+    if (w >= total) return;                 // padding (whole workgroup, before any barrier)
+    grp = w / p.n_tiles;
+    const int t = p.n_tiles - 1 - (w - grp * p.n_tiles);   // heaviest (last) tiles first
+    b = p.tile_map[2 * t];
+    tile = p.tile_map[2 * t + 1];
+  } else {
+    b = blockIdx.z;
+    tile = gridDim.x - 1 - blockIdx.x;
+    grp = blockIdx.y;
+  }
+  const int kvh = grp / wg_per_kv;
+  const int h0 = kvh * G + (grp % wg_per_kv) * GW;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 31, hh = lane >> 5;
+  if (P32_PRIO && w >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  const int R = 32 * w + c;
+  const int qh = h0 + R / TQ;
+  const int qs0 = p.q_start[b];
+  const int qlen = p.q_start[b + 1] - qs0;
+  const int t0 = tile * TQ;
+  if (t0 >= qlen) return;                   // whole workgroup idle
+  const int L = p.seq_lens[b];
+  const int tok = t0 + R % TQ;
+  const bool valid = tok < qlen;
+  const int pq = L - qlen + (valid ? tok : qlen - 1);          // this column's position
+  const int pq_lo = L - qlen + t0;                               // workgroup's first position
+  const int pq_hi = L - qlen + min(qlen - 1, t0 + TQ - 1);       // ... and last
+  const int nsteps = (pq_hi + 64) >> 6;                          // keys [0, pq_hi]
+  const int* bt = p.block_tables + (size_t)b * p.bt_stride;
+  const size_t head_stride = (size_t)p.bs * D;
+
+  // ---- Q^T operand: lane (c, hh) holds d = 16 m + 8 hh + [0, 8) of its column, m = 0..7 ----
+  // (rows past the chunk load the chunk's first token - always present - and are zeroed)
+  bf16x8 qf[D / 16];
+  {
+    const bf16* qrow = p.q + ((size_t)(qs0 + (valid ? tok : 0)) * p.nh + qh) * D + 8 * hh;
+#pragma unroll
+    for (int m = 0; m < D / 16; ++m) {
+      qf[m] = *reinterpret_cast<const bf16x8*>(qrow + 16 * m);
+      if (!valid) qf[m] = zero8();
+    }
+  }
+
+  // ---- LDS-DMA: the K image or the V^T image (16 wave-instructions of 1 KB each, 16 / NW per
+  // wave) of one 64-key step.  Instruction j covers K rows 4j..4j+3 / V^T units 64j..64j+63;
+  // j >> 3 = its 32-key half.  A half past every column is never fetched (its block-table entry
+  // may not exist).
+  auto dma = [&](int s, bf16* dst, bool is_v) {
+    const int u0 = s * 64;
+    const bool need1 = u0 + 32 <= pq_hi;
+    const int pg0 = bt_entry(bt, u0 / p.bs);
+    const int pg1 = !need1 ? pg0 : (p.bs % 64 == 0 ? pg0 : bt_entry(bt, (u0 + 32) / p.bs));
+    const size_t e00 = ((size_t)pg0 * p.nkv + kvh) * head_stride + (size_t)(u0 % p.bs) * D;
+    const size_t e01 = ((size_t)pg1 * p.nkv + kvh) * head_stride + (size_t)((u0 + 32) % p.bs) * D;
+#pragma unroll
+    for (int i = 0; i < 16 / NW; ++i) {
+      const int j = w + i * NW;                // wave-uniform
+      const int half = j >> 3;
+      if (half && !need1) continue;
+      const size_t e0 = half ? e01 : e00;
+      const int u = j * 64 + lane;             // 16-B unit of this lane in the 16 KB image
+      const bf16* g;
+      if (!is_v) {
+        const int row = u >> 4, slot = u & 15;           // LDS row (0..63), stored chunk
+        const int key = swap23(row & 31);                // key of this row inside its half
+        g = static_cast<const bf16*>(p.k_cache) + e0 + (size_t)key * D + 8 * (slot ^ (row & 15));
+      } else {
+        g = static_cast<const bf16*>(p.v_cache) + e0 + (size_t)(u & 511) * 8;
+      }
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
+                                       (__attribute__((address_space(3))) void*)(dst + j * 64 * 8),
+                                       16, 0, 0);
+    }
+  };
+  auto kbuf = [&](int i) { return &smem[i][0][0]; };
+  auto vbuf = [&](int i) { return &smem[i][1][0]; };
+
+  f32x16 o[D / 32];
+#pragma unroll
+  for (int db = 0; db < D / 32; ++db) o[db] = f32x16{};
+  float l_run = 0.f;
+  const float sl2 = p.scale_log2;
+  // LDS fragment offsets (elements): K row c (half 0) chunk (2m + hh) ^ (c & 15); V^T unit (g, d)
+  const int koff = c * CH * 8;
+  const int kx = c & 15;
+  const int voff = (hh * D + c) * 8;
+  auto full2 = [&](int s) { return s * 64 + 32 <= pq_hi; };   // second half holds a visible key
+  auto diag = [&](int s) { return s * 64 + 63 > pq_lo; };     // some key past some column
+#if P32_PIPE
+  // Software pipeline (cdna_hip_programming.md T15): iteration s runs
+  //   phase 1: S(s+1) = K(s+1) Q^T on the matrix pipe  ||  P(s) = exp2(S(s) sl2 - m) on the VALU
+  //   phase 2: O^T += V^T(s) P^T(s) on the matrix pipe   ||  mask + row max of S(s+1) (the
+  //            cross-lane step: one bpermute) and the deferred-max decision for step s+1
+  // so neither pipe waits for the other inside a wave.  K runs two steps ahead of V in the DMA
+  // (K(s+2) and V(s+1) are fetched during iteration s), so each DMA overwrites a buffer that was
+  // last read before the previous barrier.
+  f32x16 ca, cb;
+  float m_cur = -1e30f, alpha = 0.f;
+  bool resc = true;
+  // mask (diagonal steps) and row max of S(s); sets the running max / rescale for step s
+  auto smax = [&](int s, bool mask, f32x16& sa, f32x16& sb) {
+    const int kb = s * 64;
+    if (mask) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb + 16 * (r >> 3) + 8 * hh + (r & 7);
+        sa[r] = key > pq ? -INFINITY : sa[r];
+        sb[r] = key + 32 > pq ? -INFINITY : sb[r];   // (a never-loaded half: every key masked)
+      }
+    }
+    float mx = fmaxf(sa[0], sb[0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(sa[r], sb[r]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float pmax = mx * sl2;
+    // deferred max (T13): move the running max only when some column grew by more than THR
+    resc = __any(pmax > m_cur + P32_THR);
+    const float m_new = resc ? fmaxf(m_cur, pmax) : m_cur;
+    alpha = __builtin_amdgcn_exp2f(m_cur - m_new);
+    m_cur = m_new;
+  };
+  auto s_mfma = [&](const bf16* kt, f32x16& sa, f32x16& sb) {
+    sa = f32x16{};
+    sb = f32x16{};
+#pragma unroll
+    for (int m = 0; m < D / 16; ++m) {
+      const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kt + koff + ((2 * m + hh) ^ kx) * 8);
+      const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(kt + 32 * CH * 8 + koff +
+                                                         ((2 * m + hh) ^ kx) * 8);
+      sa = mfma32(k0, qf[m], sa);
+      sb = mfma32(k1, qf[m], sb);
+    }
+  };
+  dma(0, kbuf(0), false);
+  dma(0, vbuf(0), true);
+  if (nsteps > 1) dma(1, kbuf(1), false);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // S(0): the second half's K may never have been loaded (one-step tiles): its scores are masked
+  s_mfma(kbuf(0), ca, cb);
+  smax(0, diag(0), ca, cb);
+  __syncthreads();   // every wave is done with K(0) before iteration 0 refills its buffer
+
+  auto iter = [&](int s, auto maskn_c, auto next_c) {
+    constexpr bool MASKN = decltype(maskn_c)::value;   // step s+1 needs the causal mask
+    constexpr bool NEXT = decltype(next_c)::value;     // there is a step s+1
+    const int buf = s & 1;
+    if (s + 2 < nsteps) dma(s + 2, kbuf(buf), false);
+    if (NEXT) dma(s + 1, vbuf(buf ^ 1), true);
+    // ---- phase 1 (one basic block): S(s+1) MFMAs || P(s) ----
+    f32x16 na, nb;
+    if constexpr (NEXT) s_mfma(kbuf(buf ^ 1), na, nb);
+    float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      ca[r] = __builtin_amdgcn_exp2f(fmaf(ca[r], sl2, -m_cur));
+      cb[r] = __builtin_amdgcn_exp2f(fmaf(cb[r], sl2, -m_cur));
+      ps0 += ca[r];
+      ps1 += cb[r];
+    }
+    l_run = l_run * alpha + (ps0 + ps1);
+    const bf16x8 p0 = pack8(ca, 0), p1 = pack8(ca, 8), p2 = pack8(cb, 0), p3 = pack8(cb, 8);
+    if constexpr (NEXT) {
+      // pin P(s) here (the scheduler would otherwise sink the exponentials to their use in
+      // phase 2, behind the rescale branch): 2 K reads ahead, then {MFMA, K read, 7 VALU} x 14,
+      // then {MFMA, 7 VALU} x 2
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int i = 0; i < 14; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+      }
+    }
+    asm volatile("" ::"v"(__builtin_bit_cast(i32x4, p0)), "v"(__builtin_bit_cast(i32x4, p1)),
+                 "v"(__builtin_bit_cast(i32x4, p2)), "v"(__builtin_bit_cast(i32x4, p3)), "v"(l_run));
+    // ---- phase 2: O^T = alpha O^T + V^T(s) P^T(s)  ||  max of S(s+1) ----
+    if (resc) {
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) o[db] *= alpha;
+    }
+    const bf16* vt = vbuf(buf);
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+      const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(vt + voff + (0 * D + 32 * db) * 8);
+      const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(vt + voff + (2 * D + 32 * db) * 8);
+      o[db] = mfma32(v0, p0, o[db]);
+      o[db] = mfma32(v1, p1, o[db]);
+    }
+    // the second half: every step but a last one whose half is past every column (its V^T
+    // was never loaded - stale LDS must not reach the accumulators, even times zero)
+    if (NEXT || full2(s)) {
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+        const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(vt + voff + (4 * D + 32 * db) * 8);
+        const bf16x8 v3 = *reinterpret_cast<const bf16x8*>(vt + voff + (6 * D + 32 * db) * 8);
+        o[db] = mfma32(v2, p2, o[db]);
+        o[db] = mfma32(v3, p3, o[db]);
+      }
+    }
+    if constexpr (NEXT) {
+      smax(s + 1, MASKN, na, nb);
+      // 2 V reads ahead, then {MFMA, V read, 3 VALU} x 14, then the rest
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+      for (int i = 0; i < 14; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+      }
+      ca = na;
+      cb = nb;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs landed
+      __syncthreads();
+    }
+  };
+  // iterations whose next step is below every column's diagonal need no mask for it; the last
+  // step computes no S(s+1)
+  int s = 0;
+  for (; s + 1 < nsteps && !diag(s + 1); ++s) iter(s, std::false_type{}, std::true_type{});
+  for (; s + 1 < nsteps; ++s) iter(s, std::true_type{}, std::true_type{});
+  iter(s, std::false_type{}, std::false_type{});
+
+#else
+  // Plain loop: iteration s computes S(s), its softmax and O += V(s) P(s); the DMA of step s+1
+  // (K and V^T) is issued first into the other buffer.
+  float m_run = -1e30f;
+  dma(0, kbuf(0), false);
+  dma(0, vbuf(0), true);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  auto iter = [&](int s, auto mask_c) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    const int buf = s & 1;
+    if (P32_EARLYDMA && s + 1 < nsteps) {
+      dma(s + 1, kbuf(buf ^ 1), false);
+      dma(s + 1, vbuf(buf ^ 1), true);
+    }
+    const bool f2 = full2(s);
+    const bf16* kt = kbuf(buf);
+    const bf16* vt = vbuf(buf);
+    bf16x8 ka[D / 16], kb8[D / 16];
+#pragma unroll
+    for (int m = 0; m < D / 16; ++m)
+      ka[m] = *reinterpret_cast<const bf16x8*>(kt + koff + ((2 * m + hh) ^ kx) * 8);
+    f32x16 sa = {}, sb = {};
+#pragma unroll
+    for (int m = 0; m < D / 16; ++m) {
+      kb8[m] = *reinterpret_cast<const bf16x8*>(kt + 32 * CH * 8 + koff + ((2 * m + hh) ^ kx) * 8);
+      sa = mfma32(ka[m], qf[m], sa);
+    }
+    // the next step's DMA is issued behind the first half's MFMAs: its block-table lookups
+    // (scalar loads waited in place) then overlap the matrix pipe instead of delaying it
+    if (!P32_EARLYDMA && P32_KO != 2 && s + 1 < nsteps) {
+      dma(s + 1, kbuf(buf ^ 1), false);
+      dma(s + 1, vbuf(buf ^ 1), true);
+    }
+    if (f2) {
+#pragma unroll
+      for (int m = 0; m < D / 16; ++m) sb = mfma32(kb8[m], qf[m], sb);
+    }
+    bf16x8 va[D / 32][2];
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+      va[db][0] = *reinterpret_cast<const bf16x8*>(vt + voff + (0 * D + 32 * db) * 8);
+      va[db][1] = *reinterpret_cast<const bf16x8*>(vt + voff + (2 * D + 32 * db) * 8);
+    }
+    const int kb = s * 64;
+    if constexpr (MASK) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb + 16 * (r >> 3) + 8 * hh + (r & 7);
+        sa[r] = key > pq ? -INFINITY : sa[r];
+        sb[r] = key + 32 > pq ? -INFINITY : sb[r];
+      }
+    }
+    float mx = fmaxf(sa[0], sb[0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(sa[r], sb[r]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float pmax = mx * sl2;
+    if (P32_KO != 1 && __any(pmax > m_run + P32_THR)) {
+      const float mn = fmaxf(m_run, pmax);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) o[db] *= alpha;
+      l_run *= alpha;
+      m_run = mn;
+    }
+    float ps0 = 0.f, ps1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (P32_KO != 1) sa[r] = __builtin_amdgcn_exp2f(fmaf(sa[r], sl2, -m_run));
+      ps0 += sa[r];
+    }
+    const bf16x8 p0 = pack8(sa, 0), p1 = pack8(sa, 8);
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+      o[db] = mfma32(va[db][0], p0, o[db]);
+      o[db] = mfma32(va[db][1], p1, o[db]);
+    }
+    if (f2) {
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+        va[db][0] = *reinterpret_cast<const bf16x8*>(vt + voff + (4 * D + 32 * db) * 8);
+        va[db][1] = *reinterpret_cast<const bf16x8*>(vt + voff + (6 * D + 32 * db) * 8);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (P32_KO != 1) sb[r] = __builtin_amdgcn_exp2f(fmaf(sb[r], sl2, -m_run));
+        ps1 += sb[r];
+      }
+      const bf16x8 p2 = pack8(sb, 0), p3 = pack8(sb, 8);
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+        o[db] = mfma32(va[db][0], p2, o[db]);
+        o[db] = mfma32(va[db][1], p3, o[db]);
+      }
+    }
+    l_run += ps0 + ps1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step s+1 landed
+    __syncthreads();
+  };
+  int s = 0;
+  for (; s < nsteps && !diag(s); ++s) iter(s, std::false_type{});
+  for (; s < nsteps; ++s) iter(s, std::true_type{});
+
+#endif
+  // ---- normalise and store: register r of o[db] is d = 32 db + (r & 3) + 8 (r >> 2) + 4 hh ----
+  float lsum = l_run + __shfl_xor(l_run, 32, 64);
+  if (valid) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16* orow = p.out + ((size_t)(qs0 + tok) * p.nh + qh) * D + 4 * hh;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[db][4 * a + r] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 32 * db + 8 * a) = v;
+      }
+  }
+}
+
+// Eligible: head_dim 128, bf16 full cache, GQA group a multiple of 4, no custom mask.
+bool attn_prefill32_eligible(const AttnParams& p, int D) {
+  const int G = p.nh / p.nkv;
+  return p.prefill_m32 && D == P32_D && !p.kv_fp8 && p.ring == 0 && p.mask == nullptr &&
+         G % 4 == 0 && p.bs % 32 == 0;
+}
+
+// Tile = 16 * prefill_qb query tokens (the same tile attention.hip's kernel uses at 4 heads per
+// wave, so one (sequence, tile) map serves both).
+int launch_attn_prefill32(const AttnParams& p, int B, int max_q, hipStream_t stream) {
+  const int G = p.nh / p.nkv;
+  const int gw = G % 8 == 0 ? 8 : 4;
+  const int TQ = 16 * p.prefill_qb;
+  const int nw = gw * TQ / 32;
+  dim3 grid((max_q + TQ - 1) / TQ, p.nkv * (G / gw), B);
+  if (p.tile_map) {
+    const long total = (long)p.n_tiles * p.nkv * (G / gw);
+    grid = dim3((unsigned)((total + 7) / 8 * 8), 1, 1);
+  }
+  if (grid.x == 0) return 0;
+  if (gw == 8) {
+    if (TQ == 32) attn_prefill32_kernel<32, 8><<<grid, 64 * nw, 0, stream>>>(p);
+    else attn_prefill32_kernel<16, 8><<<grid, 64 * nw, 0, stream>>>(p);
+  } else {
+    if (TQ == 32) attn_prefill32_kernel<32, 4><<<grid, 64 * nw, 0, stream>>>(p);
+    else attn_prefill32_kernel<16, 4><<<grid, 64 * nw, 0, stream>>>(p);
+  }
+  return 0;
+}
+
+}  // namespace dli

@@ -19,6 +19,7 @@ struct AttnParams {
   const int* tile_map;  // prefill: [n_tiles, 2] (sequence, token tile) work list, or nullptr
   int n_tiles;          //   (nullptr: dense grid over max_q x B)
   int prefill_qb = 1;   // prefill: 16-token query blocks per wave (1 or 2); a tile = 16 TPW QB tokens
+  int prefill_m32 = 1;  // prefill: the 32x32x16-MFMA kernel (attn_prefill32.hip) where eligible
   float scale_log2;     // softmax scale * log2(e)
   int nh, nkv, bs;
   int n_sink, sink_pad, ring, window;  // window mode iff ring > 0
@@ -89,6 +90,8 @@ int launch_add(bf16* out, const bf16* a, const bf16* b, size_t n, hipStream_t st
 int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stream);
 int launch_attn_decode(const AttnParams& p, int B, int D, hipStream_t stream);
 int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_t stream);
+bool attn_prefill32_eligible(const AttnParams& p, int D);
+int launch_attn_prefill32(const AttnParams& p, int B, int max_q, hipStream_t stream);
 int launch_sample(const SampleParams& p, int B, hipStream_t stream);
 int launch_gemm_tile(void* C, const void* A, const void* B, const float* a_scale,
                      const float* b_scale, float* workspace, int M, int N, int K, int splits,

@@ -357,7 +357,8 @@ def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, m
         tile_map = None   # dense grid: the masked kernel runs one query block per wave
     native().attn_prefill(out, q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start,
                           int(max_q), float(scale), int(n_sink), int(sink_pad), int(ring),
-                          int(window), float(k_scale), float(v_scale), tile_map, int(qb), mask)
+                          int(window), float(k_scale), float(v_scale), tile_map, int(qb), mask,
+                          bool(policy().prefill_m32))
     return out
 
 

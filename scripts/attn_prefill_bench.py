@@ -16,6 +16,9 @@ from distributed_llm_inference import ops  # noqa: E402
 dev = torch.device("cuda:0")
 nh, nkv, D, bs = 64, 8, 128, 64
 CASES = [(32, 512, 0), (4, 4096, 0), (1, 2048, 6144), (256, 16, 512)]
+if os.environ.get("CASES"):   # e.g. CASES="4x4096x0,1x32768x0"
+    CASES = [tuple(int(x) for x in c.split("x")) for c in os.environ["CASES"].split(",")]
+QB = int(os.environ.get("QB", ops.PREFILL_QB))
 
 
 def run(B, q, ctx):
@@ -30,10 +33,10 @@ def run(B, q, ctx):
     Q = torch.randn(B * q, nh, D, device=dev, dtype=torch.bfloat16)
     out = torch.empty_like(Q)
 
-    tm = ops.prefill_tiles([q] * B, nh, nkv).to(dev) if os.environ.get("DENSE") != "1" else None
+    tm = ops.prefill_tiles([q] * B, nh, nkv, qb=QB).to(dev) if os.environ.get("DENSE") != "1" else None
 
     def call():
-        ops.attn_prefill(Q, None, kc, vc, bt, lens, q_start, q, D ** -0.5, tile_map=tm)
+        ops.attn_prefill(Q, None, kc, vc, bt, lens, q_start, q, D ** -0.5, tile_map=tm, qb=QB)
 
     for _ in range(3):
         call()
@@ -46,7 +49,8 @@ def run(B, q, ctx):
     us = (time.perf_counter() - t0) / n * 1e6
     pairs = B * sum(ctx + i + 1 for i in range(q))
     tf = 4 * D * nh * pairs / us / 1e6
-    return dict(B=B, q=q, ctx=ctx, us=round(us, 1), TFLOPs=round(tf, 1))
+    return dict(B=B, q=q, ctx=ctx, qb=QB, m32=int(ops.policy().prefill_m32), us=round(us, 1),
+                TFLOPs=round(tf, 1))
 
 
 res = []
@@ -55,4 +59,5 @@ for c in CASES:
     print(r, flush=True)
     res.append(r)
 os.makedirs("gpurun_out", exist_ok=True)
-json.dump(res, open("gpurun_out/attn_prefill_bench_qb%s.json" % ops.prefill_qb(), "w"), indent=1)
+tag = os.environ.get("TAG", "qb%d_m32%d" % (QB, int(ops.policy().prefill_m32)))
+json.dump(res, open("gpurun_out/attn_prefill_bench_%s.json" % tag, "w"), indent=1)

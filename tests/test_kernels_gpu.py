@@ -692,6 +692,51 @@ def test_attn_prefill_long_chunks(gpu, qb):
     _close(out, out_r, 2e-2, 2e-2, f"prefill-long-qb{qb}")
 
 
+@pytest.mark.parametrize("nh,nkv", [(64, 8), (32, 8), (64, 4)])
+@pytest.mark.parametrize("qb", ["1", "2"])
+@pytest.mark.parametrize("ramp", [False, True])
+def test_attn_prefill_m32(gpu, nh, nkv, qb, ramp):
+    """attn_prefill32.hip (32x32x16 MFMA, 64-key steps, deferred softmax max) against the fp32
+    oracle and against attention.hip's kernel: GQA groups of 8 / 4 / 16 (two workgroups per kv
+    head), 16- and 32-token tiles, chunks on top of cached context, a chunk ending mid-step, decode
+    rows in the batch.  ``ramp``: keys scaled up along the sequence, so the running max keeps
+    growing by more than the deferral threshold (every rescale branch fires, cdna T13 hazard)."""
+    qb = int(qb)
+    torch.manual_seed(31)
+    D, bs = 128, 64
+    q_lens = [300, 1, 33, 64, 96, 2]
+    ctx = [0, 500, 31, 64, 200, 0]
+    lens = torch.tensor([a + b for a, b in zip(q_lens, ctx)], dtype=torch.int32)
+    B = len(q_lens)
+    q_start = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
+    max_blocks = (int(lens.max()) + bs - 1) // bs
+    kc, vc = _make_cache(B * max_blocks, nkv, bs, D, gpu)
+    if ramp:   # slot s of every page scaled by 1 + 6 (page_pos * bs + s) / L: later keys louder
+        bt_cpu = _tables(B, max_blocks, B * max_blocks, "cpu", seed=9)
+        scale_k = torch.ones(B * max_blocks, 1, bs, 1)
+        for b in range(B):
+            for j in range(max_blocks):
+                pos = j * bs + torch.arange(bs, dtype=torch.float32)
+                scale_k[int(bt_cpu[b, j]), 0, :, 0] = 1 + 6 * pos / max(int(lens[b]), 1)
+        kc = (kc.float() * scale_k.to(gpu)).to(BF)
+    bt = _tables(B, max_blocks, B * max_blocks, gpu, seed=9)
+    q = torch.randn(int(q_start[-1]), nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    tm = ops.prefill_tiles(q_lens, nh, nkv, qb=qb).to(gpu)
+    out = ops.attn_prefill(q, None, kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens), scale,
+                           tile_map=tm, qb=qb)
+    out_r = ref.attn_prefill(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale)
+    _close(out, out_r, 2e-2, 2e-2, f"prefill-m32-{nh}/{nkv}-qb{qb}-ramp{ramp}")
+    with ops.kernel_policy(prefill_m32=False):
+        out_l = ops.attn_prefill(q, None, kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens),
+                                 scale, tile_map=tm, qb=qb)
+    _close(out, out_l, 2e-2, 2e-2, "prefill-m32-vs-legacy")
+    # dense grid (no tile map) gives the same result
+    out_d = ops.attn_prefill(q, None, kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens),
+                             scale, qb=qb)
+    assert torch.equal(out, out_d)
+
+
 def test_attn_prefill_fp8_kv(gpu):
     torch.manual_seed(13)
     nh, nkv, D, bs = 32, 8, 128, 64
