@@ -150,8 +150,11 @@ def build_block_app(worker, rebalance=None, token=None):
                 return out
             return pack_tensor(y.to(x.dtype))
 
+        from .worker import WorkerMoving
         try:
             out = await asyncio.get_running_loop().run_in_executor(None, run)
+        except WorkerMoving as e:   # loading another range: re-resolve (not a dead server)
+            raise HTTPException(409, f"moving: {e}")
         except (ValueError, MemoryError) as e:   # a bad request / no KV room: the client's call
             raise HTTPException(422, f"{type(e).__name__}: {e}")
         except KeyError as e:   # the worker moved while this request walked its blocks
@@ -182,7 +185,9 @@ def rebalance_once(worker, registry, url: str, max_layers: int, moving) -> Optio
     try:
         old = (worker.start, worker.end)
         try:
-            worker.move_to(*target)
+            # re-checked under the worker's swap lock: a session opened since the check above
+            # (or during the load, which refuses new sessions) abandons the move
+            worker.move_to(*target, require_idle=True)
         except Exception:   # noqa: BLE001 - e.g. no memory for the new layers: stay
             log.exception("move [%d, %d) -> %s failed; staying", old[0], old[1], target)
         registry.announce(worker.spec.name, url, worker.start, worker.end,
@@ -332,16 +337,66 @@ class RemoteBlocks:
         r.raise_for_status()
 
 
+class ReplayFailure(HopFailure):
+    """A replacement server failed while a session's history was replayed into it."""
+
+    def __init__(self, msg: str, url: str):
+        super().__init__(msg)
+        self.url = url
+
+
+def _concat_history(inputs: List[tuple]) -> Optional[tuple]:
+    """One chunk equivalent to a session's recorded steps into a layer range: the hidden inputs
+    concatenated along T, the 2-D padding masks along T (ones where a step had none), and the
+    RoPE positions every step used - its explicit ``position_ids``, else the server's default
+    (tokens cached so far + arange over the step's real tokens).  Replayed as ONE chunked
+    prefill, this writes the same KV as the steps did one by one (causal attention over the
+    same keys).  None when a step carried a 4-D mask (no single-chunk equivalent)."""
+    hs, ams, poss = [], [], []
+    seen = None   # per row: real tokens cached so far
+    for h, kw in inputs:
+        B, T = h.shape[0], h.shape[1]
+        am = kw.get("attention_mask")
+        if am is not None and am.dim() != 2:
+            return None
+        am = torch.ones(B, T, dtype=torch.bool) if am is None else am[:, -T:].to(torch.bool)
+        if seen is None:
+            seen = torch.zeros(B, dtype=torch.long)
+        pid = kw.get("position_ids")
+        if pid is not None:
+            pos = pid[:, -T:].to(torch.long).expand(B, -1)
+        else:
+            pos = seen[:, None] + torch.cumsum(am.to(torch.long), 1) - 1
+        seen = seen + am.sum(1)
+        hs.append(h)
+        ams.append(am)
+        poss.append(pos)
+    kw = {"position_ids": torch.cat(poss, 1)}
+    am = torch.cat(ams, 1)
+    if not bool(am.all()):
+        kw["attention_mask"] = am.to(torch.long)
+    return torch.cat(hs, 1), kw
+
+
 class RemoteSequential:
     """A chain of block servers covering consecutive layer ranges (the swarm's client side).
 
     With a ``registry`` (``from_registry``) a failed hop is replaced by ready servers from the
     registry and the session's history is replayed into them (module docstring); without one a
-    failure closes the session on the surviving servers and raises."""
+    failure closes the session on the surviving servers and raises.
+
+    History and its memory bound: per open session the client keeps the inputs it sent to each
+    layer range (hidden ``[B, T, H]`` + the stage kwargs of every step) - ``T_total x H x 2``
+    bytes per range in bf16, e.g. 16 KB per token per range for a 70B model.  A session whose
+    recorded tokens exceed ``max_history_tokens`` drops its history and can no longer be
+    recovered: if its range fails it is closed on every surviving server and a later forward on
+    it raises (``lost``).  ``close_session`` frees the history.  On failover every session's
+    history for the failed range is replayed as ONE concatenated chunk per replacement server
+    (a chunked prefill; one call per server and session, whatever the number of steps)."""
 
     def __init__(self, urls: Sequence[str], timeout: float = 120.0, registry=None,
                  model: Optional[str] = None, failover_wait_s: float = 30.0,
-                 max_failovers: int = 4):
+                 max_failovers: int = 4, max_history_tokens: int = 32768):
         self.timeout = timeout
         self.servers: List[RemoteBlocks] = [RemoteBlocks(u, timeout) for u in urls]
         infos = [s.info() for s in self.servers]
@@ -355,15 +410,20 @@ class RemoteSequential:
         self.start, self.end = infos[0]["start"], infos[-1]["end"]
         self.registry, self.model = registry, model or infos[0]["model"]
         self.failover_wait_s, self.max_failovers = failover_wait_s, max_failovers
+        self.max_history_tokens = max_history_tokens
         # per session: the inputs sent to each layer range, in order (hidden, kwargs)
         self._history: Dict[str, Dict[Tuple[int, int], List[tuple]]] = {}
+        self._hist_tokens: Dict[str, int] = {}
+        self.unrecoverable: set = set()   # sessions past max_history_tokens (no history kept)
+        self.lost: set = set()            # sessions closed by a failover they could not survive
         self.dead: set = set()
         self.failovers = 0
+        self.replay_calls = 0             # /forward calls made by replays (tests, metrics)
 
     @classmethod
     def from_registry(cls, registry_url: str, model: str, timeout: float = 120.0,
                       wait_s: float = 0.0, token: Optional[str] = None,
-                      failover_wait_s: float = 30.0) -> "RemoteSequential":
+                      failover_wait_s: float = 30.0, **kw) -> "RemoteSequential":
         """The chain of ready servers listed by a block registry (server/registry.py) that
         covers ``model`` from layer 0 to its last layer; ``wait_s``: keep polling that long
         for the swarm to cover it.  The registry also serves failed hops' replacements."""
@@ -375,10 +435,15 @@ class RemoteSequential:
         except ValueError:
             name = model
         deadline = time.monotonic() + wait_s
+        gone: set = set()   # listed until their ttl lapses, but not answering
         while True:
-            entries = reg.servers(name)
+            entries = [e for e in reg.servers(name) if e["url"] not in gone]
             L = max([int(e["num_layers"]) for e in entries] + [0])
             chain = find_chain(entries, L) if L else []
+            dead = [e["url"] for e in chain if not RemoteBlocks(e["url"], 5.0).healthy()]
+            if dead:
+                gone.update(dead)
+                continue
             if chain or time.monotonic() >= deadline:
                 break
             time.sleep(0.5)
@@ -386,7 +451,7 @@ class RemoteSequential:
             raise LookupError(f"registry {registry_url} lists no chain of ready servers covering "
                               f"{name} (servers: {[(e['start'], e['end']) for e in entries]})")
         return cls([e["url"] for e in chain], timeout=timeout, registry=reg, model=name,
-                   failover_wait_s=failover_wait_s)
+                   failover_wait_s=failover_wait_s, **kw)
 
     # ------------------------------------------------------------------ forward
     def forward(self, generation_id: str, hidden: torch.Tensor,
@@ -395,12 +460,28 @@ class RemoteSequential:
                 output_hidden_states: bool = False):
         """Walk the chain (the reference stage API over the whole model range).  Returns the
         hidden states, or ``(hidden, all_hidden_states)`` with ``output_hidden_states``."""
+        if generation_id in self.lost:
+            raise RuntimeError(f"session {generation_id!r} was lost in a failover (its history "
+                               f"exceeded max_history_tokens={self.max_history_tokens})")
         kw = {}
         if attention_mask is not None:
             kw["attention_mask"] = attention_mask
         if position_ids is not None:
             kw["position_ids"] = position_ids
-        hist = self._history.setdefault(generation_id, {})
+        keep = generation_id not in self.unrecoverable
+        if keep:
+            n = self._hist_tokens.get(generation_id, 0) + int(hidden.shape[1])
+            if n > self.max_history_tokens:
+                keep = False
+                self.unrecoverable.add(generation_id)
+                self._history.pop(generation_id, None)
+                self._hist_tokens.pop(generation_id, None)
+                log.warning("session %r: history past %d tokens dropped; it can no longer be "
+                            "recovered from a server failure", generation_id,
+                            self.max_history_tokens)
+            else:
+                self._hist_tokens[generation_id] = n
+        hist = self._history.setdefault(generation_id, {}) if keep else None
         hs: list = []
         i = 0
         while i < len(self.servers):
@@ -410,8 +491,12 @@ class RemoteSequential:
                                 **kw)
             except HopFailure as e:
                 self._failover(i, generation_id, e)
+                if generation_id in self.lost:
+                    raise RuntimeError(f"session {generation_id!r} was lost in the failover of "
+                                       f"{e}") from e
                 continue   # the replacement chain now sits at position i
-            hist.setdefault(s.range, []).append((hidden, kw))
+            if hist is not None:
+                hist.setdefault(s.range, []).append((hidden, kw))
             if output_hidden_states:
                 out, h = out
                 hs = hs[:-1] + list(h)
@@ -424,8 +509,9 @@ class RemoteSequential:
     def _failover(self, i: int, generation_id: str, err: Exception) -> None:
         """Replace hop ``i`` (its layer range) with ready servers from the registry and replay
         the history of EVERY open session into them (their KV for this range was on the dead
-        server).  Raises - after closing the sessions on the surviving servers - when no
-        replacement can be found."""
+        server).  Every replacement whose replay fails is excluded; attempts are bounded by
+        ``max_failovers`` and ``failover_wait_s``.  Raises - after closing the sessions on the
+        surviving servers - when no replacement can be found."""
         failed = self.servers[i]
         a, b = failed.range
         if not isinstance(err, HopMoved):   # a moved server is alive, just elsewhere now
@@ -434,18 +520,22 @@ class RemoteSequential:
                     b, err)
         last_err: Exception = err
         deadline = time.monotonic() + self.failover_wait_s
-        while self.registry is not None and self.failovers < self.max_failovers:
+        attempts = 0
+        while (self.registry is not None and self.failovers < self.max_failovers
+               and attempts < self.max_failovers and time.monotonic() <= deadline):
             repl = self._resolve(a, b)
             if repl is None:
-                if time.monotonic() > deadline:
-                    break
                 time.sleep(0.5)
                 continue
+            attempts += 1
             try:
-                self._replay(repl)
-            except HopFailure as e2:   # the replacement died too: exclude it and retry
-                self.dead.update(s.url for s in repl if not s.healthy())
+                self._replay(repl, (a, b))
+            except HopFailure as e2:
+                # the server that failed the replay is out whatever its /health says (a
+                # persistent 5xx on /forward, a timeout, or a move behind a 409)
+                self.dead.add(getattr(e2, "url", None) or repl[0].url)
                 last_err = e2
+                time.sleep(0.5)
                 continue
             self.servers[i:i + 1] = repl
             self.failovers += 1
@@ -471,24 +561,67 @@ class RemoteSequential:
                 return None
         return repl
 
-    def _replay(self, repl: List[RemoteBlocks]) -> None:
-        """Rebuild every open session's KV on the replacement servers: feed each server, in
-        order, the inputs the failed range received (the outputs of server k are the inputs of
-        server k+1); record them as the new ranges' history."""
-        a, b = repl[0].range[0], repl[-1].range[1]
-        for gid, hist in self._history.items():
-            inputs = hist.pop((a, b), [])
-            for s in repl:
-                hist[s.range] = list(inputs)
-                nxt = []
-                for h, kw in inputs:
-                    s_gid_out = s.forward(gid, h, **kw)
-                    nxt.append((s_gid_out, kw))
-                inputs = nxt
+    def _replay(self, repl: List[RemoteBlocks], rng: Tuple[int, int]) -> None:
+        """Rebuild every open session's KV for layer range ``rng`` on the replacement servers:
+        each server, in order, gets the session's recorded inputs for the range as ONE chunk
+        (:func:`_concat_history`; per step only for 4-D masks) - the outputs of server k are the
+        inputs of server k+1.  Atomic: the new ranges' history is committed only when every
+        session has replayed; on a failure the sessions already replayed are closed on the
+        replacements (no duplicated KV on a retry) and :class:`ReplayFailure` names the server.
+        Sessions that kept no history (``unrecoverable``) are closed everywhere and ``lost``."""
+        new_hist: Dict[str, Dict[Tuple[int, int], List[tuple]]] = {}
+        done: List[str] = []
+        try:
+            for gid, hist in self._history.items():
+                inputs = hist.get(rng, [])
+                if not inputs:
+                    continue
+                per = {}
+                cat = _concat_history(inputs)
+                for s in repl:
+                    steps = [cat] if cat is not None else inputs
+                    per[s.range] = [cat] if cat is not None else list(inputs)
+                    outs = []
+                    for h, kw in steps:
+                        try:
+                            y = s.forward(gid, h, **kw)
+                        except HopFailure as e:
+                            raise ReplayFailure(f"replay of {gid!r} into {s.url}: {e}", s.url) from e
+                        self.replay_calls += 1
+                        outs.append((y, kw))
+                    if cat is not None:
+                        cat = outs[0]
+                    else:
+                        inputs = outs
+                done.append(gid)
+                new_hist[gid] = per
+        except HopFailure:
+            for gid in done:
+                for s in repl:
+                    try:
+                        s.close_session(gid)
+                    except Exception:  # noqa: BLE001 - best effort: it may be the failed one
+                        pass
+            raise
+        for gid, per in new_hist.items():
+            hist = self._history[gid]
+            hist.pop(rng, None)
+            hist.update(per)
+        for gid in list(self.unrecoverable):
+            if gid in self.lost:
+                continue
+            self.lost.add(gid)
+            for s in self.servers:
+                if s.url in self.dead:
+                    continue
+                try:
+                    s.close_session(gid)
+                except Exception:  # noqa: BLE001
+                    pass
 
     def _abandon(self, exclude=()) -> None:
         """Close every session on the servers still alive (no orphaned KV)."""
-        for gid in list(self._history):
+        for gid in set(self._history) | self.unrecoverable:
             for s in self.servers:
                 if s.url in exclude or s.url in self.dead:
                     continue
@@ -497,8 +630,14 @@ class RemoteSequential:
                 except Exception:  # noqa: BLE001 - best effort: the server may be gone too
                     pass
         self._history.clear()
+        self._hist_tokens.clear()
 
     def close_session(self, generation_id: str) -> None:
         self._history.pop(generation_id, None)
+        self._hist_tokens.pop(generation_id, None)
+        self.unrecoverable.discard(generation_id)
+        if generation_id in self.lost:
+            self.lost.discard(generation_id)
+            return
         for s in self.servers:
             s.close_session(generation_id)

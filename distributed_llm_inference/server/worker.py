@@ -24,6 +24,10 @@ from .backend import BatchTensorDescriptor, InferenceBackend
 log = logging.getLogger(__name__)
 
 
+class WorkerMoving(RuntimeError):
+    """The worker is loading another layer range (swarm rebalancing): no new sessions now."""
+
+
 class Block(TypedDict):
     block_index: int
     block_id: str
@@ -52,6 +56,10 @@ class InferenceWorker:
         self._swap = threading.Lock()
         self.block_ids, self.blocks = self._load_range(block_index_start, block_index_end)
         self._running = False
+        # set for the whole of a move (load + swap): forwards that would open a session are
+        # refused (WorkerMoving -> HTTP 409), so nothing opened meanwhile is dropped by the swap
+        self.moving = False
+        self._inflight = 0   # submitted tasks not yet finished (a move also waits for these)
 
     def _load_range(self, start: int, end: int) -> Tuple[List[Block], Dict[str, InferenceBackend]]:
         kw = self._load_kw
@@ -76,25 +84,44 @@ class InferenceWorker:
             block_ids.append(Block(block_index=s, block_id=bid))
         return block_ids, blocks
 
-    def move_to(self, start: int, end: int) -> None:
+    def move_to(self, start: int, end: int, require_idle: bool = False) -> bool:
         """Serve layers ``[start, end)`` instead (swarm rebalancing, server/registry.py
         ``rebalance_target``): the new blocks are loaded while the old ones keep serving, then
         swapped in; the old pools finish what was submitted to them and stop.  Sessions open on
-        the old range lose their KV - the block server moves only when it holds none, and a
-        client whose chain still points here gets 409 and fails over (server/block_server.py)."""
+        the old range lose their KV - so while the move runs no new session is admitted
+        (:class:`WorkerMoving`), and with ``require_idle`` the move is abandoned (False) if a
+        session still holds KV when the swap would happen (checked under the swap lock, so no
+        forward can slip in between).  A client whose chain still points here gets 409 and
+        fails over (server/block_server.py)."""
         if not (0 <= start < end <= self.spec.num_layers):
             raise ValueError(f"bad block range [{start}, {end})")
-        block_ids, blocks = self._load_range(start, end)
-        if self._running:
-            for be in blocks.values():
-                be.inference_pool.start()
         with self._swap:
-            old = self.blocks
-            self.block_ids, self.blocks = block_ids, blocks
-            self.start, self.end = start, end
+            if require_idle and not self._idle():
+                return False
+            self.moving = True
+        try:
+            block_ids, blocks = self._load_range(start, end)
+            if self._running:
+                for be in blocks.values():
+                    be.inference_pool.start()
+            with self._swap:
+                if require_idle and not self._idle():
+                    abandon, old = blocks, None
+                else:
+                    abandon, old = None, self.blocks
+                    self.block_ids, self.blocks = block_ids, blocks
+                    self.start, self.end = start, end
+        finally:
+            self.moving = False
+        if abandon is not None:
+            for be in abandon.values():
+                be.shutdown()
+            log.info("move to [%d, %d) abandoned: sessions opened meanwhile", start, end)
+            return False
         for be in old.values():
             be.shutdown()
         log.info("worker now serves layers [%d, %d)", start, end)
+        return True
 
     def run(self) -> None:
         for be in self.blocks.values():
@@ -109,37 +136,64 @@ class InferenceWorker:
     def is_healthy(self) -> bool:
         return self._running and all(be.inference_pool.is_alive for be in self.blocks.values())
 
+    def _submit(self, blocks: Dict[str, InferenceBackend], block_id: str, generation_id: str,
+                hidden: torch.Tensor, kw: dict):
+        with self._swap:
+            if self.moving and not any(generation_id in be.cache._sessions
+                                       for be in blocks.values() if be.cache is not None):
+                raise WorkerMoving(f"moving from layers [{self.start}, {self.end}): no new "
+                                   "sessions")
+            fut = blocks[block_id].submit(hidden, generation_id=generation_id, **kw)
+            self._inflight += 1
+        fut.add_done_callback(self._task_done)
+        return fut
+
+    def _task_done(self, _fut) -> None:
+        with self._swap:
+            self._inflight -= 1
+
+    def _idle(self) -> bool:
+        """No session holds KV and no task is queued or running (call under ``_swap``)."""
+        return self._inflight == 0 and not self._sessions_of(self.blocks)
+
     def forward(self, block_id: str, generation_id: str, hidden: torch.Tensor, **kw):
         """One block.  ``kw``: the reference stage API's ``attention_mask`` / ``position_ids`` /
         ``output_hidden_states`` (reference models/llama/model.py:25-33).  Returns the hidden
         states, or ``(hidden, all_hidden_states)`` with ``output_hidden_states``."""
-        with self._swap:
-            fut = self.blocks[block_id].submit(hidden, generation_id=generation_id, **kw)
-        res = fut.result()
+        res = self._submit(self.blocks, block_id, generation_id, hidden, kw).result()
         if kw.get("output_hidden_states"):
             return res[0], tuple(res[1])
         return res[0]
 
     def forward_range(self, generation_id: str, hidden: torch.Tensor, **kw):
         """Run every block of this worker in order (the whole stage); with
-        ``output_hidden_states`` the per-layer inputs of every block and the final output."""
+        ``output_hidden_states`` the per-layer inputs of every block and the final output.  The
+        walk uses ONE snapshot of the blocks: a move that swaps them meanwhile cannot hand it a
+        same-named block of the new range (which holds no KV for the session)."""
         want = bool(kw.get("output_hidden_states"))
+        with self._swap:
+            block_ids, blocks = list(self.block_ids), self.blocks
         hs: list = []
-        for b in list(self.block_ids):
-            out = self.forward(b["block_id"], generation_id, hidden, **kw)
+        for b in block_ids:
+            res = self._submit(blocks, b["block_id"], generation_id, hidden, kw).result()
+            out = (res[0], tuple(res[1])) if want else res[0]
             if want:
                 out, blk_hs = out
                 hs = hs[:-1] + list(blk_hs)   # a block's first entry is the previous output
             hidden = out
         return (hidden, tuple(hs)) if want else hidden
 
-    def sessions(self) -> List[str]:
-        """The generation ids holding KV on any block of this worker."""
+    @staticmethod
+    def _sessions_of(blocks: Dict[str, InferenceBackend]) -> List[str]:
         ids = set()
-        for be in self.blocks.values():
+        for be in blocks.values():
             if be.cache is not None:
                 ids.update(k for k in be.cache._sessions if k != "__schema__")
         return sorted(ids)
+
+    def sessions(self) -> List[str]:
+        """The generation ids holding KV on any block of this worker."""
+        return self._sessions_of(self.blocks)
 
     def close_session(self, generation_id: str) -> None:
         for be in self.blocks.values():

@@ -96,6 +96,48 @@ def test_inference_worker_routes_blocks():
     w.shutdown()
 
 
+def test_worker_move_refuses_new_sessions_and_abandons_when_not_idle():
+    """ADVICE r5 (rebalance race): while a move loads its layers no new session is admitted
+    (WorkerMoving -> HTTP 409 at the block server); a session that slips in before the move
+    started makes the move abandon at the swap (checked under the swap lock); an idle worker
+    moves; a range walk keeps one snapshot of the blocks."""
+    from distributed_llm_inference.server.worker import WorkerMoving
+    w = InferenceWorker(SPEC, 0, 2, device="cpu")
+    w.run()
+    h = torch.randn(1, 2, 128, dtype=torch.bfloat16)
+    real_load = w._load_range
+    gate = threading.Event()
+    entered = threading.Event()
+
+    def slow_load(a, b):
+        entered.set()
+        gate.wait(30)
+        return real_load(a, b)
+
+    w._load_range = slow_load
+    res = {}
+    th = threading.Thread(target=lambda: res.setdefault("moved", w.move_to(2, 4, require_idle=True)))
+    th.start()
+    assert entered.wait(30)
+    with pytest.raises(WorkerMoving):
+        w.forward_range("new", h)
+    # a session that was admitted before the move: simulate it appearing during the load
+    w.moving = False
+    w.forward_range("early", h)
+    w.moving = True
+    gate.set()
+    th.join(60)
+    assert res["moved"] is False and (w.start, w.end) == (0, 2)
+    assert w.sessions() == ["early"] and not w.moving
+    w.close_session("early")
+    w._load_range = real_load
+    assert w.move_to(2, 4, require_idle=True) is True and (w.start, w.end) == (2, 4)
+    out = w.forward_range("after", h)
+    assert out.shape == h.shape
+    w.close_session("after")
+    w.shutdown()
+
+
 def _engine():
     cfg = EngineConfig(model="t", cache=CacheConfig(num_blocks=128, block_size=32),
                        serve=ServeConfig(max_batch_size=8, max_num_batched_tokens=128,
