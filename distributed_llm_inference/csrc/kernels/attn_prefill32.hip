@@ -46,14 +46,8 @@ namespace {
 
 constexpr int P32_D = 128;
 constexpr float P32_THR = 8.f;   // deferred-max threshold (log2 domain)
-#ifndef P32_PIPE
-#define P32_PIPE 0   // 1: the software-pipelined loop (measured slower, see the A/B in profiles/r6/)
-#endif
-#ifndef P32_EARLYDMA
-#define P32_EARLYDMA 0   // 1: issue the next step's DMA before this step's MFMAs
-#endif
-#ifndef P32_KO
-#define P32_KO 0   // diagnosis builds only: 1 = no softmax (P = S), 2 = no DMA in the loop
+#ifndef P32_STAGGER
+#define P32_STAGGER 1   // 0: every wave runs S | softmax | PV in the same order
 #endif
 #ifndef P32_PRIO
 #define P32_PRIO 0   // 1: static s_setprio 1 for the second half of the waves
@@ -82,8 +76,11 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   constexpr int CH = D / 8;                 // 16-B chunks per K row
   constexpr int NW = GW * TQ / 32;          // waves per workgroup
   constexpr int DPW = 32 / NW;              // LDS-DMA wave-instructions per wave per step
-  // [buf][K | V^T][64 keys x D]: 2 x 2 x 16 KB
-  __shared__ __attribute__((aligned(16))) bf16 smem[2][2][64 * D];
+  // staggered waves (8-wave workgroups, one per CU) keep V(s-1) while step s+1 lands: 3 buffers
+  constexpr bool STAG = P32_STAGGER && NW == 8;
+  constexpr int NBUF = STAG ? 3 : 2;
+  // [buf][K | V^T][64 keys x D]: NBUF x 2 x 16 KB
+  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF][2][64 * D];
 
   const int G = p.nh / p.nkv;
   const int wg_per_kv = G / GW;
@@ -168,6 +165,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
                                        16, 0, 0);
     }
   };
+  auto bufi = [&](int s) { return NBUF == 2 ? (s & 1) : (s % 3); };
   auto kbuf = [&](int i) { return &smem[i][0][0]; };
   auto vbuf = [&](int i) { return &smem[i][1][0]; };
 
@@ -182,197 +180,39 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   const int voff = (hh * D + c) * 8;
   auto full2 = [&](int s) { return s * 64 + 32 <= pq_hi; };   // second half holds a visible key
   auto diag = [&](int s) { return s * 64 + 63 > pq_lo; };     // some key past some column
-#if P32_PIPE
-  // Software pipeline (cdna_hip_programming.md T15): iteration s runs
-  //   phase 1: S(s+1) = K(s+1) Q^T on the matrix pipe  ||  P(s) = exp2(S(s) sl2 - m) on the VALU
-  //   phase 2: O^T += V^T(s) P^T(s) on the matrix pipe   ||  mask + row max of S(s+1) (the
-  //            cross-lane step: one bpermute) and the deferred-max decision for step s+1
-  // so neither pipe waits for the other inside a wave.  K runs two steps ahead of V in the DMA
-  // (K(s+2) and V(s+1) are fetched during iteration s), so each DMA overwrites a buffer that was
-  // last read before the previous barrier.
-  f32x16 ca, cb;
-  float m_cur = -1e30f, alpha = 0.f;
-  bool resc = true;
-  // mask (diagonal steps) and row max of S(s); sets the running max / rescale for step s
-  auto smax = [&](int s, bool mask, f32x16& sa, f32x16& sb) {
-    const int kb = s * 64;
-    if (mask) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb + 16 * (r >> 3) + 8 * hh + (r & 7);
-        sa[r] = key > pq ? -INFINITY : sa[r];
-        sb[r] = key + 32 > pq ? -INFINITY : sb[r];   // (a never-loaded half: every key masked)
-      }
-    }
-    float mx = fmaxf(sa[0], sb[0]);
-#pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(sa[r], sb[r]));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float pmax = mx * sl2;
-    // deferred max (T13): move the running max only when some column grew by more than THR
-    resc = __any(pmax > m_cur + P32_THR);
-    const float m_new = resc ? fmaxf(m_cur, pmax) : m_cur;
-    alpha = __builtin_amdgcn_exp2f(m_cur - m_new);
-    m_cur = m_new;
-  };
-  auto s_mfma = [&](const bf16* kt, f32x16& sa, f32x16& sb) {
-    sa = f32x16{};
-    sb = f32x16{};
-#pragma unroll
-    for (int m = 0; m < D / 16; ++m) {
-      const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kt + koff + ((2 * m + hh) ^ kx) * 8);
-      const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(kt + 32 * CH * 8 + koff +
-                                                         ((2 * m + hh) ^ kx) * 8);
-      sa = mfma32(k0, qf[m], sa);
-      sb = mfma32(k1, qf[m], sb);
-    }
-  };
-  dma(0, kbuf(0), false);
-  dma(0, vbuf(0), true);
-  if (nsteps > 1) dma(1, kbuf(1), false);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // S(0): the second half's K may never have been loaded (one-step tiles): its scores are masked
-  s_mfma(kbuf(0), ca, cb);
-  smax(0, diag(0), ca, cb);
-  __syncthreads();   // every wave is done with K(0) before iteration 0 refills its buffer
-
-  auto iter = [&](int s, auto maskn_c, auto next_c) {
-    constexpr bool MASKN = decltype(maskn_c)::value;   // step s+1 needs the causal mask
-    constexpr bool NEXT = decltype(next_c)::value;     // there is a step s+1
-    const int buf = s & 1;
-    if (s + 2 < nsteps) dma(s + 2, kbuf(buf), false);
-    if (NEXT) dma(s + 1, vbuf(buf ^ 1), true);
-    // ---- phase 1 (one basic block): S(s+1) MFMAs || P(s) ----
-    f32x16 na, nb;
-    if constexpr (NEXT) s_mfma(kbuf(buf ^ 1), na, nb);
-    float ps0 = 0.f, ps1 = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      ca[r] = __builtin_amdgcn_exp2f(fmaf(ca[r], sl2, -m_cur));
-      cb[r] = __builtin_amdgcn_exp2f(fmaf(cb[r], sl2, -m_cur));
-      ps0 += ca[r];
-      ps1 += cb[r];
-    }
-    l_run = l_run * alpha + (ps0 + ps1);
-    const bf16x8 p0 = pack8(ca, 0), p1 = pack8(ca, 8), p2 = pack8(cb, 0), p3 = pack8(cb, 8);
-    if constexpr (NEXT) {
-      // pin P(s) here (the scheduler would otherwise sink the exponentials to their use in
-      // phase 2, behind the rescale branch): 2 K reads ahead, then {MFMA, K read, 7 VALU} x 14,
-      // then {MFMA, 7 VALU} x 2
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-#pragma unroll
-      for (int i = 0; i < 14; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
-      }
-    }
-    asm volatile("" ::"v"(__builtin_bit_cast(i32x4, p0)), "v"(__builtin_bit_cast(i32x4, p1)),
-                 "v"(__builtin_bit_cast(i32x4, p2)), "v"(__builtin_bit_cast(i32x4, p3)), "v"(l_run));
-    // ---- phase 2: O^T = alpha O^T + V^T(s) P^T(s)  ||  max of S(s+1) ----
-    if (resc) {
-#pragma unroll
-      for (int db = 0; db < D / 32; ++db) o[db] *= alpha;
-    }
-    const bf16* vt = vbuf(buf);
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
-      const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(vt + voff + (0 * D + 32 * db) * 8);
-      const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(vt + voff + (2 * D + 32 * db) * 8);
-      o[db] = mfma32(v0, p0, o[db]);
-      o[db] = mfma32(v1, p1, o[db]);
-    }
-    // the second half: every step but a last one whose half is past every column (its V^T
-    // was never loaded - stale LDS must not reach the accumulators, even times zero)
-    if (NEXT || full2(s)) {
-#pragma unroll
-      for (int db = 0; db < D / 32; ++db) {
-        const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(vt + voff + (4 * D + 32 * db) * 8);
-        const bf16x8 v3 = *reinterpret_cast<const bf16x8*>(vt + voff + (6 * D + 32 * db) * 8);
-        o[db] = mfma32(v2, p2, o[db]);
-        o[db] = mfma32(v3, p3, o[db]);
-      }
-    }
-    if constexpr (NEXT) {
-      smax(s + 1, MASKN, na, nb);
-      // 2 V reads ahead, then {MFMA, V read, 3 VALU} x 14, then the rest
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-#pragma unroll
-      for (int i = 0; i < 14; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-      }
-      ca = na;
-      cb = nb;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs landed
-      __syncthreads();
-    }
-  };
-  // iterations whose next step is below every column's diagonal need no mask for it; the last
-  // step computes no S(s+1)
-  int s = 0;
-  for (; s + 1 < nsteps && !diag(s + 1); ++s) iter(s, std::false_type{}, std::true_type{});
-  for (; s + 1 < nsteps; ++s) iter(s, std::true_type{}, std::true_type{});
-  iter(s, std::false_type{}, std::false_type{});
-
-#else
-  // Plain loop: iteration s computes S(s), its softmax and O += V(s) P(s); the DMA of step s+1
-  // (K and V^T) is issued first into the other buffer.
+  // ---- the three products of one 64-key step ----
   float m_run = -1e30f;
-  dma(0, kbuf(0), false);
-  dma(0, vbuf(0), true);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  auto iter = [&](int s, auto mask_c) {
-    constexpr bool MASK = decltype(mask_c)::value;
-    const int buf = s & 1;
-    if (P32_EARLYDMA && s + 1 < nsteps) {
-      dma(s + 1, kbuf(buf ^ 1), false);
-      dma(s + 1, vbuf(buf ^ 1), true);
-    }
-    const bool f2 = full2(s);
-    const bf16* kt = kbuf(buf);
-    const bf16* vt = vbuf(buf);
+  // S^T(s) from K(s): fragments read ahead of their MFMAs; the second half only where it holds a
+  // visible key (its fragments are read anyway: an LDS read of a stale buffer is harmless)
+  auto scores = [&](int s, f32x16& sa, f32x16& sb) {
+    const bf16* kt = kbuf(bufi(s));
     bf16x8 ka[D / 16], kb8[D / 16];
 #pragma unroll
     for (int m = 0; m < D / 16; ++m)
       ka[m] = *reinterpret_cast<const bf16x8*>(kt + koff + ((2 * m + hh) ^ kx) * 8);
-    f32x16 sa = {}, sb = {};
+    sa = f32x16{};
+    sb = f32x16{};
 #pragma unroll
     for (int m = 0; m < D / 16; ++m) {
       kb8[m] = *reinterpret_cast<const bf16x8*>(kt + 32 * CH * 8 + koff + ((2 * m + hh) ^ kx) * 8);
       sa = mfma32(ka[m], qf[m], sa);
     }
-    // the next step's DMA is issued behind the first half's MFMAs: its block-table lookups
-    // (scalar loads waited in place) then overlap the matrix pipe instead of delaying it
-    if (!P32_EARLYDMA && P32_KO != 2 && s + 1 < nsteps) {
-      dma(s + 1, kbuf(buf ^ 1), false);
-      dma(s + 1, vbuf(buf ^ 1), true);
-    }
-    if (f2) {
+    if (full2(s)) {
 #pragma unroll
       for (int m = 0; m < D / 16; ++m) sb = mfma32(kb8[m], qf[m], sb);
     }
-    bf16x8 va[D / 32][2];
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
-      va[db][0] = *reinterpret_cast<const bf16x8*>(vt + voff + (0 * D + 32 * db) * 8);
-      va[db][1] = *reinterpret_cast<const bf16x8*>(vt + voff + (2 * D + 32 * db) * 8);
-    }
-    const int kb = s * 64;
-    if constexpr (MASK) {
+  };
+  // online softmax of S(s): causal mask on diagonal steps, row max (one cross-half exchange),
+  // deferred max (T13: the running max moves only when some column grew by more than THR),
+  // P = exp2(S sl2 - m) packed to bf16; l is rescaled here, O by the PV that consumes P
+  auto softmax = [&](int s, f32x16& sa, f32x16& sb, bf16x8 (&pp)[4], float& alpha, bool& resc) {
+    if (diag(s)) {
+      const int kb = s * 64;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kb + 16 * (r >> 3) + 8 * hh + (r & 7);
         sa[r] = key > pq ? -INFINITY : sa[r];
-        sb[r] = key + 32 > pq ? -INFINITY : sb[r];
+        sb[r] = key + 32 > pq ? -INFINITY : sb[r];   // (an unread half: every key masked)
       }
     }
     float mx = fmaxf(sa[0], sb[0]);
@@ -380,53 +220,91 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(sa[r], sb[r]));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float pmax = mx * sl2;
-    if (P32_KO != 1 && __any(pmax > m_run + P32_THR)) {
-      const float mn = fmaxf(m_run, pmax);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - mn);
-#pragma unroll
-      for (int db = 0; db < D / 32; ++db) o[db] *= alpha;
-      l_run *= alpha;
-      m_run = mn;
-    }
+    resc = __any(pmax > m_run + P32_THR);
+    const float m_new = resc ? fmaxf(m_run, pmax) : m_run;
+    alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    m_run = m_new;
     float ps0 = 0.f, ps1 = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      if (P32_KO != 1) sa[r] = __builtin_amdgcn_exp2f(fmaf(sa[r], sl2, -m_run));
+      sa[r] = __builtin_amdgcn_exp2f(fmaf(sa[r], sl2, -m_new));
+      sb[r] = __builtin_amdgcn_exp2f(fmaf(sb[r], sl2, -m_new));
       ps0 += sa[r];
+      ps1 += sb[r];
     }
-    const bf16x8 p0 = pack8(sa, 0), p1 = pack8(sa, 8);
+    l_run = l_run * alpha + (ps0 + ps1);
+    pp[0] = pack8(sa, 0);
+    pp[1] = pack8(sa, 8);
+    pp[2] = pack8(sb, 0);
+    pp[3] = pack8(sb, 8);
+  };
+  // O^T = alpha O^T + V^T(s) P^T(s); the second half only where it holds a visible key (a V^T
+  // image never loaded must not reach the accumulators, even times zero)
+  auto pv = [&](int s, const bf16x8 (&pp)[4], float alpha, bool resc) {
+    if (resc) {
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) o[db] *= alpha;
+    }
+    const bf16* vt = vbuf(bufi(s));
 #pragma unroll
     for (int db = 0; db < D / 32; ++db) {
-      o[db] = mfma32(va[db][0], p0, o[db]);
-      o[db] = mfma32(va[db][1], p1, o[db]);
+      const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(vt + voff + (0 * D + 32 * db) * 8);
+      const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(vt + voff + (2 * D + 32 * db) * 8);
+      o[db] = mfma32(v0, pp[0], o[db]);
+      o[db] = mfma32(v1, pp[1], o[db]);
     }
-    if (f2) {
+    if (full2(s)) {
 #pragma unroll
       for (int db = 0; db < D / 32; ++db) {
-        va[db][0] = *reinterpret_cast<const bf16x8*>(vt + voff + (4 * D + 32 * db) * 8);
-        va[db][1] = *reinterpret_cast<const bf16x8*>(vt + voff + (6 * D + 32 * db) * 8);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (P32_KO != 1) sb[r] = __builtin_amdgcn_exp2f(fmaf(sb[r], sl2, -m_run));
-        ps1 += sb[r];
-      }
-      const bf16x8 p2 = pack8(sb, 0), p3 = pack8(sb, 8);
-#pragma unroll
-      for (int db = 0; db < D / 32; ++db) {
-        o[db] = mfma32(va[db][0], p2, o[db]);
-        o[db] = mfma32(va[db][1], p3, o[db]);
+        const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(vt + voff + (4 * D + 32 * db) * 8);
+        const bf16x8 v3 = *reinterpret_cast<const bf16x8*>(vt + voff + (6 * D + 32 * db) * 8);
+        o[db] = mfma32(v2, pp[2], o[db]);
+        o[db] = mfma32(v3, pp[3], o[db]);
       }
     }
-    l_run += ps0 + ps1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step s+1 landed
-    __syncthreads();
   };
-  int s = 0;
-  for (; s < nsteps && !diag(s); ++s) iter(s, std::false_type{});
-  for (; s < nsteps; ++s) iter(s, std::true_type{});
+  auto dma_step = [&](int s) {   // K and V^T of step s into its buffer
+    dma(s, kbuf(bufi(s)), false);
+    dma(s, vbuf(bufi(s)), true);
+  };
 
-#endif
+  dma_step(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x16 sa, sb;
+  bf16x8 pp[4];
+  float alpha;
+  bool resc;
+  if (!STAG || w < NW / 2) {
+    // interval s: S(s) | softmax(s) | PV(s); the DMA of step s+1 is issued behind the first
+    // MFMAs, so its block-table lookups (scalar loads waited in place) overlap the matrix pipe
+    for (int s = 0; s < nsteps; ++s) {
+      scores(s, sa, sb);
+      if (s + 1 < nsteps) dma_step(s + 1);
+      softmax(s, sa, sb, pp, alpha, resc);
+      pv(s, pp, alpha, resc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step s+1 landed
+      __syncthreads();
+    }
+  } else {
+    // the stagger (MI355X_MICROARCH.md "Two waves per SIMD", item 9): waves NW/2.. (one per
+    // SIMD, paired with a wave of the first half) run interval s as softmax(s-1) | PV(s-1) |
+    // S(s), so each SIMD's two waves put vector work beside matrix work instead of both
+    // computing, then both exponentiating.  S(s-1) stays in registers across the barrier and
+    // V(s-1) in its buffer (three buffers: the DMA of interval s writes step s+1's).
+    for (int s = 0; s < nsteps; ++s) {
+      if (s > 0) {
+        softmax(s - 1, sa, sb, pp, alpha, resc);
+        pv(s - 1, pp, alpha, resc);
+      }
+      if (s + 1 < nsteps) dma_step(s + 1);
+      scores(s, sa, sb);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    softmax(nsteps - 1, sa, sb, pp, alpha, resc);
+    pv(nsteps - 1, pp, alpha, resc);
+  }
   // ---- normalise and store: register r of o[db] is d = 32 db + (r & 3) + 8 (r >> 2) + 4 hh ----
   float lsum = l_run + __shfl_xor(l_run, 32, 64);
   if (valid) {

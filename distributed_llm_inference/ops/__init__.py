@@ -307,6 +307,17 @@ def decode_workspace(rows: int, nh: int, head_dim: int, splits: int, device):
 
 PREFILL_QB = 1   # 16-token query blocks per prefill wave (attention.hip QB; 2 was +2 % on 2k-4k
                  # chunks but -25 % on 16-token ones: profiles/attn_prefill_qb_ab.json)
+PREFILL_QB_LONG = 1024   # from this longest chunk on, 32-token tiles (attn_prefill32.hip: 8 waves
+                         # per workgroup, staggered halves) beat 16-token ones (4 waves, two
+                         # workgroups per CU): 2k-on-6k 962-980 vs 935-954 TFLOP/s; below it
+                         # the 16-token tiles win (512-token prompts 414-432 vs 397)
+                         # (profiles/r6/prefill/)
+
+
+def prefill_qb_for(max_q: int) -> int:
+    """The prefill tile choice for a batch whose longest chunk is ``max_q`` tokens: one
+    function, so the tile map and the kernel launch always agree."""
+    return 2 if max_q >= PREFILL_QB_LONG else PREFILL_QB
 
 
 def prefill_tile_tokens(nh: int, nkv: int, qb: int = PREFILL_QB) -> int:
@@ -316,11 +327,13 @@ def prefill_tile_tokens(nh: int, nkv: int, qb: int = PREFILL_QB) -> int:
     return 16 * (4 // hpw) * qb
 
 
-def prefill_tiles(q_lens, nh: int, nkv: int, out=None, qb: int = PREFILL_QB) -> torch.Tensor:
+def prefill_tiles(q_lens, nh: int, nkv: int, out=None, qb: Optional[int] = None) -> torch.Tensor:
     """Compact (sequence, token-tile) work list of the prefill kernel: one row per tile that
     holds query tokens.  A 1-token decode row mixed into a prefill batch gets a single tile
     instead of ``max_q / tile`` empty workgroups.  Returns int32 [n_tiles, 2] (or fills ``out``)."""
     import numpy as np
+    if qb is None:
+        qb = prefill_qb_for(max(q_lens) if len(q_lens) else 0)
     tt = prefill_tile_tokens(nh, nkv, qb)
     ql = np.asarray(q_lens, dtype=np.int64)
     nt = (ql + tt - 1) // tt
@@ -336,7 +349,7 @@ def prefill_tiles(q_lens, nh: int, nkv: int, out=None, qb: int = PREFILL_QB) -> 
 
 def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, max_q, scale,
                  n_sink=0, sink_pad=0, ring=0, window=0, out=None, k_scale=1.0, v_scale=1.0,
-                 tile_map=None, mask=None, qb: int = PREFILL_QB):
+                 tile_map=None, mask=None, qb: Optional[int] = None):
     """Paged varlen prefill attention.  ``mask``: the reference API's pre-inverted 4-D additive
     mask ``[B, 1 | nh, T, >= L]`` (0 = attend, large negative = masked; the last ``q_len_b`` rows
     of sequence b) - it replaces the causal mask (full cache, any T incl. 1).  ``qb``: 16-token
@@ -350,6 +363,8 @@ def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, m
                                  scale, n_sink, sink_pad, ring, window, k_scale, v_scale)
         return out.copy_(y) if out is not None else y
     out = torch.empty_like(q) if out is None else out
+    if qb is None:
+        qb = prefill_qb_for(int(max_q))
     if mask is not None:
         if ring:
             raise ValueError("custom 4-D masks need a full (non-windowed) cache")

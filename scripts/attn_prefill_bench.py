@@ -18,7 +18,7 @@ nh, nkv, D, bs = 64, 8, 128, 64
 CASES = [(32, 512, 0), (4, 4096, 0), (1, 2048, 6144), (256, 16, 512)]
 if os.environ.get("CASES"):   # e.g. CASES="4x4096x0,1x32768x0"
     CASES = [tuple(int(x) for x in c.split("x")) for c in os.environ["CASES"].split(",")]
-QB = int(os.environ.get("QB", ops.PREFILL_QB))
+QB = int(os.environ["QB"]) if os.environ.get("QB") else None   # None: ops.prefill_qb_for
 
 
 def run(B, q, ctx):
@@ -49,7 +49,7 @@ def run(B, q, ctx):
     us = (time.perf_counter() - t0) / n * 1e6
     pairs = B * sum(ctx + i + 1 for i in range(q))
     tf = 4 * D * nh * pairs / us / 1e6
-    return dict(B=B, q=q, ctx=ctx, qb=QB, m32=int(ops.policy().prefill_m32), us=round(us, 1),
+    return dict(B=B, q=q, ctx=ctx, qb=QB or ops.prefill_qb_for(q), m32=int(ops.policy().prefill_m32), us=round(us, 1),
                 TFLOPs=round(tf, 1))
 
 
@@ -59,5 +59,5 @@ for c in CASES:
     print(r, flush=True)
     res.append(r)
 os.makedirs("gpurun_out", exist_ok=True)
-tag = os.environ.get("TAG", "qb%d_m32%d" % (QB, int(ops.policy().prefill_m32)))
+tag = os.environ.get("TAG", "qb%s_m32%d" % (QB or "auto", int(ops.policy().prefill_m32)))
 json.dump(res, open("gpurun_out/attn_prefill_bench_%s.json" % tag, "w"), indent=1)
