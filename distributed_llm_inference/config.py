@@ -50,6 +50,14 @@ class ModelSpec:
     o_proj_bias: Optional[bool] = None
     # Mistral-style sliding-window attention length (None = full causal attention)
     sliding_window: Optional[int] = None
+    # HF config.output_hidden_states: what LlamaBlock.forward does when its argument is None
+    # (reference models/llama/model.py:35-37)
+    output_hidden_states: bool = False
+
+    @property
+    def rope_type(self) -> Optional[str]:
+        rs = self.rope_scaling_dict
+        return None if not rs else rs.get("rope_type", rs.get("type"))
 
     @property
     def has_o_proj_bias(self) -> bool:
@@ -179,6 +187,7 @@ class ModelSpec:
             model_type=mt,
             o_proj_bias=False if qwen2 else None,
             sliding_window=int(sw) if sw else None,
+            output_hidden_states=bool(cfg.get("output_hidden_states", False)),
         )
 
     def to_hf_dict(self) -> Dict[str, Any]:
@@ -212,6 +221,7 @@ class ModelSpec:
             bos_token_id=self.bos_token_id, eos_token_id=self.eos_token_id,
             hidden_act=self.hidden_act, pretraining_tp=self.pretraining_tp,
             attention_bias=self.attention_bias, mlp_bias=self.mlp_bias,
+            output_hidden_states=self.output_hidden_states,
         )
 
 

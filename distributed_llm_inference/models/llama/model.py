@@ -45,7 +45,8 @@ class LlamaBlock(nn.Module):
         self.layers = nn.ModuleList(LlamaDecoderLayer(spec, i, device, dtype) for i in self.layer_ids)
         maxp = int(max_position or max(spec.max_position_embeddings, 8192))
         self.register_buffer("cos_sin", build_cos_sin(spec.head_dim, maxp, spec.rope_theta,
-                                                      spec.rope_scaling_dict, device=device),
+                                                      spec.rope_scaling_dict, device=device,
+                                                      max_position_embeddings=spec.max_position_embeddings),
                              persistent=False)
 
     # ------------------------------------------------------------------ construction helpers
@@ -97,9 +98,12 @@ class LlamaBlock(nn.Module):
     # ------------------------------------------------------------------ fast path
     def forward_tokens(self, hidden: torch.Tensor, meta: AttnMetadata, pool: KVPool,
                        residual: Optional[torch.Tensor] = None, layer_offset: int = 0,
-                       collect: Optional[list] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                       collect: Optional[list] = None,
+                       cos_sin: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
         """Run the local layers on packed tokens ``hidden [T, H]``.  Returns ``(out, residual)``;
-        the stage output hidden state is ``out + residual``."""
+        the stage output hidden state is ``out + residual``.  ``cos_sin``: this call's RoPE table
+        (dynamic NTK scaling) instead of the block's."""
+        cos_sin = self.cos_sin if cos_sin is None else cos_sin
         last = len(self.layers) - 1
         for i, layer in enumerate(self.layers):
             if collect is not None:
@@ -107,9 +111,24 @@ class LlamaBlock(nn.Module):
             k, v = pool.layer(layer_offset + i)
             # between layers the down projection's split-K partials go straight into the next
             # input RMSNorm; the block's output is always materialised
-            hidden, residual = layer(hidden, residual, meta, k, v, self.cos_sin,
+            hidden, residual = layer(hidden, residual, meta, k, v, cos_sin,
                                      defer_out=collect is None and i < last)
         return hidden, residual
+
+    def _dynamic_table(self, meta: AttnMetadata) -> Optional[torch.Tensor]:
+        """The RoPE table of one forward under dynamic NTK scaling: rebuilt with the rescaled
+        base when the call's longest position + 1 exceeds max_position_embeddings (HF
+        recomputes inv_freq from max(position_ids) + 1 the same way); None otherwise."""
+        spec = self.config
+        if spec.rope_type != "dynamic" or meta.positions.numel() == 0:
+            return None
+        seq_len = int(meta.positions.max()) + 1
+        if seq_len <= spec.max_position_embeddings:
+            return None
+        return build_cos_sin(spec.head_dim, max(seq_len, self.cos_sin.shape[0]), spec.rope_theta,
+                             spec.rope_scaling_dict, device=self.cos_sin.device,
+                             max_position_embeddings=spec.max_position_embeddings,
+                             seq_len=seq_len)
 
     # ------------------------------------------------------------------ reference API
     def forward(self, generation_id: str, hidden_states: torch.Tensor,
@@ -123,8 +142,15 @@ class LlamaBlock(nn.Module):
         ``attention_mask`` (optional, ``[B, T]`` or ``[B, past+T]``, 1 = real token) drops padded
         positions (their output rows are zero).  ``position_ids``/``cache_position`` override the
         default RoPE positions ``past_len + arange``.  Without ``past_key_value`` the call is
-        stateless (causal attention within the chunk only).
+        stateless (causal attention within the chunk only).  ``output_hidden_states=None`` takes
+        the config's ``output_hidden_states`` (reference model.py:35-37); the states are the L
+        layer inputs and the output (L+1 tensors), zeros for padded rows - all zeros when every
+        row is padding.  With ``rope_type: dynamic`` a call whose longest position exceeds
+        ``max_position_embeddings`` rotates with the NTK-rescaled base for that length (HF
+        ``dynamic_rope_update``).
         """
+        if output_hidden_states is None:
+            output_hidden_states = bool(getattr(self.config, "output_hidden_states", False))
         if hidden_states.dim() != 3:
             raise ValueError("hidden_states must be [batch, seq, hidden]")
         B, T, H = hidden_states.shape
@@ -185,8 +211,11 @@ class LlamaBlock(nn.Module):
         try:
             keep = [b for b in range(B) if q_lens[b] > 0]
             out_full = torch.zeros_like(hidden_states)
-            if not keep:
-                return (out_full,) if not output_hidden_states else (out_full, ())
+            if not keep:   # all padding: nothing cached; L + 1 zero states like a real call
+                if not output_hidden_states:
+                    return (out_full,)
+                return out_full, tuple(torch.zeros_like(hidden_states)
+                                       for _ in range(len(self.layers) + 1))
             sids = [rows[b] for b in keep]
             qls = [q_lens[b] for b in keep]
             meta = cache.pool.build_metadata(sids, qls)
@@ -198,7 +227,8 @@ class LlamaBlock(nn.Module):
                     torch.int32).contiguous()
             x = hidden_states[am].to(torch.bfloat16).contiguous()  # [T_total, H] packed
             collect = [] if output_hidden_states else None
-            out, res = self.forward_tokens(x, meta, cache.pool, collect=collect)
+            out, res = self.forward_tokens(x, meta, cache.pool, collect=collect,
+                                           cos_sin=self._dynamic_table(meta))
             y = ops.add(out, res)
         except BaseException:
             cache.unreserve_rows(generation_id, rows, q_lens, T)

@@ -268,9 +268,21 @@ def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
 
 # ----------------------------------------------------------------------------- rope table
 def build_cos_sin(head_dim: int, max_pos: int, theta: float, rope_scaling=None,
-                  device=None) -> torch.Tensor:
-    """fp32 table [max_pos, head_dim] = (cos | sin) of the rotate-half convention, with llama3
-    frequency scaling when configured (HF ``_compute_llama3_parameters`` semantics)."""
+                  device=None, max_position_embeddings: Optional[int] = None,
+                  seq_len: Optional[int] = None) -> torch.Tensor:
+    """fp32 table [max_pos, head_dim] = (cos | sin) of the rotate-half convention, with the
+    configured frequency scaling: llama3 (HF ``_compute_llama3_parameters``), linear, and
+    dynamic NTK (HF ``_compute_dynamic_ntk_parameters``: for a forward whose longest position is
+    ``seq_len`` > ``max_position_embeddings`` the base grows to theta * ((factor * seq_len /
+    max_pe) - (factor - 1)) ** (d / (d - 2)); the caller builds such a table per forward,
+    models/llama/model.py)."""
+    if rope_scaling and rope_scaling.get("rope_type", rope_scaling.get("type")) == "dynamic":
+        if max_position_embeddings is None:
+            raise ValueError("dynamic rope scaling needs max_position_embeddings")
+        if seq_len is not None and seq_len > max_position_embeddings:
+            f = float(rope_scaling["factor"])
+            theta = theta * ((f * seq_len / max_position_embeddings) - (f - 1)) ** (
+                head_dim / (head_dim - 2))
     inv_freq = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
     attn_factor = 1.0
     if rope_scaling:
@@ -290,7 +302,7 @@ def build_cos_sin(head_dim: int, max_pos: int, theta: float, rope_scaling=None,
         elif rt == "linear":
             inv_freq = inv_freq / rope_scaling["factor"]
         elif rt == "dynamic":
-            pass  # only changes beyond max_position_embeddings; tables are built per length
+            pass  # the base itself was rescaled above (seq_len past max_position_embeddings)
         else:
             raise ValueError(f"unsupported rope_scaling type {rt!r}")
     t = torch.arange(max_pos, dtype=torch.float64)

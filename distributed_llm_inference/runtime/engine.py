@@ -103,6 +103,13 @@ def build_executor(spec: ModelSpec, start: int, end: int, device: torch.device, 
         t = torch.tensor([num_blocks], dtype=torch.int64)
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
         num_blocks = int(t.item())
+    if spec.rope_type == "dynamic" and sc.max_seq_len > spec.max_position_embeddings:
+        # HF's dynamic NTK base depends on each forward's longest position, but the engine's
+        # captured decode steps read ONE RoPE table: serve such lengths through the reference
+        # API (LlamaBlock.forward rebuilds the table per call), or cap max_seq_len
+        raise ValueError(f"rope_type 'dynamic' past max_position_embeddings "
+                         f"({spec.max_position_embeddings}) is supported by LlamaBlock.forward "
+                         f"only; the engine needs max_seq_len <= it (got {sc.max_seq_len})")
     win, sinks = cc.window_length, cc.num_sink_tokens
     if not win and spec.sliding_window and sc.max_seq_len > spec.sliding_window:
         # Mistral-style sliding-window attention IS the ring window with no sink tokens (each
