@@ -31,6 +31,10 @@ import os
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 # per-rank device time per micro-batch step and RCCL receive stalls (HIP events; cheap)
 os.environ.setdefault("DLI_STAGE_TIMING", "1")
+# every hop's payload digested on both ends during prefill + warm-up, checked at the barrier that
+# opens the timed window (parallel/integrity.py): a corrupted or mis-routed pipeline fails the run
+# instead of reporting tokens/s.  Off inside the timed window.
+os.environ.setdefault("DLI_HOP_CHECK", "1")
 
 import argparse  # noqa: E402
 import json  # noqa: E402
@@ -108,6 +112,9 @@ def _rank_record(node, rank: int, window_s: float) -> dict:
         return rec
     rec.update({"stage": [ex.stage.start, ex.stage.end], "device": str(ex.device)})
     rec.update(node.tr.describe())
+    ig = getattr(node.tr, "integrity", None)
+    if ig is not None:
+        rec["hop_integrity"] = ig.summary()
     if len(node.snapshots) >= 2:
         from distributed_llm_inference.runtime.hostclock import per_step
         d = snapshot_delta(node.snapshots[-2], node.snapshots[-1])
@@ -299,7 +306,13 @@ def main():
         "kv_blocks": int(drv.sched.total_blocks),
         "kv_blocks_needed": int(G * drv.sched.blocks_for(a.prompt_len + params.max_tokens)),
     }
+    bad_hops = False
     if world > 1:
+        igs = [r["hop_integrity"] for r in per_rank if "hop_integrity" in r]
+        if igs:
+            res["hop_integrity"] = {k: sum(int(g.get(k, 0)) for g in igs)
+                                    for k in ("checked", "mismatch", "missing")}
+            bad_hops = res["hop_integrity"]["mismatch"] > 0 or res["hop_integrity"]["missing"] > 0
         res["stage_ranges"] = [r["stage"] for r in per_rank]
         res["head_rotation"] = any(r.get("head_rotation") for r in per_rank)
         fb = sorted({r["fallback_from"] for r in per_rank if r.get("fallback_from")})
@@ -321,6 +334,11 @@ def main():
     if world > 1:
         drv.close()
         dist.destroy_process_group()
+    if bad_hops:
+        print(f"ERROR: pipeline hop integrity failed: {res['hop_integrity']} (per rank: "
+              f"{[r.get('hop_integrity') for r in per_rank]})", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(5)
 
 
 if __name__ == "__main__":

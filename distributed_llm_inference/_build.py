@@ -31,7 +31,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 KERNEL_SOURCES = ["kernels/norm.hip", "kernels/activation.hip", "kernels/rope_cache.hip",
                   "kernels/attention.hip", "kernels/attn_prefill32.hip", "kernels/sampling.hip", "kernels/quant.hip",
                   "kernels/gemv.hip", "kernels/gemm_tile.hip", "kernels/gemm4.hip",
-                  "kernels/int8_outlier.hip"]
+                  "kernels/int8_outlier.hip", "kernels/digest.hip"]
 TORCH_SOURCES = ["bindings.hip", "comm/rccl_p2p.hip", "comm/streams.hip"]
 RUNTIME_SOURCES = ["runtime/block_manager.cpp", "runtime/shm_channel.cpp"]
 

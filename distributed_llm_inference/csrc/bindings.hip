@@ -477,6 +477,18 @@ void quant_rowwise(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> residu
            "quant_rowwise");
 }
 
+// Payload digest partials of the hop-integrity check (parallel/integrity.py): part [nblocks, 2]
+// int64 receives per-workgroup sums over t's 32-bit words; the host folds them (mod 2^64).
+void digest(Tensor part, Tensor t) {
+  CHECK_DEV(t); CHECK_CONTIG(t); CHECK_IN(part); CHECK_I64(part);
+  const int64_t nbytes = t.numel() * t.element_size();
+  TORCH_CHECK(nbytes % 4 == 0, "digest: payload must be a whole number of 32-bit words");
+  TORCH_CHECK(part.dim() == 2 && part.size(1) == 2 && part.size(0) >= 1, "digest: part must be [nblocks, 2]");
+  const c10::hip::HIPGuardMasqueradingAsCUDA g(t.device());
+  check_rc(dli::launch_digest(t.data_ptr(), (long)(nbytes / 4), part.data_ptr<int64_t>(),
+                              (int)part.size(0), cur_stream()), "digest");
+}
+
 void quant_rowwise_int8(Tensor q_out, Tensor scale, Tensor x, optional<Tensor> outlier) {
   CHECK_IN(q_out); CHECK_IN(scale); CHECK_IN(x); CHECK_BF16(x); CHECK_F32(scale);
   TORCH_CHECK(q_out.scalar_type() == at::kChar, "q_out must be int8");
@@ -974,6 +986,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample", &sample, "greedy / temperature / top-k / top-p sampling", py::arg("out_tokens"),
         py::arg("out_logprobs"), py::arg("logits"), py::arg("temperature"), py::arg("top_k"),
         py::arg("top_p"), py::arg("seeds"), py::arg("step"), py::arg("ctr") = py::none());
+  m.def("digest", &digest, "hop-integrity payload digest partials", py::arg("part"), py::arg("t"));
   m.def("quant_rowwise", &quant_rowwise, "row-wise fp8 e4m3 quantisation (+fused RMSNorm)",
         py::arg("q_out"), py::arg("scale"), py::arg("x"), py::arg("residual"), py::arg("norm_w"),
         py::arg("eps"), py::arg("residual_out") = py::none());

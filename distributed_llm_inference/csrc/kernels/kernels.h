@@ -87,6 +87,8 @@ int launch_silu_mul(bf16* out, const bf16* x, int rows, int inter, bool interlea
 int launch_gelu_bias(bf16* out, const bf16* x, const bf16* bias, int rows, int cols,
                      hipStream_t stream);
 int launch_add(bf16* out, const bf16* a, const bf16* b, size_t n, hipStream_t stream);
+// hop-integrity payload digest (digest.hip): [nblocks][2] int64 partial sums
+int launch_digest(const void* data, long nwords, int64_t* part, int nblocks, hipStream_t stream);
 int launch_rope_cache(const RopeCacheParams& p, int num_tokens, hipStream_t stream);
 int launch_attn_decode(const AttnParams& p, int B, int D, hipStream_t stream);
 int launch_attn_prefill(const AttnParams& p, int B, int max_q, int D, hipStream_t stream);

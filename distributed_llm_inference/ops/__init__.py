@@ -377,6 +377,21 @@ def attn_prefill(q, q_sink, k_cache, v_cache, block_tables, seq_lens, q_start, m
     return out
 
 
+# ----------------------------------------------------------------------------- payload digest
+def digest(t: torch.Tensor, nblocks: int = 256) -> torch.Tensor:
+    """Hop-integrity digest partials of ``t`` (csrc/kernels/digest.hip on the current stream;
+    torch on the CPU); fold them with :func:`digest_fold`.  Returns [nblocks, 2] int64."""
+    if not _gpu(t) or (t.numel() * t.element_size()) % 4:
+        return ref.digest_parts(t)
+    t = t.contiguous()
+    part = torch.empty(nblocks, 2, dtype=torch.int64, device=t.device)
+    native().digest(part, t)
+    return part
+
+
+digest_fold = ref.digest_fold
+
+
 # ----------------------------------------------------------------------------- sampling
 def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor] = None,
            top_k: Optional[torch.Tensor] = None, top_p: Optional[torch.Tensor] = None,

@@ -309,3 +309,26 @@ def build_cos_sin(head_dim: int, max_pos: int, theta: float, rope_scaling=None,
     freqs = torch.outer(t, inv_freq)
     cs = torch.cat([freqs.cos() * attn_factor, freqs.sin() * attn_factor], dim=-1)
     return cs.to(torch.float32).to(device) if device is not None else cs.to(torch.float32)
+
+
+# ----------------------------------------------------------------------------- payload digest
+_M64 = (1 << 64) - 1
+
+
+def digest_parts(t: torch.Tensor) -> torch.Tensor:
+    """[1, 2] int64: the two order-sensitive sums of csrc/kernels/digest.hip over ``t``'s 32-bit
+    words (the bytes, zero-padded to whole words), wrapped mod 2^64 in int64."""
+    b = t.detach().contiguous().reshape(-1).view(torch.uint8).cpu()
+    if b.numel() % 4:
+        b = torch.cat([b, torch.zeros(4 - b.numel() % 4, dtype=torch.uint8)])
+    w = b.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    i = torch.arange(w.numel(), dtype=torch.int64)
+    s1 = (w * (2 * i + 1)).sum()
+    s2 = ((w ^ 0x9E3779B9) * (((i * 0x85EBCA6B) & 0xFFFFFFFF) + 1)).sum()
+    return torch.stack([s1, s2]).view(1, 2)
+
+
+def digest_fold(parts: torch.Tensor) -> Tuple[int, int]:
+    """The digest (s1, s2) as unsigned 64-bit ints from per-workgroup partials [n, 2]."""
+    p = parts.detach().cpu().tolist()
+    return (sum(r[0] & _M64 for r in p) & _M64, sum(r[1] & _M64 for r in p) & _M64)

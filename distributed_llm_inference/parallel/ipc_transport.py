@@ -169,6 +169,7 @@ class IpcTransport(Transport):
         t = t.contiguous()
         self.send_stream.wait_stream(cur)
         t.record_stream(self.send_stream)
+        self._ig_send("stage", peer, t, self.send_stream)   # the bytes the send reads
         self._send_on(self._ch[("stage", self.rank, peer)], t, self.send_stream)
         self._count(t, True)
 
@@ -181,6 +182,7 @@ class IpcTransport(Transport):
             self.recv_stream.wait_stream(cur)
         t.record_stream(self.recv_stream)
         self._recv_on(self._ch[("stage", peer, self.rank)], t, self.recv_stream)
+        self._ig_recv("stage", peer, t, self.recv_stream)   # the bytes the next stage reads
         cur.wait_stream(self.recv_stream)
         self._count(t, False)
         return t
@@ -193,6 +195,7 @@ class IpcTransport(Transport):
         t = t.contiguous()
         self.send_stream.wait_stream(cur)
         t.record_stream(self.send_stream)
+        self._ig_send("head", peer, t, self.send_stream)
         self._send_on(self._ch[("head", self.rank, peer)], t, self.send_stream)
         self._count(t, True)
 
@@ -200,6 +203,7 @@ class IpcTransport(Transport):
         self.check()
         self._recv_on(self._ch[("head", peer, self.rank)], t, stream)
         self._count(t, False)
+        self._ig_recv("head", peer, t, stream)
         return t
 
     def check(self) -> None:

@@ -43,6 +43,7 @@ from ..runtime.hostclock import HOST
 from ..runtime.scheduler import Scheduler
 from ..runtime.sequence import SamplingParams, Sequence as Seq
 from ..runtime.watchdog import TRACKER, abort_job, wait_event
+from .integrity import flush as hop_flush
 from .transport import LoopbackTransport, RcclTransport, TorchDistTransport, Transport
 
 log = logging.getLogger(__name__)
@@ -328,6 +329,7 @@ class DistributedDriver(DriverBase):
         if self.ex.device.type == "cuda":
             torch.cuda.synchronize()
         if kind == "barrier":
+            hop_flush(self.tr)   # the warm-up's payload digests, checked once (integrity.py)
             dist.barrier(group=self.group)
             self.snapshots.append(self.stats.snapshot())
 
@@ -456,6 +458,7 @@ class StageFollower:
                 if self.ex.device.type == "cuda":
                     torch.cuda.synchronize()
                 self._pub_q.join()
+                hop_flush(self.tr)   # the warm-up's payload digests, checked once (integrity.py)
                 dist.barrier(group=self.group)
                 self.barrier_times.append(time.perf_counter())
                 self.snapshots.append(self.stats.snapshot())
@@ -593,6 +596,17 @@ def make_transport(rank: int, world: int, device: torch.device, job: str = "0",
     ``rank`` / ``world`` are the stage index and stage count of ONE pipeline replica; with several
     replicas (data parallel) ``rank_offset`` is the replica's first global rank and ``job`` names
     the replica, so every replica gets its own RCCL pair communicators."""
+    tr = _make_transport(rank, world, device, job, rccl_timeout_s, rank_offset, head_pairs,
+                         streams, max_bytes, head_bytes)
+    if world > 1:
+        from ..runtime.faults import raw_store
+        from .integrity import attach
+        attach(tr, raw_store(), rank, job)
+    return tr
+
+
+def _make_transport(rank, world, device, job, rccl_timeout_s, rank_offset, head_pairs, streams,
+                    max_bytes, head_bytes) -> Transport:
     if world == 1:
         return LoopbackTransport(1)
     from .transport import transport_kind

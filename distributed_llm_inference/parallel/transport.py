@@ -63,6 +63,16 @@ class Transport:
     # time the consumer waited for received data (host-blocking transports: host time; RCCL:
     # device time the compute stream stalled on the receive, from HIP events, DLI_STAGE_TIMING=1)
     recv_wait_ms: float = 0.0
+    # warm-up payload digests of every hop (parallel/integrity.py, DLI_HOP_CHECK), or None
+    integrity = None
+
+    def _ig_send(self, kind: str, peer: int, t: torch.Tensor, stream=None) -> None:
+        if self.integrity is not None:
+            self.integrity.on_send(kind, self.rank, peer, t, stream)
+
+    def _ig_recv(self, kind: str, peer: int, t: torch.Tensor, stream=None) -> None:
+        if self.integrity is not None:
+            self.integrity.on_recv(kind, peer, self.rank, t, stream)
 
     def _count(self, t: torch.Tensor, sent: bool) -> None:
         n = t.numel() * t.element_size()
@@ -108,13 +118,16 @@ class TorchDistTransport(Transport):
 
     def send(self, t, peer):
         self._count(t, True)
-        dist.send(t.contiguous(), peer + self.offset)
+        t = t.contiguous()
+        self._ig_send("stage", peer, t)
+        dist.send(t, peer + self.offset)
 
     def recv(self, t, peer, free_event=None):
         t0 = time.perf_counter()
         dist.recv(t, peer + self.offset)
         self.recv_wait_ms += (time.perf_counter() - t0) * 1e3
         self._count(t, False)
+        self._ig_recv("stage", peer, t)
         return t
 
     # rotating LM head (runtime/head.py): last stage -> the rank whose turn it is; tag 1 keeps
@@ -123,11 +136,34 @@ class TorchDistTransport(Transport):
 
     def send_head(self, t, peer):
         self._count(t, True)
-        dist.send(t.contiguous(), peer + self.offset, tag=1)
+        t = t.contiguous()
+        self._ig_send("head", peer, t)
+        dist.send(t, peer + self.offset, tag=1)
 
     def irecv_head(self, t, peer):
         self._count(t, False)
-        return dist.irecv(t, peer + self.offset, tag=1)
+        work = dist.irecv(t, peer + self.offset, tag=1)
+        if self.integrity is None:
+            return work
+        return _CheckedWork(work, lambda: self._ig_recv("head", peer, t))
+
+
+class _CheckedWork:
+    """A receive handle whose payload is digested once it has landed (hop integrity)."""
+
+    def __init__(self, work, on_done):
+        self._w, self._on_done, self._done = work, on_done, False
+
+    def is_completed(self) -> bool:
+        if not self._done and self._w.is_completed():
+            self.wait()
+        return self._done
+
+    def wait(self) -> None:
+        if not self._done:
+            self._w.wait()
+            self._on_done()
+            self._done = True
 
 
 class HostStagedTransport(Transport):
@@ -146,6 +182,7 @@ class HostStagedTransport(Transport):
 
     def send(self, t, peer):
         self._count(t, True)
+        self._ig_send("stage", peer, t.contiguous())
         dist.send(t.detach().to("cpu").contiguous(), peer + self.offset)
 
     def recv(self, t, peer, free_event=None):
@@ -157,6 +194,7 @@ class HostStagedTransport(Transport):
         self.recv_wait_ms += (time.perf_counter() - t0) * 1e3
         t.copy_(host, non_blocking=False)
         self._count(t, False)
+        self._ig_recv("stage", peer, t)
         return t
 
 
@@ -354,13 +392,16 @@ class RcclTransport(Transport):
     def send(self, t: torch.Tensor, peer: int) -> None:
         """Asynchronous: the send waits for work already queued on the current stream."""
         if not self._gpu:
-            self._comm(peer).send(t.contiguous(), self._pair_index(peer, "stage"), 0)
+            t = t.contiguous()
+            self._ig_send("stage", peer, t)
+            self._comm(peer).send(t, self._pair_index(peer, "stage"), 0)
             self._count(t, True)
             return
         cur = torch.cuda.current_stream(self.device)
         t = t.contiguous()   # copied on the compute stream, before the send stream waits on it
         self.send_stream.wait_stream(cur)
         t.record_stream(self.send_stream)
+        self._ig_send("stage", peer, t, self.send_stream)   # the bytes the send reads
         self._comm(peer).send(t, self._pair_index(peer, "stage"), self.send_stream.cuda_stream)
         self._count(t, True)
 
@@ -375,6 +416,7 @@ class RcclTransport(Transport):
             self._comm(peer).recv(t, self._pair_index(peer, "stage"), 0)
             self.recv_wait_ms += (time.perf_counter() - t0) * 1e3
             self._count(t, False)
+            self._ig_recv("stage", peer, t)
             return t
         cur = torch.cuda.current_stream(self.device)
         if free_event is not None:
@@ -383,6 +425,7 @@ class RcclTransport(Transport):
             self.recv_stream.wait_stream(cur)
         t.record_stream(self.recv_stream)
         self._comm(peer).recv(t, self._pair_index(peer, "stage"), self.recv_stream.cuda_stream)
+        self._ig_recv("stage", peer, t, self.recv_stream)   # the bytes the next stage reads
         if self._timing:
             a = torch.cuda.Event(enable_timing=True)
             a.record(cur)
@@ -399,13 +442,16 @@ class RcclTransport(Transport):
         """Last stage -> head rank ``peer``: the normed hidden states of an offloaded decode step
         (asynchronous, on the send stream, ordered after the work queued so far)."""
         if not self._gpu:
-            self._head_comm(peer).send(t.contiguous(), self._pair_index(peer, "head"), 0)
+            t = t.contiguous()
+            self._ig_send("head", peer, t)
+            self._head_comm(peer).send(t, self._pair_index(peer, "head"), 0)
             self._count(t, True)
             return
         cur = torch.cuda.current_stream(self.device)
         t = t.contiguous()   # copied on the compute stream, before the send stream waits on it
         self.send_stream.wait_stream(cur)
         t.record_stream(self.send_stream)
+        self._ig_send("head", peer, t, self.send_stream)
         self._head_comm(peer).send(t, self._pair_index(peer, "head"), self.send_stream.cuda_stream)
         self._count(t, True)
 
@@ -414,6 +460,7 @@ class RcclTransport(Transport):
         self._head_comm(peer).recv(t, self._pair_index(peer, "head"),
                                    stream.cuda_stream if stream is not None else 0)
         self._count(t, False)
+        self._ig_recv("head", peer, t, stream)
         return t
 
     def irecv_head(self, t: torch.Tensor, peer: int) -> "_HostRecv":

@@ -55,6 +55,11 @@ def test_bench_multirank_json_contract(n):
         ranges[i][1] == ranges[i + 1][0] for i in range(n - 1))
     pr = d["per_rank"]
     assert [r["rank"] for r in pr] == list(range(n))
+    # every hop of prefill + warm-up was digested on both ends and matched (parallel/integrity.py)
+    hi = d["hop_integrity"]
+    assert hi["checked"] > 0 and hi["mismatch"] == 0 and hi["missing"] == 0, hi
+    assert hi["checked"] == sum(r["hop_integrity"]["sent"] for r in pr), pr
+    assert all(r["hop_integrity"]["checked"] > 0 for r in pr[1:]), pr
     for r in pr:
         assert r["transport"] == "TorchDistTransport"
         # every rank ran one compute step per micro-batch step of the timed window

@@ -943,3 +943,18 @@ def test_skinny_gemm_qkv_rope_matches_gemv_then_rope_cache(gpu, wdtype, kv_fp8, 
         assert torch.equal(q, q_ref)
         for a, b in zip(caches[0], caches[1]):
             assert torch.equal(a.view(torch.uint8), b.view(torch.uint8))
+
+
+@pytest.mark.parametrize("shape,dtype", [((512, 8192), BF), ((3, 5, 7), torch.float32),
+                                         ((1 << 20,), torch.int32), ((2,), BF)])
+def test_digest_matches_reference(gpu, shape, dtype):
+    """csrc/kernels/digest.hip (hop integrity, parallel/integrity.py): the folded partial sums
+    equal the torch reference bit for bit at any grid size, and one flipped bit changes them."""
+    torch.manual_seed(40)
+    t = (torch.randn(shape, device=gpu) * 100).to(dtype)
+    want = ops.digest_fold(ref.digest_parts(t.cpu()))
+    for nb in (1, 7, 256):
+        assert ops.digest_fold(ops.digest(t, nblocks=nb)) == want, nb
+    u = t.clone()
+    u.view(torch.uint8).view(-1)[u.numel() * u.element_size() // 2] ^= 0x10
+    assert ops.digest_fold(ops.digest(u)) != want

@@ -56,6 +56,13 @@ class _FakeComm:
         key = f"fk/{self.uid}/{self.idx}->{peer}/{self.sent}"
         self.sent += 1
         raw = t.view(torch.uint8).numpy().tobytes() if t.numel() else b""
+        flip = os.environ.get("FAKE_FLIP")   # "<global rank>:<n>": corrupt this rank's n-th send
+        if flip and raw and int(flip.split(":")[0]) == self.n.global_rank:
+            self.n.sends += 1
+            if self.n.sends == int(flip.split(":")[1]):
+                b = bytearray(raw)
+                b[len(b) // 2] ^= 0x10          # one bit of one byte, mid-payload
+                raw = bytes(b)
         self.n.store.set(key, raw if raw else b"\0")
         self.n.log.append(("send", self.peer_rank(), t.numel()))
 
@@ -86,7 +93,7 @@ class _FakeNative:
         from distributed_llm_inference.runtime.faults import raw_store
         self.store = raw_store()
         self.global_rank = global_rank
-        self.comms, self.log, self.destroyed = [], [], 0
+        self.comms, self.log, self.destroyed, self.sends = [], [], 0, 0
 
     def rccl_version(self):
         return 22606
@@ -105,9 +112,10 @@ def _cfg(pp):
                                           max_seq_len=512, use_graphs=False))
 
 
-def _worker(rank, world, port, q, params):
+def _worker(rank, world, port, q, params, env=None):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_HEAD_ROTATION="1")
+    os.environ.update(env or {})
     import torch.distributed as dist
     from distributed_llm_inference import ops
     from distributed_llm_inference.parallel import transport as tmod
@@ -127,10 +135,13 @@ def _worker(rank, world, port, q, params):
            "rotation": obj.head_rotation}
     if role == "driver":
         out = obj.generate(PROMPTS, params)
+        obj.barrier()   # the hop-integrity check runs here (DLI_HOP_CHECK)
         obj.stop()
         rep["tokens"] = [s.output for s in out]
     else:
         obj.run()
+    ig = getattr(tr, "integrity", None)
+    rep["hop"] = ig.summary() if ig is not None else None
     rep["traffic"] = tr.traffic()
     rep["log"] = natives[0].log
     obj.close()
@@ -147,14 +158,12 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("world", [4, 8])
-def test_rccl_transport_dataplane_pipeline_equals_pp1(world):
-    params = SamplingParams(max_tokens=6, temperature=0.8, top_k=30, seed=11, ignore_eos=True)
-    ref = [s.output for s in LLMEngine(SPEC, cfg=_cfg(1)).generate(PROMPTS, params)]
+def _run(world, params, env=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, params)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, params, env))
+          for r in range(world)]
     for p in ps:
         p.start()
     reps = {}
@@ -164,7 +173,20 @@ def test_rccl_transport_dataplane_pipeline_equals_pp1(world):
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
+    return reps
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_rccl_transport_dataplane_pipeline_equals_pp1(world):
+    params = SamplingParams(max_tokens=6, temperature=0.8, top_k=30, seed=11, ignore_eos=True)
+    ref = [s.output for s in LLMEngine(SPEC, cfg=_cfg(1)).generate(PROMPTS, params)]
+    reps = _run(world, params, {"DLI_HOP_CHECK": "1"})
     assert reps[0]["tokens"] == ref
+    # every hop of the run was digested on both ends and matched
+    hops = [rep["hop"] for rep in reps.values()]
+    assert all(h is not None and h["mismatch"] == 0 and h["missing"] == 0 for h in hops), hops
+    assert sum(h["checked"] for h in hops) == sum(h["sent"] for h in hops) > 0
+    assert all(reps[r]["hop"]["checked"] > 0 for r in range(1, world)), hops   # stage + head
     last = world - 1
     for r, rep in reps.items():
         assert rep["type"] == "RcclTransport" and rep["rotation"], rep
@@ -195,3 +217,15 @@ def test_rccl_transport_dataplane_pipeline_equals_pp1(world):
     tot_sent = sum(rep["traffic"]["bytes_sent"] for rep in reps.values())
     tot_recv = sum(rep["traffic"]["bytes_recv"] for rep in reps.values())
     assert tot_sent == tot_recv > 0
+
+
+def test_hop_integrity_catches_one_flipped_byte():
+    """The simulated communicator corrupts ONE bit of ONE message (rank 1's third send, a stage
+    hop to rank 2): the receiving rank's digest disagrees with the sender's and the run reports
+    exactly that mismatch; every other hop still matches."""
+    params = SamplingParams(max_tokens=4, ignore_eos=True)
+    reps = _run(4, params, {"DLI_HOP_CHECK": "1", "FAKE_FLIP": "1:3"})
+    hops = {r: rep["hop"] for r, rep in reps.items()}
+    assert sum(h["mismatch"] for h in hops.values()) == 1, hops
+    assert hops[2]["mismatch"] == 1 and "stage/1-2/" in hops[2]["failures"][0], hops[2]
+    assert all(h["missing"] == 0 for h in hops.values()), hops
