@@ -9,9 +9,17 @@ SURVEY §7.4 item 2).  Per micro-batch step it packs:
   * prefill chunks of newly admitted sequences (chunked to ``max_num_batched_tokens``),
 and frees the KV blocks of sequences that finished in the previous step.
 
-Admission reserves the worst case (prompt + max_tokens) in KV blocks, so a running sequence can
-never run out of cache mid-generation (no preemption needed).  Every stage runs the identical
-block-manager call sequence, so stage-local block tables agree without being communicated.
+KV capacity grows on demand, like the reference's per-session cache that grows with every
+``update`` (/root/reference/distributed_llm_inference/models/llama/cache.py:103-109): admission
+reserves the prompt plus the first sampled token (keeping ``watermark`` blocks free for the
+running sequences to grow into), and a sequence takes one more block whenever its next token
+crosses a block boundary.  When the pool runs dry the youngest running sequence is preempted:
+its blocks are freed (the free rides in the plan being built, so every stage applies it after
+every step that used the blocks, in the same order) and it goes back to the front of the queue
+for recompute - its prompt and the tokens it already generated are prefilled again, and
+sampling (keyed by seed and position) continues exactly where it stopped.  Every stage runs the
+identical block-manager call sequence, so stage-local block tables agree without being
+communicated.
 """
 from __future__ import annotations
 
@@ -25,7 +33,8 @@ from .sequence import Sequence, SeqStatus
 class Scheduler:
     def __init__(self, num_micro_batches: int, max_seqs_per_mb: int, max_tokens_per_step: int,
                  blocks_for: Callable[[int], int], total_blocks: int,
-                 eos_token_id: Optional[int] = None, max_seq_len: int = 8192):
+                 eos_token_id: Optional[int] = None, max_seq_len: int = 8192,
+                 watermark: Optional[int] = None):
         self.M = max(1, num_micro_batches)
         self.max_seqs = max_seqs_per_mb
         self.max_tokens = max_tokens_per_step
@@ -39,6 +48,19 @@ class Scheduler:
         self.inflight: List[Optional[StepPlan]] = [None] * self.M
         self.reserved_blocks = 0
         self._reserve: Dict[int, int] = {}
+        # tokens per KV block (blocks_for is a ceil-division by it)
+        self.block_size = next(n for n in range(1, 1 << 20) if blocks_for(n + 1) > blocks_for(n))
+        # blocks admission leaves free for the running sequences' growth
+        self.watermark = total_blocks // 100 if watermark is None else int(watermark)
+        self._order: Dict[int, int] = {}       # seq_id -> admission counter (youngest = largest)
+        self._n_admitted = 0
+        # per micro-batch: decode steps every member can take before one needs another block
+        self._headroom: List[int] = [0] * self.M
+        # per micro-batch: ids preempted while a plan holding them was in flight (their tokens
+        # from that plan are stale, even if they were re-admitted meanwhile)
+        self._stale: List[set] = [set() for _ in range(self.M)]
+        self.preemptions = 0
+        self.max_running = 0
         self.step = 0
         self.finished: List[Sequence] = []
         # steady-state decode fast path: while a micro-batch's membership is unchanged and every
@@ -96,19 +118,70 @@ class Scheduler:
                 self.waiting.popleft()
                 self.finished.append(s)
                 continue
-            need = self.blocks_for(len(s.prompt) + s.params.max_tokens)
-            if self.reserved_blocks + need > self.total_blocks:
+            # the tokens to (re)compute and the first sampled one; a preempted sequence recomputes
+            # its prompt and everything it generated
+            need = self.blocks_for(s.total_len + 1)
+            room = self.total_blocks - (self.watermark if self.num_running() else 0)
+            if self.reserved_blocks + need > room:
                 break
             self.waiting.popleft()
             self.reserved_blocks += need
             self._reserve[s.seq_id] = need
+            self._n_admitted += 1
+            self._order[s.seq_id] = self._n_admitted
             s.status = SeqStatus.RUNNING
             s.micro_batch = mb
             m.append(s)
             admitted.append(s)
             self._dirty[mb] = True
-            budget -= min(len(s.prompt), budget)
+            budget -= min(s.total_len - s.num_computed, budget)
+        self.max_running = max(self.max_running, self.num_running())
         return admitted
+
+    # ------------------------------------------------------------------ KV growth / preemption
+    def _preempt(self, mb: int, v: Sequence) -> None:
+        """Free ``v``'s blocks (in the plan being built for ``mb``) and queue it for recompute."""
+        mv = v.micro_batch
+        self.mbs[mv].remove(v)
+        self._dirty[mv] = True
+        if self.inflight[mv] is not None or self.lookahead[mv] is not None:
+            self._stale[mv].add(v.seq_id)
+        self.reserved_blocks -= self._reserve.pop(v.seq_id, 0)
+        self._order.pop(v.seq_id, None)
+        self.pending_free[mb].append(v.seq_id)
+        v.status = SeqStatus.WAITING
+        v.num_computed = 0
+        v.micro_batch = -1
+        self.waiting.appendleft(v)
+        self.preemptions += 1
+
+    def _grow(self, mb: int, rows: List[tuple]) -> None:
+        """Reserve the blocks ``rows`` ((sequence, tokens this step)) need; when the pool is
+        short, preempt the youngest running sequence (possibly the one asking) until it fits."""
+        for s, take in rows:
+            if s.status is not SeqStatus.RUNNING:
+                continue   # preempted by an earlier row of this pass
+            need = self.blocks_for(s.num_computed + take) - self._reserve[s.seq_id]
+            while need > 0:
+                if self.reserved_blocks + need <= self.total_blocks:
+                    self._reserve[s.seq_id] += need
+                    self.reserved_blocks += need
+                    break
+                victim = max((x for q in self.mbs for x in q), key=lambda x: self._order[x.seq_id])
+                self._preempt(mb, victim)
+                if victim is s:
+                    break
+
+    @staticmethod
+    def _decoding(s: Sequence) -> bool:
+        """Only the last sampled token is pending (a preempted sequence recomputing its outputs,
+        like one prefilling its prompt, is not)."""
+        return s.num_computed >= max(len(s.prompt), s.total_len - 1)
+
+    def _set_headroom(self, mb: int) -> None:
+        bs = self.block_size
+        self._headroom[mb] = min((self._reserve[s.seq_id] * bs - s.num_computed
+                                  for s in self.mbs[mb]), default=0)
 
     def plan(self, mb: int) -> Optional[StepPlan]:
         """Next step for micro-batch ``mb`` (None if it has nothing to do)."""
@@ -117,27 +190,38 @@ class Scheduler:
         # drop aborted sequences
         for s in [s for s in m if s.status == SeqStatus.ABORTED]:
             self._retire(mb, s)
+        if not self._dirty[mb] and m and self._headroom[mb] < 1:
+            # a clean micro-batch whose next token crosses a block boundary for some member
+            self._grow(mb, [(s, 1) for s in m])
+            if not self._dirty[mb]:
+                self._set_headroom(mb)
         if self._dirty[mb]:
-            decode_n = sum(1 for s in m if s.num_computed >= len(s.prompt))
+            decode_n = sum(1 for s in m if self._decoding(s))
         else:
             decode_n = len(m)  # a clean micro-batch is all-decode (see _decode_plan)
         self._admit(mb, self.max_tokens - decode_n)
         if not self._dirty[mb] and m:
             return self._decode_plan(mb)
         budget = self.max_tokens - decode_n
-        seq_ids, q_lens, tokens, sample_rows = [], [], [], []
-        temps, topk, topp, seeds, spos = [], [], [], [], []
+        work = []
         for s in m:
             pend = s.pending_tokens()
-            if s.num_computed >= len(s.prompt):
+            if self._decoding(s):
                 take = 1  # decode: the last sampled token
                 pend = pend[-1:]
-            else:
+            else:       # prefill chunk (a prompt, or a preempted sequence's recompute)
                 take = min(len(pend), budget)
                 if take <= 0:
                     continue
                 budget -= take
                 pend = pend[:take]
+            work.append((s, take, pend))
+        self._grow(mb, [(s, take) for s, take, _ in work])
+        seq_ids, q_lens, tokens, sample_rows = [], [], [], []
+        temps, topk, topp, seeds, spos = [], [], [], [], []
+        for s, take, pend in work:
+            if s.status is not SeqStatus.RUNNING:
+                continue   # preempted to make room
             row = len(seq_ids)
             seq_ids.append(s.seq_id)
             q_lens.append(take)
@@ -164,6 +248,7 @@ class Scheduler:
             s.num_computed += q
         self._rows[mb] = rows
         self.inflight[mb] = plan if seq_ids else None
+        self._set_headroom(mb)
         # cache the all-decode layout; it stays valid until the membership changes
         if seq_ids and len(rows) == len(m) and all(q == 1 for q in q_lens) \
                 and len(sample_rows) == len(rows):
@@ -185,8 +270,8 @@ class Scheduler:
                 or self.waiting or self.pending_free[mb] or not self.mbs[mb]):
             return None
         rows = self._rows[mb]
-        if len(rows) != len(self.mbs[mb]):
-            return None
+        if len(rows) != len(self.mbs[mb]) or self._headroom[mb] < 1:
+            return None   # (a member needs another KV block first: plan it normally)
         for s in rows:
             if s.status is not SeqStatus.RUNNING or len(s.output) + 2 > s.params.max_tokens:
                 return None
@@ -199,6 +284,7 @@ class Scheduler:
                         sample_pos=[s.num_computed for s in rows], tokens=None)
         self.step += 1
         self.lookahead[mb] = plan
+        self._headroom[mb] -= 1
         return plan
 
     def _decode_plan(self, mb: int) -> StepPlan:
@@ -217,6 +303,7 @@ class Scheduler:
                         tokens=tokens)
         self.step += 1
         self.inflight[mb] = plan
+        self._headroom[mb] -= 1
         return plan
 
     # ------------------------------------------------------------------ results
@@ -225,6 +312,7 @@ class Scheduler:
         self._dirty[mb] = True
         self.pending_free[mb].append(s.seq_id)
         self.reserved_blocks -= self._reserve.pop(s.seq_id, 0)
+        self._order.pop(s.seq_id, None)
         self.finished.append(s)
 
     def on_tokens(self, mb: int, tokens: List[int], now: Optional[float] = None) -> List[Sequence]:
@@ -235,15 +323,20 @@ class Scheduler:
         if plan is None:
             return []
         rows = self._rows[mb]
+        stale = self._stale[mb]
         done = []
         for row, tok in zip(plan.sample_rows, tokens):
             s = rows[row]
-            if s.status is not SeqStatus.RUNNING:  # finished / aborted meanwhile
+            if s.status is not SeqStatus.RUNNING:  # finished / aborted / preempted meanwhile
+                continue
+            if s.seq_id in stale:   # preempted (and re-admitted) since this plan was issued
                 continue
             if s.append_token(tok, self.eos, now):
                 done.append(s)
         for s in done:
             self._retire(mb, s)
+        if self.inflight[mb] is None:
+            stale.clear()
         return done
 
     def pop_finished(self) -> List[Sequence]:
