@@ -88,7 +88,8 @@ def build_block_app(worker, rebalance=None, token=None):
     """The block server's HTTP service; ``rebalance``: a callable running one rebalancing round
     (:func:`rebalance_once`) behind POST /rebalance, for operators and tests.  ``token``: the
     registry's shared token (``--registry-token``), then required by POST /rebalance as well
-    (``Authorization: Bearer ...``), since a move changes what the swarm serves."""
+    (``Authorization: Bearer ...``), since a move changes what the swarm serves; without a
+    token only loopback clients may ask for a move."""
     import hmac
     from fastapi import FastAPI, HTTPException, Request
     from fastapi.responses import JSONResponse, Response
@@ -101,6 +102,11 @@ def build_block_app(worker, rebalance=None, token=None):
         if token is not None and not hmac.compare_digest(
                 request.headers.get("authorization", "").encode(), f"Bearer {token}".encode()):
             raise HTTPException(401, "registry token required (Authorization: Bearer ...)")
+        if token is None and (request.client is None or
+                              request.client.host not in ("127.0.0.1", "::1", "localhost")):
+            # no shared secret configured: a move reloads weights on this GPU host, so only
+            # the host itself may ask for one
+            raise HTTPException(403, "POST /rebalance without a registry token: loopback only")
         if rebalance is None:
             raise HTTPException(404, "this server has no registry to rebalance against")
         moved = await asyncio.get_running_loop().run_in_executor(None, rebalance)

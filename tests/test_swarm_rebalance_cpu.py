@@ -58,20 +58,23 @@ def test_registry_rebalance_claims_and_serialises():
 
 def test_block_server_rebalance_requires_the_registry_token():
     """With a registry token, POST /rebalance on a block server needs it too (a move changes what
-    the swarm serves); without one the endpoint stays open."""
+    the swarm serves); without one only loopback clients may ask."""
     from types import SimpleNamespace
     from fastapi.testclient import TestClient
     from distributed_llm_inference.server.block_server import build_block_app
     worker = SimpleNamespace(start=0, end=4)
     calls = []
     for token in ("s3cret", None):
-        c = TestClient(build_block_app(worker, rebalance=lambda: calls.append(1), token=token))
+        app = build_block_app(worker, rebalance=lambda: calls.append(1), token=token)
+        c = TestClient(app, client=("10.1.2.3", 40000))
         r = c.post("/rebalance")
-        assert r.status_code == (401 if token else 200)
+        assert r.status_code == (401 if token else 403)
         if token:
             assert c.post("/rebalance", headers={"Authorization": "Bearer nope"}).status_code == 401
             r = c.post("/rebalance", headers={"Authorization": f"Bearer {token}"})
-            assert r.status_code == 200
+        else:
+            r = TestClient(app, client=("127.0.0.1", 40000)).post("/rebalance")
+        assert r.status_code == 200
         assert r.json() == {"moved": False, "start": 0, "end": 4}
     assert len(calls) == 2
 
