@@ -52,9 +52,37 @@ constexpr float P32_THR = 8.f;   // deferred-max threshold (log2 domain)
 #ifndef P32_PRIO
 #define P32_PRIO 0   // 1: static s_setprio 1 for the second half of the waves
 #endif
+#ifndef P32_PERM
+#define P32_PERM 1   // 1: the cross-half row max by v_permlane32_swap instead of ds_bpermute
+#endif
+#ifndef P32_KO_PAGES
+#define P32_KO_PAGES 0   // knock-out probe only (wrong results unless pages are identity)
+#endif
+#ifndef P32_KO_Q
+#define P32_KO_Q 0   // knock-out probe only (wrong results)
+#endif
+#ifndef P32_KO_OUT
+#define P32_KO_OUT 0   // knock-out probe only (wrong results)
+#endif
+#ifndef P32_KO_LOOP
+#define P32_KO_LOOP 0   // knock-out probe only (wrong results)
+#endif
+#ifndef P32_OSTAGE
+#define P32_OSTAGE 1   // 1: the output staged through LDS and stored as whole rows
+#endif
+#ifndef P32_KREAD
+#define P32_KREAD 1   // 1: a step's 16 K fragment reads all issued ahead of its S MFMAs
+#endif
 
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// max over lanes l and l ^ 32: v_permlane32_swap of two copies leaves each lane both halves
+__device__ __forceinline__ float xhalf_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                  false);
+  return __builtin_elementwise_maximum(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
 __device__ __forceinline__ int swap23(int i) {   // pi: swap bits 2 and 3 of a 32-row index
@@ -118,7 +146,11 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   const int pq = L - qlen + (valid ? tok : qlen - 1);          // this column's position
   const int pq_lo = L - qlen + t0;                               // workgroup's first position
   const int pq_hi = L - qlen + min(qlen - 1, t0 + TQ - 1);       // ... and last
+#if P32_KO_LOOP
+  const int nsteps = 1;   // knock-out probe only: the fixed per-workgroup cost
+#else
   const int nsteps = (pq_hi + 64) >> 6;                          // keys [0, pq_hi]
+#endif
   const int* bt = p.block_tables + (size_t)b * p.bt_stride;
   const size_t head_stride = (size_t)p.bs * D;
 
@@ -129,8 +161,12 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     const bf16* qrow = p.q + ((size_t)(qs0 + (valid ? tok : 0)) * p.nh + qh) * D + 8 * hh;
 #pragma unroll
     for (int m = 0; m < D / 16; ++m) {
+#if P32_KO_Q
+      qf[m] = zero8(); (void)qrow;
+#else
       qf[m] = *reinterpret_cast<const bf16x8*>(qrow + 16 * m);
       if (!valid) qf[m] = zero8();
+#endif
     }
   }
 
@@ -138,13 +174,27 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   // wave) of one 64-key step.  Instruction j covers K rows 4j..4j+3 / V^T units 64j..64j+63;
   // j >> 3 = its 32-key half.  A half past every column is never fetched (its block-table entry
   // may not exist).
-  auto dma = [&](int s, bf16* dst, bool is_v) {
+  // (block size a power of two, eligibility: shifts, not divisions; both halves' pages by one
+  // pair of scalar loads waited once per step, shared by the K and the V^T image)
+  const int bs_lg = __builtin_ctz(p.bs);
+  auto pages = [&](int s, size_t& e00, size_t& e01) {
     const int u0 = s * 64;
-    const bool need1 = u0 + 32 <= pq_hi;
-    const int pg0 = bt_entry(bt, u0 / p.bs);
-    const int pg1 = !need1 ? pg0 : (p.bs % 64 == 0 ? pg0 : bt_entry(bt, (u0 + 32) / p.bs));
-    const size_t e00 = ((size_t)pg0 * p.nkv + kvh) * head_stride + (size_t)(u0 % p.bs) * D;
-    const size_t e01 = ((size_t)pg1 * p.nkv + kvh) * head_stride + (size_t)((u0 + 32) % p.bs) * D;
+    const int i0 = u0 >> bs_lg;
+    const int i1 = (u0 + 32 <= pq_hi) ? (u0 + 32) >> bs_lg : i0;
+    const int* a0 = bt + __builtin_amdgcn_readfirstlane(i0);
+    const int* a1 = bt + __builtin_amdgcn_readfirstlane(i1);
+    int pg0, pg1;
+#if P32_KO_PAGES
+    pg0 = i0; pg1 = i1; (void)a0; (void)a1;
+    if (false)
+#endif
+    asm volatile("s_load_dword %0, %2, 0x0\n\ts_load_dword %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(pg0), "=&s"(pg1) : "s"(a0), "s"(a1));
+    e00 = ((size_t)pg0 * p.nkv + kvh) * head_stride + (size_t)(u0 & (p.bs - 1)) * D;
+    e01 = ((size_t)pg1 * p.nkv + kvh) * head_stride + (size_t)((u0 + 32) & (p.bs - 1)) * D;
+  };
+  auto dma = [&](int s, bf16* dst, bool is_v, size_t e00, size_t e01) {
+    const bool need1 = s * 64 + 32 <= pq_hi;
 #pragma unroll
     for (int i = 0; i < 16 / NW; ++i) {
       const int j = w + i * NW;                // wave-uniform
@@ -152,17 +202,24 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
       if (half && !need1) continue;
       const size_t e0 = half ? e01 : e00;
       const int u = j * 64 + lane;             // 16-B unit of this lane in the 16 KB image
-      const bf16* g;
+      // buffer_load ... lds rather than global_load_lds: the compiler's wait model treats the
+      // global form as an out-of-order LDS (lgkm) access, which turns every LDS-read wait after
+      // it into lgkmcnt(0); the buffer form leaves the reads counted.  One 8 KB half = one
+      // 32-key run of one page (block size a multiple of 32), so the resource spans exactly it.
+      int voff;
+      const bf16* base;
       if (!is_v) {
         const int row = u >> 4, slot = u & 15;           // LDS row (0..63), stored chunk
         const int key = swap23(row & 31);                // key of this row inside its half
-        g = static_cast<const bf16*>(p.k_cache) + e0 + (size_t)key * D + 8 * (slot ^ (row & 15));
+        base = static_cast<const bf16*>(p.k_cache) + e0;
+        voff = (key * D + 8 * (slot ^ (row & 15))) * 2;
       } else {
-        g = static_cast<const bf16*>(p.v_cache) + e0 + (size_t)(u & 511) * 8;
+        base = static_cast<const bf16*>(p.v_cache) + e0;
+        voff = (u & 511) * 16;
       }
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
-                                       (__attribute__((address_space(3))) void*)(dst + j * 64 * 8),
-                                       16, 0, 0);
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 32 * D * 2, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(dst + j * 64 * 8), 16, voff, 0, 0, 0);
     }
   };
   auto bufi = [&](int s) { return NBUF == 2 ? (s & 1) : (s % 3); };
@@ -190,13 +247,26 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
 #pragma unroll
     for (int m = 0; m < D / 16; ++m)
       ka[m] = *reinterpret_cast<const bf16x8*>(kt + koff + ((2 * m + hh) ^ kx) * 8);
+#if P32_KREAD
+    // the first half's 8 reads all issued before the first MFMA, then one second-half read per
+    // MFMA (the scheduler otherwise sinks each read to just before its MFMA, and every MFMA waits
+    // out a whole LDS latency: lgkmcnt(0) per read)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     sa = f32x16{};
     sb = f32x16{};
 #pragma unroll
     for (int m = 0; m < D / 16; ++m) {
       kb8[m] = *reinterpret_cast<const bf16x8*>(kt + 32 * CH * 8 + koff + ((2 * m + hh) ^ kx) * 8);
       sa = mfma32(ka[m], qf[m], sa);
+#if P32_KREAD
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one DS read
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // then one MFMA
+#endif
     }
+#if P32_KREAD
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     if (full2(s)) {
 #pragma unroll
       for (int m = 0; m < D / 16; ++m) sb = mfma32(kb8[m], qf[m], sb);
@@ -215,20 +285,30 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
         sb[r] = key + 32 > pq ? -INFINITY : sb[r];   // (an unread half: every key masked)
       }
     }
-    float mx = fmaxf(sa[0], sb[0]);
+    // IEEE maximum (NaN-propagating) lowers to v_maximum3_f32, one per two scores; fmaxf's
+    // maxnum would first canonicalise every MFMA output with a v_max_f32 x, x of its own
+    float mx = __builtin_elementwise_maximum(sa[0], sb[0]);
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(sa[r], sb[r]));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    for (int r = 1; r < 16; ++r)
+      mx = __builtin_elementwise_maximum(mx, __builtin_elementwise_maximum(sa[r], sb[r]));
+#if P32_PERM
+    mx = xhalf_max(mx);
+#else
+    mx = __builtin_elementwise_maximum(mx, __shfl_xor(mx, 32, 64));
+#endif
     const float pmax = mx * sl2;
     resc = __any(pmax > m_run + P32_THR);
     const float m_new = resc ? fmaxf(m_run, pmax) : m_run;
     alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;
-    float ps0 = 0.f, ps1 = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       sa[r] = __builtin_amdgcn_exp2f(fmaf(sa[r], sl2, -m_new));
       sb[r] = __builtin_amdgcn_exp2f(fmaf(sb[r], sl2, -m_new));
+    }
+    float ps0 = sa[0], ps1 = sb[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {
       ps0 += sa[r];
       ps1 += sb[r];
     }
@@ -246,6 +326,36 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
       for (int db = 0; db < D / 32; ++db) o[db] *= alpha;
     }
     const bf16* vt = vbuf(bufi(s));
+#if P32_KREAD
+    // as in scores: the first half's 8 reads ahead, then one second-half read per MFMA
+    bf16x8 va[D / 16], vb[D / 16];
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+      va[2 * db] = *reinterpret_cast<const bf16x8*>(vt + voff + (0 * D + 32 * db) * 8);
+      va[2 * db + 1] = *reinterpret_cast<const bf16x8*>(vt + voff + (2 * D + 32 * db) * 8);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db) {
+      vb[2 * db] = *reinterpret_cast<const bf16x8*>(vt + voff + (4 * D + 32 * db) * 8);
+      o[db] = mfma32(va[2 * db], pp[0], o[db]);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      vb[2 * db + 1] = *reinterpret_cast<const bf16x8*>(vt + voff + (6 * D + 32 * db) * 8);
+      o[db] = mfma32(va[2 * db + 1], pp[1], o[db]);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (full2(s)) {
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+        o[db] = mfma32(vb[2 * db], pp[2], o[db]);
+        o[db] = mfma32(vb[2 * db + 1], pp[3], o[db]);
+      }
+    }
+    if (false) {
+#else
 #pragma unroll
     for (int db = 0; db < D / 32; ++db) {
       const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(vt + voff + (0 * D + 32 * db) * 8);
@@ -254,6 +364,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
       o[db] = mfma32(v1, pp[1], o[db]);
     }
     if (full2(s)) {
+#endif
 #pragma unroll
       for (int db = 0; db < D / 32; ++db) {
         const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(vt + voff + (4 * D + 32 * db) * 8);
@@ -264,8 +375,10 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     }
   };
   auto dma_step = [&](int s) {   // K and V^T of step s into its buffer
-    dma(s, kbuf(bufi(s)), false);
-    dma(s, vbuf(bufi(s)), true);
+    size_t e00, e01;
+    pages(s, e00, e01);
+    dma(s, kbuf(bufi(s)), false, e00, e01);
+    dma(s, vbuf(bufi(s)), true, e00, e01);
   };
 
   dma_step(0);
@@ -307,8 +420,49 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   }
   // ---- normalise and store: register r of o[db] is d = 32 db + (r & 3) + 8 (r >> 2) + 4 hh ----
   float lsum = l_run + __shfl_xor(l_run, 32, 64);
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+#if P32_OSTAGE
+  // through LDS, so that the stores leave as whole rows: the register layout has each lane hold
+  // 4 d values of ONE row, and direct per-lane 8-byte stores touched 32 rows (lines) per
+  // instruction - store-issue bound, the tail of every workgroup (MI355X_MICROARCH.md constants
+  // 'attention epilogue store tail').  Staging image: row R = 32 w + c (= head R / TQ, token
+  // R % TQ) of 128 d, 16-byte chunk j at j ^ (R & 15); then each wave-instruction stores 4
+  // whole rows of one token (adjacent heads: 1 KB contiguous in [token][head][d]).
+  __syncthreads();   // every wave is past its last K / V^T read
+  bf16* stg = &smem[0][0][0];
+  {
+    bf16* srow = stg + (size_t)R * D + 4 * hh;
+#pragma unroll
+    for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[db][4 * a + r] * inv);
+        *reinterpret_cast<bf16x4*>(srow + ((4 * db + a) ^ (R & 15)) * 8) = v;
+      }
+  }
+  __syncthreads();
+  constexpr int PER = TQ * GW * (D / 8) / 64 / NW;   // store instructions per wave
+  const int nvalid = min(TQ, qlen - t0);
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int i = (k * NW + w) * 64 + lane;
+    const int chunk = i & 15, rr = i >> 4;
+    const int head = rr % GW, token = rr / GW;
+    const int R2 = head * TQ + token;
+#if P32_KO_OUT
+    if (token < nvalid && lsum == 12345.f) {
+#else
+    if (token < nvalid) {
+#endif
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(stg + (size_t)R2 * D + (chunk ^ (R2 & 15)) * 8);
+      *reinterpret_cast<bf16x8*>(p.out + ((size_t)(qs0 + t0 + token) * p.nh + h0 + head) * D +
+                                 chunk * 8) = v;
+    }
+  }
+#else
   if (valid) {
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     bf16* orow = p.out + ((size_t)(qs0 + tok) * p.nh + qh) * D + 4 * hh;
 #pragma unroll
     for (int db = 0; db < D / 32; ++db)
@@ -320,13 +474,14 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
         *reinterpret_cast<bf16x4*>(orow + 32 * db + 8 * a) = v;
       }
   }
+#endif
 }
 
 // Eligible: head_dim 128, bf16 full cache, GQA group a multiple of 4, no custom mask.
 bool attn_prefill32_eligible(const AttnParams& p, int D) {
   const int G = p.nh / p.nkv;
   return p.prefill_m32 && D == P32_D && !p.kv_fp8 && p.ring == 0 && p.mask == nullptr &&
-         G % 4 == 0 && p.bs % 32 == 0;
+         G % 4 == 0 && p.bs % 32 == 0 && (p.bs & (p.bs - 1)) == 0;
 }
 
 // Tile = 16 * prefill_qb query tokens (the same tile attention.hip's kernel uses at 4 heads per
