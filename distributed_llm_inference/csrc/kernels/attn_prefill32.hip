@@ -67,6 +67,12 @@ constexpr float P32_THR = 8.f;   // deferred-max threshold (log2 domain)
 #ifndef P32_KO_LOOP
 #define P32_KO_LOOP 0   // knock-out probe only (wrong results)
 #endif
+#ifndef P32_CINIT
+#define P32_CINIT 0   // 1: S MFMA chains start from -m_run (Q pre-scaled): P = exp2(S'), no FMA
+#endif
+#ifndef P32_DEPTH2
+#define P32_DEPTH2 0   // 1: staggered workgroups fetch K / V two steps ahead (four buffers)
+#endif
 #ifndef P32_OSTAGE
 #define P32_OSTAGE 1   // 1: the output staged through LDS and stored as whole rows
 #endif
@@ -106,7 +112,10 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   constexpr int DPW = 32 / NW;              // LDS-DMA wave-instructions per wave per step
   // staggered waves (8-wave workgroups, one per CU) keep V(s-1) while step s+1 lands: 3 buffers
   constexpr bool STAG = P32_STAGGER && NW == 8;
-  constexpr int NBUF = STAG ? 3 : 2;
+  // DMA two steps ahead (staggered workgroups): four buffers, step s+2 lands during step s
+  constexpr bool DA = P32_DEPTH2 && STAG;
+  constexpr int LA = DA ? 2 : 1;            // DMA lookahead in steps
+  constexpr int NBUF = DA ? 4 : (STAG ? 3 : 2);
   // [buf][K | V^T][64 keys x D]: NBUF x 2 x 16 KB
   __shared__ __attribute__((aligned(16))) bf16 smem[NBUF][2][64 * D];
 
@@ -166,6 +175,10 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
 #else
       qf[m] = *reinterpret_cast<const bf16x8*>(qrow + 16 * m);
       if (!valid) qf[m] = zero8();
+#if P32_CINIT
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[m][j] = (bf16)((float)qf[m][j] * p.scale_log2);
+#endif
 #endif
     }
   }
@@ -176,11 +189,45 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   // may not exist).
   // (block size a power of two, eligibility: shifts, not divisions; both halves' pages by one
   // pair of scalar loads waited once per step, shared by the K and the V^T image)
+  auto bufi = [&](int s) { return NBUF == 2 ? (s & 1) : NBUF == 4 ? (s & 3) : (s % 3); };
+  auto kbuf = [&](int i) { return &smem[i][0][0]; };
+  auto vbuf = [&](int i) { return &smem[i][1][0]; };
   const int bs_lg = __builtin_ctz(p.bs);
-  auto pages = [&](int s, size_t& e00, size_t& e01) {
+  // one buffer resource per (page half, image) and step: base = the half's first key in this kv
+  // head's slice of the page (32-bit page stride: nkv * bs * D), and per-lane offsets that
+  // depend only on the piece index - computed once, outside the loop
+  const bf16* kbase = static_cast<const bf16*>(p.k_cache) + (size_t)kvh * head_stride;
+  const bf16* vbase = static_cast<const bf16*>(p.v_cache) + (size_t)kvh * head_stride;
+  const uint32_t page_elems = (uint32_t)p.nkv * (uint32_t)head_stride;
+  constexpr int NPC = 16 / NW;              // pieces per image per wave and step
+  int kvo[NPC], vvo[NPC];
+#pragma unroll
+  for (int i = 0; i < NPC; ++i) {
+    const int u = (w + i * NW) * 64 + lane;  // 16-B unit of this lane in the 16 KB image
+    const int row = u >> 4, slot = u & 15;   // K: LDS row (0..63), stored chunk
+    kvo[i] = (swap23(row & 31) * D + 8 * (slot ^ (row & 15))) * 2;   // key pi(row) of its half
+    vvo[i] = (u & 511) * 16;
+  }
+  // one 1 KB piece: the resource starts at the half's first key (its offset folded into the
+  // base: this compiler drops the host-side kernel stubs - silently, a broken object - when the
+  // soffset operand of the builtin is a runtime value or the resource is built inline in the call)
+  auto piece = [&](const bf16* base, int pg, int half_off, bf16* dst, int vo) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(base + (size_t)(uint32_t)pg * page_elems + half_off), 0, 0x7fffffff, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16,
+                                             vo, 0, 0, 0);
+  };
+  // ---- LDS-DMA of step s: K and V^T images (16 wave-instructions of 1 KB each per image,
+  // NPC per wave).  Piece i of wave w is instruction j = w + i NW: K rows 4j..4j+3 / V^T units
+  // 64j..64j+63, its 32-key half (j >> 3 = i NW >> 3) known at compile time.  A half past every
+  // column is never fetched (its block-table entry may not exist).  buffer_load ... lds rather
+  // than global_load_lds: the compiler's wait model treats the global form as an out-of-order
+  // LDS (lgkm) access, which turns every LDS-read wait after it into lgkmcnt(0).
+  auto dma_step = [&](int s) {
     const int u0 = s * 64;
+    const bool need1 = u0 + 32 <= pq_hi;
     const int i0 = u0 >> bs_lg;
-    const int i1 = (u0 + 32 <= pq_hi) ? (u0 + 32) >> bs_lg : i0;
+    const int i1 = need1 ? (u0 + 32) >> bs_lg : i0;
     const int* a0 = bt + __builtin_amdgcn_readfirstlane(i0);
     const int* a1 = bt + __builtin_amdgcn_readfirstlane(i1);
     int pg0, pg1;
@@ -190,41 +237,20 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
 #endif
     asm volatile("s_load_dword %0, %2, 0x0\n\ts_load_dword %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
                  : "=&s"(pg0), "=&s"(pg1) : "s"(a0), "s"(a1));
-    e00 = ((size_t)pg0 * p.nkv + kvh) * head_stride + (size_t)(u0 & (p.bs - 1)) * D;
-    e01 = ((size_t)pg1 * p.nkv + kvh) * head_stride + (size_t)((u0 + 32) & (p.bs - 1)) * D;
-  };
-  auto dma = [&](int s, bf16* dst, bool is_v, size_t e00, size_t e01) {
-    const bool need1 = s * 64 + 32 <= pq_hi;
+    const int so0 = (u0 & (p.bs - 1)) * D;          // the halves' element offsets in their pages
+    const int so1 = ((u0 + 32) & (p.bs - 1)) * D;
+    bf16* kd = kbuf(bufi(s));
+    bf16* vd = vbuf(bufi(s));
 #pragma unroll
-    for (int i = 0; i < 16 / NW; ++i) {
-      const int j = w + i * NW;                // wave-uniform
-      const int half = j >> 3;
+    for (int i = 0; i < NPC; ++i) {
+      const int half = (i * NW) >> 3;
       if (half && !need1) continue;
-      const size_t e0 = half ? e01 : e00;
-      const int u = j * 64 + lane;             // 16-B unit of this lane in the 16 KB image
-      // buffer_load ... lds rather than global_load_lds: the compiler's wait model treats the
-      // global form as an out-of-order LDS (lgkm) access, which turns every LDS-read wait after
-      // it into lgkmcnt(0); the buffer form leaves the reads counted.  One 8 KB half = one
-      // 32-key run of one page (block size a multiple of 32), so the resource spans exactly it.
-      int voff;
-      const bf16* base;
-      if (!is_v) {
-        const int row = u >> 4, slot = u & 15;           // LDS row (0..63), stored chunk
-        const int key = swap23(row & 31);                // key of this row inside its half
-        base = static_cast<const bf16*>(p.k_cache) + e0;
-        voff = (key * D + 8 * (slot ^ (row & 15))) * 2;
-      } else {
-        base = static_cast<const bf16*>(p.v_cache) + e0;
-        voff = (u & 511) * 16;
-      }
-      const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 32 * D * 2, 0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)(dst + j * 64 * 8), 16, voff, 0, 0, 0);
+      const int j = w + i * NW;
+      const int pg = half ? pg1 : pg0;
+      piece(kbase, pg, half ? so1 : so0, kd + j * 64 * 8, kvo[i]);
+      piece(vbase, pg, half ? so1 : so0, vd + j * 64 * 8, vvo[i]);
     }
   };
-  auto bufi = [&](int s) { return NBUF == 2 ? (s & 1) : (s % 3); };
-  auto kbuf = [&](int i) { return &smem[i][0][0]; };
-  auto vbuf = [&](int i) { return &smem[i][1][0]; };
 
   f32x16 o[D / 32];
 #pragma unroll
@@ -238,10 +264,17 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   auto full2 = [&](int s) { return s * 64 + 32 <= pq_hi; };   // second half holds a visible key
   auto diag = [&](int s) { return s * 64 + 63 > pq_lo; };     // some key past some column
   // ---- the three products of one 64-key step ----
+#if P32_CINIT
+  // Q is pre-scaled by scale * log2(e) and every S MFMA chain starts from cinit = -m_run, so
+  // S' = S log2(e) / sqrt(D) - m_run comes out of the matrix pipe and P = exp2(S') needs no FMA
+  // (the loop is vector-issue bound: MI355X_MICROARCH.md 'vector-instruction ISSUE cost')
+  float m_run = 0.f;
+#else
   float m_run = -1e30f;
+#endif
   // S^T(s) from K(s): fragments read ahead of their MFMAs; the second half only where it holds a
   // visible key (its fragments are read anyway: an LDS read of a stale buffer is harmless)
-  auto scores = [&](int s, f32x16& sa, f32x16& sb) {
+  auto scores = [&](int s, f32x16& sa, f32x16& sb, const f32x16& cinit) {
     const bf16* kt = kbuf(bufi(s));
     bf16x8 ka[D / 16], kb8[D / 16];
 #pragma unroll
@@ -253,8 +286,11 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     // out a whole LDS latency: lgkmcnt(0) per read)
     __builtin_amdgcn_sched_barrier(0);
 #endif
+#if P32_CINIT
+    sa = cinit;
+#else
     sa = f32x16{};
-    sb = f32x16{};
+#endif
 #pragma unroll
     for (int m = 0; m < D / 16; ++m) {
       kb8[m] = *reinterpret_cast<const bf16x8*>(kt + 32 * CH * 8 + koff + ((2 * m + hh) ^ kx) * 8);
@@ -267,10 +303,23 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
 #if P32_KREAD
     __builtin_amdgcn_sched_barrier(0);
 #endif
+#if P32_CINIT
+    // (the second chain's first MFMA reads cinit in place; a half past every column is never
+    // read - every one of its keys is masked - so the skipped branch leaves sb as it is)
     if (full2(s)) {
+      sb = mfma32(kb8[0], qf[0], cinit);
 #pragma unroll
-      for (int m = 0; m < D / 16; ++m) sb = mfma32(kb8[m], qf[m], sb);
+      for (int m = 1; m < D / 16; ++m) sb = mfma32(kb8[m], qf[m], sb);
     }
+#else
+    // (a half past every column keeps whatever sb held: the causal mask overwrites all of it -
+    // such a step is always a diagonal one - so no per-step zeroing of 16 registers)
+    if (full2(s)) {
+      sb = mfma32(kb8[0], qf[0], f32x16{});
+#pragma unroll
+      for (int m = 1; m < D / 16; ++m) sb = mfma32(kb8[m], qf[m], sb);
+    }
+#endif
   };
   // online softmax of S(s): causal mask on diagonal steps, row max (one cross-half exchange),
   // deferred max (T13: the running max moves only when some column grew by more than THR),
@@ -287,6 +336,47 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     }
     // IEEE maximum (NaN-propagating) lowers to v_maximum3_f32, one per two scores; fmaxf's
     // maxnum would first canonicalise every MFMA output with a v_max_f32 x, x of its own
+#if P32_CINIT
+    float mx;
+    {
+      auto mx3 = [](float a, float b, float c) {
+        return __builtin_elementwise_maximum(a, __builtin_elementwise_maximum(b, c));
+      };
+      float c4[4];   // four independent chains of v_maximum3 over 8 scores each
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const f32x16& v = k < 2 ? sa : sb;
+        const int o8 = (k & 1) * 8;
+        float a = mx3(v[o8], v[o8 + 1], v[o8 + 2]);
+        a = mx3(a, v[o8 + 3], v[o8 + 4]);
+        a = mx3(a, v[o8 + 5], v[o8 + 6]);
+        c4[k] = __builtin_elementwise_maximum(a, v[o8 + 7]);
+      }
+      mx = __builtin_elementwise_maximum(mx3(c4[0], c4[1], c4[2]), c4[3]);
+    }
+    mx = xhalf_max(mx);
+    // S' is already relative to m_run: the running max moves when some column grew by > THR
+    // (and on the first step, which sets it)
+    const bool first = s == 0;
+    resc = first || __any(mx > P32_THR);
+    if (resc) {   // wave-uniform, rare after the first step
+      const float delta = first ? mx : fmaxf(mx, 0.f);
+      alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);
+      m_run += delta;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sa[r] = __builtin_amdgcn_exp2f(sa[r] - delta);
+        sb[r] = __builtin_amdgcn_exp2f(sb[r] - delta);
+      }
+    } else {
+      alpha = 1.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sa[r] = __builtin_amdgcn_exp2f(sa[r]);
+        sb[r] = __builtin_amdgcn_exp2f(sb[r]);
+      }
+    }
+#else
     float mx = __builtin_elementwise_maximum(sa[0], sb[0]);
 #pragma unroll
     for (int r = 1; r < 16; ++r)
@@ -306,6 +396,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
       sa[r] = __builtin_amdgcn_exp2f(fmaf(sa[r], sl2, -m_new));
       sb[r] = __builtin_amdgcn_exp2f(fmaf(sb[r], sl2, -m_new));
     }
+#endif
     float ps0 = sa[0], ps1 = sb[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) {
@@ -374,30 +465,86 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
       }
     }
   };
-  auto dma_step = [&](int s) {   // K and V^T of step s into its buffer
-    size_t e00, e01;
-    pages(s, e00, e01);
-    dma(s, kbuf(bufi(s)), false, e00, e01);
-    dma(s, vbuf(bufi(s)), true, e00, e01);
-  };
 
+  // this wave's DMA of step s2 - LA + 1 has landed; with lookahead 2, step s2's pieces (issued
+  // after it, loads complete in order) may stay in flight: 2 per image with both halves, else 1
+  auto wait_landed = [&](int s2) {
+    if (!DA || s2 >= nsteps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (full2(s2)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  };
+  // (with lookahead 2 the step barrier is a bare s_barrier: __syncthreads' release fence would
+  // drain vmcnt to 0 and land the step ahead too; the waits above make the landed step visible)
+  auto step_barrier = [&]() {
+    if (DA) asm volatile("s_barrier" ::: "memory");
+    else __syncthreads();
+  };
   dma_step(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  f32x16 sa, sb;
+  if (DA && nsteps > 1) dma_step(1);
+  wait_landed(LA - 1);
+  step_barrier();
+  f32x16 sa, sb = f32x16{};
   bf16x8 pp[4];
   float alpha;
   bool resc;
+#if P32_CINIT
+  // The S chains read cinit = -m_run, which changes only when the running max moves (first
+  // step, then rarely): each "version" of it is a loop of its own, so inside one the operand is
+  // loop-invariant (a value updated on a rare branch inside the loop made the compiler shuffle
+  // all 16 registers on every step).  A step whose softmax moved the max ends its version.
+  int s = 0;
+  if (!STAG || w < NW / 2) {
+    for (bool more = nsteps > 0; more;) {
+      f32x16 ci;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ci[r] = -m_run;
+      for (;;) {
+        scores(s, sa, sb, ci);
+        if (s + 1 < nsteps) dma_step(s + 1);
+        softmax(s, sa, sb, pp, alpha, resc);
+        pv(s, pp, alpha, resc);
+        wait_landed(s + 1);
+        step_barrier();
+        if (++s == nsteps) { more = false; break; }
+        if (resc) break;
+      }
+    }
+  } else {
+    // staggered half: interval s runs softmax(s-1) | PV(s-1) | S(s); a version ends between
+    // PV(s-1) and S(s), which then reads the new cinit
+    bool first = true;
+    for (bool more = nsteps > 0; more;) {
+      f32x16 ci;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) ci[r] = -m_run;
+      for (;;) {
+        if (!first) {
+          softmax(s - 1, sa, sb, pp, alpha, resc);
+          pv(s - 1, pp, alpha, resc);
+          if (s == nsteps) { more = false; break; }
+          if (resc) { first = true; break; }   // (re-enter at the S(s) below, new cinit)
+        }
+        first = false;
+        if (s + 1 < nsteps) dma_step(s + 1);
+        scores(s, sa, sb, ci);
+        wait_landed(s + 1);
+        step_barrier();
+        ++s;
+      }
+      if (more) first = true;
+    }
+  }
+#else
   if (!STAG || w < NW / 2) {
     // interval s: S(s) | softmax(s) | PV(s); the DMA of step s+1 is issued behind the first
     // MFMAs, so its block-table lookups (scalar loads waited in place) overlap the matrix pipe
     for (int s = 0; s < nsteps; ++s) {
-      scores(s, sa, sb);
-      if (s + 1 < nsteps) dma_step(s + 1);
+      scores(s, sa, sb, o[0]);
+      if (s + LA < nsteps) dma_step(s + LA);
       softmax(s, sa, sb, pp, alpha, resc);
       pv(s, pp, alpha, resc);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of step s+1 landed
-      __syncthreads();
+      wait_landed(s + LA);   // this wave's DMA of step s+1 landed
+      step_barrier();
     }
   } else {
     // the stagger (MI355X_MICROARCH.md "Two waves per SIMD", item 9): waves NW/2.. (one per
@@ -406,18 +553,20 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     // computing, then both exponentiating.  S(s-1) stays in registers across the barrier and
     // V(s-1) in its buffer (three buffers: the DMA of interval s writes step s+1's).
     for (int s = 0; s < nsteps; ++s) {
+      if (DA && s + 2 < nsteps) dma_step(s + 2);   // its buffer held step s-2: read in s-1
       if (s > 0) {
         softmax(s - 1, sa, sb, pp, alpha, resc);
         pv(s - 1, pp, alpha, resc);
       }
-      if (s + 1 < nsteps) dma_step(s + 1);
-      scores(s, sa, sb);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      if (!DA && s + 1 < nsteps) dma_step(s + 1);
+      scores(s, sa, sb, o[0]);
+      wait_landed(s + LA);
+      step_barrier();
     }
     softmax(nsteps - 1, sa, sb, pp, alpha, resc);
     pv(nsteps - 1, pp, alpha, resc);
   }
+#endif
   // ---- normalise and store: register r of o[db] is d = 32 db + (r & 3) + 8 (r >> 2) + 4 hh ----
   float lsum = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
