@@ -34,10 +34,15 @@
 //   * causality from seq_lens / q_start (no mask tensor); steps entirely below the diagonal skip
 //     the mask, the half of a diagonal step past every column's position skips its MFMAs.
 //   * work list: the (sequence, tile) map of attention.hip walked heaviest tile first (the
-//     causal tail), XCD-grouped so consecutive tiles of one kv head share an L2.
+//     causal tail), XCD-grouped so consecutive tiles of one kv head share an L2.  (A persistent
+//     form for 4-wave workgroups, P32_PERSIST, walks several tiles with the next tile's Q and
+//     first step in flight during the stores: measured, off.)
+//   * counted LDS waits: K / V^T fragment reads issued ahead of their MFMAs, the DMA in its
+//     buffer form (docs/kernels.md "Second pass"); output staged through LDS, stored as rows.
 #include "kernels.h"
 #include "attn_core.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace dli {
@@ -49,35 +54,25 @@ constexpr float P32_THR = 8.f;   // deferred-max threshold (log2 domain)
 #ifndef P32_STAGGER
 #define P32_STAGGER 1   // 0: every wave runs S | softmax | PV in the same order
 #endif
-#ifndef P32_PRIO
-#define P32_PRIO 0   // 1: static s_setprio 1 for the second half of the waves
+#ifndef P32_PERSIST
+// 1: 4-wave workgroups persistent (two per CU), the next tile's Q and first K / V^T step
+// fetched while this tile's output is stored.  Measured off: 512-token prompts 486 vs 496 TF,
+// 4k 946 vs 984 (profiles/r6/prefill32b/r6p32j_*) - two co-resident workgroups per CU already
+// overlap one tile's Q / O traffic with another's steps, and the dispatcher balances better.
+#define P32_PERSIST 0
 #endif
-#ifndef P32_PERM
-#define P32_PERM 1   // 1: the cross-half row max by v_permlane32_swap instead of ds_bpermute
-#endif
+// knock-out probes (wrong results; scripts/prefill_so_ab.sh arms, docs/kernels.md)
 #ifndef P32_KO_PAGES
-#define P32_KO_PAGES 0   // knock-out probe only (wrong results unless pages are identity)
+#define P32_KO_PAGES 0   // block table read as identity
 #endif
 #ifndef P32_KO_Q
-#define P32_KO_Q 0   // knock-out probe only (wrong results)
+#define P32_KO_Q 0       // no Q load
 #endif
 #ifndef P32_KO_OUT
-#define P32_KO_OUT 0   // knock-out probe only (wrong results)
+#define P32_KO_OUT 0     // no output stores
 #endif
 #ifndef P32_KO_LOOP
-#define P32_KO_LOOP 0   // knock-out probe only (wrong results)
-#endif
-#ifndef P32_CINIT
-#define P32_CINIT 0   // 1: S MFMA chains start from -m_run (Q pre-scaled): P = exp2(S'), no FMA
-#endif
-#ifndef P32_DEPTH2
-#define P32_DEPTH2 0   // 1: staggered workgroups fetch K / V two steps ahead (four buffers)
-#endif
-#ifndef P32_OSTAGE
-#define P32_OSTAGE 1   // 1: the output staged through LDS and stored as whole rows
-#endif
-#ifndef P32_KREAD
-#define P32_KREAD 1   // 1: a step's 16 K fragment reads all issued ahead of its S MFMAs
+#define P32_KO_LOOP 0    // one key step per tile
 #endif
 
 __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
@@ -109,96 +104,102 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   constexpr int D = P32_D;
   constexpr int CH = D / 8;                 // 16-B chunks per K row
   constexpr int NW = GW * TQ / 32;          // waves per workgroup
-  constexpr int DPW = 32 / NW;              // LDS-DMA wave-instructions per wave per step
   // staggered waves (8-wave workgroups, one per CU) keep V(s-1) while step s+1 lands: 3 buffers
   constexpr bool STAG = P32_STAGGER && NW == 8;
-  // DMA two steps ahead (staggered workgroups): four buffers, step s+2 lands during step s
-  constexpr bool DA = P32_DEPTH2 && STAG;
-  constexpr int LA = DA ? 2 : 1;            // DMA lookahead in steps
-  constexpr int NBUF = DA ? 4 : (STAG ? 3 : 2);
+  constexpr int NBUF = STAG ? 3 : 2;
+  // persistent, with the next tile's Q / first step fetched during the last step (4-wave tiles)
+  constexpr bool PF = P32_PERSIST && !STAG;
   // [buf][K | V^T][64 keys x D]: NBUF x 2 x 16 KB
   __shared__ __attribute__((aligned(16))) bf16 smem[NBUF][2][64 * D];
 
   const int G = p.nh / p.nkv;
   const int wg_per_kv = G / GW;
-  int b, tile, grp;
-  if (p.tile_map) {
-    const int total = p.n_tiles * p.nkv * wg_per_kv;
-    const int per = (int)gridDim.x >> 3;
-    const int L8 = (int)blockIdx.x;
-    const int w = (L8 & 7) * per + (L8 >> 3);
-    if (w >= total) return;                 // padding (whole workgroup, before any barrier)
-    grp = w / p.n_tiles;
-    const int t = p.n_tiles - 1 - (w - grp * p.n_tiles);   // heaviest (last) tiles first
-    b = p.tile_map[2 * t];
-    tile = p.tile_map[2 * t + 1];
-  } else {
-    b = blockIdx.z;
-    tile = gridDim.x - 1 - blockIdx.x;
-    grp = blockIdx.y;
-  }
-  const int kvh = grp / wg_per_kv;
-  const int h0 = kvh * G + (grp % wg_per_kv) * GW;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane & 31, hh = lane >> 5;
-  if (P32_PRIO && w >= NW / 2) __builtin_amdgcn_s_setprio(1);
   const int R = 32 * w + c;
-  const int qh = h0 + R / TQ;
-  const int qs0 = p.q_start[b];
-  const int qlen = p.q_start[b + 1] - qs0;
-  const int t0 = tile * TQ;
-  if (t0 >= qlen) return;                   // whole workgroup idle
-  const int L = p.seq_lens[b];
-  const int tok = t0 + R % TQ;
-  const bool valid = tok < qlen;
-  const int pq = L - qlen + (valid ? tok : qlen - 1);          // this column's position
-  const int pq_lo = L - qlen + t0;                               // workgroup's first position
-  const int pq_hi = L - qlen + min(qlen - 1, t0 + TQ - 1);       // ... and last
-#if P32_KO_LOOP
-  const int nsteps = 1;   // knock-out probe only: the fixed per-workgroup cost
-#else
-  const int nsteps = (pq_hi + 64) >> 6;                          // keys [0, pq_hi]
-#endif
-  const int* bt = p.block_tables + (size_t)b * p.bt_stride;
   const size_t head_stride = (size_t)p.bs * D;
+  const int bs_lg = __builtin_ctz(p.bs);
+  const uint32_t page_elems = (uint32_t)p.nkv * (uint32_t)head_stride;
+
+  // ---- work items.  With a tile map the grid is 8 x `per` workgroups, XCD-major: XCD x
+  // (= blockIdx & 7) owns items [x span, (x+1) span) - one kv-head group's tiles, heaviest
+  // first - and its k-th workgroup walks items k, k + per, ... of them (per = span: one each).
+  // Without a map (dense grid) a workgroup is one (sequence, tile, group).
+  struct Item {
+    int b, t0, kvh, h0, qs0, qlen, L, pq_lo, pq_hi, nsteps;
+    const int* bt;
+  };
+  // Persistent walk: round n takes item n per + k on even rounds and n per + (per - 1 - k) on odd
+  // ones (a snake): the map lists each sequence's tiles heaviest first, so a plain stride that
+  // is a multiple of the tiles per sequence would hand one workgroup every sequence's heaviest
+  // tile and another every lightest.
+  int x0 = 0, k0 = 0, per = 1, span = 1, wi_end = 1, n = 0;
+  if (p.tile_map) {
+    const int total = p.n_tiles * p.nkv * wg_per_kv;
+    per = (int)gridDim.x >> 3;
+    span = (total + 7) >> 3;
+    x0 = ((int)blockIdx.x & 7) * span;
+    k0 = (int)blockIdx.x >> 3;
+    wi_end = min(total, x0 + span);
+  }
+  auto item_of = [&](int n_) { return x0 + n_ * per + ((n_ & 1) ? per - 1 - k0 : k0); };
+  int wi = item_of(0);
+  auto decode = [&](int wi_, Item& it) {   // false: an empty tile (dense grids only)
+    int b, tile, grp;
+    if (p.tile_map) {
+      grp = wi_ / p.n_tiles;
+      const int t = p.n_tiles - 1 - (wi_ - grp * p.n_tiles);   // heaviest (last) tiles first
+      b = p.tile_map[2 * t];
+      tile = p.tile_map[2 * t + 1];
+    } else {
+      b = blockIdx.z;
+      tile = gridDim.x - 1 - blockIdx.x;
+      grp = blockIdx.y;
+    }
+    it.b = b;
+    it.kvh = grp / wg_per_kv;
+    it.h0 = it.kvh * G + (grp % wg_per_kv) * GW;
+    it.qs0 = p.q_start[b];
+    it.qlen = p.q_start[b + 1] - it.qs0;
+    it.t0 = tile * TQ;
+    it.L = p.seq_lens[b];
+    it.pq_lo = it.L - it.qlen + it.t0;                                  // first position
+    it.pq_hi = it.L - it.qlen + min(it.qlen - 1, it.t0 + TQ - 1);      // ... and last
+#if P32_KO_LOOP
+    it.nsteps = 1;
+#else
+    it.nsteps = (it.pq_hi + 64) >> 6;                                   // keys [0, pq_hi]
+#endif
+    it.bt = p.block_tables + (size_t)b * p.bt_stride;
+    return it.t0 < it.qlen;
+  };
+  if (wi >= wi_end) return;                 // padding (whole workgroup, before any barrier)
+  Item cur;
+  if (!decode(wi, cur)) return;             // whole workgroup idle (dense grid)
 
   // ---- Q^T operand: lane (c, hh) holds d = 16 m + 8 hh + [0, 8) of its column, m = 0..7 ----
   // (rows past the chunk load the chunk's first token - always present - and are zeroed)
-  bf16x8 qf[D / 16];
-  {
-    const bf16* qrow = p.q + ((size_t)(qs0 + (valid ? tok : 0)) * p.nh + qh) * D + 8 * hh;
+  auto load_q = [&](const Item& it, bf16x8 (&q)[D / 16]) {
+    const int tok = it.t0 + R % TQ;
+    const bool valid = tok < it.qlen;
+    const bf16* qrow =
+        p.q + ((size_t)(it.qs0 + (valid ? tok : 0)) * p.nh + it.h0 + R / TQ) * D + 8 * hh;
 #pragma unroll
     for (int m = 0; m < D / 16; ++m) {
 #if P32_KO_Q
-      qf[m] = zero8(); (void)qrow;
+      q[m] = zero8(); (void)qrow;
 #else
-      qf[m] = *reinterpret_cast<const bf16x8*>(qrow + 16 * m);
-      if (!valid) qf[m] = zero8();
-#if P32_CINIT
-#pragma unroll
-      for (int j = 0; j < 8; ++j) qf[m][j] = (bf16)((float)qf[m][j] * p.scale_log2);
-#endif
+      q[m] = *reinterpret_cast<const bf16x8*>(qrow + 16 * m);
+      if (!valid) q[m] = zero8();
 #endif
     }
-  }
+  };
 
-  // ---- LDS-DMA: the K image or the V^T image (16 wave-instructions of 1 KB each, 16 / NW per
-  // wave) of one 64-key step.  Instruction j covers K rows 4j..4j+3 / V^T units 64j..64j+63;
-  // j >> 3 = its 32-key half.  A half past every column is never fetched (its block-table entry
-  // may not exist).
-  // (block size a power of two, eligibility: shifts, not divisions; both halves' pages by one
-  // pair of scalar loads waited once per step, shared by the K and the V^T image)
-  auto bufi = [&](int s) { return NBUF == 2 ? (s & 1) : NBUF == 4 ? (s & 3) : (s % 3); };
+  auto bufi = [&](int g) { return NBUF == 2 ? (g & 1) : (g % 3); };
   auto kbuf = [&](int i) { return &smem[i][0][0]; };
   auto vbuf = [&](int i) { return &smem[i][1][0]; };
-  const int bs_lg = __builtin_ctz(p.bs);
-  // one buffer resource per (page half, image) and step: base = the half's first key in this kv
-  // head's slice of the page (32-bit page stride: nkv * bs * D), and per-lane offsets that
-  // depend only on the piece index - computed once, outside the loop
-  const bf16* kbase = static_cast<const bf16*>(p.k_cache) + (size_t)kvh * head_stride;
-  const bf16* vbase = static_cast<const bf16*>(p.v_cache) + (size_t)kvh * head_stride;
-  const uint32_t page_elems = (uint32_t)p.nkv * (uint32_t)head_stride;
+  // per-lane byte offsets of the LDS-DMA pieces: they depend only on the piece index
   constexpr int NPC = 16 / NW;              // pieces per image per wave and step
   int kvo[NPC], vvo[NPC];
 #pragma unroll
@@ -208,28 +209,32 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     kvo[i] = (swap23(row & 31) * D + 8 * (slot ^ (row & 15))) * 2;   // key pi(row) of its half
     vvo[i] = (u & 511) * 16;
   }
-  // one 1 KB piece: the resource starts at the half's first key (its offset folded into the
-  // base: this compiler drops the host-side kernel stubs - silently, a broken object - when the
-  // soffset operand of the builtin is a runtime value or the resource is built inline in the call)
-  auto piece = [&](const bf16* base, int pg, int half_off, bf16* dst, int vo) {
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(base + (size_t)(uint32_t)pg * page_elems + half_off), 0, 0x7fffffff, 0x00020000);
+  // one 1 KB piece: the resource starts at the half's first key in the kv head's slice of the
+  // page (its offset folded into the base: this compiler drops the host-side kernel stubs -
+  // silently, a broken object - when the builtin's soffset is a runtime value or the resource is
+  // built inline in the call)
+  auto piece = [&](const void* cache, int kvh, int pg, int half_off, bf16* dst, int vo) {
+    const bf16* base = static_cast<const bf16*>(cache) + (size_t)kvh * head_stride +
+                       (size_t)(uint32_t)pg * page_elems + half_off;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16,
                                              vo, 0, 0, 0);
   };
-  // ---- LDS-DMA of step s: K and V^T images (16 wave-instructions of 1 KB each per image,
-  // NPC per wave).  Piece i of wave w is instruction j = w + i NW: K rows 4j..4j+3 / V^T units
-  // 64j..64j+63, its 32-key half (j >> 3 = i NW >> 3) known at compile time.  A half past every
-  // column is never fetched (its block-table entry may not exist).  buffer_load ... lds rather
-  // than global_load_lds: the compiler's wait model treats the global form as an out-of-order
-  // LDS (lgkm) access, which turns every LDS-read wait after it into lgkmcnt(0).
-  auto dma_step = [&](int s) {
+  // ---- LDS-DMA of step s of tile `it` into buffer bi: K and V^T images (16 wave-instructions of
+  // 1 KB each per image, NPC per wave).  Piece i of wave w is instruction j = w + i NW: K rows
+  // 4j..4j+3 / V^T units 64j..64j+63, its 32-key half (j >> 3 = i NW >> 3) known at compile time.
+  // A half past every column is never fetched (its block-table entry may not exist).
+  // buffer_load ... lds rather than global_load_lds: the compiler's wait model treats the global
+  // form as an out-of-order LDS (lgkm) access, which turns every LDS-read wait after it into
+  // lgkmcnt(0).  Block size a power of two: shifts, not divisions; both halves' pages by one pair
+  // of scalar loads waited once per step.
+  auto dma_step = [&](const Item& it, int s, int bi) {
     const int u0 = s * 64;
-    const bool need1 = u0 + 32 <= pq_hi;
+    const bool need1 = u0 + 32 <= it.pq_hi;
     const int i0 = u0 >> bs_lg;
     const int i1 = need1 ? (u0 + 32) >> bs_lg : i0;
-    const int* a0 = bt + __builtin_amdgcn_readfirstlane(i0);
-    const int* a1 = bt + __builtin_amdgcn_readfirstlane(i1);
+    const int* a0 = it.bt + __builtin_amdgcn_readfirstlane(i0);
+    const int* a1 = it.bt + __builtin_amdgcn_readfirstlane(i1);
     int pg0, pg1;
 #if P32_KO_PAGES
     pg0 = i0; pg1 = i1; (void)a0; (void)a1;
@@ -239,391 +244,254 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
                  : "=&s"(pg0), "=&s"(pg1) : "s"(a0), "s"(a1));
     const int so0 = (u0 & (p.bs - 1)) * D;          // the halves' element offsets in their pages
     const int so1 = ((u0 + 32) & (p.bs - 1)) * D;
-    bf16* kd = kbuf(bufi(s));
-    bf16* vd = vbuf(bufi(s));
+    bf16* kd = kbuf(bi);
+    bf16* vd = vbuf(bi);
 #pragma unroll
     for (int i = 0; i < NPC; ++i) {
       const int half = (i * NW) >> 3;
       if (half && !need1) continue;
       const int j = w + i * NW;
       const int pg = half ? pg1 : pg0;
-      piece(kbase, pg, half ? so1 : so0, kd + j * 64 * 8, kvo[i]);
-      piece(vbase, pg, half ? so1 : so0, vd + j * 64 * 8, vvo[i]);
+      piece(p.k_cache, it.kvh, pg, half ? so1 : so0, kd + j * 64 * 8, kvo[i]);
+      piece(p.v_cache, it.kvh, pg, half ? so1 : so0, vd + j * 64 * 8, vvo[i]);
     }
   };
 
-  f32x16 o[D / 32];
-#pragma unroll
-  for (int db = 0; db < D / 32; ++db) o[db] = f32x16{};
-  float l_run = 0.f;
-  const float sl2 = p.scale_log2;
   // LDS fragment offsets (elements): K row c (half 0) chunk (2m + hh) ^ (c & 15); V^T unit (g, d)
   const int koff = c * CH * 8;
   const int kx = c & 15;
   const int voff = (hh * D + c) * 8;
-  auto full2 = [&](int s) { return s * 64 + 32 <= pq_hi; };   // second half holds a visible key
-  auto diag = [&](int s) { return s * 64 + 63 > pq_lo; };     // some key past some column
-  // ---- the three products of one 64-key step ----
-#if P32_CINIT
-  // Q is pre-scaled by scale * log2(e) and every S MFMA chain starts from cinit = -m_run, so
-  // S' = S log2(e) / sqrt(D) - m_run comes out of the matrix pipe and P = exp2(S') needs no FMA
-  // (the loop is vector-issue bound: MI355X_MICROARCH.md 'vector-instruction ISSUE cost')
-  float m_run = 0.f;
-#else
-  float m_run = -1e30f;
-#endif
-  // S^T(s) from K(s): fragments read ahead of their MFMAs; the second half only where it holds a
-  // visible key (its fragments are read anyway: an LDS read of a stale buffer is harmless)
-  auto scores = [&](int s, f32x16& sa, f32x16& sb, const f32x16& cinit) {
-    const bf16* kt = kbuf(bufi(s));
-    bf16x8 ka[D / 16], kb8[D / 16];
-#pragma unroll
-    for (int m = 0; m < D / 16; ++m)
-      ka[m] = *reinterpret_cast<const bf16x8*>(kt + koff + ((2 * m + hh) ^ kx) * 8);
-#if P32_KREAD
-    // the first half's 8 reads all issued before the first MFMA, then one second-half read per
-    // MFMA (the scheduler otherwise sinks each read to just before its MFMA, and every MFMA waits
-    // out a whole LDS latency: lgkmcnt(0) per read)
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-#if P32_CINIT
-    sa = cinit;
-#else
-    sa = f32x16{};
-#endif
-#pragma unroll
-    for (int m = 0; m < D / 16; ++m) {
-      kb8[m] = *reinterpret_cast<const bf16x8*>(kt + 32 * CH * 8 + koff + ((2 * m + hh) ^ kx) * 8);
-      sa = mfma32(ka[m], qf[m], sa);
-#if P32_KREAD
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one DS read
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // then one MFMA
-#endif
-    }
-#if P32_KREAD
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-#if P32_CINIT
-    // (the second chain's first MFMA reads cinit in place; a half past every column is never
-    // read - every one of its keys is masked - so the skipped branch leaves sb as it is)
-    if (full2(s)) {
-      sb = mfma32(kb8[0], qf[0], cinit);
-#pragma unroll
-      for (int m = 1; m < D / 16; ++m) sb = mfma32(kb8[m], qf[m], sb);
-    }
-#else
-    // (a half past every column keeps whatever sb held: the causal mask overwrites all of it -
-    // such a step is always a diagonal one - so no per-step zeroing of 16 registers)
-    if (full2(s)) {
-      sb = mfma32(kb8[0], qf[0], f32x16{});
-#pragma unroll
-      for (int m = 1; m < D / 16; ++m) sb = mfma32(kb8[m], qf[m], sb);
-    }
-#endif
-  };
-  // online softmax of S(s): causal mask on diagonal steps, row max (one cross-half exchange),
-  // deferred max (T13: the running max moves only when some column grew by more than THR),
-  // P = exp2(S sl2 - m) packed to bf16; l is rescaled here, O by the PV that consumes P
-  auto softmax = [&](int s, f32x16& sa, f32x16& sb, bf16x8 (&pp)[4], float& alpha, bool& resc) {
-    if (diag(s)) {
-      const int kb = s * 64;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kb + 16 * (r >> 3) + 8 * hh + (r & 7);
-        sa[r] = key > pq ? -INFINITY : sa[r];
-        sb[r] = key + 32 > pq ? -INFINITY : sb[r];   // (an unread half: every key masked)
-      }
-    }
-    // IEEE maximum (NaN-propagating) lowers to v_maximum3_f32, one per two scores; fmaxf's
-    // maxnum would first canonicalise every MFMA output with a v_max_f32 x, x of its own
-#if P32_CINIT
-    float mx;
-    {
-      auto mx3 = [](float a, float b, float c) {
-        return __builtin_elementwise_maximum(a, __builtin_elementwise_maximum(b, c));
-      };
-      float c4[4];   // four independent chains of v_maximum3 over 8 scores each
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const f32x16& v = k < 2 ? sa : sb;
-        const int o8 = (k & 1) * 8;
-        float a = mx3(v[o8], v[o8 + 1], v[o8 + 2]);
-        a = mx3(a, v[o8 + 3], v[o8 + 4]);
-        a = mx3(a, v[o8 + 5], v[o8 + 6]);
-        c4[k] = __builtin_elementwise_maximum(a, v[o8 + 7]);
-      }
-      mx = __builtin_elementwise_maximum(mx3(c4[0], c4[1], c4[2]), c4[3]);
-    }
-    mx = xhalf_max(mx);
-    // S' is already relative to m_run: the running max moves when some column grew by > THR
-    // (and on the first step, which sets it)
-    const bool first = s == 0;
-    resc = first || __any(mx > P32_THR);
-    if (resc) {   // wave-uniform, rare after the first step
-      const float delta = first ? mx : fmaxf(mx, 0.f);
-      alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);
-      m_run += delta;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sa[r] = __builtin_amdgcn_exp2f(sa[r] - delta);
-        sb[r] = __builtin_amdgcn_exp2f(sb[r] - delta);
-      }
-    } else {
-      alpha = 1.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sa[r] = __builtin_amdgcn_exp2f(sa[r]);
-        sb[r] = __builtin_amdgcn_exp2f(sb[r]);
-      }
-    }
-#else
-    float mx = __builtin_elementwise_maximum(sa[0], sb[0]);
-#pragma unroll
-    for (int r = 1; r < 16; ++r)
-      mx = __builtin_elementwise_maximum(mx, __builtin_elementwise_maximum(sa[r], sb[r]));
-#if P32_PERM
-    mx = xhalf_max(mx);
-#else
-    mx = __builtin_elementwise_maximum(mx, __shfl_xor(mx, 32, 64));
-#endif
-    const float pmax = mx * sl2;
-    resc = __any(pmax > m_run + P32_THR);
-    const float m_new = resc ? fmaxf(m_run, pmax) : m_run;
-    alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-    m_run = m_new;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sa[r] = __builtin_amdgcn_exp2f(fmaf(sa[r], sl2, -m_new));
-      sb[r] = __builtin_amdgcn_exp2f(fmaf(sb[r], sl2, -m_new));
-    }
-#endif
-    float ps0 = sa[0], ps1 = sb[0];
-#pragma unroll
-    for (int r = 1; r < 16; ++r) {
-      ps0 += sa[r];
-      ps1 += sb[r];
-    }
-    l_run = l_run * alpha + (ps0 + ps1);
-    pp[0] = pack8(sa, 0);
-    pp[1] = pack8(sa, 8);
-    pp[2] = pack8(sb, 0);
-    pp[3] = pack8(sb, 8);
-  };
-  // O^T = alpha O^T + V^T(s) P^T(s); the second half only where it holds a visible key (a V^T
-  // image never loaded must not reach the accumulators, even times zero)
-  auto pv = [&](int s, const bf16x8 (&pp)[4], float alpha, bool resc) {
-    if (resc) {
-#pragma unroll
-      for (int db = 0; db < D / 32; ++db) o[db] *= alpha;
-    }
-    const bf16* vt = vbuf(bufi(s));
-#if P32_KREAD
-    // as in scores: the first half's 8 reads ahead, then one second-half read per MFMA
-    bf16x8 va[D / 16], vb[D / 16];
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
-      va[2 * db] = *reinterpret_cast<const bf16x8*>(vt + voff + (0 * D + 32 * db) * 8);
-      va[2 * db + 1] = *reinterpret_cast<const bf16x8*>(vt + voff + (2 * D + 32 * db) * 8);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
-      vb[2 * db] = *reinterpret_cast<const bf16x8*>(vt + voff + (4 * D + 32 * db) * 8);
-      o[db] = mfma32(va[2 * db], pp[0], o[db]);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      vb[2 * db + 1] = *reinterpret_cast<const bf16x8*>(vt + voff + (6 * D + 32 * db) * 8);
-      o[db] = mfma32(va[2 * db + 1], pp[1], o[db]);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (full2(s)) {
-#pragma unroll
-      for (int db = 0; db < D / 32; ++db) {
-        o[db] = mfma32(vb[2 * db], pp[2], o[db]);
-        o[db] = mfma32(vb[2 * db + 1], pp[3], o[db]);
-      }
-    }
-    if (false) {
-#else
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db) {
-      const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(vt + voff + (0 * D + 32 * db) * 8);
-      const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(vt + voff + (2 * D + 32 * db) * 8);
-      o[db] = mfma32(v0, pp[0], o[db]);
-      o[db] = mfma32(v1, pp[1], o[db]);
-    }
-    if (full2(s)) {
-#endif
-#pragma unroll
-      for (int db = 0; db < D / 32; ++db) {
-        const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(vt + voff + (4 * D + 32 * db) * 8);
-        const bf16x8 v3 = *reinterpret_cast<const bf16x8*>(vt + voff + (6 * D + 32 * db) * 8);
-        o[db] = mfma32(v2, pp[2], o[db]);
-        o[db] = mfma32(v3, pp[3], o[db]);
-      }
-    }
-  };
+  const float sl2 = p.scale_log2;
 
-  // this wave's DMA of step s2 - LA + 1 has landed; with lookahead 2, step s2's pieces (issued
-  // after it, loads complete in order) may stay in flight: 2 per image with both halves, else 1
-  auto wait_landed = [&](int s2) {
-    if (!DA || s2 >= nsteps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (full2(s2)) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  };
-  // (with lookahead 2 the step barrier is a bare s_barrier: __syncthreads' release fence would
-  // drain vmcnt to 0 and land the step ahead too; the waits above make the landed step visible)
-  auto step_barrier = [&]() {
-    if (DA) asm volatile("s_barrier" ::: "memory");
-    else __syncthreads();
-  };
-  dma_step(0);
-  if (DA && nsteps > 1) dma_step(1);
-  wait_landed(LA - 1);
-  step_barrier();
-  f32x16 sa, sb = f32x16{};
-  bf16x8 pp[4];
-  float alpha;
-  bool resc;
-#if P32_CINIT
-  // The S chains read cinit = -m_run, which changes only when the running max moves (first
-  // step, then rarely): each "version" of it is a loop of its own, so inside one the operand is
-  // loop-invariant (a value updated on a rare branch inside the loop made the compiler shuffle
-  // all 16 registers on every step).  A step whose softmax moved the max ends its version.
-  int s = 0;
-  if (!STAG || w < NW / 2) {
-    for (bool more = nsteps > 0; more;) {
-      f32x16 ci;
+  bf16x8 qf[D / 16];
+  load_q(cur, qf);
+  int g0 = 0;                               // global step count: buffer of (tile, step s) = g0 + s
+  dma_step(cur, 0, bufi(0));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (;;) {
+    // ---- one tile ----
+    const int nsteps = cur.nsteps;
+    const int pq_lo = cur.pq_lo, pq_hi = cur.pq_hi;
+    const int tok = cur.t0 + R % TQ;
+    const int pq = cur.L - cur.qlen + (tok < cur.qlen ? tok : cur.qlen - 1);   // column position
+
+    f32x16 o[D / 32];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) ci[r] = -m_run;
-      for (;;) {
-        scores(s, sa, sb, ci);
-        if (s + 1 < nsteps) dma_step(s + 1);
+    for (int db = 0; db < D / 32; ++db) o[db] = f32x16{};
+    float l_run = 0.f;
+    float m_run = -1e30f;
+    auto full2 = [&](int s) { return s * 64 + 32 <= pq_hi; };   // second half holds a visible key
+    auto diag = [&](int s) { return s * 64 + 63 > pq_lo; };     // some key past some column
+    // S^T(s) from K(s): the first half's 8 fragment reads all issued before the first MFMA, then
+    // one second-half read per MFMA (the scheduler otherwise sinks each read to just before its
+    // MFMA, and every MFMA waits out a whole LDS latency); the second half's MFMAs only where it
+    // holds a visible key (a half past every column keeps whatever sb held: the causal mask
+    // overwrites all of it - such a step is always a diagonal one - so no per-step zeroing)
+    auto scores = [&](int s, f32x16& sa, f32x16& sb) {
+      const bf16* kt = kbuf(bufi(g0 + s));
+      bf16x8 ka[D / 16], kb8[D / 16];
+#pragma unroll
+      for (int m = 0; m < D / 16; ++m)
+        ka[m] = *reinterpret_cast<const bf16x8*>(kt + koff + ((2 * m + hh) ^ kx) * 8);
+      __builtin_amdgcn_sched_barrier(0);
+      sa = f32x16{};
+#pragma unroll
+      for (int m = 0; m < D / 16; ++m) {
+        kb8[m] = *reinterpret_cast<const bf16x8*>(kt + 32 * CH * 8 + koff + ((2 * m + hh) ^ kx) * 8);
+        sa = mfma32(ka[m], qf[m], sa);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // one DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // then one MFMA
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (full2(s)) {
+        sb = mfma32(kb8[0], qf[0], f32x16{});
+#pragma unroll
+        for (int m = 1; m < D / 16; ++m) sb = mfma32(kb8[m], qf[m], sb);
+      }
+    };
+    // online softmax of S(s): causal mask on diagonal steps, row max (one cross-half exchange),
+    // deferred max (T13: the running max moves only when some column grew by more than THR),
+    // P = exp2(S sl2 - m) packed to bf16; l is rescaled here, O by the PV that consumes P
+    auto softmax = [&](int s, f32x16& sa, f32x16& sb, bf16x8 (&pp)[4], float& alpha, bool& resc) {
+      if (diag(s)) {
+        const int kb = s * 64;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kb + 16 * (r >> 3) + 8 * hh + (r & 7);
+          sa[r] = key > pq ? -INFINITY : sa[r];
+          sb[r] = key + 32 > pq ? -INFINITY : sb[r];   // (an unread half: every key masked)
+        }
+      }
+      // IEEE maximum (NaN-propagating) lowers to v_maximum3_f32, one per two scores; fmaxf's
+      // maxnum would first canonicalise every MFMA output with a v_max_f32 x, x of its own
+      float mx = __builtin_elementwise_maximum(sa[0], sb[0]);
+#pragma unroll
+      for (int r = 1; r < 16; ++r)
+        mx = __builtin_elementwise_maximum(mx, __builtin_elementwise_maximum(sa[r], sb[r]));
+      mx = xhalf_max(mx);
+      const float pmax = mx * sl2;
+      resc = __any(pmax > m_run + P32_THR);
+      const float m_new = resc ? fmaxf(m_run, pmax) : m_run;
+      alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      m_run = m_new;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sa[r] = __builtin_amdgcn_exp2f(fmaf(sa[r], sl2, -m_new));
+        sb[r] = __builtin_amdgcn_exp2f(fmaf(sb[r], sl2, -m_new));
+      }
+      float ps0 = sa[0], ps1 = sb[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) {
+        ps0 += sa[r];
+        ps1 += sb[r];
+      }
+      l_run = l_run * alpha + (ps0 + ps1);
+      pp[0] = pack8(sa, 0);
+      pp[1] = pack8(sa, 8);
+      pp[2] = pack8(sb, 0);
+      pp[3] = pack8(sb, 8);
+    };
+    // O^T = alpha O^T + V^T(s) P^T(s), reads as in scores; the second half only where it holds a
+    // visible key (a V^T image never loaded must not reach the accumulators, even times zero)
+    auto pv = [&](int s, const bf16x8 (&pp)[4], float alpha, bool resc) {
+      if (resc) {
+#pragma unroll
+        for (int db = 0; db < D / 32; ++db) o[db] *= alpha;
+      }
+      const bf16* vt = vbuf(bufi(g0 + s));
+      bf16x8 va[D / 16], vb[D / 16];
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+        va[2 * db] = *reinterpret_cast<const bf16x8*>(vt + voff + (0 * D + 32 * db) * 8);
+        va[2 * db + 1] = *reinterpret_cast<const bf16x8*>(vt + voff + (2 * D + 32 * db) * 8);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db) {
+        vb[2 * db] = *reinterpret_cast<const bf16x8*>(vt + voff + (4 * D + 32 * db) * 8);
+        o[db] = mfma32(va[2 * db], pp[0], o[db]);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        vb[2 * db + 1] = *reinterpret_cast<const bf16x8*>(vt + voff + (6 * D + 32 * db) * 8);
+        o[db] = mfma32(va[2 * db + 1], pp[1], o[db]);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (full2(s)) {
+#pragma unroll
+        for (int db = 0; db < D / 32; ++db) {
+          o[db] = mfma32(vb[2 * db], pp[2], o[db]);
+          o[db] = mfma32(vb[2 * db + 1], pp[3], o[db]);
+        }
+      }
+    };
+    auto dma_next = [&](int s) {   // the DMA issued in interval s: step s+1
+      if (s + 1 < nsteps) dma_step(cur, s + 1, bufi(g0 + s + 1));
+    };
+
+    f32x16 sa, sb = f32x16{};
+    bf16x8 pp[4];
+    float alpha;
+    bool resc;
+    if (!STAG || w < NW / 2) {
+      // interval s: S(s) | softmax(s) | PV(s); the DMA is issued behind the first MFMAs, so its
+      // block-table lookups (scalar loads waited in place) overlap the matrix pipe
+      for (int s = 0; s < nsteps; ++s) {
+        scores(s, sa, sb);
+        dma_next(s);
         softmax(s, sa, sb, pp, alpha, resc);
         pv(s, pp, alpha, resc);
-        wait_landed(s + 1);
-        step_barrier();
-        if (++s == nsteps) { more = false; break; }
-        if (resc) break;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA (and Q) landed
+        __syncthreads();
       }
-    }
-  } else {
-    // staggered half: interval s runs softmax(s-1) | PV(s-1) | S(s); a version ends between
-    // PV(s-1) and S(s), which then reads the new cinit
-    bool first = true;
-    for (bool more = nsteps > 0; more;) {
-      f32x16 ci;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) ci[r] = -m_run;
-      for (;;) {
-        if (!first) {
+    } else {
+      // the stagger (MI355X_MICROARCH.md "Two waves per SIMD", item 9): waves NW/2.. (one per
+      // SIMD, paired with a wave of the first half) run interval s as softmax(s-1) | PV(s-1) |
+      // S(s), so each SIMD's two waves put vector work beside matrix work instead of both
+      // computing, then both exponentiating.  S(s-1) stays in registers across the barrier and
+      // V(s-1) in its buffer (three buffers: the DMA of interval s writes step s+1's).
+      for (int s = 0; s < nsteps; ++s) {
+        if (s > 0) {
           softmax(s - 1, sa, sb, pp, alpha, resc);
           pv(s - 1, pp, alpha, resc);
-          if (s == nsteps) { more = false; break; }
-          if (resc) { first = true; break; }   // (re-enter at the S(s) below, new cinit)
         }
-        first = false;
-        if (s + 1 < nsteps) dma_step(s + 1);
-        scores(s, sa, sb, ci);
-        wait_landed(s + 1);
-        step_barrier();
-        ++s;
+        dma_next(s);
+        scores(s, sa, sb);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
       }
-      if (more) first = true;
+      softmax(nsteps - 1, sa, sb, pp, alpha, resc);
+      pv(nsteps - 1, pp, alpha, resc);
     }
-  }
-#else
-  if (!STAG || w < NW / 2) {
-    // interval s: S(s) | softmax(s) | PV(s); the DMA of step s+1 is issued behind the first
-    // MFMAs, so its block-table lookups (scalar loads waited in place) overlap the matrix pipe
-    for (int s = 0; s < nsteps; ++s) {
-      scores(s, sa, sb, o[0]);
-      if (s + LA < nsteps) dma_step(s + LA);
-      softmax(s, sa, sb, pp, alpha, resc);
-      pv(s, pp, alpha, resc);
-      wait_landed(s + LA);   // this wave's DMA of step s+1 landed
-      step_barrier();
+
+    // ---- normalise and store through LDS, so that the stores leave as whole rows: the register
+    // layout has each lane hold 4 d values (d = 32 db + (r & 3) + 8 (r >> 2) + 4 hh) of ONE row,
+    // and direct per-lane 8-byte stores touched 32 rows (lines) per instruction - store-issue
+    // bound, the tail of every workgroup (MI355X_MICROARCH.md constants 'attention epilogue store
+    // tail').  Staging image: row R = 32 w + c (= head R / TQ, token R % TQ) of 128 d, 16-byte
+    // chunk j at j ^ (R & 15), in the buffer of this tile's last step (all of it read by now; the
+    // next tile's first step lands in the other) - or, staggered, buffers 0-1 (64 KB, no
+    // prefetch in flight); then each wave-instruction stores 4 whole rows of one token (adjacent
+    // heads: 1 KB contiguous in [token][head][d]).
+    const float lsum = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    if (STAG) __syncthreads();                  // every wave is past its last V^T read
+    // persistent: the next tile's Q (into qf, dead now) and its first K / V^T step (into the
+    // buffer after this tile's last one) are in flight while this tile's output is staged and
+    // stored; the block-table, q_start and seq_lens lookups for it too
+    const int wi_next = item_of(n + 1);
+    Item nxt;
+    const bool more = PF && wi_next < wi_end && decode(wi_next, nxt);
+    if (more) {
+      dma_step(nxt, 0, bufi(g0 + nsteps));
+      load_q(nxt, qf);
     }
-  } else {
-    // the stagger (MI355X_MICROARCH.md "Two waves per SIMD", item 9): waves NW/2.. (one per
-    // SIMD, paired with a wave of the first half) run interval s as softmax(s-1) | PV(s-1) |
-    // S(s), so each SIMD's two waves put vector work beside matrix work instead of both
-    // computing, then both exponentiating.  S(s-1) stays in registers across the barrier and
-    // V(s-1) in its buffer (three buffers: the DMA of interval s writes step s+1's).
-    for (int s = 0; s < nsteps; ++s) {
-      if (DA && s + 2 < nsteps) dma_step(s + 2);   // its buffer held step s-2: read in s-1
-      if (s > 0) {
-        softmax(s - 1, sa, sb, pp, alpha, resc);
-        pv(s - 1, pp, alpha, resc);
-      }
-      if (!DA && s + 1 < nsteps) dma_step(s + 1);
-      scores(s, sa, sb, o[0]);
-      wait_landed(s + LA);
-      step_barrier();
+    bf16* stg = STAG ? &smem[0][0][0] : kbuf(bufi(g0 + nsteps - 1));
+    {
+      bf16* srow = stg + (size_t)R * D + 4 * hh;
+#pragma unroll
+      for (int db = 0; db < D / 32; ++db)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          bf16x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[db][4 * a + r] * inv);
+          *reinterpret_cast<bf16x4*>(srow + ((4 * db + a) ^ (R & 15)) * 8) = v;
+        }
     }
-    softmax(nsteps - 1, sa, sb, pp, alpha, resc);
-    pv(nsteps - 1, pp, alpha, resc);
-  }
-#endif
-  // ---- normalise and store: register r of o[db] is d = 32 db + (r & 3) + 8 (r >> 2) + 4 hh ----
-  float lsum = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-#if P32_OSTAGE
-  // through LDS, so that the stores leave as whole rows: the register layout has each lane hold
-  // 4 d values of ONE row, and direct per-lane 8-byte stores touched 32 rows (lines) per
-  // instruction - store-issue bound, the tail of every workgroup (MI355X_MICROARCH.md constants
-  // 'attention epilogue store tail').  Staging image: row R = 32 w + c (= head R / TQ, token
-  // R % TQ) of 128 d, 16-byte chunk j at j ^ (R & 15); then each wave-instruction stores 4
-  // whole rows of one token (adjacent heads: 1 KB contiguous in [token][head][d]).
-  __syncthreads();   // every wave is past its last K / V^T read
-  bf16* stg = &smem[0][0][0];
-  {
-    bf16* srow = stg + (size_t)R * D + 4 * hh;
+    __syncthreads();
+    constexpr int PER = TQ * GW * (D / 8) / 64 / NW;   // store instructions per wave
+    const int nvalid = min(TQ, cur.qlen - cur.t0);
 #pragma unroll
-    for (int db = 0; db < D / 32; ++db)
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        bf16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[db][4 * a + r] * inv);
-        *reinterpret_cast<bf16x4*>(srow + ((4 * db + a) ^ (R & 15)) * 8) = v;
-      }
-  }
-  __syncthreads();
-  constexpr int PER = TQ * GW * (D / 8) / 64 / NW;   // store instructions per wave
-  const int nvalid = min(TQ, qlen - t0);
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const int i = (k * NW + w) * 64 + lane;
-    const int chunk = i & 15, rr = i >> 4;
-    const int head = rr % GW, token = rr / GW;
-    const int R2 = head * TQ + token;
+    for (int k = 0; k < PER; ++k) {
+      const int i = (k * NW + w) * 64 + lane;
+      const int chunk = i & 15, rr = i >> 4;
+      const int head = rr % GW, token = rr / GW;
+      const int R2 = head * TQ + token;
 #if P32_KO_OUT
-    if (token < nvalid && lsum == 12345.f) {
+      if (token < nvalid && lsum == 12345.f) {
 #else
-    if (token < nvalid) {
+      if (token < nvalid) {
 #endif
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(stg + (size_t)R2 * D + (chunk ^ (R2 & 15)) * 8);
-      *reinterpret_cast<bf16x8*>(p.out + ((size_t)(qs0 + t0 + token) * p.nh + h0 + head) * D +
-                                 chunk * 8) = v;
-    }
-  }
-#else
-  if (valid) {
-    bf16* orow = p.out + ((size_t)(qs0 + tok) * p.nh + qh) * D + 4 * hh;
-#pragma unroll
-    for (int db = 0; db < D / 32; ++db)
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        bf16x4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (bf16)(o[db][4 * a + r] * inv);
-        *reinterpret_cast<bf16x4*>(orow + 32 * db + 8 * a) = v;
+        const bf16x8 v =
+            *reinterpret_cast<const bf16x8*>(stg + (size_t)R2 * D + (chunk ^ (R2 & 15)) * 8);
+        *reinterpret_cast<bf16x8*>(p.out + ((size_t)(cur.qs0 + cur.t0 + token) * p.nh + cur.h0 +
+                                            head) * D + chunk * 8) = v;
       }
+    }
+    if (!more) break;
+    // the next tile's first step (and Q) landed; the staging buffer is its step-1 buffer: every
+    // wave's reads of it first
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    g0 += nsteps;
+    ++n;
+    wi = wi_next;
+    cur = nxt;
   }
-#endif
 }
 
 // Eligible: head_dim 128, bf16 full cache, GQA group a multiple of 4, no custom mask.
@@ -643,7 +511,19 @@ int launch_attn_prefill32(const AttnParams& p, int B, int max_q, hipStream_t str
   dim3 grid((max_q + TQ - 1) / TQ, p.nkv * (G / gw), B);
   if (p.tile_map) {
     const long total = (long)p.n_tiles * p.nkv * (G / gw);
-    grid = dim3((unsigned)((total + 7) / 8 * 8), 1, 1);
+    long per = (total + 7) / 8;              // workgroups per XCD: one tile each ...
+    if (P32_PERSIST && nw != 8) {            // ... or persistent: the two a CU holds (64 KB LDS)
+      static int cus = 0;
+      if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+          cus = 0;
+        if (cus <= 0) cus = 256;
+      }
+      per = std::min(per, (long)(2 * cus / 8));
+    }
+    grid = dim3((unsigned)(per * 8), 1, 1);
   }
   if (grid.x == 0) return 0;
   if (gw == 8) {
