@@ -433,8 +433,8 @@ class KernelPolicy:
     # (1.6 vs 2.9 ms per 70B step, but one more byte per weight: a third less KV capacity)
     int8_transposed: bool = False
     # prefill attention on the 32x32x16-MFMA kernel (csrc/kernels/attn_prefill32.hip: 32 query
-    # rows per wave, 64-key steps) wherever it applies (bf16 full cache, head_dim 128, GQA group a
-    # multiple of 4, no custom mask); else attention.hip's 16x16x32 kernel
+    # rows per wave, 64-key steps) wherever it applies (bf16 full cache, head_dim 128, any GQA
+    # group incl. MHA, no custom mask); else attention.hip's 16x16x32 kernel
     prefill_m32: bool = True
 
     _FP8_SHAPES = ("qkv", "o", "gate_up", "down")

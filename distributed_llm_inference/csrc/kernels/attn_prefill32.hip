@@ -2,7 +2,7 @@
 //
 // Replaces the reference's eager prefill attention (modules.py:87-97: repeat_kv, QK^T/sqrt(D) +
 // additive causal mask, fp32 softmax, PV) for the common case - full (non-windowed) bf16 cache,
-// head_dim 128, GQA group a multiple of 4, no custom mask; attention.hip keeps the general kernel.
+// head_dim 128, no custom mask, any GQA group incl. MHA; attention.hip keeps the general kernel.
 //
 // Why a second kernel: attention.hip's prefill wave holds 16 query rows on the 16x16x32 MFMA, so
 // every K / V^T fragment read from LDS (one ds_read_b128) feeds ONE 16-cycle MFMA: four SIMDs ask
@@ -12,9 +12,10 @@
 // per FLOP (MI355X_MICROARCH.md "LDS"; cdna_hip_programming.md Appendix B "Fused attention
 // prefill").
 //
-// Layout of one workgroup = GW q heads of ONE kv head (GW = 8, or 4) x TQ query tokens (32, or 16
-// for short chunks), NW = GW * TQ / 32 waves; row R = 32 w + c of the workgroup is token R % TQ
-// of head R / TQ.  All waves share every K / V^T tile (GQA-native, no repeat_kv).
+// Layout of one workgroup = GW q heads of ONE kv head (GW = 8 or 4; 2 or 1 for groups that are
+// not a multiple of 4) x TQ query tokens (32, or 16 for short chunks; 64 / 32 for GW = 2, 128 / 64
+// for GW = 1), NW = GW * TQ / 32 waves; row R = 32 w + c of the workgroup is token R % TQ of head
+// R / TQ.  All waves share every K / V^T tile (GQA-native, no repeat_kv).
 //   * S^T[key, q] = K[key, d] . Q^T[d, q] (A = K rows from LDS, B = Q^T in registers): lane
 //     (c = l & 31, h = l >> 5) ends holding column c and accumulator rows (r&3) + 8(r>>2) + 4h.
 //     The K tile's LDS row i holds key pi(i) = i with bits 2 and 3 swapped, so register r of lane
@@ -494,19 +495,24 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   }
 }
 
-// Eligible: head_dim 128, bf16 full cache, GQA group a multiple of 4, no custom mask.
+// Eligible: head_dim 128, bf16 full cache, no custom mask, power-of-two block size; any GQA
+// group (a workgroup takes GW = 8, 4, 2 or 1 of its heads, the largest that divides it) - but a
+// group that is not a multiple of 4 only with the long-chunk tiles (prefill_qb 2): its short
+// tiles make 2-wave workgroups, and attention.hip's kernel is faster there (512-token prompts,
+// MHA 355 vs 309 TF; long chunks 571-620 vs 780-920: profiles/r6/gqa/).
 bool attn_prefill32_eligible(const AttnParams& p, int D) {
   const int G = p.nh / p.nkv;
   return p.prefill_m32 && D == P32_D && !p.kv_fp8 && p.ring == 0 && p.mask == nullptr &&
-         G % 4 == 0 && p.bs % 32 == 0 && (p.bs & (p.bs - 1)) == 0;
+         p.bs % 32 == 0 && (p.bs & (p.bs - 1)) == 0 && (G % 4 == 0 || p.prefill_qb == 2);
 }
 
-// Tile = 16 * prefill_qb query tokens (the same tile attention.hip's kernel uses at 4 heads per
-// wave, so one (sequence, tile) map serves both).
+// Tile = the one attention.hip's kernel uses (16 * (4 / min(GW, 4)) * prefill_qb query tokens:
+// 16 or 32 for groups of 4 and 8 heads, 32 or 64 for pairs, 64 or 128 for single heads - MHA or
+// an odd group such as Qwen2's 7), so one (sequence, tile) map serves both.
 int launch_attn_prefill32(const AttnParams& p, int B, int max_q, hipStream_t stream) {
   const int G = p.nh / p.nkv;
-  const int gw = G % 8 == 0 ? 8 : 4;
-  const int TQ = 16 * p.prefill_qb;
+  const int gw = G % 8 == 0 ? 8 : G % 4 == 0 ? 4 : G % 2 == 0 ? 2 : 1;
+  const int TQ = 16 * (4 / std::min(gw, 4)) * p.prefill_qb;
   const int nw = gw * TQ / 32;
   dim3 grid((max_q + TQ - 1) / TQ, p.nkv * (G / gw), B);
   if (p.tile_map) {
@@ -526,12 +532,19 @@ int launch_attn_prefill32(const AttnParams& p, int B, int max_q, hipStream_t str
     grid = dim3((unsigned)(per * 8), 1, 1);
   }
   if (grid.x == 0) return 0;
+  const bool big = p.prefill_qb == 2;
   if (gw == 8) {
-    if (TQ == 32) attn_prefill32_kernel<32, 8><<<grid, 64 * nw, 0, stream>>>(p);
+    if (big) attn_prefill32_kernel<32, 8><<<grid, 64 * nw, 0, stream>>>(p);
     else attn_prefill32_kernel<16, 8><<<grid, 64 * nw, 0, stream>>>(p);
-  } else {
-    if (TQ == 32) attn_prefill32_kernel<32, 4><<<grid, 64 * nw, 0, stream>>>(p);
+  } else if (gw == 4) {
+    if (big) attn_prefill32_kernel<32, 4><<<grid, 64 * nw, 0, stream>>>(p);
     else attn_prefill32_kernel<16, 4><<<grid, 64 * nw, 0, stream>>>(p);
+  } else if (gw == 2) {
+    if (big) attn_prefill32_kernel<64, 2><<<grid, 64 * nw, 0, stream>>>(p);
+    else attn_prefill32_kernel<32, 2><<<grid, 64 * nw, 0, stream>>>(p);
+  } else {
+    if (big) attn_prefill32_kernel<128, 1><<<grid, 64 * nw, 0, stream>>>(p);
+    else attn_prefill32_kernel<64, 1><<<grid, 64 * nw, 0, stream>>>(p);
   }
   return 0;
 }

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_llm_inference import ops  # noqa: E402
 
 dev = torch.device("cuda:0")
-nh, nkv, D, bs = 64, 8, 128, 64
+nh, nkv, D, bs = int(os.environ.get("NH", 64)), int(os.environ.get("NKV", 8)), 128, 64
 CASES = [(32, 512, 0), (4, 4096, 0), (1, 2048, 6144), (256, 16, 512)]
 if os.environ.get("CASES"):   # e.g. CASES="4x4096x0,1x32768x0"
     CASES = [tuple(int(x) for x in c.split("x")) for c in os.environ["CASES"].split(",")]
@@ -49,7 +49,7 @@ def run(B, q, ctx):
     us = (time.perf_counter() - t0) / n * 1e6
     pairs = B * sum(ctx + i + 1 for i in range(q))
     tf = 4 * D * nh * pairs / us / 1e6
-    return dict(B=B, q=q, ctx=ctx, qb=QB or ops.prefill_qb_for(q), m32=int(ops.policy().prefill_m32), us=round(us, 1),
+    return dict(nh=nh, nkv=nkv, B=B, q=q, ctx=ctx, qb=QB or ops.prefill_qb_for(q), m32=int(ops.policy().prefill_m32), us=round(us, 1),
                 TFLOPs=round(tf, 1))
 
 

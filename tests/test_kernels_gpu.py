@@ -692,15 +692,17 @@ def test_attn_prefill_long_chunks(gpu, qb):
     _close(out, out_r, 2e-2, 2e-2, f"prefill-long-qb{qb}")
 
 
-@pytest.mark.parametrize("nh,nkv", [(64, 8), (32, 8), (64, 4)])
+@pytest.mark.parametrize("nh,nkv", [(64, 8), (32, 8), (64, 4), (16, 8), (16, 16), (28, 4)])
 @pytest.mark.parametrize("qb", ["1", "2"])
 @pytest.mark.parametrize("ramp", [False, True])
 def test_attn_prefill_m32(gpu, nh, nkv, qb, ramp):
     """attn_prefill32.hip (32x32x16 MFMA, 64-key steps, deferred softmax max) against the fp32
     oracle and against attention.hip's kernel: GQA groups of 8 / 4 / 16 (two workgroups per kv
-    head), 16- and 32-token tiles, chunks on top of cached context, a chunk ending mid-step, decode
-    rows in the batch.  ``ramp``: keys scaled up along the sequence, so the running max keeps
-    growing by more than the deferral threshold (every rescale branch fires, cdna T13 hazard)."""
+    head), pairs (two heads x 32- or 64-token tiles), MHA and Qwen2's odd group of 7 (one head x
+    64- or 128-token tiles), 16- and 32-token tiles, chunks on top of cached context, a chunk
+    ending mid-step, decode rows in the batch.  ``ramp``: keys scaled up along the sequence, so
+    the running max keeps growing by more than the deferral threshold (every rescale branch
+    fires, cdna T13 hazard)."""
     qb = int(qb)
     torch.manual_seed(31)
     D, bs = 128, 64
