@@ -128,9 +128,13 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   // first - and its k-th workgroup walks items k, k + per, ... of them (per = span: one each).
   // Without a map (dense grid) a workgroup is one (sequence, tile, group).
   struct Item {
-    int b, t0, kvh, h0, qs0, qlen, L, pq_lo, pq_hi, nsteps;
+    int b, t0, kvh, h0, qs0, qlen, L, pq_lo, pq_hi, s_lo, nsteps;
     const int* bt;
   };
+  // sliding window (Mistral: a ring cache without sink tokens): a key a is visible to the column
+  // at position q iff q - win < a <= q, and lives in ring slot a % ring (ring >= win + the
+  // longest chunk - 1, so every key a chunk's queries see is still there); 0: full cache
+  const int win = p.ring > 0 ? p.window : 0;
   // Persistent walk: round n takes item n per + k on even rounds and n per + (per - 1 - k) on odd
   // ones (a snake): the map lists each sequence's tiles heaviest first, so a plain stride that
   // is a multiple of the tiles per sequence would hand one workgroup every sequence's heaviest
@@ -167,10 +171,11 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     it.L = p.seq_lens[b];
     it.pq_lo = it.L - it.qlen + it.t0;                                  // first position
     it.pq_hi = it.L - it.qlen + min(it.qlen - 1, it.t0 + TQ - 1);      // ... and last
+    it.s_lo = win ? max(0, it.pq_lo - win + 1) >> 6 : 0;               // first key step
 #if P32_KO_LOOP
     it.nsteps = 1;
 #else
-    it.nsteps = (it.pq_hi + 64) >> 6;                                   // keys [0, pq_hi]
+    it.nsteps = (it.pq_hi >> 6) - it.s_lo + 1;                          // ... through pq_hi
 #endif
     it.bt = p.block_tables + (size_t)b * p.bt_stride;
     return it.t0 < it.qlen;
@@ -230,10 +235,15 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   // lgkmcnt(0).  Block size a power of two: shifts, not divisions; both halves' pages by one pair
   // of scalar loads waited once per step.
   auto dma_step = [&](const Item& it, int s, int bi) {
-    const int u0 = s * 64;
+    const int u0 = (it.s_lo + s) * 64;      // absolute position of the step's first key
     const bool need1 = u0 + 32 <= it.pq_hi;
-    const int i0 = u0 >> bs_lg;
-    const int i1 = need1 ? (u0 + 32) >> bs_lg : i0;
+    int sl0 = u0, sl1 = u0 + 32;            // cache slots of the two halves
+    if (win) {
+      sl0 = u0 % p.ring;
+      sl1 = (u0 + 32) % p.ring;
+    }
+    const int i0 = sl0 >> bs_lg;
+    const int i1 = need1 ? sl1 >> bs_lg : i0;
     const int* a0 = it.bt + __builtin_amdgcn_readfirstlane(i0);
     const int* a1 = it.bt + __builtin_amdgcn_readfirstlane(i1);
     int pg0, pg1;
@@ -243,8 +253,8 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
 #endif
     asm volatile("s_load_dword %0, %2, 0x0\n\ts_load_dword %1, %3, 0x0\n\ts_waitcnt lgkmcnt(0)"
                  : "=&s"(pg0), "=&s"(pg1) : "s"(a0), "s"(a1));
-    const int so0 = (u0 & (p.bs - 1)) * D;          // the halves' element offsets in their pages
-    const int so1 = ((u0 + 32) & (p.bs - 1)) * D;
+    const int so0 = (sl0 & (p.bs - 1)) * D;         // the halves' element offsets in their pages
+    const int so1 = (sl1 & (p.bs - 1)) * D;
     bf16* kd = kbuf(bi);
     bf16* vd = vbuf(bi);
 #pragma unroll
@@ -283,8 +293,12 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     for (int db = 0; db < D / 32; ++db) o[db] = f32x16{};
     float l_run = 0.f;
     float m_run = -1e30f;
-    auto full2 = [&](int s) { return s * 64 + 32 <= pq_hi; };   // second half holds a visible key
-    auto diag = [&](int s) { return s * 64 + 63 > pq_lo; };     // some key past some column
+    const int kb0 = cur.s_lo * 64;          // absolute position of step 0's first key
+    auto full2 = [&](int s) { return kb0 + s * 64 + 32 <= pq_hi; };   // 2nd half has a visible key
+    auto diag = [&](int s) { return kb0 + s * 64 + 63 > pq_lo; };     // some key past some column
+    auto low = [&](int s) {                 // some key before some column's window
+      return win && kb0 + s * 64 < pq_hi - win + 1;
+    };
     // S^T(s) from K(s): the first half's 8 fragment reads all issued before the first MFMA, then
     // one second-half read per MFMA (the scheduler otherwise sinks each read to just before its
     // MFMA, and every MFMA waits out a whole LDS latency); the second half's MFMAs only where it
@@ -316,14 +330,15 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     // deferred max (T13: the running max moves only when some column grew by more than THR),
     // P = exp2(S sl2 - m) packed to bf16; l is rescaled here, O by the PV that consumes P
     auto softmax = [&](int s, f32x16& sa, f32x16& sb, bf16x8 (&pp)[4], float& alpha, bool& resc) {
-      if (diag(s)) {
-        const int kb = s * 64;
+      if (diag(s) || low(s)) {
+        const int kb = kb0 + s * 64;
+        const int lo = win ? pq - win : -1;   // keys <= lo are before this column's window
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = kb + 16 * (r >> 3) + 8 * hh + (r & 7);
-          sa[r] = key > pq ? -INFINITY : sa[r];
-          sb[r] = key + 32 > pq ? -INFINITY : sb[r];   // (an unread half: every key masked)
-        }
+          sa[r] = (key > pq || key <= lo) ? -INFINITY : sa[r];
+          sb[r] = (key + 32 > pq || key + 32 <= lo) ? -INFINITY : sb[r];   // (an unread half:
+        }                                                                  //  every key masked)
       }
       // IEEE maximum (NaN-propagating) lowers to v_maximum3_f32, one per two scores; fmaxf's
       // maxnum would first canonicalise every MFMA output with a v_max_f32 x, x of its own
@@ -495,14 +510,16 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   }
 }
 
-// Eligible: head_dim 128, bf16 full cache, no custom mask, power-of-two block size; any GQA
+// Eligible: head_dim 128, bf16 full cache or a sliding-window ring without sink tokens (sinks
+// score with a second query rotation: attention.hip), no custom mask, power-of-two block size; any GQA
 // group (a workgroup takes GW = 8, 4, 2 or 1 of its heads, the largest that divides it) - but a
 // group that is not a multiple of 4 only with the long-chunk tiles (prefill_qb 2): its short
 // tiles make 2-wave workgroups, and attention.hip's kernel is faster there (512-token prompts,
 // MHA 355 vs 309 TF; long chunks 571-620 vs 780-920: profiles/r6/gqa/).
 bool attn_prefill32_eligible(const AttnParams& p, int D) {
   const int G = p.nh / p.nkv;
-  return p.prefill_m32 && D == P32_D && !p.kv_fp8 && p.ring == 0 && p.mask == nullptr &&
+  return p.prefill_m32 && D == P32_D && !p.kv_fp8 && p.mask == nullptr &&
+         (p.ring == 0 || (p.n_sink == 0 && p.sink_pad == 0 && p.window > 0 && p.ring % 32 == 0)) &&
          p.bs % 32 == 0 && (p.bs & (p.bs - 1)) == 0 && (G % 4 == 0 || p.prefill_qb == 2);
 }
 

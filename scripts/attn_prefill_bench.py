@@ -19,11 +19,13 @@ CASES = [(32, 512, 0), (4, 4096, 0), (1, 2048, 6144), (256, 16, 512)]
 if os.environ.get("CASES"):   # e.g. CASES="4x4096x0,1x32768x0"
     CASES = [tuple(int(x) for x in c.split("x")) for c in os.environ["CASES"].split(",")]
 QB = int(os.environ["QB"]) if os.environ.get("QB") else None   # None: ops.prefill_qb_for
+WINDOW = int(os.environ.get("WINDOW", "0"))   # > 0: a sliding-window ring (Mistral), no sinks
 
 
 def run(B, q, ctx):
     L = q + ctx
-    nbps = (L + bs - 1) // bs
+    ring = ((WINDOW + q - 1 + 31) // 32) * 32 if WINDOW else 0
+    nbps = ((ring if WINDOW else L) + bs - 1) // bs
     nblk = B * nbps
     kc = torch.randn(nblk, nkv, bs, D, device=dev, dtype=torch.bfloat16)
     vc = torch.randn(nblk, nkv, bs // 8, D, 8, device=dev, dtype=torch.bfloat16)
@@ -36,7 +38,8 @@ def run(B, q, ctx):
     tm = ops.prefill_tiles([q] * B, nh, nkv, qb=QB).to(dev) if os.environ.get("DENSE") != "1" else None
 
     def call():
-        ops.attn_prefill(Q, None, kc, vc, bt, lens, q_start, q, D ** -0.5, tile_map=tm, qb=QB)
+        ops.attn_prefill(Q, None, kc, vc, bt, lens, q_start, q, D ** -0.5, 0, 0, ring, WINDOW,
+                         tile_map=tm, qb=QB)
 
     for _ in range(3):
         call()
@@ -47,9 +50,9 @@ def run(B, q, ctx):
         call()
     torch.cuda.synchronize()
     us = (time.perf_counter() - t0) / n * 1e6
-    pairs = B * sum(ctx + i + 1 for i in range(q))
+    pairs = B * sum(min(ctx + i + 1, WINDOW) if WINDOW else ctx + i + 1 for i in range(q))
     tf = 4 * D * nh * pairs / us / 1e6
-    return dict(nh=nh, nkv=nkv, B=B, q=q, ctx=ctx, qb=QB or ops.prefill_qb_for(q), m32=int(ops.policy().prefill_m32), us=round(us, 1),
+    return dict(nh=nh, nkv=nkv, window=WINDOW, B=B, q=q, ctx=ctx, qb=QB or ops.prefill_qb_for(q), m32=int(ops.policy().prefill_m32), us=round(us, 1),
                 TFLOPs=round(tf, 1))
 
 
