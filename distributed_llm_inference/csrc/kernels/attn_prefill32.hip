@@ -100,7 +100,7 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& s, int base) {
 
 }  // namespace
 
-template <int TQ, int GW>
+template <int TQ, int GW, bool F8>
 __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   constexpr int D = P32_D;
   constexpr int CH = D / 8;                 // 16-B chunks per K row
@@ -234,6 +234,32 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   // form as an out-of-order LDS (lgkm) access, which turns every LDS-read wait after it into
   // lgkmcnt(0).  Block size a power of two: shifts, not divisions; both halves' pages by one pair
   // of scalar loads waited once per step.
+  // fp8 e4m3 caches: no LDS-DMA - each lane loads 16-byte runs of fp8 (two bf16 units' worth)
+  // into registers when the DMA would be issued, and widens them into the same bf16 LDS images
+  // just before the step barrier (f8_commit), so the MFMA loop is the bf16 one; K's scale folds
+  // into the softmax scale, V's into the output normalisation
+  constexpr int NPU = 8 / NW;               // 16-B fp8 runs per image per lane and step
+  uint4 rk[F8 ? NPU : 1], rv[F8 ? NPU : 1];
+  int f8_bi = 0;
+  bool f8_need1 = false;
+  auto f8_commit = [&]() {
+    bf16* kd = kbuf(f8_bi);
+    bf16* vd = vbuf(f8_bi);
+#pragma unroll
+    for (int i = 0; i < NPU; ++i) {
+      const int pu = (i * NW + w) * 64 + lane;
+      if (((i * NW + w) >> 2) && !f8_need1) continue;   // (the K and the V^T run: same half)
+      const int row = pu >> 3, kk = pu & 7;
+      bf16* krow = kd + row * CH * 8;
+      *reinterpret_cast<bf16x8*>(krow + ((2 * kk) ^ (row & 15)) * 8) =
+          fp8x8_to_bf16x8(make_uint2(rk[i].x, rk[i].y));
+      *reinterpret_cast<bf16x8*>(krow + ((2 * kk + 1) ^ (row & 15)) * 8) =
+          fp8x8_to_bf16x8(make_uint2(rk[i].z, rk[i].w));
+      *reinterpret_cast<bf16x8*>(vd + (2 * pu) * 8) = fp8x8_to_bf16x8(make_uint2(rv[i].x, rv[i].y));
+      *reinterpret_cast<bf16x8*>(vd + (2 * pu + 1) * 8) =
+          fp8x8_to_bf16x8(make_uint2(rv[i].z, rv[i].w));
+    }
+  };
   auto dma_step = [&](const Item& it, int s, int bi) {
     const int u0 = (it.s_lo + s) * 64;      // absolute position of the step's first key
     const bool need1 = u0 + 32 <= it.pq_hi;
@@ -255,6 +281,26 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
                  : "=&s"(pg0), "=&s"(pg1) : "s"(a0), "s"(a1));
     const int so0 = (sl0 & (p.bs - 1)) * D;         // the halves' element offsets in their pages
     const int so1 = (sl1 & (p.bs - 1)) * D;
+    if constexpr (F8) {
+      f8_bi = bi;
+      f8_need1 = need1;
+      const size_t kvb = (size_t)it.kvh * head_stride;
+      const uint8_t* kh0 = static_cast<const uint8_t*>(p.k_cache) + kvb + (size_t)(uint32_t)pg0 * page_elems + so0;
+      const uint8_t* kh1 = static_cast<const uint8_t*>(p.k_cache) + kvb + (size_t)(uint32_t)pg1 * page_elems + so1;
+      const uint8_t* vh0 = static_cast<const uint8_t*>(p.v_cache) + kvb + (size_t)(uint32_t)pg0 * page_elems + so0;
+      const uint8_t* vh1 = static_cast<const uint8_t*>(p.v_cache) + kvb + (size_t)(uint32_t)pg1 * page_elems + so1;
+#pragma unroll
+      for (int i = 0; i < NPU; ++i) {
+        const int pu = (i * NW + w) * 64 + lane;
+        const int half = (i * NW + w) >> 2;           // wave-uniform
+        if (half && !need1) continue;
+        const int row = pu >> 3, kk = pu & 7;         // K: LDS row, 16-d run; key pi(row)
+        rk[i] = *reinterpret_cast<const uint4*>((half ? kh1 : kh0) + swap23(row & 31) * D + 16 * kk);
+        const int u2 = (2 * pu) & 511;                // V^T: units (g, d), (g, d+1) of the half
+        rv[i] = *reinterpret_cast<const uint4*>((half ? vh1 : vh0) + u2 * 8);
+      }
+      return;
+    }
     bf16* kd = kbuf(bi);
     bf16* vd = vbuf(bi);
 #pragma unroll
@@ -272,12 +318,13 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   const int koff = c * CH * 8;
   const int kx = c & 15;
   const int voff = (hh * D + c) * 8;
-  const float sl2 = p.scale_log2;
+  const float sl2 = F8 ? p.scale_log2 * p.k_scale : p.scale_log2;
 
   bf16x8 qf[D / 16];
   load_q(cur, qf);
   int g0 = 0;                               // global step count: buffer of (tile, step s) = g0 + s
   dma_step(cur, 0, bufi(0));
+  if constexpr (F8) f8_commit();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -420,6 +467,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
         dma_next(s);
         softmax(s, sa, sb, pp, alpha, resc);
         pv(s, pp, alpha, resc);
+        if (F8 && s + 1 < nsteps) f8_commit();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA (and Q) landed
         __syncthreads();
       }
@@ -436,6 +484,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
         }
         dma_next(s);
         scores(s, sa, sb);
+        if (F8 && s + 1 < nsteps) f8_commit();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
       }
@@ -453,7 +502,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     // prefetch in flight); then each wave-instruction stores 4 whole rows of one token (adjacent
     // heads: 1 KB contiguous in [token][head][d]).
     const float lsum = l_run + __shfl_xor(l_run, 32, 64);
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    const float inv = lsum > 0.f ? (F8 ? p.v_scale : 1.f) / lsum : 0.f;
     if (STAG) __syncthreads();                  // every wave is past its last V^T read
     // persistent: the next tile's Q (into qf, dead now) and its first K / V^T step (into the
     // buffer after this tile's last one) are in flight while this tile's output is staged and
@@ -501,6 +550,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     if (!more) break;
     // the next tile's first step (and Q) landed; the staging buffer is its step-1 buffer: every
     // wave's reads of it first
+    if constexpr (F8) f8_commit();   // (its buffer is not the staging one)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     g0 += nsteps;
@@ -518,7 +568,11 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
 // MHA 355 vs 309 TF; long chunks 571-620 vs 780-920: profiles/r6/gqa/).
 bool attn_prefill32_eligible(const AttnParams& p, int D) {
   const int G = p.nh / p.nkv;
-  return p.prefill_m32 && D == P32_D && !p.kv_fp8 && p.mask == nullptr &&
+  // fp8 caches widen through registers: 4- and 8-wave workgroups only (a 2-wave one would hold
+  // 32 registers of fp8 runs per lane and spill) - all long-chunk tiles, and 16-token tiles of
+  // groups of 8
+  if (p.kv_fp8 && !(p.prefill_qb == 2 || G % 8 == 0)) return false;
+  return p.prefill_m32 && D == P32_D && p.mask == nullptr &&
          (p.ring == 0 || (p.n_sink == 0 && p.sink_pad == 0 && p.window > 0 && p.ring % 32 == 0)) &&
          p.bs % 32 == 0 && (p.bs & (p.bs - 1)) == 0 && (G % 4 == 0 || p.prefill_qb == 2);
 }
@@ -550,18 +604,29 @@ int launch_attn_prefill32(const AttnParams& p, int B, int max_q, hipStream_t str
   }
   if (grid.x == 0) return 0;
   const bool big = p.prefill_qb == 2;
-  if (gw == 8) {
-    if (big) attn_prefill32_kernel<32, 8><<<grid, 64 * nw, 0, stream>>>(p);
-    else attn_prefill32_kernel<16, 8><<<grid, 64 * nw, 0, stream>>>(p);
+  if (p.kv_fp8) {   // fp8 caches: 4- and 8-wave workgroups only (eligibility)
+    if (gw == 8) {
+      if (big) attn_prefill32_kernel<32, 8, true><<<grid, 64 * nw, 0, stream>>>(p);
+      else attn_prefill32_kernel<16, 8, true><<<grid, 64 * nw, 0, stream>>>(p);
+    } else if (gw == 4) {
+      attn_prefill32_kernel<32, 4, true><<<grid, 64 * nw, 0, stream>>>(p);
+    } else if (gw == 2) {
+      attn_prefill32_kernel<64, 2, true><<<grid, 64 * nw, 0, stream>>>(p);
+    } else {
+      attn_prefill32_kernel<128, 1, true><<<grid, 64 * nw, 0, stream>>>(p);
+    }
+  } else if (gw == 8) {
+    if (big) attn_prefill32_kernel<32, 8, false><<<grid, 64 * nw, 0, stream>>>(p);
+    else attn_prefill32_kernel<16, 8, false><<<grid, 64 * nw, 0, stream>>>(p);
   } else if (gw == 4) {
-    if (big) attn_prefill32_kernel<32, 4><<<grid, 64 * nw, 0, stream>>>(p);
-    else attn_prefill32_kernel<16, 4><<<grid, 64 * nw, 0, stream>>>(p);
+    if (big) attn_prefill32_kernel<32, 4, false><<<grid, 64 * nw, 0, stream>>>(p);
+    else attn_prefill32_kernel<16, 4, false><<<grid, 64 * nw, 0, stream>>>(p);
   } else if (gw == 2) {
-    if (big) attn_prefill32_kernel<64, 2><<<grid, 64 * nw, 0, stream>>>(p);
-    else attn_prefill32_kernel<32, 2><<<grid, 64 * nw, 0, stream>>>(p);
+    if (big) attn_prefill32_kernel<64, 2, false><<<grid, 64 * nw, 0, stream>>>(p);
+    else attn_prefill32_kernel<32, 2, false><<<grid, 64 * nw, 0, stream>>>(p);
   } else {
-    if (big) attn_prefill32_kernel<128, 1><<<grid, 64 * nw, 0, stream>>>(p);
-    else attn_prefill32_kernel<64, 1><<<grid, 64 * nw, 0, stream>>>(p);
+    if (big) attn_prefill32_kernel<128, 1, false><<<grid, 64 * nw, 0, stream>>>(p);
+    else attn_prefill32_kernel<64, 1, false><<<grid, 64 * nw, 0, stream>>>(p);
   }
   return 0;
 }

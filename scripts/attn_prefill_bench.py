@@ -20,6 +20,7 @@ if os.environ.get("CASES"):   # e.g. CASES="4x4096x0,1x32768x0"
     CASES = [tuple(int(x) for x in c.split("x")) for c in os.environ["CASES"].split(",")]
 QB = int(os.environ["QB"]) if os.environ.get("QB") else None   # None: ops.prefill_qb_for
 WINDOW = int(os.environ.get("WINDOW", "0"))   # > 0: a sliding-window ring (Mistral), no sinks
+KV_FP8 = os.environ.get("KV_FP8", "0") == "1"   # fp8 e4m3 caches (scale 1)
 
 
 def run(B, q, ctx):
@@ -29,6 +30,8 @@ def run(B, q, ctx):
     nblk = B * nbps
     kc = torch.randn(nblk, nkv, bs, D, device=dev, dtype=torch.bfloat16)
     vc = torch.randn(nblk, nkv, bs // 8, D, 8, device=dev, dtype=torch.bfloat16)
+    if KV_FP8:
+        kc, vc = kc.to(torch.float8_e4m3fn), vc.to(torch.float8_e4m3fn)
     bt = torch.arange(nblk, device=dev, dtype=torch.int32).view(B, nbps)
     lens = torch.full((B,), L, dtype=torch.int32, device=dev)
     q_start = torch.arange(0, (B + 1) * q, q, dtype=torch.int32, device=dev)
@@ -52,7 +55,7 @@ def run(B, q, ctx):
     us = (time.perf_counter() - t0) / n * 1e6
     pairs = B * sum(min(ctx + i + 1, WINDOW) if WINDOW else ctx + i + 1 for i in range(q))
     tf = 4 * D * nh * pairs / us / 1e6
-    return dict(nh=nh, nkv=nkv, window=WINDOW, B=B, q=q, ctx=ctx, qb=QB or ops.prefill_qb_for(q), m32=int(ops.policy().prefill_m32), us=round(us, 1),
+    return dict(nh=nh, nkv=nkv, window=WINDOW, kv_fp8=int(KV_FP8), B=B, q=q, ctx=ctx, qb=QB or ops.prefill_qb_for(q), m32=int(ops.policy().prefill_m32), us=round(us, 1),
                 TFLOPs=round(tf, 1))
 
 

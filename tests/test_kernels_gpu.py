@@ -437,6 +437,38 @@ def test_attn_prefill_m32_sliding_window(gpu, qb, nh, nkv):
     _close(out, out_l, 2e-2, 2e-2, "prefill-m32-window-vs-legacy")
 
 
+@pytest.mark.parametrize("qb", ["1", "2"])
+@pytest.mark.parametrize("nh,nkv,window", [(64, 8, 0), (32, 8, 0), (16, 16, 0), (64, 8, 200)])
+def test_attn_prefill_m32_fp8_kv(gpu, qb, nh, nkv, window):
+    """attn_prefill32.hip on fp8 e4m3 caches (runs widened to bf16 on their way into LDS, K's
+    scale in the softmax scale, V's in the normalisation) against the fp32 oracle and
+    attention.hip's fp8 kernel: 8-wave and 4-wave workgroups (groups of 8 at both tile sizes, 4
+    and MHA at the long-chunk tiles; the others fall back), full cache and a sliding window."""
+    qb = int(qb)
+    torch.manual_seed(23)
+    D, bs, ks, vs = 128, 64, 2.0, 0.5
+    q_lens = [300, 1, 64, 130, 17]
+    ctx = [0, 899, 36, 400, 10]
+    lens = torch.tensor([a + b for a, b in zip(q_lens, ctx)], dtype=torch.int32)
+    ring = ((window + max(q_lens) - 1 + 31) // 32) * 32 if window else 0
+    B = len(q_lens)
+    q_start = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
+    max_blocks = ((ring or int(lens.max())) + bs - 1) // bs
+    kc, vc = _make_cache_fp8(B * max_blocks, nkv, bs, D, gpu, ks, vs)
+    bt = _tables(B, max_blocks, B * max_blocks, gpu, seed=6)
+    q = torch.randn(int(q_start[-1]), nh, D, device=gpu, dtype=BF)
+    scale = 1 / math.sqrt(D)
+    tm = ops.prefill_tiles(q_lens, nh, nkv, qb=qb).to(gpu)
+    args = (kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens), scale, 0, 0, ring, window)
+    out = ops.attn_prefill(q, None, *args, tile_map=tm, qb=qb, k_scale=ks, v_scale=vs)
+    out_r = ref.attn_prefill(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale,
+                             0, 0, ring, window, k_scale=ks, v_scale=vs)
+    _close(out, out_r, 2e-2, 2e-2, f"prefill-m32-fp8-{nh}/{nkv}-w{window}-qb{qb}")
+    with ops.kernel_policy(prefill_m32=False):
+        out_l = ops.attn_prefill(q, None, *args, tile_map=tm, qb=qb, k_scale=ks, v_scale=vs)
+    _close(out, out_l, 2e-2, 2e-2, "prefill-m32-fp8-vs-legacy")
+
+
 def test_sample_greedy_and_topk1(gpu):
     torch.manual_seed(6)
     B, V = 9, 128256
