@@ -2,7 +2,8 @@
 //
 // Replaces the reference's eager prefill attention (modules.py:87-97: repeat_kv, QK^T/sqrt(D) +
 // additive causal mask, fp32 softmax, PV) for the common case - full (non-windowed) bf16 cache,
-// head_dim 128, no custom mask, any GQA group incl. MHA; attention.hip keeps the general kernel.
+// head_dim 128, no custom mask, any GQA group incl. MHA, full caches and windowed rings (sliding
+// windows and StreamingLLM sinks), bf16 or fp8 KV; attention.hip keeps the general kernel.
 //
 // Why a second kernel: attention.hip's prefill wave holds 16 query rows on the 16x16x32 MFMA, so
 // every K / V^T fragment read from LDS (one ds_read_b128) feeds ONE 16-cycle MFMA: four SIMDs ask
@@ -128,13 +129,19 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   // first - and its k-th workgroup walks items k, k + per, ... of them (per = span: one each).
   // Without a map (dense grid) a workgroup is one (sequence, tile, group).
   struct Item {
-    int b, t0, kvh, h0, qs0, qlen, L, pq_lo, pq_hi, s_lo, nsteps;
+    int b, t0, kvh, h0, qs0, qlen, L, pq_lo, pq_hi, ns, s_lo, nsteps;
     const int* bt;
   };
-  // sliding window (Mistral: a ring cache without sink tokens): a key a is visible to the column
-  // at position q iff q - win < a <= q, and lives in ring slot a % ring (ring >= win + the
-  // longest chunk - 1, so every key a chunk's queries see is still there); 0: full cache
+  // Windowed ring caches (p.ring > 0): nsk sink tokens in slots [0, nsk) (StreamingLLM; none for
+  // Mistral's sliding window) and the rolling keys a >= nsk in slot sink_pad + (a - nsk) % ring
+  // (ring >= window - nsk + the longest chunk - 1, so every key a chunk's queries see is still
+  // there).  A rolling key is visible to the column at position q iff q - wmain < a <= q; the
+  // sinks (a < min(nsk, L)) are visible to every column at or past them and score against the
+  // query rotated for them (q_sink): one extra step, first.  Main steps are aligned in the
+  // ring's offset a - nsk, so each 32-key half is one run of slots.  win = 0: full cache.
   const int win = p.ring > 0 ? p.window : 0;
+  const int nsk = p.ring > 0 ? p.n_sink : 0;
+  const int wmain = win - nsk;
   // Persistent walk: round n takes item n per + k on even rounds and n per + (per - 1 - k) on odd
   // ones (a snake): the map lists each sequence's tiles heaviest first, so a plain stride that
   // is a multiple of the tiles per sequence would hand one workgroup every sequence's heaviest
@@ -171,11 +178,13 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     it.L = p.seq_lens[b];
     it.pq_lo = it.L - it.qlen + it.t0;                                  // first position
     it.pq_hi = it.L - it.qlen + min(it.qlen - 1, it.t0 + TQ - 1);      // ... and last
-    it.s_lo = win ? max(0, it.pq_lo - win + 1) >> 6 : 0;               // first key step
+    it.ns = nsk > 0 ? 1 : 0;                                            // the sink step
+    it.s_lo = win ? max(0, it.pq_lo - wmain + 1 - nsk) >> 6 : 0;       // first main step (offset)
+    const int o_hi = it.pq_hi - nsk;                                    // ... through pq_hi
 #if P32_KO_LOOP
     it.nsteps = 1;
 #else
-    it.nsteps = (it.pq_hi >> 6) - it.s_lo + 1;                          // ... through pq_hi
+    it.nsteps = it.ns + (o_hi >= 0 ? (o_hi >> 6) - it.s_lo + 1 : 0);
 #endif
     it.bt = p.block_tables + (size_t)b * p.bt_stride;
     return it.t0 < it.qlen;
@@ -186,11 +195,11 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
 
   // ---- Q^T operand: lane (c, hh) holds d = 16 m + 8 hh + [0, 8) of its column, m = 0..7 ----
   // (rows past the chunk load the chunk's first token - always present - and are zeroed)
-  auto load_q = [&](const Item& it, bf16x8 (&q)[D / 16]) {
+  auto load_q = [&](const Item& it, bf16x8 (&q)[D / 16], const bf16* src) {
     const int tok = it.t0 + R % TQ;
     const bool valid = tok < it.qlen;
     const bf16* qrow =
-        p.q + ((size_t)(it.qs0 + (valid ? tok : 0)) * p.nh + it.h0 + R / TQ) * D + 8 * hh;
+        src + ((size_t)(it.qs0 + (valid ? tok : 0)) * p.nh + it.h0 + R / TQ) * D + 8 * hh;
 #pragma unroll
     for (int m = 0; m < D / 16; ++m) {
 #if P32_KO_Q
@@ -261,12 +270,14 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     }
   };
   auto dma_step = [&](const Item& it, int s, int bi) {
-    const int u0 = (it.s_lo + s) * 64;      // absolute position of the step's first key
-    const bool need1 = u0 + 32 <= it.pq_hi;
-    int sl0 = u0, sl1 = u0 + 32;            // cache slots of the two halves
-    if (win) {
-      sl0 = u0 % p.ring;
-      sl1 = (u0 + 32) % p.ring;
+    const bool sink = s < it.ns;
+    const int o0 = (it.s_lo + s - it.ns) * 64;   // main step: ring offset of its first key
+    const int u0 = sink ? 0 : nsk + o0;          // absolute position of the step's first key
+    const bool need1 = sink ? min(nsk, it.L) > 32 && it.pq_hi >= 32 : u0 + 32 <= it.pq_hi;
+    int sl0 = u0, sl1 = u0 + 32;                 // cache slots of the two halves
+    if (win && !sink) {
+      sl0 = p.sink_pad + o0 % p.ring;
+      sl1 = p.sink_pad + (o0 + 32) % p.ring;
     }
     const int i0 = sl0 >> bs_lg;
     const int i1 = need1 ? sl1 >> bs_lg : i0;
@@ -321,7 +332,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   const float sl2 = F8 ? p.scale_log2 * p.k_scale : p.scale_log2;
 
   bf16x8 qf[D / 16];
-  load_q(cur, qf);
+  load_q(cur, qf, cur.ns ? p.q_sink : p.q);   // (the sink step scores against q_sink)
   int g0 = 0;                               // global step count: buffer of (tile, step s) = g0 + s
   dma_step(cur, 0, bufi(0));
   if constexpr (F8) f8_commit();
@@ -340,11 +351,16 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     for (int db = 0; db < D / 32; ++db) o[db] = f32x16{};
     float l_run = 0.f;
     float m_run = -1e30f;
-    const int kb0 = cur.s_lo * 64;          // absolute position of step 0's first key
-    auto full2 = [&](int s) { return kb0 + s * 64 + 32 <= pq_hi; };   // 2nd half has a visible key
-    auto diag = [&](int s) { return kb0 + s * 64 + 63 > pq_lo; };     // some key past some column
-    auto low = [&](int s) {                 // some key before some column's window
-      return win && kb0 + s * 64 < pq_hi - win + 1;
+    const int ns = cur.ns;
+    const int nS = min(nsk, cur.L);         // sink keys present
+    const int kb0 = nsk + (cur.s_lo - ns) * 64;   // absolute position of step s's first key:
+    auto akey = [&](int s) { return s < ns ? 0 : kb0 + s * 64; };   //  kb0 + 64 s (main steps)
+    auto full2 = [&](int s) {               // the second half holds a visible key
+      return s < ns ? nS > 32 && pq_hi >= 32 : akey(s) + 32 <= pq_hi;
+    };
+    auto diag = [&](int s) { return s < ns || akey(s) + 63 > pq_lo; };   // some key masked:
+    auto low = [&](int s) {                 //  past some column, or before some column's window
+      return win && akey(s) < pq_hi - wmain + 1;
     };
     // S^T(s) from K(s): the first half's 8 fragment reads all issued before the first MFMA, then
     // one second-half read per MFMA (the scheduler otherwise sinks each read to just before its
@@ -378,13 +394,15 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     // P = exp2(S sl2 - m) packed to bf16; l is rescaled here, O by the PV that consumes P
     auto softmax = [&](int s, f32x16& sa, f32x16& sb, bf16x8 (&pp)[4], float& alpha, bool& resc) {
       if (diag(s) || low(s)) {
-        const int kb = kb0 + s * 64;
-        const int lo = win ? pq - win : -1;   // keys <= lo are before this column's window
+        const int kb = akey(s);
+        // keys <= lo: before this column's window; sink step: keys >= nS are not sinks
+        const int lo = s < ns ? -1 : (win ? pq - wmain : -1);
+        const int hi = s < ns ? min(pq, nS - 1) : pq;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int key = kb + 16 * (r >> 3) + 8 * hh + (r & 7);
-          sa[r] = (key > pq || key <= lo) ? -INFINITY : sa[r];
-          sb[r] = (key + 32 > pq || key + 32 <= lo) ? -INFINITY : sb[r];   // (an unread half:
+          sa[r] = (key > hi || key <= lo) ? -INFINITY : sa[r];
+          sb[r] = (key + 32 > hi || key + 32 <= lo) ? -INFINITY : sb[r];   // (an unread half:
         }                                                                  //  every key masked)
       }
       // IEEE maximum (NaN-propagating) lowers to v_maximum3_f32, one per two scores; fmaxf's
@@ -464,6 +482,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
       // block-table lookups (scalar loads waited in place) overlap the matrix pipe
       for (int s = 0; s < nsteps; ++s) {
         scores(s, sa, sb);
+        if (s < ns) load_q(cur, qf, p.q);   // the main steps score against q
         dma_next(s);
         softmax(s, sa, sb, pp, alpha, resc);
         pv(s, pp, alpha, resc);
@@ -484,6 +503,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
         }
         dma_next(s);
         scores(s, sa, sb);
+        if (s < ns) load_q(cur, qf, p.q);
         if (F8 && s + 1 < nsteps) f8_commit();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -512,7 +532,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     const bool more = PF && wi_next < wi_end && decode(wi_next, nxt);
     if (more) {
       dma_step(nxt, 0, bufi(g0 + nsteps));
-      load_q(nxt, qf);
+      load_q(nxt, qf, nxt.ns ? p.q_sink : p.q);
     }
     bf16* stg = STAG ? &smem[0][0][0] : kbuf(bufi(g0 + nsteps - 1));
     {
@@ -560,8 +580,8 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   }
 }
 
-// Eligible: head_dim 128, bf16 full cache or a sliding-window ring without sink tokens (sinks
-// score with a second query rotation: attention.hip), no custom mask, power-of-two block size; any GQA
+// Eligible: head_dim 128, bf16 or fp8 caches, full or windowed (sinks up to 64 slots), no custom
+// mask, power-of-two block size; any GQA
 // group (a workgroup takes GW = 8, 4, 2 or 1 of its heads, the largest that divides it) - but a
 // group that is not a multiple of 4 only with the long-chunk tiles (prefill_qb 2): its short
 // tiles make 2-wave workgroups, and attention.hip's kernel is faster there (512-token prompts,
@@ -573,7 +593,8 @@ bool attn_prefill32_eligible(const AttnParams& p, int D) {
   // groups of 8
   if (p.kv_fp8 && !(p.prefill_qb == 2 || G % 8 == 0)) return false;
   return p.prefill_m32 && D == P32_D && p.mask == nullptr &&
-         (p.ring == 0 || (p.n_sink == 0 && p.sink_pad == 0 && p.window > 0 && p.ring % 32 == 0)) &&
+         (p.ring == 0 || (p.window > p.n_sink && p.ring % 32 == 0 && p.sink_pad % 32 == 0 &&
+                          p.sink_pad <= 64 && (p.n_sink == 0 || p.q_sink != nullptr))) &&
          p.bs % 32 == 0 && (p.bs & (p.bs - 1)) == 0 && (G % 4 == 0 || p.prefill_qb == 2);
 }
 

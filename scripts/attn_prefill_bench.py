@@ -21,12 +21,14 @@ if os.environ.get("CASES"):   # e.g. CASES="4x4096x0,1x32768x0"
 QB = int(os.environ["QB"]) if os.environ.get("QB") else None   # None: ops.prefill_qb_for
 WINDOW = int(os.environ.get("WINDOW", "0"))   # > 0: a sliding-window ring (Mistral), no sinks
 KV_FP8 = os.environ.get("KV_FP8", "0") == "1"   # fp8 e4m3 caches (scale 1)
+N_SINK = int(os.environ.get("N_SINK", "0"))      # StreamingLLM sink tokens (with WINDOW)
 
 
 def run(B, q, ctx):
     L = q + ctx
-    ring = ((WINDOW + q - 1 + 31) // 32) * 32 if WINDOW else 0
-    nbps = ((ring if WINDOW else L) + bs - 1) // bs
+    sink_pad = ((N_SINK + 31) // 32) * 32 if WINDOW else 0
+    ring = ((WINDOW - N_SINK + q - 1 + 31) // 32) * 32 if WINDOW else 0
+    nbps = ((sink_pad + ring if WINDOW else L) + bs - 1) // bs
     nblk = B * nbps
     kc = torch.randn(nblk, nkv, bs, D, device=dev, dtype=torch.bfloat16)
     vc = torch.randn(nblk, nkv, bs // 8, D, 8, device=dev, dtype=torch.bfloat16)
@@ -37,12 +39,13 @@ def run(B, q, ctx):
     q_start = torch.arange(0, (B + 1) * q, q, dtype=torch.int32, device=dev)
     Q = torch.randn(B * q, nh, D, device=dev, dtype=torch.bfloat16)
     out = torch.empty_like(Q)
+    QS = torch.randn_like(Q) if (WINDOW and N_SINK) else None
 
     tm = ops.prefill_tiles([q] * B, nh, nkv, qb=QB).to(dev) if os.environ.get("DENSE") != "1" else None
 
     def call():
-        ops.attn_prefill(Q, None, kc, vc, bt, lens, q_start, q, D ** -0.5, 0, 0, ring, WINDOW,
-                         tile_map=tm, qb=QB)
+        ops.attn_prefill(Q, QS, kc, vc, bt, lens, q_start, q, D ** -0.5,
+                         N_SINK if WINDOW else 0, sink_pad, ring, WINDOW, tile_map=tm, qb=QB)
 
     for _ in range(3):
         call()
@@ -55,7 +58,7 @@ def run(B, q, ctx):
     us = (time.perf_counter() - t0) / n * 1e6
     pairs = B * sum(min(ctx + i + 1, WINDOW) if WINDOW else ctx + i + 1 for i in range(q))
     tf = 4 * D * nh * pairs / us / 1e6
-    return dict(nh=nh, nkv=nkv, window=WINDOW, kv_fp8=int(KV_FP8), B=B, q=q, ctx=ctx, qb=QB or ops.prefill_qb_for(q), m32=int(ops.policy().prefill_m32), us=round(us, 1),
+    return dict(nh=nh, nkv=nkv, window=WINDOW, n_sink=N_SINK, kv_fp8=int(KV_FP8), B=B, q=q, ctx=ctx, qb=QB or ops.prefill_qb_for(q), m32=int(ops.policy().prefill_m32), us=round(us, 1),
                 TFLOPs=round(tf, 1))
 
 

@@ -408,32 +408,38 @@ def test_attn_prefill_window(gpu, qb):
 
 @pytest.mark.parametrize("qb", ["1", "2"])
 @pytest.mark.parametrize("nh,nkv", [(32, 8), (16, 16)])
-def test_attn_prefill_m32_sliding_window(gpu, qb, nh, nkv):
-    """attn_prefill32.hip on a Mistral-style sliding-window ring (no sink tokens): keys by
-    absolute position, slot a % ring, window mask q - W < a <= q, chunks on top of a wrapped ring,
-    against the fp32 oracle (ring semantics of cache.py / ring_abs) and attention.hip's kernel."""
+@pytest.mark.parametrize("n_sink", [0, 4, 40])
+def test_attn_prefill_m32_sliding_window(gpu, qb, nh, nkv, n_sink):
+    """attn_prefill32.hip on windowed ring caches: Mistral's sliding window (no sinks) and
+    StreamingLLM sink windows (4 sinks; 40, which spill into the step's second half): rolling keys
+    by ring offset, slot sink_pad + (a - n_sink) % ring, window mask q - (W - n_sink) < a <= q,
+    the sinks as one extra step scored against q_sink; chunks on top of a wrapped ring, against
+    the fp32 oracle (ring semantics of cache.py / ring_abs) and attention.hip's kernel."""
     qb = int(qb)
-    torch.manual_seed(17)
+    torch.manual_seed(17 + n_sink)
     D, bs, window = 128, 64, 200
-    q_lens = [300, 1, 64, 130, 17]
-    ctx = [0, 899, 636, 400, 1000]
+    q_lens = [300, 1, 64, 130, 17, 3]
+    ctx = [0, 899, 636, 400, 1000, 0]
     lens = torch.tensor([a + b for a, b in zip(q_lens, ctx)], dtype=torch.int32)
-    ring = ((window + max(q_lens) - 1 + 31) // 32) * 32   # the block manager's sizing
+    sink_pad = ((n_sink + 31) // 32) * 32
+    ring = ((window - n_sink + max(q_lens) - 1 + 31) // 32) * 32   # the block manager's sizing
     B = len(q_lens)
     q_start = torch.tensor([0] + list(torch.cumsum(torch.tensor(q_lens), 0)), dtype=torch.int32)
-    max_blocks = (ring + bs - 1) // bs
+    max_blocks = (sink_pad + ring + bs - 1) // bs
     kc, vc = _make_cache(B * max_blocks, nkv, bs, D, gpu)
     bt = _tables(B, max_blocks, B * max_blocks, gpu, seed=4)
     q = torch.randn(int(q_start[-1]), nh, D, device=gpu, dtype=BF)
+    qs = torch.randn(int(q_start[-1]), nh, D, device=gpu, dtype=BF) if n_sink else None
     scale = 1 / math.sqrt(D)
     tm = ops.prefill_tiles(q_lens, nh, nkv, qb=qb).to(gpu)
-    args = (kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens), scale, 0, 0, ring, window)
-    out = ops.attn_prefill(q, None, *args, tile_map=tm, qb=qb)
-    out_r = ref.attn_prefill(q.cpu(), None, kc.cpu(), vc.cpu(), bt.cpu(), lens, q_start, scale,
-                             0, 0, ring, window)
-    _close(out, out_r, 2e-2, 2e-2, f"prefill-m32-window-{nh}/{nkv}-qb{qb}")
+    args = (kc, vc, bt, lens.to(gpu), q_start.to(gpu), max(q_lens), scale, n_sink, sink_pad, ring,
+            window)
+    out = ops.attn_prefill(q, qs, *args, tile_map=tm, qb=qb)
+    out_r = ref.attn_prefill(q.cpu(), qs.cpu() if n_sink else None, kc.cpu(), vc.cpu(), bt.cpu(),
+                             lens, q_start, scale, n_sink, sink_pad, ring, window)
+    _close(out, out_r, 2e-2, 2e-2, f"prefill-m32-window-{nh}/{nkv}-s{n_sink}-qb{qb}")
     with ops.kernel_policy(prefill_m32=False):
-        out_l = ops.attn_prefill(q, None, *args, tile_map=tm, qb=qb)
+        out_l = ops.attn_prefill(q, qs, *args, tile_map=tm, qb=qb)
     _close(out, out_l, 2e-2, 2e-2, "prefill-m32-window-vs-legacy")
 
 
