@@ -1,9 +1,10 @@
 // Causal prefill attention on the 32x32x16 bf16 MFMA: 32 query rows per wave, 64-key steps.
 //
 // Replaces the reference's eager prefill attention (modules.py:87-97: repeat_kv, QK^T/sqrt(D) +
-// additive causal mask, fp32 softmax, PV) for the common case - full (non-windowed) bf16 cache,
-// head_dim 128, no custom mask, any GQA group incl. MHA, full caches and windowed rings (sliding
-// windows and StreamingLLM sinks), bf16 or fp8 KV; attention.hip keeps the general kernel.
+// additive causal mask, fp32 softmax, PV) and its sink-cache window (cache.py) for head_dim 128:
+// any GQA group incl. MHA, full caches and windowed rings (sliding windows, StreamingLLM sinks),
+// bf16 or fp8 KV.  attention.hip keeps the rest (custom 4-D masks, other head sizes, short
+// chunks of groups that are not a multiple of 4).
 //
 // Why a second kernel: attention.hip's prefill wave holds 16 query rows on the 16x16x32 MFMA, so
 // every K / V^T fragment read from LDS (one ds_read_b128) feeds ONE 16-cycle MFMA: four SIMDs ask
@@ -28,13 +29,16 @@
 //   * K rows are stored with 16-byte chunk c at c ^ (row & 15): the row reads of one ds_read_b128
 //     lane group (rows {0-3, 12-15, 20-27} or {4-11, 16-19, 28-31}, one chunk) then hit 16
 //     distinct bank slots; the V^T reads (consecutive d) are conflict-free as stored.
-//   * K / V^T tiles (2 x 16 KB per step) go global -> LDS by LDS-DMA into two buffers: the next
-//     step's DMA is issued before this step's MFMAs, one barrier per step.
+//   * K / V^T tiles (2 x 16 KB of bf16 per step) go global -> LDS by LDS-DMA (fp8 caches: through
+//     registers, widened to bf16 on the way) into two buffers (three for staggered workgroups):
+//     the next step's fetch is issued behind this step's first MFMAs, one barrier per step.
 //   * online softmax in the log2 domain with a deferred max (cdna_hip_programming.md T13): the
 //     running max (and the O / l rescale) moves only when some column's max grew by more than
 //     THR = 8, so P <= 2^8 (exact-scale fp32 accumulation; bf16 P keeps its relative precision).
-//   * causality from seq_lens / q_start (no mask tensor); steps entirely below the diagonal skip
-//     the mask, the half of a diagonal step past every column's position skips its MFMAs.
+//   * causality and windows from seq_lens / q_start / ring geometry (no mask tensor): steps run
+//     from the first one holding a key inside some column's window; steps entirely inside every
+//     column's window skip the mask; the half of a diagonal step past every column's position
+//     skips its MFMAs.
 //   * work list: the (sequence, tile) map of attention.hip walked heaviest tile first (the
 //     causal tail), XCD-grouped so consecutive tiles of one kv head share an L2.  (A persistent
 //     form for 4-wave workgroups, P32_PERSIST, walks several tiles with the next tile's Q and
@@ -109,7 +113,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   // staggered waves (8-wave workgroups, one per CU) keep V(s-1) while step s+1 lands: 3 buffers
   constexpr bool STAG = P32_STAGGER && NW == 8;
   constexpr int NBUF = STAG ? 3 : 2;
-  // persistent, with the next tile's Q / first step fetched during the last step (4-wave tiles)
+  // persistent, with the next tile's Q / first step fetched during the stores (4-wave tiles)
   constexpr bool PF = P32_PERSIST && !STAG;
   // [buf][K | V^T][64 keys x D]: NBUF x 2 x 16 KB
   __shared__ __attribute__((aligned(16))) bf16 smem[NBUF][2][64 * D];
@@ -126,8 +130,8 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
 
   // ---- work items.  With a tile map the grid is 8 x `per` workgroups, XCD-major: XCD x
   // (= blockIdx & 7) owns items [x span, (x+1) span) - one kv-head group's tiles, heaviest
-  // first - and its k-th workgroup walks items k, k + per, ... of them (per = span: one each).
-  // Without a map (dense grid) a workgroup is one (sequence, tile, group).
+  // first - and its k-th workgroup takes one of them (per = span), or, persistent, a snake walk
+  // over them (below).  Without a map (dense grid) a workgroup is one (sequence, tile, group).
   struct Item {
     int b, t0, kvh, h0, qs0, qlen, L, pq_lo, pq_hi, ns, s_lo, nsteps;
     const int* bt;
