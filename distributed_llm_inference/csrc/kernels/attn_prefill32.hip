@@ -268,7 +268,8 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
           fp8x8_to_bf16x8(make_uint2(rk[i].x, rk[i].y));
       *reinterpret_cast<bf16x8*>(krow + ((2 * kk + 1) ^ (row & 15)) * 8) =
           fp8x8_to_bf16x8(make_uint2(rk[i].z, rk[i].w));
-      *reinterpret_cast<bf16x8*>(vd + (2 * pu) * 8) = fp8x8_to_bf16x8(make_uint2(rv[i].x, rv[i].y));
+      *reinterpret_cast<bf16x8*>(vd + (2 * pu) * 8) =
+          fp8x8_to_bf16x8(make_uint2(rv[i].x, rv[i].y));
       *reinterpret_cast<bf16x8*>(vd + (2 * pu + 1) * 8) =
           fp8x8_to_bf16x8(make_uint2(rv[i].z, rv[i].w));
     }
@@ -300,17 +301,20 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
       f8_bi = bi;
       f8_need1 = need1;
       const size_t kvb = (size_t)it.kvh * head_stride;
-      const uint8_t* kh0 = static_cast<const uint8_t*>(p.k_cache) + kvb + (size_t)(uint32_t)pg0 * page_elems + so0;
-      const uint8_t* kh1 = static_cast<const uint8_t*>(p.k_cache) + kvb + (size_t)(uint32_t)pg1 * page_elems + so1;
-      const uint8_t* vh0 = static_cast<const uint8_t*>(p.v_cache) + kvb + (size_t)(uint32_t)pg0 * page_elems + so0;
-      const uint8_t* vh1 = static_cast<const uint8_t*>(p.v_cache) + kvb + (size_t)(uint32_t)pg1 * page_elems + so1;
+      const size_t e0 = kvb + (size_t)(uint32_t)pg0 * page_elems + so0;   // bytes = elements
+      const size_t e1 = kvb + (size_t)(uint32_t)pg1 * page_elems + so1;
+      const uint8_t* kh0 = static_cast<const uint8_t*>(p.k_cache) + e0;
+      const uint8_t* kh1 = static_cast<const uint8_t*>(p.k_cache) + e1;
+      const uint8_t* vh0 = static_cast<const uint8_t*>(p.v_cache) + e0;
+      const uint8_t* vh1 = static_cast<const uint8_t*>(p.v_cache) + e1;
 #pragma unroll
       for (int i = 0; i < NPU; ++i) {
         const int pu = (i * NW + w) * 64 + lane;
         const int half = (i * NW + w) >> 2;           // wave-uniform
         if (half && !need1) continue;
         const int row = pu >> 3, kk = pu & 7;         // K: LDS row, 16-d run; key pi(row)
-        rk[i] = *reinterpret_cast<const uint4*>((half ? kh1 : kh0) + swap23(row & 31) * D + 16 * kk);
+        rk[i] = *reinterpret_cast<const uint4*>((half ? kh1 : kh0) + swap23(row & 31) * D +
+                                                16 * kk);
         const int u2 = (2 * pu) & 511;                // V^T: units (g, d), (g, d+1) of the half
         rv[i] = *reinterpret_cast<const uint4*>((half ? vh1 : vh0) + u2 * 8);
       }
