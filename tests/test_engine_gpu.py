@@ -47,6 +47,46 @@ def test_stage_gpu_matches_cpu(gpu):
         assert err < 0.03 * max(1.0, x.abs().max().item()), err
 
 
+SPEC128 = ModelSpec(name="t128", vocab_size=1000, hidden_size=512, intermediate_size=768,
+                    num_layers=3, num_heads=8, num_kv_heads=1, head_dim=128, rope_theta=10000.0,
+                    max_position_embeddings=4096)
+
+
+@pytest.mark.parametrize("window,sinks", [(0, 0), (128, 0), (128, 4)])
+def test_stage_head128_prefill32_matches_cpu(gpu, window, sinks):
+    """head_dim 128 runs prefill on attn_prefill32.hip (the 32-dim SPEC above never reaches it):
+    prefill of prompts up to 300 tokens and forced decode steps on the GPU stage against the CPU
+    reference stage - full cache, Mistral-style sliding window, StreamingLLM sinks - the windowed
+    ones past the window (ring wrapped)."""
+    prompts = [list(range(1, 301)), list(range(500, 537)), [5, 6, 7, 8, 9], list(range(40, 170))]
+    forced = [[17, 23, 5, 9], [5, 900, 1, 2], [44, 1, 3, 7]]
+    cpu = CausalLMStage(SPEC128, 0, 3).init_random(3)
+    g = CausalLMStage(SPEC128, 0, 3, device=gpu).init_random(3)
+    g.load_state_dict({k: v.to(gpu) for k, v in cpu.state_dict().items()})
+
+    def run(stage):
+        pool = stage.make_pool(64, 64, window_length=window, num_sink_tokens=sinks, max_chunk=512)
+        sids = list(range(len(prompts)))
+        for s_, p_ in zip(sids, prompts):
+            pool.manager.append(s_, len(p_))
+        meta = pool.build_metadata(sids, [len(p_) for p_ in prompts])
+        meta.logits_rows = (torch.cumsum(torch.tensor([len(p_) for p_ in prompts]), 0) - 1).to(
+            stage.device)
+        ids = torch.tensor([t for p_ in prompts for t in p_], dtype=torch.int32, device=stage.device)
+        outs = [stage(ids, meta, pool).float().cpu()]
+        for step in forced:
+            for s_ in sids:
+                pool.manager.append(s_, 1)
+            meta = pool.build_metadata(sids, [1] * len(sids))
+            outs.append(stage(torch.tensor(step, dtype=torch.int32, device=stage.device), meta,
+                              pool).float().cpu())
+        return outs
+
+    for x, y in zip(run(cpu), run(g)):
+        err = (x - y).abs().max().item()
+        assert err < 0.03 * max(1.0, x.abs().max().item()), err
+
+
 def _engine(pp=1, graphs=True, window=0, sinks=0, quantize=False, mbs=0):
     cfg = EngineConfig(model="t", pp=pp, seed=5, quantize=quantize,
                        cache=CacheConfig(num_blocks=256, block_size=64, window_length=window,
