@@ -418,10 +418,16 @@ class KernelPolicy:
     fp8_mx: bool = True
     # hand-written tile GEMMs for the decode projections at all (False: hipBLASLt everywhere)
     tile_gemms: bool = True
-    # hipBLASLt for the products the tile kernels do not take well (M < 128, M > 2048, the LM
-    # head).  None = automatic: off when pipeline ranks share a GPU (DLI_SHARE_GPU), because its
+    # hipBLASLt for the products the tile kernels do not take well (M < 128, the LM head).  None = automatic: off when pipeline ranks share a GPU (DLI_SHARE_GPU), because its
     # stream-K kernels wait on each other's workgroups (README "What else couples streams")
     library_gemms: Optional[bool] = None
+    # largest M that stays on the tile kernels when library GEMMs are on (0: no bound - large-M
+    # prefill products run on gemm4 / gemm_tile too).  Above 2048 hipBLASLt stays: at the
+    # headline's 16384-row prefill chunks it runs the 70B projections at 1.63 PF against gemm4's
+    # 1.36 (rocprof, profiles/r6/pgemm/top_*.txt; prefill 25.5 vs 29.2 s).  A single-prompt TTFT
+    # reads the other way (32k: 4.89 vs 5.55 s) only because the first request pays hipBLASLt's
+    # lazy code-object loads for its new shapes - a one-time cost, not a per-request one.
+    tile_gemm_max_m: int = 2048
     # run the partial last wave of whole-K bf16 gemm_tile products stream-K (neutral in-step)
     stream_k_tail: bool = False
     # 1-2 decode rows on the weight-streaming GEMVs, with the input RMSNorm, RoPE/KV write and

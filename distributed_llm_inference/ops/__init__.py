@@ -614,13 +614,13 @@ def tile_gemm_stream_k(M: int, N: int, device) -> bool:
 
 
 TILE_GEMM_MIN_M = 128    # below: too few rows to fill a 256-row tile (hipBLASLt / skinny path)
-TILE_GEMM_MAX_M = 2048   # above (prefill chunks): hipBLASLt's large-M solutions
+TILE_GEMM_WIDE_N = 65536  # vocabulary-wide LM heads: hipBLASLt's wide-N solutions
 TILE_MAX_SPLITS = 8      # norm / quant / rope consumers sum up to 8 partials (SPLITS_SWITCH)
 _CUS = 256
 
 
 def library_gemms() -> bool:
-    """Whether products the tile kernel does not take well (M < 128, M > 2048, the wide LM head)
+    """Whether products the tile kernel does not take well (M < 128, the vocabulary-wide LM head)
     may go to hipBLASLt (default).  Off, every tileable product stays on the tile
     kernel: hipBLASLt picks stream-K solutions for some of these shapes - persistent kernels
     sized to the CU count whose workgroups wait for each other's partial tiles - and two of
@@ -648,12 +648,16 @@ def tile_gemm_splits(M: int, N: int, K: int, elem_bytes: int = 2) -> int:
     lib = library_gemms()
     if N % 256 or (K * elem_bytes) % 128 or M < 1:
         return 0
-    if lib and not (TILE_GEMM_MIN_M <= M <= TILE_GEMM_MAX_M):
-        return 0
+    max_m = policy().tile_gemm_max_m
     k_tiles = K * elem_bytes // 128
     tiles = ((M + 255) // 256) * (N // 256)
-    if lib and tiles > 2 * _CUS:
-        return 0  # e.g. the 128256-wide LM head: hipBLASLt's wide-N solutions are faster (690 vs 824 us)
+    if lib:
+        if M < TILE_GEMM_MIN_M:
+            return 0
+        if N >= TILE_GEMM_WIDE_N:
+            return 0  # the 128256-wide LM head: hipBLASLt's wide-N solutions (690 vs 824 us)
+        if max_m > 0 and (M > max_m or tiles > 2 * _CUS):
+            return 0  # the round-5 rule (large-M products to hipBLASLt), for A/B runs
     best, best_util = 1, 0.0
     for s in range(1, TILE_MAX_SPLITS + 1):
         if s > k_tiles or (s > 1 and tiles * s > 2 * _CUS):
