@@ -428,6 +428,9 @@ class KernelPolicy:
     # reads the other way (32k: 4.89 vs 5.55 s) only because the first request pays hipBLASLt's
     # lazy code-object loads for its new shapes - a one-time cost, not a per-request one.
     tile_gemm_max_m: int = 2048
+    # ... and the executor runs each such projection once at start-up (StageExecutor.
+    # warm_prefill_gemms), so the first long prompt does not pay hipBLASLt's code-object loads
+    warm_library_gemms: bool = True
     # run the partial last wave of whole-K bf16 gemm_tile products stream-K (neutral in-step)
     stream_k_tail: bool = False
     # 1-2 decode rows on the weight-streaming GEMVs, with the input RMSNorm, RoPE/KV write and

@@ -231,6 +231,32 @@ class StageExecutor:
         self._step_counter = 0
         # warm-up / capture stream (a pipeline rank passes its dedicated one: runtime/streams.py)
         self.capture_stream: Optional[torch.cuda.Stream] = None
+        self.warm_prefill_gemms()
+
+    def warm_prefill_gemms(self) -> None:
+        """Run each distinct prefill-sized projection of this stage once at start-up.  Above
+        ``KernelPolicy.tile_gemm_max_m`` rows the projections go to hipBLASLt, which loads a
+        kernel's code object the first time a shape selects it: without this the first long
+        prompt paid ~1 s of loads (Llama-3.1-70B 32k-token TTFT, profiles/r6/pgemm/).  The
+        vocabulary-wide LM head is skipped (prefill projects a few rows through it)."""
+        pol = ops.policy()
+        M = self.max_tokens
+        if (self.device.type != "cuda" or not pol.warm_library_gemms or not ops.library_gemms()
+                or pol.tile_gemm_max_m <= 0 or M <= pol.tile_gemm_max_m):
+            return
+        from ..models.common import Linear
+        seen = set()
+        with torch.no_grad():
+            for mod in self.stage.modules():
+                if not isinstance(mod, Linear) or mod.out_features >= ops.TILE_GEMM_WIDE_N:
+                    continue
+                key = (mod.in_features, mod.out_features, mod.is_fp8, mod.is_int8,
+                       mod.bias is not None)
+                if key in seen:
+                    continue
+                seen.add(key)
+                mod(torch.zeros(M, mod.in_features, dtype=torch.bfloat16, device=self.device))
+        torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------ capacity / bookkeeping
     def apply_frees(self, ids: Sequence[int]) -> None:
