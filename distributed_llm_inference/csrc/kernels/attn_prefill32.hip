@@ -105,16 +105,18 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& s, int base) {
 
 }  // namespace
 
-template <int TQ, int GW, bool F8>
+template <int TQ, int GW, bool F8, bool WIN>
 __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   constexpr int D = P32_D;
   constexpr int CH = D / 8;                 // 16-B chunks per K row
   constexpr int NW = GW * TQ / 32;          // waves per workgroup
   // staggered waves (8-wave workgroups, one per CU) keep V(s-1) while step s+1 lands: 3 buffers
-  constexpr bool STAG = P32_STAGGER && NW == 8;
+  // (not in window mode: the staggered half's S(s-1) held across the barrier next to the window
+  // arithmetic would spill)
+  constexpr bool STAG = P32_STAGGER && NW == 8 && !WIN;
   constexpr int NBUF = STAG ? 3 : 2;
   // persistent, with the next tile's Q / first step fetched during the stores (4-wave tiles)
-  constexpr bool PF = P32_PERSIST && !STAG;
+  constexpr bool PF = P32_PERSIST && NW < 8;
   // [buf][K | V^T][64 keys x D]: NBUF x 2 x 16 KB
   __shared__ __attribute__((aligned(16))) bf16 smem[NBUF][2][64 * D];
 
@@ -143,8 +145,9 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
   // sinks (a < min(nsk, L)) are visible to every column at or past them and score against the
   // query rotated for them (q_sink): one extra step, first.  Main steps are aligned in the
   // ring's offset a - nsk, so each 32-key half is one run of slots.  win = 0: full cache.
-  const int win = p.ring > 0 ? p.window : 0;
-  const int nsk = p.ring > 0 ? p.n_sink : 0;
+  // (a template flag: the window / sink arithmetic costs the full-cache kernels registers)
+  const int win = WIN ? p.window : 0;
+  const int nsk = WIN ? p.n_sink : 0;
   const int wmain = win - nsk;
   // Persistent walk: round n takes item n per + k on even rounds and n per + (per - 1 - k) on odd
   // ones (a snake): the map lists each sequence's tiles heaviest first, so a plain stride that
@@ -526,7 +529,7 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
     // bound, the tail of every workgroup (MI355X_MICROARCH.md constants 'attention epilogue store
     // tail').  Staging image: row R = 32 w + c (= head R / TQ, token R % TQ) of 128 d, 16-byte
     // chunk j at j ^ (R & 15), in the buffer of this tile's last step (all of it read by now; the
-    // next tile's first step lands in the other) - or, staggered, buffers 0-1 (64 KB, no
+    // next tile's first step lands in the other) - or, 8-wave workgroups, buffers 0-1 (64 KB, no
     // prefetch in flight); then each wave-instruction stores 4 whole rows of one token (adjacent
     // heads: 1 KB contiguous in [token][head][d]).
     const float lsum = l_run + __shfl_xor(l_run, 32, 64);
@@ -542,7 +545,8 @@ __global__ void __launch_bounds__(512, 2) attn_prefill32_kernel(AttnParams p) {
       dma_step(nxt, 0, bufi(g0 + nsteps));
       load_q(nxt, qf, nxt.ns ? p.q_sink : p.q);
     }
-    bf16* stg = STAG ? &smem[0][0][0] : kbuf(bufi(g0 + nsteps - 1));
+    // (8-wave workgroups stage 64 KB: buffers 0-1, nothing in flight; 4-wave ones 32 KB)
+    bf16* stg = NW == 8 ? &smem[0][0][0] : kbuf(bufi(g0 + nsteps - 1));
     {
       bf16* srow = stg + (size_t)R * D + 4 * hh;
 #pragma unroll
@@ -606,6 +610,27 @@ bool attn_prefill32_eligible(const AttnParams& p, int D) {
          p.bs % 32 == 0 && (p.bs & (p.bs - 1)) == 0 && (G % 4 == 0 || p.prefill_qb == 2);
 }
 
+// The instance for (heads per workgroup, tile size, cache dtype, window mode); fp8 caches take
+// 4- and 8-wave workgroups only (eligibility), so their 2-wave instances are never built.
+template <bool F8, bool WIN>
+static void p32_dispatch(const AttnParams& p, int gw, bool big, dim3 grid, int nw,
+                         hipStream_t stream) {
+  const dim3 block(64 * nw);
+  if (gw == 8) {
+    if (big) attn_prefill32_kernel<32, 8, F8, WIN><<<grid, block, 0, stream>>>(p);
+    else attn_prefill32_kernel<16, 8, F8, WIN><<<grid, block, 0, stream>>>(p);
+  } else if (gw == 4) {
+    if (big) attn_prefill32_kernel<32, 4, F8, WIN><<<grid, block, 0, stream>>>(p);
+    else if constexpr (!F8) attn_prefill32_kernel<16, 4, F8, WIN><<<grid, block, 0, stream>>>(p);
+  } else if (gw == 2) {
+    if (big) attn_prefill32_kernel<64, 2, F8, WIN><<<grid, block, 0, stream>>>(p);
+    else if constexpr (!F8) attn_prefill32_kernel<32, 2, F8, WIN><<<grid, block, 0, stream>>>(p);
+  } else {
+    if (big) attn_prefill32_kernel<128, 1, F8, WIN><<<grid, block, 0, stream>>>(p);
+    else if constexpr (!F8) attn_prefill32_kernel<64, 1, F8, WIN><<<grid, block, 0, stream>>>(p);
+  }
+}
+
 // Tile = the one attention.hip's kernel uses (16 * (4 / min(GW, 4)) * prefill_qb query tokens:
 // 16 or 32 for groups of 4 and 8 heads, 32 or 64 for pairs, 64 or 128 for single heads - MHA or
 // an odd group such as Qwen2's 7), so one (sequence, tile) map serves both.
@@ -633,29 +658,12 @@ int launch_attn_prefill32(const AttnParams& p, int B, int max_q, hipStream_t str
   }
   if (grid.x == 0) return 0;
   const bool big = p.prefill_qb == 2;
-  if (p.kv_fp8) {   // fp8 caches: 4- and 8-wave workgroups only (eligibility)
-    if (gw == 8) {
-      if (big) attn_prefill32_kernel<32, 8, true><<<grid, 64 * nw, 0, stream>>>(p);
-      else attn_prefill32_kernel<16, 8, true><<<grid, 64 * nw, 0, stream>>>(p);
-    } else if (gw == 4) {
-      attn_prefill32_kernel<32, 4, true><<<grid, 64 * nw, 0, stream>>>(p);
-    } else if (gw == 2) {
-      attn_prefill32_kernel<64, 2, true><<<grid, 64 * nw, 0, stream>>>(p);
-    } else {
-      attn_prefill32_kernel<128, 1, true><<<grid, 64 * nw, 0, stream>>>(p);
-    }
-  } else if (gw == 8) {
-    if (big) attn_prefill32_kernel<32, 8, false><<<grid, 64 * nw, 0, stream>>>(p);
-    else attn_prefill32_kernel<16, 8, false><<<grid, 64 * nw, 0, stream>>>(p);
-  } else if (gw == 4) {
-    if (big) attn_prefill32_kernel<32, 4, false><<<grid, 64 * nw, 0, stream>>>(p);
-    else attn_prefill32_kernel<16, 4, false><<<grid, 64 * nw, 0, stream>>>(p);
-  } else if (gw == 2) {
-    if (big) attn_prefill32_kernel<64, 2, false><<<grid, 64 * nw, 0, stream>>>(p);
-    else attn_prefill32_kernel<32, 2, false><<<grid, 64 * nw, 0, stream>>>(p);
+  if (p.kv_fp8) {
+    if (p.ring > 0) p32_dispatch<true, true>(p, gw, big, grid, nw, stream);
+    else p32_dispatch<true, false>(p, gw, big, grid, nw, stream);
   } else {
-    if (big) attn_prefill32_kernel<128, 1, false><<<grid, 64 * nw, 0, stream>>>(p);
-    else attn_prefill32_kernel<64, 1, false><<<grid, 64 * nw, 0, stream>>>(p);
+    if (p.ring > 0) p32_dispatch<false, true>(p, gw, big, grid, nw, stream);
+    else p32_dispatch<false, false>(p, gw, big, grid, nw, stream);
   }
   return 0;
 }
