@@ -239,6 +239,14 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
             ndev = torch.cuda.device_count()
             kv_share = 1.0 / ((world + ndev - 1) // ndev)
             local = local % ndev
+            if os.environ.get("DLI_RCCL_RANK_HOSTS") == "1":
+                # RCCL rehearsal on shared GPUs: every rank claims a host of its own, so RCCL's
+                # duplicate-device check (host, PCI bus id) passes and strict RCCL
+                # (DLI_TRANSPORT=rccl) connects the ranks via its socket transport on loopback.
+                # Read once by RCCL: this runs before any RCCL call.
+                os.environ["NCCL_HOSTID"] = f"dli-rehearsal-host-{rank}"
+                os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+                os.environ.setdefault("NCCL_IB_DISABLE", "1")
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:

@@ -45,11 +45,24 @@ def _cfg(world, mbs):
     return spec, cfg
 
 
-def _pipeline_worker(rank, world, port, mbs, q, transport="host", rotation=None):
+def _rank_hosts(rank):
+    """Each rank claims a host of its own (``NCCL_HOSTID``).  RCCL's duplicate-device check
+    compares (host, PCI bus id) pairs, so ranks that share the one GPU are then accepted and
+    connected through RCCL's network transport.  Here that is TCP sockets on loopback, not xGMI,
+    but the communicators, the grouped send/recv on the transport's streams and the hop digests
+    are the production code.  Must be set before the process makes any RCCL call."""
+    os.environ.update(NCCL_HOSTID=f"dli-rehearsal-host-{rank}", NCCL_SOCKET_IFNAME="lo",
+                      NCCL_IB_DISABLE="1")
+
+
+def _pipeline_worker(rank, world, port, mbs, q, transport="host", rotation=None,
+                     rank_hosts=False):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DLI_SHARE_GPU="1",
                           DLI_TUNING_DIR="off", DLI_WATCHDOG_S="60")
+        if rank_hosts:
+            _rank_hosts(rank)
         if transport is None:   # the default
             os.environ.pop("DLI_TRANSPORT", None)
         else:
@@ -242,15 +255,17 @@ def test_default_transport_on_a_shared_gpu_is_ipc(gpu):
     assert rest and rest[0] == "IpcTransport", rest
 
 
-def _rccl_worker(rank, port, q):
+def _rccl_worker(rank, port, q, rank_hosts=False):
     try:
         os.environ.update(RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
                           MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        if rank_hosts:
+            _rank_hosts(rank)
         import torch.distributed as dist
         dist.init_process_group("gloo")
         from distributed_llm_inference.parallel.transport import RcclTransport
         from distributed_llm_inference.runtime.faults import raw_store
-        dev = torch.device("cuda", rank)
+        dev = torch.device("cuda", 0 if rank_hosts else rank)
         torch.cuda.set_device(dev)
         tr = RcclTransport(raw_store(), rank, 2, dev, timeout_s=120.0)
         for n in (1 << 10, 8 << 20):  # a decode-sized and a prefill-sized hidden-state message
@@ -293,6 +308,50 @@ def test_rccl_p2p_two_gpus(gpu):
     for p in ps:
         p.join(60)
     assert all(s == "ok" for s, _ in res), res
+
+
+def test_rccl_p2p_one_gpu_rank_hosts(gpu):
+    """RcclTransport with two ranks on the ONE GPU, each claiming its own host (_rank_hosts): real
+    RCCL communicators and send/recv of decode- and prefill-sized messages on the transport's
+    streams (bytes over RCCL's loopback socket transport)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_rccl_worker, args=(r, port, q, True)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(60)
+    assert all(s == "ok" for s, _ in res), res
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+
+
+@pytest.mark.parametrize("world,mbs", [(2, 3), (4, 5)])
+def test_multiprocess_pipeline_rccl_one_gpu_rank_hosts(gpu, world, mbs):
+    """The PP pipeline over strict RCCL (``DLI_TRANSPORT=rccl``) on the one GPU, each rank its own
+    RCCL host: RCCL pair and rotating-head communicators, hop digests checked, tokens equal
+    PP=1's."""
+    from distributed_llm_inference.runtime.engine import LLMEngine
+    from distributed_llm_inference.runtime.sequence import SamplingParams
+    os.environ["DLI_TUNING_DIR"] = "off"
+    spec, cfg = _cfg(1, mbs)
+    ref = [s.output for s in LLMEngine(spec, device="cuda:0", cfg=cfg).generate(
+        PROMPTS, SamplingParams(max_tokens=8, ignore_eos=True))]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_pipeline_worker, args=(r, world, port, mbs, q, "rccl", None, True))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    status, got, kind = q.get(timeout=600)
+    for p in ps:
+        p.join(120)
+    assert status == "ok", got
+    assert kind == "RcclTransport", kind
+    assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    assert got == ref
 
 
 def _pipeline_worker_gpus(rank, world, port, q):
