@@ -7,8 +7,10 @@ a 1-rank communicator, and the RCCL-failure path (all ranks agree, fall back tog
 by asking for RCCL on a shared GPU: with an explicit ``DLI_TRANSPORT=rccl`` every rank fails
 loudly and ``DLI_TRANSPORT=rccl-or-host`` falls back to host staging.  The default (unset:
 ``rccl-or-ipc``) compares the ranks' PCI devices and takes the IPC device transport on a shared
-GPU without trying RCCL (strict RCCL on distinct GPUs).  With two or more GPUs the RCCL P2P
-transport and a PP=2 RCCL pipeline are tested for real.
+GPU without trying RCCL (strict RCCL on distinct GPUs).  RCCL itself also runs on the one GPU
+when every rank claims its own host (``NCCL_HOSTID``, :func:`_rank_hosts`): real communicators,
+bytes over RCCL's loopback socket transport (the PP=2/4 strict-RCCL pipeline tests).  With two or
+more GPUs the RCCL P2P transport and a PP=2 RCCL pipeline are tested over xGMI.
 """
 import multiprocessing as mp
 import os
