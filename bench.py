@@ -267,8 +267,9 @@ def main():
     for s in seqs:
         tt = s.token_times
         lat += [(tt[i + 1] - tt[i]) * 1e3 for i in range(len(tt) - 1)]
-    p50 = statistics.median(lat) if lat else float("nan")
-    p90 = statistics.quantiles(lat, n=10)[-1] if len(lat) >= 10 else float("nan")
+    # None (JSON null, never NaN: the line must stay strict JSON) when too few intervals
+    p50 = round(statistics.median(lat), 3) if lat else None
+    p90 = round(statistics.quantiles(lat, n=10)[-1], 3) if len(lat) >= 10 else None
     value = toks / elapsed
     res = {
         "metric": METRIC,
@@ -288,8 +289,8 @@ def main():
                    else spec.name,
                    "global_batch": G * dp, "seq_len": total_len,
                    "parallelism": f"pp{pp}" if dp == 1 else f"dp{dp}xpp{pp}"},
-        "p50_token_latency_ms": round(p50, 3),
-        "p90_token_latency_ms": round(p90, 3),
+        "p50_token_latency_ms": p50,
+        "p90_token_latency_ms": p90,
         "transport": drv.tr.describe()["transport"] if (world > 1 and pp > 1) else "none",
         "kernel_policy": a.kernels or "default",
         "micro_batches": M,

@@ -14,6 +14,10 @@ REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
             "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"]
 
 
+
+def _no_nan(tok):
+    raise AssertionError(f"bench line is not strict JSON: {tok}")
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -39,7 +43,7 @@ def test_bench_multirank_json_contract(n):
         pytest.fail("\n".join(own[-60:]) + "\n---- tail ----\n" + r.stderr[-2000:])
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
-    d = json.loads(lines[0])
+    d = json.loads(lines[0], parse_constant=_no_nan)   # strict JSON: no NaN / Infinity
     for k in REQUIRED:
         assert k in d, k
     assert d["n_gpus"] == n and d["steps"] == steps and d["warmup"] == warmup
@@ -114,7 +118,7 @@ def test_bench_replicas_json_contract(n, dp):  # noqa: C901
         pytest.fail("\n".join(own[-60:]) + "\n---- tail ----\n" + r.stderr[-2000:])
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
-    d = json.loads(lines[0])
+    d = json.loads(lines[0], parse_constant=_no_nan)   # strict JSON: no NaN / Infinity
     for k in REQUIRED:
         assert k in d, k
     assert d["config"]["parallelism"] == f"dp{dp}xpp{pp}"
