@@ -14,7 +14,6 @@ REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
             "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"]
 
 
-
 def _no_nan(tok):
     raise AssertionError(f"bench line is not strict JSON: {tok}")
 
