@@ -219,6 +219,20 @@ def _dp_from_env(cfg: EngineConfig) -> int:
     return int(os.environ.get("DLI_DP", cfg.dp or 1))
 
 
+def rccl_rank_hosts(rank: int, env=os.environ) -> bool:
+    """``DLI_RCCL_RANK_HOSTS=1`` (one-GPU RCCL rehearsals, with ``DLI_SHARE_GPU=1``): the rank
+    claims an RCCL host of its own (``NCCL_HOSTID``), so RCCL's duplicate-device check, which
+    compares (host, PCI bus id), passes for ranks sharing a GPU, and strict RCCL
+    (``DLI_TRANSPORT=rccl``) connects them through its socket transport on loopback.  RCCL reads
+    the host id once, so this must run before any RCCL call.  Returns whether it applied."""
+    if env.get("DLI_RCCL_RANK_HOSTS") != "1":
+        return False
+    env["NCCL_HOSTID"] = f"dli-rehearsal-host-{rank}"
+    env.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    env.setdefault("NCCL_IB_DISABLE", "1")
+    return True
+
+
 def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
     """Bootstrap this rank of a multi-process pipeline (env: RANK, WORLD_SIZE, LOCAL_RANK,
     MASTER_ADDR, MASTER_PORT; ``DLI_DP`` or ``cfg.dp`` = number of pipeline replicas).  Returns
@@ -239,14 +253,7 @@ def init_pipeline_rank(cfg: EngineConfig, backend: str = "gloo"):
             ndev = torch.cuda.device_count()
             kv_share = 1.0 / ((world + ndev - 1) // ndev)
             local = local % ndev
-            if os.environ.get("DLI_RCCL_RANK_HOSTS") == "1":
-                # RCCL rehearsal on shared GPUs: every rank claims a host of its own, so RCCL's
-                # duplicate-device check (host, PCI bus id) passes and strict RCCL
-                # (DLI_TRANSPORT=rccl) connects the ranks via its socket transport on loopback.
-                # Read once by RCCL: this runs before any RCCL call.
-                os.environ["NCCL_HOSTID"] = f"dli-rehearsal-host-{rank}"
-                os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-                os.environ.setdefault("NCCL_IB_DISABLE", "1")
+            rccl_rank_hosts(rank)
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:

@@ -60,3 +60,18 @@ def test_rotation_overrides(monkeypatch):
     assert not head_rotation_wanted(EngineConfig(model="llama-3-70b", pp=8), 8, GPU)
     monkeypatch.setenv("DLI_HEAD_ROTATION", "1")
     assert not head_rotation_wanted(EngineConfig(model="llama-3-70b", pp=1), 1, GPU)
+
+
+def test_rccl_rank_hosts_sets_a_host_id_per_rank():
+    """DLI_RCCL_RANK_HOSTS=1: each rank gets its own NCCL_HOSTID (what lets RCCL pair ranks that
+    share a GPU), loopback sockets unless the user chose an interface; off by default."""
+    from distributed_llm_inference.runtime.engine import rccl_rank_hosts
+    env = {}
+    assert not rccl_rank_hosts(3, env) and env == {}
+    env = {"DLI_RCCL_RANK_HOSTS": "1", "NCCL_SOCKET_IFNAME": "eth0"}
+    assert rccl_rank_hosts(3, env)
+    assert env["NCCL_HOSTID"] == "dli-rehearsal-host-3"
+    assert env["NCCL_SOCKET_IFNAME"] == "eth0" and env["NCCL_IB_DISABLE"] == "1"
+    other = {"DLI_RCCL_RANK_HOSTS": "1"}
+    rccl_rank_hosts(4, other)
+    assert other["NCCL_HOSTID"] != env["NCCL_HOSTID"] and other["NCCL_SOCKET_IFNAME"] == "lo"
